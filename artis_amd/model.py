@@ -1,0 +1,95 @@
+"""Synthetic ARTIS model (atomic data + grid + LTE cell state + initial r-packets) via libartis_model.so.
+
+Input generation for tests and bench only (the reference's input()/grid_init()/update_grid() stand-in,
+SURVEY.md §8(d)); the engine itself is in libartis_gpu.so.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import ffi
+
+_LIBDIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+_model_lib = None
+
+
+def model_lib():
+    global _model_lib
+    if _model_lib is None:
+        path = os.path.join(_LIBDIR, "libartis_model.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run __graft_entry__.build() first")
+        lib = C.CDLL(path)
+        lib.artis_synth_default_config.argtypes = [C.POINTER(ffi.SynthConfig)]
+        lib.artis_model_synth.argtypes = [C.POINTER(ffi.SynthConfig)]
+        lib.artis_model_synth.restype = C.c_void_p
+        lib.artis_model_free.argtypes = [C.c_void_p]
+        for fn in ("artis_model_atomic", "artis_model_geometry", "artis_model_cellstate"):
+            getattr(lib, fn).argtypes = [C.c_void_p]
+            getattr(lib, fn).restype = C.c_void_p
+        lib.artis_model_run_params.argtypes = [C.c_void_p, C.POINTER(ffi.RunParams)]
+        lib.artis_model_set_timestep.argtypes = [C.c_void_p, C.c_int]
+        lib.artis_model_init_rpackets.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_uint64, C.c_double, C.c_void_p]
+        lib.artis_model_npts_model.argtypes = [C.c_void_p]
+        lib.artis_model_npts_model.restype = C.c_int64
+        _model_lib = lib
+    return _model_lib
+
+
+def default_config(**overrides):
+    cfg = ffi.SynthConfig()
+    model_lib().artis_synth_default_config(C.byref(cfg))
+    for k, v in overrides.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+class Model:
+    """Owns one synthetic model; exposes the raw C struct pointers for the engine and the oracle."""
+
+    def __init__(self, cfg=None, **overrides):
+        self.cfg = cfg if cfg is not None else default_config(**overrides)
+        self._lib = model_lib()
+        self._h = self._lib.artis_model_synth(C.byref(self.cfg))
+        if not self._h:
+            raise RuntimeError("artis_model_synth failed")
+        self.atomic = self._lib.artis_model_atomic(self._h)
+        self.geometry = self._lib.artis_model_geometry(self._h)
+        self.cellstate = self._lib.artis_model_cellstate(self._h)
+        self.params = ffi.RunParams()
+        self._lib.artis_model_run_params(self._h, C.byref(self.params))
+        self.npts_model = int(self._lib.artis_model_npts_model(self._h))
+        # a few counts straight from the atomic-table header (first 8 int32 of artis_atomic_tables)
+        hdr = (C.c_int32 * 8).from_address(self.atomic)
+        (self.nelements, self.maxnions, self.nions_total, self.nlevels_total, self.nlines,
+         self.nbfcontinua, self.nbfcontinua_ground, self.ncoolingterms) = list(hdr)
+        self.nts = 0
+
+    def set_timestep(self, nts):
+        rc = self._lib.artis_model_set_timestep(self._h, int(nts))
+        if rc != 0:
+            raise RuntimeError(f"artis_model_set_timestep({nts}) -> {rc}")
+        self.nts = nts
+
+    def init_rpackets(self, nts, npkts, seed=1, etot=1e45):
+        pk = np.zeros(npkts, dtype=ffi.PACKET_DTYPE)
+        rc = self._lib.artis_model_init_rpackets(self._h, int(nts), int(npkts), C.c_uint64(seed), float(etot),
+                                                 pk.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"artis_model_init_rpackets -> {rc}")
+        return pk
+
+    def new_estimators(self):
+        return ffi.EstimatorArrays(self.npts_model, self.nelements, self.maxnions, self.nlines)
+
+    def close(self):
+        if self._h:
+            self._lib.artis_model_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

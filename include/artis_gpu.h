@@ -1,0 +1,331 @@
+/*
+ * artis_gpu.h -- C-ABI drop-in boundary of the MI355X packet-propagation engine.
+ *
+ * Replaces the reference call
+ *     void update_packets(const int my_rank, int nts, struct packet *packets);
+ * (reference update_packets.h:6, called once per timestep by do_timestep at sn3d.cc:574,
+ *  after zero_estimators() sn3d.cc:568 and before mpi_reduce_estimators sn3d.cc:582)
+ * with three calls:
+ *     artis_gpu_init()              -- once per run: atomic tables + geometry (reference input(), grid_init())
+ *     artis_gpu_upload_cellstate()  -- once per timestep after update_grid (reference update_grid.cc:1270)
+ *     artis_gpu_update_packets()    -- the hot path (reference update_packets.cc:234-333)
+ *
+ * Everything crossing this boundary is plain C: pointers, sizes, ints and doubles.  No torch, no HIP types.
+ * The packet record is the reference's 304-byte `struct packet` (packet.h:28-73), bit-identical, so the raw
+ * `packets_RRRR_tsN.tmp` restart files (sn3d.cc:387-398, packet.cc:198-209) stay valid.
+ *
+ * All returns: 0 on success, negative artis_status on failure.  The C++ host mirror
+ * (artis_amd/csrc/host/update_packets_gpu.cc) turns a failure into the reference's abort()
+ * (assert_always, sn3d.h:17-29).
+ */
+#ifndef ARTIS_GPU_H
+#define ARTIS_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------------------------------------------ */
+/* Packet record: reference packet.h:6-73 (types), boundary.h:4-12 (last_cross). sizeof == 304, offsets checked   */
+/* by static asserts in artis_layout_check.h and by tests/test_abi.py.                                          */
+/* ------------------------------------------------------------------------------------------------------------ */
+enum artis_packet_type {
+  ARTIS_TYPE_ESCAPE = 32,
+  ARTIS_TYPE_RADIOACTIVE_PELLET = 100,
+  ARTIS_TYPE_GAMMA = 10,
+  ARTIS_TYPE_RPKT = 11,
+  ARTIS_TYPE_KPKT = 12,
+  ARTIS_TYPE_MA = 13,
+  ARTIS_TYPE_NTLEPTON = 20,
+  ARTIS_TYPE_NONTHERMAL_PREDEPOSIT = 21,
+  ARTIS_TYPE_PRE_KPKT = 120,
+  ARTIS_TYPE_GAMMA_KPKT = 121,
+};
+
+enum artis_cell_boundary {
+  ARTIS_NEG_X = 101,
+  ARTIS_POS_X = 102,
+  ARTIS_NEG_Y = 103,
+  ARTIS_POS_Y = 104,
+  ARTIS_NEG_Z = 105,
+  ARTIS_POS_Z = 106,
+  ARTIS_NONE = 107,
+};
+
+typedef struct artis_mastate {
+  int32_t element;
+  int32_t ion;
+  int32_t level;
+  int32_t activatingline;
+} artis_mastate;
+
+typedef struct artis_packet {
+  int32_t where;             /*   0 */
+  int32_t type;              /*   4  enum artis_packet_type */
+  int32_t last_cross;        /*   8  enum artis_cell_boundary */
+  int32_t interactions;      /*  12 */
+  int32_t nscatterings;      /*  16 */
+  int32_t last_event;        /*  20 */
+  double pos[3];             /*  24 */
+  double dir[3];             /*  48 */
+  double e_cmf;              /*  72 */
+  double e_rf;               /*  80 */
+  double nu_cmf;             /*  88 */
+  double nu_rf;              /*  96 */
+  int32_t next_trans;        /* 104 */
+  int32_t emissiontype;      /* 108 */
+  double em_pos[3];          /* 112 */
+  int32_t em_time;           /* 136 */
+  int32_t _pad0;             /* 140 */
+  double prop_time;          /* 144 */
+  int32_t absorptiontype;    /* 152 */
+  int32_t trueemissiontype;  /* 156 */
+  int32_t trueem_time;       /* 160 */
+  int32_t _pad1;             /* 164 */
+  double absorptionfreq;     /* 168 */
+  double absorptiondir[3];   /* 176 */
+  double stokes[3];          /* 200 */
+  double pol_dir[3];         /* 224 */
+  double tdecay;             /* 248 */
+  int32_t escape_type;       /* 256 */
+  int32_t escape_time;       /* 260 */
+  int32_t scat_count;        /* 264 */
+  int32_t number;            /* 268 */
+  uint8_t originated_from_particlenotgamma; /* 272  (C++ bool in the reference) */
+  uint8_t _pad2[3];          /* 273 */
+  int32_t pellet_decaytype;  /* 276 */
+  int32_t pellet_nucindex;   /* 280 */
+  float trueemissionvelocity;/* 284 */
+  artis_mastate mastate;     /* 288 */
+} artis_packet;              /* 304 */
+
+/* ------------------------------------------------------------------------------------------------------------ */
+/* Atomic data (read-only for the whole run).  Flattened form of the reference globals::elements / linelist /    */
+/* allcont / groundcont / LUTs (globals.h:44-160, 273-294; input.cc:747-1186, 1439-1652).                       */
+/* Index conventions follow the reference: ions are numbered globally by get_uniqueionindex (atomic.cc:246),   */
+/* levels by get_uniquelevelindex (atomic.cc:278); `level` fields inside per-ion records are ion-local.          */
+/* ------------------------------------------------------------------------------------------------------------ */
+typedef struct artis_atomic_tables {
+  int32_t nelements;
+  int32_t maxnions;          /* get_max_nions() */
+  int32_t nions_total;       /* get_includedions() */
+  int32_t nlevels_total;
+  int32_t nlines;
+  int32_t nbfcontinua;
+  int32_t nbfcontinua_ground;
+  int32_t ncoolingterms;
+  int32_t nphixspoints;              /* globals::NPHIXSPOINTS */
+  double nphixsnuincrement;          /* globals::NPHIXSNUINCREMENT */
+  double last_phixs_nuovernuedge;    /* atomic.cc:8 */
+  int32_t phixs_file_version;        /* 1 or 2 (atomic.cc:12) */
+  int32_t tablesize;                 /* TABLESIZE */
+  double mintemp, maxtemp;           /* MINTEMP, MAXTEMP; T_step_log derived as ratecoeff.cc:1004 */
+
+  /* elements [nelements] */
+  const int32_t *elem_anumber;
+  const int32_t *elem_nions;
+  const int32_t *elem_uniqueionoffset; /* unique ion index of ion 0 */
+
+  /* ions [nions_total] */
+  const int32_t *ion_ionstage;
+  const int32_t *ion_nlevels;
+  const int32_t *ion_uniqueleveloffset; /* unique level index of level 0 */
+  const int32_t *ion_ionisinglevels;
+  const int32_t *ion_maxrecombininglevel;
+  const int32_t *ion_coolingoffset;
+  const int32_t *ion_ncoolingterms;
+  const double *ion_ionpot;
+
+  /* levels [nlevels_total] */
+  const double *level_epsilon;
+  const float *level_stat_weight;
+  const int32_t *level_nuptrans;
+  const int32_t *level_uptrans_offset;     /* into uptrans_lineindex */
+  const int32_t *level_ndowntrans;
+  const int32_t *level_downtrans_offset;   /* into downtrans_lineindex */
+  const int32_t *level_nphixstargets;      /* raw count; get_nphixstargets() applies the ionising-level rule */
+  const int32_t *level_phixstargets_offset;/* into phixstarget_* */
+  const int32_t *level_cont_index;         /* reference levellist_entry::cont_index (negative) */
+  const int32_t *level_closestgroundlevelcont; /* element*maxnions+ion, or -1 */
+  const int32_t *level_phixstable;         /* row into phixs_xs, -1 if none */
+  const int32_t *uptrans_lineindex;
+  const int32_t *downtrans_lineindex;
+  const int32_t *phixstarget_levelindex;   /* ion-local level index in ion+1 */
+  const double *phixstarget_probability;
+  const float *phixs_xs;                   /* [ntables * nphixspoints], cm^2 */
+
+  /* lines [nlines], sorted by descending nu (reference linelist_entry, globals.h:133-144) */
+  const double *line_nu;
+  const float *line_einstein_A;
+  const float *line_osc_strength;
+  const float *line_coll_str;
+  const int32_t *line_elementindex;
+  const int32_t *line_ionindex;
+  const int32_t *line_upperlevelindex;
+  const int32_t *line_lowerlevelindex;
+  const uint8_t *line_forbidden;
+
+  /* all bf continua [nbfcontinua], sorted by ascending nu_edge (reference fullphixslist, globals.h:53-63) */
+  const double *allcont_nu_edge;
+  const int32_t *allcont_element;
+  const int32_t *allcont_ion;
+  const int32_t *allcont_level;
+  const int32_t *allcont_phixstargetindex;
+  const int32_t *allcont_upperlevel;
+  const int32_t *allcont_phixstable;
+  const double *allcont_probability;
+  const int32_t *allcont_index_in_groundphixslist;
+
+  /* ground-level continua [nbfcontinua_ground], ascending nu_edge (reference groundphixslist, globals.h:65-71) */
+  const double *groundcont_nu_edge;
+  const int32_t *groundcont_element;
+  const int32_t *groundcont_ion;
+  const int32_t *groundcont_level;
+  const int32_t *groundcont_phixstargetindex;
+
+  /* rate-coefficient LUTs [tablesize * nbfcontinua], indexed get_bflutindex (sn3d.h:64-69) */
+  const double *spontrecombcoeff;
+  const double *corrphotoioncoeff;
+  const double *bfcooling_coeff;
+
+  /* k-packet cooling list [ncoolingterms] (kpkt.cc:339-426) */
+  const int32_t *coolinglist_type;      /* 880 ff, 881 fb, 882 collexc, 883 collion */
+  const int32_t *coolinglist_element;
+  const int32_t *coolinglist_ion;
+  const int32_t *coolinglist_level;
+  const int32_t *coolinglist_upperlevel;
+} artis_atomic_tables;
+
+/* ------------------------------------------------------------------------------------------------------------ */
+/* Geometry + time grid (reference grid.h:20-65, grid.cc:2028-2102, input.cc:2226-2381).                       */
+/* ------------------------------------------------------------------------------------------------------------ */
+enum artis_grid_type { ARTIS_GRID_UNIFORM = 1, ARTIS_GRID_SPHERICAL1D = 2 };
+
+typedef struct artis_geometry {
+  int32_t grid_type;
+  int32_t ncoordgrid[3];
+  int32_t ngrid;
+  int32_t npts_model;          /* empty propagation cells map to mgi == npts_model */
+  const double *cell_pos_min;  /* [ngrid * 3] at tmin (grid::cell[].pos_min) */
+  const int32_t *cell_mgi;     /* [ngrid] */
+  const double *modelcell_wid_init; /* [npts_model] radial extent at tmin (spherical only; may be NULL) */
+  double coordmax[3];
+  double tmin, tmax, rmax, vmax;
+  int32_t ntstep;
+  const double *ts_start;      /* [ntstep] */
+  const double *ts_width;
+  const double *ts_mid;
+  double nu_min_r, nu_max_r;   /* NU_MIN_R, NU_MAX_R (sample_planck range) */
+} artis_geometry;
+
+/* ------------------------------------------------------------------------------------------------------------ */
+/* Per-timestep model-cell state written by the host update_grid (reference modelgrid_t, grid.h:33-65).        */
+/* All arrays are indexed by model-grid index mgi in [0, npts_model).                                          */
+/* ------------------------------------------------------------------------------------------------------------ */
+typedef struct artis_cell_state {
+  const float *Te, *TR, *TJ, *W, *nne, *nnetot, *rho, *kappagrey;
+  const int16_t *thick;
+  const float *elem_abundance;        /* [npts_model * nelements] mass fractions */
+  const float *groundlevelpop;        /* [npts_model * nions_total] */
+  const float *partfunct;             /* [npts_model * nions_total] */
+  const double *totalcooling;         /* [npts_model] */
+  const double *cooling_contrib_ion;  /* [npts_model * nions_total] */
+  const double *corrphotoionrenorm;   /* [npts_model * nelements * maxnions] */
+} artis_cell_state;
+
+/* Run-time switches of input.txt / artisoptions.h that change hot-path behaviour. */
+typedef struct artis_run_params {
+  uint32_t seed;               /* input.txt line 1 (pre_zseed) */
+  int32_t rank;                /* this rank's packet ensemble ("rank" of the reference MPI run) */
+  int32_t opacity_case;        /* input.txt: 4 = full opacity */
+  int32_t do_r_lc;             /* input.txt r-light-curve flag (derived as input.cc:1976-1979) */
+  int32_t do_rlc_est;          /* input.txt line 9 */
+  int32_t n_kpktdiffusion_timesteps;
+  float kpktdiffusion_timescale;
+  double max_path_step;        /* globals::max_path_step (update_grid.cc:1400) */
+  int32_t pol_dipole;          /* DIPOLE: 1 = dipole rejection scattering (polarization.cc:26-53) */
+  int32_t relativistic_doppler;/* USE_RELATIVISTIC_DOPPLER_SHIFT */
+  int32_t record_linestat;     /* RECORD_LINESTAT */
+} artis_run_params;
+
+/* ------------------------------------------------------------------------------------------------------------ */
+/* Accumulators (reference radfield J/nuJ, globals::*estimator, time_step[nts].*, ecounter/acounter, stats).  */
+/* Un-normalised sums with the reference index conventions; the engine ADDS into them (zero_estimators is     */
+/* the caller's job, emissivities.cc:138).                                                                     */
+/* ------------------------------------------------------------------------------------------------------------ */
+#define ARTIS_COUNTER_COUNT 34   /* stats.h:49-83 */
+
+typedef struct artis_estimators {
+  double *J;                   /* [npts_model]  radfield.cc:100 */
+  double *nuJ;                 /* [npts_model]  radfield.cc:108 */
+  double *ffheatingestimator;  /* [npts_model] */
+  double *colheatingestimator; /* [npts_model] */
+  double *gammaestimator;      /* [npts_model * nelements * maxnions]  rpkt.cc:596 */
+  double *bfheatingestimator;  /* [npts_model * nelements * maxnions] */
+  int32_t *ecounter;           /* [nlines]  RECORD_LINESTAT (may be NULL) */
+  int32_t *acounter;           /* [nlines] */
+  double cmf_lum, gamma_dep, positron_dep, electron_dep, electron_emission, alpha_dep, alpha_emission,
+      gamma_emission;          /* time_step[nts].* (globals.h:20-40) */
+  int64_t pellet_decays;
+  int64_t nesc;                /* globals::nesc */
+  int64_t counters[ARTIS_COUNTER_COUNT];
+} artis_estimators;
+
+enum artis_status {
+  ARTIS_OK = 0,
+  ARTIS_ERR_NOT_INITIALISED = -1,
+  ARTIS_ERR_HIP = -2,
+  ARTIS_ERR_BAD_ARGUMENT = -3,
+  ARTIS_ERR_NO_CELLSTATE = -4,
+  ARTIS_ERR_PACKET_FAULT = -5,   /* a packet hit an abort() path of the reference (see artis_gpu_last_error) */
+  ARTIS_ERR_UNSUPPORTED = -6,    /* a packet type / option this build does not propagate */
+};
+
+/* --- lifecycle ------------------------------------------------------------------------------------------- */
+/* Bind the engine to HIP device `device` and upload read-only tables.  Replaces the table setup done by
+ * input(rank) (input.cc:1754) and grid_init (grid.cc:2132) as seen by update_packets. */
+int artis_gpu_init(int device, const artis_atomic_tables *atomic, const artis_geometry *geom,
+                   const artis_run_params *params);
+void artis_gpu_finalize(void);
+
+/* Upload the per-cell state produced by update_grid for timestep nts and build the engine's per-cell tables
+ * (level populations, cumulative k-packet cooling lists) that replace the per-thread cellhistory
+ * (update_grid.cc:659-761). */
+int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cells);
+
+/* The drop-in for update_packets(my_rank, nts, packets): packets are copied to HBM, propagated to the end of
+ * timestep nts, copied back IN PLACE (same order as given), and estimator sums are ADDED into *est. */
+int artis_gpu_update_packets(int my_rank, int nts, artis_packet *packets, int npkts, artis_estimators *est);
+
+/* --- device-resident path (bench / multi-timestep runs without PCIe traffic) ----------------------------- */
+int artis_gpu_packets_upload(const artis_packet *packets, int npkts);   /* host AoS -> HBM SoA */
+int artis_gpu_packets_download(artis_packet *packets, int npkts);       /* HBM SoA -> host AoS */
+int artis_gpu_packets_snapshot(void);          /* keep a device copy of the current packets */
+int artis_gpu_packets_restore(void);           /* reset packets to the snapshot (device-to-device) */
+int artis_gpu_update_packets_resident(int my_rank, int nts);            /* propagate resident packets */
+int artis_gpu_estimators_zero(void);                                    /* zero the device accumulators */
+int artis_gpu_estimators_download(artis_estimators *est);               /* ADD device sums into *est */
+/* Packed device estimator block (doubles then int64 counters) for an RCCL all-reduce done by the caller:
+ * copy to / from a caller-owned device buffer of artis_gpu_estimator_block_bytes() bytes. */
+size_t artis_gpu_estimator_block_doubles(void);
+int artis_gpu_estimator_block_to_device(void *dst_device);
+int artis_gpu_estimator_block_from_device(const void *src_device);
+
+/* --- timing / introspection --------------------------------------------------------------------------------- */
+/* Milliseconds of the transport kernel(s) of the last update_packets call, measured with HIP events on the
+ * engine's own stream (the stream the kernels run on). */
+double artis_gpu_last_transport_ms(void);
+/* Per-call event counts from the device (steps, lines scanned, kappa evaluations, ...), for the byte model. */
+#define ARTIS_WORK_COUNT 16
+int artis_gpu_last_work_counts(int64_t out[ARTIS_WORK_COUNT]);
+const char *artis_gpu_last_error(void);
+int artis_gpu_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ARTIS_GPU_H */

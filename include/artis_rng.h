@@ -1,0 +1,85 @@
+/*
+ * artis_rng.h -- counter-based per-packet random stream (Philox4x32-10, Salmon et al. SC'11).
+ *
+ * Replaces the reference's per-OpenMP-thread GSL ran3 generator (seeded pre_zseed + 13*rank + 17*tid,
+ * input.cc:1908-1917) whose stream order depends on which thread ran which packet.  Here every packet owns
+ * its stream, keyed by (seed, packet number) with counter (draw index, nts, rank), so any schedule -- one CPU
+ * thread, 64 OpenMP threads, or 10^7 GPU workitems -- draws identical numbers for a packet.  This is what
+ * makes per-packet parity between the oracle and the HIP engine possible.
+ *
+ * Draw semantics follow GSL: uniform() in [0,1) (gsl_rng_uniform) and uniform_pos() in (0,1)
+ * (gsl_rng_uniform_pos, which redraws on 0).  53 random bits per draw.
+ */
+#ifndef ARTIS_RNG_H
+#define ARTIS_RNG_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define ARTIS_HD __host__ __device__ __forceinline__
+#else
+#define ARTIS_HD inline
+#endif
+
+typedef struct artis_rng {
+  uint32_t key0;   /* seed */
+  uint32_t key1;   /* packet number */
+  uint32_t nts;
+  uint32_t rank;
+  uint32_t n;      /* draws so far in this timestep */
+} artis_rng;
+
+ARTIS_HD uint32_t artis_mulhilo32(uint32_t a, uint32_t b, uint32_t *hi) {
+  const uint64_t p = (uint64_t)a * (uint64_t)b;
+  *hi = (uint32_t)(p >> 32);
+  return (uint32_t)p;
+}
+
+ARTIS_HD void artis_philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; r++) {
+    uint32_t hi0, hi1;
+    const uint32_t lo0 = artis_mulhilo32(0xD2511F53u, c[0], &hi0);
+    const uint32_t lo1 = artis_mulhilo32(0xCD9E8D57u, c[2], &hi1);
+    const uint32_t n0 = hi1 ^ c[1] ^ k0;
+    const uint32_t n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0;
+    c[1] = lo1;
+    c[2] = n2;
+    c[3] = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+ARTIS_HD artis_rng artis_rng_init(uint32_t seed, int32_t packet_number, int32_t nts, int32_t rank) {
+  artis_rng s;
+  s.key0 = seed;
+  s.key1 = (uint32_t)packet_number;
+  s.nts = (uint32_t)nts;
+  s.rank = (uint32_t)rank;
+  s.n = 0;
+  return s;
+}
+
+/* 53-bit integer of draw number s->n, then advance */
+ARTIS_HD uint64_t artis_rng_next53(artis_rng *s) {
+  uint32_t c[4] = {s->n, 0x41525453u, s->nts, s->rank};
+  artis_philox4x32_10(c, s->key0, s->key1);
+  s->n++;
+  const uint64_t x = ((uint64_t)c[1] << 32) | (uint64_t)c[0];
+  return x >> 11;
+}
+
+/* gsl_rng_uniform: [0,1) */
+ARTIS_HD double artis_rng_uniform(artis_rng *s) { return (double)artis_rng_next53(s) * (1.0 / 9007199254740992.0); }
+
+/* gsl_rng_uniform_pos: (0,1) */
+ARTIS_HD double artis_rng_uniform_pos(artis_rng *s) {
+  uint64_t x;
+  do {
+    x = artis_rng_next53(s);
+  } while (x == 0);
+  return (double)x * (1.0 / 9007199254740992.0);
+}
+
+#endif /* ARTIS_RNG_H */

@@ -1,0 +1,2023 @@
+// oracle.cc -- CPU restatement of the reference ARTIS packet-propagation hot path.
+//
+// TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+// liboracle.so, and only as the checker / the reported CPU baseline.  The product path (libartis_gpu.so) never
+// links, loads or calls anything here.
+//
+// PARITY STATUS: "parity unpinned".  The reference cannot be built in this image (every hot-path TU includes
+// GSL via sn3d.h:100 and GSL is absent; stand-in headers are not allowed), and its only golden data are md5
+// sums of whole-run outputs that need a network-downloaded atomic dataset (tests/*/results_md5_*.txt,
+// tests/setup_*.sh:7).  This file is a line-by-line restatement of the reference algorithm, each function
+// citing the file:line it follows; it is checked by physics invariants and by exact-answer unit vectors in
+// tests/ (see DESIGN.md "Oracle").
+//
+// Deliberate, documented deviations from the reference (identical in the HIP engine):
+//   D1 RNG: per-packet Philox4x32-10 stream (include/artis_rng.h) instead of per-thread GSL ran3
+//       (input.cc:1908-1917).  Same draw sites, same draw order within a packet.
+//   D2 No relative-1e-4 kappa cache (rpkt.cc:1216-1221): continuum opacity is recomputed at every get_event;
+//       the reference reuses a value computed at a frequency up to 1e-4 away.
+//   D3 select_continuum_nu (ratecoeff.cc:628-684): the tail integrals of alpha_sp_E are computed as sums of
+//       per-piece 4-point Gauss-Legendre integrals instead of repeated GSL qag(GK31, epsrel 1e-2) calls; same
+//       piece grid, same inversion formula.
+//   D4 acounter is recorded for every packet, not only OpenMP thread 0 (rpkt.cc:481-488).
+//   D5 The update_packets pass loop with re-sorting (update_packets.cc:249-330) is flattened: each packet is
+//       advanced to the end of the timestep in one go.  With D2 there is no per-thread state that can change a
+//       packet's history, so the result per packet is identical.
+//   D6 do_kpkt: if the cumulative cooling search lands one past the ion's last term because the update_grid
+//       total and the summed terms differ in the last bits, the last term is taken (the reference aborts,
+//       kpkt.cc:573).
+#include <omp.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "artis_constants.h"
+#include "artis_gpu.h"
+#include "artis_rng.h"
+
+namespace {
+
+struct Ctx {
+  const artis_atomic_tables *at;
+  const artis_geometry *g;
+  const artis_cell_state *cs;
+  artis_run_params rp;
+  double T_step_log;
+};
+
+struct Est {
+  artis_estimators *e;
+  int nelements, maxnions;
+};
+
+// per-thread cellhistory (globals.h:174-208) + rpkt continuum-opacity scratch (globals.h:160-170)
+struct ThreadCache {
+  int cellnumber = -99;
+  std::vector<double> pops;               // [nlevels_total]
+  std::vector<double> departureratios;    // [nbfcontinua]
+  std::vector<double> processrates;       // [nlevels_total * 9], COLDEEXC < 0 => not computed
+  std::vector<double> individ_rad_deexc;  // [sum ndowntrans], same offsets as downtrans
+  std::vector<double> individ_internal_down_same;
+  std::vector<double> individ_internal_up_same;  // [sum nuptrans]
+  std::vector<double> corrphotoioncoeff;          // [nphixstargets total]
+  std::vector<double> cooling_contrib;            // [ncoolingterms]
+  // kappa_rpkt_cont of the current step
+  double kap_total = 0, kap_es = 0, kap_ff = 0, kap_bf = 0, kap_ffheating = 0;
+  std::vector<double> kappa_bf_sum;            // [nbfcontinua]
+  std::vector<double> groundcont_gamma_contr;  // [nbfcontinua_ground]
+  int64_t work[ARTIS_WORK_COUNT] = {0};
+};
+
+// ---------------------------------------------------------------------------------------------- accessors
+inline int uion(const Ctx &c, int element, int ion) { return c.at->elem_uniqueionoffset[element] + ion; }
+inline int ulev(const Ctx &c, int element, int ion, int level) {
+  return c.at->ion_uniqueleveloffset[uion(c, element, ion)] + level;
+}
+inline double epsilon(const Ctx &c, int e, int i, int l) { return c.at->level_epsilon[ulev(c, e, i, l)]; }
+inline double stat_weight(const Ctx &c, int e, int i, int l) { return c.at->level_stat_weight[ulev(c, e, i, l)]; }
+inline int get_nions(const Ctx &c, int e) { return c.at->elem_nions[e]; }
+inline int get_ionstage(const Ctx &c, int e, int i) { return c.at->ion_ionstage[uion(c, e, i)]; }
+inline int get_nlevels(const Ctx &c, int e, int i) { return c.at->ion_nlevels[uion(c, e, i)]; }
+inline int get_ionisinglevels(const Ctx &c, int e, int i) { return c.at->ion_ionisinglevels[uion(c, e, i)]; }
+inline int get_maxrecombininglevel(const Ctx &c, int e, int i) { return c.at->ion_maxrecombininglevel[uion(c, e, i)]; }
+// atomic.cc:408-422
+inline int get_nphixstargets(const Ctx &c, int e, int i, int l) {
+  if (i < get_nions(c, e) - 1 && l < get_ionisinglevels(c, e, i)) return c.at->level_nphixstargets[ulev(c, e, i, l)];
+  return 0;
+}
+inline int get_phixsupperlevel(const Ctx &c, int e, int i, int l, int t) {
+  return c.at->phixstarget_levelindex[c.at->level_phixstargets_offset[ulev(c, e, i, l)] + t];
+}
+inline double get_phixsprobability(const Ctx &c, int e, int i, int l, int t) {
+  return c.at->phixstarget_probability[c.at->level_phixstargets_offset[ulev(c, e, i, l)] + t];
+}
+// atomic.cc:437-453
+inline double get_phixs_threshold(const Ctx &c, int e, int i, int l, int t) {
+  return epsilon(c, e, i + 1, get_phixsupperlevel(c, e, i, l, t)) - epsilon(c, e, i, l);
+}
+inline const float *level_photoion_xs(const Ctx &c, int e, int i, int l) {
+  return c.at->phixs_xs + (size_t)c.at->level_phixstable[ulev(c, e, i, l)] * c.at->nphixspoints;
+}
+// sn3d.h:64-69
+inline int get_bflutindex(const Ctx &c, int tempindex, int e, int i, int l, int t) {
+  const int contindex = -1 - c.at->level_cont_index[ulev(c, e, i, l)] + t;
+  return tempindex * c.at->nbfcontinua + contindex;
+}
+// atomic.cc:16-30
+inline int get_continuumindex(const Ctx &c, int e, int i, int l, int upperionlevel) {
+  int target = -1;
+  for (int t = 0; t < get_nphixstargets(c, e, i, l); t++)
+    if (get_phixsupperlevel(c, e, i, l, t) == upperionlevel) {
+      target = t;
+      break;
+    }
+  if (target < 0) {
+    fprintf(stderr, "oracle: Could not find phixstargetindex\n");
+    abort();
+  }
+  return c.at->level_cont_index[ulev(c, e, i, l)] - target;
+}
+
+inline int cell_mgi(const Ctx &c, int cellindex) { return c.g->cell_mgi[cellindex]; }
+inline int npts_model(const Ctx &c) { return c.g->npts_model; }
+
+// ------------------------------------------------------------------------------------------------ vectors
+// vectors.h:15-75
+inline double vec_len(const double x[3]) { return std::sqrt((x[0] * x[0]) + (x[1] * x[1]) + (x[2] * x[2])); }
+inline void vec_norm(const double in[3], double out[3]) {
+  const double mag = vec_len(in);
+  out[0] = in[0] / mag;
+  out[1] = in[1] / mag;
+  out[2] = in[2] / mag;
+}
+inline double dot(const double x[3], const double y[3]) { return (x[0] * y[0]) + (x[1] * y[1]) + (x[2] * y[2]); }
+inline void get_velocity(const double x[3], double y[3], double t) {
+  y[0] = x[0] / t;
+  y[1] = x[1] / t;
+  y[2] = x[2] / t;
+}
+inline void cross_prod(const double v1[3], const double v2[3], double out[3]) {
+  out[0] = (v1[1] * v2[2]) - (v2[1] * v1[2]);
+  out[1] = (v1[2] * v2[0]) - (v2[2] * v1[0]);
+  out[2] = (v1[0] * v2[1]) - (v2[0] * v1[1]);
+}
+inline void vec_scale(double v[3], double s) {
+  v[0] *= s;
+  v[1] *= s;
+  v[2] *= s;
+}
+inline void vec_copy(double d[3], const double s[3]) {
+  d[0] = s[0];
+  d[1] = s[1];
+  d[2] = s[2];
+}
+// vectors.h:63-79
+inline void angle_ab(const double dir1[3], const double vel[3], double dir2[3]) {
+  const double vsqr = dot(vel, vel) / ARTIS_CLIGHTSQUARED;
+  const double gamma_rel = 1. / std::sqrt(1 - vsqr);
+  const double ndotv = dot(dir1, vel);
+  const double fact1 = gamma_rel * (1 - (ndotv / ARTIS_CLIGHT));
+  const double fact2 = (gamma_rel - (gamma_rel * gamma_rel * ndotv / (gamma_rel + 1) / ARTIS_CLIGHT)) / ARTIS_CLIGHT;
+  for (int d = 0; d < 3; d++) dir2[d] = (dir1[d] - (vel[d] * fact2)) / fact1;
+}
+// vectors.h:81-105
+inline double doppler_nucmf_on_nurf(const Ctx &c, const double dir_rf[3], const double vel_rf[3]) {
+  const double ndotv = dot(dir_rf, vel_rf);
+  double dopplerfactor = 1. - (ndotv / ARTIS_CLIGHT);
+  if (c.rp.relativistic_doppler) {
+    const double betasq = dot(vel_rf, vel_rf) / ARTIS_CLIGHTSQUARED;
+    dopplerfactor = dopplerfactor / std::sqrt(1 - betasq);
+  }
+  return dopplerfactor;
+}
+inline double doppler_packet_nucmf_on_nurf(const Ctx &c, const artis_packet *p) {
+  double v[3] = {0, 0, 0};
+  get_velocity(p->pos, v, p->prop_time);
+  return doppler_nucmf_on_nurf(c, p->dir, v);
+}
+// vectors.h:113-144
+inline void move_pkt(const Ctx &c, artis_packet *p, double distance) {
+  p->pos[0] += (p->dir[0] * distance);
+  p->pos[1] += (p->dir[1] * distance);
+  p->pos[2] += (p->dir[2] * distance);
+  const double dopplerfactor = doppler_packet_nucmf_on_nurf(c, p);
+  p->nu_cmf = p->nu_rf * dopplerfactor;
+  p->e_cmf = p->e_rf * dopplerfactor;
+}
+inline void move_pkt_withtime(const Ctx &c, artis_packet *p, double distance) {
+  const double nu_cmf_old = p->nu_cmf;
+  p->prop_time += distance / ARTIS_CLIGHT_PROP;
+  move_pkt(c, p, distance);
+  if (p->nu_cmf > nu_cmf_old) p->nu_cmf = nu_cmf_old;
+}
+// vectors.cc:43-58
+inline void get_rand_isotropic_unitvec(artis_rng *rng, double out[3]) {
+  const double zrand = artis_rng_uniform(rng);
+  const double zrand2 = artis_rng_uniform(rng);
+  const double mu = -1 + (2. * zrand);
+  const double phi = zrand2 * 2 * ARTIS_PI;
+  const double sintheta = std::sqrt(1. - (mu * mu));
+  out[0] = sintheta * std::cos(phi);
+  out[1] = sintheta * std::sin(phi);
+  out[2] = mu;
+}
+
+// ------------------------------------------------------------------------------------------ populations
+// ltepop.cc:307-327
+double get_groundlevelpop(const Ctx &c, int mgi, int e, int i) {
+  const double nn = c.cs->groundlevelpop[(size_t)mgi * c.at->nions_total + uion(c, e, i)];
+  if (nn < ARTIS_MINPOP) {
+    if (c.cs->elem_abundance[(size_t)mgi * c.at->nelements + e] > 0) return ARTIS_MINPOP;
+    return 0.;
+  }
+  return nn;
+}
+// ltepop.cc:329-347 (T_exc = T_J, artisoptions_classic.h:31)
+double calculate_levelpop_lte(const Ctx &c, int mgi, int e, int i, int l) {
+  if (l == 0) return get_groundlevelpop(c, mgi, e, i);
+  const double T_exc = c.cs->TJ[mgi];
+  const double W = 1.;
+  const double E_level = epsilon(c, e, i, l);
+  const double E_ground = epsilon(c, e, i, 0);
+  const double nnground = get_groundlevelpop(c, mgi, e, i);
+  return (nnground * W * stat_weight(c, e, i, l) / stat_weight(c, e, i, 0) *
+          exp(-(E_level - E_ground) / ARTIS_KB / T_exc));
+}
+// ltepop.cc:417-430 (NLTE_POPS_ON false)
+double calculate_levelpop(const Ctx &c, int mgi, int e, int i, int l) {
+  double nn = calculate_levelpop_lte(c, mgi, e, i, l);
+  if (nn < ARTIS_MINPOP) {
+    if (c.cs->elem_abundance[(size_t)mgi * c.at->nelements + e] > 0)
+      nn = ARTIS_MINPOP;
+    else
+      nn = 0.;
+  }
+  return nn;
+}
+// ltepop.cc:558-564
+double ionstagepop(const Ctx &c, int mgi, int e, int i) {
+  return get_groundlevelpop(c, mgi, e, i) * c.cs->partfunct[(size_t)mgi * c.at->nions_total + uion(c, e, i)] /
+         stat_weight(c, e, i, 0);
+}
+// ltepop.cc:539-556
+double calculate_sahafact(const Ctx &c, int e, int i, int l, int upperionlevel, double T, double E_threshold) {
+  const double g_lower = stat_weight(c, e, i, l);
+  const double g_upper = stat_weight(c, e, i + 1, upperionlevel);
+  return ARTIS_SAHACONST * g_lower / g_upper * pow(T, -1.5) * exp(E_threshold / ARTIS_KB / T);
+}
+
+// update_grid.cc:659-761 cellhistory_reset
+void cellhistory_reset(const Ctx &c, ThreadCache &tc, int mgi) {
+  if (tc.cellnumber == mgi) return;
+  tc.cellnumber = mgi;
+  const artis_atomic_tables &a = *c.at;
+  for (int e = 0; e < a.nelements; e++)
+    for (int i = 0; i < get_nions(c, e); i++)
+      for (int l = 0; l < get_nlevels(c, e, i); l++) tc.pops[ulev(c, e, i, l)] = calculate_levelpop(c, mgi, e, i, l);
+  std::fill(tc.departureratios.begin(), tc.departureratios.end(), -1.);
+  for (int lv = 0; lv < a.nlevels_total; lv++) tc.processrates[(size_t)lv * 9 + ARTIS_MA_ACTION_COLDEEXC] = -99.;
+  std::fill(tc.corrphotoioncoeff.begin(), tc.corrphotoioncoeff.end(), -99.);
+  std::fill(tc.cooling_contrib.begin(), tc.cooling_contrib.end(), -99.);
+}
+inline double get_levelpop(const ThreadCache &tc, const Ctx &c, int e, int i, int l) { return tc.pops[ulev(c, e, i, l)]; }
+
+// ------------------------------------------------------------------------------------------- radfield
+inline double dbb(double nu, double T, double W) {
+  return W * ARTIS_TWOHOVERCLIGHTSQUARED * pow(nu, 3) / expm1(ARTIS_HOVERKB * nu / T);  // radfield.h:44-48
+}
+// radfield.cc:898-943 (MULTIBIN_RADFIELD_MODEL_ON false)
+inline double radfield(const Ctx &c, double nu, int mgi) {
+  const float T_R = c.cs->TR[mgi];
+  const float W = c.cs->W[mgi];
+  return dbb(nu, T_R, W);
+}
+
+// ------------------------------------------------------------------------------------------ photoionisation
+// atomic.cc:87-155
+double photoionization_crosssection_fromtable(const Ctx &c, const float *xs, double nu_edge, double nu) {
+  float sigma_bf;
+  const artis_atomic_tables &a = *c.at;
+  if (a.phixs_file_version == 1) {
+    if (nu == nu_edge) {
+      sigma_bf = xs[0];
+    } else if (nu <= nu_edge * (1 + a.nphixsnuincrement * a.nphixspoints)) {
+      const int i = (int)floor(nu / (a.nphixsnuincrement * nu_edge)) - 10;
+      sigma_bf = xs[i];
+    } else {
+      sigma_bf = xs[a.nphixspoints - 1] * pow(nu_edge * (1 + a.nphixsnuincrement * a.nphixspoints) / nu, 3);
+    }
+    return sigma_bf;
+  }
+  const double ireal = (nu / nu_edge - 1.0) / a.nphixsnuincrement;
+  const int i = (int)floor(ireal);
+  if (i < 0) {
+    sigma_bf = 0.0;
+  } else if (i < a.nphixspoints - 1) {
+    const double sigma_bf_a = xs[i];
+    const double sigma_bf_b = xs[i + 1];
+    const double factor_b = ireal - i;
+    sigma_bf = ((1. - factor_b) * sigma_bf_a) + (factor_b * sigma_bf_b);
+  } else {
+    const double nu_max_phixs = nu_edge * a.last_phixs_nuovernuedge;
+    sigma_bf = xs[a.nphixspoints - 1] * pow(nu_max_phixs / nu, 3);
+  }
+  return sigma_bf;
+}
+
+// ratecoeff.cc:686-710
+double get_spontrecombcoeff(const Ctx &c, int e, int i, int l, int t, float T_e) {
+  const int tablesize = c.at->tablesize;
+  const int lowerindex = (int)floor(log(T_e / c.at->mintemp) / c.T_step_log);
+  if (lowerindex < tablesize - 1) {
+    const int upperindex = lowerindex + 1;
+    const double T_lower = c.at->mintemp * exp(lowerindex * c.T_step_log);
+    const double T_upper = c.at->mintemp * exp(upperindex * c.T_step_log);
+    const double f_upper = c.at->spontrecombcoeff[get_bflutindex(c, upperindex, e, i, l, t)];
+    const double f_lower = c.at->spontrecombcoeff[get_bflutindex(c, lowerindex, e, i, l, t)];
+    return (f_lower + (f_upper - f_lower) / (T_upper - T_lower) * (T_e - T_lower));
+  }
+  return c.at->spontrecombcoeff[get_bflutindex(c, tablesize - 1, e, i, l, t)];
+}
+// ratecoeff.cc:1026-1041
+double interpolate_corrphotoioncoeff(const Ctx &c, int e, int i, int l, int t, double T) {
+  const int tablesize = c.at->tablesize;
+  const int lowerindex = (int)floor(log(T / c.at->mintemp) / c.T_step_log);
+  if (lowerindex < tablesize - 1) {
+    const int upperindex = lowerindex + 1;
+    const double T_lower = c.at->mintemp * exp(lowerindex * c.T_step_log);
+    const double T_upper = c.at->mintemp * exp(upperindex * c.T_step_log);
+    const double f_upper = c.at->corrphotoioncoeff[get_bflutindex(c, upperindex, e, i, l, t)];
+    const double f_lower = c.at->corrphotoioncoeff[get_bflutindex(c, lowerindex, e, i, l, t)];
+    return (f_lower + (f_upper - f_lower) / (T_upper - T_lower) * (T - T_lower));
+  }
+  return c.at->corrphotoioncoeff[get_bflutindex(c, tablesize - 1, e, i, l, t)];
+}
+// ratecoeff.cc:1247-1308 (LUT path; cached per thread like cellhistory chphixstargets)
+double get_corrphotoioncoeff(const Ctx &c, ThreadCache &tc, int e, int i, int l, int t, int mgi) {
+  const int slot = c.at->level_phixstargets_offset[ulev(c, e, i, l)] + t;
+  double gammacorr = tc.corrphotoioncoeff[slot];
+  if (gammacorr < 0) {
+    const double W = c.cs->W[mgi];
+    const double T_R = c.cs->TR[mgi];
+    gammacorr = W * interpolate_corrphotoioncoeff(c, e, i, l, t, T_R);
+    const int index_in_groundlevelcontestimator = c.at->level_closestgroundlevelcont[ulev(c, e, i, l)];
+    if (index_in_groundlevelcontestimator >= 0)
+      gammacorr *= c.cs->corrphotoionrenorm[(size_t)mgi * c.at->nelements * c.at->maxnions +
+                                            index_in_groundlevelcontestimator];
+    tc.corrphotoioncoeff[slot] = gammacorr;
+  }
+  return gammacorr;
+}
+// kpkt.cc:69-82
+double get_bfcoolingcoeff(const Ctx &c, int e, int i, int l, int t, float T_e) {
+  const int tablesize = c.at->tablesize;
+  const int lowerindex = (int)floor(log(T_e / c.at->mintemp) / c.T_step_log);
+  if (lowerindex < tablesize - 1) {
+    const int upperindex = lowerindex + 1;
+    const double T_lower = c.at->mintemp * exp(lowerindex * c.T_step_log);
+    const double T_upper = c.at->mintemp * exp(upperindex * c.T_step_log);
+    const double f_upper = c.at->bfcooling_coeff[get_bflutindex(c, upperindex, e, i, l, t)];
+    const double f_lower = c.at->bfcooling_coeff[get_bflutindex(c, lowerindex, e, i, l, t)];
+    return (f_lower + (f_upper - f_lower) / (T_upper - T_lower) * (T_e - T_lower));
+  }
+  return c.at->bfcooling_coeff[get_bflutindex(c, tablesize - 1, e, i, l, t)];
+}
+
+// ratecoeff.cc:263-279 alpha_sp_E_integrand_gsl
+inline double alpha_sp_E_integrand(const Ctx &c, const float *xs, double nu_edge, float T, double nu) {
+  const float sigma_bf = (float)photoionization_crosssection_fromtable(c, xs, nu_edge, nu);
+  return ARTIS_TWOOVERCLIGHTSQUARED * sigma_bf * pow(nu, 3) / nu_edge * exp(-ARTIS_HOVERKB * nu / T);
+}
+// ratecoeff.cc:628-684 select_continuum_nu, with deviation D3 (piecewise Gauss-Legendre tail integrals)
+double select_continuum_nu(const Ctx &c, artis_rng *rng, int e, int lowerion, int lower, int upperionlevel,
+                           float T_e) {
+  int target = -1;
+  for (int t = 0; t < get_nphixstargets(c, e, lowerion, lower); t++)
+    if (get_phixsupperlevel(c, e, lowerion, lower, t) == upperionlevel) {
+      target = t;
+      break;
+    }
+  const double E_threshold = get_phixs_threshold(c, e, lowerion, lower, target);
+  const double nu_threshold = ARTIS_ONEOVERH * E_threshold;
+  const double nu_max_phixs = nu_threshold * c.at->last_phixs_nuovernuedge;
+  const int npieces = c.at->nphixspoints;
+  const float *xs = level_photoion_xs(c, e, lowerion, lower);
+  const double zrand = 1. - artis_rng_uniform(rng);
+  const double deltanu = (nu_max_phixs - nu_threshold) / npieces;
+  // piece integrals, 4-point Gauss-Legendre
+  static const double gx[4] = {-0.8611363115940526, -0.3399810435848563, 0.3399810435848563, 0.8611363115940526};
+  static const double gw[4] = {0.3478548451374538, 0.6521451548625461, 0.6521451548625461, 0.3478548451374538};
+  std::vector<double> piece(npieces);
+  for (int j = 0; j < npieces; j++) {
+    const double a = nu_threshold + j * deltanu;
+    const double half = 0.5 * deltanu;
+    const double mid = a + half;
+    double s = 0.;
+    for (int k = 0; k < 4; k++) s += gw[k] * alpha_sp_E_integrand(c, xs, nu_threshold, T_e, mid + half * gx[k]);
+    piece[j] = s * half;
+  }
+  // tail[i] = integral from nu_threshold + i*deltanu to nu_max_phixs (summed from the top)
+  std::vector<double> tail(npieces + 1);
+  tail[npieces] = 0.;
+  for (int j = npieces - 1; j >= 0; j--) tail[j] = tail[j + 1] + piece[j];
+  const double total_alpha_sp = tail[0];
+  double alpha_sp_old = total_alpha_sp;
+  double alpha_sp = total_alpha_sp;
+  int i;
+  for (i = 1; i < npieces; i++) {
+    alpha_sp_old = alpha_sp;
+    alpha_sp = tail[i];
+    if (zrand >= alpha_sp / total_alpha_sp) break;
+  }
+  const double nuoffset = (total_alpha_sp * zrand - alpha_sp_old) / (alpha_sp - alpha_sp_old) * deltanu;
+  return nu_threshold + (i - 1) * deltanu + nuoffset;
+}
+
+// -------------------------------------------------------------------------------------------- rate coeffs
+// macroatom.h:52-105
+double col_deexcitation_ratecoeff(const Ctx &c, float T_e, float nne, double epsilon_trans, int li, double lowerstatweight,
+                                  double upperstatweight) {
+  double C = 0.;
+  const double coll_str_thisline = c.at->line_coll_str[li];
+  if (coll_str_thisline < 0) {
+    if (!c.at->line_forbidden[li]) {
+      const double eoverkt = epsilon_trans / (ARTIS_KB * T_e);
+      const double g_bar = 0.2;
+      const double gauntfac =
+          (eoverkt > 0.33421) ? g_bar : 0.276 * std::exp(eoverkt) * (-0.5772156649 - std::log(eoverkt));
+      const double g_ratio = lowerstatweight / upperstatweight;
+      C = ARTIS_C_0 * 14.51039491 * nne * std::sqrt(T_e) * c.at->line_osc_strength[li] *
+          std::pow(ARTIS_H_IONPOT / epsilon_trans, 2) * eoverkt * g_ratio * gauntfac;
+    } else {
+      C = nne * 8.629e-6 * 0.01 * lowerstatweight / std::sqrt(T_e);
+    }
+  } else {
+    C = nne * 8.629e-6 * coll_str_thisline / upperstatweight / std::sqrt(T_e);
+  }
+  return C;
+}
+// macroatom.h:107-150
+double col_excitation_ratecoeff(const Ctx &c, float T_e, float nne, int li, double epsilon_trans, double lowerstatweight,
+                                double upperstatweight) {
+  double C = 0.;
+  const double coll_strength = c.at->line_coll_str[li];
+  const double eoverkt = epsilon_trans / (ARTIS_KB * T_e);
+  if (coll_strength < 0) {
+    if (!c.at->line_forbidden[li]) {
+      const double g_bar = 0.2;
+      const double exp_eoverkt = exp(eoverkt);
+      const double test = 0.276 * exp_eoverkt * (-0.5772156649 - std::log(eoverkt));
+      const double Gamma = g_bar > test ? g_bar : test;
+      C = ARTIS_C_0 * nne * std::sqrt(T_e) * 14.51039491 * c.at->line_osc_strength[li] *
+          pow(ARTIS_H_IONPOT / epsilon_trans, 2) * eoverkt / exp_eoverkt * Gamma;
+    } else {
+      C = nne * 8.629e-6 * 0.01 * std::exp(-eoverkt) * upperstatweight / std::sqrt(T_e);
+    }
+  } else {
+    C = nne * 8.629e-6 * coll_strength * std::exp(-eoverkt) / lowerstatweight / std::sqrt(T_e);
+  }
+  return C;
+}
+// macroatom.cc:503-548
+double rad_deexcitation_ratecoeff(const Ctx &c, const ThreadCache &tc, int e, int i, int upper, int lower,
+                                  double epsilon_trans, int li, double t_current) {
+  const double n_u = get_levelpop(tc, c, e, i, upper);
+  const double n_l = get_levelpop(tc, c, e, i, lower);
+  double R = 0.0;
+  const double nu_trans = epsilon_trans / ARTIS_H;
+  const double A_ul = c.at->line_einstein_A[li];
+  const double B_ul = ARTIS_CLIGHTSQUAREDOVERTWOH / std::pow(nu_trans, 3) * A_ul;
+  const double B_lu = stat_weight(c, e, i, upper) / stat_weight(c, e, i, lower) * B_ul;
+  const double tau_sobolev = (B_lu * n_l - B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_current;
+  if (tau_sobolev > 1e-100) {
+    const double beta = 1.0 / tau_sobolev * (-std::expm1(-tau_sobolev));
+    R = A_ul * beta;
+  } else {
+    R = 0.0;
+  }
+  return R;
+}
+// macroatom.cc:550-643
+double rad_excitation_ratecoeff(const Ctx &c, const ThreadCache &tc, int mgi, int e, int i, int lower, int upper,
+                                double epsilon_trans, int li, double t_current) {
+  const double n_u = get_levelpop(tc, c, e, i, upper);
+  const double n_l = get_levelpop(tc, c, e, i, lower);
+  double R = 0.0;
+  const double nu_trans = epsilon_trans / ARTIS_H;
+  const double A_ul = c.at->line_einstein_A[li];
+  const double B_ul = ARTIS_CLIGHTSQUAREDOVERTWOH / pow(nu_trans, 3) * A_ul;
+  const double B_lu = stat_weight(c, e, i, upper) / stat_weight(c, e, i, lower) * B_ul;
+  const double tau_sobolev = (B_lu * n_l - B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_current;
+  if (tau_sobolev > 1e-100) {
+    const double beta = 1.0 / tau_sobolev * (-expm1(-tau_sobolev));
+    const double R_over_J_nu = n_l > 0. ? (B_lu - B_ul * n_u / n_l) * beta : B_lu * beta;
+    R = R_over_J_nu * radfield(c, nu_trans, mgi);
+  } else {
+    R = 0.;
+  }
+  if (R < 0 || !std::isfinite(R)) {
+    fprintf(stderr, "oracle: rad_excitation_ratecoeff invalid R %g\n", R);
+    abort();
+  }
+  return R;
+}
+// macroatom.cc:645-678
+double rad_recombination_ratecoeff(const Ctx &c, float T_e, float nne, int e, int upperion, int upper, int lower) {
+  double R = 0.0;
+  const int nt = get_nphixstargets(c, e, upperion - 1, lower);
+  for (int t = 0; t < nt; t++) {
+    if (get_phixsupperlevel(c, e, upperion - 1, lower, t) == upper) {
+      R = nne * get_spontrecombcoeff(c, e, upperion - 1, lower, t, T_e);
+      break;
+    }
+  }
+  return R;
+}
+// macroatom.cc:704-743
+double col_recombination_ratecoeff(const Ctx &c, int mgi, int e, int upperion, int upper, int lower, double epsilon_trans) {
+  const int nt = get_nphixstargets(c, e, upperion - 1, lower);
+  for (int t = 0; t < nt; t++) {
+    if (get_phixsupperlevel(c, e, upperion - 1, lower, t) == upper) {
+      const float nne = c.cs->nne[mgi];
+      const float T_e = c.cs->Te[mgi];
+      const double fac1 = epsilon_trans / ARTIS_KB / T_e;
+      const int ionstage = get_ionstage(c, e, upperion);
+      double g;
+      if (ionstage - 1 == 1)
+        g = 0.1;
+      else if (ionstage - 1 == 2)
+        g = 0.2;
+      else
+        g = 0.3;
+      const double sigma_bf = (level_photoion_xs(c, e, upperion - 1, lower)[0] *
+                               get_phixsprobability(c, e, upperion - 1, lower, t));
+      const double sf = calculate_sahafact(c, e, upperion - 1, lower, upper, T_e, epsilon_trans);
+      return nne * nne * sf * 1.55e13 * pow(T_e, -0.5) * g * sigma_bf * exp(-fac1) / fac1;
+    }
+  }
+  return 0.;
+}
+// macroatom.cc:745-776
+double col_ionization_ratecoeff(const Ctx &c, float T_e, float nne, int e, int i, int lower, int t, double epsilon_trans) {
+  double g;
+  const int ionstage = get_ionstage(c, e, i);
+  if (ionstage == 1)
+    g = 0.1;
+  else if (ionstage == 2)
+    g = 0.2;
+  else
+    g = 0.3;
+  const double fac1 = epsilon_trans / ARTIS_KB / T_e;
+  const double sigma_bf = level_photoion_xs(c, e, i, lower)[0] * get_phixsprobability(c, e, i, lower, t);
+  return nne * 1.55e13 * pow(T_e, -0.5) * g * sigma_bf * exp(-fac1) / fac1;
+}
+
+// --------------------------------------------------------------------------------------------- estimators
+inline void safeadd(double *p, double v) {
+#pragma omp atomic update
+  *p += v;
+}
+inline void counter_inc(Est &E, int ctr) {
+#pragma omp atomic update
+  E.e->counters[ctr] += 1;
+}
+
+// ---------------------------------------------------------------------------------------------- emission
+// rpkt.cc:975-1025
+void emitt_rpkt(const Ctx &c, artis_rng *rng, artis_packet *p) {
+  p->type = ARTIS_TYPE_RPKT;
+  p->last_cross = ARTIS_NONE;
+  double dir_cmf[3];
+  get_rand_isotropic_unitvec(rng, dir_cmf);
+  double vel_vec[3];
+  get_velocity(p->pos, vel_vec, -1. * p->prop_time);
+  angle_ab(dir_cmf, vel_vec, p->dir);
+  const double dopplerfactor = doppler_packet_nucmf_on_nurf(c, p);
+  p->nu_rf = p->nu_cmf / dopplerfactor;
+  p->e_rf = p->e_cmf / dopplerfactor;
+  p->stokes[0] = 1.;
+  p->stokes[1] = 0.;
+  p->stokes[2] = 0.;
+  double dummy_dir[3] = {0., 0., 1.};
+  cross_prod(p->dir, dummy_dir, p->pol_dir);
+  if ((dot(p->pol_dir, p->pol_dir)) < 1.e-8) {
+    dummy_dir[0] = dummy_dir[2] = 0.0;
+    dummy_dir[1] = 1.0;
+    cross_prod(p->dir, dummy_dir, p->pol_dir);
+  }
+  vec_norm(p->pol_dir, p->pol_dir);
+}
+
+// vpkt.cc:898-929
+double rot_angle(const double n1[3], const double n2[3], const double ref1[3], const double ref2[3]) {
+  double i = 0;
+  double ref1_sc[3];
+  ref1_sc[0] = n1[0] * dot(n1, n2) - n2[0];
+  ref1_sc[1] = n1[1] * dot(n1, n2) - n2[1];
+  ref1_sc[2] = n1[2] * dot(n1, n2) - n2[2];
+  vec_norm(ref1_sc, ref1_sc);
+  double cos_stokes_rot_1 = dot(ref1_sc, ref1);
+  const double cos_stokes_rot_2 = dot(ref1_sc, ref2);
+  if (cos_stokes_rot_1 < -1) cos_stokes_rot_1 = -1;
+  if (cos_stokes_rot_1 > 1) cos_stokes_rot_1 = 1;
+  if ((cos_stokes_rot_1 > 0) && (cos_stokes_rot_2 > 0)) i = acos(cos_stokes_rot_1);
+  if ((cos_stokes_rot_1 > 0) && (cos_stokes_rot_2 < 0)) i = 2 * acos(-1.) - acos(cos_stokes_rot_1);
+  if ((cos_stokes_rot_1 < 0) && (cos_stokes_rot_2 < 0)) i = acos(-1.) + acos(fabs(cos_stokes_rot_1));
+  if ((cos_stokes_rot_1 < 0) && (cos_stokes_rot_2 > 0)) i = acos(-1.) - acos(fabs(cos_stokes_rot_1));
+  if (cos_stokes_rot_1 == 0) i = acos(-1.) / 2.;
+  if (cos_stokes_rot_2 == 0) i = 0.0;
+  return i;
+}
+// vpkt.cc:932-944
+void meridian(const double n[3], double ref1[3], double ref2[3]) {
+  ref1[0] = -1. * n[0] * n[2] / sqrt(n[0] * n[0] + n[1] * n[1]);
+  ref1[1] = -1. * n[1] * n[2] / sqrt(n[0] * n[0] + n[1] * n[1]);
+  ref1[2] = (1 - (n[2] * n[2])) / sqrt(n[0] * n[0] + n[1] * n[1]);
+  ref2[0] = n[2] * ref1[1] - n[1] * ref1[2];
+  ref2[1] = n[0] * ref1[2] - n[2] * ref1[0];
+  ref2[2] = n[1] * ref1[0] - n[0] * ref1[1];
+}
+// vpkt.cc:1022-1069
+void lorentz(const double e_rf[3], const double n_rf[3], const double v[3], double e_cmf[3]) {
+  double beta[3], e_par[3], e_perp[3], b_rf[3], b_par[3], b_perp[3], v_cr_b[3], v_cr_e[3], b_cmf[3];
+  beta[0] = v[0] / ARTIS_CLIGHT;
+  beta[1] = v[1] / ARTIS_CLIGHT;
+  beta[2] = v[2] / ARTIS_CLIGHT;
+  const double vsqr = dot(beta, beta);
+  const double gamma_rel = 1. / (sqrt(1 - vsqr));
+  const double edb = (e_rf[0] * beta[0] + e_rf[1] * beta[1] + e_rf[2] * beta[2]);
+  e_par[0] = edb * beta[0] / (vsqr);
+  e_par[1] = edb * beta[1] / (vsqr);
+  e_par[2] = edb * beta[2] / (vsqr);
+  e_perp[0] = e_rf[0] - e_par[0];
+  e_perp[1] = e_rf[1] - e_par[1];
+  e_perp[2] = e_rf[2] - e_par[2];
+  b_rf[0] = n_rf[1] * e_rf[2] - n_rf[2] * e_rf[1];
+  b_rf[1] = n_rf[2] * e_rf[0] - n_rf[0] * e_rf[2];
+  b_rf[2] = n_rf[0] * e_rf[1] - n_rf[1] * e_rf[0];
+  const double bdb = (b_rf[0] * beta[0] + b_rf[1] * beta[1] + b_rf[2] * beta[2]);
+  b_par[0] = bdb * beta[0] / (vsqr);
+  b_par[1] = bdb * beta[1] / (vsqr);
+  b_par[2] = bdb * beta[2] / (vsqr);
+  b_perp[0] = b_rf[0] - b_par[0];
+  b_perp[1] = b_rf[1] - b_par[1];
+  b_perp[2] = b_rf[2] - b_par[2];
+  v_cr_b[0] = beta[1] * b_rf[2] - beta[2] * b_rf[1];
+  v_cr_b[1] = beta[2] * b_rf[0] - beta[0] * b_rf[2];
+  v_cr_b[2] = beta[0] * b_rf[1] - beta[1] * b_rf[0];
+  v_cr_e[0] = beta[1] * e_rf[2] - beta[2] * e_rf[1];
+  v_cr_e[1] = beta[2] * e_rf[0] - beta[0] * e_rf[2];
+  v_cr_e[2] = beta[0] * e_rf[1] - beta[1] * e_rf[0];
+  e_cmf[0] = e_par[0] + gamma_rel * (e_perp[0] + v_cr_b[0]);
+  e_cmf[1] = e_par[1] + gamma_rel * (e_perp[1] + v_cr_b[1]);
+  e_cmf[2] = e_par[2] + gamma_rel * (e_perp[2] + v_cr_b[2]);
+  b_cmf[0] = b_par[0] + gamma_rel * (b_perp[0] - v_cr_e[0]);
+  b_cmf[1] = b_par[1] + gamma_rel * (b_perp[1] - v_cr_e[1]);
+  b_cmf[2] = b_par[2] + gamma_rel * (b_perp[2] - v_cr_e[2]);
+  vec_norm(e_cmf, e_cmf);
+  vec_norm(b_cmf, b_cmf);
+}
+// vpkt.cc:947-1019
+void frame_transform(const double n_rf[3], double *Q, double *U, const double v[3], double n_cmf[3]) {
+  double ref1[3], ref2[3], e_rf[3], e_cmf[3];
+  double theta_rot = 0.;
+  meridian(n_rf, ref1, ref2);
+  const double Q0 = *Q;
+  const double U0 = *U;
+  const double p = sqrt(Q0 * Q0 + U0 * U0);
+  double rot_angle_ = 0;
+  if (p > 0) {
+    const double cos2rot_angle = Q0 / p;
+    const double sin2rot_angle = U0 / p;
+    if ((cos2rot_angle > 0) && (sin2rot_angle > 0)) rot_angle_ = acos(Q0 / p) / 2.;
+    if ((cos2rot_angle < 0) && (sin2rot_angle > 0)) rot_angle_ = (acos(-1.) - acos(fabs(Q0 / p))) / 2.;
+    if ((cos2rot_angle < 0) && (sin2rot_angle < 0)) rot_angle_ = (acos(-1.) + acos(fabs(Q0 / p))) / 2.;
+    if ((cos2rot_angle > 0) && (sin2rot_angle < 0)) rot_angle_ = (2. * acos(-1.) - acos(fabs(Q0 / p))) / 2.;
+    if (cos2rot_angle == 0) {
+      rot_angle_ = 0.25 * acos(-1);
+      if (U0 < 0) rot_angle_ = 0.75 * acos(-1);
+    }
+    if (sin2rot_angle == 0) {
+      rot_angle_ = 0.0;
+      if (Q0 < 0) rot_angle_ = 0.5 * acos(-1);
+    }
+  }
+  e_rf[0] = cos(rot_angle_) * ref1[0] - sin(rot_angle_) * ref2[0];
+  e_rf[1] = cos(rot_angle_) * ref1[1] - sin(rot_angle_) * ref2[1];
+  e_rf[2] = cos(rot_angle_) * ref1[2] - sin(rot_angle_) * ref2[2];
+  angle_ab(n_rf, v, n_cmf);
+  lorentz(e_rf, n_rf, v, e_cmf);
+  meridian(n_cmf, ref1, ref2);
+  const double e_cmf_ref1 = e_cmf[0] * ref1[0] + e_cmf[1] * ref1[1] + e_cmf[2] * ref1[2];
+  const double e_cmf_ref2 = e_cmf[0] * ref2[0] + e_cmf[1] * ref2[1] + e_cmf[2] * ref2[2];
+  if ((e_cmf_ref1 > 0) && (e_cmf_ref2 < 0)) theta_rot = acos(e_cmf_ref1);
+  if ((e_cmf_ref1 < 0) && (e_cmf_ref2 < 0)) theta_rot = acos(-1.) - acos(fabs(e_cmf_ref1));
+  if ((e_cmf_ref1 < 0) && (e_cmf_ref2 > 0)) theta_rot = acos(-1.) + acos(fabs(e_cmf_ref1));
+  if ((e_cmf_ref1 > 0) && (e_cmf_ref2 > 0)) theta_rot = 2 * acos(-1.) - acos(e_cmf_ref1);
+  if (e_cmf_ref1 == 0) theta_rot = acos(-1.) / 2.;
+  if (e_cmf_ref2 == 0) theta_rot = 0.0;
+  if (e_cmf_ref1 > 1) theta_rot = 0.0;
+  if (e_cmf_ref1 < -1) theta_rot = acos(-1.);
+  *Q = cos(2 * theta_rot) * p;
+  *U = sin(2 * theta_rot) * p;
+}
+
+// polarization.cc:6-157
+void escat_rpkt(const Ctx &c, artis_rng *rng, artis_packet *p) {
+  p->type = ARTIS_TYPE_RPKT;
+  p->last_cross = ARTIS_NONE;
+  double vel_vec[3];
+  get_velocity(p->pos, vel_vec, p->prop_time);
+  double Qi = p->stokes[1];
+  double Ui = p->stokes[2];
+  double old_dir_cmf[3];
+  frame_transform(p->dir, &Qi, &Ui, vel_vec, old_dir_cmf);
+  double M = 0., mu = 0., phisc = 0.;
+  if (c.rp.pol_dipole) {
+    double pr = 0., x = 0.;
+    do {
+      const double zrand = artis_rng_uniform(rng);
+      const double zrand2 = artis_rng_uniform(rng);
+      const double zrand3 = artis_rng_uniform(rng);
+      M = 2 * zrand - 1;
+      mu = pow(M, 2.);
+      phisc = 2 * ARTIS_PI * zrand2;
+      pr = (mu + 1) + (mu - 1) * (cos(2 * phisc) * Qi + sin(2 * phisc) * Ui);
+      x = 2 * zrand3;
+    } while (x > pr);
+  } else {
+    const double zrand = artis_rng_uniform(rng);
+    const double zrand2 = artis_rng_uniform(rng);
+    M = 2. * zrand - 1;
+    mu = pow(M, 2.);
+    phisc = 2 * ARTIS_PI * zrand2;
+  }
+  const double tsc = acos(M);
+  double new_dir_cmf[3];
+  if (fabs(old_dir_cmf[2]) < 0.99999) {
+    new_dir_cmf[0] = sin(tsc) / sqrt(1. - pow(old_dir_cmf[2], 2.)) *
+                         (old_dir_cmf[1] * sin(phisc) - old_dir_cmf[0] * old_dir_cmf[2] * cos(phisc)) +
+                     old_dir_cmf[0] * cos(tsc);
+    new_dir_cmf[1] = sin(tsc) / sqrt(1 - pow(old_dir_cmf[2], 2.)) *
+                         (-old_dir_cmf[0] * sin(phisc) - old_dir_cmf[1] * old_dir_cmf[2] * cos(phisc)) +
+                     old_dir_cmf[1] * cos(tsc);
+    new_dir_cmf[2] = sin(tsc) * cos(phisc) * sqrt(1 - pow(old_dir_cmf[2], 2.)) + old_dir_cmf[2] * cos(tsc);
+  } else {
+    new_dir_cmf[0] = sin(tsc) * cos(phisc);
+    new_dir_cmf[1] = sin(tsc) * sin(phisc);
+    new_dir_cmf[2] = (old_dir_cmf[2] > 0) ? cos(tsc) : -cos(tsc);
+  }
+  double ref1[3], ref2[3];
+  meridian(old_dir_cmf, ref1, ref2);
+  const double i1 = rot_angle(old_dir_cmf, new_dir_cmf, ref1, ref2);
+  const double cos2i1 = cos(2 * i1);
+  const double sin2i1 = sin(2 * i1);
+  const double Qold = Qi * cos2i1 - Ui * sin2i1;
+  const double Uold = Qi * sin2i1 + Ui * cos2i1;
+  mu = dot(old_dir_cmf, new_dir_cmf);
+  const double Inew = 0.75 * ((mu * mu + 1.0) + Qold * (mu * mu - 1.0));
+  double Qnew = 0.75 * ((mu * mu - 1.0) + Qold * (mu * mu + 1.0));
+  double Unew = 1.5 * mu * Uold;
+  Qnew = Qnew / Inew;
+  Unew = Unew / Inew;
+  const double I = 1.0;
+  meridian(new_dir_cmf, ref1, ref2);
+  const double i2 = ARTIS_PI + rot_angle(new_dir_cmf, old_dir_cmf, ref1, ref2);
+  const double cos2i2 = cos(2 * i2);
+  const double sin2i2 = sin(2 * i2);
+  double Q = Qnew * cos2i2 + Unew * sin2i2;
+  double U = -Qnew * sin2i2 + Unew * cos2i2;
+  double vel_rev[3] = {-vel_vec[0], -vel_vec[1], -vel_vec[2]};
+  double dummy_dir[3];
+  frame_transform(new_dir_cmf, &Q, &U, vel_rev, dummy_dir);
+  p->stokes[0] = I;
+  p->stokes[1] = Q;
+  p->stokes[2] = U;
+  p->dir[0] = dummy_dir[0];
+  p->dir[1] = dummy_dir[1];
+  p->dir[2] = dummy_dir[2];
+  const double dopplerfactor = doppler_packet_nucmf_on_nurf(c, p);
+  p->nu_rf = p->nu_cmf / dopplerfactor;
+  p->e_rf = p->e_cmf / dopplerfactor;
+}
+
+// ------------------------------------------------------------------------------------------------ boundary
+// boundary.cc:101-330 (GRID_UNIFORM)
+double boundary_cross(const Ctx &c, Est &E, artis_packet *p, int *snext) {
+  const double tstart = p->prop_time;
+  const int cellindex = p->where;
+  const double tmin = c.g->tmin;
+  const int n[3] = {c.g->ncoordgrid[0], c.g->ncoordgrid[1], c.g->ncoordgrid[2]};
+  const int stride[3] = {1, n[0], n[0] * n[1]};
+  const double wid = 2 * c.g->coordmax[0] / n[0];  // grid.cc:76-91
+  double initpos[3], cellcoordmax[3], cellcoordmin[3], vel[3];
+  int pointnum[3];
+  for (int d = 0; d < 3; d++) {
+    initpos[d] = p->pos[d];
+    cellcoordmin[d] = c.g->cell_pos_min[(size_t)cellindex * 3 + d];
+    cellcoordmax[d] = cellcoordmin[d] + wid;
+    vel[d] = p->dir[d] * ARTIS_CLIGHT_PROP;
+  }
+  pointnum[0] = cellindex % n[0];
+  pointnum[1] = (cellindex / n[0]) % n[1];
+  pointnum[2] = (cellindex / (n[0] * n[1])) % n[2];
+  int last_cross = p->last_cross;
+  const int negdirections[3] = {ARTIS_NEG_X, ARTIS_NEG_Y, ARTIS_NEG_Z};
+  const int posdirections[3] = {ARTIS_POS_X, ARTIS_POS_Y, ARTIS_POS_Z};
+  for (int d = 0; d < 3; d++) {
+    for (int flip = 0; flip < 2; flip++) {
+      const int direction = flip ? posdirections[d] : negdirections[d];
+      const int invdirection = !flip ? posdirections[d] : negdirections[d];
+      const int cellindexstride = flip ? -stride[d] : stride[d];
+      bool isoutside_thisside;
+      if (flip)
+        isoutside_thisside = initpos[d] < (cellcoordmin[d] / tmin * tstart - 10.);
+      else
+        isoutside_thisside = initpos[d] > (cellcoordmax[d] / tmin * tstart + 10.);
+      if (isoutside_thisside && (last_cross != direction)) {
+        if ((vel[d] - (initpos[d] / tstart)) > 0) {
+          if ((pointnum[d] == (n[d] - 1) && cellindexstride > 0) || (pointnum[d] == 0 && cellindexstride < 0)) {
+            *snext = -99;
+            return 0;
+          } else {
+            *snext = p->where + cellindexstride;
+            p->last_cross = invdirection;
+            return 0;
+          }
+        } else {
+          last_cross = direction;
+        }
+      }
+    }
+  }
+  double t_coordmaxboundary[3], t_coordminboundary[3];
+  for (int d = 0; d < 3; d++) {
+    t_coordmaxboundary[d] = ((initpos[d] - (vel[d] * tstart)) / ((cellcoordmax[d]) - (vel[d] * tmin)) * tmin) - tstart;
+    t_coordminboundary[d] = ((initpos[d] - (vel[d] * tstart)) / ((cellcoordmin[d]) - (vel[d] * tmin)) * tmin) - tstart;
+  }
+  int choice = 0;
+  double time = 1.e99;
+  for (int d = 0; d < 3; d++) {
+    if ((t_coordmaxboundary[d] > 0) && (t_coordmaxboundary[d] < time) && (last_cross != negdirections[d])) {
+      choice = posdirections[d];
+      time = t_coordmaxboundary[d];
+      if (pointnum[d] == (n[d] - 1)) {
+        *snext = -99;
+      } else {
+        *snext = p->where + stride[d];
+        p->last_cross = posdirections[d];
+      }
+    }
+    if ((t_coordminboundary[d] > 0) && (t_coordminboundary[d] < time) && (last_cross != posdirections[d])) {
+      choice = negdirections[d];
+      time = t_coordminboundary[d];
+      if (pointnum[d] == 0) {
+        *snext = -99;
+      } else {
+        *snext = p->where - stride[d];
+        p->last_cross = negdirections[d];
+      }
+    }
+  }
+  (void)choice;
+  (void)E;
+  return ARTIS_CLIGHT_PROP * time;
+}
+// boundary.cc:332-357
+void change_cell(Est &E, artis_packet *p, int snext) {
+  if (snext == -99) {
+    p->escape_type = p->type;
+    p->escape_time = (int)p->prop_time;
+    p->type = ARTIS_TYPE_ESCAPE;
+#pragma omp atomic update
+    E.e->nesc += 1;
+  } else {
+    p->where = snext;
+    counter_inc(E, CTR_CELLCROSSINGS);
+  }
+}
+
+// --------------------------------------------------------------------------------------- continuum opacity
+// rpkt.cc:1027-1073
+double calculate_kappa_ff(const Ctx &c, int mgi, double nu) {
+  const double g_ff = 1;
+  const float nne = c.cs->nne[mgi];
+  const float T_e = c.cs->Te[mgi];
+  double kappa_ff = 0.;
+  for (int e = 0; e < c.at->nelements; e++)
+    for (int i = 0; i < get_nions(c, e); i++) {
+      const double nnion = ionstagepop(c, mgi, e, i);
+      const int Z = get_ionstage(c, e, i) - 1;
+      if (Z > 0) kappa_ff += Z * Z * g_ff * nnion;
+    }
+  kappa_ff *= 3.69255e8 / sqrt(T_e) * pow(nu, -3) * nne * (1 - exp(-ARTIS_HOVERKB * nu / T_e));
+  return kappa_ff;
+}
+// rpkt.cc:1075-1207 (SEPARATE_STIMRECOMB false, DETAILED_BF_ESTIMATORS_ON false, LUT photoion)
+double calculate_kappa_bf_gammacontr(const Ctx &c, ThreadCache &tc, int mgi, double nu) {
+  double kappa_bf_sum = 0.;
+  const artis_atomic_tables &a = *c.at;
+  for (int g = 0; g < a.nbfcontinua_ground; g++) tc.groundcont_gamma_contr[g] = 0.;
+  const double T_e = c.cs->Te[mgi];
+  const double nne = c.cs->nne[mgi];
+  const double nnetot = c.cs->nnetot[mgi];
+  int i = 0;
+  const int nbfcontinua = a.nbfcontinua;
+  for (i = 0; i < nbfcontinua; i++) {
+    const int element = a.allcont_element[i];
+    const int ion = a.allcont_ion[i];
+    const int level = a.allcont_level[i];
+    if ((ionstagepop(c, mgi, element, ion) / nnetot > 1.e-6) || (level == 0)) {
+      const double nu_edge = a.allcont_nu_edge[i];
+      const double nnlevel = get_levelpop(tc, c, element, ion, level);
+      const double nu_max_phixs = nu_edge * a.last_phixs_nuovernuedge;
+      if (nu < nu_edge) break;
+      tc.work[WK_BF_ACTIVE]++;
+      if (nu <= nu_max_phixs && nnlevel > 0) {
+        const double sigma_bf = photoionization_crosssection_fromtable(
+            c, a.phixs_xs + (size_t)a.allcont_phixstable[i] * a.nphixspoints, nu_edge, nu);
+        const double probability = a.allcont_probability[i];
+        double departure_ratio = tc.departureratios[i];
+        if (departure_ratio < 0) {
+          const int upper = a.allcont_upperlevel[i];
+          const double nnupperionlevel = get_levelpop(tc, c, element, ion + 1, upper);
+          const double sf = calculate_sahafact(c, element, ion, level, upper, T_e, ARTIS_H * nu_edge);
+          departure_ratio = nnupperionlevel / nnlevel * nne * sf;
+          tc.departureratios[i] = departure_ratio;
+        }
+        const double stimfactor = departure_ratio * exp(-ARTIS_HOVERKB * nu / T_e);
+        double corrfactor = 1 - stimfactor;
+        if (corrfactor < 0) corrfactor = 0.;
+        const double kappa_bf_contr = nnlevel * sigma_bf * probability * corrfactor;
+        if (level == 0) {
+          const int gphixsindex = a.allcont_index_in_groundphixslist[i];
+          tc.groundcont_gamma_contr[gphixsindex] += sigma_bf * probability * corrfactor;
+        }
+        if (!std::isfinite(kappa_bf_contr)) {
+          fprintf(stderr, "oracle: non-finite kappa_bf_contr\n");
+          abort();
+        }
+        kappa_bf_sum += kappa_bf_contr;
+        tc.kappa_bf_sum[i] = kappa_bf_sum;
+      } else {
+        tc.kappa_bf_sum[i] = kappa_bf_sum;
+      }
+    } else {
+      tc.kappa_bf_sum[i] = kappa_bf_sum;
+    }
+  }
+  for (; i < nbfcontinua; i++) tc.kappa_bf_sum[i] = kappa_bf_sum;
+  return kappa_bf_sum;
+}
+// rpkt.cc:1209-1295 (deviation D2: always recomputed)
+void calculate_kappa_rpkt_cont(const Ctx &c, ThreadCache &tc, const artis_packet *p) {
+  const int mgi = cell_mgi(c, p->where);
+  const double nu_cmf = p->nu_cmf;
+  const float nne = c.cs->nne[mgi];
+  double sigma = 0.0, kappa_ff = 0., kappa_bf = 0., kappa_ffheating = 0.;
+  tc.work[WK_KAPPA_EVALS]++;
+  if (c.rp.do_r_lc) {
+    if (c.rp.opacity_case == 4) {
+      sigma = ARTIS_SIGMA_T * nne;
+      kappa_ff = calculate_kappa_ff(c, mgi, nu_cmf);
+      kappa_ffheating = kappa_ff;
+      kappa_bf = calculate_kappa_bf_gammacontr(c, tc, mgi, nu_cmf);
+    } else {
+      sigma = 0.;
+      kappa_ff = 1e5 * calculate_kappa_ff(c, mgi, nu_cmf);
+      kappa_bf = 0.;
+    }
+  }
+  tc.kap_total = sigma + kappa_bf + kappa_ff;
+  tc.kap_es = sigma;
+  tc.kap_ff = kappa_ff;
+  tc.kap_bf = kappa_bf;
+  tc.kap_ffheating = kappa_ffheating;
+  if (!std::isfinite(tc.kap_total)) {
+    if (std::isfinite(tc.kap_es)) {
+      tc.kap_ff = 0.;
+      tc.kap_bf = 0.;
+      tc.kap_total = tc.kap_es;
+    } else {
+      fprintf(stderr, "oracle: non-finite kappa_rpkt_cont\n");
+      abort();
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------------- line search
+// rpkt.cc:26-65
+int closest_transition(const Ctx &c, double nu_cmf, int next_trans) {
+  const int nlines = c.at->nlines;
+  const double *lnu = c.at->line_nu;
+  const int left = next_trans;
+  const int right = nlines - 1;
+  if (nu_cmf < lnu[right]) return -1;
+  if (left > right) return -1;
+  if (left > 0) return left;
+  if (nu_cmf >= lnu[0]) return 0;
+  // lower_bound with comparator line.nu > nu_cmf  (rpkt.cc:24)
+  int lo = next_trans, hi = nlines;
+  while (lo < hi) {
+    const int mid = lo + (hi - lo) / 2;
+    if (!(lnu[mid] <= nu_cmf))
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+// rpkt.cc:511-555
+void closest_transition_empty(const Ctx &c, artis_packet *p) {
+  const int nlines = c.at->nlines;
+  const double *lnu = c.at->line_nu;
+  const int left = p->next_trans;
+  const int right = nlines - 1;
+  if (p->nu_cmf < lnu[right]) p->next_trans = nlines + 1;
+  if (left > right) p->next_trans = nlines + 1;
+  int matchindex;
+  if (p->nu_cmf >= lnu[left]) {
+    matchindex = left;
+  } else {
+    int lo = p->next_trans, hi = nlines;
+    while (lo < hi) {
+      const int mid = lo + (hi - lo) / 2;
+      if (!(lnu[mid] <= p->nu_cmf))
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    matchindex = lo;
+  }
+  p->next_trans = matchindex;
+}
+
+// rpkt.cc:67-328
+double get_event(const Ctx &c, ThreadCache &tc, int mgi, artis_packet *p, int *rpkt_eventtype, double tau_rnd,
+                 double abort_dist) {
+  double tau = 0.;
+  double dist = 0.;
+  double edist = 0.;
+  artis_packet dummypkt_abort = *p;
+  move_pkt_withtime(c, &dummypkt_abort, abort_dist / 2.);
+  move_pkt_withtime(c, &dummypkt_abort, abort_dist / 2.);
+  const double nu_cmf_abort = dummypkt_abort.nu_cmf;
+  artis_packet dummypkt = *p;
+  artis_packet *const dp = &dummypkt;
+  calculate_kappa_rpkt_cont(c, tc, p);
+  const double kap_cont = tc.kap_total * doppler_packet_nucmf_on_nurf(c, p);
+  const artis_atomic_tables &a = *c.at;
+  while (true) {
+    const int lineindex = closest_transition(c, dp->nu_cmf, dp->next_trans);
+    if (lineindex >= 0) {
+      tc.work[WK_LINES_SCANNED]++;
+      const double nu_trans = a.line_nu[lineindex];
+      dp->next_trans = lineindex + 1;
+      double ldist;
+      if (dp->nu_cmf <= nu_trans) {
+        ldist = 0;
+      } else if (!c.rp.relativistic_doppler) {
+        ldist = ARTIS_CLIGHT * dp->prop_time * (dp->nu_cmf / nu_trans - 1);
+      } else {
+        const double nu_r = nu_trans / dp->nu_rf;
+        const double ct = ARTIS_CLIGHT * dp->prop_time;
+        const double r = vec_len(dp->pos);
+        const double mu = dot(dp->dir, dp->pos) / r;
+        ldist = -mu * r + (ct - nu_r * nu_r * sqrt(ct * ct - (1 + r * r * (1 - mu * mu) * (1 + pow(nu_r, -2))))) /
+                              (1 + nu_r * nu_r);
+      }
+      if (ldist < 0.) {
+        if (!(ldist >= -100.)) {
+          fprintf(stderr, "oracle: ldist %g < -100\n", ldist);
+          abort();
+        }
+        ldist = 0.;
+      }
+      const double tau_cont = kap_cont * ldist;
+      if (tau_rnd - tau > tau_cont) {
+        if (nu_trans < nu_cmf_abort) {
+          dp->next_trans -= 1;
+          p->next_trans = dp->next_trans;
+          return std::numeric_limits<double>::max();
+        }
+        const int element = a.line_elementindex[lineindex];
+        const int ion = a.line_ionindex[lineindex];
+        const int upper = a.line_upperlevelindex[lineindex];
+        const int lower = a.line_lowerlevelindex[lineindex];
+        const double A_ul = a.line_einstein_A[lineindex];
+        const double B_ul = ARTIS_CLIGHTSQUAREDOVERTWOH / pow(nu_trans, 3) * A_ul;
+        const double B_lu = stat_weight(c, element, ion, upper) / stat_weight(c, element, ion, lower) * B_ul;
+        const double n_u = get_levelpop(tc, c, element, ion, upper);
+        const double n_l = get_levelpop(tc, c, element, ion, lower);
+        double tau_line = (B_lu * n_l - B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * dp->prop_time;
+        tc.work[WK_LINE_TAUS]++;
+        if (tau_line < 0) tau_line = 0.;
+        if (tau_rnd - tau > tau_cont + tau_line) {
+          dist = dist + ldist;
+          tau += tau_cont + tau_line;
+          move_pkt_withtime(c, dp, ldist);
+        } else {
+          p->mastate.element = element;
+          p->mastate.ion = ion;
+          p->mastate.level = upper;
+          p->mastate.activatingline = lineindex;
+          edist = dist + ldist;
+          if (edist >= abort_dist) edist = abort_dist * (1 - 2e-8);
+          *rpkt_eventtype = ARTIS_RPKT_EVENTTYPE_BB;
+          p->next_trans = dp->next_trans;
+          return edist;
+        }
+      } else {
+        edist = dist + (tau_rnd - tau) / kap_cont;
+        dp->next_trans -= 1;
+        *rpkt_eventtype = ARTIS_RPKT_EVENTTYPE_CONT;
+        p->next_trans = dp->next_trans;
+        return edist;
+      }
+    } else {
+      dp->next_trans = a.nlines + 1;
+      const double tau_cont = kap_cont * (abort_dist - dist);
+      if (tau_rnd - tau > tau_cont) {
+        edist = std::numeric_limits<double>::max();
+      } else {
+        edist = dist + (tau_rnd - tau) / kap_cont;
+        *rpkt_eventtype = ARTIS_RPKT_EVENTTYPE_CONT;
+      }
+      p->next_trans = dp->next_trans;
+      return edist;
+    }
+  }
+}
+
+// rpkt.cc:557-621 + radfield.cc:831-876
+void update_estimators(const Ctx &c, ThreadCache &tc, Est &E, const artis_packet *p, double distance) {
+  const int mgi = cell_mgi(c, p->where);
+  if (mgi == npts_model(c)) return;
+  tc.work[WK_EST_SEGMENTS]++;
+  const double distance_e_cmf = distance * p->e_cmf;
+  const double nu = p->nu_cmf;
+  safeadd(&E.e->J[mgi], distance_e_cmf);
+  safeadd(&E.e->nuJ[mgi], distance_e_cmf * nu);
+  safeadd(&E.e->ffheatingestimator[mgi], distance_e_cmf * tc.kap_ffheating);
+  const double distance_e_cmf_over_nu = distance_e_cmf / nu;
+  const artis_atomic_tables &a = *c.at;
+  for (int i = 0; i < a.nbfcontinua_ground; i++) {
+    const double nu_edge = a.groundcont_nu_edge[i];
+    if (nu > nu_edge) {
+      const int element = a.groundcont_element[i];
+      if (c.cs->elem_abundance[(size_t)mgi * a.nelements + element] > 0) {
+        const int ion = a.groundcont_ion[i];
+        const size_t idx = (size_t)mgi * E.nelements * E.maxnions + element * E.maxnions + ion;
+        safeadd(&E.e->gammaestimator[idx], tc.groundcont_gamma_contr[i] * distance_e_cmf_over_nu);
+        safeadd(&E.e->bfheatingestimator[idx], tc.groundcont_gamma_contr[i] * distance_e_cmf * (1. - nu_edge / nu));
+        tc.work[WK_GC_UPDATES]++;
+      }
+    } else {
+      break;
+    }
+  }
+}
+
+// rpkt.cc:330-447
+void rpkt_event_continuum(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_packet *p) {
+  const double nu = p->nu_cmf;
+  const double dopplerfactor = doppler_packet_nucmf_on_nurf(c, p);
+  const double kappa_cont = tc.kap_total * dopplerfactor;
+  const double sigma = tc.kap_es * dopplerfactor;
+  const double kappa_ff = tc.kap_ff * dopplerfactor;
+  const double kappa_bf = tc.kap_bf * dopplerfactor;
+  const double zrand = artis_rng_uniform(rng);
+  tc.work[WK_CONT_EVENTS]++;
+  if (zrand * kappa_cont < sigma) {
+    p->interactions += 1;
+    p->nscatterings += 1;
+    p->last_event = 12;
+    counter_inc(E, CTR_ESCOUNTER);
+    tc.work[WK_ES_SCAT]++;
+    escat_rpkt(c, rng, p);
+    vec_copy(p->em_pos, p->pos);
+    p->em_time = (int)p->prop_time;
+  } else if (zrand * kappa_cont < sigma + kappa_ff) {
+    counter_inc(E, CTR_K_STAT_FROM_FF);
+    p->interactions += 1;
+    p->last_event = 5;
+    p->type = ARTIS_TYPE_KPKT;
+    p->absorptiontype = -1;
+  } else if (zrand * kappa_cont < sigma + kappa_ff + kappa_bf) {
+    p->absorptiontype = -2;
+    const double kappa_bf_inrest = tc.kap_bf;
+    const int nbf = c.at->nbfcontinua;
+    const double zrand2 = artis_rng_uniform(rng);
+    const double kappa_bf_rand = zrand2 * kappa_bf_inrest;
+    // lower_bound over kappa_bf_sum[0 .. nbf-1)
+    int lo = 0, hi = nbf - 1;
+    while (lo < hi) {
+      const int mid = lo + (hi - lo) / 2;
+      if (tc.kappa_bf_sum[mid] < kappa_bf_rand)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    const int allcontindex = lo;
+    const double nu_edge = c.at->allcont_nu_edge[allcontindex];
+    const int element = c.at->allcont_element[allcontindex];
+    const int ion = c.at->allcont_ion[allcontindex];
+    const int level = c.at->allcont_level[allcontindex];
+    const int phixstargetindex = c.at->allcont_phixstargetindex[allcontindex];
+    const double zrand3 = artis_rng_uniform(rng);
+    if (zrand3 < nu_edge / nu) {
+      counter_inc(E, CTR_MA_STAT_ACTIVATION_BF);
+      p->interactions += 1;
+      p->last_event = 3;
+      p->type = ARTIS_TYPE_MA;
+      p->mastate.element = element;
+      p->mastate.ion = ion + 1;
+      p->mastate.level = get_phixsupperlevel(c, element, ion, level, phixstargetindex);
+      p->mastate.activatingline = -99;
+    } else {
+      counter_inc(E, CTR_K_STAT_FROM_BF);
+      p->interactions += 1;
+      p->last_event = 4;
+      p->type = ARTIS_TYPE_KPKT;
+    }
+  } else {
+    fprintf(stderr, "oracle: ERROR: could not continuum process\n");
+    abort();
+  }
+}
+// rpkt.cc:449-489
+void rpkt_event_boundbound(const Ctx &c, ThreadCache &tc, Est &E, artis_packet *p) {
+  counter_inc(E, CTR_MA_STAT_ACTIVATION_BB);
+  tc.work[WK_BB_EVENTS]++;
+  p->interactions += 1;
+  p->last_event = 1;
+  p->absorptiontype = p->mastate.activatingline;
+  p->absorptionfreq = p->nu_rf;
+  p->absorptiondir[0] = p->dir[0];
+  p->absorptiondir[1] = p->dir[1];
+  p->absorptiondir[2] = p->dir[2];
+  p->type = ARTIS_TYPE_MA;
+  if (c.rp.record_linestat && E.e->acounter) {
+#pragma omp atomic update
+    E.e->acounter[p->next_trans - 1] += 1;
+  }
+}
+// rpkt.cc:491-509
+void rpkt_event_thickcell(const Ctx &c, Est &E, artis_rng *rng, artis_packet *p) {
+  p->interactions += 1;
+  p->nscatterings += 1;
+  p->last_event = 12;
+  counter_inc(E, CTR_ESCOUNTER);
+  emitt_rpkt(c, rng, p);
+  vec_copy(p->em_pos, p->pos);
+  p->em_time = (int)p->prop_time;
+}
+
+// rpkt.cc:623-813
+bool do_rpkt_step(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_packet *p, double t2) {
+  const int cellindex = p->where;
+  int mgi = cell_mgi(c, cellindex);
+  const int oldmgi = mgi;
+  const int npm = npts_model(c);
+  tc.work[WK_RPKT_STEPS]++;
+  const double zrand = artis_rng_uniform_pos(rng);
+  const double tau_next = -1. * log(zrand);
+  int snext;
+  double sdist = boundary_cross(c, E, p, &snext);
+  if (sdist == 0) {
+    change_cell(E, p, snext);
+    mgi = cell_mgi(c, p->where);
+    return (p->type == ARTIS_TYPE_RPKT && (mgi == npm || mgi == oldmgi));
+  }
+  const double maxsdist = c.g->rmax * p->prop_time / c.g->tmin;
+  if (sdist > maxsdist) {
+    fprintf(stderr, "oracle: [fatal] do_rpkt: Unreasonably large sdist for packet %d. %g %g %g\n", p->number,
+            c.g->rmax, p->prop_time / c.g->tmin, sdist);
+    abort();
+  }
+  if (((snext != -99) && (snext < 0)) || (snext >= c.g->ngrid)) {
+    fprintf(stderr, "oracle: [fatal] r_pkt: Heading for inappropriate grid cell.\n");
+    abort();
+  }
+  if (sdist > c.rp.max_path_step) {
+    sdist = c.rp.max_path_step;
+    snext = p->where;
+  }
+  const double tdist = (t2 - p->prop_time) * ARTIS_CLIGHT_PROP;
+  if (!(tdist >= 0)) {
+    fprintf(stderr, "oracle: tdist < 0\n");
+    abort();
+  }
+  double edist;
+  int rpkt_eventtype = -1;
+  bool find_nextline = false;
+  if (mgi == npm) {
+    edist = std::numeric_limits<double>::max();
+    find_nextline = true;
+  } else if (c.cs->thick[mgi] == 1) {
+    const double kappa = c.cs->kappagrey[mgi] * c.cs->rho[mgi] * doppler_packet_nucmf_on_nurf(c, p);
+    edist = (tau_next - 0.0) / kappa;
+    find_nextline = true;
+  } else {
+    edist = get_event(c, tc, mgi, p, &rpkt_eventtype, tau_next, fmin(tdist, sdist));
+  }
+  if (!(edist >= 0)) {
+    fprintf(stderr, "oracle: edist < 0\n");
+    abort();
+  }
+  if ((sdist < tdist) && (sdist < edist)) {
+    move_pkt_withtime(c, p, sdist / 2.);
+    update_estimators(c, tc, E, p, sdist);
+    move_pkt_withtime(c, p, sdist / 2.);
+    if (snext != p->where) {
+      change_cell(E, p, snext);
+      mgi = cell_mgi(c, p->where);
+    }
+    p->scat_count = 0;
+    p->last_event = p->last_event + 100;
+    if (find_nextline) {
+      if (mgi != npm && c.cs->thick[mgi] != 1) closest_transition_empty(c, p);
+    }
+    return (p->type == ARTIS_TYPE_RPKT && (mgi == npm || mgi == oldmgi));
+  } else if ((edist < sdist) && (edist < tdist)) {
+    move_pkt_withtime(c, p, edist / 2.);
+    update_estimators(c, tc, E, p, edist);
+    move_pkt_withtime(c, p, edist / 2.);
+    if (c.cs->thick[mgi] == 1)
+      rpkt_event_thickcell(c, E, rng, p);
+    else if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_BB)
+      rpkt_event_boundbound(c, tc, E, p);
+    else if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_CONT)
+      rpkt_event_continuum(c, tc, E, rng, p);
+    else {
+      fprintf(stderr, "oracle: bad event type\n");
+      abort();
+    }
+    return (p->type == ARTIS_TYPE_RPKT && (mgi == npm || mgi == oldmgi));
+  } else if ((tdist < sdist) && (tdist < edist)) {
+    move_pkt_withtime(c, p, tdist / 2.);
+    update_estimators(c, tc, E, p, tdist);
+    p->prop_time = t2;
+    move_pkt(c, p, tdist / 2.);
+    p->last_event = p->last_event + 1000;
+    if (find_nextline) closest_transition_empty(c, p);
+    return false;
+  }
+  fprintf(stderr, "oracle: [fatal] do_rpkt: Failed to identify event. edist %g, sdist %g, tdist %g pkt %d\n", edist,
+          sdist, tdist, p->number);
+  abort();
+}
+
+// ---------------------------------------------------------------------------------------------- macro-atom
+// macroatom.cc:57-159
+void calculate_macroatom_transitionrates(const Ctx &c, ThreadCache &tc, int mgi, int e, int i, int l, double t_mid) {
+  const int ul = ulev(c, e, i, l);
+  double *processrates = &tc.processrates[(size_t)ul * 9];
+  const float T_e = c.cs->Te[mgi];
+  const float nne = c.cs->nne[mgi];
+  const double epsilon_current = epsilon(c, e, i, l);
+  const double statweight = stat_weight(c, e, i, l);
+  const artis_atomic_tables &a = *c.at;
+  processrates[ARTIS_MA_ACTION_RADDEEXC] = 0.;
+  processrates[ARTIS_MA_ACTION_COLDEEXC] = 0.;
+  processrates[ARTIS_MA_ACTION_INTERNALDOWNSAME] = 0.;
+  const int ndowntrans = a.level_ndowntrans[ul];
+  const int doff = a.level_downtrans_offset[ul];
+  for (int k = 0; k < ndowntrans; k++) {
+    const int lineindex = a.downtrans_lineindex[doff + k];
+    const int lower = a.line_lowerlevelindex[lineindex];
+    const double epsilon_target = epsilon(c, e, i, lower);
+    const double epsilon_trans = epsilon_current - epsilon_target;
+    const double R = rad_deexcitation_ratecoeff(c, tc, e, i, l, lower, epsilon_trans, lineindex, t_mid);
+    const double C = col_deexcitation_ratecoeff(c, T_e, nne, epsilon_trans, lineindex, stat_weight(c, e, i, lower),
+                                                statweight);
+    const double individ_internal_down_same = (R + C) * epsilon_target;
+    const double individ_rad_deexc = R * epsilon_trans;
+    const double individ_col_deexc = C * epsilon_trans;
+    processrates[ARTIS_MA_ACTION_RADDEEXC] += individ_rad_deexc;
+    processrates[ARTIS_MA_ACTION_COLDEEXC] += individ_col_deexc;
+    processrates[ARTIS_MA_ACTION_INTERNALDOWNSAME] += individ_internal_down_same;
+    tc.individ_rad_deexc[doff + k] = individ_rad_deexc;
+    tc.individ_internal_down_same[doff + k] = individ_internal_down_same;
+  }
+  tc.work[WK_MA_TRANS] += ndowntrans;
+  processrates[ARTIS_MA_ACTION_RADRECOMB] = 0.;
+  processrates[ARTIS_MA_ACTION_COLRECOMB] = 0.;
+  processrates[ARTIS_MA_ACTION_INTERNALDOWNLOWER] = 0.;
+  if (i > 0 && l <= get_maxrecombininglevel(c, e, i)) {
+    const int nlevels = get_ionisinglevels(c, e, i - 1);
+    for (int lower = 0; lower < nlevels; lower++) {
+      const double epsilon_target = epsilon(c, e, i - 1, lower);
+      const double epsilon_trans = epsilon_current - epsilon_target;
+      const double R = rad_recombination_ratecoeff(c, T_e, nne, e, i, l, lower);
+      const double C = col_recombination_ratecoeff(c, mgi, e, i, l, lower, epsilon_trans);
+      processrates[ARTIS_MA_ACTION_INTERNALDOWNLOWER] += (R + C) * epsilon_target;
+      processrates[ARTIS_MA_ACTION_RADRECOMB] += R * epsilon_trans;
+      processrates[ARTIS_MA_ACTION_COLRECOMB] += C * epsilon_trans;
+    }
+    tc.work[WK_MA_TRANS] += nlevels;
+  }
+  processrates[ARTIS_MA_ACTION_INTERNALUPSAME] = 0.;
+  const int nuptrans = a.level_nuptrans[ul];
+  const int uoff = a.level_uptrans_offset[ul];
+  for (int k = 0; k < nuptrans; k++) {
+    const int lineindex = a.uptrans_lineindex[uoff + k];
+    const int upper = a.line_upperlevelindex[lineindex];
+    const double epsilon_trans = epsilon(c, e, i, upper) - epsilon_current;
+    const double R = rad_excitation_ratecoeff(c, tc, mgi, e, i, l, upper, epsilon_trans, lineindex, t_mid);
+    const double C = col_excitation_ratecoeff(c, T_e, nne, lineindex, epsilon_trans, statweight,
+                                              stat_weight(c, e, i, upper));
+    const double NT = 0.;  // nonthermal.cc:1746-1750 (NT_EXCITATION_ON false)
+    const double individ_internal_up_same = (R + C + NT) * epsilon_current;
+    processrates[ARTIS_MA_ACTION_INTERNALUPSAME] += individ_internal_up_same;
+    tc.individ_internal_up_same[uoff + k] = individ_internal_up_same;
+  }
+  tc.work[WK_MA_TRANS] += nuptrans;
+  processrates[ARTIS_MA_ACTION_INTERNALUPHIGHERNT] = 0.;
+  processrates[ARTIS_MA_ACTION_INTERNALUPHIGHER] = 0.;
+  const int ionisinglevels = get_ionisinglevels(c, e, i);
+  if (i < get_nions(c, e) - 1 && l < ionisinglevels) {
+    for (int t = 0; t < get_nphixstargets(c, e, i, l); t++) {
+      const double epsilon_trans = get_phixs_threshold(c, e, i, l, t);
+      const double R = get_corrphotoioncoeff(c, tc, e, i, l, t, mgi);
+      const double C = col_ionization_ratecoeff(c, T_e, nne, e, i, l, t, epsilon_trans);
+      processrates[ARTIS_MA_ACTION_INTERNALUPHIGHER] += (R + C) * epsilon_current;
+    }
+  }
+}
+
+// macroatom.cc:416-482
+void do_macroatom(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_packet *p, int timestep) {
+  const double t_mid = c.g->ts_mid[timestep];
+  const int mgi = cell_mgi(c, p->where);
+  const float T_e = c.cs->Te[mgi];
+  const float nne = c.cs->nne[mgi];
+  const artis_atomic_tables &a = *c.at;
+  if (c.cs->thick[mgi] == 1) {
+    fprintf(stderr, "oracle: macroatom in thick cell\n");
+    abort();
+  }
+  const int element = p->mastate.element;
+  int ion = p->mastate.ion;
+  int level = p->mastate.level;
+  const int activatingline = p->mastate.activatingline;
+  bool end_packet = false;
+  while (!end_packet) {
+    tc.work[WK_MA_JUMPS]++;
+    const double epsilon_current = epsilon(c, element, ion, level);
+    const int ul = ulev(c, element, ion, level);
+    const int nuptrans = a.level_nuptrans[ul];
+    double *processrates = &tc.processrates[(size_t)ul * 9];
+    if (processrates[ARTIS_MA_ACTION_COLDEEXC] < 0)
+      calculate_macroatom_transitionrates(c, tc, mgi, element, ion, level, t_mid);
+    double total_transitions = 0.;
+    for (int action = 0; action < ARTIS_MA_ACTION_COUNT; action++) total_transitions += processrates[action];
+    int selected_action = ARTIS_MA_ACTION_COUNT;
+    double zrand = artis_rng_uniform(rng);
+    const double randomrate = zrand * total_transitions;
+    double rate = 0.;
+    for (int action = 0; action < ARTIS_MA_ACTION_COUNT; action++) {
+      rate += processrates[action];
+      if (rate > randomrate) {
+        selected_action = action;
+        break;
+      }
+    }
+    if (rate <= randomrate) {
+      fprintf(stderr, "oracle: [fatal] do_ma: problem with random numbers .. abort (pkt %d Z idx %d ion %d lvl %d)\n",
+              p->number, element, ion, level);
+      abort();
+    }
+    switch (selected_action) {
+      case ARTIS_MA_ACTION_RADDEEXC: {
+        // macroatom.cc:222-296
+        const double zr = artis_rng_uniform(rng);
+        double r = 0.;
+        int linelistindex = -99;
+        const int ndowntrans = a.level_ndowntrans[ul];
+        const int doff = a.level_downtrans_offset[ul];
+        for (int k = 0; k < ndowntrans; k++) {
+          r += tc.individ_rad_deexc[doff + k];
+          if (zr * processrates[ARTIS_MA_ACTION_RADDEEXC] < r) {
+            linelistindex = a.downtrans_lineindex[doff + k];
+            break;
+          }
+        }
+        if (linelistindex < 0) {
+          fprintf(stderr, "oracle: [fatal] problem in selecting radiative downward transition of MA\n");
+          abort();
+        }
+        if (c.rp.record_linestat && E.e->ecounter) {
+#pragma omp atomic update
+          E.e->ecounter[linelistindex] += 1;
+        }
+        const int lower = a.line_lowerlevelindex[linelistindex];
+        const double epsilon_trans = epsilon(c, element, ion, level) - epsilon(c, element, ion, lower);
+        double oldnucmf = 0.;
+        if (p->last_event == 1) oldnucmf = p->nu_cmf;
+        p->nu_cmf = epsilon_trans / ARTIS_H;
+        if (p->last_event == 1) {
+          if (oldnucmf < p->nu_cmf)
+            counter_inc(E, CTR_UPSCATTER);
+          else
+            counter_inc(E, CTR_DOWNSCATTER);
+        }
+        counter_inc(E, CTR_MA_STAT_DEACTIVATION_BB);
+        p->interactions += 1;
+        p->last_event = 0;
+        emitt_rpkt(c, rng, p);
+        if (linelistindex == activatingline) counter_inc(E, CTR_RESONANCESCATTERINGS);
+        p->next_trans = linelistindex + 1;
+        p->emissiontype = linelistindex;
+        vec_copy(p->em_pos, p->pos);
+        p->em_time = (int)p->prop_time;
+        p->nscatterings = 0;
+        end_packet = true;
+        break;
+      }
+      case ARTIS_MA_ACTION_COLDEEXC: {
+        counter_inc(E, CTR_MA_STAT_DEACTIVATION_COLLDEEXC);
+        p->interactions += 1;
+        p->last_event = 10;
+        p->type = ARTIS_TYPE_KPKT;
+        end_packet = true;
+        safeadd(&E.e->colheatingestimator[mgi], p->e_cmf);
+        break;
+      }
+      case ARTIS_MA_ACTION_INTERNALDOWNSAME: {
+        // macroatom.cc:174-220
+        p->interactions += 1;
+        const double zr = artis_rng_uniform(rng);
+        int lower = -99;
+        double r = 0.;
+        const int ndowntrans = a.level_ndowntrans[ul];
+        const int doff = a.level_downtrans_offset[ul];
+        for (int k = 0; k < ndowntrans; k++) {
+          r += tc.individ_internal_down_same[doff + k];
+          if (zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNSAME] < r) {
+            lower = a.line_lowerlevelindex[a.downtrans_lineindex[doff + k]];
+            break;
+          }
+        }
+        level = lower;
+        break;
+      }
+      case ARTIS_MA_ACTION_RADRECOMB: {
+        // macroatom.cc:298-380
+        const int upperion = ion;
+        const int upperionlevel = level;
+        const double zr = artis_rng_uniform(rng);
+        double r = 0;
+        const int nlevels = get_ionisinglevels(c, element, upperion - 1);
+        int lower = 0;
+        for (lower = 0; lower < nlevels; lower++) {
+          const double epsilon_trans = epsilon_current - epsilon(c, element, upperion - 1, lower);
+          const double R = rad_recombination_ratecoeff(c, T_e, nne, element, upperion, upperionlevel, lower);
+          r += R * epsilon_trans;
+          if (zr * processrates[ARTIS_MA_ACTION_RADRECOMB] < r) break;
+        }
+        tc.work[WK_MA_TRANS] += lower + 1;
+        if (zr * processrates[ARTIS_MA_ACTION_RADRECOMB] >= r) {
+          fprintf(stderr, "oracle: could not select lower level to recombine to\n");
+          abort();
+        }
+        ion = upperion - 1;
+        level = lower;
+        p->nu_cmf = select_continuum_nu(c, rng, element, upperion - 1, lower, upperionlevel, T_e);
+        if (!std::isfinite(p->nu_cmf)) {
+          fprintf(stderr, "oracle: rad recombination of MA: selected frequency not finite\n");
+          abort();
+        }
+        counter_inc(E, CTR_MA_STAT_DEACTIVATION_FB);
+        p->interactions += 1;
+        p->last_event = 2;
+        emitt_rpkt(c, rng, p);
+        p->next_trans = 0;
+        p->emissiontype = get_continuumindex(c, element, ion, lower, upperionlevel);
+        vec_copy(p->em_pos, p->pos);
+        p->em_time = (int)p->prop_time;
+        p->nscatterings = 0;
+        end_packet = true;
+        break;
+      }
+      case ARTIS_MA_ACTION_COLRECOMB: {
+        counter_inc(E, CTR_MA_STAT_DEACTIVATION_COLLRECOMB);
+        p->interactions += 1;
+        p->last_event = 11;
+        p->type = ARTIS_TYPE_KPKT;
+        end_packet = true;
+        safeadd(&E.e->colheatingestimator[mgi], p->e_cmf);
+        break;
+      }
+      case ARTIS_MA_ACTION_INTERNALDOWNLOWER: {
+        p->interactions += 1;
+        counter_inc(E, CTR_MA_STAT_INTERNALDOWNLOWER);
+        zrand = artis_rng_uniform(rng);
+        rate = 0.;
+        const int nlevels = get_ionisinglevels(c, element, ion - 1);
+        int lower;
+        for (lower = 0; lower < nlevels; lower++) {
+          const double epsilon_target = epsilon(c, element, ion - 1, lower);
+          const double epsilon_trans = epsilon_current - epsilon_target;
+          const double R = rad_recombination_ratecoeff(c, T_e, nne, element, ion, level, lower);
+          const double C = col_recombination_ratecoeff(c, mgi, element, ion, level, lower, epsilon_trans);
+          rate += (R + C) * epsilon_target;
+          if (zrand * processrates[ARTIS_MA_ACTION_INTERNALDOWNLOWER] < rate) break;
+        }
+        tc.work[WK_MA_TRANS] += lower + 1;
+        ion -= 1;
+        level = lower;
+        if (lower >= nlevels) {
+          fprintf(stderr, "oracle: internal_down_lower abort\n");
+          abort();
+        }
+        break;
+      }
+      case ARTIS_MA_ACTION_INTERNALUPSAME: {
+        p->interactions += 1;
+        zrand = artis_rng_uniform(rng);
+        int upper = -99;
+        rate = 0.;
+        const int uoff = a.level_uptrans_offset[ul];
+        for (int k = 0; k < nuptrans; k++) {
+          rate += tc.individ_internal_up_same[uoff + k];
+          if (zrand * processrates[ARTIS_MA_ACTION_INTERNALUPSAME] < rate) {
+            upper = a.line_upperlevelindex[a.uptrans_lineindex[uoff + k]];
+            break;
+          }
+        }
+        level = upper;
+        break;
+      }
+      case ARTIS_MA_ACTION_INTERNALUPHIGHER: {
+        // macroatom.cc:382-414
+        p->interactions += 1;
+        counter_inc(E, CTR_MA_STAT_INTERNALUPHIGHER);
+        int upper = -1;
+        const double zr = artis_rng_uniform(rng);
+        double r = 0.;
+        for (int t = 0; t < get_nphixstargets(c, element, ion, level); t++) {
+          upper = get_phixsupperlevel(c, element, ion, level, t);
+          const double epsilon_trans = get_phixs_threshold(c, element, ion, level, t);
+          const double R = get_corrphotoioncoeff(c, tc, element, ion, level, t, mgi);
+          const double C = col_ionization_ratecoeff(c, T_e, nne, element, ion, level, t, epsilon_trans);
+          r += (R + C) * epsilon_current;
+          if (zr * processrates[ARTIS_MA_ACTION_INTERNALUPHIGHER] < r) break;
+        }
+        if (zr * processrates[ARTIS_MA_ACTION_INTERNALUPHIGHER] >= r) {
+          fprintf(stderr, "oracle: could not select upper level to ionise to\n");
+          abort();
+        }
+        ion += 1;
+        level = upper;
+        break;
+      }
+      default: {
+        fprintf(stderr, "oracle: ERROR: Problem selecting MA_ACTION %d\n", selected_action);
+        abort();
+      }
+    }
+  }
+  if (p->trueemissiontype < 0) {
+    p->trueemissiontype = p->emissiontype;
+    p->trueemissionvelocity = (float)(vec_len(p->em_pos) / p->em_time);
+    p->trueem_time = p->em_time;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------- k-packets
+// kpkt.cc:167-308
+void calculate_kpkt_rates_ion(const Ctx &c, ThreadCache &tc, int mgi, int e, int i, int indexionstart,
+                              double oldcoolingsum) {
+  const float nne = c.cs->nne[mgi];
+  const float T_e = c.cs->Te[mgi];
+  double contrib = oldcoolingsum;
+  int idx = indexionstart;
+  const int nions = get_nions(c, e);
+  const int nlevels_currention = get_nlevels(c, e, i);
+  const int ionisinglevels = get_ionisinglevels(c, e, i);
+  const double nncurrention = ionstagepop(c, mgi, e, i);
+  const artis_atomic_tables &a = *c.at;
+  const int ioncharge = get_ionstage(c, e, i) - 1;
+  if (ioncharge > 0) {
+    const double C = 1.426e-27 * sqrt(T_e) * pow(ioncharge, 2) * nncurrention * nne;
+    contrib += C;
+    tc.cooling_contrib[idx] = contrib;
+    idx++;
+  }
+  for (int level = 0; level < nlevels_currention; level++) {
+    const double epsilon_current = epsilon(c, e, i, level);
+    const double nnlevel = get_levelpop(tc, c, e, i, level);
+    const double statweight = stat_weight(c, e, i, level);
+    const int ul = ulev(c, e, i, level);
+    const int nuptrans = a.level_nuptrans[ul];
+    if (nuptrans > 0) {
+      for (int ii = 0; ii < nuptrans; ii++) {
+        const int li = a.uptrans_lineindex[a.level_uptrans_offset[ul] + ii];
+        const int upper = a.line_upperlevelindex[li];
+        const double epsilon_trans = epsilon(c, e, i, upper) - epsilon_current;
+        const double C = nnlevel *
+                         col_excitation_ratecoeff(c, T_e, nne, li, epsilon_trans, statweight,
+                                                  stat_weight(c, e, i, upper)) *
+                         epsilon_trans;
+        contrib += C;
+      }
+      tc.cooling_contrib[idx] = contrib;
+      idx++;
+    }
+    if (i < (nions - 1) && level < ionisinglevels) {
+      const int nt = get_nphixstargets(c, e, i, level);
+      for (int t = 0; t < nt; t++) {
+        const int upper = get_phixsupperlevel(c, e, i, level, t);
+        const double epsilon_upper = epsilon(c, e, i + 1, upper);
+        const double epsilon_trans = epsilon_upper - epsilon_current;
+        const double C = nnlevel * col_ionization_ratecoeff(c, T_e, nne, e, i, level, t, epsilon_trans) * epsilon_trans;
+        contrib += C;
+        tc.cooling_contrib[idx] = contrib;
+        idx++;
+      }
+      for (int t = 0; t < nt; t++) {
+        const double nnupperion = ionstagepop(c, mgi, e, i + 1);
+        const double C = get_bfcoolingcoeff(c, e, i, level, t, T_e) * nnupperion * nne;
+        contrib += C;
+        tc.cooling_contrib[idx] = contrib;
+        idx++;
+      }
+    }
+  }
+}
+
+// kpkt.cc:428-446
+double sample_planck(const Ctx &c, artis_rng *rng, double T) {
+  const double nu_peak = 5.879e10 * T;
+  const double B_peak = dbb(nu_peak, T, 1);
+  while (true) {
+    const double zrand = artis_rng_uniform(rng);
+    const double zrand2 = artis_rng_uniform(rng);
+    const double nu = c.g->nu_min_r + zrand * (c.g->nu_max_r - c.g->nu_min_r);
+    if (zrand2 * B_peak <= dbb(nu, T, 1)) return nu;
+  }
+}
+// kpkt.cc:448-475
+void do_kpkt_bb(const Ctx &c, Est &E, artis_rng *rng, artis_packet *p) {
+  const int mgi = cell_mgi(c, p->where);
+  const float T_e = c.cs->Te[mgi];
+  p->nu_cmf = sample_planck(c, rng, T_e);
+  emitt_rpkt(c, rng, p);
+  p->next_trans = 0;
+  counter_inc(E, CTR_K_STAT_TO_R_BB);
+  p->interactions++;
+  p->last_event = 6;
+  p->emissiontype = -9999999;
+  vec_copy(p->em_pos, p->pos);
+  p->em_time = (int)p->prop_time;
+  p->nscatterings = 0;
+}
+// kpkt.cc:477-797
+void do_kpkt(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_packet *p, double t2, int nts) {
+  const double t1 = p->prop_time;
+  const int mgi = cell_mgi(c, p->where);
+  const float T_e = c.cs->Te[mgi];
+  const artis_atomic_tables &a = *c.at;
+  tc.work[WK_KPKT]++;
+  double deltat = 0.;
+  if (nts < c.rp.n_kpktdiffusion_timesteps) deltat = c.rp.kpktdiffusion_timescale * c.g->ts_width[nts];
+  const double t_current = t1 + deltat;
+  if (t_current <= t2) {
+    vec_scale(p->pos, t_current / t1);
+    p->prop_time = t_current;
+    double coolingsum = 0.;
+    double zrand = artis_rng_uniform(rng);
+    const double rndcool = zrand * c.cs->totalcooling[mgi];
+    double oldcoolingsum = 0.;
+    int element = -1, ion = -1;
+    for (element = 0; element < a.nelements; element++) {
+      const int nions = get_nions(c, element);
+      for (ion = 0; ion < nions; ion++) {
+        oldcoolingsum = coolingsum;
+        coolingsum += c.cs->cooling_contrib_ion[(size_t)mgi * a.nions_total + uion(c, element, ion)];
+        if (coolingsum > rndcool) break;
+      }
+      if (coolingsum > rndcool) break;
+    }
+    if (element >= a.nelements || ion >= get_nions(c, element)) {
+      fprintf(stderr, "oracle: do_kpkt: problem selecting a cooling process\n");
+      abort();
+    }
+    const int ui = uion(c, element, ion);
+    const int ilow = a.ion_coolingoffset[ui];
+    const int ihigh = ilow + a.ion_ncoolingterms[ui] - 1;
+    if (tc.cooling_contrib[ilow] < 0.) calculate_kpkt_rates_ion(c, tc, mgi, element, ion, ilow, oldcoolingsum);
+    // lower_bound over cooling_contrib[ilow .. ihigh+1)
+    int lo = ilow, hi = ihigh + 1;
+    while (lo < hi) {
+      const int mid = lo + (hi - lo) / 2;
+      if (tc.cooling_contrib[mid] < rndcool)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    int icool = lo;
+    if (icool > ihigh) icool = ihigh;  // deviation D6
+    tc.work[WK_KPKT_TERMS] += icool - ilow + 1;
+    const int ctype = a.coolinglist_type[icool];
+    if (ctype == ARTIS_COOLINGTYPE_FF) {
+      zrand = artis_rng_uniform_pos(rng);
+      p->nu_cmf = -ARTIS_KB * T_e / ARTIS_H * log(zrand);
+      emitt_rpkt(c, rng, p);
+      p->next_trans = 0;
+      counter_inc(E, CTR_K_STAT_TO_R_FF);
+      p->interactions += 1;
+      p->last_event = 6;
+      p->emissiontype = -9999999;
+      vec_copy(p->em_pos, p->pos);
+      p->em_time = (int)p->prop_time;
+      p->nscatterings = 0;
+    } else if (ctype == ARTIS_COOLINGTYPE_FB) {
+      const int el = a.coolinglist_element[icool];
+      const int lowerion = a.coolinglist_ion[icool];
+      const int level = a.coolinglist_level[icool];
+      const int upper = a.coolinglist_upperlevel[icool];
+      p->nu_cmf = select_continuum_nu(c, rng, el, lowerion, level, upper, T_e);
+      emitt_rpkt(c, rng, p);
+      p->next_trans = 0;
+      counter_inc(E, CTR_K_STAT_TO_R_FB);
+      p->interactions += 1;
+      p->last_event = 7;
+      p->emissiontype = get_continuumindex(c, el, lowerion, level, upper);
+      p->trueemissiontype = p->emissiontype;
+      vec_copy(p->em_pos, p->pos);
+      p->em_time = (int)p->prop_time;
+      p->nscatterings = 0;
+    } else if (ctype == ARTIS_COOLINGTYPE_COLLEXC) {
+      const float nne = c.cs->nne[mgi];
+      const double contrib_low = (icool > ilow) ? tc.cooling_contrib[icool - 1] : oldcoolingsum;
+      double contrib = contrib_low;
+      const int level = a.coolinglist_level[icool];
+      const double epsilon_current = epsilon(c, element, ion, level);
+      const double nnlevel = get_levelpop(tc, c, element, ion, level);
+      const double statweight = stat_weight(c, element, ion, level);
+      int upper = -1;
+      const int ul = ulev(c, element, ion, level);
+      const int nuptrans = a.level_nuptrans[ul];
+      for (int ii = 0; ii < nuptrans; ii++) {
+        const int li = a.uptrans_lineindex[a.level_uptrans_offset[ul] + ii];
+        const int tmpupper = a.line_upperlevelindex[li];
+        const double epsilon_trans = epsilon(c, element, ion, tmpupper) - epsilon_current;
+        const double C = nnlevel *
+                         col_excitation_ratecoeff(c, T_e, nne, li, epsilon_trans, statweight,
+                                                  stat_weight(c, element, ion, tmpupper)) *
+                         epsilon_trans;
+        contrib += C;
+        if (contrib >= rndcool) {
+          upper = tmpupper;
+          break;
+        }
+      }
+      if (upper < 0 && nuptrans > 0) {
+        // deviation D6: the update_grid ion total exceeded the re-summed terms in the last bits
+        upper = a.line_upperlevelindex[a.uptrans_lineindex[a.level_uptrans_offset[ul] + nuptrans - 1]];
+      }
+      if (upper < 0) {
+        fprintf(stderr, "oracle: WARNING: Could not select an upper level. pkt %d\n", p->number);
+        abort();
+      }
+      p->mastate.element = element;
+      p->mastate.ion = ion;
+      p->mastate.level = upper;
+      p->mastate.activatingline = -99;
+      p->type = ARTIS_TYPE_MA;
+      counter_inc(E, CTR_MA_STAT_ACTIVATION_COLLEXC);
+      counter_inc(E, CTR_K_STAT_TO_MA_COLLEXC);
+      p->interactions += 1;
+      p->last_event = 8;
+      p->trueemissiontype = -1;
+      p->trueemissionvelocity = -1;
+    } else if (ctype == ARTIS_COOLINGTYPE_COLLION) {
+      p->mastate.element = a.coolinglist_element[icool];
+      p->mastate.ion = a.coolinglist_ion[icool] + 1;
+      p->mastate.level = a.coolinglist_upperlevel[icool];
+      p->mastate.activatingline = -99;
+      p->type = ARTIS_TYPE_MA;
+      counter_inc(E, CTR_MA_STAT_ACTIVATION_COLLION);
+      counter_inc(E, CTR_K_STAT_TO_MA_COLLION);
+      p->interactions += 1;
+      p->last_event = 9;
+      p->trueemissiontype = -1;
+      p->trueemissionvelocity = -1;
+    } else {
+      fprintf(stderr, "oracle: [fatal] do_kpkt: coolinglist.type mismatch\n");
+      abort();
+    }
+  } else {
+    vec_scale(p->pos, t2 / t1);
+    p->prop_time = t2;
+  }
+}
+
+// ------------------------------------------------------------------------------------------- packet driver
+// update_packets.cc:137-202 do_packet (r-packet, k-packet and macro-atom paths)
+int do_packet(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_packet *p, double t2, int nts) {
+  const int pkt_type = p->type;
+  switch (pkt_type) {
+    case ARTIS_TYPE_RPKT: {
+      while (do_rpkt_step(c, tc, E, rng, p, t2)) {
+      }
+      if (p->type == ARTIS_TYPE_ESCAPE) {
+        safeadd(&E.e->cmf_lum, p->e_cmf);
+        tc.work[WK_ESCAPED]++;
+      }
+      return 0;
+    }
+    case ARTIS_TYPE_KPKT:
+    case ARTIS_TYPE_PRE_KPKT:
+    case ARTIS_TYPE_GAMMA_KPKT: {
+      const int mgi = cell_mgi(c, p->where);
+      if (pkt_type == ARTIS_TYPE_PRE_KPKT || c.cs->thick[mgi] == 1)
+        do_kpkt_bb(c, E, rng, p);
+      else if (pkt_type == ARTIS_TYPE_KPKT)
+        do_kpkt(c, tc, E, rng, p, t2, nts);
+      else {
+        fprintf(stderr, "oracle: kpkt not of type TYPE_KPKT or TYPE_PRE_KPKT\n");
+        abort();
+      }
+      return 0;
+    }
+    case ARTIS_TYPE_MA:
+      do_macroatom(c, tc, E, rng, p, nts);
+      return 0;
+    default:
+      return ARTIS_ERR_UNSUPPORTED;
+  }
+}
+
+}  // namespace
+
+// ================================================================================================== C ABI
+extern "C" {
+
+// Oracle counterpart of update_packets (update_packets.cc:234-333), deviation D5 (flattened pass loop).
+int oracle_update_packets(const artis_atomic_tables *at, const artis_geometry *geom, const artis_cell_state *cs,
+                          const artis_run_params *rp, int nts, artis_packet *packets, int npkts,
+                          artis_estimators *est, int64_t work_out[ARTIS_WORK_COUNT], int nthreads) {
+  Ctx c;
+  c.at = at;
+  c.g = geom;
+  c.cs = cs;
+  c.rp = *rp;
+  c.T_step_log = (log(at->maxtemp) - log(at->mintemp)) / (at->tablesize - 1.);
+  Est E;
+  E.e = est;
+  E.nelements = at->nelements;
+  E.maxnions = at->maxnions;
+  const double ts = geom->ts_start[nts];
+  const double tw = geom->ts_width[nts];
+  const double t2 = ts + tw;
+  std::atomic<int> status{0};
+  int64_t work[ARTIS_WORK_COUNT] = {0};
+  if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads)
+  {
+    ThreadCache tc;
+    tc.pops.assign(at->nlevels_total, 0.);
+    tc.departureratios.assign(at->nbfcontinua, -1.);
+    tc.processrates.assign((size_t)at->nlevels_total * 9, -99.);
+    size_t ndown = 0, nup = 0, ntg = 0;
+    for (int lv = 0; lv < at->nlevels_total; lv++) {
+      ndown += at->level_ndowntrans[lv];
+      nup += at->level_nuptrans[lv];
+      ntg += at->level_nphixstargets[lv];
+    }
+    tc.individ_rad_deexc.assign(ndown, 0.);
+    tc.individ_internal_down_same.assign(ndown, 0.);
+    tc.individ_internal_up_same.assign(nup, 0.);
+    tc.corrphotoioncoeff.assign(ntg + 1, -99.);
+    tc.cooling_contrib.assign(at->ncoolingterms, -99.);
+    tc.kappa_bf_sum.assign(at->nbfcontinua, 0.);
+    tc.groundcont_gamma_contr.assign(at->nbfcontinua_ground, 0.);
+#pragma omp for schedule(dynamic, 16)
+    for (int n = 0; n < npkts; n++) {
+      artis_packet *p = &packets[n];
+      p->interactions = 0;  // update_packets.cc:285-288 (pass 0)
+      p->scat_count = 0;
+      if (p->type == ARTIS_TYPE_ESCAPE || !(p->prop_time < t2)) continue;
+      tc.work[WK_PACKETS_ACTIVE]++;
+      artis_rng rng = artis_rng_init(rp->seed, p->number, nts, rp->rank);
+      long iters = 0;
+      while (p->type != ARTIS_TYPE_ESCAPE && p->prop_time < t2) {
+        if (++iters > 2000000) {
+          fprintf(stderr, "oracle: packet %d stuck: type %d where %d nu_cmf %g prop_time %.17g t2 %.17g ma %d %d %d\n",
+                  p->number, p->type, p->where, p->nu_cmf, p->prop_time, t2, p->mastate.element, p->mastate.ion,
+                  p->mastate.level);
+          if (iters > 2000020) abort();
+        }
+        const int mgi = cell_mgi(c, p->where);
+        if (mgi != npts_model(c) && tc.cellnumber != mgi) {
+          counter_inc(E, CTR_UPDATECELL);
+          cellhistory_reset(c, tc, mgi);
+        }
+        const int st = do_packet(c, tc, E, &rng, p, t2, nts);
+        if (st != 0) {
+          status = st;
+          break;
+        }
+      }
+    }
+#pragma omp critical
+    for (int k = 0; k < ARTIS_WORK_COUNT; k++) work[k] += tc.work[k];
+  }
+  if (work_out)
+    for (int k = 0; k < ARTIS_WORK_COUNT; k++) work_out[k] = work[k];
+  return status.load();
+}
+
+int oracle_abi_version(void) { return 1; }
+
+}  // extern "C"
