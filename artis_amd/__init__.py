@@ -1,0 +1,136 @@
+"""artis_amd -- MI355X-native packet-propagation engine for ARTIS (update_packets hot path).
+
+The product is the C-ABI library artis_amd/lib/libartis_gpu.so (include/artis_gpu.h): hand-written HIP
+kernels for gfx950.  This module is a thin ctypes mirror of that ABI for tests, the bench and the
+multi-GPU driver.  There is no CPU fallback: if the library or a GPU is missing, Engine() raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import ffi
+
+_LIBDIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+GPU_SO = os.path.join(_LIBDIR, "libartis_gpu.so")
+
+# every function declared in include/artis_gpu.h (tests/test_abi.py checks they are exported)
+ABI_SYMBOLS = [
+    "artis_gpu_init", "artis_gpu_finalize", "artis_gpu_upload_cellstate", "artis_gpu_update_packets",
+    "artis_gpu_packets_upload", "artis_gpu_packets_download", "artis_gpu_packets_snapshot",
+    "artis_gpu_packets_restore", "artis_gpu_update_packets_resident", "artis_gpu_estimators_zero",
+    "artis_gpu_estimators_download", "artis_gpu_estimator_block_doubles", "artis_gpu_estimator_block_to_device",
+    "artis_gpu_estimator_block_from_device", "artis_gpu_last_transport_ms", "artis_gpu_last_precompute_ms",
+    "artis_gpu_last_work_counts", "artis_gpu_last_error", "artis_gpu_abi_version",
+]
+
+_gpu_lib = None
+
+
+def gpu_lib():
+    """Load libartis_gpu.so (fails loudly if it was not built)."""
+    global _gpu_lib
+    if _gpu_lib is None:
+        if not os.path.exists(GPU_SO):
+            raise RuntimeError(f"{GPU_SO} missing: the HIP engine was not built (run __graft_entry__.build())")
+        L = C.CDLL(GPU_SO)
+        vp = C.c_void_p
+        L.artis_gpu_init.argtypes = [C.c_int, vp, vp, C.POINTER(ffi.RunParams)]
+        L.artis_gpu_upload_cellstate.argtypes = [C.c_int, vp]
+        L.artis_gpu_update_packets.argtypes = [C.c_int, C.c_int, vp, C.c_int, C.POINTER(ffi.Estimators)]
+        L.artis_gpu_packets_upload.argtypes = [vp, C.c_int]
+        L.artis_gpu_packets_download.argtypes = [vp, C.c_int]
+        L.artis_gpu_update_packets_resident.argtypes = [C.c_int, C.c_int]
+        L.artis_gpu_estimators_download.argtypes = [C.POINTER(ffi.Estimators)]
+        L.artis_gpu_estimator_block_doubles.restype = C.c_size_t
+        L.artis_gpu_estimator_block_to_device.argtypes = [vp]
+        L.artis_gpu_estimator_block_from_device.argtypes = [vp]
+        L.artis_gpu_last_transport_ms.restype = C.c_double
+        L.artis_gpu_last_precompute_ms.restype = C.c_double
+        L.artis_gpu_last_work_counts.argtypes = [vp]
+        L.artis_gpu_last_error.restype = C.c_char_p
+        _gpu_lib = L
+    return _gpu_lib
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+class Engine:
+    """One HIP device's engine instance bound to a model (atomic tables + geometry)."""
+
+    def __init__(self, model, device=0, params=None):
+        self.lib = gpu_lib()
+        self.model = model
+        self.params = params if params is not None else model.params
+        self._check(self.lib.artis_gpu_init(int(device), model.atomic, model.geometry, C.byref(self.params)), "init")
+        self.cell_nts = None
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self.lib.artis_gpu_last_error()
+            raise EngineError(f"artis_gpu_{what} -> {rc}: {msg.decode() if msg else ''}")
+
+    def upload_cellstate(self, nts):
+        self._check(self.lib.artis_gpu_upload_cellstate(int(nts), self.model.cellstate), "upload_cellstate")
+        self.cell_nts = nts
+
+    def update_packets(self, nts, packets, est=None, my_rank=None):
+        """Drop-in update_packets(my_rank, nts, packets): packets modified in place, estimators added to est."""
+        if est is None:
+            est = self.model.new_estimators()
+        rank = self.params.rank if my_rank is None else my_rank
+        self._check(self.lib.artis_gpu_update_packets(int(rank), int(nts), packets.ctypes.data, len(packets),
+                                                      C.byref(est.struct)), "update_packets")
+        return est
+
+    # device-resident path
+    def upload(self, packets):
+        self._check(self.lib.artis_gpu_packets_upload(packets.ctypes.data, len(packets)), "packets_upload")
+        self.npkts = len(packets)
+
+    def download(self, packets):
+        self._check(self.lib.artis_gpu_packets_download(packets.ctypes.data, len(packets)), "packets_download")
+
+    def snapshot(self):
+        self._check(self.lib.artis_gpu_packets_snapshot(), "packets_snapshot")
+
+    def restore(self):
+        self._check(self.lib.artis_gpu_packets_restore(), "packets_restore")
+
+    def zero_estimators(self):
+        self._check(self.lib.artis_gpu_estimators_zero(), "estimators_zero")
+
+    def step_resident(self, nts, my_rank=None):
+        rank = self.params.rank if my_rank is None else my_rank
+        self._check(self.lib.artis_gpu_update_packets_resident(int(rank), int(nts)), "update_packets_resident")
+
+    def download_estimators(self, est=None):
+        if est is None:
+            est = self.model.new_estimators()
+        self._check(self.lib.artis_gpu_estimators_download(C.byref(est.struct)), "estimators_download")
+        return est
+
+    def estimator_block_doubles(self):
+        return int(self.lib.artis_gpu_estimator_block_doubles())
+
+    def estimator_block_to_device(self, dptr):
+        self._check(self.lib.artis_gpu_estimator_block_to_device(C.c_void_p(dptr)), "estimator_block_to_device")
+
+    def estimator_block_from_device(self, dptr):
+        self._check(self.lib.artis_gpu_estimator_block_from_device(C.c_void_p(dptr)), "estimator_block_from_device")
+
+    def last_transport_ms(self):
+        return float(self.lib.artis_gpu_last_transport_ms())
+
+    def last_precompute_ms(self):
+        return float(self.lib.artis_gpu_last_precompute_ms())
+
+    def last_work(self):
+        w = np.zeros(ffi.ARTIS_WORK_COUNT, dtype=np.int64)
+        self.lib.artis_gpu_last_work_counts(w.ctypes.data)
+        return w
+
+    def close(self):
+        self.lib.artis_gpu_finalize()

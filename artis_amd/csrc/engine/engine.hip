@@ -1,0 +1,930 @@
+// engine.hip -- MI355X (gfx950) packet-propagation engine behind the C-ABI of include/artis_gpu.h.
+//
+// Per timestep:
+//   artis_gpu_upload_cellstate: H2D of the update_grid outputs, then five precompute kernels over the
+//     non-empty model cells (populations, ion-stage pops + free-free ion sums, departure ratios, corrected
+//     photoionisation coefficients, cumulative k-packet cooling lists, macro-atom process-rate totals) --
+//     the GPU replacement of the per-thread cellhistory cache (update_grid.cc:659-761).
+//   artis_gpu_update_packets: H2D of the 304-byte packet records, AoS->SoA transpose, the transport kernel
+//     (one packet per workitem, update_packets.cc:234-333 with the pass loop flattened), SoA->AoS, D2H, and
+//     the estimator sums added into the caller's arrays.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "artis_constants.h"
+#include "artis_gpu.h"
+#include "artis_rng.h"
+#include "engine_dev.h"
+#include "packet_soa.h"
+#include "physics.h"
+#include "transport.h"
+
+// ================================================================================================= kernels
+
+// ltepop.cc:307-347,417-430,558-564; rpkt.cc:1036-1058 (free-free ion sum)
+__global__ void k_cellprep(Ctx K) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K.C.n_nonempty) return;
+  const int mgi = K.C.ne_mgi[k];
+  double ffsum = 0.;
+  for (int e = 0; e < K.T.nelements; e++) {
+    for (int i = 0; i < K.T.elem_nions[e]; i++) {
+      const int ui = uion(K, e, i);
+      double gp = K.C.groundlevelpop[(int64_t)mgi * K.T.nions_total + ui];
+      if (gp < ARTIS_MINPOP) gp = (K.C.elem_abundance[(int64_t)mgi * K.T.nelements + e] > 0) ? ARTIS_MINPOP : 0.;
+      const double nnion = gp * K.C.partfunct[(int64_t)mgi * K.T.nions_total + ui] /
+                           (double)K.T.level_stat_weight[K.T.ion_uniqueleveloffset[ui]];
+      K.C.ionpop[(int64_t)k * K.T.nions_total + ui] = nnion;
+      const int Z = K.T.ion_ionstage[ui] - 1;
+      if (Z > 0) ffsum += Z * Z * 1. * nnion;
+    }
+  }
+  K.C.ffsum[k] = ffsum;
+}
+
+__global__ void k_levelpops(Ctx K) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nl = K.T.nlevels_total;
+  if (idx >= (int64_t)K.C.n_nonempty * nl) return;
+  const int k = (int)(idx / nl);
+  const int ul = (int)(idx % nl);
+  const int mgi = K.C.ne_mgi[k];
+  const int ui = K.T.level_ui[ul];
+  const int e = K.T.ion_element[ui];
+  const int l = ul - K.T.ion_uniqueleveloffset[ui];
+  const int ul0 = K.T.ion_uniqueleveloffset[ui];
+  const bool hasabund = K.C.elem_abundance[(int64_t)mgi * K.T.nelements + e] > 0;
+  double ng = K.C.groundlevelpop[(int64_t)mgi * K.T.nions_total + ui];
+  if (ng < ARTIS_MINPOP) ng = hasabund ? ARTIS_MINPOP : 0.;
+  double nn;
+  if (l == 0) {
+    nn = ng;
+  } else {
+    const double T_exc = K.C.TJ[mgi];
+    const double W = 1.;
+    nn = (ng * W * (double)K.T.level_stat_weight[ul] / (double)K.T.level_stat_weight[ul0] *
+          exp(-(K.T.level_epsilon[ul] - K.T.level_epsilon[ul0]) / ARTIS_KB / T_exc));
+  }
+  if (nn < ARTIS_MINPOP) nn = hasabund ? ARTIS_MINPOP : 0.;
+  K.C.pops[idx] = nn;
+}
+
+// rpkt.cc:1140-1151 departure ratios; ratecoeff.cc:1247-1308 corrected photoionisation coefficients
+__global__ void k_bfcells(Ctx K, const int32_t *target_ul, const int32_t *target_t) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nb = K.T.nbf, ntg = K.T.ntargets_total;
+  const int64_t total = (int64_t)K.C.n_nonempty * (nb + ntg);
+  if (idx >= total) return;
+  const int k = (int)(idx / (nb + ntg));
+  const int r = (int)(idx % (nb + ntg));
+  const int mgi = K.C.ne_mgi[k];
+  const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
+  if (r < nb) {
+    const int i = r;
+    const int element = K.T.allcont_element[i];
+    const int ion = K.T.allcont_ion[i];
+    const int level = K.T.allcont_level[i];
+    const int upper = K.T.allcont_upperlevel[i];
+    const double T_e = K.C.Te[mgi];
+    const double nne = K.C.nne[mgi];
+    const double nnlevel = pops[ulev(K, element, ion, level)];
+    const double nnupperionlevel = pops[ulev(K, element, ion + 1, upper)];
+    const double sf = calculate_sahafact(K, element, ion, level, upper, T_e, ARTIS_H * K.T.allcont_nu_edge[i]);
+    K.C.depratio[(int64_t)k * nb + i] = nnupperionlevel / nnlevel * nne * sf;
+  } else {
+    const int slot = r - (int)nb;
+    const int ul = target_ul[slot];
+    const int t = target_t[slot];
+    const int ui = K.T.level_ui[ul];
+    const int e = K.T.ion_element[ui];
+    const int i = ui - K.T.elem_uniqueionoffset[e];
+    const int l = ul - K.T.ion_uniqueleveloffset[ui];
+    const double W = K.C.W[mgi];
+    const double T_R = K.C.TR[mgi];
+    double gammacorr = W * lut_interp(K, K.T.corrphotoioncoeff, e, i, l, t, T_R);
+    const int g = K.T.level_closestgroundlevelcont[ul];
+    if (g >= 0) gammacorr *= K.C.corrphotoionrenorm[(int64_t)mgi * K.T.nelements * K.T.maxnions + g];
+    K.C.corrphot[(int64_t)k * ntg + slot] = gammacorr;
+  }
+}
+
+// kpkt.cc:167-308 calculate_kpkt_rates_ion, one workitem per (cell, ion), cumulative from oldcoolingsum
+__global__ void k_cooling(Ctx K) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int ni = K.T.nions_total;
+  if (idx >= (int64_t)K.C.n_nonempty * ni) return;
+  const int k = (int)(idx / ni);
+  const int ui = (int)(idx % ni);
+  const int mgi = K.C.ne_mgi[k];
+  const int e = K.T.ion_element[ui];
+  const int i = ui - K.T.elem_uniqueionoffset[e];
+  const float nne = K.C.nne[mgi];
+  const float T_e = K.C.Te[mgi];
+  const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
+  double *cc = K.C.cooling + (int64_t)k * K.T.ncoolingterms;
+  double oldcoolingsum = 0.;
+  for (int u = 0; u < ui; u++) oldcoolingsum += K.C.cooling_contrib_ion[(int64_t)mgi * ni + u];
+  double contrib = oldcoolingsum;
+  int idxc = K.T.ion_coolingoffset[ui];
+  const int nions = K.T.elem_nions[e];
+  const int nlevels = K.T.ion_nlevels[ui];
+  const int ionisinglevels = K.T.ion_ionisinglevels[ui];
+  const double nncurrention = K.C.ionpop[(int64_t)k * ni + ui];
+  const int ioncharge = K.T.ion_ionstage[ui] - 1;
+  if (ioncharge > 0) {
+    const double C = 1.426e-27 * sqrt((double)T_e) * pow((double)ioncharge, 2) * nncurrention * nne;
+    contrib += C;
+    cc[idxc++] = contrib;
+  }
+  for (int level = 0; level < nlevels; level++) {
+    const int ul = K.T.ion_uniqueleveloffset[ui] + level;
+    const double epsilon_current = K.T.level_epsilon[ul];
+    const double nnlevel = pops[ul];
+    const double statweight = K.T.level_stat_weight[ul];
+    const int nuptrans = K.T.level_nuptrans[ul];
+    if (nuptrans > 0) {
+      const int uoff = K.T.level_uptrans_offset[ul];
+      for (int ii = 0; ii < nuptrans; ii++) {
+        const int li = K.T.uptrans_lineindex[uoff + ii];
+        const int uu = K.T.ion_uniqueleveloffset[ui] + K.T.line_upper[li];
+        const double epsilon_trans = K.T.level_epsilon[uu] - epsilon_current;
+        const double C = nnlevel *
+                         col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight,
+                                                  (double)K.T.level_stat_weight[uu]) *
+                         epsilon_trans;
+        contrib += C;
+      }
+      cc[idxc++] = contrib;
+    }
+    if (i < (nions - 1) && level < ionisinglevels) {
+      const int nt = K.T.level_nphixstargets[ul];
+      for (int t = 0; t < nt; t++) {
+        const int upper = get_phixsupperlevel(K, e, i, level, t);
+        const double epsilon_upper = epsilon(K, e, i + 1, upper);
+        const double epsilon_trans = epsilon_upper - epsilon_current;
+        const double C = nnlevel * col_ionization_ratecoeff(K, T_e, nne, e, i, level, t, epsilon_trans) * epsilon_trans;
+        contrib += C;
+        cc[idxc++] = contrib;
+      }
+      for (int t = 0; t < nt; t++) {
+        const double nnupperion = K.C.ionpop[(int64_t)k * ni + ui + 1];
+        const double C = lut_interp(K, K.T.bfcooling_coeff, e, i, level, t, T_e) * nnupperion * nne;
+        contrib += C;
+        cc[idxc++] = contrib;
+      }
+    }
+  }
+}
+
+// macroatom.cc:57-159 calculate_macroatom_transitionrates, one workitem per (cell, level)
+__global__ void k_marates(Ctx K, int nts) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nl = K.T.nlevels_total;
+  if (idx >= (int64_t)K.C.n_nonempty * nl) return;
+  const int k = (int)(idx / nl);
+  const int ul = (int)(idx % nl);
+  const int mgi = K.C.ne_mgi[k];
+  const int ui = K.T.level_ui[ul];
+  const int e = K.T.ion_element[ui];
+  const int i = ui - K.T.elem_uniqueionoffset[e];
+  const int l = ul - K.T.ion_uniqueleveloffset[ui];
+  const double t_mid = K.G.ts_mid[nts];
+  const float T_e = K.C.Te[mgi];
+  const float nne = K.C.nne[mgi];
+  const double *pops = K.C.pops + (int64_t)k * nl;
+  const double epsilon_current = K.T.level_epsilon[ul];
+  const double statweight = K.T.level_stat_weight[ul];
+  double pr[ARTIS_MA_ACTION_COUNT];
+  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) pr[a] = 0.;
+  const int ndowntrans = K.T.level_ndowntrans[ul];
+  const int doff = K.T.level_downtrans_offset[ul];
+  for (int j = 0; j < ndowntrans; j++) {
+    const int li = K.T.downtrans_lineindex[doff + j];
+    const int lower = K.T.line_lower[li];
+    const double epsilon_target = epsilon(K, e, i, lower);
+    const double epsilon_trans = epsilon_current - epsilon_target;
+    const double R = rad_deexcitation_ratecoeff(K, pops, e, i, l, lower, epsilon_trans, li, t_mid);
+    const double C = col_deexcitation_ratecoeff(K, T_e, nne, epsilon_trans, li, stat_weight(K, e, i, lower), statweight);
+    pr[ARTIS_MA_ACTION_RADDEEXC] += R * epsilon_trans;
+    pr[ARTIS_MA_ACTION_COLDEEXC] += C * epsilon_trans;
+    pr[ARTIS_MA_ACTION_INTERNALDOWNSAME] += (R + C) * epsilon_target;
+  }
+  if (i > 0 && l <= K.T.ion_maxrecombininglevel[ui]) {
+    const int nlevels = get_ionisinglevels(K, e, i - 1);
+    for (int lower = 0; lower < nlevels; lower++) {
+      const double epsilon_target = epsilon(K, e, i - 1, lower);
+      const double epsilon_trans = epsilon_current - epsilon_target;
+      const double R = rad_recombination_ratecoeff(K, T_e, nne, e, i, l, lower);
+      const double C = col_recombination_ratecoeff(K, mgi, e, i, l, lower, epsilon_trans);
+      pr[ARTIS_MA_ACTION_INTERNALDOWNLOWER] += (R + C) * epsilon_target;
+      pr[ARTIS_MA_ACTION_RADRECOMB] += R * epsilon_trans;
+      pr[ARTIS_MA_ACTION_COLRECOMB] += C * epsilon_trans;
+    }
+  }
+  const int nuptrans = K.T.level_nuptrans[ul];
+  const int uoff = K.T.level_uptrans_offset[ul];
+  for (int j = 0; j < nuptrans; j++) {
+    const int li = K.T.uptrans_lineindex[uoff + j];
+    const int upper = K.T.line_upper[li];
+    const double epsilon_trans = epsilon(K, e, i, upper) - epsilon_current;
+    const double R = rad_excitation_ratecoeff(K, pops, mgi, e, i, l, upper, epsilon_trans, li, t_mid);
+    const double C = col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, e, i, upper));
+    pr[ARTIS_MA_ACTION_INTERNALUPSAME] += (R + C + 0.) * epsilon_current;
+  }
+  if (i < K.T.elem_nions[e] - 1 && l < K.T.ion_ionisinglevels[ui]) {
+    const int nt = K.T.level_nphixstargets[ul];
+    const int slot0 = K.T.level_phixstargets_offset[ul];
+    for (int t = 0; t < nt; t++) {
+      const double epsilon_trans = get_phixs_threshold(K, e, i, l, t);
+      const double R = K.C.corrphot[(int64_t)k * K.T.ntargets_total + slot0 + t];
+      const double C = col_ionization_ratecoeff(K, T_e, nne, e, i, l, t, epsilon_trans);
+      pr[ARTIS_MA_ACTION_INTERNALUPHIGHER] += (R + C) * epsilon_current;
+    }
+  }
+  double *out = K.C.marates + idx * ARTIS_MA_ACTION_COUNT;
+  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) out[a] = pr[a];
+}
+
+__global__ void k_aos_to_soa(const uint64_t *__restrict__ aos, uint64_t *__restrict__ soa, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  for (int w = 0; w < PKT_WORDS; w++) soa[(int64_t)w * n + i] = aos[i * PKT_WORDS + w];
+}
+__global__ void k_soa_to_aos(const uint64_t *__restrict__ soa, uint64_t *__restrict__ aos, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  for (int w = 0; w < PKT_WORDS; w++) aos[i * PKT_WORDS + w] = soa[(int64_t)w * n + i];
+}
+
+// update_packets.cc:234-333 (pass loop flattened, deviation D5) + do_packet update_packets.cc:137-202
+#define TRANSPORT_BLOCK 256
+__global__ __launch_bounds__(TRANSPORT_BLOCK) void k_transport(Ctx K, uint64_t *__restrict__ soa, int64_t n, int nts,
+                                                              double t2) {
+  __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
+  __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
+  __shared__ double s_cmflum[TRANSPORT_BLOCK / 64];
+  for (int j = threadIdx.x; j < ARTIS_COUNTER_COUNT + 1; j += blockDim.x) s_ctr[j] = 0;
+  for (int j = threadIdx.x; j < ARTIS_WORK_COUNT; j += blockDim.x) s_work[j] = 0;
+  __syncthreads();
+  LocalCounters L;
+  L.ctr = &s_ctr[0];
+  L.work = &s_work[0];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double cmf_lum = 0.;
+  if (i < n) {
+    Pkt p;
+    pkt_load(soa, n, i, p);
+    p.interactions = 0;  // update_packets.cc:285-288
+    p.scat_count = 0;
+    if (p.type != ARTIS_TYPE_ESCAPE && p.prop_time < t2) {
+      lwork(L, WK_PACKETS_ACTIVE, 1);
+      Tx x(K, L);
+      x.nts = nts;
+      x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
+      long long iters = 0;
+      while (x.ok && p.type != ARTIS_TYPE_ESCAPE && p.prop_time < t2) {
+        if (++iters > 2000000ll) {
+          x.err(ERR_STUCK, p.number, 0);
+          break;
+        }
+        const int pkt_type = p.type;
+        if (pkt_type == ARTIS_TYPE_RPKT) {
+          while (x.ok && do_rpkt_step(x, p, t2)) {
+          }
+          if (p.type == ARTIS_TYPE_ESCAPE) {
+            cmf_lum += p.e_cmf;
+            lwork(L, WK_ESCAPED, 1);
+          }
+        } else if (pkt_type == ARTIS_TYPE_KPKT || pkt_type == ARTIS_TYPE_PRE_KPKT) {
+          const int mgi = cell_mgi(K, p.where);
+          if (pkt_type == ARTIS_TYPE_PRE_KPKT || K.C.thick[mgi] == 1)
+            do_kpkt_bb(x, p);
+          else
+            do_kpkt(x, p, t2);
+        } else if (pkt_type == ARTIS_TYPE_MA) {
+          do_macroatom(x, p);
+        } else {
+          x.err(ERR_UNSUPPORTED_TYPE, p.number, pkt_type);
+        }
+      }
+    }
+    pkt_store(soa, n, i, p);
+  }
+  // cmf_lum: wave reduction then one atomic per block (update_packets.cc:161)
+  for (int off = 32; off > 0; off >>= 1) cmf_lum += __shfl_down(cmf_lum, off, 64);
+  if ((threadIdx.x & 63) == 0) s_cmflum[threadIdx.x >> 6] = cmf_lum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.;
+    for (int w = 0; w < TRANSPORT_BLOCK / 64; w++) s += s_cmflum[w];
+    if (s != 0.) unsafeAtomicAdd(&K.E.scalars[0], s);
+  }
+  for (int j = threadIdx.x; j < ARTIS_COUNTER_COUNT + 1; j += blockDim.x)
+    if (s_ctr[j]) atomicAdd(&K.E.counters[j], s_ctr[j]);
+  for (int j = threadIdx.x; j < ARTIS_WORK_COUNT; j += blockDim.x)
+    if (s_work[j]) atomicAdd(&K.E.work[j], s_work[j]);
+}
+
+// pack estimators into one double block (for an RCCL all-reduce by the caller) and back
+__global__ void k_pack_counts(const int32_t *ecounter, const int32_t *acounter, const unsigned long long *counters,
+                              double *dst, int nlines, int dir) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = 2 * (int64_t)nlines + ARTIS_COUNTER_COUNT + 1;
+  if (i >= n) return;
+  if (dir == 0) {
+    if (i < nlines)
+      dst[i] = ecounter[i];
+    else if (i < 2 * nlines)
+      dst[i] = acounter[i - nlines];
+    else
+      dst[i] = (double)counters[i - 2 * nlines];
+  } else {
+    if (i < nlines)
+      const_cast<int32_t *>(ecounter)[i] = (int32_t)llrint(dst[i]);
+    else if (i < 2 * nlines)
+      const_cast<int32_t *>(acounter)[i - nlines] = (int32_t)llrint(dst[i]);
+    else
+      const_cast<unsigned long long *>(counters)[i - 2 * nlines] = (unsigned long long)llrint(dst[i]);
+  }
+}
+
+// ================================================================================================= host side
+namespace {
+
+struct Engine {
+  bool initialised = false;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  std::vector<void *> allocs;
+  Ctx K{};
+  artis_run_params params{};
+  // sizes
+  int npts_model = 0, nelements = 0, maxnions = 0, nions_total = 0, nlines = 0, ngrid = 0;
+  int64_t n_est_doubles = 0;  // J..bfheat + scalars
+  double *d_estblock = nullptr;
+  int32_t *d_target_ul = nullptr, *d_target_t = nullptr;
+  bool have_cells = false;
+  int cellstate_nts = -1;
+  int cap_nonempty = 0;
+  // cell-state device buffers
+  float *d_cellf = nullptr;  // packed float arrays
+  int16_t *d_thick = nullptr;
+  float *d_abund = nullptr, *d_glp = nullptr, *d_pf = nullptr;
+  double *d_totcool = nullptr, *d_ccion = nullptr, *d_renorm = nullptr;
+  int32_t *d_ne_index = nullptr, *d_ne_mgi = nullptr;
+  // packets
+  uint64_t *d_soa = nullptr, *d_aos = nullptr, *d_snapshot = nullptr;
+  int64_t cap_pkts = 0, npkts = 0;
+  bool have_snapshot = false;
+  double last_transport_ms = 0., last_precompute_ms = 0.;
+  int64_t last_work[ARTIS_WORK_COUNT] = {0};
+  std::string last_error;
+};
+Engine G;
+
+#define HIPCHK(x)                                                                             \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess) {                                                                   \
+      G.last_error = std::string(#x) + ": " + hipGetErrorString(e_);                          \
+      return ARTIS_ERR_HIP;                                                                   \
+    }                                                                                         \
+  } while (0)
+
+template <typename T>
+int dalloc(T **p, size_t count) {
+  if (count == 0) count = 1;
+  HIPCHK(hipMalloc((void **)p, count * sizeof(T)));
+  G.allocs.push_back((void *)*p);
+  return 0;
+}
+template <typename T>
+int dupload(const T **dst, const T *src, size_t count) {
+  T *d = nullptr;
+  if (dalloc(&d, count)) return ARTIS_ERR_HIP;
+  if (count && src) HIPCHK(hipMemcpy(d, src, count * sizeof(T), hipMemcpyHostToDevice));
+  *dst = d;
+  return 0;
+}
+
+int64_t sum_i32(const int32_t *a, int n) {
+  int64_t s = 0;
+  for (int i = 0; i < n; i++) s += a[i];
+  return s;
+}
+
+int check_kernel_error(const char *what) {
+  int32_t err[4] = {0, 0, 0, 0};
+  HIPCHK(hipMemcpy(err, G.K.E.err, sizeof(err), hipMemcpyDeviceToHost));
+  if (err[0] != 0) {
+    char buf[256];
+    snprintf(buf, sizeof buf, "%s: device error code %d packet %d aux %d", what, err[0], err[1], err[2]);
+    G.last_error = buf;
+    return (err[0] == ERR_UNSUPPORTED_TYPE) ? ARTIS_ERR_UNSUPPORTED : ARTIS_ERR_PACKET_FAULT;
+  }
+  return 0;
+}
+
+int alloc_packets(int64_t n) {
+  if (n <= G.cap_pkts) return 0;
+  if (G.d_soa) {
+    (void)hipFree(G.d_soa);
+    (void)hipFree(G.d_aos);
+    if (G.d_snapshot) (void)hipFree(G.d_snapshot);
+    G.d_snapshot = nullptr;
+    G.have_snapshot = false;
+  }
+  HIPCHK(hipMalloc(&G.d_soa, (size_t)n * PKT_WORDS * 8));
+  HIPCHK(hipMalloc(&G.d_aos, (size_t)n * PKT_WORDS * 8));
+  G.cap_pkts = n;
+  return 0;
+}
+
+}  // namespace
+
+// ============================================================================================== C ABI
+extern "C" {
+
+int artis_gpu_abi_version(void) { return 1; }
+const char *artis_gpu_last_error(void) { return G.last_error.c_str(); }
+double artis_gpu_last_transport_ms(void) { return G.last_transport_ms; }
+double artis_gpu_last_precompute_ms(void) { return G.last_precompute_ms; }
+int artis_gpu_last_work_counts(int64_t out[ARTIS_WORK_COUNT]) {
+  for (int k = 0; k < ARTIS_WORK_COUNT; k++) out[k] = G.last_work[k];
+  return 0;
+}
+
+void artis_gpu_finalize(void) {
+  if (!G.initialised) return;
+  for (void *p : G.allocs) (void)hipFree(p);
+  G.allocs.clear();
+  if (G.d_soa) (void)hipFree(G.d_soa);
+  if (G.d_aos) (void)hipFree(G.d_aos);
+  if (G.d_snapshot) (void)hipFree(G.d_snapshot);
+  if (G.ev0) (void)hipEventDestroy(G.ev0);
+  if (G.ev1) (void)hipEventDestroy(G.ev1);
+  if (G.ev2) (void)hipEventDestroy(G.ev2);
+  if (G.stream) (void)hipStreamDestroy(G.stream);
+  G = Engine();
+}
+
+int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometry *g, const artis_run_params *rp) {
+  if (!a || !g || !rp) return ARTIS_ERR_BAD_ARGUMENT;
+  if (G.initialised) artis_gpu_finalize();
+  if (g->grid_type != ARTIS_GRID_UNIFORM) {
+    G.last_error = "only GRID_UNIFORM is propagated by this build";
+    return ARTIS_ERR_UNSUPPORTED;
+  }
+  if (rp->relativistic_doppler) {
+    G.last_error = "USE_RELATIVISTIC_DOPPLER_SHIFT is not propagated by this build";
+    return ARTIS_ERR_UNSUPPORTED;
+  }
+  G.device = device;
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipStreamCreateWithFlags(&G.stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreate(&G.ev0));
+  HIPCHK(hipEventCreate(&G.ev1));
+  HIPCHK(hipEventCreate(&G.ev2));
+  G.params = *rp;
+  DevTab &T = G.K.T;
+  T.nelements = a->nelements;
+  T.maxnions = a->maxnions;
+  T.nions_total = a->nions_total;
+  T.nlevels_total = a->nlevels_total;
+  T.nlines = a->nlines;
+  T.nbf = a->nbfcontinua;
+  T.nbfg = a->nbfcontinua_ground;
+  T.ncoolingterms = a->ncoolingterms;
+  T.nphixspoints = a->nphixspoints;
+  T.phixs_file_version = a->phixs_file_version;
+  T.tablesize = a->tablesize;
+  T.nphixsnuincrement = a->nphixsnuincrement;
+  T.last_phixs_nuovernuedge = a->last_phixs_nuovernuedge;
+  T.mintemp = a->mintemp;
+  T.T_step_log = (log(a->maxtemp) - log(a->mintemp)) / (a->tablesize - 1.);  // ratecoeff.cc:1004
+  const int ne = a->nelements, ni = a->nions_total, nl = a->nlevels_total, nli = a->nlines, nb = a->nbfcontinua;
+  const int64_t nup = sum_i32(a->level_nuptrans, nl), ndown = sum_i32(a->level_ndowntrans, nl);
+  const int64_t ntg = sum_i32(a->level_nphixstargets, nl);
+  T.ntargets_total = (int)ntg;
+  int64_t ntables = 0;
+  for (int i = 0; i < nl; i++) ntables = std::max<int64_t>(ntables, a->level_phixstable[i] + 1);
+  int rc = 0;
+  rc |= dupload(&T.elem_nions, a->elem_nions, ne);
+  rc |= dupload(&T.elem_uniqueionoffset, a->elem_uniqueionoffset, ne);
+  rc |= dupload(&T.ion_ionstage, a->ion_ionstage, ni);
+  rc |= dupload(&T.ion_nlevels, a->ion_nlevels, ni);
+  rc |= dupload(&T.ion_uniqueleveloffset, a->ion_uniqueleveloffset, ni);
+  rc |= dupload(&T.ion_ionisinglevels, a->ion_ionisinglevels, ni);
+  rc |= dupload(&T.ion_maxrecombininglevel, a->ion_maxrecombininglevel, ni);
+  rc |= dupload(&T.ion_coolingoffset, a->ion_coolingoffset, ni);
+  rc |= dupload(&T.ion_ncoolingterms, a->ion_ncoolingterms, ni);
+  std::vector<int32_t> ion_element(ni), level_ui(nl);
+  for (int e = 0; e < ne; e++)
+    for (int i = 0; i < a->elem_nions[e]; i++) ion_element[a->elem_uniqueionoffset[e] + i] = e;
+  for (int ui = 0; ui < ni; ui++)
+    for (int l = 0; l < a->ion_nlevels[ui]; l++) level_ui[a->ion_uniqueleveloffset[ui] + l] = ui;
+  rc |= dupload(&T.ion_element, ion_element.data(), ni);
+  rc |= dupload(&T.level_ui, level_ui.data(), nl);
+  rc |= dupload(&T.level_epsilon, a->level_epsilon, nl);
+  rc |= dupload(&T.level_stat_weight, a->level_stat_weight, nl);
+  rc |= dupload(&T.level_nuptrans, a->level_nuptrans, nl);
+  rc |= dupload(&T.level_uptrans_offset, a->level_uptrans_offset, nl);
+  rc |= dupload(&T.level_ndowntrans, a->level_ndowntrans, nl);
+  rc |= dupload(&T.level_downtrans_offset, a->level_downtrans_offset, nl);
+  rc |= dupload(&T.level_nphixstargets, a->level_nphixstargets, nl);
+  rc |= dupload(&T.level_phixstargets_offset, a->level_phixstargets_offset, nl);
+  rc |= dupload(&T.level_cont_index, a->level_cont_index, nl);
+  rc |= dupload(&T.level_closestgroundlevelcont, a->level_closestgroundlevelcont, nl);
+  rc |= dupload(&T.level_phixstable, a->level_phixstable, nl);
+  rc |= dupload(&T.uptrans_lineindex, a->uptrans_lineindex, nup);
+  rc |= dupload(&T.downtrans_lineindex, a->downtrans_lineindex, ndown);
+  rc |= dupload(&T.phixstarget_levelindex, a->phixstarget_levelindex, ntg);
+  rc |= dupload(&T.phixstarget_probability, a->phixstarget_probability, ntg);
+  rc |= dupload(&T.phixs_xs, a->phixs_xs, (size_t)ntables * a->nphixspoints);
+  rc |= dupload(&T.line_nu, a->line_nu, nli);
+  rc |= dupload(&T.line_A, a->line_einstein_A, nli);
+  rc |= dupload(&T.line_f, a->line_osc_strength, nli);
+  rc |= dupload(&T.line_coll, a->line_coll_str, nli);
+  rc |= dupload(&T.line_elem, a->line_elementindex, nli);
+  rc |= dupload(&T.line_ion, a->line_ionindex, nli);
+  rc |= dupload(&T.line_upper, a->line_upperlevelindex, nli);
+  rc |= dupload(&T.line_lower, a->line_lowerlevelindex, nli);
+  rc |= dupload(&T.line_forbidden, a->line_forbidden, nli);
+  // per-line Sobolev coefficients, evaluated on the host with the same expression as rpkt.cc:179-181
+  std::vector<LineTau> lt(nli);
+  for (int li = 0; li < nli; li++) {
+    const int e = a->line_elementindex[li], i = a->line_ionindex[li];
+    const int off = a->ion_uniqueleveloffset[a->elem_uniqueionoffset[e] + i];
+    const int ulo = off + a->line_lowerlevelindex[li], uup = off + a->line_upperlevelindex[li];
+    const double nu_trans = a->line_nu[li];
+    const double A_ul = a->line_einstein_A[li];
+    const double B_ul = ARTIS_CLIGHTSQUAREDOVERTWOH / pow(nu_trans, 3) * A_ul;
+    const double B_lu = (double)a->level_stat_weight[uup] / (double)a->level_stat_weight[ulo] * B_ul;
+    lt[li] = {B_ul, B_lu, ulo, uup};
+  }
+  rc |= dupload(&T.line_tau, lt.data(), nli);
+  rc |= dupload(&T.allcont_nu_edge, a->allcont_nu_edge, nb);
+  rc |= dupload(&T.allcont_probability, a->allcont_probability, nb);
+  rc |= dupload(&T.allcont_element, a->allcont_element, nb);
+  rc |= dupload(&T.allcont_ion, a->allcont_ion, nb);
+  rc |= dupload(&T.allcont_level, a->allcont_level, nb);
+  rc |= dupload(&T.allcont_target, a->allcont_phixstargetindex, nb);
+  rc |= dupload(&T.allcont_upperlevel, a->allcont_upperlevel, nb);
+  rc |= dupload(&T.allcont_phixstable, a->allcont_phixstable, nb);
+  rc |= dupload(&T.allcont_groundindex, a->allcont_index_in_groundphixslist, nb);
+  rc |= dupload(&T.groundcont_nu_edge, a->groundcont_nu_edge, a->nbfcontinua_ground);
+  rc |= dupload(&T.groundcont_element, a->groundcont_element, a->nbfcontinua_ground);
+  rc |= dupload(&T.groundcont_ion, a->groundcont_ion, a->nbfcontinua_ground);
+  rc |= dupload(&T.spontrecombcoeff, a->spontrecombcoeff, (size_t)a->tablesize * nb);
+  rc |= dupload(&T.corrphotoioncoeff, a->corrphotoioncoeff, (size_t)a->tablesize * nb);
+  rc |= dupload(&T.bfcooling_coeff, a->bfcooling_coeff, (size_t)a->tablesize * nb);
+  rc |= dupload(&T.cool_type, a->coolinglist_type, a->ncoolingterms);
+  rc |= dupload(&T.cool_element, a->coolinglist_element, a->ncoolingterms);
+  rc |= dupload(&T.cool_ion, a->coolinglist_ion, a->ncoolingterms);
+  rc |= dupload(&T.cool_level, a->coolinglist_level, a->ncoolingterms);
+  rc |= dupload(&T.cool_upper, a->coolinglist_upperlevel, a->ncoolingterms);
+  // photoionisation target slots -> (unique level, target index)
+  std::vector<int32_t> tul(ntg + 1), tt(ntg + 1);
+  for (int ul = 0; ul < nl; ul++)
+    for (int t = 0; t < a->level_nphixstargets[ul]; t++) {
+      tul[a->level_phixstargets_offset[ul] + t] = ul;
+      tt[a->level_phixstargets_offset[ul] + t] = t;
+    }
+  const int32_t *dtul, *dtt;
+  rc |= dupload(&dtul, tul.data(), ntg + 1);
+  rc |= dupload(&dtt, tt.data(), ntg + 1);
+  G.d_target_ul = const_cast<int32_t *>(dtul);
+  G.d_target_t = const_cast<int32_t *>(dtt);
+
+  // geometry
+  DevGeom &GG = G.K.G;
+  for (int d = 0; d < 3; d++) GG.ncoordgrid[d] = g->ncoordgrid[d];
+  GG.ngrid = g->ngrid;
+  GG.npts_model = g->npts_model;
+  rc |= dupload(&GG.cell_pos_min, g->cell_pos_min, (size_t)g->ngrid * 3);
+  rc |= dupload(&GG.cell_mgi, g->cell_mgi, g->ngrid);
+  GG.coordmax0 = g->coordmax[0];
+  GG.tmin = g->tmin;
+  GG.rmax = g->rmax;
+  GG.wid = 2 * g->coordmax[0] / g->ncoordgrid[0];  // grid.cc:76-91
+  rc |= dupload(&GG.ts_start, g->ts_start, g->ntstep);
+  rc |= dupload(&GG.ts_width, g->ts_width, g->ntstep);
+  rc |= dupload(&GG.ts_mid, g->ts_mid, g->ntstep);
+  GG.nu_min_r = g->nu_min_r;
+  GG.nu_max_r = g->nu_max_r;
+
+  DevRun &R = G.K.R;
+  R.seed = rp->seed;
+  R.rank = rp->rank;
+  R.opacity_case = rp->opacity_case;
+  R.do_r_lc = rp->do_r_lc;
+  R.do_rlc_est = rp->do_rlc_est;
+  R.n_kpktdiffusion_timesteps = rp->n_kpktdiffusion_timesteps;
+  R.kpktdiffusion_timescale = rp->kpktdiffusion_timescale;
+  R.max_path_step = rp->max_path_step;
+  R.pol_dipole = rp->pol_dipole;
+  R.relativistic_doppler = rp->relativistic_doppler;
+  R.record_linestat = rp->record_linestat;
+
+  // estimators: one double block [J | nuJ | ffheat | colheat | gamma | bfheat | scalars(8)]
+  const int np = g->npts_model;
+  const int64_t nion_est = (int64_t)np * ne * a->maxnions;
+  G.n_est_doubles = 4 * (int64_t)np + 2 * nion_est + 8;
+  rc |= dalloc(&G.d_estblock, G.n_est_doubles);
+  DevEst &E = G.K.E;
+  E.J = G.d_estblock;
+  E.nuJ = E.J + np;
+  E.ffheat = E.nuJ + np;
+  E.colheat = E.ffheat + np;
+  E.gamma = E.colheat + np;
+  E.bfheat = E.gamma + nion_est;
+  E.scalars = E.bfheat + nion_est;
+  rc |= dalloc(&E.ecounter, nli);
+  rc |= dalloc(&E.acounter, nli);
+  rc |= dalloc(&E.counters, ARTIS_COUNTER_COUNT + 1);
+  rc |= dalloc(&E.work, ARTIS_WORK_COUNT);
+  rc |= dalloc(&E.err, 4);
+  if (rc) return ARTIS_ERR_HIP;
+  G.npts_model = np;
+  G.nelements = ne;
+  G.maxnions = a->maxnions;
+  G.nions_total = ni;
+  G.nlines = nli;
+  G.ngrid = g->ngrid;
+  // non-empty model cells: those referenced by a propagation cell
+  std::vector<int32_t> ne_index(np, -1), ne_mgi;
+  for (int c = 0; c < g->ngrid; c++) {
+    const int mgi = g->cell_mgi[c];
+    if (mgi >= 0 && mgi < np && ne_index[mgi] < 0) {
+      ne_index[mgi] = 0;
+    }
+  }
+  for (int mgi = 0; mgi < np; mgi++)
+    if (ne_index[mgi] == 0) {
+      ne_index[mgi] = (int)ne_mgi.size();
+      ne_mgi.push_back(mgi);
+    }
+  const int nne_cells = (int)ne_mgi.size();
+  const int32_t *dnei, *dnem;
+  rc |= dupload(&dnei, ne_index.data(), np);
+  rc |= dupload(&dnem, ne_mgi.data(), nne_cells);
+  DevCells &C = G.K.C;
+  C.ne_index = dnei;
+  C.ne_mgi = dnem;
+  C.n_nonempty = nne_cells;
+  rc |= dalloc(&C.pops, (size_t)nne_cells * nl);
+  rc |= dalloc(&C.ionpop, (size_t)nne_cells * ni);
+  rc |= dalloc(&C.ffsum, (size_t)nne_cells);
+  rc |= dalloc(&C.depratio, (size_t)nne_cells * nb);
+  rc |= dalloc(&C.corrphot, (size_t)nne_cells * (ntg + 1));
+  rc |= dalloc(&C.cooling, (size_t)nne_cells * a->ncoolingterms);
+  rc |= dalloc(&C.marates, (size_t)nne_cells * nl * ARTIS_MA_ACTION_COUNT);
+  // cell-state input buffers
+  rc |= dalloc(&G.d_cellf, (size_t)8 * np);
+  rc |= dalloc(&G.d_thick, (size_t)np);
+  rc |= dalloc(&G.d_abund, (size_t)np * ne);
+  rc |= dalloc(&G.d_glp, (size_t)np * ni);
+  rc |= dalloc(&G.d_pf, (size_t)np * ni);
+  rc |= dalloc(&G.d_totcool, (size_t)np);
+  rc |= dalloc(&G.d_ccion, (size_t)np * ni);
+  rc |= dalloc(&G.d_renorm, (size_t)np * ne * a->maxnions);
+  if (rc) return ARTIS_ERR_HIP;
+  C.Te = G.d_cellf;
+  C.TR = G.d_cellf + np;
+  C.TJ = G.d_cellf + 2 * np;
+  C.W = G.d_cellf + 3 * np;
+  C.nne = G.d_cellf + 4 * np;
+  C.nnetot = G.d_cellf + 5 * np;
+  C.rho = G.d_cellf + 6 * np;
+  C.kappagrey = G.d_cellf + 7 * np;
+  C.thick = G.d_thick;
+  C.elem_abundance = G.d_abund;
+  C.groundlevelpop = G.d_glp;
+  C.partfunct = G.d_pf;
+  C.totalcooling = G.d_totcool;
+  C.cooling_contrib_ion = G.d_ccion;
+  C.corrphotoionrenorm = G.d_renorm;
+  G.initialised = true;
+  return 0;
+}
+
+int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  if (!cs || nts < 0) return ARTIS_ERR_BAD_ARGUMENT;
+  const int np = G.npts_model, ne = G.nelements, ni = G.nions_total;
+  const float *fsrc[8] = {cs->Te, cs->TR, cs->TJ, cs->W, cs->nne, cs->nnetot, cs->rho, cs->kappagrey};
+  for (int f = 0; f < 8; f++)
+    HIPCHK(hipMemcpyAsync(G.d_cellf + (size_t)f * np, fsrc[f], sizeof(float) * np, hipMemcpyHostToDevice, G.stream));
+  HIPCHK(hipMemcpyAsync(G.d_thick, cs->thick, sizeof(int16_t) * np, hipMemcpyHostToDevice, G.stream));
+  HIPCHK(hipMemcpyAsync(G.d_abund, cs->elem_abundance, sizeof(float) * np * ne, hipMemcpyHostToDevice, G.stream));
+  HIPCHK(hipMemcpyAsync(G.d_glp, cs->groundlevelpop, sizeof(float) * np * ni, hipMemcpyHostToDevice, G.stream));
+  HIPCHK(hipMemcpyAsync(G.d_pf, cs->partfunct, sizeof(float) * np * ni, hipMemcpyHostToDevice, G.stream));
+  HIPCHK(hipMemcpyAsync(G.d_totcool, cs->totalcooling, sizeof(double) * np, hipMemcpyHostToDevice, G.stream));
+  HIPCHK(hipMemcpyAsync(G.d_ccion, cs->cooling_contrib_ion, sizeof(double) * np * ni, hipMemcpyHostToDevice, G.stream));
+  HIPCHK(hipMemcpyAsync(G.d_renorm, cs->corrphotoionrenorm, sizeof(double) * np * ne * G.maxnions,
+                        hipMemcpyHostToDevice, G.stream));
+  HIPCHK(hipStreamSynchronize(G.stream));
+  HIPCHK(hipMemsetAsync(G.K.E.err, 0, 4 * sizeof(int32_t), G.stream));
+  const int n_ne = G.K.C.n_nonempty;
+  const int64_t nl = G.K.T.nlevels_total;
+  HIPCHK(hipEventRecord(G.ev0, G.stream));
+  if (n_ne > 0) {
+    const int B = 256;
+    k_cellprep<<<(n_ne + B - 1) / B, B, 0, G.stream>>>(G.K);
+    const int64_t nlv = (int64_t)n_ne * nl;
+    k_levelpops<<<(unsigned)((nlv + B - 1) / B), B, 0, G.stream>>>(G.K);
+    const int64_t nbt = (int64_t)n_ne * (G.K.T.nbf + G.K.T.ntargets_total);
+    k_bfcells<<<(unsigned)((nbt + B - 1) / B), B, 0, G.stream>>>(G.K, G.d_target_ul, G.d_target_t);
+    const int64_t nci = (int64_t)n_ne * ni;
+    k_cooling<<<(unsigned)((nci + 63) / 64), 64, 0, G.stream>>>(G.K);
+    k_marates<<<(unsigned)((nlv + 63) / 64), 64, 0, G.stream>>>(G.K, nts);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipEventRecord(G.ev1, G.stream));
+  HIPCHK(hipEventSynchronize(G.ev1));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, G.ev0, G.ev1));
+  G.last_precompute_ms = ms;
+  G.have_cells = true;
+  G.cellstate_nts = nts;
+  return 0;
+}
+
+int artis_gpu_packets_upload(const artis_packet *packets, int npkts) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  if (npkts < 0 || (npkts > 0 && !packets)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (int rc = alloc_packets(npkts)) return rc;
+  G.npkts = npkts;
+  if (npkts == 0) return 0;
+  HIPCHK(hipMemcpyAsync(G.d_aos, packets, (size_t)npkts * sizeof(artis_packet), hipMemcpyHostToDevice, G.stream));
+  k_aos_to_soa<<<(unsigned)((npkts + 255) / 256), 256, 0, G.stream>>>(G.d_aos, G.d_soa, npkts);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(G.stream));
+  return 0;
+}
+
+int artis_gpu_packets_download(artis_packet *packets, int npkts) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  if (npkts != G.npkts) return ARTIS_ERR_BAD_ARGUMENT;
+  if (npkts == 0) return 0;
+  k_soa_to_aos<<<(unsigned)((npkts + 255) / 256), 256, 0, G.stream>>>(G.d_soa, G.d_aos, npkts);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(packets, G.d_aos, (size_t)npkts * sizeof(artis_packet), hipMemcpyDeviceToHost, G.stream));
+  HIPCHK(hipStreamSynchronize(G.stream));
+  return 0;
+}
+
+int artis_gpu_packets_snapshot(void) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  if (!G.d_snapshot) HIPCHK(hipMalloc(&G.d_snapshot, (size_t)G.cap_pkts * PKT_WORDS * 8));
+  HIPCHK(hipMemcpyAsync(G.d_snapshot, G.d_soa, (size_t)G.npkts * PKT_WORDS * 8, hipMemcpyDeviceToDevice, G.stream));
+  HIPCHK(hipStreamSynchronize(G.stream));
+  G.have_snapshot = true;
+  return 0;
+}
+
+int artis_gpu_packets_restore(void) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  if (!G.have_snapshot) return ARTIS_ERR_BAD_ARGUMENT;
+  HIPCHK(hipMemcpyAsync(G.d_soa, G.d_snapshot, (size_t)G.npkts * PKT_WORDS * 8, hipMemcpyDeviceToDevice, G.stream));
+  return 0;
+}
+
+int artis_gpu_estimators_zero(void) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  const DevEst &E = G.K.E;
+  HIPCHK(hipMemsetAsync(G.d_estblock, 0, (size_t)G.n_est_doubles * sizeof(double), G.stream));
+  HIPCHK(hipMemsetAsync(E.ecounter, 0, (size_t)G.nlines * sizeof(int32_t), G.stream));
+  HIPCHK(hipMemsetAsync(E.acounter, 0, (size_t)G.nlines * sizeof(int32_t), G.stream));
+  HIPCHK(hipMemsetAsync(E.counters, 0, (ARTIS_COUNTER_COUNT + 1) * sizeof(unsigned long long), G.stream));
+  return 0;
+}
+
+int artis_gpu_update_packets_resident(int my_rank, int nts) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  if (!G.have_cells || G.cellstate_nts != nts) {
+    G.last_error = "artis_gpu_upload_cellstate(nts) must precede update_packets(nts)";
+    return ARTIS_ERR_NO_CELLSTATE;
+  }
+  if (my_rank != G.K.R.rank) G.K.R.rank = my_rank;
+  double ts = 0, tw = 0;
+  // time grid lives on the device; the host copy is not kept, so read the two scalars
+  HIPCHK(hipMemcpy(&ts, G.K.G.ts_start + nts, sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&tw, G.K.G.ts_width + nts, sizeof(double), hipMemcpyDeviceToHost));
+  const double t2 = ts + tw;
+  HIPCHK(hipMemsetAsync(G.K.E.err, 0, 4 * sizeof(int32_t), G.stream));
+  HIPCHK(hipMemsetAsync(G.K.E.work, 0, ARTIS_WORK_COUNT * sizeof(unsigned long long), G.stream));
+  const int64_t n = G.npkts;
+  HIPCHK(hipEventRecord(G.ev0, G.stream));
+  if (n > 0) {
+    k_transport<<<(unsigned)((n + TRANSPORT_BLOCK - 1) / TRANSPORT_BLOCK), TRANSPORT_BLOCK, 0, G.stream>>>(
+        G.K, G.d_soa, n, nts, t2);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipEventRecord(G.ev1, G.stream));
+  HIPCHK(hipEventSynchronize(G.ev1));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, G.ev0, G.ev1));
+  G.last_transport_ms = ms;
+  unsigned long long w[ARTIS_WORK_COUNT];
+  HIPCHK(hipMemcpy(w, G.K.E.work, sizeof(w), hipMemcpyDeviceToHost));
+  for (int k = 0; k < ARTIS_WORK_COUNT; k++) G.last_work[k] = (int64_t)w[k];
+  return check_kernel_error("update_packets");
+}
+
+int artis_gpu_estimators_download(artis_estimators *est) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  if (!est) return ARTIS_ERR_BAD_ARGUMENT;
+  HIPCHK(hipStreamSynchronize(G.stream));
+  const int np = G.npts_model;
+  const int64_t nion_est = (int64_t)np * G.nelements * G.maxnions;
+  std::vector<double> blk(G.n_est_doubles);
+  HIPCHK(hipMemcpy(blk.data(), G.d_estblock, blk.size() * sizeof(double), hipMemcpyDeviceToHost));
+  auto add = [&](double *dst, int64_t off, int64_t cnt) {
+    if (!dst) return;
+    for (int64_t j = 0; j < cnt; j++) dst[j] += blk[off + j];
+  };
+  add(est->J, 0, np);
+  add(est->nuJ, np, np);
+  add(est->ffheatingestimator, 2 * (int64_t)np, np);
+  add(est->colheatingestimator, 3 * (int64_t)np, np);
+  add(est->gammaestimator, 4 * (int64_t)np, nion_est);
+  add(est->bfheatingestimator, 4 * (int64_t)np + nion_est, nion_est);
+  const double *sc = blk.data() + 4 * (int64_t)np + 2 * nion_est;
+  est->cmf_lum += sc[0];
+  est->gamma_dep += sc[1];
+  est->positron_dep += sc[2];
+  est->electron_dep += sc[3];
+  est->electron_emission += sc[4];
+  est->alpha_dep += sc[5];
+  est->alpha_emission += sc[6];
+  est->gamma_emission += sc[7];
+  std::vector<int32_t> lc(G.nlines);
+  if (est->ecounter) {
+    HIPCHK(hipMemcpy(lc.data(), G.K.E.ecounter, lc.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+    for (int j = 0; j < G.nlines; j++) est->ecounter[j] += lc[j];
+  }
+  if (est->acounter) {
+    HIPCHK(hipMemcpy(lc.data(), G.K.E.acounter, lc.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+    for (int j = 0; j < G.nlines; j++) est->acounter[j] += lc[j];
+  }
+  unsigned long long ctr[ARTIS_COUNTER_COUNT + 1];
+  HIPCHK(hipMemcpy(ctr, G.K.E.counters, sizeof(ctr), hipMemcpyDeviceToHost));
+  for (int j = 0; j < ARTIS_COUNTER_COUNT; j++) est->counters[j] += (int64_t)ctr[j];
+  est->nesc += (int64_t)ctr[ARTIS_COUNTER_COUNT];
+  return 0;
+}
+
+size_t artis_gpu_estimator_block_doubles(void) {
+  if (!G.initialised) return 0;
+  return (size_t)G.n_est_doubles + 2 * (size_t)G.nlines + ARTIS_COUNTER_COUNT + 1;
+}
+
+int artis_gpu_estimator_block_to_device(void *dst) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  double *d = (double *)dst;
+  HIPCHK(hipMemcpyAsync(d, G.d_estblock, (size_t)G.n_est_doubles * sizeof(double), hipMemcpyDeviceToDevice, G.stream));
+  const int64_t nc = 2 * (int64_t)G.nlines + ARTIS_COUNTER_COUNT + 1;
+  k_pack_counts<<<(unsigned)((nc + 255) / 256), 256, 0, G.stream>>>(G.K.E.ecounter, G.K.E.acounter, G.K.E.counters,
+                                                                     d + G.n_est_doubles, G.nlines, 0);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(G.stream));
+  return 0;
+}
+
+int artis_gpu_estimator_block_from_device(const void *src) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  const double *s = (const double *)src;
+  HIPCHK(hipMemcpyAsync(G.d_estblock, s, (size_t)G.n_est_doubles * sizeof(double), hipMemcpyDeviceToDevice, G.stream));
+  const int64_t nc = 2 * (int64_t)G.nlines + ARTIS_COUNTER_COUNT + 1;
+  k_pack_counts<<<(unsigned)((nc + 255) / 256), 256, 0, G.stream>>>(G.K.E.ecounter, G.K.E.acounter, G.K.E.counters,
+                                                                     const_cast<double *>(s) + G.n_est_doubles,
+                                                                     G.nlines, 1);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(G.stream));
+  return 0;
+}
+
+int artis_gpu_update_packets(int my_rank, int nts, artis_packet *packets, int npkts, artis_estimators *est) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  if (npkts < 0 || (npkts > 0 && !packets) || !est) return ARTIS_ERR_BAD_ARGUMENT;
+  int rc = artis_gpu_packets_upload(packets, npkts);
+  if (rc) return rc;
+  rc = artis_gpu_estimators_zero();
+  if (rc) return rc;
+  rc = artis_gpu_update_packets_resident(my_rank, nts);
+  if (rc) return rc;
+  rc = artis_gpu_packets_download(packets, npkts);
+  if (rc) return rc;
+  return artis_gpu_estimators_download(est);
+}
+
+}  // extern "C"

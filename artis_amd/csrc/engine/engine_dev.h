@@ -1,0 +1,101 @@
+// engine_dev.h -- device-side data layout of the MI355X packet-propagation engine.
+//
+// HBM layout (DESIGN.md "Data layout in HBM"):
+//   * packets: structure-of-arrays of the 304-byte reference record viewed as 38 little-endian 8-byte words,
+//     soa[word * N + i]; word w of packet i holds bytes [8w, 8w+8) of `struct packet` (packet.h:28-73).
+//     A wave touching field f of 64 consecutive packets reads 512 contiguous bytes.
+//   * read-only atomic tables uploaded once (artis_gpu_init), plus a per-line record LineTau with the
+//     Einstein-B coefficients and unique level indices that get_event needs (rpkt.cc:168-181).
+//   * per-cell tables rebuilt per timestep (artis_gpu_upload_cellstate) for the non-empty model cells only,
+//     indexed by nonempty index k: level populations, ion-stage populations, departure ratios, cumulative
+//     k-packet cooling lists and macro-atom process-rate totals.  These replace the per-OpenMP-thread
+//     cellhistory cache (update_grid.cc:659-761) with tables every workitem can read.
+#ifndef ARTIS_ENGINE_DEV_H
+#define ARTIS_ENGINE_DEV_H
+
+#include <stdint.h>
+
+#define PKT_WORDS 38
+
+struct LineTau {
+  double B_ul;  // CLIGHTSQUAREDOVERTWOH / pow(nu, 3) * A_ul          (rpkt.cc:180)
+  double B_lu;  // g_u / g_l * B_ul                                    (rpkt.cc:181)
+  int32_t ul_lower;  // unique level index of the lower level
+  int32_t ul_upper;
+};
+
+struct DevTab {
+  int32_t nelements, maxnions, nions_total, nlevels_total, nlines, nbf, nbfg, ncoolingterms;
+  int32_t nphixspoints, phixs_file_version, tablesize, ntargets_total;
+  double nphixsnuincrement, last_phixs_nuovernuedge, mintemp, T_step_log;
+  const int32_t *elem_nions, *elem_uniqueionoffset;
+  const int32_t *ion_ionstage, *ion_nlevels, *ion_uniqueleveloffset, *ion_ionisinglevels, *ion_maxrecombininglevel,
+      *ion_coolingoffset, *ion_ncoolingterms, *ion_element;
+  const double *level_epsilon;
+  const float *level_stat_weight;
+  const int32_t *level_nuptrans, *level_uptrans_offset, *level_ndowntrans, *level_downtrans_offset,
+      *level_nphixstargets, *level_phixstargets_offset, *level_cont_index, *level_closestgroundlevelcont,
+      *level_phixstable, *level_ui;
+  const int32_t *uptrans_lineindex, *downtrans_lineindex, *phixstarget_levelindex;
+  const double *phixstarget_probability;
+  const float *phixs_xs;
+  const double *line_nu;
+  const float *line_A, *line_f, *line_coll;
+  const int32_t *line_elem, *line_ion, *line_upper, *line_lower;
+  const uint8_t *line_forbidden;
+  const LineTau *line_tau;
+  const double *allcont_nu_edge, *allcont_probability;
+  const int32_t *allcont_element, *allcont_ion, *allcont_level, *allcont_target, *allcont_upperlevel,
+      *allcont_phixstable, *allcont_groundindex;
+  const double *groundcont_nu_edge;
+  const int32_t *groundcont_element, *groundcont_ion;
+  const double *spontrecombcoeff, *corrphotoioncoeff, *bfcooling_coeff;
+  const int32_t *cool_type, *cool_element, *cool_ion, *cool_level, *cool_upper;
+};
+
+struct DevGeom {
+  int32_t ncoordgrid[3];
+  int32_t ngrid, npts_model;
+  const double *cell_pos_min;
+  const int32_t *cell_mgi;
+  double coordmax0, tmin, rmax, wid;
+  const double *ts_start, *ts_width, *ts_mid;
+  double nu_min_r, nu_max_r;
+};
+
+struct DevCells {
+  const float *Te, *TR, *TJ, *W, *nne, *nnetot, *rho, *kappagrey;
+  const int16_t *thick;
+  const float *elem_abundance, *groundlevelpop, *partfunct;
+  const double *totalcooling, *cooling_contrib_ion, *corrphotoionrenorm;
+  const int32_t *ne_index;  // [npts_model] nonempty index, -1 if the model cell is empty
+  const int32_t *ne_mgi;    // [n_nonempty]
+  int32_t n_nonempty;
+  double *pops;        // [n_nonempty * nlevels_total]  calculate_levelpop (ltepop.cc:417-430)
+  double *ionpop;      // [n_nonempty * nions_total]    ionstagepop (ltepop.cc:558-564)
+  double *ffsum;       // [n_nonempty]                  sum_ions Z^2 n_ion of calculate_kappa_ff (rpkt.cc:1036-1058)
+  double *depratio;    // [n_nonempty * nbf]            departure ratios (rpkt.cc:1140-1151)
+  double *corrphot;    // [n_nonempty * ntargets_total] get_corrphotoioncoeff (ratecoeff.cc:1247-1308)
+  double *cooling;     // [n_nonempty * ncoolingterms]  cumulative cooling_contrib (kpkt.cc:167-308)
+  double *marates;     // [n_nonempty * nlevels_total * 9] processrates (macroatom.cc:57-159)
+};
+
+struct DevEst {
+  double *J, *nuJ, *ffheat, *colheat, *gamma, *bfheat;  // contiguous block, see engine.hip
+  int32_t *ecounter, *acounter;
+  double *scalars;                 // [8] cmf_lum, gamma_dep, ... (artis_estimators order)
+  unsigned long long *counters;    // [34] + nesc at [34]
+  unsigned long long *work;        // [16]
+  int32_t *err;                    // [4] code, packet number, aux, aux
+};
+
+struct DevRun {
+  uint32_t seed;
+  int32_t rank;
+  int32_t opacity_case, do_r_lc, do_rlc_est, n_kpktdiffusion_timesteps;
+  float kpktdiffusion_timescale;
+  double max_path_step;
+  int32_t pol_dipole, relativistic_doppler, record_linestat;
+};
+
+#endif

@@ -1,0 +1,120 @@
+// packet_soa.h -- register image of one packet and its load/store to the 38-word SoA layout (engine_dev.h).
+// Word map = byte offsets of the reference `struct packet` (packet.h:28-73) divided by 8.
+#ifndef ARTIS_PACKET_SOA_H
+#define ARTIS_PACKET_SOA_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "engine_dev.h"
+
+struct Pkt {
+  int32_t where, type, last_cross, interactions, nscatterings, last_event;
+  double pos[3], dir[3];
+  double e_cmf, e_rf, nu_cmf, nu_rf;
+  int32_t next_trans, emissiontype;
+  double em_pos[3];
+  int32_t em_time, pad0;
+  double prop_time;
+  int32_t absorptiontype, trueemissiontype, trueem_time, pad1;
+  double absorptionfreq;
+  double absorptiondir[3], stokes[3], pol_dir[3];
+  int32_t escape_type, escape_time, scat_count, number;
+  int32_t pellet_nucindex;
+  float trueemissionvelocity;
+  int32_t ma_element, ma_ion, ma_level, ma_activatingline;
+};
+
+__device__ __forceinline__ uint64_t pack2(int32_t lo, int32_t hi) {
+  return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32);
+}
+__device__ __forceinline__ int32_t lo32(uint64_t w) { return (int32_t)(uint32_t)w; }
+__device__ __forceinline__ int32_t hi32(uint64_t w) { return (int32_t)(uint32_t)(w >> 32); }
+__device__ __forceinline__ double asd(uint64_t w) { return __longlong_as_double((long long)w); }
+__device__ __forceinline__ uint64_t asw(double d) { return (uint64_t)__double_as_longlong(d); }
+
+__device__ __forceinline__ void pkt_load(const uint64_t *__restrict__ soa, int64_t n, int64_t i, Pkt &p) {
+#define W(k) soa[(int64_t)(k) * n + i]
+  uint64_t w;
+  w = W(0);
+  p.where = lo32(w);
+  p.type = hi32(w);
+  w = W(1);
+  p.last_cross = lo32(w);
+  p.interactions = hi32(w);
+  w = W(2);
+  p.nscatterings = lo32(w);
+  p.last_event = hi32(w);
+  for (int d = 0; d < 3; d++) p.pos[d] = asd(W(3 + d));
+  for (int d = 0; d < 3; d++) p.dir[d] = asd(W(6 + d));
+  p.e_cmf = asd(W(9));
+  p.e_rf = asd(W(10));
+  p.nu_cmf = asd(W(11));
+  p.nu_rf = asd(W(12));
+  w = W(13);
+  p.next_trans = lo32(w);
+  p.emissiontype = hi32(w);
+  for (int d = 0; d < 3; d++) p.em_pos[d] = asd(W(14 + d));
+  w = W(17);
+  p.em_time = lo32(w);
+  p.pad0 = hi32(w);
+  p.prop_time = asd(W(18));
+  w = W(19);
+  p.absorptiontype = lo32(w);
+  p.trueemissiontype = hi32(w);
+  w = W(20);
+  p.trueem_time = lo32(w);
+  p.pad1 = hi32(w);
+  p.absorptionfreq = asd(W(21));
+  for (int d = 0; d < 3; d++) p.absorptiondir[d] = asd(W(22 + d));
+  for (int d = 0; d < 3; d++) p.stokes[d] = asd(W(25 + d));
+  for (int d = 0; d < 3; d++) p.pol_dir[d] = asd(W(28 + d));
+  w = W(32);
+  p.escape_type = lo32(w);
+  p.escape_time = hi32(w);
+  w = W(33);
+  p.scat_count = lo32(w);
+  p.number = hi32(w);
+  w = W(35);
+  p.pellet_nucindex = lo32(w);
+  p.trueemissionvelocity = __int_as_float(hi32(w));
+  w = W(36);
+  p.ma_element = lo32(w);
+  p.ma_ion = hi32(w);
+  w = W(37);
+  p.ma_level = lo32(w);
+  p.ma_activatingline = hi32(w);
+#undef W
+}
+
+// words 31 (tdecay) and 34 (pellet bookkeeping) are never written by the transport path
+__device__ __forceinline__ void pkt_store(uint64_t *__restrict__ soa, int64_t n, int64_t i, const Pkt &p) {
+#define W(k) soa[(int64_t)(k) * n + i]
+  W(0) = pack2(p.where, p.type);
+  W(1) = pack2(p.last_cross, p.interactions);
+  W(2) = pack2(p.nscatterings, p.last_event);
+  for (int d = 0; d < 3; d++) W(3 + d) = asw(p.pos[d]);
+  for (int d = 0; d < 3; d++) W(6 + d) = asw(p.dir[d]);
+  W(9) = asw(p.e_cmf);
+  W(10) = asw(p.e_rf);
+  W(11) = asw(p.nu_cmf);
+  W(12) = asw(p.nu_rf);
+  W(13) = pack2(p.next_trans, p.emissiontype);
+  for (int d = 0; d < 3; d++) W(14 + d) = asw(p.em_pos[d]);
+  W(17) = pack2(p.em_time, p.pad0);
+  W(18) = asw(p.prop_time);
+  W(19) = pack2(p.absorptiontype, p.trueemissiontype);
+  W(20) = pack2(p.trueem_time, p.pad1);
+  W(21) = asw(p.absorptionfreq);
+  for (int d = 0; d < 3; d++) W(22 + d) = asw(p.absorptiondir[d]);
+  for (int d = 0; d < 3; d++) W(25 + d) = asw(p.stokes[d]);
+  for (int d = 0; d < 3; d++) W(28 + d) = asw(p.pol_dir[d]);
+  W(32) = pack2(p.escape_type, p.escape_time);
+  W(33) = pack2(p.scat_count, p.number);
+  W(35) = pack2(p.pellet_nucindex, __float_as_int(p.trueemissionvelocity));
+  W(36) = pack2(p.ma_element, p.ma_ion);
+  W(37) = pack2(p.ma_level, p.ma_activatingline);
+#undef W
+}
+
+#endif

@@ -1,0 +1,342 @@
+// physics.h -- device restatement of the reference hot path (one packet per workitem).
+//
+// Every function cites the reference file:line it follows.  The arithmetic is written in the reference's
+// operation order and the engine is compiled with -ffp-contract=off, so that with the same per-packet random
+// stream (include/artis_rng.h) a packet's history matches the CPU oracle up to last-bit differences of the
+// device libm (exp/log/pow/trig).  Deviations D1-D6 of oracle/oracle.cc apply identically here; the per-cell
+// tables of DevCells replace the per-thread cellhistory cache (deviation-free: they are deterministic
+// functions of the cell state).
+#ifndef ARTIS_PHYSICS_H
+#define ARTIS_PHYSICS_H
+
+#include <hip/hip_runtime.h>
+
+#include "artis_constants.h"
+#include "artis_rng.h"
+#include "engine_dev.h"
+#include "packet_soa.h"
+
+#define DEVFN __device__ __forceinline__
+#define DEVNI __device__ __noinline__
+
+// error codes written to DevEst::err[0]
+enum : int32_t {
+  ERR_NONE = 0,
+  ERR_UNSUPPORTED_TYPE = 1,
+  ERR_SDIST = 2,
+  ERR_BADCELL = 3,
+  ERR_EDIST = 4,
+  ERR_NOEVENT = 5,
+  ERR_CONT = 6,
+  ERR_MA_RANDOM = 7,
+  ERR_MA_SELECT = 8,
+  ERR_KPKT = 9,
+  ERR_STUCK = 10,
+  ERR_LDIST = 11,
+  ERR_THICK_MA = 12,
+  ERR_NONFINITE = 13,
+};
+
+struct Ctx {
+  DevTab T;
+  DevGeom G;
+  DevCells C;
+  DevEst E;
+  DevRun R;
+};
+
+struct LocalCounters {
+  unsigned long long *ctr;   // LDS [35]: 34 reference counters + nesc
+  unsigned long long *work;  // LDS [16]
+};
+
+DEVFN void lctr(const LocalCounters &L, int c) { atomicAdd(&L.ctr[c], 1ull); }
+DEVFN void lwork(const LocalCounters &L, int w, unsigned long long v) { atomicAdd(&L.work[w], v); }
+
+DEVFN void fail(const Ctx &K, int code, int pktnumber, int aux) {
+  if (atomicCAS(&K.E.err[0], 0, code) == 0) {
+    K.E.err[1] = pktnumber;
+    K.E.err[2] = aux;
+  }
+}
+
+// ------------------------------------------------------------------------------------------ atomic data
+DEVFN int uion(const Ctx &K, int e, int i) { return K.T.elem_uniqueionoffset[e] + i; }
+DEVFN int ulev(const Ctx &K, int e, int i, int l) { return K.T.ion_uniqueleveloffset[uion(K, e, i)] + l; }
+DEVFN double epsilon(const Ctx &K, int e, int i, int l) { return K.T.level_epsilon[ulev(K, e, i, l)]; }
+DEVFN double stat_weight(const Ctx &K, int e, int i, int l) { return K.T.level_stat_weight[ulev(K, e, i, l)]; }
+DEVFN int get_nions(const Ctx &K, int e) { return K.T.elem_nions[e]; }
+DEVFN int get_ionstage(const Ctx &K, int e, int i) { return K.T.ion_ionstage[uion(K, e, i)]; }
+DEVFN int get_ionisinglevels(const Ctx &K, int e, int i) { return K.T.ion_ionisinglevels[uion(K, e, i)]; }
+// atomic.cc:408-422
+DEVFN int get_nphixstargets(const Ctx &K, int e, int i, int l) {
+  if (i < get_nions(K, e) - 1 && l < get_ionisinglevels(K, e, i)) return K.T.level_nphixstargets[ulev(K, e, i, l)];
+  return 0;
+}
+DEVFN int get_phixsupperlevel(const Ctx &K, int e, int i, int l, int t) {
+  return K.T.phixstarget_levelindex[K.T.level_phixstargets_offset[ulev(K, e, i, l)] + t];
+}
+DEVFN double get_phixsprobability(const Ctx &K, int e, int i, int l, int t) {
+  return K.T.phixstarget_probability[K.T.level_phixstargets_offset[ulev(K, e, i, l)] + t];
+}
+DEVFN double get_phixs_threshold(const Ctx &K, int e, int i, int l, int t) {  // atomic.cc:437-453
+  return epsilon(K, e, i + 1, get_phixsupperlevel(K, e, i, l, t)) - epsilon(K, e, i, l);
+}
+DEVFN const float *level_photoion_xs(const Ctx &K, int e, int i, int l) {
+  return K.T.phixs_xs + (int64_t)K.T.level_phixstable[ulev(K, e, i, l)] * K.T.nphixspoints;
+}
+DEVFN int get_bflutindex(const Ctx &K, int tempindex, int e, int i, int l, int t) {  // sn3d.h:64-69
+  return tempindex * K.T.nbf + (-1 - K.T.level_cont_index[ulev(K, e, i, l)] + t);
+}
+DEVFN int cell_mgi(const Ctx &K, int cellindex) { return K.G.cell_mgi[cellindex]; }
+
+// ------------------------------------------------------------------------------------------ vectors
+DEVFN double vec_len(const double x[3]) { return sqrt((x[0] * x[0]) + (x[1] * x[1]) + (x[2] * x[2])); }
+DEVFN void vec_norm(const double in[3], double out[3]) {
+  const double mag = vec_len(in);
+  out[0] = in[0] / mag;
+  out[1] = in[1] / mag;
+  out[2] = in[2] / mag;
+}
+DEVFN double dot(const double x[3], const double y[3]) { return (x[0] * y[0]) + (x[1] * y[1]) + (x[2] * y[2]); }
+DEVFN void cross_prod(const double v1[3], const double v2[3], double out[3]) {
+  out[0] = (v1[1] * v2[2]) - (v2[1] * v1[2]);
+  out[1] = (v1[2] * v2[0]) - (v2[2] * v1[0]);
+  out[2] = (v1[0] * v2[1]) - (v2[0] * v1[1]);
+}
+// vectors.h:63-79
+DEVFN void angle_ab(const double dir1[3], const double vel[3], double dir2[3]) {
+  const double vsqr = dot(vel, vel) / ARTIS_CLIGHTSQUARED;
+  const double gamma_rel = 1. / sqrt(1 - vsqr);
+  const double ndotv = dot(dir1, vel);
+  const double fact1 = gamma_rel * (1 - (ndotv / ARTIS_CLIGHT));
+  const double fact2 = (gamma_rel - (gamma_rel * gamma_rel * ndotv / (gamma_rel + 1) / ARTIS_CLIGHT)) / ARTIS_CLIGHT;
+  for (int d = 0; d < 3; d++) dir2[d] = (dir1[d] - (vel[d] * fact2)) / fact1;
+}
+// vectors.h:81-111 with the flow velocity pos/t of vectors.h:37-43
+DEVFN double doppler_pos_dir(const Ctx &K, const double pos[3], const double dir[3], double t) {
+  const double v[3] = {pos[0] / t, pos[1] / t, pos[2] / t};
+  const double ndotv = dot(dir, v);
+  double dopplerfactor = 1. - (ndotv / ARTIS_CLIGHT);
+  if (K.R.relativistic_doppler) {
+    const double betasq = dot(v, v) / ARTIS_CLIGHTSQUARED;
+    dopplerfactor = dopplerfactor / sqrt(1 - betasq);
+  }
+  return dopplerfactor;
+}
+DEVFN double doppler_packet(const Ctx &K, const Pkt &p) { return doppler_pos_dir(K, p.pos, p.dir, p.prop_time); }
+// vectors.h:113-129
+DEVFN void move_pkt(const Ctx &K, Pkt &p, double distance) {
+  p.pos[0] += (p.dir[0] * distance);
+  p.pos[1] += (p.dir[1] * distance);
+  p.pos[2] += (p.dir[2] * distance);
+  const double dopplerfactor = doppler_packet(K, p);
+  p.nu_cmf = p.nu_rf * dopplerfactor;
+  p.e_cmf = p.e_rf * dopplerfactor;
+}
+// vectors.h:131-144
+DEVFN void move_pkt_withtime(const Ctx &K, Pkt &p, double distance) {
+  const double nu_cmf_old = p.nu_cmf;
+  p.prop_time += distance / ARTIS_CLIGHT_PROP;
+  move_pkt(K, p, distance);
+  if (p.nu_cmf > nu_cmf_old) p.nu_cmf = nu_cmf_old;
+}
+// vectors.cc:43-58
+DEVFN void get_rand_isotropic_unitvec(artis_rng *rng, double out[3]) {
+  const double zrand = artis_rng_uniform(rng);
+  const double zrand2 = artis_rng_uniform(rng);
+  const double mu = -1 + (2. * zrand);
+  const double phi = zrand2 * 2 * ARTIS_PI;
+  const double sintheta = sqrt(1. - (mu * mu));
+  out[0] = sintheta * cos(phi);
+  out[1] = sintheta * sin(phi);
+  out[2] = mu;
+}
+
+// ------------------------------------------------------------------------------------------ rates
+DEVFN double dbb(double nu, double T, double W) {  // radfield.h:44-48
+  return W * ARTIS_TWOHOVERCLIGHTSQUARED * pow(nu, 3) / expm1(ARTIS_HOVERKB * nu / T);
+}
+// atomic.cc:87-155
+DEVFN double photoionization_crosssection_fromtable(const Ctx &K, const float *xs, double nu_edge, double nu) {
+  float sigma_bf;
+  if (K.T.phixs_file_version == 1) {
+    if (nu == nu_edge) {
+      sigma_bf = xs[0];
+    } else if (nu <= nu_edge * (1 + K.T.nphixsnuincrement * K.T.nphixspoints)) {
+      const int i = (int)floor(nu / (K.T.nphixsnuincrement * nu_edge)) - 10;
+      sigma_bf = xs[i];
+    } else {
+      sigma_bf = xs[K.T.nphixspoints - 1] *
+                 pow(nu_edge * (1 + K.T.nphixsnuincrement * K.T.nphixspoints) / nu, 3);
+    }
+    return sigma_bf;
+  }
+  const double ireal = (nu / nu_edge - 1.0) / K.T.nphixsnuincrement;
+  const int i = (int)floor(ireal);
+  if (i < 0) {
+    sigma_bf = 0.0;
+  } else if (i < K.T.nphixspoints - 1) {
+    const double a = xs[i];
+    const double b = xs[i + 1];
+    const double factor_b = ireal - i;
+    sigma_bf = ((1. - factor_b) * a) + (factor_b * b);
+  } else {
+    const double nu_max_phixs = nu_edge * K.T.last_phixs_nuovernuedge;
+    sigma_bf = xs[K.T.nphixspoints - 1] * pow(nu_max_phixs / nu, 3);
+  }
+  return sigma_bf;
+}
+// ratecoeff.cc:686-710 (and the identical interpolations ratecoeff.cc:1026-1041, kpkt.cc:69-82)
+DEVFN double lut_interp(const Ctx &K, const double *lut, int e, int i, int l, int t, double T) {
+  const int lowerindex = (int)floor(log(T / K.T.mintemp) / K.T.T_step_log);
+  if (lowerindex < K.T.tablesize - 1) {
+    const int upperindex = lowerindex + 1;
+    const double T_lower = K.T.mintemp * exp(lowerindex * K.T.T_step_log);
+    const double T_upper = K.T.mintemp * exp(upperindex * K.T.T_step_log);
+    const double f_upper = lut[get_bflutindex(K, upperindex, e, i, l, t)];
+    const double f_lower = lut[get_bflutindex(K, lowerindex, e, i, l, t)];
+    return (f_lower + (f_upper - f_lower) / (T_upper - T_lower) * (T - T_lower));
+  }
+  return lut[get_bflutindex(K, K.T.tablesize - 1, e, i, l, t)];
+}
+// ltepop.cc:539-556
+DEVFN double calculate_sahafact(const Ctx &K, int e, int i, int l, int upperionlevel, double T, double E_threshold) {
+  const double g_lower = stat_weight(K, e, i, l);
+  const double g_upper = stat_weight(K, e, i + 1, upperionlevel);
+  return ARTIS_SAHACONST * g_lower / g_upper * pow(T, -1.5) * exp(E_threshold / ARTIS_KB / T);
+}
+// macroatom.h:52-105
+DEVFN double col_deexcitation_ratecoeff(const Ctx &K, float T_e, float nne, double epsilon_trans, int li,
+                                        double lowerstatweight, double upperstatweight) {
+  double C = 0.;
+  const double coll_str_thisline = K.T.line_coll[li];
+  if (coll_str_thisline < 0) {
+    if (!K.T.line_forbidden[li]) {
+      const double eoverkt = epsilon_trans / (ARTIS_KB * T_e);
+      const double g_bar = 0.2;
+      const double gauntfac = (eoverkt > 0.33421) ? g_bar : 0.276 * exp(eoverkt) * (-0.5772156649 - log(eoverkt));
+      const double g_ratio = lowerstatweight / upperstatweight;
+      C = ARTIS_C_0 * 14.51039491 * nne * sqrtf(T_e) * K.T.line_f[li] *
+          pow(ARTIS_H_IONPOT / epsilon_trans, 2) * eoverkt * g_ratio * gauntfac;
+    } else {
+      C = nne * 8.629e-6 * 0.01 * lowerstatweight / sqrtf(T_e);
+    }
+  } else {
+    C = nne * 8.629e-6 * coll_str_thisline / upperstatweight / sqrtf(T_e);
+  }
+  return C;
+}
+// macroatom.h:107-150
+DEVFN double col_excitation_ratecoeff(const Ctx &K, float T_e, float nne, int li, double epsilon_trans,
+                                      double lowerstatweight, double upperstatweight) {
+  double C = 0.;
+  const double coll_strength = K.T.line_coll[li];
+  const double eoverkt = epsilon_trans / (ARTIS_KB * T_e);
+  if (coll_strength < 0) {
+    if (!K.T.line_forbidden[li]) {
+      const double g_bar = 0.2;
+      const double exp_eoverkt = exp(eoverkt);
+      const double test = 0.276 * exp_eoverkt * (-0.5772156649 - log(eoverkt));
+      const double Gamma = g_bar > test ? g_bar : test;
+      C = ARTIS_C_0 * nne * sqrtf(T_e) * 14.51039491 * K.T.line_f[li] * pow(ARTIS_H_IONPOT / epsilon_trans, 2) *
+          eoverkt / exp_eoverkt * Gamma;
+    } else {
+      C = nne * 8.629e-6 * 0.01 * exp(-eoverkt) * upperstatweight / sqrtf(T_e);
+    }
+  } else {
+    C = nne * 8.629e-6 * coll_strength * exp(-eoverkt) / lowerstatweight / sqrtf(T_e);
+  }
+  return C;
+}
+// macroatom.cc:503-548 (populations from the per-cell table)
+DEVFN double rad_deexcitation_ratecoeff(const Ctx &K, const double *pops, int e, int i, int upper, int lower,
+                                        double epsilon_trans, int li, double t_current) {
+  const double n_u = pops[ulev(K, e, i, upper)];
+  const double n_l = pops[ulev(K, e, i, lower)];
+  double R = 0.0;
+  const double nu_trans = epsilon_trans / ARTIS_H;
+  const double A_ul = K.T.line_A[li];
+  const double B_ul = ARTIS_CLIGHTSQUAREDOVERTWOH / pow(nu_trans, 3) * A_ul;
+  const double B_lu = stat_weight(K, e, i, upper) / stat_weight(K, e, i, lower) * B_ul;
+  const double tau_sobolev = (B_lu * n_l - B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_current;
+  if (tau_sobolev > 1e-100) {
+    const double beta = 1.0 / tau_sobolev * (-expm1(-tau_sobolev));
+    R = A_ul * beta;
+  }
+  return R;
+}
+// macroatom.cc:550-643 (radfield.cc:898-943: dilute blackbody)
+DEVFN double rad_excitation_ratecoeff(const Ctx &K, const double *pops, int mgi, int e, int i, int lower, int upper,
+                                      double epsilon_trans, int li, double t_current) {
+  const double n_u = pops[ulev(K, e, i, upper)];
+  const double n_l = pops[ulev(K, e, i, lower)];
+  double R = 0.0;
+  const double nu_trans = epsilon_trans / ARTIS_H;
+  const double A_ul = K.T.line_A[li];
+  const double B_ul = ARTIS_CLIGHTSQUAREDOVERTWOH / pow(nu_trans, 3) * A_ul;
+  const double B_lu = stat_weight(K, e, i, upper) / stat_weight(K, e, i, lower) * B_ul;
+  const double tau_sobolev = (B_lu * n_l - B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_current;
+  if (tau_sobolev > 1e-100) {
+    const double beta = 1.0 / tau_sobolev * (-expm1(-tau_sobolev));
+    const double R_over_J_nu = n_l > 0. ? (B_lu - B_ul * n_u / n_l) * beta : B_lu * beta;
+    const float T_R = K.C.TR[mgi];
+    const float W = K.C.W[mgi];
+    R = R_over_J_nu * dbb(nu_trans, T_R, W);
+  }
+  return R;
+}
+// macroatom.cc:645-678
+DEVFN double rad_recombination_ratecoeff(const Ctx &K, float T_e, float nne, int e, int upperion, int upper, int lower) {
+  double R = 0.0;
+  const int nt = get_nphixstargets(K, e, upperion - 1, lower);
+  for (int t = 0; t < nt; t++) {
+    if (get_phixsupperlevel(K, e, upperion - 1, lower, t) == upper) {
+      R = nne * lut_interp(K, K.T.spontrecombcoeff, e, upperion - 1, lower, t, T_e);
+      break;
+    }
+  }
+  return R;
+}
+// macroatom.cc:704-743
+DEVFN double col_recombination_ratecoeff(const Ctx &K, int mgi, int e, int upperion, int upper, int lower,
+                                         double epsilon_trans) {
+  const int nt = get_nphixstargets(K, e, upperion - 1, lower);
+  for (int t = 0; t < nt; t++) {
+    if (get_phixsupperlevel(K, e, upperion - 1, lower, t) == upper) {
+      const float nne = K.C.nne[mgi];
+      const float T_e = K.C.Te[mgi];
+      const double fac1 = epsilon_trans / ARTIS_KB / T_e;
+      const int ionstage = get_ionstage(K, e, upperion);
+      double g;
+      if (ionstage - 1 == 1)
+        g = 0.1;
+      else if (ionstage - 1 == 2)
+        g = 0.2;
+      else
+        g = 0.3;
+      const double sigma_bf =
+          (level_photoion_xs(K, e, upperion - 1, lower)[0] * get_phixsprobability(K, e, upperion - 1, lower, t));
+      const double sf = calculate_sahafact(K, e, upperion - 1, lower, upper, T_e, epsilon_trans);
+      return nne * nne * sf * 1.55e13 * pow((double)T_e, -0.5) * g * sigma_bf * exp(-fac1) / fac1;
+    }
+  }
+  return 0.;
+}
+// macroatom.cc:745-776
+DEVFN double col_ionization_ratecoeff(const Ctx &K, float T_e, float nne, int e, int i, int lower, int t,
+                                      double epsilon_trans) {
+  double g;
+  const int ionstage = get_ionstage(K, e, i);
+  if (ionstage == 1)
+    g = 0.1;
+  else if (ionstage == 2)
+    g = 0.2;
+  else
+    g = 0.3;
+  const double fac1 = epsilon_trans / ARTIS_KB / T_e;
+  const double sigma_bf = level_photoion_xs(K, e, i, lower)[0] * get_phixsprobability(K, e, i, lower, t);
+  return nne * 1.55e13 * pow((double)T_e, -0.5) * g * sigma_bf * exp(-fac1) / fac1;
+}
+
+#endif

@@ -1,0 +1,1273 @@
+// transport.h -- device r-packet / macro-atom / k-packet propagation (one packet per workitem).
+// Restates rpkt.cc, boundary.cc, polarization.cc, vpkt.cc:898-1069, macroatom.cc, kpkt.cc and
+// update_packets.cc:137-202 for GRID_UNIFORM, LTE (classic) options; see physics.h for numerics.
+#ifndef ARTIS_TRANSPORT_H
+#define ARTIS_TRANSPORT_H
+
+#include "physics.h"
+
+// kappa_rpkt_cont of the current step (globals.h:160-170), held in registers
+struct Kappa {
+  double nu;  // nu_cmf at which it was computed
+  double total, es, ff, bf, ffheating;
+};
+
+struct Tx {
+  const Ctx &K;
+  const LocalCounters &L;
+  artis_rng rng;
+  int nts;
+  bool ok;
+  DEVFN Tx(const Ctx &k, const LocalCounters &l) : K(k), L(l), ok(true) {}
+  DEVFN void err(int code, int number, int aux) {
+    fail(K, code, number, aux);
+    ok = false;
+  }
+};
+
+DEVFN void safeadd(double *p, double v) { unsafeAtomicAdd(p, v); }
+
+// ------------------------------------------------------------------------------------------ emission
+// rpkt.cc:975-1025
+DEVFN void emitt_rpkt(Tx &x, Pkt &p) {
+  p.type = ARTIS_TYPE_RPKT;
+  p.last_cross = ARTIS_NONE;
+  double dir_cmf[3];
+  get_rand_isotropic_unitvec(&x.rng, dir_cmf);
+  const double t = -1. * p.prop_time;
+  const double vel_vec[3] = {p.pos[0] / t, p.pos[1] / t, p.pos[2] / t};
+  angle_ab(dir_cmf, vel_vec, p.dir);
+  const double dopplerfactor = doppler_packet(x.K, p);
+  p.nu_rf = p.nu_cmf / dopplerfactor;
+  p.e_rf = p.e_cmf / dopplerfactor;
+  p.stokes[0] = 1.;
+  p.stokes[1] = 0.;
+  p.stokes[2] = 0.;
+  double dummy_dir[3] = {0., 0., 1.};
+  cross_prod(p.dir, dummy_dir, p.pol_dir);
+  if ((dot(p.pol_dir, p.pol_dir)) < 1.e-8) {
+    dummy_dir[0] = dummy_dir[2] = 0.0;
+    dummy_dir[1] = 1.0;
+    cross_prod(p.dir, dummy_dir, p.pol_dir);
+  }
+  vec_norm(p.pol_dir, p.pol_dir);
+}
+
+// vpkt.cc:898-929
+DEVFN double rot_angle(const double n1[3], const double n2[3], const double ref1[3], const double ref2[3]) {
+  double i = 0;
+  double ref1_sc[3];
+  ref1_sc[0] = n1[0] * dot(n1, n2) - n2[0];
+  ref1_sc[1] = n1[1] * dot(n1, n2) - n2[1];
+  ref1_sc[2] = n1[2] * dot(n1, n2) - n2[2];
+  vec_norm(ref1_sc, ref1_sc);
+  double c1 = dot(ref1_sc, ref1);
+  const double c2 = dot(ref1_sc, ref2);
+  if (c1 < -1) c1 = -1;
+  if (c1 > 1) c1 = 1;
+  if ((c1 > 0) && (c2 > 0)) i = acos(c1);
+  if ((c1 > 0) && (c2 < 0)) i = 2 * acos(-1.) - acos(c1);
+  if ((c1 < 0) && (c2 < 0)) i = acos(-1.) + acos(fabs(c1));
+  if ((c1 < 0) && (c2 > 0)) i = acos(-1.) - acos(fabs(c1));
+  if (c1 == 0) i = acos(-1.) / 2.;
+  if (c2 == 0) i = 0.0;
+  return i;
+}
+// vpkt.cc:932-944
+DEVFN void meridian(const double n[3], double ref1[3], double ref2[3]) {
+  ref1[0] = -1. * n[0] * n[2] / sqrt(n[0] * n[0] + n[1] * n[1]);
+  ref1[1] = -1. * n[1] * n[2] / sqrt(n[0] * n[0] + n[1] * n[1]);
+  ref1[2] = (1 - (n[2] * n[2])) / sqrt(n[0] * n[0] + n[1] * n[1]);
+  ref2[0] = n[2] * ref1[1] - n[1] * ref1[2];
+  ref2[1] = n[0] * ref1[2] - n[2] * ref1[0];
+  ref2[2] = n[1] * ref1[0] - n[0] * ref1[1];
+}
+// vpkt.cc:1022-1069 (only the E-field result is used)
+DEVFN void lorentz(const double e_rf[3], const double n_rf[3], const double v[3], double e_cmf[3]) {
+  double beta[3], e_par[3], e_perp[3], b_rf[3], v_cr_b[3];
+  beta[0] = v[0] / ARTIS_CLIGHT;
+  beta[1] = v[1] / ARTIS_CLIGHT;
+  beta[2] = v[2] / ARTIS_CLIGHT;
+  const double vsqr = dot(beta, beta);
+  const double gamma_rel = 1. / (sqrt(1 - vsqr));
+  const double edb = (e_rf[0] * beta[0] + e_rf[1] * beta[1] + e_rf[2] * beta[2]);
+  e_par[0] = edb * beta[0] / (vsqr);
+  e_par[1] = edb * beta[1] / (vsqr);
+  e_par[2] = edb * beta[2] / (vsqr);
+  e_perp[0] = e_rf[0] - e_par[0];
+  e_perp[1] = e_rf[1] - e_par[1];
+  e_perp[2] = e_rf[2] - e_par[2];
+  b_rf[0] = n_rf[1] * e_rf[2] - n_rf[2] * e_rf[1];
+  b_rf[1] = n_rf[2] * e_rf[0] - n_rf[0] * e_rf[2];
+  b_rf[2] = n_rf[0] * e_rf[1] - n_rf[1] * e_rf[0];
+  v_cr_b[0] = beta[1] * b_rf[2] - beta[2] * b_rf[1];
+  v_cr_b[1] = beta[2] * b_rf[0] - beta[0] * b_rf[2];
+  v_cr_b[2] = beta[0] * b_rf[1] - beta[1] * b_rf[0];
+  e_cmf[0] = e_par[0] + gamma_rel * (e_perp[0] + v_cr_b[0]);
+  e_cmf[1] = e_par[1] + gamma_rel * (e_perp[1] + v_cr_b[1]);
+  e_cmf[2] = e_par[2] + gamma_rel * (e_perp[2] + v_cr_b[2]);
+  vec_norm(e_cmf, e_cmf);
+}
+// vpkt.cc:947-1019
+DEVFN void frame_transform(const double n_rf[3], double *Q, double *U, const double v[3], double n_cmf[3]) {
+  double ref1[3], ref2[3], e_rf[3], e_cmf[3];
+  double theta_rot = 0.;
+  meridian(n_rf, ref1, ref2);
+  const double Q0 = *Q;
+  const double U0 = *U;
+  const double p = sqrt(Q0 * Q0 + U0 * U0);
+  double ra = 0;
+  if (p > 0) {
+    const double c2 = Q0 / p;
+    const double s2 = U0 / p;
+    if ((c2 > 0) && (s2 > 0)) ra = acos(Q0 / p) / 2.;
+    if ((c2 < 0) && (s2 > 0)) ra = (acos(-1.) - acos(fabs(Q0 / p))) / 2.;
+    if ((c2 < 0) && (s2 < 0)) ra = (acos(-1.) + acos(fabs(Q0 / p))) / 2.;
+    if ((c2 > 0) && (s2 < 0)) ra = (2. * acos(-1.) - acos(fabs(Q0 / p))) / 2.;
+    if (c2 == 0) {
+      ra = 0.25 * acos(-1.);
+      if (U0 < 0) ra = 0.75 * acos(-1.);
+    }
+    if (s2 == 0) {
+      ra = 0.0;
+      if (Q0 < 0) ra = 0.5 * acos(-1.);
+    }
+  }
+  e_rf[0] = cos(ra) * ref1[0] - sin(ra) * ref2[0];
+  e_rf[1] = cos(ra) * ref1[1] - sin(ra) * ref2[1];
+  e_rf[2] = cos(ra) * ref1[2] - sin(ra) * ref2[2];
+  angle_ab(n_rf, v, n_cmf);
+  lorentz(e_rf, n_rf, v, e_cmf);
+  meridian(n_cmf, ref1, ref2);
+  const double r1 = e_cmf[0] * ref1[0] + e_cmf[1] * ref1[1] + e_cmf[2] * ref1[2];
+  const double r2 = e_cmf[0] * ref2[0] + e_cmf[1] * ref2[1] + e_cmf[2] * ref2[2];
+  if ((r1 > 0) && (r2 < 0)) theta_rot = acos(r1);
+  if ((r1 < 0) && (r2 < 0)) theta_rot = acos(-1.) - acos(fabs(r1));
+  if ((r1 < 0) && (r2 > 0)) theta_rot = acos(-1.) + acos(fabs(r1));
+  if ((r1 > 0) && (r2 > 0)) theta_rot = 2 * acos(-1.) - acos(r1);
+  if (r1 == 0) theta_rot = acos(-1.) / 2.;
+  if (r2 == 0) theta_rot = 0.0;
+  if (r1 > 1) theta_rot = 0.0;
+  if (r1 < -1) theta_rot = acos(-1.);
+  *Q = cos(2 * theta_rot) * p;
+  *U = sin(2 * theta_rot) * p;
+}
+// polarization.cc:6-157
+DEVNI void escat_rpkt(Tx &x, Pkt &p) {
+  p.type = ARTIS_TYPE_RPKT;
+  p.last_cross = ARTIS_NONE;
+  const double t = p.prop_time;
+  const double vel_vec[3] = {p.pos[0] / t, p.pos[1] / t, p.pos[2] / t};
+  double Qi = p.stokes[1];
+  double Ui = p.stokes[2];
+  double old_dir_cmf[3];
+  frame_transform(p.dir, &Qi, &Ui, vel_vec, old_dir_cmf);
+  double M = 0., mu = 0., phisc = 0.;
+  if (x.K.R.pol_dipole) {
+    double pr = 0., xx = 0.;
+    int tries = 0;
+    do {
+      const double zrand = artis_rng_uniform(&x.rng);
+      const double zrand2 = artis_rng_uniform(&x.rng);
+      const double zrand3 = artis_rng_uniform(&x.rng);
+      M = 2 * zrand - 1;
+      mu = pow(M, 2.);
+      phisc = 2 * ARTIS_PI * zrand2;
+      pr = (mu + 1) + (mu - 1) * (cos(2 * phisc) * Qi + sin(2 * phisc) * Ui);
+      xx = 2 * zrand3;
+      if (++tries > 1000000) {
+        x.err(ERR_STUCK, p.number, 1);
+        return;
+      }
+    } while (xx > pr);
+  } else {
+    const double zrand = artis_rng_uniform(&x.rng);
+    const double zrand2 = artis_rng_uniform(&x.rng);
+    M = 2. * zrand - 1;
+    mu = pow(M, 2.);
+    phisc = 2 * ARTIS_PI * zrand2;
+  }
+  const double tsc = acos(M);
+  double nd[3];
+  const double *od = old_dir_cmf;
+  if (fabs(od[2]) < 0.99999) {
+    nd[0] = sin(tsc) / sqrt(1. - pow(od[2], 2.)) * (od[1] * sin(phisc) - od[0] * od[2] * cos(phisc)) + od[0] * cos(tsc);
+    nd[1] = sin(tsc) / sqrt(1 - pow(od[2], 2.)) * (-od[0] * sin(phisc) - od[1] * od[2] * cos(phisc)) + od[1] * cos(tsc);
+    nd[2] = sin(tsc) * cos(phisc) * sqrt(1 - pow(od[2], 2.)) + od[2] * cos(tsc);
+  } else {
+    nd[0] = sin(tsc) * cos(phisc);
+    nd[1] = sin(tsc) * sin(phisc);
+    nd[2] = (od[2] > 0) ? cos(tsc) : -cos(tsc);
+  }
+  double ref1[3], ref2[3];
+  meridian(od, ref1, ref2);
+  const double i1 = rot_angle(od, nd, ref1, ref2);
+  const double cos2i1 = cos(2 * i1);
+  const double sin2i1 = sin(2 * i1);
+  const double Qold = Qi * cos2i1 - Ui * sin2i1;
+  const double Uold = Qi * sin2i1 + Ui * cos2i1;
+  mu = dot(od, nd);
+  const double Inew = 0.75 * ((mu * mu + 1.0) + Qold * (mu * mu - 1.0));
+  double Qnew = 0.75 * ((mu * mu - 1.0) + Qold * (mu * mu + 1.0));
+  double Unew = 1.5 * mu * Uold;
+  Qnew = Qnew / Inew;
+  Unew = Unew / Inew;
+  meridian(nd, ref1, ref2);
+  const double i2 = ARTIS_PI + rot_angle(nd, od, ref1, ref2);
+  const double cos2i2 = cos(2 * i2);
+  const double sin2i2 = sin(2 * i2);
+  double Q = Qnew * cos2i2 + Unew * sin2i2;
+  double U = -Qnew * sin2i2 + Unew * cos2i2;
+  const double vel_rev[3] = {-vel_vec[0], -vel_vec[1], -vel_vec[2]};
+  double dummy_dir[3];
+  frame_transform(nd, &Q, &U, vel_rev, dummy_dir);
+  p.stokes[0] = 1.0;
+  p.stokes[1] = Q;
+  p.stokes[2] = U;
+  p.dir[0] = dummy_dir[0];
+  p.dir[1] = dummy_dir[1];
+  p.dir[2] = dummy_dir[2];
+  const double dopplerfactor = doppler_packet(x.K, p);
+  p.nu_rf = p.nu_cmf / dopplerfactor;
+  p.e_rf = p.e_cmf / dopplerfactor;
+}
+
+// ------------------------------------------------------------------------------------------ boundary
+// boundary.cc:101-330 (GRID_UNIFORM)
+DEVFN double boundary_cross(Tx &x, Pkt &p, int *snext) {
+  const Ctx &K = x.K;
+  const double tstart = p.prop_time;
+  const int cellindex = p.where;
+  const double tmin = K.G.tmin;
+  const int n0 = K.G.ncoordgrid[0], n1 = K.G.ncoordgrid[1], n2 = K.G.ncoordgrid[2];
+  const int n[3] = {n0, n1, n2};
+  const int stride[3] = {1, n0, n0 * n1};
+  double initpos[3], cmax[3], cmin[3], vel[3];
+  for (int d = 0; d < 3; d++) {
+    initpos[d] = p.pos[d];
+    cmin[d] = K.G.cell_pos_min[(int64_t)cellindex * 3 + d];
+    cmax[d] = cmin[d] + K.G.wid;
+    vel[d] = p.dir[d] * ARTIS_CLIGHT_PROP;
+  }
+  const int pointnum[3] = {cellindex % n0, (cellindex / n0) % n1, (cellindex / (n0 * n1)) % n2};
+  int last_cross = p.last_cross;
+  const int negd[3] = {ARTIS_NEG_X, ARTIS_NEG_Y, ARTIS_NEG_Z};
+  const int posd[3] = {ARTIS_POS_X, ARTIS_POS_Y, ARTIS_POS_Z};
+  for (int d = 0; d < 3; d++) {
+    for (int flip = 0; flip < 2; flip++) {
+      const int direction = flip ? posd[d] : negd[d];
+      const int invdirection = !flip ? posd[d] : negd[d];
+      const int cellindexstride = flip ? -stride[d] : stride[d];
+      bool outside;
+      if (flip)
+        outside = initpos[d] < (cmin[d] / tmin * tstart - 10.);
+      else
+        outside = initpos[d] > (cmax[d] / tmin * tstart + 10.);
+      if (outside && (last_cross != direction)) {
+        if ((vel[d] - (initpos[d] / tstart)) > 0) {
+          if ((pointnum[d] == (n[d] - 1) && cellindexstride > 0) || (pointnum[d] == 0 && cellindexstride < 0)) {
+            *snext = -99;
+            return 0;
+          }
+          *snext = p.where + cellindexstride;
+          p.last_cross = invdirection;
+          return 0;
+        }
+        last_cross = direction;
+      }
+    }
+  }
+  double tmaxb[3], tminb[3];
+  for (int d = 0; d < 3; d++) {
+    tmaxb[d] = ((initpos[d] - (vel[d] * tstart)) / ((cmax[d]) - (vel[d] * tmin)) * tmin) - tstart;
+    tminb[d] = ((initpos[d] - (vel[d] * tstart)) / ((cmin[d]) - (vel[d] * tmin)) * tmin) - tstart;
+  }
+  double time = 1.e99;
+  for (int d = 0; d < 3; d++) {
+    if ((tmaxb[d] > 0) && (tmaxb[d] < time) && (last_cross != negd[d])) {
+      time = tmaxb[d];
+      if (pointnum[d] == (n[d] - 1)) {
+        *snext = -99;
+      } else {
+        *snext = p.where + stride[d];
+        p.last_cross = posd[d];
+      }
+    }
+    if ((tminb[d] > 0) && (tminb[d] < time) && (last_cross != posd[d])) {
+      time = tminb[d];
+      if (pointnum[d] == 0) {
+        *snext = -99;
+      } else {
+        *snext = p.where - stride[d];
+        p.last_cross = negd[d];
+      }
+    }
+  }
+  return ARTIS_CLIGHT_PROP * time;
+}
+// boundary.cc:332-357
+DEVFN void change_cell(Tx &x, Pkt &p, int snext) {
+  if (snext == -99) {
+    p.escape_type = p.type;
+    p.escape_time = (int)p.prop_time;
+    p.type = ARTIS_TYPE_ESCAPE;
+    lctr(x.L, 34);  // nesc
+  } else {
+    p.where = snext;
+    lctr(x.L, CTR_CELLCROSSINGS);
+  }
+}
+
+// ------------------------------------------------------------------------------------------ opacity
+// rpkt.cc:1075-1207: one continuum's contribution sigma*prob*corr (returns false if not included / inactive)
+DEVFN bool bf_contribution(const Ctx &K, int k, int mgi, int i, double nu, double *nnlevel_out, double *gcontr_out) {
+  const int element = K.T.allcont_element[i];
+  const int ion = K.T.allcont_ion[i];
+  const int level = K.T.allcont_level[i];
+  const int ui = uion(K, element, ion);
+  if (!((K.C.ionpop[(int64_t)k * K.T.nions_total + ui] / (double)K.C.nnetot[mgi] > 1.e-6) || (level == 0))) return false;
+  const double nu_edge = K.T.allcont_nu_edge[i];
+  const double nnlevel = K.C.pops[(int64_t)k * K.T.nlevels_total + K.T.ion_uniqueleveloffset[ui] + level];
+  const double nu_max_phixs = nu_edge * K.T.last_phixs_nuovernuedge;
+  if (!(nu <= nu_max_phixs && nnlevel > 0)) return false;
+  const double sigma_bf = photoionization_crosssection_fromtable(
+      K, K.T.phixs_xs + (int64_t)K.T.allcont_phixstable[i] * K.T.nphixspoints, nu_edge, nu);
+  const double probability = K.T.allcont_probability[i];
+  const double departure_ratio = K.C.depratio[(int64_t)k * K.T.nbf + i];
+  const double T_e = K.C.Te[mgi];
+  const double stimfactor = departure_ratio * exp(-ARTIS_HOVERKB * nu / T_e);
+  double corrfactor = 1 - stimfactor;
+  if (corrfactor < 0) corrfactor = 0.;
+  *nnlevel_out = nnlevel;
+  *gcontr_out = sigma_bf * probability * corrfactor;
+  return true;
+}
+// rpkt.cc:1075-1207 calculate_kappa_bf_gammacontr: the kappa_bf total (the cumulative array is re-scanned on demand)
+DEVFN double kappa_bf_total(Tx &x, int k, int mgi, double nu) {
+  const Ctx &K = x.K;
+  double kappa_bf_sum = 0.;
+  unsigned long long nactive = 0;
+  for (int i = 0; i < K.T.nbf; i++) {
+    if (nu < K.T.allcont_nu_edge[i]) {
+      // the reference breaks at the first included continuum with nu < nu_edge; sorted edges => nothing
+      // beyond contributes either
+      break;
+    }
+    nactive++;
+    double nnlevel, gc;
+    if (bf_contribution(K, k, mgi, i, nu, &nnlevel, &gc)) kappa_bf_sum += nnlevel * gc;
+  }
+  lwork(x.L, WK_BF_ACTIVE, nactive);
+  return kappa_bf_sum;
+}
+// rpkt.cc:1209-1295 (deviation D2: always recomputed)
+DEVFN void calculate_kappa_rpkt_cont(Tx &x, const Pkt &p, int k, int mgi, Kappa &kap) {
+  const Ctx &K = x.K;
+  const double nu_cmf = p.nu_cmf;
+  const float nne = K.C.nne[mgi];
+  double sigma = 0.0, kappa_ff = 0., kappa_bf = 0., kappa_ffheating = 0.;
+  lwork(x.L, WK_KAPPA_EVALS, 1);
+  if (K.R.do_r_lc) {
+    const float T_e = K.C.Te[mgi];
+    const double ffsum = K.C.ffsum[k];
+    const double ff = ffsum * (3.69255e8 / sqrt((double)T_e) * pow(nu_cmf, -3) * nne *
+                               (1 - exp(-ARTIS_HOVERKB * nu_cmf / T_e)));  // rpkt.cc:1061
+    if (K.R.opacity_case == 4) {
+      sigma = ARTIS_SIGMA_T * nne;
+      kappa_ff = ff;
+      kappa_ffheating = kappa_ff;
+      kappa_bf = kappa_bf_total(x, k, mgi, nu_cmf);
+    } else {
+      kappa_ff = 1e5 * ff;
+    }
+  }
+  kap.nu = nu_cmf;
+  kap.total = sigma + kappa_bf + kappa_ff;
+  kap.es = sigma;
+  kap.ff = kappa_ff;
+  kap.bf = kappa_bf;
+  kap.ffheating = kappa_ffheating;
+  if (!isfinite(kap.total)) {
+    if (isfinite(kap.es)) {
+      kap.ff = 0.;
+      kap.bf = 0.;
+      kap.total = kap.es;
+    } else {
+      x.err(ERR_NONFINITE, p.number, 1);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------ lines
+// rpkt.cc:26-65
+DEVFN int closest_transition(const Ctx &K, double nu_cmf, int next_trans) {
+  const int nlines = K.T.nlines;
+  const double *lnu = K.T.line_nu;
+  const int left = next_trans;
+  const int right = nlines - 1;
+  if (nu_cmf < lnu[right]) return -1;
+  if (left > right) return -1;
+  if (left > 0) return left;
+  if (nu_cmf >= lnu[0]) return 0;
+  int lo = next_trans, hi = nlines;
+  while (lo < hi) {
+    const int mid = lo + (hi - lo) / 2;
+    if (!(lnu[mid] <= nu_cmf))
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+// rpkt.cc:511-555
+DEVFN void closest_transition_empty(const Ctx &K, Pkt &p) {
+  const int nlines = K.T.nlines;
+  const double *lnu = K.T.line_nu;
+  const int left = p.next_trans;
+  const int right = nlines - 1;
+  if (p.nu_cmf < lnu[right]) p.next_trans = nlines + 1;
+  if (left > right) p.next_trans = nlines + 1;
+  int matchindex;
+  if (p.nu_cmf >= lnu[left]) {
+    matchindex = left;
+  } else {
+    int lo = p.next_trans, hi = nlines;
+    while (lo < hi) {
+      const int mid = lo + (hi - lo) / 2;
+      if (!(lnu[mid] <= p.nu_cmf))
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    matchindex = lo;
+  }
+  p.next_trans = matchindex;
+}
+
+// move_pkt_withtime restricted to the fields a dummy packet needs (vectors.h:113-144)
+DEVFN void move_dummy(const Ctx &K, double pos[3], const double dir[3], double &t, double &nu_cmf, double nu_rf,
+                      double distance) {
+  const double nu_cmf_old = nu_cmf;
+  t += distance / ARTIS_CLIGHT_PROP;
+  pos[0] += (dir[0] * distance);
+  pos[1] += (dir[1] * distance);
+  pos[2] += (dir[2] * distance);
+  nu_cmf = nu_rf * doppler_pos_dir(K, pos, dir, t);
+  if (nu_cmf > nu_cmf_old) nu_cmf = nu_cmf_old;
+}
+
+// rpkt.cc:67-328
+DEVNI double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_eventtype, double tau_rnd,
+                       double abort_dist) {
+  const Ctx &K = x.K;
+  double tau = 0.;
+  double dist = 0.;
+  double nu_cmf_abort;
+  {
+    double apos[3] = {p.pos[0], p.pos[1], p.pos[2]};
+    double at = p.prop_time, anu = p.nu_cmf;
+    move_dummy(K, apos, p.dir, at, anu, p.nu_rf, abort_dist / 2.);
+    move_dummy(K, apos, p.dir, at, anu, p.nu_rf, abort_dist / 2.);
+    nu_cmf_abort = anu;
+  }
+  double dpos[3] = {p.pos[0], p.pos[1], p.pos[2]};
+  double dt = p.prop_time, dnu = p.nu_cmf;
+  int dnext = p.next_trans;
+  calculate_kappa_rpkt_cont(x, p, k, mgi, kap);
+  const double kap_cont = kap.total * doppler_packet(K, p);
+  const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
+  unsigned long long nscanned = 0, ntaus = 0;
+  double result;
+  while (true) {
+    const int lineindex = closest_transition(K, dnu, dnext);
+    if (lineindex >= 0) {
+      nscanned++;
+      const double nu_trans = K.T.line_nu[lineindex];
+      dnext = lineindex + 1;
+      double ldist;
+      if (dnu <= nu_trans) {
+        ldist = 0;
+      } else if (!K.R.relativistic_doppler) {
+        ldist = ARTIS_CLIGHT * dt * (dnu / nu_trans - 1);
+      } else {
+        const double nu_r = nu_trans / p.nu_rf;
+        const double ct = ARTIS_CLIGHT * dt;
+        const double r = vec_len(dpos);
+        const double mu = dot(p.dir, dpos) / r;
+        ldist = -mu * r + (ct - nu_r * nu_r * sqrt(ct * ct - (1 + r * r * (1 - mu * mu) * (1 + pow(nu_r, -2))))) /
+                              (1 + nu_r * nu_r);
+      }
+      if (ldist < 0.) {
+        if (!(ldist >= -100.)) {
+          x.err(ERR_LDIST, p.number, lineindex);
+          result = 0.;
+          break;
+        }
+        ldist = 0.;
+      }
+      const double tau_cont = kap_cont * ldist;
+      if (tau_rnd - tau > tau_cont) {
+        if (nu_trans < nu_cmf_abort) {
+          dnext -= 1;
+          p.next_trans = dnext;
+          result = DBL_MAX;
+          break;
+        }
+        const LineTau lt = K.T.line_tau[lineindex];
+        const double n_u = pops[lt.ul_upper];
+        const double n_l = pops[lt.ul_lower];
+        double tau_line = (lt.B_lu * n_l - lt.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * dt;
+        ntaus++;
+        if (tau_line < 0) tau_line = 0.;
+        if (tau_rnd - tau > tau_cont + tau_line) {
+          dist = dist + ldist;
+          tau += tau_cont + tau_line;
+          move_dummy(K, dpos, p.dir, dt, dnu, p.nu_rf, ldist);
+        } else {
+          p.ma_element = K.T.line_elem[lineindex];
+          p.ma_ion = K.T.line_ion[lineindex];
+          p.ma_level = K.T.line_upper[lineindex];
+          p.ma_activatingline = lineindex;
+          double edist = dist + ldist;
+          if (edist >= abort_dist) edist = abort_dist * (1 - 2e-8);
+          *rpkt_eventtype = ARTIS_RPKT_EVENTTYPE_BB;
+          p.next_trans = dnext;
+          result = edist;
+          break;
+        }
+      } else {
+        const double edist = dist + (tau_rnd - tau) / kap_cont;
+        dnext -= 1;
+        *rpkt_eventtype = ARTIS_RPKT_EVENTTYPE_CONT;
+        p.next_trans = dnext;
+        result = edist;
+        break;
+      }
+    } else {
+      dnext = K.T.nlines + 1;
+      const double tau_cont = kap_cont * (abort_dist - dist);
+      double edist;
+      if (tau_rnd - tau > tau_cont) {
+        edist = DBL_MAX;
+      } else {
+        edist = dist + (tau_rnd - tau) / kap_cont;
+        *rpkt_eventtype = ARTIS_RPKT_EVENTTYPE_CONT;
+      }
+      p.next_trans = dnext;
+      result = edist;
+      break;
+    }
+  }
+  lwork(x.L, WK_LINES_SCANNED, nscanned);
+  lwork(x.L, WK_LINE_TAUS, ntaus);
+  return result;
+}
+
+// rpkt.cc:557-621 + radfield.cc:831-876
+DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double distance) {
+  const Ctx &K = x.K;
+  const int mgi = cell_mgi(K, p.where);
+  if (mgi == K.G.npts_model) return;
+  const int k = K.C.ne_index[mgi];
+  lwork(x.L, WK_EST_SEGMENTS, 1);
+  const double distance_e_cmf = distance * p.e_cmf;
+  const double nu = p.nu_cmf;
+  safeadd(&K.E.J[mgi], distance_e_cmf);
+  safeadd(&K.E.nuJ[mgi], distance_e_cmf * nu);
+  safeadd(&K.E.ffheat[mgi], distance_e_cmf * kap.ffheating);
+  const double distance_e_cmf_over_nu = distance_e_cmf / nu;
+  for (int g = 0; g < K.T.nbfg; g++) {
+    const double nu_edge = K.T.groundcont_nu_edge[g];
+    if (nu > nu_edge) {
+      const int element = K.T.groundcont_element[g];
+      if (K.C.elem_abundance[(int64_t)mgi * K.T.nelements + element] > 0) {
+        // groundcont_gamma_contr[g] at the frequency the opacity was computed at (rpkt.cc:1166-1171)
+        double gcontr = 0.;
+        for (int i = 0; i < K.T.nbf; i++) {
+          if (kap.nu < K.T.allcont_nu_edge[i]) break;
+          if (K.T.allcont_level[i] != 0 || K.T.allcont_groundindex[i] != g) continue;
+          double nnlevel, gc;
+          if (bf_contribution(K, k, mgi, i, kap.nu, &nnlevel, &gc)) gcontr += gc;
+        }
+        const int ion = K.T.groundcont_ion[g];
+        const int64_t idx = (int64_t)mgi * K.T.nelements * K.T.maxnions + element * K.T.maxnions + ion;
+        safeadd(&K.E.gamma[idx], gcontr * distance_e_cmf_over_nu);
+        safeadd(&K.E.bfheat[idx], gcontr * distance_e_cmf * (1. - nu_edge / nu));
+        lwork(x.L, WK_GC_UPDATES, 1);
+      }
+    } else {
+      break;
+    }
+  }
+}
+
+// rpkt.cc:330-447
+DEVNI void rpkt_event_continuum(Tx &x, Pkt &p, const Kappa &kap, int k, int mgi) {
+  const Ctx &K = x.K;
+  const double nu = p.nu_cmf;
+  const double dopplerfactor = doppler_packet(K, p);
+  const double kappa_cont = kap.total * dopplerfactor;
+  const double sigma = kap.es * dopplerfactor;
+  const double kappa_ff = kap.ff * dopplerfactor;
+  const double kappa_bf = kap.bf * dopplerfactor;
+  const double zrand = artis_rng_uniform(&x.rng);
+  lwork(x.L, WK_CONT_EVENTS, 1);
+  if (zrand * kappa_cont < sigma) {
+    p.interactions += 1;
+    p.nscatterings += 1;
+    p.last_event = 12;
+    lctr(x.L, CTR_ESCOUNTER);
+    lwork(x.L, WK_ES_SCAT, 1);
+    escat_rpkt(x, p);
+    p.em_pos[0] = p.pos[0];
+    p.em_pos[1] = p.pos[1];
+    p.em_pos[2] = p.pos[2];
+    p.em_time = (int)p.prop_time;
+  } else if (zrand * kappa_cont < sigma + kappa_ff) {
+    lctr(x.L, CTR_K_STAT_FROM_FF);
+    p.interactions += 1;
+    p.last_event = 5;
+    p.type = ARTIS_TYPE_KPKT;
+    p.absorptiontype = -1;
+  } else if (zrand * kappa_cont < sigma + kappa_ff + kappa_bf) {
+    p.absorptiontype = -2;
+    const double kappa_bf_inrest = kap.bf;
+    const double zrand2 = artis_rng_uniform(&x.rng);
+    const double kappa_bf_rand = zrand2 * kappa_bf_inrest;
+    // lower_bound over kappa_bf_sum[0, nbf-1): re-scan the running sum of calculate_kappa_bf_gammacontr at the
+    // frequency the opacity was computed at
+    const int last = K.T.nbf - 1;
+    int allcontindex = last;
+    double running = 0.;
+    for (int i = 0; i < last; i++) {
+      if (!(kap.nu < K.T.allcont_nu_edge[i])) {
+        double nnlevel, gc;
+        if (bf_contribution(K, k, mgi, i, kap.nu, &nnlevel, &gc)) running += nnlevel * gc;
+      }
+      if (!(running < kappa_bf_rand)) {
+        allcontindex = i;
+        break;
+      }
+    }
+    const double nu_edge = K.T.allcont_nu_edge[allcontindex];
+    const int element = K.T.allcont_element[allcontindex];
+    const int ion = K.T.allcont_ion[allcontindex];
+    const int level = K.T.allcont_level[allcontindex];
+    const int phixstargetindex = K.T.allcont_target[allcontindex];
+    const double zrand3 = artis_rng_uniform(&x.rng);
+    if (zrand3 < nu_edge / nu) {
+      lctr(x.L, CTR_MA_STAT_ACTIVATION_BF);
+      p.interactions += 1;
+      p.last_event = 3;
+      p.type = ARTIS_TYPE_MA;
+      p.ma_element = element;
+      p.ma_ion = ion + 1;
+      p.ma_level = get_phixsupperlevel(K, element, ion, level, phixstargetindex);
+      p.ma_activatingline = -99;
+    } else {
+      lctr(x.L, CTR_K_STAT_FROM_BF);
+      p.interactions += 1;
+      p.last_event = 4;
+      p.type = ARTIS_TYPE_KPKT;
+    }
+  } else {
+    x.err(ERR_CONT, p.number, 0);
+  }
+}
+// rpkt.cc:449-489
+DEVFN void rpkt_event_boundbound(Tx &x, Pkt &p) {
+  lctr(x.L, CTR_MA_STAT_ACTIVATION_BB);
+  lwork(x.L, WK_BB_EVENTS, 1);
+  p.interactions += 1;
+  p.last_event = 1;
+  p.absorptiontype = p.ma_activatingline;
+  p.absorptionfreq = p.nu_rf;
+  p.absorptiondir[0] = p.dir[0];
+  p.absorptiondir[1] = p.dir[1];
+  p.absorptiondir[2] = p.dir[2];
+  p.type = ARTIS_TYPE_MA;
+  if (x.K.R.record_linestat) atomicAdd(&x.K.E.acounter[p.next_trans - 1], 1);
+}
+
+// rpkt.cc:623-813
+DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2) {
+  const Ctx &K = x.K;
+  const int npm = K.G.npts_model;
+  int mgi = cell_mgi(K, p.where);
+  const int oldmgi = mgi;
+  lwork(x.L, WK_RPKT_STEPS, 1);
+  const double zrand = artis_rng_uniform_pos(&x.rng);
+  const double tau_next = -1. * log(zrand);
+  int snext = -1;
+  double sdist = boundary_cross(x, p, &snext);
+  if (sdist == 0) {
+    change_cell(x, p, snext);
+    mgi = cell_mgi(K, p.where);
+    return (p.type == ARTIS_TYPE_RPKT && (mgi == npm || mgi == oldmgi));
+  }
+  const double maxsdist = K.G.rmax * p.prop_time / K.G.tmin;
+  if (sdist > maxsdist) {
+    x.err(ERR_SDIST, p.number, p.where);
+    return false;
+  }
+  if (((snext != -99) && (snext < 0)) || (snext >= K.G.ngrid)) {
+    x.err(ERR_BADCELL, p.number, snext);
+    return false;
+  }
+  if (sdist > K.R.max_path_step) {
+    sdist = K.R.max_path_step;
+    snext = p.where;
+  }
+  const double tdist = (t2 - p.prop_time) * ARTIS_CLIGHT_PROP;
+  double edist;
+  int rpkt_eventtype = -1;
+  bool find_nextline = false;
+  Kappa kap;
+  kap.nu = 0.;
+  kap.total = kap.es = kap.ff = kap.bf = kap.ffheating = 0.;
+  const int k = (mgi == npm) ? -1 : K.C.ne_index[mgi];
+  if (mgi == npm) {
+    edist = DBL_MAX;
+    find_nextline = true;
+  } else if (K.C.thick[mgi] == 1) {
+    x.err(ERR_UNSUPPORTED_TYPE, p.number, -1);  // grey thick cells: not in this build
+    return false;
+  } else {
+    edist = get_event(x, k, mgi, p, kap, &rpkt_eventtype, tau_next, fmin(tdist, sdist));
+    if (!x.ok) return false;
+  }
+  if (!(edist >= 0)) {
+    x.err(ERR_EDIST, p.number, 0);
+    return false;
+  }
+  if ((sdist < tdist) && (sdist < edist)) {
+    move_pkt_withtime(K, p, sdist / 2.);
+    update_estimators(x, p, kap, sdist);
+    move_pkt_withtime(K, p, sdist / 2.);
+    if (snext != p.where) {
+      change_cell(x, p, snext);
+      mgi = cell_mgi(K, p.where);
+    }
+    p.scat_count = 0;
+    p.last_event = p.last_event + 100;
+    if (find_nextline) {
+      if (mgi != npm && K.C.thick[mgi] != 1) closest_transition_empty(K, p);
+    }
+    return (p.type == ARTIS_TYPE_RPKT && (mgi == npm || mgi == oldmgi));
+  } else if ((edist < sdist) && (edist < tdist)) {
+    move_pkt_withtime(K, p, edist / 2.);
+    update_estimators(x, p, kap, edist);
+    move_pkt_withtime(K, p, edist / 2.);
+    if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_BB)
+      rpkt_event_boundbound(x, p);
+    else if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_CONT)
+      rpkt_event_continuum(x, p, kap, k, mgi);
+    else
+      x.err(ERR_NOEVENT, p.number, 0);
+    return (x.ok && p.type == ARTIS_TYPE_RPKT && (mgi == npm || mgi == oldmgi));
+  } else if ((tdist < sdist) && (tdist < edist)) {
+    move_pkt_withtime(K, p, tdist / 2.);
+    update_estimators(x, p, kap, tdist);
+    p.prop_time = t2;
+    move_pkt(K, p, tdist / 2.);
+    p.last_event = p.last_event + 1000;
+    if (find_nextline) closest_transition_empty(K, p);
+    return false;
+  }
+  x.err(ERR_NOEVENT, p.number, 1);
+  return false;
+}
+
+// ------------------------------------------------------------------------------------------ fb emission
+// ratecoeff.cc:263-279
+DEVFN double alpha_sp_E_integrand(const Ctx &K, const float *xs, double nu_edge, float T, double nu) {
+  const float sigma_bf = (float)photoionization_crosssection_fromtable(K, xs, nu_edge, nu);
+  return ARTIS_TWOOVERCLIGHTSQUARED * sigma_bf * pow(nu, 3) / nu_edge * exp(-ARTIS_HOVERKB * nu / T);
+}
+DEVFN double alpha_sp_piece(const Ctx &K, const float *xs, double nu_threshold, float T, double a, double half) {
+  const double gx[4] = {-0.8611363115940526, -0.3399810435848563, 0.3399810435848563, 0.8611363115940526};
+  const double gw[4] = {0.3478548451374538, 0.6521451548625461, 0.6521451548625461, 0.3478548451374538};
+  const double mid = a + half;
+  double s = 0.;
+  for (int q = 0; q < 4; q++) s += gw[q] * alpha_sp_E_integrand(K, xs, nu_threshold, T, mid + half * gx[q]);
+  return s * half;
+}
+// ratecoeff.cc:628-684 with deviation D3 (see oracle/oracle.cc)
+DEVNI double select_continuum_nu(Tx &x, int e, int lowerion, int lower, int upperionlevel, float T_e) {
+  const Ctx &K = x.K;
+  int target = 0;
+  for (int t = 0; t < get_nphixstargets(K, e, lowerion, lower); t++)
+    if (get_phixsupperlevel(K, e, lowerion, lower, t) == upperionlevel) {
+      target = t;
+      break;
+    }
+  const double E_threshold = get_phixs_threshold(K, e, lowerion, lower, target);
+  const double nu_threshold = ARTIS_ONEOVERH * E_threshold;
+  const double nu_max_phixs = nu_threshold * K.T.last_phixs_nuovernuedge;
+  const int npieces = K.T.nphixspoints;
+  const float *xs = level_photoion_xs(K, e, lowerion, lower);
+  const double zrand = 1. - artis_rng_uniform(&x.rng);
+  const double deltanu = (nu_max_phixs - nu_threshold) / npieces;
+  const double half = 0.5 * deltanu;
+  double head = 0.;
+  for (int j = 0; j < npieces; j++) head += alpha_sp_piece(K, xs, nu_threshold, T_e, nu_threshold + j * deltanu, half);
+  const double total_alpha_sp = head;
+  double alpha_sp_old = total_alpha_sp;
+  double alpha_sp = total_alpha_sp;
+  head = 0.;
+  int i;
+  for (i = 1; i < npieces; i++) {
+    alpha_sp_old = alpha_sp;
+    head += alpha_sp_piece(K, xs, nu_threshold, T_e, nu_threshold + (i - 1) * deltanu, half);
+    alpha_sp = total_alpha_sp - head;
+    if (zrand >= alpha_sp / total_alpha_sp) break;
+  }
+  const double nuoffset = (total_alpha_sp * zrand - alpha_sp_old) / (alpha_sp - alpha_sp_old) * deltanu;
+  return nu_threshold + (i - 1) * deltanu + nuoffset;
+}
+
+// ------------------------------------------------------------------------------------------ macro-atom
+// macroatom.cc:416-482 (process-rate totals from the per-cell table; individual rates recomputed while selecting)
+DEVNI void do_macroatom(Tx &x, Pkt &p) {
+  const Ctx &K = x.K;
+  const double t_mid = K.G.ts_mid[x.nts];
+  const int mgi = cell_mgi(K, p.where);
+  const int k = K.C.ne_index[mgi];
+  const float T_e = K.C.Te[mgi];
+  const float nne = K.C.nne[mgi];
+  const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
+  if (K.C.thick[mgi] == 1) {
+    x.err(ERR_THICK_MA, p.number, mgi);
+    return;
+  }
+  const int element = p.ma_element;
+  int ion = p.ma_ion;
+  int level = p.ma_level;
+  const int activatingline = p.ma_activatingline;
+  bool end_packet = false;
+  unsigned long long jumps = 0, ntrans = 0;
+  while (!end_packet) {
+    jumps++;
+    if (jumps > 10000000ull) {
+      x.err(ERR_STUCK, p.number, 2);
+      break;
+    }
+    const double epsilon_current = epsilon(K, element, ion, level);
+    const int ul = ulev(K, element, ion, level);
+    const double *pr = K.C.marates + ((int64_t)k * K.T.nlevels_total + ul) * ARTIS_MA_ACTION_COUNT;
+    double processrates[ARTIS_MA_ACTION_COUNT];
+    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) processrates[a] = pr[a];
+    double total_transitions = 0.;
+    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) total_transitions += processrates[a];
+    int selected_action = ARTIS_MA_ACTION_COUNT;
+    const double zrand = artis_rng_uniform(&x.rng);
+    const double randomrate = zrand * total_transitions;
+    double rate = 0.;
+    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
+      rate += processrates[a];
+      if (rate > randomrate) {
+        selected_action = a;
+        break;
+      }
+    }
+    if (rate <= randomrate) {
+      x.err(ERR_MA_RANDOM, p.number, ul);
+      break;
+    }
+    if (selected_action == ARTIS_MA_ACTION_RADDEEXC) {
+      // macroatom.cc:222-296
+      const double zr = artis_rng_uniform(&x.rng);
+      double r = 0.;
+      int linelistindex = -99;
+      const int ndowntrans = K.T.level_ndowntrans[ul];
+      const int doff = K.T.level_downtrans_offset[ul];
+      for (int j = 0; j < ndowntrans; j++) {
+        const int li = K.T.downtrans_lineindex[doff + j];
+        const int lower = K.T.line_lower[li];
+        const double epsilon_trans = epsilon_current - epsilon(K, element, ion, lower);
+        const double R = rad_deexcitation_ratecoeff(K, pops, element, ion, level, lower, epsilon_trans, li, t_mid);
+        r += R * epsilon_trans;
+        ntrans++;
+        if (zr * processrates[ARTIS_MA_ACTION_RADDEEXC] < r) {
+          linelistindex = li;
+          break;
+        }
+      }
+      if (linelistindex < 0) {
+        x.err(ERR_MA_SELECT, p.number, 1);
+        break;
+      }
+      if (K.R.record_linestat) atomicAdd(&K.E.ecounter[linelistindex], 1);
+      const int lower = K.T.line_lower[linelistindex];
+      const double epsilon_trans = epsilon(K, element, ion, level) - epsilon(K, element, ion, lower);
+      double oldnucmf = 0.;
+      if (p.last_event == 1) oldnucmf = p.nu_cmf;
+      p.nu_cmf = epsilon_trans / ARTIS_H;
+      if (p.last_event == 1) lctr(x.L, (oldnucmf < p.nu_cmf) ? CTR_UPSCATTER : CTR_DOWNSCATTER);
+      lctr(x.L, CTR_MA_STAT_DEACTIVATION_BB);
+      p.interactions += 1;
+      p.last_event = 0;
+      emitt_rpkt(x, p);
+      if (linelistindex == activatingline) lctr(x.L, CTR_RESONANCESCATTERINGS);
+      p.next_trans = linelistindex + 1;
+      p.emissiontype = linelistindex;
+      p.em_pos[0] = p.pos[0];
+      p.em_pos[1] = p.pos[1];
+      p.em_pos[2] = p.pos[2];
+      p.em_time = (int)p.prop_time;
+      p.nscatterings = 0;
+      end_packet = true;
+    } else if (selected_action == ARTIS_MA_ACTION_COLDEEXC || selected_action == ARTIS_MA_ACTION_COLRECOMB) {
+      const bool deexc = selected_action == ARTIS_MA_ACTION_COLDEEXC;
+      lctr(x.L, deexc ? CTR_MA_STAT_DEACTIVATION_COLLDEEXC : CTR_MA_STAT_DEACTIVATION_COLLRECOMB);
+      p.interactions += 1;
+      p.last_event = deexc ? 10 : 11;
+      p.type = ARTIS_TYPE_KPKT;
+      end_packet = true;
+      safeadd(&K.E.colheat[mgi], p.e_cmf);
+    } else if (selected_action == ARTIS_MA_ACTION_INTERNALDOWNSAME) {
+      // macroatom.cc:174-220
+      p.interactions += 1;
+      const double zr = artis_rng_uniform(&x.rng);
+      int lower = -99;
+      double r = 0.;
+      const int ndowntrans = K.T.level_ndowntrans[ul];
+      const int doff = K.T.level_downtrans_offset[ul];
+      const double statweight = stat_weight(K, element, ion, level);
+      for (int j = 0; j < ndowntrans; j++) {
+        const int li = K.T.downtrans_lineindex[doff + j];
+        const int lo = K.T.line_lower[li];
+        const double epsilon_target = epsilon(K, element, ion, lo);
+        const double epsilon_trans = epsilon_current - epsilon_target;
+        const double R = rad_deexcitation_ratecoeff(K, pops, element, ion, level, lo, epsilon_trans, li, t_mid);
+        const double C =
+            col_deexcitation_ratecoeff(K, T_e, nne, epsilon_trans, li, stat_weight(K, element, ion, lo), statweight);
+        r += (R + C) * epsilon_target;
+        ntrans++;
+        if (zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNSAME] < r) {
+          lower = lo;
+          break;
+        }
+      }
+      if (lower < 0) {
+        x.err(ERR_MA_SELECT, p.number, 4);
+        break;
+      }
+      level = lower;
+    } else if (selected_action == ARTIS_MA_ACTION_RADRECOMB) {
+      // macroatom.cc:298-380
+      const int upperion = ion;
+      const int upperionlevel = level;
+      const double zr = artis_rng_uniform(&x.rng);
+      double r = 0;
+      const int nlevels = get_ionisinglevels(K, element, upperion - 1);
+      int lower = 0;
+      for (lower = 0; lower < nlevels; lower++) {
+        const double epsilon_trans = epsilon_current - epsilon(K, element, upperion - 1, lower);
+        const double R = rad_recombination_ratecoeff(K, T_e, nne, element, upperion, upperionlevel, lower);
+        r += R * epsilon_trans;
+        if (zr * processrates[ARTIS_MA_ACTION_RADRECOMB] < r) break;
+      }
+      ntrans += lower + 1;
+      if (zr * processrates[ARTIS_MA_ACTION_RADRECOMB] >= r) {
+        x.err(ERR_MA_SELECT, p.number, 2);
+        break;
+      }
+      ion = upperion - 1;
+      level = lower;
+      p.nu_cmf = select_continuum_nu(x, element, upperion - 1, lower, upperionlevel, T_e);
+      lctr(x.L, CTR_MA_STAT_DEACTIVATION_FB);
+      p.interactions += 1;
+      p.last_event = 2;
+      emitt_rpkt(x, p);
+      p.next_trans = 0;
+      {  // get_continuumindex (atomic.cc:16-30)
+        int target = 0;
+        for (int t = 0; t < get_nphixstargets(K, element, ion, lower); t++)
+          if (get_phixsupperlevel(K, element, ion, lower, t) == upperionlevel) {
+            target = t;
+            break;
+          }
+        p.emissiontype = K.T.level_cont_index[ulev(K, element, ion, lower)] - target;
+      }
+      p.em_pos[0] = p.pos[0];
+      p.em_pos[1] = p.pos[1];
+      p.em_pos[2] = p.pos[2];
+      p.em_time = (int)p.prop_time;
+      p.nscatterings = 0;
+      end_packet = true;
+    } else if (selected_action == ARTIS_MA_ACTION_INTERNALDOWNLOWER) {
+      p.interactions += 1;
+      lctr(x.L, CTR_MA_STAT_INTERNALDOWNLOWER);
+      const double zr = artis_rng_uniform(&x.rng);
+      double r = 0.;
+      const int nlevels = get_ionisinglevels(K, element, ion - 1);
+      int lower;
+      for (lower = 0; lower < nlevels; lower++) {
+        const double epsilon_target = epsilon(K, element, ion - 1, lower);
+        const double epsilon_trans = epsilon_current - epsilon_target;
+        const double R = rad_recombination_ratecoeff(K, T_e, nne, element, ion, level, lower);
+        const double C = col_recombination_ratecoeff(K, mgi, element, ion, level, lower, epsilon_trans);
+        r += (R + C) * epsilon_target;
+        if (zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNLOWER] < r) break;
+      }
+      ntrans += lower + 1;
+      if (lower >= nlevels) {
+        x.err(ERR_MA_SELECT, p.number, 5);
+        break;
+      }
+      ion -= 1;
+      level = lower;
+    } else if (selected_action == ARTIS_MA_ACTION_INTERNALUPSAME) {
+      p.interactions += 1;
+      const double zr = artis_rng_uniform(&x.rng);
+      int upper = -99;
+      double r = 0.;
+      const int nuptrans = K.T.level_nuptrans[ul];
+      const int uoff = K.T.level_uptrans_offset[ul];
+      const double statweight = stat_weight(K, element, ion, level);
+      for (int j = 0; j < nuptrans; j++) {
+        const int li = K.T.uptrans_lineindex[uoff + j];
+        const int up = K.T.line_upper[li];
+        const double epsilon_trans = epsilon(K, element, ion, up) - epsilon_current;
+        const double R = rad_excitation_ratecoeff(K, pops, mgi, element, ion, level, up, epsilon_trans, li, t_mid);
+        const double C =
+            col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, element, ion, up));
+        r += (R + C + 0.) * epsilon_current;
+        ntrans++;
+        if (zr * processrates[ARTIS_MA_ACTION_INTERNALUPSAME] < r) {
+          upper = up;
+          break;
+        }
+      }
+      if (upper < 0) {
+        x.err(ERR_MA_SELECT, p.number, 6);
+        break;
+      }
+      level = upper;
+    } else if (selected_action == ARTIS_MA_ACTION_INTERNALUPHIGHER) {
+      // macroatom.cc:382-414
+      p.interactions += 1;
+      lctr(x.L, CTR_MA_STAT_INTERNALUPHIGHER);
+      int upper = -1;
+      const double zr = artis_rng_uniform(&x.rng);
+      double r = 0.;
+      const int nt = get_nphixstargets(K, element, ion, level);
+      const int slot0 = K.T.level_phixstargets_offset[ul];
+      for (int t = 0; t < nt; t++) {
+        upper = get_phixsupperlevel(K, element, ion, level, t);
+        const double epsilon_trans = get_phixs_threshold(K, element, ion, level, t);
+        const double R = K.C.corrphot[(int64_t)k * K.T.ntargets_total + slot0 + t];
+        const double C = col_ionization_ratecoeff(K, T_e, nne, element, ion, level, t, epsilon_trans);
+        r += (R + C) * epsilon_current;
+        if (zr * processrates[ARTIS_MA_ACTION_INTERNALUPHIGHER] < r) break;
+      }
+      if (zr * processrates[ARTIS_MA_ACTION_INTERNALUPHIGHER] >= r) {
+        x.err(ERR_MA_SELECT, p.number, 7);
+        break;
+      }
+      ion += 1;
+      level = upper;
+    } else {
+      x.err(ERR_MA_SELECT, p.number, 100 + selected_action);
+      break;
+    }
+  }
+  lwork(x.L, WK_MA_JUMPS, jumps);
+  lwork(x.L, WK_MA_TRANS, ntrans);
+  if (p.trueemissiontype < 0) {
+    p.trueemissiontype = p.emissiontype;
+    p.trueemissionvelocity = (float)(vec_len(p.em_pos) / p.em_time);
+    p.trueem_time = p.em_time;
+  }
+}
+
+// ------------------------------------------------------------------------------------------ k-packets
+// kpkt.cc:428-446
+DEVFN double sample_planck(Tx &x, double T, int number) {
+  const double nu_peak = 5.879e10 * T;
+  const double B_peak = dbb(nu_peak, T, 1);
+  for (int tries = 0; tries < 10000000; tries++) {
+    const double zrand = artis_rng_uniform(&x.rng);
+    const double zrand2 = artis_rng_uniform(&x.rng);
+    const double nu = x.K.G.nu_min_r + zrand * (x.K.G.nu_max_r - x.K.G.nu_min_r);
+    if (zrand2 * B_peak <= dbb(nu, T, 1)) return nu;
+  }
+  x.err(ERR_STUCK, number, 3);
+  return x.K.G.nu_min_r;
+}
+// kpkt.cc:448-475
+DEVNI void do_kpkt_bb(Tx &x, Pkt &p) {
+  const int mgi = cell_mgi(x.K, p.where);
+  const float T_e = x.K.C.Te[mgi];
+  p.nu_cmf = sample_planck(x, T_e, p.number);
+  emitt_rpkt(x, p);
+  p.next_trans = 0;
+  lctr(x.L, CTR_K_STAT_TO_R_BB);
+  p.interactions++;
+  p.last_event = 6;
+  p.emissiontype = -9999999;
+  p.em_pos[0] = p.pos[0];
+  p.em_pos[1] = p.pos[1];
+  p.em_pos[2] = p.pos[2];
+  p.em_time = (int)p.prop_time;
+  p.nscatterings = 0;
+}
+// kpkt.cc:477-797 (cumulative cooling list from the per-cell table)
+DEVNI void do_kpkt(Tx &x, Pkt &p, double t2) {
+  const Ctx &K = x.K;
+  const double t1 = p.prop_time;
+  const int mgi = cell_mgi(K, p.where);
+  const int k = K.C.ne_index[mgi];
+  const float T_e = K.C.Te[mgi];
+  lwork(x.L, WK_KPKT, 1);
+  double deltat = 0.;
+  if (x.nts < K.R.n_kpktdiffusion_timesteps) deltat = K.R.kpktdiffusion_timescale * K.G.ts_width[x.nts];
+  const double t_current = t1 + deltat;
+  if (!(t_current <= t2)) {
+    const double s = t2 / t1;
+    p.pos[0] *= s;
+    p.pos[1] *= s;
+    p.pos[2] *= s;
+    p.prop_time = t2;
+    return;
+  }
+  {
+    const double s = t_current / t1;
+    p.pos[0] *= s;
+    p.pos[1] *= s;
+    p.pos[2] *= s;
+  }
+  p.prop_time = t_current;
+  double coolingsum = 0.;
+  const double zrand = artis_rng_uniform(&x.rng);
+  const double rndcool = zrand * K.C.totalcooling[mgi];
+  double oldcoolingsum = 0.;
+  int element = -1, ion = -1;
+  for (element = 0; element < K.T.nelements; element++) {
+    const int nions = get_nions(K, element);
+    for (ion = 0; ion < nions; ion++) {
+      oldcoolingsum = coolingsum;
+      coolingsum += K.C.cooling_contrib_ion[(int64_t)mgi * K.T.nions_total + uion(K, element, ion)];
+      if (coolingsum > rndcool) break;
+    }
+    if (coolingsum > rndcool) break;
+  }
+  if (element >= K.T.nelements || ion >= get_nions(K, element)) {
+    x.err(ERR_KPKT, p.number, 0);
+    return;
+  }
+  const int ui = uion(K, element, ion);
+  const int ilow = K.T.ion_coolingoffset[ui];
+  const int ihigh = ilow + K.T.ion_ncoolingterms[ui] - 1;
+  const double *cc = K.C.cooling + (int64_t)k * K.T.ncoolingterms;
+  int lo = ilow, hi = ihigh + 1;
+  while (lo < hi) {
+    const int mid = lo + (hi - lo) / 2;
+    if (cc[mid] < rndcool)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  int icool = lo;
+  if (icool > ihigh) icool = ihigh;  // deviation D6
+  lwork(x.L, WK_KPKT_TERMS, (unsigned long long)(icool - ilow + 1));
+  const int ctype = K.T.cool_type[icool];
+  if (ctype == ARTIS_COOLINGTYPE_FF) {
+    const double zr = artis_rng_uniform_pos(&x.rng);
+    p.nu_cmf = -ARTIS_KB * T_e / ARTIS_H * log(zr);
+    emitt_rpkt(x, p);
+    p.next_trans = 0;
+    lctr(x.L, CTR_K_STAT_TO_R_FF);
+    p.interactions += 1;
+    p.last_event = 6;
+    p.emissiontype = -9999999;
+    p.em_pos[0] = p.pos[0];
+    p.em_pos[1] = p.pos[1];
+    p.em_pos[2] = p.pos[2];
+    p.em_time = (int)p.prop_time;
+    p.nscatterings = 0;
+  } else if (ctype == ARTIS_COOLINGTYPE_FB) {
+    const int el = K.T.cool_element[icool];
+    const int lowerion = K.T.cool_ion[icool];
+    const int level = K.T.cool_level[icool];
+    const int upper = K.T.cool_upper[icool];
+    p.nu_cmf = select_continuum_nu(x, el, lowerion, level, upper, T_e);
+    emitt_rpkt(x, p);
+    p.next_trans = 0;
+    lctr(x.L, CTR_K_STAT_TO_R_FB);
+    p.interactions += 1;
+    p.last_event = 7;
+    int target = 0;
+    for (int t = 0; t < get_nphixstargets(K, el, lowerion, level); t++)
+      if (get_phixsupperlevel(K, el, lowerion, level, t) == upper) {
+        target = t;
+        break;
+      }
+    p.emissiontype = K.T.level_cont_index[ulev(K, el, lowerion, level)] - target;
+    p.trueemissiontype = p.emissiontype;
+    p.em_pos[0] = p.pos[0];
+    p.em_pos[1] = p.pos[1];
+    p.em_pos[2] = p.pos[2];
+    p.em_time = (int)p.prop_time;
+    p.nscatterings = 0;
+  } else if (ctype == ARTIS_COOLINGTYPE_COLLEXC) {
+    const float nne = K.C.nne[mgi];
+    const double contrib_low = (icool > ilow) ? cc[icool - 1] : oldcoolingsum;
+    double contrib = contrib_low;
+    const int level = K.T.cool_level[icool];
+    const double epsilon_current = epsilon(K, element, ion, level);
+    const int ul = ulev(K, element, ion, level);
+    const double nnlevel = K.C.pops[(int64_t)k * K.T.nlevels_total + ul];
+    const double statweight = stat_weight(K, element, ion, level);
+    int upper = -1;
+    const int nuptrans = K.T.level_nuptrans[ul];
+    const int uoff = K.T.level_uptrans_offset[ul];
+    for (int ii = 0; ii < nuptrans; ii++) {
+      const int li = K.T.uptrans_lineindex[uoff + ii];
+      const int tmpupper = K.T.line_upper[li];
+      const double epsilon_trans = epsilon(K, element, ion, tmpupper) - epsilon_current;
+      const double C = nnlevel *
+                       col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight,
+                                                stat_weight(K, element, ion, tmpupper)) *
+                       epsilon_trans;
+      contrib += C;
+      if (contrib >= rndcool) {
+        upper = tmpupper;
+        break;
+      }
+    }
+    if (upper < 0 && nuptrans > 0) upper = K.T.line_upper[K.T.uptrans_lineindex[uoff + nuptrans - 1]];  // D6
+    if (upper < 0) {
+      x.err(ERR_KPKT, p.number, 1);
+      return;
+    }
+    p.ma_element = element;
+    p.ma_ion = ion;
+    p.ma_level = upper;
+    p.ma_activatingline = -99;
+    p.type = ARTIS_TYPE_MA;
+    lctr(x.L, CTR_MA_STAT_ACTIVATION_COLLEXC);
+    lctr(x.L, CTR_K_STAT_TO_MA_COLLEXC);
+    p.interactions += 1;
+    p.last_event = 8;
+    p.trueemissiontype = -1;
+    p.trueemissionvelocity = -1;
+  } else if (ctype == ARTIS_COOLINGTYPE_COLLION) {
+    p.ma_element = K.T.cool_element[icool];
+    p.ma_ion = K.T.cool_ion[icool] + 1;
+    p.ma_level = K.T.cool_upper[icool];
+    p.ma_activatingline = -99;
+    p.type = ARTIS_TYPE_MA;
+    lctr(x.L, CTR_MA_STAT_ACTIVATION_COLLION);
+    lctr(x.L, CTR_K_STAT_TO_MA_COLLION);
+    p.interactions += 1;
+    p.last_event = 9;
+    p.trueemissiontype = -1;
+    p.trueemissionvelocity = -1;
+  } else {
+    x.err(ERR_KPKT, p.number, 2);
+  }
+}
+
+#endif

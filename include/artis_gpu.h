@@ -318,6 +318,8 @@ int artis_gpu_estimator_block_from_device(const void *src_device);
 /* Milliseconds of the transport kernel(s) of the last update_packets call, measured with HIP events on the
  * engine's own stream (the stream the kernels run on). */
 double artis_gpu_last_transport_ms(void);
+/* Milliseconds of the per-cell precompute kernels of the last artis_gpu_upload_cellstate (HIP events). */
+double artis_gpu_last_precompute_ms(void);
 /* Per-call event counts from the device (steps, lines scanned, kappa evaluations, ...), for the byte model. */
 #define ARTIS_WORK_COUNT 16
 int artis_gpu_last_work_counts(int64_t out[ARTIS_WORK_COUNT]);

@@ -16,9 +16,10 @@
 //       (input.cc:1908-1917).  Same draw sites, same draw order within a packet.
 //   D2 No relative-1e-4 kappa cache (rpkt.cc:1216-1221): continuum opacity is recomputed at every get_event;
 //       the reference reuses a value computed at a frequency up to 1e-4 away.
-//   D3 select_continuum_nu (ratecoeff.cc:628-684): the tail integrals of alpha_sp_E are computed as sums of
-//       per-piece 4-point Gauss-Legendre integrals instead of repeated GSL qag(GK31, epsrel 1e-2) calls; same
-//       piece grid, same inversion formula.
+//   D3 select_continuum_nu (ratecoeff.cc:628-684): the tail integrals of alpha_sp_E from nu_threshold + i*dnu
+//       to nu_max are computed as total - head(i), with total and head(i) sums of per-piece 4-point
+//       Gauss-Legendre integrals, instead of repeated GSL qag(GK31, epsrel 1e-2) calls; same piece grid, same
+//       inversion formula.
 //   D4 acounter is recorded for every packet, not only OpenMP thread 0 (rpkt.cc:481-488).
 //   D5 The update_packets pass loop with re-sorting (update_packets.cc:249-330) is flattened: each packet is
 //       advanced to the end of the timestep in one go.  With D2 there is no per-thread state that can change a
@@ -391,29 +392,27 @@ double select_continuum_nu(const Ctx &c, artis_rng *rng, int e, int lowerion, in
   const float *xs = level_photoion_xs(c, e, lowerion, lower);
   const double zrand = 1. - artis_rng_uniform(rng);
   const double deltanu = (nu_max_phixs - nu_threshold) / npieces;
-  // piece integrals, 4-point Gauss-Legendre
+  // piece integrals, 4-point Gauss-Legendre; tail(i) = total - head(i), heads summed bottom-up
   static const double gx[4] = {-0.8611363115940526, -0.3399810435848563, 0.3399810435848563, 0.8611363115940526};
   static const double gw[4] = {0.3478548451374538, 0.6521451548625461, 0.6521451548625461, 0.3478548451374538};
-  std::vector<double> piece(npieces);
-  for (int j = 0; j < npieces; j++) {
-    const double a = nu_threshold + j * deltanu;
-    const double half = 0.5 * deltanu;
+  const double half = 0.5 * deltanu;
+  auto piece = [&](double a) {
     const double mid = a + half;
     double s = 0.;
-    for (int k = 0; k < 4; k++) s += gw[k] * alpha_sp_E_integrand(c, xs, nu_threshold, T_e, mid + half * gx[k]);
-    piece[j] = s * half;
-  }
-  // tail[i] = integral from nu_threshold + i*deltanu to nu_max_phixs (summed from the top)
-  std::vector<double> tail(npieces + 1);
-  tail[npieces] = 0.;
-  for (int j = npieces - 1; j >= 0; j--) tail[j] = tail[j + 1] + piece[j];
-  const double total_alpha_sp = tail[0];
+    for (int q = 0; q < 4; q++) s += gw[q] * alpha_sp_E_integrand(c, xs, nu_threshold, T_e, mid + half * gx[q]);
+    return s * half;
+  };
+  double head = 0.;
+  for (int j = 0; j < npieces; j++) head += piece(nu_threshold + j * deltanu);
+  const double total_alpha_sp = head;
   double alpha_sp_old = total_alpha_sp;
   double alpha_sp = total_alpha_sp;
+  head = 0.;
   int i;
   for (i = 1; i < npieces; i++) {
     alpha_sp_old = alpha_sp;
-    alpha_sp = tail[i];
+    head += piece(nu_threshold + (i - 1) * deltanu);
+    alpha_sp = total_alpha_sp - head;
     if (zrand >= alpha_sp / total_alpha_sp) break;
   }
   const double nuoffset = (total_alpha_sp * zrand - alpha_sp_old) / (alpha_sp - alpha_sp_old) * deltanu;
@@ -897,7 +896,7 @@ double calculate_kappa_ff(const Ctx &c, int mgi, double nu) {
       const int Z = get_ionstage(c, e, i) - 1;
       if (Z > 0) kappa_ff += Z * Z * g_ff * nnion;
     }
-  kappa_ff *= 3.69255e8 / sqrt(T_e) * pow(nu, -3) * nne * (1 - exp(-ARTIS_HOVERKB * nu / T_e));
+  kappa_ff *= 3.69255e8 / sqrt((double)T_e) * pow(nu, -3) * nne * (1 - exp(-ARTIS_HOVERKB * nu / T_e));
   return kappa_ff;
 }
 // rpkt.cc:1075-1207 (SEPARATE_STIMRECOMB false, DETAILED_BF_ESTIMATORS_ON false, LUT photoion)
@@ -911,6 +910,7 @@ double calculate_kappa_bf_gammacontr(const Ctx &c, ThreadCache &tc, int mgi, dou
   int i = 0;
   const int nbfcontinua = a.nbfcontinua;
   for (i = 0; i < nbfcontinua; i++) {
+    if (!(nu < a.allcont_nu_edge[i])) tc.work[WK_BF_ACTIVE]++;
     const int element = a.allcont_element[i];
     const int ion = a.allcont_ion[i];
     const int level = a.allcont_level[i];
@@ -919,7 +919,6 @@ double calculate_kappa_bf_gammacontr(const Ctx &c, ThreadCache &tc, int mgi, dou
       const double nnlevel = get_levelpop(tc, c, element, ion, level);
       const double nu_max_phixs = nu_edge * a.last_phixs_nuovernuedge;
       if (nu < nu_edge) break;
-      tc.work[WK_BF_ACTIVE]++;
       if (nu <= nu_max_phixs && nnlevel > 0) {
         const double sigma_bf = photoionization_crosssection_fromtable(
             c, a.phixs_xs + (size_t)a.allcont_phixstable[i] * a.nphixspoints, nu_edge, nu);
@@ -1687,7 +1686,7 @@ void calculate_kpkt_rates_ion(const Ctx &c, ThreadCache &tc, int mgi, int e, int
   const artis_atomic_tables &a = *c.at;
   const int ioncharge = get_ionstage(c, e, i) - 1;
   if (ioncharge > 0) {
-    const double C = 1.426e-27 * sqrt(T_e) * pow(ioncharge, 2) * nncurrention * nne;
+    const double C = 1.426e-27 * sqrt((double)T_e) * pow(ioncharge, 2) * nncurrention * nne;
     contrib += C;
     tc.cooling_contrib[idx] = contrib;
     idx++;
