@@ -183,7 +183,8 @@ __global__ void k_cooling(Ctx K) {
   }
 }
 
-// macroatom.cc:57-159 calculate_macroatom_transitionrates, one workitem per (cell, level)
+// macroatom.cc:57-159 calculate_macroatom_transitionrates, one workitem per (cell, level); with the macro-atom
+// cache it also stores the running sums of the individual rates (cellhistory individ_* arrays)
 __global__ void k_marates(Ctx K, int nts) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nl = K.T.nlevels_total;
@@ -201,6 +202,11 @@ __global__ void k_marates(Ctx K, int nts) {
   const double *pops = K.C.pops + (int64_t)k * nl;
   const double epsilon_current = K.T.level_epsilon[ul];
   const double statweight = K.T.level_stat_weight[ul];
+  const bool cache = K.C.have_macache;
+  double *cum = cache ? K.C.ma_cum + (int64_t)k * K.C.ma_cum_stride : nullptr;
+  double *cum_drad = cum, *cum_dint = cum + K.T.ndown_total, *cum_uint = cum + 2 * K.T.ndown_total;
+  double *cum_rrad = cum + 2 * K.T.ndown_total + K.T.nup_total;
+  double *cum_rint = cum_rrad + K.T.nrecomb_slots;
   double pr[ARTIS_MA_ACTION_COUNT];
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) pr[a] = 0.;
   const int ndowntrans = K.T.level_ndowntrans[ul];
@@ -215,9 +221,14 @@ __global__ void k_marates(Ctx K, int nts) {
     pr[ARTIS_MA_ACTION_RADDEEXC] += R * epsilon_trans;
     pr[ARTIS_MA_ACTION_COLDEEXC] += C * epsilon_trans;
     pr[ARTIS_MA_ACTION_INTERNALDOWNSAME] += (R + C) * epsilon_target;
+    if (cache) {
+      cum_drad[doff + j] = pr[ARTIS_MA_ACTION_RADDEEXC];
+      cum_dint[doff + j] = pr[ARTIS_MA_ACTION_INTERNALDOWNSAME];
+    }
   }
   if (i > 0 && l <= K.T.ion_maxrecombininglevel[ui]) {
     const int nlevels = get_ionisinglevels(K, e, i - 1);
+    const int roff = K.T.level_recomb_offset[ul];
     for (int lower = 0; lower < nlevels; lower++) {
       const double epsilon_target = epsilon(K, e, i - 1, lower);
       const double epsilon_trans = epsilon_current - epsilon_target;
@@ -226,6 +237,10 @@ __global__ void k_marates(Ctx K, int nts) {
       pr[ARTIS_MA_ACTION_INTERNALDOWNLOWER] += (R + C) * epsilon_target;
       pr[ARTIS_MA_ACTION_RADRECOMB] += R * epsilon_trans;
       pr[ARTIS_MA_ACTION_COLRECOMB] += C * epsilon_trans;
+      if (cache) {
+        cum_rrad[roff + lower] = pr[ARTIS_MA_ACTION_RADRECOMB];
+        cum_rint[roff + lower] = pr[ARTIS_MA_ACTION_INTERNALDOWNLOWER];
+      }
     }
   }
   const int nuptrans = K.T.level_nuptrans[ul];
@@ -237,6 +252,7 @@ __global__ void k_marates(Ctx K, int nts) {
     const double R = rad_excitation_ratecoeff(K, pops, mgi, e, i, l, upper, epsilon_trans, li, t_mid);
     const double C = col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, e, i, upper));
     pr[ARTIS_MA_ACTION_INTERNALUPSAME] += (R + C + 0.) * epsilon_current;
+    if (cache) cum_uint[uoff + j] = pr[ARTIS_MA_ACTION_INTERNALUPSAME];
   }
   if (i < K.T.elem_nions[e] - 1 && l < K.T.ion_ionisinglevels[ui]) {
     const int nt = K.T.level_nphixstargets[ul];
@@ -571,6 +587,33 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     lt[li] = {B_ul, B_lu, ulo, uup};
   }
   rc |= dupload(&T.line_tau, lt.data(), nli);
+  // macro-atom per-line constants (macroatom.cc:518-522, 563-566; radfield.h:47; macroatom.h:93,130)
+  std::vector<LineMA> lm(nli);
+  for (int li = 0; li < nli; li++) {
+    const int ulo = lt[li].ul_lower, uup = lt[li].ul_upper;
+    const double epsilon_trans = a->level_epsilon[uup] - a->level_epsilon[ulo];
+    const double nu_trans = epsilon_trans / ARTIS_H;
+    const double A_ul = a->line_einstein_A[li];
+    const double B_ul = ARTIS_CLIGHTSQUAREDOVERTWOH / pow(nu_trans, 3) * A_ul;
+    const double B_lu = (double)a->level_stat_weight[uup] / (double)a->level_stat_weight[ulo] * B_ul;
+    lm[li] = {B_ul, B_lu, pow(nu_trans, 3), pow(ARTIS_H_IONPOT / epsilon_trans, 2)};
+  }
+  rc |= dupload(&T.line_ma, lm.data(), nli);
+  // recombination lists: levels l <= maxrecombininglevel of ions i > 0 (macroatom.cc:104-124)
+  std::vector<int32_t> recoff(nl, -1);
+  int64_t nrec = 0;
+  for (int e = 0; e < ne; e++)
+    for (int i = 1; i < a->elem_nions[e]; i++) {
+      const int ui = a->elem_uniqueionoffset[e] + i;
+      for (int l = 0; l < a->ion_nlevels[ui] && l <= a->ion_maxrecombininglevel[ui]; l++) {
+        recoff[a->ion_uniqueleveloffset[ui] + l] = (int32_t)nrec;
+        nrec += a->ion_ionisinglevels[ui - 1];
+      }
+    }
+  rc |= dupload(&T.level_recomb_offset, recoff.data(), nl);
+  T.ndown_total = ndown;
+  T.nup_total = nup;
+  T.nrecomb_slots = nrec;
   rc |= dupload(&T.allcont_nu_edge, a->allcont_nu_edge, nb);
   rc |= dupload(&T.allcont_probability, a->allcont_probability, nb);
   rc |= dupload(&T.allcont_element, a->allcont_element, nb);
@@ -687,6 +730,23 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   rc |= dalloc(&C.corrphot, (size_t)nne_cells * (ntg + 1));
   rc |= dalloc(&C.cooling, (size_t)nne_cells * a->ncoolingterms);
   rc |= dalloc(&C.marates, (size_t)nne_cells * nl * ARTIS_MA_ACTION_COUNT);
+  C.ma_cum_stride = 2 * ndown + nup + 2 * nrec;
+  C.have_macache = 0;
+  C.ma_cum = nullptr;
+  {
+    size_t freeb = 0, totalb = 0;
+    (void)hipMemGetInfo(&freeb, &totalb);
+    const double need = (double)nne_cells * (double)C.ma_cum_stride * 8.0;
+    const char *env = getenv("ARTIS_GPU_NO_MACACHE");
+    if (!(env && env[0] == '1') && need < 0.75 * (double)freeb) {
+      double *mc = nullptr;
+      if (hipMalloc((void **)&mc, (size_t)need) == hipSuccess) {
+        G.allocs.push_back(mc);
+        C.ma_cum = mc;
+        C.have_macache = 1;
+      }
+    }
+  }
   // cell-state input buffers
   rc |= dalloc(&G.d_cellf, (size_t)8 * np);
   rc |= dalloc(&G.d_thick, (size_t)np);

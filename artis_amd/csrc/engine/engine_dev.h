@@ -24,6 +24,15 @@ struct LineTau {
   int32_t ul_upper;
 };
 
+// per-line constants of the macro-atom rate coefficients, evaluated on the host with the reference expressions
+// (so the device never calls pow in the hot loops):  nu_lev = (eps_upper - eps_lower) / H
+struct LineMA {
+  double B_ul;  // CLIGHTSQUAREDOVERTWOH / pow(nu_lev, 3) * A_ul   (macroatom.cc:521, 565)
+  double B_lu;  // g_u / g_l * B_ul                               (macroatom.cc:522, 566)
+  double nu3;   // pow(nu_lev, 3)                                 (radfield.h:47)
+  double P2;    // pow(H_ionpot / (eps_upper - eps_lower), 2)    (macroatom.h:93, 130)
+};
+
 struct DevTab {
   int32_t nelements, maxnions, nions_total, nlevels_total, nlines, nbf, nbfg, ncoolingterms;
   int32_t nphixspoints, phixs_file_version, tablesize, ntargets_total;
@@ -44,6 +53,9 @@ struct DevTab {
   const int32_t *line_elem, *line_ion, *line_upper, *line_lower;
   const uint8_t *line_forbidden;
   const LineTau *line_tau;
+  const LineMA *line_ma;
+  const int32_t *level_recomb_offset;  // slot of the (level -> lower-ion levels) recombination list, -1 if none
+  int64_t ndown_total, nup_total, nrecomb_slots;
   const double *allcont_nu_edge, *allcont_probability;
   const int32_t *allcont_element, *allcont_ion, *allcont_level, *allcont_target, *allcont_upperlevel,
       *allcont_phixstable, *allcont_groundindex;
@@ -78,6 +90,13 @@ struct DevCells {
   double *corrphot;    // [n_nonempty * ntargets_total] get_corrphotoioncoeff (ratecoeff.cc:1247-1308)
   double *cooling;     // [n_nonempty * ncoolingterms]  cumulative cooling_contrib (kpkt.cc:167-308)
   double *marates;     // [n_nonempty * nlevels_total * 9] processrates (macroatom.cc:57-159)
+  // cumulative individual macro-atom rates per cell (the cellhistory individ_* arrays, globals.h:174-183),
+  // summed in the reference's order so that a binary search returns the reference's linear-scan choice:
+  // [rad_deexc over downtrans | internal_down_same over downtrans | internal_up_same over uptrans |
+  //  rad_recomb over recombination lists | internal_down_lower over recombination lists]
+  double *ma_cum;      // [n_nonempty * ma_cum_stride]
+  int64_t ma_cum_stride;
+  int32_t have_macache;
 };
 
 struct DevEst {

@@ -217,8 +217,8 @@ DEVFN double col_deexcitation_ratecoeff(const Ctx &K, float T_e, float nne, doub
       const double g_bar = 0.2;
       const double gauntfac = (eoverkt > 0.33421) ? g_bar : 0.276 * exp(eoverkt) * (-0.5772156649 - log(eoverkt));
       const double g_ratio = lowerstatweight / upperstatweight;
-      C = ARTIS_C_0 * 14.51039491 * nne * sqrtf(T_e) * K.T.line_f[li] *
-          pow(ARTIS_H_IONPOT / epsilon_trans, 2) * eoverkt * g_ratio * gauntfac;
+      C = ARTIS_C_0 * 14.51039491 * nne * sqrtf(T_e) * K.T.line_f[li] * K.T.line_ma[li].P2 * eoverkt * g_ratio *
+          gauntfac;
     } else {
       C = nne * 8.629e-6 * 0.01 * lowerstatweight / sqrtf(T_e);
     }
@@ -239,8 +239,8 @@ DEVFN double col_excitation_ratecoeff(const Ctx &K, float T_e, float nne, int li
       const double exp_eoverkt = exp(eoverkt);
       const double test = 0.276 * exp_eoverkt * (-0.5772156649 - log(eoverkt));
       const double Gamma = g_bar > test ? g_bar : test;
-      C = ARTIS_C_0 * nne * sqrtf(T_e) * 14.51039491 * K.T.line_f[li] * pow(ARTIS_H_IONPOT / epsilon_trans, 2) *
-          eoverkt / exp_eoverkt * Gamma;
+      C = ARTIS_C_0 * nne * sqrtf(T_e) * 14.51039491 * K.T.line_f[li] * K.T.line_ma[li].P2 * eoverkt / exp_eoverkt *
+          Gamma;
     } else {
       C = nne * 8.629e-6 * 0.01 * exp(-eoverkt) * upperstatweight / sqrtf(T_e);
     }
@@ -249,40 +249,36 @@ DEVFN double col_excitation_ratecoeff(const Ctx &K, float T_e, float nne, int li
   }
   return C;
 }
-// macroatom.cc:503-548 (populations from the per-cell table)
+// macroatom.cc:503-548 (populations from the per-cell table, B coefficients from LineMA)
 DEVFN double rad_deexcitation_ratecoeff(const Ctx &K, const double *pops, int e, int i, int upper, int lower,
                                         double epsilon_trans, int li, double t_current) {
   const double n_u = pops[ulev(K, e, i, upper)];
   const double n_l = pops[ulev(K, e, i, lower)];
   double R = 0.0;
-  const double nu_trans = epsilon_trans / ARTIS_H;
+  const LineMA lm = K.T.line_ma[li];
   const double A_ul = K.T.line_A[li];
-  const double B_ul = ARTIS_CLIGHTSQUAREDOVERTWOH / pow(nu_trans, 3) * A_ul;
-  const double B_lu = stat_weight(K, e, i, upper) / stat_weight(K, e, i, lower) * B_ul;
-  const double tau_sobolev = (B_lu * n_l - B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_current;
+  const double tau_sobolev = (lm.B_lu * n_l - lm.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_current;
   if (tau_sobolev > 1e-100) {
     const double beta = 1.0 / tau_sobolev * (-expm1(-tau_sobolev));
     R = A_ul * beta;
   }
   return R;
 }
-// macroatom.cc:550-643 (radfield.cc:898-943: dilute blackbody)
+// macroatom.cc:550-643 (radfield.cc:898-943: dilute blackbody, radfield.h:44-48)
 DEVFN double rad_excitation_ratecoeff(const Ctx &K, const double *pops, int mgi, int e, int i, int lower, int upper,
                                       double epsilon_trans, int li, double t_current) {
   const double n_u = pops[ulev(K, e, i, upper)];
   const double n_l = pops[ulev(K, e, i, lower)];
   double R = 0.0;
-  const double nu_trans = epsilon_trans / ARTIS_H;
-  const double A_ul = K.T.line_A[li];
-  const double B_ul = ARTIS_CLIGHTSQUAREDOVERTWOH / pow(nu_trans, 3) * A_ul;
-  const double B_lu = stat_weight(K, e, i, upper) / stat_weight(K, e, i, lower) * B_ul;
-  const double tau_sobolev = (B_lu * n_l - B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_current;
+  const LineMA lm = K.T.line_ma[li];
+  const double tau_sobolev = (lm.B_lu * n_l - lm.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_current;
   if (tau_sobolev > 1e-100) {
     const double beta = 1.0 / tau_sobolev * (-expm1(-tau_sobolev));
-    const double R_over_J_nu = n_l > 0. ? (B_lu - B_ul * n_u / n_l) * beta : B_lu * beta;
-    const float T_R = K.C.TR[mgi];
-    const float W = K.C.W[mgi];
-    R = R_over_J_nu * dbb(nu_trans, T_R, W);
+    const double R_over_J_nu = n_l > 0. ? (lm.B_lu - lm.B_ul * n_u / n_l) * beta : lm.B_lu * beta;
+    const double nu_trans = epsilon_trans / ARTIS_H;
+    const double T_R = K.C.TR[mgi];
+    const double W = K.C.W[mgi];
+    R = R_over_J_nu * (W * ARTIS_TWOHOVERCLIGHTSQUARED * lm.nu3 / expm1(ARTIS_HOVERKB * nu_trans / T_R));
   }
   return R;
 }

@@ -827,6 +827,20 @@ DEVNI double select_continuum_nu(Tx &x, int e, int lowerion, int lower, int uppe
 }
 
 // ------------------------------------------------------------------------------------------ macro-atom
+// first j in [0, n) with cum[j] > x (n if none): the reference's `rate += individ[j]; if (x < rate) break;`
+// scan, exact because cum holds those running sums in the same order (non-decreasing)
+DEVFN int first_above(const double *cum, int n, double x, unsigned long long &probes) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    probes++;
+    if (cum[mid] > x)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  return lo;
+}
 // macroatom.cc:416-482 (process-rate totals from the per-cell table; individual rates recomputed while selecting)
 DEVNI void do_macroatom(Tx &x, Pkt &p) {
   const Ctx &K = x.K;
@@ -836,6 +850,7 @@ DEVNI void do_macroatom(Tx &x, Pkt &p) {
   const float T_e = K.C.Te[mgi];
   const float nne = K.C.nne[mgi];
   const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
+  const double *macum = K.C.have_macache ? K.C.ma_cum + (int64_t)k * K.C.ma_cum_stride : nullptr;
   if (K.C.thick[mgi] == 1) {
     x.err(ERR_THICK_MA, p.number, mgi);
     return;
@@ -881,16 +896,21 @@ DEVNI void do_macroatom(Tx &x, Pkt &p) {
       int linelistindex = -99;
       const int ndowntrans = K.T.level_ndowntrans[ul];
       const int doff = K.T.level_downtrans_offset[ul];
-      for (int j = 0; j < ndowntrans; j++) {
-        const int li = K.T.downtrans_lineindex[doff + j];
-        const int lower = K.T.line_lower[li];
-        const double epsilon_trans = epsilon_current - epsilon(K, element, ion, lower);
-        const double R = rad_deexcitation_ratecoeff(K, pops, element, ion, level, lower, epsilon_trans, li, t_mid);
-        r += R * epsilon_trans;
-        ntrans++;
-        if (zr * processrates[ARTIS_MA_ACTION_RADDEEXC] < r) {
-          linelistindex = li;
-          break;
+      if (macum) {
+        const int j = first_above(macum + doff, ndowntrans, zr * processrates[ARTIS_MA_ACTION_RADDEEXC], ntrans);
+        if (j < ndowntrans) linelistindex = K.T.downtrans_lineindex[doff + j];
+      } else {
+        for (int j = 0; j < ndowntrans; j++) {
+          const int li = K.T.downtrans_lineindex[doff + j];
+          const int lower = K.T.line_lower[li];
+          const double epsilon_trans = epsilon_current - epsilon(K, element, ion, lower);
+          const double R = rad_deexcitation_ratecoeff(K, pops, element, ion, level, lower, epsilon_trans, li, t_mid);
+          r += R * epsilon_trans;
+          ntrans++;
+          if (zr * processrates[ARTIS_MA_ACTION_RADDEEXC] < r) {
+            linelistindex = li;
+            break;
+          }
         }
       }
       if (linelistindex < 0) {
@@ -934,19 +954,25 @@ DEVNI void do_macroatom(Tx &x, Pkt &p) {
       const int ndowntrans = K.T.level_ndowntrans[ul];
       const int doff = K.T.level_downtrans_offset[ul];
       const double statweight = stat_weight(K, element, ion, level);
-      for (int j = 0; j < ndowntrans; j++) {
-        const int li = K.T.downtrans_lineindex[doff + j];
-        const int lo = K.T.line_lower[li];
-        const double epsilon_target = epsilon(K, element, ion, lo);
-        const double epsilon_trans = epsilon_current - epsilon_target;
-        const double R = rad_deexcitation_ratecoeff(K, pops, element, ion, level, lo, epsilon_trans, li, t_mid);
-        const double C =
-            col_deexcitation_ratecoeff(K, T_e, nne, epsilon_trans, li, stat_weight(K, element, ion, lo), statweight);
-        r += (R + C) * epsilon_target;
-        ntrans++;
-        if (zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNSAME] < r) {
-          lower = lo;
-          break;
+      if (macum) {
+        const int j = first_above(macum + K.T.ndown_total + doff, ndowntrans,
+                                  zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNSAME], ntrans);
+        if (j < ndowntrans) lower = K.T.line_lower[K.T.downtrans_lineindex[doff + j]];
+      } else {
+        for (int j = 0; j < ndowntrans; j++) {
+          const int li = K.T.downtrans_lineindex[doff + j];
+          const int lo = K.T.line_lower[li];
+          const double epsilon_target = epsilon(K, element, ion, lo);
+          const double epsilon_trans = epsilon_current - epsilon_target;
+          const double R = rad_deexcitation_ratecoeff(K, pops, element, ion, level, lo, epsilon_trans, li, t_mid);
+          const double C =
+              col_deexcitation_ratecoeff(K, T_e, nne, epsilon_trans, li, stat_weight(K, element, ion, lo), statweight);
+          r += (R + C) * epsilon_target;
+          ntrans++;
+          if (zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNSAME] < r) {
+            lower = lo;
+            break;
+          }
         }
       }
       if (lower < 0) {
@@ -962,13 +988,19 @@ DEVNI void do_macroatom(Tx &x, Pkt &p) {
       double r = 0;
       const int nlevels = get_ionisinglevels(K, element, upperion - 1);
       int lower = 0;
-      for (lower = 0; lower < nlevels; lower++) {
-        const double epsilon_trans = epsilon_current - epsilon(K, element, upperion - 1, lower);
-        const double R = rad_recombination_ratecoeff(K, T_e, nne, element, upperion, upperionlevel, lower);
-        r += R * epsilon_trans;
-        if (zr * processrates[ARTIS_MA_ACTION_RADRECOMB] < r) break;
+      if (macum) {
+        lower = first_above(macum + 2 * K.T.ndown_total + K.T.nup_total + K.T.level_recomb_offset[ul], nlevels,
+                            zr * processrates[ARTIS_MA_ACTION_RADRECOMB], ntrans);
+        r = (lower < nlevels) ? DBL_MAX : -DBL_MAX;
+      } else {
+        for (lower = 0; lower < nlevels; lower++) {
+          const double epsilon_trans = epsilon_current - epsilon(K, element, upperion - 1, lower);
+          const double R = rad_recombination_ratecoeff(K, T_e, nne, element, upperion, upperionlevel, lower);
+          r += R * epsilon_trans;
+          if (zr * processrates[ARTIS_MA_ACTION_RADRECOMB] < r) break;
+        }
+        ntrans += lower + 1;
       }
-      ntrans += lower + 1;
       if (zr * processrates[ARTIS_MA_ACTION_RADRECOMB] >= r) {
         x.err(ERR_MA_SELECT, p.number, 2);
         break;
@@ -1003,15 +1035,20 @@ DEVNI void do_macroatom(Tx &x, Pkt &p) {
       double r = 0.;
       const int nlevels = get_ionisinglevels(K, element, ion - 1);
       int lower;
-      for (lower = 0; lower < nlevels; lower++) {
-        const double epsilon_target = epsilon(K, element, ion - 1, lower);
-        const double epsilon_trans = epsilon_current - epsilon_target;
-        const double R = rad_recombination_ratecoeff(K, T_e, nne, element, ion, level, lower);
-        const double C = col_recombination_ratecoeff(K, mgi, element, ion, level, lower, epsilon_trans);
-        r += (R + C) * epsilon_target;
-        if (zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNLOWER] < r) break;
+      if (macum) {
+        lower = first_above(macum + 2 * K.T.ndown_total + K.T.nup_total + K.T.nrecomb_slots + K.T.level_recomb_offset[ul],
+                            nlevels, zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNLOWER], ntrans);
+      } else {
+        for (lower = 0; lower < nlevels; lower++) {
+          const double epsilon_target = epsilon(K, element, ion - 1, lower);
+          const double epsilon_trans = epsilon_current - epsilon_target;
+          const double R = rad_recombination_ratecoeff(K, T_e, nne, element, ion, level, lower);
+          const double C = col_recombination_ratecoeff(K, mgi, element, ion, level, lower, epsilon_trans);
+          r += (R + C) * epsilon_target;
+          if (zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNLOWER] < r) break;
+        }
+        ntrans += lower + 1;
       }
-      ntrans += lower + 1;
       if (lower >= nlevels) {
         x.err(ERR_MA_SELECT, p.number, 5);
         break;
@@ -1026,18 +1063,24 @@ DEVNI void do_macroatom(Tx &x, Pkt &p) {
       const int nuptrans = K.T.level_nuptrans[ul];
       const int uoff = K.T.level_uptrans_offset[ul];
       const double statweight = stat_weight(K, element, ion, level);
-      for (int j = 0; j < nuptrans; j++) {
-        const int li = K.T.uptrans_lineindex[uoff + j];
-        const int up = K.T.line_upper[li];
-        const double epsilon_trans = epsilon(K, element, ion, up) - epsilon_current;
-        const double R = rad_excitation_ratecoeff(K, pops, mgi, element, ion, level, up, epsilon_trans, li, t_mid);
-        const double C =
-            col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, element, ion, up));
-        r += (R + C + 0.) * epsilon_current;
-        ntrans++;
-        if (zr * processrates[ARTIS_MA_ACTION_INTERNALUPSAME] < r) {
-          upper = up;
-          break;
+      if (macum) {
+        const int j = first_above(macum + 2 * K.T.ndown_total + uoff, nuptrans,
+                                  zr * processrates[ARTIS_MA_ACTION_INTERNALUPSAME], ntrans);
+        if (j < nuptrans) upper = K.T.line_upper[K.T.uptrans_lineindex[uoff + j]];
+      } else {
+        for (int j = 0; j < nuptrans; j++) {
+          const int li = K.T.uptrans_lineindex[uoff + j];
+          const int up = K.T.line_upper[li];
+          const double epsilon_trans = epsilon(K, element, ion, up) - epsilon_current;
+          const double R = rad_excitation_ratecoeff(K, pops, mgi, element, ion, level, up, epsilon_trans, li, t_mid);
+          const double C =
+              col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, element, ion, up));
+          r += (R + C + 0.) * epsilon_current;
+          ntrans++;
+          if (zr * processrates[ARTIS_MA_ACTION_INTERNALUPSAME] < r) {
+            upper = up;
+            break;
+          }
         }
       }
       if (upper < 0) {

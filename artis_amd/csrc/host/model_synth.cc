@@ -198,19 +198,19 @@ void build_atomic(Model &m, std::mt19937_64 &rng) {
     bool forb;
   };
   std::vector<L> lines;
-  int npairs = 0;
-  for (int ui = 0; ui < m.nions_total; ui++)
-    if (m.ion_nlevels[ui] > 1) npairs += m.ion_nlevels[ui] * (m.ion_nlevels[ui] - 1) / 2;
-  const double keep = std::min(1.0, (double)m.cfg.max_lines / std::max(npairs, 1));
+  // connectivity: each level connects down to its line_window nearest lower levels and to the lowest
+  // n_resonance levels (resonance-like lines), like the sparse transition lists of real atomic data
+  const int W = std::max(1, m.cfg.line_window);
+  const int NR = std::max(0, m.cfg.n_resonance);
   // 8 pi^2 e^2 / (m_e c^3): A_ul = f_lu * g_l/g_u * coef * nu^2
   const double coef = 8. * ARTIS_PI * ARTIS_PI * ARTIS_QE * ARTIS_QE / (ARTIS_ME * pow(ARTIS_CLIGHT, 3));
   for (int e = 0; e < m.nelements; e++) {
     for (int ion = 0; ion < 4; ion++) {
       const int ui = uniqueion(m, e, ion);
       const int nl = m.ion_nlevels[ui];
-      for (int lo = 0; lo < nl; lo++) {
-        for (int up = lo + 1; up < nl; up++) {
-          if (U(rng) >= keep) continue;
+      for (int up = 1; up < nl; up++) {
+        for (int lo = 0; lo < up; lo++) {
+          if (!(lo >= up - W || lo < NR)) continue;
           if ((int)lines.size() >= m.cfg.max_lines) continue;
           const double eps_l = m.level_epsilon[uniquelevel(m, e, ion, lo)];
           const double eps_u = m.level_epsilon[uniquelevel(m, e, ion, up)];
@@ -916,14 +916,16 @@ void artis_synth_default_config(artis_synth_config *cfg) {
   std::memset(cfg, 0, sizeof(*cfg));
   cfg->ngrid_1d = 50;
   cfg->nshells_1d = 0;
-  cfg->nlevels_per_ion = 150;
+  cfg->nlevels_per_ion = 400;
   cfg->n_ionising = 56;
   cfg->max_lines = 100000;
+  cfg->line_window = 22;
+  cfg->n_resonance = 5;
   cfg->ntstep = 50;
   cfg->tmin_days = 3.;
   cfg->tmax_days = 30.;
   cfg->vmax = 1.0e9;
-  cfg->mass_msun = 1.0e-3;
+  cfg->mass_msun = 1.0e-4;
   cfg->v_e = 2.7e8;
   cfg->T0 = 1.0e4;
   cfg->n_tclasses = 32;

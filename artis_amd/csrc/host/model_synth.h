@@ -20,6 +20,8 @@ typedef struct artis_synth_config {
   int32_t nlevels_per_ion;   /* levels of each non-top ion */
   int32_t n_ionising;        /* levels with a bf continuum per non-top ion */
   int32_t max_lines;         /* cap on the line count (1e5 for the bench) */
+  int32_t line_window;       /* each level has lines down to this many nearest lower levels ... */
+  int32_t n_resonance;       /* ... and to the lowest n_resonance levels */
   int32_t ntstep;
   double tmin_days, tmax_days;
   double vmax;               /* cm/s */

@@ -104,6 +104,8 @@ class SynthConfig(C.Structure):
         ("nlevels_per_ion", C.c_int32),
         ("n_ionising", C.c_int32),
         ("max_lines", C.c_int32),
+        ("line_window", C.c_int32),
+        ("n_resonance", C.c_int32),
         ("ntstep", C.c_int32),
         ("tmin_days", C.c_double),
         ("tmax_days", C.c_double),

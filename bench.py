@@ -1,0 +1,207 @@
+"""bench.py -- packet-timesteps per second of the MI355X update_packets engine on the synthetic 50^3 grid.
+
+python bench.py --gpus N --steps K --warmup W          (N>1: launched by torch.distributed.run, one rank/GPU)
+
+One step = one update_packets(nts) of this rank's P resident packets, all in HBM before timing starts:
+  packets reset to the same initial ensemble (device-to-device copy), estimators zeroed, the per-timestep cell
+  precompute (artis_gpu_upload_cellstate: cell-state H2D + per-cell table kernels), the transport kernel, and
+  for N>1 the RCCL all-reduce of the packed estimator block (radfield J/nuJ, heating/photoionisation
+  estimators, line statistics, event counters) -- the reference's mpi_reduce_estimators (sn3d.cc:582).
+Packets are sharded: every rank propagates its own full-energy ensemble (rank-specific seed and RNG key), so
+per-GPU work is fixed as N grows ("weak").  value = N * P * K / max-over-ranks wall time.
+
+roofline: algorithmic bytes of the transport kernel (SURVEY.md §8(d) byte model over the engine's own event
+counters) / its average launch time measured with HIP events on the engine stream, against 8.0 TB/s.
+cpu_baseline: the CPU oracle (oracle/liboracle.so, OpenMP) on a bounded sample of the same workload, rank 0
+at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "MC packets/sec/timestep on 50^3 grid; emergent-spectrum L1 vs CPU ref"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+
+
+def byte_model(work, nions_total):
+    """SURVEY.md §8(d) algorithmic bytes from the work counters (include/artis_constants.h enum artis_work)."""
+    w = [float(x) for x in work]
+    return (608.0 * w[0] + 168.0 * w[1] + 64.0 * w[2] + 88.0 * w[5] + 8.0 * nions_total * w[4] + 48.0 * w[6]
+            + 32.0 * w[7] + 72.0 * w[8] + 40.0 * w[9] + 16.0 * w[11])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--packets", type=int, default=4_000_000, help="packets per GPU")
+    ap.add_argument("--ngrid", type=int, default=50)
+    ap.add_argument("--nts", type=int, default=10)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU time of the cpu_baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from artis_amd import Engine
+    from artis_amd.model import Model
+
+    model = Model(ngrid_1d=args.ngrid)
+    nts = args.nts
+    model.set_timestep(nts)
+    params = model.params
+    params.rank = rank
+    P = args.packets
+    packets = model.init_rpackets(nts, P, seed=1000 + rank)
+    eng = Engine(model, device=local_rank, params=params)
+    eng.upload_cellstate(nts)
+    eng.upload(packets)
+    eng.snapshot()
+
+    red = None
+    if world > 1:
+        red = torch.empty(eng.estimator_block_doubles(), dtype=torch.float64, device="cuda")
+
+    transport_ms = []
+    precompute_ms = []
+    work = np.zeros(16, dtype=np.int64)
+
+    def step(record):
+        eng.restore()
+        eng.zero_estimators()
+        eng.upload_cellstate(nts)
+        eng.step_resident(nts, my_rank=rank)
+        if red is not None:
+            eng.estimator_block_to_device(red.data_ptr())
+            dist.all_reduce(red)
+            eng.estimator_block_from_device(red.data_ptr())
+        if record:
+            transport_ms.append(eng.last_transport_ms())
+            precompute_ms.append(eng.last_precompute_ms())
+            work[:] = eng.last_work()
+
+    for _ in range(args.warmup):
+        step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_packet_timesteps = world * P * args.steps
+    value = total_packet_timesteps / elapsed
+    avg_transport_s = float(np.mean(transport_ms)) / 1e3
+    alg_bytes = byte_model(work, model.nions_total)
+    achieved_gbs = alg_bytes / avg_transport_s / 1e9
+    traffic = None
+    prof = os.path.join(REPO, "profiles", "pmc_transport_bytes.json")
+    if os.path.exists(prof):
+        try:
+            pm = json.load(open(prof))
+            if pm.get("packets") == P and pm.get("ngrid") == args.ngrid and pm.get("nts") == nts:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_lib
+
+        nthreads = min(16, os.cpu_count() or 1)
+        calib = packets[:256].copy()
+        t = time.perf_counter()
+        oracle_lib.update_packets(model, nts, calib, nthreads=nthreads)
+        rate = 256 / max(time.perf_counter() - t, 1e-6)
+        n_sample = int(min(P, max(256, rate * args.cpu_seconds)))
+        sample = packets[:n_sample].copy()
+        t = time.perf_counter()
+        oracle_lib.update_packets(model, nts, sample, nthreads=nthreads)
+        cpu_dt = time.perf_counter() - t
+        cpu = {
+            "value": n_sample / cpu_dt,
+            "unit": "packets/s",
+            "cores": nthreads,
+            "kind": "port",
+            "sample": f"first {n_sample} packets of the same ensemble, same timestep, {cpu_dt:.1f} s",
+        }
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "packets/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": (f"synthetic 3D {args.ngrid}^3 uniform-grid model (ARTIS model_type 3), Fe/Co/Ni II-V "
+                             f"{model.nlevels_total} levels, {model.nlines} lines, {model.nbfcontinua} bf continua; "
+                             f"pure r-packet ensemble advanced through timestep {nts} (macro-atom + k-packet "
+                             f"closure, LTE classic options)"),
+                "packets_per_gpu": P,
+                "grid": f"{args.ngrid}^3",
+                "timestep": nts,
+                "parallelism": f"packet-sharded x{world}, RCCL estimator all-reduce" if world > 1 else "1 GPU",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved_gbs,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved_gbs / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "k_transport",
+                "alg_bytes_per_launch": alg_bytes,
+                "avg_launch_ms": avg_transport_s * 1e3,
+            },
+            "cpu_baseline": cpu,
+            "precompute_ms": float(np.mean(precompute_ms)),
+            "work_per_packet": {k: float(v) / max(P, 1) for k, v in zip(
+                ["active", "rpkt_steps", "lines_scanned", "line_taus", "kappa_evals", "bf_active", "est_segments",
+                 "gc_updates", "ma_jumps", "ma_trans", "kpkt", "kpkt_terms", "escaped", "es_scat", "bb_events",
+                 "cont_events"], work)},
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
