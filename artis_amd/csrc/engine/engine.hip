@@ -383,7 +383,7 @@ struct Engine {
   Ctx K{};
   artis_run_params params{};
   // sizes
-  int npts_model = 0, nelements = 0, maxnions = 0, nions_total = 0, nlines = 0, ngrid = 0;
+  int npts_model = 0, nelements = 0, maxnions = 0, nions_total = 0, nlines = 0, ngrid = 0, ntstep = 0;
   int64_t n_est_doubles = 0;  // J..bfheat + scalars
   double *d_estblock = nullptr;
   int32_t *d_target_ul = nullptr, *d_target_t = nullptr;
@@ -658,6 +658,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   GG.tmin = g->tmin;
   GG.rmax = g->rmax;
   GG.wid = 2 * g->coordmax[0] / g->ncoordgrid[0];  // grid.cc:76-91
+  G.ntstep = g->ntstep;
   rc |= dupload(&GG.ts_start, g->ts_start, g->ntstep);
   rc |= dupload(&GG.ts_width, g->ts_width, g->ntstep);
   rc |= dupload(&GG.ts_mid, g->ts_mid, g->ntstep);
@@ -778,7 +779,10 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
 
 int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
   if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
-  if (!cs || nts < 0) return ARTIS_ERR_BAD_ARGUMENT;
+  if (!cs || nts < 0 || nts >= G.ntstep) {
+    G.last_error = "upload_cellstate: bad cell state pointer or timestep out of range";
+    return ARTIS_ERR_BAD_ARGUMENT;
+  }
   const int np = G.npts_model, ne = G.nelements, ni = G.nions_total;
   const float *fsrc[8] = {cs->Te, cs->TR, cs->TJ, cs->W, cs->nne, cs->nnetot, cs->rho, cs->kappagrey};
   for (int f = 0; f < 8; f++)

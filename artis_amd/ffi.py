@@ -18,31 +18,32 @@ TYPE_KPKT = 12
 TYPE_MA = 13
 TYPE_PRE_KPKT = 120
 
-# reference struct packet (packet.h:28-73), 304 bytes
+# reference struct packet (packet.h:28-73), 304 bytes; padding named (as in include/artis_gpu.h) so that
+# the dtype has no gaps and numpy copies are byte-exact
 PACKET_DTYPE = np.dtype(
     {
         "names": [
             "where", "type", "last_cross", "interactions", "nscatterings", "last_event",
             "pos", "dir", "e_cmf", "e_rf", "nu_cmf", "nu_rf", "next_trans", "emissiontype",
-            "em_pos", "em_time", "prop_time", "absorptiontype", "trueemissiontype", "trueem_time",
+            "em_pos", "em_time", "_pad0", "prop_time", "absorptiontype", "trueemissiontype", "trueem_time", "_pad1",
             "absorptionfreq", "absorptiondir", "stokes", "pol_dir", "tdecay", "escape_type",
-            "escape_time", "scat_count", "number", "originated_from_particlenotgamma",
+            "escape_time", "scat_count", "number", "originated_from_particlenotgamma", "_pad2",
             "pellet_decaytype", "pellet_nucindex", "trueemissionvelocity", "mastate",
         ],
         "formats": [
             "<i4", "<i4", "<i4", "<i4", "<i4", "<i4",
             ("<f8", 3), ("<f8", 3), "<f8", "<f8", "<f8", "<f8", "<i4", "<i4",
-            ("<f8", 3), "<i4", "<f8", "<i4", "<i4", "<i4",
+            ("<f8", 3), "<i4", "<i4", "<f8", "<i4", "<i4", "<i4", "<i4",
             "<f8", ("<f8", 3), ("<f8", 3), ("<f8", 3), "<f8", "<i4",
-            "<i4", "<i4", "<i4", "u1",
+            "<i4", "<i4", "<i4", "u1", ("u1", 3),
             "<i4", "<i4", "<f4", ("<i4", 4),
         ],
         "offsets": [
             0, 4, 8, 12, 16, 20,
             24, 48, 72, 80, 88, 96, 104, 108,
-            112, 136, 144, 152, 156, 160,
+            112, 136, 140, 144, 152, 156, 160, 164,
             168, 176, 200, 224, 248, 256,
-            260, 264, 268, 272,
+            260, 264, 268, 272, 273,
             276, 280, 284, 288,
         ],
         "itemsize": 304,

@@ -309,7 +309,7 @@ int artis_gpu_update_packets_resident(int my_rank, int nts);            /* propa
 int artis_gpu_estimators_zero(void);                                    /* zero the device accumulators */
 int artis_gpu_estimators_download(artis_estimators *est);               /* ADD device sums into *est */
 /* Packed device estimator block (doubles then int64 counters) for an RCCL all-reduce done by the caller:
- * copy to / from a caller-owned device buffer of artis_gpu_estimator_block_bytes() bytes. */
+ * copy to / from a caller-owned device buffer of 8 * artis_gpu_estimator_block_doubles bytes. */
 size_t artis_gpu_estimator_block_doubles(void);
 int artis_gpu_estimator_block_to_device(void *dst_device);
 int artis_gpu_estimator_block_from_device(const void *src_device);

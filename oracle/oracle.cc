@@ -2019,4 +2019,31 @@ int oracle_update_packets(const artis_atomic_tables *at, const artis_geometry *g
 
 int oracle_abi_version(void) { return 1; }
 
+// ---- unit hooks for tests/ ---------------------------------------------------------------------------------
+// Philox4x32-10 block (known-answer tests against the published Random123 vectors)
+void oracle_philox4x32_10(uint32_t ctr[4], uint32_t k0, uint32_t k1) { artis_philox4x32_10(ctr, k0, k1); }
+
+// n draws of select_continuum_nu for (element, lowerion, lower, upperionlevel) at T_e
+int oracle_select_continuum_nu_samples(const artis_atomic_tables *at, int element, int lowerion, int lower,
+                                       int upperionlevel, float T_e, int n, uint32_t seed, double *out) {
+  Ctx c;
+  c.at = at;
+  c.g = nullptr;
+  c.cs = nullptr;
+  std::memset(&c.rp, 0, sizeof(c.rp));
+  c.T_step_log = (log(at->maxtemp) - log(at->mintemp)) / (at->tablesize - 1.);
+  for (int i = 0; i < n; i++) {
+    artis_rng rng = artis_rng_init(seed, i, 0, 0);
+    out[i] = select_continuum_nu(c, &rng, element, lowerion, lower, upperionlevel, T_e);
+  }
+  return 0;
+}
+
+// photoionisation cross section lookup (atomic.cc:87-155) for table row `table`
+double oracle_phixs(const artis_atomic_tables *at, int table, double nu_edge, double nu) {
+  Ctx c;
+  c.at = at;
+  return photoionization_crosssection_fromtable(c, at->phixs_xs + (size_t)table * at->nphixspoints, nu_edge, nu);
+}
+
 }  // extern "C"

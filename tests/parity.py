@@ -1,0 +1,85 @@
+"""Packet / estimator comparison helpers shared by the GPU parity tests, the golden tests and smoke().
+
+Integer, enum and index fields of the 304-byte record must be identical.  Floating-point fields are compared
+with a relative tolerance of FP_RTOL: the engine evaluates the same double-precision expressions in the same
+order as the oracle (both built with -ffp-contract=off), but the device libm (exp/log/pow/sqrt of ROCm's ocml)
+and glibc may differ in the last ulp, and a few hundred events per packet compound that to ~1e-14.
+Estimators are float64 sums accumulated with atomics in a schedule-dependent order: ESTIMATOR_RTOL.
+"""
+import numpy as np
+
+FP_RTOL = 1e-9
+ESTIMATOR_RTOL = 1e-9
+
+INT_FIELDS = ["where", "type", "last_cross", "interactions", "nscatterings", "last_event", "next_trans",
+              "emissiontype", "absorptiontype", "trueemissiontype", "escape_type", "scat_count", "number",
+              "originated_from_particlenotgamma", "pellet_decaytype", "pellet_nucindex", "mastate"]
+FP_FIELDS = ["pos", "dir", "e_cmf", "e_rf", "nu_cmf", "nu_rf", "em_pos", "em_time", "prop_time", "trueem_time",
+             "absorptionfreq", "absorptiondir", "stokes", "pol_dir", "tdecay", "escape_time",
+             "trueemissionvelocity"]
+
+
+def discrete_mismatch(a, b):
+    """Boolean mask of packets whose integer/enum/index state differs."""
+    bad = np.zeros(len(a), dtype=bool)
+    for f in INT_FIELDS:
+        x, y = a[f], b[f]
+        if x.dtype.names:  # mastate
+            for sub in x.dtype.names:
+                bad |= x[sub] != y[sub]
+        else:
+            bad |= (x != y).reshape(len(a), -1).any(axis=1)
+    return bad
+
+
+def fp_max_rel(a, b, mask=None):
+    """max over FP fields of |a-b| / max(|b|, tiny) on the packets selected by mask."""
+    out = {}
+    sel = np.ones(len(a), dtype=bool) if mask is None else mask
+    for f in FP_FIELDS:
+        x = a[f][sel].astype(np.float64)
+        y = b[f][sel].astype(np.float64)
+        scale = np.maximum(np.abs(y), 1e-300)
+        d = np.abs(x - y)
+        # vectors: compare against the vector norm (a component can pass through zero)
+        if x.ndim == 2:
+            scale = np.maximum(np.linalg.norm(y, axis=1, keepdims=True), 1e-300)
+        out[f] = float((d / scale).max()) if d.size else 0.0
+    return out
+
+
+def assert_packets_match(gpu, ref, max_discrete_mismatch=0, rtol=FP_RTOL):
+    bad = discrete_mismatch(gpu, ref)
+    assert bad.sum() <= max_discrete_mismatch, f"{int(bad.sum())} of {len(gpu)} packets differ in discrete state"
+    rel = fp_max_rel(gpu, ref, ~bad)
+    worst = max(rel.values()) if rel else 0.0
+    assert worst <= rtol, rel
+    return int(bad.sum()), worst
+
+
+def spectrum(packets, nbins=1000, nu_min=1e14, nu_max=5e15):
+    """Energy of escaped packets binned in log nu_rf (spec.out binning over [NU_MIN_R, NU_MAX_R], spectrum.cc:339-362)."""
+    esc = packets["type"] == 32
+    nu = packets["nu_rf"][esc]
+    e = packets["e_rf"][esc]
+    edges = np.exp(np.linspace(np.log(nu_min), np.log(nu_max), nbins + 1))
+    h, _ = np.histogram(nu, bins=edges, weights=e)
+    return h
+
+
+def spectrum_l1(a, b):
+    sa, sb = spectrum(a), spectrum(b)
+    return float(np.abs(sa - sb).sum() / max(np.abs(sb).sum(), 1e-300))
+
+
+def assert_estimators_match(eg, eo, exact_counts=True, rtol=ESTIMATOR_RTOL):
+    for name in ("J", "nuJ", "ffheating", "colheating", "gamma", "bfheating"):
+        x, y = getattr(eg, name), getattr(eo, name)
+        scale = max(np.abs(y).max(), 1e-300)
+        assert np.abs(x - y).max() <= rtol * scale, (name, np.abs(x - y).max() / scale)
+    assert abs(eg.struct.cmf_lum - eo.struct.cmf_lum) <= rtol * max(abs(eo.struct.cmf_lum), 1e-300)
+    if exact_counts:
+        assert eg.struct.nesc == eo.struct.nesc
+        assert (eg.counters == eo.counters).all(), (eg.counters, eo.counters)
+        assert (eg.ecounter == eo.ecounter).all()
+        assert (eg.acounter == eo.acounter).all()

@@ -1,0 +1,187 @@
+"""HIP engine vs CPU oracle, through the C-ABI (libartis_gpu.so).  Needs an MI355X.
+
+Every packet carries its own counter-based RNG stream (deviation D1), so the engine and the oracle propagate
+the SAME packet histories: integer/enum/index fields are compared exactly, floating-point fields within
+tests/parity.py:FP_RTOL, estimators within ESTIMATOR_RTOL and their event counters exactly.
+
+At the bench size (50^3 grid, ~9.4e4 lines) the oracle cannot run the whole ensemble in seconds, but packets do
+not interact within a timestep, so the oracle re-runs a random subset of the very same packets (same packet
+numbers -> same streams) and those must match the engine's results for them one for one.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib
+import parity
+from artis_amd import Engine, ffi
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def engine_factory():
+    made = []
+
+    def make(model, **kw):
+        e = Engine(model, **kw)
+        made.append(e)
+        return e
+
+    yield make
+    for e in made:
+        e.close()
+
+
+def _pair(model, eng, nts, npkts, seed):
+    model.set_timestep(nts)
+    pk0 = model.init_rpackets(nts, npkts, seed=seed)
+    eng.upload_cellstate(nts)
+    pg = pk0.copy()
+    eg = eng.update_packets(nts, pg)
+    po = pk0.copy()
+    eo, wo = oracle_lib.update_packets(model, nts, po, nthreads=16)
+    return pk0, pg, eg, po, eo, wo
+
+
+def test_grid3d_packets_and_estimators(small_model, engine_factory):
+    eng = engine_factory(small_model)
+    _, pg, eg, po, eo, wo = _pair(small_model, eng, 10, 4000, seed=3)
+    nbad, worst = parity.assert_packets_match(pg, po)
+    parity.assert_estimators_match(eg, eo)
+    # same work on both sides (per-packet histories identical)
+    wg = eng.last_work()
+    assert (wg == wo).all(), (wg, wo)
+    assert parity.spectrum_l1(pg, po) < 1e-9
+
+
+def test_shell_model(shell_model, engine_factory):
+    eng = engine_factory(shell_model)
+    _, pg, eg, po, eo, _ = _pair(shell_model, eng, 6, 3000, seed=4)
+    parity.assert_packets_match(pg, po)
+    parity.assert_estimators_match(eg, eo)
+
+
+def test_multi_timestep_chain(small_model, engine_factory):
+    """Packets carried over three timesteps (cell state re-uploaded each step as update_grid would)."""
+    eng = engine_factory(small_model)
+    small_model.set_timestep(12)
+    pk = small_model.init_rpackets(12, 2000, seed=5)
+    pg, po = pk.copy(), pk.copy()
+    for nts in (12, 13, 14):
+        small_model.set_timestep(nts)
+        eng.upload_cellstate(nts)
+        eg = eng.update_packets(nts, pg)
+        eo, _ = oracle_lib.update_packets(small_model, nts, po, nthreads=16)
+        parity.assert_packets_match(pg, po)
+        parity.assert_estimators_match(eg, eo)
+
+
+def test_without_macroatom_cache_is_identical(small_model, engine_factory, monkeypatch):
+    """The HBM macro-atom cache (binary search over cumulative rates) picks exactly the linear-scan choice."""
+    small_model.set_timestep(9)
+    pk = small_model.init_rpackets(9, 2000, seed=6)
+    eng = engine_factory(small_model)
+    eng.upload_cellstate(9)
+    a = pk.copy()
+    eng.update_packets(9, a)
+    eng.close()
+    monkeypatch.setenv("ARTIS_GPU_NO_MACACHE", "1")
+    eng2 = engine_factory(small_model)
+    eng2.upload_cellstate(9)
+    b = pk.copy()
+    eng2.update_packets(9, b)
+    assert not parity.discrete_mismatch(a, b).any()
+    assert max(parity.fp_max_rel(a, b).values()) <= parity.FP_RTOL
+
+
+def test_resident_path_matches_host_path(small_model, engine_factory):
+    """upload + update_packets_resident + download == update_packets, and snapshot/restore replays exactly."""
+    eng = engine_factory(small_model)
+    small_model.set_timestep(8)
+    pk = small_model.init_rpackets(8, 3000, seed=8)
+    eng.upload_cellstate(8)
+    a = pk.copy()
+    ea = eng.update_packets(8, a)
+    eng.upload(pk)
+    eng.snapshot()
+    outs = []
+    for _ in range(2):
+        eng.restore()
+        eng.zero_estimators()
+        eng.step_resident(8)
+        b = np.zeros_like(pk)
+        eng.download(b)
+        outs.append((b, eng.download_estimators()))
+    for b, eb in outs:
+        assert b.tobytes() == a.tobytes()
+        assert (eb.counters == ea.counters).all()
+        assert np.allclose(eb.J, ea.J, rtol=parity.ESTIMATOR_RTOL, atol=0)
+
+
+def test_edge_cases(small_model, engine_factory):
+    eng = engine_factory(small_model)
+    nts = 7
+    small_model.set_timestep(nts)
+    eng.upload_cellstate(nts)
+    # empty batch
+    empty = np.zeros(0, dtype=ffi.PACKET_DTYPE)
+    e = eng.update_packets(nts, empty)
+    assert e.struct.nesc == 0 and e.J.sum() == 0
+    # escaped packets and packets already at the end of the step are left untouched
+    pk = small_model.init_rpackets(nts, 512, seed=9)
+    pk["type"][::3] = ffi.TYPE_ESCAPE
+    t2 = pk["prop_time"].max()
+    po = pk.copy()
+    oracle_lib.update_packets(small_model, nts, po, nthreads=16)
+    done = po["prop_time"].max()
+    pk["prop_time"][1::3] = done
+    po = pk.copy()
+    pg = pk.copy()
+    eo, _ = oracle_lib.update_packets(small_model, nts, po, nthreads=16)
+    eg = eng.update_packets(nts, pg)
+    assert pg[::3].tobytes() == pk[::3].tobytes()
+    assert pg[1::3].tobytes() == pk[1::3].tobytes()
+    parity.assert_packets_match(pg, po)
+    parity.assert_estimators_match(eg, eo)
+    assert done >= t2
+    # a single packet
+    one = small_model.init_rpackets(nts, 1, seed=10)
+    o1 = one.copy()
+    eng.update_packets(nts, one)
+    oracle_lib.update_packets(small_model, nts, o1, nthreads=1)
+    parity.assert_packets_match(one, o1)
+    # bad arguments fail loudly
+    with pytest.raises(Exception):
+        eng.update_packets(nts + 10**6, pk.copy())
+
+
+def test_bench_size_subset_parity(engine_factory):
+    """Full bench model (50^3 cells, 3 elements x 4 ions x ~300 levels, ~9.4e4 lines): 2e5 packets on the
+    engine; 1500 randomly chosen of them re-run on the oracle must match one for one."""
+    from artis_amd.model import Model
+
+    m = Model()
+    nts = 10
+    m.set_timestep(nts)
+    P = 200_000
+    pk0 = m.init_rpackets(nts, P, seed=11)
+    eng = engine_factory(m)
+    eng.upload_cellstate(nts)
+    pg = pk0.copy()
+    eg = eng.update_packets(nts, pg)
+    rng = np.random.default_rng(0)
+    idx = np.sort(rng.choice(P, size=1500, replace=False))
+    po = pk0[idx].copy()
+    oracle_lib.update_packets(m, nts, po, nthreads=16)
+    parity.assert_packets_match(pg[idx], po, max_discrete_mismatch=1)
+    # size-independent properties of the whole ensemble
+    esc = pg["type"] == ffi.TYPE_ESCAPE
+    assert eg.struct.nesc == esc.sum()
+    assert np.all(pg["prop_time"][~esc] == pg["prop_time"][~esc].max())
+    assert np.isclose(eg.struct.cmf_lum, pg["e_cmf"][esc].sum(), rtol=1e-9)
+    c = eg.counters
+    assert c[0] + c[1] + c[4] + c[5] == c[7] + c[8] + c[9] + c[10]
+    assert c[19] + c[20] + c[7] + c[8] == c[14] + c[15] + c[16] + c[17] + c[18]
+    assert np.allclose(np.linalg.norm(pg["dir"], axis=1), 1.0, atol=1e-10)

@@ -1,0 +1,148 @@
+"""The CPU oracle (test infrastructure): known-answer vectors, invariants and schedule independence.
+
+Parity of the oracle with the reference itself is *unpinned* (the reference needs GSL to build and ships no
+golden vectors usable offline; see DESIGN.md "Oracle").  What is pinned here: the RNG against the published
+Random123 Philox4x32-10 vectors, the select_continuum_nu inversion against the analytic alpha_sp_E
+distribution, conservation/counter identities that hold for the reference algorithm, and bit-identical results
+for any OpenMP schedule (the per-packet stream of deviation D1).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from artis_amd import ffi
+
+# Random123 kat_vectors for philox4x32_10 (counter, key) -> output
+PHILOX_KAT = [
+    ((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+    ((0xFFFFFFFF,) * 4, (0xFFFFFFFF, 0xFFFFFFFF), (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+    ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+     (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)),
+]
+
+
+@pytest.mark.parametrize("ctr,key,expect", PHILOX_KAT)
+def test_philox_known_answers(ctr, key, expect):
+    lib = oracle_lib.lib()
+    a = (C.c_uint32 * 4)(*ctr)
+    lib.oracle_philox4x32_10.argtypes = [C.c_uint32 * 4, C.c_uint32, C.c_uint32]
+    lib.oracle_philox4x32_10(a, key[0], key[1])
+    assert tuple(a) == expect
+
+
+def _run(model, nts, n, seed=5, nthreads=0):
+    model.set_timestep(nts)
+    pk = model.init_rpackets(nts, n, seed=seed)
+    est, work = oracle_lib.update_packets(model, nts, pk, nthreads=nthreads)
+    return pk, est, work
+
+
+def test_schedule_independence_bitwise(small_model):
+    """1 thread and 8 threads give bit-identical packets and estimators (per-packet RNG, deviation D1/D5)."""
+    pk1, e1, _ = _run(small_model, 6, 600, nthreads=1)
+    pk8, e8, _ = _run(small_model, 6, 600, nthreads=8)
+    assert pk1.tobytes() == pk8.tobytes()
+    assert np.allclose(e1.J, e8.J, rtol=1e-12, atol=0)  # atomic summation order differs
+    assert (e1.counters == e8.counters).all()
+
+
+def test_timestep_invariants(small_model):
+    nts = 8
+    pk, est, work = _run(small_model, nts, 1500)
+    # every packet either escaped or sits exactly at the end of the timestep
+    esc = pk["type"] == ffi.TYPE_ESCAPE
+    t2 = pk["prop_time"][~esc]
+    assert np.allclose(t2, t2.max(), rtol=0, atol=0)
+    assert est.struct.nesc == esc.sum()
+    assert np.isclose(est.struct.cmf_lum, pk["e_cmf"][esc].sum(), rtol=1e-12)
+    # surviving packets are r-packets (no k-packet diffusion in this configuration)
+    assert set(np.unique(pk["type"][~esc])) <= {ffi.TYPE_RPKT}
+    # unit directions, Stokes I == 1, |P| <= 1
+    assert np.allclose(np.linalg.norm(pk["dir"], axis=1), 1.0, atol=1e-10)
+    assert np.all(pk["stokes"][:, 0] == 1.0)
+    assert np.all(np.hypot(pk["stokes"][:, 1], pk["stokes"][:, 2]) <= 1.0 + 1e-12)
+    # macro-atom activations == deactivations (every MA ends in do_macroatom, macroatom.cc:465-473)
+    c = est.counters
+    act = c[0] + c[1] + c[4] + c[5]
+    deact = c[7] + c[8] + c[9] + c[10]
+    assert act == deact
+    # k-packets created == k-packets converted (no diffusion delay: do_kpkt converts immediately)
+    kin = c[19] + c[20] + c[7] + c[8]
+    kout = c[14] + c[15] + c[16] + c[17] + c[18]
+    assert kin == kout
+    assert est.J.sum() > 0 and np.all(est.J >= 0)
+    assert work[0] == 1500
+
+
+def test_select_continuum_nu_matches_alpha_sp_distribution(small_model):
+    """D3: the piecewise-Gauss-Legendre inversion samples the alpha_sp_E integrand of ratecoeff.cc:263-279."""
+    lib = oracle_lib.lib()
+    lib.oracle_select_continuum_nu_samples.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float,
+                                                       C.c_int, C.c_uint32, C.c_void_p]
+    lib.oracle_phixs.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double]
+    lib.oracle_phixs.restype = C.c_double
+    at = small_model.atomic
+    # continuum: element 0, ion 1 -> ion 2 ground; read its threshold from the model tables via ctypes
+    hdr = _atomic_arrays(small_model)
+    e, ion, lvl, upper = 0, 1, 0, 0
+    ul = hdr["ion_uniqueleveloffset"][hdr["elem_uniqueionoffset"][e] + ion] + lvl
+    uu = hdr["ion_uniqueleveloffset"][hdr["elem_uniqueionoffset"][e] + ion + 1] + upper
+    eps = hdr["level_epsilon"]
+    nu_th = (eps[uu] - eps[ul]) / 6.6260755e-27
+    table = hdr["level_phixstable"][ul]
+    T = 12000.0
+    n = 20000
+    out = np.zeros(n)
+    lib.oracle_select_continuum_nu_samples(at, e, ion, lvl, upper, T, n, 99, out.ctypes.data)
+    last = 1.0 + 0.1 * 99
+    assert out.min() >= nu_th * (1 - 1e-12) and out.max() <= nu_th * last * (1 + 1e-9)
+    # The reference inverts the tail integral piece by piece and interpolates linearly inside a piece
+    # (ratecoeff.cc:661-681), so the sampled CDF is the exact alpha_sp_E CDF at the piece edges, linear between.
+    npieces = 100
+    edges = nu_th + (nu_th * last - nu_th) / npieces * np.arange(npieces + 1)
+    fine = np.linspace(nu_th, nu_th * last, npieces * 400 + 1)
+    sig = np.array([lib.oracle_phixs(at, int(table), nu_th, x) for x in fine]).astype(np.float32).astype(np.float64)
+    f = sig * fine ** 3 * np.exp(-4.799243681748932e-11 * fine / T)
+    cum = np.concatenate([[0], np.cumsum(0.5 * (f[1:] + f[:-1]) * np.diff(fine))])
+    cdf_edges = cum[::400] / cum[-1]
+    probe = np.linspace(nu_th, nu_th * last, 50001)
+    model_cdf = np.interp(probe, edges, cdf_edges)
+    ks = np.max(np.abs(np.searchsorted(np.sort(out), probe) / n - model_cdf))
+    assert ks < 1.63 / np.sqrt(n) + 0.002, ks  # 99% KS bound + quadrature tolerance
+
+
+def _atomic_arrays(model):
+    """Read a few arrays out of the artis_atomic_tables struct (field order of include/artis_gpu.h)."""
+    class Hdr(C.Structure):
+        _fields_ = [("n", C.c_int32 * 9), ("nphixsnuincrement", C.c_double), ("last", C.c_double),
+                    ("ver", C.c_int32), ("tablesize", C.c_int32), ("mintemp", C.c_double), ("maxtemp", C.c_double),
+                    ("elem_anumber", C.POINTER(C.c_int32)), ("elem_nions", C.POINTER(C.c_int32)),
+                    ("elem_uniqueionoffset", C.POINTER(C.c_int32)), ("ion_ionstage", C.POINTER(C.c_int32)),
+                    ("ion_nlevels", C.POINTER(C.c_int32)), ("ion_uniqueleveloffset", C.POINTER(C.c_int32)),
+                    ("ion_ionisinglevels", C.POINTER(C.c_int32)), ("ion_maxrecombininglevel", C.POINTER(C.c_int32)),
+                    ("ion_coolingoffset", C.POINTER(C.c_int32)), ("ion_ncoolingterms", C.POINTER(C.c_int32)),
+                    ("ion_ionpot", C.POINTER(C.c_double)), ("level_epsilon", C.POINTER(C.c_double)),
+                    ("level_stat_weight", C.POINTER(C.c_float)), ("level_nuptrans", C.POINTER(C.c_int32)),
+                    ("level_uptrans_offset", C.POINTER(C.c_int32)), ("level_ndowntrans", C.POINTER(C.c_int32)),
+                    ("level_downtrans_offset", C.POINTER(C.c_int32)), ("level_nphixstargets", C.POINTER(C.c_int32)),
+                    ("level_phixstargets_offset", C.POINTER(C.c_int32)), ("level_cont_index", C.POINTER(C.c_int32)),
+                    ("level_closestgroundlevelcont", C.POINTER(C.c_int32)),
+                    ("level_phixstable", C.POINTER(C.c_int32))]
+    h = Hdr.from_address(model.atomic)
+    ne, ni, nl = h.n[0], h.n[2], h.n[3]
+    arr = lambda p, k: np.ctypeslib.as_array(p, shape=(k,)).copy()  # noqa: E731
+    return {
+        "elem_uniqueionoffset": arr(h.elem_uniqueionoffset, ne),
+        "ion_uniqueleveloffset": arr(h.ion_uniqueleveloffset, ni),
+        "level_epsilon": arr(h.level_epsilon, nl),
+        "level_phixstable": arr(h.level_phixstable, nl),
+        "level_nuptrans": arr(h.level_nuptrans, nl),
+    }
+
+
+def test_shell_model_runs(shell_model):
+    pk, est, work = _run(shell_model, 5, 800)
+    assert est.struct.nesc == (pk["type"] == ffi.TYPE_ESCAPE).sum()
+    assert work[1] > 0
