@@ -21,7 +21,7 @@ ABI_SYMBOLS = [
     "artis_gpu_packets_restore", "artis_gpu_update_packets_resident", "artis_gpu_estimators_zero",
     "artis_gpu_estimators_download", "artis_gpu_estimator_block_doubles", "artis_gpu_estimator_block_to_device",
     "artis_gpu_estimator_block_from_device", "artis_gpu_last_transport_ms", "artis_gpu_last_precompute_ms",
-    "artis_gpu_last_work_counts", "artis_gpu_last_error", "artis_gpu_abi_version",
+    "artis_gpu_last_work_counts", "artis_gpu_last_rounds", "artis_gpu_last_error", "artis_gpu_abi_version",
 ]
 
 _gpu_lib = None
@@ -49,6 +49,7 @@ def gpu_lib():
         L.artis_gpu_last_precompute_ms.restype = C.c_double
         L.artis_gpu_last_work_counts.argtypes = [vp]
         L.artis_gpu_last_error.restype = C.c_char_p
+        L.artis_gpu_last_rounds.restype = C.c_int64
         _gpu_lib = L
     return _gpu_lib
 
@@ -131,6 +132,9 @@ class Engine:
         w = np.zeros(ffi.ARTIS_WORK_COUNT, dtype=np.int64)
         self.lib.artis_gpu_last_work_counts(w.ctypes.data)
         return w
+
+    def last_rounds(self):
+        return int(self.lib.artis_gpu_last_rounds())
 
     def close(self):
         self.lib.artis_gpu_finalize()

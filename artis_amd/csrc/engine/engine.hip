@@ -25,6 +25,7 @@
 #include "packet_soa.h"
 #include "physics.h"
 #include "transport.h"
+#include "wavefront.h"
 
 // ================================================================================================= kernels
 
@@ -203,10 +204,10 @@ __global__ void k_marates(Ctx K, int nts) {
   const double epsilon_current = K.T.level_epsilon[ul];
   const double statweight = K.T.level_stat_weight[ul];
   const bool cache = K.C.have_macache;
-  double *cum = cache ? K.C.ma_cum + (int64_t)k * K.C.ma_cum_stride : nullptr;
-  double *cum_drad = cum, *cum_dint = cum + K.T.ndown_total, *cum_uint = cum + 2 * K.T.ndown_total;
-  double *cum_rrad = cum + 2 * K.T.ndown_total + K.T.nup_total;
-  double *cum_rint = cum_rrad + K.T.nrecomb_slots;
+  const int4 ml = K.T.ma_level[ul];
+  double *rec = cache ? K.C.ma_rec + (int64_t)k * K.C.ma_rec_stride + ml.x : nullptr;
+  double *cum_drad = rec + 9, *cum_dint = cum_drad + ml.y, *cum_uint = cum_dint + ml.y;
+  double *cum_rrad = cum_uint + ml.z, *cum_rint = cum_rrad + ml.w, *cum_uhi = cum_rint + ml.w;
   double pr[ARTIS_MA_ACTION_COUNT];
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) pr[a] = 0.;
   const int ndowntrans = K.T.level_ndowntrans[ul];
@@ -222,13 +223,12 @@ __global__ void k_marates(Ctx K, int nts) {
     pr[ARTIS_MA_ACTION_COLDEEXC] += C * epsilon_trans;
     pr[ARTIS_MA_ACTION_INTERNALDOWNSAME] += (R + C) * epsilon_target;
     if (cache) {
-      cum_drad[doff + j] = pr[ARTIS_MA_ACTION_RADDEEXC];
-      cum_dint[doff + j] = pr[ARTIS_MA_ACTION_INTERNALDOWNSAME];
+      cum_drad[j] = pr[ARTIS_MA_ACTION_RADDEEXC];
+      cum_dint[j] = pr[ARTIS_MA_ACTION_INTERNALDOWNSAME];
     }
   }
   if (i > 0 && l <= K.T.ion_maxrecombininglevel[ui]) {
     const int nlevels = get_ionisinglevels(K, e, i - 1);
-    const int roff = K.T.level_recomb_offset[ul];
     for (int lower = 0; lower < nlevels; lower++) {
       const double epsilon_target = epsilon(K, e, i - 1, lower);
       const double epsilon_trans = epsilon_current - epsilon_target;
@@ -238,8 +238,8 @@ __global__ void k_marates(Ctx K, int nts) {
       pr[ARTIS_MA_ACTION_RADRECOMB] += R * epsilon_trans;
       pr[ARTIS_MA_ACTION_COLRECOMB] += C * epsilon_trans;
       if (cache) {
-        cum_rrad[roff + lower] = pr[ARTIS_MA_ACTION_RADRECOMB];
-        cum_rint[roff + lower] = pr[ARTIS_MA_ACTION_INTERNALDOWNLOWER];
+        cum_rrad[lower] = pr[ARTIS_MA_ACTION_RADRECOMB];
+        cum_rint[lower] = pr[ARTIS_MA_ACTION_INTERNALDOWNLOWER];
       }
     }
   }
@@ -252,7 +252,7 @@ __global__ void k_marates(Ctx K, int nts) {
     const double R = rad_excitation_ratecoeff(K, pops, mgi, e, i, l, upper, epsilon_trans, li, t_mid);
     const double C = col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, e, i, upper));
     pr[ARTIS_MA_ACTION_INTERNALUPSAME] += (R + C + 0.) * epsilon_current;
-    if (cache) cum_uint[uoff + j] = pr[ARTIS_MA_ACTION_INTERNALUPSAME];
+    if (cache) cum_uint[j] = pr[ARTIS_MA_ACTION_INTERNALUPSAME];
   }
   if (i < K.T.elem_nions[e] - 1 && l < K.T.ion_ionisinglevels[ui]) {
     const int nt = K.T.level_nphixstargets[ul];
@@ -262,9 +262,10 @@ __global__ void k_marates(Ctx K, int nts) {
       const double R = K.C.corrphot[(int64_t)k * K.T.ntargets_total + slot0 + t];
       const double C = col_ionization_ratecoeff(K, T_e, nne, e, i, l, t, epsilon_trans);
       pr[ARTIS_MA_ACTION_INTERNALUPHIGHER] += (R + C) * epsilon_current;
+      if (cache) cum_uhi[t] = pr[ARTIS_MA_ACTION_INTERNALUPHIGHER];
     }
   }
-  double *out = K.C.marates + idx * ARTIS_MA_ACTION_COUNT;
+  double *out = cache ? rec : K.C.marates + idx * ARTIS_MA_ACTION_COUNT;
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) out[a] = pr[a];
 }
 
@@ -385,6 +386,7 @@ struct Engine {
   // sizes
   int npts_model = 0, nelements = 0, maxnions = 0, nions_total = 0, nlines = 0, ngrid = 0, ntstep = 0;
   int64_t n_est_doubles = 0;  // J..bfheat + scalars
+  int64_t ma_rec_stride = 0;
   double *d_estblock = nullptr;
   int32_t *d_target_ul = nullptr, *d_target_t = nullptr;
   bool have_cells = false;
@@ -400,6 +402,13 @@ struct Engine {
   uint64_t *d_soa = nullptr, *d_aos = nullptr, *d_snapshot = nullptr;
   int64_t cap_pkts = 0, npkts = 0;
   bool have_snapshot = false;
+  // wavefront engine (wavefront.h)
+  WaveState W{};
+  uint32_t *h_ctr = nullptr;  // pinned [2][NQUEUES * 2]
+  hipEvent_t ev_round[2] = {nullptr, nullptr};
+  int wave_grid = 2048;
+  bool use_megakernel = false;
+  int64_t last_rounds = 0;
   double last_transport_ms = 0., last_precompute_ms = 0.;
   int64_t last_work[ARTIS_WORK_COUNT] = {0};
   std::string last_error;
@@ -458,9 +467,66 @@ int alloc_packets(int64_t n) {
     G.d_snapshot = nullptr;
     G.have_snapshot = false;
   }
+  if (G.W.rng_n) {
+    (void)hipFree(G.W.rng_n);
+    (void)hipFree(G.W.pend);
+    (void)hipFree(G.W.pend_jumps);
+    for (int q = 0; q < NQUEUES; q++) (void)hipFree(G.W.q[q]);
+  }
   HIPCHK(hipMalloc(&G.d_soa, (size_t)n * PKT_WORDS * 8));
   HIPCHK(hipMalloc(&G.d_aos, (size_t)n * PKT_WORDS * 8));
+  HIPCHK(hipMalloc(&G.W.rng_n, (size_t)n * sizeof(uint32_t)));
+  HIPCHK(hipMalloc(&G.W.pend, (size_t)n * sizeof(int4)));
+  HIPCHK(hipMalloc(&G.W.pend_jumps, (size_t)n * sizeof(uint32_t)));
+  for (int q = 0; q < NQUEUES; q++) HIPCHK(hipMalloc(&G.W.q[q], (size_t)n * sizeof(int32_t)));
   G.cap_pkts = n;
+  return 0;
+}
+
+// Event-queue transport (wavefront.h): classify, then rounds of R -> M -> K kernels until both the R and M
+// queues stay empty.  The host learns the queue sizes one round late (pinned async copies), so it never
+// stalls the stream; a round enqueued after the work ran out finds empty queues and costs only its launches.
+#define WAVE_MAX_ROUNDS 10000000
+int run_wavefront(int64_t n, int nts, double t2) {
+  const WaveState &W = G.W;
+  const unsigned grid = (unsigned)G.wave_grid;
+  HIPCHK(hipMemsetAsync(W.ctr, 0, NQUEUES * 2 * sizeof(uint32_t), G.stream));
+  k_classify<<<(unsigned)((n + WAVE_BLOCK - 1) / WAVE_BLOCK), WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, t2);
+  HIPCHK(hipGetLastError());
+  int64_t round = 0;
+  bool done = false;
+  for (; round < WAVE_MAX_ROUNDS && !done; round++) {
+    k_rpkt<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts, t2);
+    HIPCHK(hipMemsetAsync(W.ctr + 2 * QR, 0, 2 * sizeof(uint32_t), G.stream));
+    if (G.K.C.have_macache)
+      k_ma<true><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts);
+    else
+      k_ma<false><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts);
+    HIPCHK(hipMemsetAsync(W.ctr + 2 * QM, 0, 2 * sizeof(uint32_t), G.stream));
+    k_kpkt<<<grid / 4, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts, t2);
+    HIPCHK(hipMemsetAsync(W.ctr + 2 * QK, 0, 2 * sizeof(uint32_t), G.stream));
+    HIPCHK(hipGetLastError());
+    const int slot = (int)(round & 1);
+    HIPCHK(hipMemcpyAsync(G.h_ctr + slot * NQUEUES * 2, W.ctr, NQUEUES * 2 * sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, G.stream));
+    HIPCHK(hipEventRecord(G.ev_round[slot], G.stream));
+    if (round > 0) {
+      const int prev = (int)((round - 1) & 1);
+      HIPCHK(hipEventSynchronize(G.ev_round[prev]));
+      const uint32_t *c = G.h_ctr + prev * NQUEUES * 2;
+      if (c[2 * QR] == 0 && c[2 * QM] == 0) done = true;
+    }
+  }
+  if (!done) {
+    // the loop hit its cap: check the last round before declaring a stall
+    HIPCHK(hipStreamSynchronize(G.stream));
+    const uint32_t *c = G.h_ctr + ((round - 1) & 1) * NQUEUES * 2;
+    if (c[2 * QR] != 0 || c[2 * QM] != 0) {
+      G.last_error = "wavefront transport did not converge";
+      return ARTIS_ERR_PACKET_FAULT;
+    }
+  }
+  G.last_rounds = round;
   return 0;
 }
 
@@ -473,6 +539,7 @@ int artis_gpu_abi_version(void) { return 1; }
 const char *artis_gpu_last_error(void) { return G.last_error.c_str(); }
 double artis_gpu_last_transport_ms(void) { return G.last_transport_ms; }
 double artis_gpu_last_precompute_ms(void) { return G.last_precompute_ms; }
+int64_t artis_gpu_last_rounds(void) { return G.last_rounds; }
 int artis_gpu_last_work_counts(int64_t out[ARTIS_WORK_COUNT]) {
   for (int k = 0; k < ARTIS_WORK_COUNT; k++) out[k] = G.last_work[k];
   return 0;
@@ -485,6 +552,15 @@ void artis_gpu_finalize(void) {
   if (G.d_soa) (void)hipFree(G.d_soa);
   if (G.d_aos) (void)hipFree(G.d_aos);
   if (G.d_snapshot) (void)hipFree(G.d_snapshot);
+  if (G.W.rng_n) {
+    (void)hipFree(G.W.rng_n);
+    (void)hipFree(G.W.pend);
+    (void)hipFree(G.W.pend_jumps);
+    for (int q = 0; q < NQUEUES; q++) (void)hipFree(G.W.q[q]);
+  }
+  if (G.h_ctr) (void)hipHostFree(G.h_ctr);
+  for (int r = 0; r < 2; r++)
+    if (G.ev_round[r]) (void)hipEventDestroy(G.ev_round[r]);
   if (G.ev0) (void)hipEventDestroy(G.ev0);
   if (G.ev1) (void)hipEventDestroy(G.ev1);
   if (G.ev2) (void)hipEventDestroy(G.ev2);
@@ -509,6 +585,15 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   HIPCHK(hipEventCreate(&G.ev0));
   HIPCHK(hipEventCreate(&G.ev1));
   HIPCHK(hipEventCreate(&G.ev2));
+  for (int r = 0; r < 2; r++) HIPCHK(hipEventCreateWithFlags(&G.ev_round[r], hipEventDisableTiming));
+  HIPCHK(hipHostMalloc((void **)&G.h_ctr, 2 * NQUEUES * 2 * sizeof(uint32_t), hipHostMallocDefault));
+  {
+    int ncu = 256;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+    G.wave_grid = ncu * 8;  // 32 waves per CU of 256-thread blocks; late blocks find the queue drained
+    const char *eng = getenv("ARTIS_GPU_ENGINE");
+    G.use_megakernel = eng && std::string(eng) == "mega";
+  }
   G.params = *rp;
   DevTab &T = G.K.T;
   T.nelements = a->nelements;
@@ -599,21 +684,25 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     lm[li] = {B_ul, B_lu, pow(nu_trans, 3), pow(ARTIS_H_IONPOT / epsilon_trans, 2)};
   }
   rc |= dupload(&T.line_ma, lm.data(), nli);
-  // recombination lists: levels l <= maxrecombininglevel of ions i > 0 (macroatom.cc:104-124)
-  std::vector<int32_t> recoff(nl, -1);
-  int64_t nrec = 0;
+  // macro-atom records per level (engine_dev.h DevCells::ma_rec): recombination targets are the ionising levels
+  // of the lower ion for levels l <= maxrecombininglevel of ions i > 0 (macroatom.cc:104-124); up-higher targets
+  // are the phixs targets of ionising levels of non-top ions (get_nphixstargets)
+  std::vector<int4> mal(nl);
+  int64_t marec = 0;
   for (int e = 0; e < ne; e++)
-    for (int i = 1; i < a->elem_nions[e]; i++) {
+    for (int i = 0; i < a->elem_nions[e]; i++) {
       const int ui = a->elem_uniqueionoffset[e] + i;
-      for (int l = 0; l < a->ion_nlevels[ui] && l <= a->ion_maxrecombininglevel[ui]; l++) {
-        recoff[a->ion_uniqueleveloffset[ui] + l] = (int32_t)nrec;
-        nrec += a->ion_ionisinglevels[ui - 1];
+      for (int l = 0; l < a->ion_nlevels[ui]; l++) {
+        const int ul = a->ion_uniqueleveloffset[ui] + l;
+        const int nrec = (i > 0 && l <= a->ion_maxrecombininglevel[ui]) ? a->ion_ionisinglevels[ui - 1] : 0;
+        const int nt = (i < a->elem_nions[e] - 1 && l < a->ion_ionisinglevels[ui]) ? a->level_nphixstargets[ul] : 0;
+        const int64_t len = 9 + 2 * (int64_t)a->level_ndowntrans[ul] + a->level_nuptrans[ul] + 2 * nrec + nt;
+        mal[ul] = make_int4((int)marec, a->level_ndowntrans[ul], a->level_nuptrans[ul], nrec);
+        marec += (len + 15) / 16 * 16;  // 128-byte aligned records: the 9 totals share one cache line
       }
     }
-  rc |= dupload(&T.level_recomb_offset, recoff.data(), nl);
-  T.ndown_total = ndown;
-  T.nup_total = nup;
-  T.nrecomb_slots = nrec;
+  rc |= dupload(&T.ma_level, mal.data(), nl);
+  G.ma_rec_stride = marec;
   rc |= dupload(&T.allcont_nu_edge, a->allcont_nu_edge, nb);
   rc |= dupload(&T.allcont_probability, a->allcont_probability, nb);
   rc |= dupload(&T.allcont_element, a->allcont_element, nb);
@@ -730,25 +819,27 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   rc |= dalloc(&C.depratio, (size_t)nne_cells * nb);
   rc |= dalloc(&C.corrphot, (size_t)nne_cells * (ntg + 1));
   rc |= dalloc(&C.cooling, (size_t)nne_cells * a->ncoolingterms);
-  rc |= dalloc(&C.marates, (size_t)nne_cells * nl * ARTIS_MA_ACTION_COUNT);
-  C.ma_cum_stride = 2 * ndown + nup + 2 * nrec;
+  C.ma_rec_stride = G.ma_rec_stride;
   C.have_macache = 0;
-  C.ma_cum = nullptr;
+  C.ma_rec = nullptr;
+  C.marates = nullptr;
   {
     size_t freeb = 0, totalb = 0;
     (void)hipMemGetInfo(&freeb, &totalb);
-    const double need = (double)nne_cells * (double)C.ma_cum_stride * 8.0;
+    const double need = (double)nne_cells * (double)C.ma_rec_stride * 8.0;
     const char *env = getenv("ARTIS_GPU_NO_MACACHE");
     if (!(env && env[0] == '1') && need < 0.75 * (double)freeb) {
       double *mc = nullptr;
       if (hipMalloc((void **)&mc, (size_t)need) == hipSuccess) {
         G.allocs.push_back(mc);
-        C.ma_cum = mc;
+        C.ma_rec = mc;
         C.have_macache = 1;
       }
     }
   }
+  if (!C.have_macache) rc |= dalloc(&C.marates, (size_t)nne_cells * nl * ARTIS_MA_ACTION_COUNT);
   // cell-state input buffers
+  rc |= dalloc(&G.W.ctr, (size_t)NQUEUES * 2);
   rc |= dalloc(&G.d_cellf, (size_t)8 * np);
   rc |= dalloc(&G.d_thick, (size_t)np);
   rc |= dalloc(&G.d_abund, (size_t)np * ne);
@@ -888,10 +979,13 @@ int artis_gpu_update_packets_resident(int my_rank, int nts) {
   HIPCHK(hipMemsetAsync(G.K.E.work, 0, ARTIS_WORK_COUNT * sizeof(unsigned long long), G.stream));
   const int64_t n = G.npkts;
   HIPCHK(hipEventRecord(G.ev0, G.stream));
-  if (n > 0) {
+  G.last_rounds = 0;
+  if (n > 0 && G.use_megakernel) {
     k_transport<<<(unsigned)((n + TRANSPORT_BLOCK - 1) / TRANSPORT_BLOCK), TRANSPORT_BLOCK, 0, G.stream>>>(
         G.K, G.d_soa, n, nts, t2);
     HIPCHK(hipGetLastError());
+  } else if (n > 0) {
+    if (int rc = run_wavefront(n, nts, t2)) return rc;
   }
   HIPCHK(hipEventRecord(G.ev1, G.stream));
   HIPCHK(hipEventSynchronize(G.ev1));

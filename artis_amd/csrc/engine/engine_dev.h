@@ -54,8 +54,9 @@ struct DevTab {
   const uint8_t *line_forbidden;
   const LineTau *line_tau;
   const LineMA *line_ma;
-  const int32_t *level_recomb_offset;  // slot of the (level -> lower-ion levels) recombination list, -1 if none
-  int64_t ndown_total, nup_total, nrecomb_slots;
+  // per level: offset (doubles) of its macro-atom record inside a cell's record block, #downtrans, #uptrans,
+  // #recombination targets (ionising levels of the lower ion, 0 if the level does not recombine)
+  const int4 *ma_level;
   const double *allcont_nu_edge, *allcont_probability;
   const int32_t *allcont_element, *allcont_ion, *allcont_level, *allcont_target, *allcont_upperlevel,
       *allcont_phixstable, *allcont_groundindex;
@@ -89,14 +90,16 @@ struct DevCells {
   double *depratio;    // [n_nonempty * nbf]            departure ratios (rpkt.cc:1140-1151)
   double *corrphot;    // [n_nonempty * ntargets_total] get_corrphotoioncoeff (ratecoeff.cc:1247-1308)
   double *cooling;     // [n_nonempty * ncoolingterms]  cumulative cooling_contrib (kpkt.cc:167-308)
-  double *marates;     // [n_nonempty * nlevels_total * 9] processrates (macroatom.cc:57-159)
-  // cumulative individual macro-atom rates per cell (the cellhistory individ_* arrays, globals.h:174-183),
-  // summed in the reference's order so that a binary search returns the reference's linear-scan choice:
-  // [rad_deexc over downtrans | internal_down_same over downtrans | internal_up_same over uptrans |
-  //  rad_recomb over recombination lists | internal_down_lower over recombination lists]
-  double *ma_cum;      // [n_nonempty * ma_cum_stride]
-  int64_t ma_cum_stride;
+  // macro-atom cache: per (cell, level) one contiguous record, 128-byte aligned, holding the processrates
+  // totals (macroatom.cc:57-159) and the running sums of the individual rates (the cellhistory individ_*
+  // arrays, globals.h:174-183) summed in the reference's order, so that a binary search returns the
+  // reference's linear-scan choice:
+  //   [9 totals | rad_deexc (ndown) | internal_down_same (ndown) | internal_up_same (nup) |
+  //    rad_recomb (nrec) | internal_down_lower (nrec) | internal_up_higher (nphixstargets)]
+  double *ma_rec;      // [n_nonempty * ma_rec_stride], or nullptr
+  int64_t ma_rec_stride;
   int32_t have_macache;
+  double *marates;     // without the cache: [n_nonempty * nlevels_total * 9] totals only
 };
 
 struct DevEst {

@@ -841,261 +841,242 @@ DEVFN int first_above(const double *cum, int n, double x, unsigned long long &pr
   }
   return lo;
 }
-// macroatom.cc:416-482 (process-rate totals from the per-cell table; individual rates recomputed while selecting)
-DEVNI void do_macroatom(Tx &x, Pkt &p) {
-  const Ctx &K = x.K;
-  const double t_mid = K.G.ts_mid[x.nts];
-  const int mgi = cell_mgi(K, p.where);
-  const int k = K.C.ne_index[mgi];
-  const float T_e = K.C.Te[mgi];
-  const float nne = K.C.nne[mgi];
-  const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
-  const double *macum = K.C.have_macache ? K.C.ma_cum + (int64_t)k * K.C.ma_cum_stride : nullptr;
-  if (K.C.thick[mgi] == 1) {
-    x.err(ERR_THICK_MA, p.number, mgi);
-    return;
+// One macro-atom is walked jump by jump (ma_jump) and its deactivation applied to the packet afterwards
+// (ma_finish).  The megakernel calls both back to back (do_macroatom); the wavefront engine runs the walk in a
+// lean kernel that never loads the 304-byte record and defers ma_finish to the kernel the packet moves to.
+struct MaLane {
+  int element, ion, level;
+  int k, mgi;
+  float T_e, nne;
+  unsigned jumps;
+  unsigned long long ntrans;
+};
+enum { MA_CONTINUE = 0, MA_END_BB = 1, MA_END_COLDEEXC = 2, MA_END_COLRECOMB = 3, MA_END_FB = 4, MA_FAILED = -1 };
+struct MaEnd {
+  int code, ion, a, b;  // BB: a = line, b = level; FB: ion = lower ion, a = lower level, b = upper-ion level
+};
+
+// macroatom.cc:416-482, one pass of the do_macroatom loop: select a process from the per-cell totals, then the
+// transition from the cumulative individual rates (CACHE: binary search in the level's record) or by
+// recomputing the individual rates in the reference's order (no cache)
+template <bool CACHE>
+DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &m, double t_mid, MaEnd &end,
+                  int number) {
+  m.jumps++;
+  const int element = m.element, ion = m.ion, level = m.level, k = m.k;
+  const double epsilon_current = epsilon(K, element, ion, level);
+  const int ul = ulev(K, element, ion, level);
+  int4 ml = make_int4(0, 0, 0, 0);
+  const double *rec = nullptr, *pr;
+  if constexpr (CACHE) {
+    ml = K.T.ma_level[ul];
+    rec = K.C.ma_rec + (int64_t)k * K.C.ma_rec_stride + ml.x;
+    pr = rec;
+  } else {
+    pr = K.C.marates + ((int64_t)k * K.T.nlevels_total + ul) * ARTIS_MA_ACTION_COUNT;
   }
-  const int element = p.ma_element;
-  int ion = p.ma_ion;
-  int level = p.ma_level;
-  const int activatingline = p.ma_activatingline;
-  bool end_packet = false;
-  unsigned long long jumps = 0, ntrans = 0;
-  while (!end_packet) {
-    jumps++;
-    if (jumps > 10000000ull) {
-      x.err(ERR_STUCK, p.number, 2);
+  const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
+  double processrates[ARTIS_MA_ACTION_COUNT];
+  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) processrates[a] = pr[a];
+  double total_transitions = 0.;
+  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) total_transitions += processrates[a];
+  int selected_action = ARTIS_MA_ACTION_COUNT;
+  const double zrand = artis_rng_uniform(&rng);
+  const double randomrate = zrand * total_transitions;
+  double rate = 0.;
+  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
+    rate += processrates[a];
+    if (rate > randomrate) {
+      selected_action = a;
       break;
     }
-    const double epsilon_current = epsilon(K, element, ion, level);
-    const int ul = ulev(K, element, ion, level);
-    const double *pr = K.C.marates + ((int64_t)k * K.T.nlevels_total + ul) * ARTIS_MA_ACTION_COUNT;
-    double processrates[ARTIS_MA_ACTION_COUNT];
-    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) processrates[a] = pr[a];
-    double total_transitions = 0.;
-    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) total_transitions += processrates[a];
-    int selected_action = ARTIS_MA_ACTION_COUNT;
-    const double zrand = artis_rng_uniform(&x.rng);
-    const double randomrate = zrand * total_transitions;
-    double rate = 0.;
-    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
-      rate += processrates[a];
-      if (rate > randomrate) {
-        selected_action = a;
-        break;
+  }
+  if (rate <= randomrate) {
+    fail(K, ERR_MA_RANDOM, number, ul);
+    return MA_FAILED;
+  }
+  const float T_e = m.T_e, nne = m.nne;
+  if (selected_action == ARTIS_MA_ACTION_RADDEEXC) {
+    // macroatom.cc:222-296
+    const double zr = artis_rng_uniform(&rng);
+    int linelistindex = -99;
+    const int ndowntrans = K.T.level_ndowntrans[ul];
+    const int doff = K.T.level_downtrans_offset[ul];
+    if constexpr (CACHE) {
+      const int j = first_above(rec + 9, ndowntrans, zr * processrates[ARTIS_MA_ACTION_RADDEEXC], m.ntrans);
+      if (j < ndowntrans) linelistindex = K.T.downtrans_lineindex[doff + j];
+    } else {
+      double r = 0.;
+      for (int j = 0; j < ndowntrans; j++) {
+        const int li = K.T.downtrans_lineindex[doff + j];
+        const int lower = K.T.line_lower[li];
+        const double epsilon_trans = epsilon_current - epsilon(K, element, ion, lower);
+        const double R = rad_deexcitation_ratecoeff(K, pops, element, ion, level, lower, epsilon_trans, li, t_mid);
+        r += R * epsilon_trans;
+        m.ntrans++;
+        if (zr * processrates[ARTIS_MA_ACTION_RADDEEXC] < r) {
+          linelistindex = li;
+          break;
+        }
       }
     }
-    if (rate <= randomrate) {
-      x.err(ERR_MA_RANDOM, p.number, ul);
-      break;
+    if (linelistindex < 0) {
+      fail(K, ERR_MA_SELECT, number, 1);
+      return MA_FAILED;
     }
-    if (selected_action == ARTIS_MA_ACTION_RADDEEXC) {
-      // macroatom.cc:222-296
-      const double zr = artis_rng_uniform(&x.rng);
-      double r = 0.;
-      int linelistindex = -99;
-      const int ndowntrans = K.T.level_ndowntrans[ul];
-      const int doff = K.T.level_downtrans_offset[ul];
-      if (macum) {
-        const int j = first_above(macum + doff, ndowntrans, zr * processrates[ARTIS_MA_ACTION_RADDEEXC], ntrans);
-        if (j < ndowntrans) linelistindex = K.T.downtrans_lineindex[doff + j];
-      } else {
-        for (int j = 0; j < ndowntrans; j++) {
-          const int li = K.T.downtrans_lineindex[doff + j];
-          const int lower = K.T.line_lower[li];
-          const double epsilon_trans = epsilon_current - epsilon(K, element, ion, lower);
-          const double R = rad_deexcitation_ratecoeff(K, pops, element, ion, level, lower, epsilon_trans, li, t_mid);
-          r += R * epsilon_trans;
-          ntrans++;
-          if (zr * processrates[ARTIS_MA_ACTION_RADDEEXC] < r) {
-            linelistindex = li;
-            break;
-          }
-        }
-      }
-      if (linelistindex < 0) {
-        x.err(ERR_MA_SELECT, p.number, 1);
-        break;
-      }
-      if (K.R.record_linestat) atomicAdd(&K.E.ecounter[linelistindex], 1);
-      const int lower = K.T.line_lower[linelistindex];
-      const double epsilon_trans = epsilon(K, element, ion, level) - epsilon(K, element, ion, lower);
-      double oldnucmf = 0.;
-      if (p.last_event == 1) oldnucmf = p.nu_cmf;
-      p.nu_cmf = epsilon_trans / ARTIS_H;
-      if (p.last_event == 1) lctr(x.L, (oldnucmf < p.nu_cmf) ? CTR_UPSCATTER : CTR_DOWNSCATTER);
-      lctr(x.L, CTR_MA_STAT_DEACTIVATION_BB);
-      p.interactions += 1;
-      p.last_event = 0;
-      emitt_rpkt(x, p);
-      if (linelistindex == activatingline) lctr(x.L, CTR_RESONANCESCATTERINGS);
-      p.next_trans = linelistindex + 1;
-      p.emissiontype = linelistindex;
-      p.em_pos[0] = p.pos[0];
-      p.em_pos[1] = p.pos[1];
-      p.em_pos[2] = p.pos[2];
-      p.em_time = (int)p.prop_time;
-      p.nscatterings = 0;
-      end_packet = true;
-    } else if (selected_action == ARTIS_MA_ACTION_COLDEEXC || selected_action == ARTIS_MA_ACTION_COLRECOMB) {
-      const bool deexc = selected_action == ARTIS_MA_ACTION_COLDEEXC;
-      lctr(x.L, deexc ? CTR_MA_STAT_DEACTIVATION_COLLDEEXC : CTR_MA_STAT_DEACTIVATION_COLLRECOMB);
-      p.interactions += 1;
-      p.last_event = deexc ? 10 : 11;
-      p.type = ARTIS_TYPE_KPKT;
-      end_packet = true;
-      safeadd(&K.E.colheat[mgi], p.e_cmf);
-    } else if (selected_action == ARTIS_MA_ACTION_INTERNALDOWNSAME) {
-      // macroatom.cc:174-220
-      p.interactions += 1;
-      const double zr = artis_rng_uniform(&x.rng);
-      int lower = -99;
-      double r = 0.;
-      const int ndowntrans = K.T.level_ndowntrans[ul];
-      const int doff = K.T.level_downtrans_offset[ul];
+    end.code = MA_END_BB;
+    end.ion = ion;
+    end.a = linelistindex;
+    end.b = level;
+    return MA_END_BB;
+  }
+  if (selected_action == ARTIS_MA_ACTION_COLDEEXC || selected_action == ARTIS_MA_ACTION_COLRECOMB) {
+    end.code = (selected_action == ARTIS_MA_ACTION_COLDEEXC) ? MA_END_COLDEEXC : MA_END_COLRECOMB;
+    end.ion = ion;
+    end.a = end.b = 0;
+    return end.code;
+  }
+  if (selected_action == ARTIS_MA_ACTION_INTERNALDOWNSAME) {
+    // macroatom.cc:174-220
+    const double zr = artis_rng_uniform(&rng);
+    int lower = -99;
+    const int ndowntrans = K.T.level_ndowntrans[ul];
+    const int doff = K.T.level_downtrans_offset[ul];
+    if constexpr (CACHE) {
+      const int j = first_above(rec + 9 + ml.y, ndowntrans, zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNSAME],
+                                m.ntrans);
+      if (j < ndowntrans) lower = K.T.line_lower[K.T.downtrans_lineindex[doff + j]];
+    } else {
       const double statweight = stat_weight(K, element, ion, level);
-      if (macum) {
-        const int j = first_above(macum + K.T.ndown_total + doff, ndowntrans,
-                                  zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNSAME], ntrans);
-        if (j < ndowntrans) lower = K.T.line_lower[K.T.downtrans_lineindex[doff + j]];
-      } else {
-        for (int j = 0; j < ndowntrans; j++) {
-          const int li = K.T.downtrans_lineindex[doff + j];
-          const int lo = K.T.line_lower[li];
-          const double epsilon_target = epsilon(K, element, ion, lo);
-          const double epsilon_trans = epsilon_current - epsilon_target;
-          const double R = rad_deexcitation_ratecoeff(K, pops, element, ion, level, lo, epsilon_trans, li, t_mid);
-          const double C =
-              col_deexcitation_ratecoeff(K, T_e, nne, epsilon_trans, li, stat_weight(K, element, ion, lo), statweight);
-          r += (R + C) * epsilon_target;
-          ntrans++;
-          if (zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNSAME] < r) {
-            lower = lo;
-            break;
-          }
-        }
-      }
-      if (lower < 0) {
-        x.err(ERR_MA_SELECT, p.number, 4);
-        break;
-      }
-      level = lower;
-    } else if (selected_action == ARTIS_MA_ACTION_RADRECOMB) {
-      // macroatom.cc:298-380
-      const int upperion = ion;
-      const int upperionlevel = level;
-      const double zr = artis_rng_uniform(&x.rng);
-      double r = 0;
-      const int nlevels = get_ionisinglevels(K, element, upperion - 1);
-      int lower = 0;
-      if (macum) {
-        lower = first_above(macum + 2 * K.T.ndown_total + K.T.nup_total + K.T.level_recomb_offset[ul], nlevels,
-                            zr * processrates[ARTIS_MA_ACTION_RADRECOMB], ntrans);
-        r = (lower < nlevels) ? DBL_MAX : -DBL_MAX;
-      } else {
-        for (lower = 0; lower < nlevels; lower++) {
-          const double epsilon_trans = epsilon_current - epsilon(K, element, upperion - 1, lower);
-          const double R = rad_recombination_ratecoeff(K, T_e, nne, element, upperion, upperionlevel, lower);
-          r += R * epsilon_trans;
-          if (zr * processrates[ARTIS_MA_ACTION_RADRECOMB] < r) break;
-        }
-        ntrans += lower + 1;
-      }
-      if (zr * processrates[ARTIS_MA_ACTION_RADRECOMB] >= r) {
-        x.err(ERR_MA_SELECT, p.number, 2);
-        break;
-      }
-      ion = upperion - 1;
-      level = lower;
-      p.nu_cmf = select_continuum_nu(x, element, upperion - 1, lower, upperionlevel, T_e);
-      lctr(x.L, CTR_MA_STAT_DEACTIVATION_FB);
-      p.interactions += 1;
-      p.last_event = 2;
-      emitt_rpkt(x, p);
-      p.next_trans = 0;
-      {  // get_continuumindex (atomic.cc:16-30)
-        int target = 0;
-        for (int t = 0; t < get_nphixstargets(K, element, ion, lower); t++)
-          if (get_phixsupperlevel(K, element, ion, lower, t) == upperionlevel) {
-            target = t;
-            break;
-          }
-        p.emissiontype = K.T.level_cont_index[ulev(K, element, ion, lower)] - target;
-      }
-      p.em_pos[0] = p.pos[0];
-      p.em_pos[1] = p.pos[1];
-      p.em_pos[2] = p.pos[2];
-      p.em_time = (int)p.prop_time;
-      p.nscatterings = 0;
-      end_packet = true;
-    } else if (selected_action == ARTIS_MA_ACTION_INTERNALDOWNLOWER) {
-      p.interactions += 1;
-      lctr(x.L, CTR_MA_STAT_INTERNALDOWNLOWER);
-      const double zr = artis_rng_uniform(&x.rng);
       double r = 0.;
-      const int nlevels = get_ionisinglevels(K, element, ion - 1);
-      int lower;
-      if (macum) {
-        lower = first_above(macum + 2 * K.T.ndown_total + K.T.nup_total + K.T.nrecomb_slots + K.T.level_recomb_offset[ul],
-                            nlevels, zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNLOWER], ntrans);
-      } else {
-        for (lower = 0; lower < nlevels; lower++) {
-          const double epsilon_target = epsilon(K, element, ion - 1, lower);
-          const double epsilon_trans = epsilon_current - epsilon_target;
-          const double R = rad_recombination_ratecoeff(K, T_e, nne, element, ion, level, lower);
-          const double C = col_recombination_ratecoeff(K, mgi, element, ion, level, lower, epsilon_trans);
-          r += (R + C) * epsilon_target;
-          if (zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNLOWER] < r) break;
+      for (int j = 0; j < ndowntrans; j++) {
+        const int li = K.T.downtrans_lineindex[doff + j];
+        const int lo = K.T.line_lower[li];
+        const double epsilon_target = epsilon(K, element, ion, lo);
+        const double epsilon_trans = epsilon_current - epsilon_target;
+        const double R = rad_deexcitation_ratecoeff(K, pops, element, ion, level, lo, epsilon_trans, li, t_mid);
+        const double C =
+            col_deexcitation_ratecoeff(K, T_e, nne, epsilon_trans, li, stat_weight(K, element, ion, lo), statweight);
+        r += (R + C) * epsilon_target;
+        m.ntrans++;
+        if (zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNSAME] < r) {
+          lower = lo;
+          break;
         }
-        ntrans += lower + 1;
       }
-      if (lower >= nlevels) {
-        x.err(ERR_MA_SELECT, p.number, 5);
-        break;
+    }
+    if (lower < 0) {
+      fail(K, ERR_MA_SELECT, number, 4);
+      return MA_FAILED;
+    }
+    m.level = lower;
+    return MA_CONTINUE;
+  }
+  if (selected_action == ARTIS_MA_ACTION_RADRECOMB) {
+    // macroatom.cc:298-380 (the frequency draw and emission happen in ma_finish)
+    const int upperion = ion;
+    const double zr = artis_rng_uniform(&rng);
+    double r = 0;
+    const int nlevels = get_ionisinglevels(K, element, upperion - 1);
+    int lower = 0;
+    if constexpr (CACHE) {
+      lower = first_above(rec + 9 + 2 * ml.y + ml.z, nlevels, zr * processrates[ARTIS_MA_ACTION_RADRECOMB], m.ntrans);
+      r = (lower < nlevels) ? DBL_MAX : -DBL_MAX;
+    } else {
+      for (lower = 0; lower < nlevels; lower++) {
+        const double epsilon_trans = epsilon_current - epsilon(K, element, upperion - 1, lower);
+        const double R = rad_recombination_ratecoeff(K, T_e, nne, element, upperion, level, lower);
+        r += R * epsilon_trans;
+        if (zr * processrates[ARTIS_MA_ACTION_RADRECOMB] < r) break;
       }
-      ion -= 1;
-      level = lower;
-    } else if (selected_action == ARTIS_MA_ACTION_INTERNALUPSAME) {
-      p.interactions += 1;
-      const double zr = artis_rng_uniform(&x.rng);
-      int upper = -99;
+      m.ntrans += lower + 1;
+    }
+    if (zr * processrates[ARTIS_MA_ACTION_RADRECOMB] >= r) {
+      fail(K, ERR_MA_SELECT, number, 2);
+      return MA_FAILED;
+    }
+    end.code = MA_END_FB;
+    end.ion = upperion - 1;
+    end.a = lower;
+    end.b = level;
+    return MA_END_FB;
+  }
+  if (selected_action == ARTIS_MA_ACTION_INTERNALDOWNLOWER) {
+    lctr(L, CTR_MA_STAT_INTERNALDOWNLOWER);
+    const double zr = artis_rng_uniform(&rng);
+    const int nlevels = get_ionisinglevels(K, element, ion - 1);
+    int lower;
+    if constexpr (CACHE) {
+      lower = first_above(rec + 9 + 2 * ml.y + ml.z + ml.w, nlevels, zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNLOWER],
+                          m.ntrans);
+    } else {
       double r = 0.;
-      const int nuptrans = K.T.level_nuptrans[ul];
-      const int uoff = K.T.level_uptrans_offset[ul];
+      for (lower = 0; lower < nlevels; lower++) {
+        const double epsilon_target = epsilon(K, element, ion - 1, lower);
+        const double epsilon_trans = epsilon_current - epsilon_target;
+        const double R = rad_recombination_ratecoeff(K, T_e, nne, element, ion, level, lower);
+        const double C = col_recombination_ratecoeff(K, m.mgi, element, ion, level, lower, epsilon_trans);
+        r += (R + C) * epsilon_target;
+        if (zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNLOWER] < r) break;
+      }
+      m.ntrans += lower + 1;
+    }
+    if (lower >= nlevels) {
+      fail(K, ERR_MA_SELECT, number, 5);
+      return MA_FAILED;
+    }
+    m.ion = ion - 1;
+    m.level = lower;
+    return MA_CONTINUE;
+  }
+  if (selected_action == ARTIS_MA_ACTION_INTERNALUPSAME) {
+    const double zr = artis_rng_uniform(&rng);
+    int upper = -99;
+    const int nuptrans = K.T.level_nuptrans[ul];
+    const int uoff = K.T.level_uptrans_offset[ul];
+    if constexpr (CACHE) {
+      const int j = first_above(rec + 9 + 2 * ml.y, nuptrans, zr * processrates[ARTIS_MA_ACTION_INTERNALUPSAME],
+                                m.ntrans);
+      if (j < nuptrans) upper = K.T.line_upper[K.T.uptrans_lineindex[uoff + j]];
+    } else {
       const double statweight = stat_weight(K, element, ion, level);
-      if (macum) {
-        const int j = first_above(macum + 2 * K.T.ndown_total + uoff, nuptrans,
-                                  zr * processrates[ARTIS_MA_ACTION_INTERNALUPSAME], ntrans);
-        if (j < nuptrans) upper = K.T.line_upper[K.T.uptrans_lineindex[uoff + j]];
-      } else {
-        for (int j = 0; j < nuptrans; j++) {
-          const int li = K.T.uptrans_lineindex[uoff + j];
-          const int up = K.T.line_upper[li];
-          const double epsilon_trans = epsilon(K, element, ion, up) - epsilon_current;
-          const double R = rad_excitation_ratecoeff(K, pops, mgi, element, ion, level, up, epsilon_trans, li, t_mid);
-          const double C =
-              col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, element, ion, up));
-          r += (R + C + 0.) * epsilon_current;
-          ntrans++;
-          if (zr * processrates[ARTIS_MA_ACTION_INTERNALUPSAME] < r) {
-            upper = up;
-            break;
-          }
+      double r = 0.;
+      for (int j = 0; j < nuptrans; j++) {
+        const int li = K.T.uptrans_lineindex[uoff + j];
+        const int up = K.T.line_upper[li];
+        const double epsilon_trans = epsilon(K, element, ion, up) - epsilon_current;
+        const double R = rad_excitation_ratecoeff(K, pops, m.mgi, element, ion, level, up, epsilon_trans, li, t_mid);
+        const double C =
+            col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, element, ion, up));
+        r += (R + C + 0.) * epsilon_current;
+        m.ntrans++;
+        if (zr * processrates[ARTIS_MA_ACTION_INTERNALUPSAME] < r) {
+          upper = up;
+          break;
         }
       }
-      if (upper < 0) {
-        x.err(ERR_MA_SELECT, p.number, 6);
-        break;
-      }
-      level = upper;
-    } else if (selected_action == ARTIS_MA_ACTION_INTERNALUPHIGHER) {
-      // macroatom.cc:382-414
-      p.interactions += 1;
-      lctr(x.L, CTR_MA_STAT_INTERNALUPHIGHER);
-      int upper = -1;
-      const double zr = artis_rng_uniform(&x.rng);
+    }
+    if (upper < 0) {
+      fail(K, ERR_MA_SELECT, number, 6);
+      return MA_FAILED;
+    }
+    m.level = upper;
+    return MA_CONTINUE;
+  }
+  if (selected_action == ARTIS_MA_ACTION_INTERNALUPHIGHER) {
+    // macroatom.cc:382-414
+    lctr(L, CTR_MA_STAT_INTERNALUPHIGHER);
+    int upper = -1;
+    const double zr = artis_rng_uniform(&rng);
+    const int nt = get_nphixstargets(K, element, ion, level);
+    bool found;
+    if constexpr (CACHE) {
+      const int t = first_above(rec + 9 + 2 * ml.y + ml.z + 2 * ml.w, nt,
+                                zr * processrates[ARTIS_MA_ACTION_INTERNALUPHIGHER], m.ntrans);
+      found = t < nt;
+      if (found) upper = get_phixsupperlevel(K, element, ion, level, t);
+    } else {
       double r = 0.;
-      const int nt = get_nphixstargets(K, element, ion, level);
       const int slot0 = K.T.level_phixstargets_offset[ul];
       for (int t = 0; t < nt; t++) {
         upper = get_phixsupperlevel(K, element, ion, level, t);
@@ -1105,24 +1086,124 @@ DEVNI void do_macroatom(Tx &x, Pkt &p) {
         r += (R + C) * epsilon_current;
         if (zr * processrates[ARTIS_MA_ACTION_INTERNALUPHIGHER] < r) break;
       }
-      if (zr * processrates[ARTIS_MA_ACTION_INTERNALUPHIGHER] >= r) {
-        x.err(ERR_MA_SELECT, p.number, 7);
-        break;
-      }
-      ion += 1;
-      level = upper;
-    } else {
-      x.err(ERR_MA_SELECT, p.number, 100 + selected_action);
-      break;
+      found = zr * processrates[ARTIS_MA_ACTION_INTERNALUPHIGHER] < r;
     }
+    if (!found) {
+      fail(K, ERR_MA_SELECT, number, 7);
+      return MA_FAILED;
+    }
+    m.ion = ion + 1;
+    m.level = upper;
+    return MA_CONTINUE;
   }
-  lwork(x.L, WK_MA_JUMPS, jumps);
-  lwork(x.L, WK_MA_TRANS, ntrans);
+  fail(K, ERR_MA_SELECT, number, 100 + selected_action);
+  return MA_FAILED;
+}
+
+DEVFN void ma_lane_init(const Ctx &K, MaLane &m, int where, int element, int ion, int level) {
+  m.mgi = cell_mgi(K, where);
+  m.k = K.C.ne_index[m.mgi];
+  m.T_e = K.C.Te[m.mgi];
+  m.nne = K.C.nne[m.mgi];
+  m.element = element;
+  m.ion = ion;
+  m.level = level;
+  m.jumps = 0;
+  m.ntrans = 0;
+}
+
+// the deactivation branches of do_macroatom (macroatom.cc:222-380, 445-462) and its trailer (macroatom.cc:475-482);
+// `jumps` passes of the loop each added one interaction
+DEVNI void ma_finish(Tx &x, Pkt &p, const MaEnd &e, unsigned jumps) {
+  const Ctx &K = x.K;
+  const int element = p.ma_element;
+  p.interactions += (int)jumps;
+  if (e.code == MA_END_BB) {
+    const int linelistindex = e.a, ion = e.ion, level = e.b;
+    if (K.R.record_linestat) atomicAdd(&K.E.ecounter[linelistindex], 1);
+    const int lower = K.T.line_lower[linelistindex];
+    const double epsilon_trans = epsilon(K, element, ion, level) - epsilon(K, element, ion, lower);
+    double oldnucmf = 0.;
+    if (p.last_event == 1) oldnucmf = p.nu_cmf;
+    p.nu_cmf = epsilon_trans / ARTIS_H;
+    if (p.last_event == 1) lctr(x.L, (oldnucmf < p.nu_cmf) ? CTR_UPSCATTER : CTR_DOWNSCATTER);
+    lctr(x.L, CTR_MA_STAT_DEACTIVATION_BB);
+    p.last_event = 0;
+    emitt_rpkt(x, p);
+    if (linelistindex == p.ma_activatingline) lctr(x.L, CTR_RESONANCESCATTERINGS);
+    p.next_trans = linelistindex + 1;
+    p.emissiontype = linelistindex;
+    p.em_pos[0] = p.pos[0];
+    p.em_pos[1] = p.pos[1];
+    p.em_pos[2] = p.pos[2];
+    p.em_time = (int)p.prop_time;
+    p.nscatterings = 0;
+  } else if (e.code == MA_END_COLDEEXC || e.code == MA_END_COLRECOMB) {
+    const bool deexc = e.code == MA_END_COLDEEXC;
+    lctr(x.L, deexc ? CTR_MA_STAT_DEACTIVATION_COLLDEEXC : CTR_MA_STAT_DEACTIVATION_COLLRECOMB);
+    p.last_event = deexc ? 10 : 11;
+    p.type = ARTIS_TYPE_KPKT;
+    safeadd(&K.E.colheat[cell_mgi(K, p.where)], p.e_cmf);
+  } else if (e.code == MA_END_FB) {
+    const int ion = e.ion, lower = e.a, upperionlevel = e.b;
+    const float T_e = K.C.Te[cell_mgi(K, p.where)];
+    p.nu_cmf = select_continuum_nu(x, element, ion, lower, upperionlevel, T_e);
+    lctr(x.L, CTR_MA_STAT_DEACTIVATION_FB);
+    p.last_event = 2;
+    emitt_rpkt(x, p);
+    p.next_trans = 0;
+    {  // get_continuumindex (atomic.cc:16-30)
+      int target = 0;
+      for (int t = 0; t < get_nphixstargets(K, element, ion, lower); t++)
+        if (get_phixsupperlevel(K, element, ion, lower, t) == upperionlevel) {
+          target = t;
+          break;
+        }
+      p.emissiontype = K.T.level_cont_index[ulev(K, element, ion, lower)] - target;
+    }
+    p.em_pos[0] = p.pos[0];
+    p.em_pos[1] = p.pos[1];
+    p.em_pos[2] = p.pos[2];
+    p.em_time = (int)p.prop_time;
+    p.nscatterings = 0;
+  }
   if (p.trueemissiontype < 0) {
     p.trueemissiontype = p.emissiontype;
     p.trueemissionvelocity = (float)(vec_len(p.em_pos) / p.em_time);
     p.trueem_time = p.em_time;
   }
+}
+
+#define MA_MAX_JUMPS 10000000u
+
+// macroatom.cc:416-482 (megakernel form: walk + finish)
+DEVNI void do_macroatom(Tx &x, Pkt &p) {
+  const Ctx &K = x.K;
+  const int mgi = cell_mgi(K, p.where);
+  if (K.C.thick[mgi] == 1) {
+    x.err(ERR_THICK_MA, p.number, mgi);
+    return;
+  }
+  MaLane m;
+  ma_lane_init(K, m, p.where, p.ma_element, p.ma_ion, p.ma_level);
+  const double t_mid = K.G.ts_mid[x.nts];
+  MaEnd e;
+  e.code = MA_CONTINUE;
+  int r;
+  while ((r = (K.C.have_macache ? ma_jump<true>(K, x.L, x.rng, m, t_mid, e, p.number)
+                                 : ma_jump<false>(K, x.L, x.rng, m, t_mid, e, p.number))) == MA_CONTINUE) {
+    if (m.jumps >= MA_MAX_JUMPS) {
+      x.err(ERR_STUCK, p.number, 2);
+      return;
+    }
+  }
+  lwork(x.L, WK_MA_JUMPS, m.jumps);
+  lwork(x.L, WK_MA_TRANS, m.ntrans);
+  if (r == MA_FAILED) {
+    x.ok = false;
+    return;
+  }
+  ma_finish(x, p, e, m.jumps);
 }
 
 // ------------------------------------------------------------------------------------------ k-packets

@@ -1,0 +1,292 @@
+// wavefront.h -- the event-queue ("wavefront") form of update_packets: one kernel per packet state.
+//
+// The reference advances each packet to the end of the timestep in one call chain (update_packets.cc:162-230:
+// do_rpkt / do_macroatom / do_kpkt until escape or t2).  On a GPU that megakernel is a poor fit: the r-packet
+// code needs ~200 live registers, so the macro-atom random walk -- most of the work, a chain of dependent
+// HBM lookups -- runs at one wave per SIMD with the r-packet registers idle.  Here every state has its own
+// kernel, and a packet moves between queues when its state changes:
+//
+//   k_rpkt : r-packet steps (rpkt.cc:1156-1283) until absorption (-> M or K queue), escape or t2
+//   k_ma   : macro-atom jumps (macroatom.cc:416-482) on a 4-word lane state; never touches the packet record
+//   k_kpkt : k-packet cooling (kpkt.cc:477-797) -> r-packet (R queue) or macro-atom (M queue)
+//
+// A macro-atom's deactivation (emission direction, fb frequency, estimator terms) is deferred to the kernel
+// the packet moves to, which loads the full record anyway (ma_finish).  Every packet keeps its own RNG stream
+// (draw counter in rng_n), so the sequence of draws -- and hence every result -- is identical to the
+// megakernel and the CPU oracle.
+//
+// k_rpkt and k_ma are persistent: a lane that finishes its packet takes the next one from its queue
+// (wave-aggregated atomic on the queue head), so lanes stay busy while walk lengths vary by orders of magnitude.
+// Appends to queues are wave-aggregated (ballot + popcount + one atomic per wave).
+#ifndef ARTIS_WAVEFRONT_H
+#define ARTIS_WAVEFRONT_H
+
+#include "transport.h"
+
+enum { QR = 0, QM = 1, QK = 2, NQUEUES = 3 };
+
+struct WaveState {
+  uint32_t *rng_n;     // [N] draws consumed so far this timestep (artis_rng.n)
+  int4 *pend;          // [N] deferred macro-atom deactivation (MaEnd); .x == 0: none
+  uint32_t *pend_jumps;// [N] macro-atom loop passes of that deactivation
+  int32_t *q[NQUEUES]; // [N] packet indices per state
+  uint32_t *ctr;       // [NQUEUES * 2]: appended count, fetch head
+};
+
+#define WAVE_BLOCK 256
+#define RPKT_MAX_STEPS 2000000
+
+DEVFN int lane_id() { return (int)__lane_id(); }
+
+// wave-aggregated reservation of one slot per lane with `pred` from counter *c; returns the lane's slot
+DEVFN uint32_t wave_reserve(uint32_t *c, bool pred) {
+  const unsigned long long mask = __ballot(pred);
+  if (!mask) return 0xffffffffu;
+  const int leader = __ffsll((long long)mask) - 1;
+  uint32_t base = 0;
+  if (lane_id() == leader) base = atomicAdd(c, (uint32_t)__popcll(mask));
+  base = __shfl(base, leader, 64);
+  const unsigned long long below = mask & ((1ull << lane_id()) - 1ull);
+  return pred ? base + (uint32_t)__popcll(below) : 0xffffffffu;
+}
+
+DEVFN void wave_push(const WaveState &W, int q, bool pred, int32_t idx) {
+  const uint32_t slot = wave_reserve(&W.ctr[2 * q], pred);
+  if (pred) W.q[q][slot] = idx;
+}
+
+struct BlockCounters {
+  unsigned long long *ctr, *work;
+};
+
+DEVFN void block_counters_init(unsigned long long *s_ctr, unsigned long long *s_work) {
+  for (int j = threadIdx.x; j < ARTIS_COUNTER_COUNT + 1; j += blockDim.x) s_ctr[j] = 0;
+  for (int j = threadIdx.x; j < ARTIS_WORK_COUNT; j += blockDim.x) s_work[j] = 0;
+  __syncthreads();
+}
+DEVFN void block_counters_flush(const Ctx &K, const unsigned long long *s_ctr, const unsigned long long *s_work) {
+  __syncthreads();
+  for (int j = threadIdx.x; j < ARTIS_COUNTER_COUNT + 1; j += blockDim.x)
+    if (s_ctr[j]) atomicAdd(&K.E.counters[j], s_ctr[j]);
+  for (int j = threadIdx.x; j < ARTIS_WORK_COUNT; j += blockDim.x)
+    if (s_work[j]) atomicAdd(&K.E.work[j], s_work[j]);
+}
+
+// update_packets.cc:280-309 prologue: reset the per-step counters of every packet, queue the active ones
+__global__ void k_classify(Ctx K, WaveState W, uint64_t *__restrict__ soa, int64_t n, double t2) {
+  __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
+  __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
+  block_counters_init(s_ctr, s_work);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool toR = false, toM = false, toK = false;
+  if (i < n) {
+    const uint64_t w0 = soa[i];
+    const int type = hi32(w0);
+    const uint64_t w1 = soa[1 * n + i];
+    soa[1 * n + i] = pack2(lo32(w1), 0);  // interactions = 0
+    const uint64_t w33 = soa[33 * n + i];
+    soa[33 * n + i] = pack2(0, hi32(w33));  // scat_count = 0
+    const double prop_time = asd(soa[18 * n + i]);
+    if (type != ARTIS_TYPE_ESCAPE && prop_time < t2) {
+      atomicAdd(&s_work[WK_PACKETS_ACTIVE], 1ull);
+      W.rng_n[i] = 0;
+      W.pend[i] = make_int4(0, 0, 0, 0);
+      toR = type == ARTIS_TYPE_RPKT;
+      toM = type == ARTIS_TYPE_MA;
+      toK = type == ARTIS_TYPE_KPKT || type == ARTIS_TYPE_PRE_KPKT;
+      if (!toR && !toM && !toK) fail(K, ERR_UNSUPPORTED_TYPE, hi32(soa[33 * n + i]), type);
+    }
+  }
+  wave_push(W, QR, toR, (int32_t)i);
+  wave_push(W, QM, toM, (int32_t)i);
+  wave_push(W, QK, toK, (int32_t)i);
+  block_counters_flush(K, s_ctr, s_work);
+}
+
+DEVFN void apply_pending(Tx &x, const WaveState &W, int32_t idx, Pkt &p) {
+  const int4 pd = W.pend[idx];
+  if (pd.x != 0) {
+    MaEnd e;
+    e.code = pd.x;
+    e.ion = pd.y;
+    e.a = pd.z;
+    e.b = pd.w;
+    ma_finish(x, p, e, W.pend_jumps[idx]);
+    W.pend[idx].x = 0;
+  }
+}
+
+// r-packets: persistent lanes, one do_rpkt_step per loop pass
+__global__ __launch_bounds__(WAVE_BLOCK) void k_rpkt(Ctx K, WaveState W, uint64_t *__restrict__ soa, int64_t n,
+                                                     int nts, double t2) {
+  __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
+  __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
+  __shared__ double s_cmflum[WAVE_BLOCK / 64];
+  block_counters_init(s_ctr, s_work);
+  LocalCounters L;
+  L.ctr = &s_ctr[0];
+  L.work = &s_work[0];
+  Tx x(K, L);
+  x.nts = nts;
+  const uint32_t nq = W.ctr[2 * QR];
+  Pkt p;
+  int32_t idx = -1;
+  bool have = false, drained = false;
+  int steps = 0;
+  double cmf_lum = 0.;
+  while (true) {
+    const bool need = !have && !drained;
+    const uint32_t slot = wave_reserve(&W.ctr[2 * QR + 1], need);
+    if (need) {
+      if (slot < nq) {
+        idx = W.q[QR][slot];
+        pkt_load(soa, n, idx, p);
+        x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
+        x.rng.n = W.rng_n[idx];
+        x.ok = true;
+        steps = 0;
+        have = true;
+        apply_pending(x, W, idx, p);
+      } else {
+        drained = true;
+      }
+    }
+    if (!__any(have)) break;
+    bool toM = false, toK = false;
+    if (have) {
+      if (x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
+        do_rpkt_step(x, p, t2);
+        if (++steps > RPKT_MAX_STEPS) x.err(ERR_STUCK, p.number, 1);
+      }
+      if (!x.ok || p.type != ARTIS_TYPE_RPKT || !(p.prop_time < t2)) {
+        if (p.type == ARTIS_TYPE_ESCAPE) {
+          cmf_lum += p.e_cmf;
+          lwork(L, WK_ESCAPED, 1);
+        }
+        pkt_store(soa, n, idx, p);
+        W.rng_n[idx] = x.rng.n;
+        if (x.ok && p.prop_time < t2) {
+          toM = p.type == ARTIS_TYPE_MA;
+          toK = p.type == ARTIS_TYPE_KPKT || p.type == ARTIS_TYPE_PRE_KPKT;
+        }
+        have = false;
+      }
+    }
+    wave_push(W, QM, toM, idx);
+    wave_push(W, QK, toK, idx);
+  }
+  for (int off = 32; off > 0; off >>= 1) cmf_lum += __shfl_down(cmf_lum, off, 64);
+  if ((threadIdx.x & 63) == 0) s_cmflum[threadIdx.x >> 6] = cmf_lum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.;
+    for (int w = 0; w < WAVE_BLOCK / 64; w++) s += s_cmflum[w];
+    if (s != 0.) unsafeAtomicAdd(&K.E.scalars[0], s);
+  }
+  block_counters_flush(K, s_ctr, s_work);
+}
+
+// macro-atoms: persistent lanes, one jump per loop pass, lane state = MaLane + RNG counter
+template <bool CACHE>
+__global__ __launch_bounds__(WAVE_BLOCK) void k_ma(Ctx K, WaveState W, const uint64_t *__restrict__ soa, int64_t n,
+                                                   int nts) {
+  __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
+  __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
+  block_counters_init(s_ctr, s_work);
+  LocalCounters L;
+  L.ctr = &s_ctr[0];
+  L.work = &s_work[0];
+  const uint32_t nq = W.ctr[2 * QM];
+  const double t_mid = K.G.ts_mid[nts];
+  MaLane m;
+  artis_rng rng = artis_rng_init(K.R.seed, 0, nts, K.R.rank);
+  int32_t idx = -1;
+  bool have = false, drained = false;
+  unsigned long long jumps_sum = 0, trans_sum = 0;
+  while (true) {
+    const bool need = !have && !drained;
+    const uint32_t slot = wave_reserve(&W.ctr[2 * QM + 1], need);
+    if (need) {
+      if (slot < nq) {
+        idx = W.q[QM][slot];
+        const int where = lo32(soa[idx]);
+        const uint64_t w36 = soa[36 * n + idx];
+        const uint64_t w37 = soa[37 * n + idx];
+        rng.key1 = (uint32_t)hi32(soa[33 * n + idx]);  // packet number
+        rng.n = W.rng_n[idx];
+        ma_lane_init(K, m, where, lo32(w36), hi32(w36), lo32(w37));
+        have = true;
+        if (K.C.thick[m.mgi] == 1) {
+          fail(K, ERR_THICK_MA, (int)rng.key1, m.mgi);
+          have = false;
+        }
+      } else {
+        drained = true;
+      }
+    }
+    if (!__any(have)) break;
+    bool toR = false, toK = false;
+    if (have) {
+      MaEnd e;
+      const int r = ma_jump<CACHE>(K, L, rng, m, t_mid, e, (int)rng.key1);
+      if (r != MA_CONTINUE || m.jumps >= MA_MAX_JUMPS) {
+        if (r == MA_CONTINUE) fail(K, ERR_STUCK, (int)rng.key1, 2);
+        if (r > 0) {
+          W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
+          W.pend_jumps[idx] = m.jumps;
+          W.rng_n[idx] = rng.n;
+          toR = (r == MA_END_BB || r == MA_END_FB);
+          toK = (r == MA_END_COLDEEXC || r == MA_END_COLRECOMB);
+        }
+        jumps_sum += m.jumps;
+        trans_sum += m.ntrans;
+        have = false;
+      }
+    }
+    wave_push(W, QR, toR, idx);
+    wave_push(W, QK, toK, idx);
+  }
+  if (jumps_sum) atomicAdd(&s_work[WK_MA_JUMPS], jumps_sum);
+  if (trans_sum) atomicAdd(&s_work[WK_MA_TRANS], trans_sum);
+  block_counters_flush(K, s_ctr, s_work);
+}
+
+// k-packets (rare): one packet per workitem, grid-stride
+__global__ __launch_bounds__(WAVE_BLOCK) void k_kpkt(Ctx K, WaveState W, uint64_t *__restrict__ soa, int64_t n,
+                                                     int nts, double t2) {
+  __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
+  __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
+  block_counters_init(s_ctr, s_work);
+  LocalCounters L;
+  L.ctr = &s_ctr[0];
+  L.work = &s_work[0];
+  const uint32_t nq = W.ctr[2 * QK];
+  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x) {
+    const int32_t idx = W.q[QK][slot];
+    Pkt p;
+    pkt_load(soa, n, idx, p);
+    Tx x(K, L);
+    x.nts = nts;
+    x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
+    x.rng.n = W.rng_n[idx];
+    apply_pending(x, W, idx, p);
+    int guard = 0;
+    while (x.ok && (p.type == ARTIS_TYPE_KPKT || p.type == ARTIS_TYPE_PRE_KPKT) && p.prop_time < t2) {
+      const int mgi = cell_mgi(K, p.where);
+      if (p.type == ARTIS_TYPE_PRE_KPKT || K.C.thick[mgi] == 1)
+        do_kpkt_bb(x, p);
+      else
+        do_kpkt(x, p, t2);
+      if (++guard > 1000) x.err(ERR_STUCK, p.number, 4);
+    }
+    pkt_store(soa, n, idx, p);
+    W.rng_n[idx] = x.rng.n;
+    if (x.ok && p.prop_time < t2) {
+      if (p.type == ARTIS_TYPE_RPKT) W.q[QR][atomicAdd(&W.ctr[2 * QR], 1u)] = idx;
+      if (p.type == ARTIS_TYPE_MA) W.q[QM][atomicAdd(&W.ctr[2 * QM], 1u)] = idx;
+    }
+  }
+  block_counters_flush(K, s_ctr, s_work);
+}
+
+#endif

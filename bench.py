@@ -85,6 +85,7 @@ def main():
     transport_ms = []
     precompute_ms = []
     work = np.zeros(16, dtype=np.int64)
+    rounds = []
 
     def step(record):
         eng.restore()
@@ -99,6 +100,7 @@ def main():
             transport_ms.append(eng.last_transport_ms())
             precompute_ms.append(eng.last_precompute_ms())
             work[:] = eng.last_work()
+            rounds.append(eng.last_rounds())
 
     for _ in range(args.warmup):
         step(False)
@@ -192,6 +194,8 @@ def main():
             },
             "cpu_baseline": cpu,
             "precompute_ms": float(np.mean(precompute_ms)),
+            "transport_ms": float(np.mean(transport_ms)),
+            "event_rounds": int(np.max(rounds)) if rounds else 0,
             "work_per_packet": {k: float(v) / max(P, 1) for k, v in zip(
                 ["active", "rpkt_steps", "lines_scanned", "line_taus", "kappa_evals", "bf_active", "est_segments",
                  "gc_updates", "ma_jumps", "ma_trans", "kpkt", "kpkt_terms", "escaped", "es_scat", "bb_events",

@@ -323,6 +323,7 @@ double artis_gpu_last_precompute_ms(void);
 /* Per-call event counts from the device (steps, lines scanned, kappa evaluations, ...), for the byte model. */
 #define ARTIS_WORK_COUNT 16
 int artis_gpu_last_work_counts(int64_t out[ARTIS_WORK_COUNT]);
+int64_t artis_gpu_last_rounds(void);  /* event-queue rounds of the last update (0: megakernel path) */
 const char *artis_gpu_last_error(void);
 int artis_gpu_abi_version(void);
 

@@ -9,6 +9,13 @@ Estimators are float64 sums accumulated with atomics in a schedule-dependent ord
 import numpy as np
 
 FP_RTOL = 1e-9
+# stats of the reference's per-OpenMP-thread cellhistory cache (CTR_UPDATECELL, CTR_COOLINGRATECALCCOUNTER,
+# stats.h): the engine has no per-thread cache (per-cell tables in HBM instead), so these are not compared
+CACHE_COUNTERS = [31, 32]
+# CTR_UPSCATTER / CTR_DOWNSCATTER compare nu_cmf after an electron scattering with nu_cmf before
+# (rpkt.cc escat branch); the comoving frequency is unchanged by Thomson scattering up to the rounding of the
+# frame transforms, so the split is decided by last-ulp noise.  Only their sum is an event count.
+ROUNDING_SPLIT_COUNTERS = (29, 30)
 ESTIMATOR_RTOL = 1e-9
 
 INT_FIELDS = ["where", "type", "last_cross", "interactions", "nscatterings", "last_event", "next_trans",
@@ -72,6 +79,15 @@ def spectrum_l1(a, b):
     return float(np.abs(sa - sb).sum() / max(np.abs(sb).sum(), 1e-300))
 
 
+def counters_equal(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    keep = np.ones(len(a), dtype=bool)
+    keep[CACHE_COUNTERS] = False
+    keep[list(ROUNDING_SPLIT_COUNTERS)] = False
+    up, down = ROUNDING_SPLIT_COUNTERS
+    return bool((a[keep] == b[keep]).all() and a[up] + a[down] == b[up] + b[down])
+
+
 def assert_estimators_match(eg, eo, exact_counts=True, rtol=ESTIMATOR_RTOL):
     for name in ("J", "nuJ", "ffheating", "colheating", "gamma", "bfheating"):
         x, y = getattr(eg, name), getattr(eo, name)
@@ -80,6 +96,6 @@ def assert_estimators_match(eg, eo, exact_counts=True, rtol=ESTIMATOR_RTOL):
     assert abs(eg.struct.cmf_lum - eo.struct.cmf_lum) <= rtol * max(abs(eo.struct.cmf_lum), 1e-300)
     if exact_counts:
         assert eg.struct.nesc == eo.struct.nesc
-        assert (eg.counters == eo.counters).all(), (eg.counters, eo.counters)
+        assert counters_equal(eg.counters, eo.counters), (eg.counters, eo.counters)
         assert (eg.ecounter == eo.ecounter).all()
         assert (eg.acounter == eo.acounter).all()

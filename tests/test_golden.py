@@ -44,7 +44,7 @@ def test_oracle_reproduces_golden(name):
             assert pk.view(np.uint8).tobytes() == z["packets_in"].tobytes(), "model generator drifted"
         est, _ = oracle_lib.update_packets(m, nts, pk, nthreads=4)
     assert pk.view(np.uint8).tobytes() == z["packets_out"].tobytes()
-    assert (est.counters == z["counters"]).all()
+    assert parity.counters_equal(est.counters, z["counters"])
     assert (est.ecounter == z["ecounter"]).all() and (est.acounter == z["acounter"]).all()
     assert np.allclose(est.J, z["J"], rtol=1e-12, atol=0)
 
@@ -67,7 +67,7 @@ def test_engine_reproduces_golden(name):
     finally:
         eng.close()
     parity.assert_packets_match(pk, ref)
-    assert (est.counters == z["counters"]).all()
+    assert parity.counters_equal(est.counters, z["counters"])
     assert (est.ecounter == z["ecounter"]).all() and (est.acounter == z["acounter"]).all()
     for f in ("J", "nuJ", "ffheating", "gamma", "bfheating"):
         y = z[f]

@@ -50,9 +50,11 @@ def test_grid3d_packets_and_estimators(small_model, engine_factory):
     _, pg, eg, po, eo, wo = _pair(small_model, eng, 10, 4000, seed=3)
     nbad, worst = parity.assert_packets_match(pg, po)
     parity.assert_estimators_match(eg, eo)
-    # same work on both sides (per-packet histories identical)
+    # same work on both sides (per-packet histories identical); WK_MA_TRANS counts transitions the engine
+    # actually touched (binary-search probes with the macro-atom cache) rather than the oracle's linear scan
     wg = eng.last_work()
-    assert (wg == wo).all(), (wg, wo)
+    keep = np.arange(len(wg)) != 9
+    assert (wg[keep] == wo[keep]).all(), (wg, wo)
     assert parity.spectrum_l1(pg, po) < 1e-9
 
 
@@ -185,3 +187,26 @@ def test_bench_size_subset_parity(engine_factory):
     assert c[0] + c[1] + c[4] + c[5] == c[7] + c[8] + c[9] + c[10]
     assert c[19] + c[20] + c[7] + c[8] == c[14] + c[15] + c[16] + c[17] + c[18]
     assert np.allclose(np.linalg.norm(pg["dir"], axis=1), 1.0, atol=1e-10)
+
+
+def test_event_queue_engine_matches_megakernel(small_model, engine_factory, monkeypatch):
+    """The event-queue kernels (wavefront.h) and the one-kernel path draw the same streams: identical packets."""
+    small_model.set_timestep(11)
+    pk = small_model.init_rpackets(11, 3000, seed=12)
+    eng = engine_factory(small_model)
+    eng.upload_cellstate(11)
+    a = pk.copy()
+    ea = eng.update_packets(11, a)
+    assert eng.last_rounds() > 0
+    wa = eng.last_work()
+    eng.close()
+    monkeypatch.setenv("ARTIS_GPU_ENGINE", "mega")
+    eng2 = engine_factory(small_model)
+    eng2.upload_cellstate(11)
+    b = pk.copy()
+    eb = eng2.update_packets(11, b)
+    assert eng2.last_rounds() == 0
+    assert a.tobytes() == b.tobytes()
+    assert (ea.counters == eb.counters).all()
+    assert (wa == eng2.last_work()).all()
+    parity.assert_estimators_match(ea, eb)

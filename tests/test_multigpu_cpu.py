@@ -30,7 +30,7 @@ def _rank_run(rank):
     pk = m.init_rpackets(NTS, NPKTS, seed=1000 + rank)
     p = copy.copy(m.params)
     p.rank = rank
-    est, _ = oracle_lib.update_packets(m, NTS, pk, params=p)
+    est, _ = oracle_lib.update_packets(m, NTS, pk, params=p, nthreads=1)  # cache stats are schedule-dependent
     return m, pk, est
 
 
