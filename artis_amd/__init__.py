@@ -21,7 +21,7 @@ ABI_SYMBOLS = [
     "artis_gpu_packets_restore", "artis_gpu_update_packets_resident", "artis_gpu_estimators_zero",
     "artis_gpu_estimators_download", "artis_gpu_estimator_block_doubles", "artis_gpu_estimator_block_to_device",
     "artis_gpu_estimator_block_from_device", "artis_gpu_last_transport_ms", "artis_gpu_last_precompute_ms",
-    "artis_gpu_last_work_counts", "artis_gpu_last_rounds", "artis_gpu_last_error", "artis_gpu_abi_version",
+    "artis_gpu_last_work_counts", "artis_gpu_last_rounds", "artis_gpu_last_kernel_times", "artis_gpu_last_error", "artis_gpu_abi_version",
 ]
 
 _gpu_lib = None
@@ -132,6 +132,13 @@ class Engine:
         w = np.zeros(ffi.ARTIS_WORK_COUNT, dtype=np.int64)
         self.lib.artis_gpu_last_work_counts(w.ctypes.data)
         return w
+
+    def last_kernel_times(self):
+        """{class: (ms, launches)} for the last transport: rpkt, ma, kpkt, classify."""
+        ms = (C.c_double * 4)()
+        nl = (C.c_int64 * 4)()
+        self.lib.artis_gpu_last_kernel_times(ms, nl)
+        return {k: (ms[i], nl[i]) for i, k in enumerate(("rpkt", "ma", "kpkt", "classify"))}
 
     def last_rounds(self):
         return int(self.lib.artis_gpu_last_rounds())

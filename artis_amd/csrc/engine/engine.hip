@@ -9,7 +9,9 @@
 //     (one packet per workitem, update_packets.cc:234-333 with the pass loop flattened), SoA->AoS, D2H, and
 //     the estimator sums added into the caller's arrays.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -408,7 +410,19 @@ struct Engine {
   hipEvent_t ev_round[2] = {nullptr, nullptr};
   int wave_grid = 2048;
   bool use_megakernel = false;
+  bool ma_meta_ok = true;         // MaMeta's 16-bit counts hold every level's transition counts
+  int ma_occ = 1;                 // k_ma minimum waves per SIMD (launch bounds): 1 or 8
+  uint32_t *d_binoffs = nullptr;  // exclusive prefix sums of W.bins
+  void *d_scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
   int64_t last_rounds = 0;
+  // per kernel class (rpkt, ma, kpkt, classify+bookkeeping): summed device time and launch count of the last
+  // transport, from events bracketing every launch
+  std::vector<hipEvent_t> tev;
+  std::vector<int> tev_class;
+  size_t tev_used = 0;
+  double last_kernel_ms[4] = {0, 0, 0, 0};
+  int64_t last_kernel_launches[4] = {0, 0, 0, 0};
   double last_transport_ms = 0., last_precompute_ms = 0.;
   int64_t last_work[ARTIS_WORK_COUNT] = {0};
   std::string last_error;
@@ -471,6 +485,8 @@ int alloc_packets(int64_t n) {
     (void)hipFree(G.W.rng_n);
     (void)hipFree(G.W.pend);
     (void)hipFree(G.W.pend_jumps);
+    (void)hipFree(G.W.ma_key);
+    (void)hipFree(G.W.ma_sorted);
     for (int q = 0; q < NQUEUES; q++) (void)hipFree(G.W.q[q]);
   }
   HIPCHK(hipMalloc(&G.d_soa, (size_t)n * PKT_WORDS * 8));
@@ -478,6 +494,8 @@ int alloc_packets(int64_t n) {
   HIPCHK(hipMalloc(&G.W.rng_n, (size_t)n * sizeof(uint32_t)));
   HIPCHK(hipMalloc(&G.W.pend, (size_t)n * sizeof(int4)));
   HIPCHK(hipMalloc(&G.W.pend_jumps, (size_t)n * sizeof(uint32_t)));
+  HIPCHK(hipMalloc(&G.W.ma_key, (size_t)n * sizeof(int32_t)));
+  HIPCHK(hipMalloc(&G.W.ma_sorted, (size_t)n * sizeof(int32_t)));
   for (int q = 0; q < NQUEUES; q++) HIPCHK(hipMalloc(&G.W.q[q], (size_t)n * sizeof(int32_t)));
   G.cap_pkts = n;
   return 0;
@@ -486,24 +504,78 @@ int alloc_packets(int64_t n) {
 // Event-queue transport (wavefront.h): classify, then rounds of R -> M -> K kernels until both the R and M
 // queues stay empty.  The host learns the queue sizes one round late (pinned async copies), so it never
 // stalls the stream; a round enqueued after the work ran out finds empty queues and costs only its launches.
+int tmark(int cls) {
+  if (G.tev_used + 1 > G.tev.size()) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    G.tev.push_back(e);
+    G.tev_class.push_back(cls);
+  }
+  G.tev_class[G.tev_used] = cls;
+  HIPCHK(hipEventRecord(G.tev[G.tev_used++], G.stream));
+  return 0;
+}
+// events come in (start, end) pairs; sum per class once the stream has drained
+int tcollect() {
+  for (int c = 0; c < 4; c++) {
+    G.last_kernel_ms[c] = 0.;
+    G.last_kernel_launches[c] = 0;
+  }
+  for (size_t i = 0; i + 1 < G.tev_used; i += 2) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, G.tev[i], G.tev[i + 1]));
+    G.last_kernel_ms[G.tev_class[i]] += ms;
+    G.last_kernel_launches[G.tev_class[i]]++;
+  }
+  G.tev_used = 0;
+  return 0;
+}
+#define TSTART(c) \
+  if (int rc_ = tmark(c)) return rc_
+#define TEND(c) \
+  if (int rc_ = tmark(c)) return rc_
+
 #define WAVE_MAX_ROUNDS 10000000
 int run_wavefront(int64_t n, int nts, double t2) {
   const WaveState &W = G.W;
   const unsigned grid = (unsigned)G.wave_grid;
+  G.tev_used = 0;
+  HIPCHK(hipMemsetAsync(W.stats, 0, 32 * sizeof(unsigned long long), G.stream));
   HIPCHK(hipMemsetAsync(W.ctr, 0, NQUEUES * 2 * sizeof(uint32_t), G.stream));
+  TSTART(3);
   k_classify<<<(unsigned)((n + WAVE_BLOCK - 1) / WAVE_BLOCK), WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, t2);
+  TEND(3);
   HIPCHK(hipGetLastError());
   int64_t round = 0;
   bool done = false;
   for (; round < WAVE_MAX_ROUNDS && !done; round++) {
+    TSTART(0);
     k_rpkt<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts, t2);
+    TEND(0);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QR, 0, 2 * sizeof(uint32_t), G.stream));
-    if (G.K.C.have_macache)
-      k_ma<true><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts);
-    else
-      k_ma<false><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts);
+    TSTART(1);
+    if (W.ma_binned) {
+      const int nne = G.K.C.n_nonempty;
+      HIPCHK(hipMemsetAsync(W.bins, 0, (size_t)(nne + 1) * sizeof(uint32_t), G.stream));
+      k_ma_bin<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa);
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(G.d_scan_tmp, G.scan_tmp_bytes, W.bins, G.d_binoffs, nne + 1,
+                                              G.stream));
+      k_ma_scatter<<<grid, WAVE_BLOCK, 0, G.stream>>>(W, G.d_binoffs);
+    }
+    HIPCHK(hipMemsetAsync(W.xhead, 0, 8 * sizeof(uint32_t), G.stream));
+    if (G.K.C.have_macache) {
+      if (G.ma_occ == 8)
+        k_ma<true, 8><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts);
+      else
+        k_ma<true, 1><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts);
+    } else {
+      k_ma<false, 1><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts);
+    }
+    TEND(1);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QM, 0, 2 * sizeof(uint32_t), G.stream));
+    TSTART(2);
     k_kpkt<<<grid / 4, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts, t2);
+    TEND(2);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QK, 0, 2 * sizeof(uint32_t), G.stream));
     HIPCHK(hipGetLastError());
     const int slot = (int)(round & 1);
@@ -527,7 +599,26 @@ int run_wavefront(int64_t n, int nts, double t2) {
     }
   }
   G.last_rounds = round;
-  return 0;
+  HIPCHK(hipStreamSynchronize(G.stream));
+  if (getenv("ARTIS_GPU_STATS")) {
+    unsigned long long st[32];
+    HIPCHK(hipMemcpy(st, W.stats, sizeof(st), hipMemcpyDeviceToHost));
+    const char *nm[2] = {"rpkt", "ma"};
+    for (int c = 0; c < 2; c++)
+      fprintf(stderr,
+              "[artis_gpu] %s: wave passes %llu, lane utilisation %.3f, cycles/pass %.0f, passes/refill %.1f, "
+              "cycles/refill %.0f, step cycles/pass %.0f\n",
+              nm[c], st[4 * c], st[4 * c] ? (double)st[4 * c + 1] / (64.0 * st[4 * c]) : 0.,
+              st[4 * c] ? (double)st[4 * c + 2] / st[4 * c] : 0., st[4 * c + 3] ? (double)st[4 * c] / st[4 * c + 3] : 0.,
+              st[4 * c + 3] ? (double)st[16 + 4 * c] / st[4 * c + 3] : 0.,
+              st[4 * c] ? (double)st[17 + 4 * c] / st[4 * c] : 0.);
+    fprintf(stderr,
+            "[artis_gpu] rpkt per pass: lines scanned wave-max %.2f vs lane-mean %.3f; bf continua wave-max %.2f vs "
+            "lane-mean %.3f\n",
+            st[0] ? (double)st[24] / st[0] : 0., st[0] ? (double)st[25] / (64.0 * st[0]) : 0.,
+            st[0] ? (double)st[26] / st[0] : 0., st[0] ? (double)st[27] / (64.0 * st[0]) : 0.);
+  }
+  return tcollect();
 }
 
 }  // namespace
@@ -540,6 +631,13 @@ const char *artis_gpu_last_error(void) { return G.last_error.c_str(); }
 double artis_gpu_last_transport_ms(void) { return G.last_transport_ms; }
 double artis_gpu_last_precompute_ms(void) { return G.last_precompute_ms; }
 int64_t artis_gpu_last_rounds(void) { return G.last_rounds; }
+int artis_gpu_last_kernel_times(double ms[4], int64_t launches[4]) {
+  for (int c = 0; c < 4; c++) {
+    ms[c] = G.last_kernel_ms[c];
+    launches[c] = G.last_kernel_launches[c];
+  }
+  return 0;
+}
 int artis_gpu_last_work_counts(int64_t out[ARTIS_WORK_COUNT]) {
   for (int k = 0; k < ARTIS_WORK_COUNT; k++) out[k] = G.last_work[k];
   return 0;
@@ -556,9 +654,12 @@ void artis_gpu_finalize(void) {
     (void)hipFree(G.W.rng_n);
     (void)hipFree(G.W.pend);
     (void)hipFree(G.W.pend_jumps);
+    (void)hipFree(G.W.ma_key);
+    (void)hipFree(G.W.ma_sorted);
     for (int q = 0; q < NQUEUES; q++) (void)hipFree(G.W.q[q]);
   }
   if (G.h_ctr) (void)hipHostFree(G.h_ctr);
+  for (hipEvent_t e : G.tev) (void)hipEventDestroy(e);
   for (int r = 0; r < 2; r++)
     if (G.ev_round[r]) (void)hipEventDestroy(G.ev_round[r]);
   if (G.ev0) (void)hipEventDestroy(G.ev0);
@@ -593,6 +694,14 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     G.wave_grid = ncu * 8;  // 32 waves per CU of 256-thread blocks; late blocks find the queue drained
     const char *eng = getenv("ARTIS_GPU_ENGINE");
     G.use_megakernel = eng && std::string(eng) == "mega";
+    const char *b = getenv("ARTIS_GPU_MA_BIN");
+    G.W.ma_binned = !(b && b[0] == '0');
+    const char *xr = getenv("ARTIS_GPU_MA_XCD");
+    G.W.ma_ranges = (xr && xr[0] == '0') ? 1 : 8;
+    const char *rf = getenv("ARTIS_GPU_REFILL");
+    G.W.refill_min = rf ? std::max(1, std::min(64, atoi(rf))) : 32;
+    const char *oc = getenv("ARTIS_GPU_MA_OCC");
+    G.ma_occ = (oc && oc[0] == '8') ? 8 : 1;
   }
   G.params = *rp;
   DevTab &T = G.K.T;
@@ -702,6 +811,38 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
       }
     }
   rc |= dupload(&T.ma_level, mal.data(), nl);
+  {
+    std::vector<MaMeta> mm(nl);
+    std::vector<int32_t> dt(std::max<int64_t>(ndown, 1)), ut(std::max<int64_t>(nup, 1));
+    for (int e = 0; e < ne; e++)
+      for (int i = 0; i < a->elem_nions[e]; i++) {
+        const int ui = a->elem_uniqueionoffset[e] + i;
+        const int base = a->ion_uniqueleveloffset[ui];
+        for (int l = 0; l < a->ion_nlevels[ui]; l++) {
+          const int ul = base + l;
+          MaMeta &m = mm[ul];
+          m.epsilon = a->level_epsilon[ul];
+          m.rec_off = mal[ul].x;
+          m.doff = a->level_downtrans_offset[ul];
+          m.uoff = a->level_uptrans_offset[ul];
+          m.base_lower = (i > 0) ? a->ion_uniqueleveloffset[ui - 1] : -1;
+          m.nd = (uint16_t)a->level_ndowntrans[ul];
+          m.nu = (uint16_t)a->level_nuptrans[ul];
+          m.nr = (uint16_t)mal[ul].w;
+          m.nt = (uint16_t)((i < a->elem_nions[e] - 1 && l < a->ion_ionisinglevels[ui]) ? a->level_nphixstargets[ul] : 0);
+          for (int j = 0; j < a->level_ndowntrans[ul]; j++)
+            dt[m.doff + j] = base + a->line_lowerlevelindex[a->downtrans_lineindex[m.doff + j]];
+          for (int j = 0; j < a->level_nuptrans[ul]; j++)
+            ut[m.uoff + j] = base + a->line_upperlevelindex[a->uptrans_lineindex[m.uoff + j]];
+        }
+      }
+    for (int ul = 0; ul < nl; ul++)
+      if (a->level_ndowntrans[ul] > 65535 || a->level_nuptrans[ul] > 65535 || mal[ul].w > 65535)
+        G.ma_meta_ok = false;
+    rc |= dupload(&T.ma_meta, mm.data(), nl);
+    rc |= dupload(&T.down_target_ul, dt.data(), dt.size());
+    rc |= dupload(&T.up_target_ul, ut.data(), ut.size());
+  }
   G.ma_rec_stride = marec;
   rc |= dupload(&T.allcont_nu_edge, a->allcont_nu_edge, nb);
   rc |= dupload(&T.allcont_probability, a->allcont_probability, nb);
@@ -813,6 +954,13 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   C.ne_index = dnei;
   C.ne_mgi = dnem;
   C.n_nonempty = nne_cells;
+  rc |= dalloc(&G.W.bins, (size_t)nne_cells + 1);
+  rc |= dalloc(&G.d_binoffs, (size_t)nne_cells + 1);
+  rc |= dalloc(&G.W.xhead, (size_t)8);
+  if (!rc) {
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, G.scan_tmp_bytes, G.W.bins, G.d_binoffs, nne_cells + 1);
+    rc |= dalloc((char **)&G.d_scan_tmp, G.scan_tmp_bytes);
+  }
   rc |= dalloc(&C.pops, (size_t)nne_cells * nl);
   rc |= dalloc(&C.ionpop, (size_t)nne_cells * ni);
   rc |= dalloc(&C.ffsum, (size_t)nne_cells);
@@ -828,7 +976,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     (void)hipMemGetInfo(&freeb, &totalb);
     const double need = (double)nne_cells * (double)C.ma_rec_stride * 8.0;
     const char *env = getenv("ARTIS_GPU_NO_MACACHE");
-    if (!(env && env[0] == '1') && need < 0.75 * (double)freeb) {
+    if (!(env && env[0] == '1') && G.ma_meta_ok && need < 0.75 * (double)freeb) {
       double *mc = nullptr;
       if (hipMalloc((void **)&mc, (size_t)need) == hipSuccess) {
         G.allocs.push_back(mc);
@@ -840,6 +988,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   if (!C.have_macache) rc |= dalloc(&C.marates, (size_t)nne_cells * nl * ARTIS_MA_ACTION_COUNT);
   // cell-state input buffers
   rc |= dalloc(&G.W.ctr, (size_t)NQUEUES * 2);
+  rc |= dalloc(&G.W.stats, (size_t)32);
   rc |= dalloc(&G.d_cellf, (size_t)8 * np);
   rc |= dalloc(&G.d_thick, (size_t)np);
   rc |= dalloc(&G.d_abund, (size_t)np * ne);

@@ -33,6 +33,16 @@ struct LineMA {
   double P2;    // pow(H_ionpot / (eps_upper - eps_lower), 2)    (macroatom.h:93, 130)
 };
 
+// static per-level data of the cached macro-atom walk, one 32-byte record per unique level (two 16-byte loads)
+struct __attribute__((aligned(16))) MaMeta {
+  double epsilon;      // level energy (atomic.cc epsilon)
+  int32_t rec_off;     // offset (doubles) of the level's macro-atom record inside a cell's block
+  int32_t doff, uoff;  // into downtrans_* / uptrans_* (level_downtrans_offset, level_uptrans_offset)
+  int32_t base_lower;  // unique index of level 0 of the next lower ion (-1 if none)
+  uint16_t nd, nu;     // #downtrans, #uptrans
+  uint16_t nr, nt;     // #recombination targets, #ionisation targets (get_nphixstargets)
+};
+
 struct DevTab {
   int32_t nelements, maxnions, nions_total, nlevels_total, nlines, nbf, nbfg, ncoolingterms;
   int32_t nphixspoints, phixs_file_version, tablesize, ntargets_total;
@@ -57,6 +67,8 @@ struct DevTab {
   // per level: offset (doubles) of its macro-atom record inside a cell's record block, #downtrans, #uptrans,
   // #recombination targets (ionising levels of the lower ion, 0 if the level does not recombine)
   const int4 *ma_level;
+  const MaMeta *ma_meta;                 // [nlevels_total]
+  const int32_t *down_target_ul, *up_target_ul;  // unique level index of each downtrans / uptrans target
   const double *allcont_nu_edge, *allcont_probability;
   const int32_t *allcont_element, *allcont_ion, *allcont_level, *allcont_target, *allcont_upperlevel,
       *allcont_phixstable, *allcont_groundindex;

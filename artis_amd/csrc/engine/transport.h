@@ -18,6 +18,7 @@ struct Tx {
   artis_rng rng;
   int nts;
   bool ok;
+  unsigned wl = 0, wb = 0;  // diagnostics: lines / bf continua scanned since last reset
   DEVFN Tx(const Ctx &k, const LocalCounters &l) : K(k), L(l), ok(true) {}
   DEVFN void err(int code, int number, int aux) {
     fail(K, code, number, aux);
@@ -26,6 +27,22 @@ struct Tx {
 };
 
 DEVFN void safeadd(double *p, double v) { unsafeAtomicAdd(p, v); }
+
+// Run a rarely taken noinline step on copies of the packet and the transport state.  A noinline callee needs
+// its Pkt& / Tx& in memory; handing it copies keeps the caller's packet and RNG free of address-taking, so
+// they stay in registers on the hot path instead of living in scratch.
+template <typename F>
+DEVFN void cold_call(Tx &x, Pkt &p, F &&f) {
+  Tx tx(x.K, x.L);
+  tx.rng = x.rng;
+  tx.nts = x.nts;
+  tx.ok = x.ok;
+  Pkt tp = p;
+  f(tx, tp);
+  p = tp;
+  x.rng = tx.rng;
+  x.ok = tx.ok;
+}
 
 // ------------------------------------------------------------------------------------------ emission
 // rpkt.cc:975-1025
@@ -358,6 +375,7 @@ DEVFN double kappa_bf_total(Tx &x, int k, int mgi, double nu) {
     if (bf_contribution(K, k, mgi, i, nu, &nnlevel, &gc)) kappa_bf_sum += nnlevel * gc;
   }
   lwork(x.L, WK_BF_ACTIVE, nactive);
+  x.wb += (unsigned)nactive;
   return kappa_bf_sum;
 }
 // rpkt.cc:1209-1295 (deviation D2: always recomputed)
@@ -457,7 +475,7 @@ DEVFN void move_dummy(const Ctx &K, double pos[3], const double dir[3], double &
 }
 
 // rpkt.cc:67-328
-DEVNI double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_eventtype, double tau_rnd,
+DEVFN double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_eventtype, double tau_rnd,
                        double abort_dist) {
   const Ctx &K = x.K;
   double tau = 0.;
@@ -560,6 +578,7 @@ DEVNI double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_even
   }
   lwork(x.L, WK_LINES_SCANNED, nscanned);
   lwork(x.L, WK_LINE_TAUS, ntaus);
+  x.wl += (unsigned)nscanned;
   return result;
 }
 
@@ -761,7 +780,10 @@ DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2) {
     if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_BB)
       rpkt_event_boundbound(x, p);
     else if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_CONT)
-      rpkt_event_continuum(x, p, kap, k, mgi);
+      cold_call(x, p, [&](Tx &tx, Pkt &tp) {
+        const Kappa kc = kap;
+        rpkt_event_continuum(tx, tp, kc, k, mgi);
+      });
     else
       x.err(ERR_NOEVENT, p.number, 0);
     return (x.ok && p.type == ARTIS_TYPE_RPKT && (mgi == npm || mgi == oldmgi));
@@ -853,7 +875,8 @@ struct MaLane {
 };
 enum { MA_CONTINUE = 0, MA_END_BB = 1, MA_END_COLDEEXC = 2, MA_END_COLRECOMB = 3, MA_END_FB = 4, MA_FAILED = -1 };
 struct MaEnd {
-  int code, ion, a, b;  // BB: a = line, b = level; FB: ion = lower ion, a = lower level, b = upper-ion level
+  int code, ion, a, b;  // BB: a = line, b = unique index of the emitting level;
+                        // FB: a = level of the lower ion, b = unique index of the recombining level
 };
 
 // macroatom.cc:416-482, one pass of the do_macroatom loop: select a process from the per-cell totals, then the
@@ -927,7 +950,7 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
     end.code = MA_END_BB;
     end.ion = ion;
     end.a = linelistindex;
-    end.b = level;
+    end.b = ul;
     return MA_END_BB;
   }
   if (selected_action == ARTIS_MA_ACTION_COLDEEXC || selected_action == ARTIS_MA_ACTION_COLRECOMB) {
@@ -998,7 +1021,7 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
     end.code = MA_END_FB;
     end.ion = upperion - 1;
     end.a = lower;
-    end.b = level;
+    end.b = ul;
     return MA_END_FB;
   }
   if (selected_action == ARTIS_MA_ACTION_INTERNALDOWNLOWER) {
@@ -1100,6 +1123,102 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
   return MA_FAILED;
 }
 
+// The cached walk in its lean form: lane state = (unique level, cell record block); per jump two 16-byte loads of
+// the level's static MaMeta, five of its 9 process-rate totals, the binary search in the selected cumulative
+// array and one load of the target level.  Same selections, same RNG draws as ma_jump<true>.
+struct MaLaneC {
+  int ul;
+  const double *block;  // K.C.ma_rec + k * ma_rec_stride
+  unsigned jumps;
+  unsigned long long ntrans;
+};
+
+DEVFN int ma_jump_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneC &m, MaEnd &end, int number) {
+  m.jumps++;
+  const int ul = m.ul;
+  const int4 *mp = reinterpret_cast<const int4 *>(K.T.ma_meta + ul);
+  const int4 w0 = mp[0], w1 = mp[1];
+  const int rec_off = w0.z, doff = w0.w, uoff = w1.x, base_lower = w1.y;
+  const int nd = w1.z & 0xffff, nu = (int)((unsigned)w1.z >> 16), nr = w1.w & 0xffff, nt = (int)((unsigned)w1.w >> 16);
+  const double *rec = m.block + rec_off;
+  const double2 *r2 = reinterpret_cast<const double2 *>(rec);
+  const double2 t01 = r2[0], t23 = r2[1], t45 = r2[2], t67 = r2[3];
+  const double pr[ARTIS_MA_ACTION_COUNT] = {t01.x, t01.y, t23.x, t23.y, t45.x, t45.y, t67.x, t67.y, rec[8]};
+  double total_transitions = 0.;
+  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) total_transitions += pr[a];
+  const double zrand = artis_rng_uniform(&rng);
+  const double randomrate = zrand * total_transitions;
+  double rate = 0.;
+  int sel = ARTIS_MA_ACTION_COUNT;
+  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
+    rate += pr[a];
+    if (rate > randomrate) {
+      sel = a;
+      break;
+    }
+  }
+  if (rate <= randomrate) {
+    fail(K, ERR_MA_RANDOM, number, ul);
+    return MA_FAILED;
+  }
+  if (sel == ARTIS_MA_ACTION_COLDEEXC || sel == ARTIS_MA_ACTION_COLRECOMB) {
+    end.code = (sel == ARTIS_MA_ACTION_COLDEEXC) ? MA_END_COLDEEXC : MA_END_COLRECOMB;
+    end.ion = end.a = end.b = 0;
+    return end.code;
+  }
+  if (sel == ARTIS_MA_ACTION_INTERNALUPHIGHERNT) {
+    fail(K, ERR_MA_SELECT, number, 100 + sel);
+    return MA_FAILED;
+  }
+  // the cumulative array of the selected action inside the level record (engine_dev.h DevCells::ma_rec)
+  int off, cnt;
+  switch (sel) {
+    case ARTIS_MA_ACTION_RADDEEXC: off = 9; cnt = nd; break;
+    case ARTIS_MA_ACTION_INTERNALDOWNSAME: off = 9 + nd; cnt = nd; break;
+    case ARTIS_MA_ACTION_INTERNALUPSAME: off = 9 + 2 * nd; cnt = nu; break;
+    case ARTIS_MA_ACTION_RADRECOMB: off = 9 + 2 * nd + nu; cnt = nr; break;
+    case ARTIS_MA_ACTION_INTERNALDOWNLOWER: off = 9 + 2 * nd + nu + nr; cnt = nr; break;
+    default: off = 9 + 2 * nd + nu + 2 * nr; cnt = nt; break;  // INTERNALUPHIGHER
+  }
+  const double zr = artis_rng_uniform(&rng);
+  const int j = first_above(rec + off, cnt, zr * pr[sel], m.ntrans);
+  if (j >= cnt) {
+    fail(K, ERR_MA_SELECT, number, 10 + sel);
+    return MA_FAILED;
+  }
+  switch (sel) {
+    case ARTIS_MA_ACTION_RADDEEXC:
+      end.code = MA_END_BB;
+      end.ion = 0;
+      end.a = K.T.downtrans_lineindex[doff + j];
+      end.b = ul;
+      return MA_END_BB;
+    case ARTIS_MA_ACTION_RADRECOMB:
+      end.code = MA_END_FB;
+      end.ion = 0;
+      end.a = j;
+      end.b = ul;
+      return MA_END_FB;
+    case ARTIS_MA_ACTION_INTERNALDOWNSAME:
+      m.ul = K.T.down_target_ul[doff + j];
+      return MA_CONTINUE;
+    case ARTIS_MA_ACTION_INTERNALUPSAME:
+      m.ul = K.T.up_target_ul[uoff + j];
+      return MA_CONTINUE;
+    case ARTIS_MA_ACTION_INTERNALDOWNLOWER:
+      lctr(L, CTR_MA_STAT_INTERNALDOWNLOWER);
+      m.ul = base_lower + j;
+      return MA_CONTINUE;
+    default: {  // INTERNALUPHIGHER (macroatom.cc:382-414)
+      lctr(L, CTR_MA_STAT_INTERNALUPHIGHER);
+      const int ui = K.T.level_ui[ul];
+      m.ul = K.T.ion_uniqueleveloffset[ui + 1] +
+             K.T.phixstarget_levelindex[K.T.level_phixstargets_offset[ul] + j];
+      return MA_CONTINUE;
+    }
+  }
+}
+
 DEVFN void ma_lane_init(const Ctx &K, MaLane &m, int where, int element, int ion, int level) {
   m.mgi = cell_mgi(K, where);
   m.k = K.C.ne_index[m.mgi];
@@ -1119,10 +1238,11 @@ DEVNI void ma_finish(Tx &x, Pkt &p, const MaEnd &e, unsigned jumps) {
   const int element = p.ma_element;
   p.interactions += (int)jumps;
   if (e.code == MA_END_BB) {
-    const int linelistindex = e.a, ion = e.ion, level = e.b;
+    const int linelistindex = e.a, ul = e.b;
+    const int ion = K.T.level_ui[ul] - K.T.elem_uniqueionoffset[element];
     if (K.R.record_linestat) atomicAdd(&K.E.ecounter[linelistindex], 1);
     const int lower = K.T.line_lower[linelistindex];
-    const double epsilon_trans = epsilon(K, element, ion, level) - epsilon(K, element, ion, lower);
+    const double epsilon_trans = K.T.level_epsilon[ul] - epsilon(K, element, ion, lower);
     double oldnucmf = 0.;
     if (p.last_event == 1) oldnucmf = p.nu_cmf;
     p.nu_cmf = epsilon_trans / ARTIS_H;
@@ -1145,7 +1265,9 @@ DEVNI void ma_finish(Tx &x, Pkt &p, const MaEnd &e, unsigned jumps) {
     p.type = ARTIS_TYPE_KPKT;
     safeadd(&K.E.colheat[cell_mgi(K, p.where)], p.e_cmf);
   } else if (e.code == MA_END_FB) {
-    const int ion = e.ion, lower = e.a, upperionlevel = e.b;
+    const int uiu = K.T.level_ui[e.b];
+    const int ion = uiu - K.T.elem_uniqueionoffset[element] - 1, lower = e.a;
+    const int upperionlevel = e.b - K.T.ion_uniqueleveloffset[uiu];
     const float T_e = K.C.Te[cell_mgi(K, p.where)];
     p.nu_cmf = select_continuum_nu(x, element, ion, lower, upperionlevel, T_e);
     lctr(x.L, CTR_MA_STAT_DEACTIVATION_FB);
@@ -1184,26 +1306,41 @@ DEVNI void do_macroatom(Tx &x, Pkt &p) {
     x.err(ERR_THICK_MA, p.number, mgi);
     return;
   }
-  MaLane m;
-  ma_lane_init(K, m, p.where, p.ma_element, p.ma_ion, p.ma_level);
-  const double t_mid = K.G.ts_mid[x.nts];
   MaEnd e;
   e.code = MA_CONTINUE;
   int r;
-  while ((r = (K.C.have_macache ? ma_jump<true>(K, x.L, x.rng, m, t_mid, e, p.number)
-                                 : ma_jump<false>(K, x.L, x.rng, m, t_mid, e, p.number))) == MA_CONTINUE) {
-    if (m.jumps >= MA_MAX_JUMPS) {
-      x.err(ERR_STUCK, p.number, 2);
-      return;
+  unsigned jumps;
+  unsigned long long ntrans;
+  if (K.C.have_macache) {
+    MaLaneC m;
+    m.ul = ulev(K, p.ma_element, p.ma_ion, p.ma_level);
+    m.block = K.C.ma_rec + (int64_t)K.C.ne_index[mgi] * K.C.ma_rec_stride;
+    m.jumps = 0;
+    m.ntrans = 0;
+    while ((r = ma_jump_cached(K, x.L, x.rng, m, e, p.number)) == MA_CONTINUE && m.jumps < MA_MAX_JUMPS) {
     }
+    jumps = m.jumps;
+    ntrans = m.ntrans;
+  } else {
+    MaLane m;
+    ma_lane_init(K, m, p.where, p.ma_element, p.ma_ion, p.ma_level);
+    const double t_mid = K.G.ts_mid[x.nts];
+    while ((r = ma_jump<false>(K, x.L, x.rng, m, t_mid, e, p.number)) == MA_CONTINUE && m.jumps < MA_MAX_JUMPS) {
+    }
+    jumps = m.jumps;
+    ntrans = m.ntrans;
   }
-  lwork(x.L, WK_MA_JUMPS, m.jumps);
-  lwork(x.L, WK_MA_TRANS, m.ntrans);
+  if (r == MA_CONTINUE) {
+    x.err(ERR_STUCK, p.number, 2);
+    return;
+  }
+  lwork(x.L, WK_MA_JUMPS, jumps);
+  lwork(x.L, WK_MA_TRANS, ntrans);
   if (r == MA_FAILED) {
     x.ok = false;
     return;
   }
-  ma_finish(x, p, e, m.jumps);
+  ma_finish(x, p, e, jumps);
 }
 
 // ------------------------------------------------------------------------------------------ k-packets

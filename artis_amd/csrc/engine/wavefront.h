@@ -31,12 +31,36 @@ struct WaveState {
   uint32_t *pend_jumps;// [N] macro-atom loop passes of that deactivation
   int32_t *q[NQUEUES]; // [N] packet indices per state
   uint32_t *ctr;       // [NQUEUES * 2]: appended count, fetch head
+  // macro-atom queue binned by cell before k_ma (counting sort, order within a cell arbitrary)
+  int32_t *ma_key;     // [N] nonempty-cell index of each M-queue slot
+  int32_t *ma_sorted;  // [N] M queue grouped by cell (or a copy of q[QM] order when binning is off)
+  uint32_t *bins;      // [n_nonempty + 1] counts, then running offsets
+  uint32_t *xhead;     // [8] fetch heads of the per-XCD ranges of ma_sorted
+  int ma_ranges;       // 8: blocks on XCD x take range x first (then steal), 1: one shared range
+  int ma_binned;       // 1: k_ma reads ma_sorted, 0: k_ma reads q[QM]
+  int refill_min;      // a wave refetches work (and flushes its queue appends) once this many lanes are idle
+  unsigned long long *stats;  // [32] diagnostics: per kernel class c: [4c] wave loop passes, [4c+1] busy
+                              // lane-passes, [4c+2] wave cycles (s_memtime), [4c+3] refills;
+                              // [16 + 4c] cycles in refill blocks, [17 + 4c] cycles in the work step
 };
+
+DEVFN int lane_id() { return (int)__lane_id(); }
+DEVFN unsigned long long wave_clock() { return __builtin_amdgcn_s_memtime(); }
+DEVFN void wave_stats_flush(const WaveState &W, int c, unsigned long long passes, unsigned long long busy,
+                            unsigned long long t0, unsigned long long refills, unsigned long long trefill,
+                            unsigned long long tstep) {
+  if (lane_id() == 0) {
+    atomicAdd(&W.stats[4 * c], passes);
+    atomicAdd(&W.stats[4 * c + 1], busy);
+    atomicAdd(&W.stats[4 * c + 2], wave_clock() - t0);
+    atomicAdd(&W.stats[4 * c + 3], refills);
+    atomicAdd(&W.stats[16 + 4 * c], trefill);
+    atomicAdd(&W.stats[17 + 4 * c], tstep);
+  }
+}
 
 #define WAVE_BLOCK 256
 #define RPKT_MAX_STEPS 2000000
-
-DEVFN int lane_id() { return (int)__lane_id(); }
 
 // wave-aggregated reservation of one slot per lane with `pred` from counter *c; returns the lane's slot
 DEVFN uint32_t wave_reserve(uint32_t *c, bool pred) {
@@ -111,7 +135,8 @@ DEVFN void apply_pending(Tx &x, const WaveState &W, int32_t idx, Pkt &p) {
     e.ion = pd.y;
     e.a = pd.z;
     e.b = pd.w;
-    ma_finish(x, p, e, W.pend_jumps[idx]);
+    const unsigned jumps = W.pend_jumps[idx];
+    cold_call(x, p, [&](Tx &tx, Pkt &tp) { ma_finish(tx, tp, e, jumps); });
     W.pend[idx].x = 0;
   }
 }
@@ -131,28 +156,47 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_rpkt(Ctx K, WaveState W, uint64_
   const uint32_t nq = W.ctr[2 * QR];
   Pkt p;
   int32_t idx = -1;
-  bool have = false, drained = false;
+  bool have = false, drained = false, pendM = false, pendK = false;
   int steps = 0;
   double cmf_lum = 0.;
+  unsigned long long st_pass = 0, st_busy = 0, st_refill = 0, st_trefill = 0, st_tstep = 0;
+  unsigned long long st_lmax = 0, st_lsum = 0, st_bmax = 0, st_bsum = 0;
+  const unsigned long long st_t0 = wave_clock();
   while (true) {
-    const bool need = !have && !drained;
-    const uint32_t slot = wave_reserve(&W.ctr[2 * QR + 1], need);
-    if (need) {
-      if (slot < nq) {
-        idx = W.q[QR][slot];
-        pkt_load(soa, n, idx, p);
-        x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
-        x.rng.n = W.rng_n[idx];
-        x.ok = true;
-        steps = 0;
-        have = true;
-        apply_pending(x, W, idx, p);
-      } else {
-        drained = true;
+    // refill only when enough lanes are idle: a refetch costs a queue atomic, the queue read and the record
+    // load -- paying that on every pass for one or two finished lanes would dominate the step
+    const bool idle = !have && !drained;
+    const unsigned long long imask = __ballot(idle);
+    if (!__any(have) || __popcll(imask) >= W.refill_min) {
+      st_refill++;
+      const unsigned long long tr0 = wave_clock();
+      wave_push(W, QM, pendM, idx);  // appends deferred from the lanes' last retirement
+      wave_push(W, QK, pendK, idx);
+      pendM = pendK = false;
+      if (imask) {
+        const uint32_t slot = wave_reserve(&W.ctr[2 * QR + 1], idle);
+        if (idle) {
+          if (slot < nq) {
+            idx = W.q[QR][slot];
+            pkt_load(soa, n, idx, p);
+            x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
+            x.rng.n = W.rng_n[idx];
+            x.ok = true;
+            steps = 0;
+            have = true;
+            apply_pending(x, W, idx, p);
+          } else {
+            drained = true;
+          }
+        }
       }
+      st_trefill += wave_clock() - tr0;
+      if (!__any(have)) break;  // every lane is drained and its appends are flushed
     }
-    if (!__any(have)) break;
-    bool toM = false, toK = false;
+    st_pass++;
+    st_busy += __popcll(__ballot(have));
+    const unsigned long long ts0 = wave_clock();
+    x.wl = x.wb = 0;
     if (have) {
       if (x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
         do_rpkt_step(x, p, t2);
@@ -166,15 +210,34 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_rpkt(Ctx K, WaveState W, uint64_
         pkt_store(soa, n, idx, p);
         W.rng_n[idx] = x.rng.n;
         if (x.ok && p.prop_time < t2) {
-          toM = p.type == ARTIS_TYPE_MA;
-          toK = p.type == ARTIS_TYPE_KPKT || p.type == ARTIS_TYPE_PRE_KPKT;
+          pendM = p.type == ARTIS_TYPE_MA;
+          pendK = p.type == ARTIS_TYPE_KPKT || p.type == ARTIS_TYPE_PRE_KPKT;
         }
         have = false;
       }
     }
-    wave_push(W, QM, toM, idx);
-    wave_push(W, QK, toK, idx);
+    st_tstep += wave_clock() - ts0;
+    {
+      unsigned ml = x.wl, sl = x.wl, mb = x.wb, sb = x.wb;
+      for (int off = 32; off > 0; off >>= 1) {
+        ml = max(ml, (unsigned)__shfl_xor((int)ml, off, 64));
+        sl += (unsigned)__shfl_xor((int)sl, off, 64);
+        mb = max(mb, (unsigned)__shfl_xor((int)mb, off, 64));
+        sb += (unsigned)__shfl_xor((int)sb, off, 64);
+      }
+      st_lmax += ml;
+      st_lsum += sl;
+      st_bmax += mb;
+      st_bsum += sb;
+    }
   }
+  if (lane_id() == 0) {
+    atomicAdd(&W.stats[24], st_lmax);
+    atomicAdd(&W.stats[25], st_lsum);
+    atomicAdd(&W.stats[26], st_bmax);
+    atomicAdd(&W.stats[27], st_bsum);
+  }
+  wave_stats_flush(W, 0, st_pass, st_busy, st_t0, st_refill, st_trefill, st_tstep);
   for (int off = 32; off > 0; off >>= 1) cmf_lum += __shfl_down(cmf_lum, off, 64);
   if ((threadIdx.x & 63) == 0) s_cmflum[threadIdx.x >> 6] = cmf_lum;
   __syncthreads();
@@ -186,10 +249,30 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_rpkt(Ctx K, WaveState W, uint64_
   block_counters_flush(K, s_ctr, s_work);
 }
 
-// macro-atoms: persistent lanes, one jump per loop pass, lane state = MaLane + RNG counter
-template <bool CACHE>
-__global__ __launch_bounds__(WAVE_BLOCK) void k_ma(Ctx K, WaveState W, const uint64_t *__restrict__ soa, int64_t n,
-                                                   int nts) {
+// bin the M queue by cell: count per cell and remember each slot's key
+__global__ void k_ma_bin(Ctx K, WaveState W, const uint64_t *__restrict__ soa) {
+  const uint32_t nq = W.ctr[2 * QM];
+  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x) {
+    const int32_t idx = W.q[QM][slot];
+    const int k = K.C.ne_index[cell_mgi(K, lo32(soa[idx]))];
+    W.ma_key[slot] = k;
+    atomicAdd(&W.bins[k], 1u);
+  }
+}
+// scatter into cell order using the exclusive prefix sum of the counts
+__global__ void k_ma_scatter(WaveState W, uint32_t *offs) {
+  const uint32_t nq = W.ctr[2 * QM];
+  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x)
+    W.ma_sorted[atomicAdd(&offs[W.ma_key[slot]], 1u)] = W.q[QM][slot];
+}
+
+// macro-atoms: persistent lanes, one jump per loop pass, lane state = MaLane + RNG counter.
+// The (binned) queue is cut into W.ma_ranges contiguous ranges; blocks start on range blockIdx % 8 -- the
+// XCD the block was dispatched to under round-robin placement, so one XCD's L2 sees a contiguous run of
+// cells -- and steal from the following ranges once theirs is exhausted.
+template <bool CACHE, int MINW>
+__global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(Ctx K, WaveState W, const uint64_t *__restrict__ soa,
+                                                         int64_t n, int nts) {
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   block_counters_init(s_ctr, s_work);
@@ -197,55 +280,99 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_ma(Ctx K, WaveState W, const uin
   L.ctr = &s_ctr[0];
   L.work = &s_work[0];
   const uint32_t nq = W.ctr[2 * QM];
+  const int32_t *queue = W.ma_binned ? W.ma_sorted : W.q[QM];
+  const int nr = W.ma_ranges;
   const double t_mid = K.G.ts_mid[nts];
-  MaLane m;
+  MaLane m;    // uncached walk
+  MaLaneC mc;  // cached walk
   artis_rng rng = artis_rng_init(K.R.seed, 0, nts, K.R.rank);
   int32_t idx = -1;
   bool have = false, drained = false;
+  int cur = (int)(blockIdx.x % (unsigned)nr), tried = 0;
+  bool pendR = false, pendK = false;
   unsigned long long jumps_sum = 0, trans_sum = 0;
+  unsigned long long st_pass = 0, st_busy = 0, st_refill = 0, st_trefill = 0, st_tstep = 0;
+  const unsigned long long st_t0 = wave_clock();
   while (true) {
-    const bool need = !have && !drained;
-    const uint32_t slot = wave_reserve(&W.ctr[2 * QM + 1], need);
-    if (need) {
-      if (slot < nq) {
-        idx = W.q[QM][slot];
-        const int where = lo32(soa[idx]);
-        const uint64_t w36 = soa[36 * n + idx];
-        const uint64_t w37 = soa[37 * n + idx];
-        rng.key1 = (uint32_t)hi32(soa[33 * n + idx]);  // packet number
-        rng.n = W.rng_n[idx];
-        ma_lane_init(K, m, where, lo32(w36), hi32(w36), lo32(w37));
-        have = true;
-        if (K.C.thick[m.mgi] == 1) {
-          fail(K, ERR_THICK_MA, (int)rng.key1, m.mgi);
-          have = false;
+    const bool idle = !have && !drained;
+    const unsigned long long imask = __ballot(idle);
+    if (!__any(have) || __popcll(imask) >= W.refill_min) {
+      st_refill++;
+      const unsigned long long tr0 = wave_clock();
+      wave_push(W, QR, pendR, idx);
+      wave_push(W, QK, pendK, idx);
+      pendR = pendK = false;
+      if (imask) {
+        const uint32_t lo = (uint32_t)((uint64_t)nq * cur / nr), hi = (uint32_t)((uint64_t)nq * (cur + 1) / nr);
+        const uint32_t slot = wave_reserve(&W.xhead[cur], idle);
+        const bool got = idle && lo + slot < hi;
+        if (got) {
+          idx = queue[lo + slot];
+          const int where = lo32(soa[idx]);
+          const uint64_t w36 = soa[36 * n + idx];
+          const uint64_t w37 = soa[37 * n + idx];
+          rng.key1 = (uint32_t)hi32(soa[33 * n + idx]);  // packet number
+          rng.n = W.rng_n[idx];
+          const int mgi = cell_mgi(K, where);
+          if constexpr (CACHE) {
+            mc.ul = ulev(K, lo32(w36), hi32(w36), lo32(w37));
+            mc.block = K.C.ma_rec + (int64_t)K.C.ne_index[mgi] * K.C.ma_rec_stride;
+            mc.jumps = 0;
+            mc.ntrans = 0;
+          } else {
+            ma_lane_init(K, m, where, lo32(w36), hi32(w36), lo32(w37));
+          }
+          have = true;
+          if (K.C.thick[mgi] == 1) {
+            fail(K, ERR_THICK_MA, (int)rng.key1, mgi);
+            have = false;
+          }
         }
-      } else {
-        drained = true;
+        if (__any(idle && !got)) {  // this range is used up: move on (wave-uniform)
+          cur = (cur + 1) % nr;
+          if (++tried >= nr) drained = true;
+        }
+      }
+      st_trefill += wave_clock() - tr0;
+      if (!__any(have)) {
+        if (drained) break;
+        continue;
       }
     }
-    if (!__any(have)) break;
-    bool toR = false, toK = false;
+    st_pass++;
+    st_busy += __popcll(__ballot(have));
+    const unsigned long long ts0 = wave_clock();
     if (have) {
       MaEnd e;
-      const int r = ma_jump<CACHE>(K, L, rng, m, t_mid, e, (int)rng.key1);
-      if (r != MA_CONTINUE || m.jumps >= MA_MAX_JUMPS) {
+      int r;
+      unsigned jumps;
+      if constexpr (CACHE) {
+        r = ma_jump_cached(K, L, rng, mc, e, (int)rng.key1);
+        jumps = mc.jumps;
+      } else {
+        r = ma_jump<false>(K, L, rng, m, t_mid, e, (int)rng.key1);
+        jumps = m.jumps;
+      }
+      if (r != MA_CONTINUE || jumps >= MA_MAX_JUMPS) {
         if (r == MA_CONTINUE) fail(K, ERR_STUCK, (int)rng.key1, 2);
         if (r > 0) {
           W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
-          W.pend_jumps[idx] = m.jumps;
+          W.pend_jumps[idx] = jumps;
           W.rng_n[idx] = rng.n;
-          toR = (r == MA_END_BB || r == MA_END_FB);
-          toK = (r == MA_END_COLDEEXC || r == MA_END_COLRECOMB);
+          pendR = (r == MA_END_BB || r == MA_END_FB);
+          pendK = (r == MA_END_COLDEEXC || r == MA_END_COLRECOMB);
         }
-        jumps_sum += m.jumps;
-        trans_sum += m.ntrans;
+        jumps_sum += jumps;
+        if constexpr (CACHE)
+          trans_sum += mc.ntrans;
+        else
+          trans_sum += m.ntrans;
         have = false;
       }
     }
-    wave_push(W, QR, toR, idx);
-    wave_push(W, QK, toK, idx);
+    st_tstep += wave_clock() - ts0;
   }
+  wave_stats_flush(W, 1, st_pass, st_busy, st_t0, st_refill, st_trefill, st_tstep);
   if (jumps_sum) atomicAdd(&s_work[WK_MA_JUMPS], jumps_sum);
   if (trans_sum) atomicAdd(&s_work[WK_MA_TRANS], trans_sum);
   block_counters_flush(K, s_ctr, s_work);

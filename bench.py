@@ -86,6 +86,7 @@ def main():
     precompute_ms = []
     work = np.zeros(16, dtype=np.int64)
     rounds = []
+    ktimes = []
 
     def step(record):
         eng.restore()
@@ -101,6 +102,7 @@ def main():
             precompute_ms.append(eng.last_precompute_ms())
             work[:] = eng.last_work()
             rounds.append(eng.last_rounds())
+            ktimes.append(eng.last_kernel_times())
 
     for _ in range(args.warmup):
         step(False)
@@ -196,6 +198,7 @@ def main():
             "precompute_ms": float(np.mean(precompute_ms)),
             "transport_ms": float(np.mean(transport_ms)),
             "event_rounds": int(np.max(rounds)) if rounds else 0,
+            "kernel_ms": {k: float(np.mean([kt[k][0] for kt in ktimes])) for k in ktimes[0]} if ktimes else {},
             "work_per_packet": {k: float(v) / max(P, 1) for k, v in zip(
                 ["active", "rpkt_steps", "lines_scanned", "line_taus", "kappa_evals", "bf_active", "est_segments",
                  "gc_updates", "ma_jumps", "ma_trans", "kpkt", "kpkt_terms", "escaped", "es_scat", "bb_events",

@@ -324,6 +324,9 @@ double artis_gpu_last_precompute_ms(void);
 #define ARTIS_WORK_COUNT 16
 int artis_gpu_last_work_counts(int64_t out[ARTIS_WORK_COUNT]);
 int64_t artis_gpu_last_rounds(void);  /* event-queue rounds of the last update (0: megakernel path) */
+/* device time (ms, HIP events around every launch) and launch count of the last update per kernel class:
+ * [0] r-packet, [1] macro-atom (incl. cell binning), [2] k-packet, [3] classify */
+int artis_gpu_last_kernel_times(double ms[4], int64_t launches[4]);
 const char *artis_gpu_last_error(void);
 int artis_gpu_abi_version(void);
 
