@@ -117,4 +117,120 @@ __device__ __forceinline__ void pkt_store(uint64_t *__restrict__ soa, int64_t n,
 #undef W
 }
 
+// Hot/cold split for the r-packet kernel.  Hot words are what the propagation step reads; cold words
+// (emission / absorption bookkeeping, polarisation, escape record, macro-atom state) are only read by the rare
+// event code, which runs on a copy assembled from the hot registers plus the cold words in HBM.
+__device__ __forceinline__ void pkt_load_hot(const uint64_t *__restrict__ soa, int64_t n, int64_t i, Pkt &p) {
+#define W(k) soa[(int64_t)(k) * n + i]
+  uint64_t w;
+  w = W(0);
+  p.where = lo32(w);
+  p.type = hi32(w);
+  w = W(1);
+  p.last_cross = lo32(w);
+  p.interactions = hi32(w);
+  w = W(2);
+  p.nscatterings = lo32(w);
+  p.last_event = hi32(w);
+  for (int d = 0; d < 3; d++) p.pos[d] = asd(W(3 + d));
+  for (int d = 0; d < 3; d++) p.dir[d] = asd(W(6 + d));
+  p.e_cmf = asd(W(9));
+  p.e_rf = asd(W(10));
+  p.nu_cmf = asd(W(11));
+  p.nu_rf = asd(W(12));
+  w = W(13);
+  p.next_trans = lo32(w);
+  p.emissiontype = hi32(w);
+  p.prop_time = asd(W(18));
+  w = W(33);
+  p.scat_count = lo32(w);
+  p.number = hi32(w);
+#undef W
+}
+__device__ __forceinline__ void pkt_store_hot(uint64_t *__restrict__ soa, int64_t n, int64_t i, const Pkt &p) {
+#define W(k) soa[(int64_t)(k) * n + i]
+  W(0) = pack2(p.where, p.type);
+  W(1) = pack2(p.last_cross, p.interactions);
+  W(2) = pack2(p.nscatterings, p.last_event);
+  for (int d = 0; d < 3; d++) W(3 + d) = asw(p.pos[d]);
+  for (int d = 0; d < 3; d++) W(6 + d) = asw(p.dir[d]);
+  W(9) = asw(p.e_cmf);
+  W(10) = asw(p.e_rf);
+  W(11) = asw(p.nu_cmf);
+  W(12) = asw(p.nu_rf);
+  W(13) = pack2(p.next_trans, p.emissiontype);
+  W(18) = asw(p.prop_time);
+  W(33) = pack2(p.scat_count, p.number);
+#undef W
+}
+__device__ __forceinline__ void pkt_load_cold(const uint64_t *__restrict__ soa, int64_t n, int64_t i, Pkt &p) {
+#define W(k) soa[(int64_t)(k) * n + i]
+  uint64_t w;
+  for (int d = 0; d < 3; d++) p.em_pos[d] = asd(W(14 + d));
+  w = W(17);
+  p.em_time = lo32(w);
+  p.pad0 = hi32(w);
+  w = W(19);
+  p.absorptiontype = lo32(w);
+  p.trueemissiontype = hi32(w);
+  w = W(20);
+  p.trueem_time = lo32(w);
+  p.pad1 = hi32(w);
+  p.absorptionfreq = asd(W(21));
+  for (int d = 0; d < 3; d++) p.absorptiondir[d] = asd(W(22 + d));
+  for (int d = 0; d < 3; d++) p.stokes[d] = asd(W(25 + d));
+  for (int d = 0; d < 3; d++) p.pol_dir[d] = asd(W(28 + d));
+  w = W(32);
+  p.escape_type = lo32(w);
+  p.escape_time = hi32(w);
+  w = W(35);
+  p.pellet_nucindex = lo32(w);
+  p.trueemissionvelocity = __int_as_float(hi32(w));
+  w = W(36);
+  p.ma_element = lo32(w);
+  p.ma_ion = hi32(w);
+  w = W(37);
+  p.ma_level = lo32(w);
+  p.ma_activatingline = hi32(w);
+#undef W
+}
+__device__ __forceinline__ void pkt_store_cold(uint64_t *__restrict__ soa, int64_t n, int64_t i, const Pkt &p) {
+#define W(k) soa[(int64_t)(k) * n + i]
+  for (int d = 0; d < 3; d++) W(14 + d) = asw(p.em_pos[d]);
+  W(17) = pack2(p.em_time, p.pad0);
+  W(19) = pack2(p.absorptiontype, p.trueemissiontype);
+  W(20) = pack2(p.trueem_time, p.pad1);
+  W(21) = asw(p.absorptionfreq);
+  for (int d = 0; d < 3; d++) W(22 + d) = asw(p.absorptiondir[d]);
+  for (int d = 0; d < 3; d++) W(25 + d) = asw(p.stokes[d]);
+  for (int d = 0; d < 3; d++) W(28 + d) = asw(p.pol_dir[d]);
+  W(32) = pack2(p.escape_type, p.escape_time);
+  W(35) = pack2(p.pellet_nucindex, __float_as_int(p.trueemissionvelocity));
+  W(36) = pack2(p.ma_element, p.ma_ion);
+  W(37) = pack2(p.ma_level, p.ma_activatingline);
+#undef W
+}
+// hot fields only (the cold ones of `dst` are left as they are)
+__device__ __forceinline__ void pkt_copy_hot(Pkt &dst, const Pkt &src) {
+  dst.where = src.where;
+  dst.type = src.type;
+  dst.last_cross = src.last_cross;
+  dst.interactions = src.interactions;
+  dst.nscatterings = src.nscatterings;
+  dst.last_event = src.last_event;
+  for (int d = 0; d < 3; d++) {
+    dst.pos[d] = src.pos[d];
+    dst.dir[d] = src.dir[d];
+  }
+  dst.e_cmf = src.e_cmf;
+  dst.e_rf = src.e_rf;
+  dst.nu_cmf = src.nu_cmf;
+  dst.nu_rf = src.nu_rf;
+  dst.next_trans = src.next_trans;
+  dst.emissiontype = src.emissiontype;
+  dst.prop_time = src.prop_time;
+  dst.scat_count = src.scat_count;
+  dst.number = src.number;
+}
+
 #endif

@@ -44,6 +44,34 @@ DEVFN void cold_call(Tx &x, Pkt &p, F &&f) {
   x.ok = tx.ok;
 }
 
+// cold-call policies for do_rpkt_step: the full packet is in registers (megakernel) ...
+struct ColdFull {
+  template <typename F>
+  DEVFN void operator()(Tx &x, Pkt &p, F &&f) const {
+    cold_call(x, p, f);
+  }
+};
+// ... or only its hot words are (k_rpkt): the copy is completed from, and written back to, the record in HBM
+struct ColdSoa {
+  uint64_t *soa;
+  int64_t n, idx;
+  template <typename F>
+  DEVFN void operator()(Tx &x, Pkt &p, F &&f) const {
+    Tx tx(x.K, x.L);
+    tx.rng = x.rng;
+    tx.nts = x.nts;
+    tx.ok = x.ok;
+    Pkt tp;
+    pkt_copy_hot(tp, p);
+    pkt_load_cold(soa, n, idx, tp);
+    f(tx, tp);
+    pkt_store_cold(soa, n, idx, tp);
+    pkt_copy_hot(p, tp);
+    x.rng = tx.rng;
+    x.ok = tx.ok;
+  }
+};
+
 // ------------------------------------------------------------------------------------------ emission
 // rpkt.cc:975-1025
 DEVFN void emitt_rpkt(Tx &x, Pkt &p) {
@@ -709,7 +737,8 @@ DEVFN void rpkt_event_boundbound(Tx &x, Pkt &p) {
 }
 
 // rpkt.cc:623-813
-DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2) {
+template <typename Cold = ColdFull>
+DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
   const Ctx &K = x.K;
   const int npm = K.G.npts_model;
   int mgi = cell_mgi(K, p.where);
@@ -780,7 +809,7 @@ DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2) {
     if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_BB)
       rpkt_event_boundbound(x, p);
     else if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_CONT)
-      cold_call(x, p, [&](Tx &tx, Pkt &tp) {
+      cold(x, p, [&](Tx &tx, Pkt &tp) {
         const Kappa kc = kap;
         rpkt_event_continuum(tx, tp, kc, k, mgi);
       });

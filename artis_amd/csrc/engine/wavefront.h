@@ -127,7 +127,8 @@ __global__ void k_classify(Ctx K, WaveState W, uint64_t *__restrict__ soa, int64
   block_counters_flush(K, s_ctr, s_work);
 }
 
-DEVFN void apply_pending(Tx &x, const WaveState &W, int32_t idx, Pkt &p) {
+template <typename Cold>
+DEVFN void apply_pending(Tx &x, const WaveState &W, int32_t idx, Pkt &p, const Cold &cold) {
   const int4 pd = W.pend[idx];
   if (pd.x != 0) {
     MaEnd e;
@@ -136,7 +137,7 @@ DEVFN void apply_pending(Tx &x, const WaveState &W, int32_t idx, Pkt &p) {
     e.a = pd.z;
     e.b = pd.w;
     const unsigned jumps = W.pend_jumps[idx];
-    cold_call(x, p, [&](Tx &tx, Pkt &tp) { ma_finish(tx, tp, e, jumps); });
+    cold(x, p, [&](Tx &tx, Pkt &tp) { ma_finish(tx, tp, e, jumps); });
     W.pend[idx].x = 0;
   }
 }
@@ -178,13 +179,13 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_rpkt(Ctx K, WaveState W, uint64_
         if (idle) {
           if (slot < nq) {
             idx = W.q[QR][slot];
-            pkt_load(soa, n, idx, p);
+            pkt_load_hot(soa, n, idx, p);
             x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
             x.rng.n = W.rng_n[idx];
             x.ok = true;
             steps = 0;
             have = true;
-            apply_pending(x, W, idx, p);
+            apply_pending(x, W, idx, p, ColdSoa{soa, n, idx});
           } else {
             drained = true;
           }
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_rpkt(Ctx K, WaveState W, uint64_
     x.wl = x.wb = 0;
     if (have) {
       if (x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
-        do_rpkt_step(x, p, t2);
+        do_rpkt_step(x, p, t2, ColdSoa{soa, n, idx});
         if (++steps > RPKT_MAX_STEPS) x.err(ERR_STUCK, p.number, 1);
       }
       if (!x.ok || p.type != ARTIS_TYPE_RPKT || !(p.prop_time < t2)) {
@@ -207,7 +208,17 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_rpkt(Ctx K, WaveState W, uint64_
           cmf_lum += p.e_cmf;
           lwork(L, WK_ESCAPED, 1);
         }
-        pkt_store(soa, n, idx, p);
+        pkt_store_hot(soa, n, idx, p);
+        // cold fields the propagation step itself writes: the escape record (change_cell, boundary.cc:332-357)
+        // and the absorption record + macro-atom state of a line absorption (get_event / rpkt_event_boundbound)
+        if (p.type == ARTIS_TYPE_ESCAPE) soa[32 * n + idx] = pack2(p.escape_type, p.escape_time);
+        if (p.type == ARTIS_TYPE_MA) {
+          reinterpret_cast<int32_t *>(&soa[19 * n + idx])[0] = p.absorptiontype;
+          soa[21 * n + idx] = asw(p.absorptionfreq);
+          for (int d = 0; d < 3; d++) soa[(22 + d) * n + idx] = asw(p.absorptiondir[d]);
+          soa[36 * n + idx] = pack2(p.ma_element, p.ma_ion);
+          soa[37 * n + idx] = pack2(p.ma_level, p.ma_activatingline);
+        }
         W.rng_n[idx] = x.rng.n;
         if (x.ok && p.prop_time < t2) {
           pendM = p.type == ARTIS_TYPE_MA;
@@ -396,7 +407,7 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_kpkt(Ctx K, WaveState W, uint64_
     x.nts = nts;
     x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
     x.rng.n = W.rng_n[idx];
-    apply_pending(x, W, idx, p);
+    apply_pending(x, W, idx, p, ColdFull());
     int guard = 0;
     while (x.ok && (p.type == ARTIS_TYPE_KPKT || p.type == ARTIS_TYPE_PRE_KPKT) && p.prop_time < t2) {
       const int mgi = cell_mgi(K, p.where);
