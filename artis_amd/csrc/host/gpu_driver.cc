@@ -1,0 +1,84 @@
+// gpu_driver.cc -- a C++ host that drives the engine the way sn3d.cc's timestep loop does (sn3d.cc:540-650):
+// per timestep update_grid (here: the synthetic LTE stand-in) -> upload_cellstate -> zero_estimators ->
+// update_packets -> write the raw packet file.  It exercises the C++ mirror (update_packets_gpu.h) without
+// Python.  Usage:
+//   artis_gpu_driver <outdir> <ngrid> <nlevels_per_ion> <n_ionising> <max_lines> <ntstep> <nts0> <nsteps>
+//                    <npkts> <seed>
+// Writes <outdir>/packets_0000_ts<nts>.tmp (raw 304-byte records, sn3d.cc:387-398) after every timestep and
+// prints one summary line per timestep.
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "artis_layout_check.h"
+#include "model_synth.h"
+#include "update_packets_gpu.h"
+
+int main(int argc, char **argv) {
+  if (argc != 11) {
+    std::fprintf(stderr, "usage: %s outdir ngrid nlevels_per_ion n_ionising max_lines ntstep nts0 nsteps npkts seed\n",
+                 argv[0]);
+    return 2;
+  }
+  const std::string outdir = argv[1];
+  artis_synth_config cfg;
+  artis_synth_default_config(&cfg);
+  cfg.ngrid_1d = std::atoi(argv[2]);
+  cfg.nlevels_per_ion = std::atoi(argv[3]);
+  cfg.n_ionising = std::atoi(argv[4]);
+  cfg.max_lines = std::atoi(argv[5]);
+  cfg.ntstep = std::atoi(argv[6]);
+  const int nts0 = std::atoi(argv[7]), nsteps = std::atoi(argv[8]), npkts = std::atoi(argv[9]);
+  const uint64_t seed = std::strtoull(argv[10], nullptr, 10);
+
+  artis_model *m = artis_model_synth(&cfg);
+  if (!m) {
+    std::fprintf(stderr, "model synthesis failed\n");
+    return 1;
+  }
+  const artis_atomic_tables &at = *artis_model_atomic(m);
+  artis_run_params rp;
+  artis_model_run_params(m, &rp);
+  const int64_t np = artis_model_npts_model(m);
+  const int64_t nion = np * at.nelements * at.maxnions;
+  std::vector<double> J(np), nuJ(np), ff(np), col(np), gam(nion), bfh(nion);
+  std::vector<int32_t> ec(at.nlines), ac(at.nlines);
+  std::vector<artis_packet> packets(npkts);
+  if (artis_model_init_rpackets(m, nts0, npkts, seed, 1e45, packets.data()) != 0) return 1;
+
+  {
+    artis_amd::PacketEngine engine(0, at, *artis_model_geometry(m), rp);
+    for (int nts = nts0; nts < nts0 + nsteps && nts < cfg.ntstep; nts++) {
+      artis_amd::check(artis_model_set_timestep(m, nts), "update_grid stand-in");
+      engine.upload_cellstate(nts, *artis_model_cellstate(m));
+      // zero_estimators (emissivities.cc:138-170)
+      artis_estimators est{};
+      for (auto *v : {&J, &nuJ, &ff, &col, &gam, &bfh}) std::fill(v->begin(), v->end(), 0.);
+      std::fill(ec.begin(), ec.end(), 0);
+      std::fill(ac.begin(), ac.end(), 0);
+      est.J = J.data();
+      est.nuJ = nuJ.data();
+      est.ffheatingestimator = ff.data();
+      est.colheatingestimator = col.data();
+      est.gammaestimator = gam.data();
+      est.bfheatingestimator = bfh.data();
+      est.ecounter = ec.data();
+      est.acounter = ac.data();
+      engine.update_packets(rp.rank, nts, packets.data(), npkts, est);
+      double jsum = 0.;
+      for (double v : J) jsum += v;
+      const std::string path = outdir + "/packets_0000_ts" + std::to_string(nts) + ".tmp";
+      FILE *f = std::fopen(path.c_str(), "wb");
+      if (!f || std::fwrite(packets.data(), sizeof(artis_packet), npkts, f) != (size_t)npkts) {
+        std::fprintf(stderr, "cannot write %s\n", path.c_str());
+        return 1;
+      }
+      std::fclose(f);
+      std::printf("nts %d nesc %lld cmf_lum %.17g Jsum %.17g transport_ms %.3f\n", nts, (long long)est.nesc,
+                  est.cmf_lum, jsum, engine.last_transport_ms());
+    }
+  }
+  artis_model_free(m);
+  return 0;
+}

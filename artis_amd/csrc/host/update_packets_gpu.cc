@@ -1,0 +1,37 @@
+// update_packets_gpu.cc -- see update_packets_gpu.h
+#include "update_packets_gpu.h"
+
+#include <cstdio>
+#include <cstdlib>
+
+#include "artis_layout_check.h"
+
+namespace artis_amd {
+
+void check(int rc, const char *what) {
+  if (rc != 0) {
+    std::fprintf(stderr, "[artis_gpu] %s failed (status %d): %s\n", what, rc, artis_gpu_last_error());
+    std::fflush(stderr);
+    std::abort();
+  }
+}
+
+PacketEngine::PacketEngine(int device, const artis_atomic_tables &atomic, const artis_geometry &geometry,
+                           const artis_run_params &params) {
+  check(artis_gpu_abi_version() == 1 ? 0 : ARTIS_ERR_BAD_ARGUMENT, "artis_gpu_abi_version");
+  check(artis_gpu_init(device, &atomic, &geometry, &params), "artis_gpu_init");
+}
+
+PacketEngine::~PacketEngine() { artis_gpu_finalize(); }
+
+void PacketEngine::upload_cellstate(int nts, const artis_cell_state &cells) {
+  check(artis_gpu_upload_cellstate(nts, &cells), "artis_gpu_upload_cellstate");
+}
+
+void PacketEngine::update_packets(int my_rank, int nts, artis_packet *packets, int npkts, artis_estimators &est) {
+  check(artis_gpu_update_packets(my_rank, nts, packets, npkts, &est), "artis_gpu_update_packets");
+}
+
+double PacketEngine::last_transport_ms() const { return artis_gpu_last_transport_ms(); }
+
+}  // namespace artis_amd

@@ -1,0 +1,38 @@
+// update_packets_gpu.h -- C++ host side of the drop-in: the reference's update_packets interface
+// (update_packets.h:6, called at sn3d.cc:574) on top of the C ABI of include/artis_gpu.h.
+//
+// A reference build links this file and libartis_gpu.so and replaces its update_packets call as shown in
+// INTEGRATION.md.  The error behaviour is the reference's: any failure is printed and the process aborts
+// (assert_always, sn3d.h:17-29); nothing falls back to a CPU path.
+#ifndef ARTIS_UPDATE_PACKETS_GPU_H
+#define ARTIS_UPDATE_PACKETS_GPU_H
+
+#include "artis_gpu.h"
+
+namespace artis_amd {
+
+// abort with the engine's message if rc != 0 (reference assert_always semantics)
+void check(int rc, const char *what);
+
+// One GPU's engine for the run: owns the device tables; the caller owns packets and estimator arrays.
+class PacketEngine {
+ public:
+  PacketEngine(int device, const artis_atomic_tables &atomic, const artis_geometry &geometry,
+               const artis_run_params &params);
+  ~PacketEngine();
+  PacketEngine(const PacketEngine &) = delete;
+  PacketEngine &operator=(const PacketEngine &) = delete;
+
+  // after update_grid (update_grid.cc:1270) for timestep nts
+  void upload_cellstate(int nts, const artis_cell_state &cells);
+
+  // reference update_packets(my_rank, nts, packets) with the packet count and the estimator arrays (globals::
+  // and radfield:: in the reference) made explicit; estimators are accumulated, as the reference's are
+  void update_packets(int my_rank, int nts, artis_packet *packets, int npkts, artis_estimators &est);
+
+  double last_transport_ms() const;
+};
+
+}  // namespace artis_amd
+
+#endif
