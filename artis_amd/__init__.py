@@ -13,6 +13,8 @@ from . import ffi
 
 _LIBDIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 GPU_SO = os.path.join(_LIBDIR, "libartis_gpu.so")
+# diagnostics only: load an alternative build of the same engine (e.g. the in-kernel timestamp variant)
+_GPU_SO_LOAD = os.environ.get("ARTIS_GPU_SO", GPU_SO)
 
 # every function declared in include/artis_gpu.h (tests/test_abi.py checks they are exported)
 ABI_SYMBOLS = [
@@ -31,9 +33,9 @@ def gpu_lib():
     """Load libartis_gpu.so (fails loudly if it was not built)."""
     global _gpu_lib
     if _gpu_lib is None:
-        if not os.path.exists(GPU_SO):
-            raise RuntimeError(f"{GPU_SO} missing: the HIP engine was not built (run __graft_entry__.build())")
-        L = C.CDLL(GPU_SO)
+        if not os.path.exists(_GPU_SO_LOAD):
+            raise RuntimeError(f"{_GPU_SO_LOAD} missing: the HIP engine was not built (run __graft_entry__.build())")
+        L = C.CDLL(_GPU_SO_LOAD)
         vp = C.c_void_p
         L.artis_gpu_init.argtypes = [C.c_int, vp, vp, C.POINTER(ffi.RunParams)]
         L.artis_gpu_upload_cellstate.argtypes = [C.c_int, vp]

@@ -540,7 +540,7 @@ int run_wavefront(int64_t n, int nts, double t2) {
   const WaveState &W = G.W;
   const unsigned grid = (unsigned)G.wave_grid;
   G.tev_used = 0;
-  HIPCHK(hipMemsetAsync(W.stats, 0, 32 * sizeof(unsigned long long), G.stream));
+  HIPCHK(hipMemsetAsync(W.stats, 0, 48 * sizeof(unsigned long long), G.stream));
   HIPCHK(hipMemsetAsync(W.ctr, 0, NQUEUES * 2 * sizeof(uint32_t), G.stream));
   TSTART(3);
   k_classify<<<(unsigned)((n + WAVE_BLOCK - 1) / WAVE_BLOCK), WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, t2);
@@ -601,7 +601,7 @@ int run_wavefront(int64_t n, int nts, double t2) {
   G.last_rounds = round;
   HIPCHK(hipStreamSynchronize(G.stream));
   if (getenv("ARTIS_GPU_STATS")) {
-    unsigned long long st[32];
+    unsigned long long st[48];
     HIPCHK(hipMemcpy(st, W.stats, sizeof(st), hipMemcpyDeviceToHost));
     const char *nm[2] = {"rpkt", "ma"};
     for (int c = 0; c < 2; c++)
@@ -617,6 +617,12 @@ int run_wavefront(int64_t n, int nts, double t2) {
             "lane-mean %.3f\n",
             st[0] ? (double)st[24] / st[0] : 0., st[0] ? (double)st[25] / (64.0 * st[0]) : 0.,
             st[0] ? (double)st[26] / st[0] : 0., st[0] ? (double)st[27] / (64.0 * st[0]) : 0.);
+    if (st[32] + st[33] + st[34] + st[35] + st[36])
+      fprintf(stderr,
+              "[artis_gpu] rpkt step phases (cycles/pass): boundary %.0f, kappa %.0f, line loop %.0f, move+estimators "
+              "%.0f, event %.0f\n",
+              (double)st[32] / st[0], (double)st[33] / st[0], (double)st[34] / st[0], (double)st[35] / st[0],
+              (double)st[36] / st[0]);
   }
   return tcollect();
 }
@@ -988,7 +994,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   if (!C.have_macache) rc |= dalloc(&C.marates, (size_t)nne_cells * nl * ARTIS_MA_ACTION_COUNT);
   // cell-state input buffers
   rc |= dalloc(&G.W.ctr, (size_t)NQUEUES * 2);
-  rc |= dalloc(&G.W.stats, (size_t)32);
+  rc |= dalloc(&G.W.stats, (size_t)48);
   rc |= dalloc(&G.d_cellf, (size_t)8 * np);
   rc |= dalloc(&G.d_thick, (size_t)np);
   rc |= dalloc(&G.d_abund, (size_t)np * ne);

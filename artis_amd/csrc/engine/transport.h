@@ -19,6 +19,9 @@ struct Tx {
   int nts;
   bool ok;
   unsigned wl = 0, wb = 0;  // diagnostics: lines / bf continua scanned since last reset
+#ifdef ARTIS_STAMPS
+  unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;  // diagnostic build: cycles per step phase
+#endif
   DEVFN Tx(const Ctx &k, const LocalCounters &l) : K(k), L(l), ok(true) {}
   DEVFN void err(int code, int number, int aux) {
     fail(K, code, number, aux);
@@ -71,6 +74,19 @@ struct ColdSoa {
     x.ok = tx.ok;
   }
 };
+
+#ifdef ARTIS_STAMPS
+#define STAMP(x, i)                                             \
+  do {                                                          \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    (x).st[i] += now_ - (x).tlast;                              \
+    (x).tlast = now_;                                           \
+  } while (0)
+#else
+#define STAMP(x, i) \
+  do {              \
+  } while (0)
+#endif
 
 // ------------------------------------------------------------------------------------------ emission
 // rpkt.cc:975-1025
@@ -520,14 +536,36 @@ DEVFN double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_even
   double dt = p.prop_time, dnu = p.nu_cmf;
   int dnext = p.next_trans;
   calculate_kappa_rpkt_cont(x, p, k, mgi, kap);
+  STAMP(x, 1);
   const double kap_cont = kap.total * doppler_packet(K, p);
   const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
   unsigned long long nscanned = 0, ntaus = 0;
   double result;
+  // The walk visits consecutive lines; their level populations (random gathers into the cell's pops) are
+  // fetched four lines at a time, so a long walk waits for memory once per four lines instead of per line.
+  int pf_base = -16;
+  double pf_l0 = 0, pf_l1 = 0, pf_l2 = 0, pf_l3 = 0, pf_u0 = 0, pf_u1 = 0, pf_u2 = 0, pf_u3 = 0;
   while (true) {
     const int lineindex = closest_transition(K, dnu, dnext);
     if (lineindex >= 0) {
       nscanned++;
+      if ((unsigned)(lineindex - pf_base) >= 4u) {
+        pf_base = lineindex;
+        const int nl1 = K.T.nlines - 1;
+        const int2 u0 = *reinterpret_cast<const int2 *>(&K.T.line_tau[lineindex].ul_lower);
+        const int2 u1 = *reinterpret_cast<const int2 *>(&K.T.line_tau[min(lineindex + 1, nl1)].ul_lower);
+        const int2 u2 = *reinterpret_cast<const int2 *>(&K.T.line_tau[min(lineindex + 2, nl1)].ul_lower);
+        const int2 u3 = *reinterpret_cast<const int2 *>(&K.T.line_tau[min(lineindex + 3, nl1)].ul_lower);
+        pf_l0 = pops[u0.x];
+        pf_u0 = pops[u0.y];
+        pf_l1 = pops[u1.x];
+        pf_u1 = pops[u1.y];
+        pf_l2 = pops[u2.x];
+        pf_u2 = pops[u2.y];
+        pf_l3 = pops[u3.x];
+        pf_u3 = pops[u3.y];
+      }
+      const int pj = lineindex - pf_base;
       const double nu_trans = K.T.line_nu[lineindex];
       dnext = lineindex + 1;
       double ldist;
@@ -560,8 +598,8 @@ DEVFN double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_even
           break;
         }
         const LineTau lt = K.T.line_tau[lineindex];
-        const double n_u = pops[lt.ul_upper];
-        const double n_l = pops[lt.ul_lower];
+        const double n_u = pj == 0 ? pf_u0 : pj == 1 ? pf_u1 : pj == 2 ? pf_u2 : pf_u3;
+        const double n_l = pj == 0 ? pf_l0 : pj == 1 ? pf_l1 : pj == 2 ? pf_l2 : pf_l3;
         double tau_line = (lt.B_lu * n_l - lt.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * dt;
         ntaus++;
         if (tau_line < 0) tau_line = 0.;
@@ -607,6 +645,7 @@ DEVFN double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_even
   lwork(x.L, WK_LINES_SCANNED, nscanned);
   lwork(x.L, WK_LINE_TAUS, ntaus);
   x.wl += (unsigned)nscanned;
+  STAMP(x, 2);
   return result;
 }
 
@@ -748,6 +787,7 @@ DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
   const double tau_next = -1. * log(zrand);
   int snext = -1;
   double sdist = boundary_cross(x, p, &snext);
+  STAMP(x, 0);
   if (sdist == 0) {
     change_cell(x, p, snext);
     mgi = cell_mgi(K, p.where);
@@ -792,6 +832,7 @@ DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
     move_pkt_withtime(K, p, sdist / 2.);
     update_estimators(x, p, kap, sdist);
     move_pkt_withtime(K, p, sdist / 2.);
+    STAMP(x, 3);
     if (snext != p.where) {
       change_cell(x, p, snext);
       mgi = cell_mgi(K, p.where);
@@ -806,6 +847,7 @@ DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
     move_pkt_withtime(K, p, edist / 2.);
     update_estimators(x, p, kap, edist);
     move_pkt_withtime(K, p, edist / 2.);
+    STAMP(x, 3);
     if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_BB)
       rpkt_event_boundbound(x, p);
     else if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_CONT)

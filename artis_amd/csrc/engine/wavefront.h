@@ -198,9 +198,13 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_rpkt(Ctx K, WaveState W, uint64_
     st_busy += __popcll(__ballot(have));
     const unsigned long long ts0 = wave_clock();
     x.wl = x.wb = 0;
+#ifdef ARTIS_STAMPS
+    x.tlast = ts0;
+#endif
     if (have) {
       if (x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
         do_rpkt_step(x, p, t2, ColdSoa{soa, n, idx});
+        STAMP(x, 4);
         if (++steps > RPKT_MAX_STEPS) x.err(ERR_STUCK, p.number, 1);
       }
       if (!x.ok || p.type != ARTIS_TYPE_RPKT || !(p.prop_time < t2)) {
@@ -242,6 +246,10 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_rpkt(Ctx K, WaveState W, uint64_
       st_bsum += sb;
     }
   }
+#ifdef ARTIS_STAMPS
+  if (lane_id() == 0)
+    for (int i = 0; i < 5; i++) atomicAdd(&W.stats[32 + i], x.st[i]);
+#endif
   if (lane_id() == 0) {
     atomicAdd(&W.stats[24], st_lmax);
     atomicAdd(&W.stats[25], st_lsum);
