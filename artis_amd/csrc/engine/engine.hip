@@ -284,8 +284,9 @@ __global__ void k_soa_to_aos(const uint64_t *__restrict__ soa, uint64_t *__restr
 
 // update_packets.cc:234-333 (pass loop flattened, deviation D5) + do_packet update_packets.cc:137-202
 #define TRANSPORT_BLOCK 256
-__global__ __launch_bounds__(TRANSPORT_BLOCK) void k_transport(Ctx K, uint64_t *__restrict__ soa, int64_t n, int nts,
+__global__ __launch_bounds__(TRANSPORT_BLOCK) void k_transport(const Ctx *__restrict__ ctxp, uint64_t *__restrict__ soa, int64_t n, int nts,
                                                               double t2) {
+  const Ctx &K = *ctxp;
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   __shared__ double s_cmflum[TRANSPORT_BLOCK / 64];
@@ -410,6 +411,7 @@ struct Engine {
   hipEvent_t ev_round[2] = {nullptr, nullptr};
   int wave_grid = 2048;
   bool use_megakernel = false;
+  Ctx *d_ctx = nullptr;           // device copy of K for the transport kernels
   bool ma_meta_ok = true;         // MaMeta's 16-bit counts hold every level's transition counts
   int ma_occ = 1;                 // k_ma minimum waves per SIMD (launch bounds): 1 or 8
   uint32_t *d_binoffs = nullptr;  // exclusive prefix sums of W.bins
@@ -504,6 +506,13 @@ int alloc_packets(int64_t n) {
 // Event-queue transport (wavefront.h): classify, then rounds of R -> M -> K kernels until both the R and M
 // queues stay empty.  The host learns the queue sizes one round late (pinned async copies), so it never
 // stalls the stream; a round enqueued after the work ran out finds empty queues and costs only its launches.
+// the transport kernels read the context through a pointer to this device copy (physics.h)
+int sync_ctx() {
+  HIPCHK(hipStreamSynchronize(G.stream));
+  HIPCHK(hipMemcpy(G.d_ctx, &G.K, sizeof(Ctx), hipMemcpyHostToDevice));
+  return 0;
+}
+
 int tmark(int cls) {
   if (G.tev_used + 1 > G.tev.size()) {
     hipEvent_t e;
@@ -539,25 +548,26 @@ int tcollect() {
 int run_wavefront(int64_t n, int nts, double t2) {
   const WaveState &W = G.W;
   const unsigned grid = (unsigned)G.wave_grid;
+  if (int rc = sync_ctx()) return rc;
   G.tev_used = 0;
   HIPCHK(hipMemsetAsync(W.stats, 0, 48 * sizeof(unsigned long long), G.stream));
   HIPCHK(hipMemsetAsync(W.ctr, 0, NQUEUES * 2 * sizeof(uint32_t), G.stream));
   TSTART(3);
-  k_classify<<<(unsigned)((n + WAVE_BLOCK - 1) / WAVE_BLOCK), WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, t2);
+  k_classify<<<(unsigned)((n + WAVE_BLOCK - 1) / WAVE_BLOCK), WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, t2);
   TEND(3);
   HIPCHK(hipGetLastError());
   int64_t round = 0;
   bool done = false;
   for (; round < WAVE_MAX_ROUNDS && !done; round++) {
     TSTART(0);
-    k_rpkt<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts, t2);
+    k_rpkt<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
     TEND(0);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QR, 0, 2 * sizeof(uint32_t), G.stream));
     TSTART(1);
     if (W.ma_binned) {
       const int nne = G.K.C.n_nonempty;
       HIPCHK(hipMemsetAsync(W.bins, 0, (size_t)(nne + 1) * sizeof(uint32_t), G.stream));
-      k_ma_bin<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa);
+      k_ma_bin<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa);
       HIPCHK(hipcub::DeviceScan::ExclusiveSum(G.d_scan_tmp, G.scan_tmp_bytes, W.bins, G.d_binoffs, nne + 1,
                                               G.stream));
       k_ma_scatter<<<grid, WAVE_BLOCK, 0, G.stream>>>(W, G.d_binoffs);
@@ -565,16 +575,16 @@ int run_wavefront(int64_t n, int nts, double t2) {
     HIPCHK(hipMemsetAsync(W.xhead, 0, 8 * sizeof(uint32_t), G.stream));
     if (G.K.C.have_macache) {
       if (G.ma_occ == 8)
-        k_ma<true, 8><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts);
+        k_ma<true, 8><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
       else
-        k_ma<true, 1><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts);
+        k_ma<true, 1><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
     } else {
-      k_ma<false, 1><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts);
+      k_ma<false, 1><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
     }
     TEND(1);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QM, 0, 2 * sizeof(uint32_t), G.stream));
     TSTART(2);
-    k_kpkt<<<grid / 4, WAVE_BLOCK, 0, G.stream>>>(G.K, W, G.d_soa, n, nts, t2);
+    k_kpkt<<<grid / 4, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
     TEND(2);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QK, 0, 2 * sizeof(uint32_t), G.stream));
     HIPCHK(hipGetLastError());
@@ -994,6 +1004,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   if (!C.have_macache) rc |= dalloc(&C.marates, (size_t)nne_cells * nl * ARTIS_MA_ACTION_COUNT);
   // cell-state input buffers
   rc |= dalloc(&G.W.ctr, (size_t)NQUEUES * 2);
+  rc |= dalloc(&G.d_ctx, (size_t)1);
   rc |= dalloc(&G.W.stats, (size_t)48);
   rc |= dalloc(&G.d_cellf, (size_t)8 * np);
   rc |= dalloc(&G.d_thick, (size_t)np);
@@ -1136,8 +1147,9 @@ int artis_gpu_update_packets_resident(int my_rank, int nts) {
   HIPCHK(hipEventRecord(G.ev0, G.stream));
   G.last_rounds = 0;
   if (n > 0 && G.use_megakernel) {
+    if (int rc = sync_ctx()) return rc;
     k_transport<<<(unsigned)((n + TRANSPORT_BLOCK - 1) / TRANSPORT_BLOCK), TRANSPORT_BLOCK, 0, G.stream>>>(
-        G.K, G.d_soa, n, nts, t2);
+        G.d_ctx, G.d_soa, n, nts, t2);
     HIPCHK(hipGetLastError());
   } else if (n > 0) {
     if (int rc = run_wavefront(n, nts, t2)) return rc;

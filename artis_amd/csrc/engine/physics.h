@@ -45,6 +45,12 @@ struct Ctx {
   DevRun R;
 };
 
+// The transport kernels read the context through a pointer to a device copy (engine.hip: sync_ctx) rather
+// than from a by-value kernel argument: the rare-event code is noinline and receives `const Ctx &`, and a
+// reference to a by-value kernel argument forces the whole 1 KB context into per-lane scratch, turning every
+// table-pointer read in the hot loops into a scratch load.  Through a __restrict__ pointer the reads stay
+// uniform scalar loads.
+
 struct LocalCounters {
   unsigned long long *ctr;   // LDS [35]: 34 reference counters + nesc
   unsigned long long *work;  // LDS [16]

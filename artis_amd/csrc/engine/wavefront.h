@@ -97,7 +97,8 @@ DEVFN void block_counters_flush(const Ctx &K, const unsigned long long *s_ctr, c
 }
 
 // update_packets.cc:280-309 prologue: reset the per-step counters of every packet, queue the active ones
-__global__ void k_classify(Ctx K, WaveState W, uint64_t *__restrict__ soa, int64_t n, double t2) {
+__global__ void k_classify(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa, int64_t n, double t2) {
+  const Ctx &K = *ctxp;
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   block_counters_init(s_ctr, s_work);
@@ -143,8 +144,9 @@ DEVFN void apply_pending(Tx &x, const WaveState &W, int32_t idx, Pkt &p, const C
 }
 
 // r-packets: persistent lanes, one do_rpkt_step per loop pass
-__global__ __launch_bounds__(WAVE_BLOCK) void k_rpkt(Ctx K, WaveState W, uint64_t *__restrict__ soa, int64_t n,
+__global__ __launch_bounds__(WAVE_BLOCK) void k_rpkt(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa, int64_t n,
                                                      int nts, double t2) {
+  const Ctx &K = *ctxp;
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   __shared__ double s_cmflum[WAVE_BLOCK / 64];
@@ -214,9 +216,11 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_rpkt(Ctx K, WaveState W, uint64_
         }
         pkt_store_hot(soa, n, idx, p);
         // cold fields the propagation step itself writes: the escape record (change_cell, boundary.cc:332-357)
-        // and the absorption record + macro-atom state of a line absorption (get_event / rpkt_event_boundbound)
+        // and the absorption record + macro-atom state of a line absorption (get_event / rpkt_event_boundbound,
+        // last_event 1).  A macro-atom activated by a bf absorption (last_event 3) was set up by the cold
+        // continuum-event call, which already wrote its cold words; the registers do not hold them.
         if (p.type == ARTIS_TYPE_ESCAPE) soa[32 * n + idx] = pack2(p.escape_type, p.escape_time);
-        if (p.type == ARTIS_TYPE_MA) {
+        if (p.type == ARTIS_TYPE_MA && p.last_event == 1) {
           reinterpret_cast<int32_t *>(&soa[19 * n + idx])[0] = p.absorptiontype;
           soa[21 * n + idx] = asw(p.absorptionfreq);
           for (int d = 0; d < 3; d++) soa[(22 + d) * n + idx] = asw(p.absorptiondir[d]);
@@ -269,7 +273,8 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_rpkt(Ctx K, WaveState W, uint64_
 }
 
 // bin the M queue by cell: count per cell and remember each slot's key
-__global__ void k_ma_bin(Ctx K, WaveState W, const uint64_t *__restrict__ soa) {
+__global__ void k_ma_bin(const Ctx *__restrict__ ctxp, WaveState W, const uint64_t *__restrict__ soa) {
+  const Ctx &K = *ctxp;
   const uint32_t nq = W.ctr[2 * QM];
   for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x) {
     const int32_t idx = W.q[QM][slot];
@@ -290,8 +295,9 @@ __global__ void k_ma_scatter(WaveState W, uint32_t *offs) {
 // XCD the block was dispatched to under round-robin placement, so one XCD's L2 sees a contiguous run of
 // cells -- and steal from the following ranges once theirs is exhausted.
 template <bool CACHE, int MINW>
-__global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(Ctx K, WaveState W, const uint64_t *__restrict__ soa,
+__global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__ ctxp, WaveState W, const uint64_t *__restrict__ soa,
                                                          int64_t n, int nts) {
+  const Ctx &K = *ctxp;
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   block_counters_init(s_ctr, s_work);
@@ -398,8 +404,9 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(Ctx K, WaveState W, con
 }
 
 // k-packets (rare): one packet per workitem, grid-stride
-__global__ __launch_bounds__(WAVE_BLOCK) void k_kpkt(Ctx K, WaveState W, uint64_t *__restrict__ soa, int64_t n,
+__global__ __launch_bounds__(WAVE_BLOCK) void k_kpkt(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa, int64_t n,
                                                      int nts, double t2) {
+  const Ctx &K = *ctxp;
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   block_counters_init(s_ctr, s_work);
