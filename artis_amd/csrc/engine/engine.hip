@@ -187,13 +187,17 @@ __global__ void k_cooling(Ctx K) {
 }
 
 // macroatom.cc:57-159 calculate_macroatom_transitionrates, one workitem per (cell, level); with the macro-atom
-// cache it also stores the running sums of the individual rates (cellhistory individ_* arrays)
+// cache it also stores the running sums of the individual rates (cellhistory individ_* arrays).
+// Workitems are ordered level-major (consecutive lanes = the same level in consecutive cells): every lane of
+// a wave walks the same transition lists, so the atomic-data loads are wave-uniform and the loops do not
+// diverge; only the cell's populations and temperatures differ per lane.
 __global__ void k_marates(Ctx K, int nts) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nl = K.T.nlevels_total;
-  if (idx >= (int64_t)K.C.n_nonempty * nl) return;
-  const int k = (int)(idx / nl);
-  const int ul = (int)(idx % nl);
+  const int64_t nne_cells = K.C.n_nonempty;
+  if (idx >= nne_cells * nl) return;
+  const int ul = (int)(idx / nne_cells);
+  const int k = (int)(idx % nne_cells);
   const int mgi = K.C.ne_mgi[k];
   const int ui = K.T.level_ui[ul];
   const int e = K.T.ion_element[ui];
@@ -208,7 +212,7 @@ __global__ void k_marates(Ctx K, int nts) {
   const bool cache = K.C.have_macache;
   const int4 ml = K.T.ma_level[ul];
   double *rec = cache ? K.C.ma_rec + (int64_t)k * K.C.ma_rec_stride + ml.x : nullptr;
-  double *cum_drad = rec + 9, *cum_dint = cum_drad + ml.y, *cum_uint = cum_dint + ml.y;
+  double *cum_drad = rec + MA_HEAD_DOUBLES, *cum_dint = cum_drad + ml.y, *cum_uint = cum_dint + ml.y;
   double *cum_rrad = cum_uint + ml.z, *cum_rint = cum_rrad + ml.w, *cum_uhi = cum_rint + ml.w;
   double pr[ARTIS_MA_ACTION_COUNT];
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) pr[a] = 0.;
@@ -267,8 +271,19 @@ __global__ void k_marates(Ctx K, int nts) {
       if (cache) cum_uhi[t] = pr[ARTIS_MA_ACTION_INTERNALUPHIGHER];
     }
   }
-  double *out = cache ? rec : K.C.marates + idx * ARTIS_MA_ACTION_COUNT;
+  double *out = cache ? rec : K.C.marates + ((int64_t)k * nl + ul) * ARTIS_MA_ACTION_COUNT;
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) out[a] = pr[a];
+  if (cache) {  // walk metadata in the head line (engine_dev.h MA_HEAD_*)
+    int32_t *h = reinterpret_cast<int32_t *>(rec);
+    h[MA_HEAD_DOFF] = doff;
+    h[MA_HEAD_UOFF] = uoff;
+    h[MA_HEAD_BASE_LOWER] = (i > 0) ? K.T.ion_uniqueleveloffset[ui - 1] : -1;
+    h[MA_HEAD_ND] = ndowntrans;
+    h[MA_HEAD_NU] = nuptrans;
+    h[MA_HEAD_NR] = ml.w;
+    h[MA_HEAD_NT] = (i < K.T.elem_nions[e] - 1 && l < K.T.ion_ionisinglevels[ui]) ? K.T.level_nphixstargets[ul] : 0;
+    h[MA_HEAD_UL] = ul;
+  }
 }
 
 __global__ void k_aos_to_soa(const uint64_t *__restrict__ aos, uint64_t *__restrict__ soa, int64_t n) {
@@ -412,7 +427,6 @@ struct Engine {
   int wave_grid = 2048;
   bool use_megakernel = false;
   Ctx *d_ctx = nullptr;           // device copy of K for the transport kernels
-  bool ma_meta_ok = true;         // MaMeta's 16-bit counts hold every level's transition counts
   int ma_occ = 1;                 // k_ma minimum waves per SIMD (launch bounds): 1 or 8
   uint32_t *d_binoffs = nullptr;  // exclusive prefix sums of W.bins
   void *d_scan_tmp = nullptr;
@@ -794,7 +808,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     const double A_ul = a->line_einstein_A[li];
     const double B_ul = ARTIS_CLIGHTSQUAREDOVERTWOH / pow(nu_trans, 3) * A_ul;
     const double B_lu = (double)a->level_stat_weight[uup] / (double)a->level_stat_weight[ulo] * B_ul;
-    lt[li] = {B_ul, B_lu, ulo, uup};
+    lt[li] = {nu_trans, B_ul, B_lu, ulo, uup};
   }
   rc |= dupload(&T.line_tau, lt.data(), nli);
   // macro-atom per-line constants (macroatom.cc:518-522, 563-566; radfield.h:47; macroatom.h:93,130)
@@ -821,43 +835,33 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
         const int ul = a->ion_uniqueleveloffset[ui] + l;
         const int nrec = (i > 0 && l <= a->ion_maxrecombininglevel[ui]) ? a->ion_ionisinglevels[ui - 1] : 0;
         const int nt = (i < a->elem_nions[e] - 1 && l < a->ion_ionisinglevels[ui]) ? a->level_nphixstargets[ul] : 0;
-        const int64_t len = 9 + 2 * (int64_t)a->level_ndowntrans[ul] + a->level_nuptrans[ul] + 2 * nrec + nt;
+        const int64_t len = MA_HEAD_DOUBLES + 2 * (int64_t)a->level_ndowntrans[ul] + a->level_nuptrans[ul] + 2 * nrec + nt;
         mal[ul] = make_int4((int)marec, a->level_ndowntrans[ul], a->level_nuptrans[ul], nrec);
-        marec += (len + 15) / 16 * 16;  // 128-byte aligned records: the 9 totals share one cache line
+        marec += (len + 15) / 16 * 16;  // 128-byte aligned records: the head is one cache line
       }
     }
   rc |= dupload(&T.ma_level, mal.data(), nl);
   {
-    std::vector<MaMeta> mm(nl);
-    std::vector<int32_t> dt(std::max<int64_t>(ndown, 1)), ut(std::max<int64_t>(nup, 1));
+    std::vector<int2> dt(std::max<int64_t>(ndown, 1)), ut(std::max<int64_t>(nup, 1));
     for (int e = 0; e < ne; e++)
       for (int i = 0; i < a->elem_nions[e]; i++) {
         const int ui = a->elem_uniqueionoffset[e] + i;
         const int base = a->ion_uniqueleveloffset[ui];
         for (int l = 0; l < a->ion_nlevels[ui]; l++) {
           const int ul = base + l;
-          MaMeta &m = mm[ul];
-          m.epsilon = a->level_epsilon[ul];
-          m.rec_off = mal[ul].x;
-          m.doff = a->level_downtrans_offset[ul];
-          m.uoff = a->level_uptrans_offset[ul];
-          m.base_lower = (i > 0) ? a->ion_uniqueleveloffset[ui - 1] : -1;
-          m.nd = (uint16_t)a->level_ndowntrans[ul];
-          m.nu = (uint16_t)a->level_nuptrans[ul];
-          m.nr = (uint16_t)mal[ul].w;
-          m.nt = (uint16_t)((i < a->elem_nions[e] - 1 && l < a->ion_ionisinglevels[ui]) ? a->level_nphixstargets[ul] : 0);
-          for (int j = 0; j < a->level_ndowntrans[ul]; j++)
-            dt[m.doff + j] = base + a->line_lowerlevelindex[a->downtrans_lineindex[m.doff + j]];
-          for (int j = 0; j < a->level_nuptrans[ul]; j++)
-            ut[m.uoff + j] = base + a->line_upperlevelindex[a->uptrans_lineindex[m.uoff + j]];
+          const int doff = a->level_downtrans_offset[ul], uoff = a->level_uptrans_offset[ul];
+          for (int j = 0; j < a->level_ndowntrans[ul]; j++) {
+            const int t = base + a->line_lowerlevelindex[a->downtrans_lineindex[doff + j]];
+            dt[doff + j] = make_int2(t, mal[t].x);
+          }
+          for (int j = 0; j < a->level_nuptrans[ul]; j++) {
+            const int t = base + a->line_upperlevelindex[a->uptrans_lineindex[uoff + j]];
+            ut[uoff + j] = make_int2(t, mal[t].x);
+          }
         }
       }
-    for (int ul = 0; ul < nl; ul++)
-      if (a->level_ndowntrans[ul] > 65535 || a->level_nuptrans[ul] > 65535 || mal[ul].w > 65535)
-        G.ma_meta_ok = false;
-    rc |= dupload(&T.ma_meta, mm.data(), nl);
-    rc |= dupload(&T.down_target_ul, dt.data(), dt.size());
-    rc |= dupload(&T.up_target_ul, ut.data(), ut.size());
+    rc |= dupload(&T.down_target, dt.data(), dt.size());
+    rc |= dupload(&T.up_target, ut.data(), ut.size());
   }
   G.ma_rec_stride = marec;
   rc |= dupload(&T.allcont_nu_edge, a->allcont_nu_edge, nb);
@@ -992,7 +996,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     (void)hipMemGetInfo(&freeb, &totalb);
     const double need = (double)nne_cells * (double)C.ma_rec_stride * 8.0;
     const char *env = getenv("ARTIS_GPU_NO_MACACHE");
-    if (!(env && env[0] == '1') && G.ma_meta_ok && need < 0.75 * (double)freeb) {
+    if (!(env && env[0] == '1') && need < 0.75 * (double)freeb) {
       double *mc = nullptr;
       if (hipMalloc((void **)&mc, (size_t)need) == hipSuccess) {
         G.allocs.push_back(mc);
@@ -1066,7 +1070,7 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
     k_bfcells<<<(unsigned)((nbt + B - 1) / B), B, 0, G.stream>>>(G.K, G.d_target_ul, G.d_target_t);
     const int64_t nci = (int64_t)n_ne * ni;
     k_cooling<<<(unsigned)((nci + 63) / 64), 64, 0, G.stream>>>(G.K);
-    k_marates<<<(unsigned)((nlv + 63) / 64), 64, 0, G.stream>>>(G.K, nts);
+    k_marates<<<(unsigned)((nlv + 255) / 256), 256, 0, G.stream>>>(G.K, nts);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(G.ev1, G.stream));

@@ -17,7 +17,20 @@
 
 #define PKT_WORDS 38
 
-struct LineTau {
+// macro-atom record head: doubles 0..8 = totals; int32 slots (of the 32 in the 128-byte head):
+#define MA_HEAD_DOUBLES 16
+#define MA_HEAD_DOFF 18        // level_downtrans_offset
+#define MA_HEAD_UOFF 19        // level_uptrans_offset
+#define MA_HEAD_BASE_LOWER 20  // unique index of level 0 of the next lower ion (-1 if none)
+#define MA_HEAD_ND 21
+#define MA_HEAD_NU 22
+#define MA_HEAD_NR 23          // recombination targets
+#define MA_HEAD_NT 24          // ionisation targets (get_nphixstargets)
+#define MA_HEAD_UL 25          // the level's own unique index
+
+// one 32-byte record per line for the line walk of get_event (two 16-byte loads)
+struct __attribute__((aligned(16))) LineTau {
+  double nu;    // line frequency (linelist_entry.nu)
   double B_ul;  // CLIGHTSQUAREDOVERTWOH / pow(nu, 3) * A_ul          (rpkt.cc:180)
   double B_lu;  // g_u / g_l * B_ul                                    (rpkt.cc:181)
   int32_t ul_lower;  // unique level index of the lower level
@@ -31,16 +44,6 @@ struct LineMA {
   double B_lu;  // g_u / g_l * B_ul                               (macroatom.cc:522, 566)
   double nu3;   // pow(nu_lev, 3)                                 (radfield.h:47)
   double P2;    // pow(H_ionpot / (eps_upper - eps_lower), 2)    (macroatom.h:93, 130)
-};
-
-// static per-level data of the cached macro-atom walk, one 32-byte record per unique level (two 16-byte loads)
-struct __attribute__((aligned(16))) MaMeta {
-  double epsilon;      // level energy (atomic.cc epsilon)
-  int32_t rec_off;     // offset (doubles) of the level's macro-atom record inside a cell's block
-  int32_t doff, uoff;  // into downtrans_* / uptrans_* (level_downtrans_offset, level_uptrans_offset)
-  int32_t base_lower;  // unique index of level 0 of the next lower ion (-1 if none)
-  uint16_t nd, nu;     // #downtrans, #uptrans
-  uint16_t nr, nt;     // #recombination targets, #ionisation targets (get_nphixstargets)
 };
 
 struct DevTab {
@@ -67,8 +70,8 @@ struct DevTab {
   // per level: offset (doubles) of its macro-atom record inside a cell's record block, #downtrans, #uptrans,
   // #recombination targets (ionising levels of the lower ion, 0 if the level does not recombine)
   const int4 *ma_level;
-  const MaMeta *ma_meta;                 // [nlevels_total]
-  const int32_t *down_target_ul, *up_target_ul;  // unique level index of each downtrans / uptrans target
+  // each downtrans / uptrans target as (unique level index, offset of its macro-atom record in a cell block)
+  const int2 *down_target, *up_target;
   const double *allcont_nu_edge, *allcont_probability;
   const int32_t *allcont_element, *allcont_ion, *allcont_level, *allcont_target, *allcont_upperlevel,
       *allcont_phixstable, *allcont_groundindex;
@@ -102,11 +105,12 @@ struct DevCells {
   double *depratio;    // [n_nonempty * nbf]            departure ratios (rpkt.cc:1140-1151)
   double *corrphot;    // [n_nonempty * ntargets_total] get_corrphotoioncoeff (ratecoeff.cc:1247-1308)
   double *cooling;     // [n_nonempty * ncoolingterms]  cumulative cooling_contrib (kpkt.cc:167-308)
-  // macro-atom cache: per (cell, level) one contiguous record, 128-byte aligned, holding the processrates
-  // totals (macroatom.cc:57-159) and the running sums of the individual rates (the cellhistory individ_*
-  // arrays, globals.h:174-183) summed in the reference's order, so that a binary search returns the
-  // reference's linear-scan choice:
-  //   [9 totals | rad_deexc (ndown) | internal_down_same (ndown) | internal_up_same (nup) |
+  // macro-atom cache: per (cell, level) one contiguous record, 128-byte aligned.  Its first 128 bytes (the head,
+  // one cache line) hold the 9 processrates totals (macroatom.cc:57-159) and the level's walk metadata
+  // (MA_HEAD_* int slots); then come the running sums of the individual rates (the cellhistory individ_*
+  // arrays, globals.h:174-183) summed in the reference's order, so that a search returns the reference's
+  // linear-scan choice:
+  //   [head | rad_deexc (ndown) | internal_down_same (ndown) | internal_up_same (nup) |
   //    rad_recomb (nrec) | internal_down_lower (nrec) | internal_up_higher (nphixstargets)]
   double *ma_rec;      // [n_nonempty * ma_rec_stride], or nullptr
   int64_t ma_rec_stride;

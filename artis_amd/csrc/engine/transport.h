@@ -541,10 +541,12 @@ DEVFN double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_even
   const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
   unsigned long long nscanned = 0, ntaus = 0;
   double result;
-  // The walk visits consecutive lines; their level populations (random gathers into the cell's pops) are
-  // fetched four lines at a time, so a long walk waits for memory once per four lines instead of per line.
+  // The walk visits consecutive lines.  Their 32-byte records and the two level populations each needs (random
+  // gathers into the cell's pops) are fetched four lines at a time, all loads independent, so a long walk
+  // waits for memory twice per four lines instead of three times per line.
   int pf_base = -16;
-  double pf_l0 = 0, pf_l1 = 0, pf_l2 = 0, pf_l3 = 0, pf_u0 = 0, pf_u1 = 0, pf_u2 = 0, pf_u3 = 0;
+  LineTau r0, r1, r2, r3;
+  double pl0 = 0, pl1 = 0, pl2 = 0, pl3 = 0, pu0 = 0, pu1 = 0, pu2 = 0, pu3 = 0;
   while (true) {
     const int lineindex = closest_transition(K, dnu, dnext);
     if (lineindex >= 0) {
@@ -552,21 +554,21 @@ DEVFN double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_even
       if ((unsigned)(lineindex - pf_base) >= 4u) {
         pf_base = lineindex;
         const int nl1 = K.T.nlines - 1;
-        const int2 u0 = *reinterpret_cast<const int2 *>(&K.T.line_tau[lineindex].ul_lower);
-        const int2 u1 = *reinterpret_cast<const int2 *>(&K.T.line_tau[min(lineindex + 1, nl1)].ul_lower);
-        const int2 u2 = *reinterpret_cast<const int2 *>(&K.T.line_tau[min(lineindex + 2, nl1)].ul_lower);
-        const int2 u3 = *reinterpret_cast<const int2 *>(&K.T.line_tau[min(lineindex + 3, nl1)].ul_lower);
-        pf_l0 = pops[u0.x];
-        pf_u0 = pops[u0.y];
-        pf_l1 = pops[u1.x];
-        pf_u1 = pops[u1.y];
-        pf_l2 = pops[u2.x];
-        pf_u2 = pops[u2.y];
-        pf_l3 = pops[u3.x];
-        pf_u3 = pops[u3.y];
+        r0 = K.T.line_tau[lineindex];
+        r1 = K.T.line_tau[min(lineindex + 1, nl1)];
+        r2 = K.T.line_tau[min(lineindex + 2, nl1)];
+        r3 = K.T.line_tau[min(lineindex + 3, nl1)];
+        pl0 = pops[r0.ul_lower];
+        pu0 = pops[r0.ul_upper];
+        pl1 = pops[r1.ul_lower];
+        pu1 = pops[r1.ul_upper];
+        pl2 = pops[r2.ul_lower];
+        pu2 = pops[r2.ul_upper];
+        pl3 = pops[r3.ul_lower];
+        pu3 = pops[r3.ul_upper];
       }
       const int pj = lineindex - pf_base;
-      const double nu_trans = K.T.line_nu[lineindex];
+      const double nu_trans = pj == 0 ? r0.nu : pj == 1 ? r1.nu : pj == 2 ? r2.nu : r3.nu;
       dnext = lineindex + 1;
       double ldist;
       if (dnu <= nu_trans) {
@@ -597,10 +599,11 @@ DEVFN double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_even
           result = DBL_MAX;
           break;
         }
-        const LineTau lt = K.T.line_tau[lineindex];
-        const double n_u = pj == 0 ? pf_u0 : pj == 1 ? pf_u1 : pj == 2 ? pf_u2 : pf_u3;
-        const double n_l = pj == 0 ? pf_l0 : pj == 1 ? pf_l1 : pj == 2 ? pf_l2 : pf_l3;
-        double tau_line = (lt.B_lu * n_l - lt.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * dt;
+        const double n_u = pj == 0 ? pu0 : pj == 1 ? pu1 : pj == 2 ? pu2 : pu3;
+        const double n_l = pj == 0 ? pl0 : pj == 1 ? pl1 : pj == 2 ? pl2 : pl3;
+        const double B_lu = pj == 0 ? r0.B_lu : pj == 1 ? r1.B_lu : pj == 2 ? r2.B_lu : r3.B_lu;
+        const double B_ul = pj == 0 ? r0.B_ul : pj == 1 ? r1.B_ul : pj == 2 ? r2.B_ul : r3.B_ul;
+        double tau_line = (B_lu * n_l - B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * dt;
         ntaus++;
         if (tau_line < 0) tau_line = 0.;
         if (tau_rnd - tau > tau_cont + tau_line) {
@@ -997,7 +1000,7 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
     const int ndowntrans = K.T.level_ndowntrans[ul];
     const int doff = K.T.level_downtrans_offset[ul];
     if constexpr (CACHE) {
-      const int j = first_above(rec + 9, ndowntrans, zr * processrates[ARTIS_MA_ACTION_RADDEEXC], m.ntrans);
+      const int j = first_above(rec + MA_HEAD_DOUBLES, ndowntrans, zr * processrates[ARTIS_MA_ACTION_RADDEEXC], m.ntrans);
       if (j < ndowntrans) linelistindex = K.T.downtrans_lineindex[doff + j];
     } else {
       double r = 0.;
@@ -1037,7 +1040,7 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
     const int ndowntrans = K.T.level_ndowntrans[ul];
     const int doff = K.T.level_downtrans_offset[ul];
     if constexpr (CACHE) {
-      const int j = first_above(rec + 9 + ml.y, ndowntrans, zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNSAME],
+      const int j = first_above(rec + MA_HEAD_DOUBLES + ml.y, ndowntrans, zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNSAME],
                                 m.ntrans);
       if (j < ndowntrans) lower = K.T.line_lower[K.T.downtrans_lineindex[doff + j]];
     } else {
@@ -1074,7 +1077,7 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
     const int nlevels = get_ionisinglevels(K, element, upperion - 1);
     int lower = 0;
     if constexpr (CACHE) {
-      lower = first_above(rec + 9 + 2 * ml.y + ml.z, nlevels, zr * processrates[ARTIS_MA_ACTION_RADRECOMB], m.ntrans);
+      lower = first_above(rec + MA_HEAD_DOUBLES + 2 * ml.y + ml.z, nlevels, zr * processrates[ARTIS_MA_ACTION_RADRECOMB], m.ntrans);
       r = (lower < nlevels) ? DBL_MAX : -DBL_MAX;
     } else {
       for (lower = 0; lower < nlevels; lower++) {
@@ -1101,7 +1104,7 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
     const int nlevels = get_ionisinglevels(K, element, ion - 1);
     int lower;
     if constexpr (CACHE) {
-      lower = first_above(rec + 9 + 2 * ml.y + ml.z + ml.w, nlevels, zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNLOWER],
+      lower = first_above(rec + MA_HEAD_DOUBLES + 2 * ml.y + ml.z + ml.w, nlevels, zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNLOWER],
                           m.ntrans);
     } else {
       double r = 0.;
@@ -1129,7 +1132,7 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
     const int nuptrans = K.T.level_nuptrans[ul];
     const int uoff = K.T.level_uptrans_offset[ul];
     if constexpr (CACHE) {
-      const int j = first_above(rec + 9 + 2 * ml.y, nuptrans, zr * processrates[ARTIS_MA_ACTION_INTERNALUPSAME],
+      const int j = first_above(rec + MA_HEAD_DOUBLES + 2 * ml.y, nuptrans, zr * processrates[ARTIS_MA_ACTION_INTERNALUPSAME],
                                 m.ntrans);
       if (j < nuptrans) upper = K.T.line_upper[K.T.uptrans_lineindex[uoff + j]];
     } else {
@@ -1165,7 +1168,7 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
     const int nt = get_nphixstargets(K, element, ion, level);
     bool found;
     if constexpr (CACHE) {
-      const int t = first_above(rec + 9 + 2 * ml.y + ml.z + 2 * ml.w, nt,
+      const int t = first_above(rec + MA_HEAD_DOUBLES + 2 * ml.y + ml.z + 2 * ml.w, nt,
                                 zr * processrates[ARTIS_MA_ACTION_INTERNALUPHIGHER], m.ntrans);
       found = t < nt;
       if (found) upper = get_phixsupperlevel(K, element, ion, level, t);
@@ -1194,27 +1197,76 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
   return MA_FAILED;
 }
 
-// The cached walk in its lean form: lane state = (unique level, cell record block); per jump two 16-byte loads of
-// the level's static MaMeta, five of its 9 process-rate totals, the binary search in the selected cumulative
-// array and one load of the target level.  Same selections, same RNG draws as ma_jump<true>.
+// The cached walk in its lean form: lane state = (unique level, record offset, cell block).  Per jump: the
+// level's 128-byte record head (totals + walk metadata, seven independent 16-byte loads), a two-level search
+// in the selected cumulative array, and one 8-byte load of the target (level, record offset).  Same
+// selections, same RNG draws as ma_jump<true>.
 struct MaLaneC {
-  int ul;
+  int ul, rec_off;
   const double *block;  // K.C.ma_rec + k * ma_rec_stride
   unsigned jumps;
   unsigned long long ntrans;
 };
 
+// first j in [0, n) with cum[j] > x (n if none), the same answer as first_above, in two dependent rounds of
+// independent loads: three quartile probes, then the (<= 8-entry) quarter they select.  Longer arrays fall back
+// to bisection inside the quarter.
+DEVFN int first_above_2level(const double *cum, int n, double x, unsigned long long &probes) {
+  if (n <= 0) return 0;
+  const int step = (n + 3) >> 2;
+  const int p0 = min(step - 1, n - 1), p1 = min(2 * step - 1, n - 1), p2 = min(3 * step - 1, n - 1);
+  const double c0 = cum[p0], c1 = cum[p1], c2 = cum[p2];
+  probes += 3;
+  int lo, hi;  // answer in [lo, hi]
+  if (c0 > x) {
+    lo = 0;
+    hi = p0;
+  } else if (c1 > x) {
+    lo = p0 + 1;
+    hi = p1;
+  } else if (c2 > x) {
+    lo = p1 + 1;
+    hi = p2;
+  } else {
+    lo = p2 + 1;
+    hi = n;  // n = none above
+  }
+  // within [lo, hi): at most `step` entries; hi itself (if < n) is known to be above x
+  int len = hi - lo;
+  if (len <= 8) {
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) v[q] = (q < len) ? cum[lo + q] : 0.;
+    probes += len;
+    int j = hi;
+#pragma unroll
+    for (int q = 7; q >= 0; q--)
+      if (q < len && v[q] > x) j = lo + q;
+    return j;
+  }
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    probes++;
+    if (cum[mid] > x)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  return lo;
+}
+
 DEVFN int ma_jump_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneC &m, MaEnd &end, int number) {
   m.jumps++;
+  const double *rec = m.block + m.rec_off;
+  const int4 *hp = reinterpret_cast<const int4 *>(rec);
+  const int4 h0 = hp[0], h1 = hp[1], h2 = hp[2], h3 = hp[3], h4 = hp[4], h5 = hp[5], h6 = hp[6];
+  auto dbl = [](int lo, int hi) { return __hiloint2double(hi, lo); };
+  const double pr[ARTIS_MA_ACTION_COUNT] = {dbl(h0.x, h0.y), dbl(h0.z, h0.w), dbl(h1.x, h1.y),
+                                            dbl(h1.z, h1.w), dbl(h2.x, h2.y), dbl(h2.z, h2.w),
+                                            dbl(h3.x, h3.y), dbl(h3.z, h3.w), dbl(h4.x, h4.y)};
+  // head int slots 18.. (engine_dev.h MA_HEAD_*): h4.z doff, h4.w uoff, h5 = base_lower, nd, nu, nr; h6.x nt
+  const int doff = h4.z, uoff = h4.w, base_lower = h5.x, nd = h5.y, nu = h5.z, nr = h5.w, nt = h6.x;
   const int ul = m.ul;
-  const int4 *mp = reinterpret_cast<const int4 *>(K.T.ma_meta + ul);
-  const int4 w0 = mp[0], w1 = mp[1];
-  const int rec_off = w0.z, doff = w0.w, uoff = w1.x, base_lower = w1.y;
-  const int nd = w1.z & 0xffff, nu = (int)((unsigned)w1.z >> 16), nr = w1.w & 0xffff, nt = (int)((unsigned)w1.w >> 16);
-  const double *rec = m.block + rec_off;
-  const double2 *r2 = reinterpret_cast<const double2 *>(rec);
-  const double2 t01 = r2[0], t23 = r2[1], t45 = r2[2], t67 = r2[3];
-  const double pr[ARTIS_MA_ACTION_COUNT] = {t01.x, t01.y, t23.x, t23.y, t45.x, t45.y, t67.x, t67.y, rec[8]};
   double total_transitions = 0.;
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) total_transitions += pr[a];
   const double zrand = artis_rng_uniform(&rng);
@@ -1244,15 +1296,17 @@ DEVFN int ma_jump_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
   // the cumulative array of the selected action inside the level record (engine_dev.h DevCells::ma_rec)
   int off, cnt;
   switch (sel) {
-    case ARTIS_MA_ACTION_RADDEEXC: off = 9; cnt = nd; break;
-    case ARTIS_MA_ACTION_INTERNALDOWNSAME: off = 9 + nd; cnt = nd; break;
-    case ARTIS_MA_ACTION_INTERNALUPSAME: off = 9 + 2 * nd; cnt = nu; break;
-    case ARTIS_MA_ACTION_RADRECOMB: off = 9 + 2 * nd + nu; cnt = nr; break;
-    case ARTIS_MA_ACTION_INTERNALDOWNLOWER: off = 9 + 2 * nd + nu + nr; cnt = nr; break;
-    default: off = 9 + 2 * nd + nu + 2 * nr; cnt = nt; break;  // INTERNALUPHIGHER
+    case ARTIS_MA_ACTION_RADDEEXC: off = 0; cnt = nd; break;
+    case ARTIS_MA_ACTION_INTERNALDOWNSAME: off = nd; cnt = nd; break;
+    case ARTIS_MA_ACTION_INTERNALUPSAME: off = 2 * nd; cnt = nu; break;
+    case ARTIS_MA_ACTION_RADRECOMB: off = 2 * nd + nu; cnt = nr; break;
+    case ARTIS_MA_ACTION_INTERNALDOWNLOWER: off = 2 * nd + nu + nr; cnt = nr; break;
+    default: off = 2 * nd + nu + 2 * nr; cnt = nt; break;  // INTERNALUPHIGHER
   }
   const double zr = artis_rng_uniform(&rng);
-  const int j = first_above(rec + off, cnt, zr * pr[sel], m.ntrans);
+  // bisection: fewer scattered loads per jump than the two-level variant (the walk is bound by the rate of
+  // per-lane scattered loads, not by their latency -- DESIGN.md §5)
+  const int j = first_above(rec + MA_HEAD_DOUBLES + off, cnt, zr * pr[sel], m.ntrans);
   if (j >= cnt) {
     fail(K, ERR_MA_SELECT, number, 10 + sel);
     return MA_FAILED;
@@ -1270,21 +1324,28 @@ DEVFN int ma_jump_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
       end.a = j;
       end.b = ul;
       return MA_END_FB;
-    case ARTIS_MA_ACTION_INTERNALDOWNSAME:
-      m.ul = K.T.down_target_ul[doff + j];
+    case ARTIS_MA_ACTION_INTERNALDOWNSAME: {
+      const int2 t = K.T.down_target[doff + j];
+      m.ul = t.x;
+      m.rec_off = t.y;
       return MA_CONTINUE;
-    case ARTIS_MA_ACTION_INTERNALUPSAME:
-      m.ul = K.T.up_target_ul[uoff + j];
+    }
+    case ARTIS_MA_ACTION_INTERNALUPSAME: {
+      const int2 t = K.T.up_target[uoff + j];
+      m.ul = t.x;
+      m.rec_off = t.y;
       return MA_CONTINUE;
+    }
     case ARTIS_MA_ACTION_INTERNALDOWNLOWER:
       lctr(L, CTR_MA_STAT_INTERNALDOWNLOWER);
       m.ul = base_lower + j;
+      m.rec_off = K.T.ma_level[m.ul].x;
       return MA_CONTINUE;
     default: {  // INTERNALUPHIGHER (macroatom.cc:382-414)
       lctr(L, CTR_MA_STAT_INTERNALUPHIGHER);
       const int ui = K.T.level_ui[ul];
-      m.ul = K.T.ion_uniqueleveloffset[ui + 1] +
-             K.T.phixstarget_levelindex[K.T.level_phixstargets_offset[ul] + j];
+      m.ul = K.T.ion_uniqueleveloffset[ui + 1] + K.T.phixstarget_levelindex[K.T.level_phixstargets_offset[ul] + j];
+      m.rec_off = K.T.ma_level[m.ul].x;
       return MA_CONTINUE;
     }
   }
@@ -1385,6 +1446,7 @@ DEVNI void do_macroatom(Tx &x, Pkt &p) {
   if (K.C.have_macache) {
     MaLaneC m;
     m.ul = ulev(K, p.ma_element, p.ma_ion, p.ma_level);
+    m.rec_off = K.T.ma_level[m.ul].x;
     m.block = K.C.ma_rec + (int64_t)K.C.ne_index[mgi] * K.C.ma_rec_stride;
     m.jumps = 0;
     m.ntrans = 0;

@@ -341,6 +341,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
           const int mgi = cell_mgi(K, where);
           if constexpr (CACHE) {
             mc.ul = ulev(K, lo32(w36), hi32(w36), lo32(w37));
+            mc.rec_off = K.T.ma_level[mc.ul].x;
             mc.block = K.C.ma_rec + (int64_t)K.C.ne_index[mgi] * K.C.ma_rec_stride;
             mc.jumps = 0;
             mc.ntrans = 0;
