@@ -1,5 +1,13 @@
-// packet_soa.h -- register image of one packet and its load/store to the 38-word SoA layout (engine_dev.h).
+// packet_soa.h -- register image of one packet and its load/store to the packet store in HBM (engine_dev.h).
 // Word map = byte offsets of the reference `struct packet` (packet.h:28-73) divided by 8.
+//
+// Layout: the 38 words of every packet are grouped by how the event-queue kernels touch them --
+//   hot  (16 words, 128 B = one cache line per packet): what every r-packet step reads and writes
+//   cold (20 words, 160 B): emission/absorption records, Stokes/pol_dir, escape record, macro-atom state
+//   rest (2 words): tdecay and the pellet bookkeeping, never touched by this path
+// each group stored packet-major ([group base + packet * group width + slot]).  The queues hand packets to
+// kernels in arbitrary order, so a word-major (SoA) layout would cost one 128-byte line per 8-byte word;
+// grouped, a packet's hot state is one line and its cold state two.
 #ifndef ARTIS_PACKET_SOA_H
 #define ARTIS_PACKET_SOA_H
 
@@ -7,6 +15,24 @@
 #include <stdint.h>
 
 #include "engine_dev.h"
+
+// word -> group (0 hot, 1 cold, 2 rest) and slot within the group; constant-folded for literal words
+__host__ __device__ constexpr int pkt_word_group(int w) {
+  return (w == 31 || w == 34) ? 2 : ((w >= 14 && w <= 17) || (w >= 19 && w <= 30) || w == 32 || w >= 35) ? 1 : 0;
+}
+__host__ __device__ constexpr int pkt_word_slot(int w) {
+  return w <= 13 ? w : w == 18 ? 14 : w == 33 ? 15           // hot
+       : w <= 17 ? w - 14                                    // cold: em_pos[3], em_time
+       : w <= 30 ? w - 15                                    // cold: 19..30 -> 4..15
+       : w == 32 ? 16 : w == 35 ? 17 : w == 36 ? 18 : w == 37 ? 19
+       : w == 31 ? 0 : 1;                                    // rest: 31, 34
+}
+__host__ __device__ constexpr int64_t pkt_word_index(int64_t n, int64_t i, int w) {
+  return pkt_word_group(w) == 0   ? i * 16 + pkt_word_slot(w)
+         : pkt_word_group(w) == 1 ? 16 * n + i * 20 + pkt_word_slot(w)
+                                  : 36 * n + i * 2 + pkt_word_slot(w);
+}
+#define PW(n, i, w) pkt_word_index((n), (i), (w))
 
 struct Pkt {
   int32_t where, type, last_cross, interactions, nscatterings, last_event;
@@ -34,7 +60,7 @@ __device__ __forceinline__ double asd(uint64_t w) { return __longlong_as_double(
 __device__ __forceinline__ uint64_t asw(double d) { return (uint64_t)__double_as_longlong(d); }
 
 __device__ __forceinline__ void pkt_load(const uint64_t *__restrict__ soa, int64_t n, int64_t i, Pkt &p) {
-#define W(k) soa[(int64_t)(k) * n + i]
+#define W(k) soa[pkt_word_index(n, i, (k))]
   uint64_t w;
   w = W(0);
   p.where = lo32(w);
@@ -89,7 +115,7 @@ __device__ __forceinline__ void pkt_load(const uint64_t *__restrict__ soa, int64
 
 // words 31 (tdecay) and 34 (pellet bookkeeping) are never written by the transport path
 __device__ __forceinline__ void pkt_store(uint64_t *__restrict__ soa, int64_t n, int64_t i, const Pkt &p) {
-#define W(k) soa[(int64_t)(k) * n + i]
+#define W(k) soa[pkt_word_index(n, i, (k))]
   W(0) = pack2(p.where, p.type);
   W(1) = pack2(p.last_cross, p.interactions);
   W(2) = pack2(p.nscatterings, p.last_event);
@@ -121,7 +147,7 @@ __device__ __forceinline__ void pkt_store(uint64_t *__restrict__ soa, int64_t n,
 // (emission / absorption bookkeeping, polarisation, escape record, macro-atom state) are only read by the rare
 // event code, which runs on a copy assembled from the hot registers plus the cold words in HBM.
 __device__ __forceinline__ void pkt_load_hot(const uint64_t *__restrict__ soa, int64_t n, int64_t i, Pkt &p) {
-#define W(k) soa[(int64_t)(k) * n + i]
+#define W(k) soa[pkt_word_index(n, i, (k))]
   uint64_t w;
   w = W(0);
   p.where = lo32(w);
@@ -148,7 +174,7 @@ __device__ __forceinline__ void pkt_load_hot(const uint64_t *__restrict__ soa, i
 #undef W
 }
 __device__ __forceinline__ void pkt_store_hot(uint64_t *__restrict__ soa, int64_t n, int64_t i, const Pkt &p) {
-#define W(k) soa[(int64_t)(k) * n + i]
+#define W(k) soa[pkt_word_index(n, i, (k))]
   W(0) = pack2(p.where, p.type);
   W(1) = pack2(p.last_cross, p.interactions);
   W(2) = pack2(p.nscatterings, p.last_event);
@@ -164,7 +190,7 @@ __device__ __forceinline__ void pkt_store_hot(uint64_t *__restrict__ soa, int64_
 #undef W
 }
 __device__ __forceinline__ void pkt_load_cold(const uint64_t *__restrict__ soa, int64_t n, int64_t i, Pkt &p) {
-#define W(k) soa[(int64_t)(k) * n + i]
+#define W(k) soa[pkt_word_index(n, i, (k))]
   uint64_t w;
   for (int d = 0; d < 3; d++) p.em_pos[d] = asd(W(14 + d));
   w = W(17);
@@ -195,7 +221,7 @@ __device__ __forceinline__ void pkt_load_cold(const uint64_t *__restrict__ soa, 
 #undef W
 }
 __device__ __forceinline__ void pkt_store_cold(uint64_t *__restrict__ soa, int64_t n, int64_t i, const Pkt &p) {
-#define W(k) soa[(int64_t)(k) * n + i]
+#define W(k) soa[pkt_word_index(n, i, (k))]
   for (int d = 0; d < 3; d++) W(14 + d) = asw(p.em_pos[d]);
   W(17) = pack2(p.em_time, p.pad0);
   W(19) = pack2(p.absorptiontype, p.trueemissiontype);

@@ -105,13 +105,13 @@ __global__ void k_classify(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool toR = false, toM = false, toK = false;
   if (i < n) {
-    const uint64_t w0 = soa[i];
+    const uint64_t w0 = soa[PW(n, i, 0)];
     const int type = hi32(w0);
-    const uint64_t w1 = soa[1 * n + i];
-    soa[1 * n + i] = pack2(lo32(w1), 0);  // interactions = 0
-    const uint64_t w33 = soa[33 * n + i];
-    soa[33 * n + i] = pack2(0, hi32(w33));  // scat_count = 0
-    const double prop_time = asd(soa[18 * n + i]);
+    const uint64_t w1 = soa[PW(n, i, 1)];
+    soa[PW(n, i, 1)] = pack2(lo32(w1), 0);  // interactions = 0
+    const uint64_t w33 = soa[PW(n, i, 33)];
+    soa[PW(n, i, 33)] = pack2(0, hi32(w33));  // scat_count = 0
+    const double prop_time = asd(soa[PW(n, i, 18)]);
     if (type != ARTIS_TYPE_ESCAPE && prop_time < t2) {
       atomicAdd(&s_work[WK_PACKETS_ACTIVE], 1ull);
       W.rng_n[i] = 0;
@@ -119,7 +119,7 @@ __global__ void k_classify(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *
       toR = type == ARTIS_TYPE_RPKT;
       toM = type == ARTIS_TYPE_MA;
       toK = type == ARTIS_TYPE_KPKT || type == ARTIS_TYPE_PRE_KPKT;
-      if (!toR && !toM && !toK) fail(K, ERR_UNSUPPORTED_TYPE, hi32(soa[33 * n + i]), type);
+      if (!toR && !toM && !toK) fail(K, ERR_UNSUPPORTED_TYPE, hi32(soa[PW(n, i, 33)]), type);
     }
   }
   wave_push(W, QR, toR, (int32_t)i);
@@ -219,13 +219,13 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_rpkt(const Ctx *__restrict__ ctx
         // and the absorption record + macro-atom state of a line absorption (get_event / rpkt_event_boundbound,
         // last_event 1).  A macro-atom activated by a bf absorption (last_event 3) was set up by the cold
         // continuum-event call, which already wrote its cold words; the registers do not hold them.
-        if (p.type == ARTIS_TYPE_ESCAPE) soa[32 * n + idx] = pack2(p.escape_type, p.escape_time);
+        if (p.type == ARTIS_TYPE_ESCAPE) soa[PW(n, idx, 32)] = pack2(p.escape_type, p.escape_time);
         if (p.type == ARTIS_TYPE_MA && p.last_event == 1) {
-          reinterpret_cast<int32_t *>(&soa[19 * n + idx])[0] = p.absorptiontype;
-          soa[21 * n + idx] = asw(p.absorptionfreq);
-          for (int d = 0; d < 3; d++) soa[(22 + d) * n + idx] = asw(p.absorptiondir[d]);
-          soa[36 * n + idx] = pack2(p.ma_element, p.ma_ion);
-          soa[37 * n + idx] = pack2(p.ma_level, p.ma_activatingline);
+          reinterpret_cast<int32_t *>(&soa[PW(n, idx, 19)])[0] = p.absorptiontype;
+          soa[PW(n, idx, 21)] = asw(p.absorptionfreq);
+          for (int d = 0; d < 3; d++) soa[PW(n, idx, 22 + d)] = asw(p.absorptiondir[d]);
+          soa[PW(n, idx, 36)] = pack2(p.ma_element, p.ma_ion);
+          soa[PW(n, idx, 37)] = pack2(p.ma_level, p.ma_activatingline);
         }
         W.rng_n[idx] = x.rng.n;
         if (x.ok && p.prop_time < t2) {
@@ -278,7 +278,7 @@ __global__ void k_ma_bin(const Ctx *__restrict__ ctxp, WaveState W, const uint64
   const uint32_t nq = W.ctr[2 * QM];
   for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x) {
     const int32_t idx = W.q[QM][slot];
-    const int k = K.C.ne_index[cell_mgi(K, lo32(soa[idx]))];
+    const int k = K.C.ne_index[cell_mgi(K, lo32(soa[PW(0, idx, 0)]))];  // hot group: no n term
     W.ma_key[slot] = k;
     atomicAdd(&W.bins[k], 1u);
   }
@@ -333,10 +333,10 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
         const bool got = idle && lo + slot < hi;
         if (got) {
           idx = queue[lo + slot];
-          const int where = lo32(soa[idx]);
-          const uint64_t w36 = soa[36 * n + idx];
-          const uint64_t w37 = soa[37 * n + idx];
-          rng.key1 = (uint32_t)hi32(soa[33 * n + idx]);  // packet number
+          const int where = lo32(soa[PW(n, idx, 0)]);
+          const uint64_t w36 = soa[PW(n, idx, 36)];
+          const uint64_t w37 = soa[PW(n, idx, 37)];
+          rng.key1 = (uint32_t)hi32(soa[PW(n, idx, 33)]);  // packet number
           rng.n = W.rng_n[idx];
           const int mgi = cell_mgi(K, where);
           if constexpr (CACHE) {

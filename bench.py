@@ -10,12 +10,16 @@ One step = one update_packets(nts) of this rank's P resident packets, all in HBM
 Packets are sharded: every rank propagates its own full-energy ensemble (rank-specific seed and RNG key), so
 per-GPU work is fixed as N grows ("weak").  value = N * P * K / max-over-ranks wall time.
 
-roofline: algorithmic bytes of the transport kernel (SURVEY.md §8(d) byte model over the engine's own event
-counters) / its average launch time measured with HIP events on the engine stream, against 8.0 TB/s.
+roofline: the dominant kernel class of the event-queue transport (k_ma or k_rpkt): its algorithmic bytes
+(SURVEY.md §8(d) per-unit figures over the engine's own event counters, split by the kernel that does the
+work) per launch / its average launch time, measured with HIP events around every launch on the engine
+stream, against 8.0 TB/s.  traffic: measured HBM bytes per launch of that kernel (rocprofv3 FETCH_SIZE x2 +
+WRITE_SIZE, profiles/pmc_*.json) when a PMC summary of the same configuration is committed.
 cpu_baseline: the CPU oracle (oracle/liboracle.so, OpenMP) on a bounded sample of the same workload, rank 0
 at N=1 only.
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -31,10 +35,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
 
 
 def byte_model(work, nions_total):
-    """SURVEY.md §8(d) algorithmic bytes from the work counters (include/artis_constants.h enum artis_work)."""
+    """SURVEY.md §8(d) algorithmic bytes per kernel class from the work counters (include/artis_constants.h
+    enum artis_work): the r-packet kernel reads/writes the record, steps, scans lines, evaluates kappa and
+    estimators; the macro-atom kernel reads a 72-byte rate record per jump and 40 bytes per transition touched;
+    the k-packet kernel scans cooling terms."""
     w = [float(x) for x in work]
-    return (608.0 * w[0] + 168.0 * w[1] + 64.0 * w[2] + 88.0 * w[5] + 8.0 * nions_total * w[4] + 48.0 * w[6]
-            + 32.0 * w[7] + 72.0 * w[8] + 40.0 * w[9] + 16.0 * w[11])
+    rpkt = (608.0 * w[0] + 168.0 * w[1] + 64.0 * w[2] + 88.0 * w[5] + 8.0 * nions_total * w[4] + 48.0 * w[6]
+            + 32.0 * w[7])
+    ma = 72.0 * w[8] + 40.0 * w[9]
+    kpkt = 16.0 * w[11]
+    return {"rpkt": rpkt, "ma": ma, "kpkt": kpkt}
+
+
+KERNEL_NAME = {"rpkt": "k_rpkt", "ma": "k_ma<true, 1>", "kpkt": "k_kpkt"}
 
 
 def main():
@@ -42,7 +55,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--packets", type=int, default=4_000_000, help="packets per GPU")
+    ap.add_argument("--packets", type=int, default=10_000_000, help="packets per GPU (SURVEY.md §8(d): 1e7)")
     ap.add_argument("--ngrid", type=int, default=50)
     ap.add_argument("--nts", type=int, default=10)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU time of the cpu_baseline sample")
@@ -124,18 +137,25 @@ def main():
     total_packet_timesteps = world * P * args.steps
     value = total_packet_timesteps / elapsed
     avg_transport_s = float(np.mean(transport_ms)) / 1e3
-    alg_bytes = byte_model(work, model.nions_total)
-    achieved_gbs = alg_bytes / avg_transport_s / 1e9
+    alg = byte_model(work, model.nions_total)
+    kt = {k: (float(np.mean([t[k][0] for t in ktimes])), float(np.mean([t[k][1] for t in ktimes])))
+          for k in ("rpkt", "ma", "kpkt")}
+    dom = max(("rpkt", "ma"), key=lambda k: kt[k][0])
+    dom_ms, dom_launches = kt[dom]
+    launches = max(dom_launches, 1.0)
+    bytes_per_launch = alg[dom] / launches
+    avg_launch_s = dom_ms / 1e3 / launches
+    achieved_gbs = bytes_per_launch / max(avg_launch_s, 1e-12) / 1e9
     traffic = None
-    prof = os.path.join(REPO, "profiles", "pmc_transport_bytes.json")
-    if os.path.exists(prof):
+    for prof in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json"))):
         try:
             pm = json.load(open(prof))
-            if pm.get("packets") == P and pm.get("ngrid") == args.ngrid and pm.get("nts") == nts:
-                traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
-            traffic = None
-
+            continue
+        if pm.get("packets") == P and pm.get("ngrid") == args.ngrid and pm.get("nts") == nts:
+            kd = pm.get("kernels", {}).get(KERNEL_NAME[dom])
+            if kd:
+                traffic = kd["hbm_bytes_per_launch"]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -190,15 +210,17 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "k_transport",
-                "alg_bytes_per_launch": alg_bytes,
-                "avg_launch_ms": avg_transport_s * 1e3,
+                "kernel": KERNEL_NAME[dom],
+                "alg_bytes_per_launch": bytes_per_launch,
+                "avg_launch_ms": avg_launch_s * 1e3,
+                "launches_per_step": launches,
+                "transport_alg_GBps": sum(alg.values()) / avg_transport_s / 1e9,
             },
             "cpu_baseline": cpu,
             "precompute_ms": float(np.mean(precompute_ms)),
             "transport_ms": float(np.mean(transport_ms)),
             "event_rounds": int(np.max(rounds)) if rounds else 0,
-            "kernel_ms": {k: float(np.mean([kt[k][0] for kt in ktimes])) for k in ktimes[0]} if ktimes else {},
+            "kernel_ms": {k: v[0] for k, v in kt.items()},
             "work_per_packet": {k: float(v) / max(P, 1) for k, v in zip(
                 ["active", "rpkt_steps", "lines_scanned", "line_taus", "kappa_evals", "bf_active", "est_segments",
                  "gc_updates", "ma_jumps", "ma_trans", "kpkt", "kpkt_terms", "escaped", "es_scat", "bb_events",
