@@ -148,9 +148,13 @@ void build_atomic(Model &m, std::mt19937_64 &rng) {
   const int Zs[3] = {26, 27, 28};
   const double masses[3] = {55.845, 58.933, 58.693};
   // ionisation potentials [eV] of stages I..V
-  const double ionpots[3][5] = {{7.902, 16.199, 30.651, 54.91, 75.0},
-                                {7.881, 17.084, 33.50, 51.27, 79.5},
-                                {7.640, 18.169, 35.19, 54.92, 76.06}};
+  const double ip0[3][5] = {{7.902, 16.199, 30.651, 54.91, 75.0},
+                            {7.881, 17.084, 33.50, 51.27, 79.5},
+                            {7.640, 18.169, 35.19, 54.92, 76.06}};
+  const double ipscale = (m.cfg.ionpot_scale > 0.) ? m.cfg.ionpot_scale : 1.;
+  double ionpots[3][5];
+  for (int e = 0; e < 3; e++)
+    for (int j = 0; j < 5; j++) ionpots[e][j] = ip0[e][j] * ipscale;
   m.nelements = 3;
   m.maxnions = 4;
   const int nlev = m.cfg.nlevels_per_ion;
@@ -930,6 +934,7 @@ void artis_synth_default_config(artis_synth_config *cfg) {
   cfg->T0 = 1.0e4;
   cfg->n_tclasses = 32;
   cfg->seed = 1281360349ull;
+  cfg->ionpot_scale = 1.;
 }
 
 artis_model *artis_model_synth(const artis_synth_config *cfg) {

@@ -30,6 +30,7 @@ typedef struct artis_synth_config {
   double T0;                 /* T(v) = T0 * (1 + 0.5 exp(-v / 5e8)) */
   int32_t n_tclasses;        /* temperature quantisation for the cooling-rate stand-in */
   uint64_t seed;
+  double ionpot_scale;       /* scales every ionisation potential (test configs with bf-active continua); 0 = 1 */
 } artis_synth_config;
 
 typedef struct artis_model artis_model;

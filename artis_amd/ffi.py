@@ -116,6 +116,7 @@ class SynthConfig(C.Structure):
         ("T0", C.c_double),
         ("n_tclasses", C.c_int32),
         ("seed", C.c_uint64),
+        ("ionpot_scale", C.c_double),
     ]
 
 

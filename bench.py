@@ -157,9 +157,11 @@ def main():
             if kd:
                 traffic = kd["hbm_bytes_per_launch"]
     cpu = None
+    parity_line = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import oracle_lib
+        import parity
 
         nthreads = min(16, os.cpu_count() or 1)
         calib = packets[:256].copy()
@@ -171,6 +173,18 @@ def main():
         t = time.perf_counter()
         oracle_lib.update_packets(model, nts, sample, nthreads=nthreads)
         cpu_dt = time.perf_counter() - t
+        # parity on the same sample: the engine's packets after the timed steps are the same histories
+        gpu_pk = np.zeros_like(packets)
+        eng.download(gpu_pk)
+        gs = gpu_pk[:n_sample]
+        bad = parity.discrete_mismatch(gs, sample)
+        parity_line = {
+            "sample_packets": n_sample,
+            "discrete_state_match": float(1.0 - bad.mean()),
+            "max_fp_rel": max(parity.fp_max_rel(gs, sample, ~bad).values()),
+            "spectrum_l1": parity.spectrum_l1(gs, sample),
+            "spectrum": "escaped-packet energy in 1000 log bins of nu_rf over [NU_MIN_R, NU_MAX_R] (spec.out binning)",
+        }
         cpu = {
             "value": n_sample / cpu_dt,
             "unit": "packets/s",
@@ -217,6 +231,7 @@ def main():
                 "transport_alg_GBps": sum(alg.values()) / avg_transport_s / 1e9,
             },
             "cpu_baseline": cpu,
+            "parity_vs_cpu": parity_line,
             "precompute_ms": float(np.mean(precompute_ms)),
             "transport_ms": float(np.mean(transport_ms)),
             "event_rounds": int(np.max(rounds)) if rounds else 0,

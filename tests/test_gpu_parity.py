@@ -210,3 +210,19 @@ def test_event_queue_engine_matches_megakernel(small_model, engine_factory, monk
     assert (ea.counters == eb.counters).all()
     assert (wa == eng2.last_work()).all()
     parity.assert_estimators_match(ea, eb)
+
+
+def test_bf_and_kpacket_heavy_model(engine_factory):
+    """Dense, low-ionisation-potential model: bf absorptions activate macro-atoms and k-packets, fb
+    deactivations emit through select_continuum_nu, k-packets cool through every channel.  These rare paths
+    run through the cold-call machinery of the r-packet kernel (a bug there once wrote stale cold words)."""
+    from artis_amd.model import Model
+
+    m = Model(ngrid_1d=6, nlevels_per_ion=30, n_ionising=30, max_lines=2000, ntstep=30, ionpot_scale=0.35,
+              mass_msun=0.1, T0=8000.0)
+    eng = engine_factory(m)
+    _, pg, eg, po, eo, _ = _pair(m, eng, 10, 300, seed=3)
+    c = eo.counters
+    assert c[5] > 0 and c[10] > 0 and c[20] > 0, c  # bf activations, fb deactivations, k-packets from bf
+    parity.assert_packets_match(pg, po)
+    parity.assert_estimators_match(eg, eo)
