@@ -23,7 +23,7 @@ ABI_SYMBOLS = [
     "artis_gpu_packets_restore", "artis_gpu_update_packets_resident", "artis_gpu_estimators_zero",
     "artis_gpu_estimators_download", "artis_gpu_estimator_block_doubles", "artis_gpu_estimator_block_to_device",
     "artis_gpu_estimator_block_from_device", "artis_gpu_last_transport_ms", "artis_gpu_last_precompute_ms",
-    "artis_gpu_last_work_counts", "artis_gpu_last_rounds", "artis_gpu_last_kernel_times", "artis_gpu_last_error", "artis_gpu_abi_version",
+    "artis_gpu_last_work_counts", "artis_gpu_last_rounds", "artis_gpu_spectrum", "artis_gpu_last_kernel_times", "artis_gpu_last_error", "artis_gpu_abi_version",
 ]
 
 _gpu_lib = None
@@ -52,6 +52,7 @@ def gpu_lib():
         L.artis_gpu_last_work_counts.argtypes = [vp]
         L.artis_gpu_last_error.restype = C.c_char_p
         L.artis_gpu_last_rounds.restype = C.c_int64
+        L.artis_gpu_spectrum.argtypes = [C.c_int, C.c_int, vp, vp, vp]
         _gpu_lib = L
     return _gpu_lib
 
@@ -134,6 +135,16 @@ class Engine:
         w = np.zeros(ffi.ARTIS_WORK_COUNT, dtype=np.int64)
         self.lib.artis_gpu_last_work_counts(w.ctypes.data)
         return w
+
+    def spectrum(self, nnubins=1000, nprocs=1):
+        """Device-binned spectrum [ntstep, nnubins] and light curves (lum, lumcmf) of the resident packets."""
+        nt = self.model.cfg.ntstep
+        spec = np.zeros((nt, nnubins))
+        lc = np.zeros(nt)
+        lccmf = np.zeros(nt)
+        self._check(self.lib.artis_gpu_spectrum(int(nnubins), int(nprocs), spec.ctypes.data, lc.ctypes.data,
+                                                lccmf.ctypes.data), "spectrum")
+        return spec, lc, lccmf
 
     def last_kernel_times(self):
         """{class: (ms, launches)} for the last transport: rpkt, ma, kpkt, classify."""

@@ -28,6 +28,7 @@
 #include "physics.h"
 #include "transport.h"
 #include "wavefront.h"
+#include "spectrum.h"
 
 // ================================================================================================= kernels
 
@@ -661,6 +662,37 @@ const char *artis_gpu_last_error(void) { return G.last_error.c_str(); }
 double artis_gpu_last_transport_ms(void) { return G.last_transport_ms; }
 double artis_gpu_last_precompute_ms(void) { return G.last_precompute_ms; }
 int64_t artis_gpu_last_rounds(void) { return G.last_rounds; }
+
+int artis_gpu_spectrum(int nnubins, int nprocs, double *spec_flux, double *lc_lum, double *lc_lumcmf) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  if (nnubins <= 0 || nprocs <= 0 || !spec_flux || !lc_lum || !lc_lumcmf) return ARTIS_ERR_BAD_ARGUMENT;
+  const int nt = G.ntstep;
+  // spectrum.cc:491-500 init_spectra: bin edges with the reference's expressions (host libm)
+  const double nu_min = G.K.G.nu_min_r, nu_max = G.K.G.nu_max_r;
+  const double dlognu = (log(nu_max) - log(nu_min)) / nnubins;
+  std::vector<double> delta(nnubins);
+  for (int nnu = 0; nnu < nnubins; nnu++)
+    delta[nnu] = exp(log(nu_min) + ((nnu + 1) * (dlognu))) - exp(log(nu_min) + (nnu * (dlognu)));
+  const size_t nspec = (size_t)nt * nnubins;
+  double *d = nullptr;
+  HIPCHK(hipMalloc(&d, (nspec + 2 * (size_t)nt + nnubins) * sizeof(double)));
+  double *d_spec = d, *d_lc = d + nspec, *d_lccmf = d_lc + nt, *d_delta = d_lccmf + nt;
+  int rc = 0;
+  if ((rc = sync_ctx()) == 0) {
+    HIPCHK(hipMemsetAsync(d, 0, (nspec + 2 * (size_t)nt) * sizeof(double), G.stream));
+    HIPCHK(hipMemcpyAsync(d_delta, delta.data(), nnubins * sizeof(double), hipMemcpyHostToDevice, G.stream));
+    if (G.npkts > 0)
+      k_spectrum<<<(unsigned)((G.npkts + 255) / 256), 256, 0, G.stream>>>(
+          G.d_ctx, G.d_soa, G.npkts, nt, nnubins, dlognu, d_delta, (double)nprocs, d_spec, d_lc, d_lccmf);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(spec_flux, d_spec, nspec * sizeof(double), hipMemcpyDeviceToHost, G.stream));
+    HIPCHK(hipMemcpyAsync(lc_lum, d_lc, nt * sizeof(double), hipMemcpyDeviceToHost, G.stream));
+    HIPCHK(hipMemcpyAsync(lc_lumcmf, d_lccmf, nt * sizeof(double), hipMemcpyDeviceToHost, G.stream));
+    HIPCHK(hipStreamSynchronize(G.stream));
+  }
+  (void)hipFree(d);
+  return rc;
+}
 int artis_gpu_last_kernel_times(double ms[4], int64_t launches[4]) {
   for (int c = 0; c < 4; c++) {
     ms[c] = G.last_kernel_ms[c];
@@ -908,6 +940,8 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   rc |= dupload(&GG.cell_mgi, g->cell_mgi, g->ngrid);
   GG.coordmax0 = g->coordmax[0];
   GG.tmin = g->tmin;
+  GG.tmax = g->tmax;
+  GG.vmax = g->vmax;
   GG.rmax = g->rmax;
   GG.wid = 2 * g->coordmax[0] / g->ncoordgrid[0];  // grid.cc:76-91
   G.ntstep = g->ntstep;

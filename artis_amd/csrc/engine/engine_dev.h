@@ -86,7 +86,7 @@ struct DevGeom {
   int32_t ngrid, npts_model;
   const double *cell_pos_min;
   const int32_t *cell_mgi;
-  double coordmax0, tmin, rmax, wid;
+  double coordmax0, tmin, rmax, wid, tmax, vmax;
   const double *ts_start, *ts_width, *ts_mid;
   double nu_min_r, nu_max_r;
 };

@@ -323,6 +323,13 @@ double artis_gpu_last_precompute_ms(void);
 /* Per-call event counts from the device (steps, lines scanned, kappa evaluations, ...), for the byte model. */
 #define ARTIS_WORK_COUNT 16
 int artis_gpu_last_work_counts(int64_t out[ARTIS_WORK_COUNT]);
+/* Emergent spectrum and light curve of the escaped r-packets among the resident packets, binned on the device:
+ * the binning of write_partial_lightcurve_spectra (spectrum.cc:641-721) -- add_to_spec (spectrum.cc:339-362,
+ * angle-averaged, no emission-resolved columns) and add_to_lc_res (light_curve.cc:34-54) -- over
+ * nnubins log bins in [nu_min_r, nu_max_r] (MNUBINS = 1000 in the reference).  Overwrites the caller's
+ * spec_flux[ntstep * nnubins] (timestep-major), lc_lum[ntstep], lc_lumcmf[ntstep]; nprocs is the rank count
+ * the reference divides by (globals::nprocs). */
+int artis_gpu_spectrum(int nnubins, int nprocs, double *spec_flux, double *lc_lum, double *lc_lumcmf);
 int64_t artis_gpu_last_rounds(void);  /* event-queue rounds of the last update (0: megakernel path) */
 /* device time (ms, HIP events around every launch) and launch count of the last update per kernel class:
  * [0] r-packet, [1] macro-atom (incl. cell binning), [2] k-packet, [3] classify */

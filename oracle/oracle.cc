@@ -2046,4 +2046,48 @@ double oracle_phixs(const artis_atomic_tables *at, int table, double nu_edge, do
   return photoionization_crosssection_fromtable(c, at->phixs_xs + (size_t)table * at->nphixspoints, nu_edge, nu);
 }
 
+// write_partial_lightcurve_spectra binning (spectrum.cc:641-721): add_to_lc_res (light_curve.cc:34-54) and
+// add_to_spec (spectrum.cc:339-362) for every escaped r-packet, in packet order; timestep lookup sn3d.h:168-180
+static int oracle_get_timestep(const artis_geometry *g, double t) {
+  for (int nts = 0; nts < g->ntstep; nts++) {
+    const double tsend = (nts < (g->ntstep - 1)) ? g->ts_start[nts + 1] : g->tmax;
+    if (t >= g->ts_start[nts] && t < tsend) return nts;
+  }
+  return -1;
+}
+int oracle_spectrum(const artis_geometry *g, const artis_packet *pkts, int npkts, int nnubins, int nprocs,
+                    double *spec, double *lc_lum, double *lc_lumcmf) {
+  const int nt = g->ntstep;
+  for (int64_t j = 0; j < (int64_t)nt * nnubins; j++) spec[j] = 0.;
+  for (int j = 0; j < nt; j++) lc_lum[j] = lc_lumcmf[j] = 0.;
+  const double nu_min = g->nu_min_r, nu_max = g->nu_max_r;
+  const double dlognu = (log(nu_max) - log(nu_min)) / nnubins;  // spectrum.cc:352
+  std::vector<double> delta_freq(nnubins);
+  for (int nnu = 0; nnu < nnubins; nnu++)  // spectrum.cc:497-500
+    delta_freq[nnu] = exp(log(nu_min) + ((nnu + 1) * (dlognu))) - exp(log(nu_min) + (nnu * (dlognu)));
+  const double cmfcorr = sqrt(1. - (g->vmax * g->vmax / ARTIS_CLIGHTSQUARED));
+  for (int ii = 0; ii < npkts; ii++) {
+    const artis_packet *p = &pkts[ii];
+    if (p->type != ARTIS_TYPE_ESCAPE || p->escape_type != ARTIS_TYPE_RPKT) continue;
+    const double t_arrive = p->escape_time - (dot(p->pos, p->dir) / ARTIS_CLIGHT_PROP);  // vectors.h:146-152
+    if (t_arrive > g->tmin && t_arrive < g->tmax) {
+      const int nts = oracle_get_timestep(g, t_arrive);
+      lc_lum[nts] += p->e_rf / g->ts_width[nts] / nprocs;
+    }
+    const double t_arrive_cmf = p->escape_time * cmfcorr;  // vectors.h:154-156
+    if (t_arrive_cmf > g->tmin && t_arrive_cmf < g->tmax) {
+      const int nts = oracle_get_timestep(g, t_arrive_cmf);
+      lc_lumcmf[nts] += p->e_cmf / g->ts_width[nts] / nprocs / cmfcorr;
+    }
+    if (t_arrive > g->tmin && t_arrive < g->tmax && p->nu_rf > nu_min && p->nu_rf < nu_max) {
+      const int nts = oracle_get_timestep(g, t_arrive);
+      const int nnu = (int)((log(p->nu_rf) - log(nu_min)) / dlognu);
+      if (nnu < 0 || nnu >= nnubins) return -1;  // assert_always(nnu < globals::nnubins)
+      spec[(int64_t)nts * nnubins + nnu] +=
+          p->e_rf / g->ts_width[nts] / delta_freq[nnu] / 4.e12 / ARTIS_PI / ARTIS_PARSEC / ARTIS_PARSEC / nprocs;
+    }
+  }
+  return 0;
+}
+
 }  // extern "C"

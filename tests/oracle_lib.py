@@ -39,3 +39,20 @@ def update_packets(model, nts, packets, est=None, nthreads=0, params=None):
     if rc != 0:
         raise RuntimeError(f"oracle_update_packets -> {rc}")
     return est, work
+
+
+def spectrum(model, packets, nnubins=1000, nprocs=1):
+    """Oracle binning of write_partial_lightcurve_spectra (oracle/oracle.cc: oracle_spectrum)."""
+    L = lib()
+    L.oracle_spectrum.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                  C.c_void_p]
+    L.oracle_spectrum.restype = C.c_int
+    nt = model.cfg.ntstep
+    spec = np.zeros((nt, nnubins))
+    lc = np.zeros(nt)
+    lccmf = np.zeros(nt)
+    rc = L.oracle_spectrum(model.geometry, packets.ctypes.data, len(packets), nnubins, nprocs, spec.ctypes.data,
+                           lc.ctypes.data, lccmf.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("oracle_spectrum: frequency bin out of range")
+    return spec, lc, lccmf
