@@ -211,10 +211,13 @@ __global__ void k_marates(Ctx K, int nts) {
   const double epsilon_current = K.T.level_epsilon[ul];
   const double statweight = K.T.level_stat_weight[ul];
   const bool cache = K.C.have_macache;
-  const int4 ml = K.T.ma_level[ul];
-  double *rec = cache ? K.C.ma_rec + (int64_t)k * K.C.ma_rec_stride + ml.x : nullptr;
-  double *cum_drad = rec + MA_HEAD_DOUBLES, *cum_dint = cum_drad + ml.y, *cum_uint = cum_dint + ml.y;
-  double *cum_rrad = cum_uint + ml.z, *cum_rint = cum_rrad + ml.w, *cum_uhi = cum_rint + ml.w;
+  const MaMeta mm = K.T.ma_meta[ul];
+  double *rec = cache ? K.C.ma_rec + (int64_t)k * K.C.ma_rec_stride + mm.rec_off : nullptr;
+  // record layout (engine_dev.h DevCells::ma_rec): Eytzinger arrays at rec + 8 + position (1-based)
+  double *eyt_dint = rec + 8, *eyt_uint = rec + 8 + mm.nd;
+  double *cum_drad = rec + ARTIS_MA_ACTION_COUNT + mm.nd + mm.nu, *cum_rrad = cum_drad + mm.nd;
+  double *cum_rint = cum_rrad + mm.nr, *cum_uhi = cum_rint + mm.nr;
+  const int32_t *inv_d = K.T.eyt_inv + K.T.eyt_off[mm.nd], *inv_u = K.T.eyt_inv + K.T.eyt_off[mm.nu];
   double pr[ARTIS_MA_ACTION_COUNT];
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) pr[a] = 0.;
   const int ndowntrans = K.T.level_ndowntrans[ul];
@@ -231,7 +234,7 @@ __global__ void k_marates(Ctx K, int nts) {
     pr[ARTIS_MA_ACTION_INTERNALDOWNSAME] += (R + C) * epsilon_target;
     if (cache) {
       cum_drad[j] = pr[ARTIS_MA_ACTION_RADDEEXC];
-      cum_dint[j] = pr[ARTIS_MA_ACTION_INTERNALDOWNSAME];
+      eyt_dint[inv_d[j]] = pr[ARTIS_MA_ACTION_INTERNALDOWNSAME];
     }
   }
   if (i > 0 && l <= K.T.ion_maxrecombininglevel[ui]) {
@@ -259,7 +262,7 @@ __global__ void k_marates(Ctx K, int nts) {
     const double R = rad_excitation_ratecoeff(K, pops, mgi, e, i, l, upper, epsilon_trans, li, t_mid);
     const double C = col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, e, i, upper));
     pr[ARTIS_MA_ACTION_INTERNALUPSAME] += (R + C + 0.) * epsilon_current;
-    if (cache) cum_uint[j] = pr[ARTIS_MA_ACTION_INTERNALUPSAME];
+    if (cache) eyt_uint[inv_u[j]] = pr[ARTIS_MA_ACTION_INTERNALUPSAME];
   }
   if (i < K.T.elem_nions[e] - 1 && l < K.T.ion_ionisinglevels[ui]) {
     const int nt = K.T.level_nphixstargets[ul];
@@ -274,17 +277,6 @@ __global__ void k_marates(Ctx K, int nts) {
   }
   double *out = cache ? rec : K.C.marates + ((int64_t)k * nl + ul) * ARTIS_MA_ACTION_COUNT;
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) out[a] = pr[a];
-  if (cache) {  // walk metadata in the head line (engine_dev.h MA_HEAD_*)
-    int32_t *h = reinterpret_cast<int32_t *>(rec);
-    h[MA_HEAD_DOFF] = doff;
-    h[MA_HEAD_UOFF] = uoff;
-    h[MA_HEAD_BASE_LOWER] = (i > 0) ? K.T.ion_uniqueleveloffset[ui - 1] : -1;
-    h[MA_HEAD_ND] = ndowntrans;
-    h[MA_HEAD_NU] = nuptrans;
-    h[MA_HEAD_NR] = ml.w;
-    h[MA_HEAD_NT] = (i < K.T.elem_nions[e] - 1 && l < K.T.ion_ionisinglevels[ui]) ? K.T.level_nphixstargets[ul] : 0;
-    h[MA_HEAD_UL] = ul;
-  }
 }
 
 __global__ void k_aos_to_soa(const uint64_t *__restrict__ aos, uint64_t *__restrict__ soa, int64_t n) {
@@ -860,22 +852,57 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   // macro-atom records per level (engine_dev.h DevCells::ma_rec): recombination targets are the ionising levels
   // of the lower ion for levels l <= maxrecombininglevel of ions i > 0 (macroatom.cc:104-124); up-higher targets
   // are the phixs targets of ionising levels of non-top ions (get_nphixstargets)
-  std::vector<int4> mal(nl);
+  std::vector<MaMeta> mm(nl);
   int64_t marec = 0;
+  int nmax = 1;
   for (int e = 0; e < ne; e++)
     for (int i = 0; i < a->elem_nions[e]; i++) {
       const int ui = a->elem_uniqueionoffset[e] + i;
       for (int l = 0; l < a->ion_nlevels[ui]; l++) {
         const int ul = a->ion_uniqueleveloffset[ui] + l;
-        const int nrec = (i > 0 && l <= a->ion_maxrecombininglevel[ui]) ? a->ion_ionisinglevels[ui - 1] : 0;
-        const int nt = (i < a->elem_nions[e] - 1 && l < a->ion_ionisinglevels[ui]) ? a->level_nphixstargets[ul] : 0;
-        const int64_t len = MA_HEAD_DOUBLES + 2 * (int64_t)a->level_ndowntrans[ul] + a->level_nuptrans[ul] + 2 * nrec + nt;
-        mal[ul] = make_int4((int)marec, a->level_ndowntrans[ul], a->level_nuptrans[ul], nrec);
-        marec += (len + 15) / 16 * 16;  // 128-byte aligned records: the head is one cache line
+        MaMeta &m = mm[ul];
+        m.nr = (i > 0 && l <= a->ion_maxrecombininglevel[ui]) ? a->ion_ionisinglevels[ui - 1] : 0;
+        m.nt = (i < a->elem_nions[e] - 1 && l < a->ion_ionisinglevels[ui]) ? a->level_nphixstargets[ul] : 0;
+        m.nd = a->level_ndowntrans[ul];
+        m.nu = a->level_nuptrans[ul];
+        m.doff = a->level_downtrans_offset[ul];
+        m.uoff = a->level_uptrans_offset[ul];
+        m.base_lower = (i > 0) ? a->ion_uniqueleveloffset[ui - 1] : -1;
+        m.rec_off = (int32_t)marec;
+        const int64_t len = ARTIS_MA_ACTION_COUNT + 2 * (int64_t)m.nd + m.nu + 2 * (int64_t)m.nr + m.nt;
+        marec += (len + 15) / 16 * 16;  // 128-byte aligned records: totals + the tree tops share a line
+        nmax = std::max(nmax, std::max(m.nd, m.nu));
       }
     }
-  rc |= dupload(&T.ma_level, mal.data(), nl);
+  rc |= dupload(&T.ma_meta, mm.data(), nl);
   {
+    // Eytzinger positions: in-order traversal of the implicit tree 1..n gives the sorted order
+    std::vector<int32_t> off(nmax + 2, 0), inv;
+    for (int n = 0; n <= nmax; n++) {
+      off[n] = (int32_t)inv.size();
+      std::vector<int32_t> pos(n + 1);
+      int next = 0;
+      std::vector<int> stack;
+      int k = 1;
+      while (k <= n || !stack.empty()) {  // iterative in-order walk
+        while (k <= n) {
+          stack.push_back(k);
+          k = 2 * k;
+        }
+        k = stack.back();
+        stack.pop_back();
+        pos[k] = next++;
+        k = 2 * k + 1;
+      }
+      std::vector<int32_t> iv(n);
+      for (int q = 1; q <= n; q++) iv[pos[q]] = q;
+      inv.insert(inv.end(), iv.begin(), iv.end());
+    }
+    off[nmax + 1] = (int32_t)inv.size();
+    if (inv.empty()) inv.push_back(0);
+    rc |= dupload(&T.eyt_inv, inv.data(), inv.size());
+    rc |= dupload(&T.eyt_off, off.data(), off.size());
+    // internal same-ion jump targets in the Eytzinger order of their cumulative arrays
     std::vector<int2> dt(std::max<int64_t>(ndown, 1)), ut(std::max<int64_t>(nup, 1));
     for (int e = 0; e < ne; e++)
       for (int i = 0; i < a->elem_nions[e]; i++) {
@@ -883,19 +910,19 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
         const int base = a->ion_uniqueleveloffset[ui];
         for (int l = 0; l < a->ion_nlevels[ui]; l++) {
           const int ul = base + l;
-          const int doff = a->level_downtrans_offset[ul], uoff = a->level_uptrans_offset[ul];
-          for (int j = 0; j < a->level_ndowntrans[ul]; j++) {
-            const int t = base + a->line_lowerlevelindex[a->downtrans_lineindex[doff + j]];
-            dt[doff + j] = make_int2(t, mal[t].x);
+          const MaMeta &m = mm[ul];
+          for (int j = 0; j < m.nd; j++) {
+            const int t = base + a->line_lowerlevelindex[a->downtrans_lineindex[m.doff + j]];
+            dt[m.doff + inv[off[m.nd] + j] - 1] = make_int2(t, mm[t].rec_off);
           }
-          for (int j = 0; j < a->level_nuptrans[ul]; j++) {
-            const int t = base + a->line_upperlevelindex[a->uptrans_lineindex[uoff + j]];
-            ut[uoff + j] = make_int2(t, mal[t].x);
+          for (int j = 0; j < m.nu; j++) {
+            const int t = base + a->line_upperlevelindex[a->uptrans_lineindex[m.uoff + j]];
+            ut[m.uoff + inv[off[m.nu] + j] - 1] = make_int2(t, mm[t].rec_off);
           }
         }
       }
-    rc |= dupload(&T.down_target, dt.data(), dt.size());
-    rc |= dupload(&T.up_target, ut.data(), ut.size());
+    rc |= dupload(&T.down_target_eyt, dt.data(), dt.size());
+    rc |= dupload(&T.up_target_eyt, ut.data(), ut.size());
   }
   G.ma_rec_stride = marec;
   rc |= dupload(&T.allcont_nu_edge, a->allcont_nu_edge, nb);

@@ -17,16 +17,13 @@
 
 #define PKT_WORDS 38
 
-// macro-atom record head: doubles 0..8 = totals; int32 slots (of the 32 in the 128-byte head):
-#define MA_HEAD_DOUBLES 16
-#define MA_HEAD_DOFF 18        // level_downtrans_offset
-#define MA_HEAD_UOFF 19        // level_uptrans_offset
-#define MA_HEAD_BASE_LOWER 20  // unique index of level 0 of the next lower ion (-1 if none)
-#define MA_HEAD_ND 21
-#define MA_HEAD_NU 22
-#define MA_HEAD_NR 23          // recombination targets
-#define MA_HEAD_NT 24          // ionisation targets (get_nphixstargets)
-#define MA_HEAD_UL 25          // the level's own unique index
+// static per-level data of the cached macro-atom walk (two 16-byte loads; the table is L2-resident)
+struct __attribute__((aligned(16))) MaMeta {
+  int32_t rec_off;     // offset (doubles) of the level's record inside a cell's block
+  int32_t doff, uoff;  // level_downtrans_offset, level_uptrans_offset
+  int32_t base_lower;  // unique index of level 0 of the next lower ion (-1 if none)
+  int32_t nd, nu, nr, nt;  // #downtrans, #uptrans, #recombination targets, #ionisation targets
+};
 
 // one 32-byte record per line for the line walk of get_event (two 16-byte loads)
 struct __attribute__((aligned(16))) LineTau {
@@ -69,9 +66,12 @@ struct DevTab {
   const LineMA *line_ma;
   // per level: offset (doubles) of its macro-atom record inside a cell's record block, #downtrans, #uptrans,
   // #recombination targets (ionising levels of the lower ion, 0 if the level does not recombine)
-  const int4 *ma_level;
-  // each downtrans / uptrans target as (unique level index, offset of its macro-atom record in a cell block)
-  const int2 *down_target, *up_target;
+  const MaMeta *ma_meta;  // [nlevels_total]
+  // targets of the internal same-ion jumps in Eytzinger order of their level's cumulative arrays:
+  // (unique level index, offset of its macro-atom record in a cell block)
+  const int2 *down_target_eyt, *up_target_eyt;
+  // Eytzinger position (1-based) of sorted index j in an array of n entries: eyt_inv[eyt_off[n] + j]
+  const int32_t *eyt_inv, *eyt_off;
   const double *allcont_nu_edge, *allcont_probability;
   const int32_t *allcont_element, *allcont_ion, *allcont_level, *allcont_target, *allcont_upperlevel,
       *allcont_phixstable, *allcont_groundindex;
@@ -105,13 +105,13 @@ struct DevCells {
   double *depratio;    // [n_nonempty * nbf]            departure ratios (rpkt.cc:1140-1151)
   double *corrphot;    // [n_nonempty * ntargets_total] get_corrphotoioncoeff (ratecoeff.cc:1247-1308)
   double *cooling;     // [n_nonempty * ncoolingterms]  cumulative cooling_contrib (kpkt.cc:167-308)
-  // macro-atom cache: per (cell, level) one contiguous record, 128-byte aligned.  Its first 128 bytes (the head,
-  // one cache line) hold the 9 processrates totals (macroatom.cc:57-159) and the level's walk metadata
-  // (MA_HEAD_* int slots); then come the running sums of the individual rates (the cellhistory individ_*
-  // arrays, globals.h:174-183) summed in the reference's order, so that a search returns the reference's
-  // linear-scan choice:
-  //   [head | rad_deexc (ndown) | internal_down_same (ndown) | internal_up_same (nup) |
-  //    rad_recomb (nrec) | internal_down_lower (nrec) | internal_up_higher (nphixstargets)]
+  // macro-atom cache: per (cell, level) one contiguous record, 128-byte aligned: the 9 processrates totals
+  // (macroatom.cc:57-159), then the running sums of the individual rates (the cellhistory individ_* arrays,
+  // globals.h:174-183) summed in the reference's order, so that a search returns the reference's linear-scan
+  // choice.  The two arrays of the internal same-ion jumps -- most of all jumps -- are stored in Eytzinger
+  // (BFS) order right after the totals, so the first levels of their search tree share the totals' cache line:
+  //   [9 totals | internal_down_same (nd, Eytzinger) | internal_up_same (nu, Eytzinger) | rad_deexc (nd) |
+  //    rad_recomb (nr) | internal_down_lower (nr) | internal_up_higher (nt)]
   double *ma_rec;      // [n_nonempty * ma_rec_stride], or nullptr
   int64_t ma_rec_stride;
   int32_t have_macache;

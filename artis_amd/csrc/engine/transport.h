@@ -953,25 +953,16 @@ struct MaEnd {
                         // FB: a = level of the lower ion, b = unique index of the recombining level
 };
 
-// macroatom.cc:416-482, one pass of the do_macroatom loop: select a process from the per-cell totals, then the
-// transition from the cumulative individual rates (CACHE: binary search in the level's record) or by
-// recomputing the individual rates in the reference's order (no cache)
-template <bool CACHE>
+// macroatom.cc:416-482, one pass of the do_macroatom loop without the macro-atom cache: select a process from
+// the per-cell totals, then the transition by recomputing the individual rates in the reference's order
+// (ma_jump_cached below is the cached form)
 DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &m, double t_mid, MaEnd &end,
                   int number) {
   m.jumps++;
   const int element = m.element, ion = m.ion, level = m.level, k = m.k;
   const double epsilon_current = epsilon(K, element, ion, level);
   const int ul = ulev(K, element, ion, level);
-  int4 ml = make_int4(0, 0, 0, 0);
-  const double *rec = nullptr, *pr;
-  if constexpr (CACHE) {
-    ml = K.T.ma_level[ul];
-    rec = K.C.ma_rec + (int64_t)k * K.C.ma_rec_stride + ml.x;
-    pr = rec;
-  } else {
-    pr = K.C.marates + ((int64_t)k * K.T.nlevels_total + ul) * ARTIS_MA_ACTION_COUNT;
-  }
+  const double *pr = K.C.marates + ((int64_t)k * K.T.nlevels_total + ul) * ARTIS_MA_ACTION_COUNT;
   const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
   double processrates[ARTIS_MA_ACTION_COUNT];
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) processrates[a] = pr[a];
@@ -999,10 +990,7 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
     int linelistindex = -99;
     const int ndowntrans = K.T.level_ndowntrans[ul];
     const int doff = K.T.level_downtrans_offset[ul];
-    if constexpr (CACHE) {
-      const int j = first_above(rec + MA_HEAD_DOUBLES, ndowntrans, zr * processrates[ARTIS_MA_ACTION_RADDEEXC], m.ntrans);
-      if (j < ndowntrans) linelistindex = K.T.downtrans_lineindex[doff + j];
-    } else {
+    {
       double r = 0.;
       for (int j = 0; j < ndowntrans; j++) {
         const int li = K.T.downtrans_lineindex[doff + j];
@@ -1039,11 +1027,7 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
     int lower = -99;
     const int ndowntrans = K.T.level_ndowntrans[ul];
     const int doff = K.T.level_downtrans_offset[ul];
-    if constexpr (CACHE) {
-      const int j = first_above(rec + MA_HEAD_DOUBLES + ml.y, ndowntrans, zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNSAME],
-                                m.ntrans);
-      if (j < ndowntrans) lower = K.T.line_lower[K.T.downtrans_lineindex[doff + j]];
-    } else {
+    {
       const double statweight = stat_weight(K, element, ion, level);
       double r = 0.;
       for (int j = 0; j < ndowntrans; j++) {
@@ -1076,10 +1060,7 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
     double r = 0;
     const int nlevels = get_ionisinglevels(K, element, upperion - 1);
     int lower = 0;
-    if constexpr (CACHE) {
-      lower = first_above(rec + MA_HEAD_DOUBLES + 2 * ml.y + ml.z, nlevels, zr * processrates[ARTIS_MA_ACTION_RADRECOMB], m.ntrans);
-      r = (lower < nlevels) ? DBL_MAX : -DBL_MAX;
-    } else {
+    {
       for (lower = 0; lower < nlevels; lower++) {
         const double epsilon_trans = epsilon_current - epsilon(K, element, upperion - 1, lower);
         const double R = rad_recombination_ratecoeff(K, T_e, nne, element, upperion, level, lower);
@@ -1103,10 +1084,7 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
     const double zr = artis_rng_uniform(&rng);
     const int nlevels = get_ionisinglevels(K, element, ion - 1);
     int lower;
-    if constexpr (CACHE) {
-      lower = first_above(rec + MA_HEAD_DOUBLES + 2 * ml.y + ml.z + ml.w, nlevels, zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNLOWER],
-                          m.ntrans);
-    } else {
+    {
       double r = 0.;
       for (lower = 0; lower < nlevels; lower++) {
         const double epsilon_target = epsilon(K, element, ion - 1, lower);
@@ -1131,11 +1109,7 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
     int upper = -99;
     const int nuptrans = K.T.level_nuptrans[ul];
     const int uoff = K.T.level_uptrans_offset[ul];
-    if constexpr (CACHE) {
-      const int j = first_above(rec + MA_HEAD_DOUBLES + 2 * ml.y, nuptrans, zr * processrates[ARTIS_MA_ACTION_INTERNALUPSAME],
-                                m.ntrans);
-      if (j < nuptrans) upper = K.T.line_upper[K.T.uptrans_lineindex[uoff + j]];
-    } else {
+    {
       const double statweight = stat_weight(K, element, ion, level);
       double r = 0.;
       for (int j = 0; j < nuptrans; j++) {
@@ -1167,12 +1141,7 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
     const double zr = artis_rng_uniform(&rng);
     const int nt = get_nphixstargets(K, element, ion, level);
     bool found;
-    if constexpr (CACHE) {
-      const int t = first_above(rec + MA_HEAD_DOUBLES + 2 * ml.y + ml.z + 2 * ml.w, nt,
-                                zr * processrates[ARTIS_MA_ACTION_INTERNALUPHIGHER], m.ntrans);
-      found = t < nt;
-      if (found) upper = get_phixsupperlevel(K, element, ion, level, t);
-    } else {
+    {
       double r = 0.;
       const int slot0 = K.T.level_phixstargets_offset[ul];
       for (int t = 0; t < nt; t++) {
@@ -1198,9 +1167,11 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
 }
 
 // The cached walk in its lean form: lane state = (unique level, record offset, cell block).  Per jump: the
-// level's 128-byte record head (totals + walk metadata, seven independent 16-byte loads), a two-level search
-// in the selected cumulative array, and one 8-byte load of the target (level, record offset).  Same
-// selections, same RNG draws as ma_jump<true>.
+// level's 32-byte MaMeta (L2-resident table) and its 9 totals (independent loads), then the search in the
+// selected cumulative array -- for the internal same-ion jumps (most jumps) an Eytzinger search whose first
+// tree levels sit in the totals' cache line -- and one 8-byte load of the target (level, record offset).
+// The walk is bound by HBM traffic, so the layout minimises cache lines touched per jump.
+// Same selections and RNG draws as the uncached ma_jump.
 struct MaLaneC {
   int ul, rec_off;
   const double *block;  // K.C.ma_rec + k * ma_rec_stride
@@ -1208,65 +1179,28 @@ struct MaLaneC {
   unsigned long long ntrans;
 };
 
-// first j in [0, n) with cum[j] > x (n if none), the same answer as first_above, in two dependent rounds of
-// independent loads: three quartile probes, then the (<= 8-entry) quarter they select.  Longer arrays fall back
-// to bisection inside the quarter.
-DEVFN int first_above_2level(const double *cum, int n, double x, unsigned long long &probes) {
-  if (n <= 0) return 0;
-  const int step = (n + 3) >> 2;
-  const int p0 = min(step - 1, n - 1), p1 = min(2 * step - 1, n - 1), p2 = min(3 * step - 1, n - 1);
-  const double c0 = cum[p0], c1 = cum[p1], c2 = cum[p2];
-  probes += 3;
-  int lo, hi;  // answer in [lo, hi]
-  if (c0 > x) {
-    lo = 0;
-    hi = p0;
-  } else if (c1 > x) {
-    lo = p0 + 1;
-    hi = p1;
-  } else if (c2 > x) {
-    lo = p1 + 1;
-    hi = p2;
-  } else {
-    lo = p2 + 1;
-    hi = n;  // n = none above
-  }
-  // within [lo, hi): at most `step` entries; hi itself (if < n) is known to be above x
-  int len = hi - lo;
-  if (len <= 8) {
-    double v[8];
-#pragma unroll
-    for (int q = 0; q < 8; q++) v[q] = (q < len) ? cum[lo + q] : 0.;
-    probes += len;
-    int j = hi;
-#pragma unroll
-    for (int q = 7; q >= 0; q--)
-      if (q < len && v[q] > x) j = lo + q;
-    return j;
-  }
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
+// Eytzinger (BFS-order) search: e[k], k = 1..n, holds the sorted array's entries in BFS order of its implicit
+// binary search tree.  Returns the Eytzinger position of the first sorted entry > x, 0 if none -- the same
+// entry first_above finds in the sorted array.
+DEVFN int eytzinger_first_above(const double *e, int n, double x, unsigned long long &probes) {
+  unsigned k = 1;
+  while (k <= (unsigned)n) {
+    k = 2 * k + (e[k] <= x ? 1u : 0u);
     probes++;
-    if (cum[mid] > x)
-      hi = mid;
-    else
-      lo = mid + 1;
   }
-  return lo;
+  return (int)(k >> __ffs(~k));
 }
 
 DEVFN int ma_jump_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneC &m, MaEnd &end, int number) {
   m.jumps++;
-  const double *rec = m.block + m.rec_off;
-  const int4 *hp = reinterpret_cast<const int4 *>(rec);
-  const int4 h0 = hp[0], h1 = hp[1], h2 = hp[2], h3 = hp[3], h4 = hp[4], h5 = hp[5], h6 = hp[6];
-  auto dbl = [](int lo, int hi) { return __hiloint2double(hi, lo); };
-  const double pr[ARTIS_MA_ACTION_COUNT] = {dbl(h0.x, h0.y), dbl(h0.z, h0.w), dbl(h1.x, h1.y),
-                                            dbl(h1.z, h1.w), dbl(h2.x, h2.y), dbl(h2.z, h2.w),
-                                            dbl(h3.x, h3.y), dbl(h3.z, h3.w), dbl(h4.x, h4.y)};
-  // head int slots 18.. (engine_dev.h MA_HEAD_*): h4.z doff, h4.w uoff, h5 = base_lower, nd, nu, nr; h6.x nt
-  const int doff = h4.z, uoff = h4.w, base_lower = h5.x, nd = h5.y, nu = h5.z, nr = h5.w, nt = h6.x;
   const int ul = m.ul;
+  const double *rec = m.block + m.rec_off;
+  const int4 *mp = reinterpret_cast<const int4 *>(K.T.ma_meta + ul);
+  const int4 w0 = mp[0], w1 = mp[1];
+  const int doff = w0.y, uoff = w0.z, base_lower = w0.w, nd = w1.x, nu = w1.y, nr = w1.z, nt = w1.w;
+  const double2 *r2 = reinterpret_cast<const double2 *>(rec);
+  const double2 t01 = r2[0], t23 = r2[1], t45 = r2[2], t67 = r2[3];
+  const double pr[ARTIS_MA_ACTION_COUNT] = {t01.x, t01.y, t23.x, t23.y, t45.x, t45.y, t67.x, t67.y, rec[8]};
   double total_transitions = 0.;
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) total_transitions += pr[a];
   const double zrand = artis_rng_uniform(&rng);
@@ -1293,20 +1227,31 @@ DEVFN int ma_jump_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
     fail(K, ERR_MA_SELECT, number, 100 + sel);
     return MA_FAILED;
   }
-  // the cumulative array of the selected action inside the level record (engine_dev.h DevCells::ma_rec)
+  const double zr = artis_rng_uniform(&rng);
+  const double x = zr * pr[sel];
+  if (sel == ARTIS_MA_ACTION_INTERNALDOWNSAME || sel == ARTIS_MA_ACTION_INTERNALUPSAME) {
+    const bool down = sel == ARTIS_MA_ACTION_INTERNALDOWNSAME;
+    const int cnt = down ? nd : nu;
+    const int pos = eytzinger_first_above(rec + 8 + (down ? 0 : nd), cnt, x, m.ntrans);
+    if (pos == 0) {
+      fail(K, ERR_MA_SELECT, number, 10 + sel);
+      return MA_FAILED;
+    }
+    const int2 t = down ? K.T.down_target_eyt[doff + pos - 1] : K.T.up_target_eyt[uoff + pos - 1];
+    m.ul = t.x;
+    m.rec_off = t.y;
+    return MA_CONTINUE;
+  }
+  // the sorted cumulative arrays after the two Eytzinger ones (engine_dev.h DevCells::ma_rec)
+  const double *sorted = rec + ARTIS_MA_ACTION_COUNT + nd + nu;
   int off, cnt;
   switch (sel) {
     case ARTIS_MA_ACTION_RADDEEXC: off = 0; cnt = nd; break;
-    case ARTIS_MA_ACTION_INTERNALDOWNSAME: off = nd; cnt = nd; break;
-    case ARTIS_MA_ACTION_INTERNALUPSAME: off = 2 * nd; cnt = nu; break;
-    case ARTIS_MA_ACTION_RADRECOMB: off = 2 * nd + nu; cnt = nr; break;
-    case ARTIS_MA_ACTION_INTERNALDOWNLOWER: off = 2 * nd + nu + nr; cnt = nr; break;
-    default: off = 2 * nd + nu + 2 * nr; cnt = nt; break;  // INTERNALUPHIGHER
+    case ARTIS_MA_ACTION_RADRECOMB: off = nd; cnt = nr; break;
+    case ARTIS_MA_ACTION_INTERNALDOWNLOWER: off = nd + nr; cnt = nr; break;
+    default: off = nd + 2 * nr; cnt = nt; break;  // INTERNALUPHIGHER
   }
-  const double zr = artis_rng_uniform(&rng);
-  // bisection: fewer scattered loads per jump than the two-level variant (the walk is bound by the rate of
-  // per-lane scattered loads, not by their latency -- DESIGN.md §5)
-  const int j = first_above(rec + MA_HEAD_DOUBLES + off, cnt, zr * pr[sel], m.ntrans);
+  const int j = first_above(sorted + off, cnt, x, m.ntrans);
   if (j >= cnt) {
     fail(K, ERR_MA_SELECT, number, 10 + sel);
     return MA_FAILED;
@@ -1324,28 +1269,16 @@ DEVFN int ma_jump_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
       end.a = j;
       end.b = ul;
       return MA_END_FB;
-    case ARTIS_MA_ACTION_INTERNALDOWNSAME: {
-      const int2 t = K.T.down_target[doff + j];
-      m.ul = t.x;
-      m.rec_off = t.y;
-      return MA_CONTINUE;
-    }
-    case ARTIS_MA_ACTION_INTERNALUPSAME: {
-      const int2 t = K.T.up_target[uoff + j];
-      m.ul = t.x;
-      m.rec_off = t.y;
-      return MA_CONTINUE;
-    }
     case ARTIS_MA_ACTION_INTERNALDOWNLOWER:
       lctr(L, CTR_MA_STAT_INTERNALDOWNLOWER);
       m.ul = base_lower + j;
-      m.rec_off = K.T.ma_level[m.ul].x;
+      m.rec_off = K.T.ma_meta[m.ul].rec_off;
       return MA_CONTINUE;
     default: {  // INTERNALUPHIGHER (macroatom.cc:382-414)
       lctr(L, CTR_MA_STAT_INTERNALUPHIGHER);
       const int ui = K.T.level_ui[ul];
       m.ul = K.T.ion_uniqueleveloffset[ui + 1] + K.T.phixstarget_levelindex[K.T.level_phixstargets_offset[ul] + j];
-      m.rec_off = K.T.ma_level[m.ul].x;
+      m.rec_off = K.T.ma_meta[m.ul].rec_off;
       return MA_CONTINUE;
     }
   }
@@ -1446,7 +1379,7 @@ DEVNI void do_macroatom(Tx &x, Pkt &p) {
   if (K.C.have_macache) {
     MaLaneC m;
     m.ul = ulev(K, p.ma_element, p.ma_ion, p.ma_level);
-    m.rec_off = K.T.ma_level[m.ul].x;
+    m.rec_off = K.T.ma_meta[m.ul].rec_off;
     m.block = K.C.ma_rec + (int64_t)K.C.ne_index[mgi] * K.C.ma_rec_stride;
     m.jumps = 0;
     m.ntrans = 0;
@@ -1458,7 +1391,7 @@ DEVNI void do_macroatom(Tx &x, Pkt &p) {
     MaLane m;
     ma_lane_init(K, m, p.where, p.ma_element, p.ma_ion, p.ma_level);
     const double t_mid = K.G.ts_mid[x.nts];
-    while ((r = ma_jump<false>(K, x.L, x.rng, m, t_mid, e, p.number)) == MA_CONTINUE && m.jumps < MA_MAX_JUMPS) {
+    while ((r = ma_jump(K, x.L, x.rng, m, t_mid, e, p.number)) == MA_CONTINUE && m.jumps < MA_MAX_JUMPS) {
     }
     jumps = m.jumps;
     ntrans = m.ntrans;

@@ -341,7 +341,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
           const int mgi = cell_mgi(K, where);
           if constexpr (CACHE) {
             mc.ul = ulev(K, lo32(w36), hi32(w36), lo32(w37));
-            mc.rec_off = K.T.ma_level[mc.ul].x;
+            mc.rec_off = K.T.ma_meta[mc.ul].rec_off;
             mc.block = K.C.ma_rec + (int64_t)K.C.ne_index[mgi] * K.C.ma_rec_stride;
             mc.jumps = 0;
             mc.ntrans = 0;
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
         r = ma_jump_cached(K, L, rng, mc, e, (int)rng.key1);
         jumps = mc.jumps;
       } else {
-        r = ma_jump<false>(K, L, rng, m, t_mid, e, (int)rng.key1);
+        r = ma_jump(K, L, rng, m, t_mid, e, (int)rng.key1);
         jumps = m.jumps;
       }
       if (r != MA_CONTINUE || jumps >= MA_MAX_JUMPS) {
