@@ -191,13 +191,16 @@ __global__ void k_cooling(Ctx K) {
 // cache it also stores the running sums of the individual rates (cellhistory individ_* arrays).
 // Workitems are ordered level-major (consecutive lanes = the same level in consecutive cells): every lane of
 // a wave walks the same transition lists, so the atomic-data loads are wave-uniform and the loops do not
-// diverge; only the cell's populations and temperatures differ per lane.
-__global__ void k_marates(Ctx K, int nts) {
+// diverge; only the cell's populations (level-major copy popsT) and temperatures differ per lane.
+// With the cache, one launch covers levels [ul0, ul0 + nlev) and writes the records position-major into the
+// scratch S (S[(rec_off(ul) - rec_off(ul0)) * n_ne + pos * n_ne + k]: every store is 64 consecutive doubles);
+// k_marec then transposes them into the per-cell records.
+__global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict__ S) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nl = K.T.nlevels_total;
   const int64_t nne_cells = K.C.n_nonempty;
-  if (idx >= nne_cells * nl) return;
-  const int ul = (int)(idx / nne_cells);
+  if (idx >= nne_cells * nlev) return;
+  const int ul = ul0 + (int)(idx / nne_cells);
   const int k = (int)(idx % nne_cells);
   const int mgi = K.C.ne_mgi[k];
   const int ui = K.T.level_ui[ul];
@@ -207,16 +210,19 @@ __global__ void k_marates(Ctx K, int nts) {
   const double t_mid = K.G.ts_mid[nts];
   const float T_e = K.C.Te[mgi];
   const float nne = K.C.nne[mgi];
-  const double *pops = K.C.pops + (int64_t)k * nl;
+  const double *popsT = K.C.popsT + k;  // popsT[ul * nne_cells]: level ul of this lane's cell
+  const double n_self = popsT[ul * nne_cells];
   const double epsilon_current = K.T.level_epsilon[ul];
   const double statweight = K.T.level_stat_weight[ul];
   const bool cache = K.C.have_macache;
   const MaMeta mm = K.T.ma_meta[ul];
-  double *rec = cache ? K.C.ma_rec + (int64_t)k * K.C.ma_rec_stride + mm.rec_off : nullptr;
-  // record layout (engine_dev.h DevCells::ma_rec): Eytzinger arrays at rec + 8 + position (1-based)
-  double *eyt_dint = rec + 8, *eyt_uint = rec + 8 + mm.nd;
-  double *cum_drad = rec + ARTIS_MA_ACTION_COUNT + mm.nd + mm.nu, *cum_rrad = cum_drad + mm.nd;
-  double *cum_rint = cum_rrad + mm.nr, *cum_uhi = cum_rint + mm.nr;
+  // record position p of this (cell, level) in the scratch; record layout (engine_dev.h DevCells::ma_rec):
+  // Eytzinger arrays at 8 + position (1-based), then the sorted cumulative arrays
+  double *rec = cache ? S + (int64_t)(mm.rec_off - K.T.ma_meta[ul0].rec_off) * nne_cells + k : nullptr;
+#define REC(p) rec[(int64_t)(p) * nne_cells]
+  const int eyt_d = 8, eyt_u = 8 + mm.nd;
+  const int cum_drad = ARTIS_MA_ACTION_COUNT + mm.nd + mm.nu, cum_rrad = cum_drad + mm.nd;
+  const int cum_rint = cum_rrad + mm.nr, cum_uhi = cum_rint + mm.nr;
   const int32_t *inv_d = K.T.eyt_inv + K.T.eyt_off[mm.nd], *inv_u = K.T.eyt_inv + K.T.eyt_off[mm.nu];
   double pr[ARTIS_MA_ACTION_COUNT];
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) pr[a] = 0.;
@@ -227,14 +233,15 @@ __global__ void k_marates(Ctx K, int nts) {
     const int lower = K.T.line_lower[li];
     const double epsilon_target = epsilon(K, e, i, lower);
     const double epsilon_trans = epsilon_current - epsilon_target;
-    const double R = rad_deexcitation_ratecoeff(K, pops, e, i, l, lower, epsilon_trans, li, t_mid);
+    const double n_l = popsT[(int64_t)(ul - l + lower) * nne_cells];
+    const double R = rad_deexcitation_ratecoeff_n(K, n_self, n_l, li, t_mid);
     const double C = col_deexcitation_ratecoeff(K, T_e, nne, epsilon_trans, li, stat_weight(K, e, i, lower), statweight);
     pr[ARTIS_MA_ACTION_RADDEEXC] += R * epsilon_trans;
     pr[ARTIS_MA_ACTION_COLDEEXC] += C * epsilon_trans;
     pr[ARTIS_MA_ACTION_INTERNALDOWNSAME] += (R + C) * epsilon_target;
     if (cache) {
-      cum_drad[j] = pr[ARTIS_MA_ACTION_RADDEEXC];
-      eyt_dint[inv_d[j]] = pr[ARTIS_MA_ACTION_INTERNALDOWNSAME];
+      REC(cum_drad + j) = pr[ARTIS_MA_ACTION_RADDEEXC];
+      REC(eyt_d + inv_d[j]) = pr[ARTIS_MA_ACTION_INTERNALDOWNSAME];
     }
   }
   if (i > 0 && l <= K.T.ion_maxrecombininglevel[ui]) {
@@ -248,35 +255,81 @@ __global__ void k_marates(Ctx K, int nts) {
       pr[ARTIS_MA_ACTION_RADRECOMB] += R * epsilon_trans;
       pr[ARTIS_MA_ACTION_COLRECOMB] += C * epsilon_trans;
       if (cache) {
-        cum_rrad[lower] = pr[ARTIS_MA_ACTION_RADRECOMB];
-        cum_rint[lower] = pr[ARTIS_MA_ACTION_INTERNALDOWNLOWER];
+        REC(cum_rrad + lower) = pr[ARTIS_MA_ACTION_RADRECOMB];
+        REC(cum_rint + lower) = pr[ARTIS_MA_ACTION_INTERNALDOWNLOWER];
       }
     }
   }
   const int nuptrans = K.T.level_nuptrans[ul];
   const int uoff = K.T.level_uptrans_offset[ul];
+  const double T_R = K.C.TR[mgi], W = K.C.W[mgi];
   for (int j = 0; j < nuptrans; j++) {
     const int li = K.T.uptrans_lineindex[uoff + j];
     const int upper = K.T.line_upper[li];
     const double epsilon_trans = epsilon(K, e, i, upper) - epsilon_current;
-    const double R = rad_excitation_ratecoeff(K, pops, mgi, e, i, l, upper, epsilon_trans, li, t_mid);
+    const double n_u = popsT[(int64_t)(ul - l + upper) * nne_cells];
+    const double R = rad_excitation_ratecoeff_n(K, n_u, n_self, T_R, W, epsilon_trans, li, t_mid);
     const double C = col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, e, i, upper));
     pr[ARTIS_MA_ACTION_INTERNALUPSAME] += (R + C + 0.) * epsilon_current;
-    if (cache) eyt_uint[inv_u[j]] = pr[ARTIS_MA_ACTION_INTERNALUPSAME];
+    if (cache) REC(eyt_u + inv_u[j]) = pr[ARTIS_MA_ACTION_INTERNALUPSAME];
   }
   if (i < K.T.elem_nions[e] - 1 && l < K.T.ion_ionisinglevels[ui]) {
     const int nt = K.T.level_nphixstargets[ul];
     const int slot0 = K.T.level_phixstargets_offset[ul];
     for (int t = 0; t < nt; t++) {
       const double epsilon_trans = get_phixs_threshold(K, e, i, l, t);
-      const double R = K.C.corrphot[(int64_t)k * K.T.ntargets_total + slot0 + t];
+      const double R = K.C.corrphotT[(int64_t)(slot0 + t) * nne_cells + k];
       const double C = col_ionization_ratecoeff(K, T_e, nne, e, i, l, t, epsilon_trans);
       pr[ARTIS_MA_ACTION_INTERNALUPHIGHER] += (R + C) * epsilon_current;
-      if (cache) cum_uhi[t] = pr[ARTIS_MA_ACTION_INTERNALUPHIGHER];
+      if (cache) REC(cum_uhi + t) = pr[ARTIS_MA_ACTION_INTERNALUPHIGHER];
     }
   }
-  double *out = cache ? rec : K.C.marates + ((int64_t)k * nl + ul) * ARTIS_MA_ACTION_COUNT;
-  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) out[a] = pr[a];
+  if (cache) {
+    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) REC(a) = pr[a];
+  } else {
+    double *out = K.C.marates + ((int64_t)k * nl + ul) * ARTIS_MA_ACTION_COUNT;
+    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) out[a] = pr[a];
+  }
+#undef REC
+}
+
+// Scratch -> records for the levels of one k_marates launch: block (level ul0 + blockIdx.y, 64 cells from
+// 64 * blockIdx.x); 64x64 (position x cell) tiles through LDS, read along cells, written along positions.
+__global__ __launch_bounds__(256) void k_marec(Ctx K, int ul0, const double *__restrict__ S) {
+  __shared__ double tile[64][65];
+  const int ul = ul0 + blockIdx.y;
+  const int64_t n_ne = K.C.n_nonempty;
+  const MaMeta mm = K.T.ma_meta[ul];
+  const int len = ARTIS_MA_ACTION_COUNT + 2 * mm.nd + mm.nu + 2 * mm.nr + mm.nt;
+  const double *src = S + (int64_t)(mm.rec_off - K.T.ma_meta[ul0].rec_off) * n_ne;
+  const int64_t c0 = (int64_t)blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int p0 = 0; p0 < len; p0 += 64) {
+    for (int j = ty; j < 64; j += 4)
+      if (p0 + j < len && c0 + tx < n_ne) tile[j][tx] = src[(int64_t)(p0 + j) * n_ne + c0 + tx];
+    __syncthreads();
+    for (int j = ty; j < 64; j += 4)
+      if (p0 + tx < len && c0 + j < n_ne)
+        K.C.ma_rec[(c0 + j) * K.C.ma_rec_stride + mm.rec_off + p0 + tx] = tile[tx][j];
+    __syncthreads();
+  }
+}
+
+// out[c * rows + r] = in[r * cols + c], through a 64x64 LDS tile (one wave reads rows, writes columns)
+__global__ __launch_bounds__(256) void k_transpose(const double *__restrict__ in, double *__restrict__ out,
+                                                   int64_t rows, int64_t cols) {
+  __shared__ double tile[64][65];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int j = ty; j < 64; j += 4) {
+    const int64_t r = r0 + j, c = c0 + tx;
+    if (r < rows && c < cols) tile[j][tx] = in[r * cols + c];
+  }
+  __syncthreads();
+  for (int j = ty; j < 64; j += 4) {
+    const int64_t c = c0 + j, r = r0 + tx;
+    if (r < rows && c < cols) out[c * rows + r] = tile[tx][j];
+  }
 }
 
 __global__ void k_aos_to_soa(const uint64_t *__restrict__ aos, uint64_t *__restrict__ soa, int64_t n) {
@@ -398,6 +451,9 @@ struct Engine {
   int npts_model = 0, nelements = 0, maxnions = 0, nions_total = 0, nlines = 0, ngrid = 0, ntstep = 0;
   int64_t n_est_doubles = 0;  // J..bfheat + scalars
   int64_t ma_rec_stride = 0;
+  std::vector<int64_t> h_rec_off;  // record offset per level (+ stride at the end), ascending in level index
+  double *d_marec_scratch = nullptr;  // k_marates output, [position][cell] per level (engine.hip k_marec)
+  int64_t marec_scratch_doubles = 0;
   double *d_estblock = nullptr;
   int32_t *d_target_ul = nullptr, *d_target_t = nullptr;
   bool have_cells = false;
@@ -925,6 +981,9 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     rc |= dupload(&T.up_target_eyt, ut.data(), ut.size());
   }
   G.ma_rec_stride = marec;
+  G.h_rec_off.resize(nl + 1);
+  for (int ul = 0; ul < nl; ul++) G.h_rec_off[ul] = mm[ul].rec_off;
+  G.h_rec_off[nl] = marec;
   rc |= dupload(&T.allcont_nu_edge, a->allcont_nu_edge, nb);
   rc |= dupload(&T.allcont_probability, a->allcont_probability, nb);
   rc |= dupload(&T.allcont_element, a->allcont_element, nb);
@@ -1049,6 +1108,8 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   rc |= dalloc(&C.ffsum, (size_t)nne_cells);
   rc |= dalloc(&C.depratio, (size_t)nne_cells * nb);
   rc |= dalloc(&C.corrphot, (size_t)nne_cells * (ntg + 1));
+  rc |= dalloc(&C.popsT, (size_t)nne_cells * nl);
+  rc |= dalloc(&C.corrphotT, (size_t)nne_cells * (ntg + 1));
   rc |= dalloc(&C.cooling, (size_t)nne_cells * a->ncoolingterms);
   C.ma_rec_stride = G.ma_rec_stride;
   C.have_macache = 0;
@@ -1058,13 +1119,24 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     size_t freeb = 0, totalb = 0;
     (void)hipMemGetInfo(&freeb, &totalb);
     const double need = (double)nne_cells * (double)C.ma_rec_stride * 8.0;
+    // k_marates scratch: up to 1/8 of the cache, at least the largest level's records
+    int64_t maxlev = 0;
+    for (int ul = 0; ul < nl; ul++) maxlev = std::max(maxlev, G.h_rec_off[ul + 1] - G.h_rec_off[ul]);
+    int64_t scratch = (int64_t)(need / 8.0 / 8.0);
+    if (const char *sm = getenv("ARTIS_GPU_MAREC_SCRATCH_MB")) scratch = (int64_t)(atof(sm) * (1 << 20) / 8);
+    scratch = std::max<int64_t>(maxlev * nne_cells, scratch);
     const char *env = getenv("ARTIS_GPU_NO_MACACHE");
-    if (!(env && env[0] == '1') && need < 0.75 * (double)freeb) {
-      double *mc = nullptr;
+    if (!(env && env[0] == '1') && need + 8.0 * (double)scratch < 0.75 * (double)freeb) {
+      double *mc = nullptr, *sc = nullptr;
       if (hipMalloc((void **)&mc, (size_t)need) == hipSuccess) {
         G.allocs.push_back(mc);
-        C.ma_rec = mc;
-        C.have_macache = 1;
+        if (hipMalloc((void **)&sc, (size_t)scratch * 8) == hipSuccess) {
+          G.allocs.push_back(sc);
+          C.ma_rec = mc;
+          C.have_macache = 1;
+          G.d_marec_scratch = sc;
+          G.marec_scratch_doubles = scratch;
+        }
       }
     }
   }
@@ -1133,7 +1205,27 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
     k_bfcells<<<(unsigned)((nbt + B - 1) / B), B, 0, G.stream>>>(G.K, G.d_target_ul, G.d_target_t);
     const int64_t nci = (int64_t)n_ne * ni;
     k_cooling<<<(unsigned)((nci + 63) / 64), 64, 0, G.stream>>>(G.K);
-    k_marates<<<(unsigned)((nlv + 255) / 256), 256, 0, G.stream>>>(G.K, nts);
+    const int64_t ntg = G.K.T.ntargets_total;
+    k_transpose<<<dim3((unsigned)((nl + 63) / 64), (unsigned)((n_ne + 63) / 64)), 256, 0, G.stream>>>(
+        G.K.C.pops, G.K.C.popsT, n_ne, nl);
+    if (ntg > 0)
+      k_transpose<<<dim3((unsigned)((ntg + 63) / 64), (unsigned)((n_ne + 63) / 64)), 256, 0, G.stream>>>(
+          G.K.C.corrphot, G.K.C.corrphotT, n_ne, ntg);
+    if (!G.K.C.have_macache) {
+      k_marates<<<(unsigned)((nlv + 255) / 256), 256, 0, G.stream>>>(G.K, nts, 0, (int)nl, nullptr);
+    } else {
+      // batches of levels whose records fit the scratch
+      for (int ul0 = 0; ul0 < nl;) {
+        int ul1 = ul0 + 1;
+        while (ul1 < nl && (G.h_rec_off[ul1 + 1] - G.h_rec_off[ul0]) * n_ne <= G.marec_scratch_doubles) ul1++;
+        const int nlev = ul1 - ul0;
+        k_marates<<<(unsigned)(((int64_t)nlev * n_ne + 255) / 256), 256, 0, G.stream>>>(G.K, nts, ul0, nlev,
+                                                                                        G.d_marec_scratch);
+        k_marec<<<dim3((unsigned)((n_ne + 63) / 64), (unsigned)nlev), 256, 0, G.stream>>>(G.K, ul0,
+                                                                                          G.d_marec_scratch);
+        ul0 = ul1;
+      }
+    }
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(G.ev1, G.stream));

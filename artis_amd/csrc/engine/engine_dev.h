@@ -104,6 +104,9 @@ struct DevCells {
   double *ffsum;       // [n_nonempty]                  sum_ions Z^2 n_ion of calculate_kappa_ff (rpkt.cc:1036-1058)
   double *depratio;    // [n_nonempty * nbf]            departure ratios (rpkt.cc:1140-1151)
   double *corrphot;    // [n_nonempty * ntargets_total] get_corrphotoioncoeff (ratecoeff.cc:1247-1308)
+  // level-major copies for k_marates, whose lanes run over consecutive cells of one level (coalesced reads)
+  double *popsT;       // [nlevels_total * n_nonempty]
+  double *corrphotT;   // [ntargets_total * n_nonempty]
   double *cooling;     // [n_nonempty * ncoolingterms]  cumulative cooling_contrib (kpkt.cc:167-308)
   // macro-atom cache: per (cell, level) one contiguous record, 128-byte aligned: the 9 processrates totals
   // (macroatom.cc:57-159), then the running sums of the individual rates (the cellhistory individ_* arrays,

@@ -256,10 +256,7 @@ DEVFN double col_excitation_ratecoeff(const Ctx &K, float T_e, float nne, int li
   return C;
 }
 // macroatom.cc:503-548 (populations from the per-cell table, B coefficients from LineMA)
-DEVFN double rad_deexcitation_ratecoeff(const Ctx &K, const double *pops, int e, int i, int upper, int lower,
-                                        double epsilon_trans, int li, double t_current) {
-  const double n_u = pops[ulev(K, e, i, upper)];
-  const double n_l = pops[ulev(K, e, i, lower)];
+DEVFN double rad_deexcitation_ratecoeff_n(const Ctx &K, double n_u, double n_l, int li, double t_current) {
   double R = 0.0;
   const LineMA lm = K.T.line_ma[li];
   const double A_ul = K.T.line_A[li];
@@ -270,11 +267,13 @@ DEVFN double rad_deexcitation_ratecoeff(const Ctx &K, const double *pops, int e,
   }
   return R;
 }
+DEVFN double rad_deexcitation_ratecoeff(const Ctx &K, const double *pops, int e, int i, int upper, int lower,
+                                        double epsilon_trans, int li, double t_current) {
+  return rad_deexcitation_ratecoeff_n(K, pops[ulev(K, e, i, upper)], pops[ulev(K, e, i, lower)], li, t_current);
+}
 // macroatom.cc:550-643 (radfield.cc:898-943: dilute blackbody, radfield.h:44-48)
-DEVFN double rad_excitation_ratecoeff(const Ctx &K, const double *pops, int mgi, int e, int i, int lower, int upper,
-                                      double epsilon_trans, int li, double t_current) {
-  const double n_u = pops[ulev(K, e, i, upper)];
-  const double n_l = pops[ulev(K, e, i, lower)];
+DEVFN double rad_excitation_ratecoeff_n(const Ctx &K, double n_u, double n_l, double T_R, double W,
+                                        double epsilon_trans, int li, double t_current) {
   double R = 0.0;
   const LineMA lm = K.T.line_ma[li];
   const double tau_sobolev = (lm.B_lu * n_l - lm.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_current;
@@ -282,11 +281,14 @@ DEVFN double rad_excitation_ratecoeff(const Ctx &K, const double *pops, int mgi,
     const double beta = 1.0 / tau_sobolev * (-expm1(-tau_sobolev));
     const double R_over_J_nu = n_l > 0. ? (lm.B_lu - lm.B_ul * n_u / n_l) * beta : lm.B_lu * beta;
     const double nu_trans = epsilon_trans / ARTIS_H;
-    const double T_R = K.C.TR[mgi];
-    const double W = K.C.W[mgi];
     R = R_over_J_nu * (W * ARTIS_TWOHOVERCLIGHTSQUARED * lm.nu3 / expm1(ARTIS_HOVERKB * nu_trans / T_R));
   }
   return R;
+}
+DEVFN double rad_excitation_ratecoeff(const Ctx &K, const double *pops, int mgi, int e, int i, int lower, int upper,
+                                      double epsilon_trans, int li, double t_current) {
+  return rad_excitation_ratecoeff_n(K, pops[ulev(K, e, i, upper)], pops[ulev(K, e, i, lower)], K.C.TR[mgi],
+                                    K.C.W[mgi], epsilon_trans, li, t_current);
 }
 // macroatom.cc:645-678
 DEVFN double rad_recombination_ratecoeff(const Ctx &K, float T_e, float nne, int e, int upperion, int upper, int lower) {

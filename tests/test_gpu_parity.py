@@ -98,6 +98,24 @@ def test_without_macroatom_cache_is_identical(small_model, engine_factory, monke
     assert max(parity.fp_max_rel(a, b).values()) <= parity.FP_RTOL
 
 
+def test_macroatom_records_in_many_batches_are_identical(small_model, engine_factory, monkeypatch):
+    """k_marates writes the records in level batches through a scratch (k_marec transposes them); a scratch
+    of one level's records forces one batch per level and must give the same packets."""
+    small_model.set_timestep(9)
+    pk = small_model.init_rpackets(9, 2000, seed=6)
+    eng = engine_factory(small_model)
+    eng.upload_cellstate(9)
+    a = pk.copy()
+    eng.update_packets(9, a)
+    eng.close()
+    monkeypatch.setenv("ARTIS_GPU_MAREC_SCRATCH_MB", "0")
+    eng2 = engine_factory(small_model)
+    eng2.upload_cellstate(9)
+    b = pk.copy()
+    eng2.update_packets(9, b)
+    assert a.tobytes() == b.tobytes()
+
+
 def test_resident_path_matches_host_path(small_model, engine_factory):
     """upload + update_packets_resident + download == update_packets, and snapshot/restore replays exactly."""
     eng = engine_factory(small_model)

@@ -13,18 +13,24 @@ import csv
 import glob
 import json
 import os
+import sqlite3
 
 
 def load(d, counter):
     agg = collections.defaultdict(float)
     launches = collections.Counter()
+    rows = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != counter:
-                continue
-            name = r["Kernel_Name"].split("(")[0].replace("void ", "")
-            agg[name] += float(r["Counter_Value"])
-            launches[name] += 1
+        rows += [(r["Kernel_Name"], r["Counter_Name"], r["Counter_Value"]) for r in csv.DictReader(open(f))]
+    for f in glob.glob(os.path.join(d, "**", "*.db"), recursive=True):  # rocprofv3 >= 7.2 default (rocpd sqlite)
+        rows += sqlite3.connect(f).execute(
+            "select kernel_name, counter_name, value from counters_collection").fetchall()
+    for kname, cname, value in rows:
+        if cname != counter:
+            continue
+        name = kname.split("(")[0].replace("void ", "")
+        agg[name] += float(value)
+        launches[name] += 1
     return agg, launches
 
 
