@@ -18,7 +18,7 @@ _GPU_SO_LOAD = os.environ.get("ARTIS_GPU_SO", GPU_SO)
 
 # every function declared in include/artis_gpu.h (tests/test_abi.py checks they are exported)
 ABI_SYMBOLS = [
-    "artis_gpu_init", "artis_gpu_finalize", "artis_gpu_upload_cellstate", "artis_gpu_update_packets",
+    "artis_gpu_init", "artis_gpu_init_gamma", "artis_gpu_finalize", "artis_gpu_upload_cellstate", "artis_gpu_update_packets",
     "artis_gpu_packets_upload", "artis_gpu_packets_download", "artis_gpu_packets_snapshot",
     "artis_gpu_packets_restore", "artis_gpu_update_packets_resident", "artis_gpu_estimators_zero",
     "artis_gpu_estimators_download", "artis_gpu_estimator_block_doubles", "artis_gpu_estimator_block_to_device",
@@ -38,6 +38,7 @@ def gpu_lib():
         L = C.CDLL(_GPU_SO_LOAD)
         vp = C.c_void_p
         L.artis_gpu_init.argtypes = [C.c_int, vp, vp, C.POINTER(ffi.RunParams)]
+        L.artis_gpu_init_gamma.argtypes = [vp]
         L.artis_gpu_upload_cellstate.argtypes = [C.c_int, vp]
         L.artis_gpu_update_packets.argtypes = [C.c_int, C.c_int, vp, C.c_int, C.POINTER(ffi.Estimators)]
         L.artis_gpu_packets_upload.argtypes = [vp, C.c_int]
@@ -69,6 +70,8 @@ class Engine:
         self.model = model
         self.params = params if params is not None else model.params
         self._check(self.lib.artis_gpu_init(int(device), model.atomic, model.geometry, C.byref(self.params)), "init")
+        if getattr(model, "gamma_spectra", None):
+            self._check(self.lib.artis_gpu_init_gamma(model.gamma_spectra), "init_gamma")
         self.cell_nts = None
 
     def _check(self, rc, what):

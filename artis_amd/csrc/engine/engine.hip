@@ -391,6 +391,10 @@ __global__ __launch_bounds__(TRANSPORT_BLOCK) void k_transport(const Ctx *__rest
             do_kpkt(x, p, t2);
         } else if (pkt_type == ARTIS_TYPE_MA) {
           do_macroatom(x, p);
+        } else if (is_gamma_family(pkt_type) && K.T.g_nlines) {
+          PelletInfo pi;
+          pellet_info_load(soa, n, i, pi);
+          do_gamma_family_step(x, p, pi, t2);
         } else {
           x.err(ERR_UNSUPPORTED_TYPE, p.number, pkt_type);
         }
@@ -617,6 +621,9 @@ int run_wavefront(int64_t n, int nts, double t2) {
   HIPCHK(hipMemsetAsync(W.ctr, 0, NQUEUES * 2 * sizeof(uint32_t), G.stream));
   TSTART(3);
   k_classify<<<(unsigned)((n + WAVE_BLOCK - 1) / WAVE_BLOCK), WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, t2);
+  if (G.K.T.g_nlines) {  // pellets / gammas / leptons -> k-packets ahead of the rounds (counted with classify)
+    k_gamma<<<grid / 4, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+  }
   TEND(3);
   HIPCHK(hipGetLastError());
   int64_t round = 0;
@@ -705,7 +712,7 @@ int run_wavefront(int64_t n, int nts, double t2) {
 // ============================================================================================== C ABI
 extern "C" {
 
-int artis_gpu_abi_version(void) { return 1; }
+int artis_gpu_abi_version(void) { return ARTIS_GPU_ABI_VERSION; }
 const char *artis_gpu_last_error(void) { return G.last_error.c_str(); }
 double artis_gpu_last_transport_ms(void) { return G.last_transport_ms; }
 double artis_gpu_last_precompute_ms(void) { return G.last_precompute_ms; }
@@ -784,10 +791,6 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   if (G.initialised) artis_gpu_finalize();
   if (g->grid_type != ARTIS_GRID_UNIFORM) {
     G.last_error = "only GRID_UNIFORM is propagated by this build";
-    return ARTIS_ERR_UNSUPPORTED;
-  }
-  if (rp->relativistic_doppler) {
-    G.last_error = "USE_RELATIVISTIC_DOPPLER_SHIFT is not propagated by this build";
     return ARTIS_ERR_UNSUPPORTED;
   }
   G.device = device;
@@ -1049,18 +1052,22 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   R.pol_dipole = rp->pol_dipole;
   R.relativistic_doppler = rp->relativistic_doppler;
   R.record_linestat = rp->record_linestat;
+  R.gamma_grey = rp->gamma_grey;
+  R.instant_particle_deposition = rp->instant_particle_deposition;
+  R.nt_solve_spencerfano = rp->nt_solve_spencerfano;
 
-  // estimators: one double block [J | nuJ | ffheat | colheat | gamma | bfheat | scalars(8)]
+  // estimators: one double block [J | nuJ | ffheat | colheat | rpkt_emiss | gamma | bfheat | scalars(10)]
   const int np = g->npts_model;
   const int64_t nion_est = (int64_t)np * ne * a->maxnions;
-  G.n_est_doubles = 4 * (int64_t)np + 2 * nion_est + 8;
+  G.n_est_doubles = 5 * (int64_t)np + 2 * nion_est + 10;
   rc |= dalloc(&G.d_estblock, G.n_est_doubles);
   DevEst &E = G.K.E;
   E.J = G.d_estblock;
   E.nuJ = E.J + np;
   E.ffheat = E.nuJ + np;
   E.colheat = E.ffheat + np;
-  E.gamma = E.colheat + np;
+  E.rpkt_emiss = E.colheat + np;
+  E.gamma = E.rpkt_emiss + np;
   E.bfheat = E.gamma + nion_est;
   E.scalars = E.bfheat + nion_est;
   rc |= dalloc(&E.ecounter, nli);
@@ -1145,7 +1152,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   rc |= dalloc(&G.W.ctr, (size_t)NQUEUES * 2);
   rc |= dalloc(&G.d_ctx, (size_t)1);
   rc |= dalloc(&G.W.stats, (size_t)48);
-  rc |= dalloc(&G.d_cellf, (size_t)8 * np);
+  rc |= dalloc(&G.d_cellf, (size_t)9 * np);
   rc |= dalloc(&G.d_thick, (size_t)np);
   rc |= dalloc(&G.d_abund, (size_t)np * ne);
   rc |= dalloc(&G.d_glp, (size_t)np * ni);
@@ -1162,6 +1169,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   C.nnetot = G.d_cellf + 5 * np;
   C.rho = G.d_cellf + 6 * np;
   C.kappagrey = G.d_cellf + 7 * np;
+  C.ffegrp = G.d_cellf + 8 * np;
   C.thick = G.d_thick;
   C.elem_abundance = G.d_abund;
   C.groundlevelpop = G.d_glp;
@@ -1170,6 +1178,45 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   C.cooling_contrib_ion = G.d_ccion;
   C.corrphotoionrenorm = G.d_renorm;
   G.initialised = true;
+  return 0;
+}
+
+int artis_gpu_init_gamma(const artis_gamma_spectra *gs) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  if (!gs || gs->nnuclides <= 0 || !gs->nuc_nlines || !gs->nuc_line_offset || !gs->nuc_endecay_gamma) {
+    G.last_error = "init_gamma: bad gamma spectra";
+    return ARTIS_ERR_BAD_ARGUMENT;
+  }
+  const int nn = gs->nnuclides;
+  int64_t nlines = 0;
+  for (int k = 0; k < nn; k++) {
+    if (gs->nuc_nlines[k] < 0 || gs->nuc_line_offset[k] < 0) return ARTIS_ERR_BAD_ARGUMENT;
+    nlines = std::max<int64_t>(nlines, (int64_t)gs->nuc_line_offset[k] + gs->nuc_nlines[k]);
+  }
+  if (nlines > 0 && (!gs->line_energy || !gs->line_probability)) return ARTIS_ERR_BAD_ARGUMENT;
+  DevTab &T = G.K.T;
+  int32_t *nl = nullptr, *off = nullptr;
+  double *en = nullptr, *eg = nullptr, *pr = nullptr;
+  int rc = 0;
+  rc |= dalloc(&nl, (size_t)nn);
+  rc |= dalloc(&off, (size_t)nn);
+  rc |= dalloc(&eg, (size_t)nn);
+  rc |= dalloc(&en, (size_t)std::max<int64_t>(nlines, 1));
+  rc |= dalloc(&pr, (size_t)std::max<int64_t>(nlines, 1));
+  if (rc) return ARTIS_ERR_HIP;
+  HIPCHK(hipMemcpy(nl, gs->nuc_nlines, sizeof(int32_t) * nn, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(off, gs->nuc_line_offset, sizeof(int32_t) * nn, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eg, gs->nuc_endecay_gamma, sizeof(double) * nn, hipMemcpyHostToDevice));
+  if (nlines > 0) {
+    HIPCHK(hipMemcpy(en, gs->line_energy, sizeof(double) * nlines, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(pr, gs->line_probability, sizeof(double) * nlines, hipMemcpyHostToDevice));
+  }
+  T.g_nnuc = nn;
+  T.g_nlines = nl;
+  T.g_off = off;
+  T.g_endecay = eg;
+  T.g_energy = en;
+  T.g_prob = pr;
   return 0;
 }
 
@@ -1183,6 +1230,10 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
   const float *fsrc[8] = {cs->Te, cs->TR, cs->TJ, cs->W, cs->nne, cs->nnetot, cs->rho, cs->kappagrey};
   for (int f = 0; f < 8; f++)
     HIPCHK(hipMemcpyAsync(G.d_cellf + (size_t)f * np, fsrc[f], sizeof(float) * np, hipMemcpyHostToDevice, G.stream));
+  if (cs->ffegrp)
+    HIPCHK(hipMemcpyAsync(G.d_cellf + (size_t)8 * np, cs->ffegrp, sizeof(float) * np, hipMemcpyHostToDevice, G.stream));
+  else
+    HIPCHK(hipMemsetAsync(G.d_cellf + (size_t)8 * np, 0, sizeof(float) * np, G.stream));
   HIPCHK(hipMemcpyAsync(G.d_thick, cs->thick, sizeof(int16_t) * np, hipMemcpyHostToDevice, G.stream));
   HIPCHK(hipMemcpyAsync(G.d_abund, cs->elem_abundance, sizeof(float) * np * ne, hipMemcpyHostToDevice, G.stream));
   HIPCHK(hipMemcpyAsync(G.d_glp, cs->groundlevelpop, sizeof(float) * np * ni, hipMemcpyHostToDevice, G.stream));
@@ -1340,9 +1391,10 @@ int artis_gpu_estimators_download(artis_estimators *est) {
   add(est->nuJ, np, np);
   add(est->ffheatingestimator, 2 * (int64_t)np, np);
   add(est->colheatingestimator, 3 * (int64_t)np, np);
-  add(est->gammaestimator, 4 * (int64_t)np, nion_est);
-  add(est->bfheatingestimator, 4 * (int64_t)np + nion_est, nion_est);
-  const double *sc = blk.data() + 4 * (int64_t)np + 2 * nion_est;
+  add(est->rpkt_emiss, 4 * (int64_t)np, np);
+  add(est->gammaestimator, 5 * (int64_t)np, nion_est);
+  add(est->bfheatingestimator, 5 * (int64_t)np + nion_est, nion_est);
+  const double *sc = blk.data() + 5 * (int64_t)np + 2 * nion_est;
   est->cmf_lum += sc[0];
   est->gamma_dep += sc[1];
   est->positron_dep += sc[2];
@@ -1351,6 +1403,8 @@ int artis_gpu_estimators_download(artis_estimators *est) {
   est->alpha_dep += sc[5];
   est->alpha_emission += sc[6];
   est->gamma_emission += sc[7];
+  est->nt_energy_deposited += sc[8];
+  est->pellet_decays += (int64_t)llrint(sc[9]);
   std::vector<int32_t> lc(G.nlines);
   if (est->ecounter) {
     HIPCHK(hipMemcpy(lc.data(), G.K.E.ecounter, lc.size() * sizeof(int32_t), hipMemcpyDeviceToHost));

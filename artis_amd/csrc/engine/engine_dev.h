@@ -79,6 +79,10 @@ struct DevTab {
   const int32_t *groundcont_element, *groundcont_ion;
   const double *spontrecombcoeff, *corrphotoioncoeff, *bfcooling_coeff;
   const int32_t *cool_type, *cool_element, *cool_ion, *cool_level, *cool_upper;
+  // gamma-ray line spectra per nuclide (gammapkt.cc:27-33), uploaded by artis_gpu_init_gamma
+  int32_t g_nnuc;
+  const int32_t *g_nlines, *g_off;
+  const double *g_endecay, *g_energy, *g_prob;
 };
 
 struct DevGeom {
@@ -96,6 +100,7 @@ struct DevCells {
   const int16_t *thick;
   const float *elem_abundance, *groundlevelpop, *partfunct;
   const double *totalcooling, *cooling_contrib_ion, *corrphotoionrenorm;
+  const float *ffegrp;      // [npts_model] or nullptr (gamma opacities, photo_electric.cc:34)
   const int32_t *ne_index;  // [npts_model] nonempty index, -1 if the model cell is empty
   const int32_t *ne_mgi;    // [n_nonempty]
   int32_t n_nonempty;
@@ -122,9 +127,10 @@ struct DevCells {
 };
 
 struct DevEst {
-  double *J, *nuJ, *ffheat, *colheat, *gamma, *bfheat;  // contiguous block, see engine.hip
+  double *J, *nuJ, *ffheat, *colheat, *rpkt_emiss, *gamma, *bfheat;  // contiguous block, see engine.hip
   int32_t *ecounter, *acounter;
-  double *scalars;                 // [8] cmf_lum, gamma_dep, ... (artis_estimators order)
+  double *scalars;                 // [10] cmf_lum, gamma_dep, ... (artis_estimators order), nt_energy_deposited,
+                                   // pellet_decays
   unsigned long long *counters;    // [34] + nesc at [34]
   unsigned long long *work;        // [16]
   int32_t *err;                    // [4] code, packet number, aux, aux
@@ -137,6 +143,8 @@ struct DevRun {
   float kpktdiffusion_timescale;
   double max_path_step;
   int32_t pol_dipole, relativistic_doppler, record_linestat;
+  double gamma_grey;
+  int32_t instant_particle_deposition, nt_solve_spencerfano;
 };
 
 #endif

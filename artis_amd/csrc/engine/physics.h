@@ -35,6 +35,7 @@ enum : int32_t {
   ERR_LDIST = 11,
   ERR_THICK_MA = 12,
   ERR_NONFINITE = 13,
+  ERR_GAMMA = 14,  // an abort() path of the pellet / gamma code (aux = which)
 };
 
 struct Ctx {

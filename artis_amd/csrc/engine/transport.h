@@ -778,6 +778,17 @@ DEVFN void rpkt_event_boundbound(Tx &x, Pkt &p) {
   if (x.K.R.record_linestat) atomicAdd(&x.K.E.acounter[p.next_trans - 1], 1);
 }
 
+// rpkt.cc:491-509: grey thick cell, coherent electron scattering into a new direction
+DEVNI void rpkt_event_thickcell(Tx &x, Pkt &p) {
+  p.interactions += 1;
+  p.nscatterings += 1;
+  p.last_event = 12;
+  lctr(x.L, CTR_ESCOUNTER);
+  emitt_rpkt(x, p);
+  for (int d = 0; d < 3; d++) p.em_pos[d] = p.pos[d];
+  p.em_time = (int)p.prop_time;
+}
+
 // rpkt.cc:623-813
 template <typename Cold = ColdFull>
 DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
@@ -821,8 +832,11 @@ DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
     edist = DBL_MAX;
     find_nextline = true;
   } else if (K.C.thick[mgi] == 1) {
-    x.err(ERR_UNSUPPORTED_TYPE, p.number, -1);  // grey thick cells: not in this build
-    return false;
+    // grey optically thick cell: electron scattering only (rpkt.cc:697-703); no continuum opacity is evaluated,
+    // so the estimator terms of this step use kappa = 0 (deviation D7)
+    const double kappa = K.C.kappagrey[mgi] * K.C.rho[mgi] * doppler_packet(K, p);
+    edist = (tau_next - 0.0) / kappa;
+    find_nextline = true;
   } else {
     edist = get_event(x, k, mgi, p, kap, &rpkt_eventtype, tau_next, fmin(tdist, sdist));
     if (!x.ok) return false;
@@ -851,7 +865,9 @@ DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
     update_estimators(x, p, kap, edist);
     move_pkt_withtime(K, p, edist / 2.);
     STAMP(x, 3);
-    if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_BB)
+    if (K.C.thick[mgi] == 1)
+      cold(x, p, [&](Tx &tx, Pkt &tp) { rpkt_event_thickcell(tx, tp); });
+    else if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_BB)
       rpkt_event_boundbound(x, p);
     else if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_CONT)
       cold(x, p, [&](Tx &tx, Pkt &tp) {

@@ -21,9 +21,9 @@
 #ifndef ARTIS_WAVEFRONT_H
 #define ARTIS_WAVEFRONT_H
 
-#include "transport.h"
+#include "gamma.h"
 
-enum { QR = 0, QM = 1, QK = 2, NQUEUES = 3 };
+enum { QR = 0, QM = 1, QK = 2, QG = 3, NQUEUES = 4 };
 
 struct WaveState {
   uint32_t *rng_n;     // [N] draws consumed so far this timestep (artis_rng.n)
@@ -103,7 +103,7 @@ __global__ void k_classify(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   block_counters_init(s_ctr, s_work);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool toR = false, toM = false, toK = false;
+  bool toR = false, toM = false, toK = false, toG = false;
   if (i < n) {
     const uint64_t w0 = soa[PW(n, i, 0)];
     const int type = hi32(w0);
@@ -119,12 +119,14 @@ __global__ void k_classify(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *
       toR = type == ARTIS_TYPE_RPKT;
       toM = type == ARTIS_TYPE_MA;
       toK = type == ARTIS_TYPE_KPKT || type == ARTIS_TYPE_PRE_KPKT;
-      if (!toR && !toM && !toK) fail(K, ERR_UNSUPPORTED_TYPE, hi32(soa[PW(n, i, 33)]), type);
+      toG = is_gamma_family(type) && K.T.g_nlines;
+      if (!toR && !toM && !toK && !toG) fail(K, ERR_UNSUPPORTED_TYPE, hi32(soa[PW(n, i, 33)]), type);
     }
   }
   wave_push(W, QR, toR, (int32_t)i);
   wave_push(W, QM, toM, (int32_t)i);
   wave_push(W, QK, toK, (int32_t)i);
+  wave_push(W, QG, toG, (int32_t)i);
   block_counters_flush(K, s_ctr, s_work);
 }
 
@@ -401,6 +403,55 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   wave_stats_flush(W, 1, st_pass, st_busy, st_t0, st_refill, st_trefill, st_tstep);
   if (jumps_sum) atomicAdd(&s_work[WK_MA_JUMPS], jumps_sum);
   if (trans_sum) atomicAdd(&s_work[WK_MA_TRANS], trans_sum);
+  block_counters_flush(K, s_ctr, s_work);
+}
+
+// pellets, gamma rays and non-thermal leptons (gamma.h): one packet per workitem, grid-stride over the G queue,
+// each advanced until it becomes a k-packet (-> K queue), escapes or reaches t2.  Runs once per timestep before
+// the r-packet / macro-atom / k-packet rounds (nothing on those paths turns back into this family).
+__global__ __launch_bounds__(WAVE_BLOCK) void k_gamma(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa,
+                                                      int64_t n, int nts, double t2) {
+  const Ctx &K = *ctxp;
+  __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
+  __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
+  block_counters_init(s_ctr, s_work);
+  LocalCounters L;
+  L.ctr = &s_ctr[0];
+  L.work = &s_work[0];
+  const uint32_t nq = W.ctr[2 * QG];
+  const uint32_t stride = gridDim.x * blockDim.x;
+  // uniform trip count so the wave-aggregated queue appends see every lane of the wave
+  const uint32_t nslots = (nq + stride - 1) / stride * stride;
+  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nslots; slot += stride) {
+    bool toR = false, toM = false, toK = false;
+    int32_t idx = -1;
+    if (slot < nq) {
+      idx = W.q[QG][slot];
+      Pkt p;
+      pkt_load(soa, n, idx, p);
+      PelletInfo pi;
+      pellet_info_load(soa, n, idx, pi);
+      Tx x(K, L);
+      x.nts = nts;
+      x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
+      x.rng.n = W.rng_n[idx];
+      int guard = 0;
+      while (x.ok && is_gamma_family(p.type) && p.prop_time < t2) {
+        do_gamma_family_step(x, p, pi, t2);
+        if (++guard > 1000000) x.err(ERR_STUCK, p.number, 5);
+      }
+      pkt_store(soa, n, idx, p);
+      W.rng_n[idx] = x.rng.n;
+      if (x.ok && p.prop_time < t2) {
+        toR = p.type == ARTIS_TYPE_RPKT;
+        toM = p.type == ARTIS_TYPE_MA;
+        toK = p.type == ARTIS_TYPE_KPKT || p.type == ARTIS_TYPE_PRE_KPKT;
+      }
+    }
+    wave_push(W, QR, toR, idx);
+    wave_push(W, QM, toM, idx);
+    wave_push(W, QK, toK, idx);
+  }
   block_counters_flush(K, s_ctr, s_work);
 }
 

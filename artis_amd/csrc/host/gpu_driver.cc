@@ -3,11 +3,14 @@
 // update_packets -> write the raw packet file.  It exercises the C++ mirror (update_packets_gpu.h) without
 // Python.  Usage:
 //   artis_gpu_driver <outdir> <ngrid> <nlevels_per_ion> <n_ionising> <max_lines> <ntstep> <nts0> <nsteps>
-//                    <npkts> <seed>
+//                    <npkts> <seed> [<gamma_lines_dir>]
+// With <gamma_lines_dir> (holding ni56_lines.txt / co56_lines.txt, the reference's data/ files) the run starts
+// from radioactive pellets at tmin (packet_init, packet.cc:59-149) instead of r-packets.
 // Writes <outdir>/packets_0000_ts<nts>.tmp (raw 304-byte records, sn3d.cc:387-398) after every timestep and
 // prints one summary line per timestep.
 #include <cstdio>
 #include <cstdlib>
+#include <fstream>
 #include <string>
 #include <vector>
 
@@ -16,11 +19,14 @@
 #include "update_packets_gpu.h"
 
 int main(int argc, char **argv) {
-  if (argc != 11) {
-    std::fprintf(stderr, "usage: %s outdir ngrid nlevels_per_ion n_ionising max_lines ntstep nts0 nsteps npkts seed\n",
+  if (argc != 11 && argc != 12) {
+    std::fprintf(stderr,
+                 "usage: %s outdir ngrid nlevels_per_ion n_ionising max_lines ntstep nts0 nsteps npkts seed "
+                 "[gamma_lines_dir]\n",
                  argv[0]);
     return 2;
   }
+  const bool pellets = argc == 12;
   const std::string outdir = argv[1];
   artis_synth_config cfg;
   artis_synth_default_config(&cfg);
@@ -42,13 +48,31 @@ int main(int argc, char **argv) {
   artis_model_run_params(m, &rp);
   const int64_t np = artis_model_npts_model(m);
   const int64_t nion = np * at.nelements * at.maxnions;
-  std::vector<double> J(np), nuJ(np), ff(np), col(np), gam(nion), bfh(nion);
+  std::vector<double> J(np), nuJ(np), ff(np), col(np), gam(nion), bfh(nion), emiss(np);
   std::vector<int32_t> ec(at.nlines), ac(at.nlines);
   std::vector<artis_packet> packets(npkts);
-  if (artis_model_init_rpackets(m, nts0, npkts, seed, 1e45, packets.data()) != 0) return 1;
+  if (pellets) {
+    // read_gamma_spectrum (gammapkt.cc:58-89): line count, then "E[MeV] probability" rows
+    const char *files[2] = {"ni56_lines.txt", "co56_lines.txt"};
+    for (int nuc = 0; nuc < 2; nuc++) {
+      std::ifstream in(std::string(argv[11]) + "/" + files[nuc]);
+      int nl = 0;
+      if (!(in >> nl) || nl <= 0) {
+        std::fprintf(stderr, "cannot read %s\n", files[nuc]);
+        return 1;
+      }
+      std::vector<double> en(nl), pr(nl);
+      for (int j = 0; j < nl; j++) in >> en[j] >> pr[j];
+      if (artis_model_set_gamma_lines(m, nuc, nl, en.data(), pr.data()) != 0) return 1;
+    }
+    if (artis_model_init_pellets(m, npkts, seed, 1e45, 0.5 * cfg.tmin_days, 0.02, packets.data()) != 0) return 1;
+  } else if (artis_model_init_rpackets(m, nts0, npkts, seed, 1e45, packets.data()) != 0) {
+    return 1;
+  }
 
   {
     artis_amd::PacketEngine engine(0, at, *artis_model_geometry(m), rp);
+    if (pellets) engine.init_gamma(*artis_model_gamma_spectra(m));
     for (int nts = nts0; nts < nts0 + nsteps && nts < cfg.ntstep; nts++) {
       artis_amd::check(artis_model_set_timestep(m, nts), "update_grid stand-in");
       engine.upload_cellstate(nts, *artis_model_cellstate(m));
@@ -65,6 +89,8 @@ int main(int argc, char **argv) {
       est.bfheatingestimator = bfh.data();
       est.ecounter = ec.data();
       est.acounter = ac.data();
+      std::fill(emiss.begin(), emiss.end(), 0.);
+      est.rpkt_emiss = emiss.data();
       engine.update_packets(rp.rank, nts, packets.data(), npkts, est);
       double jsum = 0.;
       for (double v : J) jsum += v;
@@ -75,8 +101,9 @@ int main(int argc, char **argv) {
         return 1;
       }
       std::fclose(f);
-      std::printf("nts %d nesc %lld cmf_lum %.17g Jsum %.17g transport_ms %.3f\n", nts, (long long)est.nesc,
-                  est.cmf_lum, jsum, engine.last_transport_ms());
+      std::printf("nts %d nesc %lld cmf_lum %.17g gamma_dep %.17g pellet_decays %lld Jsum %.17g transport_ms %.3f\n",
+                  nts, (long long)est.nesc, est.cmf_lum, est.gamma_dep, (long long)est.pellet_decays, jsum,
+                  engine.last_transport_ms());
     }
   }
   artis_model_free(m);

@@ -80,7 +80,15 @@ struct Model {
   std::vector<int16_t> thick;
   std::vector<float> elem_abundance, groundlevelpop, partfunct;
   std::vector<double> totalcooling, cooling_contrib_ion, corrphotoionrenorm;
+  std::vector<float> ffegrp;
   artis_cell_state cs{};
+
+  // ---- decay stand-in (decay.cc nuclides + gammapkt.cc gamma_spectra)
+  static constexpr int NNUC = 5;
+  std::vector<double> gl_energy[NNUC], gl_prob[NNUC];
+  std::vector<int32_t> gs_nlines, gs_offset;
+  std::vector<double> gs_endecay, gs_energy, gs_prob;
+  artis_gamma_spectra gs{};
   int current_nts = -1;
 };
 
@@ -712,6 +720,7 @@ void compute_cellstate(Model &m, int nts) {
   m.rho.assign(np, 0.f);
   m.kappagrey.assign(np, 0.f);
   m.thick.assign(np, 0);
+  m.ffegrp.assign(np, 0.f);
   m.elem_abundance.assign((size_t)np * ne, 0.f);
   m.groundlevelpop.assign((size_t)np * ni, 0.f);
   m.partfunct.assign((size_t)np * ni, 1.f);
@@ -802,6 +811,18 @@ void compute_cellstate(Model &m, int nts) {
     ionfracs(nne_sol);
     m.nne[mgi] = (float)nne_sol;
     m.nnetot[mgi] = (float)nnetot;
+    // Fe-group fraction stand-in (the 56Ni-rich core of a W7-like model) and the grey opacity of opacity_case 4
+    // style kappagrey = GREY_OP (0.9 ffegrp + 0.1) (grid.cc:629); a cell is thick when its grey optical depth
+    // across one cell width exceeds thick_tau (input.txt cell_is_optically_thick)
+    {
+      const double v = m.mgi_vel[mgi];
+      m.ffegrp[mgi] = (float)(0.2 + 0.6 * exp(-(v / 6e8) * (v / 6e8)));
+      m.kappagrey[mgi] = (float)(0.1 * (0.9 * m.ffegrp[mgi] + 0.1));
+      if (m.cfg.thick_tau > 0) {
+        const double wid_t = 2 * m.geom.coordmax[0] / m.cfg.ngrid_1d * t / m.tmin;
+        if (m.kappagrey[mgi] * rho * wid_t > m.cfg.thick_tau) m.thick[mgi] = 1;
+      }
+    }
     for (int e = 0; e < ne; e++) {
       const int u0 = m.elem_uniqueionoffset[e];
       for (int ion = 0; ion < m.elem_nions[e]; ion++) {
@@ -907,7 +928,64 @@ void compute_cellstate(Model &m, int nts) {
   cs.totalcooling = m.totalcooling.data();
   cs.cooling_contrib_ion = m.cooling_contrib_ion.data();
   cs.corrphotoionrenorm = m.corrphotoionrenorm.data();
+  cs.ffegrp = m.ffegrp.data();
   m.current_nts = nts;
+}
+
+
+// ---------------------------------------------------------------------------------------- decay stand-in
+// Five stand-in nuclides (decay.cc nuclides[]): mean life [d], particle energy per decay [MeV] and its decay
+// type; the gamma energy per decay is the line-list sum (read_gamma_spectrum, gammapkt.cc:74-81) or, for the
+// Fe52-like nuclide, set without a line list (gammapkt.cc:183-185).
+struct NucDef {
+  double meanlife_d, e_particle_mev, e_gamma_nolines_mev;
+};
+const NucDef kNuc[Model::NNUC] = {
+    {6.075 / 0.69314718056, 0., 0.},        // 0 Ni56: EC
+    {77.236 / 0.69314718056, 0.1158, 0.},   // 1 Co56: EC / beta+ (branch-weighted positron KE)
+    {8.275 / 24. / 0.69314718056, 0., 0.86},// 2 Fe52-like: gamma energy, no line list
+    {20., 0.3, 0.},                         // 3 beta- emitter
+    {50., 5.0, 0.},                         // 4 alpha emitter
+};
+// decay paths (decay.cc decaypaths[]): chain of nuclides, final decay type, share of the decay energy
+struct PathDef {
+  int len, nuc[2], decaytype;
+  double share;
+};
+const PathDef kPath[] = {
+    {1, {0, -1}, ARTIS_DECAYTYPE_ELECTRONCAPTURE, 0.30},
+    {2, {0, 1}, ARTIS_DECAYTYPE_ELECTRONCAPTURE, 0.30},
+    {2, {0, 1}, ARTIS_DECAYTYPE_BETAPLUS, 0.10},
+    {1, {2, -1}, ARTIS_DECAYTYPE_ELECTRONCAPTURE, 0.10},
+    {1, {3, -1}, ARTIS_DECAYTYPE_BETAMINUS, 0.10},
+    {1, {4, -1}, ARTIS_DECAYTYPE_ALPHA, 0.10},
+};
+constexpr int kNPath = sizeof(kPath) / sizeof(kPath[0]);
+
+void rebuild_gamma_spectra(Model &m) {
+  m.gs_nlines.assign(Model::NNUC, 0);
+  m.gs_offset.assign(Model::NNUC, 0);
+  m.gs_endecay.assign(Model::NNUC, 0.);
+  m.gs_energy.clear();
+  m.gs_prob.clear();
+  for (int n = 0; n < Model::NNUC; n++) {
+    m.gs_offset[n] = (int32_t)m.gs_energy.size();
+    m.gs_nlines[n] = (int32_t)m.gl_energy[n].size();
+    double eavg = 0.;
+    for (size_t j = 0; j < m.gl_energy[n].size(); j++) {
+      const double en = m.gl_energy[n][j] * ARTIS_MEV;
+      m.gs_energy.push_back(en);
+      m.gs_prob.push_back(m.gl_prob[n][j]);
+      eavg += en * m.gl_prob[n][j];
+    }
+    m.gs_endecay[n] = m.gs_nlines[n] > 0 ? eavg : kNuc[n].e_gamma_nolines_mev * ARTIS_MEV;
+  }
+  m.gs.nnuclides = Model::NNUC;
+  m.gs.nuc_nlines = m.gs_nlines.data();
+  m.gs.nuc_line_offset = m.gs_offset.data();
+  m.gs.nuc_endecay_gamma = m.gs_endecay.data();
+  m.gs.line_energy = m.gs_energy.data();
+  m.gs.line_probability = m.gs_prob.data();
 }
 
 }  // namespace
@@ -935,6 +1013,11 @@ void artis_synth_default_config(artis_synth_config *cfg) {
   cfg->n_tclasses = 32;
   cfg->seed = 1281360349ull;
   cfg->ionpot_scale = 1.;
+  cfg->thick_tau = 0.;
+  cfg->relativistic = 0;
+  cfg->instant_particle_deposition = 1;
+  cfg->n_kpktdiffusion_timesteps = 0;
+  cfg->kpktdiffusion_timescale = 0.;
 }
 
 artis_model *artis_model_synth(const artis_synth_config *cfg) {
@@ -944,6 +1027,7 @@ artis_model *artis_model_synth(const artis_synth_config *cfg) {
   build_atomic(*m, rng);
   build_grid(*m);
   compute_cellstate(*m, 0);
+  rebuild_gamma_spectra(*m);
   return m;
 }
 
@@ -960,12 +1044,113 @@ void artis_model_run_params(const artis_model *m, artis_run_params *p) {
   p->opacity_case = 4;
   p->do_r_lc = 1;
   p->do_rlc_est = 3;   // test configs: line 9 "4" -> do_rlc_est=3 (input.cc:1976-1979): rlc_emiss_rpkt skipped
-  p->n_kpktdiffusion_timesteps = 0;
-  p->kpktdiffusion_timescale = 0.f;
+  p->n_kpktdiffusion_timesteps = m->cfg.n_kpktdiffusion_timesteps;
+  p->kpktdiffusion_timescale = (float)m->cfg.kpktdiffusion_timescale;
   p->max_path_step = 1.e35;  // update_grid.cc:1303 initial value (no cell limits it in this model)
   p->pol_dipole = 1;         // artisoptions_classic.h:64 DIPOLE
-  p->relativistic_doppler = 0;
+  p->relativistic_doppler = m->cfg.relativistic;
   p->record_linestat = 1;
+  p->gamma_grey = -1.;       // test configs: "use grey opacity for gammas? -1"
+  p->instant_particle_deposition = m->cfg.instant_particle_deposition;
+  p->nt_solve_spencerfano = 0;
+}
+
+int artis_model_set_gamma_lines(artis_model *m, int nuc, int nlines, const double *energy_mev, const double *prob) {
+  if (nuc < 0 || nuc >= Model::NNUC || nlines < 0 || (nlines > 0 && (!energy_mev || !prob)))
+    return ARTIS_ERR_BAD_ARGUMENT;
+  m->gl_energy[nuc].assign(energy_mev, energy_mev + nlines);
+  m->gl_prob[nuc].assign(prob, prob + nlines);
+  rebuild_gamma_spectra(*m);
+  return 0;
+}
+
+const artis_gamma_spectra *artis_model_gamma_spectra(const artis_model *m) { return &m->gs; }
+
+int artis_model_init_pellets(const artis_model *m, int npkts, uint64_t seed, double etot, double t_model_days,
+                             double frac_initial, artis_packet *out) {
+  if (npkts <= 0 || !out) return ARTIS_ERR_BAD_ARGUMENT;
+  const double t_model = t_model_days * ARTIS_DAY;
+  const double wid = 2 * m->geom.coordmax[0] / m->cfg.ngrid_1d;
+  // packet_init (packet.cc:77-100): cumulative decay energy per propagation cell, q ~ X(56Ni)(v)
+  std::vector<double> cdf(m->ngrid);
+  double acc = 0.;
+  for (int c = 0; c < m->ngrid; c++) {
+    const int mgi = m->cell_mgi[c];
+    if (mgi < m->npts_model) {
+      const double v = m->mgi_vel[mgi];
+      acc += m->mgi_rho_tmin[mgi] * 0.6 * exp(-(v / 6e8) * (v / 6e8));
+    }
+    cdf[c] = acc;
+  }
+  if (!(acc > 0)) return ARTIS_ERR_BAD_ARGUMENT;
+  double share_tot = 0.;
+  for (int k = 0; k < kNPath; k++) share_tot += kPath[k].share;
+  const double e0 = etot / npkts;
+  std::mt19937_64 rng(seed);
+  std::uniform_real_distribution<double> U(0., 1.);
+  auto upos = [&]() {
+    double z;
+    do z = U(rng);
+    while (z <= 0.);
+    return z;
+  };
+  for (int i = 0; i < npkts; i++) {
+    artis_packet p;
+    std::memset(&p, 0, sizeof(p));  // packets are calloc'ed (sn3d.cc:816)
+    const double r = U(rng) * acc;
+    int c = (int)(std::lower_bound(cdf.begin(), cdf.end(), r) - cdf.begin());
+    if (c >= m->ngrid) c = m->ngrid - 1;
+    while (m->cell_mgi[c] >= m->npts_model) c = (c + 1) % m->ngrid;
+    // place_pellet (packet.cc:18-56)
+    p.where = c;
+    p.number = i;
+    p.prop_time = m->tmin;
+    p.originated_from_particlenotgamma = 0;
+    for (int ax = 0; ax < 3; ax++) p.pos[ax] = m->cell_pos_min[(size_t)c * 3 + ax] + upos() * wid;
+    // setup_radioactive_pellet (decay.cc:1371-1458)
+    if (U(rng) < frac_initial) {
+      p.tdecay = m->tmin;
+      p.type = ARTIS_TYPE_RADIOACTIVE_PELLET;
+      p.e_cmf = e0;
+      p.nu_cmf = e0 / ARTIS_H;
+      p.pellet_nucindex = -1;
+      p.pellet_decaytype = -1;
+    } else {
+      const double zc = U(rng) * share_tot;
+      int path = 0;
+      double cum = 0.;
+      for (; path < kNPath - 1; path++) {
+        cum += kPath[path].share;
+        if (cum > zc) break;
+      }
+      const PathDef &pd = kPath[path];
+      double tdecay = -1;
+      while (tdecay <= t_model || tdecay >= m->tmax) {  // sample_decaytime (decay.cc:716-732)
+        tdecay = t_model;
+        for (int j = 0; j < pd.len; j++) tdecay += -kNuc[pd.nuc[j]].meanlife_d * ARTIS_DAY * log(upos());
+      }
+      p.tdecay = tdecay;
+      p.e_cmf = e0;
+      const int nuc = pd.nuc[pd.len - 1];
+      p.type = ARTIS_TYPE_RADIOACTIVE_PELLET;
+      p.pellet_nucindex = nuc;
+      p.pellet_decaytype = pd.decaytype;
+      const double e_particle = (pd.decaytype == ARTIS_DECAYTYPE_ELECTRONCAPTURE) ? 0. : kNuc[nuc].e_particle_mev * ARTIS_MEV;
+      const double e_gamma = m->gs_endecay[nuc];
+      p.originated_from_particlenotgamma = (U(rng) >= e_gamma / (e_gamma + e_particle)) ? 1 : 0;
+      p.nu_cmf = e_particle / ARTIS_H;
+    }
+    const double len = sqrt(p.pos[0] * p.pos[0] + p.pos[1] * p.pos[1] + p.pos[2] * p.pos[2]);
+    for (int ax = 0; ax < 3; ax++) p.dir[ax] = p.pos[ax] / len;
+    const double t = p.prop_time;
+    const double v[3] = {p.pos[0] / t, p.pos[1] / t, p.pos[2] / t};
+    double dop = 1. - (p.dir[0] * v[0] + p.dir[1] * v[1] + p.dir[2] * v[2]) / ARTIS_CLIGHT;
+    if (m->cfg.relativistic) dop = dop / sqrt(1 - (v[0] * v[0] + v[1] * v[1] + v[2] * v[2]) / ARTIS_CLIGHTSQUARED);
+    p.e_rf = p.e_cmf / dop;
+    p.trueemissiontype = -1;
+    out[i] = p;
+  }
+  return 0;
 }
 
 int artis_model_set_timestep(artis_model *m, int nts) {

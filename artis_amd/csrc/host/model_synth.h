@@ -31,6 +31,12 @@ typedef struct artis_synth_config {
   int32_t n_tclasses;        /* temperature quantisation for the cooling-rate stand-in */
   uint64_t seed;
   double ionpot_scale;       /* scales every ionisation potential (test configs with bf-active continua); 0 = 1 */
+  double thick_tau;          /* >0: cells whose grey optical depth across the cell exceeds this are "thick"
+                                (input.txt cell_is_optically_thick, update_grid.cc); 0: none */
+  int32_t relativistic;      /* USE_RELATIVISTIC_DOPPLER_SHIFT of the run parameters */
+  int32_t instant_particle_deposition; /* INSTANT_PARTICLE_DEPOSITION (default 1, artisoptions_classic.h:222) */
+  int32_t n_kpktdiffusion_timesteps;   /* input.txt "kpktdiffusion_timescale n_kpktdiffusion_timesteps"; the  */
+  double kpktdiffusion_timescale;      /* reference test inputs use 0.001 1000 (default here: 0 0)         */
 } artis_synth_config;
 
 typedef struct artis_model artis_model;
@@ -53,6 +59,20 @@ int artis_model_init_rpackets(const artis_model *m, int nts, int npkts, uint64_t
                               artis_packet *out);
 
 int64_t artis_model_npts_model(const artis_model *m);
+
+/* Gamma-ray line spectrum of stand-in nuclide `nuc` (energies in MeV, photons per decay), as read by
+ * read_gamma_spectrum (gammapkt.cc:58-89); nucdecayenergygamma = sum E p.  Nuclides (decay.cc stand-in):
+ * 0 Ni56 (EC), 1 Co56 (EC / beta+), 2 Fe52-like (gamma energy but no line list -> k-packet,
+ * gammapkt.cc:266-270), 3 a beta- emitter, 4 an alpha emitter (no gammas). */
+int artis_model_set_gamma_lines(artis_model *m, int nuc, int nlines, const double *energy_mev, const double *prob);
+const artis_gamma_spectra *artis_model_gamma_spectra(const artis_model *m);
+
+/* Initial radioactive pellets (packet_init + place_pellet + setup_radioactive_pellet, packet.cc:18-149,
+ * decay.cc:1371-1458): cell ~ rho * q, position uniform in the cell at tmin, decay path by energy share,
+ * tdecay by the chain's summed exponential draws in (t_model, tmax) (decay.cc:716-732), a fraction
+ * frac_initial of USE_MODEL_INITIAL_ENERGY pellets with tdecay = tmin. */
+int artis_model_init_pellets(const artis_model *m, int npkts, uint64_t seed, double etot, double t_model_days,
+                             double frac_initial, artis_packet *out);
 
 #ifdef __cplusplus
 }

@@ -18,11 +18,15 @@ void check(int rc, const char *what) {
 
 PacketEngine::PacketEngine(int device, const artis_atomic_tables &atomic, const artis_geometry &geometry,
                            const artis_run_params &params) {
-  check(artis_gpu_abi_version() == 1 ? 0 : ARTIS_ERR_BAD_ARGUMENT, "artis_gpu_abi_version");
+  check(artis_gpu_abi_version() == ARTIS_GPU_ABI_VERSION ? 0 : ARTIS_ERR_BAD_ARGUMENT, "artis_gpu_abi_version");
   check(artis_gpu_init(device, &atomic, &geometry, &params), "artis_gpu_init");
 }
 
 PacketEngine::~PacketEngine() { artis_gpu_finalize(); }
+
+void PacketEngine::init_gamma(const artis_gamma_spectra &spectra) {
+  check(artis_gpu_init_gamma(&spectra), "artis_gpu_init_gamma");
+}
 
 void PacketEngine::upload_cellstate(int nts, const artis_cell_state &cells) {
   check(artis_gpu_upload_cellstate(nts, &cells), "artis_gpu_upload_cellstate");

@@ -23,6 +23,9 @@ class PacketEngine {
   PacketEngine(const PacketEngine &) = delete;
   PacketEngine &operator=(const PacketEngine &) = delete;
 
+  // gamma-ray line spectra for pellet decays (gammapkt::init_gamma_linelist, gammapkt.cc:194; called from input())
+  void init_gamma(const artis_gamma_spectra &spectra);
+
   // after update_grid (update_grid.cc:1270) for timestep nts
   void upload_cellstate(int nts, const artis_cell_state &cells);
 

@@ -16,6 +16,8 @@ TYPE_GAMMA = 10
 TYPE_RPKT = 11
 TYPE_KPKT = 12
 TYPE_MA = 13
+TYPE_NTLEPTON = 20
+TYPE_NONTHERMAL_PREDEPOSIT = 21
 TYPE_PRE_KPKT = 120
 
 # reference struct packet (packet.h:28-73), 304 bytes; padding named (as in include/artis_gpu.h) so that
@@ -71,6 +73,9 @@ class RunParams(C.Structure):
         ("pol_dipole", C.c_int32),
         ("relativistic_doppler", C.c_int32),
         ("record_linestat", C.c_int32),
+        ("gamma_grey", C.c_double),
+        ("instant_particle_deposition", C.c_int32),
+        ("nt_solve_spencerfano", C.c_int32),
     ]
 
 
@@ -95,6 +100,8 @@ class Estimators(C.Structure):
         ("pellet_decays", C.c_int64),
         ("nesc", C.c_int64),
         ("counters", C.c_int64 * ARTIS_COUNTER_COUNT),
+        ("rpkt_emiss", C.POINTER(C.c_double)),
+        ("nt_energy_deposited", C.c_double),
     ]
 
 
@@ -117,6 +124,22 @@ class SynthConfig(C.Structure):
         ("n_tclasses", C.c_int32),
         ("seed", C.c_uint64),
         ("ionpot_scale", C.c_double),
+        ("thick_tau", C.c_double),
+        ("relativistic", C.c_int32),
+        ("instant_particle_deposition", C.c_int32),
+        ("n_kpktdiffusion_timesteps", C.c_int32),
+        ("kpktdiffusion_timescale", C.c_double),
+    ]
+
+
+class GammaSpectra(C.Structure):
+    _fields_ = [
+        ("nnuclides", C.c_int32),
+        ("nuc_nlines", C.POINTER(C.c_int32)),
+        ("nuc_line_offset", C.POINTER(C.c_int32)),
+        ("nuc_endecay_gamma", C.POINTER(C.c_double)),
+        ("line_energy", C.POINTER(C.c_double)),
+        ("line_probability", C.POINTER(C.c_double)),
     ]
 
 
@@ -132,6 +155,7 @@ class EstimatorArrays:
         self.bfheating = np.zeros(npts_model * nelements * maxnions)
         self.ecounter = np.zeros(nlines, dtype=np.int32)
         self.acounter = np.zeros(nlines, dtype=np.int32)
+        self.rpkt_emiss = np.zeros(npts_model)
         self.struct = Estimators()
         dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
         ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))  # noqa: E731
@@ -140,6 +164,7 @@ class EstimatorArrays:
         s.ffheatingestimator, s.colheatingestimator = dp(self.ffheating), dp(self.colheating)
         s.gammaestimator, s.bfheatingestimator = dp(self.gamma), dp(self.bfheating)
         s.ecounter, s.acounter = ip(self.ecounter), ip(self.acounter)
+        s.rpkt_emiss = dp(self.rpkt_emiss)
 
     @property
     def counters(self):
@@ -149,5 +174,14 @@ class EstimatorArrays:
         s = self.struct
         return {
             "cmf_lum": s.cmf_lum,
+            "gamma_dep": s.gamma_dep,
+            "positron_dep": s.positron_dep,
+            "electron_dep": s.electron_dep,
+            "electron_emission": s.electron_emission,
+            "alpha_dep": s.alpha_dep,
+            "alpha_emission": s.alpha_emission,
+            "gamma_emission": s.gamma_emission,
+            "pellet_decays": s.pellet_decays,
+            "nt_energy_deposited": s.nt_energy_deposited,
             "nesc": s.nesc,
         }

@@ -31,6 +31,11 @@ def model_lib():
         lib.artis_model_run_params.argtypes = [C.c_void_p, C.POINTER(ffi.RunParams)]
         lib.artis_model_set_timestep.argtypes = [C.c_void_p, C.c_int]
         lib.artis_model_init_rpackets.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_uint64, C.c_double, C.c_void_p]
+        lib.artis_model_set_gamma_lines.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        lib.artis_model_gamma_spectra.argtypes = [C.c_void_p]
+        lib.artis_model_gamma_spectra.restype = C.c_void_p
+        lib.artis_model_init_pellets.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.c_double, C.c_double, C.c_double,
+                                                 C.c_void_p]
         lib.artis_model_npts_model.argtypes = [C.c_void_p]
         lib.artis_model_npts_model.restype = C.c_int64
         _model_lib = lib
@@ -65,6 +70,27 @@ class Model:
         (self.nelements, self.maxnions, self.nions_total, self.nlevels_total, self.nlines,
          self.nbfcontinua, self.nbfcontinua_ground, self.ncoolingterms) = list(hdr)
         self.nts = 0
+        self._load_gamma_lines()
+        self.gamma_spectra = self._lib.artis_model_gamma_spectra(self._h)
+
+    # the reference's own gamma-line data files (data/ni56_lines.txt, data/co56_lines.txt), kept as fixtures
+    GAMMA_LINE_FILES = {0: "ni56_lines.txt", 1: "co56_lines.txt"}
+
+    def _load_gamma_lines(self):
+        d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "gamma_lines")
+        for nuc, fn in self.GAMMA_LINE_FILES.items():
+            path = os.path.join(d, fn)
+            if not os.path.exists(path):
+                continue
+            with open(path) as f:  # read_gamma_spectrum (gammapkt.cc:58-89): count, then "E[MeV] prob" rows
+                tok = f.read().split()
+            n = int(tok[0])
+            vals = np.array([float(x) for x in tok[1:1 + 2 * n]]).reshape(n, 2)
+            en = np.ascontiguousarray(vals[:, 0])
+            pr = np.ascontiguousarray(vals[:, 1])
+            rc = self._lib.artis_model_set_gamma_lines(self._h, nuc, n, en.ctypes.data, pr.ctypes.data)
+            if rc != 0:
+                raise RuntimeError(f"artis_model_set_gamma_lines({nuc}) -> {rc}")
 
     def set_timestep(self, nts):
         rc = self._lib.artis_model_set_timestep(self._h, int(nts))
@@ -78,6 +104,17 @@ class Model:
                                                  pk.ctypes.data)
         if rc != 0:
             raise RuntimeError(f"artis_model_init_rpackets -> {rc}")
+        return pk
+
+    def init_pellets(self, npkts, seed=1, etot=1e45, t_model_days=None, frac_initial=0.02):
+        """Radioactive pellets at tmin (packet_init stand-in, see model_synth.h)."""
+        if t_model_days is None:
+            t_model_days = 0.5 * self.cfg.tmin_days
+        pk = np.zeros(npkts, dtype=ffi.PACKET_DTYPE)
+        rc = self._lib.artis_model_init_pellets(self._h, int(npkts), C.c_uint64(seed), float(etot),
+                                                float(t_model_days), float(frac_initial), pk.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"artis_model_init_pellets -> {rc}")
         return pk
 
     def new_estimators(self):

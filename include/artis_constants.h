@@ -20,6 +20,7 @@
 #define ARTIS_MEV 1.6021772e-6
 #define ARTIS_DAY 86400.0
 #define ARTIS_SIGMA_T 6.6524e-25
+#define ARTIS_THOMSON_LIMIT 1e-2 /* constants.h:19 */
 #define ARTIS_PARSEC 3.0857e+18
 #define ARTIS_KB 1.38064852e-16
 #define ARTIS_SAHACONST 2.0706659e-16
@@ -63,6 +64,13 @@
 #define ARTIS_MA_ACTION_INTERNALUPHIGHER 7
 #define ARTIS_MA_ACTION_INTERNALUPHIGHERNT 8
 #define ARTIS_MA_ACTION_COUNT 9
+
+/* decay.h:15-22 */
+#define ARTIS_DECAYTYPE_ALPHA 0
+#define ARTIS_DECAYTYPE_ELECTRONCAPTURE 1
+#define ARTIS_DECAYTYPE_BETAPLUS 2
+#define ARTIS_DECAYTYPE_BETAMINUS 3
+#define ARTIS_DECAYTYPE_NONE 4
 
 /* stats.h:49-83 event counters */
 enum artis_counter {

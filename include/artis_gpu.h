@@ -234,6 +234,8 @@ typedef struct artis_cell_state {
   const double *totalcooling;         /* [npts_model] */
   const double *cooling_contrib_ion;  /* [npts_model * nions_total] */
   const double *corrphotoionrenorm;   /* [npts_model * nelements * maxnions] */
+  const float *ffegrp;                /* [npts_model] Fe-group mass fraction (grid.cc:223), gamma opacities;
+                                         may be NULL when no gamma packets are propagated */
 } artis_cell_state;
 
 /* Run-time switches of input.txt / artisoptions.h that change hot-path behaviour. */
@@ -249,6 +251,9 @@ typedef struct artis_run_params {
   int32_t pol_dipole;          /* DIPOLE: 1 = dipole rejection scattering (polarization.cc:26-53) */
   int32_t relativistic_doppler;/* USE_RELATIVISTIC_DOPPLER_SHIFT */
   int32_t record_linestat;     /* RECORD_LINESTAT */
+  double gamma_grey;           /* input.txt "use grey opacity for gammas?" (input.cc:1992); < 0: full treatment */
+  int32_t instant_particle_deposition; /* INSTANT_PARTICLE_DEPOSITION (update_packets.cc:23) */
+  int32_t nt_solve_spencerfano;/* NT_ON && NT_SOLVE_SPENCERFANO (nonthermal.cc:1883): not propagated here */
 } artis_run_params;
 
 /* ------------------------------------------------------------------------------------------------------------ */
@@ -272,7 +277,24 @@ typedef struct artis_estimators {
   int64_t pellet_decays;
   int64_t nesc;                /* globals::nesc */
   int64_t counters[ARTIS_COUNTER_COUNT];
+  double *rpkt_emiss;          /* [npts_model] grey gamma heating estimator rlc_emiss_gamma (grey_emissivities.cc:28-77,
+                                  globals.cc:30); may be NULL */
+  double nt_energy_deposited;  /* nonthermal.cc:115, added by do_ntlepton (nonthermal.cc:1878) */
 } artis_estimators;
+
+/* ------------------------------------------------------------------------------------------------------------ */
+/* Gamma-ray line spectra per nuclide, as read by read_gamma_spectrum (gammapkt.cc:58-89) into gamma_spectra    */
+/* (gammapkt.cc:27-33), plus nucdecayenergygamma(z, a) (decay.cc) that choose_gamma_ray divides by             */
+/* (gammapkt.cc:234).  Indexed by the reference nuclide index = packet.pellet_nucindex.                        */
+/* ------------------------------------------------------------------------------------------------------------ */
+typedef struct artis_gamma_spectra {
+  int32_t nnuclides;
+  const int32_t *nuc_nlines;        /* [nnuclides]; 0: no gamma spectrum, the pellet becomes a k-packet */
+  const int32_t *nuc_line_offset;   /* [nnuclides] into line_energy / line_probability */
+  const double *nuc_endecay_gamma;  /* [nnuclides] average gamma energy per decay [erg] */
+  const double *line_energy;        /* [sum nlines] erg */
+  const double *line_probability;   /* [sum nlines] photons per decay */
+} artis_gamma_spectra;
 
 enum artis_status {
   ARTIS_OK = 0,
@@ -290,6 +312,10 @@ enum artis_status {
 int artis_gpu_init(int device, const artis_atomic_tables *atomic, const artis_geometry *geom,
                    const artis_run_params *params);
 void artis_gpu_finalize(void);
+/* Upload the gamma-ray line spectra used by pellet decays (replaces gammapkt::init_gamma_linelist,
+ * gammapkt.cc:194, as seen by pellet_gamma_decay / do_gamma).  Needed before pellets or gamma packets are
+ * propagated; without it such packets fail with ARTIS_ERR_UNSUPPORTED. */
+int artis_gpu_init_gamma(const artis_gamma_spectra *spectra);
 
 /* Upload the per-cell state produced by update_grid for timestep nts and build the engine's per-cell tables
  * (level populations, cumulative k-packet cooling lists) that replace the per-thread cellhistory
@@ -335,6 +361,7 @@ int64_t artis_gpu_last_rounds(void);  /* event-queue rounds of the last update (
  * [0] r-packet, [1] macro-atom (incl. cell binning), [2] k-packet, [3] classify */
 int artis_gpu_last_kernel_times(double ms[4], int64_t launches[4]);
 const char *artis_gpu_last_error(void);
+#define ARTIS_GPU_ABI_VERSION 2  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields) */
 int artis_gpu_abi_version(void);
 
 #ifdef __cplusplus

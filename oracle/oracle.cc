@@ -27,6 +27,11 @@
 //   D6 do_kpkt: if the cumulative cooling search lands one past the ion's last term because the update_grid
 //       total and the summed terms differ in the last bits, the last term is taken (the reference aborts,
 //       kpkt.cc:573).
+//   D7 In a grey optically thick cell no continuum opacity is evaluated; the reference's update_estimators then
+//       adds ffheating / gamma / bfheating terms with the kappa its OpenMP thread computed last for some other
+//       packet (rpkt.cc:583, 1166), a per-thread artefact.  Here those terms are zero.
+//   D8 Gamma packets need do_r_lc (do_comp_est = false, sn3d.cc:539): the Compton emissivity estimators
+//       (emissivities.cc:14-137) are not restated; every reference test configuration sets do_r_lc.
 #include <omp.h>
 
 #include <algorithm>
@@ -51,6 +56,7 @@ struct Ctx {
   const artis_cell_state *cs;
   artis_run_params rp;
   double T_step_log;
+  const artis_gamma_spectra *gs;  // may be NULL: no pellets / gamma packets in the ensemble
 };
 
 struct Est {
@@ -1301,6 +1307,10 @@ bool do_rpkt_step(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
     edist = std::numeric_limits<double>::max();
     find_nextline = true;
   } else if (c.cs->thick[mgi] == 1) {
+    // D7: no continuum opacity is evaluated in a grey thick cell, so the estimator terms of this step use zero
+    // (the reference uses whatever its thread computed last, rpkt.cc:583, 1166)
+    tc.kap_total = tc.kap_es = tc.kap_ff = tc.kap_bf = tc.kap_ffheating = 0.;
+    std::fill(tc.groundcont_gamma_contr.begin(), tc.groundcont_gamma_contr.end(), 0.);
     const double kappa = c.cs->kappagrey[mgi] * c.cs->rho[mgi] * doppler_packet_nucmf_on_nurf(c, p);
     edist = (tau_next - 0.0) / kappa;
     find_nextline = true;
@@ -1901,6 +1911,444 @@ void do_kpkt(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_packet
   }
 }
 
+// ------------------------------------------------------------------------------------ pellets and gammas
+// Cell properties of the model cell mgi; the empty-cell sentinel mgi == npts_model reads as zero, as the
+// reference's zero-initialised modelgrid[npts_model] entry does (grid.cc:840).
+inline double cell_rho(const Ctx &c, int mgi) { return mgi == npts_model(c) ? 0. : (double)c.cs->rho[mgi]; }
+inline double cell_nnetot(const Ctx &c, int mgi) { return mgi == npts_model(c) ? 0. : (double)c.cs->nnetot[mgi]; }
+inline double cell_ffegrp(const Ctx &c, int mgi) {
+  return (mgi == npts_model(c) || !c.cs->ffegrp) ? 0. : (double)c.cs->ffegrp[mgi];
+}
+
+// vectors.cc:10-44
+void scatter_dir(artis_rng *rng, const double dir_in[3], double cos_theta, double dir_out[3]) {
+  const double zrand = artis_rng_uniform(rng);
+  const double phi = zrand * 2 * ARTIS_PI;
+  const double sin_theta_sq = 1. - (cos_theta * cos_theta);
+  const double sin_theta = std::sqrt(sin_theta_sq);
+  const double zprime = cos_theta;
+  const double xprime = sin_theta * std::cos(phi);
+  const double yprime = sin_theta * std::sin(phi);
+  const double norm1 = 1. / std::sqrt((dir_in[0] * dir_in[0]) + (dir_in[1] * dir_in[1]));
+  const double norm2 = 1. / std::sqrt((dir_in[0] * dir_in[0]) + (dir_in[1] * dir_in[1]) + (dir_in[2] * dir_in[2]));
+  const double r11 = dir_in[1] * norm1;
+  const double r12 = -1 * dir_in[0] * norm1;
+  const double r13 = 0.0;
+  const double r21 = dir_in[0] * dir_in[2] * norm1 * norm2;
+  const double r22 = dir_in[1] * dir_in[2] * norm1 * norm2;
+  const double r23 = -1 * norm2 / norm1;
+  const double r31 = dir_in[0] * norm2;
+  const double r32 = dir_in[1] * norm2;
+  const double r33 = dir_in[2] * norm2;
+  dir_out[0] = (r11 * xprime) + (r21 * yprime) + (r31 * zprime);
+  dir_out[1] = (r12 * xprime) + (r22 * yprime) + (r32 * zprime);
+  dir_out[2] = (r13 * xprime) + (r23 * yprime) + (r33 * zprime);
+}
+
+[[noreturn]] void gamma_fatal(const char *what, const artis_packet *p) {
+  fprintf(stderr, "oracle: [fatal] %s (packet %d type %d where %d nu_cmf %g)\n", what, p->number, p->type, p->where,
+          p->nu_cmf);
+  abort();
+}
+
+// gammapkt.cc:227-253
+void choose_gamma_ray(const Ctx &c, artis_rng *rng, artis_packet *p) {
+  const int nucindex = p->pellet_nucindex;
+  const double E_gamma = c.gs->nuc_endecay_gamma[nucindex];
+  const double zrand = artis_rng_uniform(rng);
+  const int off = c.gs->nuc_line_offset[nucindex];
+  int nselected = -1;
+  double runtot = 0.;
+  for (int n = 0; n < c.gs->nuc_nlines[nucindex]; n++) {
+    runtot += c.gs->line_probability[off + n] * c.gs->line_energy[off + n] / E_gamma;
+    if (zrand <= runtot) {
+      nselected = n;
+      break;
+    }
+  }
+  if (nselected < 0) gamma_fatal("Failure to choose line", p);
+  p->nu_cmf = c.gs->line_energy[off + nselected] / ARTIS_H;
+}
+
+// gammapkt.cc:255-313
+void pellet_gamma_decay(const Ctx &c, artis_rng *rng, artis_packet *p) {
+  if (c.gs->nuc_nlines[p->pellet_nucindex] == 0) {
+    p->type = ARTIS_TYPE_KPKT;
+    p->absorptiontype = -6;
+    return;
+  }
+  double dir_cmf[3];
+  get_rand_isotropic_unitvec(rng, dir_cmf);
+  double vel_vec[3];
+  get_velocity(p->pos, vel_vec, -1. * p->tdecay);
+  angle_ab(dir_cmf, vel_vec, p->dir);
+  choose_gamma_ray(c, rng, p);
+  p->prop_time = p->tdecay;
+  const double dopplerfactor = doppler_packet_nucmf_on_nurf(c, p);
+  p->nu_rf = p->nu_cmf / dopplerfactor;
+  p->e_rf = p->e_cmf / dopplerfactor;
+  p->type = ARTIS_TYPE_GAMMA;
+  p->last_cross = ARTIS_NONE;
+  p->stokes[0] = 1.0;
+  p->stokes[1] = p->stokes[2] = 0.0;
+  double dummy_dir[3] = {0., 0., 1.};
+  cross_prod(p->dir, dummy_dir, p->pol_dir);
+  if ((dot(p->pol_dir, p->pol_dir)) < 1.e-8) {
+    dummy_dir[0] = dummy_dir[2] = 0.0;
+    dummy_dir[1] = 1.0;
+    cross_prod(p->dir, dummy_dir, p->pol_dir);
+  }
+  vec_norm(p->pol_dir, p->pol_dir);
+}
+
+// gammapkt.cc:315-326
+inline double sigma_compton_partial(double x, double f) {
+  const double term1 = ((x * x) - (2 * x) - 2) * std::log(f) / x / x;
+  const double term2 = (((f * f) - 1) / (f * f)) / 2;
+  const double term3 = ((f - 1) / x) * ((1 / x) + (2 / f) + (1 / (x * f)));
+  return (3 * ARTIS_SIGMA_T * (term1 + term2 + term3) / (8 * x));
+}
+
+// gammapkt.cc:328-354
+double sig_comp(const Ctx &c, const artis_packet *p) {
+  const double xx = ARTIS_H * p->nu_cmf / ARTIS_ME / ARTIS_CLIGHT / ARTIS_CLIGHT;
+  double sigma_cmf;
+  if (xx < ARTIS_THOMSON_LIMIT) {
+    sigma_cmf = ARTIS_SIGMA_T;
+  } else {
+    const double fmax = (1 + (2 * xx));
+    sigma_cmf = sigma_compton_partial(xx, fmax);
+  }
+  sigma_cmf *= cell_nnetot(c, cell_mgi(c, p->where));
+  return sigma_cmf * doppler_packet_nucmf_on_nurf(c, p);
+}
+
+// gammapkt.cc:356-397
+double choose_f(double xx, double zrand) {
+  double f_max = 1 + (2 * xx);
+  double f_min = 1;
+  const double norm = zrand * sigma_compton_partial(xx, f_max);
+  int count = 0;
+  double err = 1e20;
+  double ftry = (f_max + f_min) / 2;
+  while ((err > 1.e-4) && (count < 1000)) {
+    ftry = (f_max + f_min) / 2;
+    const double sigma_try = sigma_compton_partial(xx, ftry);
+    if (sigma_try > norm) {
+      f_max = ftry;
+      err = (sigma_try - norm) / norm;
+    } else {
+      f_min = ftry;
+      err = (norm - sigma_try) / norm;
+    }
+    count++;
+  }
+  return ftry;
+}
+
+// gammapkt.cc:399-420
+double thomson_angle(artis_rng *rng, const artis_packet *p) {
+  const double zrand = artis_rng_uniform(rng);
+  const double B_coeff = (8. * zrand) - 4.;
+  double t_coeff = std::sqrt((B_coeff * B_coeff) + 4);
+  t_coeff = t_coeff - B_coeff;
+  t_coeff = t_coeff / 2;
+  t_coeff = std::cbrt(t_coeff);
+  const double mu = (1 / t_coeff) - t_coeff;
+  if (std::fabs(mu) > 1) gamma_fatal("Error in Thomson", p);
+  return mu;
+}
+
+// gammapkt.cc:422-531
+void compton_scatter(const Ctx &c, Est &E, artis_rng *rng, artis_packet *p) {
+  double f;
+  const double xx = ARTIS_H * p->nu_cmf / ARTIS_ME / ARTIS_CLIGHT / ARTIS_CLIGHT;
+  bool stay_gamma;
+  if (xx < ARTIS_THOMSON_LIMIT) {
+    f = 1.0;
+    stay_gamma = true;
+  } else {
+    const double zrand = artis_rng_uniform(rng);
+    f = choose_f(xx, zrand);
+    if ((f < 1) || (f > (2 * xx + 1))) gamma_fatal("Compton f out of bounds", p);
+    const double prob_gamma = 1. / f;
+    const double zrand2 = artis_rng_uniform(rng);
+    stay_gamma = (zrand2 < prob_gamma);
+  }
+  if (stay_gamma) {
+    p->nu_cmf = p->nu_cmf / f;
+    double vel_vec[3];
+    get_velocity(p->pos, vel_vec, p->prop_time);
+    double cmf_dir[3];
+    angle_ab(p->dir, vel_vec, cmf_dir);
+    double cos_theta;
+    if (xx < ARTIS_THOMSON_LIMIT)
+      cos_theta = thomson_angle(rng, p);
+    else
+      cos_theta = 1. - ((f - 1) / xx);
+    double new_dir[3];
+    scatter_dir(rng, cmf_dir, cos_theta, new_dir);
+    const double test = dot(new_dir, new_dir);
+    if (std::fabs(1. - test) > 1.e-8) gamma_fatal("Not a unit vector - Compton", p);
+    const double test2 = dot(new_dir, cmf_dir);
+    if (std::fabs(test2 - cos_theta) > 1.e-8) gamma_fatal("Problem with angle - Compton", p);
+    vec_scale(vel_vec, -1.);
+    double final_dir[3];
+    angle_ab(new_dir, vel_vec, final_dir);
+    vec_copy(p->dir, final_dir);
+    const double dopplerfactor = doppler_packet_nucmf_on_nurf(c, p);
+    p->nu_rf = p->nu_cmf / dopplerfactor;
+    p->e_rf = p->e_cmf / dopplerfactor;
+    p->last_cross = ARTIS_NONE;
+  } else {
+    p->type = ARTIS_TYPE_NTLEPTON;
+    p->absorptiontype = -3;
+    counter_inc(E, CTR_NT_STAT_FROM_GAMMA);
+  }
+}
+
+// photo_electric.cc:10-48
+double sig_photo_electric(const Ctx &c, const artis_packet *p) {
+  double sigma_cmf;
+  const int mgi = cell_mgi(c, p->where);
+  const double rho = cell_rho(c, mgi);
+  if (c.rp.gamma_grey < 0) {
+    double sigma_cmf_si = 1.16e-24 * std::pow(p->nu_cmf / 2.41326e19, -3.13);
+    double sigma_cmf_fe = 25.7e-24 * std::pow(p->nu_cmf / 2.41326e19, -3.0);
+    sigma_cmf_si *= rho / ARTIS_MH / 28;
+    sigma_cmf_fe *= rho / ARTIS_MH / 56;
+    const double f_fe = cell_ffegrp(c, mgi);
+    sigma_cmf = (sigma_cmf_fe * f_fe) + (sigma_cmf_si * (1. - f_fe));
+  } else {
+    sigma_cmf = c.rp.gamma_grey * rho;
+  }
+  return sigma_cmf * doppler_packet_nucmf_on_nurf(c, p);
+}
+
+// photo_electric.cc:50-111
+double sig_pair_prod(const Ctx &c, const artis_packet *p) {
+  double sigma_cmf;
+  const int mgi = cell_mgi(c, p->where);
+  const double rho = cell_rho(c, mgi);
+  if (c.rp.gamma_grey < 0) {
+    if (p->nu_cmf > 2.46636e+20) {
+      double sigma_cmf_si;
+      double sigma_cmf_fe;
+      const double f_fe = cell_ffegrp(c, mgi);
+      if (p->nu_cmf > 3.61990e+20) {
+        sigma_cmf_si = (0.0481 + (0.301 * ((p->nu_cmf / 2.41326e+20) - 1.5))) * 196.e-27;
+        sigma_cmf_fe = (0.0481 + (0.301 * ((p->nu_cmf / 2.41326e+20) - 1.5))) * 784.e-27;
+      } else {
+        sigma_cmf_si = 1.0063 * ((p->nu_cmf / 2.41326e+20) - 1.022) * 196.e-27;
+        sigma_cmf_fe = 1.0063 * ((p->nu_cmf / 2.41326e+20) - 1.022) * 784.e-27;
+      }
+      sigma_cmf_si *= rho / ARTIS_MH / 28;
+      sigma_cmf_fe *= rho / ARTIS_MH / 56;
+      sigma_cmf = (sigma_cmf_fe * f_fe) + (sigma_cmf_si * (1. - f_fe));
+    } else {
+      sigma_cmf = 0.0;
+    }
+  } else {
+    sigma_cmf = 0.0;
+  }
+  double sigma_rf = sigma_cmf * doppler_packet_nucmf_on_nurf(c, p);
+  if (sigma_rf < 0) sigma_rf = 0.0;
+  return sigma_rf;
+}
+
+// photo_electric.cc:113-166
+void pair_prod(const Ctx &c, Est &E, artis_rng *rng, artis_packet *p) {
+  const double prob_gamma = 1.022 * ARTIS_MEV / (ARTIS_H * p->nu_cmf);
+  if (prob_gamma < 0) gamma_fatal("prob_gamma < 0. pair_prod", p);
+  const double zrand = artis_rng_uniform(rng);
+  if (zrand > prob_gamma) {
+    p->type = ARTIS_TYPE_NTLEPTON;
+    p->absorptiontype = -5;
+    counter_inc(E, CTR_NT_STAT_FROM_GAMMA);
+  } else {
+    p->nu_cmf = 0.511 * ARTIS_MEV / ARTIS_H;
+    double dir_cmf[3];
+    get_rand_isotropic_unitvec(rng, dir_cmf);
+    double vel_vec[3];
+    get_velocity(p->pos, vel_vec, -1. * p->prop_time);
+    angle_ab(dir_cmf, vel_vec, p->dir);
+    const double dopplerfactor = doppler_packet_nucmf_on_nurf(c, p);
+    p->nu_rf = p->nu_cmf / dopplerfactor;
+    p->e_rf = p->e_cmf / dopplerfactor;
+    p->type = ARTIS_TYPE_GAMMA;
+    p->last_cross = ARTIS_NONE;
+  }
+}
+
+// grey_emissivities.cc:12-26
+inline double meanf_sigma(double x) {
+  double f = 1 + (2 * x);
+  double term0 = 2 / x;
+  double term1 = (1 - (2 / x) - (3 / (x * x))) * std::log(f);
+  double term2 = ((4 / x) + (3 / (x * x)) - 1) * 2 * x / f;
+  double term3 = (1 - (2 / x) - (1 / (x * x))) * 2 * x * (1 + x) / f / f;
+  double term4 = -2. * x * ((4 * x * x) + (6 * x) + 3) / 3 / f / f / f;
+  double tot = 3 * ARTIS_SIGMA_T * (term0 + term1 + term2 + term3 + term4) / (8 * x);
+  return tot;
+}
+
+// grey_emissivities.cc:28-77
+void rlc_emiss_gamma(const Ctx &c, Est &E, const artis_packet *p, double dist) {
+  const int mgi = cell_mgi(c, p->where);
+  if (dist > 0) {
+    double vel_vec[3];
+    get_velocity(p->pos, vel_vec, p->prop_time);
+    const double xx = ARTIS_H * p->nu_cmf / ARTIS_ME / ARTIS_CLIGHT / ARTIS_CLIGHT;
+    double heating_cont = ((meanf_sigma(xx) * cell_nnetot(c, mgi)) + sig_photo_electric(c, p) +
+                           (sig_pair_prod(c, p) * (1. - (2.46636e+20 / p->nu_cmf))));
+    heating_cont = heating_cont * p->e_rf * dist * (1. - (2. * dot(vel_vec, p->dir) / ARTIS_CLIGHT));
+    if (E.e->rpkt_emiss) safeadd(&E.e->rpkt_emiss[mgi], 1.e-20 * heating_cont);
+  }
+}
+
+// gammapkt.cc:533-700: one step of a gamma packet (cell boundary, end of timestep or interaction)
+void do_gamma(const Ctx &c, Est &E, artis_rng *rng, artis_packet *p, double t2) {
+  double zrand = artis_rng_uniform_pos(rng);
+  const double tau_next = -1. * std::log(zrand);
+  const double tau_current = 0.0;
+  int snext;
+  double sdist = boundary_cross(c, E, p, &snext);
+  const double maxsdist = c.g->rmax * p->prop_time / c.g->tmin;
+  if (sdist > maxsdist) gamma_fatal("Unreasonably large sdist (gamma)", p);
+  if (sdist < 0) sdist = 0;
+  if (((snext < 0) && (snext != -99)) || (snext >= c.g->ngrid)) gamma_fatal("Heading for inappropriate grid cell", p);
+  if (sdist > c.rp.max_path_step) {
+    sdist = c.rp.max_path_step;
+    snext = p->where;
+  }
+  double kap_compton = 0.0;
+  if (c.rp.gamma_grey < 0) kap_compton = sig_comp(c, p);
+  const double kap_photo_electric = sig_photo_electric(c, p);
+  const double kap_pair_prod = sig_pair_prod(c, p);
+  const double kap_tot = kap_compton + kap_photo_electric + kap_pair_prod;
+  const double edist = (tau_next - tau_current) / kap_tot;
+  if (edist < 0) gamma_fatal("Negative distance (edist)", p);
+  const double tdist = (t2 - p->prop_time) * ARTIS_CLIGHT_PROP;
+  if (tdist < 0) gamma_fatal("Negative distance (tdist)", p);
+  const bool rlc = c.rp.do_rlc_est != 0;
+  if ((sdist < tdist) && (sdist < edist)) {
+    p->prop_time += sdist / 2. / ARTIS_CLIGHT_PROP;
+    move_pkt(c, p, sdist / 2.);
+    if (kap_tot > 0 && rlc) rlc_emiss_gamma(c, E, p, sdist);
+    p->prop_time += sdist / 2. / ARTIS_CLIGHT_PROP;
+    move_pkt(c, p, sdist / 2.);
+    if (snext != p->where) change_cell(E, p, snext);
+  } else if ((tdist < sdist) && (tdist < edist)) {
+    p->prop_time += tdist / 2. / ARTIS_CLIGHT_PROP;
+    move_pkt(c, p, tdist / 2.);
+    if (kap_tot > 0 && rlc) rlc_emiss_gamma(c, E, p, tdist);
+    p->prop_time = t2;
+    move_pkt(c, p, tdist / 2.);
+  } else if ((edist < sdist) && (edist < tdist)) {
+    p->prop_time += edist / 2. / ARTIS_CLIGHT_PROP;
+    move_pkt(c, p, edist / 2.);
+    if (kap_tot > 0 && rlc) rlc_emiss_gamma(c, E, p, edist);
+    p->prop_time += edist / 2. / ARTIS_CLIGHT_PROP;
+    move_pkt(c, p, edist / 2.);
+    zrand = artis_rng_uniform(rng);
+    if (kap_compton > (zrand * kap_tot)) {
+      compton_scatter(c, E, rng, p);
+    } else if ((kap_compton + kap_photo_electric) > (zrand * kap_tot)) {
+      p->type = ARTIS_TYPE_NTLEPTON;
+      p->absorptiontype = -4;
+      counter_inc(E, CTR_NT_STAT_FROM_GAMMA);
+    } else if ((kap_compton + kap_photo_electric + kap_pair_prod) > (zrand * kap_tot)) {
+      pair_prod(c, E, rng, p);
+    } else {
+      gamma_fatal("Failed to identify event. Gamma (1)", p);
+    }
+  } else {
+    gamma_fatal("Failed to identify event. Gamma (2)", p);
+  }
+}
+
+// update_packets.cc:16-69
+void do_nonthermal_predeposit(const Ctx &c, Est &E, artis_rng *rng, artis_packet *p, double t2) {
+  const double ts = p->prop_time;
+  const double particle_en = ARTIS_H * p->nu_cmf;
+  double endot = 0.;
+  double t_absorb = ts;
+  if (!c.rp.instant_particle_deposition) {
+    const double rho = cell_rho(c, cell_mgi(c, p->where));
+    endot = (p->pellet_decaytype == ARTIS_DECAYTYPE_ALPHA) ? 5.e11 * ARTIS_MEV * rho : 4.e10 * ARTIS_MEV * rho;
+    const double zrand = artis_rng_uniform(rng);
+    const double en_absorb = zrand * particle_en;
+    t_absorb = ts + en_absorb / endot;
+  }
+  if (t_absorb <= t2) {
+    if (p->pellet_decaytype == ARTIS_DECAYTYPE_ALPHA)
+      safeadd(&E.e->alpha_dep, p->e_cmf);
+    else if (p->pellet_decaytype == ARTIS_DECAYTYPE_BETAMINUS)
+      safeadd(&E.e->electron_dep, p->e_cmf);
+    else if (p->pellet_decaytype == ARTIS_DECAYTYPE_BETAPLUS)
+      safeadd(&E.e->positron_dep, p->e_cmf);
+    vec_scale(p->pos, t_absorb / ts);
+    p->prop_time = t_absorb;
+    p->type = ARTIS_TYPE_NTLEPTON;
+  } else {
+    p->nu_cmf = (particle_en - endot * (t2 - ts)) / ARTIS_H;
+    vec_scale(p->pos, t2 / ts);
+    p->prop_time = t2;
+  }
+}
+
+// update_packets.cc:71-135
+void update_pellet(const Ctx &c, Est &E, artis_rng *rng, artis_packet *p, int nts, double t2) {
+  if (!(p->prop_time < t2)) gamma_fatal("update_pellet: prop_time >= t2", p);
+  const double ts = p->prop_time;
+  const double tdecay = p->tdecay;
+  if (tdecay > t2) {
+    vec_scale(p->pos, t2 / ts);
+    p->prop_time = t2;
+  } else if (tdecay > ts) {
+#pragma omp atomic update
+    E.e->pellet_decays += 1;
+    p->prop_time = tdecay;
+    vec_scale(p->pos, tdecay / ts);
+    if (p->originated_from_particlenotgamma) {
+      if (p->pellet_decaytype == ARTIS_DECAYTYPE_BETAPLUS) {
+        safeadd(&E.e->positron_dep, p->e_cmf);
+        p->type = ARTIS_TYPE_NTLEPTON;
+        p->absorptiontype = -10;
+      } else if (p->pellet_decaytype == ARTIS_DECAYTYPE_BETAMINUS) {
+        safeadd(&E.e->electron_emission, p->e_cmf);
+        p->em_time = (int)p->prop_time;
+        p->type = ARTIS_TYPE_NONTHERMAL_PREDEPOSIT;
+        p->absorptiontype = -10;
+      } else if (p->pellet_decaytype == ARTIS_DECAYTYPE_ALPHA) {
+        safeadd(&E.e->alpha_emission, p->e_cmf);
+        p->em_time = (int)p->prop_time;
+        p->type = ARTIS_TYPE_NONTHERMAL_PREDEPOSIT;
+        p->absorptiontype = -10;
+      }
+    } else {
+      safeadd(&E.e->gamma_emission, p->e_cmf);
+      pellet_gamma_decay(c, rng, p);
+    }
+  } else if ((tdecay > 0) && (nts == 0)) {
+    p->e_cmf *= tdecay / c.g->tmin;
+    p->type = ARTIS_TYPE_PRE_KPKT;
+    p->absorptiontype = -7;
+    counter_inc(E, CTR_K_STAT_FROM_EARLIERDECAY);
+    p->prop_time = c.g->tmin;
+  } else {
+    gamma_fatal("Something gone wrong with decaying pellets", p);
+  }
+}
+
+// nonthermal.cc:1877-1977 with NT_SOLVE_SPENCERFANO off (classic / kilonova-LTE options): straight to a k-packet
+void do_ntlepton(Est &E, artis_packet *p) {
+  safeadd(&E.e->nt_energy_deposited, p->e_cmf);
+  p->last_event = 22;
+  p->type = ARTIS_TYPE_KPKT;
+  counter_inc(E, CTR_NT_STAT_TO_KPKT);
+}
+
 // ------------------------------------------------------------------------------------------- packet driver
 // update_packets.cc:137-202 do_packet (r-packet, k-packet and macro-atom paths)
 int do_packet(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_packet *p, double t2, int nts) {
@@ -1932,6 +2380,22 @@ int do_packet(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_packe
     case ARTIS_TYPE_MA:
       do_macroatom(c, tc, E, rng, p, nts);
       return 0;
+    case ARTIS_TYPE_RADIOACTIVE_PELLET:
+      if (!c.gs) return ARTIS_ERR_UNSUPPORTED;
+      update_pellet(c, E, rng, p, nts, t2);
+      return 0;
+    case ARTIS_TYPE_GAMMA:
+      if (!c.gs || !c.rp.do_r_lc) return ARTIS_ERR_UNSUPPORTED;
+      do_gamma(c, E, rng, p, t2);
+      if (p->type != ARTIS_TYPE_GAMMA && p->type != ARTIS_TYPE_ESCAPE) safeadd(&E.e->gamma_dep, p->e_cmf);
+      return 0;
+    case ARTIS_TYPE_NONTHERMAL_PREDEPOSIT:
+      do_nonthermal_predeposit(c, E, rng, p, t2);
+      return 0;
+    case ARTIS_TYPE_NTLEPTON:
+      if (c.rp.nt_solve_spencerfano) return ARTIS_ERR_UNSUPPORTED;
+      do_ntlepton(E, p);
+      return 0;
     default:
       return ARTIS_ERR_UNSUPPORTED;
   }
@@ -1943,14 +2407,16 @@ int do_packet(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_packe
 extern "C" {
 
 // Oracle counterpart of update_packets (update_packets.cc:234-333), deviation D5 (flattened pass loop).
-int oracle_update_packets(const artis_atomic_tables *at, const artis_geometry *geom, const artis_cell_state *cs,
-                          const artis_run_params *rp, int nts, artis_packet *packets, int npkts,
-                          artis_estimators *est, int64_t work_out[ARTIS_WORK_COUNT], int nthreads) {
+// gs (the gamma-ray line spectra, gammapkt.cc:27-33) may be NULL when no pellets or gamma packets are present.
+int oracle_update_packets_g(const artis_atomic_tables *at, const artis_geometry *geom, const artis_cell_state *cs,
+                            const artis_run_params *rp, const artis_gamma_spectra *gs, int nts, artis_packet *packets,
+                            int npkts, artis_estimators *est, int64_t work_out[ARTIS_WORK_COUNT], int nthreads) {
   Ctx c;
   c.at = at;
   c.g = geom;
   c.cs = cs;
   c.rp = *rp;
+  c.gs = gs;
   c.T_step_log = (log(at->maxtemp) - log(at->mintemp)) / (at->tablesize - 1.);
   Est E;
   E.e = est;
@@ -2017,7 +2483,13 @@ int oracle_update_packets(const artis_atomic_tables *at, const artis_geometry *g
   return status.load();
 }
 
-int oracle_abi_version(void) { return 1; }
+int oracle_update_packets(const artis_atomic_tables *at, const artis_geometry *geom, const artis_cell_state *cs,
+                          const artis_run_params *rp, int nts, artis_packet *packets, int npkts,
+                          artis_estimators *est, int64_t work_out[ARTIS_WORK_COUNT], int nthreads) {
+  return oracle_update_packets_g(at, geom, cs, rp, nullptr, nts, packets, npkts, est, work_out, nthreads);
+}
+
+int oracle_abi_version(void) { return 2; }
 
 // ---- unit hooks for tests/ ---------------------------------------------------------------------------------
 // Philox4x32-10 block (known-answer tests against the published Random123 vectors)

@@ -23,6 +23,10 @@ def lib():
         L.oracle_update_packets.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(ffi.RunParams), C.c_int,
                                             C.c_void_p, C.c_int, C.POINTER(ffi.Estimators), C.c_void_p, C.c_int]
         L.oracle_update_packets.restype = C.c_int
+        L.oracle_update_packets_g.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(ffi.RunParams),
+                                              C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.POINTER(ffi.Estimators),
+                                              C.c_void_p, C.c_int]
+        L.oracle_update_packets_g.restype = C.c_int
         _lib = L
     return _lib
 
@@ -33,9 +37,9 @@ def update_packets(model, nts, packets, est=None, nthreads=0, params=None):
         est = model.new_estimators()
     work = np.zeros(ffi.ARTIS_WORK_COUNT, dtype=np.int64)
     p = params if params is not None else model.params
-    rc = lib().oracle_update_packets(model.atomic, model.geometry, model.cellstate, C.byref(p), int(nts),
-                                     packets.ctypes.data, len(packets), C.byref(est.struct), work.ctypes.data,
-                                     int(nthreads))
+    rc = lib().oracle_update_packets_g(model.atomic, model.geometry, model.cellstate, C.byref(p),
+                                       getattr(model, "gamma_spectra", None), int(nts), packets.ctypes.data,
+                                       len(packets), C.byref(est.struct), work.ctypes.data, int(nthreads))
     if rc != 0:
         raise RuntimeError(f"oracle_update_packets -> {rc}")
     return est, work

@@ -89,13 +89,18 @@ def counters_equal(a, b):
 
 
 def assert_estimators_match(eg, eo, exact_counts=True, rtol=ESTIMATOR_RTOL):
-    for name in ("J", "nuJ", "ffheating", "colheating", "gamma", "bfheating"):
+    for name in ("J", "nuJ", "ffheating", "colheating", "gamma", "bfheating", "rpkt_emiss"):
         x, y = getattr(eg, name), getattr(eo, name)
-        scale = max(np.abs(y).max(), 1e-300)
-        assert np.abs(x - y).max() <= rtol * scale, (name, np.abs(x - y).max() / scale)
-    assert abs(eg.struct.cmf_lum - eo.struct.cmf_lum) <= rtol * max(abs(eo.struct.cmf_lum), 1e-300)
+        scale = max(np.abs(y).max(), 1e-300) if y.size else 1e-300
+        assert np.abs(x - y).max(initial=0.0) <= rtol * scale, (name, np.abs(x - y).max() / scale)
+    # time_step[nts] scalars (globals.h:20-40) and nt_energy_deposited
+    for name in ("cmf_lum", "gamma_dep", "positron_dep", "electron_dep", "electron_emission", "alpha_dep",
+                 "alpha_emission", "gamma_emission", "nt_energy_deposited"):
+        x, y = getattr(eg.struct, name), getattr(eo.struct, name)
+        assert abs(x - y) <= rtol * max(abs(y), 1e-300), (name, x, y)
     if exact_counts:
         assert eg.struct.nesc == eo.struct.nesc
+        assert eg.struct.pellet_decays == eo.struct.pellet_decays
         assert counters_equal(eg.counters, eo.counters), (eg.counters, eo.counters)
         assert (eg.ecounter == eo.ecounter).all()
         assert (eg.acounter == eo.acounter).all()

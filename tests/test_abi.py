@@ -39,6 +39,8 @@ int main(void) {
   O(pellet_nucindex) O(trueemissionvelocity) O(mastate) O(_pad0) O(_pad1) O(_pad2)
   printf("estimators %zu\n", sizeof(artis_estimators));
   printf("run_params %zu\n", sizeof(artis_run_params));
+  printf("cell_state %zu\n", sizeof(artis_cell_state));
+  printf("gamma_spectra %zu\n", sizeof(artis_gamma_spectra));
   return 0;
 }
 """
@@ -58,6 +60,8 @@ def test_c_header_layout_matches_numpy_and_ctypes():
         assert lay[name] == ffi.PACKET_DTYPE.fields[name][1], name
     assert lay["estimators"] == C.sizeof(ffi.Estimators)
     assert lay["run_params"] == C.sizeof(ffi.RunParams)
+    assert lay["gamma_spectra"] == C.sizeof(ffi.GammaSpectra)
+    assert lay["cell_state"] == 16 * 8  # 15 array pointers + ffegrp
 
 
 def test_header_declares_exactly_the_abi_symbols():
@@ -76,7 +80,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_without_gpu_and_reports_version():
     lib = C.CDLL(GPU_SO)
-    assert lib.artis_gpu_abi_version() == 1
+    assert lib.artis_gpu_abi_version() == 2
     lib.artis_gpu_last_error.restype = C.c_char_p
     assert lib.artis_gpu_last_error() is not None
 
