@@ -24,6 +24,7 @@ ABI_SYMBOLS = [
     "artis_gpu_estimators_download", "artis_gpu_estimator_block_doubles", "artis_gpu_estimator_block_to_device",
     "artis_gpu_estimator_block_from_device", "artis_gpu_last_transport_ms", "artis_gpu_last_precompute_ms",
     "artis_gpu_last_work_counts", "artis_gpu_last_rounds", "artis_gpu_spectrum", "artis_gpu_last_kernel_times", "artis_gpu_last_error", "artis_gpu_abi_version",
+    "artis_gpu_vpkt_init", "artis_gpu_vpkt_zero", "artis_gpu_vpkt_download", "artis_gpu_vpkt_last_stats",
 ]
 
 _gpu_lib = None
@@ -54,6 +55,9 @@ def gpu_lib():
         L.artis_gpu_last_error.restype = C.c_char_p
         L.artis_gpu_last_rounds.restype = C.c_int64
         L.artis_gpu_spectrum.argtypes = [C.c_int, C.c_int, vp, vp, vp]
+        L.artis_gpu_vpkt_init.argtypes = [C.POINTER(ffi.VpktParams)]
+        L.artis_gpu_vpkt_download.argtypes = [C.POINTER(ffi.VpktResult), C.c_int]
+        L.artis_gpu_vpkt_last_stats.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
         _gpu_lib = L
     return _gpu_lib
 
@@ -148,6 +152,30 @@ class Engine:
         self._check(self.lib.artis_gpu_spectrum(int(nnubins), int(nprocs), spec.ctypes.data, lc.ctypes.data,
                                                 lccmf.ctypes.data), "spectrum")
         return spec, lc, lccmf
+
+    # virtual packets (VPKT_ON)
+    def vpkt_init(self, cfg):
+        """Switch virtual packets on (cfg: ffi.VpktConfig); accumulators start at zero."""
+        self._vpkt_cfg = cfg
+        self._check(self.lib.artis_gpu_vpkt_init(C.byref(cfg.struct)), "vpkt_init")
+
+    def vpkt_zero(self):
+        self._check(self.lib.artis_gpu_vpkt_zero(), "vpkt_zero")
+
+    def vpkt_download(self, out=None, reset_counters=False):
+        """ADD the device virtual-packet spectra / grid / counters into out (ffi.VpktArrays)."""
+        if out is None:
+            out = ffi.VpktArrays(self._vpkt_cfg)
+        self._check(self.lib.artis_gpu_vpkt_download(C.byref(out.struct), int(bool(reset_counters))), "vpkt_download")
+        return out
+
+    def vpkt_last_stats(self):
+        """(ms of the k_vpkt launches, spawn records, traced virtual packets) of the last update."""
+        ms = C.c_double()
+        sp = C.c_int64()
+        tr = C.c_int64()
+        self.lib.artis_gpu_vpkt_last_stats(C.byref(ms), C.byref(sp), C.byref(tr))
+        return ms.value, sp.value, tr.value
 
     def last_kernel_times(self):
         """{class: (ms, launches)} for the last transport: rpkt, ma, kpkt, classify."""

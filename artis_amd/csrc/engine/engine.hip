@@ -29,6 +29,7 @@
 #include "transport.h"
 #include "wavefront.h"
 #include "spectrum.h"
+#include "vpkt.h"
 
 // ================================================================================================= kernels
 
@@ -494,6 +495,15 @@ struct Engine {
   int64_t last_kernel_launches[4] = {0, 0, 0, 0};
   double last_transport_ms = 0., last_precompute_ms = 0.;
   int64_t last_work[ARTIS_WORK_COUNT] = {0};
+  // virtual packets (vpkt.h): device accumulators and the spawn buffer (sized per update)
+  int64_t vpkt_cap_param = 0;
+  std::vector<int32_t> h_anumber;  // artis_atomic_tables.elem_anumber
+  double *d_vpkt_spawn = nullptr;
+  uint32_t vpkt_spawn_cap = 0;
+  std::vector<hipEvent_t> vev;  // (start, end) pairs around the k_vpkt launches of the last update
+  size_t vev_used = 0;
+  double last_vpkt_ms = 0.;
+  int64_t last_vpkt_spawns = 0, last_vpkt_traces = 0;
   std::string last_error;
 };
 Engine G;
@@ -611,6 +621,56 @@ int tcollect() {
 #define TEND(c) \
   if (int rc_ = tmark(c)) return rc_
 
+// virtual packets: trace the spawn records appended since the last flush, then empty the buffer
+// (stream-ordered; the spawn count is read by the kernel itself)
+int vpkt_flush() {
+  if (!G.K.V.on) return 0;
+  if (G.vev_used + 2 > G.vev.size()) {
+    for (int k = 0; k < 2; k++) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      G.vev.push_back(e);
+    }
+  }
+  HIPCHK(hipEventRecord(G.vev[G.vev_used++], G.stream));
+  k_vpkt<<<(unsigned)G.wave_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, G.W.refill_min);
+  HIPCHK(hipEventRecord(G.vev[G.vev_used++], G.stream));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemsetAsync(G.K.V.spawn_ctr, 0, 2 * sizeof(uint32_t), G.stream));
+  return 0;
+}
+// size the spawn buffer for n packets (artis_vpkt_params.spawn_capacity, default 16 per packet, >= 2^20)
+int vpkt_prepare(int64_t n) {
+  if (!G.K.V.on) return 0;
+  int64_t cap = G.vpkt_cap_param > 0 ? G.vpkt_cap_param : std::max<int64_t>(16 * n, 1 << 20);
+  cap = std::min<int64_t>(cap, 0x7fffffff / 2);
+  if ((uint32_t)cap > G.vpkt_spawn_cap) {
+    if (G.d_vpkt_spawn) (void)hipFree(G.d_vpkt_spawn);
+    G.d_vpkt_spawn = nullptr;
+    HIPCHK(hipMalloc(&G.d_vpkt_spawn, (size_t)cap * VPKT_SPAWN_WORDS * sizeof(double)));
+    G.vpkt_spawn_cap = (uint32_t)cap;
+  }
+  G.K.V.spawn = G.d_vpkt_spawn;
+  G.K.V.cap = G.vpkt_spawn_cap;
+  HIPCHK(hipMemsetAsync(G.K.V.spawn_ctr, 0, 2 * sizeof(uint32_t), G.stream));
+  G.vev_used = 0;
+  return 0;
+}
+int vpkt_collect(const unsigned long long before[8]) {
+  G.last_vpkt_ms = 0.;
+  for (size_t i = 0; i + 1 < G.vev_used; i += 2) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, G.vev[i], G.vev[i + 1]));
+    G.last_vpkt_ms += ms;
+  }
+  G.vev_used = 0;
+  unsigned long long after[8];
+  HIPCHK(hipMemcpy(after, G.K.V.ctr, sizeof(after), hipMemcpyDeviceToHost));
+  G.last_vpkt_traces = (int64_t)(after[0] - before[0]);
+  G.last_vpkt_spawns = (int64_t)(after[4] - before[4]);
+  return 0;
+}
+
 #define WAVE_MAX_ROUNDS 10000000
 int run_wavefront(int64_t n, int nts, double t2) {
   const WaveState &W = G.W;
@@ -657,6 +717,7 @@ int run_wavefront(int64_t n, int nts, double t2) {
     k_kpkt<<<grid / 4, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
     TEND(2);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QK, 0, 2 * sizeof(uint32_t), G.stream));
+    if (int rc = vpkt_flush()) return rc;
     HIPCHK(hipGetLastError());
     const int slot = (int)(round & 1);
     HIPCHK(hipMemcpyAsync(G.h_ctr + slot * NQUEUES * 2, W.ctr, NQUEUES * 2 * sizeof(uint32_t),
@@ -748,6 +809,134 @@ int artis_gpu_spectrum(int nnubins, int nprocs, double *spec_flux, double *lc_lu
   (void)hipFree(d);
   return rc;
 }
+int artis_gpu_vpkt_init(const artis_vpkt_params *vp) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  if (!vp || vp->nobs <= 0 || vp->nspectra <= 0 || vp->nspectra > ARTIS_VPKT_MAX_SPECTRA || vp->nrange < 0 ||
+      vp->nrange > ARTIS_VPKT_MRANGE || vp->vmtbins <= 0 || vp->vmnubins <= 0 || !vp->nz_obs || !vp->phi_obs ||
+      !vp->exclude || vp->nprocs <= 0 || vp->spawn_capacity < 0 ||
+      (vp->vgrid_flag == 1 && (vp->nrange_grid < 0 || vp->nrange_grid > ARTIS_VPKT_MRANGE_GRID ||
+                               vp->ny_vgrid <= 0 || vp->nz_vgrid <= 0))) {
+    G.last_error = "vpkt_init: bad virtual-packet parameters";
+    return ARTIS_ERR_BAD_ARGUMENT;
+  }
+  static_assert(VPKT_MAX_SPECTRA == ARTIS_VPKT_MAX_SPECTRA && VPKT_MRANGE == ARTIS_VPKT_MRANGE &&
+                    VPKT_MRANGE_GRID == ARTIS_VPKT_MRANGE_GRID,
+                "device and ABI vpkt limits differ");
+  DevVpkt V{};
+  V.nobs = vp->nobs;
+  V.nspectra = vp->nspectra;
+  V.vmtbins = vp->vmtbins;
+  V.vmnubins = vp->vmnubins;
+  V.nrange = vp->nrange;
+  V.vgrid_flag = vp->vgrid_flag;
+  V.nrange_grid = vp->vgrid_flag == 1 ? vp->nrange_grid : 0;
+  V.ny_vgrid = vp->ny_vgrid;
+  V.nz_vgrid = vp->nz_vgrid;
+  V.nprocs = vp->nprocs;
+  for (int i = 0; i < VPKT_MAX_SPECTRA; i++) V.exclude[i] = i < vp->nspectra ? vp->exclude[i] : 0.;
+  V.tmin_vspec = vp->tmin_vspec;
+  V.tmax_vspec = vp->tmax_vspec;
+  V.numin_vspec = vp->numin_vspec;
+  V.numax_vspec = vp->numax_vspec;
+  V.tmin_input = vp->tmin_vspec_input;
+  V.tmax_input = vp->tmax_vspec_input;
+  for (int i = 0; i < VPKT_MRANGE; i++) {
+    V.numin_input[i] = vp->numin_vspec_input[i];
+    V.numax_input[i] = vp->numax_vspec_input[i];
+  }
+  V.tau_max = vp->tau_max_vpkt;
+  V.tmin_grid = vp->tmin_grid;
+  V.tmax_grid = vp->tmax_grid;
+  for (int i = 0; i < VPKT_MRANGE_GRID; i++) {
+    V.nu_grid_min[i] = vp->nu_grid_min[i];
+    V.nu_grid_max[i] = vp->nu_grid_max[i];
+  }
+  // observer vectors (vpkt.cc:863-865) and the float bin edges of init_vspecpol (vpkt.cc:425-436), host libm
+  std::vector<double> obs(3 * (size_t)vp->nobs);
+  for (int b = 0; b < vp->nobs; b++) {
+    const double nz = vp->nz_obs[b], phi = vp->phi_obs[b];
+    obs[3 * b] = sqrt(1 - nz * nz) * cos(phi);
+    obs[3 * b + 1] = sqrt(1 - nz * nz) * sin(phi);
+    obs[3 * b + 2] = nz;
+  }
+  V.dlogt = (log(vp->tmax_vspec) - log(vp->tmin_vspec)) / vp->vmtbins;
+  V.dlognu = (log(vp->numax_vspec) - log(vp->numin_vspec)) / vp->vmnubins;
+  std::vector<float> delta_t(vp->vmtbins), delta_freq(vp->vmnubins);
+  for (int n = 0; n < vp->vmtbins; n++) {
+    const float lower = (float)exp(log(vp->tmin_vspec) + (n * (V.dlogt)));
+    delta_t[n] = (float)(exp(log(vp->tmin_vspec) + ((n + 1) * (V.dlogt))) - lower);
+  }
+  for (int m = 0; m < vp->vmnubins; m++) {
+    const float lower = (float)exp(log(vp->numin_vspec) + (m * (V.dlognu)));
+    delta_freq[m] = (float)(exp(log(vp->numin_vspec) + ((m + 1) * (V.dlognu))) - lower);
+  }
+  const std::vector<int32_t> &anum = G.h_anumber;
+  int rc = 0;
+  rc |= dupload(&V.obs, obs.data(), obs.size());
+  rc |= dupload(&V.delta_t, delta_t.data(), delta_t.size());
+  rc |= dupload(&V.delta_freq, delta_freq.data(), delta_freq.size());
+  rc |= dupload(&V.anumber, anum.data(), anum.size());
+  V.vstokes_stride = (int64_t)vp->vmtbins * vp->nobs * vp->nspectra * vp->vmnubins;
+  V.vgrid_stride = (vp->vgrid_flag == 1) ? (int64_t)vp->ny_vgrid * vp->nz_vgrid * vp->nrange_grid * vp->nobs : 0;
+  rc |= dalloc(&V.vstokes, (size_t)(3 * V.vstokes_stride));
+  rc |= dalloc(&V.vgrid, (size_t)std::max<int64_t>(3 * V.vgrid_stride, 1));
+  rc |= dalloc(&V.ctr, 8);
+  rc |= dalloc(&V.spawn_ctr, 2);
+  if (rc) return ARTIS_ERR_HIP;
+  V.spawn = G.d_vpkt_spawn;
+  V.cap = G.vpkt_spawn_cap;
+  V.on = 1;
+  G.K.V = V;
+  G.vpkt_cap_param = vp->spawn_capacity;
+  return artis_gpu_vpkt_zero();
+}
+
+int artis_gpu_vpkt_zero(void) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  const DevVpkt &V = G.K.V;
+  if (!V.on) return ARTIS_ERR_BAD_ARGUMENT;
+  HIPCHK(hipMemsetAsync(V.vstokes, 0, (size_t)3 * V.vstokes_stride * sizeof(double), G.stream));
+  if (V.vgrid_stride) HIPCHK(hipMemsetAsync(V.vgrid, 0, (size_t)3 * V.vgrid_stride * sizeof(double), G.stream));
+  HIPCHK(hipMemsetAsync(V.ctr, 0, 8 * sizeof(unsigned long long), G.stream));
+  HIPCHK(hipMemsetAsync(V.spawn_ctr, 0, 2 * sizeof(uint32_t), G.stream));
+  HIPCHK(hipStreamSynchronize(G.stream));
+  return 0;
+}
+
+int artis_gpu_vpkt_download(artis_vpkt_result *out, int reset_counters) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  const DevVpkt &V = G.K.V;
+  if (!V.on || !out || !out->vstokes_i || !out->vstokes_q || !out->vstokes_u) return ARTIS_ERR_BAD_ARGUMENT;
+  if (V.vgrid_stride && (!out->vgrid_i || !out->vgrid_q || !out->vgrid_u)) return ARTIS_ERR_BAD_ARGUMENT;
+  HIPCHK(hipStreamSynchronize(G.stream));
+  std::vector<double> h((size_t)3 * std::max(V.vstokes_stride, V.vgrid_stride));
+  HIPCHK(hipMemcpy(h.data(), V.vstokes, (size_t)3 * V.vstokes_stride * sizeof(double), hipMemcpyDeviceToHost));
+  double *dst[3] = {out->vstokes_i, out->vstokes_q, out->vstokes_u};
+  for (int c = 0; c < 3; c++)
+    for (int64_t j = 0; j < V.vstokes_stride; j++) dst[c][j] += h[c * V.vstokes_stride + j];
+  if (V.vgrid_stride) {
+    HIPCHK(hipMemcpy(h.data(), V.vgrid, (size_t)3 * V.vgrid_stride * sizeof(double), hipMemcpyDeviceToHost));
+    double *gd[3] = {out->vgrid_i, out->vgrid_q, out->vgrid_u};
+    for (int c = 0; c < 3; c++)
+      for (int64_t j = 0; j < V.vgrid_stride; j++) gd[c][j] += h[c * V.vgrid_stride + j];
+  }
+  unsigned long long ctr[8];
+  HIPCHK(hipMemcpy(ctr, V.ctr, sizeof(ctr), hipMemcpyDeviceToHost));
+  out->nvpkt += (int64_t)ctr[0];
+  out->nvpkt_esc1 += (int64_t)ctr[1];
+  out->nvpkt_esc2 += (int64_t)ctr[2];
+  out->nvpkt_esc3 += (int64_t)ctr[3];
+  if (reset_counters) HIPCHK(hipMemset(V.ctr, 0, 4 * sizeof(unsigned long long)));
+  return 0;
+}
+
+int artis_gpu_vpkt_last_stats(double *ms, int64_t *spawns, int64_t *traces) {
+  if (ms) *ms = G.last_vpkt_ms;
+  if (spawns) *spawns = G.last_vpkt_spawns;
+  if (traces) *traces = G.last_vpkt_traces;
+  return 0;
+}
+
 int artis_gpu_last_kernel_times(double ms[4], int64_t launches[4]) {
   for (int c = 0; c < 4; c++) {
     ms[c] = G.last_kernel_ms[c];
@@ -776,6 +965,8 @@ void artis_gpu_finalize(void) {
     for (int q = 0; q < NQUEUES; q++) (void)hipFree(G.W.q[q]);
   }
   if (G.h_ctr) (void)hipHostFree(G.h_ctr);
+  if (G.d_vpkt_spawn) (void)hipFree(G.d_vpkt_spawn);
+  for (hipEvent_t e : G.vev) (void)hipEventDestroy(e);
   for (hipEvent_t e : G.tev) (void)hipEventDestroy(e);
   for (int r = 0; r < 2; r++)
     if (G.ev_round[r]) (void)hipEventDestroy(G.ev_round[r]);
@@ -819,6 +1010,8 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     G.ma_occ = (oc && oc[0] == '8') ? 8 : 1;
   }
   G.params = *rp;
+  G.h_anumber.assign(a->nelements, 0);
+  if (a->elem_anumber) G.h_anumber.assign(a->elem_anumber, a->elem_anumber + a->nelements);
   DevTab &T = G.K.T;
   T.nelements = a->nelements;
   T.maxnions = a->maxnions;
@@ -1354,6 +1547,11 @@ int artis_gpu_update_packets_resident(int my_rank, int nts) {
   HIPCHK(hipMemsetAsync(G.K.E.err, 0, 4 * sizeof(int32_t), G.stream));
   HIPCHK(hipMemsetAsync(G.K.E.work, 0, ARTIS_WORK_COUNT * sizeof(unsigned long long), G.stream));
   const int64_t n = G.npkts;
+  unsigned long long vbefore[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (G.K.V.on) {
+    if (int rc = vpkt_prepare(n)) return rc;
+    HIPCHK(hipMemcpy(vbefore, G.K.V.ctr, sizeof(vbefore), hipMemcpyDeviceToHost));
+  }
   HIPCHK(hipEventRecord(G.ev0, G.stream));
   G.last_rounds = 0;
   if (n > 0 && G.use_megakernel) {
@@ -1361,6 +1559,7 @@ int artis_gpu_update_packets_resident(int my_rank, int nts) {
     k_transport<<<(unsigned)((n + TRANSPORT_BLOCK - 1) / TRANSPORT_BLOCK), TRANSPORT_BLOCK, 0, G.stream>>>(
         G.d_ctx, G.d_soa, n, nts, t2);
     HIPCHK(hipGetLastError());
+    if (int rc = vpkt_flush()) return rc;
   } else if (n > 0) {
     if (int rc = run_wavefront(n, nts, t2)) return rc;
   }
@@ -1369,6 +1568,8 @@ int artis_gpu_update_packets_resident(int my_rank, int nts) {
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, G.ev0, G.ev1));
   G.last_transport_ms = ms;
+  if (G.K.V.on)
+    if (int rc = vpkt_collect(vbefore)) return rc;
   unsigned long long w[ARTIS_WORK_COUNT];
   HIPCHK(hipMemcpy(w, G.K.E.work, sizeof(w), hipMemcpyDeviceToHost));
   for (int k = 0; k < ARTIS_WORK_COUNT; k++) G.last_work[k] = (int64_t)w[k];

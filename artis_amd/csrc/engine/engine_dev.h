@@ -136,6 +136,36 @@ struct DevEst {
   int32_t *err;                    // [4] code, packet number, aux, aux
 };
 
+// virtual packets (VPKT_ON, vpkt.cc): parameters of artis_vpkt_params, derived bins, accumulators, and the spawn
+// buffer the emission sites append to (vpkt.h)
+#define VPKT_MAX_SPECTRA 8
+#define VPKT_MRANGE 4
+#define VPKT_MRANGE_GRID 5
+#define VPKT_SPAWN_WORDS 13
+struct DevVpkt {
+  int32_t on;
+  int32_t nobs, nspectra, vmtbins, vmnubins, nrange, vgrid_flag, nrange_grid, ny_vgrid, nz_vgrid, nprocs;
+  double exclude[VPKT_MAX_SPECTRA];
+  double tmin_vspec, tmax_vspec, numin_vspec, numax_vspec, dlogt, dlognu;
+  double tmin_input, tmax_input, numin_input[VPKT_MRANGE], numax_input[VPKT_MRANGE];
+  double tau_max;
+  double tmin_grid, tmax_grid, nu_grid_min[VPKT_MRANGE_GRID], nu_grid_max[VPKT_MRANGE_GRID];
+  const double *obs;        // [nobs * 3] observer unit vectors (host libm, vpkt.cc:863-865)
+  const float *delta_t;     // [vmtbins]  vspecpol.delta_t (float, vpkt.cc:18)
+  const float *delta_freq;  // [vmnubins] delta_freq_vspec (float, vpkt.cc:26)
+  const int32_t *anumber;   // [nelements]
+  double *vstokes;          // [3][vmtbins][nobs * nspectra][vmnubins]: I, Q, U
+  int64_t vstokes_stride;   // doubles per Stokes component
+  double *vgrid;            // [3][ny][nz][nrange_grid][nobs]
+  int64_t vgrid_stride;
+  unsigned long long *ctr;  // [8]: nvpkt, nvpkt_esc1..3, traces, cell segments, lines scanned, spawns dropped
+  // spawn records, word-major: spawn[w * cap + s]; words: 0-2 pos, 3-5 dir, 6 nu_cmf, 7 e_cmf, 8-9 stokes Q, U,
+  // 10 prop_time (= t_current at every call site), 11 (where, next_trans), 12 (last_cross, realtype)
+  double *spawn;
+  uint32_t *spawn_ctr;      // [2]: appended, trace fetch head
+  uint32_t cap;
+};
+
 struct DevRun {
   uint32_t seed;
   int32_t rank;

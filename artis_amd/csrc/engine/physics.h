@@ -36,6 +36,7 @@ enum : int32_t {
   ERR_THICK_MA = 12,
   ERR_NONFINITE = 13,
   ERR_GAMMA = 14,  // an abort() path of the pellet / gamma code (aux = which)
+  ERR_VPKT_OVERFLOW = 15,  // the virtual-packet spawn buffer of one event round is full
 };
 
 struct Ctx {
@@ -44,6 +45,7 @@ struct Ctx {
   DevCells C;
   DevEst E;
   DevRun R;
+  DevVpkt V;
 };
 
 // The transport kernels read the context through a pointer to a device copy (engine.hip: sync_ctx) rather

@@ -690,6 +690,49 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
   }
 }
 
+// ------------------------------------------------------------------------------------------ virtual packets
+// vpkt.cc:837-896, the part at the emission site: the cut on thick cells and the observer time / frequency
+// windows.  A packet passing some window is recorded in the spawn buffer; the traversals themselves run in
+// k_vpkt (vpkt.h), which repeats the per-observer cuts.  The next_trans fix-up of vpkt.cc:853-858 only ever
+// writes 0 over 0 and is omitted.
+DEVFN void vpkt_spawn(Tx &x, const Pkt &p, int realtype) {
+  const Ctx &K = x.K;
+  const DevVpkt &V = K.V;
+  const int mgi = cell_mgi(K, p.where);
+  if (mgi == K.G.npts_model || K.C.thick[mgi] != 0) return;
+  const double t_current = p.prop_time;
+  bool any = false;
+  for (int b = 0; b < V.nobs && !any; b++) {
+    const double obs[3] = {V.obs[3 * b], V.obs[3 * b + 1], V.obs[3 * b + 2]};
+    const double t_arrive = t_current - (dot(p.pos, obs) / ARTIS_CLIGHT_PROP);
+    if (t_arrive >= V.tmin_input && t_arrive <= V.tmax_input) {
+      const double nu_rf = p.nu_cmf / doppler_pos_dir(K, p.pos, obs, t_current);
+      for (int i = 0; i < V.nrange; i++)
+        if (nu_rf > V.numin_input[i] && nu_rf < V.numax_input[i]) any = true;
+    }
+  }
+  if (!any) return;
+  const uint32_t s = atomicAdd(&V.spawn_ctr[0], 1u);
+  if (s >= V.cap) {
+    fail(K, ERR_VPKT_OVERFLOW, p.number, (int)V.cap);
+    x.ok = false;
+    return;
+  }
+  const int64_t cap = V.cap;
+  double *sp = V.spawn;
+  for (int d = 0; d < 3; d++) {
+    sp[d * cap + s] = p.pos[d];
+    sp[(3 + d) * cap + s] = p.dir[d];
+  }
+  sp[6 * cap + s] = p.nu_cmf;
+  sp[7 * cap + s] = p.e_cmf;
+  sp[8 * cap + s] = p.stokes[1];
+  sp[9 * cap + s] = p.stokes[2];
+  sp[10 * cap + s] = t_current;
+  reinterpret_cast<uint64_t *>(sp)[11 * cap + s] = pack2(p.where, p.next_trans);
+  reinterpret_cast<uint64_t *>(sp)[12 * cap + s] = pack2(p.last_cross, realtype);
+}
+
 // rpkt.cc:330-447
 DEVNI void rpkt_event_continuum(Tx &x, Pkt &p, const Kappa &kap, int k, int mgi) {
   const Ctx &K = x.K;
@@ -707,6 +750,10 @@ DEVNI void rpkt_event_continuum(Tx &x, Pkt &p, const Kappa &kap, int k, int mgi)
     p.last_event = 12;
     lctr(x.L, CTR_ESCOUNTER);
     lwork(x.L, WK_ES_SCAT, 1);
+    if (K.V.on) {  // rpkt.cc:358-363
+      p.last_cross = ARTIS_NONE;
+      vpkt_spawn(x, p, 1);
+    }
     escat_rpkt(x, p);
     p.em_pos[0] = p.pos[0];
     p.em_pos[1] = p.pos[1];
@@ -1339,6 +1386,7 @@ DEVNI void ma_finish(Tx &x, Pkt &p, const MaEnd &e, unsigned jumps) {
     p.em_pos[2] = p.pos[2];
     p.em_time = (int)p.prop_time;
     p.nscatterings = 0;
+    if (K.V.on) vpkt_spawn(x, p, 3);  // macroatom.cc:292-295
   } else if (e.code == MA_END_COLDEEXC || e.code == MA_END_COLRECOMB) {
     const bool deexc = e.code == MA_END_COLDEEXC;
     lctr(x.L, deexc ? CTR_MA_STAT_DEACTIVATION_COLLDEEXC : CTR_MA_STAT_DEACTIVATION_COLLRECOMB);
@@ -1369,6 +1417,7 @@ DEVNI void ma_finish(Tx &x, Pkt &p, const MaEnd &e, unsigned jumps) {
     p.em_pos[2] = p.pos[2];
     p.em_time = (int)p.prop_time;
     p.nscatterings = 0;
+    if (K.V.on) vpkt_spawn(x, p, 3);  // macroatom.cc:376-379
   }
   if (p.trueemissiontype < 0) {
     p.trueemissiontype = p.emissiontype;
@@ -1530,6 +1579,7 @@ DEVNI void do_kpkt(Tx &x, Pkt &p, double t2) {
     p.em_pos[2] = p.pos[2];
     p.em_time = (int)p.prop_time;
     p.nscatterings = 0;
+    if (K.V.on) vpkt_spawn(x, p, 2);  // kpkt.cc:631-634
   } else if (ctype == ARTIS_COOLINGTYPE_FB) {
     const int el = K.T.cool_element[icool];
     const int lowerion = K.T.cool_ion[icool];
@@ -1554,6 +1604,7 @@ DEVNI void do_kpkt(Tx &x, Pkt &p, double t2) {
     p.em_pos[2] = p.pos[2];
     p.em_time = (int)p.prop_time;
     p.nscatterings = 0;
+    if (K.V.on) vpkt_spawn(x, p, 2);  // kpkt.cc:691-694
   } else if (ctype == ARTIS_COOLINGTYPE_COLLEXC) {
     const float nne = K.C.nne[mgi];
     const double contrib_low = (icool > ilow) ? cc[icool - 1] : oldcoolingsum;

@@ -1,0 +1,356 @@
+// vpkt.h -- virtual packets (VPKT_ON, reference vpkt.cc) on the device.
+//
+// The reference traces, at every r-packet emission (electron scattering, macro-atom bb / fb deactivation,
+// k-packet ff / fb cooling), one virtual packet per observer direction and frequency range inline, on the
+// emitting packet's thread (vpkt_call_estimators vpkt.cc:837-896 -> rlc_emiss_vpkt vpkt.cc:76-368).  Here the
+// emission site only records the emitting packet's state in a spawn buffer (vpkt_spawn, transport.h), and
+// k_vpkt traces the virtual packets afterwards, one (spawn, observer) work item per lane:
+//
+//   * persistent lanes with a wave-aggregated work fetch, one cell segment (boundary, continuum opacity, the
+//     lines up to the boundary, move) per loop pass, so lanes whose packet dies early (tau > tau_max) pick up
+//     new work instead of idling while the wave's longest traversal runs;
+//   * the per-observer cuts (time window, frequency ranges) and the order of the range loop are the
+//     reference's, including the observer vector that a scattering-type traversal overwrites (vpkt.cc:179);
+//   * spectra are float64 atomics into vstokes_i/q/u (add_to_vspecpol vpkt.cc:388-406) and the velocity-grid
+//     map (add_to_vpkt_grid vpkt.cc:581-627).
+//
+// The virtual packets draw no random numbers and change nothing in the real packets, so deferring them is
+// exact; only the order of the floating-point sums differs from the reference's serial loop.
+#ifndef ARTIS_VPKT_H
+#define ARTIS_VPKT_H
+
+#include "wavefront.h"
+
+#define VPKT_MAX_CELLS 1000000
+
+// vpkt.cc:374-385
+DEVFN bool vpkt_alive(const DevVpkt &V, const double *tau) {
+  int count = 0;
+  for (int i = 0; i < VPKT_MAX_SPECTRA; i++)
+    if (i < V.nspectra && tau[i] > V.tau_max) count += 1;
+  return count != V.nspectra;
+}
+
+// vpkt.cc:388-406 (deviation D9: a bin index rounded up to the array end is skipped)
+DEVFN void add_to_vspecpol(const DevVpkt &V, double nu_rf, double e_rf, const double st[3], int bin, int ind,
+                           double t_arrive) {
+  const int ind_comb = V.nspectra * bin + ind;
+  if (t_arrive > V.tmin_vspec && t_arrive < V.tmax_vspec) {
+    const int nt = (int)((log(t_arrive) - log(V.tmin_vspec)) / V.dlogt);
+    if (nu_rf > V.numin_vspec && nu_rf < V.numax_vspec) {
+      const int nnu = (int)((log(nu_rf) - log(V.numin_vspec)) / V.dlognu);
+      if (nt >= V.vmtbins || nnu >= V.vmnubins) return;
+      const double pktcontrib = e_rf / V.delta_t[nt] / V.delta_freq[nnu] / 4.e12 / ARTIS_PI / ARTIS_PARSEC /
+                                ARTIS_PARSEC / V.nprocs * 4 * ARTIS_PI;
+      const int64_t idx = ((int64_t)nt * V.nobs * V.nspectra + ind_comb) * V.vmnubins + nnu;
+      unsafeAtomicAdd(&V.vstokes[idx], st[0] * pktcontrib);
+      unsafeAtomicAdd(&V.vstokes[V.vstokes_stride + idx], st[1] * pktcontrib);
+      unsafeAtomicAdd(&V.vstokes[2 * V.vstokes_stride + idx], st[2] * pktcontrib);
+    }
+  }
+}
+
+// vpkt.cc:581-627
+DEVFN void add_to_vpkt_grid(const Ctx &K, double nu_rf, double e_rf, const double st[3], const double vel[3],
+                            int bin_range, int bin, const double obs[3]) {
+  const DevVpkt &V = K.V;
+  double vref1, vref2;
+  const double nx = obs[0], ny = obs[1], nz = obs[2];
+  if (nx == 1) {
+    vref1 = vel[1];
+    vref2 = vel[2];
+  } else if (nx == -1) {
+    vref1 = -vel[1];
+    vref2 = -vel[2];
+  } else {
+    vref1 = -ny * vel[0] + (nx + nz * nz / (1 + nx)) * vel[1] - ny * nz * (1 - nx) / sqrt(1 - nx * nx) * vel[2];
+    vref2 = -nz * vel[0] - ny * nz * (1 - nx) / sqrt(1 - nx * nx) * vel[1] + (nx + ny * ny / (1 + nx)) * vel[2];
+  }
+  const double vmax = K.G.vmax;
+  if (fabs(vref1) >= vmax || fabs(vref2) >= vmax) return;
+  const double ybin = 2 * vmax / V.ny_vgrid;
+  const double zbin = 2 * vmax / V.nz_vgrid;
+  const int nt = (int)((vmax - vref1) / ybin);
+  const int mt = (int)((vmax - vref2) / zbin);
+  if (nu_rf > V.nu_grid_min[bin_range] && nu_rf < V.nu_grid_max[bin_range]) {
+    const int64_t idx = (((int64_t)nt * V.nz_vgrid + mt) * V.nrange_grid + bin_range) * V.nobs + bin;
+    unsafeAtomicAdd(&V.vgrid[idx], st[0] * e_rf);
+    unsafeAtomicAdd(&V.vgrid[V.vgrid_stride + idx], st[1] * e_rf);
+    unsafeAtomicAdd(&V.vgrid[2 * V.vgrid_stride + idx], st[2] * e_rf);
+  }
+}
+
+// state of one lane: the work item (spawn, observer, next range) and the traversal in progress
+struct VLane {
+  uint32_t s;
+  int b, range, realtype;
+  double t_current, pos0[3], obs[3];
+  bool tracing;
+  Pkt d;  // the dummy packet (only the fields boundary_cross / move_pkt / change_cell use are live)
+  double tau[VPKT_MAX_SPECTRA];
+  double I, Q, U, pn, t_future;
+  int mgi, cells;
+};
+
+// rlc_emiss_vpkt prologue (vpkt.cc:93-193): the dummy packet, its Stokes vector and weight p_n
+DEVFN void vpkt_trace_init(const Ctx &K, const LocalCounters &L, VLane &v) {
+  const DevVpkt &V = K.V;
+  const int64_t cap = V.cap;
+  const double *sp = V.spawn;
+  const uint32_t s = v.s;
+  const uint64_t w11 = reinterpret_cast<const uint64_t *>(sp)[11 * cap + s];
+  const uint64_t w12 = reinterpret_cast<const uint64_t *>(sp)[12 * cap + s];
+  Pkt &d = v.d;
+  for (int k = 0; k < 3; k++) {
+    d.pos[k] = v.pos0[k];
+    d.dir[k] = v.obs[k];
+  }
+  d.where = lo32(w11);
+  d.next_trans = hi32(w11);
+  d.last_cross = lo32(w12);
+  d.type = ARTIS_TYPE_RPKT;
+  d.prop_time = v.t_current;
+  d.nu_cmf = sp[6 * cap + s];
+  d.e_cmf = sp[7 * cap + s];
+  d.number = -1;
+  for (int i = 0; i < VPKT_MAX_SPECTRA; i++) v.tau[i] = 0.;
+  atomicAdd(&V.ctr[0], 1ull);  // nvpkt
+  const double t_current = v.t_current;
+  const double vel_vec[3] = {v.pos0[0] / t_current, v.pos0[1] / t_current, v.pos0[2] / t_current};
+  d.nu_rf = d.nu_cmf / doppler_pos_dir(K, v.pos0, d.dir, t_current);
+  d.e_rf = d.e_cmf * d.nu_rf / d.nu_cmf;
+  if (v.realtype == 1) {
+    double Qi = sp[8 * cap + s];
+    double Ui = sp[9 * cap + s];
+    const double pkt_dir[3] = {sp[3 * cap + s], sp[4 * cap + s], sp[5 * cap + s]};
+    double old_dir_cmf[3], obs_cmf[3], ref1[3], ref2[3];
+    frame_transform(pkt_dir, &Qi, &Ui, vel_vec, old_dir_cmf);
+    angle_ab(d.dir, vel_vec, obs_cmf);
+    meridian(old_dir_cmf, ref1, ref2);
+    const double i1 = rot_angle(old_dir_cmf, obs_cmf, ref1, ref2);
+    const double cos2i1 = cos(2 * i1);
+    const double sin2i1 = sin(2 * i1);
+    const double Qold = Qi * cos2i1 - Ui * sin2i1;
+    const double Uold = Qi * sin2i1 + Ui * cos2i1;
+    const double mu = dot(old_dir_cmf, obs_cmf);
+    v.pn = 3. / (16. * ARTIS_PI) * (1 + pow(mu, 2.) + (pow(mu, 2.) - 1) * Qold);
+    const double Inew = 0.75 * ((mu * mu + 1.0) + Qold * (mu * mu - 1.0));
+    double Qnew = 0.75 * ((mu * mu - 1.0) + Qold * (mu * mu + 1.0));
+    double Unew = 1.5 * mu * Uold;
+    Qnew = Qnew / Inew;
+    Unew = Unew / Inew;
+    v.I = Inew / Inew;
+    meridian(obs_cmf, ref1, ref2);
+    const double i2 = ARTIS_PI + rot_angle(obs_cmf, old_dir_cmf, ref1, ref2);
+    const double cos2i2 = cos(2 * i2);
+    const double sin2i2 = sin(2 * i2);
+    v.Q = Qnew * cos2i2 + Unew * sin2i2;
+    v.U = -Qnew * sin2i2 + Unew * cos2i2;
+    const double vel_rev[3] = {-vel_vec[0], -vel_vec[1], -vel_vec[2]};
+    frame_transform(obs_cmf, &v.Q, &v.U, vel_rev, v.obs);  // overwrites obs, as vpkt.cc:179
+  } else {
+    v.I = 1;
+    v.Q = 0;
+    v.U = 0;
+    v.pn = 1 / (4 * ARTIS_PI);
+  }
+  v.mgi = cell_mgi(K, d.where);
+  v.t_future = t_current;
+  v.cells = 0;
+}
+
+// the escape branch of rlc_emiss_vpkt (vpkt.cc:314-367)
+DEVFN void vpkt_trace_finish(const Ctx &K, VLane &v) {
+  const DevVpkt &V = K.V;
+  if (v.realtype >= 1 && v.realtype <= 3) atomicAdd(&V.ctr[v.realtype], 1ull);  // nvpkt_esc1..3
+  double t_arrive = 0.;
+  for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++) {
+    if (ind >= V.nspectra) break;
+    const double prob = v.pn * exp(-v.tau[ind]);
+    const double st[3] = {v.I * prob, v.Q * prob, v.U * prob};
+    t_arrive = v.t_current - (dot(v.pos0, v.d.dir) / ARTIS_CLIGHT_PROP);
+    add_to_vspecpol(V, v.d.nu_rf, v.d.e_rf, st, v.b, ind, t_arrive);
+  }
+  if (V.vgrid_flag == 1) {
+    const double prob = v.pn * exp(-v.tau[0]);
+    const double st[3] = {v.I * prob, v.Q * prob, v.U * prob};
+    const double t = v.t_current;
+    const double vel_vec[3] = {v.pos0[0] / t, v.pos0[1] / t, v.pos0[2] / t};
+    for (int bin_range = 0; bin_range < V.nrange_grid; bin_range++)
+      if (v.d.nu_rf > V.nu_grid_min[bin_range] && v.d.nu_rf < V.nu_grid_max[bin_range])
+        if (t_arrive > V.tmin_grid && t_arrive < V.tmax_grid)
+          add_to_vpkt_grid(K, v.d.nu_rf, v.d.e_rf, st, vel_vec, bin_range, v.b, v.obs);
+  }
+}
+
+enum { VSEG_CONTINUE = 0, VSEG_ESCAPED = 1, VSEG_KILLED = 2 };
+
+// one pass of rlc_emiss_vpkt's cell loop (vpkt.cc:195-312); deviation D9 for the line loop
+DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
+  const Ctx &K = x.K;
+  const DevVpkt &V = K.V;
+  Pkt &d = v.d;
+  const double t_current = v.t_current;
+  double ldist = 0;
+  int snext = -1;
+  const double sdist = boundary_cross(x, d, &snext);
+  if (((snext != -99) && (snext < 0)) || (snext >= K.G.ngrid)) {
+    x.err(ERR_BADCELL, -1, snext);
+    return VSEG_KILLED;
+  }
+  const double tf = v.t_future;
+  const double s_cont = sdist * t_current * t_current * t_current / (tf * tf * tf);
+  Kappa kap;
+  calculate_kappa_rpkt_cont(x, d, K.C.ne_index[v.mgi], v.mgi, kap);
+  const double kap_cont = kap.total;
+  const double kap_cont_nobf = kap_cont - kap.bf;
+  const double kap_cont_noff = kap_cont - kap.ff;
+  const double kap_cont_noes = kap_cont - kap.es;
+  for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++) {
+    if (ind >= V.nspectra) break;
+    const double ex = V.exclude[ind];
+    if (ex == -2)
+      v.tau[ind] += kap_cont_nobf * s_cont;
+    else if (ex == -3)
+      v.tau[ind] += kap_cont_noff * s_cont;
+    else if (ex == -4)
+      v.tau[ind] += kap_cont_noes * s_cont;
+    else
+      v.tau[ind] += kap_cont * s_cont;
+  }
+  if (!vpkt_alive(V, v.tau)) return VSEG_KILLED;
+  const int64_t popbase = (int64_t)K.C.ne_index[v.mgi] * K.T.nlevels_total;
+  while (ldist < sdist) {
+    const int lineindex = closest_transition(K, d.nu_cmf, d.next_trans);
+    if (lineindex < 0) {
+      d.next_trans = K.T.nlines + 1;
+      break;  // D9
+    }
+    const LineTau lt = K.T.line_tau[lineindex];
+    const double nutrans = lt.nu;
+    d.next_trans = lineindex + 1;
+    if (d.nu_cmf < nutrans)
+      ldist = 0;
+    else
+      ldist = ARTIS_CLIGHT * t_current * (d.nu_cmf / nutrans - 1);
+    if (ldist > sdist) {
+      d.next_trans -= 1;
+      break;
+    }
+    lines++;
+    const double t_line = t_current + ldist / ARTIS_CLIGHT;
+    const double n_u = K.C.pops[popbase + lt.ul_upper];
+    const double n_l = K.C.pops[popbase + lt.ul_lower];
+    const double dtau = (lt.B_lu * n_l - lt.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_line;
+    bool anyex = false;
+    for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
+      if (ind < V.nspectra && V.exclude[ind] != 0) anyex = true;
+    if (!anyex) {
+      for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
+        if (ind < V.nspectra) v.tau[ind] += dtau;
+    } else {
+      const int anumber = V.anumber[K.T.line_elem[lineindex]];
+      for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
+        if (ind < V.nspectra && V.exclude[ind] != -1 && (anumber != V.exclude[ind])) v.tau[ind] += dtau;
+    }
+    if (!vpkt_alive(V, v.tau)) return VSEG_KILLED;
+  }
+  v.t_future += (sdist / ARTIS_CLIGHT_PROP);
+  d.prop_time = v.t_future;
+  move_pkt(K, d, sdist);
+  change_cell(x, d, snext);
+  const bool end_packet = (d.type == ARTIS_TYPE_ESCAPE);
+  v.mgi = cell_mgi(K, d.where);
+  if (v.mgi == K.G.npts_model) return VSEG_ESCAPED;
+  if (K.C.thick[v.mgi] == 1) return VSEG_KILLED;
+  if (++v.cells > VPKT_MAX_CELLS) {
+    x.err(ERR_STUCK, -1, 6);
+    return VSEG_KILLED;
+  }
+  return end_packet ? VSEG_ESCAPED : VSEG_CONTINUE;
+}
+
+// all (spawn, observer) work items of the spawn buffer; spawn_ctr[1] is the fetch head
+__global__ __launch_bounds__(WAVE_BLOCK) void k_vpkt(const Ctx *__restrict__ ctxp, int refill_min) {
+  const Ctx &K = *ctxp;
+  const DevVpkt &V = K.V;
+  __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
+  __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
+  block_counters_init(s_ctr, s_work);
+  LocalCounters L;
+  L.ctr = &s_ctr[0];
+  L.work = &s_work[0];
+  Tx x(K, L);
+  const uint32_t nspawn = min(V.spawn_ctr[0], V.cap);
+  const uint64_t nitems = (uint64_t)nspawn * (uint64_t)V.nobs;
+  VLane v;
+  v.tracing = false;
+  bool have = false, drained = false;
+  unsigned long long lines = 0;
+  const int64_t cap = V.cap;
+  while (true) {
+    const bool idle = !have && !drained;
+    const unsigned long long imask = __ballot(idle);
+    if (!__any(have) || __popcll(imask) >= refill_min) {
+      if (imask) {
+        const uint32_t slot = wave_reserve(&V.spawn_ctr[1], idle);
+        if (idle) {
+          if ((uint64_t)slot < nitems) {
+            v.s = slot / (uint32_t)V.nobs;
+            v.b = (int)(slot % (uint32_t)V.nobs);
+            const double *sp = V.spawn;
+            for (int k = 0; k < 3; k++) {
+              v.pos0[k] = sp[k * cap + v.s];
+              v.obs[k] = V.obs[3 * v.b + k];
+            }
+            v.t_current = sp[10 * cap + v.s];
+            v.realtype = hi32(reinterpret_cast<const uint64_t *>(sp)[12 * cap + v.s]);
+            const double t_arrive = v.t_current - (dot(v.pos0, v.obs) / ARTIS_CLIGHT_PROP);
+            v.range = (t_arrive >= V.tmin_input && t_arrive <= V.tmax_input) ? 0 : V.nrange;
+            v.tracing = false;
+            have = true;
+          } else {
+            drained = true;
+          }
+        }
+      }
+      if (!__any(have)) break;
+    }
+    if (have) {
+      if (!v.tracing) {
+        // vpkt.cc:872-888: the next frequency range this emission falls into, with the current observer vector
+        const double nu_cmf = V.spawn[6 * cap + v.s];
+        while (v.range < V.nrange) {
+          const double nu_rf = nu_cmf / doppler_pos_dir(K, v.pos0, v.obs, v.t_current);
+          if (nu_rf > V.numin_input[v.range] && nu_rf < V.numax_input[v.range]) break;
+          v.range++;
+        }
+        if (v.range < V.nrange) {
+          v.range++;
+          vpkt_trace_init(K, L, v);
+          v.tracing = true;
+        } else {
+          have = false;
+        }
+      } else {
+        const int r = vpkt_trace_segment(x, v, lines);
+        if (r != VSEG_CONTINUE) {
+          if (r == VSEG_ESCAPED) vpkt_trace_finish(K, v);
+          v.tracing = false;
+        }
+      }
+    }
+  }
+  if (lines) atomicAdd(&V.ctr[6], lines);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nspawn) atomicAdd(&V.ctr[4], (unsigned long long)nspawn);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (s_work[WK_KAPPA_EVALS]) atomicAdd(&V.ctr[5], s_work[WK_KAPPA_EVALS]);
+    if (s_work[WK_BF_ACTIVE]) atomicAdd(&V.ctr[7], s_work[WK_BF_ACTIVE]);
+  }
+  // the reference's change_cell counts virtual packets too (nesc, COUNTER_CELLCROSSINGS; boundary.cc:341-356)
+  for (int j = threadIdx.x; j < ARTIS_COUNTER_COUNT + 1; j += blockDim.x)
+    if (s_ctr[j]) atomicAdd(&K.E.counters[j], s_ctr[j]);
+}
+
+#endif

@@ -185,3 +185,149 @@ class EstimatorArrays:
             "nt_energy_deposited": s.nt_energy_deposited,
             "nesc": s.nesc,
         }
+
+
+# virtual packets (include/artis_gpu.h artis_vpkt_params / artis_vpkt_result; vpkt.cc, vpkt.h:30-47)
+VPKT_MAX_SPECTRA = 8
+VPKT_MRANGE = 4
+VPKT_MRANGE_GRID = 5
+DAY = 86400.0
+CLIGHT = 2.99792458e10
+
+
+class VpktParams(C.Structure):
+    _fields_ = [
+        ("nobs", C.c_int32),
+        ("nz_obs", C.POINTER(C.c_double)),
+        ("phi_obs", C.POINTER(C.c_double)),
+        ("nspectra", C.c_int32),
+        ("exclude", C.POINTER(C.c_double)),
+        ("tmin_vspec", C.c_double),
+        ("tmax_vspec", C.c_double),
+        ("numin_vspec", C.c_double),
+        ("numax_vspec", C.c_double),
+        ("vmtbins", C.c_int32),
+        ("vmnubins", C.c_int32),
+        ("tmin_vspec_input", C.c_double),
+        ("tmax_vspec_input", C.c_double),
+        ("nrange", C.c_int32),
+        ("numin_vspec_input", C.c_double * VPKT_MRANGE),
+        ("numax_vspec_input", C.c_double * VPKT_MRANGE),
+        ("tau_max_vpkt", C.c_double),
+        ("vgrid_flag", C.c_int32),
+        ("tmin_grid", C.c_double),
+        ("tmax_grid", C.c_double),
+        ("nrange_grid", C.c_int32),
+        ("nu_grid_min", C.c_double * VPKT_MRANGE_GRID),
+        ("nu_grid_max", C.c_double * VPKT_MRANGE_GRID),
+        ("ny_vgrid", C.c_int32),
+        ("nz_vgrid", C.c_int32),
+        ("nprocs", C.c_int32),
+        ("spawn_capacity", C.c_int64),
+    ]
+
+
+class VpktResult(C.Structure):
+    _fields_ = [
+        ("vstokes_i", C.POINTER(C.c_double)),
+        ("vstokes_q", C.POINTER(C.c_double)),
+        ("vstokes_u", C.POINTER(C.c_double)),
+        ("vgrid_i", C.POINTER(C.c_double)),
+        ("vgrid_q", C.POINTER(C.c_double)),
+        ("vgrid_u", C.POINTER(C.c_double)),
+        ("nvpkt", C.c_int64),
+        ("nvpkt_esc1", C.c_int64),
+        ("nvpkt_esc2", C.c_int64),
+        ("nvpkt_esc3", C.c_int64),
+    ]
+
+
+class VpktConfig:
+    """vpkt.txt parameters (read_parameterfile_vpkt, vpkt.cc:667-835) with the vpkt.h compile-time binning as
+    defaults; `struct` is the artis_vpkt_params view (the numpy arrays it points to are kept alive here)."""
+
+    def __init__(self, nz_obs=(0.5,), phi_obs_deg=(0.0,), exclude=(0.0,), tmin_days=10.0, tmax_days=30.0,
+                 lambda_min=3500.0, lambda_max=10000.0, vmtbins=30, vmnubins=2500, tmin_input_days=None,
+                 tmax_input_days=None, ranges_angstrom=None, tau_max=10.0, vgrid=False, grid_tmin_days=None,
+                 grid_tmax_days=None, grid_ranges_angstrom=((3500.0, 10000.0),), ny_vgrid=50, nz_vgrid=50, nprocs=1,
+                 spawn_capacity=0):
+        nz = np.array(nz_obs, dtype=np.float64)
+        nz[nz == 1] = 0.9999  # vpkt.cc:683-687
+        nz[nz == -1] = -0.9999
+        self.nz_obs = np.ascontiguousarray(nz)
+        self.phi_obs = np.ascontiguousarray(np.array(phi_obs_deg, dtype=np.float64) * np.pi / 180.0)
+        self.exclude = np.ascontiguousarray(np.array(exclude, dtype=np.float64))
+        assert len(self.nz_obs) == len(self.phi_obs) and len(self.exclude) <= VPKT_MAX_SPECTRA
+        s = VpktParams()
+        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+        s.nobs = len(self.nz_obs)
+        s.nz_obs, s.phi_obs = dp(self.nz_obs), dp(self.phi_obs)
+        s.nspectra = len(self.exclude)
+        s.exclude = dp(self.exclude)
+        s.tmin_vspec, s.tmax_vspec = tmin_days * DAY, tmax_days * DAY
+        s.numin_vspec = CLIGHT / lambda_max * 1e8  # vpkt.h:36-37
+        s.numax_vspec = CLIGHT / lambda_min * 1e8
+        s.vmtbins, s.vmnubins = vmtbins, vmnubins
+        s.tmin_vspec_input = (tmin_input_days if tmin_input_days is not None else tmin_days) * DAY
+        s.tmax_vspec_input = (tmax_input_days if tmax_input_days is not None else tmax_days) * DAY
+        if ranges_angstrom is None:
+            s.nrange = 1
+            s.numin_vspec_input[0], s.numax_vspec_input[0] = s.numin_vspec, s.numax_vspec
+        else:
+            s.nrange = len(ranges_angstrom)
+            for i, (lmin, lmax) in enumerate(ranges_angstrom):  # vpkt.cc:767-768
+                s.numin_vspec_input[i] = CLIGHT / (lmax * 1e-8)
+                s.numax_vspec_input[i] = CLIGHT / (lmin * 1e-8)
+        s.tau_max_vpkt = tau_max
+        s.vgrid_flag = 1 if vgrid else 0
+        s.tmin_grid = (grid_tmin_days if grid_tmin_days is not None else tmin_days) * DAY
+        s.tmax_grid = (grid_tmax_days if grid_tmax_days is not None else tmax_days) * DAY
+        s.nrange_grid = len(grid_ranges_angstrom) if vgrid else 0
+        for i, (lmin, lmax) in enumerate(grid_ranges_angstrom if vgrid else ()):  # vpkt.cc:826-827
+            s.nu_grid_max[i] = CLIGHT / (lmin * 1e-8)
+            s.nu_grid_min[i] = CLIGHT / (lmax * 1e-8)
+        s.ny_vgrid, s.nz_vgrid = ny_vgrid, nz_vgrid
+        s.nprocs = nprocs
+        s.spawn_capacity = spawn_capacity
+        self.struct = s
+
+    @property
+    def nobs(self):
+        return self.struct.nobs
+
+    @property
+    def nspectra(self):
+        return self.struct.nspectra
+
+    def bins(self):
+        """init_vspecpol (vpkt.cc:425-436): float32 lower_time/delta_t [vmtbins], lower_freq/delta_freq [vmnubins]."""
+        s = self.struct
+        dlogt = (np.log(s.tmax_vspec) - np.log(s.tmin_vspec)) / s.vmtbins
+        dlognu = (np.log(s.numax_vspec) - np.log(s.numin_vspec)) / s.vmnubins
+        n = np.arange(s.vmtbins)
+        lt = np.exp(np.log(s.tmin_vspec) + n * dlogt).astype(np.float32)
+        dt = (np.exp(np.log(s.tmin_vspec) + (n + 1) * dlogt) - lt.astype(np.float64)).astype(np.float32)
+        m = np.arange(s.vmnubins)
+        lf = np.exp(np.log(s.numin_vspec) + m * dlognu).astype(np.float32)
+        df = (np.exp(np.log(s.numin_vspec) + (m + 1) * dlognu) - lf.astype(np.float64)).astype(np.float32)
+        return lt, dt, lf, df
+
+
+class VpktArrays:
+    """Host storage for one artis_vpkt_result: vstokes [3][vmtbins][nobs*nspectra][vmnubins], vgrid
+    [3][ny][nz][nrange_grid][nobs]."""
+
+    def __init__(self, cfg):
+        s = cfg.struct
+        self.vstokes = np.zeros((3, s.vmtbins, s.nobs * s.nspectra, s.vmnubins))
+        ng = max(s.nrange_grid, 1)
+        self.vgrid = np.zeros((3, s.ny_vgrid, s.nz_vgrid, ng, s.nobs))
+        self.struct = VpktResult()
+        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+        r = self.struct
+        r.vstokes_i, r.vstokes_q, r.vstokes_u = dp(self.vstokes[0]), dp(self.vstokes[1]), dp(self.vstokes[2])
+        r.vgrid_i, r.vgrid_q, r.vgrid_u = dp(self.vgrid[0]), dp(self.vgrid[1]), dp(self.vgrid[2])
+
+    def counters(self):
+        r = self.struct
+        return {"nvpkt": r.nvpkt, "nvpkt_esc1": r.nvpkt_esc1, "nvpkt_esc2": r.nvpkt_esc2, "nvpkt_esc3": r.nvpkt_esc3}

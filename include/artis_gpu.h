@@ -296,6 +296,54 @@ typedef struct artis_gamma_spectra {
   const double *line_probability;   /* [sum nlines] photons per decay */
 } artis_gamma_spectra;
 
+/* ------------------------------------------------------------------------------------------------------------ */
+/* Virtual packets (VPKT_ON): vpkt.cc.  Every r-packet emission -- electron scattering (rpkt.cc:358-363),        */
+/* macro-atom bb / fb deactivation (macroatom.cc:292-295, 376-379), k-packet ff / fb cooling (kpkt.cc:631-634,  */
+/* 691-694) -- spawns one virtual packet per observer direction and frequency range (vpkt_call_estimators,     */
+/* vpkt.cc:837-896), traced to the grid edge through line and continuum opacity without interacting            */
+/* (rlc_emiss_vpkt, vpkt.cc:76-368) and binned with weight p_n e^-tau into the polarised spectra vstokes_i/q/u  */
+/* (add_to_vspecpol, vpkt.cc:388-406) and, optionally, the velocity-grid map (add_to_vpkt_grid, vpkt.cc:581-627).*/
+/* The parameters are those of vpkt.txt (read_parameterfile_vpkt, vpkt.cc:667-835) plus the compile-time       */
+/* binning constants of vpkt.h:30-47, given here at run time.                                                  */
+/* ------------------------------------------------------------------------------------------------------------ */
+#define ARTIS_VPKT_MAX_SPECTRA 8   /* Nspectra (opacity choices per observer) */
+#define ARTIS_VPKT_MRANGE 4        /* frequency ranges (MRANGE = 1 in vpkt.h:47) */
+#define ARTIS_VPKT_MRANGE_GRID 5   /* MRANGE_GRID (vpkt.h:30) */
+
+typedef struct artis_vpkt_params {
+  int32_t nobs;                    /* Nobs */
+  const double *nz_obs;            /* [nobs] cos(theta), after the +-1 -> +-0.9999 rewrite (vpkt.cc:680-687) */
+  const double *phi_obs;           /* [nobs] radians */
+  int32_t nspectra;                /* Nspectra <= ARTIS_VPKT_MAX_SPECTRA */
+  const double *exclude;           /* [nspectra] 0: all opacity; -1: no lines; -2: no bf; -3: no ff; -4: no es;
+                                      Z > 0: without the lines of element Z (vpkt.cc:209-218, 272-277) */
+  double tmin_vspec, tmax_vspec;   /* vpkt.h:42-43 (10 d, 30 d) */
+  double numin_vspec, numax_vspec; /* vpkt.h:36-37 */
+  int32_t vmtbins, vmnubins;       /* VMTBINS (30), VMNUBINS (2500) */
+  double tmin_vspec_input, tmax_vspec_input;  /* vpkt.txt time window (within [tmin_vspec, tmax_vspec]) */
+  int32_t nrange;                  /* Nrange <= ARTIS_VPKT_MRANGE */
+  double numin_vspec_input[ARTIS_VPKT_MRANGE], numax_vspec_input[ARTIS_VPKT_MRANGE];
+  double tau_max_vpkt;
+  int32_t vgrid_flag;              /* 1: velocity-grid map */
+  double tmin_grid, tmax_grid;
+  int32_t nrange_grid;             /* <= ARTIS_VPKT_MRANGE_GRID */
+  double nu_grid_min[ARTIS_VPKT_MRANGE_GRID], nu_grid_max[ARTIS_VPKT_MRANGE_GRID];
+  int32_t ny_vgrid, nz_vgrid;      /* NY_VGRID, NZ_VGRID (50, 50; vpkt.h:31-32) */
+  int32_t nprocs;                  /* globals::nprocs of the add_to_vspecpol normalisation (vpkt.cc:398-399) */
+  int64_t spawn_capacity;          /* engine only: virtual-packet spawn records held in HBM per event round;
+                                      0 = default (16 per packet, at least 2^20) */
+} artis_vpkt_params;
+
+/* Accumulators of the virtual packets, un-normalised beyond what add_to_vspecpol / add_to_vpkt_grid apply.
+ * vstokes_* [vmtbins][nobs * nspectra][vmnubins] (vstokes_i[nt][ind_comb].flux[nnu], vpkt.cc:21-23, 391);
+ * vgrid_* [ny_vgrid][nz_vgrid][nrange_grid][nobs] (vgrid_i[n][m].flux[range][obs], vpkt.cc:53-55), may be NULL
+ * when vgrid_flag == 0; the counters are nvpkt / nvpkt_esc1-3 (vpkt.cc:69-74). */
+typedef struct artis_vpkt_result {
+  double *vstokes_i, *vstokes_q, *vstokes_u;
+  double *vgrid_i, *vgrid_q, *vgrid_u;
+  int64_t nvpkt, nvpkt_esc1, nvpkt_esc2, nvpkt_esc3;
+} artis_vpkt_result;
+
 enum artis_status {
   ARTIS_OK = 0,
   ARTIS_ERR_NOT_INITIALISED = -1,
@@ -356,12 +404,28 @@ int artis_gpu_last_work_counts(int64_t out[ARTIS_WORK_COUNT]);
  * spec_flux[ntstep * nnubins] (timestep-major), lc_lum[ntstep], lc_lumcmf[ntstep]; nprocs is the rank count
  * the reference divides by (globals::nprocs). */
 int artis_gpu_spectrum(int nnubins, int nprocs, double *spec_flux, double *lc_lum, double *lc_lumcmf);
+
+/* --- virtual packets (VPKT_ON) ------------------------------------------------------------------------------ */
+/* Switch virtual packets on for all following updates (replaces read_parameterfile_vpkt + init_vspecpol +
+ * init_vpkt_grid, vpkt.cc:408-443, 547-578, 667-835): allocates and zeroes the device accumulators.  exclude[] > 0
+ * refers to the atomic numbers elem_anumber of the tables given to artis_gpu_init.  Emission sites then also set
+ * last_cross = NONE before an electron scattering (rpkt.cc:361), as the reference does under VPKT_ON. */
+int artis_gpu_vpkt_init(const artis_vpkt_params *params);
+int artis_gpu_vpkt_zero(void);                         /* zero the device accumulators and counters */
+/* ADD the device accumulators into *out (arrays sized as documented at artis_vpkt_result); the
+ * per-timestep counters nvpkt* are zeroed afterwards when reset_counters != 0 (sn3d.cc:621-624). */
+int artis_gpu_vpkt_download(artis_vpkt_result *out, int reset_counters);
+/* device time (ms) of the virtual-packet kernels of the last update, and the number of spawn records and
+ * traced (spawn, observer, range) virtual packets it processed */
+int artis_gpu_vpkt_last_stats(double *ms, int64_t *spawns, int64_t *traces);
+
 int64_t artis_gpu_last_rounds(void);  /* event-queue rounds of the last update (0: megakernel path) */
 /* device time (ms, HIP events around every launch) and launch count of the last update per kernel class:
  * [0] r-packet, [1] macro-atom (incl. cell binning), [2] k-packet, [3] classify */
 int artis_gpu_last_kernel_times(double ms[4], int64_t launches[4]);
 const char *artis_gpu_last_error(void);
-#define ARTIS_GPU_ABI_VERSION 2  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields) */
+#define ARTIS_GPU_ABI_VERSION 3  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
+                                    3: virtual packets (artis_vpkt_params / artis_vpkt_result) */
 int artis_gpu_abi_version(void);
 
 #ifdef __cplusplus

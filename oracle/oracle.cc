@@ -32,6 +32,10 @@
 //       packet (rpkt.cc:583, 1166), a per-thread artefact.  Here those terms are zero.
 //   D8 Gamma packets need do_r_lc (do_comp_est = false, sn3d.cc:539): the Compton emissivity estimators
 //       (emissivities.cc:14-137) are not restated; every reference test configuration sets do_r_lc.
+//   D9 Virtual packets (vpkt.cc:76-406): when no redder line is left, rlc_emiss_vpkt's line loop ends and the
+//       virtual packet moves on to the cell boundary (the reference keeps ldist = 0 < sdist and spins forever);
+//       a spectrum bin index that rounds up to the array end is skipped (the reference writes past the array).
+//       The observer directions and bin edges are computed once with the host libm (vpkt.cc:863-865, 425-436).
 #include <omp.h>
 
 #include <algorithm>
@@ -50,6 +54,18 @@
 
 namespace {
 
+// vpkt.cc globals under VPKT_ON: vpkt.txt parameters, observer directions, bin edges, accumulators
+struct VpktCfg {
+  artis_vpkt_params p;
+  std::vector<double> exclude;                // [nspectra]
+  std::vector<double> obs;                    // [nobs * 3] (vpkt.cc:863-865)
+  std::vector<float> lower_time, delta_t;     // [vmtbins]  vspecpol.lower_time / delta_t are floats (vpkt.cc:15-19)
+  std::vector<float> lower_freq, delta_freq;  // [vmnubins] lower_freq_vspec / delta_freq_vspec (vpkt.cc:25-26)
+  double dlogt = 0., dlognu = 0.;
+  std::vector<int32_t> anumber;               // [nelements]
+  artis_vpkt_result *out = nullptr;
+};
+
 struct Ctx {
   const artis_atomic_tables *at;
   const artis_geometry *g;
@@ -57,6 +73,7 @@ struct Ctx {
   artis_run_params rp;
   double T_step_log;
   const artis_gamma_spectra *gs;  // may be NULL: no pellets / gamma packets in the ensemble
+  const VpktCfg *vp = nullptr;    // NULL: VPKT_ON undefined
 };
 
 struct Est {
@@ -1044,6 +1061,245 @@ void closest_transition_empty(const Ctx &c, artis_packet *p) {
   p->next_trans = matchindex;
 }
 
+// ------------------------------------------------------------------------------------------ virtual packets
+// vpkt.cc:374-385: 0 once every spectrum's optical depth exceeds tau_max_vpkt
+int check_tau(const VpktCfg &v, const double *tau) {
+  int count = 0;
+  for (int i = 0; i < v.p.nspectra; i++)
+    if (tau[i] > v.p.tau_max_vpkt) count += 1;
+  return (count == v.p.nspectra) ? 0 : 1;
+}
+// vpkt.cc:388-406 (deviation D9: a bin index rounded up to the array end is skipped)
+void add_to_vspecpol(const VpktCfg &v, const artis_packet *d, int bin, int ind, double t_arrive) {
+  const int ind_comb = v.p.nspectra * bin + ind;
+  if (t_arrive > v.p.tmin_vspec && t_arrive < v.p.tmax_vspec) {
+    const int nt = (int)((log(t_arrive) - log(v.p.tmin_vspec)) / v.dlogt);
+    if (d->nu_rf > v.p.numin_vspec && d->nu_rf < v.p.numax_vspec) {
+      const int nnu = (int)((log(d->nu_rf) - log(v.p.numin_vspec)) / v.dlognu);
+      if (nt >= v.p.vmtbins || nnu >= v.p.vmnubins) return;
+      const double pktcontrib = d->e_rf / v.delta_t[nt] / v.delta_freq[nnu] / 4.e12 / ARTIS_PI / ARTIS_PARSEC /
+                                ARTIS_PARSEC / v.p.nprocs * 4 * ARTIS_PI;
+      const size_t idx = ((size_t)nt * v.p.nobs * v.p.nspectra + ind_comb) * v.p.vmnubins + nnu;
+      safeadd(&v.out->vstokes_i[idx], d->stokes[0] * pktcontrib);
+      safeadd(&v.out->vstokes_q[idx], d->stokes[1] * pktcontrib);
+      safeadd(&v.out->vstokes_u[idx], d->stokes[2] * pktcontrib);
+    }
+  }
+}
+// vpkt.cc:581-627
+void add_to_vpkt_grid(const Ctx &c, const VpktCfg &v, const artis_packet *d, const double vel[3], int bin_range,
+                      int bin, const double obs[3]) {
+  double vref1, vref2;
+  const double nx = obs[0], ny = obs[1], nz = obs[2];
+  if (nx == 1) {
+    vref1 = vel[1];
+    vref2 = vel[2];
+  } else if (nx == -1) {
+    vref1 = -vel[1];
+    vref2 = -vel[2];
+  } else {
+    vref1 = -ny * vel[0] + (nx + nz * nz / (1 + nx)) * vel[1] - ny * nz * (1 - nx) / sqrt(1 - nx * nx) * vel[2];
+    vref2 = -nz * vel[0] - ny * nz * (1 - nx) / sqrt(1 - nx * nx) * vel[1] + (nx + ny * ny / (1 + nx)) * vel[2];
+  }
+  const double vmax = c.g->vmax;
+  if (fabs(vref1) >= vmax || fabs(vref2) >= vmax) return;
+  const double ybin = 2 * vmax / v.p.ny_vgrid;
+  const double zbin = 2 * vmax / v.p.nz_vgrid;
+  const int nt = (int)((vmax - vref1) / ybin);
+  const int mt = (int)((vmax - vref2) / zbin);
+  if (d->nu_rf > v.p.nu_grid_min[bin_range] && d->nu_rf < v.p.nu_grid_max[bin_range]) {
+    const size_t idx = (((size_t)nt * v.p.nz_vgrid + mt) * v.p.nrange_grid + bin_range) * v.p.nobs + bin;
+    safeadd(&v.out->vgrid_i[idx], d->stokes[0] * d->e_rf);
+    safeadd(&v.out->vgrid_q[idx], d->stokes[1] * d->e_rf);
+    safeadd(&v.out->vgrid_u[idx], d->stokes[2] * d->e_rf);
+  }
+}
+inline void vcount(int64_t *ctr) {
+#pragma omp atomic update
+  *ctr += 1;
+}
+// vpkt.cc:76-368.  The dummy's level populations and continuum opacity come from a cellhistory of its own
+// (vtc), as the reference's get_levelpop / calculate_kappa_rpkt_cont compute them for a cell other than the
+// thread's cached one.  Deviation D9: when no redder line is left (closest_transition < 0) the line loop ends
+// and the dummy moves on to the cell boundary (the reference keeps ldist = 0 < sdist and never leaves the loop).
+void rlc_emiss_vpkt(const Ctx &c, ThreadCache &vtc, Est &E, const artis_packet *pkt, double t_current, int bin,
+                    double obs[3], int realtype) {
+  const VpktCfg &v = *c.vp;
+  const artis_atomic_tables &a = *c.at;
+  artis_packet dummy = *pkt;
+  double tau[ARTIS_VPKT_MAX_SPECTRA];
+  for (int ind = 0; ind < v.p.nspectra; ind++) tau[ind] = 0;
+  dummy.dir[0] = obs[0];
+  dummy.dir[1] = obs[1];
+  dummy.dir[2] = obs[2];
+  vcount(&v.out->nvpkt);
+  double vel_vec[3];
+  get_velocity(pkt->pos, vel_vec, t_current);
+  dummy.nu_rf = dummy.nu_cmf / doppler_nucmf_on_nurf(c, dummy.dir, vel_vec);
+  dummy.e_rf = dummy.e_cmf * dummy.nu_rf / dummy.nu_cmf;
+  double Qi = dummy.stokes[1];
+  double Ui = dummy.stokes[2];
+  double I = 0., Q = 0., U = 0., pn = 0.;
+  if (realtype == 1) {
+    double old_dir_cmf[3], obs_cmf[3], ref1[3], ref2[3];
+    frame_transform(pkt->dir, &Qi, &Ui, vel_vec, old_dir_cmf);
+    angle_ab(dummy.dir, vel_vec, obs_cmf);
+    meridian(old_dir_cmf, ref1, ref2);
+    const double i1 = rot_angle(old_dir_cmf, obs_cmf, ref1, ref2);
+    const double cos2i1 = cos(2 * i1);
+    const double sin2i1 = sin(2 * i1);
+    const double Qold = Qi * cos2i1 - Ui * sin2i1;
+    const double Uold = Qi * sin2i1 + Ui * cos2i1;
+    const double mu = dot(old_dir_cmf, obs_cmf);
+    pn = 3. / (16. * ARTIS_PI) * (1 + pow(mu, 2.) + (pow(mu, 2.) - 1) * Qold);
+    const double Inew = 0.75 * ((mu * mu + 1.0) + Qold * (mu * mu - 1.0));
+    double Qnew = 0.75 * ((mu * mu - 1.0) + Qold * (mu * mu + 1.0));
+    double Unew = 1.5 * mu * Uold;
+    Qnew = Qnew / Inew;
+    Unew = Unew / Inew;
+    I = Inew / Inew;
+    meridian(obs_cmf, ref1, ref2);
+    const double i2 = ARTIS_PI + rot_angle(obs_cmf, old_dir_cmf, ref1, ref2);
+    const double cos2i2 = cos(2 * i2);
+    const double sin2i2 = sin(2 * i2);
+    Q = Qnew * cos2i2 + Unew * sin2i2;
+    U = -Qnew * sin2i2 + Unew * cos2i2;
+    const double vel_rev[3] = {-vel_vec[0], -vel_vec[1], -vel_vec[2]};
+    frame_transform(obs_cmf, &Q, &U, vel_rev, obs);  // overwrites the caller's obs, as vpkt.cc:179
+  }
+  if (realtype == 2 || realtype == 3) {
+    I = 1;
+    Q = 0;
+    U = 0;
+    pn = 1 / (4 * ARTIS_PI);
+  }
+  int mgi = cell_mgi(c, dummy.where);
+  bool end_packet = false;
+  double t_future = t_current;
+  while (!end_packet) {
+    double ldist = 0;
+    int snext;
+    const double sdist = boundary_cross(c, E, &dummy, &snext);
+    const double s_cont = sdist * t_current * t_current * t_current / (t_future * t_future * t_future);
+    cellhistory_reset(c, vtc, mgi);
+    calculate_kappa_rpkt_cont(c, vtc, &dummy);
+    const double kap_cont = vtc.kap_total;
+    const double kap_cont_nobf = kap_cont - vtc.kap_bf;
+    const double kap_cont_noff = kap_cont - vtc.kap_ff;
+    const double kap_cont_noes = kap_cont - vtc.kap_es;
+    for (int ind = 0; ind < v.p.nspectra; ind++) {
+      if (v.exclude[ind] == -2)
+        tau[ind] += kap_cont_nobf * s_cont;
+      else if (v.exclude[ind] == -3)
+        tau[ind] += kap_cont_noff * s_cont;
+      else if (v.exclude[ind] == -4)
+        tau[ind] += kap_cont_noes * s_cont;
+      else
+        tau[ind] += kap_cont * s_cont;
+    }
+    if (check_tau(v, tau) == 0) return;
+    while (ldist < sdist) {
+      const int lineindex = closest_transition(c, dummy.nu_cmf, dummy.next_trans);
+      if (lineindex >= 0) {
+        const double nutrans = a.line_nu[lineindex];
+        const int element = a.line_elementindex[lineindex];
+        const int ion = a.line_ionindex[lineindex];
+        const int upper = a.line_upperlevelindex[lineindex];
+        const int lower = a.line_lowerlevelindex[lineindex];
+        const double A_ul = a.line_einstein_A[lineindex];
+        const int anumber = v.anumber[element];
+        dummy.next_trans = lineindex + 1;
+        if (dummy.nu_cmf < nutrans)
+          ldist = 0;
+        else
+          ldist = ARTIS_CLIGHT * t_current * (dummy.nu_cmf / nutrans - 1);
+        if (ldist > sdist) {
+          dummy.next_trans -= 1;
+          break;
+        }
+        const double t_line = t_current + ldist / ARTIS_CLIGHT;
+        const double B_ul = ARTIS_CLIGHTSQUAREDOVERTWOH / pow(nutrans, 3) * A_ul;
+        const double B_lu = stat_weight(c, element, ion, upper) / stat_weight(c, element, ion, lower) * B_ul;
+        const double n_u = get_levelpop(vtc, c, element, ion, upper);
+        const double n_l = get_levelpop(vtc, c, element, ion, lower);
+        for (int ind = 0; ind < v.p.nspectra; ind++)
+          if (v.exclude[ind] != -1 && (anumber != v.exclude[ind]))
+            tau[ind] += (B_lu * n_l - B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_line;
+        if (check_tau(v, tau) == 0) return;
+      } else {
+        dummy.next_trans = a.nlines + 1;
+        break;  // D9
+      }
+    }
+    t_future += (sdist / ARTIS_CLIGHT_PROP);
+    dummy.prop_time = t_future;
+    move_pkt(c, &dummy, sdist);
+    change_cell(E, &dummy, snext);
+    end_packet = (dummy.type == ARTIS_TYPE_ESCAPE);
+    mgi = cell_mgi(c, dummy.where);
+    if (mgi == npts_model(c)) break;
+    if (c.cs->thick[mgi] == 1) return;
+  }
+  if (realtype == 1)
+    vcount(&v.out->nvpkt_esc1);
+  else if (realtype == 2)
+    vcount(&v.out->nvpkt_esc2);
+  else if (realtype == 3)
+    vcount(&v.out->nvpkt_esc3);
+  double t_arrive = 0.;
+  for (int ind = 0; ind < v.p.nspectra; ind++) {
+    const double prob = pn * exp(-tau[ind]);
+    dummy.stokes[0] = I * prob;
+    dummy.stokes[1] = Q * prob;
+    dummy.stokes[2] = U * prob;
+    t_arrive = t_current - (dot(pkt->pos, dummy.dir) / ARTIS_CLIGHT_PROP);
+    add_to_vspecpol(v, &dummy, bin, ind, t_arrive);
+  }
+  if (v.p.vgrid_flag == 1) {
+    const double prob = pn * exp(-tau[0]);
+    dummy.stokes[0] = I * prob;
+    dummy.stokes[1] = Q * prob;
+    dummy.stokes[2] = U * prob;
+    for (int bin_range = 0; bin_range < v.p.nrange_grid; bin_range++)
+      if (dummy.nu_rf > v.p.nu_grid_min[bin_range] && dummy.nu_rf < v.p.nu_grid_max[bin_range])
+        if (t_arrive > v.p.tmin_grid && t_arrive < v.p.tmax_grid)
+          add_to_vpkt_grid(c, v, &dummy, vel_vec, bin_range, bin, obs);
+  }
+}
+// vpkt.cc:837-896.  The next_trans fix-up of vpkt.cc:853-858 only ever writes 0 over 0 and is omitted; the final
+// calculate_kappa_rpkt_cont of the real packet restores per-thread state that deviation D2 does not keep.
+void vpkt_call_estimators(const Ctx &c, Est &E, const artis_packet *p, double t_current, int realtype) {
+  const VpktCfg &v = *c.vp;
+  double vel_vec[3];
+  get_velocity(p->pos, vel_vec, t_current);
+  const int mgi = cell_mgi(c, p->where);
+  if (mgi == npts_model(c) || c.cs->thick[mgi] != 0) return;
+  thread_local ThreadCache vtc;
+  if (vtc.pops.size() != (size_t)c.at->nlevels_total || vtc.kappa_bf_sum.size() != (size_t)c.at->nbfcontinua) {
+    vtc = ThreadCache();
+    vtc.pops.assign(c.at->nlevels_total, 0.);
+    vtc.departureratios.assign(c.at->nbfcontinua, -1.);
+    vtc.processrates.assign((size_t)c.at->nlevels_total * 9, -99.);
+    vtc.corrphotoioncoeff.assign(1, -99.);
+    vtc.cooling_contrib.assign(c.at->ncoolingterms, -99.);
+    vtc.kappa_bf_sum.assign(c.at->nbfcontinua, 0.);
+    vtc.groundcont_gamma_contr.assign(c.at->nbfcontinua_ground, 0.);
+  }
+  vtc.cellnumber = -99;  // the cell state may have changed since the last call
+  for (int bin = 0; bin < v.p.nobs; bin++) {
+    double obs[3] = {v.obs[3 * bin], v.obs[3 * bin + 1], v.obs[3 * bin + 2]};
+    const double t_arrive = t_current - (dot(p->pos, obs) / ARTIS_CLIGHT_PROP);
+    if (t_arrive >= v.p.tmin_vspec_input && t_arrive <= v.p.tmax_vspec_input) {
+      for (int i = 0; i < v.p.nrange; i++) {
+        if (p->nu_cmf / doppler_nucmf_on_nurf(c, obs, vel_vec) > v.p.numin_vspec_input[i] &&
+            p->nu_cmf / doppler_nucmf_on_nurf(c, obs, vel_vec) < v.p.numax_vspec_input[i]) {
+          rlc_emiss_vpkt(c, vtc, E, p, t_current, bin, obs, realtype);
+        }
+      }
+    }
+  }
+}
+
 // rpkt.cc:67-328
 double get_event(const Ctx &c, ThreadCache &tc, int mgi, artis_packet *p, int *rpkt_eventtype, double tau_rnd,
                  double abort_dist) {
@@ -1186,6 +1442,10 @@ void rpkt_event_continuum(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng,
     p->last_event = 12;
     counter_inc(E, CTR_ESCOUNTER);
     tc.work[WK_ES_SCAT]++;
+    if (c.vp) {  // rpkt.cc:358-363
+      p->last_cross = ARTIS_NONE;
+      vpkt_call_estimators(c, E, p, p->prop_time, 1);
+    }
     escat_rpkt(c, rng, p);
     vec_copy(p->em_pos, p->pos);
     p->em_time = (int)p->prop_time;
@@ -1528,6 +1788,7 @@ void do_macroatom(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
         vec_copy(p->em_pos, p->pos);
         p->em_time = (int)p->prop_time;
         p->nscatterings = 0;
+        if (c.vp) vpkt_call_estimators(c, E, p, p->prop_time, 3);  // macroatom.cc:292-295
         end_packet = true;
         break;
       }
@@ -1593,6 +1854,7 @@ void do_macroatom(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
         vec_copy(p->em_pos, p->pos);
         p->em_time = (int)p->prop_time;
         p->nscatterings = 0;
+        if (c.vp) vpkt_call_estimators(c, E, p, p->prop_time, 3);  // macroatom.cc:376-379
         end_packet = true;
         break;
       }
@@ -1829,6 +2091,7 @@ void do_kpkt(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_packet
       vec_copy(p->em_pos, p->pos);
       p->em_time = (int)p->prop_time;
       p->nscatterings = 0;
+      if (c.vp) vpkt_call_estimators(c, E, p, t_current, 2);  // kpkt.cc:631-634
     } else if (ctype == ARTIS_COOLINGTYPE_FB) {
       const int el = a.coolinglist_element[icool];
       const int lowerion = a.coolinglist_ion[icool];
@@ -1845,6 +2108,7 @@ void do_kpkt(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_packet
       vec_copy(p->em_pos, p->pos);
       p->em_time = (int)p->prop_time;
       p->nscatterings = 0;
+      if (c.vp) vpkt_call_estimators(c, E, p, t_current, 2);  // kpkt.cc:691-694
     } else if (ctype == ARTIS_COOLINGTYPE_COLLEXC) {
       const float nne = c.cs->nne[mgi];
       const double contrib_low = (icool > ilow) ? tc.cooling_contrib[icool - 1] : oldcoolingsum;
@@ -2401,6 +2665,50 @@ int do_packet(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_packe
   }
 }
 
+// read_parameterfile_vpkt / init_vspecpol (vpkt.cc:408-443, 667-835): observer unit vectors (vpkt.cc:863-865)
+// and the float bin edges, with the host libm, as the engine computes them
+int vpkt_config(const artis_vpkt_params *vp, const int32_t *anumber, int nelements, VpktCfg &v) {  // NOLINT
+  if (!vp || vp->nobs <= 0 || vp->nspectra <= 0 || vp->nspectra > ARTIS_VPKT_MAX_SPECTRA || vp->nrange < 0 ||
+      vp->nrange > ARTIS_VPKT_MRANGE || vp->vmtbins <= 0 || vp->vmnubins <= 0 || !vp->nz_obs || !vp->phi_obs ||
+      !vp->exclude || vp->nprocs <= 0)
+    return ARTIS_ERR_BAD_ARGUMENT;
+  if (vp->vgrid_flag == 1 && (vp->nrange_grid < 0 || vp->nrange_grid > ARTIS_VPKT_MRANGE_GRID || vp->ny_vgrid <= 0 ||
+                              vp->nz_vgrid <= 0))
+    return ARTIS_ERR_BAD_ARGUMENT;
+  v.p = *vp;
+  v.exclude.assign(vp->exclude, vp->exclude + vp->nspectra);
+  v.obs.resize(3 * vp->nobs);
+  for (int b = 0; b < vp->nobs; b++) {
+    const double nz = vp->nz_obs[b], phi = vp->phi_obs[b];
+    v.obs[3 * b] = sqrt(1 - nz * nz) * cos(phi);
+    v.obs[3 * b + 1] = sqrt(1 - nz * nz) * sin(phi);
+    v.obs[3 * b + 2] = nz;
+  }
+  v.dlogt = (log(vp->tmax_vspec) - log(vp->tmin_vspec)) / vp->vmtbins;
+  v.dlognu = (log(vp->numax_vspec) - log(vp->numin_vspec)) / vp->vmnubins;
+  v.lower_time.resize(vp->vmtbins);
+  v.delta_t.resize(vp->vmtbins);
+  for (int n = 0; n < vp->vmtbins; n++) {
+    v.lower_time[n] = (float)exp(log(vp->tmin_vspec) + (n * (v.dlogt)));
+    v.delta_t[n] = (float)(exp(log(vp->tmin_vspec) + ((n + 1) * (v.dlogt))) - v.lower_time[n]);
+  }
+  v.lower_freq.resize(vp->vmnubins);
+  v.delta_freq.resize(vp->vmnubins);
+  for (int m = 0; m < vp->vmnubins; m++) {
+    v.lower_freq[m] = (float)exp(log(vp->numin_vspec) + (m * (v.dlognu)));
+    v.delta_freq[m] = (float)(exp(log(vp->numin_vspec) + ((m + 1) * (v.dlognu))) - v.lower_freq[m]);
+  }
+  v.anumber.assign(nelements, 0);
+  if (anumber)
+    for (int e = 0; e < nelements; e++) v.anumber[e] = anumber[e];
+  return 0;
+}
+
+int update_packets_impl(const artis_atomic_tables *at, const artis_geometry *geom, const artis_cell_state *cs,
+                        const artis_run_params *rp, const artis_gamma_spectra *gs, const VpktCfg *vp, int nts,
+                        artis_packet *packets, int npkts, artis_estimators *est, int64_t work_out[ARTIS_WORK_COUNT],
+                        int nthreads);
+
 }  // namespace
 
 // ================================================================================================== C ABI
@@ -2411,12 +2719,37 @@ extern "C" {
 int oracle_update_packets_g(const artis_atomic_tables *at, const artis_geometry *geom, const artis_cell_state *cs,
                             const artis_run_params *rp, const artis_gamma_spectra *gs, int nts, artis_packet *packets,
                             int npkts, artis_estimators *est, int64_t work_out[ARTIS_WORK_COUNT], int nthreads) {
+  return update_packets_impl(at, geom, cs, rp, gs, nullptr, nts, packets, npkts, est, work_out, nthreads);
+}
+
+// The same with VPKT_ON: virtual packets of the given vpkt.txt parameters are ADDED into *vout
+// (arrays sized as artis_vpkt_result documents).
+int oracle_update_packets_v(const artis_atomic_tables *at, const artis_geometry *geom, const artis_cell_state *cs,
+                            const artis_run_params *rp, const artis_gamma_spectra *gs, const artis_vpkt_params *vp,
+                            artis_vpkt_result *vout, int nts, artis_packet *packets,
+                            int npkts, artis_estimators *est, int64_t work_out[ARTIS_WORK_COUNT], int nthreads) {
+  VpktCfg v;
+  if (int rc = vpkt_config(vp, at->elem_anumber, at->nelements, v)) return rc;
+  if (!vout || !vout->vstokes_i || !vout->vstokes_q || !vout->vstokes_u) return ARTIS_ERR_BAD_ARGUMENT;
+  if (vp->vgrid_flag == 1 && (!vout->vgrid_i || !vout->vgrid_q || !vout->vgrid_u)) return ARTIS_ERR_BAD_ARGUMENT;
+  v.out = vout;
+  return update_packets_impl(at, geom, cs, rp, gs, &v, nts, packets, npkts, est, work_out, nthreads);
+}
+
+}  // extern "C"
+
+namespace {
+int update_packets_impl(const artis_atomic_tables *at, const artis_geometry *geom, const artis_cell_state *cs,
+                        const artis_run_params *rp, const artis_gamma_spectra *gs, const VpktCfg *vp, int nts,
+                        artis_packet *packets, int npkts, artis_estimators *est, int64_t work_out[ARTIS_WORK_COUNT],
+                        int nthreads) {
   Ctx c;
   c.at = at;
   c.g = geom;
   c.cs = cs;
   c.rp = *rp;
   c.gs = gs;
+  c.vp = vp;
   c.T_step_log = (log(at->maxtemp) - log(at->mintemp)) / (at->tablesize - 1.);
   Est E;
   E.e = est;
@@ -2482,6 +2815,9 @@ int oracle_update_packets_g(const artis_atomic_tables *at, const artis_geometry 
     for (int k = 0; k < ARTIS_WORK_COUNT; k++) work_out[k] = work[k];
   return status.load();
 }
+}  // namespace
+
+extern "C" {
 
 int oracle_update_packets(const artis_atomic_tables *at, const artis_geometry *geom, const artis_cell_state *cs,
                           const artis_run_params *rp, int nts, artis_packet *packets, int npkts,
@@ -2489,7 +2825,7 @@ int oracle_update_packets(const artis_atomic_tables *at, const artis_geometry *g
   return oracle_update_packets_g(at, geom, cs, rp, nullptr, nts, packets, npkts, est, work_out, nthreads);
 }
 
-int oracle_abi_version(void) { return 2; }
+int oracle_abi_version(void) { return 3; }
 
 // ---- unit hooks for tests/ ---------------------------------------------------------------------------------
 // Philox4x32-10 block (known-answer tests against the published Random123 vectors)

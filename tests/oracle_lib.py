@@ -27,6 +27,11 @@ def lib():
                                               C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.POINTER(ffi.Estimators),
                                               C.c_void_p, C.c_int]
         L.oracle_update_packets_g.restype = C.c_int
+        L.oracle_update_packets_v.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(ffi.RunParams),
+                                              C.c_void_p, C.POINTER(ffi.VpktParams), C.POINTER(ffi.VpktResult),
+                                              C.c_int, C.c_void_p, C.c_int, C.POINTER(ffi.Estimators), C.c_void_p,
+                                              C.c_int]
+        L.oracle_update_packets_v.restype = C.c_int
         _lib = L
     return _lib
 
@@ -43,6 +48,23 @@ def update_packets(model, nts, packets, est=None, nthreads=0, params=None):
     if rc != 0:
         raise RuntimeError(f"oracle_update_packets -> {rc}")
     return est, work
+
+
+def update_packets_vpkt(model, nts, packets, vcfg, vout=None, est=None, nthreads=0, params=None):
+    """update_packets with VPKT_ON: virtual-packet spectra ADDED into vout (ffi.VpktArrays)."""
+    if est is None:
+        est = model.new_estimators()
+    if vout is None:
+        vout = ffi.VpktArrays(vcfg)
+    work = np.zeros(ffi.ARTIS_WORK_COUNT, dtype=np.int64)
+    p = params if params is not None else model.params
+    rc = lib().oracle_update_packets_v(model.atomic, model.geometry, model.cellstate, C.byref(p),
+                                       getattr(model, "gamma_spectra", None), C.byref(vcfg.struct),
+                                       C.byref(vout.struct), int(nts), packets.ctypes.data, len(packets),
+                                       C.byref(est.struct), work.ctypes.data, int(nthreads))
+    if rc != 0:
+        raise RuntimeError(f"oracle_update_packets_v -> {rc}")
+    return est, vout, work
 
 
 def spectrum(model, packets, nnubins=1000, nprocs=1):

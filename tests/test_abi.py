@@ -41,6 +41,10 @@ int main(void) {
   printf("run_params %zu\n", sizeof(artis_run_params));
   printf("cell_state %zu\n", sizeof(artis_cell_state));
   printf("gamma_spectra %zu\n", sizeof(artis_gamma_spectra));
+  printf("vpkt_params %zu\n", sizeof(artis_vpkt_params));
+  printf("vpkt_result %zu\n", sizeof(artis_vpkt_result));
+  printf("vpkt_tau_max %zu\n", offsetof(artis_vpkt_params, tau_max_vpkt));
+  printf("vpkt_spawn_capacity %zu\n", offsetof(artis_vpkt_params, spawn_capacity));
   return 0;
 }
 """
@@ -61,6 +65,10 @@ def test_c_header_layout_matches_numpy_and_ctypes():
     assert lay["estimators"] == C.sizeof(ffi.Estimators)
     assert lay["run_params"] == C.sizeof(ffi.RunParams)
     assert lay["gamma_spectra"] == C.sizeof(ffi.GammaSpectra)
+    assert lay["vpkt_params"] == C.sizeof(ffi.VpktParams)
+    assert lay["vpkt_result"] == C.sizeof(ffi.VpktResult)
+    assert lay["vpkt_tau_max"] == ffi.VpktParams.tau_max_vpkt.offset
+    assert lay["vpkt_spawn_capacity"] == ffi.VpktParams.spawn_capacity.offset
     assert lay["cell_state"] == 16 * 8  # 15 array pointers + ffegrp
 
 
@@ -80,7 +88,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_without_gpu_and_reports_version():
     lib = C.CDLL(GPU_SO)
-    assert lib.artis_gpu_abi_version() == 2
+    assert lib.artis_gpu_abi_version() == 3
     lib.artis_gpu_last_error.restype = C.c_char_p
     assert lib.artis_gpu_last_error() is not None
 
