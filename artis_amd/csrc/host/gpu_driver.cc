@@ -6,14 +6,15 @@
 //                    <npkts> <seed> [<gamma_lines_dir>]
 // With <gamma_lines_dir> (holding ni56_lines.txt / co56_lines.txt, the reference's data/ files) the run starts
 // from radioactive pellets at tmin (packet_init, packet.cc:59-149) instead of r-packets.
-// Writes <outdir>/packets_0000_ts<nts>.tmp (raw 304-byte records, sn3d.cc:387-398) after every timestep and
-// prints one summary line per timestep.
+// Writes <outdir>/packets_0000_ts<nts>.tmp (raw 304-byte records, sn3d.cc:387-398) after every timestep, the
+// final <outdir>/packets00_0000.out (packet.cc:152-196), and prints one summary line per timestep.
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
 #include <string>
 #include <vector>
 
+#include "artis_io.h"
 #include "artis_layout_check.h"
 #include "model_synth.h"
 #include "update_packets_gpu.h"
@@ -94,18 +95,16 @@ int main(int argc, char **argv) {
       engine.update_packets(rp.rank, nts, packets.data(), npkts, est);
       double jsum = 0.;
       for (double v : J) jsum += v;
-      const std::string path = outdir + "/packets_0000_ts" + std::to_string(nts) + ".tmp";
-      FILE *f = std::fopen(path.c_str(), "wb");
-      if (!f || std::fwrite(packets.data(), sizeof(artis_packet), npkts, f) != (size_t)npkts) {
-        std::fprintf(stderr, "cannot write %s\n", path.c_str());
-        return 1;
-      }
-      std::fclose(f);
+      artis_amd::check(artis_write_temp_packetsfile(outdir.c_str(), nts, rp.rank, packets.data(), npkts),
+                       "write_temp_packetsfile");
       std::printf("nts %d nesc %lld cmf_lum %.17g gamma_dep %.17g pellet_decays %lld Jsum %.17g transport_ms %.3f\n",
                   nts, (long long)est.nesc, est.cmf_lum, est.gamma_dep, (long long)est.pellet_decays, jsum,
                   engine.last_transport_ms());
     }
   }
+  // the final packet list as the reference writes it at the end of the run (sn3d.cc:640-645)
+  artis_amd::check(artis_write_packets((outdir + "/packets00_0000.out").c_str(), packets.data(), npkts),
+                   "write_packets");
   artis_model_free(m);
   return 0;
 }

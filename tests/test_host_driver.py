@@ -48,3 +48,11 @@ def test_driver_matches_oracle(tmp_path):
         pg = np.fromfile(tmp_path / f"packets_0000_ts{nts}.tmp", dtype=ffi.PACKET_DTYPE)
         assert len(pg) == NPKTS
         parity.assert_packets_match(pg, po)
+    # the final text packet list (packet.cc:152-196) reads back to the last raw records at %g precision
+    from artis_amd import io
+
+    back = np.zeros(NPKTS, dtype=ffi.PACKET_DTYPE)
+    io.read_packets(str(tmp_path / "packets00_0000.out"), back)
+    np.testing.assert_array_equal(back["number"], pg["number"])
+    np.testing.assert_array_equal(back["type"], pg["type"])
+    np.testing.assert_allclose(back["nu_rf"], pg["nu_rf"], rtol=1e-5)
