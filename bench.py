@@ -60,6 +60,9 @@ def main():
     ap.add_argument("--nts", type=int, default=10)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU time of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--vpkt", type=int, default=0,
+                    help="virtual packets (BASELINE config 5, vpkt.cc) with this many observer directions; the "
+                         "timestep must lie in the vspec window [10 d, 30 d] (e.g. --nts 30)")
     args = ap.parse_args()
 
     import torch
@@ -87,6 +90,16 @@ def main():
     P = args.packets
     packets = model.init_rpackets(nts, P, seed=1000 + rank)
     eng = Engine(model, device=local_rank, params=params)
+    vcfg = None
+    if args.vpkt > 0:
+        from artis_amd import ffi
+
+        nobs = args.vpkt
+        # observers spread in cos(theta) and phi; spectra: all opacity + three with one source removed
+        vcfg = ffi.VpktConfig(nz_obs=tuple(np.linspace(-0.9, 0.9, nobs)),
+                              phi_obs_deg=tuple(np.linspace(0.0, 300.0, nobs)), exclude=(0.0, -1.0, -2.0, 26.0),
+                              nprocs=world)
+        eng.vpkt_init(vcfg)
     eng.upload_cellstate(nts)
     eng.upload(packets)
     eng.snapshot()
@@ -100,6 +113,7 @@ def main():
     work = np.zeros(16, dtype=np.int64)
     rounds = []
     ktimes = []
+    vstats = []
 
     def step(record):
         eng.restore()
@@ -116,6 +130,8 @@ def main():
             work[:] = eng.last_work()
             rounds.append(eng.last_rounds())
             ktimes.append(eng.last_kernel_times())
+            if vcfg is not None:
+                vstats.append(eng.vpkt_last_stats())
 
     for _ in range(args.warmup):
         step(False)
@@ -158,7 +174,7 @@ def main():
                 traffic = kd["hbm_bytes_per_launch"]
     cpu = None
     parity_line = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and vcfg is None:
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import oracle_lib
         import parity
@@ -241,6 +257,13 @@ def main():
                  "gc_updates", "ma_jumps", "ma_trans", "kpkt", "kpkt_terms", "escaped", "es_scat", "bb_events",
                  "cont_events"], work)},
         }
+        if vcfg is not None:
+            vms = float(np.mean([v[0] for v in vstats]))
+            line["config"]["workload"] += (f"; virtual packets: {vcfg.nobs} observers x {vcfg.nspectra} spectra, "
+                                           f"vspec window 10-30 d, 3500-10000 A (vpkt.h defaults)")
+            line["vpkt"] = {"ms": vms, "spawns": int(np.mean([v[1] for v in vstats])),
+                            "traces": int(np.mean([v[2] for v in vstats])),
+                            "traces_per_s": float(np.mean([v[2] for v in vstats])) / max(vms / 1e3, 1e-12)}
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:
