@@ -24,7 +24,7 @@ ABI_SYMBOLS = [
     "artis_gpu_estimators_download", "artis_gpu_estimator_block_doubles", "artis_gpu_estimator_block_to_device",
     "artis_gpu_estimator_block_from_device", "artis_gpu_last_transport_ms", "artis_gpu_last_precompute_ms",
     "artis_gpu_last_work_counts", "artis_gpu_last_rounds", "artis_gpu_spectrum", "artis_gpu_last_kernel_times", "artis_gpu_last_error", "artis_gpu_abi_version",
-    "artis_gpu_vpkt_init", "artis_gpu_vpkt_zero", "artis_gpu_vpkt_download", "artis_gpu_vpkt_last_stats",
+    "artis_gpu_vpkt_init", "artis_gpu_vpkt_zero", "artis_gpu_vpkt_download", "artis_gpu_vpkt_last_stats", "artis_gpu_vpkt_last_work",
 ]
 
 _gpu_lib = None
@@ -58,6 +58,7 @@ def gpu_lib():
         L.artis_gpu_vpkt_init.argtypes = [C.POINTER(ffi.VpktParams)]
         L.artis_gpu_vpkt_download.argtypes = [C.POINTER(ffi.VpktResult), C.c_int]
         L.artis_gpu_vpkt_last_stats.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+        L.artis_gpu_vpkt_last_work.argtypes = [C.POINTER(C.c_int64)]
         _gpu_lib = L
     return _gpu_lib
 
@@ -176,6 +177,12 @@ class Engine:
         tr = C.c_int64()
         self.lib.artis_gpu_vpkt_last_stats(C.byref(ms), C.byref(sp), C.byref(tr))
         return ms.value, sp.value, tr.value
+
+    def vpkt_last_work(self):
+        """{segments, lines, bf_active, escaped} of the last update's virtual packets."""
+        w = (C.c_int64 * 4)()
+        self.lib.artis_gpu_vpkt_last_work(w)
+        return dict(zip(("segments", "lines", "bf_active", "escaped"), (int(x) for x in w)))
 
     def last_kernel_times(self):
         """{class: (ms, launches)} for the last transport: rpkt, ma, kpkt, classify."""

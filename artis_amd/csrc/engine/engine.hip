@@ -503,6 +503,7 @@ struct Engine {
   std::vector<hipEvent_t> vev;  // (start, end) pairs around the k_vpkt launches of the last update
   size_t vev_used = 0;
   double last_vpkt_ms = 0.;
+  int64_t last_vpkt_work[4] = {0, 0, 0, 0};
   int64_t last_vpkt_spawns = 0, last_vpkt_traces = 0;
   std::string last_error;
 };
@@ -633,7 +634,19 @@ int vpkt_flush() {
     }
   }
   HIPCHK(hipEventRecord(G.vev[G.vev_used++], G.stream));
-  k_vpkt<<<(unsigned)G.wave_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, G.W.refill_min);
+  // minimum waves per SIMD the virtual-packet kernel is compiled for (ARTIS_VPKT_OCC = 1, 2 or 3; more waves
+  // hide more of the FP64 and memory latency of the walk at the price of register spills)
+  static const int occ = [] {
+    const char *e = getenv("ARTIS_VPKT_OCC");
+    const int v = e ? atoi(e) : VPKT_OCC_DEFAULT;
+    return (v == 2 || v == 3) ? v : 1;
+  }();
+  if (occ == 3)
+    k_vpkt<VPKT_PF, 3><<<(unsigned)G.wave_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, G.W.refill_min);
+  else if (occ == 2)
+    k_vpkt<VPKT_PF, 2><<<(unsigned)G.wave_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, G.W.refill_min);
+  else
+    k_vpkt<VPKT_PF, 1><<<(unsigned)G.wave_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, G.W.refill_min);
   HIPCHK(hipEventRecord(G.vev[G.vev_used++], G.stream));
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemsetAsync(G.K.V.spawn_ctr, 0, 2 * sizeof(uint32_t), G.stream));
@@ -668,6 +681,10 @@ int vpkt_collect(const unsigned long long before[8]) {
   HIPCHK(hipMemcpy(after, G.K.V.ctr, sizeof(after), hipMemcpyDeviceToHost));
   G.last_vpkt_traces = (int64_t)(after[0] - before[0]);
   G.last_vpkt_spawns = (int64_t)(after[4] - before[4]);
+  G.last_vpkt_work[0] = (int64_t)(after[5] - before[5]);
+  G.last_vpkt_work[1] = (int64_t)(after[6] - before[6]);
+  G.last_vpkt_work[2] = (int64_t)(after[7] - before[7]);
+  G.last_vpkt_work[3] = (int64_t)((after[1] + after[2] + after[3]) - (before[1] + before[2] + before[3]));
   return 0;
 }
 
@@ -690,7 +707,15 @@ int run_wavefront(int64_t n, int nts, double t2) {
   bool done = false;
   for (; round < WAVE_MAX_ROUNDS && !done; round++) {
     TSTART(0);
-    k_rpkt<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+    // ARTIS_GPU_RPKT_OCC=2: compile-time minimum of two waves per SIMD (register spills in exchange)
+    static const bool rpkt_occ2 = [] {
+      const char *e = getenv("ARTIS_GPU_RPKT_OCC");
+      return e && e[0] == '2';
+    }();
+    if (rpkt_occ2)
+      k_rpkt<2><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+    else
+      k_rpkt<1><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
     TEND(0);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QR, 0, 2 * sizeof(uint32_t), G.stream));
     TSTART(1);
@@ -934,6 +959,12 @@ int artis_gpu_vpkt_last_stats(double *ms, int64_t *spawns, int64_t *traces) {
   if (ms) *ms = G.last_vpkt_ms;
   if (spawns) *spawns = G.last_vpkt_spawns;
   if (traces) *traces = G.last_vpkt_traces;
+  return 0;
+}
+
+int artis_gpu_vpkt_last_work(int64_t work[4]) {
+  if (!work) return ARTIS_ERR_BAD_ARGUMENT;
+  for (int i = 0; i < 4; i++) work[i] = G.last_vpkt_work[i];
   return 0;
 }
 

@@ -22,6 +22,10 @@
 #include "wavefront.h"
 
 #define VPKT_MAX_CELLS 1000000
+// lines fetched per memory round trip in the line walk (A/B on MI355X, 1e6 packets: 4 -> 5.61 s, 8 -> 5.57 s,
+// 16 -> 6.16 s)
+#define VPKT_PF 8
+#define VPKT_OCC_DEFAULT 1
 
 // vpkt.cc:374-385
 DEVFN bool vpkt_alive(const DevVpkt &V, const double *tau) {
@@ -186,6 +190,7 @@ DEVFN void vpkt_trace_finish(const Ctx &K, VLane &v) {
 enum { VSEG_CONTINUE = 0, VSEG_ESCAPED = 1, VSEG_KILLED = 2 };
 
 // one pass of rlc_emiss_vpkt's cell loop (vpkt.cc:195-312); deviation D9 for the line loop
+template <int PF>
 DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
   const Ctx &K = x.K;
   const DevVpkt &V = K.V;
@@ -219,15 +224,51 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
       v.tau[ind] += kap_cont * s_cont;
   }
   if (!vpkt_alive(V, v.tau)) return VSEG_KILLED;
-  const int64_t popbase = (int64_t)K.C.ne_index[v.mgi] * K.T.nlevels_total;
+  const double *pops = K.C.pops + (int64_t)K.C.ne_index[v.mgi] * K.T.nlevels_total;
+  bool anyex = false;
+  for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
+    if (ind < V.nspectra && V.exclude[ind] != 0) anyex = true;
+  // As in get_event: the line records, the two populations each needs and (with element exclusions) the line's
+  // atomic number are fetched PF consecutive lines at a time, all loads independent, so the walk waits for memory
+  // twice per PF lines instead of three to four times per line.  The tau sums are unchanged.
+  int pf_base = -(1 << 20);
+  LineTau r[PF];
+  double pl[PF], pu[PF];
+  int z[PF] = {};
   while (ldist < sdist) {
     const int lineindex = closest_transition(K, d.nu_cmf, d.next_trans);
     if (lineindex < 0) {
       d.next_trans = K.T.nlines + 1;
       break;  // D9
     }
-    const LineTau lt = K.T.line_tau[lineindex];
-    const double nutrans = lt.nu;
+    if ((unsigned)(lineindex - pf_base) >= (unsigned)PF) {
+      pf_base = lineindex;
+      const int nl1 = K.T.nlines - 1;
+#pragma unroll
+      for (int q = 0; q < PF; q++) r[q] = K.T.line_tau[min(lineindex + q, nl1)];
+      if (anyex) {
+#pragma unroll
+        for (int q = 0; q < PF; q++) z[q] = K.T.line_elem[min(lineindex + q, nl1)];
+      }
+#pragma unroll
+      for (int q = 0; q < PF; q++) {
+        pl[q] = pops[r[q].ul_lower];
+        pu[q] = pops[r[q].ul_upper];
+      }
+    }
+    const int pj = lineindex - pf_base;
+    double nutrans = r[0].nu, n_u = pu[0], n_l = pl[0], B_lu = r[0].B_lu, B_ul = r[0].B_ul;
+    int zl = z[0];
+#pragma unroll
+    for (int q = 1; q < PF; q++)
+      if (pj == q) {
+        nutrans = r[q].nu;
+        n_u = pu[q];
+        n_l = pl[q];
+        B_lu = r[q].B_lu;
+        B_ul = r[q].B_ul;
+        zl = z[q];
+      }
     d.next_trans = lineindex + 1;
     if (d.nu_cmf < nutrans)
       ldist = 0;
@@ -239,17 +280,12 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
     }
     lines++;
     const double t_line = t_current + ldist / ARTIS_CLIGHT;
-    const double n_u = K.C.pops[popbase + lt.ul_upper];
-    const double n_l = K.C.pops[popbase + lt.ul_lower];
-    const double dtau = (lt.B_lu * n_l - lt.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_line;
-    bool anyex = false;
-    for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
-      if (ind < V.nspectra && V.exclude[ind] != 0) anyex = true;
+    const double dtau = (B_lu * n_l - B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_line;
     if (!anyex) {
       for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
         if (ind < V.nspectra) v.tau[ind] += dtau;
     } else {
-      const int anumber = V.anumber[K.T.line_elem[lineindex]];
+      const int anumber = V.anumber[zl];
       for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
         if (ind < V.nspectra && V.exclude[ind] != -1 && (anumber != V.exclude[ind])) v.tau[ind] += dtau;
     }
@@ -271,7 +307,8 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
 }
 
 // all (spawn, observer) work items of the spawn buffer; spawn_ctr[1] is the fetch head
-__global__ __launch_bounds__(WAVE_BLOCK) void k_vpkt(const Ctx *__restrict__ ctxp, int refill_min) {
+template <int PF, int MINW>
+__global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict__ ctxp, int refill_min) {
   const Ctx &K = *ctxp;
   const DevVpkt &V = K.V;
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
@@ -333,7 +370,7 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_vpkt(const Ctx *__restrict__ ctx
           have = false;
         }
       } else {
-        const int r = vpkt_trace_segment(x, v, lines);
+        const int r = vpkt_trace_segment<PF>(x, v, lines);
         if (r != VSEG_CONTINUE) {
           if (r == VSEG_ESCAPED) vpkt_trace_finish(K, v);
           v.tracing = false;

@@ -146,7 +146,8 @@ DEVFN void apply_pending(Tx &x, const WaveState &W, int32_t idx, Pkt &p, const C
 }
 
 // r-packets: persistent lanes, one do_rpkt_step per loop pass
-__global__ __launch_bounds__(WAVE_BLOCK) void k_rpkt(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa, int64_t n,
+template <int MINW>
+__global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa, int64_t n,
                                                      int nts, double t2) {
   const Ctx &K = *ctxp;
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];

@@ -47,7 +47,7 @@ def byte_model(work, nions_total):
     return {"rpkt": rpkt, "ma": ma, "kpkt": kpkt}
 
 
-KERNEL_NAME = {"rpkt": "k_rpkt", "ma": "k_ma<true, 1>", "kpkt": "k_kpkt"}
+KERNEL_NAME = {"rpkt": "k_rpkt<1>", "ma": "k_ma<true, 1>", "kpkt": "k_kpkt"}
 
 
 def main():
@@ -114,6 +114,7 @@ def main():
     rounds = []
     ktimes = []
     vstats = []
+    vwork = []
 
     def step(record):
         eng.restore()
@@ -132,6 +133,7 @@ def main():
             ktimes.append(eng.last_kernel_times())
             if vcfg is not None:
                 vstats.append(eng.vpkt_last_stats())
+                vwork.append(eng.vpkt_last_work())
 
     for _ in range(args.warmup):
         step(False)
@@ -264,6 +266,8 @@ def main():
             line["vpkt"] = {"ms": vms, "spawns": int(np.mean([v[1] for v in vstats])),
                             "traces": int(np.mean([v[2] for v in vstats])),
                             "traces_per_s": float(np.mean([v[2] for v in vstats])) / max(vms / 1e3, 1e-12)}
+            ntr = max(line["vpkt"]["traces"], 1)
+            line["vpkt"]["work_per_trace"] = {k: float(np.mean([w[k] for w in vwork])) / ntr for k in vwork[0]}
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:

@@ -418,6 +418,9 @@ int artis_gpu_vpkt_download(artis_vpkt_result *out, int reset_counters);
 /* device time (ms) of the virtual-packet kernels of the last update, and the number of spawn records and
  * traced (spawn, observer, range) virtual packets it processed */
 int artis_gpu_vpkt_last_stats(double *ms, int64_t *spawns, int64_t *traces);
+/* work counters of the last update's virtual packets: [0] cell segments (continuum-opacity evaluations),
+ * [1] lines whose opacity was added, [2] active bf continua scanned, [3] virtual packets that escaped */
+int artis_gpu_vpkt_last_work(int64_t work[4]);
 
 int64_t artis_gpu_last_rounds(void);  /* event-queue rounds of the last update (0: megakernel path) */
 /* device time (ms, HIP events around every launch) and launch count of the last update per kernel class:

@@ -39,7 +39,9 @@ def test_vpkt_leaves_real_packets_untouched():
     np.testing.assert_allclose(ea.J, eb.J, rtol=1e-12)
     np.testing.assert_allclose(ea.gamma, eb.gamma, rtol=1e-12, atol=1e-300)
     ca, cb = ea.counters, eb.counters
-    others = [k for k in range(ffi.ARTIS_COUNTER_COUNT) if k != 28]  # 28: COUNTER_CELLCROSSINGS
+    # 28: COUNTER_CELLCROSSINGS (virtual packets cross cells too); 31/32: UPDATECELL / COOLINGRATECALCCOUNTER are
+    # statistics of the per-thread cellhistory cache and depend on the OpenMP schedule
+    others = [k for k in range(ffi.ARTIS_COUNTER_COUNT) if k not in (28, 31, 32)]
     np.testing.assert_array_equal(ca[others], cb[others])
     assert cb[28] > ca[28] and eb.struct.nesc > ea.struct.nesc
     c = vout.counters()
