@@ -707,12 +707,16 @@ int run_wavefront(int64_t n, int nts, double t2) {
   bool done = false;
   for (; round < WAVE_MAX_ROUNDS && !done; round++) {
     TSTART(0);
-    // ARTIS_GPU_RPKT_OCC=2: compile-time minimum of two waves per SIMD (register spills in exchange)
-    static const bool rpkt_occ2 = [] {
+    // waves per SIMD k_rpkt is compiled for (ARTIS_GPU_RPKT_OCC = 1, 2 or 3).  The r-packet step needs ~300
+    // registers; at 1 wave/SIMD nothing hides its FP64 latency, and forcing 2 (spilling to scratch) measured
+    // 1.80 s -> 1.53 s per bench step on MI355X, so 2 is the default.
+    static const int rpkt_occ = [] {
       const char *e = getenv("ARTIS_GPU_RPKT_OCC");
-      return e && e[0] == '2';
+      return (e && (e[0] == '1' || e[0] == '3')) ? e[0] - '0' : 2;
     }();
-    if (rpkt_occ2)
+    if (rpkt_occ == 3)
+      k_rpkt<3><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+    else if (rpkt_occ == 2)
       k_rpkt<2><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
     else
       k_rpkt<1><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
@@ -728,11 +732,19 @@ int run_wavefront(int64_t n, int nts, double t2) {
       k_ma_scatter<<<grid, WAVE_BLOCK, 0, G.stream>>>(W, G.d_binoffs);
     }
     HIPCHK(hipMemsetAsync(W.xhead, 0, 8 * sizeof(uint32_t), G.stream));
+    // ARTIS_GPU_MA_WAVES=w: launch only w blocks per CU (w resident waves per SIMD) -- fewer concurrent walks
+    // thrash the caches less; the walk is bound by the memory system, not by latency hiding
+    static const int ma_waves = [] {
+      const char *e = getenv("ARTIS_GPU_MA_WAVES");
+      const int v = e ? atoi(e) : 0;
+      return (v >= 1 && v <= 8) ? v : 0;
+    }();
+    const unsigned ma_grid = ma_waves ? (unsigned)(G.wave_grid / 8 * ma_waves) : grid;
     if (G.K.C.have_macache) {
       if (G.ma_occ == 8)
-        k_ma<true, 8><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+        k_ma<true, 8><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
       else
-        k_ma<true, 1><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+        k_ma<true, 1><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
     } else {
       k_ma<false, 1><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
     }

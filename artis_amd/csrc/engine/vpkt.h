@@ -25,7 +25,8 @@
 // lines fetched per memory round trip in the line walk (A/B on MI355X, 1e6 packets: 4 -> 5.61 s, 8 -> 5.57 s,
 // 16 -> 6.16 s)
 #define VPKT_PF 8
-#define VPKT_OCC_DEFAULT 1
+// waves per SIMD (A/B at 1e6 packets: 1 -> 5.56 s, 2 -> 4.43 s, 3 -> 6.63 s; spills grow with the bound)
+#define VPKT_OCC_DEFAULT 2
 
 // vpkt.cc:374-385
 DEVFN bool vpkt_alive(const DevVpkt &V, const double *tau) {

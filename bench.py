@@ -47,7 +47,7 @@ def byte_model(work, nions_total):
     return {"rpkt": rpkt, "ma": ma, "kpkt": kpkt}
 
 
-KERNEL_NAME = {"rpkt": "k_rpkt<1>", "ma": "k_ma<true, 1>", "kpkt": "k_kpkt"}
+KERNEL_NAME = {"rpkt": "k_rpkt<2>", "ma": "k_ma<true, 1>", "kpkt": "k_kpkt"}
 
 
 def main():
