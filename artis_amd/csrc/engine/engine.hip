@@ -72,7 +72,7 @@ __global__ void k_levelpops(Ctx K) {
   if (l == 0) {
     nn = ng;
   } else {
-    const double T_exc = K.C.TJ[mgi];
+    const double T_exc = K.R.exc_te ? K.C.Te[mgi] : K.C.TJ[mgi];  // ltepop.cc:338
     const double W = 1.;
     nn = (ng * W * (double)K.T.level_stat_weight[ul] / (double)K.T.level_stat_weight[ul0] *
           exp(-(K.T.level_epsilon[ul] - K.T.level_epsilon[ul0]) / ARTIS_KB / T_exc));
@@ -1291,6 +1291,11 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   R.gamma_grey = rp->gamma_grey;
   R.instant_particle_deposition = rp->instant_particle_deposition;
   R.nt_solve_spencerfano = rp->nt_solve_spencerfano;
+  if (rp->excitation_temperature != ARTIS_TEXC_TJ && rp->excitation_temperature != ARTIS_TEXC_TE) {
+    G.last_error = "artis_run_params.excitation_temperature must be ARTIS_TEXC_TJ or ARTIS_TEXC_TE";
+    return ARTIS_ERR_BAD_ARGUMENT;
+  }
+  R.exc_te = rp->excitation_temperature == ARTIS_TEXC_TE;
 
   // estimators: one double block [J | nuJ | ffheat | colheat | rpkt_emiss | gamma | bfheat | scalars(10)]
   const int np = g->npts_model;

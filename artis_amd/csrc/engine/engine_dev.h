@@ -175,6 +175,7 @@ struct DevRun {
   int32_t pol_dipole, relativistic_doppler, record_linestat;
   double gamma_grey;
   int32_t instant_particle_deposition, nt_solve_spencerfano;
+  int32_t exc_te;  // 1: level populations at T_e (LTEPOP_EXCITATIONTEMPERATURE), 0: at T_J
 };
 
 #endif

@@ -3,6 +3,8 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <fstream>
 #include <sstream>
 #include <string>
@@ -53,9 +55,293 @@ std::string temp_packets_name(const char *dir, int timestep, int my_rank) {
   return (dir && dir[0]) ? std::string(dir) + "/" + name : std::string(name);
 }
 
+// input.h:16-30 lineiscommentonly: blank up to an optional '#' (only ' ' counts as blank)
+bool ref_comment_only(const std::string &line) {
+  size_t n = line.find('#');
+  if (n == std::string::npos) n = line.length();
+  for (size_t i = 0; i < n; i++)
+    if (line[i] != ' ') return false;
+  return true;
+}
+
+// input.cc:1833-1846 get_noncommentline
+bool noncomment_line(std::istream &in, std::string &line) {
+  while (std::getline(in, line))
+    if (!ref_comment_only(line)) return true;
+  return false;
+}
+
+// grid.cc:1080-1156 read_model_headerline: the number of custom columns after the standard ones, with the
+// reference's column-position checks
+bool model_header_columns(const std::string &line, int model_type, int *ncustom) {
+  std::istringstream iss(line);
+  std::string token;
+  int columnindex = -1;
+  *ncustom = 0;
+  while (std::getline(iss, token, ' ')) {
+    bool blank = true;
+    for (char ch : token)
+      if (!isspace((unsigned char)ch)) blank = false;
+    if (blank) continue;
+    columnindex++;
+    if (token == "#inputcellid") {
+      if (columnindex != 0) return false;
+    } else if (token == "velocity_outer") {
+      if (columnindex != 1) return false;
+    } else if (token == "logrho") {
+      if (columnindex != 2 || model_type != 1) return false;
+    } else if (token == "rho") {
+      if (columnindex != 4 || model_type == 1) return false;
+    } else if (token == "X_Fegroup" || token == "X_Ni56" || token == "X_Co56" || token == "X_Fe52" ||
+               token == "X_Cr48" || token == "X_Ni57" || token == "X_Co57" || token.rfind("pos_", 0) == 0) {
+      continue;
+    } else {
+      if (model_type == 1 && columnindex < 10) return false;
+      if (model_type == 3 && columnindex < 12) return false;
+      (*ncustom)++;
+    }
+  }
+  return true;
+}
+
+void alloc_model_arrays(artis_ejecta_model *m, int n) {
+  double **arrs[8] = {&m->rho_model, &m->ffegrp, &m->x_ni56, &m->x_co56, &m->x_fe52, &m->x_cr48, &m->x_ni57,
+                      &m->x_co57};
+  for (double **a : arrs) *a = (double *)std::calloc((size_t)n, sizeof(double));
+}
+
+// read_2d3d_modelradioabundanceline (grid.cc:1158-1226): 5 or 7 abundances, then with 7 the custom columns
+bool model_abundance_line(const std::string &line, artis_ejecta_model *m, int mgi, bool keepcell) {
+  double v[7] = {0, 0, 0, 0, 0, 0, 0};
+  const int items = std::sscanf(line.c_str(), "%lg %lg %lg %lg %lg %lg %lg", &v[0], &v[1], &v[2], &v[3], &v[4],
+                                &v[5], &v[6]);
+  if (items != 5 && items != 7) return false;
+  if (keepcell) {
+    m->ffegrp[mgi] = v[0];
+    m->x_ni56[mgi] = v[1];
+    m->x_co56[mgi] = v[2];
+    m->x_fe52[mgi] = v[3];
+    m->x_cr48[mgi] = v[4];
+    m->x_ni57[mgi] = v[5];
+    m->x_co57[mgi] = v[6];
+    if (items == 7) {
+      std::istringstream ss(line);
+      double x;
+      for (int i = 0; i < 7 + m->n_custom_columns; i++)
+        if (!(ss >> x)) return false;
+      if (ss >> x) return false;  // no tokens left (grid.cc:1217-1218)
+    }
+  }
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
+
+// input.cc:1874-2140 read_parameterfile
+int artis_read_input_file(const char *filename, artis_input_params *p) {
+  if (!filename || !p) return ARTIS_ERR_BAD_ARGUMENT;
+  std::ifstream in(filename);
+  if (!in.is_open()) return ARTIS_ERR_BAD_ARGUMENT;
+  std::memset(p, 0, sizeof(*p));
+  std::string line;
+  auto next = [&](std::istringstream &ss) {
+    if (!noncomment_line(in, line)) return false;
+    ss.clear();
+    ss.str(line);
+    return true;
+  };
+  std::istringstream ss;
+  long dum1 = 0;
+  float dum2 = 0.f, dum3 = 0.f;
+  if (!next(ss) || !(ss >> dum1)) return ARTIS_ERR_BAD_ARGUMENT;
+  p->pre_zseed = dum1 > 0 ? (uint32_t)dum1 : 0u;
+  if (!next(ss) || !(ss >> p->ntstep) || p->ntstep <= 0) return ARTIS_ERR_BAD_ARGUMENT;
+  if (!next(ss) || !(ss >> p->itstep >> p->ftstep)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (!(p->itstep < p->ntstep && p->itstep <= p->ftstep && p->ftstep <= p->ntstep)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (!next(ss) || !(ss >> p->tmin_days >> p->tmax_days)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (!(p->tmin_days > 0 && p->tmax_days > 0 && p->tmin_days < p->tmax_days)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (!next(ss) || !(ss >> dum2 >> dum3)) return ARTIS_ERR_BAD_ARGUMENT;
+  p->nusyn_min_mev = dum2;
+  p->nusyn_max_mev = dum3;
+  if (!next(ss) || !(ss >> p->nsyn_time)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (!next(ss) || !(ss >> dum2 >> dum3)) return ARTIS_ERR_BAD_ARGUMENT;
+  p->syn_time_start_days = dum2;
+  p->syn_time_dlog = dum3;
+  if (!next(ss) || !(ss >> p->model_type)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (!next(ss) || !(ss >> p->rlc_mode) || p->rlc_mode < 0 || p->rlc_mode > 4) return ARTIS_ERR_BAD_ARGUMENT;
+  p->do_r_lc = (p->rlc_mode != 0);
+  p->do_rlc_est = (p->rlc_mode > 0) ? p->rlc_mode - 1 : 0;
+  if (!next(ss) || !(ss >> p->n_out_it)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (!next(ss) || !(ss >> dum2) || std::fabs(dum2 - 1.) >= 1e-3) return ARTIS_ERR_BAD_ARGUMENT;
+  p->clight_factor = dum2;
+  if (!next(ss) || !(ss >> p->gamma_grey)) return ARTIS_ERR_BAD_ARGUMENT;
+  float sd[3] = {0.f, 0.f, 0.f};
+  if (!next(ss) || !(ss >> sd[0] >> sd[1] >> sd[2])) return ARTIS_ERR_BAD_ARGUMENT;
+  const double rr = (sd[0] * sd[0]) + (sd[1] * sd[1]) + (sd[2] * sd[2]);
+  for (int d = 0; d < 3; d++) p->syn_dir[d] = rr > 1.e-6 ? sd[d] / sqrt(rr) : 0.;
+  if (!next(ss) || !(ss >> p->opacity_case)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (!next(ss) || !(ss >> p->rho_crit_para)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (!next(ss) || !(ss >> p->debug_packet)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (!next(ss) || !(ss >> p->continued_from_saved)) return ARTIS_ERR_BAD_ARGUMENT;
+  p->continued_from_saved = (p->continued_from_saved == 1);
+  if (!p->continued_from_saved && p->itstep != 0) return ARTIS_ERR_BAD_ARGUMENT;  // input.cc:2033
+  if (!next(ss) || !(ss >> dum2)) return ARTIS_ERR_BAD_ARGUMENT;
+  p->rfcut_angstroms = dum2;
+  if (!next(ss) || !(ss >> p->num_lte_timesteps)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (!next(ss) || !(ss >> p->cell_is_optically_thick >> p->num_grey_timesteps)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (!next(ss) || !(ss >> p->max_bf_continua)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (p->max_bf_continua == -1) p->max_bf_continua = 1000000;
+  if (!next(ss) || !(ss >> p->nprocs_exspec)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (!next(ss) || !(ss >> p->do_emission_res)) return ARTIS_ERR_BAD_ARGUMENT;
+  float kts = 0.f;
+  if (!next(ss) || !(ss >> kts >> p->n_kpktdiffusion_timesteps)) return ARTIS_ERR_BAD_ARGUMENT;
+  p->kpktdiffusion_timescale = kts;
+  return 0;
+}
+
+void artis_free_model(artis_ejecta_model *m) {
+  if (!m) return;
+  double *arrs[9] = {m->vout, m->rho_model, m->ffegrp, m->x_ni56, m->x_co56, m->x_fe52, m->x_cr48, m->x_ni57,
+                     m->x_co57};
+  for (double *a : arrs) std::free(a);
+  std::free(m->pos_model);
+  std::memset(m, 0, sizeof(*m));
+}
+
+// grid.cc:1228-1370 (1D) and 1459-1600 (3D)
+int artis_read_model(const char *filename, int model_type, artis_ejecta_model *m) {
+  if (!filename || !m || (model_type != 1 && model_type != 3)) return ARTIS_ERR_BAD_ARGUMENT;
+  std::memset(m, 0, sizeof(*m));
+  std::ifstream in(filename);
+  if (!in.is_open()) return ARTIS_ERR_BAD_ARGUMENT;
+  m->model_type = model_type;
+  std::string line;
+  int npts = 0;
+  if (!noncomment_line(in, line) || !(std::stringstream(line) >> npts) || npts <= 0) return ARTIS_ERR_BAD_ARGUMENT;
+  m->npts_model = npts;
+  double t_model_days = 0.;
+  if (!noncomment_line(in, line) || !(std::stringstream(line) >> t_model_days)) return ARTIS_ERR_BAD_ARGUMENT;
+  m->t_model = t_model_days * kDay;
+  if (model_type == 3) {
+    const int n = (int)std::lround(std::pow(npts, 1 / 3.));
+    if (n * n * n != npts) return ARTIS_ERR_BAD_ARGUMENT;  // grid.cc:1475-1476
+    m->ncoord_model[0] = m->ncoord_model[1] = m->ncoord_model[2] = n;
+    if (!noncomment_line(in, line) || !(std::stringstream(line) >> m->vmax)) return ARTIS_ERR_BAD_ARGUMENT;
+  } else {
+    m->ncoord_model[0] = npts;
+    m->ncoord_model[1] = m->ncoord_model[2] = 1;
+  }
+  // optional custom header line (grid.cc:1262-1268)
+  std::streampos oldpos = in.tellg();
+  if (std::getline(in, line) && ref_comment_only(line)) {
+    if (!model_header_columns(line, model_type, &m->n_custom_columns)) return ARTIS_ERR_BAD_ARGUMENT;
+  } else {
+    in.clear();
+    in.seekg(oldpos);
+  }
+  alloc_model_arrays(m, npts);
+  int rc = 0;
+  int mgi = 0;
+  if (model_type == 1) {
+    m->vout = (double *)std::calloc((size_t)npts, sizeof(double));
+    while (rc == 0 && mgi < npts && std::getline(in, line)) {
+      int cellnumberin = 0;
+      double vout_kmps = 0, log_rho = 0, v[7] = {0, 0, 0, 0, 0, 0, 0};
+      const int items = std::sscanf(line.c_str(), "%d %lg %lg %lg %lg %lg %lg %lg %lg %lg", &cellnumberin, &vout_kmps,
+                                    &log_rho, &v[0], &v[1], &v[2], &v[3], &v[4], &v[5], &v[6]);
+      if ((items != 8 && items != 10) || cellnumberin != mgi + 1) {
+        rc = ARTIS_ERR_BAD_ARGUMENT;
+        break;
+      }
+      m->vout[mgi] = vout_kmps * 1.e5;
+      m->rho_model[mgi] = std::pow(10., log_rho);
+      m->ffegrp[mgi] = v[0];
+      m->x_ni56[mgi] = v[1];
+      m->x_co56[mgi] = v[2];
+      m->x_fe52[mgi] = v[3];
+      m->x_cr48[mgi] = v[4];
+      m->x_ni57[mgi] = v[5];
+      m->x_co57[mgi] = v[6];
+      if (items == 10) {  // custom columns follow, and nothing after them (grid.cc:1328-1354)
+        std::istringstream ss(line);
+        double x;
+        for (int i = 0; i < 10 + m->n_custom_columns; i++)
+          if (!(ss >> x)) rc = ARTIS_ERR_BAD_ARGUMENT;
+        if (ss >> x) rc = ARTIS_ERR_BAD_ARGUMENT;
+      }
+      mgi++;
+    }
+    if (rc == 0 && mgi == npts) m->vmax = m->vout[npts - 1];
+  } else {
+    m->pos_model = (float *)std::calloc((size_t)npts * 3, sizeof(float));
+    const double xmax_tmodel = m->vmax * m->t_model;
+    const int n = m->ncoord_model[0];
+    bool posmatch_xyz = true, posmatch_zyx = true;
+    while (rc == 0 && mgi < npts && std::getline(in, line)) {
+      int mgi_in = 0;
+      float pos[3] = {0, 0, 0}, rho = 0;
+      if (std::sscanf(line.c_str(), "%d %g %g %g %g", &mgi_in, &pos[0], &pos[1], &pos[2], &rho) != 5 ||
+          mgi_in != mgi + 1 || rho < 0) {
+        rc = ARTIS_ERR_BAD_ARGUMENT;
+        break;
+      }
+      const int coord[3] = {mgi % n, (mgi / n) % n, mgi / (n * n)};  // get_cellcoordpointnum (grid.cc:172-199)
+      for (int axis = 0; axis < 3; axis++) {
+        const double cellwidth = 2 * xmax_tmodel / n;
+        const double expected = -xmax_tmodel + cellwidth * coord[axis];
+        if (std::fabs(expected - pos[axis]) > 0.5 * cellwidth) posmatch_xyz = false;
+        if (std::fabs(expected - pos[2 - axis]) > 0.5 * cellwidth) posmatch_zyx = false;
+        m->pos_model[(size_t)mgi * 3 + axis] = pos[axis];
+      }
+      m->rho_model[mgi] = rho;
+      if (!std::getline(in, line) || !model_abundance_line(line, m, mgi, rho > 0)) {
+        rc = ARTIS_ERR_BAD_ARGUMENT;
+        break;
+      }
+      mgi++;
+    }
+    if (rc == 0 && !(posmatch_xyz ^ posmatch_zyx)) rc = ARTIS_ERR_BAD_ARGUMENT;  // grid.cc:1586
+    m->posorder_zyx = posmatch_zyx ? 1 : 0;
+  }
+  if (rc == 0 && mgi != npts) rc = ARTIS_ERR_BAD_ARGUMENT;
+  if (rc) artis_free_model(m);
+  return rc;
+}
+
+// grid.cc:1007-1073 abundances_read
+int artis_read_abundances(const char *filename, int npts_model, int model_type, int nelements,
+                          const int32_t *anumber, float *elem_abund) {
+  if (!filename || npts_model <= 0 || nelements < 0 || (nelements > 0 && (!anumber || !elem_abund)))
+    return ARTIS_ERR_BAD_ARGUMENT;
+  std::ifstream in(filename);
+  if (!in.is_open()) return ARTIS_ERR_BAD_ARGUMENT;
+  std::string line;
+  for (int mgi = 0; mgi < npts_model; mgi++) {
+    if (!noncomment_line(in, line)) return ARTIS_ERR_BAD_ARGUMENT;
+    std::istringstream ss(line);
+    int cellnumberinput = -1;
+    if (!(ss >> cellnumberinput) || cellnumberinput != mgi + 1) return ARTIS_ERR_BAD_ARGUMENT;
+    double normfactor = 0.;
+    float abundances_in[150] = {0.f};
+    for (int z = 1; z <= 150; z++) {
+      abundances_in[z - 1] = 0.;
+      if (!(ss >> abundances_in[z - 1])) {
+        if (z == 1) return ARTIS_ERR_BAD_ARGUMENT;  // at least hydrogen
+        break;
+      }
+      if (abundances_in[z - 1] < 0.) return ARTIS_ERR_BAD_ARGUMENT;
+      normfactor += abundances_in[z - 1];
+    }
+    if (model_type == 3 || normfactor <= 0.) normfactor = 1.;
+    for (int e = 0; e < nelements; e++) {
+      const int z = anumber[e];
+      elem_abund[(size_t)mgi * nelements + e] = (z >= 1 && z <= 150) ? (float)(abundances_in[z - 1] / normfactor) : 0.f;
+    }
+  }
+  return 0;
+}
 
 // packet.cc:152-196
 int artis_write_packets(const char *filename, const artis_packet *pkt, int npkts) {

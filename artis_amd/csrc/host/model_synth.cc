@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "artis_constants.h"
+#include "artis_io.h"
 
 namespace {
 
@@ -72,6 +73,11 @@ struct Model {
   std::vector<float> mgi_X;          // [npts_model * nelements]
   std::vector<int32_t> mgi_tclass;
   std::vector<double> tclass_T;
+  // model read from the reference's input files (artis_model_from_files) instead of the synthetic profile
+  bool from_files = false;
+  artis_input_params inp{};
+  std::vector<double> mgi_ffegrp, mgi_ni56, mgi_rpos;  // model.txt X_Fegroup / X_Ni56; mean radial pos at tmin
+  double kappagrey_norm = 1.;                           // (0.9 mfeg / mtot) + 0.1 of calculate_kappagrey
   double tmin = 0, tmax = 0, vmax = 0, rmax = 0;
   artis_geometry geom{};
 
@@ -567,6 +573,8 @@ void build_atomic(Model &m, std::mt19937_64 &rng) {
   a.coolinglist_upperlevel = m.cool_upper.data();
 }
 
+void finish_geometry(Model &m);
+
 void build_grid(Model &m) {
   const artis_synth_config &c = m.cfg;
   m.tmin = c.tmin_days * ARTIS_DAY;
@@ -651,7 +659,109 @@ void build_grid(Model &m) {
     }
   }
 
-  // logarithmic timesteps (input.cc:2236-2243)
+  finish_geometry(m);
+}
+
+// Grid from the reference's model.txt / abundances.txt: uniform_grid_setup (grid.cc:2028-2102) with
+// map_1dmodeltogrid (grid.cc:910-940) or map_3dmodeltogrid (grid.cc:988-1005), densities scaled to tmin
+// (grid.cc:1302, 1565), and the masses of calc_totmassradionuclides (grid.cc:1602-1655) for kappagrey.
+int build_grid_from_model(Model &m, const artis_ejecta_model &em, const std::vector<float> &abund) {
+  artis_synth_config &c = m.cfg;
+  m.tmin = m.inp.tmin_days * ARTIS_DAY;
+  m.tmax = m.inp.tmax_days * ARTIS_DAY;
+  m.vmax = em.vmax;
+  m.rmax = m.vmax * m.tmin;
+  if (!(m.vmax > 0) || sqrt(3 * m.vmax * m.vmax) >= ARTIS_CLIGHT) return ARTIS_ERR_BAD_ARGUMENT;  // grid.cc:2035
+  if (em.model_type == 3) c.ngrid_1d = em.ncoord_model[0];
+  const int n = c.ngrid_1d;
+  m.ngrid = n * n * n;
+  const double coordmax[3] = {m.rmax, m.rmax, m.rmax};
+  m.cell_pos_min.resize((size_t)m.ngrid * 3);
+  for (int idx = 0; idx < m.ngrid; idx++) {
+    const int nxyz[3] = {idx % n, (idx / n) % n, (idx / (n * n)) % n};
+    for (int ax = 0; ax < 3; ax++)
+      m.cell_pos_min[(size_t)idx * 3 + ax] = -coordmax[ax] + (2 * nxyz[ax] * coordmax[ax] / n);
+  }
+  const double wid = 2 * coordmax[0] / n;
+  auto radialpos = [&](int idx) {  // get_cellradialpos: distance of the cell centre at tmin
+    double d[3];
+    for (int ax = 0; ax < 3; ax++) d[ax] = m.cell_pos_min[(size_t)idx * 3 + ax] + 0.5 * wid;
+    return sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+  };
+  const int np = em.npts_model;
+  m.npts_model = np;
+  m.mgi_rho_tmin.assign(np, 0.);
+  m.mgi_vel.assign(np, 0.);
+  m.mgi_X.assign((size_t)np * 3, 0.f);
+  m.mgi_tclass.assign(np, 0);
+  m.mgi_ffegrp.assign(np, 0.);
+  m.mgi_ni56.assign(np, 0.);
+  m.mgi_rpos.assign(np, 0.);
+  const double tratio3 = pow(em.t_model / m.tmin, 3);
+  for (int mgi = 0; mgi < np; mgi++) {
+    m.mgi_rho_tmin[mgi] = em.rho_model[mgi] * tratio3;
+    m.mgi_ffegrp[mgi] = em.ffegrp[mgi];
+    m.mgi_ni56[mgi] = em.x_ni56[mgi];
+    for (int e = 0; e < 3; e++) m.mgi_X[(size_t)mgi * 3 + e] = abund[(size_t)mgi * 3 + e];
+  }
+  std::vector<int> nassoc(np, 0);
+  m.cell_mgi.assign(m.ngrid, np);
+  for (int idx = 0; idx < m.ngrid; idx++) {
+    const double rpos = radialpos(idx);
+    int mgi = np;
+    if (em.model_type == 1) {
+      if (rpos < m.rmax) {
+        const double vcell = rpos / m.tmin;
+        mgi = 0;
+        for (int i = 0; i < np - 1; i++)
+          if (em.vout[mgi] < vcell) mgi = i + 1;
+        if (!(em.vout[mgi] >= 0. && m.mgi_rho_tmin[mgi] > 0)) mgi = np;
+      }
+    } else {
+      mgi = (m.mgi_rho_tmin[idx] > 0) ? idx : np;
+    }
+    m.cell_mgi[idx] = mgi;
+    if (mgi < np) {
+      m.mgi_rpos[mgi] += rpos;
+      nassoc[mgi]++;
+    }
+  }
+  for (int mgi = 0; mgi < np; mgi++) {
+    if (nassoc[mgi] > 0) m.mgi_rpos[mgi] /= nassoc[mgi];
+    // the cell-state stand-in's temperature class: velocity of the shell middle (1D) or the cell centre (3D)
+    m.mgi_vel[mgi] = (em.model_type == 1) ? 0.5 * ((mgi > 0 ? em.vout[mgi - 1] : 0.) + em.vout[mgi])
+                                          : radialpos(mgi) / m.tmin;
+  }
+  // calc_totmassradionuclides: mtot and mfeg over the model cells with rho > 0
+  double mtot = 0., mfeg = 0.;
+  for (int mgi = 0; mgi < np; mgi++) {
+    if (m.mgi_rho_tmin[mgi] <= 0.) continue;
+    double vol;
+    if (em.model_type == 1) {
+      const double v_inner = (mgi == 0) ? 0. : em.vout[mgi - 1];
+      vol = (pow(em.vout[mgi], 3) - pow(v_inner, 3)) * 4 * ARTIS_PI * pow(m.tmin, 3) / 3.;
+    } else {
+      vol = pow((2 * m.vmax * m.tmin), 3.) / (n * n * n);
+    }
+    mtot += m.mgi_rho_tmin[mgi] * vol;
+    mfeg += m.mgi_rho_tmin[mgi] * vol * m.mgi_ffegrp[mgi];
+  }
+  m.kappagrey_norm = (mtot > 0.) ? (0.9 * mfeg / mtot) + 0.1 : 1.;
+  const int ntc = std::max(1, c.n_tclasses);
+  m.tclass_T.resize(ntc);
+  for (int k = 0; k < ntc; k++) {
+    const double v = (k + 0.5) / ntc * m.vmax;
+    m.tclass_T[k] = c.T0 * (1. + 0.5 * exp(-v / 5e8));
+  }
+  for (int mgi = 0; mgi < np; mgi++)
+    m.mgi_tclass[mgi] = std::min(ntc - 1, std::max(0, (int)(m.mgi_vel[mgi] / m.vmax * ntc)));
+  return 0;
+}
+
+// time grid and geometry record shared by both grid builders (input.cc:2236-2243)
+void finish_geometry(Model &m) {
+  const artis_synth_config &c = m.cfg;
+  const int n = c.ngrid_1d;
   m.ts_start.resize(c.ntstep);
   m.ts_width.resize(c.ntstep);
   m.ts_mid.resize(c.ntstep);
@@ -661,7 +771,6 @@ void build_grid(Model &m) {
     m.ts_mid[i] = m.tmin * exp((i + 0.5) * dlogt);
     m.ts_width[i] = (m.tmin * exp((i + 1) * dlogt)) - m.ts_start[i];
   }
-
   artis_geometry &g = m.geom;
   g.grid_type = ARTIS_GRID_UNIFORM;
   g.ncoordgrid[0] = g.ncoordgrid[1] = g.ncoordgrid[2] = n;
@@ -670,7 +779,7 @@ void build_grid(Model &m) {
   g.cell_pos_min = m.cell_pos_min.data();
   g.cell_mgi = m.cell_mgi.data();
   g.modelcell_wid_init = nullptr;
-  for (int ax = 0; ax < 3; ax++) g.coordmax[ax] = coordmax[ax];
+  for (int ax = 0; ax < 3; ax++) g.coordmax[ax] = m.rmax;
   g.tmin = m.tmin;
   g.tmax = m.tmax;
   g.rmax = m.rmax;
@@ -763,7 +872,8 @@ void compute_cellstate(Model &m, int nts) {
     if (!(rho > 0)) continue;
     const int k = m.mgi_tclass[mgi];
     const float T = (float)m.tclass_T[k];
-    m.Te[mgi] = m.TR[mgi] = m.TJ[mgi] = T;
+    m.Te[mgi] = m.TR[mgi] = T;
+    m.TJ[mgi] = (m.cfg.tj_scale > 0.) ? (float)(m.cfg.tj_scale * T) : T;
     m.W[mgi] = 1.f;
     m.rho[mgi] = (float)rho;
     double nntot_e[8], nnetot = 0.;
@@ -814,7 +924,20 @@ void compute_cellstate(Model &m, int nts) {
     // Fe-group fraction stand-in (the 56Ni-rich core of a W7-like model) and the grey opacity of opacity_case 4
     // style kappagrey = GREY_OP (0.9 ffegrp + 0.1) (grid.cc:629); a cell is thick when its grey optical depth
     // across one cell width exceeds thick_tau (input.txt cell_is_optically_thick)
-    {
+    if (m.from_files) {
+      // model.txt X_Fegroup; calculate_kappagrey opacity_case 4 (grid.cc:670-673); the grey-depth thick-cell
+      // rule of update_grid_cell (update_grid.cc:1162-1197, 1209-1212)
+      m.ffegrp[mgi] = (float)m.mgi_ffegrp[mgi];
+      m.kappagrey[mgi] = (float)(((0.9 * m.mgi_ffegrp[mgi]) + 0.1) * ARTIS_GREY_OP / m.kappagrey_norm);
+      const double tratmid = t / m.tmin;
+      if (m.inp.opacity_case == 4) {
+        const double radial_pos = m.mgi_rpos[mgi] * tratmid;
+        const double grey_optical_depth = (double)m.kappagrey[mgi] * (double)m.rho[mgi] * (m.rmax * tratmid - radial_pos);
+        if (grey_optical_depth > m.inp.cell_is_optically_thick && nts < m.inp.num_grey_timesteps) m.thick[mgi] = 1;
+      } else {
+        m.thick[mgi] = 1;
+      }
+    } else {
       const double v = m.mgi_vel[mgi];
       m.ffegrp[mgi] = (float)(0.2 + 0.6 * exp(-(v / 6e8) * (v / 6e8)));
       m.kappagrey[mgi] = (float)(0.1 * (0.9 * m.ffegrp[mgi] + 0.1));
@@ -847,7 +970,8 @@ void compute_cellstate(Model &m, int nts) {
       const double ng = groundpop(e, ui);
       if (l == 0) return ng;
       nn = ng * 1. * m.level_stat_weight[off + l] / m.level_stat_weight[off] *
-           exp(-(m.level_epsilon[off + l] - m.level_epsilon[off]) / ARTIS_KB / m.TJ[mgi]);
+           exp(-(m.level_epsilon[off + l] - m.level_epsilon[off]) / ARTIS_KB /
+               (m.cfg.excitation_te ? m.Te[mgi] : m.TJ[mgi]));
       if (nn < ARTIS_MINPOP) nn = m.elem_abundance[(size_t)mgi * ne + e] > 0 ? ARTIS_MINPOP : 0.;
       return nn;
     };
@@ -1018,6 +1142,43 @@ void artis_synth_default_config(artis_synth_config *cfg) {
   cfg->instant_particle_deposition = 1;
   cfg->n_kpktdiffusion_timesteps = 0;
   cfg->kpktdiffusion_timescale = 0.;
+  cfg->excitation_te = 0;
+  cfg->tj_scale = 0.;
+}
+
+artis_model *artis_model_from_files(const artis_synth_config *cfg, const char *input_txt, const char *model_txt,
+                                    const char *abundances_txt) {
+  artis_model *m = new artis_model();
+  m->cfg = *cfg;
+  m->from_files = true;
+  artis_ejecta_model em{};
+  if (artis_read_input_file(input_txt, &m->inp) != 0 ||
+      (m->inp.model_type != 1 && m->inp.model_type != 3) ||
+      artis_read_model(model_txt, m->inp.model_type, &em) != 0) {
+    delete m;
+    return nullptr;
+  }
+  m->cfg.ntstep = m->inp.ntstep;
+  m->cfg.tmin_days = m->inp.tmin_days;
+  m->cfg.tmax_days = m->inp.tmax_days;
+  if (m->inp.pre_zseed > 0) m->cfg.seed = m->inp.pre_zseed;
+  m->cfg.n_kpktdiffusion_timesteps = m->inp.n_kpktdiffusion_timesteps;
+  m->cfg.kpktdiffusion_timescale = m->inp.kpktdiffusion_timescale;
+  std::mt19937_64 rng(m->cfg.seed);
+  build_atomic(*m, rng);
+  std::vector<float> abund((size_t)em.npts_model * m->nelements, 0.f);
+  int rc = artis_read_abundances(abundances_txt, em.npts_model, em.model_type, m->nelements, m->elem_anumber.data(),
+                                 abund.data());
+  if (rc == 0) rc = build_grid_from_model(*m, em, abund);
+  artis_free_model(&em);
+  if (rc != 0) {
+    delete m;
+    return nullptr;
+  }
+  finish_geometry(*m);
+  compute_cellstate(*m, 0);
+  rebuild_gamma_spectra(*m);
+  return m;
 }
 
 artis_model *artis_model_synth(const artis_synth_config *cfg) {
@@ -1036,6 +1197,7 @@ const artis_atomic_tables *artis_model_atomic(const artis_model *m) { return &m-
 const artis_geometry *artis_model_geometry(const artis_model *m) { return &m->geom; }
 const artis_cell_state *artis_model_cellstate(const artis_model *m) { return &m->cs; }
 int64_t artis_model_npts_model(const artis_model *m) { return m->npts_model; }
+void artis_model_config(const artis_model *m, artis_synth_config *out) { *out = m->cfg; }
 
 void artis_model_run_params(const artis_model *m, artis_run_params *p) {
   std::memset(p, 0, sizeof(*p));
@@ -1053,6 +1215,13 @@ void artis_model_run_params(const artis_model *m, artis_run_params *p) {
   p->gamma_grey = -1.;       // test configs: "use grey opacity for gammas? -1"
   p->instant_particle_deposition = m->cfg.instant_particle_deposition;
   p->nt_solve_spencerfano = 0;
+  p->excitation_temperature = m->cfg.excitation_te ? ARTIS_TEXC_TE : ARTIS_TEXC_TJ;
+  if (m->from_files) {  // input.txt run switches (input.cc:1976-1992, 2013, 2130)
+    p->opacity_case = m->inp.opacity_case;
+    p->do_r_lc = m->inp.do_r_lc;
+    p->do_rlc_est = m->inp.do_rlc_est;
+    p->gamma_grey = m->inp.gamma_grey;
+  }
 }
 
 int artis_model_set_gamma_lines(artis_model *m, int nuc, int nlines, const double *energy_mev, const double *prob) {
@@ -1078,7 +1247,10 @@ int artis_model_init_pellets(const artis_model *m, int npkts, uint64_t seed, dou
     const int mgi = m->cell_mgi[c];
     if (mgi < m->npts_model) {
       const double v = m->mgi_vel[mgi];
-      acc += m->mgi_rho_tmin[mgi] * 0.6 * exp(-(v / 6e8) * (v / 6e8));
+      if (m->from_files)
+        acc += m->mgi_rho_tmin[mgi] * m->mgi_ni56[mgi];  // model.txt X_Ni56
+      else
+        acc += m->mgi_rho_tmin[mgi] * 0.6 * exp(-(v / 6e8) * (v / 6e8));
     }
     cdf[c] = acc;
   }

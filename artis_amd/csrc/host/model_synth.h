@@ -37,12 +37,20 @@ typedef struct artis_synth_config {
   int32_t instant_particle_deposition; /* INSTANT_PARTICLE_DEPOSITION (default 1, artisoptions_classic.h:222) */
   int32_t n_kpktdiffusion_timesteps;   /* input.txt "kpktdiffusion_timescale n_kpktdiffusion_timesteps"; the  */
   double kpktdiffusion_timescale;      /* reference test inputs use 0.001 1000 (default here: 0 0)         */
+  int32_t excitation_te;     /* run parameter excitation_temperature: 0 T_J (classic), 1 T_e (kilonova, nebular) */
+  double tj_scale;           /* T_J = tj_scale * T_e in the cell-state stand-in (0 = 1: T_J == T_e, as in the LTE
+                                timesteps, update_grid.cc:1111-1114) */
 } artis_synth_config;
 
 typedef struct artis_model artis_model;
 
 void artis_synth_default_config(artis_synth_config *cfg);
 artis_model *artis_model_synth(const artis_synth_config *cfg);
+/* The reference's own run inputs: input.txt (times, seed, run switches), model.txt (1D or 3D) and
+ * abundances.txt (Fe/Co/Ni mass fractions), read by include/artis_io.h; the atomic data stay synthetic (cfg),
+ * cfg->ngrid_1d is CUBOID_NCOORDGRID for 1D models.  NULL on a malformed file. */
+artis_model *artis_model_from_files(const artis_synth_config *cfg, const char *input_txt, const char *model_txt,
+                                    const char *abundances_txt);
 void artis_model_free(artis_model *m);
 
 const artis_atomic_tables *artis_model_atomic(const artis_model *m);
@@ -59,6 +67,8 @@ int artis_model_init_rpackets(const artis_model *m, int nts, int npkts, uint64_t
                               artis_packet *out);
 
 int64_t artis_model_npts_model(const artis_model *m);
+/* the configuration the model was built with (after artis_model_from_files adopted input.txt's values) */
+void artis_model_config(const artis_model *m, artis_synth_config *out);
 
 /* Gamma-ray line spectrum of stand-in nuclide `nuc` (energies in MeV, photons per decay), as read by
  * read_gamma_spectrum (gammapkt.cc:58-89); nucdecayenergygamma = sum E p.  Nuclides (decay.cc stand-in):

@@ -76,7 +76,12 @@ class RunParams(C.Structure):
         ("gamma_grey", C.c_double),
         ("instant_particle_deposition", C.c_int32),
         ("nt_solve_spencerfano", C.c_int32),
+        ("excitation_temperature", C.c_int32),
     ]
+
+
+TEXC_TJ = 0
+TEXC_TE = 1
 
 
 class Estimators(C.Structure):
@@ -129,6 +134,8 @@ class SynthConfig(C.Structure):
         ("instant_particle_deposition", C.c_int32),
         ("n_kpktdiffusion_timesteps", C.c_int32),
         ("kpktdiffusion_timescale", C.c_double),
+        ("excitation_te", C.c_int32),
+        ("tj_scale", C.c_double),
     ]
 
 

@@ -24,6 +24,8 @@ def model_lib():
         lib.artis_synth_default_config.argtypes = [C.POINTER(ffi.SynthConfig)]
         lib.artis_model_synth.argtypes = [C.POINTER(ffi.SynthConfig)]
         lib.artis_model_synth.restype = C.c_void_p
+        lib.artis_model_from_files.argtypes = [C.POINTER(ffi.SynthConfig), C.c_char_p, C.c_char_p, C.c_char_p]
+        lib.artis_model_from_files.restype = C.c_void_p
         lib.artis_model_free.argtypes = [C.c_void_p]
         for fn in ("artis_model_atomic", "artis_model_geometry", "artis_model_cellstate"):
             getattr(lib, fn).argtypes = [C.c_void_p]
@@ -36,6 +38,7 @@ def model_lib():
         lib.artis_model_gamma_spectra.restype = C.c_void_p
         lib.artis_model_init_pellets.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.c_double, C.c_double, C.c_double,
                                                  C.c_void_p]
+        lib.artis_model_config.argtypes = [C.c_void_p, C.POINTER(ffi.SynthConfig)]
         lib.artis_model_npts_model.argtypes = [C.c_void_p]
         lib.artis_model_npts_model.restype = C.c_int64
         _model_lib = lib
@@ -51,12 +54,35 @@ def default_config(**overrides):
 
 
 class Model:
-    """Owns one synthetic model; exposes the raw C struct pointers for the engine and the oracle."""
+    """Owns one model; exposes the raw C struct pointers for the engine and the oracle.
 
-    def __init__(self, cfg=None, **overrides):
+    Synthetic by default; with files=(input.txt, model.txt, abundances.txt) the run
+    parameters, time grid, ejecta model and abundances come from the reference's own input files
+    (artis_model_from_files), with synthetic atomic data.  A model.txt.xz is decompressed next to a temp copy.
+    """
+
+    def __init__(self, cfg=None, files=None, **overrides):
         self.cfg = cfg if cfg is not None else default_config(**overrides)
         self._lib = model_lib()
-        self._h = self._lib.artis_model_synth(C.byref(self.cfg))
+        self._tmp = None
+        if files is not None:
+            inp, mod, ab = (os.fspath(f) for f in files)
+            if mod.endswith(".xz"):
+                import lzma
+                import tempfile
+
+                self._tmp = tempfile.TemporaryDirectory()
+                plain = os.path.join(self._tmp.name, "model.txt")
+                with lzma.open(mod, "rb") as fin, open(plain, "wb") as fout:
+                    fout.write(fin.read())
+                mod = plain
+            self._h = self._lib.artis_model_from_files(C.byref(self.cfg), inp.encode(), mod.encode(), ab.encode())
+            if not self._h:
+                raise RuntimeError(f"artis_model_from_files({inp}, {mod}, {ab}) failed")
+            # the C side adopted ntstep / times / seed from input.txt: mirror them in self.cfg
+            self._lib.artis_model_config(self._h, C.byref(self.cfg))
+        else:
+            self._h = self._lib.artis_model_synth(C.byref(self.cfg))
         if not self._h:
             raise RuntimeError("artis_model_synth failed")
         self.atomic = self._lib.artis_model_atomic(self._h)

@@ -16,6 +16,7 @@
 #define ARTIS_ME 9.1093897e-28
 #define ARTIS_QE 4.80325E-10
 #define ARTIS_PI 3.1415926535987
+#define ARTIS_GREY_OP 0.1 /* globals.h:266 GREY_OP [cm^2/g] */
 #define ARTIS_EV 1.6021772e-12
 #define ARTIS_MEV 1.6021772e-6
 #define ARTIS_DAY 86400.0

@@ -254,7 +254,11 @@ typedef struct artis_run_params {
   double gamma_grey;           /* input.txt "use grey opacity for gammas?" (input.cc:1992); < 0: full treatment */
   int32_t instant_particle_deposition; /* INSTANT_PARTICLE_DEPOSITION (update_packets.cc:23) */
   int32_t nt_solve_spencerfano;/* NT_ON && NT_SOLVE_SPENCERFANO (nonthermal.cc:1883): not propagated here */
+  int32_t excitation_temperature; /* LTEPOP_EXCITATIONTEMPERATURE of calculate_levelpop_lte (ltepop.cc:338):
+                                     ARTIS_TEXC_TJ (artisoptions_classic.h:32) or ARTIS_TEXC_TE
+                                     (artisoptions_kilonova_lte.h:36, artisoptions_nltenebular.h:36) */
 } artis_run_params;
+enum artis_excitation_temperature { ARTIS_TEXC_TJ = 0, ARTIS_TEXC_TE = 1 };
 
 /* ------------------------------------------------------------------------------------------------------------ */
 /* Accumulators (reference radfield J/nuJ, globals::*estimator, time_step[nts].*, ecounter/acounter, stats).  */
@@ -427,8 +431,9 @@ int64_t artis_gpu_last_rounds(void);  /* event-queue rounds of the last update (
  * [0] r-packet, [1] macro-atom (incl. cell binning), [2] k-packet, [3] classify */
 int artis_gpu_last_kernel_times(double ms[4], int64_t launches[4]);
 const char *artis_gpu_last_error(void);
-#define ARTIS_GPU_ABI_VERSION 3  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
-                                    3: virtual packets (artis_vpkt_params / artis_vpkt_result) */
+#define ARTIS_GPU_ABI_VERSION 4  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
+                                    3: virtual packets (artis_vpkt_params / artis_vpkt_result);
+                                    4: artis_run_params.excitation_temperature */
 int artis_gpu_abi_version(void);
 
 #ifdef __cplusplus

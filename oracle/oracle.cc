@@ -243,10 +243,11 @@ double get_groundlevelpop(const Ctx &c, int mgi, int e, int i) {
   }
   return nn;
 }
-// ltepop.cc:329-347 (T_exc = T_J, artisoptions_classic.h:31)
+// ltepop.cc:329-347; T_exc = LTEPOP_EXCITATIONTEMPERATURE (ltepop.cc:338): T_J in artisoptions_classic.h:32,
+// T_e in artisoptions_kilonova_lte.h:36 / artisoptions_nltenebular.h:36
 double calculate_levelpop_lte(const Ctx &c, int mgi, int e, int i, int l) {
   if (l == 0) return get_groundlevelpop(c, mgi, e, i);
-  const double T_exc = c.cs->TJ[mgi];
+  const double T_exc = (c.rp.excitation_temperature == ARTIS_TEXC_TE) ? c.cs->Te[mgi] : c.cs->TJ[mgi];
   const double W = 1.;
   const double E_level = epsilon(c, e, i, l);
   const double E_ground = epsilon(c, e, i, 0);
