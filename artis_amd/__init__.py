@@ -25,9 +25,27 @@ ABI_SYMBOLS = [
     "artis_gpu_estimator_block_from_device", "artis_gpu_last_transport_ms", "artis_gpu_last_precompute_ms",
     "artis_gpu_last_work_counts", "artis_gpu_last_rounds", "artis_gpu_spectrum", "artis_gpu_last_kernel_times", "artis_gpu_last_error", "artis_gpu_abi_version",
     "artis_gpu_vpkt_init", "artis_gpu_vpkt_zero", "artis_gpu_vpkt_download", "artis_gpu_vpkt_last_stats", "artis_gpu_vpkt_last_work",
+    "artis_estimator_block_len", "artis_estimator_block_pack", "artis_estimator_block_unpack",
+    "artis_gpu_comm_unique_id", "artis_gpu_comm_init", "artis_gpu_estimators_allreduce", "artis_gpu_comm_finalize",
 ]
 
 _gpu_lib = None
+
+
+def engine_src_sha():
+    """sha256 (16 hex) of the engine's sources (artis_amd/csrc/engine/*, include/*.h): keys committed profiles
+    (profiles/pmc_*.json) to the code they measured -- the GPU box gets the tree without .git."""
+    import hashlib
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    h = hashlib.sha256()
+    for d in (os.path.join(repo, "artis_amd", "csrc", "engine"), os.path.join(repo, "include")):
+        for f in sorted(os.listdir(d)):
+            if f.endswith((".hip", ".h")):
+                h.update(f.encode())
+                with open(os.path.join(d, f), "rb") as fh:
+                    h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def gpu_lib():
@@ -59,12 +77,28 @@ def gpu_lib():
         L.artis_gpu_vpkt_download.argtypes = [C.POINTER(ffi.VpktResult), C.c_int]
         L.artis_gpu_vpkt_last_stats.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
         L.artis_gpu_vpkt_last_work.argtypes = [C.POINTER(C.c_int64)]
+        L.artis_estimator_block_len.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int]
+        L.artis_estimator_block_len.restype = C.c_size_t
+        L.artis_estimator_block_pack.argtypes = [C.POINTER(ffi.Estimators), C.c_int, C.c_int, C.c_int, C.c_int, vp]
+        L.artis_estimator_block_unpack.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(ffi.Estimators)]
+        L.artis_gpu_comm_unique_id.argtypes = [vp]
+        L.artis_gpu_comm_init.argtypes = [C.c_int, C.c_int, vp]
+        L.artis_gpu_comm_finalize.restype = None
         _gpu_lib = L
     return _gpu_lib
 
 
 class EngineError(RuntimeError):
     pass
+
+
+def comm_unique_id():
+    """ncclGetUniqueId on this process (rank 0), as bytes to hand to every rank."""
+    buf = C.create_string_buffer(ffi.COMM_ID_BYTES)
+    rc = gpu_lib().artis_gpu_comm_unique_id(buf)
+    if rc != 0:
+        raise EngineError(f"artis_gpu_comm_unique_id -> {rc}: {gpu_lib().artis_gpu_last_error().decode()}")
+    return buf.raw
 
 
 class Engine:
@@ -190,6 +224,14 @@ class Engine:
         nl = (C.c_int64 * 4)()
         self.lib.artis_gpu_last_kernel_times(ms, nl)
         return {k: (ms[i], nl[i]) for i, k in enumerate(("rpkt", "ma", "kpkt", "classify"))}
+
+    # multi-GPU (RCCL): one communicator per engine, the packed estimator block all-reduced in HBM
+    def comm_init(self, rank, nranks, uid):
+        buf = C.create_string_buffer(bytes(uid), ffi.COMM_ID_BYTES)
+        self._check(self.lib.artis_gpu_comm_init(int(rank), int(nranks), buf), "comm_init")
+
+    def allreduce_estimators(self):
+        self._check(self.lib.artis_gpu_estimators_allreduce(), "estimators_allreduce")
 
     def last_rounds(self):
         return int(self.lib.artis_gpu_last_rounds())

@@ -10,6 +10,7 @@
 //     the estimator sums added into the caller's arrays.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cfloat>
@@ -505,6 +506,10 @@ struct Engine {
   double last_vpkt_ms = 0.;
   int64_t last_vpkt_work[4] = {0, 0, 0, 0};
   int64_t last_vpkt_spawns = 0, last_vpkt_traces = 0;
+  // RCCL communicator of this rank (artis_gpu_comm_init) and the packed block it all-reduces
+  ncclComm_t comm = nullptr;
+  int comm_ranks = 0;
+  double *d_redblock = nullptr;
   std::string last_error;
 };
 Engine G;
@@ -552,31 +557,62 @@ int check_kernel_error(const char *what) {
   return 0;
 }
 
+// Device allocation with an optional injected failure (ARTIS_GPU_FAIL_ALLOC_ABOVE=<bytes>: any single request
+// above that size fails as out-of-memory) so the error paths can be tested.
+hipError_t dmalloc(void **p, size_t bytes) {
+  *p = nullptr;
+  if (const char *lim = getenv("ARTIS_GPU_FAIL_ALLOC_ABOVE"))
+    if (bytes > (size_t)strtoull(lim, nullptr, 10)) return hipErrorOutOfMemory;
+  return hipMalloc(p, bytes);
+}
+
+template <typename T>
+void dfree(T *&p) {
+  if (p) (void)hipFree((void *)p);
+  p = nullptr;
+}
+
+// packet store + per-packet side state; after this every pointer is null and the capacity zero
+void free_packets() {
+  dfree(G.d_soa);
+  dfree(G.d_aos);
+  dfree(G.d_snapshot);
+  G.have_snapshot = false;
+  dfree(G.W.rng_n);
+  dfree(G.W.pend);
+  dfree(G.W.pend_jumps);
+  dfree(G.W.ma_key);
+  dfree(G.W.ma_sorted);
+  for (int q = 0; q < NQUEUES; q++) dfree(G.W.q[q]);
+  G.cap_pkts = 0;
+  G.npkts = 0;
+}
+
 int alloc_packets(int64_t n) {
   if (n <= G.cap_pkts) return 0;
-  if (G.d_soa) {
-    (void)hipFree(G.d_soa);
-    (void)hipFree(G.d_aos);
-    if (G.d_snapshot) (void)hipFree(G.d_snapshot);
-    G.d_snapshot = nullptr;
-    G.have_snapshot = false;
+  free_packets();
+  const size_t un = (size_t)n;
+  struct Req {
+    void **p;
+    size_t bytes;
+  };
+  std::vector<Req> reqs = {{(void **)&G.d_soa, un * PKT_WORDS * 8},
+                           {(void **)&G.d_aos, un * PKT_WORDS * 8},
+                           {(void **)&G.W.rng_n, un * sizeof(uint32_t)},
+                           {(void **)&G.W.pend, un * sizeof(int4)},
+                           {(void **)&G.W.pend_jumps, un * sizeof(uint32_t)},
+                           {(void **)&G.W.ma_key, un * sizeof(int32_t)},
+                           {(void **)&G.W.ma_sorted, un * sizeof(int32_t)}};
+  for (int q = 0; q < NQUEUES; q++) reqs.push_back({(void **)&G.W.q[q], un * sizeof(int32_t)});
+  const int nreq = (int)reqs.size();
+  for (int r = 0; r < nreq; r++) {
+    const hipError_t e = dmalloc(reqs[r].p, reqs[r].bytes);
+    if (e != hipSuccess) {
+      G.last_error = std::string("packet store allocation (") + std::to_string(n) + " packets): " + hipGetErrorString(e);
+      free_packets();
+      return ARTIS_ERR_HIP;
+    }
   }
-  if (G.W.rng_n) {
-    (void)hipFree(G.W.rng_n);
-    (void)hipFree(G.W.pend);
-    (void)hipFree(G.W.pend_jumps);
-    (void)hipFree(G.W.ma_key);
-    (void)hipFree(G.W.ma_sorted);
-    for (int q = 0; q < NQUEUES; q++) (void)hipFree(G.W.q[q]);
-  }
-  HIPCHK(hipMalloc(&G.d_soa, (size_t)n * PKT_WORDS * 8));
-  HIPCHK(hipMalloc(&G.d_aos, (size_t)n * PKT_WORDS * 8));
-  HIPCHK(hipMalloc(&G.W.rng_n, (size_t)n * sizeof(uint32_t)));
-  HIPCHK(hipMalloc(&G.W.pend, (size_t)n * sizeof(int4)));
-  HIPCHK(hipMalloc(&G.W.pend_jumps, (size_t)n * sizeof(uint32_t)));
-  HIPCHK(hipMalloc(&G.W.ma_key, (size_t)n * sizeof(int32_t)));
-  HIPCHK(hipMalloc(&G.W.ma_sorted, (size_t)n * sizeof(int32_t)));
-  for (int q = 0; q < NQUEUES; q++) HIPCHK(hipMalloc(&G.W.q[q], (size_t)n * sizeof(int32_t)));
   G.cap_pkts = n;
   return 0;
 }
@@ -657,10 +693,16 @@ int vpkt_prepare(int64_t n) {
   if (!G.K.V.on) return 0;
   int64_t cap = G.vpkt_cap_param > 0 ? G.vpkt_cap_param : std::max<int64_t>(16 * n, 1 << 20);
   cap = std::min<int64_t>(cap, 0x7fffffff / 2);
+  // k_vpkt's 32-bit fetch head runs over cap * nobs work items and overshoots by at most one wave per resident
+  // wave: keep that below 2^32 so the head cannot wrap onto items already traced
+  const int64_t overshoot = (int64_t)G.wave_grid * WAVE_BLOCK;
+  cap = std::min<int64_t>(cap, (((int64_t)1 << 32) - 1 - overshoot) / std::max(1, G.K.V.nobs));
   if ((uint32_t)cap > G.vpkt_spawn_cap) {
-    if (G.d_vpkt_spawn) (void)hipFree(G.d_vpkt_spawn);
-    G.d_vpkt_spawn = nullptr;
-    HIPCHK(hipMalloc(&G.d_vpkt_spawn, (size_t)cap * VPKT_SPAWN_WORDS * sizeof(double)));
+    dfree(G.d_vpkt_spawn);
+    G.vpkt_spawn_cap = 0;
+    G.K.V.spawn = nullptr;
+    G.K.V.cap = 0;
+    HIPCHK(dmalloc((void **)&G.d_vpkt_spawn, (size_t)cap * VPKT_SPAWN_WORDS * sizeof(double)));
     G.vpkt_spawn_cap = (uint32_t)cap;
   }
   G.K.V.spawn = G.d_vpkt_spawn;
@@ -746,7 +788,7 @@ int run_wavefront(int64_t n, int nts, double t2) {
       else
         k_ma<true, 1><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
     } else {
-      k_ma<false, 1><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+      k_ma<false, 1><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
     }
     TEND(1);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QM, 0, 2 * sizeof(uint32_t), G.stream));
@@ -828,10 +870,11 @@ int artis_gpu_spectrum(int nnubins, int nprocs, double *spec_flux, double *lc_lu
     delta[nnu] = exp(log(nu_min) + ((nnu + 1) * (dlognu))) - exp(log(nu_min) + (nnu * (dlognu)));
   const size_t nspec = (size_t)nt * nnubins;
   double *d = nullptr;
-  HIPCHK(hipMalloc(&d, (nspec + 2 * (size_t)nt + nnubins) * sizeof(double)));
+  HIPCHK(dmalloc((void **)&d, (nspec + 2 * (size_t)nt + nnubins) * sizeof(double)));
   double *d_spec = d, *d_lc = d + nspec, *d_lccmf = d_lc + nt, *d_delta = d_lccmf + nt;
-  int rc = 0;
-  if ((rc = sync_ctx()) == 0) {
+  // every step below may fail; the scratch is released on all paths
+  auto run = [&]() -> int {
+    if (int rc = sync_ctx()) return rc;
     HIPCHK(hipMemsetAsync(d, 0, (nspec + 2 * (size_t)nt) * sizeof(double), G.stream));
     HIPCHK(hipMemcpyAsync(d_delta, delta.data(), nnubins * sizeof(double), hipMemcpyHostToDevice, G.stream));
     if (G.npkts > 0)
@@ -842,7 +885,10 @@ int artis_gpu_spectrum(int nnubins, int nprocs, double *spec_flux, double *lc_lu
     HIPCHK(hipMemcpyAsync(lc_lum, d_lc, nt * sizeof(double), hipMemcpyDeviceToHost, G.stream));
     HIPCHK(hipMemcpyAsync(lc_lumcmf, d_lccmf, nt * sizeof(double), hipMemcpyDeviceToHost, G.stream));
     HIPCHK(hipStreamSynchronize(G.stream));
-  }
+    return 0;
+  };
+  const int rc = run();
+  (void)hipStreamSynchronize(G.stream);
   (void)hipFree(d);
   return rc;
 }
@@ -994,19 +1040,11 @@ int artis_gpu_last_work_counts(int64_t out[ARTIS_WORK_COUNT]) {
 
 void artis_gpu_finalize(void) {
   if (!G.initialised) return;
+  artis_gpu_comm_finalize();
+  dfree(G.d_redblock);
   for (void *p : G.allocs) (void)hipFree(p);
   G.allocs.clear();
-  if (G.d_soa) (void)hipFree(G.d_soa);
-  if (G.d_aos) (void)hipFree(G.d_aos);
-  if (G.d_snapshot) (void)hipFree(G.d_snapshot);
-  if (G.W.rng_n) {
-    (void)hipFree(G.W.rng_n);
-    (void)hipFree(G.W.pend);
-    (void)hipFree(G.W.pend_jumps);
-    (void)hipFree(G.W.ma_key);
-    (void)hipFree(G.W.ma_sorted);
-    for (int q = 0; q < NQUEUES; q++) (void)hipFree(G.W.q[q]);
-  }
+  free_packets();
   if (G.h_ctr) (void)hipHostFree(G.h_ctr);
   if (G.d_vpkt_spawn) (void)hipFree(G.d_vpkt_spawn);
   for (hipEvent_t e : G.vev) (void)hipEventDestroy(e);
@@ -1556,7 +1594,7 @@ int artis_gpu_packets_download(artis_packet *packets, int npkts) {
 
 int artis_gpu_packets_snapshot(void) {
   if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
-  if (!G.d_snapshot) HIPCHK(hipMalloc(&G.d_snapshot, (size_t)G.cap_pkts * PKT_WORDS * 8));
+  if (!G.d_snapshot) HIPCHK(dmalloc((void **)&G.d_snapshot, (size_t)G.cap_pkts * PKT_WORDS * 8));
   HIPCHK(hipMemcpyAsync(G.d_snapshot, G.d_soa, (size_t)G.npkts * PKT_WORDS * 8, hipMemcpyDeviceToDevice, G.stream));
   HIPCHK(hipStreamSynchronize(G.stream));
   G.have_snapshot = true;
@@ -1698,6 +1736,125 @@ int artis_gpu_estimator_block_from_device(const void *src) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(G.stream));
   return 0;
+}
+
+// host mirror of the device block (artis_gpu_estimator_block_to_device / estimators_download)
+size_t artis_estimator_block_len(int np, int ne, int mi, int nl) {
+  if (np < 0 || ne < 0 || mi < 0 || nl < 0) return 0;
+  return 5 * (size_t)np + 2 * (size_t)np * ne * mi + 10 + 2 * (size_t)nl + ARTIS_COUNTER_COUNT + 1;
+}
+
+int artis_estimator_block_pack(const artis_estimators *est, int np, int ne, int mi, int nl, double *b) {
+  if (!est || !b || np < 0 || ne < 0 || mi < 0 || nl < 0) return ARTIS_ERR_BAD_ARGUMENT;
+  const size_t ni = (size_t)np * ne * mi;
+  auto put = [&](const double *src, size_t n) {
+    for (size_t j = 0; j < n; j++) *b++ = src ? src[j] : 0.;
+  };
+  put(est->J, np);
+  put(est->nuJ, np);
+  put(est->ffheatingestimator, np);
+  put(est->colheatingestimator, np);
+  put(est->rpkt_emiss, np);
+  put(est->gammaestimator, ni);
+  put(est->bfheatingestimator, ni);
+  const double sc[10] = {est->cmf_lum,        est->gamma_dep,   est->positron_dep,        est->electron_dep,
+                         est->electron_emission, est->alpha_dep, est->alpha_emission,     est->gamma_emission,
+                         est->nt_energy_deposited, (double)est->pellet_decays};
+  put(sc, 10);
+  for (int j = 0; j < nl; j++) *b++ = est->ecounter ? est->ecounter[j] : 0.;
+  for (int j = 0; j < nl; j++) *b++ = est->acounter ? est->acounter[j] : 0.;
+  for (int j = 0; j < ARTIS_COUNTER_COUNT; j++) *b++ = (double)est->counters[j];
+  *b++ = (double)est->nesc;
+  return 0;
+}
+
+int artis_estimator_block_unpack(const double *b, int np, int ne, int mi, int nl, artis_estimators *est) {
+  if (!est || !b || np < 0 || ne < 0 || mi < 0 || nl < 0) return ARTIS_ERR_BAD_ARGUMENT;
+  const size_t ni = (size_t)np * ne * mi;
+  auto get = [&](double *dst, size_t n) {
+    if (dst)
+      for (size_t j = 0; j < n; j++) dst[j] = b[j];
+    b += n;
+  };
+  get(est->J, np);
+  get(est->nuJ, np);
+  get(est->ffheatingestimator, np);
+  get(est->colheatingestimator, np);
+  get(est->rpkt_emiss, np);
+  get(est->gammaestimator, ni);
+  get(est->bfheatingestimator, ni);
+  est->cmf_lum = b[0];
+  est->gamma_dep = b[1];
+  est->positron_dep = b[2];
+  est->electron_dep = b[3];
+  est->electron_emission = b[4];
+  est->alpha_dep = b[5];
+  est->alpha_emission = b[6];
+  est->gamma_emission = b[7];
+  est->nt_energy_deposited = b[8];
+  est->pellet_decays = (int64_t)llrint(b[9]);
+  b += 10;
+  for (int j = 0; j < nl; j++)
+    if (est->ecounter) est->ecounter[j] = (int32_t)llrint(b[j]);
+  b += nl;
+  for (int j = 0; j < nl; j++)
+    if (est->acounter) est->acounter[j] = (int32_t)llrint(b[j]);
+  b += nl;
+  for (int j = 0; j < ARTIS_COUNTER_COUNT; j++) est->counters[j] = (int64_t)llrint(b[j]);
+  est->nesc = (int64_t)llrint(b[ARTIS_COUNTER_COUNT]);
+  return 0;
+}
+
+#define NCCLCHK(x)                                                                            \
+  do {                                                                                        \
+    ncclResult_t r_ = (x);                                                                    \
+    if (r_ != ncclSuccess) {                                                                  \
+      G.last_error = std::string(#x) + ": " + ncclGetErrorString(r_);                         \
+      return ARTIS_ERR_HIP;                                                                   \
+    }                                                                                         \
+  } while (0)
+
+int artis_gpu_comm_unique_id(void *id) {
+  if (!id) return ARTIS_ERR_BAD_ARGUMENT;
+  static_assert(sizeof(ncclUniqueId) == ARTIS_COMM_ID_BYTES, "RCCL unique id size");
+  ncclUniqueId uid;
+  NCCLCHK(ncclGetUniqueId(&uid));
+  memcpy(id, &uid, sizeof uid);
+  return 0;
+}
+
+int artis_gpu_comm_init(int rank, int nranks, const void *id) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  if (!id || nranks <= 0 || rank < 0 || rank >= nranks) return ARTIS_ERR_BAD_ARGUMENT;
+  artis_gpu_comm_finalize();
+  HIPCHK(hipSetDevice(G.device));
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof uid);
+  NCCLCHK(ncclCommInitRank(&G.comm, nranks, uid, rank));
+  G.comm_ranks = nranks;
+  if (!G.d_redblock) HIPCHK(dmalloc((void **)&G.d_redblock, artis_gpu_estimator_block_doubles() * sizeof(double)));
+  return 0;
+}
+
+int artis_gpu_estimators_allreduce(void) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  if (!G.comm || !G.d_redblock) {
+    G.last_error = "artis_gpu_comm_init must precede artis_gpu_estimators_allreduce";
+    return ARTIS_ERR_BAD_ARGUMENT;
+  }
+  if (int rc = artis_gpu_estimator_block_to_device(G.d_redblock)) return rc;
+  NCCLCHK(ncclAllReduce(G.d_redblock, G.d_redblock, artis_gpu_estimator_block_doubles(), ncclFloat64, ncclSum, G.comm,
+                        G.stream));
+  return artis_gpu_estimator_block_from_device(G.d_redblock);
+}
+
+void artis_gpu_comm_finalize(void) {
+  if (G.comm) {
+    (void)hipStreamSynchronize(G.stream);
+    (void)ncclCommDestroy(G.comm);
+  }
+  G.comm = nullptr;
+  G.comm_ranks = 0;
 }
 
 int artis_gpu_update_packets(int my_rank, int nts, artis_packet *packets, int npkts, artis_estimators *est) {

@@ -8,6 +8,8 @@
 // from radioactive pellets at tmin (packet_init, packet.cc:59-149) instead of r-packets.
 // Writes <outdir>/packets_0000_ts<nts>.tmp (raw 304-byte records, sn3d.cc:387-398) after every timestep, the
 // final <outdir>/packets00_0000.out (packet.cc:152-196), and prints one summary line per timestep.
+// ARTIS_DRIVER_RCCL=1: the estimators go through the RCCL all-reduce of update_packets_reduced (a
+// communicator of this one rank -- the multi-rank host hands rank 0's id to every rank).
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -74,6 +76,13 @@ int main(int argc, char **argv) {
   {
     artis_amd::PacketEngine engine(0, at, *artis_model_geometry(m), rp);
     if (pellets) engine.init_gamma(*artis_model_gamma_spectra(m));
+    const char *rccl = std::getenv("ARTIS_DRIVER_RCCL");
+    const bool reduced = rccl && rccl[0] == '1';
+    if (reduced) {
+      unsigned char id[ARTIS_COMM_ID_BYTES];
+      artis_amd::PacketEngine::unique_id(id);
+      engine.comm_init(0, 1, id);
+    }
     for (int nts = nts0; nts < nts0 + nsteps && nts < cfg.ntstep; nts++) {
       artis_amd::check(artis_model_set_timestep(m, nts), "update_grid stand-in");
       engine.upload_cellstate(nts, *artis_model_cellstate(m));
@@ -92,7 +101,10 @@ int main(int argc, char **argv) {
       est.acounter = ac.data();
       std::fill(emiss.begin(), emiss.end(), 0.);
       est.rpkt_emiss = emiss.data();
-      engine.update_packets(rp.rank, nts, packets.data(), npkts, est);
+      if (reduced)
+        engine.update_packets_reduced(rp.rank, nts, packets.data(), npkts, est);
+      else
+        engine.update_packets(rp.rank, nts, packets.data(), npkts, est);
       double jsum = 0.;
       for (double v : J) jsum += v;
       artis_amd::check(artis_write_temp_packetsfile(outdir.c_str(), nts, rp.rank, packets.data(), npkts),

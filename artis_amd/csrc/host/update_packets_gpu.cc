@@ -36,6 +36,24 @@ void PacketEngine::update_packets(int my_rank, int nts, artis_packet *packets, i
   check(artis_gpu_update_packets(my_rank, nts, packets, npkts, &est), "artis_gpu_update_packets");
 }
 
+void PacketEngine::unique_id(unsigned char id[ARTIS_COMM_ID_BYTES]) {
+  check(artis_gpu_comm_unique_id(id), "artis_gpu_comm_unique_id");
+}
+
+void PacketEngine::comm_init(int rank, int nranks, const unsigned char id[ARTIS_COMM_ID_BYTES]) {
+  check(artis_gpu_comm_init(rank, nranks, id), "artis_gpu_comm_init");
+}
+
+void PacketEngine::update_packets_reduced(int my_rank, int nts, artis_packet *packets, int npkts,
+                                          artis_estimators &est) {
+  check(artis_gpu_packets_upload(packets, npkts), "artis_gpu_packets_upload");
+  check(artis_gpu_estimators_zero(), "artis_gpu_estimators_zero");
+  check(artis_gpu_update_packets_resident(my_rank, nts), "artis_gpu_update_packets_resident");
+  check(artis_gpu_estimators_allreduce(), "artis_gpu_estimators_allreduce");
+  check(artis_gpu_packets_download(packets, npkts), "artis_gpu_packets_download");
+  check(artis_gpu_estimators_download(&est), "artis_gpu_estimators_download");
+}
+
 double PacketEngine::last_transport_ms() const { return artis_gpu_last_transport_ms(); }
 
 }  // namespace artis_amd

@@ -33,6 +33,16 @@ class PacketEngine {
   // and radfield:: in the reference) made explicit; estimators are accumulated, as the reference's are
   void update_packets(int my_rank, int nts, artis_packet *packets, int npkts, artis_estimators &est);
 
+  // Multi-GPU (one process per GPU): join the RCCL communicator of all ranks.  Rank 0 makes the id with
+  // unique_id(); the host distributes it (MPI_Bcast in sn3d).
+  static void unique_id(unsigned char id[ARTIS_COMM_ID_BYTES]);
+  void comm_init(int rank, int nranks, const unsigned char id[ARTIS_COMM_ID_BYTES]);
+
+  // update_packets followed by the reference's mpi_reduce_estimators (sn3d.cc:316-377, radfield.cc:1502-1564)
+  // done in HBM: the packed estimator block is all-reduced over RCCL before it is copied into est, so every rank
+  // receives the summed estimators (which it would otherwise get from MPI_Allreduce of its host arrays)
+  void update_packets_reduced(int my_rank, int nts, artis_packet *packets, int npkts, artis_estimators &est);
+
   double last_transport_ms() const;
 };
 

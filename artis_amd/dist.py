@@ -2,61 +2,61 @@
 sn3d.cc:316-377) as ONE all-reduce of one packed float64 block per timestep.
 
 Each rank propagates its own full-energy packet ensemble (packet.cc:106-149; rank-specific RNG key), so the
-only exchange is a SUM of the estimator accumulators.  The block layout is the engine's device layout
-(engine.hip artis_gpu_estimator_block_to_device):
-  [J | nuJ | ffheating | colheating (npts_model each) | gammaestimator | bfheatingestimator (npts*E*I each)
-   | time_step scalars (8) | ecounter | acounter (nlines each) | counters (34) | nesc]
-Counts travel as float64 (exact below 2**53).  On GPUs the block is reduced in HBM over RCCL/xGMI
-(torch.distributed "nccl"); the same layout is reduced on host arrays with "gloo" in the CPU tests.
+only exchange is a SUM of the estimator accumulators.  The block layout is defined once, by the engine library
+(include/artis_gpu.h: artis_gpu_estimator_block_to_device on the device, artis_estimator_block_pack / _unpack on
+the host), and used here unchanged:
+  [J | nuJ | ffheating | colheating | rpkt_emiss | gammaestimator | bfheatingestimator | 10 time_step scalars
+   | ecounter | acounter | counters (34) | nesc]
+On GPUs the block is all-reduced in HBM by the engine's own RCCL communicator over xGMI
+(artis_gpu_comm_init / artis_gpu_estimators_allreduce; Engine.comm_init / Engine.allreduce_estimators);
+host arrays are packed with the same layout and reduced with gloo in the CPU tests.
 """
+import ctypes as C
+
 import numpy as np
 
-from . import ffi
+from . import gpu_lib
 
 
 def block_len(npts_model, nelements, maxnions, nlines):
-    return 4 * npts_model + 2 * npts_model * nelements * maxnions + 8 + 2 * nlines + ffi.ARTIS_COUNTER_COUNT + 1
+    return int(gpu_lib().artis_estimator_block_len(npts_model, nelements, maxnions, nlines))
+
+
+def _dims(est):
+    return est.npts_model, est.nelements, est.maxnions, len(est.ecounter)
 
 
 def pack_estimators(est):
-    """EstimatorArrays -> float64 block (host mirror of the device layout)."""
-    s = est.struct
-    scal = np.array([s.cmf_lum, s.gamma_dep, s.positron_dep, s.electron_dep, s.electron_emission, s.alpha_dep,
-                     s.alpha_emission, s.gamma_emission])
-    return np.concatenate([est.J, est.nuJ, est.ffheating, est.colheating, est.gamma, est.bfheating, scal,
-                           est.ecounter.astype(np.float64), est.acounter.astype(np.float64),
-                           est.counters.astype(np.float64), np.array([float(s.nesc)])])
+    """ffi.EstimatorArrays -> float64 block in the device layout (artis_estimator_block_pack)."""
+    dims = _dims(est)
+    block = np.zeros(block_len(*dims))
+    rc = gpu_lib().artis_estimator_block_pack(C.byref(est.struct), *dims, block.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"artis_estimator_block_pack -> {rc}")
+    return block
 
 
 def unpack_estimators(block, est):
-    """float64 block -> EstimatorArrays (overwrites)."""
-    n = len(est.J)
-    ni = len(est.gamma)
-    nl = len(est.ecounter)
-    o = 0
-    for arr in (est.J, est.nuJ, est.ffheating, est.colheating):
-        arr[:] = block[o:o + n]
-        o += n
-    for arr in (est.gamma, est.bfheating):
-        arr[:] = block[o:o + ni]
-        o += ni
-    s = est.struct
-    (s.cmf_lum, s.gamma_dep, s.positron_dep, s.electron_dep, s.electron_emission, s.alpha_dep, s.alpha_emission,
-     s.gamma_emission) = [float(x) for x in block[o:o + 8]]
-    o += 8
-    est.ecounter[:] = np.rint(block[o:o + nl]).astype(np.int32)
-    o += nl
-    est.acounter[:] = np.rint(block[o:o + nl]).astype(np.int32)
-    o += nl
-    for k in range(ffi.ARTIS_COUNTER_COUNT):
-        s.counters[k] = int(round(block[o + k]))
-    o += ffi.ARTIS_COUNTER_COUNT
-    s.nesc = int(round(block[o]))
+    """float64 block -> ffi.EstimatorArrays (overwrites; artis_estimator_block_unpack)."""
+    dims = _dims(est)
+    block = np.ascontiguousarray(block, dtype=np.float64)
+    if len(block) != block_len(*dims):
+        raise ValueError("estimator block length does not match the estimator arrays")
+    rc = gpu_lib().artis_estimator_block_unpack(block.ctypes.data, *dims, C.byref(est.struct))
+    if rc != 0:
+        raise RuntimeError(f"artis_estimator_block_unpack -> {rc}")
     return est
 
 
-def allreduce_engine_estimators(engine, torch_buffer, dist_module):
-    """Sum the device estimator blocks of all ranks in place (RCCL over xGMI when backend is nccl)."""
-    engine.estimator_block_to_device(torch_buffer.data_ptr())
-    dist_module.all_reduce(torch_buffer)
-    engine.estimator_block_from_device(torch_buffer.data_ptr())
+def join(engine, rank, world, dist_module):
+    """Every rank joins the engine's RCCL communicator; rank 0's id travels over dist_module (any backend)."""
+    from . import comm_unique_id
+
+    obj = [comm_unique_id() if rank == 0 else None]
+    dist_module.broadcast_object_list(obj, src=0)
+    engine.comm_init(rank, world, obj[0])
+
+
+def allreduce_engine_estimators(engine):
+    """Sum the device estimator blocks of all ranks in place (RCCL over xGMI, engine stream)."""
+    engine.allreduce_estimators()

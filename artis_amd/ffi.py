@@ -9,6 +9,7 @@ import numpy as np
 
 ARTIS_WORK_COUNT = 16
 ARTIS_COUNTER_COUNT = 34
+COMM_ID_BYTES = 128
 
 TYPE_ESCAPE = 32
 TYPE_RADIOACTIVE_PELLET = 100
@@ -154,6 +155,7 @@ class EstimatorArrays:
     """Host-side numpy storage for one artis_estimators block (reference zero_estimators shapes)."""
 
     def __init__(self, npts_model, nelements, maxnions, nlines):
+        self.npts_model, self.nelements, self.maxnions = npts_model, nelements, maxnions
         self.J = np.zeros(npts_model)
         self.nuJ = np.zeros(npts_model)
         self.ffheating = np.zeros(npts_model)

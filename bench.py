@@ -10,13 +10,19 @@ One step = one update_packets(nts) of this rank's P resident packets, all in HBM
 Packets are sharded: every rank propagates its own full-energy ensemble (rank-specific seed and RNG key), so
 per-GPU work is fixed as N grows ("weak").  value = N * P * K / max-over-ranks wall time.
 
-roofline: the dominant kernel class of the event-queue transport (k_ma or k_rpkt): its algorithmic bytes
-(SURVEY.md §8(d) per-unit figures over the engine's own event counters, split by the kernel that does the
-work) per launch / its average launch time, measured with HIP events around every launch on the engine
-stream, against 8.0 TB/s.  traffic: measured HBM bytes per launch of that kernel (rocprofv3 FETCH_SIZE x2 +
-WRITE_SIZE, profiles/pmc_*.json) when a PMC summary of the same configuration is committed.
+roofline: the dominant kernel class of the step (k_ma, k_rpkt, or k_vpkt with --vpkt): its algorithmic bytes
+per launch / its average launch time, measured with HIP events around every launch on the engine stream,
+against 8.0 TB/s.  Bytes: SURVEY.md §8(d)'s per-unit figures over the engine's own event counters, split by
+the kernel that does the work, except that a macro-atom transition probe of the cached walk (a binary-search
+step over running sums) is charged the 8 bytes it reads, not §8(d)'s 40-byte transition record
+("achieved"); the §8(d) figure is reported beside it ("achieved_survey_model").  traffic: measured HBM bytes
+per launch of that kernel (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_*.json), used only when the
+summary was made from the same engine sources (engine_src_sha) and configuration.
 cpu_baseline: the CPU oracle (oracle/liboracle.so, OpenMP) on a bounded sample of the same workload, rank 0
-at N=1 only.
+at N=1 only, on the CPU share this process may use (affinity and cgroup quota; host CPU model recorded).
+N>1: ranks join the engine's RCCL communicator (rank 0's id broadcast over a gloo process group that also
+provides the barriers and the max-over-ranks time); the estimator block is all-reduced in HBM by the engine
+(artis_gpu_estimators_allreduce).
 """
 import argparse
 import glob
@@ -34,20 +40,51 @@ METRIC = "MC packets/sec/timestep on 50^3 grid; emergent-spectrum L1 vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
 
 
-def byte_model(work, nions_total):
-    """SURVEY.md §8(d) algorithmic bytes per kernel class from the work counters (include/artis_constants.h
-    enum artis_work): the r-packet kernel reads/writes the record, steps, scans lines, evaluates kappa and
-    estimators; the macro-atom kernel reads a 72-byte rate record per jump and 40 bytes per transition touched;
+def byte_model(work, nions_total, probe_bytes=8.0):
+    """Algorithmic bytes per kernel class from the work counters (include/artis_constants.h enum artis_work),
+    SURVEY.md §8(d) per-unit figures: the r-packet kernel reads/writes the record, steps, scans lines, evaluates
+    kappa and estimators; the macro-atom kernel reads a 72-byte rate record per jump and probe_bytes per
+    transition probe (8: the running sum a binary-search step of the cached walk reads; §8(d) charges 40);
     the k-packet kernel scans cooling terms."""
     w = [float(x) for x in work]
     rpkt = (608.0 * w[0] + 168.0 * w[1] + 64.0 * w[2] + 88.0 * w[5] + 8.0 * nions_total * w[4] + 48.0 * w[6]
             + 32.0 * w[7])
-    ma = 72.0 * w[8] + 40.0 * w[9]
+    ma = 72.0 * w[8] + probe_bytes * w[9]
     kpkt = 16.0 * w[11]
     return {"rpkt": rpkt, "ma": ma, "kpkt": kpkt}
 
 
-KERNEL_NAME = {"rpkt": "k_rpkt<2>", "ma": "k_ma<true, 1>", "kpkt": "k_kpkt"}
+def vpkt_byte_model(vwork, traces, nions_total):
+    """Virtual packets (vpkt.cc:76-406) with the same per-unit figures: a 104-byte spawn record per trace, a cell
+    step (168 B + kappa: 8 B per ion) per segment, 64 B per line whose opacity is added, 88 B per active bf
+    continuum, and the three vstokes read-modify-writes (48 B) of an escaped virtual packet."""
+    return (104.0 * traces + (168.0 + 8.0 * nions_total) * vwork["segments"] + 64.0 * vwork["lines"]
+            + 88.0 * vwork["bf_active"] + 48.0 * vwork["escaped"])
+
+
+KERNEL_NAME = {"rpkt": "k_rpkt<2>", "ma": "k_ma<true, 1>", "kpkt": "k_kpkt", "vpkt": "k_vpkt"}
+
+
+def cpu_share():
+    """Threads this process may run on: affinity mask, capped by the cgroup v2 CPU quota; plus host facts."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(float(q) / float(per)))
+    except (OSError, ValueError):
+        pass
+    threads = min(n, quota) if quota else n
+    model = ""
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return threads, {"nproc": os.cpu_count(), "affinity": n, "cgroup_quota_cpus": quota, "cpu_model": model}
 
 
 def main():
@@ -77,9 +114,10 @@ def main():
         raise SystemExit("bench.py needs a GPU")
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist.init_process_group("gloo")
 
-    from artis_amd import Engine
+    from artis_amd import Engine, engine_src_sha
+    from artis_amd import dist as adist
     from artis_amd.model import Model
 
     model = Model(ngrid_1d=args.ngrid)
@@ -104,9 +142,8 @@ def main():
     eng.upload(packets)
     eng.snapshot()
 
-    red = None
     if world > 1:
-        red = torch.empty(eng.estimator_block_doubles(), dtype=torch.float64, device="cuda")
+        adist.join(eng, rank, world, dist)
 
     transport_ms = []
     precompute_ms = []
@@ -121,10 +158,8 @@ def main():
         eng.zero_estimators()
         eng.upload_cellstate(nts)
         eng.step_resident(nts, my_rank=rank)
-        if red is not None:
-            eng.estimator_block_to_device(red.data_ptr())
-            dist.all_reduce(red)
-            eng.estimator_block_from_device(red.data_ptr())
+        if world > 1:
+            adist.allreduce_engine_estimators(eng)
         if record:
             transport_ms.append(eng.last_transport_ms())
             precompute_ms.append(eng.last_precompute_ms())
@@ -148,7 +183,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -156,24 +191,34 @@ def main():
     value = total_packet_timesteps / elapsed
     avg_transport_s = float(np.mean(transport_ms)) / 1e3
     alg = byte_model(work, model.nions_total)
+    alg_survey = byte_model(work, model.nions_total, probe_bytes=40.0)
     kt = {k: (float(np.mean([t[k][0] for t in ktimes])), float(np.mean([t[k][1] for t in ktimes])))
           for k in ("rpkt", "ma", "kpkt")}
-    dom = max(("rpkt", "ma"), key=lambda k: kt[k][0])
+    if vcfg is not None:
+        ntr = float(np.mean([v[2] for v in vstats]))
+        vw = {k: float(np.mean([w[k] for w in vwork])) for k in vwork[0]}
+        alg["vpkt"] = alg_survey["vpkt"] = vpkt_byte_model(vw, ntr, model.nions_total)
+        kt["vpkt"] = (float(np.mean([v[0] for v in vstats])), float(max(np.mean(rounds), 1)))
+    dom = max((k for k in kt if k != "kpkt"), key=lambda k: kt[k][0])
     dom_ms, dom_launches = kt[dom]
     launches = max(dom_launches, 1.0)
     bytes_per_launch = alg[dom] / launches
     avg_launch_s = dom_ms / 1e3 / launches
     achieved_gbs = bytes_per_launch / max(avg_launch_s, 1e-12) / 1e9
-    traffic = None
+    achieved_survey = alg_survey[dom] / launches / max(avg_launch_s, 1e-12) / 1e9
+    src_sha = engine_src_sha()
+    traffic, traffic_src = None, None
     for prof in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json"))):
         try:
             pm = json.load(open(prof))
         except Exception:
             continue
-        if pm.get("packets") == P and pm.get("ngrid") == args.ngrid and pm.get("nts") == nts:
-            kd = pm.get("kernels", {}).get(KERNEL_NAME[dom])
+        if (pm.get("engine_src_sha") == src_sha and pm.get("packets") == P and pm.get("ngrid") == args.ngrid
+                and pm.get("nts") == nts and pm.get("vpkt", 0) == args.vpkt):
+            kd = next((v for k, v in pm.get("kernels", {}).items() if k.startswith(KERNEL_NAME[dom])), None)
             if kd:
                 traffic = kd["hbm_bytes_per_launch"]
+                traffic_src = os.path.relpath(prof, REPO)
     cpu = None
     parity_line = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and vcfg is None:
@@ -181,7 +226,7 @@ def main():
         import oracle_lib
         import parity
 
-        nthreads = min(16, os.cpu_count() or 1)
+        nthreads, host = cpu_share()
         calib = packets[:256].copy()
         t = time.perf_counter()
         oracle_lib.update_packets(model, nts, calib, nthreads=nthreads)
@@ -207,6 +252,7 @@ def main():
             "value": n_sample / cpu_dt,
             "unit": "packets/s",
             "cores": nthreads,
+            "host": host,
             "kind": "port",
             "sample": f"first {n_sample} packets of the same ensemble, same timestep, {cpu_dt:.1f} s",
         }
@@ -233,7 +279,8 @@ def main():
                 "packets_per_gpu": P,
                 "grid": f"{args.ngrid}^3",
                 "timestep": nts,
-                "parallelism": f"packet-sharded x{world}, RCCL estimator all-reduce" if world > 1 else "1 GPU",
+                "parallelism": (f"packet-sharded x{world}, engine RCCL all-reduce of the estimator block"
+                                if world > 1 else "1 GPU"),
             },
             "roofline": {
                 "bound": "hbm",
@@ -242,7 +289,11 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_profile": traffic_src,
+                "engine_src_sha": src_sha,
                 "kernel": KERNEL_NAME[dom],
+                "achieved_survey_model": achieved_survey,
+                "frac_survey_model": achieved_survey / HBM_PEAK_GBS,
                 "alg_bytes_per_launch": bytes_per_launch,
                 "avg_launch_ms": avg_launch_s * 1e3,
                 "launches_per_step": launches,

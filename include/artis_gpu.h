@@ -391,6 +391,30 @@ int artis_gpu_estimators_download(artis_estimators *est);               /* ADD d
 size_t artis_gpu_estimator_block_doubles(void);
 int artis_gpu_estimator_block_to_device(void *dst_device);
 int artis_gpu_estimator_block_from_device(const void *src_device);
+/* The same block layout on the host (no device needed), so a host-side reduction (MPI / gloo) of
+ * artis_estimators sums exactly what the device block carries:
+ *   [J | nuJ | ffheating | colheating | rpkt_emiss (npts_model each) | gammaestimator | bfheatingestimator
+ *    (npts_model * nelements * maxnions each) | cmf_lum gamma_dep positron_dep electron_dep electron_emission
+ *    alpha_dep alpha_emission gamma_emission nt_energy_deposited pellet_decays | ecounter | acounter (nlines each)
+ *   | counters (ARTIS_COUNTER_COUNT) | nesc]   -- counts as float64 (exact below 2^53).
+ * pack: NULL array pointers of *est pack as zeros; unpack OVERWRITES *est (NULL arrays skipped). */
+size_t artis_estimator_block_len(int npts_model, int nelements, int maxnions, int nlines);
+int artis_estimator_block_pack(const artis_estimators *est, int npts_model, int nelements, int maxnions, int nlines,
+                               double *block);
+int artis_estimator_block_unpack(const double *block, int npts_model, int nelements, int maxnions, int nlines,
+                                 artis_estimators *est);
+
+/* --- multi-GPU: RCCL over xGMI (the reference's mpi_reduce_estimators, sn3d.cc:316-377, radfield.cc:1502-1564) */
+/* One process per GPU; every rank propagates its own full-energy ensemble and the only exchange per timestep
+ * is the SUM of the packed device estimator block.  Rank 0 creates the id (ncclGetUniqueId), the host hands
+ * it to every rank (MPI_Bcast in sn3d, a torch.distributed broadcast in bench.py), each rank joins with
+ * artis_gpu_comm_init on the engine's device; artis_gpu_estimators_allreduce then all-reduces the block in
+ * HBM on the engine stream (ncclAllReduce, ncclSum, ncclFloat64).  id: ARTIS_COMM_ID_BYTES opaque bytes. */
+#define ARTIS_COMM_ID_BYTES 128
+int artis_gpu_comm_unique_id(void *id);
+int artis_gpu_comm_init(int rank, int nranks, const void *id);
+int artis_gpu_estimators_allreduce(void);
+void artis_gpu_comm_finalize(void);
 
 /* --- timing / introspection --------------------------------------------------------------------------------- */
 /* Milliseconds of the transport kernel(s) of the last update_packets call, measured with HIP events on the
@@ -431,9 +455,10 @@ int64_t artis_gpu_last_rounds(void);  /* event-queue rounds of the last update (
  * [0] r-packet, [1] macro-atom (incl. cell binning), [2] k-packet, [3] classify */
 int artis_gpu_last_kernel_times(double ms[4], int64_t launches[4]);
 const char *artis_gpu_last_error(void);
-#define ARTIS_GPU_ABI_VERSION 4  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
+#define ARTIS_GPU_ABI_VERSION 5  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
                                     3: virtual packets (artis_vpkt_params / artis_vpkt_result);
-                                    4: artis_run_params.excitation_temperature */
+                                    4: artis_run_params.excitation_temperature;
+                                    5: host estimator block pack/unpack, RCCL communicator + all-reduce */
 int artis_gpu_abi_version(void);
 
 #ifdef __cplusplus

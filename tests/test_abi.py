@@ -74,7 +74,7 @@ def test_c_header_layout_matches_numpy_and_ctypes():
 
 def test_header_declares_exactly_the_abi_symbols():
     text = open(HEADER).read()
-    declared = set(re.findall(r"\b(artis_gpu_\w+)\s*\(", text))
+    declared = set(re.findall(r"\b(artis_(?:gpu|estimator)_\w+)\s*\(", text))
     assert declared == set(ABI_SYMBOLS)
 
 
@@ -88,7 +88,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_without_gpu_and_reports_version():
     lib = C.CDLL(GPU_SO)
-    assert lib.artis_gpu_abi_version() == 4
+    assert lib.artis_gpu_abi_version() == 5
     lib.artis_gpu_last_error.restype = C.c_char_p
     assert lib.artis_gpu_last_error() is not None
 

@@ -244,3 +244,71 @@ def test_bf_and_kpacket_heavy_model(engine_factory):
     assert c[5] > 0 and c[10] > 0 and c[20] > 0, c  # bf activations, fb deactivations, k-packets from bf
     parity.assert_packets_match(pg, po)
     parity.assert_estimators_match(eg, eo)
+
+
+def test_allocation_failures_fail_cleanly(small_model, engine_factory, monkeypatch):
+    """An out-of-memory packet store, spectrum scratch or snapshot returns an error (no dangling pointers): with
+    the injected limit removed the same engine runs normally and finalizes once (engine.hip alloc_packets,
+    artis_gpu_spectrum)."""
+    from artis_amd import EngineError
+
+    eng = engine_factory(small_model)
+    small_model.set_timestep(10)
+    eng.upload_cellstate(10)
+    pk = small_model.init_rpackets(10, 2000, seed=61)
+    monkeypatch.setenv("ARTIS_GPU_FAIL_ALLOC_ABOVE", "4096")
+    with pytest.raises(EngineError):
+        eng.update_packets(10, pk.copy())
+    with pytest.raises(EngineError):
+        eng.spectrum()
+    monkeypatch.delenv("ARTIS_GPU_FAIL_ALLOC_ABOVE")
+    eng.upload(pk)
+    monkeypatch.setenv("ARTIS_GPU_FAIL_ALLOC_ABOVE", "4096")
+    with pytest.raises(EngineError):
+        eng.snapshot()
+    monkeypatch.delenv("ARTIS_GPU_FAIL_ALLOC_ABOVE")
+    pg = pk.copy()
+    eg = eng.update_packets(10, pg)
+    po = pk.copy()
+    eo, _ = oracle_lib.update_packets(small_model, 10, po, nthreads=16)
+    parity.assert_packets_match(pg, po)
+    parity.assert_estimators_match(eg, eo)
+    spec, lc, _ = eng.spectrum()
+    assert lc.sum() > 0
+    eng.close()
+    eng.close()  # idempotent
+
+
+def test_estimator_block_roundtrip_and_rccl(small_model, engine_factory):
+    """The device block (artis_gpu_estimator_block_to_device) equals the host pack of the downloaded estimators
+    (artis_estimator_block_pack, what the gloo test reduces); a block written back (from_device) is what the next
+    download returns; a one-rank RCCL communicator all-reduces it unchanged (artis_gpu_estimators_allreduce)."""
+    import torch
+
+    from artis_amd import comm_unique_id, dist as adist
+
+    eng = engine_factory(small_model)
+    small_model.set_timestep(10)
+    eng.upload_cellstate(10)
+    pk = small_model.init_rpackets(10, 2000, seed=62)
+    eng.upload(pk)
+    eng.zero_estimators()
+    eng.step_resident(10)
+    host = eng.download_estimators()
+    hb = adist.pack_estimators(host)
+    n = eng.estimator_block_doubles()
+    assert n == len(hb)
+    buf = torch.zeros(n, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    eng.estimator_block_to_device(buf.data_ptr())
+    db = buf.cpu().numpy()
+    assert np.array_equal(db, hb)
+    buf.mul_(2.0)
+    torch.cuda.synchronize()
+    eng.estimator_block_from_device(buf.data_ptr())
+    twice = eng.download_estimators()
+    assert np.array_equal(adist.pack_estimators(twice), 2 * hb)
+    eng.comm_init(0, 1, comm_unique_id())
+    eng.allreduce_estimators()
+    again = eng.download_estimators()
+    assert np.array_equal(adist.pack_estimators(again), 2 * hb)

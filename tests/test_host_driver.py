@@ -56,3 +56,27 @@ def test_driver_matches_oracle(tmp_path):
     np.testing.assert_array_equal(back["number"], pg["number"])
     np.testing.assert_array_equal(back["type"], pg["type"])
     np.testing.assert_allclose(back["nu_rf"], pg["nu_rf"], rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_driver_rccl_reduced_path(tmp_path):
+    """ARTIS_DRIVER_RCCL=1: the estimators pass through the RCCL all-reduce of the device block
+    (update_packets_reduced, artis_gpu_estimators_allreduce) -- with one rank the sums are unchanged and the
+    packets identical to the plain path."""
+    a, b = tmp_path / "plain", tmp_path / "rccl"
+    a.mkdir()
+    b.mkdir()
+    ra = subprocess.run(_args(a), capture_output=True, text=True, timeout=600)
+    rb = subprocess.run(_args(b), capture_output=True, text=True, timeout=600,
+                        env={**os.environ, "ARTIS_DRIVER_RCCL": "1"})
+    assert ra.returncode == 0 and rb.returncode == 0, rb.stderr
+    def summary(out):  # "nts N nesc N cmf_lum X gamma_dep X pellet_decays N Jsum X transport_ms X" per timestep
+        rows = [ln.split() for ln in out.splitlines() if ln.startswith("nts ")]
+        return np.array([[float(r[i]) for i in (1, 3, 5, 7, 9, 11)] for r in rows])
+
+    sa, sb = summary(ra.stdout), summary(rb.stdout)
+    assert sa.shape == (NSTEPS, 6)
+    # float64 atomic sums: the order of accumulation differs between runs
+    np.testing.assert_allclose(sb, sa, rtol=1e-12, atol=0)
+    for nts in range(NTS0, NTS0 + NSTEPS):
+        assert (a / f"packets_0000_ts{nts}.tmp").read_bytes() == (b / f"packets_0000_ts{nts}.tmp").read_bytes()

@@ -3,7 +3,9 @@
 Each rank propagates its own packet ensemble (packet.cc:106-149 gives every rank a full-energy set with a
 rank-specific RNG key) and the ranks exchange exactly one thing: the SUM of the estimator accumulators
 (mpi_reduce_estimators, sn3d.cc:582 / radfield.cc:1502-1564).  artis_amd.dist packs them into the engine's
-device block layout; here the block is all-reduced with gloo and must equal the serial sum of both ranks.
+device block layout (the engine library's artis_estimator_block_pack, the host twin of
+artis_gpu_estimator_block_to_device); here the block is all-reduced with gloo and must equal the serial sum of
+both ranks.
 """
 import copy
 import os
@@ -76,6 +78,8 @@ def test_estimator_allreduce_world2(tmp_path):
     assert (tot.counters == e0.counters + e1.counters).all()
     assert tot.struct.nesc == e0.struct.nesc + e1.struct.nesc
     assert (tot.acounter == e0.acounter + e1.acounter).all()
+    assert np.allclose(tot.gamma, e0.gamma + e1.gamma, rtol=1e-14)
+    assert tot.struct.cmf_lum == b0[adist.block_len(m.npts_model, m.nelements, m.maxnions, 0) - 45]
     assert len(b0) == adist.block_len(m.npts_model, m.nelements, m.maxnions, m.nlines)
 
 
@@ -94,3 +98,35 @@ def test_ranks_draw_independent_streams():
         oracle_lib.update_packets(m, NTS, pk, params=p)
         outs.append(pk)
     assert outs[0].tobytes() != outs[1].tobytes()
+
+
+def test_block_layout_is_the_device_layout():
+    """Field positions of the packed block (include/artis_gpu.h): a marker in each array / scalar lands where
+    the device block puts it, and unpack inverts pack."""
+    from artis_amd import ffi
+
+    np_, ne, mi, nl = 3, 2, 4, 5
+    est = ffi.EstimatorArrays(np_, ne, mi, nl)
+    est.J[:] = 1
+    est.nuJ[:] = 2
+    est.ffheating[:] = 3
+    est.colheating[:] = 4
+    est.rpkt_emiss[:] = 5
+    est.gamma[:] = 6
+    est.bfheating[:] = 7
+    s = est.struct
+    (s.cmf_lum, s.gamma_dep, s.positron_dep, s.electron_dep, s.electron_emission, s.alpha_dep, s.alpha_emission,
+     s.gamma_emission, s.nt_energy_deposited) = range(11, 20)
+    s.pellet_decays = 20
+    est.ecounter[:] = 21
+    est.acounter[:] = 22
+    for k in range(ffi.ARTIS_COUNTER_COUNT):
+        s.counters[k] = 100 + k
+    s.nesc = 23
+    b = adist.pack_estimators(est)
+    ni = np_ * ne * mi
+    expect = np.concatenate([np.repeat([1, 2, 3, 4, 5], np_), np.full(ni, 6), np.full(ni, 7), np.arange(11, 21),
+                             np.full(nl, 21), np.full(nl, 22), 100 + np.arange(ffi.ARTIS_COUNTER_COUNT), [23]])
+    assert np.array_equal(b, expect.astype(np.float64))
+    back = adist.unpack_estimators(b, ffi.EstimatorArrays(np_, ne, mi, nl))
+    assert np.array_equal(adist.pack_estimators(back), b)

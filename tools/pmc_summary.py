@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--ngrid", type=int, required=True)
     ap.add_argument("--nts", type=int, required=True)
     ap.add_argument("--steps", type=int, default=1, help="transport steps in the profiled run (warmup included)")
+    ap.add_argument("--vpkt", type=int, default=0, help="observer directions of the profiled run (bench.py --vpkt)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     fetch, nf = load(a.fetch, "FETCH_SIZE")
@@ -54,7 +55,13 @@ def main():
         kernels[name] = {"launches": n, "fetch_bytes_per_launch": fb / n, "write_bytes_per_launch": wb / n,
                          "hbm_bytes_per_launch": (fb + wb) / n,
                          "hbm_bytes_per_step": (fb + wb) / a.steps}
-    out = {"packets": a.packets, "ngrid": a.ngrid, "nts": a.nts, "steps": a.steps,
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from artis_amd import engine_src_sha
+
+    out = {"engine_src_sha": engine_src_sha(), "packets": a.packets, "ngrid": a.ngrid, "nts": a.nts,
+           "vpkt": a.vpkt, "steps": a.steps,
            "correction": "FETCH_SIZE x2 (gfx950), KiB -> bytes", "kernels": kernels}
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
