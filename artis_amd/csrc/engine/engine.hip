@@ -189,14 +189,16 @@ __global__ void k_cooling(Ctx K) {
   }
 }
 
-// macroatom.cc:57-159 calculate_macroatom_transitionrates, one workitem per (cell, level); with the macro-atom
-// cache it also stores the running sums of the individual rates (cellhistory individ_* arrays).
+// macroatom.cc:57-159 calculate_macroatom_transitionrates, one workitem per (cell, level) (ma_foreach_rate); with the
+// macro-atom cache it also stores the running sums of the individual rates (cellhistory individ_* arrays).
 // Workitems are ordered level-major (consecutive lanes = the same level in consecutive cells): every lane of
 // a wave walks the same transition lists, so the atomic-data loads are wave-uniform and the loops do not
 // diverge; only the cell's populations (level-major copy popsT) and temperatures differ per lane.
-// With the cache, one launch covers levels [ul0, ul0 + nlev) and writes the records position-major into the
-// scratch S (S[(rec_off(ul) - rec_off(ul0)) * n_ne + pos * n_ne + k]: every store is 64 consecutive doubles);
-// k_marec then transposes them into the per-cell records.
+// With the cache, one launch covers levels [ul0, ul0 + nlev) and writes the exact double running sums
+// position-major into the scratch S (S[(dbl_off(ul) - dbl_off(ul0)) * n_ne + pos * n_ne + k]: every store is 64
+// consecutive doubles); k_mapack then turns them into the compact key records.  Record positions:
+//   [9 totals | internal_down_same (nd, Eytzinger order) | internal_up_same (nu, Eytzinger) | rad_deexc (nd) |
+//    rad_recomb (nr) | internal_down_lower (nr) | internal_up_higher (nt)]
 __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict__ S) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nl = K.T.nlevels_total;
@@ -205,22 +207,10 @@ __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict_
   const int ul = ul0 + (int)(idx / nne_cells);
   const int k = (int)(idx % nne_cells);
   const int mgi = K.C.ne_mgi[k];
-  const int ui = K.T.level_ui[ul];
-  const int e = K.T.ion_element[ui];
-  const int i = ui - K.T.elem_uniqueionoffset[e];
-  const int l = ul - K.T.ion_uniqueleveloffset[ui];
   const double t_mid = K.G.ts_mid[nts];
-  const float T_e = K.C.Te[mgi];
-  const float nne = K.C.nne[mgi];
-  const double *popsT = K.C.popsT + k;  // popsT[ul * nne_cells]: level ul of this lane's cell
-  const double n_self = popsT[ul * nne_cells];
-  const double epsilon_current = K.T.level_epsilon[ul];
-  const double statweight = K.T.level_stat_weight[ul];
   const bool cache = K.C.have_macache;
   const MaMeta mm = K.T.ma_meta[ul];
-  // record position p of this (cell, level) in the scratch; record layout (engine_dev.h DevCells::ma_rec):
-  // Eytzinger arrays at 8 + position (1-based), then the sorted cumulative arrays
-  double *rec = cache ? S + (int64_t)(mm.rec_off - K.T.ma_meta[ul0].rec_off) * nne_cells + k : nullptr;
+  double *rec = cache ? S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * nne_cells + k : nullptr;
 #define REC(p) rec[(int64_t)(p) * nne_cells]
   const int eyt_d = 8, eyt_u = 8 + mm.nd;
   const int cum_drad = ARTIS_MA_ACTION_COUNT + mm.nd + mm.nu, cum_rrad = cum_drad + mm.nd;
@@ -228,64 +218,27 @@ __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict_
   const int32_t *inv_d = K.T.eyt_inv + K.T.eyt_off[mm.nd], *inv_u = K.T.eyt_inv + K.T.eyt_off[mm.nu];
   double pr[ARTIS_MA_ACTION_COUNT];
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) pr[a] = 0.;
-  const int ndowntrans = K.T.level_ndowntrans[ul];
-  const int doff = K.T.level_downtrans_offset[ul];
-  for (int j = 0; j < ndowntrans; j++) {
-    const int li = K.T.downtrans_lineindex[doff + j];
-    const int lower = K.T.line_lower[li];
-    const double epsilon_target = epsilon(K, e, i, lower);
-    const double epsilon_trans = epsilon_current - epsilon_target;
-    const double n_l = popsT[(int64_t)(ul - l + lower) * nne_cells];
-    const double R = rad_deexcitation_ratecoeff_n(K, n_self, n_l, li, t_mid);
-    const double C = col_deexcitation_ratecoeff(K, T_e, nne, epsilon_trans, li, stat_weight(K, e, i, lower), statweight);
-    pr[ARTIS_MA_ACTION_RADDEEXC] += R * epsilon_trans;
-    pr[ARTIS_MA_ACTION_COLDEEXC] += C * epsilon_trans;
-    pr[ARTIS_MA_ACTION_INTERNALDOWNSAME] += (R + C) * epsilon_target;
-    if (cache) {
-      REC(cum_drad + j) = pr[ARTIS_MA_ACTION_RADDEEXC];
-      REC(eyt_d + inv_d[j]) = pr[ARTIS_MA_ACTION_INTERNALDOWNSAME];
-    }
-  }
-  if (i > 0 && l <= K.T.ion_maxrecombininglevel[ui]) {
-    const int nlevels = get_ionisinglevels(K, e, i - 1);
-    for (int lower = 0; lower < nlevels; lower++) {
-      const double epsilon_target = epsilon(K, e, i - 1, lower);
-      const double epsilon_trans = epsilon_current - epsilon_target;
-      const double R = rad_recombination_ratecoeff(K, T_e, nne, e, i, l, lower);
-      const double C = col_recombination_ratecoeff(K, mgi, e, i, l, lower, epsilon_trans);
-      pr[ARTIS_MA_ACTION_INTERNALDOWNLOWER] += (R + C) * epsilon_target;
-      pr[ARTIS_MA_ACTION_RADRECOMB] += R * epsilon_trans;
-      pr[ARTIS_MA_ACTION_COLRECOMB] += C * epsilon_trans;
-      if (cache) {
-        REC(cum_rrad + lower) = pr[ARTIS_MA_ACTION_RADRECOMB];
-        REC(cum_rint + lower) = pr[ARTIS_MA_ACTION_INTERNALDOWNLOWER];
-      }
-    }
-  }
-  const int nuptrans = K.T.level_nuptrans[ul];
-  const int uoff = K.T.level_uptrans_offset[ul];
-  const double T_R = K.C.TR[mgi], W = K.C.W[mgi];
-  for (int j = 0; j < nuptrans; j++) {
-    const int li = K.T.uptrans_lineindex[uoff + j];
-    const int upper = K.T.line_upper[li];
-    const double epsilon_trans = epsilon(K, e, i, upper) - epsilon_current;
-    const double n_u = popsT[(int64_t)(ul - l + upper) * nne_cells];
-    const double R = rad_excitation_ratecoeff_n(K, n_u, n_self, T_R, W, epsilon_trans, li, t_mid);
-    const double C = col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, e, i, upper));
-    pr[ARTIS_MA_ACTION_INTERNALUPSAME] += (R + C + 0.) * epsilon_current;
-    if (cache) REC(eyt_u + inv_u[j]) = pr[ARTIS_MA_ACTION_INTERNALUPSAME];
-  }
-  if (i < K.T.elem_nions[e] - 1 && l < K.T.ion_ionisinglevels[ui]) {
-    const int nt = K.T.level_nphixstargets[ul];
-    const int slot0 = K.T.level_phixstargets_offset[ul];
-    for (int t = 0; t < nt; t++) {
-      const double epsilon_trans = get_phixs_threshold(K, e, i, l, t);
-      const double R = K.C.corrphotT[(int64_t)(slot0 + t) * nne_cells + k];
-      const double C = col_ionization_ratecoeff(K, T_e, nne, e, i, l, t, epsilon_trans);
-      pr[ARTIS_MA_ACTION_INTERNALUPHIGHER] += (R + C) * epsilon_current;
-      if (cache) REC(cum_uhi + t) = pr[ARTIS_MA_ACTION_INTERNALUPHIGHER];
-    }
-  }
+  const double *popsT = K.C.popsT + k;  // popsT[u * nne_cells]: level u of this lane's cell
+  ma_foreach_rate(
+      K, mgi, ul, t_mid, [&](int u) { return popsT[(int64_t)u * nne_cells]; },
+      [&](int slot) { return K.C.corrphotT[(int64_t)slot * nne_cells + k]; },
+      [&](int kind, int j, double R, double C, double et, double eg, double ec) {
+        ma_accumulate(pr, kind, R, C, et, eg, ec);
+        if (cache) {
+          if (kind == MA_KIND_DOWN) {
+            REC(cum_drad + j) = pr[ARTIS_MA_ACTION_RADDEEXC];
+            REC(eyt_d + inv_d[j]) = pr[ARTIS_MA_ACTION_INTERNALDOWNSAME];
+          } else if (kind == MA_KIND_RECOMB) {
+            REC(cum_rrad + j) = pr[ARTIS_MA_ACTION_RADRECOMB];
+            REC(cum_rint + j) = pr[ARTIS_MA_ACTION_INTERNALDOWNLOWER];
+          } else if (kind == MA_KIND_UP) {
+            REC(eyt_u + inv_u[j]) = pr[ARTIS_MA_ACTION_INTERNALUPSAME];
+          } else {
+            REC(cum_uhi + j) = pr[ARTIS_MA_ACTION_INTERNALUPHIGHER];
+          }
+        }
+        return false;
+      });
   if (cache) {
     for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) REC(a) = pr[a];
   } else {
@@ -295,25 +248,60 @@ __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict_
 #undef REC
 }
 
-// Scratch -> records for the levels of one k_marates launch: block (level ul0 + blockIdx.y, 64 cells from
-// 64 * blockIdx.x); 64x64 (position x cell) tiles through LDS, read along cells, written along positions.
-__global__ __launch_bounds__(256) void k_marec(Ctx K, int ul0, const double *__restrict__ S) {
+// Exact running sums (scratch) -> the compact key record of each (cell, level) of one k_marates batch
+// (engine_dev.h DevCells::ma_key): every sum divided by its action's total (the action totals by their grand
+// total, summed in the reference's order, macroatom.cc:515-525) and rounded to 32 bits, split into halves.  Block = (level
+// ul0 + blockIdx.y, 64 cells): 64 x 64 (position x cell) tiles through LDS, read along cells from the
+// position-major scratch, written along positions (64 consecutive keys of one record per row: coalesced).
+__global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, const double *__restrict__ S) {
   __shared__ double tile[64][65];
+  __shared__ double s_norm[ARTIS_MA_ACTION_COUNT][64];  // action totals per cell
+  __shared__ uint32_t s_akey[ARTIS_MA_ACTION_COUNT][64];
   const int ul = ul0 + blockIdx.y;
   const int64_t n_ne = K.C.n_nonempty;
   const MaMeta mm = K.T.ma_meta[ul];
   const int len = ARTIS_MA_ACTION_COUNT + 2 * mm.nd + mm.nu + 2 * mm.nr + mm.nt;
-  const double *src = S + (int64_t)(mm.rec_off - K.T.ma_meta[ul0].rec_off) * n_ne;
+  const double *src = S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * n_ne;
   const int64_t c0 = (int64_t)blockIdx.x * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  if (ty == 0 && c0 + tx < n_ne) {
+    double pr[ARTIS_MA_ACTION_COUNT];
+    double total = 0.;
+    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
+      pr[a] = src[(int64_t)a * n_ne + c0 + tx];
+      s_norm[a][tx] = pr[a];
+      total += pr[a];
+    }
+    double rate = 0.;
+    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
+      rate += pr[a];
+      s_akey[a][tx] = ma_key32(rate, total);
+    }
+  }
+  // segment boundaries of the record (positions >= 9): the action whose total normalises each
+  const int b1 = ARTIS_MA_ACTION_COUNT + mm.nd, b2 = b1 + mm.nu, b3 = b2 + mm.nd, b4 = b3 + mm.nr, b5 = b4 + mm.nr;
   for (int p0 = 0; p0 < len; p0 += 64) {
+    __syncthreads();
     for (int j = ty; j < 64; j += 4)
       if (p0 + j < len && c0 + tx < n_ne) tile[j][tx] = src[(int64_t)(p0 + j) * n_ne + c0 + tx];
     __syncthreads();
-    for (int j = ty; j < 64; j += 4)
-      if (p0 + tx < len && c0 + j < n_ne)
-        K.C.ma_rec[(c0 + j) * K.C.ma_rec_stride + mm.rec_off + p0 + tx] = tile[tx][j];
-    __syncthreads();
+    const int p = p0 + tx;
+    if (p < len) {
+      const int a = (p < ARTIS_MA_ACTION_COUNT) ? -1
+                    : (p < b1)                 ? ARTIS_MA_ACTION_INTERNALDOWNSAME
+                    : (p < b2)                 ? ARTIS_MA_ACTION_INTERNALUPSAME
+                    : (p < b3)                 ? ARTIS_MA_ACTION_RADDEEXC
+                    : (p < b4)                 ? ARTIS_MA_ACTION_RADRECOMB
+                    : (p < b5)                 ? ARTIS_MA_ACTION_INTERNALDOWNLOWER
+                                               : ARTIS_MA_ACTION_INTERNALUPHIGHER;
+      for (int j = ty; j < 64; j += 4) {
+        if (c0 + j >= n_ne) break;
+        const uint32_t key = (a < 0) ? s_akey[p][j] : ma_key32(tile[tx][j], s_norm[a][j]);
+        uint16_t *rec = K.C.ma_key + (c0 + j) * K.C.ma_key_stride + mm.rec_off;
+        rec[p] = (uint16_t)(key >> 16);
+        rec[ma_lo_off(len) + p] = (uint16_t)(key & 0xffffu);
+      }
+    }
   }
 }
 
@@ -456,9 +444,9 @@ struct Engine {
   // sizes
   int npts_model = 0, nelements = 0, maxnions = 0, nions_total = 0, nlines = 0, ngrid = 0, ntstep = 0;
   int64_t n_est_doubles = 0;  // J..bfheat + scalars
-  int64_t ma_rec_stride = 0;
-  std::vector<int64_t> h_rec_off;  // record offset per level (+ stride at the end), ascending in level index
-  double *d_marec_scratch = nullptr;  // k_marates output, [position][cell] per level (engine.hip k_marec)
+  int64_t ma_key_stride = 0;          // 16-bit keys per cell block of the macro-atom cache
+  std::vector<int64_t> h_dbl_off;     // per level: offset (doubles) of its exact sums in the k_marates scratch
+  double *d_marec_scratch = nullptr;  // k_marates output, [position][cell] per level (k_mapack input)
   int64_t marec_scratch_doubles = 0;
   double *d_estblock = nullptr;
   int32_t *d_target_ul = nullptr, *d_target_t = nullptr;
@@ -774,12 +762,13 @@ int run_wavefront(int64_t n, int nts, double t2) {
       k_ma_scatter<<<grid, WAVE_BLOCK, 0, G.stream>>>(W, G.d_binoffs);
     }
     HIPCHK(hipMemsetAsync(W.xhead, 0, 8 * sizeof(uint32_t), G.stream));
-    // ARTIS_GPU_MA_WAVES=w: launch only w blocks per CU (w resident waves per SIMD) -- fewer concurrent walks
-    // thrash the caches less; the walk is bound by the memory system, not by latency hiding
+    // ARTIS_GPU_MA_WAVES=w (default 4): launch only w blocks per CU (w resident waves per SIMD) -- fewer
+    // concurrent walks thrash the caches less; the walk is bound by the memory system, not by latency hiding
+    // (1e7-packet bench: 2 waves 4694 ms, 3: 3761 ms, 4: 3317 ms, 8: 3725 ms; profiles/r02_ab_ma_waves.txt)
     static const int ma_waves = [] {
       const char *e = getenv("ARTIS_GPU_MA_WAVES");
-      const int v = e ? atoi(e) : 0;
-      return (v >= 1 && v <= 8) ? v : 0;
+      const int v = e ? atoi(e) : 4;
+      return (v >= 1 && v <= 8) ? v : 4;
     }();
     const unsigned ma_grid = ma_waves ? (unsigned)(G.wave_grid / 8 * ma_waves) : grid;
     if (G.K.C.have_macache) {
@@ -790,8 +779,12 @@ int run_wavefront(int64_t n, int nts, double t2) {
     } else {
       k_ma<false, 1><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
     }
-    TEND(1);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QM, 0, 2 * sizeof(uint32_t), G.stream));
+    if (G.K.C.have_macache) {  // jumps the 32-bit keys could not decide (rare), exact; walks go back to M
+      k_ma_exact<<<grid / 8, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+      HIPCHK(hipMemsetAsync(W.ctr + 2 * QX, 0, 2 * sizeof(uint32_t), G.stream));
+    }
+    TEND(1);
     TSTART(2);
     k_kpkt<<<grid / 4, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
     TEND(2);
@@ -837,6 +830,7 @@ int run_wavefront(int64_t n, int nts, double t2) {
             "lane-mean %.3f\n",
             st[0] ? (double)st[24] / st[0] : 0., st[0] ? (double)st[25] / (64.0 * st[0]) : 0.,
             st[0] ? (double)st[26] / st[0] : 0., st[0] ? (double)st[27] / (64.0 * st[0]) : 0.);
+    fprintf(stderr, "[artis_gpu] macro-atom jumps made with the exact sums (undecided 32-bit keys): %llu\n", st[40]);
     if (st[32] + st[33] + st[34] + st[35] + st[36])
       fprintf(stderr,
               "[artis_gpu] rpkt step phases (cycles/pass): boundary %.0f, kappa %.0f, line loop %.0f, move+estimators "
@@ -1186,6 +1180,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   // of the lower ion for levels l <= maxrecombininglevel of ions i > 0 (macroatom.cc:104-124); up-higher targets
   // are the phixs targets of ionising levels of non-top ions (get_nphixstargets)
   std::vector<MaMeta> mm(nl);
+  std::vector<int64_t> dbl_off(nl + 1, 0);  // exact-sum scratch of k_marates (doubles, unpadded)
   int64_t marec = 0;
   int nmax = 1;
   for (int e = 0; e < ne; e++)
@@ -1203,11 +1198,15 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
         m.base_lower = (i > 0) ? a->ion_uniqueleveloffset[ui - 1] : -1;
         m.rec_off = (int32_t)marec;
         const int64_t len = ARTIS_MA_ACTION_COUNT + 2 * (int64_t)m.nd + m.nu + 2 * (int64_t)m.nr + m.nt;
-        marec += (len + 15) / 16 * 16;  // 128-byte aligned records: totals + the tree tops share a line
+        marec += (2 * len + 63) / 64 * 64;  // high then low key halves, records 128-byte aligned
+        dbl_off[ul + 1] = len;
         nmax = std::max(nmax, std::max(m.nd, m.nu));
       }
     }
   rc |= dupload(&T.ma_meta, mm.data(), nl);
+  for (int ul = 0; ul < nl; ul++) dbl_off[ul + 1] += dbl_off[ul];
+  rc |= dupload(&T.ma_dbl_off, dbl_off.data(), nl + 1);
+  G.h_dbl_off = dbl_off;
   {
     // Eytzinger positions: in-order traversal of the implicit tree 1..n gives the sorted order
     std::vector<int32_t> off(nmax + 2, 0), inv;
@@ -1257,10 +1256,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     rc |= dupload(&T.down_target_eyt, dt.data(), dt.size());
     rc |= dupload(&T.up_target_eyt, ut.data(), ut.size());
   }
-  G.ma_rec_stride = marec;
-  G.h_rec_off.resize(nl + 1);
-  for (int ul = 0; ul < nl; ul++) G.h_rec_off[ul] = mm[ul].rec_off;
-  G.h_rec_off[nl] = marec;
+  G.ma_key_stride = marec;
   rc |= dupload(&T.allcont_nu_edge, a->allcont_nu_edge, nb);
   rc |= dupload(&T.allcont_probability, a->allcont_probability, nb);
   rc |= dupload(&T.allcont_element, a->allcont_element, nb);
@@ -1397,30 +1393,35 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   rc |= dalloc(&C.popsT, (size_t)nne_cells * nl);
   rc |= dalloc(&C.corrphotT, (size_t)nne_cells * (ntg + 1));
   rc |= dalloc(&C.cooling, (size_t)nne_cells * a->ncoolingterms);
-  C.ma_rec_stride = G.ma_rec_stride;
+  C.ma_key_stride = G.ma_key_stride;
   C.have_macache = 0;
-  C.ma_rec = nullptr;
+  C.ma_key = nullptr;
   C.marates = nullptr;
   {
     size_t freeb = 0, totalb = 0;
     (void)hipMemGetInfo(&freeb, &totalb);
-    const double need = (double)nne_cells * (double)C.ma_rec_stride * 8.0;
-    // k_marates scratch: up to 1/8 of the cache, at least the largest level's records
+    const double need = (double)nne_cells * (double)C.ma_key_stride * 2.0;
+    // k_marates scratch (exact double sums of a batch of levels): at least the largest level's, by default
+    // up to 2 GiB (ARTIS_GPU_MAREC_SCRATCH_MB)
     int64_t maxlev = 0;
-    for (int ul = 0; ul < nl; ul++) maxlev = std::max(maxlev, G.h_rec_off[ul + 1] - G.h_rec_off[ul]);
-    int64_t scratch = (int64_t)(need / 8.0 / 8.0);
+    for (int ul = 0; ul < nl; ul++) maxlev = std::max(maxlev, G.h_dbl_off[ul + 1] - G.h_dbl_off[ul]);
+    int64_t scratch = std::min<int64_t>(G.h_dbl_off[nl] * nne_cells, ((int64_t)2 << 30) / 8);
     if (const char *sm = getenv("ARTIS_GPU_MAREC_SCRATCH_MB")) scratch = (int64_t)(atof(sm) * (1 << 20) / 8);
     scratch = std::max<int64_t>(maxlev * nne_cells, scratch);
+    // the cache takes at most ARTIS_GPU_MACACHE_MAX_GB (default: half of the free HBM, the rest is left for the
+    // packet store); without it the walk recomputes the individual rates (k_ma<false>, identical results)
+    double budget = 0.5 * (double)freeb;
+    if (const char *mx = getenv("ARTIS_GPU_MACACHE_MAX_GB")) budget = atof(mx) * (double)(1ull << 30);
     const char *env = getenv("ARTIS_GPU_NO_MACACHE");
-    if (!(env && env[0] == '1') && need + 8.0 * (double)scratch < 0.75 * (double)freeb) {
-      double *mc = nullptr, *sc = nullptr;
-      if (hipMalloc((void **)&mc, (size_t)need) == hipSuccess) {
+    if (!(env && env[0] == '1') && need + 8.0 * (double)scratch < budget) {
+      void *mc = nullptr, *sc = nullptr;
+      if (dmalloc(&mc, (size_t)need) == hipSuccess) {
         G.allocs.push_back(mc);
-        if (hipMalloc((void **)&sc, (size_t)scratch * 8) == hipSuccess) {
+        if (dmalloc(&sc, (size_t)scratch * 8) == hipSuccess) {
           G.allocs.push_back(sc);
-          C.ma_rec = mc;
+          C.ma_key = (uint16_t *)mc;
           C.have_macache = 1;
-          G.d_marec_scratch = sc;
+          G.d_marec_scratch = (double *)sc;
           G.marec_scratch_doubles = scratch;
         }
       }
@@ -1547,11 +1548,11 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
       // batches of levels whose records fit the scratch
       for (int ul0 = 0; ul0 < nl;) {
         int ul1 = ul0 + 1;
-        while (ul1 < nl && (G.h_rec_off[ul1 + 1] - G.h_rec_off[ul0]) * n_ne <= G.marec_scratch_doubles) ul1++;
+        while (ul1 < nl && (G.h_dbl_off[ul1 + 1] - G.h_dbl_off[ul0]) * n_ne <= G.marec_scratch_doubles) ul1++;
         const int nlev = ul1 - ul0;
         k_marates<<<(unsigned)(((int64_t)nlev * n_ne + 255) / 256), 256, 0, G.stream>>>(G.K, nts, ul0, nlev,
                                                                                         G.d_marec_scratch);
-        k_marec<<<dim3((unsigned)((n_ne + 63) / 64), (unsigned)nlev), 256, 0, G.stream>>>(G.K, ul0,
+        k_mapack<<<dim3((unsigned)((n_ne + 63) / 64), (unsigned)nlev), 256, 0, G.stream>>>(G.K, ul0,
                                                                                           G.d_marec_scratch);
         ul0 = ul1;
       }

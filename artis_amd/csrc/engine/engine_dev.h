@@ -19,7 +19,7 @@
 
 // static per-level data of the cached macro-atom walk (two 16-byte loads; the table is L2-resident)
 struct __attribute__((aligned(16))) MaMeta {
-  int32_t rec_off;     // offset (doubles) of the level's record inside a cell's block
+  int32_t rec_off;     // offset (16-bit keys) of the level's compact record inside a cell's key block
   int32_t doff, uoff;  // level_downtrans_offset, level_uptrans_offset
   int32_t base_lower;  // unique index of level 0 of the next lower ion (-1 if none)
   int32_t nd, nu, nr, nt;  // #downtrans, #uptrans, #recombination targets, #ionisation targets
@@ -67,6 +67,7 @@ struct DevTab {
   // per level: offset (doubles) of its macro-atom record inside a cell's record block, #downtrans, #uptrans,
   // #recombination targets (ionising levels of the lower ion, 0 if the level does not recombine)
   const MaMeta *ma_meta;  // [nlevels_total]
+  const int64_t *ma_dbl_off;  // [nlevels_total + 1] offset (doubles) of each level's exact record in k_marates' scratch
   // targets of the internal same-ion jumps in Eytzinger order of their level's cumulative arrays:
   // (unique level index, offset of its macro-atom record in a cell block)
   const int2 *down_target_eyt, *up_target_eyt;
@@ -84,6 +85,9 @@ struct DevTab {
   const int32_t *g_nlines, *g_off;
   const double *g_endecay, *g_energy, *g_prob;
 };
+
+// offset (keys) of the low halves inside a macro-atom record of len positions (right after the high halves)
+static inline __host__ __device__ int ma_lo_off(int len) { return len; }
 
 struct DevGeom {
   int32_t ncoordgrid[3];
@@ -113,15 +117,20 @@ struct DevCells {
   double *popsT;       // [nlevels_total * n_nonempty]
   double *corrphotT;   // [ntargets_total * n_nonempty]
   double *cooling;     // [n_nonempty * ncoolingterms]  cumulative cooling_contrib (kpkt.cc:167-308)
-  // macro-atom cache: per (cell, level) one contiguous record, 128-byte aligned: the 9 processrates totals
-  // (macroatom.cc:57-159), then the running sums of the individual rates (the cellhistory individ_* arrays,
-  // globals.h:174-183) summed in the reference's order, so that a search returns the reference's linear-scan
-  // choice.  The two arrays of the internal same-ion jumps -- most of all jumps -- are stored in Eytzinger
-  // (BFS) order right after the totals, so the first levels of their search tree share the totals' cache line:
-  //   [9 totals | internal_down_same (nd, Eytzinger) | internal_up_same (nu, Eytzinger) | rad_deexc (nd) |
-  //    rad_recomb (nr) | internal_down_lower (nr) | internal_up_higher (nt)]
-  double *ma_rec;      // [n_nonempty * ma_rec_stride], or nullptr
-  int64_t ma_rec_stride;
+  // macro-atom cache: per (cell, level) one compact record of 32-bit keys, 128-byte aligned.  A key is a running
+  // sum of the reference's individual rates (the cellhistory individ_* arrays, globals.h:174-183, summed in the
+  // reference's order, macroatom.cc:57-159) divided by its action's total and rounded to 32 bits; the first 9 are
+  // the running sums of the 9 process-rate totals over their grand total.  The keys' high halves come first (the
+  // hot part: a typical jump reads one 128-byte line of them) and their low halves after (read only when the high
+  // half cannot decide a comparison).  A search compares the uniform draw with the keys; a key within rounding of
+  // the draw leaves the comparison undecided and the jump is made with the exact sums (ma_jump_exact) -- the
+  // selections are the reference's linear-scan choices either way.  The two arrays of the internal same-ion
+  // jumps (most jumps) come first, in Eytzinger (BFS) order:
+  //   [9 action keys | internal_down_same (nd, Eytzinger) | internal_up_same (nu, Eytzinger) | rad_deexc (nd) |
+  //    rad_recomb (nr) | internal_down_lower (nr) | internal_up_higher (nt)]  high halves, then the same
+  //   positions' low halves; the record padded to a multiple of 64 keys
+  uint16_t *ma_key;    // [n_nonempty * ma_key_stride], or nullptr
+  int64_t ma_key_stride;
   int32_t have_macache;
   double *marates;     // without the cache: [n_nonempty * nlevels_total * 9] totals only
 };

@@ -346,4 +346,108 @@ DEVFN double col_ionization_ratecoeff(const Ctx &K, float T_e, float nne, int e,
   return nne * 1.55e13 * pow((double)T_e, -0.5) * g * sigma_bf * exp(-fac1) / fac1;
 }
 
+// calculate_macroatom_transitionrates (macroatom.cc:57-159): every individual rate of unique level ul in cell mgi,
+// in the reference's order -- down transitions, recombination targets, up transitions, photoionisation targets --
+// handed to f(kind, j, R, C, epsilon_trans, epsilon_target, epsilon_current); pop(u) is the cell's population of
+// unique level u, corrphot(slot) its corrected photoionisation coefficient.  The precompute (k_marates) and the
+// exact path of the cached walk both go through here, so their running sums are the same bit for bit.
+// f returns true to stop early.
+enum { MA_KIND_DOWN = 0, MA_KIND_RECOMB = 1, MA_KIND_UP = 2, MA_KIND_UPHIGHER = 3 };
+template <typename Pop, typename Corr, typename F>
+DEVFN void ma_foreach_rate(const Ctx &K, int mgi, int ul, double t_mid, Pop pop, Corr corrphot, F f) {
+  const int ui = K.T.level_ui[ul];
+  const int e = K.T.ion_element[ui];
+  const int i = ui - K.T.elem_uniqueionoffset[e];
+  const int l = ul - K.T.ion_uniqueleveloffset[ui];
+  const float T_e = K.C.Te[mgi];
+  const float nne = K.C.nne[mgi];
+  const double n_self = pop(ul);
+  const double epsilon_current = K.T.level_epsilon[ul];
+  const double statweight = K.T.level_stat_weight[ul];
+  const int ndowntrans = K.T.level_ndowntrans[ul];
+  const int doff = K.T.level_downtrans_offset[ul];
+  for (int j = 0; j < ndowntrans; j++) {
+    const int li = K.T.downtrans_lineindex[doff + j];
+    const int lower = K.T.line_lower[li];
+    const double epsilon_target = epsilon(K, e, i, lower);
+    const double epsilon_trans = epsilon_current - epsilon_target;
+    const double n_l = pop(ul - l + lower);
+    const double R = rad_deexcitation_ratecoeff_n(K, n_self, n_l, li, t_mid);
+    const double C = col_deexcitation_ratecoeff(K, T_e, nne, epsilon_trans, li, stat_weight(K, e, i, lower), statweight);
+    if (f(MA_KIND_DOWN, j, R, C, epsilon_trans, epsilon_target, epsilon_current)) return;
+  }
+  if (i > 0 && l <= K.T.ion_maxrecombininglevel[ui]) {
+    const int nlevels = get_ionisinglevels(K, e, i - 1);
+    for (int lower = 0; lower < nlevels; lower++) {
+      const double epsilon_target = epsilon(K, e, i - 1, lower);
+      const double epsilon_trans = epsilon_current - epsilon_target;
+      const double R = rad_recombination_ratecoeff(K, T_e, nne, e, i, l, lower);
+      const double C = col_recombination_ratecoeff(K, mgi, e, i, l, lower, epsilon_trans);
+      if (f(MA_KIND_RECOMB, lower, R, C, epsilon_trans, epsilon_target, epsilon_current)) return;
+    }
+  }
+  const int nuptrans = K.T.level_nuptrans[ul];
+  const int uoff = K.T.level_uptrans_offset[ul];
+  const double T_R = K.C.TR[mgi], W = K.C.W[mgi];
+  for (int j = 0; j < nuptrans; j++) {
+    const int li = K.T.uptrans_lineindex[uoff + j];
+    const int upper = K.T.line_upper[li];
+    const double epsilon_trans = epsilon(K, e, i, upper) - epsilon_current;
+    const double n_u = pop(ul - l + upper);
+    const double R = rad_excitation_ratecoeff_n(K, n_u, n_self, T_R, W, epsilon_trans, li, t_mid);
+    const double C = col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, e, i, upper));
+    if (f(MA_KIND_UP, j, R, C, epsilon_trans, 0., epsilon_current)) return;
+  }
+  if (i < K.T.elem_nions[e] - 1 && l < K.T.ion_ionisinglevels[ui]) {
+    const int nt = K.T.level_nphixstargets[ul];
+    const int slot0 = K.T.level_phixstargets_offset[ul];
+    for (int t = 0; t < nt; t++) {
+      const double epsilon_trans = get_phixs_threshold(K, e, i, l, t);
+      const double R = corrphot(slot0 + t);
+      const double C = col_ionization_ratecoeff(K, T_e, nne, e, i, l, t, epsilon_trans);
+      if (f(MA_KIND_UPHIGHER, t, R, C, epsilon_trans, 0., epsilon_current)) return;
+    }
+  }
+}
+
+// 32-bit key of a running sum v of an action whose total is norm (DevCells::ma_key): round(v / norm * (2^32 - 1)),
+// stored as two 16-bit halves (hi in the hot array, lo in the record's second half)
+#define MA_KEY_SCALE 4294967295.0
+DEVFN uint32_t ma_key32(double v, double norm) {
+  if (!(norm > 0.)) return 0u;
+  const double q = floor(v / norm * MA_KEY_SCALE + 0.5);
+  return (uint32_t)(q < 0. ? 0. : (q > MA_KEY_SCALE ? MA_KEY_SCALE : q));
+}
+// Decides `running sum > x` for x = u * norm (u the uniform draw, q = u * MA_KEY_SCALE) from the key: +1 greater,
+// -1 not greater, 0 undecided.  A key is within 0.5 (+ ~1e-5 of rounding in the divisions) of the exact value on
+// the 2^32 scale, and q within ~1e-5 of x / norm on that scale.  ma_key_cmp_hi decides from the high half alone
+// when it can (the key lies in [hi * 65536, hi * 65536 + 65535]) and returns 2 when the low half is needed.
+#define MA_KEY_BAND (0.5 + 1e-4)
+DEVFN int ma_key_cmp(uint32_t key, double q) {
+  const double d = (double)key - q;
+  return d > MA_KEY_BAND ? 1 : (d < -MA_KEY_BAND ? -1 : 0);
+}
+DEVFN int ma_key_cmp_hi(uint32_t hi, double q) {
+  const double d = (double)hi * 65536.0 - q;
+  return d > MA_KEY_BAND ? 1 : (d < -(65535.0 + MA_KEY_BAND) ? -1 : 2);
+}
+
+// the processrates sums of macroatom.cc:57-159 for one individual rate
+DEVFN void ma_accumulate(double pr[ARTIS_MA_ACTION_COUNT], int kind, double R, double C, double epsilon_trans,
+                         double epsilon_target, double epsilon_current) {
+  if (kind == MA_KIND_DOWN) {
+    pr[ARTIS_MA_ACTION_RADDEEXC] += R * epsilon_trans;
+    pr[ARTIS_MA_ACTION_COLDEEXC] += C * epsilon_trans;
+    pr[ARTIS_MA_ACTION_INTERNALDOWNSAME] += (R + C) * epsilon_target;
+  } else if (kind == MA_KIND_RECOMB) {
+    pr[ARTIS_MA_ACTION_INTERNALDOWNLOWER] += (R + C) * epsilon_target;
+    pr[ARTIS_MA_ACTION_RADRECOMB] += R * epsilon_trans;
+    pr[ARTIS_MA_ACTION_COLRECOMB] += C * epsilon_trans;
+  } else if (kind == MA_KIND_UP) {
+    pr[ARTIS_MA_ACTION_INTERNALUPSAME] += (R + C + 0.) * epsilon_current;
+  } else {
+    pr[ARTIS_MA_ACTION_INTERNALUPHIGHER] += (R + C) * epsilon_current;
+  }
+}
+
 #endif

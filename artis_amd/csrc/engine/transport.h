@@ -1010,7 +1010,11 @@ struct MaLane {
   unsigned jumps;
   unsigned long long ntrans;
 };
-enum { MA_CONTINUE = 0, MA_END_BB = 1, MA_END_COLDEEXC = 2, MA_END_COLRECOMB = 3, MA_END_FB = 4, MA_FAILED = -1 };
+enum { MA_CONTINUE = 0, MA_END_BB = 1, MA_END_COLDEEXC = 2, MA_END_COLRECOMB = 3, MA_END_FB = 4, MA_FAILED = -1,
+       MA_DEFER = -2 };
+// WaveState::pend code of a walk parked between jumps (.y = unique level it stands on): set when a jump of the
+// cached walk needs the exact sums (k_ma_exact), read when the walk resumes in k_ma
+#define MA_RESUME 16
 struct MaEnd {
   int code, ion, a, b;  // BB: a = line, b = unique index of the emitting level;
                         // FB: a = level of the lower ion, b = unique index of the recombining level
@@ -1229,15 +1233,17 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
   return MA_FAILED;
 }
 
-// The cached walk in its lean form: lane state = (unique level, record offset, cell block).  Per jump: the
-// level's 32-byte MaMeta (L2-resident table) and its 9 totals (independent loads), then the search in the
-// selected cumulative array -- for the internal same-ion jumps (most jumps) an Eytzinger search whose first
-// tree levels sit in the totals' cache line -- and one 8-byte load of the target (level, record offset).
-// The walk is bound by HBM traffic, so the layout minimises cache lines touched per jump.
-// Same selections and RNG draws as the uncached ma_jump.
+// The cached walk in its lean form: lane state = (unique level, record offset, cell key block).  Per jump: the
+// level's 32-byte MaMeta (L2-resident table) and its compact key record (DevCells::ma_key): the 9 action keys,
+// then for the internal same-ion jumps (most jumps) an Eytzinger search over the keys of the selected action
+// that stays in the record's first 128-byte line for typical levels, and one 8-byte load of the target
+// (level, record offset).  The walk is bound by the memory system's random-access rate: one HBM
+// line per jump instead of the three to four of full double records.  A comparison the 32-bit keys cannot
+// decide sends the jump to ma_jump_exact, which recomputes the reference's exact sums; the selections -- and so
+// the RNG draws and every result -- are those of the uncached ma_jump.
 struct MaLaneC {
-  int ul, rec_off;
-  const double *block;  // K.C.ma_rec + k * ma_rec_stride
+  int ul, rec_off, k;
+  const uint16_t *block;  // K.C.ma_key + k * ma_key_stride
   unsigned jumps;
   unsigned long long ntrans;
 };
@@ -1254,16 +1260,67 @@ DEVFN int eytzinger_first_above(const double *e, int n, double x, unsigned long 
   return (int)(k >> __ffs(~k));
 }
 
-DEVFN int ma_jump_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneC &m, MaEnd &end, int number) {
-  m.jumps++;
+// the outcome of selecting transition j (reference list order) of action sel at level ul: MA_CONTINUE with the
+// lane moved to the target level, or a deactivation in `end` (macroatom.cc:174-414)
+DEVFN int ma_apply_selection(const Ctx &K, const LocalCounters &L, MaLaneC &m, MaEnd &end, int sel, int j, int doff,
+                             int uoff, int base_lower) {
   const int ul = m.ul;
-  const double *rec = m.block + m.rec_off;
-  const int4 *mp = reinterpret_cast<const int4 *>(K.T.ma_meta + ul);
-  const int4 w0 = mp[0], w1 = mp[1];
-  const int doff = w0.y, uoff = w0.z, base_lower = w0.w, nd = w1.x, nu = w1.y, nr = w1.z, nt = w1.w;
-  const double2 *r2 = reinterpret_cast<const double2 *>(rec);
-  const double2 t01 = r2[0], t23 = r2[1], t45 = r2[2], t67 = r2[3];
-  const double pr[ARTIS_MA_ACTION_COUNT] = {t01.x, t01.y, t23.x, t23.y, t45.x, t45.y, t67.x, t67.y, rec[8]};
+  switch (sel) {
+    case ARTIS_MA_ACTION_INTERNALDOWNSAME:
+      m.ul = K.T.ion_uniqueleveloffset[K.T.level_ui[ul]] + K.T.line_lower[K.T.downtrans_lineindex[doff + j]];
+      m.rec_off = K.T.ma_meta[m.ul].rec_off;
+      return MA_CONTINUE;
+    case ARTIS_MA_ACTION_INTERNALUPSAME:
+      m.ul = K.T.ion_uniqueleveloffset[K.T.level_ui[ul]] + K.T.line_upper[K.T.uptrans_lineindex[uoff + j]];
+      m.rec_off = K.T.ma_meta[m.ul].rec_off;
+      return MA_CONTINUE;
+    case ARTIS_MA_ACTION_RADDEEXC:
+      end.code = MA_END_BB;
+      end.ion = 0;
+      end.a = K.T.downtrans_lineindex[doff + j];
+      end.b = ul;
+      return MA_END_BB;
+    case ARTIS_MA_ACTION_RADRECOMB:
+      end.code = MA_END_FB;
+      end.ion = 0;
+      end.a = j;
+      end.b = ul;
+      return MA_END_FB;
+    case ARTIS_MA_ACTION_INTERNALDOWNLOWER:
+      lctr(L, CTR_MA_STAT_INTERNALDOWNLOWER);
+      m.ul = base_lower + j;
+      m.rec_off = K.T.ma_meta[m.ul].rec_off;
+      return MA_CONTINUE;
+    default: {  // INTERNALUPHIGHER (macroatom.cc:382-414)
+      lctr(L, CTR_MA_STAT_INTERNALUPHIGHER);
+      const int ui = K.T.level_ui[ul];
+      m.ul = K.T.ion_uniqueleveloffset[ui + 1] + K.T.phixstarget_levelindex[K.T.level_phixstargets_offset[ul] + j];
+      m.rec_off = K.T.ma_meta[m.ul].rec_off;
+      return MA_CONTINUE;
+    }
+  }
+}
+
+// One jump of the cached walk with the reference's exact double sums, recomputed from the cell tables through
+// ma_foreach_rate (the very sums k_marates condensed into keys): macroatom.cc:502-525 and the transition search of
+// the selected action.  Draws zrand (and zr) itself; runs where a key comparison was undecided (k_ma_exact,
+// do_macroatom), with the lane's RNG counter reset to the start of the jump.
+DEVNI int ma_jump_exact(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneC &m, MaEnd &end, int number,
+                        double t_mid) {
+  m.jumps++;
+  const int ul = m.ul, k = m.k;
+  const int mgi = K.C.ne_mgi[k];
+  const MaMeta mm = K.T.ma_meta[ul];
+  const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
+  const double *corr = K.C.corrphot + (int64_t)k * K.T.ntargets_total;
+  auto pop = [&](int u) { return pops[u]; };
+  auto cph = [&](int slot) { return corr[slot]; };
+  double pr[ARTIS_MA_ACTION_COUNT];
+  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) pr[a] = 0.;
+  ma_foreach_rate(K, mgi, ul, t_mid, pop, cph, [&](int kind, int j, double R, double C, double et, double eg, double ec) {
+    ma_accumulate(pr, kind, R, C, et, eg, ec);
+    return false;
+  });
   double total_transitions = 0.;
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) total_transitions += pr[a];
   const double zrand = artis_rng_uniform(&rng);
@@ -1290,12 +1347,124 @@ DEVFN int ma_jump_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
     fail(K, ERR_MA_SELECT, number, 100 + sel);
     return MA_FAILED;
   }
+  // the transition: first running sum of action sel above zr * total, in the reference's list order
   const double zr = artis_rng_uniform(&rng);
   const double x = zr * pr[sel];
+  const int kind = (sel == ARTIS_MA_ACTION_RADDEEXC || sel == ARTIS_MA_ACTION_INTERNALDOWNSAME) ? MA_KIND_DOWN
+                   : (sel == ARTIS_MA_ACTION_RADRECOMB || sel == ARTIS_MA_ACTION_INTERNALDOWNLOWER) ? MA_KIND_RECOMB
+                   : (sel == ARTIS_MA_ACTION_INTERNALUPSAME) ? MA_KIND_UP
+                                                             : MA_KIND_UPHIGHER;
+  double run[ARTIS_MA_ACTION_COUNT];
+  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) run[a] = 0.;
+  int found = -1;
+  ma_foreach_rate(K, mgi, ul, t_mid, pop, cph, [&](int kd, int j, double R, double C, double et, double eg, double ec) {
+    ma_accumulate(run, kd, R, C, et, eg, ec);
+    if (kd == kind) m.ntrans++;
+    if (kd == kind && run[sel] > x) {
+      found = j;
+      return true;
+    }
+    return false;
+  });
+  if (found < 0) {
+    fail(K, ERR_MA_SELECT, number, 10 + sel);
+    return MA_FAILED;
+  }
+  return ma_apply_selection(K, L, m, end, sel, found, mm.doff, mm.uoff, mm.base_lower);
+}
+
+// MA_DEFER: a key comparison was undecided; the jump has not happened (m.jumps unchanged) and the caller resets
+// the RNG counter to its value before the call and runs ma_jump_exact.
+// line != nullptr (k_ma): the lane's 128-byte LDS slot, laid out chunk-major for the wave ([8][64] 16-byte
+// chunks, lane-linear per chunk: conflict-free writes).  When the action keys and both same-ion trees fit the
+// record's first 128-byte line (9 + nd + nu <= 64, ~99% of levels), the line is fetched with 8 independent
+// 16-byte loads, staged there, and the tree search probes LDS instead of making one dependent trip to the
+// cache hierarchy per tree level.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds_uint4;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef const __attribute__((address_space(1))) u32x4 glb_uint4;
+DEVFN int ma_jump_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneC &m, MaEnd &end, int number,
+                         lds_uint4 *line = nullptr) {
+  const int ul = m.ul;
+  const uint16_t *rec = m.block + m.rec_off;
+  const int4 *mp = reinterpret_cast<const int4 *>(K.T.ma_meta + ul);
+  const int4 w0 = mp[0], w1 = mp[1];
+  const int doff = w0.y, uoff = w0.z, base_lower = w0.w, nd = w1.x, nu = w1.y, nr = w1.z, nt = w1.w;
+  const bool staged = line != nullptr && ARTIS_MA_ACTION_COUNT + nd + nu <= 64;
+  if (staged) {
+    glb_uint4 *src = (glb_uint4 *)rec;
+    const u32x4 c0 = src[0], c1 = src[1], c2 = src[2], c3 = src[3], c4 = src[4], c5 = src[5], c6 = src[6],
+                c7 = src[7];
+    line[0] = c0;
+    line[64] = c1;
+    line[128] = c2;
+    line[192] = c3;
+    line[256] = c4;
+    line[320] = c5;
+    line[384] = c6;
+    line[448] = c7;
+  }
+  auto hot = [&](int p) -> uint32_t {
+    return (staged && p < 64) ? (uint32_t)((lds_u16 *)(line + (p >> 3) * 64))[p & 7] : (uint32_t)rec[p];
+  };
+  const int loff = ma_lo_off(ARTIS_MA_ACTION_COUNT + 2 * nd + nu + 2 * nr + nt);  // low halves
+  const u32x4 a8 = staged ? line[0] : *(glb_uint4 *)rec;  // action keys 0..7 (records are 128-byte aligned)
+  const uint32_t key8 = hot(8);
+  const double zrand = artis_rng_uniform(&rng);
+  const double q = zrand * MA_KEY_SCALE;
+  // high half first; the low half only when needed; undecided at 32 bits: park the jump (MA_DEFER)
+  auto cmp = [&](int p, uint32_t hi) {
+    const int c = ma_key_cmp_hi(hi, q);
+    return c != 2 ? c : ma_key_cmp((hi << 16) | rec[loff + p], q);
+  };
+  int sel = -1;
+  {
+#pragma unroll
+    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
+      const uint32_t wd = (a < 2) ? a8.x : (a < 4) ? a8.y : (a < 6) ? a8.z : a8.w;
+      const uint32_t hi = (a < 8) ? (wd >> (16 * (a & 1))) & 0xffffu : key8;
+      const int c = cmp(a, hi);
+      if (c > 0) {
+        sel = a;
+        break;
+      }
+      if (c == 0) break;
+    }
+  }
+  if (sel < 0) return MA_DEFER;
+  m.jumps++;
+  if (sel == ARTIS_MA_ACTION_COLDEEXC || sel == ARTIS_MA_ACTION_COLRECOMB) {
+    end.code = (sel == ARTIS_MA_ACTION_COLDEEXC) ? MA_END_COLDEEXC : MA_END_COLRECOMB;
+    end.ion = end.a = end.b = 0;
+    return end.code;
+  }
+  if (sel == ARTIS_MA_ACTION_INTERNALUPHIGHERNT) {
+    fail(K, ERR_MA_SELECT, number, 100 + sel);
+    return MA_FAILED;
+  }
+  const double zr = artis_rng_uniform(&rng);
+  const double q2 = zr * MA_KEY_SCALE;
+  auto cmp2 = [&](int p) {
+    const uint32_t hi = hot(p);
+    const int c = ma_key_cmp_hi(hi, q2);
+    return c != 2 ? c : ma_key_cmp((hi << 16) | rec[loff + p], q2);
+  };
   if (sel == ARTIS_MA_ACTION_INTERNALDOWNSAME || sel == ARTIS_MA_ACTION_INTERNALUPSAME) {
     const bool down = sel == ARTIS_MA_ACTION_INTERNALDOWNSAME;
     const int cnt = down ? nd : nu;
-    const int pos = eytzinger_first_above(rec + 8 + (down ? 0 : nd), cnt, x, m.ntrans);
+    const int e0 = ARTIS_MA_ACTION_COUNT - 1 + (down ? 0 : nd);  // e[k] at position e0 + k, k = 1..cnt
+    unsigned kk = 1;
+    while (kk <= (unsigned)cnt) {
+      const int c = cmp2(e0 + (int)kk);
+      m.ntrans++;
+      if (c == 0) {
+        m.jumps--;
+        return MA_DEFER;
+      }
+      kk = 2 * kk + (c < 0 ? 1u : 0u);
+    }
+    const int pos = (int)(kk >> __ffs(~kk));
     if (pos == 0) {
       fail(K, ERR_MA_SELECT, number, 10 + sel);
       return MA_FAILED;
@@ -1305,8 +1474,8 @@ DEVFN int ma_jump_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
     m.rec_off = t.y;
     return MA_CONTINUE;
   }
-  // the sorted cumulative arrays after the two Eytzinger ones (engine_dev.h DevCells::ma_rec)
-  const double *sorted = rec + ARTIS_MA_ACTION_COUNT + nd + nu;
+  // the sorted key arrays after the two Eytzinger ones
+  const int sorted = ARTIS_MA_ACTION_COUNT + nd + nu;
   int off, cnt;
   switch (sel) {
     case ARTIS_MA_ACTION_RADDEEXC: off = 0; cnt = nd; break;
@@ -1314,37 +1483,25 @@ DEVFN int ma_jump_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
     case ARTIS_MA_ACTION_INTERNALDOWNLOWER: off = nd + nr; cnt = nr; break;
     default: off = nd + 2 * nr; cnt = nt; break;  // INTERNALUPHIGHER
   }
-  const int j = first_above(sorted + off, cnt, x, m.ntrans);
-  if (j >= cnt) {
+  int lo = 0, hi = cnt;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    const int c = cmp2(sorted + off + mid);
+    m.ntrans++;
+    if (c == 0) {
+      m.jumps--;
+      return MA_DEFER;
+    }
+    if (c > 0)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  if (lo >= cnt) {
     fail(K, ERR_MA_SELECT, number, 10 + sel);
     return MA_FAILED;
   }
-  switch (sel) {
-    case ARTIS_MA_ACTION_RADDEEXC:
-      end.code = MA_END_BB;
-      end.ion = 0;
-      end.a = K.T.downtrans_lineindex[doff + j];
-      end.b = ul;
-      return MA_END_BB;
-    case ARTIS_MA_ACTION_RADRECOMB:
-      end.code = MA_END_FB;
-      end.ion = 0;
-      end.a = j;
-      end.b = ul;
-      return MA_END_FB;
-    case ARTIS_MA_ACTION_INTERNALDOWNLOWER:
-      lctr(L, CTR_MA_STAT_INTERNALDOWNLOWER);
-      m.ul = base_lower + j;
-      m.rec_off = K.T.ma_meta[m.ul].rec_off;
-      return MA_CONTINUE;
-    default: {  // INTERNALUPHIGHER (macroatom.cc:382-414)
-      lctr(L, CTR_MA_STAT_INTERNALUPHIGHER);
-      const int ui = K.T.level_ui[ul];
-      m.ul = K.T.ion_uniqueleveloffset[ui + 1] + K.T.phixstarget_levelindex[K.T.level_phixstargets_offset[ul] + j];
-      m.rec_off = K.T.ma_meta[m.ul].rec_off;
-      return MA_CONTINUE;
-    }
-  }
+  return ma_apply_selection(K, L, m, end, sel, lo, doff, uoff, base_lower);
 }
 
 DEVFN void ma_lane_init(const Ctx &K, MaLane &m, int where, int element, int ion, int level) {
@@ -1445,10 +1602,19 @@ DEVNI void do_macroatom(Tx &x, Pkt &p) {
     MaLaneC m;
     m.ul = ulev(K, p.ma_element, p.ma_ion, p.ma_level);
     m.rec_off = K.T.ma_meta[m.ul].rec_off;
-    m.block = K.C.ma_rec + (int64_t)K.C.ne_index[mgi] * K.C.ma_rec_stride;
+    m.k = K.C.ne_index[mgi];
+    m.block = K.C.ma_key + (int64_t)m.k * K.C.ma_key_stride;
     m.jumps = 0;
     m.ntrans = 0;
-    while ((r = ma_jump_cached(K, x.L, x.rng, m, e, p.number)) == MA_CONTINUE && m.jumps < MA_MAX_JUMPS) {
+    const double t_mid = K.G.ts_mid[x.nts];
+    while (true) {
+      const uint32_t n0 = x.rng.n;
+      r = ma_jump_cached(K, x.L, x.rng, m, e, p.number);
+      if (r == MA_DEFER) {
+        x.rng.n = n0;
+        r = ma_jump_exact(K, x.L, x.rng, m, e, p.number, t_mid);
+      }
+      if (r != MA_CONTINUE || m.jumps >= MA_MAX_JUMPS) break;
     }
     jumps = m.jumps;
     ntrans = m.ntrans;

@@ -23,7 +23,7 @@
 
 #include "gamma.h"
 
-enum { QR = 0, QM = 1, QK = 2, QG = 3, NQUEUES = 4 };
+enum { QR = 0, QM = 1, QK = 2, QG = 3, QX = 4, NQUEUES = 5 };  // QX: macro-atom jumps for k_ma_exact
 
 struct WaveState {
   uint32_t *rng_n;     // [N] draws consumed so far this timestep (artis_rng.n)
@@ -303,10 +303,13 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   const Ctx &K = *ctxp;
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
+  // per wave: the 128-byte hot line of each lane's current macro-atom record (ma_jump_cached), chunk-major
+  __shared__ uint4 s_line[WAVE_BLOCK / 64][8 * 64];
   block_counters_init(s_ctr, s_work);
   LocalCounters L;
   L.ctr = &s_ctr[0];
   L.work = &s_work[0];
+  lds_uint4 *line = CACHE ? (lds_uint4 *)&s_line[threadIdx.x >> 6][threadIdx.x & 63] : nullptr;
   const uint32_t nq = W.ctr[2 * QM];
   const int32_t *queue = W.ma_binned ? W.ma_sorted : W.q[QM];
   const int nr = W.ma_ranges;
@@ -317,7 +320,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   int32_t idx = -1;
   bool have = false, drained = false;
   int cur = (int)(blockIdx.x % (unsigned)nr), tried = 0;
-  bool pendR = false, pendK = false;
+  bool pendR = false, pendK = false, pendX = false;
   unsigned long long jumps_sum = 0, trans_sum = 0;
   unsigned long long st_pass = 0, st_busy = 0, st_refill = 0, st_trefill = 0, st_tstep = 0;
   const unsigned long long st_t0 = wave_clock();
@@ -329,7 +332,8 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
       const unsigned long long tr0 = wave_clock();
       wave_push(W, QR, pendR, idx);
       wave_push(W, QK, pendK, idx);
-      pendR = pendK = false;
+      wave_push(W, QX, pendX, idx);
+      pendR = pendK = pendX = false;
       if (imask) {
         const uint32_t lo = (uint32_t)((uint64_t)nq * cur / nr), hi = (uint32_t)((uint64_t)nq * (cur + 1) / nr);
         const uint32_t slot = wave_reserve(&W.xhead[cur], idle);
@@ -343,10 +347,18 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
           rng.n = W.rng_n[idx];
           const int mgi = cell_mgi(K, where);
           if constexpr (CACHE) {
-            mc.ul = ulev(K, lo32(w36), hi32(w36), lo32(w37));
+            const int4 pd = W.pend[idx];
+            if (pd.x == MA_RESUME) {  // a walk parked by k_ma_exact: continue from its level and jump count
+              mc.ul = pd.y;
+              mc.jumps = W.pend_jumps[idx];
+              W.pend[idx].x = 0;
+            } else {
+              mc.ul = ulev(K, lo32(w36), hi32(w36), lo32(w37));
+              mc.jumps = 0;
+            }
             mc.rec_off = K.T.ma_meta[mc.ul].rec_off;
-            mc.block = K.C.ma_rec + (int64_t)K.C.ne_index[mgi] * K.C.ma_rec_stride;
-            mc.jumps = 0;
+            mc.k = K.C.ne_index[mgi];
+            mc.block = K.C.ma_key + (int64_t)mc.k * K.C.ma_key_stride;
             mc.ntrans = 0;
           } else {
             ma_lane_init(K, m, where, lo32(w36), hi32(w36), lo32(w37));
@@ -376,13 +388,22 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
       int r;
       unsigned jumps;
       if constexpr (CACHE) {
-        r = ma_jump_cached(K, L, rng, mc, e, (int)rng.key1);
+        const uint32_t n0 = rng.n;
+        r = ma_jump_cached(K, L, rng, mc, e, (int)rng.key1, line);
         jumps = mc.jumps;
+        if (r == MA_DEFER) {  // park the walk before this jump; k_ma_exact makes it with the exact sums
+          W.pend[idx] = make_int4(MA_RESUME, mc.ul, 0, 0);
+          W.pend_jumps[idx] = jumps;
+          W.rng_n[idx] = n0;
+          trans_sum += mc.ntrans;
+          pendX = true;
+          have = false;
+        }
       } else {
         r = ma_jump(K, L, rng, m, t_mid, e, (int)rng.key1);
         jumps = m.jumps;
       }
-      if (r != MA_CONTINUE || jumps >= MA_MAX_JUMPS) {
+      if (have && (r != MA_CONTINUE || jumps >= MA_MAX_JUMPS)) {
         if (r == MA_CONTINUE) fail(K, ERR_STUCK, (int)rng.key1, 2);
         if (r > 0) {
           W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
@@ -404,6 +425,55 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   wave_stats_flush(W, 1, st_pass, st_busy, st_t0, st_refill, st_trefill, st_tstep);
   if (jumps_sum) atomicAdd(&s_work[WK_MA_JUMPS], jumps_sum);
   if (trans_sum) atomicAdd(&s_work[WK_MA_TRANS], trans_sum);
+  block_counters_flush(K, s_ctr, s_work);
+}
+
+// macro-atom jumps whose key comparisons were undecided (QX): one jump each with the exact sums (ma_jump_exact),
+// then the walk is parked again for k_ma (-> M queue) or its deactivation deferred like k_ma's (-> R / K queue).
+// Rare (a few per 10^5 jumps): one workitem per packet, grid-stride.
+__global__ __launch_bounds__(WAVE_BLOCK) void k_ma_exact(const Ctx *__restrict__ ctxp, WaveState W,
+                                                         const uint64_t *__restrict__ soa, int64_t n, int nts) {
+  const Ctx &K = *ctxp;
+  __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
+  __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
+  block_counters_init(s_ctr, s_work);
+  LocalCounters L;
+  L.ctr = &s_ctr[0];
+  L.work = &s_work[0];
+  const uint32_t nq = W.ctr[2 * QX];
+  const double t_mid = K.G.ts_mid[nts];
+  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x) {
+    const int32_t idx = W.q[QX][slot];
+    const int where = lo32(soa[PW(n, idx, 0)]);
+    artis_rng rng = artis_rng_init(K.R.seed, (int)hi32(soa[PW(n, idx, 33)]), nts, K.R.rank);
+    rng.n = W.rng_n[idx];
+    MaLaneC m;
+    m.ul = W.pend[idx].y;
+    m.jumps = W.pend_jumps[idx];
+    m.k = K.C.ne_index[cell_mgi(K, where)];
+    m.rec_off = K.T.ma_meta[m.ul].rec_off;
+    m.block = K.C.ma_key + (int64_t)m.k * K.C.ma_key_stride;
+    m.ntrans = 0;
+    MaEnd e;
+    const int r = ma_jump_exact(K, L, rng, m, e, (int)rng.key1, t_mid);
+    lwork(L, WK_MA_TRANS, m.ntrans);
+    atomicAdd(&W.stats[40], 1ull);  // diagnostics: exact jumps
+    W.rng_n[idx] = rng.n;
+    W.pend_jumps[idx] = m.jumps;
+    if (r == MA_CONTINUE) {
+      if (m.jumps >= MA_MAX_JUMPS) {
+        fail(K, ERR_STUCK, (int)rng.key1, 2);
+        continue;
+      }
+      W.pend[idx] = make_int4(MA_RESUME, m.ul, 0, 0);
+      W.q[QM][atomicAdd(&W.ctr[2 * QM], 1u)] = idx;
+    } else if (r > 0) {
+      W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
+      lwork(L, WK_MA_JUMPS, m.jumps);
+      const int q = (r == MA_END_BB || r == MA_END_FB) ? QR : QK;
+      W.q[q][atomicAdd(&W.ctr[2 * q], 1u)] = idx;
+    }
+  }
   block_counters_flush(K, s_ctr, s_work);
 }
 

@@ -78,6 +78,17 @@ class RunParams(C.Structure):
         ("instant_particle_deposition", C.c_int32),
         ("nt_solve_spencerfano", C.c_int32),
         ("excitation_temperature", C.c_int32),
+        # ABI 6: the nebular options
+        ("nlte_pops_on", C.c_int32),
+        ("multibin_radfield", C.c_int32),
+        ("first_nlte_radfield_timestep", C.c_int32),
+        ("detailed_bf_estimators", C.c_int32),
+        ("detailed_bf_usefromtimestep", C.c_int32),
+        ("no_lut_photoion", C.c_int32),
+        ("no_lut_bfheating", C.c_int32),
+        ("nt_on", C.c_int32),
+        ("nt_max_auger_electrons", C.c_int32),
+        ("minpop", C.c_double),
     ]
 
 
@@ -108,6 +119,11 @@ class Estimators(C.Structure):
         ("counters", C.c_int64 * ARTIS_COUNTER_COUNT),
         ("rpkt_emiss", C.POINTER(C.c_double)),
         ("nt_energy_deposited", C.c_double),
+        # ABI 6 (NULL unless the nebular options are on)
+        ("bfrate_raw", C.POINTER(C.c_double)),
+        ("radfield_J_raw", C.POINTER(C.c_double)),
+        ("radfield_nuJ_raw", C.POINTER(C.c_double)),
+        ("radfield_contribcount", C.POINTER(C.c_int64)),
     ]
 
 

@@ -197,6 +197,19 @@ typedef struct artis_atomic_tables {
   const int32_t *coolinglist_ion;
   const int32_t *coolinglist_level;
   const int32_t *coolinglist_upperlevel;
+
+  /* ABI 6 -- NLTE populations (NLTE_POPS_ON; ltepop.cc:349-415, input.cc:1711-1746): per ion the number of NLTE
+     excited levels (levels 1..nlevels_nlte; the remaining excited levels form one superlevel if there are any) and
+     the index of its first entry in a cell's nlte_pops vector; total_nlte_levels entries per cell.  NULL / 0 when
+     NLTE populations are off. */
+  const int32_t *ion_nlevels_nlte;
+  const int32_t *ion_first_nlte;
+  int32_t total_nlte_levels;
+  /* binned radiation field (MULTIBIN_RADFIELD_MODEL_ON; radfield.cc:131-188, 574-608): upper frequency edge of each
+     bin and the lower edge of bin 0 */
+  int32_t radfield_nbins;
+  const double *radfield_nu_upper;   /* [radfield_nbins] */
+  double radfield_nu_lower_first;
 } artis_atomic_tables;
 
 /* ------------------------------------------------------------------------------------------------------------ */
@@ -236,6 +249,19 @@ typedef struct artis_cell_state {
   const double *corrphotoionrenorm;   /* [npts_model * nelements * maxnions] */
   const float *ffegrp;                /* [npts_model] Fe-group mass fraction (grid.cc:223), gamma opacities;
                                          may be NULL when no gamma packets are propagated */
+  /* ABI 6 (all may be NULL when the option that reads them is off) */
+  const double *nlte_pops;            /* [npts_model * total_nlte_levels] NLTE level population / rho (grid.h:33-65);
+                                         < -0.9: no solution yet, LTE is used (ltepop.cc:367-370) */
+  const float *radfield_bin_TR;       /* [npts_model * radfield_nbins] radfieldbin_solutions T_R and W of the fitted */
+  const float *radfield_bin_W;        /*   dilute blackbody per bin (radfield.cc:908-920); W < 0: no fit */
+  const float *bfrate_estimator;      /* [npts_model * nbfcontinua] prev_bfrate_normed, the normalised bf-rate
+                                         estimators of the previous timestep (radfield.cc:73, 1306-1316, used by
+                                         get_corrphotoioncoeff, ratecoeff.cc:1255-1261); <= 0: none */
+  const double *nt_deposition_rate_density;  /* [npts_model] (nonthermal.cc:659) */
+  const double *nt_ionization_ratecoeff;     /* [npts_model * nions_total] nt_ionization_ratecoeff (nonthermal.cc:
+                                                1684-1709, evaluated by the host update_grid incl. its fallbacks) */
+  const float *nt_prob_num_auger;            /* [npts_model * nions_total * (nt_max_auger_electrons + 1)] */
+  const float *nt_ionenfrac_num_auger;       /*   nt_solution prob_num_auger / ionenfrac_num_auger (nonthermal.cc:136-139) */
 } artis_cell_state;
 
 /* Run-time switches of input.txt / artisoptions.h that change hot-path behaviour. */
@@ -257,6 +283,19 @@ typedef struct artis_run_params {
   int32_t excitation_temperature; /* LTEPOP_EXCITATIONTEMPERATURE of calculate_levelpop_lte (ltepop.cc:338):
                                      ARTIS_TEXC_TJ (artisoptions_classic.h:32) or ARTIS_TEXC_TE
                                      (artisoptions_kilonova_lte.h:36, artisoptions_nltenebular.h:36) */
+  /* ABI 6: the nebular options (artisoptions_nltenebular.h) */
+  int32_t nlte_pops_on;                 /* NLTE_POPS_ON */
+  int32_t multibin_radfield;            /* MULTIBIN_RADFIELD_MODEL_ON: bin estimators; J_nu from the bins ... */
+  int32_t first_nlte_radfield_timestep; /* ... from timestep FIRST_NLTE_RADFIELD_TIMESTEP on (radfield.cc:901) */
+  int32_t detailed_bf_estimators;       /* DETAILED_BF_ESTIMATORS_ON: bfrate_raw, kappa_bf inclusion (rpkt.cc:1116) */
+  int32_t detailed_bf_usefromtimestep;  /* DETAILED_BF_ESTIMATORS_USEFROMTIMESTEP (ratecoeff.cc:1262) */
+  int32_t no_lut_photoion;              /* NO_LUT_PHOTOION: corrphotoioncoeff by integration (ratecoeff.cc:1184-1245) */
+  int32_t no_lut_bfheating;             /* NO_LUT_BFHEATING: no bfheatingestimator (rpkt.cc:576-613) */
+  int32_t nt_on;                        /* NT_ON: non-thermal ionisation macro-atom action (macroatom.cc:143-146) */
+  int32_t nt_max_auger_electrons;       /* NT_MAX_AUGER_ELECTRONS (artisoptions_nltenebular.h:193) */
+  double minpop;                        /* MINPOP: 1e-30 classic (artisoptions_classic.h:78), 1e-40 kilonova and
+                                           nebular (artisoptions_kilonova_lte.h:79, artisoptions_nltenebular.h:82);
+                                           0 is read as 1e-30 */
 } artis_run_params;
 enum artis_excitation_temperature { ARTIS_TEXC_TJ = 0, ARTIS_TEXC_TE = 1 };
 
@@ -284,6 +323,11 @@ typedef struct artis_estimators {
   double *rpkt_emiss;          /* [npts_model] grey gamma heating estimator rlc_emiss_gamma (grey_emissivities.cc:28-77,
                                   globals.cc:30); may be NULL */
   double nt_energy_deposited;  /* nonthermal.cc:115, added by do_ntlepton (nonthermal.cc:1878) */
+  /* ABI 6 (may be NULL when the option is off) */
+  double *bfrate_raw;          /* [npts_model * nbfcontinua] DETAILED_BF_ESTIMATORS_ON (radfield.cc:764-829) */
+  double *radfield_J_raw;      /* [npts_model * radfield_nbins] MULTIBIN_RADFIELD_MODEL_ON (radfield.cc:859-866) */
+  double *radfield_nuJ_raw;
+  int64_t *radfield_contribcount;
 } artis_estimators;
 
 /* ------------------------------------------------------------------------------------------------------------ */
@@ -455,10 +499,12 @@ int64_t artis_gpu_last_rounds(void);  /* event-queue rounds of the last update (
  * [0] r-packet, [1] macro-atom (incl. cell binning), [2] k-packet, [3] classify */
 int artis_gpu_last_kernel_times(double ms[4], int64_t launches[4]);
 const char *artis_gpu_last_error(void);
-#define ARTIS_GPU_ABI_VERSION 5  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
+#define ARTIS_GPU_ABI_VERSION 6  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
                                     3: virtual packets (artis_vpkt_params / artis_vpkt_result);
                                     4: artis_run_params.excitation_temperature;
-                                    5: host estimator block pack/unpack, RCCL communicator + all-reduce */
+                                    5: host estimator block pack/unpack, RCCL communicator + all-reduce;
+                                    6: the nebular path (NLTE / superlevel populations, binned radiation field,
+                                       detailed bf estimators, NO_LUT photoionisation, non-thermal ionisation) */
 int artis_gpu_abi_version(void);
 
 #ifdef __cplusplus

@@ -69,7 +69,7 @@ def test_c_header_layout_matches_numpy_and_ctypes():
     assert lay["vpkt_result"] == C.sizeof(ffi.VpktResult)
     assert lay["vpkt_tau_max"] == ffi.VpktParams.tau_max_vpkt.offset
     assert lay["vpkt_spawn_capacity"] == ffi.VpktParams.spawn_capacity.offset
-    assert lay["cell_state"] == 16 * 8  # 15 array pointers + ffegrp
+    assert lay["cell_state"] == 24 * 8  # 15 array pointers + ffegrp + 8 nebular (ABI 6)
 
 
 def test_header_declares_exactly_the_abi_symbols():
@@ -88,7 +88,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_without_gpu_and_reports_version():
     lib = C.CDLL(GPU_SO)
-    assert lib.artis_gpu_abi_version() == 5
+    assert lib.artis_gpu_abi_version() == 6
     lib.artis_gpu_last_error.restype = C.c_char_p
     assert lib.artis_gpu_last_error() is not None
 

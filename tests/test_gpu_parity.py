@@ -282,12 +282,14 @@ def test_allocation_failures_fail_cleanly(small_model, engine_factory, monkeypat
 def test_estimator_block_roundtrip_and_rccl(small_model, engine_factory):
     """The device block (artis_gpu_estimator_block_to_device) equals the host pack of the downloaded estimators
     (artis_estimator_block_pack, what the gloo test reduces); a block written back (from_device) is what the next
-    download returns; a one-rank RCCL communicator all-reduces it unchanged (artis_gpu_estimators_allreduce)."""
-    import torch
+    download returns; a one-rank RCCL communicator all-reduces it unchanged (artis_gpu_estimators_allreduce).
+    The device buffer comes from the engine's own HIP runtime (libamdhip64.so.7, loaded by libartis_gpu.so)."""
+    import ctypes as C
 
     from artis_amd import comm_unique_id, dist as adist
 
     eng = engine_factory(small_model)
+    hip = C.CDLL("libamdhip64.so.7")
     small_model.set_timestep(10)
     eng.upload_cellstate(10)
     pk = small_model.init_rpackets(10, 2000, seed=62)
@@ -298,14 +300,18 @@ def test_estimator_block_roundtrip_and_rccl(small_model, engine_factory):
     hb = adist.pack_estimators(host)
     n = eng.estimator_block_doubles()
     assert n == len(hb)
-    buf = torch.zeros(n, dtype=torch.float64, device="cuda")
-    torch.cuda.synchronize()
-    eng.estimator_block_to_device(buf.data_ptr())
-    db = buf.cpu().numpy()
-    assert np.array_equal(db, hb)
-    buf.mul_(2.0)
-    torch.cuda.synchronize()
-    eng.estimator_block_from_device(buf.data_ptr())
+    dptr = C.c_void_p()
+    assert hip.hipMalloc(C.byref(dptr), C.c_size_t(8 * n)) == 0
+    try:
+        eng.estimator_block_to_device(dptr.value)
+        db = np.zeros(n)
+        assert hip.hipMemcpy(C.c_void_p(db.ctypes.data), dptr, C.c_size_t(8 * n), 2) == 0  # D2H
+        assert np.array_equal(db, hb)
+        db *= 2.0
+        assert hip.hipMemcpy(dptr, C.c_void_p(db.ctypes.data), C.c_size_t(8 * n), 1) == 0  # H2D
+        eng.estimator_block_from_device(dptr.value)
+    finally:
+        hip.hipFree(dptr)
     twice = eng.download_estimators()
     assert np.array_equal(adist.pack_estimators(twice), 2 * hb)
     eng.comm_init(0, 1, comm_unique_id())
