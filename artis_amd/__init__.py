@@ -77,10 +77,10 @@ def gpu_lib():
         L.artis_gpu_vpkt_download.argtypes = [C.POINTER(ffi.VpktResult), C.c_int]
         L.artis_gpu_vpkt_last_stats.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
         L.artis_gpu_vpkt_last_work.argtypes = [C.POINTER(C.c_int64)]
-        L.artis_estimator_block_len.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int]
+        L.artis_estimator_block_len.argtypes = [C.c_int] * 6
         L.artis_estimator_block_len.restype = C.c_size_t
-        L.artis_estimator_block_pack.argtypes = [C.POINTER(ffi.Estimators), C.c_int, C.c_int, C.c_int, C.c_int, vp]
-        L.artis_estimator_block_unpack.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(ffi.Estimators)]
+        L.artis_estimator_block_pack.argtypes = [C.POINTER(ffi.Estimators)] + [C.c_int] * 6 + [vp]
+        L.artis_estimator_block_unpack.argtypes = [vp] + [C.c_int] * 6 + [C.POINTER(ffi.Estimators)]
         L.artis_gpu_comm_unique_id.argtypes = [vp]
         L.artis_gpu_comm_init.argtypes = [C.c_int, C.c_int, vp]
         L.artis_gpu_comm_finalize.restype = None

@@ -31,6 +31,7 @@
 #include "wavefront.h"
 #include "spectrum.h"
 #include "vpkt.h"
+#include "qag.h"
 
 // ================================================================================================= kernels
 
@@ -44,7 +45,7 @@ __global__ void k_cellprep(Ctx K) {
     for (int i = 0; i < K.T.elem_nions[e]; i++) {
       const int ui = uion(K, e, i);
       double gp = K.C.groundlevelpop[(int64_t)mgi * K.T.nions_total + ui];
-      if (gp < ARTIS_MINPOP) gp = (K.C.elem_abundance[(int64_t)mgi * K.T.nelements + e] > 0) ? ARTIS_MINPOP : 0.;
+      if (gp < K.R.minpop) gp = (K.C.elem_abundance[(int64_t)mgi * K.T.nelements + e] > 0) ? K.R.minpop : 0.;
       const double nnion = gp * K.C.partfunct[(int64_t)mgi * K.T.nions_total + ui] /
                            (double)K.T.level_stat_weight[K.T.ion_uniqueleveloffset[ui]];
       K.C.ionpop[(int64_t)k * K.T.nions_total + ui] = nnion;
@@ -67,18 +68,42 @@ __global__ void k_levelpops(Ctx K) {
   const int l = ul - K.T.ion_uniqueleveloffset[ui];
   const int ul0 = K.T.ion_uniqueleveloffset[ui];
   const bool hasabund = K.C.elem_abundance[(int64_t)mgi * K.T.nelements + e] > 0;
+  const double minpop = K.R.minpop;
   double ng = K.C.groundlevelpop[(int64_t)mgi * K.T.nions_total + ui];
-  if (ng < ARTIS_MINPOP) ng = hasabund ? ARTIS_MINPOP : 0.;
+  if (ng < minpop) ng = hasabund ? minpop : 0.;
+  const double T_exc = K.R.exc_te ? K.C.Te[mgi] : K.C.TJ[mgi];  // ltepop.cc:338
   double nn;
   if (l == 0) {
     nn = ng;
   } else {
-    const double T_exc = K.R.exc_te ? K.C.Te[mgi] : K.C.TJ[mgi];  // ltepop.cc:338
+    if (K.R.nlte_on) {
+      // ltepop.cc:349-415: NLTE levels 1..nlevels_nlte and the superlevel (nltepop.cc:1543-1554), unless the
+      // stored value marks "no NLTE solution yet" (< -0.9)
+      const int nn_nlte = K.T.ion_nlevels_nlte[ui];
+      const double *row = K.C.nlte_pops + (int64_t)mgi * K.T.total_nlte_levels + K.T.ion_first_nlte[ui];
+      const double rho = K.C.rho[mgi];
+      if (l <= nn_nlte) {
+        const double v = row[l - 1];
+        if (!(v < -0.9)) {
+          K.C.pops[idx] = v * rho;
+          return;
+        }
+      } else {
+        const double v = row[nn_nlte];
+        if (!(v < -0.9)) {
+          const int sl = ul0 + nn_nlte + 1;
+          const double boltz = (double)K.T.level_stat_weight[ul] / (double)K.T.level_stat_weight[sl] *
+                               exp(-(K.T.level_epsilon[ul] - K.T.level_epsilon[sl]) / ARTIS_KB / T_exc);
+          K.C.pops[idx] = v * rho * boltz;
+          return;
+        }
+      }
+    }
     const double W = 1.;
     nn = (ng * W * (double)K.T.level_stat_weight[ul] / (double)K.T.level_stat_weight[ul0] *
           exp(-(K.T.level_epsilon[ul] - K.T.level_epsilon[ul0]) / ARTIS_KB / T_exc));
   }
-  if (nn < ARTIS_MINPOP) nn = hasabund ? ARTIS_MINPOP : 0.;
+  if (nn < minpop) nn = hasabund ? minpop : 0.;
   K.C.pops[idx] = nn;
 }
 
@@ -112,6 +137,12 @@ __global__ void k_bfcells(Ctx K, const int32_t *target_ul, const int32_t *target
     const int e = K.T.ion_element[ui];
     const int i = ui - K.T.elem_uniqueionoffset[e];
     const int l = ul - K.T.ion_uniqueleveloffset[ui];
+    // ratecoeff.cc:1255-1261: the previous timestep's bf-rate estimator when there is one
+    if (bfrate_override(K, mgi, slot)) {
+      K.C.corrphot[(int64_t)k * ntg + slot] = K.C.bfrate_est[(int64_t)mgi * K.T.nbf + K.T.slot_allcont[slot]];
+      return;
+    }
+    if (K.R.no_lut_photoion) return;  // k_corrphot_integral
     const double W = K.C.W[mgi];
     const double T_R = K.C.TR[mgi];
     double gammacorr = W * lut_interp(K, K.T.corrphotoioncoeff, e, i, l, t, T_R);
@@ -119,6 +150,35 @@ __global__ void k_bfcells(Ctx K, const int32_t *target_ul, const int32_t *target
     if (g >= 0) gammacorr *= K.C.corrphotoionrenorm[(int64_t)mgi * K.T.nelements * K.T.maxnions + g];
     K.C.corrphot[(int64_t)k * ntg + slot] = gammacorr;
   }
+}
+
+// nonthermal.cc:1827-1875 per non-empty cell: ion_ntion_energyrate of every (element, lower ion) summed in
+// select_nt_ionization2's order (running sums at the lower ion's unique index, total = get_ntion_energyrate)
+__global__ void k_ntcells(Ctx K) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K.C.n_nonempty) return;
+  const int mgi = K.C.ne_mgi[k];
+  const int ni = K.T.nions_total;
+  double *cum = K.C.nt_cum + (int64_t)k * ni;
+  double ratesum = 0.;
+  for (int e = 0; e < K.T.nelements; e++) {
+    const int nions = K.T.elem_nions[e];
+    for (int lowerion = 0; lowerion < nions; lowerion++) {
+      const int ui = uion(K, e, lowerion);
+      if (lowerion < nions - 1) {
+        const double nnlowerion = K.C.ionpop[(int64_t)k * ni + ui];
+        double enrate = 0.;
+        for (int upperion = lowerion + 1; upperion <= nt_ionisation_maxupperion(K, e, lowerion); upperion++) {
+          const double upperionprobfrac = nt_ionization_upperion_probability(K, mgi, e, lowerion, upperion, false);
+          const double epsilon_trans = epsilon(K, e, upperion, 0) - epsilon(K, e, lowerion, 0);
+          enrate += nnlowerion * upperionprobfrac * epsilon_trans;
+        }
+        ratesum += K.C.nt_Y[(int64_t)mgi * ni + ui] * enrate;
+      }
+      cum[ui] = ratesum;
+    }
+  }
+  K.C.nt_total[k] = ratesum;
 }
 
 // kpkt.cc:167-308 calculate_kpkt_rates_ion, one workitem per (cell, ion), cumulative from oldcoolingsum
@@ -239,6 +299,7 @@ __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict_
         }
         return false;
       });
+  pr[ARTIS_MA_ACTION_INTERNALUPHIGHERNT] = ma_nt_total(K, mgi, ul);
   if (cache) {
     for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) REC(a) = pr[a];
   } else {
@@ -458,6 +519,12 @@ struct Engine {
   int16_t *d_thick = nullptr;
   float *d_abund = nullptr, *d_glp = nullptr, *d_pf = nullptr;
   double *d_totcool = nullptr, *d_ccion = nullptr, *d_renorm = nullptr;
+  // nebular inputs (device copies, npts_model-indexed) and the NO_LUT integration workspace
+  double *d_nltepops = nullptr, *d_ntdep = nullptr, *d_ntY = nullptr;
+  float *d_rfTR = nullptr, *d_rfW = nullptr, *d_bfest = nullptr, *d_ntprob = nullptr, *d_ntionen = nullptr;
+  QagWs qag{};
+  int qag_waves = 0;
+  int64_t nbf_est = 0, nbins_est = 0;  // nebular estimator sections of the block (0 when off)
   int32_t *d_ne_index = nullptr, *d_ne_mgi = nullptr;
   // packets
   uint64_t *d_soa = nullptr, *d_aos = nullptr, *d_snapshot = nullptr;
@@ -1330,11 +1397,48 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     return ARTIS_ERR_BAD_ARGUMENT;
   }
   R.exc_te = rp->excitation_temperature == ARTIS_TEXC_TE;
+  R.minpop = rp->minpop > 0. ? rp->minpop : 1e-30;
+  R.nlte_on = rp->nlte_pops_on;
+  R.multibin = rp->multibin_radfield;
+  R.first_nlte_rf = rp->first_nlte_radfield_timestep;
+  R.detailed_bf = rp->detailed_bf_estimators;
+  R.detailed_bf_usefrom = rp->detailed_bf_usefromtimestep;
+  R.no_lut_photoion = rp->no_lut_photoion;
+  R.no_lut_bfheating = rp->no_lut_bfheating;
+  R.nt_on = rp->nt_on;
+  R.nt_max_auger = rp->nt_max_auger_electrons;
+  R.nts = -1;
+  if ((R.nlte_on && (!a->ion_nlevels_nlte || !a->ion_first_nlte || a->total_nlte_levels < 0)) ||
+      (R.multibin && (a->radfield_nbins <= 0 || !a->radfield_nu_upper)) || R.nt_max_auger < 0) {
+    G.last_error = "nebular run parameters without the atomic tables they need (ion_nlevels_nlte / radfield bins)";
+    return ARTIS_ERR_BAD_ARGUMENT;
+  }
+  T.total_nlte_levels = R.nlte_on ? a->total_nlte_levels : 0;
+  T.rf_nbins = R.multibin ? a->radfield_nbins : 0;
+  T.rf_nu_lower_first = a->radfield_nu_lower_first;
+  if (R.nlte_on) {
+    rc |= dupload(&T.ion_nlevels_nlte, a->ion_nlevels_nlte, ni);
+    rc |= dupload(&T.ion_first_nlte, a->ion_first_nlte, ni);
+  }
+  if (R.multibin) rc |= dupload(&T.rf_nu_upper, a->radfield_nu_upper, a->radfield_nbins);
+  {
+    // get_bfcontindex (radfield.cc:1329-1341): the allcont entry of each photoionisation target slot
+    std::vector<int32_t> sa(ntg + 1, -1);
+    for (int ib = 0; ib < nb; ib++) {
+      const int ul = a->ion_uniqueleveloffset[a->elem_uniqueionoffset[a->allcont_element[ib]] + a->allcont_ion[ib]] +
+                     a->allcont_level[ib];
+      sa[a->level_phixstargets_offset[ul] + a->allcont_phixstargetindex[ib]] = ib;
+    }
+    rc |= dupload(&T.slot_allcont, sa.data(), ntg + 1);
+  }
 
-  // estimators: one double block [J | nuJ | ffheat | colheat | rpkt_emiss | gamma | bfheat | scalars(10)]
+  // estimators: one double block [J | nuJ | ffheat | colheat | rpkt_emiss | gamma | bfheat | scalars(10) |
+  // bfrate_raw | radfield J_raw | nuJ_raw | contribcount] (the nebular sections only when their option is on)
   const int np = g->npts_model;
   const int64_t nion_est = (int64_t)np * ne * a->maxnions;
-  G.n_est_doubles = 5 * (int64_t)np + 2 * nion_est + 10;
+  G.nbf_est = R.detailed_bf ? nb : 0;
+  G.nbins_est = T.rf_nbins;
+  G.n_est_doubles = 5 * (int64_t)np + 2 * nion_est + 10 + (int64_t)np * (G.nbf_est + 3 * G.nbins_est);
   rc |= dalloc(&G.d_estblock, G.n_est_doubles);
   DevEst &E = G.K.E;
   E.J = G.d_estblock;
@@ -1345,6 +1449,10 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   E.gamma = E.rpkt_emiss + np;
   E.bfheat = E.gamma + nion_est;
   E.scalars = E.bfheat + nion_est;
+  E.bfrate = E.scalars + 10;
+  E.rfJ = E.bfrate + (int64_t)np * G.nbf_est;
+  E.rfnuJ = E.rfJ + (int64_t)np * G.nbins_est;
+  E.rfcount = E.rfnuJ + (int64_t)np * G.nbins_est;
   rc |= dalloc(&E.ecounter, nli);
   rc |= dalloc(&E.acounter, nli);
   rc |= dalloc(&E.counters, ARTIS_COUNTER_COUNT + 1);
@@ -1440,7 +1548,41 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   rc |= dalloc(&G.d_totcool, (size_t)np);
   rc |= dalloc(&G.d_ccion, (size_t)np * ni);
   rc |= dalloc(&G.d_renorm, (size_t)np * ne * a->maxnions);
+  if (R.nlte_on) rc |= dalloc(&G.d_nltepops, (size_t)np * std::max(1, T.total_nlte_levels));
+  if (R.multibin) {
+    rc |= dalloc(&G.d_rfTR, (size_t)np * T.rf_nbins);
+    rc |= dalloc(&G.d_rfW, (size_t)np * T.rf_nbins);
+  }
+  if (R.detailed_bf) rc |= dalloc(&G.d_bfest, (size_t)np * std::max(1, nb));
+  if (R.nt_on) {
+    const size_t na = (size_t)R.nt_max_auger + 1;
+    rc |= dalloc(&G.d_ntdep, (size_t)np);
+    rc |= dalloc(&G.d_ntY, (size_t)np * ni);
+    rc |= dalloc(&G.d_ntprob, (size_t)np * ni * na);
+    rc |= dalloc(&G.d_ntionen, (size_t)np * ni * na);
+    rc |= dalloc(&C.nt_cum, (size_t)std::max(1, nne_cells) * ni);
+    rc |= dalloc(&C.nt_total, (size_t)std::max(1, nne_cells));
+  }
+  if (R.no_lut_photoion && nne_cells > 0 && ntg > 0) {
+    // one integration workspace of GSLWSIZE intervals per resident wave of k_corrphot_integral (48 B each)
+    G.qag_waves = (int)std::min<int64_t>((int64_t)nne_cells * ntg, 512);
+    const size_t nw = (size_t)G.qag_waves * QAG_LIMIT;
+    rc |= dalloc(&G.qag.alist, nw);
+    rc |= dalloc(&G.qag.blist, nw);
+    rc |= dalloc(&G.qag.rlist, nw);
+    rc |= dalloc(&G.qag.elist, nw);
+    rc |= dalloc(&G.qag.order, nw);
+    rc |= dalloc(&G.qag.level, nw);
+  }
   if (rc) return ARTIS_ERR_HIP;
+  C.nlte_pops = G.d_nltepops;
+  C.rf_TR = G.d_rfTR;
+  C.rf_W = G.d_rfW;
+  C.bfrate_est = G.d_bfest;
+  C.nt_dep = G.d_ntdep;
+  C.nt_Y = G.d_ntY;
+  C.nt_prob = G.d_ntprob;
+  C.nt_ionen = G.d_ntionen;
   C.Te = G.d_cellf;
   C.TR = G.d_cellf + np;
   C.TJ = G.d_cellf + 2 * np;
@@ -1522,6 +1664,42 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
   HIPCHK(hipMemcpyAsync(G.d_ccion, cs->cooling_contrib_ion, sizeof(double) * np * ni, hipMemcpyHostToDevice, G.stream));
   HIPCHK(hipMemcpyAsync(G.d_renorm, cs->corrphotoionrenorm, sizeof(double) * np * ne * G.maxnions,
                         hipMemcpyHostToDevice, G.stream));
+  {
+    // the nebular inputs (ABI 6) of the options switched on
+    const DevRun &R = G.K.R;
+    const int nb = G.K.T.nbf, nbins = G.K.T.rf_nbins;
+    const size_t na = (size_t)R.nt_max_auger + 1;
+    if ((R.nlte_on && !cs->nlte_pops) || (R.multibin && (!cs->radfield_bin_TR || !cs->radfield_bin_W)) ||
+        (R.detailed_bf && !cs->bfrate_estimator) || (R.nt_on && !cs->nt_ionization_ratecoeff) ||
+        (R.nt_on && R.nt_solve_spencerfano &&
+         (!cs->nt_deposition_rate_density || (R.nt_max_auger > 0 && (!cs->nt_prob_num_auger || !cs->nt_ionenfrac_num_auger))))) {
+      G.last_error = "upload_cellstate: a nebular option is on but its cell-state array is NULL";
+      return ARTIS_ERR_BAD_ARGUMENT;
+    }
+    if (R.nlte_on && G.K.T.total_nlte_levels > 0)
+      HIPCHK(hipMemcpyAsync(G.d_nltepops, cs->nlte_pops, sizeof(double) * np * G.K.T.total_nlte_levels,
+                            hipMemcpyHostToDevice, G.stream));
+    if (R.multibin) {
+      HIPCHK(hipMemcpyAsync(G.d_rfTR, cs->radfield_bin_TR, sizeof(float) * np * nbins, hipMemcpyHostToDevice, G.stream));
+      HIPCHK(hipMemcpyAsync(G.d_rfW, cs->radfield_bin_W, sizeof(float) * np * nbins, hipMemcpyHostToDevice, G.stream));
+    }
+    if (R.detailed_bf && nb > 0)
+      HIPCHK(hipMemcpyAsync(G.d_bfest, cs->bfrate_estimator, sizeof(float) * np * nb, hipMemcpyHostToDevice, G.stream));
+    if (R.nt_on) {
+      HIPCHK(hipMemcpyAsync(G.d_ntY, cs->nt_ionization_ratecoeff, sizeof(double) * np * ni, hipMemcpyHostToDevice,
+                            G.stream));
+      if (cs->nt_deposition_rate_density)
+        HIPCHK(hipMemcpyAsync(G.d_ntdep, cs->nt_deposition_rate_density, sizeof(double) * np, hipMemcpyHostToDevice,
+                              G.stream));
+      if (cs->nt_prob_num_auger && cs->nt_ionenfrac_num_auger) {
+        HIPCHK(hipMemcpyAsync(G.d_ntprob, cs->nt_prob_num_auger, sizeof(float) * np * ni * na, hipMemcpyHostToDevice,
+                              G.stream));
+        HIPCHK(hipMemcpyAsync(G.d_ntionen, cs->nt_ionenfrac_num_auger, sizeof(float) * np * ni * na,
+                              hipMemcpyHostToDevice, G.stream));
+      }
+    }
+  }
+  G.K.R.nts = nts;
   HIPCHK(hipStreamSynchronize(G.stream));
   HIPCHK(hipMemsetAsync(G.K.E.err, 0, 4 * sizeof(int32_t), G.stream));
   const int n_ne = G.K.C.n_nonempty;
@@ -1534,6 +1712,9 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
     k_levelpops<<<(unsigned)((nlv + B - 1) / B), B, 0, G.stream>>>(G.K);
     const int64_t nbt = (int64_t)n_ne * (G.K.T.nbf + G.K.T.ntargets_total);
     k_bfcells<<<(unsigned)((nbt + B - 1) / B), B, 0, G.stream>>>(G.K, G.d_target_ul, G.d_target_t);
+    if (G.K.R.no_lut_photoion && G.qag_waves > 0)
+      k_corrphot_integral<<<(unsigned)G.qag_waves, 64, 0, G.stream>>>(G.K, G.d_target_ul, G.d_target_t, G.qag);
+    if (G.K.R.nt_on) k_ntcells<<<(n_ne + B - 1) / B, B, 0, G.stream>>>(G.K);
     const int64_t nci = (int64_t)n_ne * ni;
     k_cooling<<<(unsigned)((nci + 63) / 64), 64, 0, G.stream>>>(G.K);
     const int64_t ntg = G.K.T.ntargets_total;
@@ -1693,6 +1874,15 @@ int artis_gpu_estimators_download(artis_estimators *est) {
   est->gamma_emission += sc[7];
   est->nt_energy_deposited += sc[8];
   est->pellet_decays += (int64_t)llrint(sc[9]);
+  const int64_t off_bf = 5 * (int64_t)np + 2 * nion_est + 10;
+  if (G.nbf_est) add(est->bfrate_raw, off_bf, (int64_t)np * G.nbf_est);
+  if (G.nbins_est) {
+    const int64_t nbn = (int64_t)np * G.nbins_est, off_rf = off_bf + (int64_t)np * G.nbf_est;
+    add(est->radfield_J_raw, off_rf, nbn);
+    add(est->radfield_nuJ_raw, off_rf + nbn, nbn);
+    if (est->radfield_contribcount)
+      for (int64_t j = 0; j < nbn; j++) est->radfield_contribcount[j] += (int64_t)llrint(blk[off_rf + 2 * nbn + j]);
+  }
   std::vector<int32_t> lc(G.nlines);
   if (est->ecounter) {
     HIPCHK(hipMemcpy(lc.data(), G.K.E.ecounter, lc.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
@@ -1740,13 +1930,15 @@ int artis_gpu_estimator_block_from_device(const void *src) {
 }
 
 // host mirror of the device block (artis_gpu_estimator_block_to_device / estimators_download)
-size_t artis_estimator_block_len(int np, int ne, int mi, int nl) {
-  if (np < 0 || ne < 0 || mi < 0 || nl < 0) return 0;
-  return 5 * (size_t)np + 2 * (size_t)np * ne * mi + 10 + 2 * (size_t)nl + ARTIS_COUNTER_COUNT + 1;
+size_t artis_estimator_block_len(int np, int ne, int mi, int nl, int nbf, int nbins) {
+  if (np < 0 || ne < 0 || mi < 0 || nl < 0 || nbf < 0 || nbins < 0) return 0;
+  return 5 * (size_t)np + 2 * (size_t)np * ne * mi + 10 + (size_t)np * (nbf + 3 * (size_t)nbins) + 2 * (size_t)nl +
+         ARTIS_COUNTER_COUNT + 1;
 }
 
-int artis_estimator_block_pack(const artis_estimators *est, int np, int ne, int mi, int nl, double *b) {
-  if (!est || !b || np < 0 || ne < 0 || mi < 0 || nl < 0) return ARTIS_ERR_BAD_ARGUMENT;
+int artis_estimator_block_pack(const artis_estimators *est, int np, int ne, int mi, int nl, int nbf, int nbins,
+                               double *b) {
+  if (!est || !b || np < 0 || ne < 0 || mi < 0 || nl < 0 || nbf < 0 || nbins < 0) return ARTIS_ERR_BAD_ARGUMENT;
   const size_t ni = (size_t)np * ne * mi;
   auto put = [&](const double *src, size_t n) {
     for (size_t j = 0; j < n; j++) *b++ = src ? src[j] : 0.;
@@ -1762,6 +1954,11 @@ int artis_estimator_block_pack(const artis_estimators *est, int np, int ne, int 
                          est->electron_emission, est->alpha_dep, est->alpha_emission,     est->gamma_emission,
                          est->nt_energy_deposited, (double)est->pellet_decays};
   put(sc, 10);
+  put(est->bfrate_raw, (size_t)np * nbf);
+  put(est->radfield_J_raw, (size_t)np * nbins);
+  put(est->radfield_nuJ_raw, (size_t)np * nbins);
+  for (size_t j = 0; j < (size_t)np * nbins; j++)
+    *b++ = est->radfield_contribcount ? (double)est->radfield_contribcount[j] : 0.;
   for (int j = 0; j < nl; j++) *b++ = est->ecounter ? est->ecounter[j] : 0.;
   for (int j = 0; j < nl; j++) *b++ = est->acounter ? est->acounter[j] : 0.;
   for (int j = 0; j < ARTIS_COUNTER_COUNT; j++) *b++ = (double)est->counters[j];
@@ -1769,8 +1966,9 @@ int artis_estimator_block_pack(const artis_estimators *est, int np, int ne, int 
   return 0;
 }
 
-int artis_estimator_block_unpack(const double *b, int np, int ne, int mi, int nl, artis_estimators *est) {
-  if (!est || !b || np < 0 || ne < 0 || mi < 0 || nl < 0) return ARTIS_ERR_BAD_ARGUMENT;
+int artis_estimator_block_unpack(const double *b, int np, int ne, int mi, int nl, int nbf, int nbins,
+                                 artis_estimators *est) {
+  if (!est || !b || np < 0 || ne < 0 || mi < 0 || nl < 0 || nbf < 0 || nbins < 0) return ARTIS_ERR_BAD_ARGUMENT;
   const size_t ni = (size_t)np * ne * mi;
   auto get = [&](double *dst, size_t n) {
     if (dst)
@@ -1795,6 +1993,12 @@ int artis_estimator_block_unpack(const double *b, int np, int ne, int mi, int nl
   est->nt_energy_deposited = b[8];
   est->pellet_decays = (int64_t)llrint(b[9]);
   b += 10;
+  get(est->bfrate_raw, (size_t)np * nbf);
+  get(est->radfield_J_raw, (size_t)np * nbins);
+  get(est->radfield_nuJ_raw, (size_t)np * nbins);
+  for (size_t j = 0; j < (size_t)np * nbins; j++)
+    if (est->radfield_contribcount) est->radfield_contribcount[j] = (int64_t)llrint(b[j]);
+  b += (size_t)np * nbins;
   for (int j = 0; j < nl; j++)
     if (est->ecounter) est->ecounter[j] = (int32_t)llrint(b[j]);
   b += nl;

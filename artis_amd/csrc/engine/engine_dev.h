@@ -80,6 +80,13 @@ struct DevTab {
   const int32_t *groundcont_element, *groundcont_ion;
   const double *spontrecombcoeff, *corrphotoioncoeff, *bfcooling_coeff;
   const int32_t *cool_type, *cool_element, *cool_ion, *cool_level, *cool_upper;
+  // nebular options (ABI 6): NLTE level bookkeeping (input.cc:1711-1746), radiation-field bin edges
+  // (radfield.cc:131-188), the allcont index of each photoionisation target slot (get_bfcontindex)
+  const int32_t *ion_nlevels_nlte, *ion_first_nlte;
+  int32_t total_nlte_levels, rf_nbins;
+  const double *rf_nu_upper;
+  double rf_nu_lower_first;
+  const int32_t *slot_allcont;
   // gamma-ray line spectra per nuclide (gammapkt.cc:27-33), uploaded by artis_gpu_init_gamma
   int32_t g_nnuc;
   const int32_t *g_nlines, *g_off;
@@ -133,10 +140,23 @@ struct DevCells {
   int64_t ma_key_stride;
   int32_t have_macache;
   double *marates;     // without the cache: [n_nonempty * nlevels_total * 9] totals only
+  // nebular inputs (ABI 6; nullptr when the option is off), model-cell indexed like the arrays above
+  const double *nlte_pops;    // [npts_model * total_nlte_levels]
+  const float *rf_TR, *rf_W;  // [npts_model * rf_nbins]
+  const float *bfrate_est;    // [npts_model * nbf]
+  const double *nt_dep;       // [npts_model]
+  const double *nt_Y;         // [npts_model * nions_total]
+  const float *nt_prob, *nt_ionen;  // [npts_model * nions_total * (nt_max_auger + 1)]
+  // derived per non-empty cell (k_ntcells): running sums of ion_ntion_energyrate over (element, lower ion) in
+  // select_nt_ionization2 order, at the unique index of the lower ion (nonthermal.cc:1827-1875), and their total
+  double *nt_cum;             // [n_nonempty * nions_total]
+  double *nt_total;           // [n_nonempty]
 };
 
 struct DevEst {
   double *J, *nuJ, *ffheat, *colheat, *rpkt_emiss, *gamma, *bfheat;  // contiguous block, see engine.hip
+  double *bfrate;                  // [npts_model * nbf] bfrate_raw (DETAILED_BF_ESTIMATORS_ON), in the block
+  double *rfJ, *rfnuJ, *rfcount;   // [npts_model * rf_nbins] radfield bin estimators (contribcount as double)
   int32_t *ecounter, *acounter;
   double *scalars;                 // [10] cmf_lum, gamma_dep, ... (artis_estimators order), nt_energy_deposited,
                                    // pellet_decays
@@ -185,6 +205,10 @@ struct DevRun {
   double gamma_grey;
   int32_t instant_particle_deposition, nt_solve_spencerfano;
   int32_t exc_te;  // 1: level populations at T_e (LTEPOP_EXCITATIONTEMPERATURE), 0: at T_J
+  double minpop;   // MINPOP
+  int32_t nts;     // timestep of the uploaded cell state (globals::nts_global for radfield / get_corrphotoioncoeff)
+  int32_t nlte_on, multibin, first_nlte_rf, detailed_bf, detailed_bf_usefrom, no_lut_photoion, no_lut_bfheating;
+  int32_t nt_on, nt_max_auger;
 };
 
 #endif

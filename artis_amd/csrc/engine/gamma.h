@@ -487,9 +487,49 @@ DEVFN void update_pellet(Tx &x, Pkt &p, const PelletInfo &pi, double t2) {
   }
 }
 
-// nonthermal.cc:1877-1977 with NT_SOLVE_SPENCERFANO off: the lepton's energy goes straight to a k-packet
+// nonthermal.cc:1877-1977 (NT_EXCITATION_ON false): with NT_ON && NT_SOLVE_SPENCERFANO outside thick cells the
+// fraction frac_ionization = get_ntion_energyrate / deposition_rate_density activates a macro-atom by non-thermal
+// ionisation (select_nt_ionization2 over the per-cell running sums of k_ntcells, then the Auger upper ion); the
+// rest, and every deposition without the Spencer-Fano solution, becomes a k-packet
 DEVFN void do_ntlepton(Tx &x, Pkt &p) {
-  safeadd(&x.K.E.scalars[8], p.e_cmf);  // nt_energy_deposited
+  const Ctx &K = x.K;
+  safeadd(&K.E.scalars[8], p.e_cmf);  // nt_energy_deposited
+  const int mgi = cell_mgi(K, p.where);
+  if (K.R.nt_on && K.R.nt_solve_spencerfano && K.C.thick[mgi] != 1) {
+    const int k = K.C.ne_index[mgi];
+    const double zrand = artis_rng_uniform(&x.rng);
+    const double ratetotal = K.C.nt_total[k];
+    const double frac_ionization = ratetotal / K.C.nt_dep[mgi];
+    if (zrand < frac_ionization) {
+      const double z2 = artis_rng_uniform(&x.rng);
+      const double *cum = K.C.nt_cum + (int64_t)k * K.T.nions_total;
+      int element = -1, lowerion = -1;
+      for (int e = 0; e < K.T.nelements && element < 0; e++)
+        for (int li = 0; li < K.T.elem_nions[e] - 1; li++)
+          if (cum[uion(K, e, li)] >= z2 * ratetotal) {
+            element = e;
+            lowerion = li;
+            break;
+          }
+      const int upperion = element < 0 ? -1 : nt_random_upperion(K, x.rng, mgi, element, lowerion, true);
+      if (upperion < 0) {
+        x.err(ERR_MA_SELECT, p.number, 20);
+        return;
+      }
+      p.ma_element = element;
+      p.ma_ion = upperion;
+      p.ma_level = 0;
+      p.ma_activatingline = -99;
+      p.type = ARTIS_TYPE_MA;
+      lctr(x.L, CTR_MA_STAT_ACTIVATION_NTCOLLION);
+      p.interactions += 1;
+      p.last_event = 20;
+      p.trueemissiontype = -1;
+      p.trueemissionvelocity = -1;
+      lctr(x.L, CTR_NT_STAT_TO_IONIZATION);
+      return;
+    }
+  }
   p.last_event = 22;
   p.type = ARTIS_TYPE_KPKT;
   lctr(x.L, CTR_NT_STAT_TO_KPKT);
@@ -514,10 +554,6 @@ DEVFN void do_gamma_family_step(Tx &x, Pkt &p, const PelletInfo &pi, double t2) 
       do_nonthermal_predeposit(x, p, pi, t2);
       break;
     case ARTIS_TYPE_NTLEPTON:
-      if (K.R.nt_solve_spencerfano) {
-        x.err(ERR_UNSUPPORTED_TYPE, p.number, p.type);
-        return;
-      }
       do_ntlepton(x, p);
       break;
     default:

@@ -274,9 +274,46 @@ DEVFN double rad_deexcitation_ratecoeff(const Ctx &K, const double *pops, int e,
                                         double epsilon_trans, int li, double t_current) {
   return rad_deexcitation_ratecoeff_n(K, pops[ulev(K, e, i, upper)], pops[ulev(K, e, i, lower)], li, t_current);
 }
-// macroatom.cc:550-643 (radfield.cc:898-943: dilute blackbody, radfield.h:44-48)
-DEVFN double rad_excitation_ratecoeff_n(const Ctx &K, double n_u, double n_l, double T_R, double W,
-                                        double epsilon_trans, int li, double t_current) {
+// radfield.cc:575-600 select_bin: the lowest bin whose upper edge exceeds nu; -2 below the first bin, -1 above
+// the last
+DEVFN int rf_select_bin(const Ctx &K, double nu) {
+  if (nu < K.T.rf_nu_lower_first) return -2;
+  int lo = 0, hi = K.T.rf_nbins;  // upper_bound
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (K.T.rf_nu_upper[mid] > nu)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  return lo >= K.T.rf_nbins ? -1 : lo;
+}
+// radfield.cc:898-943 radfield(nu, mgi) as the dilute blackbody (T_R, W) it evaluates (radfield.h:44-48): the
+// fitted bin's from FIRST_NLTE_RADFIELD_TIMESTEP on under MULTIBIN_RADFIELD_MODEL_ON (false: J_nu = 0, no bin
+// or no fit), the cell's full-spectrum one otherwise
+DEVFN bool radfield_TW(const Ctx &K, int mgi, double nu, float &T_R, float &W) {
+  if (K.R.multibin && K.R.nts >= K.R.first_nlte_rf) {
+    const int b = rf_select_bin(K, nu);
+    if (b < 0) return false;
+    const int64_t mb = (int64_t)mgi * K.T.rf_nbins + b;
+    W = K.C.rf_W[mb];
+    if (!(W >= 0.f)) return false;
+    T_R = K.C.rf_TR[mb];
+    return true;
+  }
+  T_R = K.C.TR[mgi];
+  W = K.C.W[mgi];
+  return true;
+}
+DEVFN double radfield_J(const Ctx &K, int mgi, double nu) {
+  float T_R, W;
+  if (!radfield_TW(K, mgi, nu, T_R, W)) return 0.;
+  return dbb(nu, T_R, W);
+}
+// macroatom.cc:550-643 (J_nu = radfield(nu_trans), radfield.cc:898-943 / radfield.h:44-48, with pow(nu, 3)
+// precomputed per line)
+DEVFN double rad_excitation_ratecoeff_n(const Ctx &K, int mgi, double n_u, double n_l, double epsilon_trans, int li,
+                                        double t_current) {
   double R = 0.0;
   const LineMA lm = K.T.line_ma[li];
   const double tau_sobolev = (lm.B_lu * n_l - lm.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_current;
@@ -284,14 +321,18 @@ DEVFN double rad_excitation_ratecoeff_n(const Ctx &K, double n_u, double n_l, do
     const double beta = 1.0 / tau_sobolev * (-expm1(-tau_sobolev));
     const double R_over_J_nu = n_l > 0. ? (lm.B_lu - lm.B_ul * n_u / n_l) * beta : lm.B_lu * beta;
     const double nu_trans = epsilon_trans / ARTIS_H;
-    R = R_over_J_nu * (W * ARTIS_TWOHOVERCLIGHTSQUARED * lm.nu3 / expm1(ARTIS_HOVERKB * nu_trans / T_R));
+    float T_R, W;
+    if (radfield_TW(K, mgi, nu_trans, T_R, W))
+      R = R_over_J_nu * (W * ARTIS_TWOHOVERCLIGHTSQUARED * lm.nu3 / expm1(ARTIS_HOVERKB * nu_trans / T_R));
+    else
+      R = R_over_J_nu * 0.;
   }
   return R;
 }
 DEVFN double rad_excitation_ratecoeff(const Ctx &K, const double *pops, int mgi, int e, int i, int lower, int upper,
                                       double epsilon_trans, int li, double t_current) {
-  return rad_excitation_ratecoeff_n(K, pops[ulev(K, e, i, upper)], pops[ulev(K, e, i, lower)], K.C.TR[mgi],
-                                    K.C.W[mgi], epsilon_trans, li, t_current);
+  return rad_excitation_ratecoeff_n(K, mgi, pops[ulev(K, e, i, upper)], pops[ulev(K, e, i, lower)], epsilon_trans, li,
+                                    t_current);
 }
 // macroatom.cc:645-678
 DEVFN double rad_recombination_ratecoeff(const Ctx &K, float T_e, float nne, int e, int upperion, int upper, int lower) {
@@ -388,13 +429,12 @@ DEVFN void ma_foreach_rate(const Ctx &K, int mgi, int ul, double t_mid, Pop pop,
   }
   const int nuptrans = K.T.level_nuptrans[ul];
   const int uoff = K.T.level_uptrans_offset[ul];
-  const double T_R = K.C.TR[mgi], W = K.C.W[mgi];
   for (int j = 0; j < nuptrans; j++) {
     const int li = K.T.uptrans_lineindex[uoff + j];
     const int upper = K.T.line_upper[li];
     const double epsilon_trans = epsilon(K, e, i, upper) - epsilon_current;
     const double n_u = pop(ul - l + upper);
-    const double R = rad_excitation_ratecoeff_n(K, n_u, n_self, T_R, W, epsilon_trans, li, t_mid);
+    const double R = rad_excitation_ratecoeff_n(K, mgi, n_u, n_self, epsilon_trans, li, t_mid);
     const double C = col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, e, i, upper));
     if (f(MA_KIND_UP, j, R, C, epsilon_trans, 0., epsilon_current)) return;
   }
@@ -408,6 +448,60 @@ DEVFN void ma_foreach_rate(const Ctx &K, int mgi, int ul, double t_mid, Pop pop,
       if (f(MA_KIND_UPHIGHER, t, R, C, epsilon_trans, 0., epsilon_current)) return;
     }
   }
+}
+
+// macroatom.cc:139-146: the INTERNALUPHIGHERNT total of unique level ul (NT_ON; the host's
+// nt_ionization_ratecoeff, nonthermal.cc:1684-1712, times epsilon_current)
+DEVFN double ma_nt_total(const Ctx &K, int mgi, int ul) {
+  if (!K.R.nt_on) return 0.;
+  const int ui = K.T.level_ui[ul];
+  const int e = K.T.ion_element[ui];
+  const int i = ui - K.T.elem_uniqueionoffset[e];
+  const int l = ul - K.T.ion_uniqueleveloffset[ui];
+  if (!(i < K.T.elem_nions[e] - 1 && l < K.T.ion_ionisinglevels[ui])) return 0.;
+  return K.C.nt_Y[(int64_t)mgi * K.T.nions_total + ui] * K.T.level_epsilon[ul];
+}
+// nonthermal.cc:1640-1655
+DEVFN int nt_ionisation_maxupperion(const Ctx &K, int e, int lowerion) {
+  const int nions = K.T.elem_nions[e];
+  int maxupper = lowerion + 1;
+  if (K.R.nt_solve_spencerfano) maxupper = lowerion + 1 + K.R.nt_max_auger;
+  if (maxupper > nions - 1) maxupper = nions - 1;
+  return maxupper;
+}
+// nonthermal.cc:1584-1635
+DEVFN double nt_ionization_upperion_probability(const Ctx &K, int mgi, int e, int lowerion, int upperion,
+                                                bool energyweighted) {
+  const int A = K.R.nt_max_auger;
+  if (K.R.nt_solve_spencerfano && A > 0) {
+    const int numaugerelec = upperion - lowerion - 1;
+    const int64_t base = ((int64_t)mgi * K.T.nions_total + uion(K, e, lowerion)) * (A + 1);
+    const float *tab = energyweighted ? K.C.nt_ionen : K.C.nt_prob;
+    if (numaugerelec < A) return tab[base + numaugerelec];
+    if (numaugerelec == A) {
+      double prob_remaining = 1.;
+      for (int a = 0; a < A; a++) prob_remaining -= tab[base + a];
+      return prob_remaining;
+    }
+    return 0.;
+  }
+  return (upperion == lowerion + 1) ? 1.0 : 0.;
+}
+// nonthermal.cc:1657-1682 (a draw that the probabilities do not reach is repeated); -1 if none succeeds
+DEVFN int nt_random_upperion(const Ctx &K, artis_rng &rng, int mgi, int e, int lowerion, bool energyweighted) {
+  if (K.R.nt_solve_spencerfano && K.R.nt_max_auger > 0) {
+    const int maxupper = nt_ionisation_maxupperion(K, e, lowerion);
+    for (int attempt = 0; attempt < 1000; attempt++) {
+      const double zrand = artis_rng_uniform(&rng);
+      double prob_sum = 0.;
+      for (int upperion = lowerion + 1; upperion <= maxupper; upperion++) {
+        prob_sum += nt_ionization_upperion_probability(K, mgi, e, lowerion, upperion, energyweighted);
+        if (zrand <= prob_sum) return upperion;
+      }
+    }
+    return -1;
+  }
+  return lowerion + 1;
 }
 
 // 32-bit key of a running sum v of an action whose total is norm (DevCells::ma_key): round(v / norm * (2^32 - 1)),

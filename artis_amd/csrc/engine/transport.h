@@ -386,7 +386,12 @@ DEVFN bool bf_contribution(const Ctx &K, int k, int mgi, int i, double nu, doubl
   const int ion = K.T.allcont_ion[i];
   const int level = K.T.allcont_level[i];
   const int ui = uion(K, element, ion);
-  if (!((K.C.ionpop[(int64_t)k * K.T.nions_total + ui] / (double)K.C.nnetot[mgi] > 1.e-6) || (level == 0))) return false;
+  // rpkt.cc:1116-1118: DETAILED_BF_ESTIMATORS_ON includes every continuum of an element present in the cell
+  if (K.R.detailed_bf) {
+    if (!(K.C.elem_abundance[(int64_t)mgi * K.T.nelements + element] > 0)) return false;
+  } else if (!((K.C.ionpop[(int64_t)k * K.T.nions_total + ui] / (double)K.C.nnetot[mgi] > 1.e-6) || (level == 0))) {
+    return false;
+  }
   const double nu_edge = K.T.allcont_nu_edge[i];
   const double nnlevel = K.C.pops[(int64_t)k * K.T.nlevels_total + K.T.ion_uniqueleveloffset[ui] + level];
   const double nu_max_phixs = nu_edge * K.T.last_phixs_nuovernuedge;
@@ -664,6 +669,35 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
   safeadd(&K.E.J[mgi], distance_e_cmf);
   safeadd(&K.E.nuJ[mgi], distance_e_cmf * nu);
   safeadd(&K.E.ffheat[mgi], distance_e_cmf * kap.ffheating);
+  if (K.R.detailed_bf && distance_e_cmf != 0) {
+    // radfield.cc:764-829 update_bfestimators: gamma_contr[i] at the frequency the opacity was computed at
+    // (rpkt.cc:1166-1171; zero for continua above kap.nu or not included), the window test at the current nu
+    const double dopplerfactor = doppler_packet(K, p);
+    const double d_over_nu = distance_e_cmf / nu * dopplerfactor;
+    const int64_t row = (int64_t)mgi * K.T.nbf;
+    for (int i = 0; i < K.T.nbf; i++) {
+      const double nu_edge = K.T.allcont_nu_edge[i];
+      const double nu_max_phixs = nu_edge * K.T.last_phixs_nuovernuedge;
+      if (nu >= nu_edge && nu <= nu_max_phixs) {
+        double gc = 0., nnlevel;
+        if (!(kap.nu < nu_edge) && !bf_contribution(K, k, mgi, i, kap.nu, &nnlevel, &gc)) gc = 0.;
+        safeadd(&K.E.bfrate[row + i], gc * d_over_nu);
+      } else if (nu < nu_edge) {
+        break;
+      }
+    }
+  }
+  if (K.R.multibin) {  // radfield.cc:845-866
+    const int b = rf_select_bin(K, nu);
+    if (b >= 0) {
+      const int64_t mb = (int64_t)mgi * K.T.rf_nbins + b;
+      safeadd(&K.E.rfJ[mb], distance_e_cmf);
+      safeadd(&K.E.rfnuJ[mb], distance_e_cmf * nu);
+      safeadd(&K.E.rfcount[mb], 1.);
+    }
+  }
+  // the ground-continuum estimators exist unless both NO_LUT_PHOTOION and NO_LUT_BFHEATING (rpkt.cc:573-614)
+  if (K.R.no_lut_photoion && K.R.no_lut_bfheating) return;
   const double distance_e_cmf_over_nu = distance_e_cmf / nu;
   for (int g = 0; g < K.T.nbfg; g++) {
     const double nu_edge = K.T.groundcont_nu_edge[g];
@@ -680,8 +714,8 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
         }
         const int ion = K.T.groundcont_ion[g];
         const int64_t idx = (int64_t)mgi * K.T.nelements * K.T.maxnions + element * K.T.maxnions + ion;
-        safeadd(&K.E.gamma[idx], gcontr * distance_e_cmf_over_nu);
-        safeadd(&K.E.bfheat[idx], gcontr * distance_e_cmf * (1. - nu_edge / nu));
+        if (!K.R.no_lut_photoion) safeadd(&K.E.gamma[idx], gcontr * distance_e_cmf_over_nu);
+        if (!K.R.no_lut_bfheating) safeadd(&K.E.bfheat[idx], gcontr * distance_e_cmf * (1. - nu_edge / nu));
         lwork(x.L, WK_GC_UPDATES, 1);
       }
     } else {
@@ -1229,6 +1263,18 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
     m.level = upper;
     return MA_CONTINUE;
   }
+  if (selected_action == ARTIS_MA_ACTION_INTERNALUPHIGHERNT) {
+    // macroatom.cc:866-884
+    lctr(L, CTR_MA_STAT_INTERNALUPHIGHERNT);
+    const int upperion = nt_random_upperion(K, rng, m.mgi, element, ion, false);
+    if (upperion < 0) {
+      fail(K, ERR_MA_SELECT, number, 9);
+      return MA_FAILED;
+    }
+    m.ion = upperion;
+    m.level = 0;
+    return MA_CONTINUE;
+  }
   fail(K, ERR_MA_SELECT, number, 100 + selected_action);
   return MA_FAILED;
 }
@@ -1301,6 +1347,22 @@ DEVFN int ma_apply_selection(const Ctx &K, const LocalCounters &L, MaLaneC &m, M
   }
 }
 
+// macroatom.cc:866-884 for the cached walk: the upper ion from the Auger-electron probabilities, its ground level
+DEVFN int ma_apply_nt(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneC &m, int number) {
+  lctr(L, CTR_MA_STAT_INTERNALUPHIGHERNT);
+  const int ui = K.T.level_ui[m.ul];
+  const int e = K.T.ion_element[ui];
+  const int ion = ui - K.T.elem_uniqueionoffset[e];
+  const int upperion = nt_random_upperion(K, rng, K.C.ne_mgi[m.k], e, ion, false);
+  if (upperion < 0) {
+    fail(K, ERR_MA_SELECT, number, 9);
+    return MA_FAILED;
+  }
+  m.ul = K.T.ion_uniqueleveloffset[ui + upperion - ion];
+  m.rec_off = K.T.ma_meta[m.ul].rec_off;
+  return MA_CONTINUE;
+}
+
 // One jump of the cached walk with the reference's exact double sums, recomputed from the cell tables through
 // ma_foreach_rate (the very sums k_marates condensed into keys): macroatom.cc:502-525 and the transition search of
 // the selected action.  Draws zrand (and zr) itself; runs where a key comparison was undecided (k_ma_exact,
@@ -1321,6 +1383,7 @@ DEVNI int ma_jump_exact(const Ctx &K, const LocalCounters &L, artis_rng &rng, Ma
     ma_accumulate(pr, kind, R, C, et, eg, ec);
     return false;
   });
+  pr[ARTIS_MA_ACTION_INTERNALUPHIGHERNT] = ma_nt_total(K, mgi, ul);
   double total_transitions = 0.;
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) total_transitions += pr[a];
   const double zrand = artis_rng_uniform(&rng);
@@ -1343,10 +1406,7 @@ DEVNI int ma_jump_exact(const Ctx &K, const LocalCounters &L, artis_rng &rng, Ma
     end.ion = end.a = end.b = 0;
     return end.code;
   }
-  if (sel == ARTIS_MA_ACTION_INTERNALUPHIGHERNT) {
-    fail(K, ERR_MA_SELECT, number, 100 + sel);
-    return MA_FAILED;
-  }
+  if (sel == ARTIS_MA_ACTION_INTERNALUPHIGHERNT) return ma_apply_nt(K, L, rng, m, number);
   // the transition: first running sum of action sel above zr * total, in the reference's list order
   const double zr = artis_rng_uniform(&rng);
   const double x = zr * pr[sel];
@@ -1439,10 +1499,7 @@ DEVFN int ma_jump_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
     end.ion = end.a = end.b = 0;
     return end.code;
   }
-  if (sel == ARTIS_MA_ACTION_INTERNALUPHIGHERNT) {
-    fail(K, ERR_MA_SELECT, number, 100 + sel);
-    return MA_FAILED;
-  }
+  if (sel == ARTIS_MA_ACTION_INTERNALUPHIGHERNT) return ma_apply_nt(K, L, rng, m, number);
   const double zr = artis_rng_uniform(&rng);
   const double q2 = zr * MA_KEY_SCALE;
   auto cmp2 = [&](int p) {

@@ -88,6 +88,12 @@ struct Model {
   std::vector<double> totalcooling, cooling_contrib_ion, corrphotoionrenorm;
   std::vector<float> ffegrp;
   artis_cell_state cs{};
+  // ---- nebular options (cfg.nebular)
+  std::vector<int32_t> ion_nlevels_nlte, ion_first_nlte;
+  int total_nlte_levels = 0;
+  std::vector<double> rf_nu_upper;
+  std::vector<double> nlte_pops, nt_dep, nt_Y;
+  std::vector<float> rf_TR, rf_W, bfrate_est, nt_prob, nt_ionen;
 
   // ---- decay stand-in (decay.cc nuclides + gammapkt.cc gamma_spectra)
   static constexpr int NNUC = 5;
@@ -148,6 +154,52 @@ double calculate_sahafact(const Model &m, int element, int ion, int level, int u
   const double g_lower = m.level_stat_weight[uniquelevel(m, element, ion, level)];
   const double g_upper = m.level_stat_weight[uniquelevel(m, element, ion + 1, upperionlevel)];
   return ARTIS_SAHACONST * g_lower / g_upper * pow(T, -1.5) * exp(E_threshold / ARTIS_KB / T);
+}
+
+double minpop_of(const Model &m) { return m.cfg.minpop > 0. ? m.cfg.minpop : (m.cfg.nebular ? 1e-40 : ARTIS_MINPOP); }
+
+// deterministic uniform in [0, 1) from (a, b, salt) (splitmix64): the nebular stand-ins do not depend on the
+// order cells are visited in
+double hash_u01(uint64_t a, uint64_t b, uint64_t salt) {
+  uint64_t z = a * 0x9E3779B97F4A7C15ull ^ (b + 0x632BE59BD9B4E019ull) * 0xBF58476D1CE4E5B9ull ^ salt * 0x94D049BB133111EBull;
+  z ^= z >> 30;
+  z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 27;
+  z *= 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (double)(z >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// input.cc:1711-1746 (NLTE level bookkeeping, LEVEL_IS_NLTE contiguous from the ground state) and
+// radfield.cc:131-188 setup_bin_boundaries (equal frequency bins + the top super bin)
+void setup_nebular_atomic(Model &m) {
+  artis_atomic_tables &a = m.at;
+  if (!m.cfg.nebular) return;
+  const int ni = m.nions_total;
+  m.ion_nlevels_nlte.assign(ni, 0);
+  m.ion_first_nlte.assign(ni, 0);
+  m.total_nlte_levels = 0;
+  for (int ui = 0; ui < ni; ui++) {
+    m.ion_first_nlte[ui] = m.total_nlte_levels;
+    const int nlevels = m.ion_nlevels[ui];
+    const int n = std::max(0, std::min(nlevels - 1, m.cfg.nlte_level_max));
+    m.ion_nlevels_nlte[ui] = n;
+    m.total_nlte_levels += n + ((nlevels > n + 1) ? 1 : 0);
+  }
+  a.ion_nlevels_nlte = m.ion_nlevels_nlte.data();
+  a.ion_first_nlte = m.ion_first_nlte.data();
+  a.total_nlte_levels = m.total_nlte_levels;
+  const int nb = m.cfg.radfield_nbins > 1 ? m.cfg.radfield_nbins : 256;
+  const double nu_lower_first_initial = ARTIS_CLIGHT / (40000e-8);
+  const double nu_upper_last_initial = ARTIS_CLIGHT / (1085e-8);
+  const double nu_upper_superbin = ARTIS_CLIGHT / (10e-8);
+  const double delta_nu = (nu_upper_last_initial - nu_lower_first_initial) / (nb - 1);
+  m.rf_nu_upper.assign(nb, 0.);
+  for (int b = 0; b < nb - 1; b++) m.rf_nu_upper[b] = nu_lower_first_initial + (b + 1) * delta_nu;
+  m.rf_nu_upper[nb - 1] = nu_upper_superbin;
+  a.radfield_nbins = nb;
+  a.radfield_nu_upper = m.rf_nu_upper.data();
+  a.radfield_nu_lower_first = nu_lower_first_initial;
 }
 
 int get_nphixstargets(const Model &m, int element, int ion, int level) {
@@ -788,8 +840,8 @@ void finish_geometry(Model &m) {
   g.ts_start = m.ts_start.data();
   g.ts_width = m.ts_width.data();
   g.ts_mid = m.ts_mid.data();
-  g.nu_min_r = ARTIS_NU_MIN_R;
-  g.nu_max_r = ARTIS_NU_MAX_R;
+  g.nu_min_r = c.nu_min_r > 0. ? c.nu_min_r : (c.nebular ? 1e13 : ARTIS_NU_MIN_R);
+  g.nu_max_r = c.nu_max_r > 0. ? c.nu_max_r : ARTIS_NU_MAX_R;
 }
 
 // ---- LTE cell state (update_grid stand-in) --------------------------------------------------------------
@@ -836,6 +888,16 @@ void compute_cellstate(Model &m, int nts) {
   m.totalcooling.assign(np, 0.);
   m.cooling_contrib_ion.assign((size_t)np * ni, 0.);
   m.corrphotoionrenorm.assign((size_t)np * ne * m.maxnions, 1.);
+  if (m.cfg.nebular) {
+    m.nlte_pops.assign((size_t)np * std::max(m.total_nlte_levels, 1), -1.);
+    m.rf_TR.assign((size_t)np * m.at.radfield_nbins, 0.f);
+    m.rf_W.assign((size_t)np * m.at.radfield_nbins, -1.f);
+    m.bfrate_est.assign((size_t)np * std::max(m.nbfcontinua, 1), 0.f);
+    m.nt_dep.assign(np, 0.);
+    m.nt_Y.assign((size_t)np * ni, 0.);
+    m.nt_prob.assign((size_t)np * ni * 3, 0.f);
+    m.nt_ionen.assign((size_t)np * ni * 3, 0.f);
+  }
 
   // per temperature class: partition functions, and per-level collisional-excitation cooling / nne
   const int ntc = (int)m.tclass_T.size();
@@ -957,22 +1019,59 @@ void compute_cellstate(Model &m, int nts) {
             (float)(nion * m.level_stat_weight[m.ion_uniqueleveloffset[ui]] / Uion);
       }
     }
-    // cooling totals (kpkt.cc:84-165) with LTE level populations (ltepop.cc:307-430, MINPOP clamp)
+    // cooling totals (kpkt.cc:84-165) with the level populations of ltepop.cc:307-430 (MINPOP clamp; NLTE and
+    // superlevel populations under the nebular options)
     const float nne = m.nne[mgi];
+    const double minpop = minpop_of(m);
     auto groundpop = [&](int e, int ui) {
       const double nn = m.groundlevelpop[(size_t)mgi * ni + ui];
-      if (nn < ARTIS_MINPOP) return m.elem_abundance[(size_t)mgi * ne + e] > 0 ? ARTIS_MINPOP : 0.;
+      if (nn < minpop) return m.elem_abundance[(size_t)mgi * ne + e] > 0 ? minpop : 0.;
       return nn;
     };
-    auto levelpop = [&](int e, int ui, int l) {
+    const double T_exc = (m.cfg.excitation_te || m.cfg.nebular) ? m.Te[mgi] : m.TJ[mgi];
+    auto lte_nominpop = [&](int e, int ui, int l) {
       const int off = m.ion_uniqueleveloffset[ui];
-      double nn;
       const double ng = groundpop(e, ui);
       if (l == 0) return ng;
-      nn = ng * 1. * m.level_stat_weight[off + l] / m.level_stat_weight[off] *
-           exp(-(m.level_epsilon[off + l] - m.level_epsilon[off]) / ARTIS_KB /
-               (m.cfg.excitation_te ? m.Te[mgi] : m.TJ[mgi]));
-      if (nn < ARTIS_MINPOP) nn = m.elem_abundance[(size_t)mgi * ne + e] > 0 ? ARTIS_MINPOP : 0.;
+      return ng * 1. * m.level_stat_weight[off + l] / m.level_stat_weight[off] *
+             exp(-(m.level_epsilon[off + l] - m.level_epsilon[off]) / ARTIS_KB / T_exc);
+    };
+    auto sl_boltzmann = [&](int ui, int l) {
+      const int off = m.ion_uniqueleveloffset[ui];
+      const int sl = m.ion_nlevels_nlte[ui] + 1;
+      return (double)m.level_stat_weight[off + l] / m.level_stat_weight[off + sl] *
+             exp(-(m.level_epsilon[off + l] - m.level_epsilon[off + sl]) / ARTIS_KB / T_exc);
+    };
+    if (m.cfg.nebular) {
+      // NLTE population stand-in: LTE / rho times a factor in [0.5, 2); some ions without a solution (-1, the
+      // "no NLTE information yet" marker of ltepop.cc:367); the superlevel from the LTE sum over its levels
+      double *np_row = &m.nlte_pops[(size_t)mgi * m.total_nlte_levels];
+      for (int ui = 0; ui < ni; ui++) {
+        const int e = m.ion_element[ui];
+        const int n = m.ion_nlevels_nlte[ui];
+        const int f0 = m.ion_first_nlte[ui];
+        const bool none = ((mgi + ui) % 7) == 3;
+        for (int l = 1; l <= n; l++)
+          np_row[f0 + l - 1] = none ? -1. : lte_nominpop(e, ui, l) / m.rho[mgi] * (0.5 + 1.5 * hash_u01(mgi, f0 + l, 11));
+        if (m.ion_nlevels[ui] > n + 1) {
+          double sum = 0., part = 0.;
+          for (int l = n + 1; l < m.ion_nlevels[ui]; l++) {
+            sum += lte_nominpop(e, ui, l);
+            part += sl_boltzmann(ui, l);
+          }
+          np_row[f0 + n] = (((mgi + ui) % 5) == 1) ? -1. : sum / part / m.rho[mgi] * (0.5 + 1.5 * hash_u01(mgi, ui, 12));
+        }
+      }
+    }
+    auto levelpop = [&](int e, int ui, int l) {
+      double nn = lte_nominpop(e, ui, l);
+      if (l > 0 && m.cfg.nebular) {
+        const double *np_row = &m.nlte_pops[(size_t)mgi * m.total_nlte_levels + m.ion_first_nlte[ui]];
+        const int n = m.ion_nlevels_nlte[ui];
+        const double v = (l <= n) ? np_row[l - 1] : np_row[n];
+        if (!(v < -0.9)) return (l <= n) ? v * m.rho[mgi] : v * m.rho[mgi] * sl_boltzmann(ui, l);
+      }
+      if (nn < minpop) nn = m.elem_abundance[(size_t)mgi * ne + e] > 0 ? minpop : 0.;
       return nn;
     };
     auto ionstagepop = [&](int e, int ui) {
@@ -1034,6 +1133,67 @@ void compute_cellstate(Model &m, int nts) {
       }
     }
     m.totalcooling[mgi] = C_total;
+    if (m.cfg.nebular) {
+      // binned radiation field fits around the cell's T_R / W (radfield.cc:908-920), some bins without a fit
+      const int nb = m.at.radfield_nbins;
+      for (int b = 0; b < nb; b++) {
+        const size_t mb = (size_t)mgi * nb + b;
+        m.rf_TR[mb] = (float)(m.TR[mgi] * (0.7 + 0.6 * hash_u01(mgi, b, 21)));
+        m.rf_W[mb] = ((b % 13) == 5) ? -1.f : (float)(m.W[mgi] * (0.3 + 1.4 * hash_u01(mgi, b, 22)));
+      }
+      // normalised bf-rate estimators of a previous timestep: W * LUT(T_R) of the cell (ratecoeff.cc:1026-1041)
+      // times a factor in [0.5, 1.5), some absent
+      const int lowerindex = std::min((int)floor(log(m.TR[mgi] / m.mintemp) / T_step_log), m.tablesize - 2);
+      const double fT = (m.TR[mgi] - m.mintemp * exp(lowerindex * T_step_log)) /
+                        (m.mintemp * exp((lowerindex + 1) * T_step_log) - m.mintemp * exp(lowerindex * T_step_log));
+      for (int i = 0; i < m.nbfcontinua; i++) {
+        const int e = m.allcont_element[i], ion = m.allcont_ion[i], l = m.allcont_level[i], t = m.allcont_target[i];
+        const int contindex = -1 - m.level_cont_index[uniquelevel(m, e, ion, l)] + t;
+        const double lo = m.corrphotoioncoeff[(size_t)std::max(lowerindex, 0) * m.nbfcontinua + contindex];
+        const double hi = m.corrphotoioncoeff[(size_t)(std::max(lowerindex, 0) + 1) * m.nbfcontinua + contindex];
+        const double v = m.W[mgi] * (lo + (hi - lo) * std::max(0., fT)) * (0.5 + hash_u01(mgi, i, 23));
+        m.bfrate_est[(size_t)mgi * m.nbfcontinua + i] = (i % 9 == 4) ? 0.f : ((i % 11 == 7) ? -1.f : (float)v);
+      }
+      // Spencer-Fano solution stand-in: ionisation rate coefficients, Auger-electron probabilities, and the
+      // deposition rate density that makes the ionisation fraction of do_ntlepton 0.3 .. 0.8
+      const int A = 2;
+      double enrate_total = 0.;
+      for (int e = 0; e < ne; e++) {
+        const int nions = m.elem_nions[e];
+        for (int ion = 0; ion < nions; ion++) {
+          const int ui = m.elem_uniqueionoffset[e] + ion;
+          m.nt_Y[(size_t)mgi * ni + ui] = (ion < nions - 1) ? pow(10., -3. + 4. * hash_u01(mgi, ui, 31)) : 0.;
+          const double p0 = 0.7 + 0.2 * hash_u01(mgi, ui, 32), p1 = (1. - p0) * 0.7;
+          const double q0 = 0.6 + 0.3 * hash_u01(mgi, ui, 33), q1 = (1. - q0) * 0.6;
+          float *pr = &m.nt_prob[((size_t)mgi * ni + ui) * (A + 1)];
+          float *pe = &m.nt_ionen[((size_t)mgi * ni + ui) * (A + 1)];
+          pr[0] = (float)p0;
+          pr[1] = (float)p1;
+          pr[2] = (float)(1. - p0 - p1);
+          pe[0] = (float)q0;
+          pe[1] = (float)q1;
+          pe[2] = (float)(1. - q0 - q1);
+        }
+        for (int lowerion = 0; lowerion < nions - 1; lowerion++) {
+          const int ui = m.elem_uniqueionoffset[e] + lowerion;
+          const double nnlowerion = groundpop(e, ui) * m.partfunct[(size_t)mgi * ni + ui] /
+                                    m.level_stat_weight[m.ion_uniqueleveloffset[ui]];
+          const int maxupper = std::min(lowerion + 1 + A, nions - 1);
+          double enrate = 0.;
+          for (int upperion = lowerion + 1; upperion <= maxupper; upperion++) {
+            const float *pr = &m.nt_prob[((size_t)mgi * ni + ui) * (A + 1)];
+            const int na = upperion - lowerion - 1;
+            const double prob = (na < A) ? pr[na] : 1. - pr[0] - pr[1];
+            enrate += nnlowerion * prob *
+                      (m.level_epsilon[m.ion_uniqueleveloffset[ui + upperion - lowerion]] -
+                       m.level_epsilon[m.ion_uniqueleveloffset[ui]]);
+          }
+          enrate_total += m.nt_Y[(size_t)mgi * ni + ui] * enrate;
+        }
+      }
+      const double frac = 0.3 + 0.5 * hash_u01(mgi, 0, 34);
+      m.nt_dep[mgi] = enrate_total > 0. ? enrate_total / frac : 1.;
+    }
   }
 
   artis_cell_state &cs = m.cs;
@@ -1053,6 +1213,16 @@ void compute_cellstate(Model &m, int nts) {
   cs.cooling_contrib_ion = m.cooling_contrib_ion.data();
   cs.corrphotoionrenorm = m.corrphotoionrenorm.data();
   cs.ffegrp = m.ffegrp.data();
+  if (m.cfg.nebular) {
+    cs.nlte_pops = m.nlte_pops.data();
+    cs.radfield_bin_TR = m.rf_TR.data();
+    cs.radfield_bin_W = m.rf_W.data();
+    cs.bfrate_estimator = m.bfrate_est.data();
+    cs.nt_deposition_rate_density = m.nt_dep.data();
+    cs.nt_ionization_ratecoeff = m.nt_Y.data();
+    cs.nt_prob_num_auger = m.nt_prob.data();
+    cs.nt_ionenfrac_num_auger = m.nt_ionen.data();
+  }
   m.current_nts = nts;
 }
 
@@ -1144,6 +1314,14 @@ void artis_synth_default_config(artis_synth_config *cfg) {
   cfg->kpktdiffusion_timescale = 0.;
   cfg->excitation_te = 0;
   cfg->tj_scale = 0.;
+  cfg->nebular = 0;
+  cfg->nlte_level_max = 80;
+  cfg->radfield_nbins = 256;
+  cfg->first_nlte_radfield_timestep = 12;
+  cfg->detailed_bf_usefromtimestep = 13;
+  cfg->minpop = 0.;
+  cfg->nu_min_r = 0.;
+  cfg->nu_max_r = 0.;
 }
 
 artis_model *artis_model_from_files(const artis_synth_config *cfg, const char *input_txt, const char *model_txt,
@@ -1166,6 +1344,7 @@ artis_model *artis_model_from_files(const artis_synth_config *cfg, const char *i
   m->cfg.kpktdiffusion_timescale = m->inp.kpktdiffusion_timescale;
   std::mt19937_64 rng(m->cfg.seed);
   build_atomic(*m, rng);
+  setup_nebular_atomic(*m);
   std::vector<float> abund((size_t)em.npts_model * m->nelements, 0.f);
   int rc = artis_read_abundances(abundances_txt, em.npts_model, em.model_type, m->nelements, m->elem_anumber.data(),
                                  abund.data());
@@ -1186,6 +1365,7 @@ artis_model *artis_model_synth(const artis_synth_config *cfg) {
   m->cfg = *cfg;
   std::mt19937_64 rng(cfg->seed);
   build_atomic(*m, rng);
+  setup_nebular_atomic(*m);
   build_grid(*m);
   compute_cellstate(*m, 0);
   rebuild_gamma_spectra(*m);
@@ -1197,6 +1377,7 @@ const artis_atomic_tables *artis_model_atomic(const artis_model *m) { return &m-
 const artis_geometry *artis_model_geometry(const artis_model *m) { return &m->geom; }
 const artis_cell_state *artis_model_cellstate(const artis_model *m) { return &m->cs; }
 int64_t artis_model_npts_model(const artis_model *m) { return m->npts_model; }
+int artis_model_radfield_nbins(const artis_model *m) { return m->at.radfield_nbins; }
 void artis_model_config(const artis_model *m, artis_synth_config *out) { *out = m->cfg; }
 
 void artis_model_run_params(const artis_model *m, artis_run_params *p) {
@@ -1216,6 +1397,21 @@ void artis_model_run_params(const artis_model *m, artis_run_params *p) {
   p->instant_particle_deposition = m->cfg.instant_particle_deposition;
   p->nt_solve_spencerfano = 0;
   p->excitation_temperature = m->cfg.excitation_te ? ARTIS_TEXC_TE : ARTIS_TEXC_TJ;
+  p->minpop = minpop_of(*m);
+  if (m->cfg.nebular) {  // artisoptions_nltenebular.h
+    p->excitation_temperature = ARTIS_TEXC_TE;
+    p->nlte_pops_on = 1;
+    p->multibin_radfield = 1;
+    p->first_nlte_radfield_timestep = m->cfg.first_nlte_radfield_timestep;
+    p->detailed_bf_estimators = 1;
+    p->detailed_bf_usefromtimestep = m->cfg.detailed_bf_usefromtimestep;
+    p->no_lut_photoion = 1;
+    p->no_lut_bfheating = 1;
+    p->nt_on = 1;
+    p->nt_solve_spencerfano = 1;
+    p->nt_max_auger_electrons = 2;
+    p->pol_dipole = 0;  // DIPOLE undefined (artisoptions_nltenebular.h:68)
+  }
   if (m->from_files) {  // input.txt run switches (input.cc:1976-1992, 2013, 2130)
     p->opacity_case = m->inp.opacity_case;
     p->do_r_lc = m->inp.do_r_lc;

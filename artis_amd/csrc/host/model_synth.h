@@ -40,6 +40,18 @@ typedef struct artis_synth_config {
   int32_t excitation_te;     /* run parameter excitation_temperature: 0 T_J (classic), 1 T_e (kilonova, nebular) */
   double tj_scale;           /* T_J = tj_scale * T_e in the cell-state stand-in (0 = 1: T_J == T_e, as in the LTE
                                 timesteps, update_grid.cc:1111-1114) */
+  /* the nebular options (artisoptions_nltenebular.h): NLTE + superlevel populations, the binned radiation field,
+     detailed bf estimators, NO_LUT photoionisation / bf-heating, non-thermal ionisation with Auger electrons,
+     MINPOP 1e-40, NU_MIN_R 1e13, T_e excitation.  The update_grid outputs these read (NLTE populations, bin fits,
+     normalised bf-rate estimators, the Spencer-Fano solution's rates and Auger fractions) are stand-ins drawn
+     around the LTE state. */
+  int32_t nebular;
+  int32_t nlte_level_max;    /* LEVEL_IS_NLTE: levels 1..nlte_level_max of every ion are NLTE (default 80) */
+  int32_t radfield_nbins;    /* RADFIELDBINCOUNT (default 256) */
+  int32_t first_nlte_radfield_timestep;  /* FIRST_NLTE_RADFIELD_TIMESTEP (default 12) */
+  int32_t detailed_bf_usefromtimestep;   /* DETAILED_BF_ESTIMATORS_USEFROMTIMESTEP (default 13) */
+  double minpop;             /* MINPOP (0: 1e-30 classic, 1e-40 nebular) */
+  double nu_min_r, nu_max_r; /* NU_MIN_R / NU_MAX_R (0: 1e14 / 5e15 classic; nebular 1e13 / 5e15) */
 } artis_synth_config;
 
 typedef struct artis_model artis_model;
@@ -67,6 +79,8 @@ int artis_model_init_rpackets(const artis_model *m, int nts, int npkts, uint64_t
                               artis_packet *out);
 
 int64_t artis_model_npts_model(const artis_model *m);
+/* RADFIELDBINCOUNT of the nebular options, 0 otherwise */
+int artis_model_radfield_nbins(const artis_model *m);
 /* the configuration the model was built with (after artis_model_from_files adopted input.txt's values) */
 void artis_model_config(const artis_model *m, artis_synth_config *out);
 

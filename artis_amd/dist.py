@@ -6,7 +6,7 @@ only exchange is a SUM of the estimator accumulators.  The block layout is defin
 (include/artis_gpu.h: artis_gpu_estimator_block_to_device on the device, artis_estimator_block_pack / _unpack on
 the host), and used here unchanged:
   [J | nuJ | ffheating | colheating | rpkt_emiss | gammaestimator | bfheatingestimator | 10 time_step scalars
-   | ecounter | acounter | counters (34) | nesc]
+   | bfrate_raw | radfield bins J, nuJ, contribcount (nebular options) | ecounter | acounter | counters (34) | nesc]
 On GPUs the block is all-reduced in HBM by the engine's own RCCL communicator over xGMI
 (artis_gpu_comm_init / artis_gpu_estimators_allreduce; Engine.comm_init / Engine.allreduce_estimators);
 host arrays are packed with the same layout and reduced with gloo in the CPU tests.
@@ -18,12 +18,12 @@ import numpy as np
 from . import gpu_lib
 
 
-def block_len(npts_model, nelements, maxnions, nlines):
-    return int(gpu_lib().artis_estimator_block_len(npts_model, nelements, maxnions, nlines))
+def block_len(npts_model, nelements, maxnions, nlines, nbf_est=0, nbins_est=0):
+    return int(gpu_lib().artis_estimator_block_len(npts_model, nelements, maxnions, nlines, nbf_est, nbins_est))
 
 
 def _dims(est):
-    return est.npts_model, est.nelements, est.maxnions, len(est.ecounter)
+    return est.npts_model, est.nelements, est.maxnions, len(est.ecounter), est.nbfcontinua, est.radfield_nbins
 
 
 def pack_estimators(est):

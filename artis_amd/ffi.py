@@ -153,6 +153,14 @@ class SynthConfig(C.Structure):
         ("kpktdiffusion_timescale", C.c_double),
         ("excitation_te", C.c_int32),
         ("tj_scale", C.c_double),
+        ("nebular", C.c_int32),
+        ("nlte_level_max", C.c_int32),
+        ("radfield_nbins", C.c_int32),
+        ("first_nlte_radfield_timestep", C.c_int32),
+        ("detailed_bf_usefromtimestep", C.c_int32),
+        ("minpop", C.c_double),
+        ("nu_min_r", C.c_double),
+        ("nu_max_r", C.c_double),
     ]
 
 
@@ -170,8 +178,11 @@ class GammaSpectra(C.Structure):
 class EstimatorArrays:
     """Host-side numpy storage for one artis_estimators block (reference zero_estimators shapes)."""
 
-    def __init__(self, npts_model, nelements, maxnions, nlines):
+    def __init__(self, npts_model, nelements, maxnions, nlines, nbfcontinua=0, radfield_nbins=0):
+        """nbfcontinua > 0: bfrate_raw (DETAILED_BF_ESTIMATORS_ON); radfield_nbins > 0: the bin estimators
+        (MULTIBIN_RADFIELD_MODEL_ON)."""
         self.npts_model, self.nelements, self.maxnions = npts_model, nelements, maxnions
+        self.nbfcontinua, self.radfield_nbins = nbfcontinua, radfield_nbins
         self.J = np.zeros(npts_model)
         self.nuJ = np.zeros(npts_model)
         self.ffheating = np.zeros(npts_model)
@@ -190,6 +201,15 @@ class EstimatorArrays:
         s.gammaestimator, s.bfheatingestimator = dp(self.gamma), dp(self.bfheating)
         s.ecounter, s.acounter = ip(self.ecounter), ip(self.acounter)
         s.rpkt_emiss = dp(self.rpkt_emiss)
+        self.bfrate_raw = np.zeros(npts_model * nbfcontinua)
+        self.radfield_J = np.zeros(npts_model * radfield_nbins)
+        self.radfield_nuJ = np.zeros(npts_model * radfield_nbins)
+        self.radfield_count = np.zeros(npts_model * radfield_nbins, dtype=np.int64)
+        if nbfcontinua > 0:
+            s.bfrate_raw = dp(self.bfrate_raw)
+        if radfield_nbins > 0:
+            s.radfield_J_raw, s.radfield_nuJ_raw = dp(self.radfield_J), dp(self.radfield_nuJ)
+            s.radfield_contribcount = self.radfield_count.ctypes.data_as(C.POINTER(C.c_int64))
 
     @property
     def counters(self):

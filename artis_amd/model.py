@@ -41,6 +41,7 @@ def model_lib():
         lib.artis_model_config.argtypes = [C.c_void_p, C.POINTER(ffi.SynthConfig)]
         lib.artis_model_npts_model.argtypes = [C.c_void_p]
         lib.artis_model_npts_model.restype = C.c_int64
+        lib.artis_model_radfield_nbins.argtypes = [C.c_void_p]
         _model_lib = lib
     return _model_lib
 
@@ -144,7 +145,14 @@ class Model:
         return pk
 
     def new_estimators(self):
-        return ffi.EstimatorArrays(self.npts_model, self.nelements, self.maxnions, self.nlines)
+        p = self.params
+        return ffi.EstimatorArrays(self.npts_model, self.nelements, self.maxnions, self.nlines,
+                                   self.nbfcontinua if p.detailed_bf_estimators else 0,
+                                   self.radfield_nbins if p.multibin_radfield else 0)
+
+    @property
+    def radfield_nbins(self):
+        return int(self._lib.artis_model_radfield_nbins(self._h))
 
     def close(self):
         if self._h:

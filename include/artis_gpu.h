@@ -439,14 +439,17 @@ int artis_gpu_estimator_block_from_device(const void *src_device);
  * artis_estimators sums exactly what the device block carries:
  *   [J | nuJ | ffheating | colheating | rpkt_emiss (npts_model each) | gammaestimator | bfheatingestimator
  *    (npts_model * nelements * maxnions each) | cmf_lum gamma_dep positron_dep electron_dep electron_emission
- *    alpha_dep alpha_emission gamma_emission nt_energy_deposited pellet_decays | ecounter | acounter (nlines each)
- *   | counters (ARTIS_COUNTER_COUNT) | nesc]   -- counts as float64 (exact below 2^53).
+ *    alpha_dep alpha_emission gamma_emission nt_energy_deposited pellet_decays | bfrate_raw (npts_model * nbf_est)
+ *   | radfield_J_raw | radfield_nuJ_raw | radfield_contribcount (npts_model * nbins_est each) | ecounter | acounter
+ *    (nlines each) | counters (ARTIS_COUNTER_COUNT) | nesc]   -- counts as float64 (exact below 2^53).
+ * nbf_est = nbfcontinua under DETAILED_BF_ESTIMATORS_ON, else 0; nbins_est = radfield_nbins under
+ * MULTIBIN_RADFIELD_MODEL_ON, else 0 (the engine's block has the sections its run parameters switch on).
  * pack: NULL array pointers of *est pack as zeros; unpack OVERWRITES *est (NULL arrays skipped). */
-size_t artis_estimator_block_len(int npts_model, int nelements, int maxnions, int nlines);
+size_t artis_estimator_block_len(int npts_model, int nelements, int maxnions, int nlines, int nbf_est, int nbins_est);
 int artis_estimator_block_pack(const artis_estimators *est, int npts_model, int nelements, int maxnions, int nlines,
-                               double *block);
+                               int nbf_est, int nbins_est, double *block);
 int artis_estimator_block_unpack(const double *block, int npts_model, int nelements, int maxnions, int nlines,
-                                 artis_estimators *est);
+                                 int nbf_est, int nbins_est, artis_estimators *est);
 
 /* --- multi-GPU: RCCL over xGMI (the reference's mpi_reduce_estimators, sn3d.cc:316-377, radfield.cc:1502-1564) */
 /* One process per GPU; every rank propagates its own full-energy ensemble and the only exchange per timestep

@@ -50,6 +50,7 @@
 
 #include "artis_constants.h"
 #include "artis_gpu.h"
+#include "artis_qk61.h"
 #include "artis_rng.h"
 
 namespace {
@@ -72,6 +73,9 @@ struct Ctx {
   const artis_cell_state *cs;
   artis_run_params rp;
   double T_step_log;
+  int nts = 0;          // globals::nts_global (sn3d.cc:1038)
+  double minpop = 1e-30;  // MINPOP of the options file (artis_run_params.minpop)
+  std::vector<int32_t> slot_allcont;  // photoionisation target slot -> allcont index (get_bfcontindex)
   const artis_gamma_spectra *gs;  // may be NULL: no pellets / gamma packets in the ensemble
   const VpktCfg *vp = nullptr;    // NULL: VPKT_ON undefined
 };
@@ -96,6 +100,7 @@ struct ThreadCache {
   double kap_total = 0, kap_es = 0, kap_ff = 0, kap_bf = 0, kap_ffheating = 0;
   std::vector<double> kappa_bf_sum;            // [nbfcontinua]
   std::vector<double> groundcont_gamma_contr;  // [nbfcontinua_ground]
+  std::vector<double> gamma_contr;             // [nbfcontinua] DETAILED_BF_ESTIMATORS_ON (globals.h:165)
   int64_t work[ARTIS_WORK_COUNT] = {0};
 };
 
@@ -237,17 +242,21 @@ inline void get_rand_isotropic_unitvec(artis_rng *rng, double out[3]) {
 // ltepop.cc:307-327
 double get_groundlevelpop(const Ctx &c, int mgi, int e, int i) {
   const double nn = c.cs->groundlevelpop[(size_t)mgi * c.at->nions_total + uion(c, e, i)];
-  if (nn < ARTIS_MINPOP) {
-    if (c.cs->elem_abundance[(size_t)mgi * c.at->nelements + e] > 0) return ARTIS_MINPOP;
+  if (nn < c.minpop) {
+    if (c.cs->elem_abundance[(size_t)mgi * c.at->nelements + e] > 0) return c.minpop;
     return 0.;
   }
   return nn;
 }
-// ltepop.cc:329-347; T_exc = LTEPOP_EXCITATIONTEMPERATURE (ltepop.cc:338): T_J in artisoptions_classic.h:32,
-// T_e in artisoptions_kilonova_lte.h:36 / artisoptions_nltenebular.h:36
+// LTEPOP_EXCITATIONTEMPERATURE (ltepop.cc:338): T_J in artisoptions_classic.h:32, T_e in
+// artisoptions_kilonova_lte.h:36 / artisoptions_nltenebular.h:36 (grid::get_Te / get_TJ return float)
+inline double excitation_temperature(const Ctx &c, int mgi) {
+  return (c.rp.excitation_temperature == ARTIS_TEXC_TE) ? c.cs->Te[mgi] : c.cs->TJ[mgi];
+}
+// ltepop.cc:329-347
 double calculate_levelpop_lte(const Ctx &c, int mgi, int e, int i, int l) {
   if (l == 0) return get_groundlevelpop(c, mgi, e, i);
-  const double T_exc = (c.rp.excitation_temperature == ARTIS_TEXC_TE) ? c.cs->Te[mgi] : c.cs->TJ[mgi];
+  const double T_exc = excitation_temperature(c, mgi);
   const double W = 1.;
   const double E_level = epsilon(c, e, i, l);
   const double E_ground = epsilon(c, e, i, 0);
@@ -255,12 +264,66 @@ double calculate_levelpop_lte(const Ctx &c, int mgi, int e, int i, int l) {
   return (nnground * W * stat_weight(c, e, i, l) / stat_weight(c, e, i, 0) *
           exp(-(E_level - E_ground) / ARTIS_KB / T_exc));
 }
-// ltepop.cc:417-430 (NLTE_POPS_ON false)
+// atomic.cc:235-241, 69-85, 367-371 with LEVEL_IS_NLTE contiguous from the ground state
+// (artisoptions_nltenebular.h:26-34): levels 1..nlevels_nlte are NLTE, the rest of the excited levels form the
+// superlevel
+inline int get_nlevels_nlte(const Ctx &c, int e, int i) { return c.at->ion_nlevels_nlte[uion(c, e, i)]; }
+inline bool is_nlte(const Ctx &c, int e, int i, int l) { return c.rp.nlte_pops_on && l <= get_nlevels_nlte(c, e, i); }
+// nltepop.cc:1543-1554
+double superlevel_boltzmann(const Ctx &c, int mgi, int e, int i, int l) {
+  const int superlevel_index = get_nlevels_nlte(c, e, i) + 1;
+  const double T_exc = excitation_temperature(c, mgi);
+  const double E_level = epsilon(c, e, i, l);
+  const double E_superlevel = epsilon(c, e, i, superlevel_index);
+  return stat_weight(c, e, i, l) / stat_weight(c, e, i, superlevel_index) * exp(-(E_level - E_superlevel) / ARTIS_KB / T_exc);
+}
+// ltepop.cc:349-415
+double calculate_levelpop_nominpop(const Ctx &c, int mgi, int e, int i, int l, bool *skipminpop) {
+  double nn;
+  if (l == 0) {
+    nn = get_groundlevelpop(c, mgi, e, i);
+  } else if (c.rp.nlte_pops_on) {
+    const size_t base = (size_t)mgi * c.at->total_nlte_levels + c.at->ion_first_nlte[uion(c, e, i)];
+    if (is_nlte(c, e, i, l)) {
+      const double nltepop_over_rho = c.cs->nlte_pops[base + l - 1];
+      if (nltepop_over_rho < -0.9) {
+        nn = calculate_levelpop_lte(c, mgi, e, i, l);
+      } else {
+        nn = nltepop_over_rho * c.cs->rho[mgi];
+        if (!std::isfinite(nn)) {
+          fprintf(stderr, "oracle: [fatal] NLTE population failure\n");
+          abort();
+        }
+        *skipminpop = true;
+        return nn;
+      }
+    } else {
+      const double superlevelpop_over_rho = c.cs->nlte_pops[base + get_nlevels_nlte(c, e, i)];
+      if (superlevelpop_over_rho < -0.9) {
+        nn = calculate_levelpop_lte(c, mgi, e, i, l);
+      } else {
+        nn = superlevelpop_over_rho * c.cs->rho[mgi] * superlevel_boltzmann(c, mgi, e, i, l);
+        if (!std::isfinite(nn)) {
+          fprintf(stderr, "oracle: [fatal] NLTE population failure\n");
+          abort();
+        }
+        *skipminpop = true;
+        return nn;
+      }
+    }
+  } else {
+    nn = calculate_levelpop_lte(c, mgi, e, i, l);
+  }
+  *skipminpop = false;
+  return nn;
+}
+// ltepop.cc:417-430
 double calculate_levelpop(const Ctx &c, int mgi, int e, int i, int l) {
-  double nn = calculate_levelpop_lte(c, mgi, e, i, l);
-  if (nn < ARTIS_MINPOP) {
+  bool skipminpop = false;
+  double nn = calculate_levelpop_nominpop(c, mgi, e, i, l, &skipminpop);
+  if (!skipminpop && nn < c.minpop) {
     if (c.cs->elem_abundance[(size_t)mgi * c.at->nelements + e] > 0)
-      nn = ARTIS_MINPOP;
+      nn = c.minpop;
     else
       nn = 0.;
   }
@@ -297,8 +360,26 @@ inline double get_levelpop(const ThreadCache &tc, const Ctx &c, int e, int i, in
 inline double dbb(double nu, double T, double W) {
   return W * ARTIS_TWOHOVERCLIGHTSQUARED * pow(nu, 3) / expm1(ARTIS_HOVERKB * nu / T);  // radfield.h:44-48
 }
-// radfield.cc:898-943 (MULTIBIN_RADFIELD_MODEL_ON false)
+// radfield.cc:575-600 select_bin: -2 below the first bin, -1 above the last
+int select_bin(const Ctx &c, double nu) {
+  if (nu < c.at->radfield_nu_lower_first) return -2;
+  const double *up = c.at->radfield_nu_upper;
+  const int binindex = (int)(std::upper_bound(up, up + c.at->radfield_nbins, nu) - up);
+  if (binindex >= c.at->radfield_nbins) return -1;
+  return binindex;
+}
+// radfield.cc:898-943: J_nu of the fitted dilute blackbody of the bin from FIRST_NLTE_RADFIELD_TIMESTEP on
+// (MULTIBIN_RADFIELD_MODEL_ON), the full-spectrum dilute blackbody otherwise
 inline double radfield(const Ctx &c, double nu, int mgi) {
+  if (c.rp.multibin_radfield && c.nts >= c.rp.first_nlte_radfield_timestep) {
+    const int binindex = select_bin(c, nu);
+    if (binindex >= 0) {
+      const size_t mb = (size_t)mgi * c.at->radfield_nbins + binindex;
+      const float W = c.cs->radfield_bin_W[mb];
+      if (W >= 0.) return dbb(nu, c.cs->radfield_bin_TR[mb], W);
+    }
+    return 0.;
+  }
   const float T_R = c.cs->TR[mgi];
   const float W = c.cs->W[mgi];
   return dbb(nu, T_R, W);
@@ -364,18 +445,299 @@ double interpolate_corrphotoioncoeff(const Ctx &c, int e, int i, int l, int t, d
   }
   return c.at->corrphotoioncoeff[get_bflutindex(c, tablesize - 1, e, i, l, t)];
 }
-// ratecoeff.cc:1247-1308 (LUT path; cached per thread like cellhistory chphixstargets)
+// ---- gsl_integration_qag with GSL_INTEG_GAUSS61 (GSL 2.x integration/qag.c, qk.c, qk61.c, qpsrt.c, util.c,
+// err.c), the quadrature calculate_corrphotoioncoeff_integral hands its integrand to (ratecoeff.cc:1225-1226).
+// GSL is a dependency the reference links and this image lacks; this is its published algorithm: the 61-point
+// Gauss-Kronrod rule (include/artis_qk61.h, generated by tools/gen_qk61.py) and adaptive bisection of the
+// interval with the largest error estimate, the error list kept ordered by qpsrt.
+constexpr double kGslDblEpsilon = 2.2204460492503131e-16;
+constexpr double kGslDblMin = 2.2250738585072014e-308;
+const double qk61_xgk[31] = ARTIS_QK61_XGK;
+const double qk61_wg[15] = ARTIS_QK61_WG;
+const double qk61_wgk[31] = ARTIS_QK61_WGK;
+
+double gsl_rescale_error(double err, const double result_abs, const double result_asc) {
+  err = fabs(err);
+  if (result_asc != 0 && err != 0) {
+    const double scale = pow((200 * err / result_asc), 1.5);
+    if (scale < 1)
+      err = result_asc * scale;
+    else
+      err = result_asc;
+  }
+  if (result_abs > 2 * kGslDblMin / (50 * kGslDblEpsilon)) {
+    const double min_err = 50 * kGslDblEpsilon * result_abs;
+    if (min_err > err) err = min_err;
+  }
+  return err;
+}
+
+template <typename F>
+void gsl_qk61(const F &f, double a, double b, double *result, double *abserr, double *resabs, double *resasc) {
+  const int n = 31;
+  double fv1[31], fv2[31];
+  const double center = 0.5 * (a + b);
+  const double half_length = 0.5 * (b - a);
+  const double abs_half_length = fabs(half_length);
+  const double f_center = f(center);
+  double result_gauss = 0;
+  double result_kronrod = f_center * qk61_wgk[n - 1];
+  double result_abs = fabs(result_kronrod);
+  double result_asc = 0;
+  for (int j = 0; j < (n - 1) / 2; j++) {
+    const int jtw = j * 2 + 1;
+    const double abscissa = half_length * qk61_xgk[jtw];
+    const double fval1 = f(center - abscissa);
+    const double fval2 = f(center + abscissa);
+    const double fsum = fval1 + fval2;
+    fv1[jtw] = fval1;
+    fv2[jtw] = fval2;
+    result_gauss += qk61_wg[j] * fsum;
+    result_kronrod += qk61_wgk[jtw] * fsum;
+    result_abs += qk61_wgk[jtw] * (fabs(fval1) + fabs(fval2));
+  }
+  for (int j = 0; j < n / 2; j++) {
+    const int jtwm1 = j * 2;
+    const double abscissa = half_length * qk61_xgk[jtwm1];
+    const double fval1 = f(center - abscissa);
+    const double fval2 = f(center + abscissa);
+    fv1[jtwm1] = fval1;
+    fv2[jtwm1] = fval2;
+    result_kronrod += qk61_wgk[jtwm1] * (fval1 + fval2);
+    result_abs += qk61_wgk[jtwm1] * (fabs(fval1) + fabs(fval2));
+  }
+  const double mean = result_kronrod * 0.5;
+  result_asc = qk61_wgk[n - 1] * fabs(f_center - mean);
+  for (int j = 0; j < n - 1; j++) result_asc += qk61_wgk[j] * (fabs(fv1[j] - mean) + fabs(fv2[j] - mean));
+  const double err = (result_kronrod - result_gauss) * half_length;
+  result_kronrod *= half_length;
+  result_abs *= abs_half_length;
+  result_asc *= abs_half_length;
+  *result = result_kronrod;
+  *resabs = result_abs;
+  *resasc = result_asc;
+  *abserr = gsl_rescale_error(err, result_abs, result_asc);
+}
+
+struct GslWorkspace {
+  size_t limit = 0, size = 0, nrmax = 0, i = 0, maximum_level = 0;
+  std::vector<double> alist, blist, rlist, elist;
+  std::vector<size_t> order, level;
+  explicit GslWorkspace(size_t n) : limit(n), alist(n), blist(n), rlist(n), elist(n), order(n), level(n) {}
+};
+
+void gsl_qpsrt(GslWorkspace &w) {
+  const size_t last = w.size - 1;
+  const size_t limit = w.limit;
+  double *elist = w.elist.data();
+  size_t *order = w.order.data();
+  size_t i_nrmax = w.nrmax;
+  size_t i_maxerr = order[i_nrmax];
+  if (last < 2) {
+    order[0] = 0;
+    order[1] = 1;
+    w.i = i_maxerr;
+    return;
+  }
+  const double errmax = elist[i_maxerr];
+  while (i_nrmax > 0 && errmax > elist[order[i_nrmax - 1]]) {
+    order[i_nrmax] = order[i_nrmax - 1];
+    i_nrmax--;
+  }
+  int top;
+  if (last < (limit / 2 + 2))
+    top = (int)last;
+  else
+    top = (int)(limit - last + 1);
+  int i = (int)i_nrmax + 1;
+  while (i < top && errmax < elist[order[i]]) {
+    order[i - 1] = order[i];
+    i++;
+  }
+  order[i - 1] = i_maxerr;
+  const double errmin = elist[last];
+  int k = top - 1;
+  while (k > i - 2 && errmin >= elist[order[k]]) {
+    order[k + 1] = order[k];
+    k--;
+  }
+  order[k + 1] = last;
+  i_maxerr = order[i_nrmax];
+  w.i = i_maxerr;
+  w.nrmax = i_nrmax;
+}
+
+void gsl_ws_update(GslWorkspace &w, double a1, double b1, double area1, double error1, double a2, double b2,
+                   double area2, double error2) {
+  const size_t i_max = w.i;
+  const size_t i_new = w.size;
+  const size_t new_level = w.level[i_max] + 1;
+  if (error2 > error1) {
+    w.alist[i_max] = a2;
+    w.rlist[i_max] = area2;
+    w.elist[i_max] = error2;
+    w.level[i_max] = new_level;
+    w.alist[i_new] = a1;
+    w.blist[i_new] = b1;
+    w.rlist[i_new] = area1;
+    w.elist[i_new] = error1;
+    w.level[i_new] = new_level;
+  } else {
+    w.blist[i_max] = b1;
+    w.rlist[i_max] = area1;
+    w.elist[i_max] = error1;
+    w.level[i_max] = new_level;
+    w.alist[i_new] = a2;
+    w.blist[i_new] = b2;
+    w.rlist[i_new] = area2;
+    w.elist[i_new] = error2;
+    w.level[i_new] = new_level;
+  }
+  w.size++;
+  if (new_level > w.maximum_level) w.maximum_level = new_level;
+  gsl_qpsrt(w);
+}
+
+// returns the GSL status (0, GSL_EROUND 18, GSL_ESING 21, GSL_EMAXITER 11, GSL_EFAILED 5)
+template <typename F>
+int gsl_qag61(const F &f, double a, double b, double epsabs, double epsrel, size_t limit, GslWorkspace &w,
+              double *result, double *abserr) {
+  w.size = 0;
+  w.nrmax = 0;
+  w.i = 0;
+  w.alist[0] = a;
+  w.blist[0] = b;
+  w.rlist[0] = 0.0;
+  w.elist[0] = 0.0;
+  w.order[0] = 0;
+  w.level[0] = 0;
+  w.maximum_level = 0;
+  *result = 0;
+  *abserr = 0;
+  double result0, abserr0, resabs0, resasc0;
+  gsl_qk61(f, a, b, &result0, &abserr0, &resabs0, &resasc0);
+  w.size = 1;
+  w.rlist[0] = result0;
+  w.elist[0] = abserr0;
+  double tolerance = std::max(epsabs, epsrel * fabs(result0));
+  const double round_off = 50 * kGslDblEpsilon * resabs0;
+  if (abserr0 <= round_off && abserr0 > tolerance) {
+    *result = result0;
+    *abserr = abserr0;
+    return 18;
+  } else if ((abserr0 <= tolerance && abserr0 != resasc0) || abserr0 == 0.0) {
+    *result = result0;
+    *abserr = abserr0;
+    return 0;
+  } else if (limit == 1) {
+    *result = result0;
+    *abserr = abserr0;
+    return 11;
+  }
+  double area = result0;
+  double errsum = abserr0;
+  size_t iteration = 1;
+  int roundoff_type1 = 0, roundoff_type2 = 0, error_type = 0;
+  do {
+    const size_t ii = w.i;
+    const double a_i = w.alist[ii], b_i = w.blist[ii], r_i = w.rlist[ii], e_i = w.elist[ii];
+    const double a1 = a_i;
+    const double b1 = 0.5 * (a_i + b_i);
+    const double a2 = b1;
+    const double b2 = b_i;
+    double area1 = 0, area2 = 0, error1 = 0, error2 = 0, resasc1, resasc2, resabs1, resabs2;
+    gsl_qk61(f, a1, b1, &area1, &error1, &resabs1, &resasc1);
+    gsl_qk61(f, a2, b2, &area2, &error2, &resabs2, &resasc2);
+    const double area12 = area1 + area2;
+    const double error12 = error1 + error2;
+    errsum += (error12 - e_i);
+    area += area12 - r_i;
+    if (resasc1 != error1 && resasc2 != error2) {
+      const double delta = r_i - area12;
+      if (fabs(delta) <= 1.0e-5 * fabs(area12) && error12 >= 0.99 * e_i) roundoff_type1++;
+      if (iteration >= 10 && error12 > e_i) roundoff_type2++;
+    }
+    tolerance = std::max(epsabs, epsrel * fabs(area));
+    if (errsum > tolerance) {
+      if (roundoff_type1 >= 6 || roundoff_type2 >= 20) error_type = 2;
+      const double tmp = (1 + 100 * kGslDblEpsilon) * (fabs(a2) + 1000 * kGslDblMin);
+      if (fabs(a1) <= tmp && fabs(b2) <= tmp) error_type = 3;
+    }
+    gsl_ws_update(w, a1, b1, area1, error1, a2, b2, area2, error2);
+    iteration++;
+  } while (iteration < limit && !error_type && errsum > tolerance);
+  double result_sum = 0;
+  for (size_t k = 0; k < w.size; k++) result_sum += w.rlist[k];
+  *result = result_sum;
+  *abserr = errsum;
+  if (errsum <= tolerance) return 0;
+  if (error_type == 2) return 18;
+  if (error_type == 3) return 21;
+  if (iteration == limit) return 11;
+  return 5;
+}
+
+constexpr size_t kGslWsSize = 16384;  // GSLWSIZE (artisoptions_nltenebular.h:75)
+
+// ratecoeff.cc:1159-1245 calculate_corrphotoioncoeff_integral (NO_LUT_PHOTOION)
+double calculate_corrphotoioncoeff_integral(const Ctx &c, const ThreadCache &tc, int e, int i, int l, int t, int mgi) {
+  constexpr double epsrel = 1e-3;
+  constexpr double epsabs = 0.;
+  const double E_threshold = get_phixs_threshold(c, e, i, l, t);
+  const double nu_threshold = ARTIS_ONEOVERH * E_threshold;
+  const double nu_max_phixs = nu_threshold * c.at->last_phixs_nuovernuedge;
+  const float T_e = c.cs->Te[mgi];
+  const double nnlevel = get_levelpop(tc, c, e, i, l);
+  const double nne = c.cs->nne[mgi];
+  const int upperionlevel = get_phixsupperlevel(c, e, i, l, t);
+  const double sf = calculate_sahafact(c, e, i, l, upperionlevel, T_e, ARTIS_H * nu_threshold);
+  const double nnupperionlevel = get_levelpop(tc, c, e, i + 1, upperionlevel);
+  double departure_ratio = nnlevel > 0. ? nnupperionlevel / nnlevel * nne * sf : 1.0;
+  if (!std::isfinite(departure_ratio)) departure_ratio = 0.;
+  const float *xs = level_photoion_xs(c, e, i, l);
+  // integrand_corrphotoioncoeff_custom_radfield (ratecoeff.cc:1159-1181)
+  auto integrand = [&](double nu) {
+    double corrfactor = 1. - departure_ratio * exp(-ARTIS_HOVERKB * nu / T_e);
+    if (corrfactor < 0) corrfactor = 0.;
+    const float sigma_bf = (float)photoionization_crosssection_fromtable(c, xs, nu_threshold, nu);
+    const double Jnu = radfield(c, nu, mgi);
+    return ARTIS_ONEOVERH * sigma_bf / nu * Jnu * corrfactor;
+  };
+  static thread_local GslWorkspace ws(kGslWsSize);
+  double gammacorr = 0.0, error = 0.0;
+  const int status = gsl_qag61(integrand, nu_threshold, nu_max_phixs, epsabs, epsrel, kGslWsSize, ws, &gammacorr, &error);
+  if (status != 0 && (status != 18 || (error / gammacorr) > 1e-1)) {
+    if (!std::isfinite(gammacorr)) gammacorr = 0.;
+  }
+  gammacorr *= ARTIS_FOURPI * get_phixsprobability(c, e, i, l, t);
+  return gammacorr;
+}
+
+// ratecoeff.cc:1247-1308 (cached per thread like cellhistory chphixstargets): the previous timestep's bf-rate
+// estimator when DETAILED_BF_ESTIMATORS_ON from DETAILED_BF_ESTIMATORS_USEFROMTIMESTEP (radfield.cc:1440-1455,
+// get_bfcontindex radfield.cc:1329-1341), else the integral (NO_LUT_PHOTOION) or W * LUT * renormalisation
 double get_corrphotoioncoeff(const Ctx &c, ThreadCache &tc, int e, int i, int l, int t, int mgi) {
   const int slot = c.at->level_phixstargets_offset[ulev(c, e, i, l)] + t;
+  if (c.rp.detailed_bf_estimators && c.nts >= c.rp.detailed_bf_usefromtimestep) {
+    const int allcontindex = c.slot_allcont[slot];
+    if (allcontindex >= 0) {
+      const double gammacorr = c.cs->bfrate_estimator[(size_t)mgi * c.at->nbfcontinua + allcontindex];
+      if (gammacorr > 0) return gammacorr;
+    }
+  }
   double gammacorr = tc.corrphotoioncoeff[slot];
   if (gammacorr < 0) {
-    const double W = c.cs->W[mgi];
-    const double T_R = c.cs->TR[mgi];
-    gammacorr = W * interpolate_corrphotoioncoeff(c, e, i, l, t, T_R);
-    const int index_in_groundlevelcontestimator = c.at->level_closestgroundlevelcont[ulev(c, e, i, l)];
-    if (index_in_groundlevelcontestimator >= 0)
-      gammacorr *= c.cs->corrphotoionrenorm[(size_t)mgi * c.at->nelements * c.at->maxnions +
-                                            index_in_groundlevelcontestimator];
+    if (c.rp.no_lut_photoion) {
+      gammacorr = calculate_corrphotoioncoeff_integral(c, tc, e, i, l, t, mgi);
+    } else {
+      const double W = c.cs->W[mgi];
+      const double T_R = c.cs->TR[mgi];
+      gammacorr = W * interpolate_corrphotoioncoeff(c, e, i, l, t, T_R);
+      const int index_in_groundlevelcontestimator = c.at->level_closestgroundlevelcont[ulev(c, e, i, l)];
+      if (index_in_groundlevelcontestimator >= 0)
+        gammacorr *= c.cs->corrphotoionrenorm[(size_t)mgi * c.at->nelements * c.at->maxnions +
+                                              index_in_groundlevelcontestimator];
+    }
     tc.corrphotoioncoeff[slot] = gammacorr;
   }
   return gammacorr;
@@ -923,10 +1285,12 @@ double calculate_kappa_ff(const Ctx &c, int mgi, double nu) {
   kappa_ff *= 3.69255e8 / sqrt((double)T_e) * pow(nu, -3) * nne * (1 - exp(-ARTIS_HOVERKB * nu / T_e));
   return kappa_ff;
 }
-// rpkt.cc:1075-1207 (SEPARATE_STIMRECOMB false, DETAILED_BF_ESTIMATORS_ON false, LUT photoion)
+// rpkt.cc:1075-1207 (SEPARATE_STIMRECOMB false); DETAILED_BF_ESTIMATORS_ON: every continuum of an element
+// present in the cell is included (rpkt.cc:1116-1118) and gamma_contr[i] is kept for update_bfestimators
 double calculate_kappa_bf_gammacontr(const Ctx &c, ThreadCache &tc, int mgi, double nu) {
   double kappa_bf_sum = 0.;
   const artis_atomic_tables &a = *c.at;
+  const bool detailed = c.rp.detailed_bf_estimators;
   for (int g = 0; g < a.nbfcontinua_ground; g++) tc.groundcont_gamma_contr[g] = 0.;
   const double T_e = c.cs->Te[mgi];
   const double nne = c.cs->nne[mgi];
@@ -938,7 +1302,8 @@ double calculate_kappa_bf_gammacontr(const Ctx &c, ThreadCache &tc, int mgi, dou
     const int element = a.allcont_element[i];
     const int ion = a.allcont_ion[i];
     const int level = a.allcont_level[i];
-    if ((ionstagepop(c, mgi, element, ion) / nnetot > 1.e-6) || (level == 0)) {
+    if ((detailed && c.cs->elem_abundance[(size_t)mgi * a.nelements + element] > 0) ||
+        (!detailed && ((ionstagepop(c, mgi, element, ion) / nnetot > 1.e-6) || (level == 0)))) {
       const double nu_edge = a.allcont_nu_edge[i];
       const double nnlevel = get_levelpop(tc, c, element, ion, level);
       const double nu_max_phixs = nu_edge * a.last_phixs_nuovernuedge;
@@ -963,6 +1328,7 @@ double calculate_kappa_bf_gammacontr(const Ctx &c, ThreadCache &tc, int mgi, dou
           const int gphixsindex = a.allcont_index_in_groundphixslist[i];
           tc.groundcont_gamma_contr[gphixsindex] += sigma_bf * probability * corrfactor;
         }
+        if (detailed) tc.gamma_contr[i] = sigma_bf * probability * corrfactor;
         if (!std::isfinite(kappa_bf_contr)) {
           fprintf(stderr, "oracle: non-finite kappa_bf_contr\n");
           abort();
@@ -971,12 +1337,17 @@ double calculate_kappa_bf_gammacontr(const Ctx &c, ThreadCache &tc, int mgi, dou
         tc.kappa_bf_sum[i] = kappa_bf_sum;
       } else {
         tc.kappa_bf_sum[i] = kappa_bf_sum;
+        if (detailed) tc.gamma_contr[i] = 0.;
       }
     } else {
       tc.kappa_bf_sum[i] = kappa_bf_sum;
+      if (detailed) tc.gamma_contr[i] = 0.;
     }
   }
-  for (; i < nbfcontinua; i++) tc.kappa_bf_sum[i] = kappa_bf_sum;
+  for (; i < nbfcontinua; i++) {
+    tc.kappa_bf_sum[i] = kappa_bf_sum;
+    if (detailed) tc.gamma_contr[i] = 0.;
+  }
   return kappa_bf_sum;
 }
 // rpkt.cc:1209-1295 (deviation D2: always recomputed)
@@ -1285,6 +1656,7 @@ void vpkt_call_estimators(const Ctx &c, Est &E, const artis_packet *p, double t_
     vtc.cooling_contrib.assign(c.at->ncoolingterms, -99.);
     vtc.kappa_bf_sum.assign(c.at->nbfcontinua, 0.);
     vtc.groundcont_gamma_contr.assign(c.at->nbfcontinua_ground, 0.);
+    vtc.gamma_contr.assign(c.at->nbfcontinua, 0.);
   }
   vtc.cellnumber = -99;  // the cell state may have changed since the last call
   for (int bin = 0; bin < v.p.nobs; bin++) {
@@ -1398,6 +1770,25 @@ double get_event(const Ctx &c, ThreadCache &tc, int mgi, artis_packet *p, int *r
   }
 }
 
+// radfield.cc:764-829 update_bfestimators (DETAILED_BF_ESTIMATORS_ON, DETAILED_BF_ESTIMATORS_BYTYPE false)
+void update_bfestimators(const Ctx &c, const ThreadCache &tc, Est &E, int mgi, double distance_e_cmf, double nu_cmf,
+                         const artis_packet *p) {
+  if (distance_e_cmf == 0) return;
+  const int nbfcontinua = c.at->nbfcontinua;
+  const double dopplerfactor = doppler_packet_nucmf_on_nurf(c, p);
+  const double distance_e_cmf_over_nu = distance_e_cmf / nu_cmf * dopplerfactor;
+  for (int allcontindex = 0; allcontindex < nbfcontinua; allcontindex++) {
+    const double nu_edge = c.at->allcont_nu_edge[allcontindex];
+    const double nu_max_phixs = nu_edge * c.at->last_phixs_nuovernuedge;
+    if (nu_cmf >= nu_edge && nu_cmf <= nu_max_phixs) {
+      safeadd(&E.e->bfrate_raw[(size_t)mgi * nbfcontinua + allcontindex],
+              tc.gamma_contr[allcontindex] * distance_e_cmf_over_nu);
+    } else if (nu_cmf < nu_edge) {
+      break;
+    }
+  }
+}
+
 // rpkt.cc:557-621 + radfield.cc:831-876
 void update_estimators(const Ctx &c, ThreadCache &tc, Est &E, const artis_packet *p, double distance) {
   const int mgi = cell_mgi(c, p->where);
@@ -1407,7 +1798,20 @@ void update_estimators(const Ctx &c, ThreadCache &tc, Est &E, const artis_packet
   const double nu = p->nu_cmf;
   safeadd(&E.e->J[mgi], distance_e_cmf);
   safeadd(&E.e->nuJ[mgi], distance_e_cmf * nu);
+  if (c.rp.detailed_bf_estimators) update_bfestimators(c, tc, E, mgi, distance_e_cmf, nu, p);
+  if (c.rp.multibin_radfield) {
+    const int binindex = select_bin(c, nu);
+    if (binindex >= 0) {
+      const size_t mb = (size_t)mgi * c.at->radfield_nbins + binindex;
+      safeadd(&E.e->radfield_J_raw[mb], distance_e_cmf);
+      safeadd(&E.e->radfield_nuJ_raw[mb], distance_e_cmf * nu);
+#pragma omp atomic update
+      E.e->radfield_contribcount[mb] += 1;
+    }
+  }
   safeadd(&E.e->ffheatingestimator[mgi], distance_e_cmf * tc.kap_ffheating);
+  // the ground-continuum estimators exist unless both NO_LUT_PHOTOION and NO_LUT_BFHEATING (rpkt.cc:573-614)
+  if (c.rp.no_lut_photoion && c.rp.no_lut_bfheating) return;
   const double distance_e_cmf_over_nu = distance_e_cmf / nu;
   const artis_atomic_tables &a = *c.at;
   for (int i = 0; i < a.nbfcontinua_ground; i++) {
@@ -1417,8 +1821,10 @@ void update_estimators(const Ctx &c, ThreadCache &tc, Est &E, const artis_packet
       if (c.cs->elem_abundance[(size_t)mgi * a.nelements + element] > 0) {
         const int ion = a.groundcont_ion[i];
         const size_t idx = (size_t)mgi * E.nelements * E.maxnions + element * E.maxnions + ion;
-        safeadd(&E.e->gammaestimator[idx], tc.groundcont_gamma_contr[i] * distance_e_cmf_over_nu);
-        safeadd(&E.e->bfheatingestimator[idx], tc.groundcont_gamma_contr[i] * distance_e_cmf * (1. - nu_edge / nu));
+        if (!c.rp.no_lut_photoion)
+          safeadd(&E.e->gammaestimator[idx], tc.groundcont_gamma_contr[i] * distance_e_cmf_over_nu);
+        if (!c.rp.no_lut_bfheating)
+          safeadd(&E.e->bfheatingestimator[idx], tc.groundcont_gamma_contr[i] * distance_e_cmf * (1. - nu_edge / nu));
         tc.work[WK_GC_UPDATES]++;
       }
     } else {
@@ -1572,6 +1978,7 @@ bool do_rpkt_step(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
     // (the reference uses whatever its thread computed last, rpkt.cc:583, 1166)
     tc.kap_total = tc.kap_es = tc.kap_ff = tc.kap_bf = tc.kap_ffheating = 0.;
     std::fill(tc.groundcont_gamma_contr.begin(), tc.groundcont_gamma_contr.end(), 0.);
+    std::fill(tc.gamma_contr.begin(), tc.gamma_contr.end(), 0.);
     const double kappa = c.cs->kappagrey[mgi] * c.cs->rho[mgi] * doppler_packet_nucmf_on_nurf(c, p);
     edist = (tau_next - 0.0) / kappa;
     find_nextline = true;
@@ -1622,6 +2029,85 @@ bool do_rpkt_step(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
   }
   fprintf(stderr, "oracle: [fatal] do_rpkt: Failed to identify event. edist %g, sdist %g, tdist %g pkt %d\n", edist,
           sdist, tdist, p->number);
+  abort();
+}
+
+// --------------------------------------------------------------------------------------- non-thermal ionisation
+// nonthermal.cc:1640-1655
+int nt_ionisation_maxupperion(const Ctx &c, int e, int lowerion) {
+  const int nions = get_nions(c, e);
+  int maxupper = lowerion + 1;
+  if (c.rp.nt_solve_spencerfano) maxupper = lowerion + 1 + c.rp.nt_max_auger_electrons;
+  if (maxupper > nions - 1) maxupper = nions - 1;
+  return maxupper;
+}
+// nonthermal.cc:1584-1635 (prob_num_auger / ionenfrac_num_auger of the cell's Spencer-Fano solution)
+double nt_ionization_upperion_probability(const Ctx &c, int mgi, int e, int lowerion, int upperion, bool energyweighted) {
+  const int A = c.rp.nt_max_auger_electrons;
+  if (c.rp.nt_solve_spencerfano && A > 0) {
+    const int numaugerelec = upperion - lowerion - 1;
+    const size_t base = ((size_t)mgi * c.at->nions_total + uion(c, e, lowerion)) * (A + 1);
+    const float *tab = energyweighted ? c.cs->nt_ionenfrac_num_auger : c.cs->nt_prob_num_auger;
+    if (numaugerelec < A) return tab[base + numaugerelec];
+    if (numaugerelec == A) {
+      double prob_remaining = 1.;
+      for (int k = 0; k < A; k++) prob_remaining -= tab[base + k];
+      return prob_remaining;
+    }
+    return 0.;
+  }
+  return (upperion == lowerion + 1) ? 1.0 : 0.;
+}
+// nonthermal.cc:1657-1682
+int nt_random_upperion(const Ctx &c, artis_rng *rng, int mgi, int e, int lowerion, bool energyweighted) {
+  if (c.rp.nt_solve_spencerfano && c.rp.nt_max_auger_electrons > 0) {
+    for (int attempt = 0; attempt < 1000; attempt++) {
+      const double zrand = artis_rng_uniform(rng);
+      double prob_sum = 0.;
+      for (int upperion = lowerion + 1; upperion <= nt_ionisation_maxupperion(c, e, lowerion); upperion++) {
+        prob_sum += nt_ionization_upperion_probability(c, mgi, e, lowerion, upperion, energyweighted);
+        if (zrand <= prob_sum) return upperion;
+      }
+    }
+    fprintf(stderr, "oracle: nt_random_upperion: probabilities do not sum to one\n");
+    abort();
+  }
+  return lowerion + 1;
+}
+// nonthermal.cc:1827-1845
+double ion_ntion_energyrate(const Ctx &c, int mgi, int e, int lowerion) {
+  const double nnlowerion = ionstagepop(c, mgi, e, lowerion);
+  double enrate = 0.;
+  for (int upperion = lowerion + 1; upperion <= nt_ionisation_maxupperion(c, e, lowerion); upperion++) {
+    const double upperionprobfrac = nt_ionization_upperion_probability(c, mgi, e, lowerion, upperion, false);
+    const double epsilon_trans = epsilon(c, e, upperion, 0) - epsilon(c, e, lowerion, 0);
+    enrate += nnlowerion * upperionprobfrac * epsilon_trans;
+  }
+  const double gamma_nt = c.cs->nt_ionization_ratecoeff[(size_t)mgi * c.at->nions_total + uion(c, e, lowerion)];
+  return gamma_nt * enrate;
+}
+// nonthermal.cc:1847-1856
+double get_ntion_energyrate(const Ctx &c, int mgi) {
+  double ratetotal = 0.;
+  for (int e = 0; e < c.at->nelements; e++)
+    for (int lowerion = 0; lowerion < get_nions(c, e) - 1; lowerion++) ratetotal += ion_ntion_energyrate(c, mgi, e, lowerion);
+  return ratetotal;
+}
+// nonthermal.cc:1858-1875
+void select_nt_ionization2(const Ctx &c, artis_rng *rng, int mgi, int *element, int *lowerion) {
+  const double ratetotal = get_ntion_energyrate(c, mgi);
+  const double zrand = artis_rng_uniform(rng);
+  double ratesum = 0.;
+  for (int e = 0; e < c.at->nelements; e++)
+    for (int li = 0; li < get_nions(c, e) - 1; li++) {
+      ratesum += ion_ntion_energyrate(c, mgi, e, li);
+      if (ratesum >= zrand * ratetotal) {
+        *element = e;
+        *lowerion = li;
+        return;
+      }
+    }
+  fprintf(stderr, "oracle: select_nt_ionization2 failed\n");
   abort();
 }
 
@@ -1694,6 +2180,9 @@ void calculate_macroatom_transitionrates(const Ctx &c, ThreadCache &tc, int mgi,
   processrates[ARTIS_MA_ACTION_INTERNALUPHIGHER] = 0.;
   const int ionisinglevels = get_ionisinglevels(c, e, i);
   if (i < get_nions(c, e) - 1 && l < ionisinglevels) {
+    if (c.rp.nt_on)  // macroatom.cc:143-146, nonthermal.cc:1684-1712 (the host's nt_ionization_ratecoeff)
+      processrates[ARTIS_MA_ACTION_INTERNALUPHIGHERNT] =
+          c.cs->nt_ionization_ratecoeff[(size_t)mgi * a.nions_total + uion(c, e, i)] * epsilon_current;
     for (int t = 0; t < get_nphixstargets(c, e, i, l); t++) {
       const double epsilon_trans = get_phixs_threshold(c, e, i, l, t);
       const double R = get_corrphotoioncoeff(c, tc, e, i, l, t, mgi);
@@ -1929,6 +2418,14 @@ void do_macroatom(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
         }
         ion += 1;
         level = upper;
+        break;
+      }
+      case ARTIS_MA_ACTION_INTERNALUPHIGHERNT: {
+        // macroatom.cc:866-884
+        p->interactions += 1;
+        ion = nt_random_upperion(c, rng, mgi, element, ion, false);
+        level = 0;
+        counter_inc(E, CTR_MA_STAT_INTERNALUPHIGHERNT);
         break;
       }
       default: {
@@ -2606,9 +3103,33 @@ void update_pellet(const Ctx &c, Est &E, artis_rng *rng, artis_packet *p, int nt
   }
 }
 
-// nonthermal.cc:1877-1977 with NT_SOLVE_SPENCERFANO off (classic / kilonova-LTE options): straight to a k-packet
-void do_ntlepton(Est &E, artis_packet *p) {
+// nonthermal.cc:1877-1977 (NT_EXCITATION_ON false): with NT_ON && NT_SOLVE_SPENCERFANO outside thick cells a
+// fraction frac_ionization of the deposition activates a macro-atom by non-thermal ionisation; the rest (and
+// every deposition under the classic / kilonova-LTE options) becomes a k-packet
+void do_ntlepton(const Ctx &c, Est &E, artis_rng *rng, artis_packet *p) {
   safeadd(&E.e->nt_energy_deposited, p->e_cmf);
+  const int mgi = cell_mgi(c, p->where);
+  if (c.rp.nt_on && c.rp.nt_solve_spencerfano && c.cs->thick[mgi] != 1) {
+    const double zrand = artis_rng_uniform(rng);
+    const double frac_ionization = get_ntion_energyrate(c, mgi) / c.cs->nt_deposition_rate_density[mgi];
+    if (zrand < frac_ionization) {
+      int element = -1, lowerion = -1;
+      select_nt_ionization2(c, rng, mgi, &element, &lowerion);
+      const int upperion = nt_random_upperion(c, rng, mgi, element, lowerion, true);
+      p->mastate.element = element;
+      p->mastate.ion = upperion;
+      p->mastate.level = 0;
+      p->mastate.activatingline = -99;
+      p->type = ARTIS_TYPE_MA;
+      counter_inc(E, CTR_MA_STAT_ACTIVATION_NTCOLLION);
+      p->interactions += 1;
+      p->last_event = 20;
+      p->trueemissiontype = -1;
+      p->trueemissionvelocity = -1;
+      counter_inc(E, CTR_NT_STAT_TO_IONIZATION);
+      return;
+    }
+  }
   p->last_event = 22;
   p->type = ARTIS_TYPE_KPKT;
   counter_inc(E, CTR_NT_STAT_TO_KPKT);
@@ -2658,8 +3179,7 @@ int do_packet(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_packe
       do_nonthermal_predeposit(c, E, rng, p, t2);
       return 0;
     case ARTIS_TYPE_NTLEPTON:
-      if (c.rp.nt_solve_spencerfano) return ARTIS_ERR_UNSUPPORTED;
-      do_ntlepton(E, p);
+      do_ntlepton(c, E, rng, p);
       return 0;
     default:
       return ARTIS_ERR_UNSUPPORTED;
@@ -2710,6 +3230,23 @@ int update_packets_impl(const artis_atomic_tables *at, const artis_geometry *geo
                         artis_packet *packets, int npkts, artis_estimators *est, int64_t work_out[ARTIS_WORK_COUNT],
                         int nthreads);
 
+// the arrays the nebular options read must be present
+int check_nebular_inputs(const artis_atomic_tables *at, const artis_cell_state *cs, const artis_run_params *rp,
+                         const artis_estimators *est) {
+  if (rp->nlte_pops_on && (!at->ion_nlevels_nlte || !at->ion_first_nlte || !cs->nlte_pops)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (rp->multibin_radfield && (at->radfield_nbins <= 0 || !at->radfield_nu_upper || !cs->radfield_bin_TR ||
+                                !cs->radfield_bin_W || !est->radfield_J_raw || !est->radfield_nuJ_raw ||
+                                !est->radfield_contribcount))
+    return ARTIS_ERR_BAD_ARGUMENT;
+  if (rp->detailed_bf_estimators && (!cs->bfrate_estimator || !est->bfrate_raw)) return ARTIS_ERR_BAD_ARGUMENT;
+  if (rp->nt_on && !cs->nt_ionization_ratecoeff) return ARTIS_ERR_BAD_ARGUMENT;
+  if (rp->nt_on && rp->nt_solve_spencerfano &&
+      (!cs->nt_deposition_rate_density || (rp->nt_max_auger_electrons > 0 &&
+                                           (!cs->nt_prob_num_auger || !cs->nt_ionenfrac_num_auger))))
+    return ARTIS_ERR_BAD_ARGUMENT;
+  return 0;
+}
+
 }  // namespace
 
 // ================================================================================================== C ABI
@@ -2752,6 +3289,20 @@ int update_packets_impl(const artis_atomic_tables *at, const artis_geometry *geo
   c.gs = gs;
   c.vp = vp;
   c.T_step_log = (log(at->maxtemp) - log(at->mintemp)) / (at->tablesize - 1.);
+  c.nts = nts;
+  c.minpop = rp->minpop > 0. ? rp->minpop : 1e-30;
+  if (int rc = check_nebular_inputs(at, cs, rp, est)) return rc;
+  {
+    // get_bfcontindex (radfield.cc:1329-1341): the allcont entry of each photoionisation target
+    int64_t ntg = 0;
+    for (int lv = 0; lv < at->nlevels_total; lv++) ntg += at->level_nphixstargets[lv];
+    c.slot_allcont.assign(ntg + 1, -1);
+    for (int ib = 0; ib < at->nbfcontinua; ib++) {
+      const int ul = at->ion_uniqueleveloffset[at->elem_uniqueionoffset[at->allcont_element[ib]] + at->allcont_ion[ib]] +
+                     at->allcont_level[ib];
+      c.slot_allcont[at->level_phixstargets_offset[ul] + at->allcont_phixstargetindex[ib]] = ib;
+    }
+  }
   Est E;
   E.e = est;
   E.nelements = at->nelements;
@@ -2781,6 +3332,7 @@ int update_packets_impl(const artis_atomic_tables *at, const artis_geometry *geo
     tc.cooling_contrib.assign(at->ncoolingterms, -99.);
     tc.kappa_bf_sum.assign(at->nbfcontinua, 0.);
     tc.groundcont_gamma_contr.assign(at->nbfcontinua_ground, 0.);
+    tc.gamma_contr.assign(at->nbfcontinua, 0.);
 #pragma omp for schedule(dynamic, 16)
     for (int n = 0; n < npkts; n++) {
       artis_packet *p = &packets[n];
@@ -2826,7 +3378,106 @@ int oracle_update_packets(const artis_atomic_tables *at, const artis_geometry *g
   return oracle_update_packets_g(at, geom, cs, rp, nullptr, nts, packets, npkts, est, work_out, nthreads);
 }
 
-int oracle_abi_version(void) { return 3; }
+int oracle_abi_version(void) { return 4; }
+
+// Checks of the gsl_integration_qag restatement on integrals with closed forms: fn 0 x^2, 1 exp(x), 2 sqrt(x),
+// 3 a step (1 below 0.3, 2 above), 4 1/sqrt(x).  Returns the integral; *status the GSL status.
+double oracle_qag61_test(int fn, double a, double b, double epsrel, int *status, double *abserr) {
+  auto f = [fn](double x) -> double {
+    switch (fn) {
+      case 0: return x * x;
+      case 1: return exp(x);
+      case 2: return sqrt(x);
+      case 3: return x < 0.3 ? 1. : 2.;
+      default: return 1. / sqrt(x);
+    }
+  };
+  GslWorkspace ws(kGslWsSize);
+  double result = 0., err = 0.;
+  const int st = gsl_qag61(f, a, b, 0., epsrel, kGslWsSize, ws, &result, &err);
+  if (status) *status = st;
+  if (abserr) *abserr = err;
+  return result;
+}
+
+// get_corrphotoioncoeff of model cell mgi, unique level ul, target t at timestep nts (the oracle's
+// NO_LUT_PHOTOION integral or estimator, as the macro-atom sees it); brute != 0: the same integrand summed by
+// composite 8-point Gauss-Legendre over 4096 pieces per radiation-field bin crossing -- a quadrature check
+double oracle_corrphotoioncoeff(const artis_atomic_tables *at, const artis_geometry *geom, const artis_cell_state *cs,
+                                const artis_run_params *rp, int nts, int mgi, int ul, int t, int brute) {
+  Ctx c;
+  c.at = at;
+  c.g = geom;
+  c.cs = cs;
+  c.rp = *rp;
+  c.gs = nullptr;
+  c.T_step_log = (log(at->maxtemp) - log(at->mintemp)) / (at->tablesize - 1.);
+  c.nts = nts;
+  c.minpop = rp->minpop > 0. ? rp->minpop : 1e-30;
+  int64_t ntg = 0;
+  for (int lv = 0; lv < at->nlevels_total; lv++) ntg += at->level_nphixstargets[lv];
+  c.slot_allcont.assign(ntg + 1, -1);
+  for (int ib = 0; ib < at->nbfcontinua; ib++) {
+    const int u = at->ion_uniqueleveloffset[at->elem_uniqueionoffset[at->allcont_element[ib]] + at->allcont_ion[ib]] +
+                  at->allcont_level[ib];
+    c.slot_allcont[at->level_phixstargets_offset[u] + at->allcont_phixstargetindex[ib]] = ib;
+  }
+  ThreadCache tc;
+  tc.pops.assign(at->nlevels_total, 0.);
+  tc.departureratios.assign(at->nbfcontinua, -1.);
+  tc.processrates.assign((size_t)at->nlevels_total * 9, -99.);
+  tc.corrphotoioncoeff.assign(ntg + 1, -99.);
+  tc.cooling_contrib.assign(at->ncoolingterms, -99.);
+  cellhistory_reset(c, tc, mgi);
+  int e = 0;
+  while (e + 1 < at->nelements && at->ion_uniqueleveloffset[at->elem_uniqueionoffset[e + 1]] <= ul) e++;
+  int i = 0;
+  while (i + 1 < at->elem_nions[e] && at->ion_uniqueleveloffset[at->elem_uniqueionoffset[e] + i + 1] <= ul) i++;
+  const int l = ul - at->ion_uniqueleveloffset[at->elem_uniqueionoffset[e] + i];
+  if (!brute) return get_corrphotoioncoeff(c, tc, e, i, l, t, mgi);
+  // brute-force quadrature of the same integrand
+  const double nu_threshold = ARTIS_ONEOVERH * get_phixs_threshold(c, e, i, l, t);
+  const double nu_max_phixs = nu_threshold * at->last_phixs_nuovernuedge;
+  const float T_e = cs->Te[mgi];
+  const double nnlevel = get_levelpop(tc, c, e, i, l);
+  const int upper = get_phixsupperlevel(c, e, i, l, t);
+  const double sf = calculate_sahafact(c, e, i, l, upper, T_e, ARTIS_H * nu_threshold);
+  double departure_ratio = nnlevel > 0. ? get_levelpop(tc, c, e, i + 1, upper) / nnlevel * cs->nne[mgi] * sf : 1.0;
+  if (!std::isfinite(departure_ratio)) departure_ratio = 0.;
+  const float *xs = level_photoion_xs(c, e, i, l);
+  auto f = [&](double nu) {
+    double corrfactor = 1. - departure_ratio * exp(-ARTIS_HOVERKB * nu / T_e);
+    if (corrfactor < 0) corrfactor = 0.;
+    const float sigma_bf = (float)photoionization_crosssection_fromtable(c, xs, nu_threshold, nu);
+    return ARTIS_ONEOVERH * sigma_bf / nu * radfield(c, nu, mgi) * corrfactor;
+  };
+  // breakpoints: the phixs table nodes and the radiation-field bin edges inside the range
+  std::vector<double> br = {nu_threshold, nu_max_phixs};
+  for (int k = 1; k < at->nphixspoints; k++) {
+    const double x = nu_threshold * (1. + k * at->nphixsnuincrement);
+    if (x < nu_max_phixs) br.push_back(x);
+  }
+  if (rp->multibin_radfield)
+    for (int b = -1; b < at->radfield_nbins; b++) {
+      const double x = b < 0 ? at->radfield_nu_lower_first : at->radfield_nu_upper[b];
+      if (x > nu_threshold && x < nu_max_phixs) br.push_back(x);
+    }
+  std::sort(br.begin(), br.end());
+  static const double gx[8] = {-0.9602898564975363, -0.7966664774136267, -0.5255324099163290, -0.1834346424956498,
+                               0.1834346424956498,  0.5255324099163290,  0.7966664774136267,  0.9602898564975363};
+  static const double gw[8] = {0.1012285362903763, 0.2223810344533745, 0.3137066458778873, 0.3626837833783620,
+                               0.3626837833783620, 0.3137066458778873, 0.2223810344533745, 0.1012285362903763};
+  double sum = 0.;
+  for (size_t s0 = 0; s0 + 1 < br.size(); s0++) {
+    const int npc = 64;
+    const double h = (br[s0 + 1] - br[s0]) / npc;
+    for (int p = 0; p < npc; p++) {
+      const double mid = br[s0] + (p + 0.5) * h;
+      for (int q = 0; q < 8; q++) sum += gw[q] * 0.5 * h * f(mid + 0.5 * h * gx[q]);
+    }
+  }
+  return sum * ARTIS_FOURPI * get_phixsprobability(c, e, i, l, t);
+}
 
 // ---- unit hooks for tests/ ---------------------------------------------------------------------------------
 // Philox4x32-10 block (known-answer tests against the published Random123 vectors)

@@ -32,6 +32,12 @@ def lib():
                                               C.c_int, C.c_void_p, C.c_int, C.POINTER(ffi.Estimators), C.c_void_p,
                                               C.c_int]
         L.oracle_update_packets_v.restype = C.c_int
+        L.oracle_qag61_test.argtypes = [C.c_int, C.c_double, C.c_double, C.c_double, C.POINTER(C.c_int),
+                                        C.POINTER(C.c_double)]
+        L.oracle_qag61_test.restype = C.c_double
+        L.oracle_corrphotoioncoeff.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(ffi.RunParams)] + \
+            [C.c_int] * 5
+        L.oracle_corrphotoioncoeff.restype = C.c_double
         _lib = L
     return _lib
 
@@ -82,3 +88,17 @@ def spectrum(model, packets, nnubins=1000, nprocs=1):
     if rc != 0:
         raise RuntimeError("oracle_spectrum: frequency bin out of range")
     return spec, lc, lccmf
+
+
+def qag61_test(fn, a, b, epsrel):
+    """The oracle's gsl_integration_qag(GAUSS61) restatement on closed-form test integrands."""
+    st, err = C.c_int(), C.c_double()
+    r = lib().oracle_qag61_test(fn, a, b, epsrel, C.byref(st), C.byref(err))
+    return r, st.value, err.value
+
+
+def corrphotoioncoeff(model, nts, mgi, ul, t, brute=False, params=None):
+    """get_corrphotoioncoeff as the oracle's macro-atom sees it (brute: dense-quadrature check of the integral)."""
+    p = params if params is not None else model.params
+    return lib().oracle_corrphotoioncoeff(model.atomic, model.geometry, model.cellstate, C.byref(p),
+                                          int(nts), int(mgi), int(ul), int(t), int(brute))

@@ -98,6 +98,15 @@ def assert_estimators_match(eg, eo, exact_counts=True, rtol=ESTIMATOR_RTOL):
                  "alpha_emission", "gamma_emission", "nt_energy_deposited"):
         x, y = getattr(eg.struct, name), getattr(eo.struct, name)
         assert abs(x - y) <= rtol * max(abs(y), 1e-300), (name, x, y)
+    # nebular estimators (DETAILED_BF_ESTIMATORS_ON / MULTIBIN_RADFIELD_MODEL_ON); bin contribution counts exact
+    for name in ("bfrate_raw", "radfield_J", "radfield_nuJ"):
+        x, y = getattr(eg, name, np.zeros(0)), getattr(eo, name, np.zeros(0))
+        assert x.shape == y.shape, name
+        if y.size:
+            scale = max(np.abs(y).max(), 1e-300)
+            assert np.abs(x - y).max() <= rtol * scale, (name, np.abs(x - y).max() / scale)
+    if exact_counts and getattr(eo, "radfield_count", np.zeros(0)).size:
+        assert np.array_equal(eg.radfield_count, eo.radfield_count)
     if exact_counts:
         assert eg.struct.nesc == eo.struct.nesc
         assert eg.struct.pellet_decays == eo.struct.pellet_decays

@@ -130,3 +130,29 @@ def test_block_layout_is_the_device_layout():
     assert np.array_equal(b, expect.astype(np.float64))
     back = adist.unpack_estimators(b, ffi.EstimatorArrays(np_, ne, mi, nl))
     assert np.array_equal(adist.pack_estimators(back), b)
+
+
+def test_block_layout_with_nebular_sections():
+    """DETAILED_BF_ESTIMATORS_ON / MULTIBIN_RADFIELD_MODEL_ON: bfrate_raw and the radiation-field bin estimators
+    (contribcount carried as float64) sit after the scalars, before the line counters."""
+    from artis_amd import ffi
+
+    np_, ne, mi, nl, nbf, nbins = 2, 1, 3, 4, 5, 6
+    est = ffi.EstimatorArrays(np_, ne, mi, nl, nbf, nbins)
+    est.J[:] = 1
+    est.bfrate_raw[:] = np.arange(np_ * nbf) + 0.5
+    est.radfield_J[:] = 7
+    est.radfield_nuJ[:] = 8
+    est.radfield_count[:] = np.arange(np_ * nbins) + 1000
+    est.ecounter[:] = 21
+    b = adist.pack_estimators(est)
+    assert len(b) == adist.block_len(np_, ne, mi, nl, nbf, nbins)
+    off = 5 * np_ + 2 * np_ * ne * mi + 10
+    assert np.array_equal(b[off:off + np_ * nbf], est.bfrate_raw)
+    off += np_ * nbf
+    assert np.all(b[off:off + np_ * nbins] == 7) and np.all(b[off + np_ * nbins:off + 2 * np_ * nbins] == 8)
+    assert np.array_equal(b[off + 2 * np_ * nbins:off + 3 * np_ * nbins], est.radfield_count.astype(np.float64))
+    assert np.all(b[off + 3 * np_ * nbins:off + 3 * np_ * nbins + nl] == 21)
+    back = adist.unpack_estimators(b, ffi.EstimatorArrays(np_, ne, mi, nl, nbf, nbins))
+    assert np.array_equal(back.radfield_count, est.radfield_count)
+    assert np.array_equal(adist.pack_estimators(back), b)

@@ -1,0 +1,118 @@
+"""The nebular options (artisoptions_nltenebular.h) on the CPU oracle: the gsl_integration_qag restatement behind
+NO_LUT_PHOTOION, the corrected photoionisation integral against dense quadrature, and the bookkeeping of a nebular
+run (NLTE / superlevel populations, binned radiation field, detailed bf estimators, non-thermal ionisation).
+
+Parity unpinned for these rows: the reference's nebular test (tests/nebularonezone_inputfiles) compares md5 sums of
+whole-run outputs made with a downloaded atomic dataset; the checks here are closed forms, an independent
+quadrature and conservation properties.  CPU only.
+"""
+import copy
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from artis_amd import ffi
+from artis_amd.model import Model
+
+REF = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_inputs")
+NEB = dict(ngrid_1d=4, nlevels_per_ion=30, n_ionising=10, max_lines=2000, ntstep=20, nebular=1, nlte_level_max=12,
+           tmin_days=100., tmax_days=300., T0=6000., ionpot_scale=0.5)
+
+
+@pytest.mark.parametrize("fn,a,b,exact", [(0, 0., 1., 1. / 3.), (1, 0., 2., np.exp(2.) - 1.), (2, 0., 1., 2. / 3.),
+                                          (3, 0., 1., 1.7), (4, 0., 1., 2.)])
+def test_qag61_closed_forms(fn, a, b, exact):
+    """GK61 integrates polynomials to degree 91 exactly in one step (status 0); the adaptive bisection reaches
+    epsrel on a kink (sqrt), a jump and an integrable singularity."""
+    r, st, err = oracle_lib.qag61_test(fn, a, b, 1e-10)
+    assert st == 0
+    assert abs(r - exact) <= 1e-10 * abs(exact)
+    assert err <= 1e-10 * abs(r)
+    r3, st3, _ = oracle_lib.qag61_test(3, 0., 1., 1e-3)
+    assert st3 == 0 and abs(r3 - 1.7) <= 1e-3 * 1.7
+
+
+@pytest.fixture(scope="module")
+def neb():
+    return Model(**NEB)
+
+
+@pytest.mark.parametrize("nts", [5, 14])
+def test_corrphot_integral_matches_dense_quadrature(neb, nts):
+    """calculate_corrphotoioncoeff_integral (ratecoeff.cc:1184-1245) against 8-point Gauss-Legendre on 64 pieces
+    between every phixs node / radiation-field bin edge: within the reference's epsrel 1e-3."""
+    neb.set_timestep(nts)
+    p = copy.copy(neb.params)
+    p.detailed_bf_usefromtimestep = 99  # the integral, not the estimator
+    n = 0
+    for ul in range(0, 60, 3):  # ionising levels of the first ions (n_ionising = 10 of 30 per ion)
+        for mgi in (0, 5):
+            a = oracle_lib.corrphotoioncoeff(neb, nts, mgi, ul, 0, params=p)
+            b = oracle_lib.corrphotoioncoeff(neb, nts, mgi, ul, 0, brute=True, params=p)
+            assert abs(a - b) <= 1e-3 * abs(b) + 1e-300, (ul, mgi, a, b)
+            n += b > 0
+    assert n > 5
+
+
+def test_corrphot_uses_bfrate_estimator_from_usefromtimestep(neb):
+    """get_corrphotoioncoeff (ratecoeff.cc:1255-1261): from DETAILED_BF_ESTIMATORS_USEFROMTIMESTEP a positive
+    estimator replaces the integral."""
+    neb.set_timestep(14)
+    p = copy.copy(neb.params)
+    p.detailed_bf_usefromtimestep = 99
+    differs = 0
+    for ul in range(0, 60, 3):
+        a = oracle_lib.corrphotoioncoeff(neb, 14, 5, ul, 0)  # model cell 5: inside the ejecta
+        b = oracle_lib.corrphotoioncoeff(neb, 14, 5, ul, 0, params=p)
+        differs += a != b
+    assert differs > 3
+
+
+@pytest.mark.parametrize("nts", [5, 14])
+def test_nebular_rpacket_bookkeeping(neb, nts):
+    neb.set_timestep(nts)
+    pk = neb.init_rpackets(nts, 1500, seed=3)
+    est, work = oracle_lib.update_packets(neb, nts, pk, nthreads=8)
+    esc = pk["type"] == ffi.TYPE_ESCAPE
+    assert est.struct.nesc == esc.sum()
+    assert np.isclose(est.struct.cmf_lum, pk["e_cmf"][esc].sum(), rtol=1e-12)
+    c = est.counters
+    # macro-atom activations == deactivations (stats.h)
+    assert c[0] + c[1] + c[2] + c[3] + c[4] + c[5] == c[7] + c[8] + c[9] + c[10]
+    # NO_LUT_PHOTOION && NO_LUT_BFHEATING: no ground-continuum estimators (rpkt.cc:573-614)
+    assert not est.gamma.any() and not est.bfheating.any()
+    # the bin estimators see every segment whose nu_cmf lies inside the bins
+    assert est.radfield_count.sum() > 0
+    assert est.radfield_J.sum() <= est.J.sum() * (1 + 1e-12)
+    if nts >= 12:
+        assert est.bfrate_raw.sum() > 0
+
+
+def test_nebular_ntlepton_ionisation():
+    """do_ntlepton with the Spencer-Fano solution (nonthermal.cc:1877-1977): leptons activate macro-atoms by
+    non-thermal ionisation (NT_STAT_TO_IONIZATION == MA activations NTCOLLION) or become k-packets."""
+    m = Model(**NEB)
+    m.set_timestep(0)
+    pe = m.init_pellets(4000, seed=5)
+    est, _ = oracle_lib.update_packets(m, 0, pe, nthreads=8)
+    c = est.counters
+    assert c[22] > 0 and c[22] == c[3] and c[24] > 0
+    assert est.struct.nt_energy_deposited > 0
+
+
+def test_nebularonezone_reference_model():
+    """tests/nebularonezone_inputfiles: the one-zone model (input-newrun.txt, model.txt, abundances.txt) with the
+    nebular options on the oracle."""
+    d = os.path.join(REF, "nebularonezone")
+    m = Model(files=(os.path.join(d, "input-newrun.txt"), os.path.join(d, "model.txt"),
+                     os.path.join(d, "abundances.txt")), ngrid_1d=10, nlevels_per_ion=30, n_ionising=10,
+              max_lines=2000, nebular=1, nlte_level_max=12)
+    assert m.npts_model == 1 and m.params.nlte_pops_on == 1 and m.params.minpop == 1e-40
+    m.set_timestep(5)
+    pk = m.init_rpackets(5, 800, seed=4)
+    est, work = oracle_lib.update_packets(m, 5, pk, nthreads=8)
+    esc = pk["type"] == ffi.TYPE_ESCAPE
+    assert est.struct.nesc == esc.sum()
+    assert work[8] > 0  # macro-atom jumps
