@@ -23,7 +23,7 @@ ABI_SYMBOLS = [
     "artis_gpu_packets_restore", "artis_gpu_update_packets_resident", "artis_gpu_estimators_zero",
     "artis_gpu_estimators_download", "artis_gpu_estimator_block_doubles", "artis_gpu_estimator_block_to_device",
     "artis_gpu_estimator_block_from_device", "artis_gpu_last_transport_ms", "artis_gpu_last_precompute_ms",
-    "artis_gpu_last_work_counts", "artis_gpu_last_rounds", "artis_gpu_spectrum", "artis_gpu_last_kernel_times", "artis_gpu_last_error", "artis_gpu_abi_version",
+    "artis_gpu_last_work_counts", "artis_gpu_last_rounds", "artis_gpu_spectrum", "artis_gpu_spectra", "artis_gpu_last_kernel_times", "artis_gpu_last_error", "artis_gpu_abi_version",
     "artis_gpu_vpkt_init", "artis_gpu_vpkt_zero", "artis_gpu_vpkt_download", "artis_gpu_vpkt_last_stats", "artis_gpu_vpkt_last_work",
     "artis_estimator_block_len", "artis_estimator_block_pack", "artis_estimator_block_unpack",
     "artis_gpu_comm_unique_id", "artis_gpu_comm_init", "artis_gpu_estimators_allreduce", "artis_gpu_comm_finalize",
@@ -73,6 +73,7 @@ def gpu_lib():
         L.artis_gpu_last_error.restype = C.c_char_p
         L.artis_gpu_last_rounds.restype = C.c_int64
         L.artis_gpu_spectrum.argtypes = [C.c_int, C.c_int, vp, vp, vp]
+        L.artis_gpu_spectra.argtypes = [C.POINTER(ffi.SpectraRequest), C.POINTER(ffi.SpectraOut)]
         L.artis_gpu_vpkt_init.argtypes = [C.POINTER(ffi.VpktParams)]
         L.artis_gpu_vpkt_download.argtypes = [C.POINTER(ffi.VpktResult), C.c_int]
         L.artis_gpu_vpkt_last_stats.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
@@ -187,6 +188,16 @@ class Engine:
         self._check(self.lib.artis_gpu_spectrum(int(nnubins), int(nprocs), spec.ctypes.data, lc.ctypes.data,
                                                 lccmf.ctypes.data), "spectrum")
         return spec, lc, lccmf
+
+    def spectra(self, nnubins=1000, nprocs=1, abin=-1, syn_dir=(0., 0., 1.), emission_res=True, stokes=False,
+                out=None):
+        """exspec spectra of the resident packets (artis_gpu_spectra): ADDED into out (ffi.SpectraArrays)."""
+        if out is None:
+            out = ffi.SpectraArrays(self.model.cfg.ntstep, nnubins, self.model.nelements, self.model.maxnions,
+                                    emission_res, stokes)
+        req = ffi.spectra_request(nnubins, nprocs, abin, syn_dir)
+        self._check(self.lib.artis_gpu_spectra(C.byref(req), C.byref(out.struct)), "spectra")
+        return out
 
     # virtual packets (VPKT_ON)
     def vpkt_init(self, cfg):

@@ -523,6 +523,7 @@ struct Engine {
   double *d_nltepops = nullptr, *d_ntdep = nullptr, *d_ntY = nullptr;
   float *d_rfTR = nullptr, *d_rfW = nullptr, *d_bfest = nullptr, *d_ntprob = nullptr, *d_ntionen = nullptr;
   QagWs qag{};
+  int32_t *d_bfcol = nullptr;  // bflist index -> element * maxnions + ion (spectra emission columns)
   int qag_waves = 0;
   int64_t nbf_est = 0, nbins_est = 0;  // nebular estimator sections of the block (0 when off)
   int32_t *d_ne_index = nullptr, *d_ne_mgi = nullptr;
@@ -919,6 +920,12 @@ double artis_gpu_last_transport_ms(void) { return G.last_transport_ms; }
 double artis_gpu_last_precompute_ms(void) { return G.last_precompute_ms; }
 int64_t artis_gpu_last_rounds(void) { return G.last_rounds; }
 
+// init_spectra (spectrum.cc:495-500): lower_freq and delta_freq are float arrays (spectrum.h:18-19), so the
+// bin width every deltaE divides by is the float difference of the float lower edge
+static inline double spec_delta_freq(double nu_min, double dlognu, int nnu) {
+  const float lower_freq = (float)exp(log(nu_min) + (nnu * (dlognu)));
+  return (float)(exp(log(nu_min) + ((nnu + 1) * (dlognu))) - lower_freq);
+}
 int artis_gpu_spectrum(int nnubins, int nprocs, double *spec_flux, double *lc_lum, double *lc_lumcmf) {
   if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
   if (nnubins <= 0 || nprocs <= 0 || !spec_flux || !lc_lum || !lc_lumcmf) return ARTIS_ERR_BAD_ARGUMENT;
@@ -928,7 +935,7 @@ int artis_gpu_spectrum(int nnubins, int nprocs, double *spec_flux, double *lc_lu
   const double dlognu = (log(nu_max) - log(nu_min)) / nnubins;
   std::vector<double> delta(nnubins);
   for (int nnu = 0; nnu < nnubins; nnu++)
-    delta[nnu] = exp(log(nu_min) + ((nnu + 1) * (dlognu))) - exp(log(nu_min) + (nnu * (dlognu)));
+    delta[nnu] = spec_delta_freq(nu_min, dlognu, nnu);
   const size_t nspec = (size_t)nt * nnubins;
   double *d = nullptr;
   HIPCHK(dmalloc((void **)&d, (nspec + 2 * (size_t)nt + nnubins) * sizeof(double)));
@@ -953,6 +960,98 @@ int artis_gpu_spectrum(int nnubins, int nprocs, double *spec_flux, double *lc_lu
   (void)hipFree(d);
   return rc;
 }
+int artis_gpu_spectra(const artis_spectra_request *req, artis_spectra_out *out) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  if (!req || !out || req->nnubins <= 0 || req->nprocs <= 0 || req->abin < -1 || req->abin >= ARTIS_MABINS ||
+      (!out->emission != !out->absorption) || (out->trueemission && !out->emission) ||
+      ((out->stokes_emission || out->stokes_absorption) && !out->emission)) {
+    G.last_error = "spectra: bad request (nnubins, nprocs, abin) or inconsistent emission/absorption arrays";
+    return ARTIS_ERR_BAD_ARGUMENT;
+  }
+  const int nt = G.ntstep, nnb = req->nnubins;
+  const int ioncount = G.nelements * G.maxnions, proccount = 2 * ioncount + 1;
+  const double nu_min = G.K.G.nu_min_r, nu_max = G.K.G.nu_max_r;
+  const double dlognu = (log(nu_max) - log(nu_min)) / nnb;  // spectrum.cc:352, 491-500 (host libm)
+  std::vector<double> delta(nnb);
+  for (int nnu = 0; nnu < nnb; nnu++)
+    delta[nnu] = spec_delta_freq(nu_min, dlognu, nnu);
+  const size_t nb = (size_t)nt * nnb;
+  // device accumulators, in the order of the sections below
+  struct Sec {
+    double *host;
+    size_t n;
+  } secs[] = {{out->flux, nb},
+              {out->emission, nb * proccount},
+              {out->trueemission, nb * proccount},
+              {out->absorption, nb * ioncount},
+              {out->stokes_flux, 3 * nb},
+              {out->stokes_emission, 3 * nb * proccount},
+              {out->stokes_absorption, 3 * nb * ioncount},
+              {out->lc_lum, (size_t)nt},
+              {out->lc_lumcmf, (size_t)nt},
+              {out->gamma_lc_lum, (size_t)nt},
+              {out->gamma_lc_lumcmf, (size_t)nt}};
+  constexpr int NSEC = sizeof(secs) / sizeof(secs[0]);
+  size_t total = nnb;  // delta_freq first
+  for (const Sec &x : secs)
+    if (x.host) total += x.n;
+  double *d = nullptr;
+  HIPCHK(dmalloc((void **)&d, total * sizeof(double)));
+  double *dptr[NSEC];
+  size_t off = nnb;
+  for (int k = 0; k < NSEC; k++) {
+    dptr[k] = secs[k].host ? d + off : nullptr;
+    if (secs[k].host) off += secs[k].n;
+  }
+  auto run = [&]() -> int {
+    if (int rc = sync_ctx()) return rc;
+    HIPCHK(hipMemsetAsync(d + nnb, 0, (total - nnb) * sizeof(double), G.stream));
+    HIPCHK(hipMemcpyAsync(d, delta.data(), nnb * sizeof(double), hipMemcpyHostToDevice, G.stream));
+    SpecArgs A{};
+    A.nnubins = nnb;
+    A.nprocs = req->nprocs;
+    A.abin = req->abin;
+    A.ntstep = nt;
+    A.proccount = proccount;
+    A.ioncount = ioncount;
+    A.maxnions = G.maxnions;
+    A.nbf = G.K.T.nbf;
+    for (int k = 0; k < 3; k++) A.syn_dir[k] = req->syn_dir[k];
+    A.dlognu = dlognu;
+    A.delta_freq = d;
+    A.bf_col = G.d_bfcol;
+    A.line_elem = G.K.T.line_elem;
+    A.line_ion = G.K.T.line_ion;
+    A.flux = dptr[0];
+    A.emission = dptr[1];
+    A.trueemission = dptr[2];
+    A.absorption = dptr[3];
+    A.sflux = dptr[4];
+    A.semission = dptr[5];
+    A.sabsorption = dptr[6];
+    A.lc = dptr[7];
+    A.lccmf = dptr[8];
+    A.glc = dptr[9];
+    A.glccmf = dptr[10];
+    if (G.npkts > 0)
+      k_spectra<<<(unsigned)((G.npkts + 255) / 256), 256, 0, G.stream>>>(G.d_ctx, G.d_soa, G.npkts, A);
+    HIPCHK(hipGetLastError());
+    std::vector<double> h;
+    for (int k = 0; k < NSEC; k++) {
+      if (!secs[k].host) continue;
+      h.resize(secs[k].n);
+      HIPCHK(hipMemcpyAsync(h.data(), dptr[k], secs[k].n * sizeof(double), hipMemcpyDeviceToHost, G.stream));
+      HIPCHK(hipStreamSynchronize(G.stream));
+      for (size_t j = 0; j < secs[k].n; j++) secs[k].host[j] += h[j];
+    }
+    return 0;
+  };
+  const int rc = run();
+  (void)hipStreamSynchronize(G.stream);
+  (void)hipFree(d);
+  return rc;
+}
+
 int artis_gpu_vpkt_init(const artis_vpkt_params *vp) {
   if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
   if (!vp || vp->nobs <= 0 || vp->nspectra <= 0 || vp->nspectra > ARTIS_VPKT_MAX_SPECTRA || vp->nrange < 0 ||
@@ -1430,6 +1529,22 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
       sa[a->level_phixstargets_offset[ul] + a->allcont_phixstargetindex[ib]] = ib;
     }
     rc |= dupload(&T.slot_allcont, sa.data(), ntg + 1);
+    // bflist (input.cc:1153-1160: cont_index counts down from -1 over every level's targets) -> ion column
+    std::vector<int32_t> bc(std::max(nb, 1), 0);
+    for (int e = 0; e < ne; e++)
+      for (int i = 0; i < a->elem_nions[e]; i++) {
+        const int ui = a->elem_uniqueionoffset[e] + i;
+        for (int l = 0; l < a->ion_nlevels[ui]; l++) {
+          const int ul = a->ion_uniqueleveloffset[ui] + l;
+          for (int t = 0; t < a->level_nphixstargets[ul]; t++) {
+            const int bi = -1 - (a->level_cont_index[ul] - t);
+            if (bi >= 0 && bi < nb) bc[bi] = e * a->maxnions + i;
+          }
+        }
+      }
+    const int32_t *dbc;
+    rc |= dupload(&dbc, bc.data(), bc.size());
+    G.d_bfcol = const_cast<int32_t *>(dbc);
   }
 
   // estimators: one double block [J | nuJ | ffheat | colheat | rpkt_emiss | gamma | bfheat | scalars(10) |

@@ -554,3 +554,121 @@ int artis_read_vpkt_grid(const char *filename, const artis_vpkt_params *p, artis
 }
 
 }  // extern "C"
+
+// ---- spectra / light curves (spectrum.cc:144-298, light_curve.cc:9-32) ------------------------------------------
+namespace {
+void spec_bins(int nnubins, double nu_min, double nu_max, std::vector<float> &lower, std::vector<float> &delta) {
+  const double dlognu = (log(nu_max) - log(nu_min)) / nnubins;  // spectrum.cc:491-500
+  lower.resize(nnubins);
+  delta.resize(nnubins);
+  for (int nnu = 0; nnu < nnubins; nnu++) {
+    lower[nnu] = (float)exp(log(nu_min) + (nnu * (dlognu)));
+    delta[nnu] = (float)(exp(log(nu_min) + ((nnu + 1) * (dlognu))) - lower[nnu]);
+  }
+}
+struct FileCloser {
+  FILE *f = nullptr;
+  ~FileCloser() {
+    if (f) fclose(f);
+  }
+};
+constexpr double kLsun = 3.826e+33;
+}  // namespace
+
+int artis_write_spectrum(const char *spec_filename, const char *emission_filename, const char *trueemission_filename,
+                         const char *absorption_filename, int ntstep, int numtimesteps, const double *ts_mid,
+                         int nnubins, double nu_min, double nu_max, int proccount, int ioncount, const double *flux,
+                         const double *emission, const double *trueemission, const double *absorption) {
+  if (!spec_filename || !ts_mid || !flux || nnubins <= 0 || numtimesteps > ntstep || numtimesteps < 0) return -1;
+  const bool do_emission_res = emission && trueemission && absorption && emission_filename && trueemission_filename &&
+                               absorption_filename;
+  FileCloser fs, fe, ft, fa;
+  fs.f = fopen(spec_filename, "w");
+  if (!fs.f) return -1;
+  if (do_emission_res) {
+    fe.f = fopen(emission_filename, "w");
+    ft.f = fopen(trueemission_filename, "w");
+    fa.f = fopen(absorption_filename, "w");
+    if (!fe.f || !ft.f || !fa.f) return -1;
+  }
+  std::vector<float> lower, delta;
+  spec_bins(nnubins, nu_min, nu_max, lower, delta);
+  fprintf(fs.f, "%g ", 0.0);
+  for (int p = 0; p < numtimesteps; p++) fprintf(fs.f, "%g ", ts_mid[p] / kDay);
+  fprintf(fs.f, "\n");
+  for (int nnu = 0; nnu < nnubins; nnu++) {
+    fprintf(fs.f, "%g ", (lower[nnu] + (delta[nnu] / 2)));
+    for (int nts = 0; nts < numtimesteps; nts++) {
+      const size_t fi = (size_t)nts * nnubins + nnu;
+      fprintf(fs.f, "%g ", flux[fi]);
+      if (do_emission_res) {
+        for (int i = 0; i < proccount; i++) fprintf(fe.f, "%g ", emission[fi * proccount + i]);
+        fprintf(fe.f, "\n");
+        for (int i = 0; i < proccount; i++) fprintf(ft.f, "%g ", trueemission[fi * proccount + i]);
+        fprintf(ft.f, "\n");
+        for (int i = 0; i < ioncount; i++) fprintf(fa.f, "%g ", absorption[fi * ioncount + i]);
+        fprintf(fa.f, "\n");
+      }
+    }
+    fprintf(fs.f, "\n");
+  }
+  return 0;
+}
+
+int artis_write_specpol(const char *specpol_filename, const char *emission_filename, const char *absorption_filename,
+                        int ntstep, const double *ts_mid, int nnubins, double nu_min, double nu_max, int proccount,
+                        int ioncount, const double *stokes_flux, const double *stokes_emission,
+                        const double *stokes_absorption) {
+  if (!specpol_filename || !ts_mid || !stokes_flux || nnubins <= 0 || ntstep <= 0) return -1;
+  const bool do_emission_res = stokes_emission && stokes_absorption && emission_filename && absorption_filename;
+  FileCloser fs, fe, fa;
+  fs.f = fopen(specpol_filename, "w");
+  if (!fs.f) return -1;
+  if (do_emission_res) {
+    fe.f = fopen(emission_filename, "w");
+    fa.f = fopen(absorption_filename, "w");
+    if (!fe.f || !fa.f) return -1;
+  }
+  std::vector<float> lower, delta;
+  spec_bins(nnubins, nu_min, nu_max, lower, delta);
+  fprintf(fs.f, "%g ", 0.0);
+  for (int l = 0; l < 3; l++)
+    for (int p = 0; p < ntstep; p++) fprintf(fs.f, "%g ", ts_mid[p] / kDay);
+  fprintf(fs.f, "\n");
+  const size_t nb = (size_t)ntstep * nnubins;
+  for (int m = 0; m < nnubins; m++) {
+    fprintf(fs.f, "%g ", (lower[m] + (delta[m] / 2)));
+    for (int k = 0; k < 3; k++) {  // Stokes I, Q, U
+      for (int p = 0; p < ntstep; p++) {
+        const size_t fi = (size_t)p * nnubins + m;
+        fprintf(fs.f, "%g ", stokes_flux[k * nb + fi]);
+        if (do_emission_res) {
+          for (int i = 0; i < proccount; i++) fprintf(fe.f, "%g ", stokes_emission[k * nb * proccount + fi * proccount + i]);
+          fprintf(fe.f, "\n");
+          for (int i = 0; i < ioncount; i++) fprintf(fa.f, "%g ", stokes_absorption[k * nb * ioncount + fi * ioncount + i]);
+          fprintf(fa.f, "\n");
+        }
+      }
+    }
+    fprintf(fs.f, "\n");
+  }
+  return 0;
+}
+
+int artis_write_light_curve(const char *lc_filename, int abin, int numtimesteps, const double *ts_mid,
+                            const double *ts_width, const double *lc_lum, const double *lc_lumcmf,
+                            const double *gamma_dep, const double *cmf_lum) {
+  if (!lc_filename || !ts_mid || !lc_lum || !lc_lumcmf || numtimesteps < 0) return -1;
+  FileCloser f;
+  f.f = fopen(lc_filename, "w");
+  if (!f.f) return -1;
+  for (int nts = 0; nts < numtimesteps; nts++)
+    fprintf(f.f, "%g %g %g\n", ts_mid[nts] / kDay, (lc_lum[nts] / kLsun), (lc_lumcmf[nts] / kLsun));
+  if (abin == -1) {
+    for (int m = 0; m < numtimesteps; m++) {
+      const double gd = gamma_dep ? gamma_dep[m] : 0., cl = cmf_lum ? cmf_lum[m] : 0.;
+      fprintf(f.f, "%g %g %g\n", ts_mid[m] / kDay, (gd / kLsun / ts_width[m]), (cl / ts_width[m] / kLsun));
+    }
+  }
+  return 0;
+}

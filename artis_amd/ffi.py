@@ -376,3 +376,54 @@ class VpktArrays:
     def counters(self):
         r = self.struct
         return {"nvpkt": r.nvpkt, "nvpkt_esc1": r.nvpkt_esc1, "nvpkt_esc2": r.nvpkt_esc2, "nvpkt_esc3": r.nvpkt_esc3}
+
+
+# exspec spectra (include/artis_gpu.h artis_spectra_request / artis_spectra_out)
+MABINS = 100
+
+
+class SpectraRequest(C.Structure):
+    _fields_ = [("nnubins", C.c_int32), ("nprocs", C.c_int32), ("abin", C.c_int32), ("syn_dir", C.c_double * 3)]
+
+
+class SpectraOut(C.Structure):
+    _fields_ = [(n, C.POINTER(C.c_double)) for n in (
+        "flux", "emission", "trueemission", "absorption", "stokes_flux", "stokes_emission", "stokes_absorption",
+        "lc_lum", "lc_lumcmf", "gamma_lc_lum", "gamma_lc_lumcmf")]
+
+
+class SpectraArrays:
+    """Host storage of one artis_spectra_out: flux [ntstep, nnubins]; emission / trueemission
+    [ntstep, nnubins, proccount]; absorption [ntstep, nnubins, ioncount]; stokes_* with a leading axis of 3
+    (I, Q, U); light curves [ntstep]."""
+
+    def __init__(self, ntstep, nnubins, nelements, maxnions, emission_res=True, stokes=False):
+        self.ioncount = nelements * maxnions
+        self.proccount = 2 * self.ioncount + 1
+        self.nnubins = nnubins
+        z = np.zeros
+        self.flux = z((ntstep, nnubins))
+        self.emission = z((ntstep, nnubins, self.proccount)) if emission_res else None
+        self.trueemission = z((ntstep, nnubins, self.proccount)) if emission_res else None
+        self.absorption = z((ntstep, nnubins, self.ioncount)) if emission_res else None
+        self.stokes_flux = z((3, ntstep, nnubins)) if stokes else None
+        self.stokes_emission = z((3, ntstep, nnubins, self.proccount)) if stokes and emission_res else None
+        self.stokes_absorption = z((3, ntstep, nnubins, self.ioncount)) if stokes and emission_res else None
+        self.lc_lum, self.lc_lumcmf = z(ntstep), z(ntstep)
+        self.gamma_lc_lum, self.gamma_lc_lumcmf = z(ntstep), z(ntstep)
+        self.struct = SpectraOut()
+        for name, _ in SpectraOut._fields_:
+            a = getattr(self, name)
+            if a is not None:
+                setattr(self.struct, name, a.ctypes.data_as(C.POINTER(C.c_double)))
+
+    def arrays(self):
+        return {n: getattr(self, n) for n, _ in SpectraOut._fields_ if getattr(self, n) is not None}
+
+
+def spectra_request(nnubins=1000, nprocs=1, abin=-1, syn_dir=(0., 0., 1.)):
+    r = SpectraRequest()
+    r.nnubins, r.nprocs, r.abin = nnubins, nprocs, abin
+    for k in range(3):
+        r.syn_dir[k] = syn_dir[k]
+    return r

@@ -1,44 +1,82 @@
-"""spec.out / light_curve.out writers for the device-binned spectra (artis_gpu_spectrum).
+"""Spectrum and light-curve output files for the device-binned spectra (artis_gpu_spectrum / artis_gpu_spectra).
 
-Formats follow the reference writers exactly: write_spectrum (spectrum.cc:172-186): a header row "0 t_mid/DAY..."
-then one row per frequency bin "nu_center flux(t0) flux(t1) ..."; write_light_curve (light_curve.cc:9-32):
-rows "t_mid/DAY lum/LSUN lumcmf/LSUN" then the gamma-deposition / cmf_lum block.  printf("%g ") formatting.
+The writers are the C++ ones of libartis_io (include/artis_io.h: artis_write_spectrum, artis_write_specpol,
+artis_write_light_curve), in the formats of write_spectrum / write_specpol (spectrum.cc:144-298) and
+write_light_curve (light_curve.cc:9-32).
 """
+import ctypes as C
+
 import numpy as np
+
+from . import io as aio
 
 DAY = 86400.0
 LSUN = 3.826e33
 
 
 def bin_edges(nnubins, nu_min, nu_max):
-    """lower_freq and delta_freq of init_spectra (spectrum.cc:491-500)."""
+    """lower_freq and delta_freq of init_spectra (spectrum.cc:491-500): float arrays (spectrum.h:18-19)."""
     dlognu = (np.log(nu_max) - np.log(nu_min)) / nnubins
     k = np.arange(nnubins)
-    lower = np.exp(np.log(nu_min) + k * dlognu)
-    delta = np.exp(np.log(nu_min) + (k + 1) * dlognu) - lower
-    return lower, delta
+    lower = np.exp(np.log(nu_min) + k * dlognu).astype(np.float32)
+    delta = (np.exp(np.log(nu_min) + (k + 1) * dlognu) - lower.astype(np.float64)).astype(np.float32)
+    return lower.astype(np.float64), delta.astype(np.float64)
 
 
-def _g(x):
-    return "%g" % x
+def _dp(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))
 
 
-def write_spec_out(path, ts_mid, spec, nu_min, nu_max, numtimesteps=None):
-    nt = spec.shape[0] if numtimesteps is None else numtimesteps
-    lower, delta = bin_edges(spec.shape[1], nu_min, nu_max)
-    with open(path, "w") as f:
-        f.write(" ".join([_g(0.0)] + [_g(ts_mid[p] / DAY) for p in range(nt)]) + " \n")
-        for nnu in range(spec.shape[1]):
-            f.write(" ".join([_g(lower[nnu] + delta[nnu] / 2)] + [_g(spec[p, nnu]) for p in range(nt)]) + " \n")
+def _lib():
+    L = aio.lib()
+    dp = C.POINTER(C.c_double)
+    L.artis_write_spectrum.argtypes = [C.c_char_p] * 4 + [C.c_int, C.c_int, dp, C.c_int, C.c_double, C.c_double,
+                                                          C.c_int, C.c_int, dp, dp, dp, dp]
+    L.artis_write_specpol.argtypes = [C.c_char_p] * 3 + [C.c_int, dp, C.c_int, C.c_double, C.c_double, C.c_int,
+                                                         C.c_int, dp, dp, dp]
+    L.artis_write_light_curve.argtypes = [C.c_char_p, C.c_int, C.c_int, dp, dp, dp, dp, dp, dp]
+    return L
 
 
-def write_light_curve(path, ts_mid, ts_width, lc, lccmf, gamma_dep=None, cmf_lum=None, numtimesteps=None):
+def _b(path):
+    return None if path is None else str(path).encode()
+
+
+def _c(x):
+    return None if x is None else np.ascontiguousarray(x, dtype=np.float64)
+
+
+def write_spec_out(path, ts_mid, spec, nu_min, nu_max, numtimesteps=None, emission=None, trueemission=None,
+                   absorption=None, emission_path=None, trueemission_path=None, absorption_path=None):
+    """spec.out (and emission.out / emissiontrue.out / absorption.out when their arrays and paths are given)."""
+    keep = [_c(x) for x in (ts_mid, spec, emission, trueemission, absorption)]
+    nt, nnb = keep[1].shape
+    n = nt if numtimesteps is None else numtimesteps
+    proccount = emission.shape[-1] if emission is not None else 0
+    ioncount = absorption.shape[-1] if absorption is not None else 0
+    rc = _lib().artis_write_spectrum(_b(path), _b(emission_path), _b(trueemission_path), _b(absorption_path), nt, n,
+                                     _dp(keep[0]), nnb, nu_min, nu_max, proccount, ioncount, _dp(keep[1]),
+                                     _dp(keep[2]), _dp(keep[3]), _dp(keep[4]))
+    if rc != 0:
+        raise OSError(f"artis_write_spectrum({path}) -> {rc}")
+
+
+def write_specpol(path, ts_mid, stokes_flux, nu_min, nu_max, stokes_emission=None, stokes_absorption=None,
+                  emission_path=None, absorption_path=None):
+    """specpol.out (and emissionpol.out / absorptionpol.out)."""
+    keep = [_c(x) for x in (ts_mid, stokes_flux, stokes_emission, stokes_absorption)]
+    _, nt, nnb = keep[1].shape
+    proccount = stokes_emission.shape[-1] if stokes_emission is not None else 0
+    ioncount = stokes_absorption.shape[-1] if stokes_absorption is not None else 0
+    rc = _lib().artis_write_specpol(_b(path), _b(emission_path), _b(absorption_path), nt, _dp(keep[0]), nnb, nu_min,
+                                    nu_max, proccount, ioncount, _dp(keep[1]), _dp(keep[2]), _dp(keep[3]))
+    if rc != 0:
+        raise OSError(f"artis_write_specpol({path}) -> {rc}")
+
+
+def write_light_curve(path, ts_mid, ts_width, lc, lccmf, gamma_dep=None, cmf_lum=None, numtimesteps=None, abin=-1):
     nt = len(lc) if numtimesteps is None else numtimesteps
-    gamma_dep = np.zeros(nt) if gamma_dep is None else gamma_dep
-    cmf_lum = np.zeros(nt) if cmf_lum is None else cmf_lum
-    with open(path, "w") as f:
-        for t in range(nt):
-            f.write(f"{_g(ts_mid[t] / DAY)} {_g(lc[t] / LSUN)} {_g(lccmf[t] / LSUN)}\n")
-        for t in range(nt):
-            f.write(f"{_g(ts_mid[t] / DAY)} {_g(gamma_dep[t] / LSUN / ts_width[t])} "
-                    f"{_g(cmf_lum[t] / ts_width[t] / LSUN)}\n")
+    keep = [_c(x) for x in (ts_mid, ts_width, lc, lccmf, gamma_dep, cmf_lum)]
+    rc = _lib().artis_write_light_curve(_b(path), abin, nt, *[_dp(k) for k in keep])
+    if rc != 0:
+        raise OSError(f"artis_write_light_curve({path}) -> {rc}")

@@ -480,6 +480,35 @@ int artis_gpu_last_work_counts(int64_t out[ARTIS_WORK_COUNT]);
  * the reference divides by (globals::nprocs). */
 int artis_gpu_spectrum(int nnubins, int nprocs, double *spec_flux, double *lc_lum, double *lc_lumcmf);
 
+/* The full spectra of exspec / write_partial_lightcurve_spectra (exspec.cc, spectrum.cc:306-452,
+ * light_curve.cc:34-62) for the resident packets: add_to_spec_res for every escaped r-packet -- the flux, the
+ * emission / true-emission spectra resolved by emitting process (bound-bound per ion, bound-free per ion,
+ * free-free: proccount = 2 nelements maxnions + 1 columns, columnindex_from_emissiontype, spectrum.cc:306-337),
+ * the absorption spectrum by absorbing ion at absorptionfreq (ioncount = nelements maxnions columns), POL_ON
+ * Stokes I/Q/U flux and their emission/absorption spectra -- and add_to_lc_res for the r-packet and gamma-ray
+ * light curves.  abin -1: all directions; 0 .. ARTIS_MABINS-1: only packets escaping into that direction bin
+ * (get_escapedirectionbin about syn_dir, vectors.h:158-193), weighted by ARTIS_MABINS (the gamma-ray light
+ * curve is angle-averaged only).  Every array is timestep-major ([ntstep][nnubins][columns]) and ADDED into;
+ * NULL arrays are not produced. */
+#define ARTIS_MABINS 100
+typedef struct artis_spectra_request {
+  int32_t nnubins;          /* MNUBINS (1000) log bins over [nu_min_r, nu_max_r] */
+  int32_t nprocs;           /* globals::nprocs: every bin is divided by it */
+  int32_t abin;
+  double syn_dir[3];
+} artis_spectra_request;
+typedef struct artis_spectra_out {
+  double *flux;                       /* [ntstep * nnubins] */
+  double *emission, *trueemission;    /* [ntstep * nnubins * proccount] */
+  double *absorption;                 /* [ntstep * nnubins * ioncount] */
+  double *stokes_flux;                /* [3][ntstep * nnubins]: I, Q, U (POL_ON) */
+  double *stokes_emission;            /* [3][ntstep * nnubins * proccount] */
+  double *stokes_absorption;          /* [3][ntstep * nnubins * ioncount] */
+  double *lc_lum, *lc_lumcmf;         /* [ntstep] */
+  double *gamma_lc_lum, *gamma_lc_lumcmf;  /* [ntstep] */
+} artis_spectra_out;
+int artis_gpu_spectra(const artis_spectra_request *req, artis_spectra_out *out);
+
 /* --- virtual packets (VPKT_ON) ------------------------------------------------------------------------------ */
 /* Switch virtual packets on for all following updates (replaces read_parameterfile_vpkt + init_vspecpol +
  * init_vpkt_grid, vpkt.cc:408-443, 547-578, 667-835): allocates and zeroes the device accumulators.  exclude[] > 0

@@ -96,6 +96,30 @@ void artis_free_model(artis_ejecta_model *m);
 int artis_read_abundances(const char *filename, int npts_model, int model_type, int nelements,
                           const int32_t *anumber, float *elem_abund);
 
+/* Spectrum and light-curve writers (the formats of spectrum.cc:172-298 write_spectrum / write_specpol and
+ * light_curve.cc:9-32 write_light_curve), for the arrays artis_gpu_spectra fills (include/artis_gpu.h):
+ *   spec.out: "0 t_mid/DAY ..." then per frequency bin "nu_mid flux(t) ..."; nu_mid from the float bin edges
+ *     of init_spectra (spectrum.cc:495-500);
+ *   emission.out / emissiontrue.out / absorption.out: per (frequency bin, timestep) one row of proccount
+ *     (ioncount) columns;
+ *   specpol.out: header with the timestep list three times, then per bin "nu_mid I(t)... Q(t)... U(t)...";
+ *     emissionpol.out / absorptionpol.out rows in the order I, Q, U per bin;
+ *   light_curve.out: "t_mid/DAY lum/LSUN lumcmf/LSUN" rows, then (abin -1) "t_mid/DAY gamma_dep/LSUN/width
+ *     cmf_lum/width/LSUN" rows.
+ * Every value printed with "%g " as the reference does.  NULL emission filenames / arrays skip those files.
+ * 0 on success, -1 when a file cannot be written. */
+int artis_write_spectrum(const char *spec_filename, const char *emission_filename, const char *trueemission_filename,
+                         const char *absorption_filename, int ntstep, int numtimesteps, const double *ts_mid,
+                         int nnubins, double nu_min, double nu_max, int proccount, int ioncount, const double *flux,
+                         const double *emission, const double *trueemission, const double *absorption);
+int artis_write_specpol(const char *specpol_filename, const char *emission_filename, const char *absorption_filename,
+                        int ntstep, const double *ts_mid, int nnubins, double nu_min, double nu_max, int proccount,
+                        int ioncount, const double *stokes_flux, const double *stokes_emission,
+                        const double *stokes_absorption);
+int artis_write_light_curve(const char *lc_filename, int abin, int numtimesteps, const double *ts_mid,
+                            const double *ts_width, const double *lc_lum, const double *lc_lumcmf,
+                            const double *gamma_dep, const double *cmf_lum);
+
 #ifdef __cplusplus
 }
 #endif

@@ -3508,6 +3508,12 @@ double oracle_phixs(const artis_atomic_tables *at, int table, double nu_edge, do
 
 // write_partial_lightcurve_spectra binning (spectrum.cc:641-721): add_to_lc_res (light_curve.cc:34-54) and
 // add_to_spec (spectrum.cc:339-362) for every escaped r-packet, in packet order; timestep lookup sn3d.h:168-180
+// init_spectra (spectrum.cc:495-500): lower_freq and delta_freq are float arrays (spectrum.h:18-19), so the
+// bin width every deltaE divides by is the float difference of the float lower edge
+static inline double spec_delta_freq(double nu_min, double dlognu, int nnu) {
+  const float lower_freq = (float)exp(log(nu_min) + (nnu * (dlognu)));
+  return (float)(exp(log(nu_min) + ((nnu + 1) * (dlognu))) - lower_freq);
+}
 static int oracle_get_timestep(const artis_geometry *g, double t) {
   for (int nts = 0; nts < g->ntstep; nts++) {
     const double tsend = (nts < (g->ntstep - 1)) ? g->ts_start[nts + 1] : g->tmax;
@@ -3524,7 +3530,7 @@ int oracle_spectrum(const artis_geometry *g, const artis_packet *pkts, int npkts
   const double dlognu = (log(nu_max) - log(nu_min)) / nnubins;  // spectrum.cc:352
   std::vector<double> delta_freq(nnubins);
   for (int nnu = 0; nnu < nnubins; nnu++)  // spectrum.cc:497-500
-    delta_freq[nnu] = exp(log(nu_min) + ((nnu + 1) * (dlognu))) - exp(log(nu_min) + (nnu * (dlognu)));
+    delta_freq[nnu] = spec_delta_freq(nu_min, dlognu, nnu);
   const double cmfcorr = sqrt(1. - (g->vmax * g->vmax / ARTIS_CLIGHTSQUARED));
   for (int ii = 0; ii < npkts; ii++) {
     const artis_packet *p = &pkts[ii];
@@ -3545,6 +3551,123 @@ int oracle_spectrum(const artis_geometry *g, const artis_packet *pkts, int npkts
       if (nnu < 0 || nnu >= nnubins) return -1;  // assert_always(nnu < globals::nnubins)
       spec[(int64_t)nts * nnubins + nnu] +=
           p->e_rf / g->ts_width[nts] / delta_freq[nnu] / 4.e12 / ARTIS_PI / ARTIS_PARSEC / ARTIS_PARSEC / nprocs;
+    }
+  }
+  return 0;
+}
+
+
+// exspec spectra (spectrum.cc:306-452 add_to_spec / add_to_spec_res, light_curve.cc:34-62 add_to_lc_res,
+// spectrum.cc:671-681 the packet loop) for the escaped packets, in packet order, ADDED into *out
+static int oracle_escapedirectionbin(const double dir_in[3], const double syn_dir[3]) {  // vectors.h:158-193
+  const double xhat[3] = {1.0, 0.0, 0.0};
+  const double dirmag = vec_len(dir_in);
+  const double dir[3] = {dir_in[0] / dirmag, dir_in[1] / dirmag, dir_in[2] / dirmag};
+  const double costheta = dot(dir, syn_dir);
+  const int costhetabin = (int)((costheta + 1.0) * 10 / 2.0);
+  double vec1[3] = {0}, vec2[3] = {0}, vec3[3] = {0};
+  cross_prod(dir, syn_dir, vec1);
+  cross_prod(xhat, syn_dir, vec2);
+  const double cosphi = dot(vec1, vec2) / vec_len(vec1) / vec_len(vec2);
+  cross_prod(vec2, syn_dir, vec3);
+  const double testphi = dot(vec1, vec3);
+  int phibin = 0;
+  if (testphi > 0)
+    phibin = (int)(acos(cosphi) / 2. / ARTIS_PI * 10);
+  else
+    phibin = (int)((acos(cosphi) + ARTIS_PI) / 2. / ARTIS_PI * 10);
+  return (costhetabin * 10) + phibin;
+}
+
+int oracle_spectra(const artis_atomic_tables *at, const artis_geometry *g, const artis_packet *pkts, int npkts,
+                   const artis_spectra_request *req, artis_spectra_out *out) {
+  if (!req || !out || req->nnubins <= 0 || req->nprocs <= 0) return ARTIS_ERR_BAD_ARGUMENT;
+  const int nnubins = req->nnubins, nt_all = g->ntstep;
+  const int maxnions = at->maxnions, ioncount = at->nelements * maxnions, proccount = 2 * ioncount + 1;
+  const double nu_min = g->nu_min_r, nu_max = g->nu_max_r;
+  const double dlognu = (log(nu_max) - log(nu_min)) / nnubins;
+  std::vector<double> delta_freq(nnubins);
+  for (int nnu = 0; nnu < nnubins; nnu++)
+    delta_freq[nnu] = spec_delta_freq(nu_min, dlognu, nnu);
+  // bflist (input.cc:1153-1160) -> (element, ion)
+  std::vector<int> bf_col(std::max(at->nbfcontinua, 1), 0);
+  for (int e = 0; e < at->nelements; e++)
+    for (int i = 0; i < at->elem_nions[e]; i++) {
+      const int ui = at->elem_uniqueionoffset[e] + i;
+      for (int l = 0; l < at->ion_nlevels[ui]; l++) {
+        const int ul = at->ion_uniqueleveloffset[ui] + l;
+        for (int t = 0; t < at->level_nphixstargets[ul]; t++) {
+          const int bi = -1 - (at->level_cont_index[ul] - t);
+          if (bi >= 0 && bi < at->nbfcontinua) bf_col[bi] = e * maxnions + i;
+        }
+      }
+    }
+  auto column = [&](int et) {  // spectrum.cc:306-337
+    if (et >= 0) return at->line_elementindex[et] * maxnions + at->line_ionindex[et];
+    if (et == -9999999 || at->nbfcontinua == 0) return 2 * ioncount;
+    return ioncount + bf_col[-1 - et];
+  };
+  const size_t nb = (size_t)nt_all * nnubins;
+  const double cmfcorr = sqrt(1. - (g->vmax * g->vmax / ARTIS_CLIGHTSQUARED));
+  const double anglefactor = (req->abin >= 0) ? ARTIS_MABINS : 1.;
+  for (int ii = 0; ii < npkts; ii++) {
+    const artis_packet *p = &pkts[ii];
+    if (p->type != ARTIS_TYPE_ESCAPE) continue;
+    const double t_arrive = p->escape_time - (dot(p->pos, p->dir) / ARTIS_CLIGHT_PROP);
+    const double t_arrive_cmf = p->escape_time * cmfcorr;
+    if (p->escape_type == ARTIS_TYPE_GAMMA) {
+      if (req->abin != -1) continue;
+      if (out->gamma_lc_lum && t_arrive > g->tmin && t_arrive < g->tmax) {
+        const int nts = oracle_get_timestep(g, t_arrive);
+        out->gamma_lc_lum[nts] += p->e_rf / g->ts_width[nts] / req->nprocs;
+      }
+      if (out->gamma_lc_lumcmf && t_arrive_cmf > g->tmin && t_arrive_cmf < g->tmax) {
+        const int nts = oracle_get_timestep(g, t_arrive_cmf);
+        out->gamma_lc_lumcmf[nts] += p->e_cmf / g->ts_width[nts] / req->nprocs / cmfcorr;
+      }
+      continue;
+    }
+    if (p->escape_type != ARTIS_TYPE_RPKT) continue;
+    if (req->abin >= 0 && oracle_escapedirectionbin(p->dir, req->syn_dir) != req->abin) continue;
+    // add_to_lc_res
+    if (out->lc_lum && t_arrive > g->tmin && t_arrive < g->tmax) {
+      const int nts = oracle_get_timestep(g, t_arrive);
+      out->lc_lum[nts] += p->e_rf / g->ts_width[nts] * anglefactor / req->nprocs;
+    }
+    if (req->abin == -1 && out->lc_lumcmf && t_arrive_cmf > g->tmin && t_arrive_cmf < g->tmax) {
+      const int nts = oracle_get_timestep(g, t_arrive_cmf);
+      out->lc_lumcmf[nts] += p->e_cmf / g->ts_width[nts] / req->nprocs / cmfcorr;
+    }
+    // add_to_spec
+    if (!(t_arrive > g->tmin && t_arrive < g->tmax && p->nu_rf > nu_min && p->nu_rf < nu_max)) continue;
+    const int nt = oracle_get_timestep(g, t_arrive);
+    const int nnu = (int)((log(p->nu_rf) - log(nu_min)) / dlognu);
+    if (nnu < 0 || nnu >= nnubins) return -1;  // assert_always(nnu < globals::nnubins)
+    const double deltaE = p->e_rf / g->ts_width[nt] / delta_freq[nnu] / 4.e12 / ARTIS_PI / ARTIS_PARSEC /
+                          ARTIS_PARSEC / req->nprocs * anglefactor;
+    const size_t fi = (size_t)nt * nnubins + nnu;
+    if (out->flux) out->flux[fi] += deltaE;
+    if (out->stokes_flux)
+      for (int k = 0; k < 3; k++) out->stokes_flux[k * nb + fi] += p->stokes[k] * deltaE;
+    if (!out->emission) continue;
+    const int nproc = column(p->emissiontype);
+    const int truenproc = column(p->trueemissiontype);
+    out->emission[fi * proccount + nproc] += deltaE;
+    if (out->trueemission) out->trueemission[fi * proccount + truenproc] += deltaE;
+    if (out->stokes_emission)
+      for (int k = 0; k < 3; k++) out->stokes_emission[k * nb * proccount + fi * proccount + nproc] += p->stokes[k] * deltaE;
+    const int nnu_abs = (int)((log(p->absorptionfreq) - log(nu_min)) / dlognu);
+    if (nnu_abs >= 0 && nnu_abs < nnubins && out->absorption) {
+      const double deltaE_absorption = p->e_rf / g->ts_width[nt] / delta_freq[nnu_abs] / 4.e12 / ARTIS_PI /
+                                       ARTIS_PARSEC / ARTIS_PARSEC / req->nprocs * anglefactor;
+      const int at_ = p->absorptiontype;
+      if (at_ >= 0) {
+        const size_t ai = ((size_t)nt * nnubins + nnu_abs) * ioncount + at->line_elementindex[at_] * maxnions +
+                          at->line_ionindex[at_];
+        out->absorption[ai] += deltaE_absorption;
+        if (out->stokes_absorption)
+          for (int k = 0; k < 3; k++) out->stokes_absorption[k * nb * ioncount + ai] += p->stokes[k] * deltaE_absorption;
+      }
     }
   }
   return 0;

@@ -102,3 +102,18 @@ def corrphotoioncoeff(model, nts, mgi, ul, t, brute=False, params=None):
     p = params if params is not None else model.params
     return lib().oracle_corrphotoioncoeff(model.atomic, model.geometry, model.cellstate, C.byref(p),
                                           int(nts), int(mgi), int(ul), int(t), int(brute))
+
+
+def spectra(model, packets, nnubins=1000, nprocs=1, abin=-1, syn_dir=(0., 0., 1.), emission_res=True, stokes=False):
+    """The oracle's exspec binning (oracle_spectra: add_to_spec_res / add_to_lc_res in packet order)."""
+    L = lib()
+    L.oracle_spectra.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(ffi.SpectraRequest),
+                                 C.POINTER(ffi.SpectraOut)]
+    L.oracle_spectra.restype = C.c_int
+    out = ffi.SpectraArrays(model.cfg.ntstep, nnubins, model.nelements, model.maxnions, emission_res, stokes)
+    req = ffi.spectra_request(nnubins, nprocs, abin, syn_dir)
+    rc = L.oracle_spectra(model.atomic, model.geometry, packets.ctypes.data, len(packets), C.byref(req),
+                          C.byref(out.struct))
+    if rc != 0:
+        raise RuntimeError(f"oracle_spectra -> {rc}")
+    return out

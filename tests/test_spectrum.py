@@ -81,3 +81,87 @@ def test_device_spectrum_matches_oracle(small_model):
     assert np.abs(spec - so).sum() / scale < 1e-12
     assert np.allclose(lc, lo, rtol=1e-12, atol=0)
     assert np.allclose(lccmf, lco, rtol=1e-12, atol=0)
+
+
+def test_oracle_spectra_resolved_columns_sum_to_flux(small_model):
+    """add_to_spec_res (spectrum.cc:339-452): every escaped packet adds deltaE once to the flux and once to an
+    emission / true-emission column, so the columns sum to the flux; unpolarised packets (Stokes I = 1) give
+    stokes_I == flux; the 100 direction bins (weight MABINS) average to the angle-averaged spectrum."""
+    pk = _escaped_packets(small_model, 9, 3000, 24)
+    s = oracle_lib.spectra(small_model, pk, nnubins=200, emission_res=True, stokes=True)
+    flux = s.flux
+    assert flux.sum() > 0
+    assert np.allclose(s.emission.sum(-1), flux, rtol=1e-12, atol=1e-300)
+    assert np.allclose(s.trueemission.sum(-1), flux, rtol=1e-12, atol=1e-300)
+    assert s.absorption.sum() > 0
+    esc = pk["type"] == ffi.TYPE_ESCAPE
+    if np.all(pk["stokes"][esc][:, 0] == 1.0):
+        assert np.allclose(s.stokes_flux[0], flux, rtol=1e-12, atol=1e-300)
+    assert np.allclose(s.stokes_emission[0].sum(-1), s.stokes_flux[0], rtol=1e-12, atol=1e-300)
+    simple, lc, lccmf = oracle_lib.spectrum(small_model, pk, nnubins=200)
+    assert np.array_equal(simple, flux) and np.array_equal(lc, s.lc_lum) and np.array_equal(lccmf, s.lc_lumcmf)
+    tot = np.zeros_like(flux)
+    lct = np.zeros_like(lc)
+    for abin in range(ffi.MABINS):
+        sa = oracle_lib.spectra(small_model, pk, nnubins=200, abin=abin, syn_dir=(0., 0., 1.), emission_res=False)
+        tot += sa.flux
+        lct += sa.lc_lum
+        assert not sa.lc_lumcmf.any()
+    assert np.allclose(tot / ffi.MABINS, flux, rtol=1e-10, atol=1e-300)
+    assert np.allclose(lct / ffi.MABINS, lc, rtol=1e-10, atol=1e-300)
+
+
+def test_resolved_writers_follow_reference_format(tmp_path, small_model):
+    """emission.out / emissiontrue.out / absorption.out: one row per (frequency bin, timestep) of proccount /
+    ioncount columns (spectrum.cc:176-200); specpol.out: header with the timesteps three times, rows
+    "nu I.. Q.. U.." (spectrum.cc:232-298)."""
+    from artis_amd.spectrum import write_specpol
+
+    pk = _escaped_packets(small_model, 9, 1000, 25)
+    s = oracle_lib.spectra(small_model, pk, nnubins=40, emission_res=True, stokes=True)
+    nt = s.flux.shape[0]
+    ts_mid = np.linspace(1, 2, nt) * 86400.0
+    write_spec_out(tmp_path / "spec.out", ts_mid, s.flux, 1e14, 5e15, numtimesteps=12, emission=s.emission,
+                   trueemission=s.trueemission, absorption=s.absorption, emission_path=tmp_path / "emission.out",
+                   trueemission_path=tmp_path / "emissiontrue.out", absorption_path=tmp_path / "absorption.out")
+    em = (tmp_path / "emission.out").read_text().splitlines()
+    ab = (tmp_path / "absorption.out").read_text().splitlines()
+    assert len(em) == 40 * 12 and len(em[0].split()) == s.proccount and len(ab[0].split()) == s.ioncount
+    back = np.array([[float(v) for v in r.split()] for r in em]).reshape(40, 12, s.proccount)
+    assert np.allclose(back, s.emission[:12].transpose(1, 0, 2), rtol=1e-5)
+    write_specpol(tmp_path / "specpol.out", ts_mid, s.stokes_flux, 1e14, 5e15, s.stokes_emission,
+                  s.stokes_absorption, tmp_path / "emissionpol.out", tmp_path / "absorptionpol.out")
+    rows = (tmp_path / "specpol.out").read_text().splitlines()
+    assert len(rows) == 41 and len(rows[0].split()) == 1 + 3 * nt
+    back = np.array([[float(v) for v in r.split()] for r in rows[1:]])
+    assert np.allclose(back[:, 1:1 + nt], s.stokes_flux[0].T, rtol=1e-5)
+    assert np.allclose(back[:, 1 + 2 * nt:], s.stokes_flux[2].T, rtol=1e-5, atol=1e-300)
+    lower, delta = bin_edges(40, 1e14, 5e15)
+    assert np.allclose(back[:, 0], (lower + delta / 2), rtol=1e-5)  # "%g": 6 significant digits
+    assert len((tmp_path / "emissionpol.out").read_text().splitlines()) == 40 * 3 * nt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("abin", [-1, 37])
+def test_device_spectra_match_oracle(small_model, abin):
+    """artis_gpu_spectra vs oracle_spectra: flux, emission / true-emission / absorption, Stokes I/Q/U and the
+    light curves of the engine-propagated packets (float64 atomics vs serial sums: ESTIMATOR_RTOL)."""
+    from artis_amd import Engine
+
+    nts = 9
+    small_model.set_timestep(nts)
+    pk = small_model.init_rpackets(nts, 4000, seed=26)
+    eng = Engine(small_model)
+    try:
+        eng.upload_cellstate(nts)
+        eng.update_packets(nts, pk)
+        g = eng.spectra(nnubins=300, abin=abin, syn_dir=(0.3, 0.4, np.sqrt(0.75)), emission_res=True, stokes=True)
+    finally:
+        eng.close()
+    o = oracle_lib.spectra(small_model, pk, nnubins=300, abin=abin, syn_dir=(0.3, 0.4, np.sqrt(0.75)),
+                           emission_res=True, stokes=True)
+    for name, a in o.arrays().items():
+        b = getattr(g, name)
+        scale = max(np.abs(a).max(), 1e-300)
+        assert np.abs(a - b).max() <= 1e-9 * scale, name
+    assert o.flux.sum() > 0 and o.emission.sum() > 0
