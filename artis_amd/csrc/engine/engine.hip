@@ -849,7 +849,7 @@ int run_wavefront(int64_t n, int nts, double t2) {
     }
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QM, 0, 2 * sizeof(uint32_t), G.stream));
     if (G.K.C.have_macache) {  // jumps the 32-bit keys could not decide (rare), exact; walks go back to M
-      k_ma_exact<<<grid / 8, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+      k_ma_exact<<<grid / 4, 64, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
       HIPCHK(hipMemsetAsync(W.ctr + 2 * QX, 0, 2 * sizeof(uint32_t), G.stream));
     }
     TEND(1);

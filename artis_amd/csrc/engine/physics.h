@@ -450,6 +450,68 @@ DEVFN void ma_foreach_rate(const Ctx &K, int mgi, int ul, double t_mid, Pop pop,
   }
 }
 
+// The pos-th individual rate of ma_foreach_rate's sequence (pos in [0, nd + nr + nu + nt) of the level's MaMeta),
+// with the very expressions of ma_foreach_rate, so that rates evaluated one per lane and summed in order give the
+// same sums bit for bit (the wave-parallel exact jump of k_ma_exact)
+struct MaItem {
+  int kind, j;
+  double R, C, et, eg;
+};
+template <typename Pop, typename Corr>
+DEVFN MaItem ma_rate_at(const Ctx &K, int mgi, int ul, double t_mid, int pos, Pop pop, Corr corrphot) {
+  const int ui = K.T.level_ui[ul];
+  const int e = K.T.ion_element[ui];
+  const int i = ui - K.T.elem_uniqueionoffset[e];
+  const int l = ul - K.T.ion_uniqueleveloffset[ui];
+  const float T_e = K.C.Te[mgi];
+  const float nne = K.C.nne[mgi];
+  const double epsilon_current = K.T.level_epsilon[ul];
+  const double statweight = K.T.level_stat_weight[ul];
+  MaItem it;
+  const int ndowntrans = K.T.level_ndowntrans[ul];
+  if (pos < ndowntrans) {
+    const int li = K.T.downtrans_lineindex[K.T.level_downtrans_offset[ul] + pos];
+    const int lower = K.T.line_lower[li];
+    const double epsilon_target = epsilon(K, e, i, lower);
+    const double epsilon_trans = epsilon_current - epsilon_target;
+    const double n_self = pop(ul);
+    const double n_l = pop(ul - l + lower);
+    it = {MA_KIND_DOWN, pos, rad_deexcitation_ratecoeff_n(K, n_self, n_l, li, t_mid),
+          col_deexcitation_ratecoeff(K, T_e, nne, epsilon_trans, li, stat_weight(K, e, i, lower), statweight),
+          epsilon_trans, epsilon_target};
+    return it;
+  }
+  pos -= ndowntrans;
+  const int nrl = (i > 0 && l <= K.T.ion_maxrecombininglevel[ui]) ? get_ionisinglevels(K, e, i - 1) : 0;
+  if (pos < nrl) {
+    const int lower = pos;
+    const double epsilon_target = epsilon(K, e, i - 1, lower);
+    const double epsilon_trans = epsilon_current - epsilon_target;
+    it = {MA_KIND_RECOMB, lower, rad_recombination_ratecoeff(K, T_e, nne, e, i, l, lower),
+          col_recombination_ratecoeff(K, mgi, e, i, l, lower, epsilon_trans), epsilon_trans, epsilon_target};
+    return it;
+  }
+  pos -= nrl;
+  const int nuptrans = K.T.level_nuptrans[ul];
+  if (pos < nuptrans) {
+    const int li = K.T.uptrans_lineindex[K.T.level_uptrans_offset[ul] + pos];
+    const int upper = K.T.line_upper[li];
+    const double epsilon_trans = epsilon(K, e, i, upper) - epsilon_current;
+    const double n_self = pop(ul);
+    const double n_u = pop(ul - l + upper);
+    it = {MA_KIND_UP, pos, rad_excitation_ratecoeff_n(K, mgi, n_u, n_self, epsilon_trans, li, t_mid),
+          col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, e, i, upper)),
+          epsilon_trans, 0.};
+    return it;
+  }
+  pos -= nuptrans;
+  const int t = pos;
+  const double epsilon_trans = get_phixs_threshold(K, e, i, l, t);
+  it = {MA_KIND_UPHIGHER, t, corrphot(K.T.level_phixstargets_offset[ul] + t),
+        col_ionization_ratecoeff(K, T_e, nne, e, i, l, t, epsilon_trans), epsilon_trans, 0.};
+  return it;
+}
+
 // macroatom.cc:139-146: the INTERNALUPHIGHERNT total of unique level ul (NT_ON; the host's
 // nt_ionization_ratecoeff, nonthermal.cc:1684-1712, times epsilon_current)
 DEVFN double ma_nt_total(const Ctx &K, int mgi, int ul) {

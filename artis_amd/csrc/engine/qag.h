@@ -6,8 +6,9 @@
 // Gauss-Kronrod rule spread over the wave's lanes: lane 0 the centre, lanes 1..30 the left nodes, lanes 31..60
 // the right nodes.  The rule's sums, the error estimate and the interval bookkeeping (bisection of the interval
 // with the largest error, the error list ordered by qpsrt) then run on every lane alike, in GSL's operation
-// order, with the interval lists in a per-wave global workspace -- the same values on every lane, each lane
-// reading back only what it wrote itself.
+// order -- the same values on every lane, each lane reading back only what it wrote itself.  The error list and
+// its order (walked by qpsrt at every bisection) sit in LDS for the first QAG_LDS intervals, the interval ends,
+// results and levels (touched O(1) times per bisection) in a per-wave global workspace of GSLWSIZE entries.
 #ifndef ARTIS_QAG_H
 #define ARTIS_QAG_H
 
@@ -96,52 +97,76 @@ DEVFN void qag_qk61(const F &f, double a, double b, double *s_f, double *result,
   *abserr = qag_rescale_error(err, result_abs, result_asc);
 }
 
-// integration/qpsrt.c on the wave's workspace slice (ordered list of error indices)
-DEVFN void qag_qpsrt(double *elist, int32_t *order, int size, int &nrmax, int &imax) {
+// The error list and its order (the arrays qpsrt walks, O(size) dependent reads per bisection) live in LDS for the
+// first QAG_LDS intervals; intervals beyond that, up to GSLWSIZE, in the wave's global workspace.
+#define QAG_LDS 4096
+struct QagLists {
+  double *s_el;
+  int32_t *s_ord;
+  double *g_el;
+  int32_t *g_ord;
+  DEVFN double el(int i) const { return i < QAG_LDS ? s_el[i] : g_el[i]; }
+  DEVFN void set_el(int i, double v) const {
+    if (i < QAG_LDS)
+      s_el[i] = v;
+    else
+      g_el[i] = v;
+  }
+  DEVFN int32_t ord(int i) const { return i < QAG_LDS ? s_ord[i] : g_ord[i]; }
+  DEVFN void set_ord(int i, int32_t v) const {
+    if (i < QAG_LDS)
+      s_ord[i] = v;
+    else
+      g_ord[i] = v;
+  }
+};
+
+// integration/qpsrt.c on the wave's workspace (ordered list of error indices)
+DEVFN void qag_qpsrt(const QagLists &Q, int size, int &nrmax, int &imax) {
   const int last = size - 1;
   const int limit = QAG_LIMIT;
   int i_nrmax = nrmax;
-  int i_maxerr = order[i_nrmax];
+  int i_maxerr = Q.ord(i_nrmax);
   if (last < 2) {
-    order[0] = 0;
-    order[1] = 1;
+    Q.set_ord(0, 0);
+    Q.set_ord(1, 1);
     imax = i_maxerr;
     return;
   }
-  const double errmax = elist[i_maxerr];
-  while (i_nrmax > 0 && errmax > elist[order[i_nrmax - 1]]) {
-    order[i_nrmax] = order[i_nrmax - 1];
+  const double errmax = Q.el(i_maxerr);
+  while (i_nrmax > 0 && errmax > Q.el(Q.ord(i_nrmax - 1))) {
+    Q.set_ord(i_nrmax, Q.ord(i_nrmax - 1));
     i_nrmax--;
   }
   const int top = (last < (limit / 2 + 2)) ? last : (limit - last + 1);
   int i = i_nrmax + 1;
-  while (i < top && errmax < elist[order[i]]) {
-    order[i - 1] = order[i];
+  while (i < top && errmax < Q.el(Q.ord(i))) {
+    Q.set_ord(i - 1, Q.ord(i));
     i++;
   }
-  order[i - 1] = i_maxerr;
-  const double errmin = elist[last];
+  Q.set_ord(i - 1, i_maxerr);
+  const double errmin = Q.el(last);
   int k = top - 1;
-  while (k > i - 2 && errmin >= elist[order[k]]) {
-    order[k + 1] = order[k];
+  while (k > i - 2 && errmin >= Q.el(Q.ord(k))) {
+    Q.set_ord(k + 1, Q.ord(k));
     k--;
   }
-  order[k + 1] = last;
-  imax = order[i_nrmax];
+  Q.set_ord(k + 1, last);
+  imax = Q.ord(i_nrmax);
   nrmax = i_nrmax;
 }
 
 // integration/qag.c; returns the GSL status (0, 18 GSL_EROUND, 21 GSL_ESING, 11 GSL_EMAXITER, 5 GSL_EFAILED)
 template <typename F>
 DEVFN int qag61(const F &f, double a, double b, double epsabs, double epsrel, double *al, double *bl, double *rl,
-                double *el, int32_t *order, int32_t *lev, double *s_f, double *result, double *abserr) {
+                const QagLists &Q, int32_t *lev, double *s_f, double *result, double *abserr) {
   const int limit = QAG_LIMIT;
   int size = 0, nrmax = 0, imax = 0;
   al[0] = a;
   bl[0] = b;
   rl[0] = 0.0;
-  el[0] = 0.0;
-  order[0] = 0;
+  Q.set_el(0, 0.0);
+  Q.set_ord(0, 0);
   lev[0] = 0;
   *result = 0;
   *abserr = 0;
@@ -149,7 +174,7 @@ DEVFN int qag61(const F &f, double a, double b, double epsabs, double epsrel, do
   qag_qk61(f, a, b, s_f, &result0, &abserr0, &resabs0, &resasc0);
   size = 1;
   rl[0] = result0;
-  el[0] = abserr0;
+  Q.set_el(0, abserr0);
   double tolerance = fmax(epsabs, epsrel * fabs(result0));
   const double round_off = 50 * QAG_EPS * resabs0;
   if (abserr0 <= round_off && abserr0 > tolerance) {
@@ -167,7 +192,7 @@ DEVFN int qag61(const F &f, double a, double b, double epsabs, double epsrel, do
   int roundoff_type1 = 0, roundoff_type2 = 0, error_type = 0;
   do {
     const int ii = imax;
-    const double a_i = al[ii], b_i = bl[ii], r_i = rl[ii], e_i = el[ii];
+    const double a_i = al[ii], b_i = bl[ii], r_i = rl[ii], e_i = Q.el(ii);
     const double a1 = a_i;
     const double b1 = 0.5 * (a_i + b_i);
     const double a2 = b1;
@@ -196,26 +221,26 @@ DEVFN int qag61(const F &f, double a, double b, double epsabs, double epsrel, do
     if (error2 > error1) {
       al[ii] = a2;
       rl[ii] = area2;
-      el[ii] = error2;
+      Q.set_el(ii, error2);
       lev[ii] = new_level;
       al[i_new] = a1;
       bl[i_new] = b1;
       rl[i_new] = area1;
-      el[i_new] = error1;
+      Q.set_el(i_new, error1);
       lev[i_new] = new_level;
     } else {
       bl[ii] = b1;
       rl[ii] = area1;
-      el[ii] = error1;
+      Q.set_el(ii, error1);
       lev[ii] = new_level;
       al[i_new] = a2;
       bl[i_new] = b2;
       rl[i_new] = area2;
-      el[i_new] = error2;
+      Q.set_el(i_new, error2);
       lev[i_new] = new_level;
     }
     size++;
-    qag_qpsrt(el, order, size, nrmax, imax);
+    qag_qpsrt(Q, size, nrmax, imax);
     iteration++;
   } while (iteration < limit && !error_type && errsum > tolerance);
   double result_sum = 0;
@@ -242,11 +267,14 @@ DEVFN bool bfrate_override(const Ctx &K, int mgi, int slot) {
 __global__ __launch_bounds__(64) void k_corrphot_integral(Ctx K, const int32_t *target_ul, const int32_t *target_t,
                                                           QagWs ws) {
   __shared__ double s_f[64];
+  __shared__ double s_el[QAG_LDS];
+  __shared__ int32_t s_ord[QAG_LDS];
   const int64_t ntg = K.T.ntargets_total;
   const int64_t total = (int64_t)K.C.n_nonempty * ntg;
   const int64_t wbase = (int64_t)blockIdx.x * QAG_LIMIT;
-  double *al = ws.alist + wbase, *bl = ws.blist + wbase, *rl = ws.rlist + wbase, *el = ws.elist + wbase;
-  int32_t *order = ws.order + wbase, *lev = ws.level + wbase;
+  double *al = ws.alist + wbase, *bl = ws.blist + wbase, *rl = ws.rlist + wbase;
+  int32_t *lev = ws.level + wbase;
+  const QagLists Q{s_el, s_ord, ws.elist + wbase, ws.order + wbase};
   for (int64_t item = blockIdx.x; item < total; item += gridDim.x) {
     const int k = (int)(item / ntg);
     const int slot = (int)(item % ntg);
@@ -280,8 +308,8 @@ __global__ __launch_bounds__(64) void k_corrphot_integral(Ctx K, const int32_t *
       return ARTIS_ONEOVERH * sigma_bf / nu * Jnu * corrfactor;
     };
     double gammacorr = 0., error = 0.;
-    const int status = qag61(integrand, nu_threshold, nu_max_phixs, 0., 1e-3, al, bl, rl, el, order, lev, s_f,
-                             &gammacorr, &error);
+    const int status = qag61(integrand, nu_threshold, nu_max_phixs, 0., 1e-3, al, bl, rl, Q, lev, s_f, &gammacorr,
+                             &error);
     if (status != 0 && (status != 18 || (error / gammacorr) > 1e-1)) {
       if (!isfinite(gammacorr)) gammacorr = 0.;
     }

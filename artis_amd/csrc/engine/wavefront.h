@@ -428,50 +428,140 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   block_counters_flush(K, s_ctr, s_work);
 }
 
-// macro-atom jumps whose key comparisons were undecided (QX): one jump each with the exact sums (ma_jump_exact),
-// then the walk is parked again for k_ma (-> M queue) or its deactivation deferred like k_ma's (-> R / K queue).
-// Rare (a few per 10^5 jumps): one workitem per packet, grid-stride.
-__global__ __launch_bounds__(WAVE_BLOCK) void k_ma_exact(const Ctx *__restrict__ ctxp, WaveState W,
-                                                         const uint64_t *__restrict__ soa, int64_t n, int nts) {
+// macro-atom jumps whose key comparisons were undecided (QX): one jump each with the reference's exact sums, then
+// the walk is parked again for k_ma (-> M queue) or its deactivation deferred like k_ma's (-> R / K queue).
+// One wave per jump: the lanes evaluate the level's individual rates (ma_rate_at, the expressions of
+// ma_foreach_rate) MAXCH at a time into LDS, and every lane then sums them in the reference's order
+// (macroatom.cc:57-159, 502-525) -- the same sums as the single-thread ma_jump_exact, without its chain of
+// dependent loads.  Rare (~1 per 10^5 jumps), so blocks of one wave, grid-stride over the queue.
+#define MAX_CH 256
+__global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, WaveState W,
+                                                 const uint64_t *__restrict__ soa, int64_t n, int nts) {
   const Ctx &K = *ctxp;
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
+  __shared__ double s_R[MAX_CH], s_C[MAX_CH], s_et[MAX_CH], s_eg[MAX_CH];
+  __shared__ int s_kind[MAX_CH], s_j[MAX_CH];
   block_counters_init(s_ctr, s_work);
   LocalCounters L;
   L.ctr = &s_ctr[0];
   L.work = &s_work[0];
+  const int lane = threadIdx.x & 63;
   const uint32_t nq = W.ctr[2 * QX];
   const double t_mid = K.G.ts_mid[nts];
-  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x) {
+  for (uint32_t slot = blockIdx.x; slot < nq; slot += gridDim.x) {
     const int32_t idx = W.q[QX][slot];
     const int where = lo32(soa[PW(n, idx, 0)]);
     artis_rng rng = artis_rng_init(K.R.seed, (int)hi32(soa[PW(n, idx, 33)]), nts, K.R.rank);
     rng.n = W.rng_n[idx];
+    const int number = (int)rng.key1;
     MaLaneC m;
     m.ul = W.pend[idx].y;
-    m.jumps = W.pend_jumps[idx];
+    m.jumps = W.pend_jumps[idx] + 1;
     m.k = K.C.ne_index[cell_mgi(K, where)];
     m.rec_off = K.T.ma_meta[m.ul].rec_off;
     m.block = K.C.ma_key + (int64_t)m.k * K.C.ma_key_stride;
     m.ntrans = 0;
-    MaEnd e;
-    const int r = ma_jump_exact(K, L, rng, m, e, (int)rng.key1, t_mid);
-    lwork(L, WK_MA_TRANS, m.ntrans);
-    atomicAdd(&W.stats[40], 1ull);  // diagnostics: exact jumps
-    W.rng_n[idx] = rng.n;
-    W.pend_jumps[idx] = m.jumps;
-    if (r == MA_CONTINUE) {
-      if (m.jumps >= MA_MAX_JUMPS) {
-        fail(K, ERR_STUCK, (int)rng.key1, 2);
-        continue;
+    const int ul = m.ul, k = m.k;
+    const int mgi = K.C.ne_mgi[k];
+    const MaMeta mm = K.T.ma_meta[ul];
+    const int cnt = mm.nd + mm.nr + mm.nu + mm.nt;
+    const double ec = K.T.level_epsilon[ul];
+    const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
+    const double *corr = K.C.corrphot + (int64_t)k * K.T.ntargets_total;
+    auto pop = [&](int u) { return pops[u]; };
+    auto cph = [&](int s) { return corr[s]; };
+    // rates of positions [c0, c0 + MAX_CH) into LDS, one per lane per pass
+    auto fill = [&](int c0) {
+      __syncthreads();
+      for (int q = lane; q < MAX_CH && c0 + q < cnt; q += 64) {
+        const MaItem it = ma_rate_at(K, mgi, ul, t_mid, c0 + q, pop, cph);
+        s_R[q] = it.R;
+        s_C[q] = it.C;
+        s_et[q] = it.et;
+        s_eg[q] = it.eg;
+        s_kind[q] = it.kind;
+        s_j[q] = it.j;
       }
-      W.pend[idx] = make_int4(MA_RESUME, m.ul, 0, 0);
-      W.q[QM][atomicAdd(&W.ctr[2 * QM], 1u)] = idx;
-    } else if (r > 0) {
-      W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
-      lwork(L, WK_MA_JUMPS, m.jumps);
-      const int q = (r == MA_END_BB || r == MA_END_FB) ? QR : QK;
-      W.q[q][atomicAdd(&W.ctr[2 * q], 1u)] = idx;
+      __syncthreads();
+    };
+    double pr[ARTIS_MA_ACTION_COUNT];
+    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) pr[a] = 0.;
+    for (int c0 = 0; c0 < cnt; c0 += MAX_CH) {
+      fill(c0);
+      for (int q = 0; q < MAX_CH && c0 + q < cnt; q++) ma_accumulate(pr, s_kind[q], s_R[q], s_C[q], s_et[q], s_eg[q], ec);
+    }
+    pr[ARTIS_MA_ACTION_INTERNALUPHIGHERNT] = ma_nt_total(K, mgi, ul);
+    double total_transitions = 0.;
+    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) total_transitions += pr[a];
+    const double zrand = artis_rng_uniform(&rng);
+    const double randomrate = zrand * total_transitions;
+    double rate = 0.;
+    int sel = ARTIS_MA_ACTION_COUNT;
+    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
+      rate += pr[a];
+      if (rate > randomrate) {
+        sel = a;
+        break;
+      }
+    }
+    MaEnd e{};
+    int r;
+    if (rate <= randomrate) {
+      if (lane == 0) fail(K, ERR_MA_RANDOM, number, ul);
+      r = MA_FAILED;
+    } else if (sel == ARTIS_MA_ACTION_COLDEEXC || sel == ARTIS_MA_ACTION_COLRECOMB) {
+      e.code = (sel == ARTIS_MA_ACTION_COLDEEXC) ? MA_END_COLDEEXC : MA_END_COLRECOMB;
+      r = e.code;
+    } else if (sel == ARTIS_MA_ACTION_INTERNALUPHIGHERNT) {
+      r = (lane == 0) ? ma_apply_nt(K, L, rng, m, number) : MA_CONTINUE;
+    } else {
+      // the transition: first running sum of action sel above zr * total, in the reference's list order
+      const double zr = artis_rng_uniform(&rng);
+      const double x = zr * pr[sel];
+      const int kind = (sel == ARTIS_MA_ACTION_RADDEEXC || sel == ARTIS_MA_ACTION_INTERNALDOWNSAME) ? MA_KIND_DOWN
+                       : (sel == ARTIS_MA_ACTION_RADRECOMB || sel == ARTIS_MA_ACTION_INTERNALDOWNLOWER) ? MA_KIND_RECOMB
+                       : (sel == ARTIS_MA_ACTION_INTERNALUPSAME) ? MA_KIND_UP
+                                                                 : MA_KIND_UPHIGHER;
+      double run[ARTIS_MA_ACTION_COUNT];
+      for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) run[a] = 0.;
+      int found = -1;
+      for (int c0 = 0; c0 < cnt && found < 0; c0 += MAX_CH) {
+        fill(c0);
+        for (int q = 0; q < MAX_CH && c0 + q < cnt; q++) {
+          ma_accumulate(run, s_kind[q], s_R[q], s_C[q], s_et[q], s_eg[q], ec);
+          if (s_kind[q] == kind) m.ntrans++;
+          if (s_kind[q] == kind && run[sel] > x) {
+            found = s_j[q];
+            break;
+          }
+        }
+      }
+      if (found < 0) {
+        if (lane == 0) fail(K, ERR_MA_SELECT, number, 10 + sel);
+        r = MA_FAILED;
+      } else {
+        r = (lane == 0) ? ma_apply_selection(K, L, m, e, sel, found, mm.doff, mm.uoff, mm.base_lower) : MA_CONTINUE;
+      }
+    }
+    if (lane == 0) {
+      lwork(L, WK_MA_TRANS, m.ntrans);
+      atomicAdd(&W.stats[40], 1ull);  // diagnostics: exact jumps
+      W.rng_n[idx] = rng.n;
+      W.pend_jumps[idx] = m.jumps;
+      if (r == MA_CONTINUE) {
+        if (m.jumps >= MA_MAX_JUMPS) {
+          fail(K, ERR_STUCK, number, 2);
+        } else {
+          W.pend[idx] = make_int4(MA_RESUME, m.ul, 0, 0);
+          W.q[QM][atomicAdd(&W.ctr[2 * QM], 1u)] = idx;
+        }
+      } else if (r > 0) {
+        W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
+        lwork(L, WK_MA_JUMPS, m.jumps);
+        const int q = (r == MA_END_BB || r == MA_END_FB) ? QR : QK;
+        W.q[q][atomicAdd(&W.ctr[2 * q], 1u)] = idx;
+      }
     }
   }
   block_counters_flush(K, s_ctr, s_work);

@@ -1134,12 +1134,13 @@ void compute_cellstate(Model &m, int nts) {
     }
     m.totalcooling[mgi] = C_total;
     if (m.cfg.nebular) {
-      // binned radiation field fits around the cell's T_R / W (radfield.cc:908-920), some bins without a fit
+      // binned radiation field fits within 5-10 % of the cell's T_R / W (radfield.cc:908-920), some bins without
+      // a fit
       const int nb = m.at.radfield_nbins;
       for (int b = 0; b < nb; b++) {
         const size_t mb = (size_t)mgi * nb + b;
-        m.rf_TR[mb] = (float)(m.TR[mgi] * (0.7 + 0.6 * hash_u01(mgi, b, 21)));
-        m.rf_W[mb] = ((b % 13) == 5) ? -1.f : (float)(m.W[mgi] * (0.3 + 1.4 * hash_u01(mgi, b, 22)));
+        m.rf_TR[mb] = (float)(m.TR[mgi] * (0.95 + 0.1 * hash_u01(mgi, b, 21)));
+        m.rf_W[mb] = ((b % 13) == 5) ? -1.f : (float)(m.W[mgi] * (0.9 + 0.2 * hash_u01(mgi, b, 22)));
       }
       // normalised bf-rate estimators of a previous timestep: W * LUT(T_R) of the cell (ratecoeff.cc:1026-1041)
       // times a factor in [0.5, 1.5), some absent
@@ -1162,7 +1163,7 @@ void compute_cellstate(Model &m, int nts) {
         const int nions = m.elem_nions[e];
         for (int ion = 0; ion < nions; ion++) {
           const int ui = m.elem_uniqueionoffset[e] + ion;
-          m.nt_Y[(size_t)mgi * ni + ui] = (ion < nions - 1) ? pow(10., -3. + 4. * hash_u01(mgi, ui, 31)) : 0.;
+          m.nt_Y[(size_t)mgi * ni + ui] = (ion < nions - 1) ? pow(10., 1. + 3. * hash_u01(mgi, ui, 31)) : 0.;
           const double p0 = 0.7 + 0.2 * hash_u01(mgi, ui, 32), p1 = (1. - p0) * 0.7;
           const double q0 = 0.6 + 0.3 * hash_u01(mgi, ui, 33), q1 = (1. - q0) * 0.6;
           float *pr = &m.nt_prob[((size_t)mgi * ni + ui) * (A + 1)];

@@ -88,6 +88,7 @@ def test_nebular_rpacket_bookkeeping(neb, nts):
     assert est.radfield_J.sum() <= est.J.sum() * (1 + 1e-12)
     if nts >= 12:
         assert est.bfrate_raw.sum() > 0
+    assert c[12] > 0  # the non-thermal ionisation action (CTR_MA_STAT_INTERNALUPHIGHERNT)
 
 
 def test_nebular_ntlepton_ionisation():
