@@ -120,6 +120,10 @@ def main():
     from artis_amd import dist as adist
     from artis_amd.model import Model
 
+    def progress(msg):  # rank 0, stderr: a long run shows its phases as they finish
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
     model = Model(ngrid_1d=args.ngrid)
     nts = args.nts
     model.set_timestep(nts)
@@ -127,6 +131,7 @@ def main():
     params.rank = rank
     P = args.packets
     packets = model.init_rpackets(nts, P, seed=1000 + rank)
+    progress(f"model and {P} packets ready")
     eng = Engine(model, device=local_rank, params=params)
     vcfg = None
     if args.vpkt > 0:
@@ -141,6 +146,7 @@ def main():
     eng.upload_cellstate(nts)
     eng.upload(packets)
     eng.snapshot()
+    progress("engine initialised, packets resident")
 
     if world > 1:
         adist.join(eng, rank, world, dist)
@@ -170,14 +176,16 @@ def main():
                 vstats.append(eng.vpkt_last_stats())
                 vwork.append(eng.vpkt_last_work())
 
-    for _ in range(args.warmup):
+    for w in range(args.warmup):
         step(False)
+        progress(f"warmup step {w} done: transport {eng.last_transport_ms():.0f} ms")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k in range(args.steps):
         step(True)
+        progress(f"step {k} done: transport {transport_ms[-1]:.0f} ms")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
