@@ -256,9 +256,9 @@ __global__ void k_cooling(Ctx K) {
 // diverge; only the cell's populations (level-major copy popsT) and temperatures differ per lane.
 // With the cache, one launch covers levels [ul0, ul0 + nlev) and writes the exact double running sums
 // position-major into the scratch S (S[(dbl_off(ul) - dbl_off(ul0)) * n_ne + pos * n_ne + k]: every store is 64
-// consecutive doubles); k_mapack then turns them into the compact key records.  Record positions:
-//   [9 totals | internal_down_same (nd, Eytzinger order) | internal_up_same (nu, Eytzinger) | rad_deexc (nd) |
-//    rad_recomb (nr) | internal_down_lower (nr) | internal_up_higher (nt)]
+// consecutive doubles); k_mapack then turns them into the compact key records.  Scratch positions:
+//   [9 totals | internal_down_same (nd) | internal_up_same (nu) | rad_deexc (nd) | rad_recomb (nr) |
+//    internal_down_lower (nr) | internal_up_higher (nt)]     (each array in the reference's order)
 __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict__ S) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nl = K.T.nlevels_total;
@@ -272,10 +272,9 @@ __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict_
   const MaMeta mm = K.T.ma_meta[ul];
   double *rec = cache ? S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * nne_cells + k : nullptr;
 #define REC(p) rec[(int64_t)(p) * nne_cells]
-  const int eyt_d = 8, eyt_u = 8 + mm.nd;
+  const int cum_d = ARTIS_MA_ACTION_COUNT, cum_u = ARTIS_MA_ACTION_COUNT + mm.nd;
   const int cum_drad = ARTIS_MA_ACTION_COUNT + mm.nd + mm.nu, cum_rrad = cum_drad + mm.nd;
   const int cum_rint = cum_rrad + mm.nr, cum_uhi = cum_rint + mm.nr;
-  const int32_t *inv_d = K.T.eyt_inv + K.T.eyt_off[mm.nd], *inv_u = K.T.eyt_inv + K.T.eyt_off[mm.nu];
   double pr[ARTIS_MA_ACTION_COUNT];
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) pr[a] = 0.;
   const double *popsT = K.C.popsT + k;  // popsT[u * nne_cells]: level u of this lane's cell
@@ -287,12 +286,12 @@ __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict_
         if (cache) {
           if (kind == MA_KIND_DOWN) {
             REC(cum_drad + j) = pr[ARTIS_MA_ACTION_RADDEEXC];
-            REC(eyt_d + inv_d[j]) = pr[ARTIS_MA_ACTION_INTERNALDOWNSAME];
+            REC(cum_d + j) = pr[ARTIS_MA_ACTION_INTERNALDOWNSAME];
           } else if (kind == MA_KIND_RECOMB) {
             REC(cum_rrad + j) = pr[ARTIS_MA_ACTION_RADRECOMB];
             REC(cum_rint + j) = pr[ARTIS_MA_ACTION_INTERNALDOWNLOWER];
           } else if (kind == MA_KIND_UP) {
-            REC(eyt_u + inv_u[j]) = pr[ARTIS_MA_ACTION_INTERNALUPSAME];
+            REC(cum_u + j) = pr[ARTIS_MA_ACTION_INTERNALUPSAME];
           } else {
             REC(cum_uhi + j) = pr[ARTIS_MA_ACTION_INTERNALUPHIGHER];
           }
@@ -322,6 +321,7 @@ __global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, const double *__
   const int64_t n_ne = K.C.n_nonempty;
   const MaMeta mm = K.T.ma_meta[ul];
   const int len = ARTIS_MA_ACTION_COUNT + 2 * mm.nd + mm.nu + 2 * mm.nr + mm.nt;
+  const MaLayout lay = ma_layout(mm.nd, mm.nu, mm.nr, mm.nt);
   const double *src = S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * n_ne;
   const int64_t c0 = (int64_t)blockIdx.x * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -359,8 +359,14 @@ __global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, const double *__
         if (c0 + j >= n_ne) break;
         const uint32_t key = (a < 0) ? s_akey[p][j] : ma_key32(tile[tx][j], s_norm[a][j]);
         uint16_t *rec = K.C.ma_key + (c0 + j) * K.C.ma_key_stride + mm.rec_off;
-        rec[p] = (uint16_t)(key >> 16);
-        rec[ma_lo_off(len) + p] = (uint16_t)(key & 0xffffu);
+        int sp;
+        const int rp = ma_rec_pos(lay, p, mm.nd, mm.nu, &sp);
+        rec[rp] = (uint16_t)(key >> 16);
+        rec[lay.hot + rp] = (uint16_t)(key & 0xffffu);
+        if (sp >= 0) {  // also a block separator on the record's first line
+          rec[sp] = (uint16_t)(key >> 16);
+          rec[lay.hot + sp] = (uint16_t)(key & 0xffffu);
+        }
       }
     }
   }
@@ -506,6 +512,7 @@ struct Engine {
   int npts_model = 0, nelements = 0, maxnions = 0, nions_total = 0, nlines = 0, ngrid = 0, ntstep = 0;
   int64_t n_est_doubles = 0;  // J..bfheat + scalars
   int64_t ma_key_stride = 0;          // 16-bit keys per cell block of the macro-atom cache
+  bool ma_cache_ok = true;             // the atomic data fit the cache's record layout (engine_dev.h ma_layout)
   std::vector<int64_t> h_dbl_off;     // per level: offset (doubles) of its exact sums in the k_marates scratch
   double *d_marec_scratch = nullptr;  // k_marates output, [position][cell] per level (k_mapack input)
   int64_t marec_scratch_doubles = 0;
@@ -905,6 +912,18 @@ int run_wavefront(int64_t n, int nts, double t2) {
               "%.0f, event %.0f\n",
               (double)st[32] / st[0], (double)st[33] / st[0], (double)st[34] / st[0], (double)st[35] / st[0],
               (double)st[36] / st[0]);
+#ifdef ARTIS_STAMPS
+    {
+      unsigned long long dg[48];
+      HIPCHK(hipMemcpyFromSymbol(dg, HIP_SYMBOL(g_ma_diag), sizeof(dg)));
+      for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++)
+        fprintf(stderr, "[artis_gpu] ma action %d: searches %llu, pending %llu, probes %llu\n", a, dg[a], dg[16 + a],
+                dg[32 + a]);
+    }
+#endif
+    if (st[41] + st[42] + st[43])
+      fprintf(stderr, "[artis_gpu] ma pass phases (cycles/pass): fetch %.0f, jump %.0f, rest %.0f\n",
+              (double)st[41] / st[4], (double)st[42] / st[4], (double)st[43] / st[4]);
   }
   return tcollect();
 }
@@ -1348,7 +1367,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   std::vector<MaMeta> mm(nl);
   std::vector<int64_t> dbl_off(nl + 1, 0);  // exact-sum scratch of k_marates (doubles, unpadded)
   int64_t marec = 0;
-  int nmax = 1;
+  bool ma_cache_ok = true;  // every level's same-ion arrays fit the two-level record layout
   for (int e = 0; e < ne; e++)
     for (int i = 0; i < a->elem_nions[e]; i++) {
       const int ui = a->elem_uniqueionoffset[e] + i;
@@ -1364,9 +1383,10 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
         m.base_lower = (i > 0) ? a->ion_uniqueleveloffset[ui - 1] : -1;
         m.rec_off = (int32_t)marec;
         const int64_t len = ARTIS_MA_ACTION_COUNT + 2 * (int64_t)m.nd + m.nu + 2 * (int64_t)m.nr + m.nt;
-        marec += (2 * len + 63) / 64 * 64;  // high then low key halves, records 128-byte aligned
+        // high then low key halves (engine_dev.h ma_layout), records 128-byte aligned
+        marec += (2 * (int64_t)ma_layout(m.nd, m.nu, m.nr, m.nt).hot + 63) / 64 * 64;
         dbl_off[ul + 1] = len;
-        nmax = std::max(nmax, std::max(m.nd, m.nu));
+        if (!ma_layout_ok(m.nd, m.nu)) ma_cache_ok = false;
       }
     }
   rc |= dupload(&T.ma_meta, mm.data(), nl);
@@ -1374,33 +1394,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   rc |= dupload(&T.ma_dbl_off, dbl_off.data(), nl + 1);
   G.h_dbl_off = dbl_off;
   {
-    // Eytzinger positions: in-order traversal of the implicit tree 1..n gives the sorted order
-    std::vector<int32_t> off(nmax + 2, 0), inv;
-    for (int n = 0; n <= nmax; n++) {
-      off[n] = (int32_t)inv.size();
-      std::vector<int32_t> pos(n + 1);
-      int next = 0;
-      std::vector<int> stack;
-      int k = 1;
-      while (k <= n || !stack.empty()) {  // iterative in-order walk
-        while (k <= n) {
-          stack.push_back(k);
-          k = 2 * k;
-        }
-        k = stack.back();
-        stack.pop_back();
-        pos[k] = next++;
-        k = 2 * k + 1;
-      }
-      std::vector<int32_t> iv(n);
-      for (int q = 1; q <= n; q++) iv[pos[q]] = q;
-      inv.insert(inv.end(), iv.begin(), iv.end());
-    }
-    off[nmax + 1] = (int32_t)inv.size();
-    if (inv.empty()) inv.push_back(0);
-    rc |= dupload(&T.eyt_inv, inv.data(), inv.size());
-    rc |= dupload(&T.eyt_off, off.data(), off.size());
-    // internal same-ion jump targets in the Eytzinger order of their cumulative arrays
+    // internal same-ion jump targets in the (reference) order of their cumulative arrays
     std::vector<int2> dt(std::max<int64_t>(ndown, 1)), ut(std::max<int64_t>(nup, 1));
     for (int e = 0; e < ne; e++)
       for (int i = 0; i < a->elem_nions[e]; i++) {
@@ -1411,18 +1405,19 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
           const MaMeta &m = mm[ul];
           for (int j = 0; j < m.nd; j++) {
             const int t = base + a->line_lowerlevelindex[a->downtrans_lineindex[m.doff + j]];
-            dt[m.doff + inv[off[m.nd] + j] - 1] = make_int2(t, mm[t].rec_off);
+            dt[m.doff + j] = make_int2(t, mm[t].rec_off);
           }
           for (int j = 0; j < m.nu; j++) {
             const int t = base + a->line_upperlevelindex[a->uptrans_lineindex[m.uoff + j]];
-            ut[m.uoff + inv[off[m.nu] + j] - 1] = make_int2(t, mm[t].rec_off);
+            ut[m.uoff + j] = make_int2(t, mm[t].rec_off);
           }
         }
       }
-    rc |= dupload(&T.down_target_eyt, dt.data(), dt.size());
-    rc |= dupload(&T.up_target_eyt, ut.data(), ut.size());
+    rc |= dupload(&T.down_target, dt.data(), dt.size());
+    rc |= dupload(&T.up_target, ut.data(), ut.size());
   }
   G.ma_key_stride = marec;
+  G.ma_cache_ok = ma_cache_ok;
   rc |= dupload(&T.allcont_nu_edge, a->allcont_nu_edge, nb);
   rc |= dupload(&T.allcont_probability, a->allcont_probability, nb);
   rc |= dupload(&T.allcont_element, a->allcont_element, nb);
@@ -1636,7 +1631,8 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     double budget = 0.5 * (double)freeb;
     if (const char *mx = getenv("ARTIS_GPU_MACACHE_MAX_GB")) budget = atof(mx) * (double)(1ull << 30);
     const char *env = getenv("ARTIS_GPU_NO_MACACHE");
-    if (!(env && env[0] == '1') && need + 8.0 * (double)scratch < budget) {
+    // (k_ma addresses the cache by 32-bit 128-byte line indices; every level must fit the record layout)
+    if (!(env && env[0] == '1') && G.ma_cache_ok && need / 128.0 < 4.0e9 && need + 8.0 * (double)scratch < budget) {
       void *mc = nullptr, *sc = nullptr;
       if (dmalloc(&mc, (size_t)need) == hipSuccess) {
         G.allocs.push_back(mc);

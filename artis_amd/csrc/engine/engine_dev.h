@@ -68,11 +68,9 @@ struct DevTab {
   // #recombination targets (ionising levels of the lower ion, 0 if the level does not recombine)
   const MaMeta *ma_meta;  // [nlevels_total]
   const int64_t *ma_dbl_off;  // [nlevels_total + 1] offset (doubles) of each level's exact record in k_marates' scratch
-  // targets of the internal same-ion jumps in Eytzinger order of their level's cumulative arrays:
-  // (unique level index, offset of its macro-atom record in a cell block)
-  const int2 *down_target_eyt, *up_target_eyt;
-  // Eytzinger position (1-based) of sorted index j in an array of n entries: eyt_inv[eyt_off[n] + j]
-  const int32_t *eyt_inv, *eyt_off;
+  // targets of the internal same-ion jumps in the order of their level's cumulative arrays (downtrans / uptrans
+  // order): (unique level index, offset of its macro-atom record in a cell block)
+  const int2 *down_target, *up_target;
   const double *allcont_nu_edge, *allcont_probability;
   const int32_t *allcont_element, *allcont_ion, *allcont_level, *allcont_target, *allcont_upperlevel,
       *allcont_phixstable, *allcont_groundindex;
@@ -93,8 +91,67 @@ struct DevTab {
   const double *g_endecay, *g_energy, *g_prob;
 };
 
-// offset (keys) of the low halves inside a macro-atom record of len positions (right after the high halves)
-static inline __host__ __device__ int ma_lo_off(int len) { return len; }
+// Record layout of the macro-atom key cache (DevCells::ma_key), in 16-bit key positions.  k_ma stages one 128-byte
+// line (64 positions) of a record per lane and pass, so the layout puts what most jumps need on the first line:
+//   line 0:  [0, 9) the action keys | [9, 9 + sd) down-same area | [9 + sd, 9 + sd + su) up-same area
+//   lines 1 .. nbd:            the down-same keys in 64-key blocks (only if the array does not fit its area)
+//   lines nbd + 1 .. nbd+nbu:  the up-same keys in 64-key blocks (likewise)
+//   from line 1 + nbd + nbu:   rad_deexc (nd) | rad_recomb (nr) | internal_down_lower (nr) | internal_up_higher (nt)
+// then the low halves of all positions (offset `hot`).  A same-ion array that fits its area (most levels) is
+// stored there whole; otherwise its area holds the last key of every block but the last (separators), so a search
+// reads line 0, then at most one block line: two passes.  The 55 area slots go to whichever array needs them.
+struct MaLayout {
+  int sd, su;    // line-0 slots of the down / up array (its keys, or its block separators)
+  int nbd, nbu;  // 64-key blocks of the down / up array outside line 0 (0: the array is on line 0)
+  int sorted0;   // record position of the first rad_deexc key
+  int hot;       // high-half positions = offset of the low halves
+};
+#define MA_AREA 55
+static inline __host__ __device__ MaLayout ma_layout(int nd, int nu, int nr, int nt) {
+  MaLayout L;
+  if (nd + nu <= MA_AREA) {
+    L.sd = nd;
+    L.su = nu;
+  } else if (nd <= MA_AREA / 2) {
+    L.sd = nd;
+    L.su = MA_AREA - nd;
+  } else if (nu <= MA_AREA / 2) {
+    L.su = nu;
+    L.sd = MA_AREA - nu;
+  } else {
+    L.sd = MA_AREA / 2;
+    L.su = MA_AREA - MA_AREA / 2;
+  }
+  L.nbd = nd > L.sd ? (nd + 63) / 64 : 0;
+  L.nbu = nu > L.su ? (nu + 63) / 64 : 0;
+  L.sorted0 = 64 * (1 + L.nbd + L.nbu);
+  L.hot = L.sorted0 + nd + 2 * nr + nt;
+  return L;
+}
+// a blocked array needs one separator slot per block but the last
+static inline __host__ __device__ bool ma_layout_ok(int nd, int nu) {
+  const MaLayout L = ma_layout(nd, nu, 0, 0);
+  return (L.nbd == 0 || L.nbd - 1 <= L.sd) && (L.nbu == 0 || L.nbu - 1 <= L.su);
+}
+// record position of scratch position p (k_marates order: [9 totals | down nd | up nu | the sorted arrays]);
+// *sep: the separator position on line 0 the key is also stored at, or -1
+static inline __host__ __device__ int ma_rec_pos(const MaLayout &L, int p, int nd, int nu, int *sep) {
+  *sep = -1;
+  if (p < 9) return p;
+  if (p < 9 + nd) {  // down-same key j
+    const int j = p - 9;
+    if (!L.nbd) return 9 + j;
+    if ((j & 63) == 63 && (j >> 6) < L.nbd - 1) *sep = 9 + (j >> 6);
+    return 64 * (1 + (j >> 6)) + (j & 63);
+  }
+  if (p < 9 + nd + nu) {  // up-same key j
+    const int j = p - 9 - nd;
+    if (!L.nbu) return 9 + L.sd + j;
+    if ((j & 63) == 63 && (j >> 6) < L.nbu - 1) *sep = 9 + L.sd + (j >> 6);
+    return 64 * (1 + L.nbd + (j >> 6)) + (j & 63);
+  }
+  return L.sorted0 + (p - 9 - nd - nu);
+}
 
 struct DevGeom {
   int32_t ncoordgrid[3];
@@ -132,7 +189,8 @@ struct DevCells {
   // half cannot decide a comparison).  A search compares the uniform draw with the keys; a key within rounding of
   // the draw leaves the comparison undecided and the jump is made with the exact sums (ma_jump_exact) -- the
   // selections are the reference's linear-scan choices either way.  The two arrays of the internal same-ion
-  // jumps (most jumps) come first, in Eytzinger (BFS) order:
+  // jumps (most jumps) come first, in Eytzinger (BFS) order, their top entries on the record's first line
+  // (ma_rec_pos above):
   //   [9 action keys | internal_down_same (nd, Eytzinger) | internal_up_same (nu, Eytzinger) | rad_deexc (nd) |
   //    rad_recomb (nr) | internal_down_lower (nr) | internal_up_higher (nt)]  high halves, then the same
   //   positions' low halves; the record padded to a multiple of 64 keys

@@ -57,6 +57,9 @@ struct Ctx {
 struct LocalCounters {
   unsigned long long *ctr;   // LDS [35]: 34 reference counters + nesc
   unsigned long long *work;  // LDS [16]
+#ifdef ARTIS_STAMPS
+  unsigned long long *diag = nullptr;  // diagnostic build: LDS [48] (k_ma)
+#endif
 };
 
 DEVFN void lctr(const LocalCounters &L, int c) { atomicAdd(&L.ctr[c], 1ull); }

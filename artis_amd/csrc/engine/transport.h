@@ -1045,7 +1045,7 @@ struct MaLane {
   unsigned long long ntrans;
 };
 enum { MA_CONTINUE = 0, MA_END_BB = 1, MA_END_COLDEEXC = 2, MA_END_COLRECOMB = 3, MA_END_FB = 4, MA_FAILED = -1,
-       MA_DEFER = -2 };
+       MA_DEFER = -2, MA_PENDING = -3 };
 // WaveState::pend code of a walk parked between jumps (.y = unique level it stands on): set when a jump of the
 // cached walk needs the exact sums (k_ma_exact), read when the walk resumes in k_ma
 #define MA_RESUME 16
@@ -1281,30 +1281,17 @@ DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &
 
 // The cached walk in its lean form: lane state = (unique level, record offset, cell key block).  Per jump: the
 // level's 32-byte MaMeta (L2-resident table) and its compact key record (DevCells::ma_key): the 9 action keys,
-// then for the internal same-ion jumps (most jumps) an Eytzinger search over the keys of the selected action
-// that stays in the record's first 128-byte line for typical levels, and one 8-byte load of the target
-// (level, record offset).  The walk is bound by the memory system's random-access rate: one HBM
-// line per jump instead of the three to four of full double records.  A comparison the 32-bit keys cannot
-// decide sends the jump to ma_jump_exact, which recomputes the reference's exact sums; the selections -- and so
-// the RNG draws and every result -- are those of the uncached ma_jump.
+// then a binary search over the keys of the selected action -- for the internal same-ion jumps (most jumps) on
+// the record's first 128-byte line, or via its separators there and one 64-key block line -- and one 8-byte load
+// of the target (level, record offset).  A comparison the 32-bit keys cannot decide sends the jump to
+// ma_jump_exact, which recomputes the reference's exact sums; the selections -- and so the RNG draws and every
+// result -- are those of the uncached ma_jump.
 struct MaLaneC {
   int ul, rec_off, k;
   const uint16_t *block;  // K.C.ma_key + k * ma_key_stride
   unsigned jumps;
   unsigned long long ntrans;
 };
-
-// Eytzinger (BFS-order) search: e[k], k = 1..n, holds the sorted array's entries in BFS order of its implicit
-// binary search tree.  Returns the Eytzinger position of the first sorted entry > x, 0 if none -- the same
-// entry first_above finds in the sorted array.
-DEVFN int eytzinger_first_above(const double *e, int n, double x, unsigned long long &probes) {
-  unsigned k = 1;
-  while (k <= (unsigned)n) {
-    k = 2 * k + (e[k] <= x ? 1u : 0u);
-    probes++;
-  }
-  return (int)(k >> __ffs(~k));
-}
 
 // the outcome of selecting transition j (reference list order) of action sel at level ul: MA_CONTINUE with the
 // lane moved to the target level, or a deactivation in `end` (macroatom.cc:174-414)
@@ -1436,117 +1423,199 @@ DEVNI int ma_jump_exact(const Ctx &K, const LocalCounters &L, artis_rng &rng, Ma
 // MA_DEFER: a key comparison was undecided; the jump has not happened (m.jumps unchanged) and the caller resets
 // the RNG counter to its value before the call and runs ma_jump_exact.
 // line != nullptr (k_ma): the lane's 128-byte LDS slot, laid out chunk-major for the wave ([8][64] 16-byte
-// chunks, lane-linear per chunk: conflict-free writes).  When the action keys and both same-ion trees fit the
-// record's first 128-byte line (9 + nd + nu <= 64, ~99% of levels), the line is fetched with 8 independent
-// 16-byte loads, staged there, and the tree search probes LDS instead of making one dependent trip to the
-// cache hierarchy per tree level.
+// chunks, lane-linear per chunk), already holding the first line of the record (positions 0..63: the action keys
+// and, for ~99% of levels, both same-ion trees), fetched for the whole wave by ma_fetch_lines; the tree search
+// then probes LDS instead of making one dependent trip to the cache hierarchy per tree level.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4 lds_uint4;
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 typedef const __attribute__((address_space(1))) u32x4 glb_uint4;
-DEVFN int ma_jump_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneC &m, MaEnd &end, int number,
-                         lds_uint4 *line = nullptr) {
-  const int ul = m.ul;
+
+// Wave-cooperative fetch of one 128-byte line per lane (line index `myline` in units of 128 bytes from `base`,
+// 0xffffffff: none) into the wave's chunk-major LDS image wl[chunk * 64 + lane].  Instruction i has lanes
+// 8j..8j+7 read the eight 16-byte chunks of the line of lane 8i + j, so each load instruction touches 8 lines
+// instead of 64.  The memory system's rate is set by the (instruction, line) pairs it serves: random 128-byte
+// lines fetched this way arrive at 45 G lines/s (5.8 TB/s) on MI355X against 9.7 G lines/s (1.24 TB/s) when every
+// lane loads its own line (tools/linerate.hip, profiles/r02_linerate.txt).  Wave-uniform control flow only.
+struct WaveLines {
+  u32x4 c[8];
+};
+// xi: the wave's 64-word LDS exchange slot for the line indices (lane L's index at (L & 7) * 8 + (L >> 3), so
+// that the eight indices a lane loads for are contiguous: one write, two 16-byte reads, one wait)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+DEVFN void wave_fetch_issue(const void *base, uint32_t myline, WaveLines &w, lds_u32 *xi) {
+  const int lane = (int)__lane_id();
+  glb_uint4 *g = (glb_uint4 *)base;
+  xi[(lane & 7) * 8 + (lane >> 3)] = myline;
+  __builtin_amdgcn_wave_barrier();
+  const u32x4 i0 = ((lds_uint4 *)xi)[2 * (lane >> 3)], i1 = ((lds_uint4 *)xi)[2 * (lane >> 3) + 1];
+  const uint32_t ls[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    w.c[i] = g[(size_t)(ls[i] == 0xffffffffu ? 0u : ls[i]) * 8 + (lane & 7)];  // idle lanes: a harmless line-0 read
+}
+DEVFN void wave_fetch_commit(const WaveLines &w, lds_uint4 *wl) {
+  const int lane = (int)__lane_id();
+#pragma unroll
+  for (int i = 0; i < 8; i++) wl[(lane & 7) * 64 + 8 * i + (lane >> 3)] = w.c[i];  // idle lanes' slots: unread
+  __builtin_amdgcn_wave_barrier();
+}
+
+// a load through the global address space (global_load, counted by vmcnt only; a flat load also holds lgkmcnt)
+template <typename T>
+DEVFN T gload(const T *p) {
+  return *(const __attribute__((address_space(1))) T *)p;
+}
+
+// the level's MaMeta words the cached walk reads: (rec_off, doff, uoff, base_lower), (nd, nu, nr, nt)
+struct MaMetaW {
+  int4 w0, w1;
+};
+DEVFN MaMetaW ma_meta_load(const Ctx &K, int ul) {
+  glb_uint4 *mp = (glb_uint4 *)(K.T.ma_meta + ul);
+  const u32x4 a = mp[0], b = mp[1];
+  return MaMetaW{make_int4((int)a.x, (int)a.y, (int)a.z, (int)a.w), make_int4((int)b.x, (int)b.y, (int)b.z, (int)b.w)};
+}
+
+// The cached walk as a resumable per-pass step (k_ma).  In SIMT every pass of a wave lasts as long as its slowest
+// lane; a search that probed record lines other than the staged one made one dependent trip to memory per probe,
+// and nearly every pass of a 64-lane wave waited for some lane doing that (profiles/r02_ma_phase_stamps.txt).
+// Here a search that needs a line other than the one staged in the lane's LDS slot stops (MA_PENDING) and names
+// that line (pline); the next pass fetches it with everybody else's lines (wave_fetch_issue) and the search
+// resumes where it stopped.  With the two-level record layout (engine_dev.h ma_layout) a jump needs at most two
+// lines.  Every comparison is decided exactly as by ma_key_cmp, so the selections -- and every result -- are the
+// uncached walk's.
+//
+// Key comparisons in integers: qh = the high 16 bits of floor(q).  A key whose high half is below qh lies at
+// least 1 below q (decided "not greater"); above qh + 1, at least 65536 above q (decided "greater"); only a high
+// half of qh or qh + 1 needs the low half and the banded comparison ma_key_cmp (~2 in 65536 comparisons).
+DEVFN uint32_t ma_qh(double q) { return ((uint32_t)q) >> 16; }
+
+#ifdef ARTIS_STAMPS
+// diagnostic build: per selected action, [a] searches, [16 + a] MA_PENDING returns, [32 + a] probes
+__device__ unsigned long long g_ma_diag[48];
+#define MA_DIAG(i)                             \
+  do {                                         \
+    if (L.diag) atomicAdd(&L.diag[i], 1ull); \
+  } while (0)
+#else
+#define MA_DIAG(i) \
+  do {             \
+  } while (0)
+#endif
+
+struct MaLaneR : MaLaneC {
+  uint32_t n0;         // RNG counter at the start of the jump in progress (the caller's reset point for MA_DEFER)
+  int sel;             // -1: the next step starts a jump; otherwise the action whose transition search is pending
+  int pline;           // record line (64 key positions) staged for this step
+  int lo, hi, end;     // binary search in progress over entries [lo, hi) of a range of `end` entries ...
+  int base;            // ... at record positions base + i
+  int blk;             // same-ion array in blocks: -1 while its separators are searched, then the block
+  double q2;           // the transition draw on the key scale
+  uint32_t q2h;
+};
+
+// where a step reads record keys (high halves): k_ma's staged line, or the whole record in global memory
+struct KeysLds {
+  lds_uint4 *line;
+  int pl;
+  DEVFN bool has(int p) const { return (p >> 6) == pl; }
+  DEVFN uint32_t hi(int p) const { return (uint32_t)((lds_u16 *)(line + ((p & 63) >> 3) * 64))[p & 7]; }
+};
+struct KeysGlobal {
+  const uint16_t *rec;
+  DEVFN bool has(int) const { return true; }
+  DEVFN uint32_t hi(int p) const { return (uint32_t)gload(rec + p); }
+};
+
+// meta: the level's MaMetaW (k_ma loads it beside the record-line fetch); z1, z2: the values of the lane's next two
+// draws (used only by a step that starts a jump; the RNG counter advances over the draws the jump consumes)
+template <class Keys>
+DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneR &m, MaEnd &end, int number,
+                         const Keys &keys, const MaMetaW &meta, double z1, double z2) {
   const uint16_t *rec = m.block + m.rec_off;
-  const int4 *mp = reinterpret_cast<const int4 *>(K.T.ma_meta + ul);
-  const int4 w0 = mp[0], w1 = mp[1];
-  const int doff = w0.y, uoff = w0.z, base_lower = w0.w, nd = w1.x, nu = w1.y, nr = w1.z, nt = w1.w;
-  const bool staged = line != nullptr && ARTIS_MA_ACTION_COUNT + nd + nu <= 64;
-  if (staged) {
-    glb_uint4 *src = (glb_uint4 *)rec;
-    const u32x4 c0 = src[0], c1 = src[1], c2 = src[2], c3 = src[3], c4 = src[4], c5 = src[5], c6 = src[6],
-                c7 = src[7];
-    line[0] = c0;
-    line[64] = c1;
-    line[128] = c2;
-    line[192] = c3;
-    line[256] = c4;
-    line[320] = c5;
-    line[384] = c6;
-    line[448] = c7;
-  }
-  auto hot = [&](int p) -> uint32_t {
-    return (staged && p < 64) ? (uint32_t)((lds_u16 *)(line + (p >> 3) * 64))[p & 7] : (uint32_t)rec[p];
+  const int doff = meta.w0.y, uoff = meta.w0.z, base_lower = meta.w0.w;
+  const int nd = meta.w1.x, nu = meta.w1.y, nr = meta.w1.z, nt = meta.w1.w;
+  const MaLayout lay = ma_layout(nd, nu, nr, nt);
+  auto cmp = [&](int p, uint32_t hi, double q, uint32_t qh) -> int {
+    if (hi < qh) return -1;
+    if (hi > qh + 1) return 1;
+    return ma_key_cmp((hi << 16) | (uint32_t)gload(rec + lay.hot + p), q);
   };
-  const int loff = ma_lo_off(ARTIS_MA_ACTION_COUNT + 2 * nd + nu + 2 * nr + nt);  // low halves
-  const u32x4 a8 = staged ? line[0] : *(glb_uint4 *)rec;  // action keys 0..7 (records are 128-byte aligned)
-  const uint32_t key8 = hot(8);
-  const double zrand = artis_rng_uniform(&rng);
-  const double q = zrand * MA_KEY_SCALE;
-  // high half first; the low half only when needed; undecided at 32 bits: park the jump (MA_DEFER)
-  auto cmp = [&](int p, uint32_t hi) {
-    const int c = ma_key_cmp_hi(hi, q);
-    return c != 2 ? c : ma_key_cmp((hi << 16) | rec[loff + p], q);
-  };
-  int sel = -1;
-  {
+  if (m.sel < 0) {  // a new jump: the action is the first of the 9 running-sum keys (line 0) above q
+    m.n0 = rng.n;
+    const double q = z1 * MA_KEY_SCALE;
+    const uint32_t qh = ma_qh(q);
+    rng.n++;
+    uint32_t hk[ARTIS_MA_ACTION_COUNT];
+    int nless = 0, nund = 0;
 #pragma unroll
     for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
-      const uint32_t wd = (a < 2) ? a8.x : (a < 4) ? a8.y : (a < 6) ? a8.z : a8.w;
-      const uint32_t hi = (a < 8) ? (wd >> (16 * (a & 1))) & 0xffffu : key8;
-      const int c = cmp(a, hi);
-      if (c > 0) {
-        sel = a;
-        break;
+      hk[a] = keys.hi(a);
+      nless += hk[a] < qh ? 1 : 0;
+      nund += (hk[a] - qh) <= 1u ? 1 : 0;
+    }
+    int sel = -1;
+    if (nund == 0) {  // the keys are non-decreasing: the first nless are decided below q, the next above
+      if (nless < ARTIS_MA_ACTION_COUNT) sel = nless;
+    } else {
+      for (int a = nless; a < ARTIS_MA_ACTION_COUNT; a++) {
+        const int c = cmp(a, hk[a], q, qh);
+        if (c > 0) {
+          sel = a;
+          break;
+        }
+        if (c == 0) break;
       }
-      if (c == 0) break;
     }
-  }
-  if (sel < 0) return MA_DEFER;
-  m.jumps++;
-  if (sel == ARTIS_MA_ACTION_COLDEEXC || sel == ARTIS_MA_ACTION_COLRECOMB) {
-    end.code = (sel == ARTIS_MA_ACTION_COLDEEXC) ? MA_END_COLDEEXC : MA_END_COLRECOMB;
-    end.ion = end.a = end.b = 0;
-    return end.code;
-  }
-  if (sel == ARTIS_MA_ACTION_INTERNALUPHIGHERNT) return ma_apply_nt(K, L, rng, m, number);
-  const double zr = artis_rng_uniform(&rng);
-  const double q2 = zr * MA_KEY_SCALE;
-  auto cmp2 = [&](int p) {
-    const uint32_t hi = hot(p);
-    const int c = ma_key_cmp_hi(hi, q2);
-    return c != 2 ? c : ma_key_cmp((hi << 16) | rec[loff + p], q2);
-  };
-  if (sel == ARTIS_MA_ACTION_INTERNALDOWNSAME || sel == ARTIS_MA_ACTION_INTERNALUPSAME) {
-    const bool down = sel == ARTIS_MA_ACTION_INTERNALDOWNSAME;
-    const int cnt = down ? nd : nu;
-    const int e0 = ARTIS_MA_ACTION_COUNT - 1 + (down ? 0 : nd);  // e[k] at position e0 + k, k = 1..cnt
-    unsigned kk = 1;
-    while (kk <= (unsigned)cnt) {
-      const int c = cmp2(e0 + (int)kk);
-      m.ntrans++;
-      if (c == 0) {
-        m.jumps--;
-        return MA_DEFER;
-      }
-      kk = 2 * kk + (c < 0 ? 1u : 0u);
+    if (sel < 0) return MA_DEFER;
+    m.jumps++;
+    if (sel == ARTIS_MA_ACTION_COLDEEXC || sel == ARTIS_MA_ACTION_COLRECOMB) {
+      end.code = (sel == ARTIS_MA_ACTION_COLDEEXC) ? MA_END_COLDEEXC : MA_END_COLRECOMB;
+      end.ion = end.a = end.b = 0;
+      return end.code;
     }
-    const int pos = (int)(kk >> __ffs(~kk));
-    if (pos == 0) {
-      fail(K, ERR_MA_SELECT, number, 10 + sel);
-      return MA_FAILED;
+    if (sel == ARTIS_MA_ACTION_INTERNALUPHIGHERNT) return ma_apply_nt(K, L, rng, m, number);
+    m.q2 = z2 * MA_KEY_SCALE;
+    m.q2h = ma_qh(m.q2);
+    rng.n++;
+    m.sel = sel;
+    MA_DIAG(sel);
+    m.lo = 0;
+    m.blk = -1;
+    if (sel == ARTIS_MA_ACTION_INTERNALDOWNSAME || sel == ARTIS_MA_ACTION_INTERNALUPSAME) {
+      const bool down = sel == ARTIS_MA_ACTION_INTERNALDOWNSAME;
+      const int nb = down ? lay.nbd : lay.nbu;
+      m.base = down ? 9 : 9 + lay.sd;
+      m.end = nb ? nb - 1 : (down ? nd : nu);  // the separators, or the whole array
+    } else {
+      m.base = lay.sorted0 + ((sel == ARTIS_MA_ACTION_RADDEEXC)            ? 0
+                              : (sel == ARTIS_MA_ACTION_RADRECOMB)         ? nd
+                              : (sel == ARTIS_MA_ACTION_INTERNALDOWNLOWER) ? nd + nr
+                                                                           : nd + 2 * nr);  // INTERNALUPHIGHER
+      m.end = (sel == ARTIS_MA_ACTION_RADDEEXC) ? nd : (sel == ARTIS_MA_ACTION_INTERNALUPHIGHER) ? nt : nr;
     }
-    const int2 t = down ? K.T.down_target_eyt[doff + pos - 1] : K.T.up_target_eyt[uoff + pos - 1];
-    m.ul = t.x;
-    m.rec_off = t.y;
-    return MA_CONTINUE;
+    m.hi = m.end;
   }
-  // the sorted key arrays after the two Eytzinger ones
-  const int sorted = ARTIS_MA_ACTION_COUNT + nd + nu;
-  int off, cnt;
-  switch (sel) {
-    case ARTIS_MA_ACTION_RADDEEXC: off = 0; cnt = nd; break;
-    case ARTIS_MA_ACTION_RADRECOMB: off = nd; cnt = nr; break;
-    case ARTIS_MA_ACTION_INTERNALDOWNLOWER: off = nd + nr; cnt = nr; break;
-    default: off = nd + 2 * nr; cnt = nt; break;  // INTERNALUPHIGHER
-  }
-  int lo = 0, hi = cnt;
+  // binary search for the first entry above q2, resumed where it stopped
+  int lo = m.lo, hi = m.hi;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
-    const int c = cmp2(sorted + off + mid);
+    const int p = m.base + mid;
+    if (!keys.has(p)) {
+      m.lo = lo;
+      m.hi = hi;
+      m.pline = p >> 6;
+      MA_DIAG(16 + m.sel);
+      return MA_PENDING;
+    }
+    MA_DIAG(32 + m.sel);
+    const int c = cmp(p, keys.hi(p), m.q2, m.q2h);
     m.ntrans++;
     if (c == 0) {
       m.jumps--;
+      m.sel = -1;
+      m.pline = 0;
       return MA_DEFER;
     }
     if (c > 0)
@@ -1554,11 +1623,62 @@ DEVFN int ma_jump_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
     else
       lo = mid + 1;
   }
-  if (lo >= cnt) {
+  const int sel = m.sel;
+  if (sel == ARTIS_MA_ACTION_INTERNALDOWNSAME || sel == ARTIS_MA_ACTION_INTERNALUPSAME) {
+    const bool down = sel == ARTIS_MA_ACTION_INTERNALDOWNSAME;
+    const int cnt = down ? nd : nu, nb = down ? lay.nbd : lay.nbu;
+    if (nb && m.blk < 0) {  // separators searched: the key is in block lo (the last if no separator is above q2)
+      m.blk = lo;
+      m.base = 64 * (1 + (down ? 0 : lay.nbd) + lo);
+      m.lo = 0;
+      m.end = m.hi = min(64, cnt - 64 * lo);
+      m.pline = m.base >> 6;
+      MA_DIAG(16 + sel);
+      return MA_PENDING;
+    }
+    const int j = (m.blk >= 0 ? 64 * m.blk : 0) + lo;
+    const bool found = lo < m.end;
+    m.sel = -1;
+    m.pline = 0;
+    if (!found) {
+      fail(K, ERR_MA_SELECT, number, 10 + sel);
+      return MA_FAILED;
+    }
+    typedef const __attribute__((address_space(1))) uint64_t glb_u64;
+    const uint64_t tw = *(glb_u64 *)(down ? K.T.down_target + doff + j : K.T.up_target + uoff + j);
+    m.ul = (int)(uint32_t)tw;
+    m.rec_off = (int)(uint32_t)(tw >> 32);
+    return MA_CONTINUE;
+  }
+  const bool found = lo < m.end;
+  m.sel = -1;
+  m.pline = 0;
+  if (!found) {
     fail(K, ERR_MA_SELECT, number, 10 + sel);
     return MA_FAILED;
   }
   return ma_apply_selection(K, L, m, end, sel, lo, doff, uoff, base_lower);
+}
+
+// One whole jump of the cached walk from the record in global memory (the megakernel's do_macroatom): the step
+// never waits for a line, so it runs to the end of the jump (the block of a two-level array: a second call).
+DEVFN int ma_jump_cached_global(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneC &mc, MaEnd &end,
+                                int number) {
+  artis_rng r2 = rng;
+  const double z1 = artis_rng_uniform(&r2), z2 = artis_rng_uniform(&r2);
+  MaLaneR m;
+  static_cast<MaLaneC &>(m) = mc;
+  m.sel = -1;
+  m.pline = 0;
+  const MaMetaW meta = ma_meta_load(K, m.ul);
+  const KeysGlobal keys{m.block + m.rec_off};
+  int r;
+  do {
+    r = ma_step_cached(K, L, rng, m, end, number, keys, meta, z1, z2);
+  } while (r == MA_PENDING);
+  if (r == MA_DEFER) rng.n = m.n0;
+  mc = static_cast<MaLaneC &>(m);
+  return r;
 }
 
 DEVFN void ma_lane_init(const Ctx &K, MaLane &m, int where, int element, int ion, int level) {
@@ -1666,7 +1786,7 @@ DEVNI void do_macroatom(Tx &x, Pkt &p) {
     const double t_mid = K.G.ts_mid[x.nts];
     while (true) {
       const uint32_t n0 = x.rng.n;
-      r = ma_jump_cached(K, x.L, x.rng, m, e, p.number);
+      r = ma_jump_cached_global(K, x.L, x.rng, m, e, p.number);
       if (r == MA_DEFER) {
         x.rng.n = n0;
         r = ma_jump_exact(K, x.L, x.rng, m, e, p.number, t_mid);

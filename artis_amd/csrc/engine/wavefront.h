@@ -305,6 +305,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   // per wave: the 128-byte hot line of each lane's current macro-atom record (ma_jump_cached), chunk-major
   __shared__ uint4 s_line[WAVE_BLOCK / 64][8 * 64];
+  __shared__ uint32_t s_xidx[WAVE_BLOCK / 64][64];  // line indices exchanged for the cooperative fetch
   block_counters_init(s_ctr, s_work);
   LocalCounters L;
   L.ctr = &s_ctr[0];
@@ -315,7 +316,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   const int nr = W.ma_ranges;
   const double t_mid = K.G.ts_mid[nts];
   MaLane m;    // uncached walk
-  MaLaneC mc;  // cached walk
+  MaLaneR mc;  // cached walk (resumable steps)
   artis_rng rng = artis_rng_init(K.R.seed, 0, nts, K.R.rank);
   int32_t idx = -1;
   bool have = false, drained = false;
@@ -323,6 +324,13 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   bool pendR = false, pendK = false, pendX = false;
   unsigned long long jumps_sum = 0, trans_sum = 0;
   unsigned long long st_pass = 0, st_busy = 0, st_refill = 0, st_trefill = 0, st_tstep = 0;
+#ifdef ARTIS_STAMPS
+  unsigned long long ma_st[3] = {0, 0, 0};
+  __shared__ unsigned long long s_diag[48];
+  for (int j = threadIdx.x; j < 48; j += blockDim.x) s_diag[j] = 0;
+  __syncthreads();
+  L.diag = s_diag;
+#endif
   const unsigned long long st_t0 = wave_clock();
   while (true) {
     const bool idle = !have && !drained;
@@ -360,6 +368,8 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
             mc.k = K.C.ne_index[mgi];
             mc.block = K.C.ma_key + (int64_t)mc.k * K.C.ma_key_stride;
             mc.ntrans = 0;
+            mc.sel = -1;
+            mc.pline = 0;
           } else {
             ma_lane_init(K, m, where, lo32(w36), hi32(w36), lo32(w37));
           }
@@ -383,18 +393,50 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     st_pass++;
     st_busy += __popcll(__ballot(have));
     const unsigned long long ts0 = wave_clock();
+    MaMetaW meta;
+    double z1 = 0., z2 = 0.;
+    if constexpr (CACHE) {
+      // the level's metadata and, 8 lines per load instruction, every busy lane's record line; the lane's next two
+      // draws are computed while they are in flight
+      if (have) meta = ma_meta_load(K, mc.ul);
+      const uint32_t myline =
+          have ? (uint32_t)(((uint64_t)(mc.block - K.C.ma_key) + (uint64_t)mc.rec_off) >> 6) + (uint32_t)mc.pline
+               : 0xffffffffu;
+      WaveLines wl;
+      wave_fetch_issue(K.C.ma_key, myline, wl, (lds_u32 *)&s_xidx[threadIdx.x >> 6][0]);
+      if (have && mc.sel < 0) {
+#ifdef ARTIS_DIAG_CHEAPRNG  // timing diagnostic only (wrong stream): the walk's cost without Philox
+        uint64_t h = ((uint64_t)rng.key1 << 32) ^ rng.n;
+        h = (h ^ (h >> 30)) * 0xbf58476d1ce4e5b9ull;
+        h = (h ^ (h >> 27)) * 0x94d049bb133111ebull;
+        z1 = (double)(h >> 11) * (1.0 / 9007199254740992.0);
+        z2 = (double)((h * 0x9E3779B97F4A7C15ull) >> 11) * (1.0 / 9007199254740992.0);
+#else
+        artis_rng r2 = rng;
+        z1 = artis_rng_uniform(&r2);
+        z2 = artis_rng_uniform(&r2);
+#endif
+      }
+      wave_fetch_commit(wl, line - (threadIdx.x & 63));
+    }
+#ifdef ARTIS_STAMPS
+    const unsigned long long ts1 = wave_clock();
+    unsigned long long ts2 = ts1;
+#endif
     if (have) {
       MaEnd e;
       int r;
       unsigned jumps;
       if constexpr (CACHE) {
-        const uint32_t n0 = rng.n;
-        r = ma_jump_cached(K, L, rng, mc, e, (int)rng.key1, line);
+        r = ma_step_cached(K, L, rng, mc, e, (int)rng.key1, KeysLds{line, mc.pline}, meta, z1, z2);
+#ifdef ARTIS_STAMPS
+        ts2 = wave_clock();
+#endif
         jumps = mc.jumps;
         if (r == MA_DEFER) {  // park the walk before this jump; k_ma_exact makes it with the exact sums
           W.pend[idx] = make_int4(MA_RESUME, mc.ul, 0, 0);
           W.pend_jumps[idx] = jumps;
-          W.rng_n[idx] = n0;
+          W.rng_n[idx] = mc.n0;
           trans_sum += mc.ntrans;
           pendX = true;
           have = false;
@@ -403,7 +445,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
         r = ma_jump(K, L, rng, m, t_mid, e, (int)rng.key1);
         jumps = m.jumps;
       }
-      if (have && (r != MA_CONTINUE || jumps >= MA_MAX_JUMPS)) {
+      if (have && r != MA_PENDING && (r != MA_CONTINUE || jumps >= MA_MAX_JUMPS)) {
         if (r == MA_CONTINUE) fail(K, ERR_STUCK, (int)rng.key1, 2);
         if (r > 0) {
           W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
@@ -421,7 +463,24 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
       }
     }
     st_tstep += wave_clock() - ts0;
+#ifdef ARTIS_STAMPS
+    // k_ma phases (cycles per pass): fetch (metadata + record lines in LDS), jump, the rest of the pass
+    {
+      unsigned long long t2max = ts2;
+      for (int off = 32; off > 0; off >>= 1) t2max = max(t2max, (unsigned long long)__shfl_xor((long long)t2max, off, 64));
+      ma_st[0] += ts1 - ts0;
+      ma_st[1] += t2max - ts1;
+      ma_st[2] += wave_clock() - t2max;
+    }
+#endif
   }
+#ifdef ARTIS_STAMPS
+  if (lane_id() == 0)
+    for (int i = 0; i < 3; i++) atomicAdd(&W.stats[41 + i], ma_st[i]);
+  __syncthreads();
+  for (int j = threadIdx.x; j < 48; j += blockDim.x)
+    if (s_diag[j]) atomicAdd(&g_ma_diag[j], s_diag[j]);
+#endif
   wave_stats_flush(W, 1, st_pass, st_busy, st_t0, st_refill, st_trefill, st_tstep);
   if (jumps_sum) atomicAdd(&s_work[WK_MA_JUMPS], jumps_sum);
   if (trans_sum) atomicAdd(&s_work[WK_MA_TRANS], trans_sum);
