@@ -372,6 +372,24 @@ __global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, const double *__
   }
 }
 
+// DevCells::linecoef: the Sobolev coefficient (B_lu n_l - B_ul n_u) * HCLIGHTOVERFOURPI of every line in every
+// non-empty cell, in get_event's operation order (rpkt.cc:168-187); lanes run along a cell's row (coalesced
+// writes, line records from L2, population gathers from the cell's 29 kB row)
+__global__ __launch_bounds__(256) void k_linecoef(Ctx K) {
+  const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= K.C.linecoef_stride) return;
+  for (int k = blockIdx.y; k < K.C.n_nonempty; k += gridDim.y) {
+    double v = 0.;
+    if (li < K.T.nlines) {
+      const LineTau r = K.T.line_tau[li];
+      const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
+      const double n_u = pops[r.ul_upper], n_l = pops[r.ul_lower];
+      v = (r.B_lu * n_l - r.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI;
+    }
+    K.C.linecoef[(int64_t)k * K.C.linecoef_stride + li] = v;
+  }
+}
+
 // out[c * rows + r] = in[r * cols + c], through a 64x64 LDS tile (one wave reads rows, writes columns)
 __global__ __launch_bounds__(256) void k_transpose(const double *__restrict__ in, double *__restrict__ out,
                                                    int64_t rows, int64_t cols) {
@@ -404,7 +422,7 @@ __global__ void k_soa_to_aos(const uint64_t *__restrict__ soa, uint64_t *__restr
 #define TRANSPORT_BLOCK 256
 __global__ __launch_bounds__(TRANSPORT_BLOCK) void k_transport(const Ctx *__restrict__ ctxp, uint64_t *__restrict__ soa, int64_t n, int nts,
                                                               double t2) {
-  const Ctx &K = *ctxp;
+  CTX_IN_LDS(ctxp)
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   __shared__ double s_cmflum[TRANSPORT_BLOCK / 64];
@@ -1328,6 +1346,11 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   rc |= dupload(&T.phixstarget_probability, a->phixstarget_probability, ntg);
   rc |= dupload(&T.phixs_xs, a->phixs_xs, (size_t)ntables * a->nphixspoints);
   rc |= dupload(&T.line_nu, a->line_nu, nli);
+  {
+    std::vector<double> nu8((size_t)(nli + 7) / 8 * 8 + 8, 0.);
+    std::copy(a->line_nu, a->line_nu + nli, nu8.begin());
+    rc |= dupload(&T.line_nu8, nu8.data(), nu8.size());
+  }
   rc |= dupload(&T.line_A, a->line_einstein_A, nli);
   rc |= dupload(&T.line_f, a->line_osc_strength, nli);
   rc |= dupload(&T.line_coll, a->line_coll_str, nli);
@@ -1647,6 +1670,23 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     }
   }
   if (!C.have_macache) rc |= dalloc(&C.marates, (size_t)nne_cells * nl * ARTIS_MA_ACTION_COUNT);
+  // per-cell line coefficients for the r-packet line walk: at most 30% of the HBM still free (the packet store
+  // comes later), ARTIS_GPU_NO_LINECOEF=1 switches them off
+  C.linecoef = nullptr;
+  C.linecoef_stride = ((int64_t)G.K.T.nlines + 7) / 8 * 8;
+  {
+    size_t freeb = 0, totalb = 0;
+    (void)hipMemGetInfo(&freeb, &totalb);
+    const double need = (double)nne_cells * (double)C.linecoef_stride * 8.0;
+    const char *env = getenv("ARTIS_GPU_NO_LINECOEF");
+    if (!(env && env[0] == '1') && nne_cells > 0 && need < 0.3 * (double)freeb) {
+      void *lc = nullptr;
+      if (dmalloc(&lc, (size_t)need) == hipSuccess) {
+        G.allocs.push_back(lc);
+        C.linecoef = (double *)lc;
+      }
+    }
+  }
   // cell-state input buffers
   rc |= dalloc(&G.W.ctr, (size_t)NQUEUES * 2);
   rc |= dalloc(&G.d_ctx, (size_t)1);
@@ -1834,6 +1874,9 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
     if (ntg > 0)
       k_transpose<<<dim3((unsigned)((ntg + 63) / 64), (unsigned)((n_ne + 63) / 64)), 256, 0, G.stream>>>(
           G.K.C.corrphot, G.K.C.corrphotT, n_ne, ntg);
+    if (G.K.C.linecoef)
+      k_linecoef<<<dim3((unsigned)((G.K.C.linecoef_stride + 255) / 256), (unsigned)std::min(n_ne, 32768)), 256, 0,
+                    G.stream>>>(G.K);
     if (!G.K.C.have_macache) {
       k_marates<<<(unsigned)((nlv + 255) / 256), 256, 0, G.stream>>>(G.K, nts, 0, (int)nl, nullptr);
     } else {

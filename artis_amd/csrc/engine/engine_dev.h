@@ -59,6 +59,7 @@ struct DevTab {
   const double *phixstarget_probability;
   const float *phixs_xs;
   const double *line_nu;
+  const double *line_nu8;  // line_nu padded with zeros to a multiple of 8 (64-byte windows of the line walk)
   const float *line_A, *line_f, *line_coll;
   const int32_t *line_elem, *line_ion, *line_upper, *line_lower;
   const uint8_t *line_forbidden;
@@ -181,6 +182,11 @@ struct DevCells {
   double *popsT;       // [nlevels_total * n_nonempty]
   double *corrphotT;   // [ntargets_total * n_nonempty]
   double *cooling;     // [n_nonempty * ncoolingterms]  cumulative cooling_contrib (kpkt.cc:167-308)
+  // Sobolev coefficient of every line in every cell, (B_lu n_l - B_ul n_u) * HCLIGHTOVERFOURPI (rpkt.cc:168-187;
+  // tau_line = coefficient * t), rows padded to linecoef_stride = nlines rounded up to 8; nullptr when it does not
+  // fit the HBM budget (the line walk then gathers the two populations per line itself)
+  double *linecoef;    // [n_nonempty * linecoef_stride]
+  int64_t linecoef_stride;
   // macro-atom cache: per (cell, level) one compact record of 32-bit keys, 128-byte aligned.  A key is a running
   // sum of the reference's individual rates (the cellhistory individ_* arrays, globals.h:174-183, summed in the
   // reference's order, macroatom.cc:57-159) divided by its action's total and rounded to 32 bits; the first 9 are

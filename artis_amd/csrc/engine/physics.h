@@ -39,7 +39,7 @@ enum : int32_t {
   ERR_VPKT_OVERFLOW = 15,  // the virtual-packet spawn buffer of one event round is full
 };
 
-struct Ctx {
+struct __attribute__((aligned(16))) Ctx {
   DevTab T;
   DevGeom G;
   DevCells C;
@@ -48,11 +48,19 @@ struct Ctx {
   DevVpkt V;
 };
 
-// The transport kernels read the context through a pointer to a device copy (engine.hip: sync_ctx) rather
-// than from a by-value kernel argument: the rare-event code is noinline and receives `const Ctx &`, and a
-// reference to a by-value kernel argument forces the whole 1 KB context into per-lane scratch, turning every
-// table-pointer read in the hot loops into a scratch load.  Through a __restrict__ pointer the reads stay
-// uniform scalar loads.
+// The transport kernels receive the context as a pointer to a device copy (engine.hip: sync_ctx) rather than
+// as a by-value kernel argument: the rare-event code is noinline and receives `const Ctx &`, and a reference to a
+// by-value kernel argument forces the whole context into per-lane scratch.  Read through that pointer, though,
+// every field is a vector load from memory, repeated after any store of the kernel (the compiler cannot prove
+// the stores leave the context unchanged): two dependent trips to memory per table access in the hot loops.  So
+// each block first copies the context into LDS (CTX_IN_LDS) and works on that copy: a field read is an LDS read.
+static_assert(sizeof(Ctx) % 16 == 0, "Ctx is copied in 16-byte chunks");
+#define CTX_IN_LDS(ctxp)                                                                  \
+  __shared__ Ctx s_ctx_;                                                                  \
+  for (int i_ = threadIdx.x; i_ < (int)(sizeof(Ctx) / 16); i_ += blockDim.x)             \
+    reinterpret_cast<uint4 *>(&s_ctx_)[i_] = reinterpret_cast<const uint4 *>(ctxp)[i_]; \
+  __syncthreads();                                                                        \
+  const Ctx &K = s_ctx_;
 
 struct LocalCounters {
   unsigned long long *ctr;   // LDS [35]: 34 reference counters + nesc
@@ -126,15 +134,18 @@ DEVFN void angle_ab(const double dir1[3], const double vel[3], double dir2[3]) {
   for (int d = 0; d < 3; d++) dir2[d] = (dir1[d] - (vel[d] * fact2)) / fact1;
 }
 // vectors.h:81-111 with the flow velocity pos/t of vectors.h:37-43
-DEVFN double doppler_pos_dir(const Ctx &K, const double pos[3], const double dir[3], double t) {
+DEVFN double doppler_pos_dir(bool rel, const double pos[3], const double dir[3], double t) {
   const double v[3] = {pos[0] / t, pos[1] / t, pos[2] / t};
   const double ndotv = dot(dir, v);
   double dopplerfactor = 1. - (ndotv / ARTIS_CLIGHT);
-  if (K.R.relativistic_doppler) {
+  if (rel) {
     const double betasq = dot(v, v) / ARTIS_CLIGHTSQUARED;
     dopplerfactor = dopplerfactor / sqrt(1 - betasq);
   }
   return dopplerfactor;
+}
+DEVFN double doppler_pos_dir(const Ctx &K, const double pos[3], const double dir[3], double t) {
+  return doppler_pos_dir((bool)K.R.relativistic_doppler, pos, dir, t);
 }
 DEVFN double doppler_packet(const Ctx &K, const Pkt &p) { return doppler_pos_dir(K, p.pos, p.dir, p.prop_time); }
 // vectors.h:113-129

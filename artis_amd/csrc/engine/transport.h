@@ -19,6 +19,9 @@ struct Tx {
   int nts;
   bool ok;
   unsigned wl = 0, wb = 0;  // diagnostics: lines / bf continua scanned since last reset
+  // k_rpkt: the lane's column of the block's line-window image in LDS (16 doubles: nu, then tau coefficients, of
+  // 8 consecutive lines; element q at win[q * WAVE_BLOCK]); nullptr: the walk gathers populations itself
+  __attribute__((address_space(3))) double *win = nullptr;
 #ifdef ARTIS_STAMPS
   unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;  // diagnostic build: cycles per step phase
 #endif
@@ -466,16 +469,16 @@ DEVFN void calculate_kappa_rpkt_cont(Tx &x, const Pkt &p, int k, int mgi, Kappa 
 }
 
 // ------------------------------------------------------------------------------------------ lines
-// rpkt.cc:26-65
-DEVFN int closest_transition(const Ctx &K, double nu_cmf, int next_trans) {
-  const int nlines = K.T.nlines;
-  const double *lnu = K.T.line_nu;
+// rpkt.cc:26-65.  lnu_first, lnu_last: line_nu[0] and line_nu[nlines - 1], loaded once by a caller that walks many
+// lines (a dependent load per line otherwise)
+DEVFN int closest_transition(int nlines, const double *lnu, double nu_cmf, int next_trans, double lnu_first,
+                             double lnu_last) {
   const int left = next_trans;
   const int right = nlines - 1;
-  if (nu_cmf < lnu[right]) return -1;
+  if (nu_cmf < lnu_last) return -1;
   if (left > right) return -1;
   if (left > 0) return left;
-  if (nu_cmf >= lnu[0]) return 0;
+  if (nu_cmf >= lnu_first) return 0;
   int lo = next_trans, hi = nlines;
   while (lo < hi) {
     const int mid = lo + (hi - lo) / 2;
@@ -485,6 +488,12 @@ DEVFN int closest_transition(const Ctx &K, double nu_cmf, int next_trans) {
       hi = mid;
   }
   return lo;
+}
+DEVFN int closest_transition(const Ctx &K, double nu_cmf, int next_trans, double lnu_first, double lnu_last) {
+  return closest_transition(K.T.nlines, K.T.line_nu, nu_cmf, next_trans, lnu_first, lnu_last);
+}
+DEVFN int closest_transition(const Ctx &K, double nu_cmf, int next_trans) {
+  return closest_transition(K, nu_cmf, next_trans, K.T.line_nu[0], K.T.line_nu[max(K.T.nlines - 1, 0)]);
 }
 // rpkt.cc:511-555
 DEVFN void closest_transition_empty(const Ctx &K, Pkt &p) {
@@ -512,15 +521,45 @@ DEVFN void closest_transition_empty(const Ctx &K, Pkt &p) {
 }
 
 // move_pkt_withtime restricted to the fields a dummy packet needs (vectors.h:113-144)
-DEVFN void move_dummy(const Ctx &K, double pos[3], const double dir[3], double &t, double &nu_cmf, double nu_rf,
+DEVFN void move_dummy(bool rel, double pos[3], const double dir[3], double &t, double &nu_cmf, double nu_rf,
                       double distance) {
   const double nu_cmf_old = nu_cmf;
   t += distance / ARTIS_CLIGHT_PROP;
   pos[0] += (dir[0] * distance);
   pos[1] += (dir[1] * distance);
   pos[2] += (dir[2] * distance);
-  nu_cmf = nu_rf * doppler_pos_dir(K, pos, dir, t);
+  nu_cmf = nu_rf * doppler_pos_dir(rel, pos, dir, t);
   if (nu_cmf > nu_cmf_old) nu_cmf = nu_cmf_old;
+}
+DEVFN void move_dummy(const Ctx &K, double pos[3], const double dir[3], double &t, double &nu_cmf, double nu_rf,
+                      double distance) {
+  move_dummy((bool)K.R.relativistic_doppler, pos, dir, t, nu_cmf, nu_rf, distance);
+}
+
+// The line walk over the per-cell Sobolev coefficient table (DevCells::linecoef): a window of 8 consecutive
+// lines' frequencies and coefficients is two 64-byte runs -- four 16-byte loads each, all independent, one trip to
+// memory per 8 lines -- staged in the lane's LDS column; no population gathers.  tau_line = coef * dt is the
+// reference's (B_lu n_l - B_ul n_u) * HCLIGHTOVERFOURPI * dt evaluated in the same order (k_linecoef).
+#define LC_WIN 8
+#define WAVE_BLOCK_T 256  // threads per block of the kernels that set Tx::win (k_rpkt: WAVE_BLOCK)
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(1))) f64x2 glb_f64x2;
+DEVFN void lc_window(const double *nu8, const double *coef, __attribute__((address_space(3))) double *win) {
+  glb_f64x2 *nu = (glb_f64x2 *)nu8;
+  glb_f64x2 *co = (glb_f64x2 *)coef;
+  f64x2 a[LC_WIN / 2], b[LC_WIN / 2];
+#pragma unroll
+  for (int i = 0; i < LC_WIN / 2; i++) {
+    a[i] = nu[i];
+    b[i] = co[i];
+  }
+#pragma unroll
+  for (int i = 0; i < LC_WIN / 2; i++) {
+    win[(2 * i) * WAVE_BLOCK_T] = a[i].x;
+    win[(2 * i + 1) * WAVE_BLOCK_T] = a[i].y;
+    win[(LC_WIN + 2 * i) * WAVE_BLOCK_T] = b[i].x;
+    win[(LC_WIN + 2 * i + 1) * WAVE_BLOCK_T] = b[i].y;
+  }
 }
 
 // rpkt.cc:67-328
@@ -544,8 +583,106 @@ DEVFN double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_even
   STAMP(x, 1);
   const double kap_cont = kap.total * doppler_packet(K, p);
   const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
+  const double lnu_first = K.T.line_nu[0], lnu_last = K.T.line_nu[max(K.T.nlines - 1, 0)];
   unsigned long long nscanned = 0, ntaus = 0;
   double result;
+  if (x.win && K.C.linecoef) {
+    // the context fields the walk reads, in registers: through the context pointer they are reloaded from memory
+    // on every line (the compiler cannot prove the kernel's stores leave them unchanged)
+    __attribute__((address_space(3))) double *win = x.win;
+    const bool rel = K.R.relativistic_doppler;
+    const int nlines = K.T.nlines;
+    const double *lnu = K.T.line_nu, *nu8 = K.T.line_nu8;
+    const double *crow = K.C.linecoef + (int64_t)k * K.C.linecoef_stride;
+    int wb = -16;
+    while (true) {
+      const int lineindex = closest_transition(nlines, lnu, dnu, dnext, lnu_first, lnu_last);
+      if (lineindex >= 0) {
+        nscanned++;
+        if ((unsigned)(lineindex - wb) >= (unsigned)LC_WIN) {
+          wb = lineindex & ~(LC_WIN - 1);
+          lc_window(nu8 + wb, crow + wb, win);
+        }
+        const int pj = lineindex - wb;
+        const double nu_trans = win[pj * WAVE_BLOCK_T];
+        dnext = lineindex + 1;
+        double ldist;
+        if (dnu <= nu_trans) {
+          ldist = 0;
+        } else if (!rel) {
+          ldist = ARTIS_CLIGHT * dt * (dnu / nu_trans - 1);
+        } else {
+          const double nu_r = nu_trans / p.nu_rf;
+          const double ct = ARTIS_CLIGHT * dt;
+          const double r = vec_len(dpos);
+          const double mu = dot(p.dir, dpos) / r;
+          ldist = -mu * r + (ct - nu_r * nu_r * sqrt(ct * ct - (1 + r * r * (1 - mu * mu) * (1 + pow(nu_r, -2))))) /
+                                (1 + nu_r * nu_r);
+        }
+        if (ldist < 0.) {
+          if (!(ldist >= -100.)) {
+            x.err(ERR_LDIST, p.number, lineindex);
+            result = 0.;
+            break;
+          }
+          ldist = 0.;
+        }
+        const double tau_cont = kap_cont * ldist;
+        if (tau_rnd - tau > tau_cont) {
+          if (nu_trans < nu_cmf_abort) {
+            dnext -= 1;
+            p.next_trans = dnext;
+            result = DBL_MAX;
+            break;
+          }
+          double tau_line = win[(LC_WIN + pj) * WAVE_BLOCK_T] * dt;
+          ntaus++;
+          if (tau_line < 0) tau_line = 0.;
+          if (tau_rnd - tau > tau_cont + tau_line) {
+            dist = dist + ldist;
+            tau += tau_cont + tau_line;
+            move_dummy(rel, dpos, p.dir, dt, dnu, p.nu_rf, ldist);
+          } else {
+            p.ma_element = K.T.line_elem[lineindex];
+            p.ma_ion = K.T.line_ion[lineindex];
+            p.ma_level = K.T.line_upper[lineindex];
+            p.ma_activatingline = lineindex;
+            double edist = dist + ldist;
+            if (edist >= abort_dist) edist = abort_dist * (1 - 2e-8);
+            *rpkt_eventtype = ARTIS_RPKT_EVENTTYPE_BB;
+            p.next_trans = dnext;
+            result = edist;
+            break;
+          }
+        } else {
+          const double edist = dist + (tau_rnd - tau) / kap_cont;
+          dnext -= 1;
+          *rpkt_eventtype = ARTIS_RPKT_EVENTTYPE_CONT;
+          p.next_trans = dnext;
+          result = edist;
+          break;
+        }
+      } else {
+        dnext = K.T.nlines + 1;
+        const double tau_cont = kap_cont * (abort_dist - dist);
+        double edist;
+        if (tau_rnd - tau > tau_cont) {
+          edist = DBL_MAX;
+        } else {
+          edist = dist + (tau_rnd - tau) / kap_cont;
+          *rpkt_eventtype = ARTIS_RPKT_EVENTTYPE_CONT;
+        }
+        p.next_trans = dnext;
+        result = edist;
+        break;
+      }
+    }
+    lwork(x.L, WK_LINES_SCANNED, nscanned);
+    lwork(x.L, WK_LINE_TAUS, ntaus);
+    x.wl += (unsigned)nscanned;
+    STAMP(x, 2);
+    return result;
+  }
   // The walk visits consecutive lines.  Their 32-byte records and the two level populations each needs (random
   // gathers into the cell's pops) are fetched four lines at a time, all loads independent, so a long walk
   // waits for memory twice per four lines instead of three times per line.
@@ -553,7 +690,7 @@ DEVFN double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_even
   LineTau r0, r1, r2, r3;
   double pl0 = 0, pl1 = 0, pl2 = 0, pl3 = 0, pu0 = 0, pu1 = 0, pu2 = 0, pu3 = 0;
   while (true) {
-    const int lineindex = closest_transition(K, dnu, dnext);
+    const int lineindex = closest_transition(K, dnu, dnext, lnu_first, lnu_last);
     if (lineindex >= 0) {
       nscanned++;
       if ((unsigned)(lineindex - pf_base) >= 4u) {

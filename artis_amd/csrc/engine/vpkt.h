@@ -236,8 +236,9 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
   LineTau r[PF];
   double pl[PF], pu[PF];
   int z[PF] = {};
+  const double lnu_first = K.T.line_nu[0], lnu_last = K.T.line_nu[max(K.T.nlines - 1, 0)];
   while (ldist < sdist) {
-    const int lineindex = closest_transition(K, d.nu_cmf, d.next_trans);
+    const int lineindex = closest_transition(K, d.nu_cmf, d.next_trans, lnu_first, lnu_last);
     if (lineindex < 0) {
       d.next_trans = K.T.nlines + 1;
       break;  // D9
@@ -310,7 +311,7 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
 // all (spawn, observer) work items of the spawn buffer; spawn_ctr[1] is the fetch head
 template <int PF, int MINW>
 __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict__ ctxp, int refill_min) {
-  const Ctx &K = *ctxp;
+  CTX_IN_LDS(ctxp)
   const DevVpkt &V = K.V;
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];

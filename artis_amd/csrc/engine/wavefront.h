@@ -98,7 +98,7 @@ DEVFN void block_counters_flush(const Ctx &K, const unsigned long long *s_ctr, c
 
 // update_packets.cc:280-309 prologue: reset the per-step counters of every packet, queue the active ones
 __global__ void k_classify(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa, int64_t n, double t2) {
-  const Ctx &K = *ctxp;
+  CTX_IN_LDS(ctxp)
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   block_counters_init(s_ctr, s_work);
@@ -149,16 +149,19 @@ DEVFN void apply_pending(Tx &x, const WaveState &W, int32_t idx, Pkt &p, const C
 template <int MINW>
 __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa, int64_t n,
                                                      int nts, double t2) {
-  const Ctx &K = *ctxp;
+  CTX_IN_LDS(ctxp)
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   __shared__ double s_cmflum[WAVE_BLOCK / 64];
+  __shared__ double s_win[2 * LC_WIN][WAVE_BLOCK];  // line windows of the walk over DevCells::linecoef
+  static_assert(WAVE_BLOCK == WAVE_BLOCK_T, "Tx::win column stride");
   block_counters_init(s_ctr, s_work);
   LocalCounters L;
   L.ctr = &s_ctr[0];
   L.work = &s_work[0];
   Tx x(K, L);
   x.nts = nts;
+  x.win = (__attribute__((address_space(3))) double *)&s_win[0][threadIdx.x];
   const uint32_t nq = W.ctr[2 * QR];
   Pkt p;
   int32_t idx = -1;
@@ -277,7 +280,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
 
 // bin the M queue by cell: count per cell and remember each slot's key
 __global__ void k_ma_bin(const Ctx *__restrict__ ctxp, WaveState W, const uint64_t *__restrict__ soa) {
-  const Ctx &K = *ctxp;
+  CTX_IN_LDS(ctxp)
   const uint32_t nq = W.ctr[2 * QM];
   for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x) {
     const int32_t idx = W.q[QM][slot];
@@ -300,7 +303,7 @@ __global__ void k_ma_scatter(WaveState W, uint32_t *offs) {
 template <bool CACHE, int MINW>
 __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__ ctxp, WaveState W, const uint64_t *__restrict__ soa,
                                                          int64_t n, int nts) {
-  const Ctx &K = *ctxp;
+  CTX_IN_LDS(ctxp)
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   // per wave: the 128-byte hot line of each lane's current macro-atom record (ma_jump_cached), chunk-major
@@ -496,7 +499,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
 #define MAX_CH 256
 __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, WaveState W,
                                                  const uint64_t *__restrict__ soa, int64_t n, int nts) {
-  const Ctx &K = *ctxp;
+  CTX_IN_LDS(ctxp)
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   __shared__ double s_R[MAX_CH], s_C[MAX_CH], s_et[MAX_CH], s_eg[MAX_CH];
@@ -631,7 +634,7 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
 // the r-packet / macro-atom / k-packet rounds (nothing on those paths turns back into this family).
 __global__ __launch_bounds__(WAVE_BLOCK) void k_gamma(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa,
                                                       int64_t n, int nts, double t2) {
-  const Ctx &K = *ctxp;
+  CTX_IN_LDS(ctxp)
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   block_counters_init(s_ctr, s_work);
@@ -678,7 +681,7 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_gamma(const Ctx *__restrict__ ct
 // k-packets (rare): one packet per workitem, grid-stride
 __global__ __launch_bounds__(WAVE_BLOCK) void k_kpkt(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa, int64_t n,
                                                      int nts, double t2) {
-  const Ctx &K = *ctxp;
+  CTX_IN_LDS(ctxp)
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   block_counters_init(s_ctr, s_work);
