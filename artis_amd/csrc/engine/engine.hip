@@ -664,6 +664,7 @@ void free_packets() {
   dfree(G.W.pend_jumps);
   dfree(G.W.ma_key);
   dfree(G.W.ma_sorted);
+  dfree(G.W.ma_tick);
   for (int q = 0; q < NQUEUES; q++) dfree(G.W.q[q]);
   G.cap_pkts = 0;
   G.npkts = 0;
@@ -683,7 +684,8 @@ int alloc_packets(int64_t n) {
                            {(void **)&G.W.pend, un * sizeof(int4)},
                            {(void **)&G.W.pend_jumps, un * sizeof(uint32_t)},
                            {(void **)&G.W.ma_key, un * sizeof(int32_t)},
-                           {(void **)&G.W.ma_sorted, un * sizeof(int32_t)}};
+                           {(void **)&G.W.ma_sorted, un * sizeof(int32_t)},
+                           {(void **)&G.W.ma_tick, un * 2 * sizeof(int4)}};
   for (int q = 0; q < NQUEUES; q++) reqs.push_back({(void **)&G.W.q[q], un * sizeof(int32_t)});
   const int nreq = (int)reqs.size();
   for (int r = 0; r < nreq; r++) {
@@ -813,7 +815,8 @@ int vpkt_collect(const unsigned long long before[8]) {
 
 #define WAVE_MAX_ROUNDS 10000000
 int run_wavefront(int64_t n, int nts, double t2) {
-  const WaveState &W = G.W;
+  WaveState W = G.W;
+  if (!(G.K.C.have_macache && W.ma_binned)) W.ma_tick = nullptr;  // tickets: cached walk over the binned queue
   const unsigned grid = (unsigned)G.wave_grid;
   if (int rc = sync_ctx()) return rc;
   G.tev_used = 0;
@@ -852,7 +855,7 @@ int run_wavefront(int64_t n, int nts, double t2) {
       k_ma_bin<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa);
       HIPCHK(hipcub::DeviceScan::ExclusiveSum(G.d_scan_tmp, G.scan_tmp_bytes, W.bins, G.d_binoffs, nne + 1,
                                               G.stream));
-      k_ma_scatter<<<grid, WAVE_BLOCK, 0, G.stream>>>(W, G.d_binoffs);
+      k_ma_scatter<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, G.d_binoffs);
     }
     HIPCHK(hipMemsetAsync(W.xhead, 0, 8 * sizeof(uint32_t), G.stream));
     // ARTIS_GPU_MA_WAVES=w (default 4): launch only w blocks per CU (w resident waves per SIMD) -- fewer
@@ -1284,6 +1287,10 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     G.W.ma_ranges = (xr && xr[0] == '1') ? 8 : 1;
     const char *rf = getenv("ARTIS_GPU_REFILL");
     G.W.refill_min = rf ? std::max(1, std::min(64, atoi(rf))) : 32;
+    // k_ma refills from one coalesced ticket read, so it refills early (1e7-packet bench, before tickets:
+    // 32 idle lanes 2212 ms, 16: 2064 ms, 8: 2042 ms)
+    const char *rfm = getenv("ARTIS_GPU_REFILL_MA");
+    G.W.refill_ma = rfm ? std::max(1, std::min(64, atoi(rfm))) : 8;
     const char *oc = getenv("ARTIS_GPU_MA_OCC");
     G.ma_occ = (oc && oc[0] == '8') ? 8 : 1;
   }

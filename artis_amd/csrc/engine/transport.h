@@ -1734,22 +1734,41 @@ DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
     }
     m.hi = m.end;
   }
-  // binary search for the first entry above q2, resumed where it stopped
+  // binary search for the first entry above q2, resumed where it stopped.  The inner loop is the branch-light
+  // common case (probe on the staged line, decided by the high half); it leaves for a probe off the line
+  // (MA_PENDING) or a high half that needs its low half (rare).
   int lo = m.lo, hi = m.hi;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    const int p = m.base + mid;
+  const int base = m.base;
+  const uint32_t q2h = m.q2h;
+  unsigned probes = 0;
+  while (true) {
+    int mid = 0, p = 0;
+    uint32_t h = 0;
+    while (lo < hi) {
+      mid = (lo + hi) >> 1;
+      p = base + mid;
+      if (!keys.has(p)) break;
+      h = keys.hi(p);
+      if ((h - q2h) <= 1u) break;  // high half qh or qh + 1: undecided at 16 bits
+      probes++;
+      if (h > q2h)
+        hi = mid;
+      else
+        lo = mid + 1;
+    }
+    if (lo >= hi) break;
     if (!keys.has(p)) {
       m.lo = lo;
       m.hi = hi;
       m.pline = p >> 6;
+      m.ntrans += probes;
       MA_DIAG(16 + m.sel);
       return MA_PENDING;
     }
-    MA_DIAG(32 + m.sel);
-    const int c = cmp(p, keys.hi(p), m.q2, m.q2h);
-    m.ntrans++;
+    probes++;
+    const int c = ma_key_cmp((h << 16) | (uint32_t)gload(rec + lay.hot + p), m.q2);
     if (c == 0) {
+      m.ntrans += probes;
       m.jumps--;
       m.sel = -1;
       m.pline = 0;
@@ -1760,6 +1779,7 @@ DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
     else
       lo = mid + 1;
   }
+  m.ntrans += probes;
   const int sel = m.sel;
   if (sel == ARTIS_MA_ACTION_INTERNALDOWNSAME || sel == ARTIS_MA_ACTION_INTERNALUPSAME) {
     const bool down = sel == ARTIS_MA_ACTION_INTERNALDOWNSAME;

@@ -39,6 +39,10 @@ struct WaveState {
   int ma_ranges;       // 8: blocks on XCD x take range x first (then steal), 1: one shared range
   int ma_binned;       // 1: k_ma reads ma_sorted, 0: k_ma reads q[QM]
   int refill_min;      // a wave refetches work (and flushes its queue appends) once this many lanes are idle
+  int refill_ma;       // the same for k_ma (a macro-atom refill is cheap: one coalesced ticket read)
+  // cell-sorted macro-atom tickets written by k_ma_scatter when the key cache is on (else nullptr): per slot
+  // {packet index, unique level, record offset, nonempty cell}, {packet number, RNG counter, jumps so far, 0}
+  int4 *ma_tick;       // [2N]
   unsigned long long *stats;  // [32] diagnostics: per kernel class c: [4c] wave loop passes, [4c+1] busy
                               // lane-passes, [4c+2] wave cycles (s_memtime), [4c+3] refills;
                               // [16 + 4c] cycles in refill blocks, [17 + 4c] cycles in the work step
@@ -289,11 +293,43 @@ __global__ void k_ma_bin(const Ctx *__restrict__ ctxp, WaveState W, const uint64
     atomicAdd(&W.bins[k], 1u);
   }
 }
-// scatter into cell order using the exclusive prefix sum of the counts
-__global__ void k_ma_scatter(WaveState W, uint32_t *offs) {
+// scatter into cell order using the exclusive prefix sum of the counts.  With the key cache, each slot becomes a
+// ticket holding everything k_ma's refill needs (the walk's level, record, cell, RNG stream and jump count), so a
+// k_ma lane starts a walk with one coalesced read instead of a chain of dependent packet and table loads.
+__global__ void k_ma_scatter(const Ctx *__restrict__ ctxp, WaveState W, const uint64_t *__restrict__ soa, int64_t n,
+                             uint32_t *offs) {
+  CTX_IN_LDS(ctxp)
   const uint32_t nq = W.ctr[2 * QM];
-  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x)
-    W.ma_sorted[atomicAdd(&offs[W.ma_key[slot]], 1u)] = W.q[QM][slot];
+  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x) {
+    const int32_t idx = W.q[QM][slot];
+    const uint32_t pos = atomicAdd(&offs[W.ma_key[slot]], 1u);
+    if (!W.ma_tick) {
+      W.ma_sorted[pos] = idx;
+      continue;
+    }
+    const int where = lo32(soa[PW(n, idx, 0)]);
+    const uint64_t w36 = soa[PW(n, idx, 36)], w37 = soa[PW(n, idx, 37)];
+    const int number = (int)hi32(soa[PW(n, idx, 33)]);
+    const int4 pd = W.pend[idx];
+    int ul;
+    unsigned jumps;
+    if (pd.x == MA_RESUME) {  // a walk parked by k_ma_exact: continue from its level and jump count
+      ul = pd.y;
+      jumps = W.pend_jumps[idx];
+      W.pend[idx].x = 0;
+    } else {
+      ul = ulev(K, lo32(w36), hi32(w36), lo32(w37));
+      jumps = 0;
+    }
+    const int mgi = cell_mgi(K, where);
+    int32_t tidx = idx;
+    if (K.C.thick[mgi] == 1) {
+      fail(K, ERR_THICK_MA, number, mgi);
+      tidx = -1;
+    }
+    W.ma_tick[2 * (int64_t)pos] = make_int4(tidx, ul, K.T.ma_meta[ul].rec_off, K.C.ne_index[mgi]);
+    W.ma_tick[2 * (int64_t)pos + 1] = make_int4(number, (int)W.rng_n[idx], (int)jumps, 0);
+  }
 }
 
 // macro-atoms: persistent lanes, one jump per loop pass, lane state = MaLane + RNG counter.
@@ -338,7 +374,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   while (true) {
     const bool idle = !have && !drained;
     const unsigned long long imask = __ballot(idle);
-    if (!__any(have) || __popcll(imask) >= W.refill_min) {
+    if (!__any(have) || __popcll(imask) >= (CACHE ? W.refill_ma : W.refill_min)) {
       st_refill++;
       const unsigned long long tr0 = wave_clock();
       wave_push(W, QR, pendR, idx);
@@ -349,7 +385,21 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
         const uint32_t lo = (uint32_t)((uint64_t)nq * cur / nr), hi = (uint32_t)((uint64_t)nq * (cur + 1) / nr);
         const uint32_t slot = wave_reserve(&W.xhead[cur], idle);
         const bool got = idle && lo + slot < hi;
-        if (got) {
+        if (got && CACHE && W.ma_tick) {
+          const int4 t0 = W.ma_tick[2 * (int64_t)(lo + slot)], t1 = W.ma_tick[2 * (int64_t)(lo + slot) + 1];
+          idx = t0.x;
+          mc.ul = t0.y;
+          mc.rec_off = t0.z;
+          mc.k = t0.w;
+          rng.key1 = (uint32_t)t1.x;
+          rng.n = (uint32_t)t1.y;
+          mc.jumps = (unsigned)t1.z;
+          mc.block = K.C.ma_key + (int64_t)mc.k * K.C.ma_key_stride;
+          mc.ntrans = 0;
+          mc.sel = -1;
+          mc.pline = 0;
+          have = idx >= 0;
+        } else if (got) {
           idx = queue[lo + slot];
           const int where = lo32(soa[PW(n, idx, 0)]);
           const uint64_t w36 = soa[PW(n, idx, 36)];
