@@ -580,6 +580,7 @@ struct Engine {
   // virtual packets (vpkt.h): device accumulators and the spawn buffer (sized per update)
   int64_t vpkt_cap_param = 0;
   std::vector<int32_t> h_anumber;  // artis_atomic_tables.elem_anumber
+  std::vector<int32_t> h_line_elem;  // artis_atomic_tables.line_elementindex (virtual-packet line masks)
   double *d_vpkt_spawn = nullptr;
   uint32_t vpkt_spawn_cap = 0;
   std::vector<hipEvent_t> vev;  // (start, end) pairs around the k_vpkt launches of the last update
@@ -1159,6 +1160,20 @@ int artis_gpu_vpkt_init(const artis_vpkt_params *vp) {
   rc |= dupload(&V.delta_t, delta_t.data(), delta_t.size());
   rc |= dupload(&V.delta_freq, delta_freq.data(), delta_freq.size());
   rc |= dupload(&V.anumber, anum.data(), anum.size());
+  {
+    // per line, the spectra whose optical depth its opacity enters (vpkt.cc:283-294: exclude -1 drops every
+    // line, exclude Z the lines of element Z); padded for the walk's 8-line windows
+    const size_t nli = G.h_line_elem.size();
+    std::vector<uint8_t> mask((nli + 7) / 8 * 8 + 8, 0);
+    for (size_t li = 0; li < nli; li++) {
+      const int an = anum.empty() ? 0 : anum[G.h_line_elem[li]];
+      uint8_t m = 0;
+      for (int ind = 0; ind < vp->nspectra; ind++)
+        if (V.exclude[ind] != -1 && (an != V.exclude[ind])) m |= (uint8_t)(1u << ind);
+      mask[li] = m;
+    }
+    rc |= dupload(&V.line_mask, mask.data(), mask.size());
+  }
   V.vstokes_stride = (int64_t)vp->vmtbins * vp->nobs * vp->nspectra * vp->vmnubins;
   V.vgrid_stride = (vp->vgrid_flag == 1) ? (int64_t)vp->ny_vgrid * vp->nz_vgrid * vp->nrange_grid * vp->nobs : 0;
   rc |= dalloc(&V.vstokes, (size_t)(3 * V.vstokes_stride));
@@ -1362,6 +1377,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   rc |= dupload(&T.line_f, a->line_osc_strength, nli);
   rc |= dupload(&T.line_coll, a->line_coll_str, nli);
   rc |= dupload(&T.line_elem, a->line_elementindex, nli);
+  G.h_line_elem.assign(a->line_elementindex, a->line_elementindex + nli);
   rc |= dupload(&T.line_ion, a->line_ionindex, nli);
   rc |= dupload(&T.line_upper, a->line_upperlevelindex, nli);
   rc |= dupload(&T.line_lower, a->line_lowerlevelindex, nli);

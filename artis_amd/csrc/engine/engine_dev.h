@@ -247,6 +247,7 @@ struct DevVpkt {
   const float *delta_t;     // [vmtbins]  vspecpol.delta_t (float, vpkt.cc:18)
   const float *delta_freq;  // [vmnubins] delta_freq_vspec (float, vpkt.cc:26)
   const int32_t *anumber;   // [nelements]
+  const uint8_t *line_mask; // [nlines padded to 8 + 8] bit ind: the line's opacity enters spectrum ind
   double *vstokes;          // [3][vmtbins][nobs * nspectra][vmnubins]: I, Q, U
   int64_t vstokes_stride;   // doubles per Stokes component
   double *vgrid;            // [3][ny][nz][nrange_grid][nobs]

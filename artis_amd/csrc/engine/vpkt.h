@@ -190,6 +190,25 @@ DEVFN void vpkt_trace_finish(const Ctx &K, VLane &v) {
 
 enum { VSEG_CONTINUE = 0, VSEG_ESCAPED = 1, VSEG_KILLED = 2 };
 
+// the end of a pass of rlc_emiss_vpkt's cell loop: move to the cell boundary and into the next cell (vpkt.cc:296-312)
+DEVFN int vpkt_segment_end(Tx &x, VLane &v, double sdist, int snext) {
+  const Ctx &K = x.K;
+  Pkt &d = v.d;
+  v.t_future += (sdist / ARTIS_CLIGHT_PROP);
+  d.prop_time = v.t_future;
+  move_pkt(K, d, sdist);
+  change_cell(x, d, snext);
+  const bool end_packet = (d.type == ARTIS_TYPE_ESCAPE);
+  v.mgi = cell_mgi(K, d.where);
+  if (v.mgi == K.G.npts_model) return VSEG_ESCAPED;
+  if (K.C.thick[v.mgi] == 1) return VSEG_KILLED;
+  if (++v.cells > VPKT_MAX_CELLS) {
+    x.err(ERR_STUCK, -1, 6);
+    return VSEG_KILLED;
+  }
+  return end_packet ? VSEG_ESCAPED : VSEG_CONTINUE;
+}
+
 // one pass of rlc_emiss_vpkt's cell loop (vpkt.cc:195-312); deviation D9 for the line loop
 template <int PF>
 DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
@@ -233,10 +252,68 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
   // atomic number are fetched PF consecutive lines at a time, all loads independent, so the walk waits for memory
   // twice per PF lines instead of three to four times per line.  The tau sums are unchanged.
   int pf_base = -(1 << 20);
+  const double lnu_first = K.T.line_nu[0], lnu_last = K.T.line_nu[max(K.T.nlines - 1, 0)];
+  if (K.C.linecoef) {
+    // over the per-cell Sobolev coefficients (DevCells::linecoef, as get_event): an aligned window of LC_WIN lines'
+    // frequencies and coefficients is eight independent 16-byte loads; dtau = coefficient * t_line is the
+    // reference's (B_lu n_l - B_ul n_u) * HCLIGHTOVERFOURPI * t_line in the same operation order
+    const int nlines = K.T.nlines;
+    const double *lnu = K.T.line_nu, *nu8 = K.T.line_nu8;
+    const double *crow = K.C.linecoef + (int64_t)K.C.ne_index[v.mgi] * K.C.linecoef_stride;
+    const uint8_t *lmask = V.line_mask;
+    const int nspec = V.nspectra;
+    const double tau_max = V.tau_max;
+    f64x2 wn[LC_WIN / 2], wc[LC_WIN / 2];
+    uint64_t wm = 0;  // the window's 8 line masks
+    while (ldist < sdist) {
+      const int lineindex = closest_transition(nlines, lnu, d.nu_cmf, d.next_trans, lnu_first, lnu_last);
+      if (lineindex < 0) {
+        d.next_trans = nlines + 1;
+        break;  // D9
+      }
+      if ((unsigned)(lineindex - pf_base) >= (unsigned)LC_WIN) {
+        pf_base = lineindex & ~(LC_WIN - 1);
+#pragma unroll
+        for (int q = 0; q < LC_WIN / 2; q++) {
+          wn[q] = ((glb_f64x2 *)(nu8 + pf_base))[q];
+          wc[q] = ((glb_f64x2 *)(crow + pf_base))[q];
+        }
+        wm = *(const __attribute__((address_space(1))) uint64_t *)(lmask + pf_base);
+      }
+      const int pj = lineindex - pf_base;
+      double nutrans = wn[0].x, coef = wc[0].x;
+#pragma unroll
+      for (int q = 1; q < LC_WIN; q++)
+        if (pj == q) {
+          nutrans = (q & 1) ? wn[q >> 1].y : wn[q >> 1].x;
+          coef = (q & 1) ? wc[q >> 1].y : wc[q >> 1].x;
+        }
+      const unsigned lm = (unsigned)(wm >> (8 * pj)) & 0xffu;
+      d.next_trans = lineindex + 1;
+      if (d.nu_cmf < nutrans)
+        ldist = 0;
+      else
+        ldist = ARTIS_CLIGHT * t_current * (d.nu_cmf / nutrans - 1);
+      if (ldist > sdist) {
+        d.next_trans -= 1;
+        break;
+      }
+      lines++;
+      const double t_line = t_current + ldist / ARTIS_CLIGHT;
+      const double dtau = coef * t_line;
+      int dead = 0;
+#pragma unroll
+      for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++) {
+        if ((lm >> ind) & 1u) v.tau[ind] += dtau;
+        if (ind < nspec && v.tau[ind] > tau_max) dead++;
+      }
+      if (dead == nspec) return VSEG_KILLED;  // vpkt_alive
+    }
+    return vpkt_segment_end(x, v, sdist, snext);
+  }
   LineTau r[PF];
   double pl[PF], pu[PF];
   int z[PF] = {};
-  const double lnu_first = K.T.line_nu[0], lnu_last = K.T.line_nu[max(K.T.nlines - 1, 0)];
   while (ldist < sdist) {
     const int lineindex = closest_transition(K, d.nu_cmf, d.next_trans, lnu_first, lnu_last);
     if (lineindex < 0) {
@@ -293,19 +370,7 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
     }
     if (!vpkt_alive(V, v.tau)) return VSEG_KILLED;
   }
-  v.t_future += (sdist / ARTIS_CLIGHT_PROP);
-  d.prop_time = v.t_future;
-  move_pkt(K, d, sdist);
-  change_cell(x, d, snext);
-  const bool end_packet = (d.type == ARTIS_TYPE_ESCAPE);
-  v.mgi = cell_mgi(K, d.where);
-  if (v.mgi == K.G.npts_model) return VSEG_ESCAPED;
-  if (K.C.thick[v.mgi] == 1) return VSEG_KILLED;
-  if (++v.cells > VPKT_MAX_CELLS) {
-    x.err(ERR_STUCK, -1, 6);
-    return VSEG_KILLED;
-  }
-  return end_packet ? VSEG_ESCAPED : VSEG_CONTINUE;
+  return vpkt_segment_end(x, v, sdist, snext);
 }
 
 // all (spawn, observer) work items of the spawn buffer; spawn_ctr[1] is the fetch head
