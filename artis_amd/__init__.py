@@ -230,7 +230,8 @@ class Engine:
         return dict(zip(("segments", "lines", "bf_active", "escaped"), (int(x) for x in w)))
 
     def last_kernel_times(self):
-        """{class: (ms, launches)} for the last transport: rpkt, ma, kpkt, classify."""
+        """{class: (ms, launches)} for the last transport: rpkt (k_rpkt), ma (k_ma), kpkt (k_kpkt), classify (the
+        rest: classify, gamma, macro-atom queue binning, exact jumps)."""
         ms = (C.c_double * 4)()
         nl = (C.c_int64 * 4)()
         self.lib.artis_gpu_last_kernel_times(ms, nl)

@@ -849,7 +849,7 @@ int run_wavefront(int64_t n, int nts, double t2) {
       k_rpkt<1><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
     TEND(0);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QR, 0, 2 * sizeof(uint32_t), G.stream));
-    TSTART(1);
+    TSTART(3);  // class 3: the macro-atom queue binning and the rare exact jumps (class 1 is k_ma alone)
     if (W.ma_binned) {
       const int nne = G.K.C.n_nonempty;
       HIPCHK(hipMemsetAsync(W.bins, 0, (size_t)(nne + 1) * sizeof(uint32_t), G.stream));
@@ -859,6 +859,8 @@ int run_wavefront(int64_t n, int nts, double t2) {
       k_ma_scatter<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, G.d_binoffs);
     }
     HIPCHK(hipMemsetAsync(W.xhead, 0, 8 * sizeof(uint32_t), G.stream));
+    TEND(3);
+    TSTART(1);
     // ARTIS_GPU_MA_WAVES=w (default 4): launch only w blocks per CU (w resident waves per SIMD) -- fewer
     // concurrent walks thrash the caches less; the walk is bound by the memory system, not by latency hiding
     // (1e7-packet bench: 2 waves 4694 ms, 3: 3761 ms, 4: 3317 ms, 8: 3725 ms; profiles/r02_ab_ma_waves.txt)
@@ -876,12 +878,14 @@ int run_wavefront(int64_t n, int nts, double t2) {
     } else {
       k_ma<false, 1><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
     }
+    TEND(1);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QM, 0, 2 * sizeof(uint32_t), G.stream));
     if (G.K.C.have_macache) {  // jumps the 32-bit keys could not decide (rare), exact; walks go back to M
+      TSTART(3);
       k_ma_exact<<<grid / 4, 64, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+      TEND(3);
       HIPCHK(hipMemsetAsync(W.ctr + 2 * QX, 0, 2 * sizeof(uint32_t), G.stream));
     }
-    TEND(1);
     TSTART(2);
     k_kpkt<<<grid / 4, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
     TEND(2);
@@ -1474,6 +1478,21 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   rc |= dupload(&T.allcont_phixstable, a->allcont_phixstable, nb);
   rc |= dupload(&T.allcont_groundindex, a->allcont_index_in_groundphixslist, nb);
   rc |= dupload(&T.groundcont_nu_edge, a->groundcont_nu_edge, a->nbfcontinua_ground);
+  {
+    // per ground continuum, the allcont indices (ascending) of the ground-level continua that enter its
+    // groundcont_gamma_contr (rpkt.cc:1166-1171): update_estimators sums these instead of scanning all continua
+    const int nbfg = a->nbfcontinua_ground;
+    std::vector<int32_t> off(nbfg + 1, 0), lst;
+    for (int g = 0; g < nbfg; g++) {
+      off[g] = (int32_t)lst.size();
+      for (int i = 0; i < nb; i++)
+        if (a->allcont_level[i] == 0 && a->allcont_index_in_groundphixslist[i] == g) lst.push_back(i);
+    }
+    off[nbfg] = (int32_t)lst.size();
+    if (lst.empty()) lst.push_back(0);
+    rc |= dupload(&T.gc_cont_off, off.data(), off.size());
+    rc |= dupload(&T.gc_cont, lst.data(), lst.size());
+  }
   rc |= dupload(&T.groundcont_element, a->groundcont_element, a->nbfcontinua_ground);
   rc |= dupload(&T.groundcont_ion, a->groundcont_ion, a->nbfcontinua_ground);
   rc |= dupload(&T.spontrecombcoeff, a->spontrecombcoeff, (size_t)a->tablesize * nb);

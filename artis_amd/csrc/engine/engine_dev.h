@@ -77,6 +77,7 @@ struct DevTab {
       *allcont_phixstable, *allcont_groundindex;
   const double *groundcont_nu_edge;
   const int32_t *groundcont_element, *groundcont_ion;
+  const int32_t *gc_cont_off, *gc_cont;  // per ground continuum: its ground-level allcont indices (CSR, ascending)
   const double *spontrecombcoeff, *corrphotoioncoeff, *bfcooling_coeff;
   const int32_t *cool_type, *cool_element, *cool_ion, *cool_level, *cool_upper;
   // nebular options (ABI 6): NLTE level bookkeeping (input.cc:1711-1746), radiation-field bin edges

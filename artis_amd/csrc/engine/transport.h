@@ -22,6 +22,11 @@ struct Tx {
   // k_rpkt: the lane's column of the block's line-window image in LDS (16 doubles: nu, then tau coefficients, of
   // 8 consecutive lines; element q at win[q * WAVE_BLOCK]); nullptr: the walk gathers populations itself
   __attribute__((address_space(3))) double *win = nullptr;
+  // k_rpkt: the J / nuJ / ffheating terms of the step's estimator segment are left here (est_mgi >= 0) and added
+  // after the wave has converged (wave_flush_estimators), so that lanes in the same cell add once per wave
+  bool defer_est = false;
+  int est_mgi = -1;
+  double est_de = 0., est_denu = 0., est_deff = 0.;
 #ifdef ARTIS_STAMPS
   unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;  // diagnostic build: cycles per step phase
 #endif
@@ -803,9 +808,16 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
   lwork(x.L, WK_EST_SEGMENTS, 1);
   const double distance_e_cmf = distance * p.e_cmf;
   const double nu = p.nu_cmf;
-  safeadd(&K.E.J[mgi], distance_e_cmf);
-  safeadd(&K.E.nuJ[mgi], distance_e_cmf * nu);
-  safeadd(&K.E.ffheat[mgi], distance_e_cmf * kap.ffheating);
+  if (x.defer_est) {
+    x.est_mgi = mgi;
+    x.est_de = distance_e_cmf;
+    x.est_denu = distance_e_cmf * nu;
+    x.est_deff = distance_e_cmf * kap.ffheating;
+  } else {
+    safeadd(&K.E.J[mgi], distance_e_cmf);
+    safeadd(&K.E.nuJ[mgi], distance_e_cmf * nu);
+    safeadd(&K.E.ffheat[mgi], distance_e_cmf * kap.ffheating);
+  }
   if (K.R.detailed_bf && distance_e_cmf != 0) {
     // radfield.cc:764-829 update_bfestimators: gamma_contr[i] at the frequency the opacity was computed at
     // (rpkt.cc:1166-1171; zero for continua above kap.nu or not included), the window test at the current nu
@@ -843,9 +855,9 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
       if (K.C.elem_abundance[(int64_t)mgi * K.T.nelements + element] > 0) {
         // groundcont_gamma_contr[g] at the frequency the opacity was computed at (rpkt.cc:1166-1171)
         double gcontr = 0.;
-        for (int i = 0; i < K.T.nbf; i++) {
+        for (int q = K.T.gc_cont_off[g]; q < K.T.gc_cont_off[g + 1]; q++) {  // ascending allcont order
+          const int i = K.T.gc_cont[q];
           if (kap.nu < K.T.allcont_nu_edge[i]) break;
-          if (K.T.allcont_level[i] != 0 || K.T.allcont_groundindex[i] != g) continue;
           double nnlevel, gc;
           if (bf_contribution(K, k, mgi, i, kap.nu, &nnlevel, &gc)) gcontr += gc;
         }
@@ -859,6 +871,38 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
       break;
     }
   }
+}
+
+// The deferred J / nuJ / ffheating terms of a converged wave (radfield.cc:831-836, rpkt.cc:569-579; N1): when all
+// the wave's contributing lanes are in one cell -- the common case of few-cell models, where per-lane atomics on
+// the same three addresses serialise -- the terms are summed across the wave and added by one lane; otherwise
+// every lane adds its own.  Float atomics are unordered either way, so the sums agree to rounding.
+DEVFN void wave_flush_estimators(Tx &x) {
+  const Ctx &K = x.K;
+  const bool pend = x.est_mgi >= 0;
+  const unsigned long long pm = __ballot(pend);
+  if (pm) {
+    const int leader = __ffsll((long long)pm) - 1;
+    const int m0 = __shfl(x.est_mgi, leader, 64);
+    if (__ballot(pend && x.est_mgi != m0) == 0) {
+      double a = pend ? x.est_de : 0., b = pend ? x.est_denu : 0., c = pend ? x.est_deff : 0.;
+      for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off, 64);
+        b += __shfl_xor(b, off, 64);
+        c += __shfl_xor(c, off, 64);
+      }
+      if ((int)__lane_id() == leader) {
+        safeadd(&K.E.J[m0], a);
+        safeadd(&K.E.nuJ[m0], b);
+        safeadd(&K.E.ffheat[m0], c);
+      }
+    } else if (pend) {
+      safeadd(&K.E.J[x.est_mgi], x.est_de);
+      safeadd(&K.E.nuJ[x.est_mgi], x.est_denu);
+      safeadd(&K.E.ffheat[x.est_mgi], x.est_deff);
+    }
+  }
+  x.est_mgi = -1;
 }
 
 // ------------------------------------------------------------------------------------------ virtual packets

@@ -166,6 +166,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
   Tx x(K, L);
   x.nts = nts;
   x.win = (__attribute__((address_space(3))) double *)&s_win[0][threadIdx.x];
+  x.defer_est = true;
   const uint32_t nq = W.ctr[2 * QR];
   Pkt p;
   int32_t idx = -1;
@@ -245,6 +246,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
         have = false;
       }
     }
+    wave_flush_estimators(x);  // the step's J / nuJ / ffheating terms, once per cell and wave where possible
     st_tstep += wave_clock() - ts0;
     {
       unsigned ml = x.wl, sl = x.wl, mb = x.wb, sb = x.wb;

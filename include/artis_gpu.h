@@ -528,7 +528,8 @@ int artis_gpu_vpkt_last_work(int64_t work[4]);
 
 int64_t artis_gpu_last_rounds(void);  /* event-queue rounds of the last update (0: megakernel path) */
 /* device time (ms, HIP events around every launch) and launch count of the last update per kernel class:
- * [0] r-packet, [1] macro-atom (incl. cell binning), [2] k-packet, [3] classify */
+ * [0] r-packet (k_rpkt), [1] macro-atom (k_ma), [2] k-packet (k_kpkt), [3] other: classify, gamma, the macro-atom
+ * queue binning (k_ma_bin / scan / k_ma_scatter) and the exact jumps (k_ma_exact) */
 int artis_gpu_last_kernel_times(double ms[4], int64_t launches[4]);
 const char *artis_gpu_last_error(void);
 #define ARTIS_GPU_ABI_VERSION 6  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
