@@ -27,6 +27,7 @@ ABI_SYMBOLS = [
     "artis_gpu_vpkt_init", "artis_gpu_vpkt_zero", "artis_gpu_vpkt_download", "artis_gpu_vpkt_last_stats", "artis_gpu_vpkt_last_work",
     "artis_estimator_block_len", "artis_estimator_block_pack", "artis_estimator_block_unpack",
     "artis_gpu_comm_unique_id", "artis_gpu_comm_init", "artis_gpu_estimators_allreduce", "artis_gpu_comm_finalize",
+    "artis_gpu_solve_temperatures", "artis_gpu_last_te_ms",
 ]
 
 _gpu_lib = None
@@ -85,6 +86,8 @@ def gpu_lib():
         L.artis_gpu_comm_unique_id.argtypes = [vp]
         L.artis_gpu_comm_init.argtypes = [C.c_int, C.c_int, vp]
         L.artis_gpu_comm_finalize.restype = None
+        L.artis_gpu_solve_temperatures.argtypes = [vp, C.POINTER(ffi.TeParams), C.POINTER(ffi.TeCells)]
+        L.artis_gpu_last_te_ms.restype = C.c_double
         _gpu_lib = L
     return _gpu_lib
 
@@ -118,6 +121,14 @@ class Engine:
         if rc != 0:
             msg = self.lib.artis_gpu_last_error()
             raise EngineError(f"artis_gpu_{what} -> {rc}: {msg.decode() if msg else ''}")
+
+    def solve_temperatures(self, te):
+        """update_grid's temperature / ionisation solution (artis_gpu_solve_temperatures) on a TeArrays block, in
+        place; returns the device milliseconds."""
+        s = te.struct()
+        self._check(self.lib.artis_gpu_solve_temperatures(te.tables, C.byref(te.params), C.byref(s)),
+                    "solve_temperatures")
+        return float(self.lib.artis_gpu_last_te_ms())
 
     def upload_cellstate(self, nts):
         self._check(self.lib.artis_gpu_upload_cellstate(int(nts), self.model.cellstate), "upload_cellstate")

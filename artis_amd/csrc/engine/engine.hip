@@ -32,6 +32,7 @@
 #include "spectrum.h"
 #include "vpkt.h"
 #include "qag.h"
+#include "te_solver.h"
 
 // ================================================================================================= kernels
 
@@ -592,6 +593,7 @@ struct Engine {
   ncclComm_t comm = nullptr;
   int comm_ranks = 0;
   double *d_redblock = nullptr;
+  double last_te_ms = 0.;
   std::string last_error;
 };
 Engine G;
@@ -958,6 +960,152 @@ int run_wavefront(int64_t n, int nts, double t2) {
 
 // ============================================================================================== C ABI
 extern "C" {
+
+
+}  // extern "C"
+
+// ============================================================================ update_grid temperature solution
+// artis_gpu_solve_temperatures (include/artis_gpu.h, te_solver.h): every caller array is copied in, the solution
+// is computed for the listed cells and every array is copied back, so cells not listed round-trip unchanged.
+namespace {
+struct DevBufs {
+  std::vector<void *> p;
+  ~DevBufs() {
+    for (void *q : p) (void)hipFree(q);
+  }
+  template <typename T>
+  int get(T **d, size_t count, const T *src) {
+    if (count == 0) count = 1;
+    HIPCHK(hipMalloc((void **)d, count * sizeof(T)));
+    p.push_back((void *)*d);
+    if (src) HIPCHK(hipMemcpyAsync(*d, src, count * sizeof(T), hipMemcpyHostToDevice, G.stream));
+    return 0;
+  }
+};
+template <typename T>
+std::vector<T> d2h_vec(const T *d, size_t n) {
+  std::vector<T> h(n);
+  if (n) (void)hipMemcpy(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost);
+  return h;
+}
+}  // namespace
+
+extern "C" {
+int artis_gpu_solve_temperatures(const artis_te_tables *tab, const artis_te_params *par, artis_te_cells *c) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  const DevRun &R = G.K.R;
+  if (R.nlte_on || R.no_lut_photoion || R.no_lut_bfheating || R.nt_on) {
+    G.last_error = "solve_temperatures: only the LTE-population options (NLTE_POPS_ON, NO_LUT_*, NT_ON false)";
+    return ARTIS_ERR_UNSUPPORTED;
+  }
+  if (!tab || !par || !c || !tab->bfheating_coeff || !tab->ion_alpha_sp || c->ncells < 0 || (c->ncells > 0 && !c->mgi) ||
+      !c->TR || !c->W || !c->TJ || !c->rho || !c->thick || !c->elem_abundance || !c->elem_meanweight || !c->vol_init ||
+      !c->ffheatingestimator || !c->colheatingestimator || !c->gammaestimator || !c->bfheatingestimator || !c->Te ||
+      !c->groundlevelpop || !c->nne || !c->nnetot || !c->partfunct || !c->totalcooling || !c->cooling_contrib_ion ||
+      !(par->T_min > 0. && par->T_max > par->T_min && par->accuracy > 0. && par->tmin > 0. && par->t_current > 0.)) {
+    G.last_error = "solve_temperatures: NULL table / cell array or bad parameters";
+    return ARTIS_ERR_BAD_ARGUMENT;
+  }
+  const int np = G.npts_model, ne = G.nelements, ni = G.nions_total, nmx = G.maxnions;
+  const DevTab &T = G.K.T;
+  for (int k = 0; k < c->ncells; k++)
+    if (c->mgi[k] < 0 || c->mgi[k] >= np) {
+      G.last_error = "solve_temperatures: cell index out of range";
+      return ARTIS_ERR_BAD_ARGUMENT;
+    }
+  if (c->ncells == 0) return 0;
+  // the heating sum's level list (thermalbalance.cc:304-310): ionising levels of every ion but the top one
+  const std::vector<int32_t> nions = d2h_vec(T.elem_nions, ne), uoff = d2h_vec(T.elem_uniqueionoffset, ne),
+                             ionis = d2h_vec(T.ion_ionisinglevels, ni), ul0 = d2h_vec(T.ion_uniqueleveloffset, ni);
+  std::vector<int32_t> hb;
+  for (int e = 0; e < ne; e++) {
+    if (nions[e] > TE_MAX_IONS_PER_ELEMENT) {
+      G.last_error = "solve_temperatures: more ions per element than TE_MAX_IONS_PER_ELEMENT";
+      return ARTIS_ERR_UNSUPPORTED;
+    }
+    for (int i = 0; i < nions[e] - 1; i++)
+      for (int l = 0; l < ionis[uoff[e] + i]; l++) hb.push_back(ul0[uoff[e] + i] + l);
+  }
+  DevBufs B;
+  TeDev D{};
+  const size_t npf = (size_t)np, npi = (size_t)np * ni, npe = (size_t)np * ne, npg = (size_t)np * ne * nmx;
+  int rc = 0;
+  rc |= B.get((double **)&D.bfheat_lut, (size_t)T.tablesize * T.nbf, tab->bfheating_coeff);
+  rc |= B.get((float **)&D.alpha_sp, (size_t)ni * T.tablesize, tab->ion_alpha_sp);
+  rc |= B.get((int32_t **)&D.anumber, (size_t)ne, G.h_anumber.data());
+  rc |= B.get((int32_t **)&D.hb_ul, hb.size(), hb.data());
+  rc |= B.get((int32_t **)&D.mgi, (size_t)c->ncells, c->mgi);
+  rc |= B.get((float **)&D.TR, npf, c->TR);
+  rc |= B.get((float **)&D.W, npf, c->W);
+  rc |= B.get((float **)&D.TJ, npf, c->TJ);
+  rc |= B.get((float **)&D.rho, npf, c->rho);
+  rc |= B.get((int16_t **)&D.thick, npf, c->thick);
+  rc |= B.get((float **)&D.abund, npe, c->elem_abundance);
+  rc |= B.get((float **)&D.meanw, npe, c->elem_meanweight);
+  rc |= B.get((double **)&D.vol, npf, c->vol_init);
+  rc |= B.get((double **)&D.ffheat, npf, c->ffheatingestimator);
+  rc |= B.get((double **)&D.colheat, npf, c->colheatingestimator);
+  rc |= B.get((double **)&D.gamma, npg, c->gammaestimator);
+  rc |= B.get((double **)&D.bfest, npg, c->bfheatingestimator);
+  if (c->heating_dep) rc |= B.get((double **)&D.hdep, npf, c->heating_dep);
+  rc |= B.get(&D.Te, npf, c->Te);
+  rc |= B.get(&D.gp, npi, c->groundlevelpop);
+  rc |= B.get(&D.nne, npf, c->nne);
+  rc |= B.get(&D.nnetot, npf, c->nnetot);
+  rc |= B.get(&D.pf, npi, c->partfunct);
+  rc |= B.get(&D.totcool, npf, c->totalcooling);
+  rc |= B.get(&D.ccion, npi, c->cooling_contrib_ion);
+  if (c->heatingcoolingrates) rc |= B.get(&D.rates, npf * ARTIS_TE_NRATES, (const double *)c->heatingcoolingrates);
+  if (c->te_iterations) rc |= B.get(&D.iters, npf, (const int32_t *)c->te_iterations);
+  rc |= B.get(&D.upp, npe, (const int32_t *)nullptr);
+  rc |= B.get(&D.hbc, hb.size() * (size_t)c->ncells, (const double *)nullptr);
+  rc |= B.get(&D.fail, 1, (const int32_t *)nullptr);
+  if (rc) return ARTIS_ERR_HIP;
+  HIPCHK(hipMemsetAsync(D.fail, 0, sizeof(int32_t), G.stream));
+  D.nhb = (int32_t)hb.size();
+  D.ncells = c->ncells;
+  D.t_current = par->t_current;
+  D.tmin = par->tmin;
+  D.T_min = par->T_min;
+  D.T_max = par->T_max;
+  D.accuracy = par->accuracy;
+  D.initial_iteration = par->initial_iteration;
+  HIPCHK(hipEventRecord(G.ev0, G.stream));
+  if (D.nhb > 0) {
+    const int64_t nw = (int64_t)D.nhb * D.ncells;
+    k_te_bfheat<<<(unsigned)((nw + 255) / 256), 256, 0, G.stream>>>(G.K, D);
+  }
+  k_te_solve<<<(unsigned)((D.ncells + 63) / 64), 64, 0, G.stream>>>(G.K, D);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(G.ev1, G.stream));
+  HIPCHK(hipEventSynchronize(G.ev1));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, G.ev0, G.ev1));
+  G.last_te_ms = ms;
+  int32_t fail = 0;
+  HIPCHK(hipMemcpy(&fail, D.fail, sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c->Te, D.Te, npf * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c->groundlevelpop, D.gp, npi * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c->nne, D.nne, npf * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c->nnetot, D.nnetot, npf * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c->partfunct, D.pf, npi * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c->totalcooling, D.totcool, npf * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c->cooling_contrib_ion, D.ccion, npi * sizeof(double), hipMemcpyDeviceToHost));
+  if (c->heatingcoolingrates)
+    HIPCHK(hipMemcpy(c->heatingcoolingrates, D.rates, npf * ARTIS_TE_NRATES * sizeof(double), hipMemcpyDeviceToHost));
+  if (c->te_iterations) HIPCHK(hipMemcpy(c->te_iterations, D.iters, npf * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (fail) {
+    char buf[160];
+    snprintf(buf, sizeof buf,
+             "solve_temperatures: a GSL root-finder error (endpoints do not straddle zero / non-finite value) in "
+             "model cell %d -- the reference aborts here",
+             fail - 1);
+    G.last_error = buf;
+    return ARTIS_ERR_PACKET_FAULT;
+  }
+  return 0;
+}
+double artis_gpu_last_te_ms(void) { return G.last_te_ms; }
 
 int artis_gpu_abi_version(void) { return ARTIS_GPU_ABI_VERSION; }
 const char *artis_gpu_last_error(void) { return G.last_error.c_str(); }

@@ -60,6 +60,9 @@ struct Model {
   std::vector<double> groundcont_nu_edge;
   std::vector<int32_t> groundcont_element, groundcont_ion, groundcont_level, groundcont_target;
   std::vector<double> spontrecombcoeff, corrphotoioncoeff, bfcooling_coeff;
+  std::vector<double> bfheating_coeff;  // ratecoeff.cc:583-599 (update_grid's thermal balance)
+  std::vector<float> ion_alpha_sp;      // [nions_total * tablesize] ratecoeff.cc:967-990
+  artis_te_tables te_tables;
   std::vector<int32_t> cool_type, cool_element, cool_ion, cool_level, cool_upper;
   artis_atomic_tables at{};
 
@@ -473,6 +476,7 @@ void build_atomic(Model &m, std::mt19937_64 &rng) {
   m.spontrecombcoeff.assign((size_t)m.tablesize * m.nbfcontinua, 0.);
   m.corrphotoioncoeff.assign((size_t)m.tablesize * m.nbfcontinua, 0.);
   m.bfcooling_coeff.assign((size_t)m.tablesize * m.nbfcontinua, 0.);
+  m.bfheating_coeff.assign((size_t)m.tablesize * m.nbfcontinua, 0.);
   struct Job {
     int e, ion, lvl, t;
   };
@@ -514,8 +518,46 @@ void build_atomic(Model &m, std::mt19937_64 &rng) {
       m.spontrecombcoeff[idx] = alpha_sp * ARTIS_FOURPI * sfac * prob;
       m.corrphotoioncoeff[idx] = gammacorr * ARTIS_FOURPI * prob;
       m.bfcooling_coeff[idx] = bfcool * ARTIS_FOURPI * sfac * prob;
+      // approx_bfheating_integrand_gsl (ratecoeff.cc:325-343)
+      const double bfheat = integrate_phixs_range(m, nu_threshold, [&](double nu) {
+        const float s = phixs_xs_at(m, table, nu_threshold, nu);
+        const double dbb = ARTIS_TWOHOVERCLIGHTSQUARED * pow(nu, 3) / expm1(ARTIS_HOVERKB * nu / T);
+        return s * (1 - nu_threshold / nu) * dbb * (1 - exp(-ARTIS_HOVERKB * nu / T));
+      });
+      m.bfheating_coeff[idx] = bfheat * ARTIS_FOURPI * prob;
     }
   }
+  // precalculate_ion_alpha_sp (ratecoeff.cc:967-990): per ion, the sum of get_spontrecombcoeff (ratecoeff.cc:686-710)
+  // over its ionising levels and their targets at every table temperature; the top ion keeps calloc's zeros
+  m.ion_alpha_sp.assign((size_t)m.nions_total * m.tablesize, 0.f);
+  for (int iter = 0; iter < m.tablesize; iter++) {
+    const float T_e = m.mintemp * exp(iter * T_step_log);
+    for (int e = 0; e < m.nelements; e++)
+      for (int ion = 0; ion < m.elem_nions[e] - 1; ion++) {
+        const int ui = uniqueion(m, e, ion);
+        double zeta = 0.;
+        for (int lvl = 0; lvl < m.ion_ionisinglevels[ui]; lvl++)
+          for (int t = 0; t < get_nphixstargets(m, e, ion, lvl); t++) {
+            const int contindex = -1 - m.level_cont_index[uniquelevel(m, e, ion, lvl)] + t;
+            const int lowerindex = floor(log(T_e / m.mintemp) / T_step_log);
+            double a_sp;
+            if (lowerindex < m.tablesize - 1) {
+              const int upperindex = lowerindex + 1;
+              const double T_lower = m.mintemp * exp(lowerindex * T_step_log);
+              const double T_upper = m.mintemp * exp(upperindex * T_step_log);
+              const double f_upper = m.spontrecombcoeff[(size_t)upperindex * m.nbfcontinua + contindex];
+              const double f_lower = m.spontrecombcoeff[(size_t)lowerindex * m.nbfcontinua + contindex];
+              a_sp = (f_lower + (f_upper - f_lower) / (T_upper - T_lower) * (T_e - T_lower));
+            } else {
+              a_sp = m.spontrecombcoeff[(size_t)(m.tablesize - 1) * m.nbfcontinua + contindex];
+            }
+            zeta += a_sp;
+          }
+        m.ion_alpha_sp[(size_t)ui * m.tablesize + iter] = zeta;
+      }
+  }
+  m.te_tables.bfheating_coeff = m.bfheating_coeff.data();
+  m.te_tables.ion_alpha_sp = m.ion_alpha_sp.data();
 
   // ---- cooling list (kpkt.cc:313-426)
   m.ion_coolingoffset.assign(m.nions_total, 0);
@@ -1377,6 +1419,7 @@ void artis_model_free(artis_model *m) { delete m; }
 const artis_atomic_tables *artis_model_atomic(const artis_model *m) { return &m->at; }
 const artis_geometry *artis_model_geometry(const artis_model *m) { return &m->geom; }
 const artis_cell_state *artis_model_cellstate(const artis_model *m) { return &m->cs; }
+const artis_te_tables *artis_model_te_tables(const artis_model *m) { return &m->te_tables; }
 int64_t artis_model_npts_model(const artis_model *m) { return m->npts_model; }
 int artis_model_radfield_nbins(const artis_model *m) { return m->at.radfield_nbins; }
 void artis_model_config(const artis_model *m, artis_synth_config *out) { *out = m->cfg; }

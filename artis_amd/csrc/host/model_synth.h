@@ -68,6 +68,8 @@ void artis_model_free(artis_model *m);
 const artis_atomic_tables *artis_model_atomic(const artis_model *m);
 const artis_geometry *artis_model_geometry(const artis_model *m);
 const artis_cell_state *artis_model_cellstate(const artis_model *m);
+/* bf-heating LUT and per-ion Alpha_sp of the model (update_grid's thermal balance, artis_gpu_solve_temperatures) */
+const artis_te_tables *artis_model_te_tables(const artis_model *m);
 void artis_model_run_params(const artis_model *m, artis_run_params *out);
 
 /* LTE update_grid stand-in for timestep nts (densities scaled to ts_mid[nts]). */

@@ -427,3 +427,123 @@ def spectra_request(nnubins=1000, nprocs=1, abin=-1, syn_dir=(0., 0., 1.)):
     for k in range(3):
         r.syn_dir[k] = syn_dir[k]
     return r
+
+
+# update_grid's temperature / ionisation solution (include/artis_gpu.h artis_te_*; ABI 7)
+TE_NRATES = 8
+TE_RATE_NAMES = ["cooling_collisional", "cooling_fb", "cooling_ff", "cooling_adiabatic", "heating_collisional",
+                 "heating_bf", "heating_ff", "heating_dep"]
+
+
+class TeTables(C.Structure):
+    _fields_ = [("bfheating_coeff", C.c_void_p), ("ion_alpha_sp", C.c_void_p)]
+
+
+class TeParams(C.Structure):
+    _fields_ = [("t_current", C.c_double), ("tmin", C.c_double), ("T_min", C.c_double), ("T_max", C.c_double),
+                ("accuracy", C.c_double), ("initial_iteration", C.c_int32), ("pad0", C.c_int32)]
+
+
+_TE_CELL_PTRS = ["mgi", "TR", "W", "TJ", "rho", "thick", "elem_abundance", "elem_meanweight", "vol_init",
+                 "ffheatingestimator", "colheatingestimator", "gammaestimator", "bfheatingestimator", "heating_dep",
+                 "Te", "groundlevelpop", "nne", "nnetot", "partfunct", "totalcooling", "cooling_contrib_ion",
+                 "heatingcoolingrates", "te_iterations"]
+
+
+class TeCells(C.Structure):
+    _fields_ = [("ncells", C.c_int32), ("pad0", C.c_int32)] + [(n, C.c_void_p) for n in _TE_CELL_PTRS]
+
+
+class CellState(C.Structure):
+    """artis_cell_state (read-only view of a model's update_grid outputs)."""
+    _fields_ = [(n, C.c_void_p) for n in ("Te", "TR", "TJ", "W", "nne", "nnetot", "rho", "kappagrey", "thick",
+                                           "elem_abundance", "groundlevelpop", "partfunct", "totalcooling",
+                                           "cooling_contrib_ion", "corrphotoionrenorm", "ffegrp", "nlte_pops",
+                                           "radfield_bin_TR", "radfield_bin_W", "bfrate_estimator",
+                                           "nt_deposition_rate_density", "nt_ionization_ratecoeff",
+                                           "nt_prob_num_auger", "nt_ionenfrac_num_auger")]
+
+
+class AtomicHeader(C.Structure):
+    """The leading fields of artis_atomic_tables (counts, LUT grid, element arrays)."""
+    _fields_ = [("nelements", C.c_int32), ("maxnions", C.c_int32), ("nions_total", C.c_int32),
+                ("nlevels_total", C.c_int32), ("nlines", C.c_int32), ("nbfcontinua", C.c_int32),
+                ("nbfcontinua_ground", C.c_int32), ("ncoolingterms", C.c_int32), ("nphixspoints", C.c_int32),
+                ("nphixsnuincrement", C.c_double), ("last_phixs_nuovernuedge", C.c_double),
+                ("phixs_file_version", C.c_int32), ("tablesize", C.c_int32), ("mintemp", C.c_double),
+                ("maxtemp", C.c_double), ("elem_anumber", C.c_void_p), ("elem_nions", C.c_void_p),
+                ("elem_uniqueionoffset", C.c_void_p)]
+
+
+MH = 1.67352e-24
+
+
+class TeArrays:
+    """Host storage for one artis_te_cells block: the update_grid inputs of a model's non-empty cells (its current
+    cell state as the previous timestep's solution) plus synthetic normalised heating / photoionisation estimators
+    (seeded), and the output arrays.  The same block feeds the engine and the oracle."""
+
+    def __init__(self, model, t_current, seed=3, thick_frac=0.0, lte_all=False, gamma_zero_frac=0.1):
+        m = model
+        cs = CellState.from_address(m.cellstate)
+        hdr = AtomicHeader.from_address(m.atomic)
+        np_, nel, ni, mx = m.npts_model, m.nelements, m.nions_total, m.maxnions
+        f32 = lambda p, n: np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), (n,)).copy()  # noqa: E731
+        self.TR, self.W, self.TJ = f32(cs.TR, np_), f32(cs.W, np_), f32(cs.TJ, np_)
+        self.rho = f32(cs.rho, np_)
+        self.Te = f32(cs.Te, np_)
+        self.elem_abundance = f32(cs.elem_abundance, np_ * nel)
+        self.groundlevelpop = f32(cs.groundlevelpop, np_ * ni)
+        anum = np.ctypeslib.as_array(C.cast(hdr.elem_anumber, C.POINTER(C.c_int32)), (nel,)).copy()
+        rng = np.random.default_rng(seed)
+        self.thick = (rng.random(np_) < thick_frac).astype(np.int16)
+        if lte_all:
+            self.thick[:] = 1
+        # initstablemeannucmass stand-in: A ~ 2.1 Z nucleons
+        self.elem_meanweight = np.tile((2.1 * anum * MH).astype(np.float32), np_)
+        self.vol_init = np.full(np_, 1e45)
+        self.mgi_list = np.nonzero(self.rho > 0)[0].astype(np.int32)
+        # normalised estimators: heating terms of the order of the cell's LTE bf heating, spread per cell
+        self.ffheating = 10 ** rng.uniform(-12, -9, np_) * self.rho / 1e-14
+        self.colheating = 10 ** rng.uniform(-12, -9, np_) * self.rho / 1e-14
+        cell_scale = np.repeat(10 ** rng.uniform(-1.5, 3.0, np_), nel * mx)  # some cells balance inside [T_min, T_max]
+        self.bfheating = cell_scale * 10 ** rng.uniform(-0.3, 0.3, np_ * nel * mx)
+        self.gamma = 10 ** rng.uniform(-4., 1., np_ * nel * mx)
+        self.gamma[rng.random(np_ * nel * mx) < gamma_zero_frac] = 0.
+        self.heating_dep = None
+        self.nne = np.zeros(np_, np.float32)
+        self.nnetot = np.zeros(np_, np.float32)
+        self.partfunct = np.zeros(np_ * ni, np.float32)
+        self.totalcooling = np.zeros(np_)
+        self.cooling_contrib_ion = np.zeros(np_ * ni)
+        self.rates = np.zeros(np_ * TE_NRATES)
+        self.iters = np.zeros(np_, np.int32)
+        self.params = TeParams(t_current=float(t_current), tmin=float(m.cfg.tmin_days) * 86400.0,
+                               T_min=float(hdr.mintemp), T_max=float(hdr.maxtemp), accuracy=1e-2,
+                               initial_iteration=0)
+        self.tables = C.c_void_p(model._lib.artis_model_te_tables(model._h))
+
+    def struct(self):
+        s = TeCells()
+        s.ncells = len(self.mgi_list)
+        for n, a in (("mgi", self.mgi_list), ("TR", self.TR), ("W", self.W), ("TJ", self.TJ), ("rho", self.rho),
+                     ("thick", self.thick), ("elem_abundance", self.elem_abundance),
+                     ("elem_meanweight", self.elem_meanweight), ("vol_init", self.vol_init),
+                     ("ffheatingestimator", self.ffheating), ("colheatingestimator", self.colheating),
+                     ("gammaestimator", self.gamma), ("bfheatingestimator", self.bfheating), ("Te", self.Te),
+                     ("groundlevelpop", self.groundlevelpop), ("nne", self.nne), ("nnetot", self.nnetot),
+                     ("partfunct", self.partfunct), ("totalcooling", self.totalcooling),
+                     ("cooling_contrib_ion", self.cooling_contrib_ion), ("heatingcoolingrates", self.rates),
+                     ("te_iterations", self.iters)):
+            setattr(s, n, a.ctypes.data)
+        if self.heating_dep is not None:
+            s.heating_dep = self.heating_dep.ctypes.data
+        return s
+
+    def copy(self):
+        import copy as _c
+        o = _c.copy(self)
+        for k, v in self.__dict__.items():
+            if isinstance(v, np.ndarray):
+                setattr(o, k, v.copy())
+        return o

@@ -27,7 +27,7 @@ def model_lib():
         lib.artis_model_from_files.argtypes = [C.POINTER(ffi.SynthConfig), C.c_char_p, C.c_char_p, C.c_char_p]
         lib.artis_model_from_files.restype = C.c_void_p
         lib.artis_model_free.argtypes = [C.c_void_p]
-        for fn in ("artis_model_atomic", "artis_model_geometry", "artis_model_cellstate"):
+        for fn in ("artis_model_atomic", "artis_model_geometry", "artis_model_cellstate", "artis_model_te_tables"):
             getattr(lib, fn).argtypes = [C.c_void_p]
             getattr(lib, fn).restype = C.c_void_p
         lib.artis_model_run_params.argtypes = [C.c_void_p, C.POINTER(ffi.RunParams)]

@@ -532,12 +532,76 @@ int64_t artis_gpu_last_rounds(void);  /* event-queue rounds of the last update (
  * queue binning (k_ma_bin / scan / k_ma_scatter) and the exact jumps (k_ma_exact) */
 int artis_gpu_last_kernel_times(double ms[4], int64_t launches[4]);
 const char *artis_gpu_last_error(void);
-#define ARTIS_GPU_ABI_VERSION 6  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
+
+/* ------------------------------------------------------------------------------------------------------------ */
+/* update_grid's temperature / ionisation solution for the LTE-population options (NLTE_POPS_ON false, LUT       */
+/* photoionisation and bf heating, NT_ON false: artisoptions_classic.h, artisoptions_kilonova_lte.h), SURVEY.md */
+/* §8(f) row 4.  Per model cell, what update_grid_cell does once the estimators are normalised                  */
+/* (update_grid.cc:1104-1158, 1199-1205):                                                                       */
+/*  - LTE branch (initial_iteration or thick == 1, update_grid.cc:1106-1125): T_e = T_J, precalculate_partfuncts */
+/*    (update_grid.cc:23-38), calculate_populations (update_grid.cc:1427-1658);                                 */
+/*  - otherwise solve_Te_nltepops (update_grid.cc:763-886): calculate_bfheatingcoeffs (thermalbalance.cc:141-187),*/
+/*    precalculate_partfuncts, call_T_e_finder (thermalbalance.cc:397-597: GSL Brent on heating - cooling, each */
+/*    evaluation re-solving the ionisation balance with its own Brent on n_e) and calculate_populations;        */
+/*  - then kpkt::calculate_cooling_rates (kpkt.cc:84-165): totalcooling and cooling_contrib_ion.               */
+/* The run-wide switches (excitation temperature, MINPOP) are those given to artis_gpu_init.                    */
+/* ------------------------------------------------------------------------------------------------------------ */
+typedef struct artis_te_tables {
+  const double *bfheating_coeff;  /* [tablesize * nbfcontinua] globals::bfheating_coeff, get_bflutindex order */
+  const float *ion_alpha_sp;      /* [nions_total * tablesize] elements[].ions[].Alpha_sp (input.cc:938) */
+} artis_te_tables;
+
+typedef struct artis_te_params {
+  double t_current;           /* globals::time_step[nts_for_te].mid (update_grid.cc:804-806) */
+  double tmin;                /* globals::tmin */
+  double T_min, T_max;        /* MINTEMP, MAXTEMP (the T_e search interval) */
+  double accuracy;            /* TEMPERATURE_SOLVER_ACCURACY */
+  int32_t initial_iteration;  /* globals::initial_iteration */
+  int32_t pad0;
+} artis_te_params;
+
+#define ARTIS_TE_NRATES 8  /* heatingcoolingrates (thermalbalance.h:4-14): cooling collisional, fb, ff, adiabatic,
+                              heating collisional, bf, ff, dep */
+typedef struct artis_te_cells {
+  int32_t ncells;
+  int32_t pad0;
+  const int32_t *mgi;                  /* [ncells] model cells to solve */
+  /* inputs, indexed by mgi ([npts_model] unless stated) */
+  const float *TR, *W, *TJ, *rho;
+  const int16_t *thick;                /* before this timestep's update (grid::modelgrid[].thick) */
+  const float *elem_abundance;         /* [npts_model * nelements] mass fractions */
+  const float *elem_meanweight;        /* [npts_model * nelements] grid::get_element_meanweight [g] */
+  const double *vol_init;              /* grid::vol_init_modelcell */
+  const double *ffheatingestimator;    /* normalised (update_grid.cc:1133-1134) */
+  const double *colheatingestimator;
+  const double *gammaestimator;        /* [npts_model * nelements * maxnions] normalised (update_grid.cc:888-975) */
+  const double *bfheatingestimator;    /*   ditto */
+  const double *heating_dep;           /* do_rlc_est == 3: deposition rate density * nt_frac_heating
+                                          (thermalbalance.cc:373-376); NULL: 0 */
+  /* in / out */
+  float *Te;                           /* in: T_e of the previous timestep; out: the solution */
+  float *groundlevelpop;               /* [npts_model * nions_total] in: previous values (partition functions) */
+  /* outputs */
+  float *nne, *nnetot;
+  float *partfunct;                    /* [npts_model * nions_total] */
+  double *totalcooling;
+  double *cooling_contrib_ion;         /* [npts_model * nions_total] */
+  double *heatingcoolingrates;         /* [npts_model * ARTIS_TE_NRATES] of the last thermal-balance evaluation (0 for
+                                          LTE-branch cells); may be NULL */
+  int32_t *te_iterations;              /* [npts_model] Brent iterations of call_T_e_finder (-1: no root in [T_min,
+                                          T_max], 0: LTE branch); may be NULL */
+} artis_te_cells;
+int artis_gpu_solve_temperatures(const artis_te_tables *tables, const artis_te_params *params, artis_te_cells *cells);
+/* device time (ms) of the last artis_gpu_solve_temperatures (the k_te_solve kernel alone) */
+double artis_gpu_last_te_ms(void);
+
+#define ARTIS_GPU_ABI_VERSION 7  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
                                     3: virtual packets (artis_vpkt_params / artis_vpkt_result);
                                     4: artis_run_params.excitation_temperature;
                                     5: host estimator block pack/unpack, RCCL communicator + all-reduce;
                                     6: the nebular path (NLTE / superlevel populations, binned radiation field,
-                                       detailed bf estimators, NO_LUT photoionisation, non-thermal ionisation) */
+                                       detailed bf estimators, NO_LUT photoionisation, non-thermal ionisation);
+                                    7: update_grid's temperature / ionisation solution (artis_gpu_solve_temperatures) */
 int artis_gpu_abi_version(void);
 
 #ifdef __cplusplus

@@ -39,6 +39,7 @@
 #include <omp.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <atomic>
 #include <cmath>
 #include <cstdint>
@@ -3673,4 +3674,645 @@ int oracle_spectra(const artis_atomic_tables *at, const artis_geometry *g, const
   return 0;
 }
 
+}  // extern "C"
+
+// ================================================================================================================
+// update_grid's temperature / ionisation solution for the LTE-population options, the
+// checker of artis_gpu_solve_temperatures.  Restated in the reference's order throughout (no deviations): GSL's
+// Brent root finder, calculate_populations, precalculate_partfuncts, calculate_bfheatingcoeffs (LUT branch),
+// calculate_cooling_rates, calculate_heating_rates, T_e_eqn_heating_minus_cooling and call_T_e_finder.
+// ================================================================================================================
+namespace {
+
+// GSL 2.x roots/brent.c + roots/fsolver.c (gsl_root_fsolver_set / _iterate / _root / _x_lower / _x_upper) and
+// roots/convergence.c (gsl_root_test_interval), as update_grid.cc:1583-1599 and thermalbalance.cc:460-477 drive
+// them.  A non-finite function value or endpoints that do not straddle zero are GSL_ERROR calls, i.e. an abort()
+// under GSL's default error handler (the reference never switches it off): reported here as status -1.
+struct GslBrent {
+  double a, b, c, d, e, fa, fb, fc;
+  double root, x_lower, x_upper;
+};
+template <class F>
+int gsl_brent_set(GslBrent &s, F &f, double x_lower, double x_upper) {
+  s.root = 0.5 * (x_lower + x_upper);
+  s.x_lower = x_lower;
+  s.x_upper = x_upper;
+  const double f_lower = f(x_lower);
+  if (!std::isfinite(f_lower)) return -1;
+  const double f_upper = f(x_upper);
+  if (!std::isfinite(f_upper)) return -1;
+  s.a = x_lower;
+  s.fa = f_lower;
+  s.b = x_upper;
+  s.fb = f_upper;
+  s.c = x_upper;
+  s.fc = f_upper;
+  s.d = x_upper - x_lower;
+  s.e = x_upper - x_lower;
+  if ((f_lower < 0.0 && f_upper < 0.0) || (f_lower > 0.0 && f_upper > 0.0)) return -1;
+  return 0;
+}
+template <class F>
+int gsl_brent_iterate(GslBrent &s, F &f) {
+  double a = s.a, b = s.b, c = s.c, fa = s.fa, fb = s.fb, fc = s.fc, d = s.d, e = s.e;
+  int ac_equal = 0;
+  if ((fb < 0 && fc < 0) || (fb > 0 && fc > 0)) {
+    ac_equal = 1;
+    c = a;
+    fc = fa;
+    d = b - a;
+    e = b - a;
+  }
+  if (fabs(fc) < fabs(fb)) {
+    ac_equal = 1;
+    a = b;
+    b = c;
+    c = a;
+    fa = fb;
+    fb = fc;
+    fc = fa;
+  }
+  const double tol = 0.5 * DBL_EPSILON * fabs(b);
+  const double m = 0.5 * (c - b);
+  if (fb == 0) {
+    s.root = b;
+    s.x_lower = b;
+    s.x_upper = b;
+    return 0;
+  }
+  if (fabs(m) <= tol) {
+    s.root = b;
+    if (b < c) {
+      s.x_lower = b;
+      s.x_upper = c;
+    } else {
+      s.x_lower = c;
+      s.x_upper = b;
+    }
+    return 0;
+  }
+  if (fabs(e) < tol || fabs(fa) <= fabs(fb)) {
+    d = m;
+    e = m;
+  } else {
+    double p, q, r;
+    const double sr = fb / fa;
+    if (ac_equal) {
+      p = 2 * m * sr;
+      q = 1 - sr;
+    } else {
+      q = fa / fc;
+      r = fb / fc;
+      p = sr * (2 * m * q * (q - r) - (b - a) * (r - 1));
+      q = (q - 1) * (r - 1) * (sr - 1);
+    }
+    if (p > 0)
+      q = -q;
+    else
+      p = -p;
+    if (2 * p < std::min(3 * m * q - fabs(tol * q), fabs(e * q))) {
+      e = d;
+      d = p / q;
+    } else {
+      d = m;
+      e = m;
+    }
+  }
+  a = b;
+  fa = fb;
+  if (fabs(d) > tol)
+    b += d;
+  else
+    b += (m > 0 ? +tol : -tol);
+  fb = f(b);
+  if (!std::isfinite(fb)) return -1;
+  s.a = a;
+  s.b = b;
+  s.c = c;
+  s.d = d;
+  s.e = e;
+  s.fa = fa;
+  s.fb = fb;
+  s.fc = fc;
+  s.root = b;
+  if ((fb < 0 && fc < 0) || (fb > 0 && fc > 0)) c = a;
+  if (b < c) {
+    s.x_lower = b;
+    s.x_upper = c;
+  } else {
+    s.x_lower = c;
+    s.x_upper = b;
+  }
+  return 0;
+}
+// gsl_root_test_interval: 1 = GSL_CONTINUE
+inline int gsl_test_interval(double x_lower, double x_upper, double epsabs, double epsrel) {
+  const double abs_lower = fabs(x_lower), abs_upper = fabs(x_upper);
+  double min_abs;
+  if ((x_lower > 0.0 && x_upper > 0.0) || (x_lower < 0.0 && x_upper < 0.0))
+    min_abs = std::min(abs_lower, abs_upper);
+  else
+    min_abs = 0;
+  const double tolerance = epsabs + epsrel * min_abs;
+  return fabs(x_upper - x_lower) < tolerance ? 0 : 1;
+}
+
+// the mutable grid state one cell's solution writes (grid::modelgrid[mgi]); Ctx::cs points at these arrays
+struct TeGrid {
+  std::vector<float> Te, TJ, nne, nnetot, gp, pf;
+  std::vector<int> uppermost;  // [npts_model * nelements] elements_uppermost_ion
+};
+struct TeRun {
+  const artis_te_tables *tab;
+  const artis_te_params *par;
+  const artis_te_cells *in;
+  TeGrid *g;
+};
+
+inline float elem_meanweight(const Ctx &c, const TeRun &r, int mgi, int e) {
+  return r.in->elem_meanweight[(size_t)mgi * c.at->nelements + e];
+}
+inline float elem_abundance(const Ctx &c, int mgi, int e) { return c.cs->elem_abundance[(size_t)mgi * c.at->nelements + e]; }
+// grid.cc:231-236
+inline double get_elem_numberdens(const Ctx &c, const TeRun &r, int mgi, int e) {
+  const double mw = elem_meanweight(c, r, mgi, e);
+  return elem_abundance(c, mgi, e) / mw * (double)c.cs->rho[mgi];
+}
+inline float &gp_ref(const Ctx &c, const TeRun &r, int mgi, int e, int i) {
+  return r.g->gp[(size_t)mgi * c.at->nions_total + uion(c, e, i)];
+}
+inline float &pf_ref(const Ctx &c, const TeRun &r, int mgi, int e, int i) {
+  return r.g->pf[(size_t)mgi * c.at->nions_total + uion(c, e, i)];
+}
+
+// ltepop.cc:488-537 (LTE populations: calculate_levelpop_nominpop = calculate_levelpop_lte)
+double te_calculate_partfunct(const Ctx &c, const TeRun &r, int mgi, int e, int i) {
+  int initial = 0;
+  double pop_store = 0.;
+  if (get_groundlevelpop(c, mgi, e, i) < c.minpop) {
+    pop_store = get_groundlevelpop(c, mgi, e, i);
+    initial = 1;
+    gp_ref(c, r, mgi, e, i) = 1.0;
+  }
+  double U = 1.;
+  const int nlevels = get_nlevels(c, e, i);
+  const double groundpop = get_groundlevelpop(c, mgi, e, i);
+  for (int level = 1; level < nlevels; level++) {
+    bool skipminpop;
+    const double nn = calculate_levelpop_nominpop(c, mgi, e, i, level, &skipminpop) / groundpop;
+    U += nn;
+  }
+  U *= stat_weight(c, e, i, 0);
+  if (initial == 1) gp_ref(c, r, mgi, e, i) = pop_store;
+  return U;
+}
+// update_grid.cc:23-38
+void te_precalculate_partfuncts(const Ctx &c, const TeRun &r, int mgi) {
+  for (int e = 0; e < c.at->nelements; e++)
+    for (int i = 0; i < get_nions(c, e); i++) pf_ref(c, r, mgi, e, i) = te_calculate_partfunct(c, r, mgi, e, i);
+}
+
+// ltepop.cc:97-113
+double interpolate_ions_spontrecombcoeff(const Ctx &c, const TeRun &r, int e, int i, double T) {
+  const int tablesize = c.at->tablesize;
+  const float *alpha = r.tab->ion_alpha_sp + (size_t)uion(c, e, i) * tablesize;
+  const int lowerindex = floor(log(T / c.at->mintemp) / c.T_step_log);
+  if (lowerindex < tablesize - 1) {
+    const int upperindex = lowerindex + 1;
+    const double T_lower = c.at->mintemp * exp(lowerindex * c.T_step_log);
+    const double T_upper = c.at->mintemp * exp(upperindex * c.T_step_log);
+    const double f_upper = alpha[upperindex];
+    const double f_lower = alpha[lowerindex];
+    return f_lower + (f_upper - f_lower) / (T_upper - T_lower) * (T - T_lower);
+  }
+  return alpha[tablesize - 1];
+}
+inline bool te_use_lte_ratio(const TeRun &r, int mgi) { return r.par->initial_iteration || r.in->thick[mgi] == 1; }
+inline double gammaestimator(const Ctx &c, const TeRun &r, int mgi, int e, int i) {
+  return r.in->gammaestimator[(size_t)mgi * c.at->nelements * c.at->maxnions + e * c.at->maxnions + i];
+}
+// ltepop.cc:115-239 (NT_ON false: Y_nt = 0; NLTE_POPS_ON false: Alpha_sp from the ion table)
+double te_phi(const Ctx &c, const TeRun &r, int mgi, int e, int i) {
+  double phi = 0;
+  const float T_e = c.cs->Te[mgi];
+  if (te_use_lte_ratio(r, mgi)) {
+    const double ionpot = epsilon(c, e, i + 1, 0) - epsilon(c, e, i, 0);
+    const double partfunct_ratio = pf_ref(c, r, mgi, e, i) / pf_ref(c, r, mgi, e, i + 1);
+    phi = partfunct_ratio * ARTIS_SAHACONST * pow(T_e, -1.5) * exp(ionpot / ARTIS_KB / T_e);
+  } else {
+    const double Gamma = gammaestimator(c, r, mgi, e, i);
+    const double Gamma_ion = Gamma * stat_weight(c, e, i, 0) / pf_ref(c, r, mgi, e, i);
+    const double Alpha_st = 0.;
+    const double Alpha_sp = interpolate_ions_spontrecombcoeff(c, r, e, i, T_e);
+    const double Col_rec = 0.;
+    const double Y_nt = 0.0;
+    phi = (Alpha_sp + Alpha_st + Col_rec) / (Gamma_ion + Y_nt);
+  }
+  return phi;
+}
+// ltepop.cc:61-95
+void te_get_ionfractions(const Ctx &c, const TeRun &r, int e, int mgi, double nne, double *ionfractions, int uppermost_ion) {
+  double nnionfactor[64];
+  nnionfactor[uppermost_ion] = 1;
+  double denominator = 1.;
+  for (int ion = uppermost_ion - 1; ion >= 0; ion--) {
+    nnionfactor[ion] = nnionfactor[ion + 1] * nne * te_phi(c, r, mgi, e, ion);
+    denominator += nnionfactor[ion];
+  }
+  for (int ion = 0; ion <= uppermost_ion; ion++) {
+    const double numerator = nnionfactor[ion];
+    ionfractions[ion] = numerator / denominator;
+    if (!std::isfinite(ionfractions[ion])) ionfractions[ion] = 0;
+  }
+}
+// ltepop.cc:20-59
+double te_nne_solution_f(const Ctx &c, const TeRun &r, int mgi, double x) {
+  const double rho = c.cs->rho[mgi];
+  double outersum = 0.;
+  for (int e = 0; e < c.at->nelements; e++) {
+    const float abundance = elem_abundance(c, mgi, e);
+    if (abundance > 0 && get_nions(c, e) > 0) {
+      const double elem_mw = elem_meanweight(c, r, mgi, e);
+      double innersum = 0.;
+      const int uppermost_ion = r.g->uppermost[(size_t)mgi * c.at->nelements + e];
+      double ionfractions[64];
+      te_get_ionfractions(c, r, e, mgi, x, ionfractions, uppermost_ion);
+      for (int ion = 0; ion <= uppermost_ion; ion++) innersum += (get_ionstage(c, e, ion) - 1) * ionfractions[ion];
+      outersum += abundance / elem_mw * innersum;
+    }
+  }
+  return rho * outersum - x;
+}
+// update_grid.cc:1427-1658 (NO_LUT_PHOTOION false, NT_ON false, FORCE_LTE undefined); -1: the GSL abort path
+int te_calculate_populations(const Ctx &c, const TeRun &r, int mgi, double *nntot_out) {
+  const int nel = c.at->nelements;
+  double nne_hi = c.cs->rho[mgi] / ARTIS_MH;
+  int only_neutral_ions = 0;
+  int nelements_in_cell = 0;
+  for (int e = 0; e < nel; e++) {
+    const int nions = get_nions(c, e);
+    int &upp = r.g->uppermost[(size_t)mgi * nel + e];
+    upp = nions - 1;
+    const double abundance = elem_abundance(c, mgi, e);
+    if (abundance > 0) {
+      int uppermost_ion;
+      if (te_use_lte_ratio(r, mgi)) {
+        uppermost_ion = get_nions(c, e) - 1;
+      } else {
+        int ion;
+        for (ion = 0; ion < nions - 1; ion++) {
+          const double Gamma = gammaestimator(c, r, mgi, e, ion);
+          if (Gamma == 0) break;
+        }
+        uppermost_ion = ion;
+      }
+      double factor = 1.;
+      int ion;
+      for (ion = 0; ion < uppermost_ion; ion++) {
+        factor *= nne_hi * te_phi(c, r, mgi, e, ion);
+        if (!std::isfinite(factor)) break;
+      }
+      uppermost_ion = ion;
+      upp = uppermost_ion;
+      if (uppermost_ion == 0) only_neutral_ions++;
+      nelements_in_cell++;
+    }
+  }
+  float nne = 0.;
+  double nne_tot = 0.;
+  double nntot = 0.;
+  if (only_neutral_ions == nelements_in_cell) {
+    for (int e = 0; e < nel; e++) {
+      const double nnelement = get_elem_numberdens(c, r, mgi, e);
+      nne_tot += nnelement * c.at->elem_anumber[e];
+      const int nions = get_nions(c, e);
+      for (int ion = 0; ion < nions; ion++) {
+        double nnion;
+        if (ion == 0)
+          nnion = nnelement;
+        else if (nnelement > 0.)
+          nnion = c.minpop;
+        else
+          nnion = 0.;
+        nntot += nnion;
+        nne += nnion * (get_ionstage(c, e, ion) - 1);
+        gp_ref(c, r, mgi, e, ion) = (nnion * stat_weight(c, e, ion, 0) / pf_ref(c, r, mgi, e, ion));
+      }
+    }
+    nntot += nne;
+    if (nne < c.minpop) nne = c.minpop;
+    r.g->nne[mgi] = nne;
+  } else {
+    double nne_lo = 0.;
+    auto f = [&](double x) { return te_nne_solution_f(c, r, mgi, x); };
+    GslBrent s;
+    if (gsl_brent_set(s, f, nne_lo, nne_hi) != 0) return -1;
+    int iter = 0;
+    const int maxit = 100;
+    const double fractional_accuracy = 1e-3;
+    int status;
+    do {
+      iter++;
+      if (gsl_brent_iterate(s, f) != 0) return -1;
+      nne = s.root;
+      nne_lo = s.x_lower;
+      nne_hi = s.x_upper;
+      status = gsl_test_interval(nne_lo, nne_hi, 0, fractional_accuracy);
+    } while (status == 1 && iter < maxit);
+    if (nne < c.minpop) nne = c.minpop;
+    r.g->nne[mgi] = nne;
+    nne_tot = 0.;
+    nntot = nne;
+    for (int e = 0; e < nel; e++) {
+      const int nions = get_nions(c, e);
+      const double nnelement = get_elem_numberdens(c, r, mgi, e);
+      nne_tot += nnelement * c.at->elem_anumber[e];
+      const int uppermost_ion = r.g->uppermost[(size_t)mgi * nel + e];
+      double ionfractions[64];
+      if (nnelement > 0) te_get_ionfractions(c, r, e, mgi, nne, ionfractions, uppermost_ion);
+      for (int ion = 0; ion < nions; ion++) {
+        double nnion;
+        if (ion <= uppermost_ion) {
+          if (nnelement > 0) {
+            nnion = nnelement * ionfractions[ion];
+            if (nnion < c.minpop) nnion = c.minpop;
+          } else {
+            nnion = 0.;
+          }
+        } else {
+          nnion = c.minpop;
+        }
+        nntot += nnion;
+        gp_ref(c, r, mgi, e, ion) = (nnion * stat_weight(c, e, ion, 0) / pf_ref(c, r, mgi, e, ion));
+      }
+    }
+  }
+  r.g->nnetot[mgi] = nne_tot;
+  *nntot_out = nntot;
+  return 0;
+}
+
+struct TeRates {
+  double cooling_collisional, cooling_fb, cooling_ff, cooling_adiabatic, heating_collisional, heating_bf, heating_ff,
+      heating_dep;
+};
+// kpkt.cc:41-67, 84-165
+void te_calculate_cooling_rates(const Ctx &c, int mgi, TeRates *hc, double *totalcooling, double *contrib_ion) {
+  const float nne = c.cs->nne[mgi];
+  const float T_e = c.cs->Te[mgi];
+  const artis_atomic_tables &a = *c.at;
+  double C_total = 0., C_ff_all = 0., C_fb_all = 0., C_exc_all = 0., C_ionization_all = 0.;
+  for (int e = 0; e < a.nelements; e++) {
+    const int nions = get_nions(c, e);
+    for (int i = 0; i < nions; i++) {
+      double C_ion = 0.;
+      const int nionisinglevels = get_ionisinglevels(c, e, i);
+      const double nncurrention = ionstagepop(c, mgi, e, i);
+      const int ioncharge = get_ionstage(c, e, i) - 1;
+      if (ioncharge > 0) {
+        const double C_ff_ion = 1.426e-27 * sqrt((double)T_e) * pow(ioncharge, 2) * nncurrention * nne;
+        C_ff_all += C_ff_ion;
+        C_ion += C_ff_ion;
+      }
+      double C_exc = 0.;
+      const int nlevels = get_nlevels(c, e, i);
+      for (int level = 0; level < nlevels; level++) {
+        const double nnlevel = calculate_levelpop(c, mgi, e, i, level);
+        const double epsilon_current = epsilon(c, e, i, level);
+        const double statweight = stat_weight(c, e, i, level);
+        const int ul = ulev(c, e, i, level);
+        const int nuptrans = a.level_nuptrans[ul];
+        for (int ii = 0; ii < nuptrans; ii++) {
+          const int li = a.uptrans_lineindex[a.level_uptrans_offset[ul] + ii];
+          const int upper = a.line_upperlevelindex[li];
+          const double epsilon_trans = epsilon(c, e, i, upper) - epsilon_current;
+          const double C = nnlevel *
+                           col_excitation_ratecoeff(c, T_e, nne, li, epsilon_trans, statweight, stat_weight(c, e, i, upper)) *
+                           epsilon_trans;
+          C_exc += C;
+        }
+      }
+      C_exc_all += C_exc;
+      C_ion += C_exc;
+      if (i < nions - 1) {
+        for (int level = 0; level < nionisinglevels; level++) {
+          const double epsilon_current = epsilon(c, e, i, level);
+          const double nnlevel = calculate_levelpop(c, mgi, e, i, level);
+          const int nt = get_nphixstargets(c, e, i, level);
+          for (int t = 0; t < nt; t++) {
+            const int upper = get_phixsupperlevel(c, e, i, level, t);
+            const double epsilon_trans = epsilon(c, e, i + 1, upper) - epsilon_current;
+            const double C = nnlevel * col_ionization_ratecoeff(c, T_e, nne, e, i, level, t, epsilon_trans) * epsilon_trans;
+            C_ionization_all += C;
+            C_ion += C;
+          }
+          for (int t = 0; t < nt; t++) {
+            const double nnupperion = ionstagepop(c, mgi, e, i + 1);
+            const double C = get_bfcoolingcoeff(c, e, i, level, t, T_e) * nnupperion * nne;
+            C_fb_all += C;
+            C_ion += C;
+          }
+        }
+      }
+      C_total += C_ion;
+      if (contrib_ion) contrib_ion[uion(c, e, i)] = C_ion;
+    }
+  }
+  if (totalcooling) *totalcooling = C_total;
+  if (hc) {
+    hc->cooling_collisional = C_exc_all + C_ionization_all;
+    hc->cooling_fb = C_fb_all;
+    hc->cooling_ff = C_ff_all;
+  }
+}
+// thermalbalance.cc:34-57 get_bfheatingcoeff_ana
+double te_bfheatingcoeff_ana(const Ctx &c, const TeRun &r, int e, int i, int l, int t, double T, double W) {
+  const int tablesize = c.at->tablesize;
+  double bfheatingcoeff = 0.;
+  const int lowerindex = floor(log(T / c.at->mintemp) / c.T_step_log);
+  if (lowerindex < tablesize - 1) {
+    const int upperindex = lowerindex + 1;
+    const double T_lower = c.at->mintemp * exp(lowerindex * c.T_step_log);
+    const double T_upper = c.at->mintemp * exp(upperindex * c.T_step_log);
+    const double f_upper = r.tab->bfheating_coeff[get_bflutindex(c, upperindex, e, i, l, t)];
+    const double f_lower = r.tab->bfheating_coeff[get_bflutindex(c, lowerindex, e, i, l, t)];
+    bfheatingcoeff = (f_lower + (f_upper - f_lower) / (T_upper - T_lower) * (T - T_lower));
+  } else {
+    bfheatingcoeff = r.tab->bfheating_coeff[get_bflutindex(c, tablesize - 1, e, i, l, t)];
+  }
+  return W * bfheatingcoeff;
+}
+// thermalbalance.cc:141-187 (NO_LUT_BFHEATING false): per level of the cell
+void te_calculate_bfheatingcoeffs(const Ctx &c, const TeRun &r, int mgi, std::vector<double> &coeff) {
+  coeff.assign(c.at->nlevels_total, 0.);
+  for (int e = 0; e < c.at->nelements; e++)
+    for (int i = 0; i < get_nions(c, e); i++)
+      for (int l = 0; l < get_nlevels(c, e, i); l++) {
+        double bfheatingcoeff = 0.;
+        for (int t = 0; t < get_nphixstargets(c, e, i, l); t++) {
+          const double T_R = r.in->TR[mgi];
+          const double W = r.in->W[mgi];
+          bfheatingcoeff += te_bfheatingcoeff_ana(c, r, e, i, l, t, T_R, W);
+        }
+        const int g = c.at->level_closestgroundlevelcont[ulev(c, e, i, l)];
+        if (g >= 0) bfheatingcoeff *= r.in->bfheatingestimator[(size_t)mgi * c.at->nelements * c.at->maxnions + g];
+        coeff[ulev(c, e, i, l)] = bfheatingcoeff;
+      }
+}
+// thermalbalance.cc:218-346 (DIRECT_COL_HEAT undefined)
+void te_calculate_heating_rates(const Ctx &c, const TeRun &r, int mgi, const std::vector<double> &coeff, TeRates *hc) {
+  double bfheating = 0.;
+  for (int e = 0; e < c.at->nelements; e++) {
+    const int nions = get_nions(c, e);
+    for (int i = 0; i < nions - 1; i++) {
+      const int nbflevels = get_ionisinglevels(c, e, i);
+      for (int level = 0; level < nbflevels; level++) {
+        const double nnlevel = calculate_levelpop(c, mgi, e, i, level);
+        bfheating += nnlevel * coeff[ulev(c, e, i, level)];
+      }
+    }
+  }
+  hc->heating_collisional = r.in->colheatingestimator[mgi];
+  hc->heating_bf = bfheating;
+  hc->heating_ff = r.in->ffheatingestimator[mgi];
+}
+// thermalbalance.cc:348-395; -1 in *fail on the GSL abort path
+double te_eqn_heating_minus_cooling(const Ctx &c, const TeRun &r, int mgi, double T_e, const std::vector<double> &coeff,
+                                    TeRates *hc, int *fail) {
+  r.g->Te[mgi] = T_e;
+  double nntot = 0.;
+  if (te_calculate_populations(c, r, mgi, &nntot) != 0) {
+    *fail = 1;
+    return NAN;
+  }
+  te_calculate_cooling_rates(c, mgi, hc, nullptr, nullptr);
+  te_calculate_heating_rates(c, r, mgi, coeff, hc);
+  hc->heating_dep = r.in->heating_dep ? r.in->heating_dep[mgi] : 0.;
+  const double p = nntot * ARTIS_KB * T_e;
+  const double volumetmin = r.in->vol_init[mgi];
+  const double dV = 3 * volumetmin / pow(r.par->tmin, 3) * pow(r.par->t_current, 2);
+  const double V = volumetmin * pow(r.par->t_current / r.par->tmin, 3);
+  hc->cooling_adiabatic = p * dV / V;
+  const double total_heating_rate = hc->heating_ff + hc->heating_bf + hc->heating_collisional + hc->heating_dep;
+  const double total_coolingrate = hc->cooling_ff + hc->cooling_fb + hc->cooling_collisional + hc->cooling_adiabatic;
+  return total_heating_rate - total_coolingrate;
+}
+// thermalbalance.cc:397-597; returns the Brent iteration count (-1: no root in the interval), -2 on the abort path
+int te_call_T_e_finder(const Ctx &c, const TeRun &r, int mgi, const std::vector<double> &coeff, TeRates *hc) {
+  const double T_min = r.par->T_min, T_max = r.par->T_max;
+  const double T_e_old = r.g->Te[mgi];
+  int fail = 0;
+  auto f = [&](double T) { return te_eqn_heating_minus_cooling(c, r, mgi, T, coeff, hc, &fail); };
+  double thermalmin = f(T_min);
+  double thermalmax = f(T_max);
+  if (fail) return -2;
+  if (!std::isfinite(thermalmin) || !std::isfinite(thermalmax)) thermalmax = thermalmin = -1;
+  double T_e = 0.;
+  int iters = -1;
+  if (thermalmin * thermalmax < 0) {
+    GslBrent s;
+    if (gsl_brent_set(s, f, T_min, T_max) != 0 || fail) return -2;
+    const int maxit = 100;
+    for (int iternum = 0; iternum < maxit; iternum++) {
+      if (gsl_brent_iterate(s, f) != 0 || fail) return -2;
+      T_e = s.root;
+      iters = iternum + 1;
+      if (gsl_test_interval(s.x_lower, s.x_upper, 0, r.par->accuracy) != 1) break;
+    }
+  } else if (thermalmax < 0) {
+    T_e = T_min;
+  } else {
+    T_e = T_max;
+  }
+  if (T_e > 2 * T_e_old) {
+    T_e = 2 * T_e_old;
+    if (T_e > T_max) T_e = T_max;
+  } else if (T_e < 0.5 * T_e_old) {
+    T_e = 0.5 * T_e_old;
+    if (T_e < T_min) T_e = T_min;
+  }
+  r.g->Te[mgi] = T_e;
+  f(T_e);
+  if (fail) return -2;
+  return iters;
+}
+
+}  // namespace
+
+extern "C" {
+// artis_gpu_solve_temperatures restated (include/artis_gpu.h): the reference's per-cell update_grid solution for the
+// LTE-population options, cells in parallel (OpenMP), each in the reference's serial order.
+int oracle_solve_temperatures(const artis_atomic_tables *at, const artis_run_params *rp, const artis_te_tables *tab,
+                              const artis_te_params *par, artis_te_cells *in, int npts_model, int nthreads) {
+  if (rp->nlte_pops_on || rp->no_lut_photoion || rp->no_lut_bfheating || rp->nt_on) return ARTIS_ERR_UNSUPPORTED;
+  const size_t ni = at->nions_total, nel = at->nelements;
+  TeGrid g;
+  g.Te.assign(in->Te, in->Te + npts_model);
+  g.TJ.assign(in->TJ, in->TJ + npts_model);
+  g.nne.assign(npts_model, 0.f);
+  g.nnetot.assign(npts_model, 0.f);
+  g.gp.assign(in->groundlevelpop, in->groundlevelpop + (size_t)npts_model * ni);
+  g.pf.assign((size_t)npts_model * ni, 0.f);
+  g.uppermost.assign((size_t)npts_model * nel, 0);
+  artis_cell_state cs;
+  memset(&cs, 0, sizeof(cs));
+  cs.Te = g.Te.data();
+  cs.TJ = g.TJ.data();
+  cs.TR = in->TR;
+  cs.W = in->W;
+  cs.nne = g.nne.data();
+  cs.rho = in->rho;
+  cs.elem_abundance = in->elem_abundance;
+  cs.groundlevelpop = g.gp.data();
+  cs.partfunct = g.pf.data();
+  Ctx c;
+  c.at = at;
+  c.g = nullptr;
+  c.cs = &cs;
+  c.rp = *rp;
+  c.gs = nullptr;
+  c.T_step_log = (log(at->maxtemp) - log(at->mintemp)) / (at->tablesize - 1.);
+  c.minpop = rp->minpop > 0. ? rp->minpop : 1e-30;
+  TeRun r{tab, par, in, &g};
+  int rc = 0;
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic)
+  for (int k = 0; k < in->ncells; k++) {
+    const int mgi = in->mgi[k];
+    TeRates hc;
+    memset(&hc, 0, sizeof(hc));
+    int iters = 0;
+    if (te_use_lte_ratio(r, mgi)) {
+      // update_grid.cc:1111-1124 (T_J from get_T_J_from_J is the caller's TJ)
+      g.Te[mgi] = in->TJ[mgi];
+      te_precalculate_partfuncts(c, r, mgi);
+      double nntot;
+      if (te_calculate_populations(c, r, mgi, &nntot) != 0) iters = -2;
+    } else {
+      // update_grid.cc:763-886 without NLTE_POPS_ON (one pass of the nlte_iter loop)
+      std::vector<double> coeff;
+      te_calculate_bfheatingcoeffs(c, r, mgi, coeff);
+      te_precalculate_partfuncts(c, r, mgi);
+      iters = te_call_T_e_finder(c, r, mgi, coeff, &hc);
+      double nntot;
+      if (iters != -2 && te_calculate_populations(c, r, mgi, &nntot) != 0) iters = -2;
+    }
+    if (iters == -2) {
+#pragma omp critical
+      rc = ARTIS_ERR_PACKET_FAULT;
+      continue;
+    }
+    te_calculate_cooling_rates(c, mgi, nullptr, &in->totalcooling[mgi], in->cooling_contrib_ion + (size_t)mgi * ni);
+    in->Te[mgi] = g.Te[mgi];
+    in->nne[mgi] = g.nne[mgi];
+    in->nnetot[mgi] = g.nnetot[mgi];
+    for (size_t u = 0; u < ni; u++) {
+      in->groundlevelpop[(size_t)mgi * ni + u] = g.gp[(size_t)mgi * ni + u];
+      in->partfunct[(size_t)mgi * ni + u] = g.pf[(size_t)mgi * ni + u];
+    }
+    if (in->heatingcoolingrates) memcpy(in->heatingcoolingrates + (size_t)mgi * ARTIS_TE_NRATES, &hc, sizeof(hc));
+    if (in->te_iterations) in->te_iterations[mgi] = iters;
+  }
+  return rc;
+}
 }  // extern "C"

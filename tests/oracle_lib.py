@@ -117,3 +117,14 @@ def spectra(model, packets, nnubins=1000, nprocs=1, abin=-1, syn_dir=(0., 0., 1.
     if rc != 0:
         raise RuntimeError(f"oracle_spectra -> {rc}")
     return out
+
+
+def solve_temperatures(model, te, params=None, nthreads=0):
+    """oracle_solve_temperatures on a TeArrays block (in place); returns the status."""
+    L = lib()
+    L.oracle_solve_temperatures.argtypes = [C.c_void_p, C.POINTER(ffi.RunParams), C.c_void_p,
+                                            C.POINTER(ffi.TeParams), C.POINTER(ffi.TeCells), C.c_int, C.c_int]
+    s = te.struct()
+    rc = L.oracle_solve_temperatures(model.atomic, C.byref(params if params is not None else model.params), te.tables,
+                                     C.byref(te.params), C.byref(s), model.npts_model, nthreads)
+    return rc

