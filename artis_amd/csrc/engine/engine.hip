@@ -1060,6 +1060,14 @@ int artis_gpu_solve_temperatures(const artis_te_tables *tab, const artis_te_para
   rc |= B.get(&D.upp, npe, (const int32_t *)nullptr);
   rc |= B.get(&D.hbc, hb.size() * (size_t)c->ncells, (const double *)nullptr);
   rc |= B.get(&D.fail, 1, (const int32_t *)nullptr);
+  {
+    // the packed excitation items, indexed like uptrans_lineindex (whose extent is the largest offset + count)
+    const std::vector<int32_t> nup = d2h_vec(T.level_nuptrans, T.nlevels_total),
+                               upo = d2h_vec(T.level_uptrans_offset, T.nlevels_total);
+    size_t nitems = 0;
+    for (int l = 0; l < T.nlevels_total; l++) nitems = std::max(nitems, (size_t)upo[l] + (size_t)nup[l]);
+    rc |= B.get((TeExcItem **)&D.exc, nitems, (const TeExcItem *)nullptr);
+  }
   if (rc) return ARTIS_ERR_HIP;
   HIPCHK(hipMemsetAsync(D.fail, 0, sizeof(int32_t), G.stream));
   D.nhb = (int32_t)hb.size();
@@ -1071,11 +1079,24 @@ int artis_gpu_solve_temperatures(const artis_te_tables *tab, const artis_te_para
   D.accuracy = par->accuracy;
   D.initial_iteration = par->initial_iteration;
   HIPCHK(hipEventRecord(G.ev0, G.stream));
+  k_te_items<<<(unsigned)((T.nlevels_total + 255) / 256), 256, 0, G.stream>>>(G.K, (TeExcItem *)D.exc);
   if (D.nhb > 0) {
     const int64_t nw = (int64_t)D.nhb * D.ncells;
     k_te_bfheat<<<(unsigned)((nw + 255) / 256), 256, 0, G.stream>>>(G.K, D);
   }
-  k_te_solve<<<(unsigned)((D.ncells + 63) / 64), 64, 0, G.stream>>>(G.K, D);
+  // lanes per cell: enough for the per-ion collisional-excitation sums of the cooling rate (te_cooling_rates);
+  // ARTIS_GPU_TE_LANES overrides (1 = one cell per lane)
+  int g = 1;
+  while (g < ni && g < 64) g *= 2;
+  if (const char *ev = getenv("ARTIS_GPU_TE_LANES")) {
+    const int v = atoi(ev);
+    if (v >= 1 && v <= 64 && (v & (v - 1)) == 0) g = v;
+  }
+  const int cpw = 64 / g;
+  Ctx *dK = nullptr;
+  TeDev *dD = nullptr;
+  if (B.get(&dK, 1, &G.K) || B.get(&dD, 1, &D)) return ARTIS_ERR_HIP;
+  k_te_solve<<<(unsigned)((D.ncells + cpw - 1) / cpw), 64, 0, G.stream>>>(dK, dD, g);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(G.ev1, G.stream));
   HIPCHK(hipEventSynchronize(G.ev1));

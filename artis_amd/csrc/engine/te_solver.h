@@ -14,7 +14,17 @@
 //                 calculate_populations and calculate_cooling_rates; or the LTE branch (update_grid.cc:1106-1125)
 #pragma once
 
+// one collisional-excitation term of get_cooling_ion_coll_exc (kpkt.cc:53-63) at its up-transition index: what
+// col_excitation_ratecoeff (macroatom.h:107-150) reads, so the per-line loop is one independent 32-byte load
+struct TeExcItem {
+  double epsilon_trans;  // epsilon(upper) - epsilon(level)
+  double P2;             // LineMA::P2 of the line
+  float coll_str, osc_f, upper_sw;
+  int32_t forbidden;
+};
+
 struct TeDev {
+  const TeExcItem *exc;  // [sum nuptrans] by level_uptrans_offset
   // tables
   const double *bfheat_lut;  // [tablesize * nbf]
   const float *alpha_sp;     // [nions_total * tablesize]
@@ -45,6 +55,7 @@ struct TeDev {
 struct TeState {
   int k, mgi;
   float Te;
+  int g, sub, lane0;  // the cell's lane group: size, this lane's index in it, its first lane in the wave
 };
 
 // ltepop.cc:307-327
@@ -81,7 +92,7 @@ DEVFN double te_ionstagepop(const Ctx &K, const TeDev &D, const TeState &s, int 
 }
 
 // ltepop.cc:488-537 + update_grid.cc:23-38
-DEVFN void te_precalculate_partfuncts(const Ctx &K, const TeDev &D, const TeState &s) {
+DEVNI void te_precalculate_partfuncts(const Ctx &K, const TeDev &D, const TeState &s) {
   const int ni = K.T.nions_total;
   for (int e = 0; e < K.T.nelements; e++)
     for (int i = 0; i < K.T.elem_nions[e]; i++) {
@@ -290,7 +301,7 @@ DEVFN double te_elem_numberdens(const Ctx &K, const TeDev &D, int mgi, int e) {
   return D.abund[(int64_t)mgi * K.T.nelements + e] / mw * (double)D.rho[mgi];
 }
 // ltepop.cc:20-59
-DEVFN double te_nne_solution_f(const Ctx &K, const TeDev &D, const TeState &s, double x) {
+DEVNI double te_nne_solution_f(const Ctx &K, const TeDev &D, const TeState &s, double x) {
   const double rho = D.rho[s.mgi];
   double outersum = 0.;
   for (int e = 0; e < K.T.nelements; e++) {
@@ -308,7 +319,7 @@ DEVFN double te_nne_solution_f(const Ctx &K, const TeDev &D, const TeState &s, d
   return rho * outersum - x;
 }
 // update_grid.cc:1427-1658 (NO_LUT_PHOTOION false, NT_ON false); -1: the GSL abort path
-DEVFN int te_calculate_populations(const Ctx &K, const TeDev &D, const TeState &s, double *nntot_out) {
+DEVNI int te_calculate_populations(const Ctx &K, const TeDev &D, const TeState &s, double *nntot_out) {
   const int nel = K.T.nelements, ni = K.T.nions_total;
   const int mgi = s.mgi;
   double nne_hi = D.rho[mgi] / ARTIS_MH;
@@ -425,16 +436,66 @@ struct TeRates {
   double cooling_collisional, cooling_fb, cooling_ff, cooling_adiabatic, heating_collisional, heating_bf, heating_ff,
       heating_dep;
 };
-// kpkt.cc:41-67, 84-165
-DEVFN void te_cooling_rates(const Ctx &K, const TeDev &D, const TeState &s, TeRates *hc, bool store) {
+// macroatom.h:107-150 col_excitation_ratecoeff on a packed item (the same expressions)
+DEVFN double te_col_exc(const TeExcItem &it, float T_e, float nne, double lowerstatweight) {
+  double C = 0.;
+  const double coll_strength = it.coll_str;
+  const double eoverkt = it.epsilon_trans / (ARTIS_KB * T_e);
+  if (coll_strength < 0) {
+    if (!it.forbidden) {
+      const double g_bar = 0.2;
+      const double exp_eoverkt = exp(eoverkt);
+      const double test = 0.276 * exp_eoverkt * (-0.5772156649 - log(eoverkt));
+      const double Gamma = g_bar > test ? g_bar : test;
+      C = ARTIS_C_0 * nne * sqrtf(T_e) * 14.51039491 * it.osc_f * it.P2 * eoverkt / exp_eoverkt * Gamma;
+    } else {
+      C = nne * 8.629e-6 * 0.01 * exp(-eoverkt) * (double)it.upper_sw / sqrtf(T_e);
+    }
+  } else {
+    C = nne * 8.629e-6 * coll_strength * exp(-eoverkt) / lowerstatweight / sqrtf(T_e);
+  }
+  return C;
+}
+// kpkt.cc:41-67 get_cooling_ion_coll_exc for one ion: its own serial sum over levels and up-transitions
+DEVNI double te_coll_exc_ion(const Ctx &K, const TeDev &D, const TeState &s, int ui, float T_e, float nne) {
+  const int e = K.T.ion_element[ui];
+  const int ul0 = K.T.ion_uniqueleveloffset[ui];
+  double C_exc = 0.;
+  const int nlevels = K.T.ion_nlevels[ui];
+  for (int level = 0; level < nlevels; level++) {
+    const int ul = ul0 + level;
+    const int nuptrans = K.T.level_nuptrans[ul];
+    if (nuptrans == 0) continue;
+    const double nnlevel = te_levelpop(K, D, s, e, ui, level);
+    const double statweight = K.T.level_stat_weight[ul];
+    const TeExcItem *it = D.exc + K.T.level_uptrans_offset[ul];
+#pragma unroll 2
+    for (int ii = 0; ii < nuptrans; ii++) {
+      const TeExcItem x = it[ii];
+      const double C = nnlevel * te_col_exc(x, T_e, nne, statweight) * x.epsilon_trans;
+      C_exc += C;
+    }
+  }
+  return C_exc;
+}
+// kpkt.cc:84-165 calculate_cooling_rates.  The cell's G lanes (s.g lanes from s.lane0, all on the same control path)
+// split the per-ion collisional-excitation sums -- independent sums in the reference, each kept in its order -- and
+// exchange them by lane shuffles; every lane then combines the ions in the reference's order.
+DEVNI void te_cooling_rates(const Ctx &K, const TeDev &D, const TeState &s, TeRates *hc, bool store) {
   const float nne = D.nne[s.mgi];
   const float T_e = s.Te;
   const int ni = K.T.nions_total;
   double C_total = 0., C_ff_all = 0., C_fb_all = 0., C_exc_all = 0., C_ionization_all = 0.;
-  for (int e = 0; e < K.T.nelements; e++) {
-    const int nions = K.T.elem_nions[e];
-    for (int i = 0; i < nions; i++) {
-      const int ui = uion(K, e, i);
+  for (int ub = 0; ub < ni; ub += s.g) {
+    const int my_ui = ub + s.sub;
+    double mine = 0.;
+    if (my_ui < ni) mine = te_coll_exc_ion(K, D, s, my_ui, T_e, nne);
+    for (int j = 0; j < s.g && ub + j < ni; j++) {
+      const double C_exc = __shfl(mine, s.lane0 + j, 64);
+      const int ui = ub + j;
+      const int e = K.T.ion_element[ui];
+      const int i = ui - K.T.elem_uniqueionoffset[e];
+      const int nions = K.T.elem_nions[e];
       const int ul0 = K.T.ion_uniqueleveloffset[ui];
       double C_ion = 0.;
       const int nionisinglevels = K.T.ion_ionisinglevels[ui];
@@ -444,27 +505,6 @@ DEVFN void te_cooling_rates(const Ctx &K, const TeDev &D, const TeState &s, TeRa
         const double C_ff_ion = 1.426e-27 * sqrt((double)T_e) * pow((double)ioncharge, 2) * nncurrention * nne;
         C_ff_all += C_ff_ion;
         C_ion += C_ff_ion;
-      }
-      double C_exc = 0.;
-      const int nlevels = K.T.ion_nlevels[ui];
-      for (int level = 0; level < nlevels; level++) {
-        const int ul = ul0 + level;
-        const int nuptrans = K.T.level_nuptrans[ul];
-        if (nuptrans == 0) continue;
-        const double nnlevel = te_levelpop(K, D, s, e, ui, level);
-        const double epsilon_current = K.T.level_epsilon[ul];
-        const double statweight = K.T.level_stat_weight[ul];
-        const int uoff = K.T.level_uptrans_offset[ul];
-        for (int ii = 0; ii < nuptrans; ii++) {
-          const int li = K.T.uptrans_lineindex[uoff + ii];
-          const int uu = ul0 + K.T.line_upper[li];
-          const double epsilon_trans = K.T.level_epsilon[uu] - epsilon_current;
-          const double C = nnlevel *
-                           col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight,
-                                                    (double)K.T.level_stat_weight[uu]) *
-                           epsilon_trans;
-          C_exc += C;
-        }
       }
       C_exc_all += C_exc;
       C_ion += C_exc;
@@ -500,7 +540,7 @@ DEVFN void te_cooling_rates(const Ctx &K, const TeDev &D, const TeState &s, TeRa
   }
 }
 // thermalbalance.cc:218-346 (DIRECT_COL_HEAT undefined)
-DEVFN void te_heating_rates(const Ctx &K, const TeDev &D, const TeState &s, TeRates *hc) {
+DEVNI void te_heating_rates(const Ctx &K, const TeDev &D, const TeState &s, TeRates *hc) {
   double bfheating = 0.;
   for (int j = 0; j < D.nhb; j++) {
     const int ul = D.hb_ul[j];
@@ -514,7 +554,7 @@ DEVFN void te_heating_rates(const Ctx &K, const TeDev &D, const TeState &s, TeRa
   hc->heating_ff = D.ffheat[s.mgi];
 }
 // thermalbalance.cc:348-395
-DEVFN double te_eqn(const Ctx &K, const TeDev &D, TeState &s, double T_e, TeRates *hc, int *fail) {
+DEVNI double te_eqn(const Ctx &K, const TeDev &D, TeState &s, double T_e, TeRates *hc, int *fail) {
   s.Te = T_e;
   double nntot = 0.;
   if (te_calculate_populations(K, D, s, &nntot) != 0) {
@@ -532,6 +572,28 @@ DEVFN double te_eqn(const Ctx &K, const TeDev &D, TeState &s, double T_e, TeRate
   const double total_heating_rate = hc->heating_ff + hc->heating_bf + hc->heating_collisional + hc->heating_dep;
   const double total_coolingrate = hc->cooling_ff + hc->cooling_fb + hc->cooling_collisional + hc->cooling_adiabatic;
   return total_heating_rate - total_coolingrate;
+}
+
+// the packed collisional-excitation items, one workitem per level
+__global__ void k_te_items(Ctx K, TeExcItem *exc) {
+  const int ul = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ul >= K.T.nlevels_total) return;
+  const int ui = K.T.level_ui[ul];
+  const int ul0 = K.T.ion_uniqueleveloffset[ui];
+  const double epsilon_current = K.T.level_epsilon[ul];
+  const int uoff = K.T.level_uptrans_offset[ul];
+  for (int ii = 0; ii < K.T.level_nuptrans[ul]; ii++) {
+    const int li = K.T.uptrans_lineindex[uoff + ii];
+    const int uu = ul0 + K.T.line_upper[li];
+    TeExcItem x;
+    x.epsilon_trans = K.T.level_epsilon[uu] - epsilon_current;
+    x.P2 = K.T.line_ma[li].P2;
+    x.coll_str = K.T.line_coll[li];
+    x.osc_f = K.T.line_f[li];
+    x.upper_sw = K.T.level_stat_weight[uu];
+    x.forbidden = K.T.line_forbidden[li];
+    exc[uoff + ii] = x;
+  }
 }
 
 // thermalbalance.cc:141-187 (NO_LUT_BFHEATING false) for the levels the heating sum visits; workitem = (j, cell)
@@ -557,11 +619,20 @@ __global__ void k_te_bfheat(Ctx K, TeDev D) {
   D.hbc[(int64_t)j * D.ncells + k] = bfheatingcoeff;
 }
 
-__global__ __launch_bounds__(64) void k_te_solve(Ctx K, TeDev D) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= D.ncells) return;
+// one wave = 64 / g cells, g lanes each (g a power of two); every lane of a group runs its cell's solution
+__global__ __launch_bounds__(64, 4) void k_te_solve(const Ctx *__restrict__ Kp, const TeDev *__restrict__ Dp, int g) {
+  // context and parameters by device pointer: the solver's functions are not inlined (register pressure), and a
+  // by-value kernel argument referenced from them would be copied to scratch
+  const Ctx &K = *Kp;
+  const TeDev &D = *Dp;
+  const int lane = threadIdx.x;
+  const int k = blockIdx.x * (64 / g) + lane / g;
+  if (k >= D.ncells) return;  // whole groups leave together
   TeState s;
   s.k = k;
+  s.g = g;
+  s.sub = lane & (g - 1);
+  s.lane0 = lane & ~(g - 1);
   s.mgi = D.mgi[k];
   s.Te = D.Te[s.mgi];
   const int mgi = s.mgi;

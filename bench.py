@@ -97,6 +97,8 @@ def main():
     ap.add_argument("--nts", type=int, default=10)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU time of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-update-grid", action="store_true",
+                    help="skip the update_grid temperature-solution measurement (artis_gpu_solve_temperatures)")
     ap.add_argument("--vpkt", type=int, default=0,
                     help="virtual packets (BASELINE config 5, vpkt.cc) with this many observer directions; the "
                          "timestep must lie in the vspec window [10 d, 30 d] (e.g. --nts 30)")
@@ -265,6 +267,35 @@ def main():
             "sample": f"first {n_sample} packets of the same ensemble, same timestep, {cpu_dt:.1f} s",
         }
 
+    ugrid = None
+    if rank == 0 and not args.no_update_grid and vcfg is None:
+        # SURVEY §8(f) row 4, after the timed region: update_grid's temperature / ionisation solution for every
+        # non-empty cell (artis_gpu_solve_temperatures), and the oracle on a cell sample for the CPU rate and parity
+        from artis_amd import ffi
+
+        t_cur = 1.5 * float(model.cfg.tmin_days) * 86400.0
+        te = ffi.TeArrays(model, t_current=t_cur, seed=4)
+        eng.solve_temperatures(te.copy())  # warm
+        te_ms = eng.solve_temperatures(te)
+        ugrid = {"kernel": "k_te_bfheat + k_te_solve", "cells": int(len(te.mgi_list)), "gpu_ms": te_ms,
+                 "rooted_cells": int((te.iters[te.mgi_list] > 0).sum())}
+        if not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(REPO, "tests"))
+            import oracle_lib
+
+            nthreads, _ = cpu_share()
+            sub = ffi.TeArrays(model, t_current=t_cur, seed=4)
+            sub.mgi_list = te.mgi_list[:: max(1, len(te.mgi_list) // 128)][:128].copy()
+            t = time.perf_counter()
+            oracle_lib.solve_temperatures(model, sub, nthreads=nthreads)
+            dt = time.perf_counter() - t
+            g = sub.mgi_list
+            agree = (sub.iters[g] == te.iters[g]) & (np.abs(sub.Te[g] - te.Te[g]) <= 1e-9 * np.abs(sub.Te[g]))
+            ugrid["cpu_baseline"] = {"cells": int(len(g)), "seconds": dt, "threads": nthreads, "kind": "port",
+                                     "cells_per_s": len(g) / dt}
+            ugrid["gpu_cells_per_s"] = len(te.mgi_list) / (te_ms / 1e3)
+            ugrid["parity_sample"] = {"cells": int(len(g)), "iterations_and_Te_agree": float(agree.mean())}
+
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -318,6 +349,8 @@ def main():
                  "gc_updates", "ma_jumps", "ma_trans", "kpkt", "kpkt_terms", "escaped", "es_scat", "bb_events",
                  "cont_events"], work)},
         }
+        if ugrid is not None:
+            line["update_grid"] = ugrid
         if vcfg is not None:
             vms = float(np.mean([v[0] for v in vstats]))
             line["config"]["workload"] += (f"; virtual packets: {vcfg.nobs} observers x {vcfg.nspectra} spectra, "
