@@ -217,15 +217,12 @@ __global__ void k_cooling(Ctx K) {
     const double statweight = K.T.level_stat_weight[ul];
     const int nuptrans = K.T.level_nuptrans[ul];
     if (nuptrans > 0) {
-      const int uoff = K.T.level_uptrans_offset[ul];
+      // the packed excitation terms (TeExcItem): one independent load per line instead of a dependent chain
+      const TeExcItem *it = K.T.exc_items + K.T.level_uptrans_offset[ul];
+#pragma unroll 2
       for (int ii = 0; ii < nuptrans; ii++) {
-        const int li = K.T.uptrans_lineindex[uoff + ii];
-        const int uu = K.T.ion_uniqueleveloffset[ui] + K.T.line_upper[li];
-        const double epsilon_trans = K.T.level_epsilon[uu] - epsilon_current;
-        const double C = nnlevel *
-                         col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight,
-                                                  (double)K.T.level_stat_weight[uu]) *
-                         epsilon_trans;
+        const TeExcItem x = it[ii];
+        const double C = nnlevel * te_col_exc(x, T_e, nne, statweight) * x.epsilon_trans;
         contrib += C;
       }
       cc[idxc++] = contrib;
@@ -1060,14 +1057,6 @@ int artis_gpu_solve_temperatures(const artis_te_tables *tab, const artis_te_para
   rc |= B.get(&D.upp, npe, (const int32_t *)nullptr);
   rc |= B.get(&D.hbc, hb.size() * (size_t)c->ncells, (const double *)nullptr);
   rc |= B.get(&D.fail, 1, (const int32_t *)nullptr);
-  {
-    // the packed excitation items, indexed like uptrans_lineindex (whose extent is the largest offset + count)
-    const std::vector<int32_t> nup = d2h_vec(T.level_nuptrans, T.nlevels_total),
-                               upo = d2h_vec(T.level_uptrans_offset, T.nlevels_total);
-    size_t nitems = 0;
-    for (int l = 0; l < T.nlevels_total; l++) nitems = std::max(nitems, (size_t)upo[l] + (size_t)nup[l]);
-    rc |= B.get((TeExcItem **)&D.exc, nitems, (const TeExcItem *)nullptr);
-  }
   if (rc) return ARTIS_ERR_HIP;
   HIPCHK(hipMemsetAsync(D.fail, 0, sizeof(int32_t), G.stream));
   D.nhb = (int32_t)hb.size();
@@ -1079,7 +1068,6 @@ int artis_gpu_solve_temperatures(const artis_te_tables *tab, const artis_te_para
   D.accuracy = par->accuracy;
   D.initial_iteration = par->initial_iteration;
   HIPCHK(hipEventRecord(G.ev0, G.stream));
-  k_te_items<<<(unsigned)((T.nlevels_total + 255) / 256), 256, 0, G.stream>>>(G.K, (TeExcItem *)D.exc);
   if (D.nhb > 0) {
     const int64_t nw = (int64_t)D.nhb * D.ncells;
     k_te_bfheat<<<(unsigned)((nw + 255) / 256), 256, 0, G.stream>>>(G.K, D);
@@ -1580,6 +1568,32 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     lm[li] = {B_ul, B_lu, pow(nu_trans, 3), pow(ARTIS_H_IONPOT / epsilon_trans, 2)};
   }
   rc |= dupload(&T.line_ma, lm.data(), nli);
+  {
+    // packed collisional-excitation terms (TeExcItem) indexed like uptrans_lineindex
+    size_t nitems = 0;
+    for (int ul = 0; ul < nl; ul++)
+      nitems = std::max(nitems, (size_t)a->level_uptrans_offset[ul] + (size_t)a->level_nuptrans[ul]);
+    std::vector<TeExcItem> items(std::max<size_t>(nitems, 1));
+    for (int ui = 0; ui < a->nions_total; ui++) {
+      const int ul0 = a->ion_uniqueleveloffset[ui];
+      for (int l = 0; l < a->ion_nlevels[ui]; l++) {
+        const int ul = ul0 + l;
+        for (int ii = 0; ii < a->level_nuptrans[ul]; ii++) {
+          const int j = a->level_uptrans_offset[ul] + ii;
+          const int li = a->uptrans_lineindex[j];
+          const int uu = ul0 + a->line_upperlevelindex[li];
+          TeExcItem &x = items[j];
+          x.epsilon_trans = a->level_epsilon[uu] - a->level_epsilon[ul];
+          x.P2 = lm[li].P2;
+          x.coll_str = a->line_coll_str[li];
+          x.osc_f = a->line_osc_strength[li];
+          x.upper_sw = a->level_stat_weight[uu];
+          x.forbidden = a->line_forbidden[li];
+        }
+      }
+    }
+    rc |= dupload(&T.exc_items, items.data(), items.size());
+  }
   // macro-atom records per level (engine_dev.h DevCells::ma_rec): recombination targets are the ionising levels
   // of the lower ion for levels l <= maxrecombininglevel of ions i > 0 (macroatom.cc:104-124); up-higher targets
   // are the phixs targets of ionising levels of non-top ions (get_nphixstargets)

@@ -43,6 +43,15 @@ struct LineMA {
   double P2;    // pow(H_ionpot / (eps_upper - eps_lower), 2)    (macroatom.h:93, 130)
 };
 
+// one collisional-excitation term of get_cooling_ion_coll_exc (kpkt.cc:53-63) at its up-transition index: what
+// col_excitation_ratecoeff (macroatom.h:107-150) reads, so a per-line cooling loop is one independent 32-byte load
+struct TeExcItem {
+  double epsilon_trans;  // epsilon(upper) - epsilon(level)
+  double P2;             // LineMA::P2 of the line
+  float coll_str, osc_f, upper_sw;
+  int32_t forbidden;
+};
+
 struct DevTab {
   int32_t nelements, maxnions, nions_total, nlevels_total, nlines, nbf, nbfg, ncoolingterms;
   int32_t nphixspoints, phixs_file_version, tablesize, ntargets_total;
@@ -65,6 +74,7 @@ struct DevTab {
   const uint8_t *line_forbidden;
   const LineTau *line_tau;
   const LineMA *line_ma;
+  const TeExcItem *exc_items;  // [sum nuptrans] indexed like uptrans_lineindex (k_cooling, k_te_solve)
   // per level: offset (doubles) of its macro-atom record inside a cell's record block, #downtrans, #uptrans,
   // #recombination targets (ionising levels of the lower ion, 0 if the level does not recombine)
   const MaMeta *ma_meta;  // [nlevels_total]

@@ -14,17 +14,7 @@
 //                 calculate_populations and calculate_cooling_rates; or the LTE branch (update_grid.cc:1106-1125)
 #pragma once
 
-// one collisional-excitation term of get_cooling_ion_coll_exc (kpkt.cc:53-63) at its up-transition index: what
-// col_excitation_ratecoeff (macroatom.h:107-150) reads, so the per-line loop is one independent 32-byte load
-struct TeExcItem {
-  double epsilon_trans;  // epsilon(upper) - epsilon(level)
-  double P2;             // LineMA::P2 of the line
-  float coll_str, osc_f, upper_sw;
-  int32_t forbidden;
-};
-
 struct TeDev {
-  const TeExcItem *exc;  // [sum nuptrans] by level_uptrans_offset
   // tables
   const double *bfheat_lut;  // [tablesize * nbf]
   const float *alpha_sp;     // [nions_total * tablesize]
@@ -468,7 +458,7 @@ DEVNI double te_coll_exc_ion(const Ctx &K, const TeDev &D, const TeState &s, int
     if (nuptrans == 0) continue;
     const double nnlevel = te_levelpop(K, D, s, e, ui, level);
     const double statweight = K.T.level_stat_weight[ul];
-    const TeExcItem *it = D.exc + K.T.level_uptrans_offset[ul];
+    const TeExcItem *it = K.T.exc_items + K.T.level_uptrans_offset[ul];
 #pragma unroll 2
     for (int ii = 0; ii < nuptrans; ii++) {
       const TeExcItem x = it[ii];
@@ -572,28 +562,6 @@ DEVNI double te_eqn(const Ctx &K, const TeDev &D, TeState &s, double T_e, TeRate
   const double total_heating_rate = hc->heating_ff + hc->heating_bf + hc->heating_collisional + hc->heating_dep;
   const double total_coolingrate = hc->cooling_ff + hc->cooling_fb + hc->cooling_collisional + hc->cooling_adiabatic;
   return total_heating_rate - total_coolingrate;
-}
-
-// the packed collisional-excitation items, one workitem per level
-__global__ void k_te_items(Ctx K, TeExcItem *exc) {
-  const int ul = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ul >= K.T.nlevels_total) return;
-  const int ui = K.T.level_ui[ul];
-  const int ul0 = K.T.ion_uniqueleveloffset[ui];
-  const double epsilon_current = K.T.level_epsilon[ul];
-  const int uoff = K.T.level_uptrans_offset[ul];
-  for (int ii = 0; ii < K.T.level_nuptrans[ul]; ii++) {
-    const int li = K.T.uptrans_lineindex[uoff + ii];
-    const int uu = ul0 + K.T.line_upper[li];
-    TeExcItem x;
-    x.epsilon_trans = K.T.level_epsilon[uu] - epsilon_current;
-    x.P2 = K.T.line_ma[li].P2;
-    x.coll_str = K.T.line_coll[li];
-    x.osc_f = K.T.line_f[li];
-    x.upper_sw = K.T.level_stat_weight[uu];
-    x.forbidden = K.T.line_forbidden[li];
-    exc[uoff + ii] = x;
-  }
 }
 
 // thermalbalance.cc:141-187 (NO_LUT_BFHEATING false) for the levels the heating sum visits; workitem = (j, cell)

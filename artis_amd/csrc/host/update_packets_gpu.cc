@@ -32,6 +32,11 @@ void PacketEngine::upload_cellstate(int nts, const artis_cell_state &cells) {
   check(artis_gpu_upload_cellstate(nts, &cells), "artis_gpu_upload_cellstate");
 }
 
+void PacketEngine::solve_temperatures(const artis_te_tables &tables, const artis_te_params &params,
+                                      artis_te_cells &cells) {
+  check(artis_gpu_solve_temperatures(&tables, &params, &cells), "artis_gpu_solve_temperatures");
+}
+
 void PacketEngine::update_packets(int my_rank, int nts, artis_packet *packets, int npkts, artis_estimators &est) {
   check(artis_gpu_update_packets(my_rank, nts, packets, npkts, &est), "artis_gpu_update_packets");
 }

@@ -43,6 +43,11 @@ class PacketEngine {
   // receives the summed estimators (which it would otherwise get from MPI_Allreduce of its host arrays)
   void update_packets_reduced(int my_rank, int nts, artis_packet *packets, int npkts, artis_estimators &est);
 
+  // update_grid's per-cell temperature / ionisation solution for the LTE-population options (the reference's
+  // solve_Te_nltepops / LTE branch + calculate_cooling_rates, update_grid.cc:1104-1158, 1199-1205) for the cells in
+  // `cells.mgi`, after the host normalised the estimators (update_grid.cc:1041-1150); results written into `cells`
+  void solve_temperatures(const artis_te_tables &tables, const artis_te_params &params, artis_te_cells &cells);
+
   double last_transport_ms() const;
 };
 
