@@ -118,3 +118,17 @@ def test_gpu_te_solver_bench_grid_subset():
     te.mgi_list = sub.mgi_list
     compare(m, te, sub)
     print(f"50^3: {len(ffi.TeArrays(m, t_current=15 * DAY).mgi_list)} cells solved in {ms:.1f} ms")
+
+
+def test_gpu_te_solver_kilonova_inputs():
+    """The kilonova run inputs (tests/kilonova_inputfiles: 25 shells, MINTEMP 500 K) with the T_e excitation
+    temperature of artisoptions_kilonova_lte.h:36."""
+    d = os.path.join(REF, "kilonova")
+    m = Model(files=(os.path.join(d, "input-newrun.txt"), os.path.join(d, "model.txt.xz"),
+                     os.path.join(d, "abundances.txt")), nlevels_per_ion=40, n_ionising=15, max_lines=4000)
+    m.set_timestep(6)
+    p = ffi.RunParams.from_buffer_copy(m.params)
+    p.excitation_temperature = 1
+    te = ffi.TeArrays(m, t_current=m.cfg.tmin_days * DAY * 3, seed=8)
+    g, c, _ = run_both(m, te, params=p)
+    compare(m, g, c)
