@@ -1084,7 +1084,7 @@ int artis_gpu_solve_temperatures(const artis_te_tables *tab, const artis_te_para
   Ctx *dK = nullptr;
   TeDev *dD = nullptr;
   if (B.get(&dK, 1, &G.K) || B.get(&dD, 1, &D)) return ARTIS_ERR_HIP;
-  k_te_solve<<<(unsigned)((D.ncells + cpw - 1) / cpw), 64, 0, G.stream>>>(dK, dD, g);
+  k_te_solve<<<(unsigned)((D.ncells + cpw - 1) / cpw), 64, (size_t)cpw * ni * sizeof(double), G.stream>>>(dK, dD, g);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(G.ev1, G.stream));
   HIPCHK(hipEventSynchronize(G.ev1));

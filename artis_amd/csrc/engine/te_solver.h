@@ -46,6 +46,8 @@ struct TeState {
   int k, mgi;
   float Te;
   int g, sub, lane0;  // the cell's lane group: size, this lane's index in it, its first lane in the wave
+  double *phi;        // [nions_total] in LDS: phi of the ions below each element's uppermost ion (one per cell;
+                      // the group's lanes store identical values)
 };
 
 // ltepop.cc:307-327
@@ -270,21 +272,24 @@ DEVFN double te_phi(const Ctx &K, const TeDev &D, const TeState &s, int e, int i
   return phi;
 }
 #define TE_MAX_IONS_PER_ELEMENT 32
-// ltepop.cc:61-95
-DEVFN void te_get_ionfractions(const Ctx &K, const TeDev &D, const TeState &s, int e, double nne, double *ionfractions,
-                               int uppermost_ion) {
-  double nnionfactor[TE_MAX_IONS_PER_ELEMENT];
-  nnionfactor[uppermost_ion] = 1;
-  double denominator = 1.;
+// ltepop.cc:61-95 get_ionfractions without its arrays: the denominator runs down from the uppermost ion as in the
+// reference, and each ion's factor nnionfactor[ion] = nnionfactor[ion + 1] * nne * phi is rebuilt by the same chain
+// of products (identical bits; the chains are a few ions long).  phi of every ion below the uppermost one is the value
+// te_calculate_populations stored for this T_e (the reference recomputes the same pure function).
+DEVFN double te_ionfrac_denominator(const double *phi, int ui0, int uppermost_ion, double nne) {
+  double f = 1., denominator = 1.;
   for (int ion = uppermost_ion - 1; ion >= 0; ion--) {
-    nnionfactor[ion] = nnionfactor[ion + 1] * nne * te_phi(K, D, s, e, ion);
-    denominator += nnionfactor[ion];
+    f = f * nne * phi[ui0 + ion];
+    denominator += f;
   }
-  for (int ion = 0; ion <= uppermost_ion; ion++) {
-    const double numerator = nnionfactor[ion];
-    ionfractions[ion] = numerator / denominator;
-    if (!isfinite(ionfractions[ion])) ionfractions[ion] = 0;
-  }
+  return denominator;
+}
+DEVFN double te_ionfraction(const double *phi, int ui0, int uppermost_ion, double nne, double denominator, int ion) {
+  double numerator = 1.;
+  for (int j = uppermost_ion - 1; j >= ion; j--) numerator = numerator * nne * phi[ui0 + j];
+  double fr = numerator / denominator;
+  if (!isfinite(fr)) fr = 0;
+  return fr;
 }
 DEVFN double te_elem_numberdens(const Ctx &K, const TeDev &D, int mgi, int e) {
   const double mw = D.meanw[(int64_t)mgi * K.T.nelements + e];
@@ -300,9 +305,10 @@ DEVNI double te_nne_solution_f(const Ctx &K, const TeDev &D, const TeState &s, d
       const double elem_mw = D.meanw[(int64_t)s.mgi * K.T.nelements + e];
       double innersum = 0.;
       const int uppermost_ion = D.upp[(int64_t)s.mgi * K.T.nelements + e];
-      double ionfractions[TE_MAX_IONS_PER_ELEMENT];
-      te_get_ionfractions(K, D, s, e, x, ionfractions, uppermost_ion);
-      for (int ion = 0; ion <= uppermost_ion; ion++) innersum += (get_ionstage(K, e, ion) - 1) * ionfractions[ion];
+      const int ui0 = K.T.elem_uniqueionoffset[e];
+      const double den = te_ionfrac_denominator(s.phi, ui0, uppermost_ion, x);
+      for (int ion = 0; ion <= uppermost_ion; ion++)
+        innersum += (get_ionstage(K, e, ion) - 1) * te_ionfraction(s.phi, ui0, uppermost_ion, x, den, ion);
       outersum += abundance / elem_mw * innersum;
     }
   }
@@ -335,7 +341,9 @@ DEVNI int te_calculate_populations(const Ctx &K, const TeDev &D, const TeState &
       double factor = 1.;
       int ion;
       for (ion = 0; ion < uppermost_ion; ion++) {
-        factor *= nne_hi * te_phi(K, D, s, e, ion);
+        const double phi = te_phi(K, D, s, e, ion);
+        s.phi[uion(K, e, ion)] = phi;
+        factor *= nne_hi * phi;
         if (!isfinite(factor)) break;
       }
       uppermost_ion = ion;
@@ -396,13 +404,13 @@ DEVNI int te_calculate_populations(const Ctx &K, const TeDev &D, const TeState &
       const double nnelement = te_elem_numberdens(K, D, mgi, e);
       nne_tot += nnelement * D.anumber[e];
       const int uppermost_ion = D.upp[(int64_t)mgi * nel + e];
-      double ionfractions[TE_MAX_IONS_PER_ELEMENT];
-      if (nnelement > 0) te_get_ionfractions(K, D, s, e, nne, ionfractions, uppermost_ion);
+      const int ui0 = K.T.elem_uniqueionoffset[e];
+      const double den = nnelement > 0 ? te_ionfrac_denominator(s.phi, ui0, uppermost_ion, nne) : 1.;
       for (int ion = 0; ion < nions; ion++) {
         double nnion;
         if (ion <= uppermost_ion) {
           if (nnelement > 0) {
-            nnion = nnelement * ionfractions[ion];
+            nnion = nnelement * te_ionfraction(s.phi, ui0, uppermost_ion, nne, den, ion);
             if (nnion < K.R.minpop) nnion = K.R.minpop;
           } else {
             nnion = 0.;
@@ -601,6 +609,8 @@ __global__ __launch_bounds__(64, 4) void k_te_solve(const Ctx *__restrict__ Kp, 
   s.g = g;
   s.sub = lane & (g - 1);
   s.lane0 = lane & ~(g - 1);
+  extern __shared__ double te_lds[];
+  s.phi = te_lds + (lane / g) * K.T.nions_total;
   s.mgi = D.mgi[k];
   s.Te = D.Te[s.mgi];
   const int mgi = s.mgi;
