@@ -80,3 +80,58 @@ def test_driver_rccl_reduced_path(tmp_path):
     np.testing.assert_allclose(sb, sa, rtol=1e-12, atol=0)
     for nts in range(NTS0, NTS0 + NSTEPS):
         assert (a / f"packets_0000_ts{nts}.tmp").read_bytes() == (b / f"packets_0000_ts{nts}.tmp").read_bytes()
+
+
+def _read_te_case(path, m):
+    """te_case.bin of artis_gpu_driver (ARTIS_DRIVER_TE=1): length-prefixed arrays, inputs then outputs."""
+    raw = open(path, "rb").read()
+    pos = 0
+
+    def arr(dt):
+        nonlocal pos
+        n = int(np.frombuffer(raw, np.int64, 1, pos)[0])
+        pos += 8
+        a = np.frombuffer(raw, dt, n, pos).copy()
+        pos += n * np.dtype(dt).itemsize
+        return a
+
+    te = ffi.TeArrays(m, t_current=1.0)
+    te.TR, te.W, te.TJ, te.Te, te.groundlevelpop = (arr(np.float32) for _ in range(5))
+    te.mgi_list = arr(np.int32)
+    te.thick = arr(np.int16)
+    te.ffheating, te.colheating, te.gamma, te.bfheating, te.vol_init = (arr(np.float64) for _ in range(5))
+    te.elem_meanweight = arr(np.float32)
+    t_current, tmin = np.frombuffer(raw, np.float64, 2, pos)
+    pos += 16
+    te.params.t_current, te.params.tmin = float(t_current), float(tmin)
+    out = {}
+    for k in ("Te", "groundlevelpop", "nne", "nnetot", "partfunct"):
+        out[k] = arr(np.float32)
+    for k in ("totalcooling", "cooling_contrib_ion", "rates"):
+        out[k] = arr(np.float64)
+    out["iters"] = arr(np.int32)
+    return te, out
+
+
+@pytest.mark.gpu
+def test_driver_update_grid_on_gpu_matches_oracle(tmp_path):
+    """The C++ host loop with update_grid's temperature / ionisation solution on the GPU
+    (PacketEngine::solve_temperatures) from the run's own normalised estimators, replayed on the CPU oracle."""
+    env = dict(os.environ, ARTIS_DRIVER_TE="1")
+    r = subprocess.run(_args(tmp_path), capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr
+    from artis_amd.model import Model
+
+    m = Model(**CFG)
+    m.set_timestep(NTS0 + NSTEPS - 1)
+    te, out = _read_te_case(os.path.join(tmp_path, "te_case.bin"), m)
+    assert oracle_lib.solve_temperatures(m, te) == 0
+    g = te.mgi_list
+    assert len(g) > 0
+    same = (te.iters[g] == out["iters"][g]) & (np.abs(te.Te[g] - out["Te"][g]) <= 1e-9 * np.abs(te.Te[g]))
+    assert same.mean() >= 0.99, same.mean()
+    assert np.all(np.abs(te.Te[g] - out["Te"][g]) <= 2e-2 * np.abs(te.Te[g]))
+    ok = g[same]
+    for k in ("nne", "totalcooling"):
+        a, b = getattr(te, k)[ok].astype(np.float64), out[k][ok].astype(np.float64)
+        assert np.all(np.abs(a - b) <= 1e-6 * np.maximum(np.abs(a), np.abs(b)) + 1e-300), k
