@@ -4,7 +4,7 @@
 # (separate rocprofv3 runs) that key roofline.traffic to this engine source hash.
 cd /root/repo
 export TMPDIR=/tmp
-O=gpurun_out/r2e
+O=gpurun_out/${RUN_TAG:-r2e}
 mkdir -p $O/pmc
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u bench.py --no-cpu-baseline > $O/bench_prof.json 2> $O/bench_prof.err &&
