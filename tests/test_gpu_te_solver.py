@@ -132,3 +132,20 @@ def test_gpu_te_solver_kilonova_inputs():
     te = ffi.TeArrays(m, t_current=m.cfg.tmin_days * DAY * 3, seed=8)
     g, c, _ = run_both(m, te, params=p)
     compare(m, g, c)
+
+
+def test_gpu_te_solver_gsl_abort_path(small):
+    """The reference's abort path (an n_e bracket that does not straddle zero) comes back as ARTIS_ERR_PACKET_FAULT
+    naming the model cell, on the device as in the oracle."""
+    from artis_amd import EngineError
+
+    te = ffi.TeArrays(small, t_current=12 * DAY, lte_all=True)
+    bad = int(te.mgi_list[3])
+    te.elem_meanweight.reshape(-1, small.nelements)[bad, :] = 1e-30
+    assert oracle_lib.solve_temperatures(small, te.copy()) == -5
+    eng = Engine(small)
+    try:
+        with pytest.raises(EngineError, match=f"model cell {bad}"):
+            eng.solve_temperatures(te)
+    finally:
+        eng.close()

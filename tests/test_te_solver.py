@@ -111,3 +111,13 @@ def test_solver_is_deterministic_and_leaves_unlisted_cells(te_model):
     other = np.ones(m.npts_model, bool)
     other[te.mgi_list] = False
     assert np.array_equal(te.Te[other], before.Te[other])
+
+
+def test_gsl_abort_path_is_an_error(te_model):
+    """A cell whose n_e bracket [0, rho/m_H] does not straddle zero is a GSL_ERROR in gsl_root_fsolver_set, i.e. the
+    reference aborts (update_grid.cc:1561-1585): the restatement reports ARTIS_ERR_PACKET_FAULT instead of a value."""
+    m = te_model
+    te = ffi.TeArrays(m, t_current=10 * DAY, lte_all=True)
+    bad = te.mgi_list[3]
+    te.elem_meanweight.reshape(-1, m.nelements)[bad, :] = 1e-30  # n_element huge: f(rho/m_H) > 0 as well
+    assert oracle_lib.solve_temperatures(m, te) == -5
