@@ -27,7 +27,7 @@ ABI_SYMBOLS = [
     "artis_gpu_vpkt_init", "artis_gpu_vpkt_zero", "artis_gpu_vpkt_download", "artis_gpu_vpkt_last_stats", "artis_gpu_vpkt_last_work",
     "artis_estimator_block_len", "artis_estimator_block_pack", "artis_estimator_block_unpack",
     "artis_gpu_comm_unique_id", "artis_gpu_comm_init", "artis_gpu_estimators_allreduce", "artis_gpu_comm_finalize",
-    "artis_gpu_solve_temperatures", "artis_gpu_last_te_ms",
+    "artis_gpu_solve_temperatures", "artis_gpu_last_te_ms", "artis_gpu_prepare_temperatures",
 ]
 
 _gpu_lib = None
@@ -88,6 +88,8 @@ def gpu_lib():
         L.artis_gpu_comm_finalize.restype = None
         L.artis_gpu_solve_temperatures.argtypes = [vp, C.POINTER(ffi.TeParams), C.POINTER(ffi.TeCells)]
         L.artis_gpu_last_te_ms.restype = C.c_double
+        L.artis_gpu_prepare_temperatures.argtypes = [vp, C.POINTER(ffi.TeParams), C.POINTER(ffi.UgPrepare),
+                                                     C.POINTER(ffi.TeCells)]
         _gpu_lib = L
     return _gpu_lib
 
@@ -129,6 +131,13 @@ class Engine:
         self._check(self.lib.artis_gpu_solve_temperatures(te.tables, C.byref(te.params), C.byref(s)),
                     "solve_temperatures")
         return float(self.lib.artis_gpu_last_te_ms())
+
+    def prepare_temperatures(self, te, prep):
+        """update_grid_cell's estimator preparation (artis_gpu_prepare_temperatures) for the cells of a TeArrays
+        block from the raw estimators in a UgArrays block; fills prep's outputs."""
+        s = te.struct()
+        self._check(self.lib.artis_gpu_prepare_temperatures(te.tables, C.byref(te.params), C.byref(prep.struct()),
+                                                            C.byref(s)), "prepare_temperatures")
 
     def upload_cellstate(self, nts):
         self._check(self.lib.artis_gpu_upload_cellstate(int(nts), self.model.cellstate), "upload_cellstate")

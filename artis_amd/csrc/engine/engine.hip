@@ -1116,6 +1116,86 @@ int artis_gpu_solve_temperatures(const artis_te_tables *tab, const artis_te_para
 }
 double artis_gpu_last_te_ms(void) { return G.last_te_ms; }
 
+int artis_gpu_prepare_temperatures(const artis_te_tables *tab, const artis_te_params *par, const artis_ug_prepare *pr,
+                                   const artis_te_cells *c) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  const DevRun &R = G.K.R;
+  if (R.nlte_on || R.no_lut_photoion || R.no_lut_bfheating || R.nt_on) {
+    G.last_error = "prepare_temperatures: only the LTE-population options (NLTE_POPS_ON, NO_LUT_*, NT_ON false)";
+    return ARTIS_ERR_UNSUPPORTED;
+  }
+  if (!tab || !par || !pr || !c || !tab->bfheating_coeff || c->ncells < 0 || (c->ncells > 0 && !c->mgi) || !c->TR ||
+      !c->W || !c->TJ || !c->Te || !c->rho || !c->thick || !c->elem_abundance || !c->vol_init || !c->groundlevelpop ||
+      !pr->J || !pr->nuJ || !pr->ffheating || !pr->colheating || !pr->gammaestimator || !pr->bfheatingestimator ||
+      !pr->nne || !pr->partfunct || !pr->TR_out || !pr->W_out || !pr->TJ_out || !pr->ffheating_out ||
+      !pr->colheating_out || !pr->gamma_out || !pr->bfheating_out || !pr->corrphotoionrenorm_out ||
+      !(pr->deltat > 0. && pr->tratmid > 0. && pr->nprocs > 0 && par->T_max > par->T_min && par->T_min > 0.)) {
+    G.last_error = "prepare_temperatures: NULL array or bad parameters";
+    return ARTIS_ERR_BAD_ARGUMENT;
+  }
+  const int np = G.npts_model, ne = G.nelements, ni = G.nions_total, nmx = G.maxnions;
+  for (int k = 0; k < c->ncells; k++)
+    if (c->mgi[k] < 0 || c->mgi[k] >= np) {
+      G.last_error = "prepare_temperatures: cell index out of range";
+      return ARTIS_ERR_BAD_ARGUMENT;
+    }
+  if (c->ncells == 0) return 0;
+  const size_t npf = (size_t)np, npi = (size_t)np * ni, npe = (size_t)np * ne, npg = (size_t)np * ne * nmx;
+  DevBufs B;
+  UgDev U{};
+  int rc = 0;
+  rc |= B.get((int32_t **)&U.mgi, (size_t)c->ncells, c->mgi);
+  rc |= B.get((float **)&U.TR, npf, c->TR);
+  rc |= B.get((float **)&U.W, npf, c->W);
+  rc |= B.get((float **)&U.TJ, npf, c->TJ);
+  rc |= B.get((float **)&U.Te, npf, (const float *)c->Te);
+  rc |= B.get((float **)&U.nne, npf, pr->nne);
+  rc |= B.get((float **)&U.gp, npi, (const float *)c->groundlevelpop);
+  rc |= B.get((float **)&U.pf, npi, pr->partfunct);
+  rc |= B.get((float **)&U.rho, npf, c->rho);
+  rc |= B.get((float **)&U.abund, npe, c->elem_abundance);
+  rc |= B.get((int16_t **)&U.thick, npf, c->thick);
+  rc |= B.get((double **)&U.vol, npf, c->vol_init);
+  rc |= B.get((double **)&U.J, npf, pr->J);
+  rc |= B.get((double **)&U.nuJ, npf, pr->nuJ);
+  rc |= B.get((double **)&U.ff, npf, pr->ffheating);
+  rc |= B.get((double **)&U.col, npf, pr->colheating);
+  rc |= B.get((double **)&U.gam, npg, pr->gammaestimator);
+  rc |= B.get((double **)&U.bfh, npg, pr->bfheatingestimator);
+  rc |= B.get((double **)&U.bfheat_lut, (size_t)G.K.T.tablesize * G.K.T.nbf, tab->bfheating_coeff);
+  rc |= B.get(&U.TR_out, npf, (const float *)pr->TR_out);
+  rc |= B.get(&U.W_out, npf, (const float *)pr->W_out);
+  rc |= B.get(&U.TJ_out, npf, (const float *)pr->TJ_out);
+  rc |= B.get(&U.ff_out, npf, (const double *)pr->ffheating_out);
+  rc |= B.get(&U.col_out, npf, (const double *)pr->colheating_out);
+  rc |= B.get(&U.gam_out, npg, (const double *)pr->gamma_out);
+  rc |= B.get(&U.bfh_out, npg, (const double *)pr->bfheating_out);
+  rc |= B.get(&U.renorm_out, npg, (const double *)pr->corrphotoionrenorm_out);
+  if (rc) return ARTIS_ERR_HIP;
+  U.ncells = c->ncells;
+  U.nprocs = pr->nprocs;
+  U.initial_iteration = par->initial_iteration;
+  U.deltat = pr->deltat;
+  U.tratmid = pr->tratmid;
+  U.T_min = par->T_min;
+  U.T_max = par->T_max;
+  Ctx *dK = nullptr;
+  UgDev *dU = nullptr;
+  if (B.get(&dK, 1, &G.K) || B.get(&dU, 1, &U)) return ARTIS_ERR_HIP;
+  k_ug_prepare<<<(unsigned)((U.ncells + 255) / 256), 256, 0, G.stream>>>(dK, dU);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(G.stream));
+  HIPCHK(hipMemcpy(pr->TR_out, U.TR_out, npf * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(pr->W_out, U.W_out, npf * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(pr->TJ_out, U.TJ_out, npf * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(pr->ffheating_out, U.ff_out, npf * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(pr->colheating_out, U.col_out, npf * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(pr->gamma_out, U.gam_out, npg * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(pr->bfheating_out, U.bfh_out, npg * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(pr->corrphotoionrenorm_out, U.renorm_out, npg * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int artis_gpu_abi_version(void) { return ARTIS_GPU_ABI_VERSION; }
 const char *artis_gpu_last_error(void) { return G.last_error.c_str(); }
 double artis_gpu_last_transport_ms(void) { return G.last_transport_ms; }

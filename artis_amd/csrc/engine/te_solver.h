@@ -688,3 +688,125 @@ __global__ __launch_bounds__(64, 4) void k_te_solve(const Ctx *__restrict__ Kp, 
   }
   if (D.iters) D.iters[mgi] = iters;
 }
+
+// ============================================================ update_grid_cell's estimator preparation
+// (artis_gpu_prepare_temperatures; update_grid.cc:1041-1150, LTE options): one cell per workitem, in the reference's
+// order.  Reads the previous T_R / W / T_J / T_e / n_e / populations, writes the normalised inputs of k_te_solve.
+struct UgDev {
+  const int32_t *mgi;
+  int32_t ncells, nprocs, initial_iteration;
+  double deltat, tratmid, T_min, T_max;
+  const float *TR, *W, *TJ, *Te, *nne, *gp, *pf, *rho, *abund;
+  const int16_t *thick;
+  const double *vol, *J, *nuJ, *ff, *col, *gam, *bfh;
+  const double *bfheat_lut;
+  float *TR_out, *W_out, *TJ_out;
+  double *ff_out, *col_out, *gam_out, *bfh_out, *renorm_out;
+};
+// ltepop.cc:417-430 with the previous populations (NLTE_POPS_ON false)
+DEVFN double ug_levelpop(const Ctx &K, const UgDev &U, int mgi, int e, int ui, int l) {
+  const double raw = U.gp[(int64_t)mgi * K.T.nions_total + ui];
+  const bool hasab = U.abund[(int64_t)mgi * K.T.nelements + e] > 0;
+  const double nnground = raw < K.R.minpop ? (hasab ? K.R.minpop : 0.) : raw;
+  double nn = nnground;
+  if (l > 0) {
+    const double T_exc = K.R.exc_te ? (double)U.Te[mgi] : (double)U.TJ[mgi];
+    const double W = 1.;
+    const int ul0 = K.T.ion_uniqueleveloffset[ui];
+    nn = (nnground * W * (double)K.T.level_stat_weight[ul0 + l] / (double)K.T.level_stat_weight[ul0] *
+          exp(-(K.T.level_epsilon[ul0 + l] - K.T.level_epsilon[ul0]) / ARTIS_KB / T_exc));
+  }
+  if (nn < K.R.minpop) nn = hasab ? K.R.minpop : 0.;
+  return nn;
+}
+__global__ __launch_bounds__(256) void k_ug_prepare(const Ctx *__restrict__ Kp, const UgDev *__restrict__ Up) {
+  const Ctx &K = *Kp;
+  const UgDev &U = *Up;
+  const int kk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (kk >= U.ncells) return;
+  const int mgi = U.mgi[kk];
+  const int nel = K.T.nelements, mx = K.T.maxnions;
+  const int64_t row = (int64_t)mgi * nel * mx;
+  const double deltaV = U.vol[mgi] * pow(U.tratmid, 3.);
+  const double estimator_normfactor = 1 / deltaV / U.deltat / U.nprocs;
+  const double estimator_normfactor_over4pi = ARTIS_ONEOVER4PI * estimator_normfactor;
+  const double J = U.J[mgi] * estimator_normfactor_over4pi;
+  float TR = U.TR[mgi], W = U.W[mgi], TJ = U.TJ[mgi];
+  U.ff_out[mgi] = U.ff[mgi];
+  U.col_out[mgi] = U.col[mgi];
+  for (int q = 0; q < nel * mx; q++) {
+    U.gam_out[row + q] = U.gam[row + q];
+    U.bfh_out[row + q] = U.bfh[row + q];
+  }
+  if (U.initial_iteration || U.thick[mgi] == 1) {
+    double T_J = pow(J * ARTIS_PI / ARTIS_STEBO, 1. / 4.);
+    if (!isfinite(T_J))
+      T_J = U.TR[mgi];
+    else if (T_J > U.T_max)
+      T_J = U.T_max;
+    else if (T_J < U.T_min)
+      T_J = U.T_min;
+    TR = T_J;
+    TJ = T_J;
+    W = 1;
+    for (int q = 0; q < nel * mx; q++) U.renorm_out[row + q] = 1.;
+  } else {
+    const double nuJ = U.nuJ[mgi] * estimator_normfactor_over4pi;
+    U.ff_out[mgi] = U.ff[mgi] * estimator_normfactor;
+    U.col_out[mgi] = U.col[mgi] * estimator_normfactor;
+    const double W_old = U.W[mgi], TR_old = U.TR[mgi];
+    for (int e = 0; e < nel; e++)
+      for (int i = 0; i < K.T.elem_nions[e] - 1; i++) {
+        const int64_t ix = row + e * mx + i;
+        const double g = U.gam[ix] * (estimator_normfactor / ARTIS_H);
+        U.renorm_out[ix] = g / (W_old * lut_interp(K, K.T.corrphotoioncoeff, e, i, 0, 0, TR_old));
+      }
+    const float T_e = U.Te[mgi];
+    const float nne = U.nne[mgi];
+    for (int e = 0; e < nel; e++)
+      for (int i = 0; i < K.T.elem_nions[e] - 1; i++) {
+        const int64_t ix = row + e * mx + i;
+        const int ui = uion(K, e, i);
+        double Gamma = 0., Col_ion = 0.;
+        for (int level = 0; level < K.T.ion_nlevels[ui]; level++) {
+          const double nnlevel = ug_levelpop(K, U, mgi, e, ui, level);
+          for (int t = 0; t < get_nphixstargets(K, e, i, level); t++) {
+            const int upperlevel = get_phixsupperlevel(K, e, i, level, t);
+            double gammacorr = W_old * lut_interp(K, K.T.corrphotoioncoeff, e, i, level, t, TR_old);
+            const int gi = K.T.level_closestgroundlevelcont[ulev(K, e, i, level)];
+            if (gi >= 0) gammacorr *= U.renorm_out[row + gi];
+            Gamma += nnlevel * gammacorr;
+            const double epsilon_trans = epsilon(K, e, i + 1, upperlevel) - epsilon(K, e, i, level);
+            Col_ion += nnlevel * col_ionization_ratecoeff(K, T_e, nne, e, i, level, t, epsilon_trans);
+          }
+        }
+        Gamma += Col_ion;
+        const double gpraw = U.gp[(int64_t)mgi * K.T.nions_total + ui];
+        const double gpop = gpraw < K.R.minpop ? (U.abund[(int64_t)mgi * nel + e] > 0 ? K.R.minpop : 0.) : gpraw;
+        Gamma /= gpop;  // get_groundlevelpop
+        U.gam_out[ix] = Gamma;
+        const double b = U.bfh[ix] * estimator_normfactor;
+        const double ana = W_old * lut_interp(K, U.bfheat_lut, e, i, 0, 0, TR_old);
+        U.bfh_out[ix] = b / ana;
+      }
+    const double nubar = nuJ / J;
+    if (isfinite(nubar) && nubar != 0.) {
+      float T_J = pow(J * ARTIS_PI / ARTIS_STEBO, 1 / 4.);
+      if (T_J > U.T_max)
+        T_J = U.T_max;
+      else if (T_J < U.T_min)
+        T_J = U.T_min;
+      TJ = T_J;
+      float T_R = ARTIS_H * nubar / ARTIS_KB / 3.832229494;
+      if (T_R > U.T_max)
+        T_R = U.T_max;
+      else if (T_R < U.T_min)
+        T_R = U.T_min;
+      TR = T_R;
+      W = J * ARTIS_PI / ARTIS_STEBO / pow((double)T_R, 4.);
+    }
+  }
+  U.TR_out[mgi] = TR;
+  U.W_out[mgi] = W;
+  U.TJ_out[mgi] = TJ;
+}

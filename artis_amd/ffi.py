@@ -547,3 +547,53 @@ class TeArrays:
             if isinstance(v, np.ndarray):
                 setattr(o, k, v.copy())
         return o
+
+
+class UgPrepare(C.Structure):
+    """artis_ug_prepare (ABI 7): update_grid_cell's estimator preparation."""
+    _fields_ = [("deltat", C.c_double), ("tratmid", C.c_double), ("nprocs", C.c_int32), ("pad0", C.c_int32)] + [
+        (n, C.c_void_p) for n in ("J", "nuJ", "ffheating", "colheating", "gammaestimator", "bfheatingestimator", "nne",
+                                  "partfunct", "TR_out", "W_out", "TJ_out", "ffheating_out", "colheating_out",
+                                  "gamma_out", "bfheating_out", "corrphotoionrenorm_out")]
+
+
+class UgArrays:
+    """Raw transport estimators for artis_ug_prepare (seeded, of the magnitude a 1e4-packet step accumulates per cell
+    of a small model) plus the previous n_e / partition functions of the model's cell state, and the outputs."""
+
+    def __init__(self, model, deltat, tratmid, seed=6):
+        m = model
+        cs = CellState.from_address(m.cellstate)
+        np_, nel, ni, mx = m.npts_model, m.nelements, m.nions_total, m.maxnions
+        f32 = lambda p, n: np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), (n,)).copy()  # noqa: E731
+        rng = np.random.default_rng(seed)
+        self.deltat, self.tratmid, self.nprocs = float(deltat), float(tratmid), 1
+        self.nne = f32(cs.nne, np_)
+        self.partfunct = f32(cs.partfunct, np_ * ni)
+        # J ~ 4 pi sigma T^4 / pi * volume * deltat, with nubar giving T_R ~ 5000-15000 K
+        T = rng.uniform(5e3, 1.5e4, np_)
+        self.J = 4 * np.pi * 5.6704e-5 * T ** 4 / np.pi * 1e45 * deltat * rng.uniform(0.5, 1.5, np_)
+        self.nuJ = self.J * (1.38064852e-16 * 3.832229494 * T * rng.uniform(0.8, 1.2, np_) / 6.6260755e-27)
+        self.ffheating = self.J * 1e-18
+        self.colheating = self.J * 1e-17
+        self.gamma = self.J.repeat(nel * mx) * 10 ** rng.uniform(-22, -20, np_ * nel * mx)
+        self.bfheating = self.J.repeat(nel * mx) * 10 ** rng.uniform(-20, -18, np_ * nel * mx)
+        self.TR_out = np.zeros(np_, np.float32)
+        self.W_out = np.zeros(np_, np.float32)
+        self.TJ_out = np.zeros(np_, np.float32)
+        self.ff_out = np.zeros(np_)
+        self.col_out = np.zeros(np_)
+        self.gamma_out = np.zeros(np_ * nel * mx)
+        self.bfheating_out = np.zeros(np_ * nel * mx)
+        self.renorm_out = np.zeros(np_ * nel * mx)
+
+    def struct(self):
+        s = UgPrepare(deltat=self.deltat, tratmid=self.tratmid, nprocs=self.nprocs)
+        for n, a in (("J", self.J), ("nuJ", self.nuJ), ("ffheating", self.ffheating), ("colheating", self.colheating),
+                     ("gammaestimator", self.gamma), ("bfheatingestimator", self.bfheating), ("nne", self.nne),
+                     ("partfunct", self.partfunct), ("TR_out", self.TR_out), ("W_out", self.W_out),
+                     ("TJ_out", self.TJ_out), ("ffheating_out", self.ff_out), ("colheating_out", self.col_out),
+                     ("gamma_out", self.gamma_out), ("bfheating_out", self.bfheating_out),
+                     ("corrphotoionrenorm_out", self.renorm_out)):
+            setattr(s, n, a.ctypes.data)
+        return s

@@ -34,6 +34,7 @@
 #define ARTIS_HOVERKB 4.799243681748932e-11
 #define ARTIS_FOURPI 1.256637061600000e+01
 #define ARTIS_ONEOVER4PI 7.957747153555701e-02
+#define ARTIS_STEBO 5.670400e-5  /* constants.h:22 */
 #define ARTIS_HCLIGHTOVERFOURPI 1.580764662876770e-17
 #define ARTIS_OSCSTRENGTHCONVERSION 1.3473837e+21
 #define ARTIS_H_IONPOT (13.5979996 * ARTIS_EV)

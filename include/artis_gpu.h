@@ -592,6 +592,33 @@ typedef struct artis_te_cells {
                                           T_max], 0: LTE branch); may be NULL */
 } artis_te_cells;
 int artis_gpu_solve_temperatures(const artis_te_tables *tables, const artis_te_params *params, artis_te_cells *cells);
+/* The estimator preparation update_grid_cell does before that solution (update_grid.cc:1041-1150, LTE options,
+   DO_TITER undefined), for the same cells: estimator_normfactor = 1 / (vol_init tratmid^3) / deltat / nprocs;
+   LTE-branch cells: T_J = get_T_J_from_J (radfield.cc:1464-1481), T_R = T_J, W = 1, corrphotoionrenorm = 1;
+   other cells: J, nuJ and the ff / collisional heating normalised, update_gamma_corrphotoionrenorm_bfheating_
+   estimators (update_grid.cc:888-975: corrphotoionrenorm = Gamma / get_corrphotoioncoeff_ana, then Gamma per
+   ground-level population = calculate_iongamma_per_gspop (ratecoeff.cc:1353-1389) with the previous T_R, W, T_e,
+   n_e and populations, the bf-heating estimator over get_bfheatingcoeff_ana), then set_params_fullspec
+   (radfield.cc:1136-1175) for T_J, T_R, W.  Writes the *_out arrays, which then feed artis_gpu_solve_temperatures
+   (cells->TR / W / TJ and the four estimator inputs). */
+typedef struct artis_ug_prepare {
+  double deltat;             /* globals::time_step[nts_prev].width (update_grid.cc:1316) */
+  double tratmid;            /* globals::time_step[nts].mid / globals::tmin */
+  int32_t nprocs;
+  int32_t pad0;
+  /* raw accumulators of the transport step (summed over ranks) */
+  const double *J, *nuJ, *ffheating, *colheating;   /* [npts_model] */
+  const double *gammaestimator, *bfheatingestimator; /* [npts_model * nelements * maxnions] */
+  const float *nne;          /* previous update_grid state read by calculate_iongamma_per_gspop */
+  const float *partfunct;    /* [npts_model * nions_total] */
+  /* outputs */
+  float *TR_out, *W_out, *TJ_out;
+  double *ffheating_out, *colheating_out, *gamma_out, *bfheating_out;
+  double *corrphotoionrenorm_out;  /* [npts_model * nelements * maxnions] */
+} artis_ug_prepare;
+int artis_gpu_prepare_temperatures(const artis_te_tables *tables, const artis_te_params *params,
+                                   const artis_ug_prepare *prep, const artis_te_cells *cells);
+
 /* device time (ms) of the last artis_gpu_solve_temperatures (the k_te_solve kernel alone) */
 double artis_gpu_last_te_ms(void);
 

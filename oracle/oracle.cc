@@ -4316,3 +4316,142 @@ int oracle_solve_temperatures(const artis_atomic_tables *at, const artis_run_par
   return rc;
 }
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------------------------
+// update_grid_cell's estimator preparation before the temperature solution (update_grid.cc:1041-1150, LTE options,
+// DO_TITER undefined): the checker of artis_gpu_prepare_temperatures.
+namespace {
+// ratecoeff.cc:686-710-style interpolation of a [tablesize * nbfcontinua] LUT (interpolate_corrphotoioncoeff)
+double lut_at(const Ctx &c, const double *lut, int e, int i, int l, int t, double T) {
+  const int tablesize = c.at->tablesize;
+  const int lowerindex = floor(log(T / c.at->mintemp) / c.T_step_log);
+  if (lowerindex < tablesize - 1) {
+    const int upperindex = lowerindex + 1;
+    const double T_lower = c.at->mintemp * exp(lowerindex * c.T_step_log);
+    const double T_upper = c.at->mintemp * exp(upperindex * c.T_step_log);
+    const double f_upper = lut[get_bflutindex(c, upperindex, e, i, l, t)];
+    const double f_lower = lut[get_bflutindex(c, lowerindex, e, i, l, t)];
+    return (f_lower + (f_upper - f_lower) / (T_upper - T_lower) * (T - T_lower));
+  }
+  return lut[get_bflutindex(c, tablesize - 1, e, i, l, t)];
+}
+}  // namespace
+
+extern "C" {
+int oracle_prepare_temperatures(const artis_atomic_tables *at, const artis_run_params *rp, const artis_te_tables *tab,
+                                const artis_te_params *par, const artis_ug_prepare *pr, const artis_te_cells *in,
+                                int npts_model, int nthreads) {
+  if (rp->nlte_pops_on || rp->no_lut_photoion || rp->no_lut_bfheating || rp->nt_on) return ARTIS_ERR_UNSUPPORTED;
+  const int nel = at->nelements, mx = at->maxnions;
+  artis_cell_state cs;
+  memset(&cs, 0, sizeof(cs));
+  cs.Te = in->Te;
+  cs.TJ = in->TJ;
+  cs.TR = in->TR;
+  cs.W = in->W;
+  cs.nne = pr->nne;
+  cs.rho = in->rho;
+  cs.elem_abundance = in->elem_abundance;
+  cs.groundlevelpop = in->groundlevelpop;
+  cs.partfunct = pr->partfunct;
+  Ctx c;
+  c.at = at;
+  c.g = nullptr;
+  c.cs = &cs;
+  c.rp = *rp;
+  c.gs = nullptr;
+  c.T_step_log = (log(at->maxtemp) - log(at->mintemp)) / (at->tablesize - 1.);
+  c.minpop = rp->minpop > 0. ? rp->minpop : 1e-30;
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic)
+  for (int kk = 0; kk < in->ncells; kk++) {
+    const int mgi = in->mgi[kk];
+    const size_t row = (size_t)mgi * nel * mx;
+    const double deltaV = in->vol_init[mgi] * pow(pr->tratmid, 3);
+    const double estimator_normfactor = 1 / deltaV / pr->deltat / pr->nprocs;
+    const double estimator_normfactor_over4pi = ARTIS_ONEOVER4PI * estimator_normfactor;
+    const double J = pr->J[mgi] * estimator_normfactor_over4pi;  // radfield::normalise_J
+    float TR = in->TR[mgi], W = in->W[mgi], TJ = in->TJ[mgi];
+    pr->ffheating_out[mgi] = pr->ffheating[mgi];
+    pr->colheating_out[mgi] = pr->colheating[mgi];
+    for (int q = 0; q < nel * mx; q++) {
+      pr->gamma_out[row + q] = pr->gammaestimator[row + q];
+      pr->bfheating_out[row + q] = pr->bfheatingestimator[row + q];
+    }
+    if (par->initial_iteration || in->thick[mgi] == 1) {
+      // update_grid.cc:1111-1120, radfield.cc:1464-1481 get_T_J_from_J
+      double T_J = pow(J * ARTIS_PI / ARTIS_STEBO, 1. / 4.);
+      if (!std::isfinite(T_J))
+        T_J = in->TR[mgi];
+      else if (T_J > par->T_max)
+        T_J = par->T_max;
+      else if (T_J < par->T_min)
+        T_J = par->T_min;
+      TR = T_J;
+      TJ = T_J;
+      W = 1;
+      for (int q = 0; q < nel * mx; q++) pr->corrphotoionrenorm_out[row + q] = 1.;  // set_all_corrphotoionrenorm
+    } else {
+      const double nuJ = pr->nuJ[mgi] * estimator_normfactor_over4pi;  // radfield::normalise_nuJ
+      pr->ffheating_out[mgi] = pr->ffheating[mgi] * estimator_normfactor;
+      pr->colheating_out[mgi] = pr->colheating[mgi] * estimator_normfactor;
+      // update_grid.cc:888-975 with the previous T_R, W (fit_parameters comes after)
+      const double W_old = in->W[mgi], TR_old = in->TR[mgi];
+      for (int e = 0; e < nel; e++)
+        for (int i = 0; i < get_nions(c, e) - 1; i++) {
+          const size_t ix = row + e * mx + i;
+          const double g = pr->gammaestimator[ix] * (estimator_normfactor / ARTIS_H);
+          pr->corrphotoionrenorm_out[ix] = g / (W_old * lut_at(c, at->corrphotoioncoeff, e, i, 0, 0, TR_old));
+        }
+      for (int e = 0; e < nel; e++)
+        for (int i = 0; i < get_nions(c, e) - 1; i++) {
+          const size_t ix = row + e * mx + i;
+          // ratecoeff.cc:1353-1389 calculate_iongamma_per_gspop
+          const float T_e = c.cs->Te[mgi];
+          const float nne = c.cs->nne[mgi];
+          double Gamma = 0., Col_ion = 0.;
+          for (int level = 0; level < get_nlevels(c, e, i); level++) {
+            const double nnlevel = calculate_levelpop(c, mgi, e, i, level);
+            for (int t = 0; t < get_nphixstargets(c, e, i, level); t++) {
+              const int upperlevel = get_phixsupperlevel(c, e, i, level, t);
+              // get_corrphotoioncoeff (ratecoeff.cc:1255-1290, LUT branch)
+              double gammacorr = W_old * lut_at(c, at->corrphotoioncoeff, e, i, level, t, TR_old);
+              const int gi = at->level_closestgroundlevelcont[ulev(c, e, i, level)];
+              if (gi >= 0) gammacorr *= pr->corrphotoionrenorm_out[row + gi];
+              Gamma += nnlevel * gammacorr;
+              const double epsilon_trans = epsilon(c, e, i + 1, upperlevel) - epsilon(c, e, i, level);
+              Col_ion += nnlevel * col_ionization_ratecoeff(c, T_e, nne, e, i, level, t, epsilon_trans);
+            }
+          }
+          Gamma += Col_ion;
+          Gamma /= get_groundlevelpop(c, mgi, e, i);
+          pr->gamma_out[ix] = Gamma;
+          const double b = pr->bfheatingestimator[ix] * estimator_normfactor;
+          const double ana = W_old * lut_at(c, tab->bfheating_coeff, e, i, 0, 0, TR_old);  // get_bfheatingcoeff_ana
+          pr->bfheating_out[ix] = b / ana;
+        }
+      // radfield.cc:1136-1175 set_params_fullspec
+      const double nubar = nuJ / J;
+      if (std::isfinite(nubar) && nubar != 0.) {
+        float T_J = pow(J * ARTIS_PI / ARTIS_STEBO, 1 / 4.);
+        if (T_J > par->T_max)
+          T_J = par->T_max;
+        else if (T_J < par->T_min)
+          T_J = par->T_min;
+        TJ = T_J;
+        float T_R = ARTIS_H * nubar / ARTIS_KB / 3.832229494;
+        if (T_R > par->T_max)
+          T_R = par->T_max;
+        else if (T_R < par->T_min)
+          T_R = par->T_min;
+        TR = T_R;
+        W = J * ARTIS_PI / ARTIS_STEBO / pow(T_R, 4);
+      }
+    }
+    pr->TR_out[mgi] = TR;
+    pr->W_out[mgi] = W;
+    pr->TJ_out[mgi] = TJ;
+  }
+  return 0;
+}
+}  // extern "C"

@@ -128,3 +128,16 @@ def solve_temperatures(model, te, params=None, nthreads=0):
     rc = L.oracle_solve_temperatures(model.atomic, C.byref(params if params is not None else model.params), te.tables,
                                      C.byref(te.params), C.byref(s), model.npts_model, nthreads)
     return rc
+
+
+def prepare_temperatures(model, te, prep, params=None, nthreads=0):
+    """oracle_prepare_temperatures on a TeArrays + UgArrays pair (fills prep's outputs); returns the status."""
+    L = lib()
+    L.oracle_prepare_temperatures.argtypes = [C.c_void_p, C.POINTER(ffi.RunParams), C.c_void_p,
+                                              C.POINTER(ffi.TeParams), C.POINTER(ffi.UgPrepare),
+                                              C.POINTER(ffi.TeCells), C.c_int, C.c_int]
+    s = te.struct()
+    p = prep.struct()
+    return L.oracle_prepare_temperatures(model.atomic, C.byref(params if params is not None else model.params),
+                                         te.tables, C.byref(te.params), C.byref(p), C.byref(s), model.npts_model,
+                                         nthreads)

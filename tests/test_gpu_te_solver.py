@@ -149,3 +149,38 @@ def test_gpu_te_solver_gsl_abort_path(small):
             eng.solve_temperatures(te)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("thick_frac", [0.0, 0.3])
+def test_gpu_prepare_temperatures_matches_oracle(small, thick_frac):
+    """update_grid_cell's estimator preparation (artis_gpu_prepare_temperatures, update_grid.cc:1041-1150) against
+    the oracle, then the temperature solution on the prepared block: float outputs within one float ulp, doubles
+    within TE_RTOL (device exp/log/pow last-ulp differences)."""
+    te = ffi.TeArrays(small, t_current=12 * DAY, thick_frac=thick_frac, seed=11)
+    pg = ffi.UgArrays(small, deltat=0.5 * DAY, tratmid=3.0, seed=3)
+    pc = ffi.UgArrays(small, deltat=0.5 * DAY, tratmid=3.0, seed=3)
+    assert oracle_lib.prepare_temperatures(small, te, pc) == 0
+    eng = Engine(small)
+    try:
+        eng.prepare_temperatures(te, pg)
+        idx = te.mgi_list
+        for k in ("TR_out", "W_out", "TJ_out"):
+            a, b = getattr(pg, k)[idx], getattr(pc, k)[idx]
+            assert np.all(rel(a, b) <= 2.5e-7), (k, rel(a, b).max())
+        nm = small.nelements * small.maxnions
+        for k, w in (("ff_out", 1), ("col_out", 1), ("gamma_out", nm), ("bfheating_out", nm), ("renorm_out", nm)):
+            a, b = getattr(pg, k).reshape(-1, w)[idx], getattr(pc, k).reshape(-1, w)[idx]
+            fin = np.isfinite(b)
+            assert np.array_equal(np.isfinite(a), fin), k
+            assert np.all(rel(a[fin], b[fin]) <= TE_RTOL), (k, rel(a[fin], b[fin]).max())
+        # chained: the solution from the device-prepared inputs against the oracle's
+        for t, p in ((te, pg),):
+            t.TR, t.W, t.TJ = p.TR_out.copy(), p.W_out.copy(), p.TJ_out.copy()
+            t.ffheating, t.colheating = p.ff_out.copy(), p.col_out.copy()
+            t.gamma, t.bfheating = p.gamma_out.copy(), p.bfheating_out.copy()
+        cpu = te.copy()
+        assert oracle_lib.solve_temperatures(small, cpu) == 0
+        eng.solve_temperatures(te)
+    finally:
+        eng.close()
+    compare(small, te, cpu)

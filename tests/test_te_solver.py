@@ -121,3 +121,35 @@ def test_gsl_abort_path_is_an_error(te_model):
     bad = te.mgi_list[3]
     te.elem_meanweight.reshape(-1, m.nelements)[bad, :] = 1e-30  # n_element huge: f(rho/m_H) > 0 as well
     assert oracle_lib.solve_temperatures(m, te) == -5
+
+
+def _prepared(m, seed=6, **kw):
+    g = ffi.AtomicHeader.from_address(m.atomic)
+    te = ffi.TeArrays(m, t_current=10 * DAY, **kw)
+    prep = ffi.UgArrays(m, deltat=0.5 * DAY, tratmid=3.0, seed=seed)
+    assert oracle_lib.prepare_temperatures(m, te, prep) == 0
+    return te, prep, g
+
+
+def test_prepare_lte_and_fit_branches(te_model):
+    """update_grid.cc:1106-1150: grey / initial cells get T_R = T_J = get_T_J_from_J, W = 1, corrphotoionrenorm 1;
+    the others the fitted T_J, T_R (clamped to [MINTEMP, MAXTEMP]), W = pi J / sigma / T_R^4 and normalised
+    estimators."""
+    m = te_model
+    te, prep, hdr = _prepared(m, thick_frac=0.3)
+    idx = te.mgi_list
+    lte = te.thick[idx] == 1
+    assert lte.any() and (~lte).any()
+    a, b = idx[lte], idx[~lte]
+    assert np.array_equal(prep.TR_out[a], prep.TJ_out[a]) and np.all(prep.W_out[a] == 1.0)
+    nm = m.nelements * m.maxnions
+    assert np.all(prep.renorm_out.reshape(-1, nm)[a] == 1.0)
+    assert np.all((prep.TR_out[b] >= hdr.mintemp) & (prep.TR_out[b] <= hdr.maxtemp))
+    assert np.all(prep.W_out[b] > 0)
+    assert np.all(prep.ff_out[b] > 0) and np.all(prep.col_out[b] > 0)
+    # the prepared block feeds the temperature solution
+    te.TR, te.W, te.TJ = prep.TR_out.copy(), prep.W_out.copy(), prep.TJ_out.copy()
+    te.ffheating, te.colheating = prep.ff_out.copy(), prep.col_out.copy()
+    te.gamma, te.bfheating = prep.gamma_out.copy(), prep.bfheating_out.copy()
+    assert oracle_lib.solve_temperatures(m, te) == 0
+    assert np.all(np.isfinite(te.Te[idx]))
