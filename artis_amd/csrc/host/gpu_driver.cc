@@ -10,10 +10,9 @@
 // final <outdir>/packets00_0000.out (packet.cc:152-196), and prints one summary line per timestep.
 // ARTIS_DRIVER_RCCL=1: the estimators go through the RCCL all-reduce of update_packets_reduced (a
 // communicator of this one rank -- the multi-rank host hands rank 0's id to every rank).
-// ARTIS_DRIVER_TE=1: after the last timestep, update_grid's temperature / ionisation solution on the GPU
-// (PacketEngine::solve_temperatures) from that timestep's own estimators, normalised as update_grid.cc:1041-1150
-// does (see te_from_estimators); inputs and outputs go to <outdir>/te_case.bin for the oracle replay in
-// tests/test_host_driver.py.
+// ARTIS_DRIVER_TE=1: after the last timestep, update_grid's estimator preparation and temperature / ionisation
+// solution on the GPU (PacketEngine::prepare_temperatures + solve_temperatures) from that timestep's own raw
+// estimators; inputs and outputs go to <outdir>/te_case.bin for the oracle replay in tests/test_host_driver.py.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -28,33 +27,26 @@
 
 
 namespace {
-// One artis_te_cells block built from a timestep's raw estimators, as update_grid_cell prepares them
-// (update_grid.cc:1041-1150): estimator_normfactor = 1 / deltaV / deltat / nprocs; J, nuJ normalised with an extra
-// 1/4pi (radfield::normalise_J / normalise_nuJ); T_J = (pi J / sigma)^(1/4), T_R = h nubar / k / 3.832229494 and
-// W = pi J / sigma / T_R^4, each clamped to [MINTEMP, MAXTEMP] (radfield.cc:1136-1175, set_params_fullspec);
-// ff / collisional heating times the factor (update_grid.cc:1133-1134); the bf-heating estimator times the factor
-// over the ground level's analytic coefficient (update_grid.cc:950-960).  Stand-ins where the reference needs data
-// this synthetic model does not carry: Gamma per ground-level population = gammaestimator * factor / h (the
-// reference's calculate_iongamma_per_gspop sums the corrected photoionisation coefficients), mean atomic weight
-// 2.1 Z m_H, and vol_init from the uniform grid's cell count per model cell.
+// update_grid for the timestep after the run's last one, on the GPU: the cells' previous state (the model's cell
+// state), the run's raw estimators, artis_gpu_prepare_temperatures (update_grid.cc:1041-1150) and then
+// artis_gpu_solve_temperatures.  Stand-ins where the reference needs data this synthetic model does not carry:
+// mean atomic weight 2.1 Z m_H, vol_init from the uniform grid's cell count per model cell.
 struct TeCase {
   std::vector<int32_t> mgi;
-  std::vector<float> TR, W, TJ, rho, abund, meanw, Te, gp, nne, nnetot, pf;
+  std::vector<float> TR, W, TJ, rho, abund, meanw, Te, gp, nne, nnetot, pf, nne_old, pf_old, TR_new, W_new, TJ_new;
   std::vector<int16_t> thick;
-  std::vector<double> vol, ff, col, gam, bfh, totcool, ccion, rates;
+  std::vector<double> vol, ff, col, gam, bfh, totcool, ccion, rates, renorm;
   std::vector<int32_t> iters;
   artis_te_cells cells{};
   artis_te_params par{};
+  artis_ug_prepare prep{};
 };
-void te_from_estimators(const artis_atomic_tables &at, const artis_geometry &g, const artis_cell_state &cs,
-                        const artis_te_tables &tab, int nts, int np, const std::vector<double> &J,
-                        const std::vector<double> &nuJ, const std::vector<double> &ff,
-                        const std::vector<double> &col, const std::vector<double> &gam,
-                        const std::vector<double> &bfh, TeCase &c) {
+void te_setup(const artis_atomic_tables &at, const artis_geometry &g, const artis_cell_state &cs, int nts_next, int nts,
+              int np, const std::vector<double> &J, const std::vector<double> &nuJ, const std::vector<double> &ff,
+              const std::vector<double> &col, const std::vector<double> &gam, const std::vector<double> &bfh,
+              TeCase &c) {
   const int nel = at.nelements, ni = at.nions_total, mx = at.maxnions;
-  const double PI = 3.14159265358979323846, STEBO = 5.670400e-5, H = 6.6260755e-27, KB = 1.38064852e-16,
-               MH = 1.67352e-24;
-  const double T_step_log = (std::log(at.maxtemp) - std::log(at.mintemp)) / (at.tablesize - 1.);
+  const double MH = 1.67352e-24;
   std::vector<int> count(np + 1, 0);
   for (int i = 0; i < g.ngrid; i++) count[g.cell_mgi[i]]++;
   const double wid = 2 * g.coordmax[0] / g.ncoordgrid[0];
@@ -66,57 +58,23 @@ void te_from_estimators(const artis_atomic_tables &at, const artis_geometry &g, 
   c.abund.assign(cs.elem_abundance, cs.elem_abundance + (size_t)np * nel);
   c.Te.assign(cs.Te, cs.Te + np);
   c.gp.assign(cs.groundlevelpop, cs.groundlevelpop + (size_t)np * ni);
+  c.nne_old.assign(cs.nne, cs.nne + np);
+  c.pf_old.assign(cs.partfunct, cs.partfunct + (size_t)np * ni);
   c.meanw.resize((size_t)np * nel);
   c.vol.resize(np);
-  c.ff.assign(np, 0.);
-  c.col.assign(np, 0.);
-  c.gam.assign((size_t)np * nel * mx, 0.);
-  c.bfh.assign((size_t)np * nel * mx, 1.);
-  const double tmid = g.ts_mid[nts], deltat = g.ts_width[nts];
   for (int mgi = 0; mgi < np; mgi++) {
     for (int e = 0; e < nel; e++) c.meanw[(size_t)mgi * nel + e] = (float)(2.1 * at.elem_anumber[e] * MH);
     c.vol[mgi] = wid * wid * wid * count[mgi];
-    if (!(c.rho[mgi] > 0) || count[mgi] == 0) continue;
-    c.mgi.push_back(mgi);
-    const double deltaV = c.vol[mgi] * std::pow(tmid / g.tmin, 3);
-    const double normfactor = 1. / deltaV / deltat / 1;
-    const double Jn = J[mgi] * normfactor / (4 * PI), nuJn = nuJ[mgi] * normfactor / (4 * PI);
-    const double nubar = nuJn / Jn;
-    if (std::isfinite(nubar) && nubar != 0.) {
-      float T_J = std::pow(Jn * PI / STEBO, 1 / 4.);
-      T_J = std::min<float>(std::max<float>(T_J, at.mintemp), at.maxtemp);
-      float T_R = H * nubar / KB / 3.832229494;
-      T_R = std::min<float>(std::max<float>(T_R, at.mintemp), at.maxtemp);
-      c.TJ[mgi] = T_J;
-      c.TR[mgi] = T_R;
-      c.W[mgi] = Jn * PI / STEBO / std::pow(T_R, 4);
-    }
-    c.ff[mgi] = ff[mgi] * normfactor;
-    c.col[mgi] = col[mgi] * normfactor;
-    for (int e = 0; e < nel; e++)
-      for (int i = 0; i < at.elem_nions[e] - 1; i++) {
-        const size_t ix = (size_t)mgi * nel * mx + e * mx + i;
-        c.gam[ix] = gam[ix] * normfactor / H;
-        // thermalbalance.cc:34-57 get_bfheatingcoeff_ana for (ion, level 0, target 0) at this cell's T_R, W
-        const int ul = at.ion_uniqueleveloffset[at.elem_uniqueionoffset[e] + i];
-        if (at.level_nphixstargets[ul] <= 0) continue;
-        const int contindex = -1 - at.level_cont_index[ul];
-        const double T = c.TR[mgi];
-        const int lo = (int)std::floor(std::log(T / at.mintemp) / T_step_log);
-        double coeff;
-        if (lo < at.tablesize - 1) {
-          const double Tl = at.mintemp * std::exp(lo * T_step_log), Tu = at.mintemp * std::exp((lo + 1) * T_step_log);
-          const double fl = tab.bfheating_coeff[(size_t)lo * at.nbfcontinua + contindex];
-          const double fu = tab.bfheating_coeff[(size_t)(lo + 1) * at.nbfcontinua + contindex];
-          coeff = fl + (fu - fl) / (Tu - Tl) * (T - Tl);
-        } else {
-          coeff = tab.bfheating_coeff[(size_t)(at.tablesize - 1) * at.nbfcontinua + contindex];
-        }
-        coeff *= c.W[mgi];
-        const double v = bfh[ix] * normfactor / coeff;
-        c.bfh[ix] = (std::isfinite(v) && v > 0.) ? v : 1.;
-      }
+    if (c.rho[mgi] > 0 && count[mgi] > 0) c.mgi.push_back(mgi);
   }
+  c.TR_new.assign(np, 0.f);
+  c.W_new.assign(np, 0.f);
+  c.TJ_new.assign(np, 0.f);
+  c.ff.assign(np, 0.);
+  c.col.assign(np, 0.);
+  c.gam.assign((size_t)np * nel * mx, 0.);
+  c.bfh.assign((size_t)np * nel * mx, 0.);
+  c.renorm.assign((size_t)np * nel * mx, 0.);
   c.nne.assign(np, 0.f);
   c.nnetot.assign(np, 0.f);
   c.pf.assign((size_t)np * ni, 0.f);
@@ -124,6 +82,26 @@ void te_from_estimators(const artis_atomic_tables &at, const artis_geometry &g, 
   c.ccion.assign((size_t)np * ni, 0.);
   c.rates.assign((size_t)np * ARTIS_TE_NRATES, 0.);
   c.iters.assign(np, 0);
+  artis_ug_prepare &p = c.prep;
+  p.deltat = g.ts_width[nts];                // time_step[nts_prev].width (update_grid.cc:1316)
+  p.tratmid = g.ts_mid[nts_next] / g.tmin;   // time_step[nts].mid / tmin of the timestep being prepared
+  p.nprocs = 1;
+  p.J = J.data();
+  p.nuJ = nuJ.data();
+  p.ffheating = ff.data();
+  p.colheating = col.data();
+  p.gammaestimator = gam.data();
+  p.bfheatingestimator = bfh.data();
+  p.nne = c.nne_old.data();
+  p.partfunct = c.pf_old.data();
+  p.TR_out = c.TR_new.data();
+  p.W_out = c.W_new.data();
+  p.TJ_out = c.TJ_new.data();
+  p.ffheating_out = c.ff.data();
+  p.colheating_out = c.col.data();
+  p.gamma_out = c.gam.data();
+  p.bfheating_out = c.bfh.data();
+  p.corrphotoionrenorm_out = c.renorm.data();
   artis_te_cells &x = c.cells;
   x.ncells = (int32_t)c.mgi.size();
   x.mgi = c.mgi.data();
@@ -149,7 +127,7 @@ void te_from_estimators(const artis_atomic_tables &at, const artis_geometry &g, 
   x.cooling_contrib_ion = c.ccion.data();
   x.heatingcoolingrates = c.rates.data();
   x.te_iterations = c.iters.data();
-  c.par.t_current = tmid;
+  c.par.t_current = g.ts_mid[nts];  // nts_for_te = nts - 1 at titer 0 (update_grid.cc:804)
   c.par.tmin = g.tmin;
   c.par.T_min = at.mintemp;
   c.par.T_max = at.maxtemp;
@@ -260,20 +238,28 @@ int main(int argc, char **argv) {
     }
     const char *tev = std::getenv("ARTIS_DRIVER_TE");
     if (tev && tev[0] == '1' && last_nts >= 0) {
-      // update_grid for the next timestep: the temperature / ionisation solution from this timestep's estimators
+      // update_grid for the next timestep on the GPU: estimator preparation, then the temperature solution
       TeCase c;
-      te_from_estimators(at, *artis_model_geometry(m), *artis_model_cellstate(m), *artis_model_te_tables(m), last_nts,
-                         (int)np, J, nuJ, ff, col, gam, bfh, c);
+      const int nts_next = std::min(last_nts + 1, cfg.ntstep - 1);
+      te_setup(at, *artis_model_geometry(m), *artis_model_cellstate(m), nts_next, last_nts, (int)np, J, nuJ, ff, col,
+               gam, bfh, c);
       std::ofstream o(outdir + "/te_case.bin", std::ios::binary);
-      // inputs (as handed to the engine), then the outputs
-      for (const auto *v : {&c.TR, &c.W, &c.TJ, &c.Te, &c.gp}) put(o, *v);
+      // inputs: the previous state, the raw estimators, the parameters; then the outputs
+      for (const auto *v : {&c.TR, &c.W, &c.TJ, &c.Te, &c.gp, &c.nne_old, &c.pf_old}) put(o, *v);
       put(o, c.mgi);
       put(o, c.thick);
-      for (const auto *v : {&c.ff, &c.col, &c.gam, &c.bfh, &c.vol}) put(o, *v);
+      for (const auto *v : {&J, &nuJ, &ff, &col, &gam, &bfh, &c.vol}) put(o, *v);
       put(o, c.meanw);
-      const double pv[2] = {c.par.t_current, c.par.tmin};
+      const double pv[4] = {c.par.t_current, c.par.tmin, c.prep.deltat, c.prep.tratmid};
       o.write((const char *)pv, sizeof pv);
-      engine.solve_temperatures(*artis_model_te_tables(m), c.par, c.cells);
+      const artis_te_tables &tab = *artis_model_te_tables(m);
+      engine.prepare_temperatures(tab, c.par, c.prep, c.cells);
+      for (const auto *v : {&c.TR_new, &c.W_new, &c.TJ_new}) put(o, *v);
+      // the solution reads the prepared radiation field (the estimator inputs already point at the prepared arrays)
+      c.cells.TR = c.TR_new.data();
+      c.cells.W = c.W_new.data();
+      c.cells.TJ = c.TJ_new.data();
+      engine.solve_temperatures(tab, c.par, c.cells);
       for (const auto *v : {&c.Te, &c.gp, &c.nne, &c.nnetot, &c.pf}) put(o, *v);
       for (const auto *v : {&c.totcool, &c.ccion, &c.rates}) put(o, *v);
       put(o, c.iters);

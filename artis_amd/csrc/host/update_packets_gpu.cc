@@ -37,6 +37,11 @@ void PacketEngine::solve_temperatures(const artis_te_tables &tables, const artis
   check(artis_gpu_solve_temperatures(&tables, &params, &cells), "artis_gpu_solve_temperatures");
 }
 
+void PacketEngine::prepare_temperatures(const artis_te_tables &tables, const artis_te_params &params,
+                                        const artis_ug_prepare &prep, const artis_te_cells &cells) {
+  check(artis_gpu_prepare_temperatures(&tables, &params, &prep, &cells), "artis_gpu_prepare_temperatures");
+}
+
 void PacketEngine::update_packets(int my_rank, int nts, artis_packet *packets, int npkts, artis_estimators &est) {
   check(artis_gpu_update_packets(my_rank, nts, packets, npkts, &est), "artis_gpu_update_packets");
 }

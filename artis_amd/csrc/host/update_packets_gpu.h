@@ -47,6 +47,10 @@ class PacketEngine {
   // solve_Te_nltepops / LTE branch + calculate_cooling_rates, update_grid.cc:1104-1158, 1199-1205) for the cells in
   // `cells.mgi`, after the host normalised the estimators (update_grid.cc:1041-1150); results written into `cells`
   void solve_temperatures(const artis_te_tables &tables, const artis_te_params &params, artis_te_cells &cells);
+  // the estimator preparation before it (update_grid.cc:1041-1150): raw accumulators -> the inputs of
+  // solve_temperatures, written to prep's *_out arrays
+  void prepare_temperatures(const artis_te_tables &tables, const artis_te_params &params, const artis_ug_prepare &prep,
+                            const artis_te_cells &cells);
 
   double last_transport_ms() const;
 };

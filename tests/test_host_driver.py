@@ -83,7 +83,8 @@ def test_driver_rccl_reduced_path(tmp_path):
 
 
 def _read_te_case(path, m):
-    """te_case.bin of artis_gpu_driver (ARTIS_DRIVER_TE=1): length-prefixed arrays, inputs then outputs."""
+    """te_case.bin of artis_gpu_driver (ARTIS_DRIVER_TE=1): length-prefixed arrays -- the previous state and the raw
+    estimators, the parameters, then the prepared radiation field and the solution."""
     raw = open(path, "rb").read()
     pos = 0
 
@@ -97,26 +98,31 @@ def _read_te_case(path, m):
 
     te = ffi.TeArrays(m, t_current=1.0)
     te.TR, te.W, te.TJ, te.Te, te.groundlevelpop = (arr(np.float32) for _ in range(5))
+    nne_old, pf_old = arr(np.float32), arr(np.float32)
     te.mgi_list = arr(np.int32)
     te.thick = arr(np.int16)
-    te.ffheating, te.colheating, te.gamma, te.bfheating, te.vol_init = (arr(np.float64) for _ in range(5))
+    J, nuJ, ff, col, gam, bfh, te.vol_init = (arr(np.float64) for _ in range(7))
     te.elem_meanweight = arr(np.float32)
-    t_current, tmin = np.frombuffer(raw, np.float64, 2, pos)
-    pos += 16
+    t_current, tmin, deltat, tratmid = np.frombuffer(raw, np.float64, 4, pos)
+    pos += 32
     te.params.t_current, te.params.tmin = float(t_current), float(tmin)
+    prep = ffi.UgArrays(m, deltat=deltat, tratmid=tratmid)
+    prep.J, prep.nuJ, prep.ffheating, prep.colheating, prep.gamma, prep.bfheating = J, nuJ, ff, col, gam, bfh
+    prep.nne, prep.partfunct = nne_old, pf_old
     out = {}
-    for k in ("Te", "groundlevelpop", "nne", "nnetot", "partfunct"):
+    for k in ("TR", "W", "TJ", "Te", "groundlevelpop", "nne", "nnetot", "partfunct"):
         out[k] = arr(np.float32)
     for k in ("totalcooling", "cooling_contrib_ion", "rates"):
         out[k] = arr(np.float64)
     out["iters"] = arr(np.int32)
-    return te, out
+    return te, prep, out
 
 
 @pytest.mark.gpu
 def test_driver_update_grid_on_gpu_matches_oracle(tmp_path):
-    """The C++ host loop with update_grid's temperature / ionisation solution on the GPU
-    (PacketEngine::solve_temperatures) from the run's own normalised estimators, replayed on the CPU oracle."""
+    """The C++ host loop with update_grid on the GPU -- the estimator preparation (PacketEngine::prepare_temperatures)
+    from the run's own raw estimators, then the temperature / ionisation solution (solve_temperatures) -- replayed
+    on the CPU oracle."""
     env = dict(os.environ, ARTIS_DRIVER_TE="1")
     r = subprocess.run(_args(tmp_path), capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr
@@ -124,10 +130,17 @@ def test_driver_update_grid_on_gpu_matches_oracle(tmp_path):
 
     m = Model(**CFG)
     m.set_timestep(NTS0 + NSTEPS - 1)
-    te, out = _read_te_case(os.path.join(tmp_path, "te_case.bin"), m)
-    assert oracle_lib.solve_temperatures(m, te) == 0
+    te, prep, out = _read_te_case(os.path.join(tmp_path, "te_case.bin"), m)
+    assert oracle_lib.prepare_temperatures(m, te, prep) == 0
     g = te.mgi_list
     assert len(g) > 0
+    for a, k in ((prep.TR_out, "TR"), (prep.W_out, "W"), (prep.TJ_out, "TJ")):
+        x, y = a[g].astype(np.float64), out[k][g].astype(np.float64)
+        assert np.all(np.abs(x - y) <= 2.5e-7 * np.abs(x)), k
+    te.TR, te.W, te.TJ = prep.TR_out.copy(), prep.W_out.copy(), prep.TJ_out.copy()
+    te.ffheating, te.colheating = prep.ff_out.copy(), prep.col_out.copy()
+    te.gamma, te.bfheating = prep.gamma_out.copy(), prep.bfheating_out.copy()
+    assert oracle_lib.solve_temperatures(m, te) == 0
     same = (te.iters[g] == out["iters"][g]) & (np.abs(te.Te[g] - out["Te"][g]) <= 1e-9 * np.abs(te.Te[g]))
     assert same.mean() >= 0.99, same.mean()
     assert np.all(np.abs(te.Te[g] - out["Te"][g]) <= 2e-2 * np.abs(te.Te[g]))
