@@ -980,10 +980,10 @@ struct DevBufs {
   }
 };
 template <typename T>
-std::vector<T> d2h_vec(const T *d, size_t n) {
-  std::vector<T> h(n);
-  if (n) (void)hipMemcpy(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost);
-  return h;
+int d2h_vec(std::vector<T> &h, const T *d, size_t n) {
+  h.assign(n, T());
+  if (n) HIPCHK(hipMemcpy(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost));
+  return 0;
 }
 }  // namespace
 
@@ -1012,8 +1012,10 @@ int artis_gpu_solve_temperatures(const artis_te_tables *tab, const artis_te_para
     }
   if (c->ncells == 0) return 0;
   // the heating sum's level list (thermalbalance.cc:304-310): ionising levels of every ion but the top one
-  const std::vector<int32_t> nions = d2h_vec(T.elem_nions, ne), uoff = d2h_vec(T.elem_uniqueionoffset, ne),
-                             ionis = d2h_vec(T.ion_ionisinglevels, ni), ul0 = d2h_vec(T.ion_uniqueleveloffset, ni);
+  std::vector<int32_t> nions, uoff, ionis, ul0;
+  if (d2h_vec(nions, T.elem_nions, ne) || d2h_vec(uoff, T.elem_uniqueionoffset, ne) ||
+      d2h_vec(ionis, T.ion_ionisinglevels, ni) || d2h_vec(ul0, T.ion_uniqueleveloffset, ni))
+    return ARTIS_ERR_HIP;
   std::vector<int32_t> hb;
   for (int e = 0; e < ne; e++) {
     if (nions[e] > TE_MAX_IONS_PER_ELEMENT) {
