@@ -48,6 +48,8 @@ int main(void) {
   printf("te_params %zu\n", sizeof(artis_te_params));
   printf("te_cells %zu\n", sizeof(artis_te_cells));
   printf("te_cells_te_iterations %zu\n", offsetof(artis_te_cells, te_iterations));
+  printf("ug_prepare %zu\n", sizeof(artis_ug_prepare));
+  printf("ug_prepare_renorm %zu\n", offsetof(artis_ug_prepare, corrphotoionrenorm_out));
   return 0;
 }
 """
@@ -75,6 +77,8 @@ def test_c_header_layout_matches_numpy_and_ctypes():
     assert lay["te_params"] == C.sizeof(ffi.TeParams)
     assert lay["te_cells"] == C.sizeof(ffi.TeCells)
     assert lay["te_cells_te_iterations"] == ffi.TeCells.te_iterations.offset
+    assert lay["ug_prepare"] == C.sizeof(ffi.UgPrepare)
+    assert lay["ug_prepare_renorm"] == ffi.UgPrepare.corrphotoionrenorm_out.offset
     assert lay["cell_state"] == 24 * 8  # 15 array pointers + ffegrp + 8 nebular (ABI 6)
 
 
