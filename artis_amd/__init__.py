@@ -26,6 +26,7 @@ ABI_SYMBOLS = [
     "artis_gpu_last_work_counts", "artis_gpu_last_rounds", "artis_gpu_spectrum", "artis_gpu_spectra", "artis_gpu_last_kernel_times", "artis_gpu_last_error", "artis_gpu_abi_version",
     "artis_gpu_vpkt_init", "artis_gpu_vpkt_zero", "artis_gpu_vpkt_download", "artis_gpu_vpkt_last_stats", "artis_gpu_vpkt_last_work",
     "artis_estimator_block_len", "artis_estimator_block_pack", "artis_estimator_block_unpack",
+    "artis_estimator_block_average_scalars",
     "artis_gpu_comm_unique_id", "artis_gpu_comm_init", "artis_gpu_estimators_allreduce", "artis_gpu_comm_finalize",
     "artis_gpu_solve_temperatures", "artis_gpu_last_te_ms", "artis_gpu_prepare_temperatures",
 ]
@@ -83,6 +84,7 @@ def gpu_lib():
         L.artis_estimator_block_len.restype = C.c_size_t
         L.artis_estimator_block_pack.argtypes = [C.POINTER(ffi.Estimators)] + [C.c_int] * 6 + [vp]
         L.artis_estimator_block_unpack.argtypes = [vp] + [C.c_int] * 6 + [C.POINTER(ffi.Estimators)]
+        L.artis_estimator_block_average_scalars.argtypes = [vp] + [C.c_int] * 4
         L.artis_gpu_comm_unique_id.argtypes = [vp]
         L.artis_gpu_comm_init.argtypes = [C.c_int, C.c_int, vp]
         L.artis_gpu_comm_finalize.restype = None

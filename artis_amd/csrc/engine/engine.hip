@@ -1095,6 +1095,16 @@ int artis_gpu_solve_temperatures(const artis_te_tables *tab, const artis_te_para
   G.last_te_ms = ms;
   int32_t fail = 0;
   HIPCHK(hipMemcpy(&fail, D.fail, sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (fail) {
+    // the caller's cell state is left as it was: the reference aborts before writing a partial solution
+    char buf[160];
+    snprintf(buf, sizeof buf,
+             "solve_temperatures: a GSL root-finder error (endpoints do not straddle zero / non-finite value) in "
+             "model cell %d -- the reference aborts here",
+             fail - 1);
+    G.last_error = buf;
+    return ARTIS_ERR_PACKET_FAULT;
+  }
   HIPCHK(hipMemcpy(c->Te, D.Te, npf * sizeof(float), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(c->groundlevelpop, D.gp, npi * sizeof(float), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(c->nne, D.nne, npf * sizeof(float), hipMemcpyDeviceToHost));
@@ -1105,15 +1115,6 @@ int artis_gpu_solve_temperatures(const artis_te_tables *tab, const artis_te_para
   if (c->heatingcoolingrates)
     HIPCHK(hipMemcpy(c->heatingcoolingrates, D.rates, npf * ARTIS_TE_NRATES * sizeof(double), hipMemcpyDeviceToHost));
   if (c->te_iterations) HIPCHK(hipMemcpy(c->te_iterations, D.iters, npf * sizeof(int32_t), hipMemcpyDeviceToHost));
-  if (fail) {
-    char buf[160];
-    snprintf(buf, sizeof buf,
-             "solve_temperatures: a GSL root-finder error (endpoints do not straddle zero / non-finite value) in "
-             "model cell %d -- the reference aborts here",
-             fail - 1);
-    G.last_error = buf;
-    return ARTIS_ERR_PACKET_FAULT;
-  }
   return 0;
 }
 double artis_gpu_last_te_ms(void) { return G.last_te_ms; }
@@ -1129,7 +1130,7 @@ int artis_gpu_prepare_temperatures(const artis_te_tables *tab, const artis_te_pa
   if (!tab || !par || !pr || !c || !tab->bfheating_coeff || c->ncells < 0 || (c->ncells > 0 && !c->mgi) || !c->TR ||
       !c->W || !c->TJ || !c->Te || !c->rho || !c->thick || !c->elem_abundance || !c->vol_init || !c->groundlevelpop ||
       !pr->J || !pr->nuJ || !pr->ffheating || !pr->colheating || !pr->gammaestimator || !pr->bfheatingestimator ||
-      !pr->nne || !pr->partfunct || !pr->TR_out || !pr->W_out || !pr->TJ_out || !pr->ffheating_out ||
+      !pr->nne || !pr->TR_out || !pr->W_out || !pr->TJ_out || !pr->ffheating_out ||
       !pr->colheating_out || !pr->gamma_out || !pr->bfheating_out || !pr->corrphotoionrenorm_out ||
       !(pr->deltat > 0. && pr->tratmid > 0. && pr->nprocs > 0 && par->T_max > par->T_min && par->T_min > 0.)) {
     G.last_error = "prepare_temperatures: NULL array or bad parameters";
@@ -1153,7 +1154,6 @@ int artis_gpu_prepare_temperatures(const artis_te_tables *tab, const artis_te_pa
   rc |= B.get((float **)&U.Te, npf, (const float *)c->Te);
   rc |= B.get((float **)&U.nne, npf, pr->nne);
   rc |= B.get((float **)&U.gp, npi, (const float *)c->groundlevelpop);
-  rc |= B.get((float **)&U.pf, npi, pr->partfunct);
   rc |= B.get((float **)&U.rho, npf, c->rho);
   rc |= B.get((float **)&U.abund, npe, c->elem_abundance);
   rc |= B.get((int16_t **)&U.thick, npf, c->thick);
@@ -1173,7 +1173,9 @@ int artis_gpu_prepare_temperatures(const artis_te_tables *tab, const artis_te_pa
   rc |= B.get(&U.gam_out, npg, (const double *)pr->gamma_out);
   rc |= B.get(&U.bfh_out, npg, (const double *)pr->bfheating_out);
   rc |= B.get(&U.renorm_out, npg, (const double *)pr->corrphotoionrenorm_out);
+  rc |= B.get(&U.fail, 1, (const int32_t *)nullptr);
   if (rc) return ARTIS_ERR_HIP;
+  HIPCHK(hipMemsetAsync(U.fail, 0, sizeof(int32_t), G.stream));
   U.ncells = c->ncells;
   U.nprocs = pr->nprocs;
   U.initial_iteration = par->initial_iteration;
@@ -1187,6 +1189,18 @@ int artis_gpu_prepare_temperatures(const artis_te_tables *tab, const artis_te_pa
   k_ug_prepare<<<(unsigned)((U.ncells + 255) / 256), 256, 0, G.stream>>>(dK, dU);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(G.stream));
+  int32_t fail = 0;
+  HIPCHK(hipMemcpy(&fail, U.fail, sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (fail) {
+    char buf[320];
+    snprintf(buf, sizeof buf,
+             "prepare_temperatures: non-finite corrphotoionrenorm or bf-heating renormalisation in model cell %d "
+             "(e.g. W = 0 or a zero analytic coefficient) -- the reference aborts here (update_grid.cc:911-918, "
+             "959-965)",
+             fail - 1);
+    G.last_error = buf;
+    return ARTIS_ERR_PACKET_FAULT;
+  }
   HIPCHK(hipMemcpy(pr->TR_out, U.TR_out, npf * sizeof(float), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(pr->W_out, U.W_out, npf * sizeof(float), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(pr->TJ_out, U.TJ_out, npf * sizeof(float), hipMemcpyDeviceToHost));
@@ -2427,6 +2441,13 @@ int artis_estimator_block_pack(const artis_estimators *est, int np, int ne, int 
   return 0;
 }
 
+int artis_estimator_block_average_scalars(double *b, int np, int ne, int mi, int nranks) {
+  if (!b || np < 0 || ne < 0 || mi < 0 || nranks <= 0) return ARTIS_ERR_BAD_ARGUMENT;
+  double *sc = b + 5 * (size_t)np + 2 * (size_t)np * ne * mi;
+  for (int j = 0; j < 8; j++) sc[j] /= nranks;  // sn3d.cc:370-377
+  return 0;
+}
+
 int artis_estimator_block_unpack(const double *b, int np, int ne, int mi, int nl, int nbf, int nbins,
                                  artis_estimators *est) {
   if (!est || !b || np < 0 || ne < 0 || mi < 0 || nl < 0 || nbf < 0 || nbins < 0) return ARTIS_ERR_BAD_ARGUMENT;
@@ -2502,6 +2523,12 @@ int artis_gpu_comm_init(int rank, int nranks, const void *id) {
   return 0;
 }
 
+// mpi_reduce_estimators divides the eight time_step scalars by nprocs after the sum (sn3d.cc:370-377): every rank
+// carries a full-energy ensemble.  The arrays stay sums (update_grid divides them by nprocs, update_grid.cc:1041).
+__global__ void k_average_timestep_scalars(double *sc, int nranks) {
+  if (threadIdx.x < 8) sc[threadIdx.x] /= nranks;
+}
+
 int artis_gpu_estimators_allreduce(void) {
   if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
   if (!G.comm || !G.d_redblock) {
@@ -2511,6 +2538,9 @@ int artis_gpu_estimators_allreduce(void) {
   if (int rc = artis_gpu_estimator_block_to_device(G.d_redblock)) return rc;
   NCCLCHK(ncclAllReduce(G.d_redblock, G.d_redblock, artis_gpu_estimator_block_doubles(), ncclFloat64, ncclSum, G.comm,
                         G.stream));
+  const int64_t off_sc = 5 * (int64_t)G.npts_model + 2 * (int64_t)G.npts_model * G.nelements * G.maxnions;
+  k_average_timestep_scalars<<<1, 64, 0, G.stream>>>(G.d_redblock + off_sc, G.comm_ranks);
+  HIPCHK(hipGetLastError());
   return artis_gpu_estimator_block_from_device(G.d_redblock);
 }
 

@@ -696,12 +696,14 @@ struct UgDev {
   const int32_t *mgi;
   int32_t ncells, nprocs, initial_iteration;
   double deltat, tratmid, T_min, T_max;
-  const float *TR, *W, *TJ, *Te, *nne, *gp, *pf, *rho, *abund;
+  const float *TR, *W, *TJ, *Te, *nne, *gp, *rho, *abund;
   const int16_t *thick;
   const double *vol, *J, *nuJ, *ff, *col, *gam, *bfh;
   const double *bfheat_lut;
   float *TR_out, *W_out, *TJ_out;
   double *ff_out, *col_out, *gam_out, *bfh_out, *renorm_out;
+  int32_t *fail;  // first cell (mgi + 1) whose corrphotoionrenorm / bf-heating ratio is not finite (the reference's
+                  // [fatal] aborts, update_grid.cc:911-918, 959-965)
 };
 // ltepop.cc:417-430 with the previous populations (NLTE_POPS_ON false)
 DEVFN double ug_levelpop(const Ctx &K, const UgDev &U, int mgi, int e, int ui, int l) {
@@ -760,6 +762,7 @@ __global__ __launch_bounds__(256) void k_ug_prepare(const Ctx *__restrict__ Kp, 
         const int64_t ix = row + e * mx + i;
         const double g = U.gam[ix] * (estimator_normfactor / ARTIS_H);
         U.renorm_out[ix] = g / (W_old * lut_interp(K, K.T.corrphotoioncoeff, e, i, 0, 0, TR_old));
+        if (!isfinite(U.renorm_out[ix])) atomicCAS(U.fail, 0, mgi + 1);
       }
     const float T_e = U.Te[mgi];
     const float nne = U.nne[mgi];
@@ -788,6 +791,7 @@ __global__ __launch_bounds__(256) void k_ug_prepare(const Ctx *__restrict__ Kp, 
         const double b = U.bfh[ix] * estimator_normfactor;
         const double ana = W_old * lut_interp(K, U.bfheat_lut, e, i, 0, 0, TR_old);
         U.bfh_out[ix] = b / ana;
+        if (!isfinite(U.bfh_out[ix])) atomicCAS(U.fail, 0, mgi + 1);
       }
     const double nubar = nuJ / J;
     if (isfinite(nubar) && nubar != 0.) {

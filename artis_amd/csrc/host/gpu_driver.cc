@@ -237,10 +237,14 @@ int main(int argc, char **argv) {
                   engine.last_transport_ms());
     }
     const char *tev = std::getenv("ARTIS_DRIVER_TE");
-    if (tev && tev[0] == '1' && last_nts >= 0) {
-      // update_grid for the next timestep on the GPU: estimator preparation, then the temperature solution
+    if (tev && tev[0] == '1' && last_nts >= 0 && last_nts + 1 >= cfg.ntstep) {
+      // there is no next timestep to prepare: the reference's update_grid pairs nts with nts_prev = nts - 1
+      std::printf("te skipped: the run ended at the last timestep %d\n", last_nts);
+    } else if (tev && tev[0] == '1' && last_nts >= 0) {
+      // update_grid for the next timestep on the GPU (nts = last_nts + 1, nts_prev = last_nts, as update_grid.cc:1316
+      // pairs them): estimator preparation, then the temperature solution
       TeCase c;
-      const int nts_next = std::min(last_nts + 1, cfg.ntstep - 1);
+      const int nts_next = last_nts + 1;
       te_setup(at, *artis_model_geometry(m), *artis_model_cellstate(m), nts_next, last_nts, (int)np, J, nuJ, ff, col,
                gam, bfh, c);
       std::ofstream o(outdir + "/te_case.bin", std::ios::binary);

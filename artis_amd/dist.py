@@ -7,6 +7,8 @@ only exchange is a SUM of the estimator accumulators.  The block layout is defin
 the host), and used here unchanged:
   [J | nuJ | ffheating | colheating | rpkt_emiss | gammaestimator | bfheatingestimator | 10 time_step scalars
    | bfrate_raw | radfield bins J, nuJ, contribcount (nebular options) | ecounter | acounter | counters (34) | nesc]
+After the sum the eight time_step scalars are divided by the rank count, as mpi_reduce_estimators does
+(sn3d.cc:370-377); everything else stays a sum (update_grid normalises by nprocs, update_grid.cc:1041).
 On GPUs the block is all-reduced in HBM by the engine's own RCCL communicator over xGMI
 (artis_gpu_comm_init / artis_gpu_estimators_allreduce; Engine.comm_init / Engine.allreduce_estimators);
 host arrays are packed with the same layout and reduced with gloo in the CPU tests.
@@ -48,6 +50,17 @@ def unpack_estimators(block, est):
     return est
 
 
+def average_timestep_scalars(block, est, nranks):
+    """After the SUM over nranks: the eight time_step scalars divided by nranks, as mpi_reduce_estimators does
+    (sn3d.cc:370-377; artis_estimator_block_average_scalars).  The device all-reduce does the same in HBM."""
+    block = np.ascontiguousarray(block, dtype=np.float64)
+    rc = gpu_lib().artis_estimator_block_average_scalars(block.ctypes.data, est.npts_model, est.nelements,
+                                                          est.maxnions, int(nranks))
+    if rc != 0:
+        raise RuntimeError(f"artis_estimator_block_average_scalars -> {rc}")
+    return block
+
+
 def join(engine, rank, world, dist_module):
     """Every rank joins the engine's RCCL communicator; rank 0's id travels over dist_module (any backend)."""
     from . import comm_unique_id
@@ -58,5 +71,6 @@ def join(engine, rank, world, dist_module):
 
 
 def allreduce_engine_estimators(engine):
-    """Sum the device estimator blocks of all ranks in place (RCCL over xGMI, engine stream)."""
+    """Sum the device estimator blocks of all ranks in place (RCCL over xGMI, engine stream); the eight time_step
+    scalars are then divided by the rank count (sn3d.cc:370-377)."""
     engine.allreduce_estimators()

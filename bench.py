@@ -1,6 +1,11 @@
 """bench.py -- packet-timesteps per second of the MI355X update_packets engine on the synthetic 50^3 grid.
 
-python bench.py --gpus N --steps K --warmup W          (N>1: launched by torch.distributed.run, one rank/GPU)
+python bench.py --gpus N --steps K --warmup W
+
+N>1: one process per GPU.  Under torch.distributed.run (RANK / WORLD_SIZE set) this process is one rank; a bare
+`python bench.py --gpus N` starts the N rank processes itself (before anything touches torch or the GPU), waits for
+them and exits with their status -- rank 0 prints the JSON line.  --dry-launch does the same rank bring-up without a
+GPU (gloo only) and prints the ranks that joined, for the CPU test of the launcher.
 
 One step = one update_packets(nts) of this rank's P resident packets, all in HBM before timing starts:
   packets reset to the same initial ensemble (device-to-device copy), estimators zeroed, the per-timestep cell
@@ -87,6 +92,61 @@ def cpu_share():
     return threads, {"nproc": os.cpu_count(), "affinity": n, "cgroup_quota_cpus": quota, "cpu_model": model}
 
 
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(n, argv):
+    """Start n rank processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torch.distributed.run
+    sets them, rendezvous on 127.0.0.1), wait for all of them and return the exit status.  Called before anything
+    initialises the GPU: the children are new processes, nothing is exec'd in place.  If one rank fails the others
+    are stopped, so a failed rank cannot leave its peers waiting in a barrier."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    status = 0
+    pending = set(range(n))
+    while pending:
+        for r in list(pending):
+            rc = procs[r].poll()
+            if rc is None:
+                continue
+            pending.discard(r)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 1
+                for q in pending:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    return status
+
+
+def dry_launch(world, rank):
+    """Rank bring-up without a GPU: join the gloo group, gather the ranks, rank 0 prints them."""
+    if os.environ.get("BENCH_DRY_FAIL_RANK") == str(rank):  # launcher test: a rank that dies before the rendezvous
+        sys.exit(3)
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    got = [None] * world
+    dist.all_gather_object(got, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "pid": os.getpid()})
+    if rank == 0:
+        print(json.dumps({"dry_launch": True, "world": world, "ranks": got}), flush=True)
+    dist.destroy_process_group()
+    del torch
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -102,16 +162,24 @@ def main():
     ap.add_argument("--vpkt", type=int, default=0,
                     help="virtual packets (BASELINE config 5, vpkt.cc) with this many observer directions; the "
                          "timestep must lie in the vspec window [10 d, 30 d] (e.g. --nts 30)")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="bring up the N ranks over gloo without a GPU and print them (tests the launcher)")
     args = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
-
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_launch:
+        dry_launch(world, rank)
+        return
+
+    import torch
+    import torch.distributed as dist
+
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
     torch.cuda.set_device(local_rank)

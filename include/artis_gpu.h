@@ -450,6 +450,10 @@ int artis_estimator_block_pack(const artis_estimators *est, int npts_model, int 
                                int nbf_est, int nbins_est, double *block);
 int artis_estimator_block_unpack(const double *block, int npts_model, int nelements, int maxnions, int nlines,
                                  int nbf_est, int nbins_est, artis_estimators *est);
+/* After a host-side SUM of the blocks of nranks ranks: divide the eight time_step scalars (cmf_lum .. gamma_emission)
+ * by nranks, as mpi_reduce_estimators does after its MPI_Allreduce (sn3d.cc:370-377).  artis_gpu_estimators_allreduce
+ * applies the same division to the device block. */
+int artis_estimator_block_average_scalars(double *block, int npts_model, int nelements, int maxnions, int nranks);
 
 /* --- multi-GPU: RCCL over xGMI (the reference's mpi_reduce_estimators, sn3d.cc:316-377, radfield.cc:1502-1564) */
 /* One process per GPU; every rank propagates its own full-energy ensemble and the only exchange per timestep
@@ -600,7 +604,9 @@ int artis_gpu_solve_temperatures(const artis_te_tables *tables, const artis_te_p
    ground-level population = calculate_iongamma_per_gspop (ratecoeff.cc:1353-1389) with the previous T_R, W, T_e,
    n_e and populations, the bf-heating estimator over get_bfheatingcoeff_ana), then set_params_fullspec
    (radfield.cc:1136-1175) for T_J, T_R, W.  Writes the *_out arrays, which then feed artis_gpu_solve_temperatures
-   (cells->TR / W / TJ and the four estimator inputs). */
+   (cells->TR / W / TJ and the four estimator inputs).  A non-finite corrphotoionrenorm or bf-heating ratio (the
+   reference's [fatal] aborts, update_grid.cc:911-918, 959-965) returns ARTIS_ERR_PACKET_FAULT naming the cell and
+   leaves the outputs unwritten; so does a GSL abort path of artis_gpu_solve_temperatures. */
 typedef struct artis_ug_prepare {
   double deltat;             /* globals::time_step[nts_prev].width (update_grid.cc:1316) */
   double tratmid;            /* globals::time_step[nts].mid / globals::tmin */
@@ -610,7 +616,8 @@ typedef struct artis_ug_prepare {
   const double *J, *nuJ, *ffheating, *colheating;   /* [npts_model] */
   const double *gammaestimator, *bfheatingestimator; /* [npts_model * nelements * maxnions] */
   const float *nne;          /* previous update_grid state read by calculate_iongamma_per_gspop */
-  const float *partfunct;    /* [npts_model * nions_total] */
+  const float *partfunct;    /* unused (the LUT branch of calculate_iongamma_per_gspop needs no partition function);
+                                kept for the layout, may be NULL */
   /* outputs */
   float *TR_out, *W_out, *TJ_out;
   double *ffheating_out, *colheating_out, *gamma_out, *bfheating_out;

@@ -4363,7 +4363,8 @@ int oracle_prepare_temperatures(const artis_atomic_tables *at, const artis_run_p
   c.T_step_log = (log(at->maxtemp) - log(at->mintemp)) / (at->tablesize - 1.);
   c.minpop = rp->minpop > 0. ? rp->minpop : 1e-30;
   if (nthreads > 0) omp_set_num_threads(nthreads);
-#pragma omp parallel for schedule(dynamic)
+  int nfail = 0;  // the reference's [fatal] aborts (update_grid.cc:911-918, 959-965)
+#pragma omp parallel for schedule(dynamic) reduction(+ : nfail)
   for (int kk = 0; kk < in->ncells; kk++) {
     const int mgi = in->mgi[kk];
     const size_t row = (size_t)mgi * nel * mx;
@@ -4402,6 +4403,7 @@ int oracle_prepare_temperatures(const artis_atomic_tables *at, const artis_run_p
           const size_t ix = row + e * mx + i;
           const double g = pr->gammaestimator[ix] * (estimator_normfactor / ARTIS_H);
           pr->corrphotoionrenorm_out[ix] = g / (W_old * lut_at(c, at->corrphotoioncoeff, e, i, 0, 0, TR_old));
+          if (!std::isfinite(pr->corrphotoionrenorm_out[ix])) nfail++;  // update_grid.cc:911-918
         }
       for (int e = 0; e < nel; e++)
         for (int i = 0; i < get_nions(c, e) - 1; i++) {
@@ -4429,6 +4431,7 @@ int oracle_prepare_temperatures(const artis_atomic_tables *at, const artis_run_p
           const double b = pr->bfheatingestimator[ix] * estimator_normfactor;
           const double ana = W_old * lut_at(c, tab->bfheating_coeff, e, i, 0, 0, TR_old);  // get_bfheatingcoeff_ana
           pr->bfheating_out[ix] = b / ana;
+          if (!std::isfinite(pr->bfheating_out[ix])) nfail++;  // update_grid.cc:959-965
         }
       // radfield.cc:1136-1175 set_params_fullspec
       const double nubar = nuJ / J;
@@ -4452,6 +4455,6 @@ int oracle_prepare_temperatures(const artis_atomic_tables *at, const artis_run_p
     pr->W_out[mgi] = W;
     pr->TJ_out[mgi] = TJ;
   }
-  return 0;
+  return nfail ? ARTIS_ERR_PACKET_FAULT : 0;
 }
 }  // extern "C"

@@ -184,3 +184,25 @@ def test_gpu_prepare_temperatures_matches_oracle(small, thick_frac):
     finally:
         eng.close()
     compare(small, te, cpu)
+
+
+def test_gpu_prepare_temperatures_fatal_nonfinite(small):
+    """W_old = 0 in one non-LTE cell makes corrphotoionrenorm = Gamma / (W LUT) infinite: the reference aborts
+    (update_grid.cc:911-918); device and oracle return ARTIS_ERR_PACKET_FAULT naming the cell, and the device leaves
+    the caller's outputs unwritten."""
+    from artis_amd import EngineError
+
+    te = ffi.TeArrays(small, t_current=12 * DAY, thick_frac=0.0, seed=11)
+    bad = int(te.mgi_list[2])
+    te.W[bad] = 0
+    pc = ffi.UgArrays(small, deltat=0.5 * DAY, tratmid=3.0, seed=3)
+    assert oracle_lib.prepare_temperatures(small, te, pc) == -5
+    pg = ffi.UgArrays(small, deltat=0.5 * DAY, tratmid=3.0, seed=3)
+    before = pg.TR_out.copy()
+    eng = Engine(small)
+    try:
+        with pytest.raises(EngineError, match=f"model cell {bad}"):
+            eng.prepare_temperatures(te, pg)
+    finally:
+        eng.close()
+    assert np.array_equal(pg.TR_out, before)

@@ -44,7 +44,8 @@ def _worker(rank, world, port, outdir):
         _, pk, est = _rank_run(rank)
         block = torch.from_numpy(adist.pack_estimators(est))
         dist.all_reduce(block)
-        np.save(os.path.join(outdir, f"block{rank}.npy"), block.numpy())
+        block = adist.average_timestep_scalars(block.numpy(), est, world)
+        np.save(os.path.join(outdir, f"block{rank}.npy"), block)
         np.save(os.path.join(outdir, f"pk{rank}.npy"), pk.view(np.uint8))
     finally:
         dist.destroy_process_group()
@@ -70,7 +71,13 @@ def test_estimator_allreduce_world2(tmp_path):
     assert np.load(tmp_path / "pk0.npy").tobytes() == pk0.tobytes()
     assert np.load(tmp_path / "pk1.npy").tobytes() == pk1.tobytes()
     expect = adist.pack_estimators(e0) + adist.pack_estimators(e1)
+    # mpi_reduce_estimators (sn3d.cc:370-377): the eight time_step scalars are averaged over the ranks, the arrays
+    # and counters stay sums
+    off = 5 * m.npts_model + 2 * m.npts_model * m.nelements * m.maxnions
+    expect[off:off + 8] /= 2
     assert np.allclose(b0, expect, rtol=1e-14, atol=0)
+    assert b0[off] == (e0.struct.cmf_lum + e1.struct.cmf_lum) / 2 and b0[off] > 0
+    assert b0[off + 8] == e0.struct.nt_energy_deposited + e1.struct.nt_energy_deposited
 
     # unpack round-trips into the estimator arrays the next update_grid would read
     tot = adist.unpack_estimators(b0, m.new_estimators())
@@ -80,6 +87,7 @@ def test_estimator_allreduce_world2(tmp_path):
     assert (tot.acounter == e0.acounter + e1.acounter).all()
     assert np.allclose(tot.gamma, e0.gamma + e1.gamma, rtol=1e-14)
     assert tot.struct.cmf_lum == b0[adist.block_len(m.npts_model, m.nelements, m.maxnions, 0) - 45]
+    assert tot.struct.cmf_lum == (e0.struct.cmf_lum + e1.struct.cmf_lum) / 2
     assert len(b0) == adist.block_len(m.npts_model, m.nelements, m.maxnions, m.nlines)
 
 

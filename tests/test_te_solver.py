@@ -153,3 +153,18 @@ def test_prepare_lte_and_fit_branches(te_model):
     te.gamma, te.bfheating = prep.gamma_out.copy(), prep.bfheating_out.copy()
     assert oracle_lib.solve_temperatures(m, te) == 0
     assert np.all(np.isfinite(te.Te[idx]))
+
+
+def test_prepare_nonfinite_renorm_is_fatal(te_model):
+    """update_gamma_corrphotoionrenorm_bfheating_estimators aborts on a non-finite corrphotoionrenorm or bf-heating
+    ratio (update_grid.cc:911-918, 959-965): W_old = 0 in a non-LTE cell is such a case, an LTE-branch cell is not."""
+    m = te_model
+    te = ffi.TeArrays(m, t_current=10 * DAY, seed=11)
+    prep = ffi.UgArrays(m, deltat=0.5 * DAY, tratmid=3.0, seed=3)
+    assert oracle_lib.prepare_temperatures(m, te, prep) == 0
+    te.W[te.mgi_list[1]] = 0
+    prep = ffi.UgArrays(m, deltat=0.5 * DAY, tratmid=3.0, seed=3)
+    assert oracle_lib.prepare_temperatures(m, te, prep) == -5
+    te.thick[te.mgi_list[1]] = 1
+    prep = ffi.UgArrays(m, deltat=0.5 * DAY, tratmid=3.0, seed=3)
+    assert oracle_lib.prepare_temperatures(m, te, prep) == 0
