@@ -1,6 +1,8 @@
 // artis_io.cc -- the reference's packet and virtual-packet file formats (include/artis_io.h).
 #include "artis_io.h"
 
+#include "artis_constants.h"
+
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -671,4 +673,144 @@ int artis_write_light_curve(const char *lc_filename, int abin, int numtimesteps,
     }
   }
   return 0;
+}
+
+// ------------------------------------------------------------------------------------ Spencer-Fano input data
+namespace {
+struct NtStorage {
+  std::vector<int32_t> Z, nelec, n, l;
+  std::vector<double> ionpot_ev, A, B, C, D, prob, g_accumulated;
+  std::vector<float> en_auger_ev, n_auger_elec_avg;
+  std::vector<double> binding;
+};
+}  // namespace
+
+int artis_read_nt_data(const char *dir, int nelements, const int32_t *anumber, const int32_t *ionstage0,
+                       const int32_t *nions, int sfpts, double sf_emin, double sf_emax, artis_nt_data *out) {
+  if (!dir || !out || nelements < 0 || (nelements > 0 && (!anumber || !ionstage0 || !nions)) || sfpts < 2 ||
+      !(sf_emax > sf_emin) || !(sf_emin > 0.))
+    return ARTIS_ERR_BAD_ARGUMENT;
+  const int A1 = ARTIS_NT_MAX_AUGER + 1;
+  auto path = [&](const char *name) { return std::string(dir) + "/" + name; };
+  auto included = [&](int Z, int ionstage) {  // get_elementindex + the ion-stage range (nonthermal.cc:410-413)
+    for (int e = 0; e < nelements; e++)
+      if (anumber[e] == Z) return ionstage0[e] <= ionstage && ionstage < ionstage0[e] + nions[e];
+    return false;
+  };
+  auto *st = new NtStorage();
+  auto fail = [&]() {
+    delete st;
+    return ARTIS_ERR_BAD_ARGUMENT;
+  };
+  // read_binding_energies (nonthermal.cc:183-204): a 30 x 10 table in eV
+  {
+    File f(path("binding_energies.txt").c_str(), "r");
+    int dum1 = 0, dum2 = 0;
+    if (!f.f || std::fscanf(f.f, "%d %d", &dum1, &dum2) != 2 || dum1 != 10 || dum2 != 30) return fail();
+    st->binding.assign(300, 0.);
+    for (int i = 0; i < 30; i++)
+      for (int j = 0; j < 10; j++) {
+        float v = 0.f;
+        if (std::fscanf(f.f, "%g", &v) != 1) return fail();
+        st->binding[(size_t)i * 10 + j] = v * ARTIS_EV;
+      }
+  }
+  // read_collion_data (nonthermal.cc:387-437)
+  {
+    File f(path("collion.txt").c_str(), "r");
+    int count = 0;
+    if (!f.f || std::fscanf(f.f, "%d", &count) != 1 || count < 0) return fail();
+    for (int i = 0; i < count; i++) {
+      int Z, nelec, n, l;
+      double ip, A, B, C, D;
+      if (std::fscanf(f.f, "%2d %2d %1d %1d %lg %lg %lg %lg %lg", &Z, &nelec, &n, &l, &ip, &A, &B, &C, &D) != 9)
+        return fail();
+      if (!included(Z, Z - nelec + 1)) continue;
+      st->Z.push_back(Z);
+      st->nelec.push_back(nelec);
+      st->n.push_back(n);
+      st->l.push_back(l);
+      st->ionpot_ev.push_back(ip);
+      st->A.push_back(A);
+      st->B.push_back(B);
+      st->C.push_back(C);
+      st->D.push_back(D);
+      for (int a = 0; a < A1; a++) st->prob.push_back(a == 0 ? 1. : 0.);
+      st->g_accumulated.push_back(0.);
+      st->en_auger_ev.push_back(0.f);
+      st->n_auger_elec_avg.push_back(0.f);
+    }
+  }
+  // read_auger_data (nonthermal.cc:255-385): fixed columns; X-ray subshells K L1 L2 L3 M1 M2 M3
+  {
+    File f(path("auger-km1993-table2.txt").c_str(), "r");
+    if (!f.f) return fail();
+    static const int xrayn[7] = {1, 2, 2, 2, 3, 3, 3}, xrayl[7] = {0, 0, 1, 1, 0, 1, 1}, xrayg[7] = {2, 2, 2, 4, 2, 2, 4};
+    char line[151];
+    while (std::fgets(line, 151, f.f)) {
+      int Z = -1, ionstage = -1, offset = 0;
+      if (std::sscanf(line, "%d %d%n", &Z, &ionstage, &offset) != 2 || offset != 5) return fail();
+      if (!included(Z, ionstage)) continue;
+      int shellnum = -1, epsilon_e3 = -1;
+      float ionpot_ev = -1, en_total = -1;
+      if (std::sscanf(line + 5, "%d %g %g %d%n", &shellnum, &ionpot_ev, &en_total, &epsilon_e3, &offset) != 4 ||
+          offset != 20 || shellnum < 1 || shellnum > 7)
+        return fail();
+      float n_auger_elec_avg = 0;
+      double prob[ARTIS_NT_MAX_AUGER + 1];
+      for (int a = 0; a < 9; a++) {
+        char strprob[6] = "00000";
+        std::memcpy(strprob, line + 26 + a * 5, 5);
+        strprob[5] = '\0';
+        int probe4 = -1;
+        if (std::sscanf(strprob, "%d", &probe4) != 1) return fail();
+        const double p = probe4 / 10000.;
+        if (!(p <= 1.0)) return fail();
+        n_auger_elec_avg += a * p;
+        if (a <= ARTIS_NT_MAX_AUGER)
+          prob[a] = p;
+        else
+          prob[ARTIS_NT_MAX_AUGER] += p;
+      }
+      float en_auger_ev = en_total - (epsilon_e3 / 1000. * ionpot_ev);
+      const int n = xrayn[shellnum - 1], l = xrayl[shellnum - 1], g = xrayg[shellnum - 1];
+      if (!std::isfinite(en_auger_ev) || en_auger_ev < 0) en_auger_ev = 0.;
+      for (size_t i = 0; i < st->Z.size(); i++) {
+        if (st->Z[i] != Z || st->nelec[i] != Z - ionstage + 1 || st->n[i] != n || st->l[i] != l) continue;
+        const double oldweight = st->g_accumulated[i] / (g + st->g_accumulated[i]);
+        const double newweight = g / (g + st->g_accumulated[i]);
+        st->g_accumulated[i] += g;
+        st->en_auger_ev[i] = oldweight * st->en_auger_ev[i] + newweight * en_auger_ev;
+        st->n_auger_elec_avg[i] = oldweight * st->n_auger_elec_avg[i] + newweight * n_auger_elec_avg;
+        for (int a = 0; a < A1; a++) st->prob[i * A1 + a] = oldweight * st->prob[i * A1 + a] + newweight * prob[a];
+      }
+    }
+  }
+  artis_nt_shells &s = out->shells;
+  std::memset(&s, 0, sizeof s);
+  s.nshells = (int32_t)st->Z.size();
+  s.sfpts = sfpts;
+  s.sf_emin = sf_emin;
+  s.sf_emax = sf_emax;
+  s.Z = st->Z.data();
+  s.nelec = st->nelec.data();
+  s.n = st->n.data();
+  s.l = st->l.data();
+  s.ionpot_ev = st->ionpot_ev.data();
+  s.A = st->A.data();
+  s.B = st->B.data();
+  s.C = st->C.data();
+  s.D = st->D.data();
+  s.prob_num_auger = st->prob.data();
+  s.en_auger_ev = st->en_auger_ev.data();
+  s.electron_binding = st->binding.data();
+  out->storage = st;
+  return 0;
+}
+
+void artis_free_nt_data(artis_nt_data *d) {
+  if (!d) return;
+  delete static_cast<NtStorage *>(d->storage);
+  d->storage = nullptr;
+  std::memset(&d->shells, 0, sizeof d->shells);
 }

@@ -1422,6 +1422,8 @@ const artis_cell_state *artis_model_cellstate(const artis_model *m) { return &m-
 const artis_te_tables *artis_model_te_tables(const artis_model *m) { return &m->te_tables; }
 int64_t artis_model_npts_model(const artis_model *m) { return m->npts_model; }
 int artis_model_radfield_nbins(const artis_model *m) { return m->at.radfield_nbins; }
+int artis_model_total_nlte_levels(const artis_model *m) { return m->at.total_nlte_levels; }
+const int32_t *artis_model_ion_ionstage(const artis_model *m) { return m->at.ion_ionstage; }
 void artis_model_config(const artis_model *m, artis_synth_config *out) { *out = m->cfg; }
 
 void artis_model_run_params(const artis_model *m, artis_run_params *p) {

@@ -83,6 +83,8 @@ int artis_model_init_rpackets(const artis_model *m, int nts, int npkts, uint64_t
 int64_t artis_model_npts_model(const artis_model *m);
 /* RADFIELDBINCOUNT of the nebular options, 0 otherwise */
 int artis_model_radfield_nbins(const artis_model *m);
+int artis_model_total_nlte_levels(const artis_model *m);
+const int32_t *artis_model_ion_ionstage(const artis_model *m);
 /* the configuration the model was built with (after artis_model_from_files adopted input.txt's values) */
 void artis_model_config(const artis_model *m, artis_synth_config *out);
 

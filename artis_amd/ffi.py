@@ -4,6 +4,7 @@ Plain data plumbing: every struct here has the same field order and types as the
 tests/test_abi.py checks sizes/offsets against the compiled libraries.
 """
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -441,7 +442,7 @@ class TeTables(C.Structure):
 
 class TeParams(C.Structure):
     _fields_ = [("t_current", C.c_double), ("tmin", C.c_double), ("T_min", C.c_double), ("T_max", C.c_double),
-                ("accuracy", C.c_double), ("initial_iteration", C.c_int32), ("pad0", C.c_int32)]
+                ("accuracy", C.c_double), ("initial_iteration", C.c_int32), ("direct_col_heat", C.c_int32)]
 
 
 _TE_CELL_PTRS = ["mgi", "TR", "W", "TJ", "rho", "thick", "elem_abundance", "elem_meanweight", "vol_init",
@@ -597,3 +598,202 @@ class UgArrays:
                      ("corrphotoionrenorm_out", self.renorm_out)):
             setattr(s, n, a.ctypes.data)
         return s
+
+
+# ----------------------------------------------------------------------- update_grid for the nebular options (ABI 8)
+NT_MAX_AUGER = 2  # ARTIS_NT_MAX_AUGER
+
+
+class NtShells(C.Structure):
+    """artis_nt_shells: the Spencer-Fano inputs of nonthermal::init (nonthermal.cc:183-437)."""
+    _fields_ = [("nshells", C.c_int32), ("sfpts", C.c_int32), ("sf_emin", C.c_double), ("sf_emax", C.c_double)] + [
+        (n, C.c_void_p) for n in ("Z", "nelec", "n", "l", "ionpot_ev", "A", "B", "C", "D", "prob_num_auger",
+                                  "en_auger_ev", "electron_binding")]
+
+
+class NtData(C.Structure):
+    _fields_ = [("shells", NtShells), ("storage", C.c_void_p)]
+
+
+class Geometry(C.Structure):
+    """artis_geometry (include/artis_gpu.h)."""
+    _fields_ = [("grid_type", C.c_int32), ("ncoordgrid", C.c_int32 * 3), ("ngrid", C.c_int32),
+                ("npts_model", C.c_int32), ("cell_pos_min", C.POINTER(C.c_double)), ("cell_mgi", C.POINTER(C.c_int32)),
+                ("modelcell_wid_init", C.POINTER(C.c_double)), ("coordmax", C.c_double * 3), ("tmin", C.c_double),
+                ("tmax", C.c_double), ("rmax", C.c_double), ("vmax", C.c_double), ("ntstep", C.c_int32),
+                ("ts_start", C.POINTER(C.c_double)), ("ts_width", C.POINTER(C.c_double)),
+                ("ts_mid", C.POINTER(C.c_double)), ("nu_min_r", C.c_double), ("nu_max_r", C.c_double)]
+
+
+class NlteParams(C.Structure):
+    _fields_ = [("nts", C.c_int32), ("num_lte_timesteps", C.c_int32), ("initial_iteration", C.c_int32),
+                ("nprocs", C.c_int32), ("nlteiter", C.c_int32), ("do_rlc_est", C.c_int32), ("deltat", C.c_double),
+                ("tratmid", C.c_double), ("t_mid", C.c_double), ("t_current_te", C.c_double), ("tmin", C.c_double),
+                ("T_min", C.c_double), ("T_max", C.c_double), ("accuracy", C.c_double), ("T_R_min", C.c_double),
+                ("T_R_max", C.c_double)]
+
+
+_NLTE_CELL_PTRS = ["mgi", "rho", "elem_abundance", "elem_meanweight", "vol_init", "thick", "deposition_rate_density",
+                   "J", "nuJ", "ffheating", "colheating", "bfrate_raw", "bin_J_raw", "bin_nuJ_raw",
+                   "bin_contribcount", "TR", "W", "TJ", "Te", "nne", "nnetot", "groundlevelpop", "partfunct",
+                   "nlte_pops", "bin_TR", "bin_W", "bfrate_estimator", "nt_frac_heating", "nt_frac_ionization",
+                   "nt_frac_excitation", "nt_nneperion_when_solved", "nt_timestep_last_solved", "nt_eff_ionpot",
+                   "nt_fracdep_ionization_ion", "nt_prob_num_auger", "nt_ionenfrac_num_auger",
+                   "nt_ionization_ratecoeff", "totalcooling", "cooling_contrib_ion", "heatingcoolingrates",
+                   "nlte_iterations"]
+
+
+class NlteCells(C.Structure):
+    _fields_ = [("ncells", C.c_int32), ("pad0", C.c_int32)] + [(n, C.c_void_p) for n in _NLTE_CELL_PTRS]
+
+
+def nt_data_dir():
+    return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "nt_data")
+
+
+class NtDataHandle:
+    """The Spencer-Fano inputs read by the host library (artis_read_nt_data) for a model's included ions."""
+
+    def __init__(self, model, sfpts=4096, sf_emin=0.1, sf_emax=16000., datadir=None):
+        from . import io as _io
+
+        lib = _io.lib()
+        lib.artis_read_nt_data.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                           C.c_double, C.c_double, C.POINTER(NtData)]
+        lib.artis_free_nt_data.argtypes = [C.POINTER(NtData)]
+        lib.artis_free_nt_data.restype = None
+        self._lib = lib
+        hdr = AtomicHeader.from_address(model.atomic)
+        nel = model.nelements
+        anum = np.ctypeslib.as_array(C.cast(hdr.elem_anumber, C.POINTER(C.c_int32)), (nel,)).copy()
+        nions = np.ctypeslib.as_array(C.cast(hdr.elem_nions, C.POINTER(C.c_int32)), (nel,)).copy()
+        uoff = np.ctypeslib.as_array(C.cast(hdr.elem_uniqueionoffset, C.POINTER(C.c_int32)), (nel,)).copy()
+        ionstage_all = model.ion_ionstage()
+        ionstage0 = np.array([ionstage_all[u] for u in uoff], dtype=np.int32)
+        self.data = NtData()
+        rc = lib.artis_read_nt_data((datadir or nt_data_dir()).encode(), nel, anum.ctypes.data, ionstage0.ctypes.data,
+                                    nions.ctypes.data, int(sfpts), float(sf_emin), float(sf_emax),
+                                    C.byref(self.data))
+        if rc != 0:
+            raise RuntimeError(f"artis_read_nt_data -> {rc}")
+        self.shells = self.data.shells
+
+    def __del__(self):
+        try:
+            self._lib.artis_free_nt_data(C.byref(self.data))
+        except Exception:
+            pass
+
+
+def model_vol_init(model):
+    """vol_init_modelcell (grid.cc): the uniform grid's cell volume at tmin times the number of propagation cells
+    mapped to each model cell."""
+    g = Geometry.from_address(model.geometry)
+    mgi = np.ctypeslib.as_array(g.cell_mgi, (g.ngrid,))
+    counts = np.bincount(mgi[mgi < g.npts_model], minlength=g.npts_model)[:g.npts_model]
+    wid = [2 * g.coordmax[d] / g.ncoordgrid[d] for d in range(3)]
+    return counts * (wid[0] * wid[1] * wid[2])
+
+
+def model_time_grid(model):
+    g = Geometry.from_address(model.geometry)
+    n = g.ntstep
+    return (np.ctypeslib.as_array(g.ts_start, (n,)).copy(), np.ctypeslib.as_array(g.ts_width, (n,)).copy(),
+            np.ctypeslib.as_array(g.ts_mid, (n,)).copy(), g.tmin)
+
+
+class NlteArrays:
+    """Host storage for one artis_nlte_cells block: a nebular model's non-empty cells with its current cell state as
+    the previous timestep's solution, the raw estimators of a transport step (an EstimatorArrays) or seeded ones, the
+    non-thermal solution state and the outputs.  The same block feeds the engine and the oracle."""
+
+    def __init__(self, model, nts, est=None, seed=3, thick_frac=0.0, initial_iteration=0, nprocs=1, dep_scale=1.0):
+        m = model
+        cs = CellState.from_address(m.cellstate)
+        hdr = AtomicHeader.from_address(m.atomic)
+        np_, nel, ni = m.npts_model, m.nelements, m.nions_total
+        nb, nbf, ntl = m.radfield_nbins, m.nbfcontinua, m.total_nlte_levels
+        f32 = lambda p, n: np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), (n,)).copy()  # noqa: E731
+        f64 = lambda p, n: np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_double)), (n,)).copy()  # noqa: E731
+        rng = np.random.default_rng(seed)
+        self.rho = f32(cs.rho, np_)
+        self.elem_abundance = f32(cs.elem_abundance, np_ * nel)
+        anum = np.ctypeslib.as_array(C.cast(hdr.elem_anumber, C.POINTER(C.c_int32)), (nel,)).copy()
+        self.elem_meanweight = np.tile((2.1 * anum * MH).astype(np.float32), np_)
+        self.vol_init = model_vol_init(m).astype(np.float64)
+        self.thick = (rng.random(np_) < thick_frac).astype(np.int16)
+        self.mgi_list = np.nonzero(self.rho > 0)[0].astype(np.int32)
+        self.deposition_rate_density = f64(cs.nt_deposition_rate_density, np_) * dep_scale
+        # the previous timestep's state
+        self.TR, self.W, self.TJ, self.Te = (f32(getattr(cs, n), np_) for n in ("TR", "W", "TJ", "Te"))
+        self.nne, self.nnetot = f32(cs.nne, np_), f32(cs.nnetot, np_)
+        self.groundlevelpop, self.partfunct = f32(cs.groundlevelpop, np_ * ni), f32(cs.partfunct, np_ * ni)
+        self.nlte_pops = f64(cs.nlte_pops, np_ * max(ntl, 1))
+        self.bin_TR, self.bin_W = f32(cs.radfield_bin_TR, np_ * nb), f32(cs.radfield_bin_W, np_ * nb)
+        self.bfrate_estimator = f32(cs.bfrate_estimator, np_ * max(nbf, 1))
+        # nt_solution as nonthermal::init leaves it (nonthermal.cc:508-548)
+        A1 = NT_MAX_AUGER + 1
+        self.nt_frac_heating = np.full(np_, 0.97, np.float32)
+        self.nt_frac_ionization = np.full(np_, 0.03, np.float32)
+        self.nt_frac_excitation = np.zeros(np_, np.float32)
+        self.nt_nneperion_when_solved = np.full(np_, -1., np.float32)
+        self.nt_timestep_last_solved = np.full(np_, -1, np.int32)
+        self.nt_eff_ionpot = np.zeros(np_ * ni, np.float32)
+        self.nt_fracdep_ionization_ion = np.zeros(np_ * ni)
+        self.nt_prob_num_auger = np.zeros(np_ * ni * A1, np.float32)
+        self.nt_prob_num_auger[::A1] = 1.
+        self.nt_ionenfrac_num_auger = self.nt_prob_num_auger.copy()
+        # raw estimators of the transport step
+        if est is not None:
+            self.J, self.nuJ = est.J.copy(), est.nuJ.copy()
+            self.ffheating, self.colheating = est.ffheating.copy(), est.colheating.copy()
+            self.bfrate_raw = est.bfrate_raw.copy() if est.nbfcontinua else np.zeros(np_ * nbf)
+            self.bin_J_raw, self.bin_nuJ_raw = est.radfield_J.copy(), est.radfield_nuJ.copy()
+            self.bin_contribcount = est.radfield_count.copy()
+        else:
+            raise ValueError("NlteArrays needs the raw estimators of a transport step")
+        # outputs
+        self.nt_ionization_ratecoeff = np.zeros(np_ * ni)
+        self.totalcooling = np.zeros(np_)
+        self.cooling_contrib_ion = np.zeros(np_ * ni)
+        self.rates = np.zeros(np_ * TE_NRATES)
+        self.iters = np.zeros(np_, np.int32)
+        ts_start, ts_width, ts_mid, tmin = model_time_grid(m)
+        self.params = NlteParams(nts=int(nts), num_lte_timesteps=0, initial_iteration=int(initial_iteration),
+                                 nprocs=int(nprocs), nlteiter=30, do_rlc_est=3, deltat=float(ts_width[nts - 1]),
+                                 tratmid=float(ts_mid[nts] / tmin), t_mid=float(ts_mid[nts]),
+                                 t_current_te=float(ts_mid[nts - 1]), tmin=float(tmin), T_min=float(hdr.mintemp),
+                                 T_max=float(hdr.maxtemp), accuracy=1e-3, T_R_min=500., T_R_max=250000.)
+
+    _ARRAYS = {"rho": "rho", "elem_abundance": "elem_abundance", "elem_meanweight": "elem_meanweight",
+               "vol_init": "vol_init", "thick": "thick", "deposition_rate_density": "deposition_rate_density",
+               "J": "J", "nuJ": "nuJ", "ffheating": "ffheating", "colheating": "colheating",
+               "bfrate_raw": "bfrate_raw", "bin_J_raw": "bin_J_raw", "bin_nuJ_raw": "bin_nuJ_raw",
+               "bin_contribcount": "bin_contribcount", "TR": "TR", "W": "W", "TJ": "TJ", "Te": "Te", "nne": "nne",
+               "nnetot": "nnetot", "groundlevelpop": "groundlevelpop", "partfunct": "partfunct",
+               "nlte_pops": "nlte_pops", "bin_TR": "bin_TR", "bin_W": "bin_W", "bfrate_estimator": "bfrate_estimator",
+               "nt_frac_heating": "nt_frac_heating", "nt_frac_ionization": "nt_frac_ionization",
+               "nt_frac_excitation": "nt_frac_excitation", "nt_nneperion_when_solved": "nt_nneperion_when_solved",
+               "nt_timestep_last_solved": "nt_timestep_last_solved", "nt_eff_ionpot": "nt_eff_ionpot",
+               "nt_fracdep_ionization_ion": "nt_fracdep_ionization_ion", "nt_prob_num_auger": "nt_prob_num_auger",
+               "nt_ionenfrac_num_auger": "nt_ionenfrac_num_auger",
+               "nt_ionization_ratecoeff": "nt_ionization_ratecoeff", "totalcooling": "totalcooling",
+               "cooling_contrib_ion": "cooling_contrib_ion", "heatingcoolingrates": "rates",
+               "nlte_iterations": "iters"}
+
+    def struct(self):
+        s = NlteCells()
+        s.ncells = len(self.mgi_list)
+        s.mgi = self.mgi_list.ctypes.data
+        for field, attr in self._ARRAYS.items():
+            setattr(s, field, getattr(self, attr).ctypes.data)
+        return s
+
+    def copy(self):
+        import copy as _c
+        o = _c.copy(self)
+        for k, v in self.__dict__.items():
+            if isinstance(v, np.ndarray):
+                setattr(o, k, v.copy())
+        o.params = NlteParams.from_buffer_copy(self.params)
+        return o

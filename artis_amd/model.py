@@ -42,6 +42,9 @@ def model_lib():
         lib.artis_model_npts_model.argtypes = [C.c_void_p]
         lib.artis_model_npts_model.restype = C.c_int64
         lib.artis_model_radfield_nbins.argtypes = [C.c_void_p]
+        lib.artis_model_total_nlte_levels.argtypes = [C.c_void_p]
+        lib.artis_model_ion_ionstage.argtypes = [C.c_void_p]
+        lib.artis_model_ion_ionstage.restype = C.c_void_p
         _model_lib = lib
     return _model_lib
 
@@ -153,6 +156,14 @@ class Model:
     @property
     def radfield_nbins(self):
         return int(self._lib.artis_model_radfield_nbins(self._h))
+
+    @property
+    def total_nlte_levels(self):
+        return int(self._lib.artis_model_total_nlte_levels(self._h))
+
+    def ion_ionstage(self):
+        p = self._lib.artis_model_ion_ionstage(self._h)
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int32)), (self.nions_total,)).copy()
 
     def close(self):
         if self._h:

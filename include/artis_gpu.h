@@ -561,7 +561,9 @@ typedef struct artis_te_params {
   double T_min, T_max;        /* MINTEMP, MAXTEMP (the T_e search interval) */
   double accuracy;            /* TEMPERATURE_SOLVER_ACCURACY */
   int32_t initial_iteration;  /* globals::initial_iteration */
-  int32_t pad0;
+  int32_t direct_col_heat;    /* DIRECT_COL_HEAT (artisoptions_kilonova_lte.h:49, artisoptions_nltenebular.h:51): the
+                                 collisional heating is the de-excitation sum over every line (thermalbalance.cc:189-216,
+                                 223-238) instead of colheatingestimator (ABI 8; was padding, 0 = the classic options) */
 } artis_te_params;
 
 #define ARTIS_TE_NRATES 8  /* heatingcoolingrates (thermalbalance.h:4-14): cooling collisional, fb, ff, adiabatic,
@@ -629,13 +631,107 @@ int artis_gpu_prepare_temperatures(const artis_te_tables *tables, const artis_te
 /* device time (ms) of the last artis_gpu_solve_temperatures (the k_te_solve kernel alone) */
 double artis_gpu_last_te_ms(void);
 
-#define ARTIS_GPU_ABI_VERSION 7  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
+/* ------------------------------------------------------------------------------------------------------------ */
+/* update_grid for the nebular options (ABI 8; artisoptions_nltenebular.h: NLTE_POPS_ON with                    */
+/* NLTE_POPS_ALL_IONS_SIMULTANEOUS, MULTIBIN_RADFIELD_MODEL_ON, DETAILED_BF_ESTIMATORS_ON, NO_LUT_PHOTOION /    */
+/* NO_LUT_BFHEATING, NT_ON + NT_SOLVE_SPENCERFANO, DIRECT_COL_HEAT), SURVEY.md §8(f) row 4.  Per listed model     */
+/* cell, what update_grid_cell does for timestep nts (update_grid.cc:1012-1205):                                */
+/*  - LTE branch (initial_iteration or thick == 1): T_J from J, T_R = T_e = T_J, W = 1, precalculate_partfuncts, */
+/*    calculate_populations (LTE phi);                                                                          */
+/*  - otherwise: J, nuJ, ff / collisional heating normalised; radfield::fit_parameters (radfield.cc:1136-1291:  */
+/*    full-spectrum T_J / T_R / W, and per bin a GSL Brent on the mean frequency of a dilute Planck function with */
+/*    GSL qag Planck integrals, the top bin at T_e); normalise_bf_estimators (radfield.cc:1306-1327);           */
+/*    solve_Te_nltepops (update_grid.cc:763-886): calculate_bfheatingcoeffs (NO_LUT integrals,                  */
+/*    thermalbalance.cc:60-187), then up to NLTEITER + 1 passes of: solve_spencerfano (nonthermal.cc:2522-2713,   */
+/*    the SFPTS x SFPTS upper-triangular Spencer-Fano system with its LU refinement, then analyse_sf_solution,  */
+/*    nonthermal.cc:1996-2280), call_T_e_finder (thermalbalance.cc:397-597 with calculate_electron_densities),   */
+/*    solve_nlte_pops_element for every element (nltepop.cc:798-1113: rate matrix, LTE normalisation, LU solve  */
+/*    with iterative refinement), precalculate_partfuncts and calculate_electron_densities, until n_e and T_e    */
+/*    change by at most 4 %;                                                                                    */
+/*  - then kpkt::calculate_cooling_rates.                                                                      */
+/* Third-party arithmetic: GSL's LU (version unpinned; 2.7.1 in the reference CI) is restated as LU with partial */
+/* pivoting, right-looking, with column-oriented triangular solves (oracle and engine alike).                  */
+/* ------------------------------------------------------------------------------------------------------------ */
+#define ARTIS_NT_MAX_AUGER 2  /* NT_MAX_AUGER_ELECTRONS (artisoptions_nltenebular.h:193) */
+
+/* The Spencer-Fano inputs nonthermal::init reads (nonthermal.cc:183-437): impact-ionisation shells of the included
+ * ions (collion.txt, Younger fit coefficients) with their g-weighted Auger data (auger-km1993-table2.txt), the
+ * binding energies of the work-function approximation (binding_energies.txt), and the energy grid. */
+typedef struct artis_nt_shells {
+  int32_t nshells;
+  int32_t sfpts;                     /* SFPTS (4096) */
+  double sf_emin, sf_emax;           /* SF_EMIN, SF_EMAX [eV] (linear grid, SF_USE_LOG_E_INCREMENT false) */
+  const int32_t *Z, *nelec, *n, *l;  /* [nshells] in collion.txt order */
+  const double *ionpot_ev, *A, *B, *C, *D;
+  const double *prob_num_auger;      /* [nshells * (ARTIS_NT_MAX_AUGER + 1)] */
+  const float *en_auger_ev;          /* [nshells] */
+  const double *electron_binding;    /* [30 * 10] erg, binding_energies.txt */
+} artis_nt_shells;
+
+typedef struct artis_nlte_params {
+  int32_t nts;                 /* globals::nts_global: the timestep update_grid prepares */
+  int32_t num_lte_timesteps;   /* input.txt */
+  int32_t initial_iteration;   /* globals::initial_iteration */
+  int32_t nprocs;              /* globals::nprocs */
+  int32_t nlteiter;            /* NLTEITER (30) */
+  int32_t do_rlc_est;          /* 3: gamma-ray heating into the thermal balance (thermalbalance.cc:373-376) */
+  double deltat;               /* time_step[nts_prev].width */
+  double tratmid;              /* time_step[nts].mid / tmin */
+  double t_mid;                /* time_step[nts].mid: the bound-bound rates of the NLTE matrix (nltepop.cc:818) */
+  double t_current_te;         /* time_step[nts - 1].mid: call_T_e_finder at titer 0 (update_grid.cc:804-806) */
+  double tmin;
+  double T_min, T_max;         /* MINTEMP, MAXTEMP */
+  double accuracy;             /* TEMPERATURE_SOLVER_ACCURACY */
+  double T_R_min, T_R_max;     /* bin fit range (artisoptions_nltenebular.h:109-110) */
+} artis_nlte_params;
+
+typedef struct artis_nlte_cells {
+  int32_t ncells;
+  int32_t pad0;
+  const int32_t *mgi;                   /* [ncells] */
+  /* inputs, indexed by mgi */
+  const float *rho;                     /* grid::get_rho at this timestep */
+  const float *elem_abundance, *elem_meanweight;  /* [npts_model * nelements] */
+  const double *vol_init;
+  const int16_t *thick;
+  const double *deposition_rate_density;/* nonthermal::calculate_deposition_rate_density (nonthermal.cc:626-657) */
+  /* raw estimators of the transport step (summed over ranks; the arrays of artis_estimators) */
+  const double *J, *nuJ, *ffheating, *colheating;
+  const double *bfrate_raw;             /* [npts_model * nbfcontinua] */
+  const double *bin_J_raw, *bin_nuJ_raw;/* [npts_model * radfield_nbins] */
+  const int64_t *bin_contribcount;
+  /* in: the previous timestep's state; out: this timestep's (the artis_cell_state arrays the transport reads) */
+  float *TR, *W, *TJ, *Te, *nne, *nnetot;
+  float *groundlevelpop, *partfunct;    /* [npts_model * nions_total] */
+  double *nlte_pops;                    /* [npts_model * total_nlte_levels] */
+  float *bin_TR, *bin_W;                /* [npts_model * radfield_nbins] radfieldbin_solutions */
+  float *bfrate_estimator;              /* [npts_model * nbfcontinua] prev_bfrate_normed */
+  /* the non-thermal solution (nt_solution[mgi], nonthermal.cc:123-146), in / out */
+  float *nt_frac_heating, *nt_frac_ionization, *nt_frac_excitation;   /* [npts_model] */
+  float *nt_nneperion_when_solved;      /* [npts_model] */
+  int32_t *nt_timestep_last_solved;     /* [npts_model] */
+  float *nt_eff_ionpot;                 /* [npts_model * nions_total] */
+  double *nt_fracdep_ionization_ion;    /* [npts_model * nions_total] */
+  float *nt_prob_num_auger, *nt_ionenfrac_num_auger;  /* [npts_model * nions_total * (ARTIS_NT_MAX_AUGER + 1)] */
+  /* outputs */
+  double *nt_ionization_ratecoeff;      /* [npts_model * nions_total] nt_ionization_ratecoeff (nonthermal.cc:1684) */
+  double *totalcooling, *cooling_contrib_ion;
+  double *heatingcoolingrates;          /* [npts_model * ARTIS_TE_NRATES]; may be NULL */
+  int32_t *nlte_iterations;             /* [npts_model] passes of the solve_Te_nltepops loop (0: LTE branch);
+                                           may be NULL */
+} artis_nlte_cells;
+int artis_gpu_update_grid_nlte(const artis_nt_shells *nt, const artis_nlte_params *params, artis_nlte_cells *cells);
+double artis_gpu_last_nlte_ms(void);  /* device time (ms) of the last artis_gpu_update_grid_nlte */
+
+#define ARTIS_GPU_ABI_VERSION 8  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
                                     3: virtual packets (artis_vpkt_params / artis_vpkt_result);
                                     4: artis_run_params.excitation_temperature;
                                     5: host estimator block pack/unpack, RCCL communicator + all-reduce;
                                     6: the nebular path (NLTE / superlevel populations, binned radiation field,
                                        detailed bf estimators, NO_LUT photoionisation, non-thermal ionisation);
-                                    7: update_grid's temperature / ionisation solution (artis_gpu_solve_temperatures) */
+                                    7: update_grid's temperature / ionisation solution (artis_gpu_solve_temperatures);
+                                    8: update_grid for the nebular options (artis_gpu_update_grid_nlte),
+                                       artis_te_params.direct_col_heat */
 int artis_gpu_abi_version(void);
 
 #ifdef __cplusplus

@@ -120,6 +120,20 @@ int artis_write_light_curve(const char *lc_filename, int abin, int numtimesteps,
                             const double *ts_width, const double *lc_lum, const double *lc_lumcmf,
                             const double *gamma_dep, const double *cmf_lum);
 
+/* The Spencer-Fano data nonthermal::init reads (nonthermal.cc:183-437) from directory dir: binding_energies.txt
+ * (read_binding_energies), collion.txt (read_collion_data: the rows of the included ions -- elements anumber[e]
+ * with ion stages ionstage0[e] .. ionstage0[e] + nions[e] - 1 -- in file order) and auger-km1993-table2.txt
+ * (read_auger_data: Auger-electron probabilities and mean energies, g-weighted over the X-ray subshells that map to
+ * each row's n, l).  Fills out->shells (whose arrays out owns) with the energy grid sfpts / sf_emin / sf_emax.
+ * Release with artis_free_nt_data. */
+typedef struct artis_nt_data {
+  artis_nt_shells shells;
+  void *storage;
+} artis_nt_data;
+int artis_read_nt_data(const char *dir, int nelements, const int32_t *anumber, const int32_t *ionstage0,
+                       const int32_t *nions, int sfpts, double sf_emin, double sf_emax, artis_nt_data *out);
+void artis_free_nt_data(artis_nt_data *d);
+
 #ifdef __cplusplus
 }
 #endif

@@ -4458,3 +4458,6 @@ int oracle_prepare_temperatures(const artis_atomic_tables *at, const artis_run_p
   return nfail ? ARTIS_ERR_PACKET_FAULT : 0;
 }
 }  // extern "C"
+
+// update_grid for the nebular options (the checker of artis_gpu_update_grid_nlte)
+#include "nebular_update_grid.cc"

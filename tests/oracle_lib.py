@@ -141,3 +141,13 @@ def prepare_temperatures(model, te, prep, params=None, nthreads=0):
     return L.oracle_prepare_temperatures(model.atomic, C.byref(params if params is not None else model.params),
                                          te.tables, C.byref(te.params), C.byref(p), C.byref(s), model.npts_model,
                                          nthreads)
+
+
+def update_grid_nlte(model, nt, arr, params=None, nthreads=0):
+    """oracle_update_grid_nlte on an NlteArrays block (in place) with an NtDataHandle; returns the status."""
+    L = lib()
+    L.oracle_update_grid_nlte.argtypes = [C.c_void_p, C.POINTER(ffi.RunParams), C.POINTER(ffi.NtShells),
+                                          C.POINTER(ffi.NlteParams), C.POINTER(ffi.NlteCells), C.c_int, C.c_int]
+    s = arr.struct()
+    return L.oracle_update_grid_nlte(model.atomic, C.byref(params if params is not None else model.params),
+                                     C.byref(nt.shells), C.byref(arr.params), C.byref(s), model.npts_model, nthreads)
