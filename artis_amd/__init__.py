@@ -29,6 +29,7 @@ ABI_SYMBOLS = [
     "artis_estimator_block_average_scalars",
     "artis_gpu_comm_unique_id", "artis_gpu_comm_init", "artis_gpu_estimators_allreduce", "artis_gpu_comm_finalize",
     "artis_gpu_solve_temperatures", "artis_gpu_last_te_ms", "artis_gpu_prepare_temperatures",
+    "artis_gpu_update_grid_nlte", "artis_gpu_last_nlte_ms",
 ]
 
 _gpu_lib = None
@@ -92,6 +93,9 @@ def gpu_lib():
         L.artis_gpu_last_te_ms.restype = C.c_double
         L.artis_gpu_prepare_temperatures.argtypes = [vp, C.POINTER(ffi.TeParams), C.POINTER(ffi.UgPrepare),
                                                      C.POINTER(ffi.TeCells)]
+        L.artis_gpu_update_grid_nlte.argtypes = [C.POINTER(ffi.NtShells), C.POINTER(ffi.NlteParams),
+                                                 C.POINTER(ffi.NlteCells)]
+        L.artis_gpu_last_nlte_ms.restype = C.c_double
         _gpu_lib = L
     return _gpu_lib
 
@@ -140,6 +144,14 @@ class Engine:
         s = te.struct()
         self._check(self.lib.artis_gpu_prepare_temperatures(te.tables, C.byref(te.params), C.byref(prep.struct()),
                                                             C.byref(s)), "prepare_temperatures")
+
+    def update_grid_nlte(self, nt, arr):
+        """update_grid for the nebular options (artis_gpu_update_grid_nlte) on an NlteArrays block, in place; nt: an
+        NtDataHandle (the Spencer-Fano shells) or None.  Returns the device milliseconds."""
+        s = arr.struct()
+        self._check(self.lib.artis_gpu_update_grid_nlte(C.byref(nt.shells) if nt is not None else None,
+                                                        C.byref(arr.params), C.byref(s)), "update_grid_nlte")
+        return float(self.lib.artis_gpu_last_nlte_ms())
 
     def upload_cellstate(self, nts):
         self._check(self.lib.artis_gpu_upload_cellstate(int(nts), self.model.cellstate), "upload_cellstate")

@@ -19,6 +19,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <map>
+#include <type_traits>
 #include <vector>
 
 #include "artis_constants.h"
@@ -33,6 +35,7 @@
 #include "vpkt.h"
 #include "qag.h"
 #include "te_solver.h"
+#include "nlte_solver.h"
 
 // ================================================================================================= kernels
 
@@ -578,6 +581,8 @@ struct Engine {
   // virtual packets (vpkt.h): device accumulators and the spawn buffer (sized per update)
   int64_t vpkt_cap_param = 0;
   std::vector<int32_t> h_anumber;  // artis_atomic_tables.elem_anumber
+  std::vector<double> h_ion_ionpot;  // artis_atomic_tables.ion_ionpot (get_mean_binding_energy)
+  double last_nlte_ms = 0.;
   std::vector<int32_t> h_line_elem;  // artis_atomic_tables.line_elementindex (virtual-packet line masks)
   double *d_vpkt_spawn = nullptr;
   uint32_t vpkt_spawn_cap = 0;
@@ -975,7 +980,9 @@ struct DevBufs {
     if (count == 0) count = 1;
     HIPCHK(hipMalloc((void **)d, count * sizeof(T)));
     p.push_back((void *)*d);
-    if (src) HIPCHK(hipMemcpyAsync(*d, src, count * sizeof(T), hipMemcpyHostToDevice, G.stream));
+    // host-synchronous: a pageable source may be a temporary, and an asynchronous copy queued behind running
+    // kernels would read it after it is gone
+    if (src) HIPCHK(hipMemcpy(*d, src, count * sizeof(T), hipMemcpyHostToDevice));
     return 0;
   }
 };
@@ -1069,6 +1076,7 @@ int artis_gpu_solve_temperatures(const artis_te_tables *tab, const artis_te_para
   D.T_max = par->T_max;
   D.accuracy = par->accuracy;
   D.initial_iteration = par->initial_iteration;
+  D.direct_col_heat = par->direct_col_heat;
   HIPCHK(hipEventRecord(G.ev0, G.stream));
   if (D.nhb > 0) {
     const int64_t nw = (int64_t)D.nhb * D.ncells;
@@ -1211,6 +1219,811 @@ int artis_gpu_prepare_temperatures(const artis_te_tables *tab, const artis_te_pa
   HIPCHK(hipMemcpy(pr->corrphotoionrenorm_out, U.renorm_out, npg * sizeof(double), hipMemcpyDeviceToHost));
   return 0;
 }
+
+}  // extern "C"
+
+// ============================================================================== update_grid, nebular options
+// artis_gpu_update_grid_nlte (include/artis_gpu.h, nlte_solver.h).  Host side: the atomic bookkeeping of the
+// Spencer-Fano and rate-matrix layouts, the caller's arrays copied in, the kernels of solve_Te_nltepops per pass for
+// the cells still iterating (the host reads back the convergence flags between passes), every array copied back on
+// success.
+namespace {
+// nonthermal.cc:994-1007
+double sf_get_J_host(int Z, int ionstage, double ionpot_ev) {
+  if (ionstage == 1) {
+    if (Z == 2) return 15.8;
+    if (Z == 10) return 24.2;
+    if (Z == 18) return 10.0;
+  }
+  return 0.6 * ionpot_ev;
+}
+// nonthermal.cc:1193-1309 get_mean_binding_energy; false on the reference's abort paths
+bool sf_mean_binding_energy_host(const artis_nt_shells *nt, int Zel, int ioncharge, double ionpot, double *out) {
+  const int nbound = Zel - ioncharge;
+  double total = 0.0;
+  if (nbound > 0) {
+    int q[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int electron_loop = 0; electron_loop < nbound; electron_loop++) {
+      if (q[0] < 2)
+        q[0]++;
+      else if (q[1] < 2)
+        q[1]++;
+      else if (q[2] < 2)
+        q[2]++;
+      else if (q[3] < 4)
+        q[3]++;
+      else if (q[4] < 2)
+        q[4]++;
+      else if (q[5] < 2)
+        q[5]++;
+      else if (q[6] < 4)
+        q[6]++;
+      else if (ioncharge == 0) {
+        if (q[9] < 2)
+          q[9]++;
+        else if (q[7] < 4)
+          q[7]++;
+        else if (q[8] < 6)
+          q[8]++;
+        else
+          return false;
+      } else if (ioncharge == 1) {
+        if (q[9] < 1)
+          q[9]++;
+        else if (q[7] < 4)
+          q[7]++;
+        else if (q[8] < 6)
+          q[8]++;
+        else
+          return false;
+      } else if (ioncharge > 1) {
+        if (q[7] < 4)
+          q[7]++;
+        else if (q[8] < 6)
+          q[8]++;
+        else
+          return false;
+      }
+    }
+    if (Zel < 1 || Zel > 30) return false;
+    for (int electron_loop = 0; electron_loop < 10; electron_loop++) {
+      const double electronsinshell = q[electron_loop];
+      if (electronsinshell > 0) {
+        double use2 = nt->electron_binding[(Zel - 1) * 10 + electron_loop];
+        const double use3 = ionpot;
+        if (use2 <= 0) {
+          use2 = nt->electron_binding[(Zel - 1) * 10 + electron_loop - 1];
+          if (electron_loop != 8) return false;
+        }
+        if (use2 < use3)
+          total += electronsinshell / use3;
+        else
+          total += electronsinshell / use2;
+      }
+    }
+  }
+  *out = total;
+  return true;
+}
+}  // namespace
+
+extern "C" {
+int artis_gpu_update_grid_nlte(const artis_nt_shells *nt, const artis_nlte_params *p, artis_nlte_cells *c) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  const DevRun &R = G.K.R;
+  if (!R.nlte_on || !R.no_lut_photoion || !R.no_lut_bfheating || !R.multibin) {
+    G.last_error = "update_grid_nlte: needs the nebular options (NLTE_POPS_ON, NO_LUT_PHOTOION / BFHEATING, MULTIBIN)";
+    return ARTIS_ERR_UNSUPPORTED;
+  }
+  const bool sf_on = R.nt_on && R.nt_solve_spencerfano;
+  if (R.nt_on && R.nt_max_auger != ARTIS_NT_MAX_AUGER) {
+    G.last_error = "update_grid_nlte: nt_max_auger_electrons must be ARTIS_NT_MAX_AUGER";
+    return ARTIS_ERR_UNSUPPORTED;
+  }
+  if (!p || !c || c->ncells < 0 || (c->ncells > 0 && !c->mgi) || !c->rho || !c->elem_abundance ||
+      !c->elem_meanweight || !c->vol_init || !c->thick || !c->J || !c->nuJ || !c->ffheating || !c->bin_J_raw ||
+      !c->bin_nuJ_raw || !c->bin_contribcount || !c->TR || !c->W || !c->TJ || !c->Te || !c->nne || !c->nnetot ||
+      !c->groundlevelpop || !c->partfunct || !c->nlte_pops || !c->bin_TR || !c->bin_W || !c->totalcooling ||
+      !c->cooling_contrib_ion || (R.detailed_bf && (!c->bfrate_raw || !c->bfrate_estimator)) ||
+      (R.nt_on && (!c->deposition_rate_density || !c->nt_ionization_ratecoeff || !c->nt_eff_ionpot ||
+                   !c->nt_frac_heating || !c->nt_frac_ionization || !c->nt_frac_excitation ||
+                   !c->nt_nneperion_when_solved || !c->nt_timestep_last_solved || !c->nt_fracdep_ionization_ion ||
+                   !c->nt_prob_num_auger || !c->nt_ionenfrac_num_auger)) ||
+      (sf_on && (!nt || nt->sfpts < 2 || nt->sfpts > SF_NMAX || !(nt->sf_emax > nt->sf_emin) || nt->nshells < 0 ||
+                 (nt->nshells > 0 && (!nt->Z || !nt->nelec || !nt->ionpot_ev || !nt->A || !nt->B || !nt->C ||
+                                      !nt->D || !nt->prob_num_auger || !nt->en_auger_ev)) ||
+                 !nt->electron_binding)) ||
+      !(p->T_min > 0. && p->T_max > p->T_min && p->accuracy > 0. && p->tmin > 0. && p->t_current_te > 0. &&
+        p->deltat > 0. && p->tratmid > 0. && p->nprocs > 0 && p->T_R_max > p->T_R_min && p->nlteiter >= 0)) {
+    G.last_error = "update_grid_nlte: NULL array or bad parameters";
+    return ARTIS_ERR_BAD_ARGUMENT;
+  }
+  const int np = G.npts_model, ne = G.nelements, ni = G.nions_total;
+  const DevTab &T = G.K.T;
+  const int nl = T.nlevels_total, nbf = T.nbf, nbins = T.rf_nbins, ntl = T.total_nlte_levels;
+  const int64_t ntg = T.ntargets_total;
+  for (int k = 0; k < c->ncells; k++)
+    if (c->mgi[k] < 0 || c->mgi[k] >= np) {
+      G.last_error = "update_grid_nlte: cell index out of range";
+      return ARTIS_ERR_BAD_ARGUMENT;
+    }
+  if (c->ncells == 0) return 0;
+  HIPCHK(hipEventRecord(G.ev2, G.stream));
+  // host copies of the atomic bookkeeping the layouts need
+  std::vector<int32_t> nions, uoff, ion_nlev, ion_ul0, ionis, nlte_n, nlte_first, ionstage, lev_nup, lev_upoff;
+  std::vector<double> lev_eps;
+  std::vector<float> lev_g;
+  if (d2h_vec(nions, T.elem_nions, ne) || d2h_vec(uoff, T.elem_uniqueionoffset, ne) ||
+      d2h_vec(ion_nlev, T.ion_nlevels, ni) || d2h_vec(ion_ul0, T.ion_uniqueleveloffset, ni) ||
+      d2h_vec(ionis, T.ion_ionisinglevels, ni) || d2h_vec(nlte_n, T.ion_nlevels_nlte, ni) ||
+      d2h_vec(nlte_first, T.ion_first_nlte, ni) || d2h_vec(ionstage, T.ion_ionstage, ni) ||
+      d2h_vec(lev_nup, T.level_nuptrans, nl) || d2h_vec(lev_upoff, T.level_uptrans_offset, nl) ||
+      d2h_vec(lev_eps, T.level_epsilon, nl) || d2h_vec(lev_g, T.level_stat_weight, nl))
+    return ARTIS_ERR_HIP;
+  // calculate_heating_rates' bf-heating levels (thermalbalance.cc:304-310)
+  std::vector<int32_t> hb;
+  for (int e = 0; e < ne; e++) {
+    if (nions[e] > TE_MAX_IONS_PER_ELEMENT) {
+      G.last_error = "update_grid_nlte: more ions per element than TE_MAX_IONS_PER_ELEMENT";
+      return ARTIS_ERR_UNSUPPORTED;
+    }
+    for (int i = 0; i < nions[e] - 1; i++)
+      for (int l = 0; l < ionis[uoff[e] + i]; l++) hb.push_back(ion_ul0[uoff[e] + i] + l);
+  }
+  // the LTE-branch and the iterated cells
+  std::vector<int32_t> lte_list, nl_list;
+  for (int k = 0; k < c->ncells; k++) {
+    const int mgi = c->mgi[k];
+    if (p->initial_iteration || c->thick[mgi] == 1)
+      lte_list.push_back(mgi);
+    else
+      nl_list.push_back(mgi);
+  }
+  const int nnl = (int)nl_list.size();
+  const size_t npf = np, npi = (size_t)np * ni, npe = (size_t)np * ne, A1 = NL_A1;
+  DevBufs B;
+  NlDev N{};
+  int rc = 0;
+  N.np = np;
+  N.ncells = c->ncells;
+  rc |= B.get((int32_t **)&N.mgi, (size_t)c->ncells, c->mgi);
+  N.nts = p->nts;
+  N.num_lte_timesteps = p->num_lte_timesteps;
+  N.initial_iteration = p->initial_iteration;
+  N.nprocs = p->nprocs;
+  N.do_rlc_est = p->do_rlc_est;
+  N.nt_on = R.nt_on;
+  N.sf_on = sf_on;
+  N.deltat = p->deltat;
+  N.tratmid = p->tratmid;
+  N.T_min = p->T_min;
+  N.T_max = p->T_max;
+  N.T_R_min = p->T_R_min;
+  N.T_R_max = p->T_R_max;
+  rc |= B.get((float **)&N.rho, npf, c->rho);
+  rc |= B.get((float **)&N.abund, npe, c->elem_abundance);
+  rc |= B.get((float **)&N.meanw, npe, c->elem_meanweight);
+  rc |= B.get((double **)&N.vol, npf, c->vol_init);
+  rc |= B.get((int16_t **)&N.thick, npf, c->thick);
+  rc |= B.get((double **)&N.dep, npf, R.nt_on ? c->deposition_rate_density : nullptr);
+  rc |= B.get((double **)&N.J, npf, c->J);
+  rc |= B.get((double **)&N.nuJ, npf, c->nuJ);
+  rc |= B.get((double **)&N.ffraw, npf, c->ffheating);
+  rc |= B.get((double **)&N.bfraw, (size_t)np * nbf, R.detailed_bf ? c->bfrate_raw : nullptr);
+  rc |= B.get((double **)&N.binJ, (size_t)np * nbins, c->bin_J_raw);
+  rc |= B.get((double **)&N.binnuJ, (size_t)np * nbins, c->bin_nuJ_raw);
+  rc |= B.get((int64_t **)&N.bincount, (size_t)np * nbins, c->bin_contribcount);
+  rc |= B.get(&N.TR, npf, c->TR);
+  rc |= B.get(&N.W, npf, c->W);
+  rc |= B.get(&N.TJ, npf, c->TJ);
+  rc |= B.get(&N.Te, npf, c->Te);
+  rc |= B.get(&N.nne, npf, c->nne);
+  rc |= B.get(&N.nnetot, npf, c->nnetot);
+  rc |= B.get(&N.gp, npi, c->groundlevelpop);
+  rc |= B.get(&N.pf, npi, c->partfunct);
+  rc |= B.get(&N.nlte, (size_t)np * std::max(1, ntl), c->nlte_pops);
+  rc |= B.get(&N.binTR, (size_t)np * nbins, c->bin_TR);
+  rc |= B.get(&N.binW, (size_t)np * nbins, c->bin_W);
+  rc |= B.get(&N.bfrate, (size_t)np * std::max(1, nbf), R.detailed_bf ? c->bfrate_estimator : nullptr);
+  if (R.nt_on) {
+    rc |= B.get(&N.nt_fh, npf, c->nt_frac_heating);
+    rc |= B.get(&N.nt_fi, npf, c->nt_frac_ionization);
+    rc |= B.get(&N.nt_fe, npf, c->nt_frac_excitation);
+    rc |= B.get(&N.nt_nneper, npf, c->nt_nneperion_when_solved);
+    rc |= B.get(&N.nt_tls, npf, c->nt_timestep_last_solved);
+    rc |= B.get(&N.nt_effion, npi, c->nt_eff_ionpot);
+    rc |= B.get(&N.nt_fracdep, npi, c->nt_fracdep_ionization_ion);
+    rc |= B.get(&N.nt_prob, npi * A1, c->nt_prob_num_auger);
+    rc |= B.get(&N.nt_ionen, npi * A1, c->nt_ionenfrac_num_auger);
+    rc |= B.get(&N.ntY, npi, (const double *)nullptr);
+  }
+  rc |= B.get(&N.ffheat, npf, (const double *)nullptr);
+  rc |= B.get(&N.hdep, npf, (const double *)nullptr);
+  rc |= B.get(&N.prevTe, npf, (const double *)nullptr);
+  rc |= B.get(&N.fail, 2, (const int32_t *)nullptr);
+  double *d_totcool = nullptr, *d_ccion = nullptr, *d_rates = nullptr;
+  rc |= B.get(&d_totcool, npf, c->totalcooling);
+  rc |= B.get(&d_ccion, npi, c->cooling_contrib_ion);
+  rc |= B.get(&d_rates, npf * ARTIS_TE_NRATES, (const double *)c->heatingcoolingrates);
+  if (rc) return ARTIS_ERR_HIP;
+  if (R.nt_on) HIPCHK(hipMemcpyAsync(N.ntY, c->nt_ionization_ratecoeff, npi * sizeof(double), hipMemcpyHostToDevice, G.stream));
+  if (!c->heatingcoolingrates) HIPCHK(hipMemsetAsync(d_rates, 0, npf * ARTIS_TE_NRATES * sizeof(double), G.stream));
+  HIPCHK(hipMemsetAsync(N.fail, 0, 2 * sizeof(int32_t), G.stream));
+  HIPCHK(hipMemsetAsync(N.ffheat, 0, npf * sizeof(double), G.stream));
+  HIPCHK(hipMemsetAsync(N.hdep, 0, npf * sizeof(double), G.stream));
+  // the solver's context: the cell-state pointers at the solver's arrays, the active cells as the "non-empty" list
+  Ctx KN = G.K;
+  KN.R.nts = p->nts;
+  KN.C.Te = N.Te;
+  KN.C.TR = N.TR;
+  KN.C.TJ = N.TJ;
+  KN.C.W = N.W;
+  KN.C.nne = N.nne;
+  KN.C.nnetot = N.nnetot;
+  KN.C.rho = N.rho;
+  KN.C.thick = N.thick;
+  KN.C.elem_abundance = N.abund;
+  KN.C.groundlevelpop = N.gp;
+  KN.C.partfunct = N.pf;
+  KN.C.nlte_pops = N.nlte;
+  KN.C.rf_TR = N.binTR;
+  KN.C.rf_W = N.binW;
+  KN.C.bfrate_est = N.bfrate;
+  KN.C.nt_dep = N.dep;
+  KN.C.nt_Y = N.ntY;
+  KN.C.nt_prob = N.nt_prob;
+  KN.C.nt_ionen = N.nt_ionen;
+  const int nact_max = std::max(1, nnl);
+  int32_t *d_act = nullptr, *d_actk = nullptr, *d_lte = nullptr, *d_nl = nullptr;
+  double *d_pops = nullptr, *d_corr = nullptr, *d_depr = nullptr, *d_hbc = nullptr;
+  rc |= B.get(&d_act, (size_t)nact_max, (const int32_t *)nullptr);
+  rc |= B.get(&d_actk, (size_t)nact_max, (const int32_t *)nullptr);
+  rc |= B.get(&d_lte, std::max<size_t>(1, lte_list.size()), lte_list.empty() ? nullptr : lte_list.data());
+  rc |= B.get(&d_nl, (size_t)nact_max, nl_list.empty() ? nullptr : nl_list.data());
+  rc |= B.get(&d_pops, (size_t)nact_max * nl, (const double *)nullptr);
+  rc |= B.get(&d_corr, (size_t)nact_max * (ntg + 1), (const double *)nullptr);
+  rc |= B.get(&d_depr, (size_t)nact_max * std::max(1, nbf), (const double *)nullptr);
+  rc |= B.get(&d_hbc, std::max<size_t>(1, hb.size()) * nact_max, (const double *)nullptr);
+  if (rc) return ARTIS_ERR_HIP;
+  KN.C.pops = d_pops;
+  KN.C.corrphot = d_corr;
+  KN.C.depratio = d_depr;
+  KN.C.ne_mgi = d_act;
+  KN.C.n_nonempty = 0;
+  // the thermal-balance solver's view (te_solver.h) of the same state
+  TeDev D{};
+  rc |= B.get((int32_t **)&D.anumber, (size_t)ne, G.h_anumber.data());
+  rc |= B.get((int32_t **)&D.hb_ul, std::max<size_t>(1, hb.size()), hb.empty() ? nullptr : hb.data());
+  rc |= B.get(&D.upp, npe, (const int32_t *)nullptr);
+  if (rc) return ARTIS_ERR_HIP;
+  D.nhb = (int32_t)hb.size();
+  D.t_current = p->t_current_te;
+  D.tmin = p->tmin;
+  D.T_min = p->T_min;
+  D.T_max = p->T_max;
+  D.accuracy = p->accuracy;
+  D.initial_iteration = p->initial_iteration;
+  D.TR = N.TR;
+  D.W = N.W;
+  D.TJ = N.TJ;
+  D.rho = N.rho;
+  D.abund = N.abund;
+  D.meanw = N.meanw;
+  D.thick = N.thick;
+  D.vol = N.vol;
+  D.ffheat = N.ffheat;
+  D.hdep = N.hdep;
+  D.Te = N.Te;
+  D.gp = N.gp;
+  D.nne = N.nne;
+  D.nnetot = N.nnetot;
+  D.pf = N.pf;
+  D.totcool = d_totcool;
+  D.ccion = d_ccion;
+  D.rates = d_rates;
+  D.hbc = d_hbc;
+  D.fail = N.fail;
+  D.direct_col_heat = 1;
+  D.nlte = N.nlte;
+  D.hbstride = nact_max;
+  Ctx *dK = nullptr;
+  TeDev *dD = nullptr;
+  NlDev *dN = nullptr;
+  if (B.get(&dK, 1, &KN) || B.get(&dD, 1, (const TeDev *)nullptr) || B.get(&dN, 1, &N)) return ARTIS_ERR_HIP;
+  int g = 1;
+  while (g < ni && g < 64) g *= 2;
+  const int cpw = 64 / g;
+  auto te_launch = [&](const int32_t *list, int n, int mode, const int32_t *hbk) -> int {
+    if (n <= 0) return 0;
+    D.mgi = list;
+    D.ncells = n;
+    D.mode = mode;
+    D.hbk = hbk;
+    HIPCHK(hipStreamSynchronize(G.stream));  // dD is read by the previous launch
+    HIPCHK(hipMemcpy(dD, &D, sizeof(TeDev), hipMemcpyHostToDevice));
+    k_te_solve<<<(unsigned)((n + cpw - 1) / cpw), 64, (size_t)cpw * ni * sizeof(double), G.stream>>>(dK, dD, g);
+    HIPCHK(hipGetLastError());
+    return 0;
+  };
+  auto read_fail = [&](const char *where) -> int {
+    int32_t f[2] = {0, 0};
+    HIPCHK(hipStreamSynchronize(G.stream));
+    HIPCHK(hipMemcpy(f, N.fail, sizeof f, hipMemcpyDeviceToHost));
+    if (!f[0]) return 0;
+    static const char *why[] = {"a GSL root-finder error of call_T_e_finder / calculate_populations",
+                                "a GSL root-finder error of the radiation-field bin fit (find_T_R)",
+                                "a non-finite bf-heating coefficient",
+                                "get_mean_binding_energy has no shell data for the work-function approximation",
+                                "non-finite or negative NLTE populations", "the T_e finder"};
+    char buf[320];
+    snprintf(buf, sizeof buf, "update_grid_nlte (%s): %s in model cell %d -- the reference aborts here", where,
+             why[(f[1] >= 0 && f[1] <= 5) ? f[1] : 0], f[0] - 1);
+    G.last_error = buf;
+    return ARTIS_ERR_PACKET_FAULT;
+  };
+  // ARTIS_GPU_NL_DEBUG=1: synchronise after every step and name the first one that fails
+  const bool nl_debug = getenv("ARTIS_GPU_NL_DEBUG") && getenv("ARTIS_GPU_NL_DEBUG")[0] == '1';
+  auto step = [&](const char *what) -> int {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && nl_debug) e = hipStreamSynchronize(G.stream);
+    if (e != hipSuccess) {
+      G.last_error = std::string("update_grid_nlte: ") + what + ": " + hipGetErrorString(e);
+      return ARTIS_ERR_HIP;
+    }
+    return 0;
+  };
+#define NLSTEP(what)                  \
+  do {                                \
+    if (int e_ = step(what)) return e_; \
+  } while (0)
+  NLSTEP("uploads");
+  const int TB = 256;
+  k_nl_prepare<<<(c->ncells + TB - 1) / TB, TB, 0, G.stream>>>(N);
+  NLSTEP("k_nl_prepare");
+  // LTE-branch cells: precalculate_partfuncts + calculate_populations (LTE phi) + the cooling rates
+  if (int e2 = te_launch(d_lte, (int)lte_list.size(), 0, nullptr)) return e2;
+  NLSTEP("k_te_solve (LTE branch)");
+  // Spencer-Fano tables
+  SfDev S{};
+  std::vector<int32_t> h_solve;
+  if (sf_on && nnl > 0) {
+    const int n = nt->sfpts;
+    S.n = n;
+    S.emin = nt->sf_emin;
+    S.emax = nt->sf_emax;
+    S.DE = (S.emax - S.emin) / (n - 1);
+    std::vector<double> envec(n), logenvec(n), sourcevec(n), pw2(n), rhs(n, 0.);
+    const int source_spread_pts = (int)ceil(n * 0.03333);
+    const double source_spread_en = source_spread_pts * S.DE;
+    const int sourcelowerindex = n - source_spread_pts;
+    for (int k = 0; k < n; k++) {
+      envec[k] = S.emin + k * S.DE;
+      logenvec[k] = log(envec[k]);
+      sourcevec[k] = (k < sourcelowerindex) ? 0. : 1. / source_spread_en;
+      pw2[k] = pow(envec[k] * ARTIS_EV, -2);
+    }
+    double E = 0.;
+    for (int k = 0; k < n; k++) E += fabs((sourcevec[k] * S.DE) * envec[k]);
+    S.E_init_ev = E;
+    for (int i = 0; i < n - 1; i++) {
+      double dasum = 0.;
+      for (int j = i + 1; j < n; j++) dasum += fabs(sourcevec[j]);
+      rhs[i] = dasum * S.DE;
+    }
+    auto gteq = [&](double en) {
+      const int index = (int)ceil((en - S.emin) / S.DE);
+      return index < 0 ? 0 : (index > n - 1 ? n - 1 : index);
+    };
+    // shells (collion.txt entries of each ion) and their tables
+    std::vector<int32_t> sh_off(ni + 1, 0), sh_k, sh_start, sh_astop;
+    std::vector<double> sh_ip, sh_J, sh_xs, sh_ieu, sh_atn, sh_ie2, sh_prob;
+    std::vector<int32_t> tr_off(ni + 1, 0), tr_ul, tr_kind, tr_start, tr_build;
+    std::vector<double> tr_cf, tr_logeps, tr_eps_ev, tr_eps, binding(ni, 0.);
+    std::vector<int32_t> binding_ok(ni, 0);
+    std::vector<int32_t> line_upper;
+    std::vector<float> line_coll, line_f;
+    std::vector<uint8_t> line_forb;
+    std::vector<int32_t> upidx;
+    const int64_t nup = lev_upoff.empty() ? 0 : (int64_t)lev_upoff[nl - 1] + lev_nup[nl - 1];
+    if (d2h_vec(line_upper, T.line_upper, T.nlines) || d2h_vec(line_coll, T.line_coll, T.nlines) ||
+        d2h_vec(line_f, T.line_f, T.nlines) || d2h_vec(line_forb, T.line_forbidden, T.nlines) ||
+        d2h_vec(upidx, T.uptrans_lineindex, (size_t)std::max<int64_t>(nup, 0)))
+      return ARTIS_ERR_HIP;
+    int band = 1;
+    for (int e = 0; e < ne; e++)
+      for (int i = 0; i < nions[e]; i++) {
+        const int u = uoff[e] + i;
+        const int Z = G.h_anumber[e];
+        const int ist = ionstage[u];
+        for (int k = 0; k < nt->nshells; k++) {
+          if (!(nt->Z[k] == Z && nt->nelec[k] == Z - ist + 1)) continue;
+          const double ionpot_ev = nt->ionpot_ev[k];
+          const double J = sf_get_J_host(Z, ist, ionpot_ev);
+          const int xsstart = gteq(ionpot_ev);
+          sh_k.push_back(k);
+          sh_ip.push_back(ionpot_ev);
+          sh_J.push_back(J);
+          sh_start.push_back(xsstart);
+          sh_astop.push_back(gteq((double)nt->en_auger_ev[k]));
+          for (int q = 0; q < NL_A1; q++) sh_prob.push_back(nt->prob_num_auger[k * NL_A1 + q]);
+          const double A = nt->A[k], Bc = nt->B[k], Cc = nt->C[k], Dc = nt->D[k];
+          for (int j = 0; j < n; j++) {  // nonthermal.cc:952-976, 2370-2380
+            double xs = 0., ieu = 0., atn = 0.;
+            if (j >= xsstart) {
+              const double uu = envec[j] / ionpot_ev;
+              xs = 1e-14 * (A * (1 - 1 / uu) + Bc * pow((1 - 1 / uu), 2) + Cc * log(uu) + Dc * log(uu) / uu) /
+                   (uu * pow(ionpot_ev, 2));
+              const double endash = envec[j];
+              const double epsilon_upper = std::min((endash + ionpot_ev) / 2, endash);
+              ieu = atan((epsilon_upper - ionpot_ev) / J);
+              atn = atan((endash - ionpot_ev) / 2 / J);
+            }
+            sh_xs.push_back(xs);
+            sh_ieu.push_back(ieu);
+            sh_atn.push_back(atn);
+            sh_ie2.push_back(atan(envec[j] / J));
+          }
+        }
+        sh_off[u + 1] = (int32_t)sh_k.size();
+        // excitation transitions (nonthermal.cc:2282-2341, 872-929)
+        const int nlev5 = std::min(ion_nlev[u], 5);
+        for (int lower = 0; lower < nlev5; lower++) {
+          const int ul = ion_ul0[u] + lower;
+          const double statweight_lower = lev_g[ul];
+          for (int t = 0; t < lev_nup[ul]; t++) {
+            const int li = upidx[lev_upoff[ul] + t];
+            const int upper = line_upper[li];
+            if (upper >= 250) continue;
+            const double epsilon_trans = lev_eps[ion_ul0[u] + upper] - lev_eps[ul];
+            const double eps_ev = epsilon_trans / ARTIS_EV;
+            const double coll_str = line_coll[li];
+            int kind;
+            double cf, logeps = 0.;
+            if (coll_str >= 0) {
+              kind = 0;
+              cf = pow(ARTIS_H_IONPOT, 2) / statweight_lower * coll_str * ARTIS_PI * 2.800285203e-17;
+            } else if (!line_forb[li]) {
+              kind = 1;
+              const double fij = line_f[li];
+              cf = eps_ev * 45.585750051 * 2.800285203e-17 * pow(ARTIS_H_IONPOT / epsilon_trans, 2) * fij;
+              logeps = log(eps_ev);
+            } else {
+              continue;
+            }
+            tr_ul.push_back(ul);
+            tr_kind.push_back(kind);
+            tr_start.push_back(gteq(eps_ev));
+            tr_build.push_back(!(eps_ev < S.emin));
+            tr_cf.push_back(cf);
+            tr_logeps.push_back(logeps);
+            tr_eps_ev.push_back(eps_ev);
+            tr_eps.push_back(epsilon_trans);
+            if (!(eps_ev < S.emin)) band = std::max(band, (int)ceil(eps_ev / S.DE) + 2);
+          }
+        }
+        tr_off[u + 1] = (int32_t)tr_ul.size();
+        double bnd = 0.;
+        binding_ok[u] = sf_mean_binding_energy_host(nt, Z, ist - 1, G.h_ion_ionpot[u], &bnd) ? 1 : 0;
+        binding[u] = bnd;
+      }
+    S.band = band;
+    S.nsh = (int32_t)sh_k.size();
+    S.nitems = S.nsh + (int32_t)tr_ul.size();
+    auto up = [&](auto **d, const auto &v) {
+      using Tv = typename std::remove_reference<decltype(v)>::type::value_type;
+      return B.get((Tv **)d, std::max<size_t>(1, v.size()), v.empty() ? nullptr : v.data());
+    };
+    rc |= up(&S.envec, envec);
+    rc |= up(&S.logenvec, logenvec);
+    rc |= up(&S.pw2, pw2);
+    rc |= up(&S.rhs, rhs);
+    rc |= up(&S.ion_sh_off, sh_off);
+    rc |= up(&S.sh_k, sh_k);
+    rc |= up(&S.sh_xsstart, sh_start);
+    rc |= up(&S.sh_augerstop, sh_astop);
+    rc |= up(&S.sh_ionpot_ev, sh_ip);
+    rc |= up(&S.sh_J, sh_J);
+    rc |= up(&S.sh_xs, sh_xs);
+    rc |= up(&S.sh_ieu, sh_ieu);
+    rc |= up(&S.sh_atn, sh_atn);
+    rc |= up(&S.sh_ie2, sh_ie2);
+    rc |= up(&S.sh_prob, sh_prob);
+    rc |= up(&S.ion_tr_off, tr_off);
+    rc |= up(&S.tr_ul, tr_ul);
+    rc |= up(&S.tr_kind, tr_kind);
+    rc |= up(&S.tr_start, tr_start);
+    rc |= up(&S.tr_build, tr_build);
+    rc |= up(&S.tr_cf, tr_cf);
+    rc |= up(&S.tr_logeps, tr_logeps);
+    rc |= up(&S.tr_eps_ev, tr_eps_ev);
+    rc |= up(&S.tr_eps, tr_eps);
+    rc |= up(&S.ion_binding, binding);
+    rc |= up(&S.ion_binding_ok, binding_ok);
+    S.anumber = D.anumber;
+    rc |= B.get(&S.nnion, (size_t)ni, (const double *)nullptr);
+    rc |= B.get(&S.incl, (size_t)ni, (const int32_t *)nullptr);
+    rc |= B.get(&S.tot_nion, 1, (const double *)nullptr);
+    rc |= B.get(&S.MT, (size_t)n * n, (const double *)nullptr);
+    rc |= B.get(&S.x, (size_t)n, (const double *)nullptr);
+    rc |= B.get(&S.best, (size_t)n, (const double *)nullptr);
+    rc |= B.get(&S.work, (size_t)n, (const double *)nullptr);
+    rc |= B.get(&S.res, (size_t)n, (const double *)nullptr);
+    rc |= B.get(&S.errbest, 1, (const double *)nullptr);
+    rc |= B.get(&S.dots, (size_t)std::max(1, S.nitems), (const double *)nullptr);
+    rc |= B.get(&S.solve, (size_t)nact_max, (const int32_t *)nullptr);
+    if (rc) return ARTIS_ERR_HIP;
+  } else if (R.nt_on) {
+    // the binding energies the work-function fallback of nt_ionization_ratecoeff reads
+    std::vector<double> binding(ni, 0.);
+    std::vector<int32_t> binding_ok(ni, 0);
+    if (nt && nt->electron_binding)
+      for (int e = 0; e < ne; e++)
+        for (int i = 0; i < nions[e]; i++) {
+          const int u = uoff[e] + i;
+          double bnd = 0.;
+          binding_ok[u] = sf_mean_binding_energy_host(nt, G.h_anumber[e], ionstage[u] - 1, G.h_ion_ionpot[u], &bnd);
+          binding[u] = bnd;
+        }
+    rc |= B.get((double **)&S.ion_binding, (size_t)ni, binding.data());
+    rc |= B.get((int32_t **)&S.ion_binding_ok, (size_t)ni, binding_ok.data());
+    S.anumber = D.anumber;
+    if (rc) return ARTIS_ERR_HIP;
+  }
+  // the rate-matrix layout: per element D = sum over ions of nlevels_nlte + 1 (+ 1 with a superlevel)
+  NlMat M{};
+  std::vector<int32_t> el_D(ne, 0), el_off1(ne, 0), col_e, col_ion, col_l0, col_l1;
+  std::vector<int64_t> el_off2(ne, 0);
+  int64_t cell2 = 0;
+  int cell1 = 0;
+  for (int e = 0; e < ne; e++) {
+    el_off1[e] = cell1;
+    el_off2[e] = cell2;
+    int Dm = 0;
+    for (int i = 0; i < nions[e]; i++) {
+      const int u = uoff[e] + i;
+      const int nn = nlte_n[u];
+      for (int l = 0; l <= nn && l < ion_nlev[u]; l++) {
+        col_e.push_back(e);
+        col_ion.push_back(i);
+        col_l0.push_back(l);
+        col_l1.push_back(l);
+      }
+      Dm += nn + 1;
+      if (ion_nlev[u] > nn + 1) {
+        col_e.push_back(e);
+        col_ion.push_back(i);
+        col_l0.push_back(nn + 1);
+        col_l1.push_back(ion_nlev[u] - 1);
+        Dm += 1;
+      }
+    }
+    el_D[e] = Dm;
+    cell1 += Dm;
+    cell2 += (int64_t)Dm * Dm;
+  }
+  if ((int)col_e.size() != cell1) {
+    G.last_error = "update_grid_nlte: an ion with fewer levels than nlevels_nlte + 1";
+    return ARTIS_ERR_UNSUPPORTED;
+  }
+  M.cell1 = cell1;
+  M.cell2 = cell2;
+  M.t_mid = p->t_mid;
+  const double per_cell = (7.0 * cell2 + 8.0 * cell1) * 8.0 + 4.0 * (cell1 + ne);
+  const int chunk = std::max(1, std::min(nact_max, (int)std::min(1e9, (double)(1ll << 30) / per_cell)));
+  rc |= B.get((int32_t **)&M.el_D, (size_t)ne, el_D.data());
+  rc |= B.get((int32_t **)&M.el_off1, (size_t)ne, el_off1.data());
+  rc |= B.get((int64_t **)&M.el_off2, (size_t)ne, el_off2.data());
+  rc |= B.get((int32_t **)&M.col_e, std::max<size_t>(1, col_e.size()), col_e.data());
+  rc |= B.get((int32_t **)&M.col_ion, std::max<size_t>(1, col_ion.size()), col_ion.data());
+  rc |= B.get((int32_t **)&M.col_l0, std::max<size_t>(1, col_l0.size()), col_l0.data());
+  rc |= B.get((int32_t **)&M.col_l1, std::max<size_t>(1, col_l1.size()), col_l1.data());
+  rc |= B.get(&M.A, (size_t)chunk * std::max<int64_t>(1, cell2), (const double *)nullptr);
+  rc |= B.get(&M.LU, (size_t)chunk * std::max<int64_t>(1, cell2), (const double *)nullptr);
+  rc |= B.get(&M.P, (size_t)chunk * 5 * std::max<int64_t>(1, cell2), (const double *)nullptr);
+  for (double **v : {&M.b, &M.norm, &M.pv, &M.xv, &M.best, &M.work, &M.res})
+    rc |= B.get(v, (size_t)chunk * std::max(1, cell1), (const double *)nullptr);
+  rc |= B.get(&M.perm, (size_t)chunk * std::max(1, cell1), (const int32_t *)nullptr);
+  rc |= B.get(&M.status, (size_t)chunk * ne, (const int32_t *)nullptr);
+  rc |= B.get(&M.slpf, (size_t)nact_max * ni, (const double *)nullptr);
+  rc |= B.get(&M.done, (size_t)nact_max, (const int32_t *)nullptr);
+  // the integration workspace (the engine's, or one of its own)
+  QagWs ws = G.qag;
+  int qwaves = G.qag_waves;
+  if (qwaves <= 0) {
+    qwaves = 64;
+    const size_t nw = (size_t)qwaves * QAG_LIMIT;
+    rc |= B.get(&ws.alist, nw, (const double *)nullptr);
+    rc |= B.get(&ws.blist, nw, (const double *)nullptr);
+    rc |= B.get(&ws.rlist, nw, (const double *)nullptr);
+    rc |= B.get(&ws.elist, nw, (const double *)nullptr);
+    rc |= B.get(&ws.order, nw, (const int32_t *)nullptr);
+    rc |= B.get(&ws.level, nw, (const int32_t *)nullptr);
+  }
+  if (rc) return ARTIS_ERR_HIP;
+  std::vector<int32_t> h_iters(c->ncells, 0);
+  if (nnl > 0) {
+    // radiation-field fit and bf-heating coefficients of the iterated cells
+    if (nbf > 0 && R.detailed_bf)
+      k_nl_bfnorm<<<(unsigned)(((int64_t)nnl * nbf + TB - 1) / TB), TB, 0, G.stream>>>(KN, N, d_nl, nnl);
+    NLSTEP("k_nl_bfnorm");
+    if (nbins > 0)
+      k_nl_binfit<<<(unsigned)std::min<int64_t>((int64_t)nnl * nbins, qwaves), 64, 0, G.stream>>>(dK, dN, d_nl, nnl, ws);
+    NLSTEP("k_nl_binfit");
+    if (!hb.empty())
+      k_nl_bfheat<<<(unsigned)std::min<int64_t>((int64_t)nnl * hb.size(), qwaves), 64, 0, G.stream>>>(
+          dK, dN, d_nl, nnl, D.hb_ul, (int)hb.size(), d_hbc, ws);
+    NLSTEP("k_nl_bfheat");
+    if (int e2 = read_fail("radiation field / bf heating")) return e2;
+    D.hbstride = nnl;
+    // solve_Te_nltepops passes for the cells still iterating
+    std::vector<int32_t> act = nl_list, actk(nnl);
+    for (int k = 0; k < nnl; k++) actk[k] = k;
+    std::map<int, int> k_of_mgi;
+    for (int k = 0; k < c->ncells; k++) k_of_mgi[c->mgi[k]] = k;
+    for (int iter = 0; iter <= p->nlteiter && !act.empty(); iter++) {
+      const int nact = (int)act.size();
+      HIPCHK(hipMemcpyAsync(d_act, act.data(), nact * sizeof(int32_t), hipMemcpyHostToDevice, G.stream));
+      HIPCHK(hipMemcpyAsync(d_actk, actk.data(), nact * sizeof(int32_t), hipMemcpyHostToDevice, G.stream));
+      KN.C.n_nonempty = nact;
+      const int64_t nlv = (int64_t)nact * nl;
+      if (sf_on) {
+        k_levelpops<<<(unsigned)((nlv + TB - 1) / TB), TB, 0, G.stream>>>(KN);
+        NLSTEP("k_levelpops (Spencer-Fano)");
+        k_sf_decide<<<(nact + TB - 1) / TB, TB, 0, G.stream>>>(KN, N, S, d_act, nact);
+        NLSTEP("k_sf_decide");
+        HIPCHK(hipStreamSynchronize(G.stream));
+        if (d2h_vec(h_solve, S.solve, nact)) return ARTIS_ERR_HIP;
+        const int n = S.n;
+        for (int a = 0; a < nact; a++) {
+          if (!h_solve[a]) continue;
+          const int mgi = act[a];
+          const double *cpops = d_pops + (int64_t)a * nl;
+          k_sf_ions<<<(ni + 63) / 64, 64, 0, G.stream>>>(KN, N, S, mgi);
+          NLSTEP("k_sf_ions");
+          k_sf_matrix<<<dim3((unsigned)((n + 255) / 256), (unsigned)n), 256, 0, G.stream>>>(KN, N, S, mgi, cpops);
+          NLSTEP("k_sf_matrix");
+          HIPCHK(hipMemcpyAsync(S.x, S.rhs, n * sizeof(double), hipMemcpyDeviceToDevice, G.stream));
+          k_sf_backsub<<<1, SF_WG, 0, G.stream>>>(S.MT, n, S.x);
+          NLSTEP("k_sf_backsub");
+          static const double none_yet = -1.;
+          HIPCHK(hipMemcpyAsync(S.errbest, &none_yet, sizeof(double), hipMemcpyHostToDevice, G.stream));
+          for (int it = 0; it < 10; it++) {
+            if (it > 0) {
+              k_sf_residual<<<(n + 255) / 256, 256, 0, G.stream>>>(S.MT, n, S.x, S.rhs, S.work);
+              k_sf_backsub<<<1, SF_WG, 0, G.stream>>>(S.MT, n, S.work);
+              k_sf_axpy<<<(n + 255) / 256, 256, 0, G.stream>>>(n, S.x, S.work);
+            }
+            k_sf_residual<<<(n + 255) / 256, 256, 0, G.stream>>>(S.MT, n, S.x, S.rhs, S.res);
+            k_sf_best<<<1, 1024, 0, G.stream>>>(n, S.res, S.x, S.best, S.errbest);
+            NLSTEP("Spencer-Fano refinement");
+          }
+          k_sf_dots<<<(S.nitems + 63) / 64, 64, 0, G.stream>>>(S, S.best);
+          NLSTEP("k_sf_dots");
+          k_sf_combine<<<1, 64, 0, G.stream>>>(KN, N, S, mgi, cpops);
+          NLSTEP("k_sf_combine");
+        }
+      }
+      k_nl_ntrates<<<(nact + TB - 1) / TB, TB, 0, G.stream>>>(KN, N, S, d_act, nact);
+      NLSTEP("k_nl_ntrates");
+      if (int e2 = te_launch(d_act, nact, 1, d_actk)) return e2;
+      NLSTEP("k_te_solve (call_T_e_finder)");
+      if (int e2 = read_fail("call_T_e_finder")) return e2;
+      // populations and corrected photoionisation coefficients at the new T_e; the rate matrices
+      k_levelpops<<<(unsigned)((nlv + TB - 1) / TB), TB, 0, G.stream>>>(KN);
+      NLSTEP("k_levelpops");
+      const int64_t nbt = (int64_t)nact * (nbf + ntg);
+      if (nbt > 0) k_bfcells<<<(unsigned)((nbt + TB - 1) / TB), TB, 0, G.stream>>>(KN, G.d_target_ul, G.d_target_t);
+      NLSTEP("k_bfcells");
+      if (ntg > 0)
+        k_corrphot_integral<<<(unsigned)std::min<int64_t>((int64_t)nact * ntg, qwaves), 64, 0, G.stream>>>(
+            KN, G.d_target_ul, G.d_target_t, ws);
+      NLSTEP("k_corrphot_integral");
+      k_nl_slpf<<<(unsigned)(((int64_t)nact * ni + TB - 1) / TB), TB, 0, G.stream>>>(KN, N, M, d_act, nact);
+      NLSTEP("k_nl_slpf");
+      for (int a0 = 0; a0 < nact; a0 += chunk) {
+        const int nch = std::min(chunk, nact - a0);
+        if (cell1 > 0) {
+          k_nl_matrix<<<(unsigned)(((int64_t)nch * cell1 + 63) / 64), 64, 0, G.stream>>>(KN, N, M, d_act, a0, nch);
+          NLSTEP("k_nl_matrix");
+          k_nl_lu<<<(unsigned)(nch * ne), NL_LU_WG, 0, G.stream>>>(KN, M, nch);
+          NLSTEP("k_nl_lu");
+          if (iter == 0 && a0 == 0 && getenv("ARTIS_GPU_NL_DUMP")) {
+            // diagnostics: the first pass's rate matrices of the first active cell (tools/nl_dump_cmp.py)
+            HIPCHK(hipStreamSynchronize(G.stream));
+            std::vector<double> hA, hb, hn, hp, hpops, hcorr;
+            std::vector<int32_t> hs;
+            if (d2h_vec(hA, M.A, (size_t)cell2) || d2h_vec(hb, M.b, (size_t)cell1) || d2h_vec(hn, M.norm, (size_t)cell1) ||
+                d2h_vec(hp, M.pv, (size_t)cell1) || d2h_vec(hs, M.status, (size_t)ne) || d2h_vec(hpops, d_pops, (size_t)nl) ||
+                d2h_vec(hcorr, d_corr, (size_t)ntg))
+              return ARTIS_ERR_HIP;
+            const std::string path = std::string(getenv("ARTIS_GPU_NL_DUMP")) + "_gpu.bin";
+            if (FILE *fp = fopen(path.c_str(), "wb")) {
+              const int32_t hdr[5] = {ne, cell1, (int32_t)cell2, nl, (int32_t)ntg};
+              fwrite(hdr, sizeof hdr, 1, fp);
+              fwrite(el_D.data(), 4, ne, fp);
+              fwrite(hs.data(), 4, ne, fp);
+              fwrite(hA.data(), 8, hA.size(), fp);
+              fwrite(hb.data(), 8, hb.size(), fp);
+              fwrite(hn.data(), 8, hn.size(), fp);
+              fwrite(hp.data(), 8, hp.size(), fp);
+              fwrite(hpops.data(), 8, hpops.size(), fp);
+              fwrite(hcorr.data(), 8, hcorr.size(), fp);
+              fclose(fp);
+            }
+          }
+        }
+        k_nl_store<<<(nch + 63) / 64, 64, 0, G.stream>>>(dK, dD, N, M, d_act, a0, nch);
+        NLSTEP("k_nl_store");
+      }
+      if (int e2 = read_fail("solve_nlte_pops_element")) return e2;
+      std::vector<int32_t> done;
+      if (d2h_vec(done, M.done, nact)) return ARTIS_ERR_HIP;
+      std::vector<int32_t> act2, actk2;
+      for (int a = 0; a < nact; a++) {
+        h_iters[k_of_mgi[act[a]]] = iter + 1;
+        if (!done[a]) {
+          act2.push_back(act[a]);
+          actk2.push_back(actk[a]);
+        }
+      }
+      act.swap(act2);
+      actk.swap(actk2);
+    }
+  }
+  // nt_ionization_ratecoeff of every listed cell, the cooling rates of the iterated ones
+  if (R.nt_on) {
+    k_nl_ntrates<<<(c->ncells + TB - 1) / TB, TB, 0, G.stream>>>(KN, N, S, N.mgi, c->ncells);
+    HIPCHK(hipGetLastError());
+  }
+  NLSTEP("k_nl_ntrates (final)");
+  if (int e2 = te_launch(d_nl, nnl, 2, nullptr)) return e2;
+  NLSTEP("k_te_solve (cooling)");
+#undef NLSTEP
+  HIPCHK(hipEventRecord(G.ev1, G.stream));
+  HIPCHK(hipEventSynchronize(G.ev1));
+  {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, G.ev2, G.ev1));
+    G.last_nlte_ms = ms;
+  }
+  if (int e2 = read_fail("update_grid_nlte")) return e2;
+  // success: every array back to the caller
+  HIPCHK(hipMemcpy(c->TR, N.TR, npf * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c->W, N.W, npf * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c->TJ, N.TJ, npf * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c->Te, N.Te, npf * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c->nne, N.nne, npf * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c->nnetot, N.nnetot, npf * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c->groundlevelpop, N.gp, npi * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c->partfunct, N.pf, npi * sizeof(float), hipMemcpyDeviceToHost));
+  if (ntl > 0) HIPCHK(hipMemcpy(c->nlte_pops, N.nlte, (size_t)np * ntl * sizeof(double), hipMemcpyDeviceToHost));
+  if (nbins > 0) {
+    HIPCHK(hipMemcpy(c->bin_TR, N.binTR, (size_t)np * nbins * sizeof(float), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(c->bin_W, N.binW, (size_t)np * nbins * sizeof(float), hipMemcpyDeviceToHost));
+  }
+  if (R.detailed_bf && nbf > 0)
+    HIPCHK(hipMemcpy(c->bfrate_estimator, N.bfrate, (size_t)np * nbf * sizeof(float), hipMemcpyDeviceToHost));
+  if (R.nt_on) {
+    HIPCHK(hipMemcpy(c->nt_frac_heating, N.nt_fh, npf * sizeof(float), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(c->nt_frac_ionization, N.nt_fi, npf * sizeof(float), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(c->nt_frac_excitation, N.nt_fe, npf * sizeof(float), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(c->nt_nneperion_when_solved, N.nt_nneper, npf * sizeof(float), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(c->nt_timestep_last_solved, N.nt_tls, npf * sizeof(int32_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(c->nt_eff_ionpot, N.nt_effion, npi * sizeof(float), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(c->nt_fracdep_ionization_ion, N.nt_fracdep, npi * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(c->nt_prob_num_auger, N.nt_prob, npi * A1 * sizeof(float), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(c->nt_ionenfrac_num_auger, N.nt_ionen, npi * A1 * sizeof(float), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(c->nt_ionization_ratecoeff, N.ntY, npi * sizeof(double), hipMemcpyDeviceToHost));
+  }
+  HIPCHK(hipMemcpy(c->totalcooling, d_totcool, npf * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(c->cooling_contrib_ion, d_ccion, npi * sizeof(double), hipMemcpyDeviceToHost));
+  if (c->heatingcoolingrates)
+    HIPCHK(hipMemcpy(c->heatingcoolingrates, d_rates, npf * ARTIS_TE_NRATES * sizeof(double), hipMemcpyDeviceToHost));
+  if (c->nlte_iterations)
+    for (int k = 0; k < c->ncells; k++) c->nlte_iterations[c->mgi[k]] = h_iters[k];
+  return 0;
+}
+double artis_gpu_last_nlte_ms(void) { return G.last_nlte_ms; }
 
 int artis_gpu_abi_version(void) { return ARTIS_GPU_ABI_VERSION; }
 const char *artis_gpu_last_error(void) { return G.last_error.c_str(); }
@@ -1569,6 +2382,8 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   G.params = *rp;
   G.h_anumber.assign(a->nelements, 0);
   if (a->elem_anumber) G.h_anumber.assign(a->elem_anumber, a->elem_anumber + a->nelements);
+  G.h_ion_ionpot.assign(a->nions_total, 0.);
+  if (a->ion_ionpot) G.h_ion_ionpot.assign(a->ion_ionpot, a->ion_ionpot + a->nions_total);
   DevTab &T = G.K.T;
   T.nelements = a->nelements;
   T.maxnions = a->maxnions;

@@ -40,6 +40,17 @@ struct TeDev {
   int32_t *upp;
   double *hbc;
   int32_t *fail;  // first failing cell (mgi + 1): the reference's GSL abort paths
+  // DIRECT_COL_HEAT: the collisional heating is the de-excitation sum (thermalbalance.cc:189-238)
+  int32_t direct_col_heat;
+  // the nebular solution (nlte_solver.h): NLTE / superlevel populations by mgi (ltepop.cc:349-415; nullptr: LTE
+  // populations), and the mode of k_te_solve: 0 the full solution above, 1 only call_T_e_finder with
+  // calculate_electron_densities (NLTE_POPS_ALL_IONS_SIMULTANEOUS, thermalbalance.cc:357-361), 2 only the final
+  // calculate_cooling_rates
+  const double *nlte;
+  int32_t mode;
+  // row of a cell's bf-heating coefficients in hbc: hbk[k] (nullptr: k) of hbstride rows
+  const int32_t *hbk;
+  int32_t hbstride;
 };
 
 struct TeState {
@@ -59,10 +70,35 @@ DEVFN double te_get_gp(const Ctx &K, const TeDev &D, int mgi, int ui, int e) {
   }
   return nn;
 }
-// ltepop.cc:329-347, 349-415 (NLTE_POPS_ON false)
+// ltepop.cc:349-415 with NLTE_POPS_ON: an NLTE level's (or the superlevel's, nltepop.cc:1543-1554) stored population
+// when there is one (not < -0.9); returns false for the LTE expression
+DEVFN bool te_nlte_levelpop(const Ctx &K, const TeDev &D, const TeState &s, int ui, int l, double *nn) {
+  if (!D.nlte || l == 0) return false;
+  const int nn_nlte = K.T.ion_nlevels_nlte[ui];
+  const double *row = D.nlte + (int64_t)s.mgi * K.T.total_nlte_levels + K.T.ion_first_nlte[ui];
+  const double rho = D.rho[s.mgi];
+  if (l <= nn_nlte) {
+    const double v = row[l - 1];
+    if (v < -0.9) return false;
+    *nn = v * rho;
+    return true;
+  }
+  const double v = row[nn_nlte];
+  if (v < -0.9) return false;
+  const int ul0 = K.T.ion_uniqueleveloffset[ui];
+  const int sl = ul0 + nn_nlte + 1;
+  const double T_exc = K.R.exc_te ? (double)s.Te : (double)D.TJ[s.mgi];
+  const double boltz = (double)K.T.level_stat_weight[ul0 + l] / (double)K.T.level_stat_weight[sl] *
+                       exp(-(K.T.level_epsilon[ul0 + l] - K.T.level_epsilon[sl]) / ARTIS_KB / T_exc);
+  *nn = v * rho * boltz;
+  return true;
+}
+// ltepop.cc:329-347, 349-415
 DEVFN double te_levelpop_nominpop(const Ctx &K, const TeDev &D, const TeState &s, int e, int ui, int l) {
   const double nnground = te_get_gp(K, D, s.mgi, ui, e);
   if (l == 0) return nnground;
+  double nlte;
+  if (te_nlte_levelpop(K, D, s, ui, l, &nlte)) return nlte;
   const double T_exc = K.R.exc_te ? (double)s.Te : (double)D.TJ[s.mgi];
   const double W = 1.;
   const int ul0 = K.T.ion_uniqueleveloffset[ui];
@@ -73,7 +109,9 @@ DEVFN double te_levelpop_nominpop(const Ctx &K, const TeDev &D, const TeState &s
 }
 // ltepop.cc:417-430
 DEVFN double te_levelpop(const Ctx &K, const TeDev &D, const TeState &s, int e, int ui, int l) {
-  double nn = te_levelpop_nominpop(K, D, s, e, ui, l);
+  double nn;
+  if (te_nlte_levelpop(K, D, s, ui, l, &nn)) return nn;  // skipminpop
+  nn = te_levelpop_nominpop(K, D, s, e, ui, l);
   if (nn < K.R.minpop) nn = (D.abund[(int64_t)s.mgi * K.T.nelements + e] > 0) ? K.R.minpop : 0.;
   return nn;
 }
@@ -430,6 +468,21 @@ DEVNI int te_calculate_populations(const Ctx &K, const TeDev &D, const TeState &
   return 0;
 }
 
+// update_grid.cc:1660-1685 calculate_electron_densities: n_e from the ion-stage populations; returns nne_tot
+DEVNI double te_electron_densities(const Ctx &K, const TeDev &D, const TeState &s) {
+  double nne_tot = 0.;
+  float nne = 0.;
+  for (int e = 0; e < K.T.nelements; e++) {
+    const double nnelement = te_elem_numberdens(K, D, s.mgi, e);
+    nne_tot += nnelement * D.anumber[e];
+    if (nnelement > 0)
+      for (int i = 0; i < K.T.elem_nions[e]; i++) nne += (get_ionstage(K, e, i) - 1) * te_ionstagepop(K, D, s, e, uion(K, e, i));
+  }
+  D.nne[s.mgi] = nne;
+  D.nnetot[s.mgi] = nne_tot;
+  return nne_tot;
+}
+
 struct TeRates {
   double cooling_collisional, cooling_fb, cooling_ff, cooling_adiabatic, heating_collisional, heating_bf, heating_ff,
       heating_dep;
@@ -537,17 +590,56 @@ DEVNI void te_cooling_rates(const Ctx &K, const TeDev &D, const TeState &s, TeRa
     hc->cooling_ff = C_ff_all;
   }
 }
-// thermalbalance.cc:218-346 (DIRECT_COL_HEAT undefined)
+// thermalbalance.cc:189-216 get_heating_ion_coll_deexc (DIRECT_COL_HEAT)
+DEVNI double te_heating_ion_coll_deexc(const Ctx &K, const TeDev &D, const TeState &s, int ui, float T_e, float nne) {
+  const int e = K.T.ion_element[ui];
+  const int ul0 = K.T.ion_uniqueleveloffset[ui];
+  double C_deexc = 0.;
+  for (int level = 0; level < K.T.ion_nlevels[ui]; level++) {
+    const int ul = ul0 + level;
+    const int nd = K.T.level_ndowntrans[ul];
+    if (nd == 0) continue;
+    const double nnlevel = te_levelpop(K, D, s, e, ui, level);
+    const double epsilon_level = K.T.level_epsilon[ul];
+    const double statweight = K.T.level_stat_weight[ul];
+    for (int k = 0; k < nd; k++) {
+      const int li = K.T.downtrans_lineindex[K.T.level_downtrans_offset[ul] + k];
+      const int lower = K.T.line_lower[li];
+      const double epsilon_trans = epsilon_level - K.T.level_epsilon[ul0 + lower];
+      C_deexc += nnlevel *
+                 col_deexcitation_ratecoeff(K, T_e, nne, epsilon_trans, li, K.T.level_stat_weight[ul0 + lower], statweight) *
+                 epsilon_trans;
+    }
+  }
+  return C_deexc;
+}
+// thermalbalance.cc:218-346; the bf-heating sum over hb_ul (every element's ionising levels of its non-top ions)
 DEVNI void te_heating_rates(const Ctx &K, const TeDev &D, const TeState &s, TeRates *hc) {
   double bfheating = 0.;
+  const int64_t kk = D.hbk ? D.hbk[s.k] : s.k;
+  const int64_t stride = D.hbk ? D.hbstride : D.ncells;
   for (int j = 0; j < D.nhb; j++) {
     const int ul = D.hb_ul[j];
     const int ui = K.T.level_ui[ul];
     const int e = K.T.ion_element[ui];
     const double nnlevel = te_levelpop(K, D, s, e, ui, ul - K.T.ion_uniqueleveloffset[ui]);
-    bfheating += nnlevel * D.hbc[(int64_t)j * D.ncells + s.k];
+    bfheating += nnlevel * D.hbc[(int64_t)j * stride + kk];
   }
-  hc->heating_collisional = D.colheat[s.mgi];
+  if (D.direct_col_heat) {
+    // the ions' sums added in unique-ion order (the bf sum is separate, so the reference's per-element interleaving
+    // is immaterial); the cell's lanes split the ions as in te_cooling_rates
+    double C_deexc = 0.;
+    const int ni = K.T.nions_total;
+    for (int ub = 0; ub < ni; ub += s.g) {
+      const int my_ui = ub + s.sub;
+      double mine = 0.;
+      if (my_ui < ni) mine = te_heating_ion_coll_deexc(K, D, s, my_ui, s.Te, D.nne[s.mgi]);
+      for (int j = 0; j < s.g && ub + j < ni; j++) C_deexc += __shfl(mine, s.lane0 + j, 64);
+    }
+    hc->heating_collisional = C_deexc;
+  } else {
+    hc->heating_collisional = D.colheat[s.mgi];
+  }
   hc->heating_bf = bfheating;
   hc->heating_ff = D.ffheat[s.mgi];
 }
@@ -555,7 +647,9 @@ DEVNI void te_heating_rates(const Ctx &K, const TeDev &D, const TeState &s, TeRa
 DEVNI double te_eqn(const Ctx &K, const TeDev &D, TeState &s, double T_e, TeRates *hc, int *fail) {
   s.Te = T_e;
   double nntot = 0.;
-  if (te_calculate_populations(K, D, s, &nntot) != 0) {
+  if (D.mode == 1) {
+    nntot = te_electron_densities(K, D, s);
+  } else if (te_calculate_populations(K, D, s, &nntot) != 0) {
     *fail = 1;
     return NAN;
   }
@@ -617,6 +711,66 @@ __global__ __launch_bounds__(64, 4) void k_te_solve(const Ctx *__restrict__ Kp, 
   TeRates hc = {0., 0., 0., 0., 0., 0., 0., 0.};
   int iters = 0;
   int fail = 0;
+  if (D.mode == 2) {
+    te_cooling_rates(K, D, s, nullptr, true);
+    return;
+  }
+  if (D.mode == 1) {
+    // the nebular pass (update_grid.cc:819-838): call_T_e_finder alone, populations from the NLTE solution; the
+    // last evaluation at the final T_e leaves n_e and the rates of that T_e
+    const double T_min = D.T_min, T_max = D.T_max;
+    const double T_e_old = s.Te;
+    auto f = [&](double T) { return te_eqn(K, D, s, T, &hc, &fail); };
+    double thermalmin = f(T_min);
+    double thermalmax = f(T_max);
+    if (!isfinite(thermalmin) || !isfinite(thermalmax)) thermalmax = thermalmin = -1;
+    double T_e = 0.;
+    iters = -1;
+    if (thermalmin * thermalmax < 0) {
+      TeBrent b;
+      if (te_brent_set(b, f, T_min, T_max) != 0) fail = 1;
+      for (int iternum = 0; iternum < 100 && !fail; iternum++) {
+        if (te_brent_iterate(b, f) != 0) {
+          fail = 1;
+          break;
+        }
+        T_e = b.root;
+        iters = iternum + 1;
+        if (te_test_interval(b.x_lower, b.x_upper, 0, D.accuracy) != 1) break;
+      }
+    } else if (thermalmax < 0) {
+      T_e = T_min;
+    } else {
+      T_e = T_max;
+    }
+    if (!fail) {
+      if (T_e > 2 * T_e_old) {
+        T_e = 2 * T_e_old;
+        if (T_e > T_max) T_e = T_max;
+      } else if (T_e < 0.5 * T_e_old) {
+        T_e = 0.5 * T_e_old;
+        if (T_e < T_min) T_e = T_min;
+      }
+      f(T_e);
+    }
+    if (fail) {
+      atomicCAS(D.fail, 0, mgi + 1);
+      return;
+    }
+    D.Te[mgi] = s.Te;
+    if (D.rates) {
+      double *r = D.rates + (int64_t)mgi * ARTIS_TE_NRATES;
+      r[0] = hc.cooling_collisional;
+      r[1] = hc.cooling_fb;
+      r[2] = hc.cooling_ff;
+      r[3] = hc.cooling_adiabatic;
+      r[4] = hc.heating_collisional;
+      r[5] = hc.heating_bf;
+      r[6] = hc.heating_ff;
+      r[7] = hc.heating_dep;
+    }
+    return;
+  }
   if (te_use_lte_ratio(D, mgi)) {
     // update_grid.cc:1106-1125 (T_J from get_T_J_from_J is the caller's TJ)
     s.Te = D.TJ[mgi];

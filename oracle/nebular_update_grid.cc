@@ -913,24 +913,6 @@ void nl_store_nt_rates(const Ctx &c, const NlteRun &r, int mgi, int *fail) {
 }
 
 // --------------------------------------------------------------------------------------------- T_e solver
-// thermalbalance.cc:189-216 get_heating_ion_coll_deexc
-double nl_heating_ion_coll_deexc(const Ctx &c, int mgi, int e, int i, float T_e, float nne) {
-  double C_deexc = 0.;
-  for (int level = 0; level < get_nlevels(c, e, i); level++) {
-    const double nnlevel = calculate_levelpop(c, mgi, e, i, level);
-    const double epsilon_level = epsilon(c, e, i, level);
-    const int ul = ulev(c, e, i, level);
-    for (int k = 0; k < c.at->level_ndowntrans[ul]; k++) {
-      const int li = c.at->downtrans_lineindex[c.at->level_downtrans_offset[ul] + k];
-      const int lower = c.at->line_lowerlevelindex[li];
-      const double epsilon_trans = epsilon_level - epsilon(c, e, i, lower);
-      const double statweight = stat_weight(c, e, i, level);
-      C_deexc += nnlevel * col_deexcitation_ratecoeff(c, T_e, nne, epsilon_trans, li, stat_weight(c, e, i, lower), statweight) *
-                 epsilon_trans;
-    }
-  }
-  return C_deexc;
-}
 // thermalbalance.cc:218-346 (DIRECT_COL_HEAT)
 void nl_calculate_heating_rates(const Ctx &c, const NlteRun &r, int mgi, const std::vector<double> &coeff, TeRates *hc) {
   double C_deexc = 0., bfheating = 0.;
@@ -938,7 +920,7 @@ void nl_calculate_heating_rates(const Ctx &c, const NlteRun &r, int mgi, const s
   const float nne = r.g->nne[mgi];
   for (int e = 0; e < c.at->nelements; e++) {
     const int nions = get_nions(c, e);
-    for (int i = 0; i < nions; i++) C_deexc += nl_heating_ion_coll_deexc(c, mgi, e, i, T_e, nne);
+    for (int i = 0; i < nions; i++) C_deexc += te_heating_ion_coll_deexc(c, mgi, e, i, T_e, nne);
     for (int i = 0; i < nions - 1; i++)
       for (int level = 0; level < get_ionisinglevels(c, e, i); level++)
         bfheating += calculate_levelpop(c, mgi, e, i, level) * coeff[ulev(c, e, i, level)];
@@ -1269,7 +1251,23 @@ int nl_solve_nlte_pops_element(const Ctx &c, const NlteRun &r, int e, int mgi, s
   const int D = nlte_build(c, r, mgi, e, A, b, norm, slpf);
   if (A_out) *A_out = A;
   std::vector<double> popvec(D);
-  if (!nlte_matrix_solve(A.data(), b.data(), D, popvec.data(), norm.data())) {
+  const bool solved = nlte_matrix_solve(A.data(), b.data(), D, popvec.data(), norm.data());
+  if (const char *dump = getenv("ORACLE_NL_DUMP")) {
+    // diagnostics: the first solve of each element (tools/nl_dump_cmp.py)
+    const std::string path = std::string(dump) + "_ora_e" + std::to_string(e) + ".bin";
+    if (FILE *probe = fopen(path.c_str(), "rb")) {
+      fclose(probe);
+    } else if (FILE *fp = fopen(path.c_str(), "wb")) {
+      const int32_t hdr[2] = {D, solved ? 0 : 1};
+      fwrite(hdr, sizeof hdr, 1, fp);
+      fwrite(A.data(), 8, A.size(), fp);
+      fwrite(b.data(), 8, b.size(), fp);
+      fwrite(norm.data(), 8, norm.size(), fp);
+      fwrite(popvec.data(), 8, popvec.size(), fp);
+      fclose(fp);
+    }
+  }
+  if (!solved) {
     nlte_reset_element(c, r, mgi, e);  // set_element_pops_lte
     return 0;
   }

@@ -47,6 +47,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <string>
 #include <vector>
 
 #include "artis_constants.h"
@@ -4159,11 +4160,32 @@ void te_calculate_bfheatingcoeffs(const Ctx &c, const TeRun &r, int mgi, std::ve
         coeff[ulev(c, e, i, l)] = bfheatingcoeff;
       }
 }
-// thermalbalance.cc:218-346 (DIRECT_COL_HEAT undefined)
+// thermalbalance.cc:189-216 get_heating_ion_coll_deexc
+double te_heating_ion_coll_deexc(const Ctx &c, int mgi, int e, int i, float T_e, float nne) {
+  double C_deexc = 0.;
+  for (int level = 0; level < get_nlevels(c, e, i); level++) {
+    const double nnlevel = calculate_levelpop(c, mgi, e, i, level);
+    const double epsilon_level = epsilon(c, e, i, level);
+    const int ul = ulev(c, e, i, level);
+    for (int k = 0; k < c.at->level_ndowntrans[ul]; k++) {
+      const int li = c.at->downtrans_lineindex[c.at->level_downtrans_offset[ul] + k];
+      const int lower = c.at->line_lowerlevelindex[li];
+      const double epsilon_trans = epsilon_level - epsilon(c, e, i, lower);
+      const double statweight = stat_weight(c, e, i, level);
+      C_deexc += nnlevel * col_deexcitation_ratecoeff(c, T_e, nne, epsilon_trans, li, stat_weight(c, e, i, lower), statweight) *
+                 epsilon_trans;
+    }
+  }
+  return C_deexc;
+}
+// thermalbalance.cc:218-346: the collisional heating is the de-excitation sum with DIRECT_COL_HEAT
+// (artis_te_params.direct_col_heat), the normalised estimator otherwise
 void te_calculate_heating_rates(const Ctx &c, const TeRun &r, int mgi, const std::vector<double> &coeff, TeRates *hc) {
-  double bfheating = 0.;
+  double bfheating = 0., C_deexc = 0.;
   for (int e = 0; e < c.at->nelements; e++) {
     const int nions = get_nions(c, e);
+    if (r.par->direct_col_heat)
+      for (int i = 0; i < nions; i++) C_deexc += te_heating_ion_coll_deexc(c, mgi, e, i, r.g->Te[mgi], r.g->nne[mgi]);
     for (int i = 0; i < nions - 1; i++) {
       const int nbflevels = get_ionisinglevels(c, e, i);
       for (int level = 0; level < nbflevels; level++) {
@@ -4172,7 +4194,7 @@ void te_calculate_heating_rates(const Ctx &c, const TeRun &r, int mgi, const std
       }
     }
   }
-  hc->heating_collisional = r.in->colheatingestimator[mgi];
+  hc->heating_collisional = r.par->direct_col_heat ? C_deexc : r.in->colheatingestimator[mgi];
   hc->heating_bf = bfheating;
   hc->heating_ff = r.in->ffheatingestimator[mgi];
 }
