@@ -1847,7 +1847,7 @@ int artis_gpu_update_grid_nlte(const artis_nt_shells *nt, const artis_nlte_param
       k_nl_bfnorm<<<(unsigned)(((int64_t)nnl * nbf + TB - 1) / TB), TB, 0, G.stream>>>(KN, N, d_nl, nnl);
     NLSTEP("k_nl_bfnorm");
     if (nbins > 0)
-      k_nl_binfit<<<(unsigned)std::min<int64_t>((int64_t)nnl * nbins, qwaves), 64, 0, G.stream>>>(dK, dN, d_nl, nnl, ws);
+      k_nl_binfit<<<(unsigned)(((int64_t)nnl * nbins + 63) / 64), 64, 0, G.stream>>>(dK, dN, d_nl, nnl);
     NLSTEP("k_nl_binfit");
     if (!hb.empty())
       k_nl_bfheat<<<(unsigned)std::min<int64_t>((int64_t)nnl * hb.size(), qwaves), 64, 0, G.stream>>>(
@@ -1927,7 +1927,7 @@ int artis_gpu_update_grid_nlte(const artis_nt_shells *nt, const artis_nlte_param
           NLSTEP("k_nl_matrix");
           k_nl_lu<<<(unsigned)(nch * ne), NL_LU_WG, 0, G.stream>>>(KN, M, nch);
           NLSTEP("k_nl_lu");
-          if (iter == 0 && a0 == 0 && getenv("ARTIS_GPU_NL_DUMP")) {
+          if (a0 == 0 && getenv("ARTIS_GPU_NL_DUMP") && iter < 4) {
             // diagnostics: the first pass's rate matrices of the first active cell (tools/nl_dump_cmp.py)
             HIPCHK(hipStreamSynchronize(G.stream));
             std::vector<double> hA, hb, hn, hp, hpops, hcorr;
@@ -1936,7 +1936,7 @@ int artis_gpu_update_grid_nlte(const artis_nt_shells *nt, const artis_nlte_param
                 d2h_vec(hp, M.pv, (size_t)cell1) || d2h_vec(hs, M.status, (size_t)ne) || d2h_vec(hpops, d_pops, (size_t)nl) ||
                 d2h_vec(hcorr, d_corr, (size_t)ntg))
               return ARTIS_ERR_HIP;
-            const std::string path = std::string(getenv("ARTIS_GPU_NL_DUMP")) + "_gpu.bin";
+            const std::string path = std::string(getenv("ARTIS_GPU_NL_DUMP")) + "_p" + std::to_string(iter) + "_gpu.bin";
             if (FILE *fp = fopen(path.c_str(), "wb")) {
               const int32_t hdr[5] = {ne, cell1, (int32_t)cell2, nl, (int32_t)ntg};
               fwrite(hdr, sizeof hdr, 1, fp);

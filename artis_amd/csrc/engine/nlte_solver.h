@@ -6,8 +6,8 @@
 //
 //   k_nl_prepare     estimator normalisation, the LTE branch's T_J, the full-spectrum fit (radfield.cc:1136-1175)
 //   k_nl_bfnorm      normalise_bf_estimators (radfield.cc:1306-1327), workitem = (cell, continuum)
-//   k_nl_binfit      the per-bin fit (radfield.cc:1177-1291): one wave per (cell, bin) running GSL Brent on the mean
-//                    frequency, each evaluation two wave-parallel GK61 qag Planck integrals (qag.h)
+//   k_nl_binfit      the per-bin fit (radfield.cc:1177-1291): one workitem per (cell, bin) running GSL Brent on the
+//                    mean frequency, the Planck integrals by the GK61 rule on kT-sized panels (D14)
 //   k_nl_bfheat      calculate_bfheatingcoeffs with NO_LUT_BFHEATING (thermalbalance.cc:60-187): one wave per (cell,
 //                    ionising level), its targets' qag integrals in order
 //   Spencer-Fano     (nonthermal.cc:2522-2713) one cell at a time, the SFPTS x SFPTS system in HBM (128 MiB):
@@ -147,108 +147,110 @@ __global__ void k_nl_bfnorm(Ctx K, NlDev N, const int32_t *list, int nlist) {
   N.bfrate[q] = N.bfraw[q] * (nl_estimator_normfactor(N, mgi) / ARTIS_H);
 }
 
-// radfield.cc:945-979 planck_integral (qag GK61, epsrel 1e-10; a failed integral is 0), on the whole wave
-// (not inlined: inlined into the Brent iteration's many call sites, the qag code trips an instruction-selection bug
-// of the gfx950 backend on its LDS-or-global list accesses)
-DEVNI double nl_planck_integral(double *al, double *bl, double *rl, QagLists Q, int32_t *lev, double *s_f,
-                                double T_R, double nu_lower, double nu_upper, bool times_nu) {
+// radfield.cc:945-979 planck_integral: the reference integrates the Planck function over a bin with GSL qag
+// (GK61, epsrel 1e-10).  The integrand is analytic on the whole bin, so the engine evaluates the integral directly
+// with the same 61-point Kronrod rule on panels at most 8 kT/h wide (deviation D14): on a bin qag accepts after its
+// first rule this is that rule's value, otherwise it agrees with qag's result to qag's 1e-10 tolerance.  Per lane, no
+// workspace; contributions beyond 800 kT/h above the lower edge (e^-800 of the integrand there) are dropped.
+DEVFN double nl_planck_integral(double T_R, double nu_lower, double nu_upper, bool times_nu) {
   auto f = [&](double nu) {
     double integrand = ARTIS_TWOHOVERCLIGHTSQUARED * pow(nu, 3) / (expm1(ARTIS_HOVERKB * nu / T_R));
     if (times_nu) integrand *= nu;
     return integrand;
   };
-  double integral = 0., error = 0.;
-  const int status = qag61(f, nu_lower, nu_upper, 0., 1e-10, al, bl, rl, Q, lev, s_f, &integral, &error);
-  if (status != 0) integral = 0.;
+  const double dnu_kT = T_R / ARTIS_HOVERKB;  // nu of one kT / h
+  double b_end = nu_upper;
+  if (b_end > nu_lower + 800. * dnu_kT) b_end = nu_lower + 800. * dnu_kT;
+  const int npan = (int)fmin(fmax(ceil((b_end - nu_lower) / (8. * dnu_kT)), 1.), 200.);
+  const double width = (b_end - nu_lower) / npan;
+  double integral = 0.;
+  for (int p = 0; p < npan; p++) {
+    const double a = nu_lower + p * width;
+    const double b = (p == npan - 1) ? b_end : a + width;
+    const double center = 0.5 * (a + b), half_length = 0.5 * (b - a);
+    double result_kronrod = f(center) * c_qk61_wgk[30];
+    for (int j = 0; j < 30; j++) {
+      const double abscissa = half_length * c_qk61_xgk[j];
+      result_kronrod += c_qk61_wgk[j] * (f(center - abscissa) + f(center + abscissa));
+    }
+    integral += result_kronrod * half_length;
+  }
   return integral;
 }
 DEVFN double nl_bin_nu_lower(const Ctx &K, int b) { return b > 0 ? K.T.rf_nu_upper[b - 1] : K.T.rf_nu_lower_first; }
 
-// radfield.cc:1177-1291 fit_parameters' bin loop: one wave per (listed non-LTE cell, bin); every lane runs the same
-// Brent iteration (radfield.cc:1070-1133 find_T_R) on the wave's common integrals
+// radfield.cc:1177-1291 fit_parameters' bin loop, one workitem per (listed non-LTE cell, bin): GSL Brent on the mean
+// frequency of a dilute Planck function (radfield.cc:1070-1133 find_T_R), the bin's dilution factor
 __global__ __launch_bounds__(64) void k_nl_binfit(const Ctx *__restrict__ Kp, const NlDev *__restrict__ Np,
-                                                  const int32_t *list, int nlist, QagWs ws) {
+                                                  const int32_t *list, int nlist) {
   const Ctx &K = *Kp;
   const NlDev &N = *Np;
-  __shared__ double s_f[64];
-  __shared__ double s_el[QAG_LDS];
-  __shared__ int32_t s_ord[QAG_LDS];
   const int nb = K.T.rf_nbins;
-  const int64_t total = (int64_t)nlist * nb;
-  const int64_t wbase = (int64_t)blockIdx.x * QAG_LIMIT;
-  double *al = ws.alist + wbase, *bl = ws.blist + wbase, *rl = ws.rlist + wbase;
-  int32_t *lev = ws.level + wbase;
-  const QagLists Q{s_el, s_ord, ws.elist + wbase, ws.order + wbase};
-  double *sf = s_f;
-  const bool lane0 = (threadIdx.x & 63) == 0;
-  for (int64_t item = blockIdx.x; item < total; item += gridDim.x) {
-    const int mgi = list[item / nb];
-    const int b = (int)(item % nb);
-    const int64_t mb = (int64_t)mgi * nb + b;
-    const double J_normfactor = ARTIS_ONEOVER4PI * nl_estimator_normfactor(N, mgi);
-    const double nu_lower = nl_bin_nu_lower(K, b), nu_upper = K.T.rf_nu_upper[b];
-    const double J_bin = N.binJ[mb] * J_normfactor;
-    float T_R_bin = -1.0;
-    double W_bin = -1.0;
-    if (N.bincount[mb] > 0) {
-      const double nu_bar = (N.binnuJ[mb] * J_normfactor) / J_bin;
-      // find_T_R
-      auto delta_nu_bar = [&](double T_R) {
-        const double nu_times_planck = nl_planck_integral(al, bl, rl, Q, lev, sf, T_R, nu_lower, nu_upper, true);
-        const double planck = nl_planck_integral(al, bl, rl, Q, lev, sf, T_R, nu_lower, nu_upper, false);
-        return nu_times_planck / planck - nu_bar;
-      };
-      const double T_R_min = N.T_R_min, T_R_max = N.T_R_max;
-      double delta_nu_bar_min = delta_nu_bar(T_R_min);
-      double delta_nu_bar_max = delta_nu_bar(T_R_max);
-      if (!isfinite(delta_nu_bar_min) || !isfinite(delta_nu_bar_max)) delta_nu_bar_max = delta_nu_bar_min = -1;
-      double T_R = 0.;
-      bool bad = false;
-      if (delta_nu_bar_min * delta_nu_bar_max < 0) {
-        TeBrent s;
-        if (te_brent_set(s, delta_nu_bar, T_R_min, T_R_max) != 0) bad = true;
-        int iteration_num = 0, status = 1;
-        while (!bad && status == 1 && iteration_num < 100) {
-          iteration_num++;
-          if (te_brent_iterate(s, delta_nu_bar) != 0) {
-            bad = true;
-            break;
-          }
-          T_R = s.root;
-          status = te_test_interval(s.x_lower, s.x_upper, 0., 1e-4);
+  const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= (int64_t)nlist * nb) return;
+  const int mgi = list[item / nb];
+  const int b = (int)(item % nb);
+  const int64_t mb = (int64_t)mgi * nb + b;
+  const double J_normfactor = ARTIS_ONEOVER4PI * nl_estimator_normfactor(N, mgi);
+  const double nu_lower = nl_bin_nu_lower(K, b), nu_upper = K.T.rf_nu_upper[b];
+  const double J_bin = N.binJ[mb] * J_normfactor;
+  float T_R_bin = -1.0;
+  double W_bin = -1.0;
+  if (N.bincount[mb] > 0) {
+    const double nu_bar = (N.binnuJ[mb] * J_normfactor) / J_bin;
+    auto delta_nu_bar = [&](double T_R) {
+      const double nu_times_planck = nl_planck_integral(T_R, nu_lower, nu_upper, true);
+      const double planck = nl_planck_integral(T_R, nu_lower, nu_upper, false);
+      return nu_times_planck / planck - nu_bar;
+    };
+    const double T_R_min = N.T_R_min, T_R_max = N.T_R_max;
+    double delta_nu_bar_min = delta_nu_bar(T_R_min);
+    double delta_nu_bar_max = delta_nu_bar(T_R_max);
+    if (!isfinite(delta_nu_bar_min) || !isfinite(delta_nu_bar_max)) delta_nu_bar_max = delta_nu_bar_min = -1;
+    double T_R = 0.;
+    bool bad = false;
+    if (delta_nu_bar_min * delta_nu_bar_max < 0) {
+      TeBrent s;
+      if (te_brent_set(s, delta_nu_bar, T_R_min, T_R_max) != 0) bad = true;
+      int iteration_num = 0, status = 1;
+      while (!bad && status == 1 && iteration_num < 100) {
+        iteration_num++;
+        if (te_brent_iterate(s, delta_nu_bar) != 0) {
+          bad = true;
+          break;
         }
-      } else if (delta_nu_bar_max < 0) {
-        T_R = T_R_max;
-      } else {
-        T_R = T_R_min;
+        T_R = s.root;
+        status = te_test_interval(s.x_lower, s.x_upper, 0., 1e-4);
       }
-      if (bad) {
-        if (lane0) nl_fail(N, mgi, NLF_BINFIT);
-        T_R = 0.;
-      }
-      T_R_bin = T_R;
-      if (b == nb - 1) T_R_bin = N.Te[mgi];
-      double planck_integral_result = nl_planck_integral(al, bl, rl, Q, lev, sf, T_R_bin, nu_lower, nu_upper, false);
+    } else if (delta_nu_bar_max < 0) {
+      T_R = T_R_max;
+    } else {
+      T_R = T_R_min;
+    }
+    if (bad) {
+      nl_fail(N, mgi, NLF_BINFIT);
+      T_R = 0.;
+    }
+    T_R_bin = T_R;
+    if (b == nb - 1) T_R_bin = N.Te[mgi];
+    double planck_integral_result = nl_planck_integral(T_R_bin, nu_lower, nu_upper, false);
+    W_bin = J_bin / planck_integral_result;
+    if (W_bin > 1e4) {
+      planck_integral_result = nl_planck_integral(N.T_R_max, nu_lower, nu_upper, false);
       W_bin = J_bin / planck_integral_result;
       if (W_bin > 1e4) {
-        planck_integral_result = nl_planck_integral(al, bl, rl, Q, lev, sf, N.T_R_max, nu_lower, nu_upper, false);
-        W_bin = J_bin / planck_integral_result;
-        if (W_bin > 1e4) {
-          T_R_bin = -99.0;
-          W_bin = 0.;
-        } else {
-          T_R_bin = N.T_R_max;
-        }
+        T_R_bin = -99.0;
+        W_bin = 0.;
+      } else {
+        T_R_bin = N.T_R_max;
       }
-    } else {
-      T_R_bin = 0.;
-      W_bin = 0.;
     }
-    if (lane0) {
-      N.binTR[mb] = T_R_bin;
-      N.binW[mb] = W_bin;
-    }
+  } else {
+    T_R_bin = 0.;
+    W_bin = 0.;
   }
+  N.binTR[mb] = T_R_bin;
+  N.binW[mb] = W_bin;
 }
 
 // thermalbalance.cc:60-132 calculate_bfheatingcoeff of one target (not inlined, see nl_planck_integral)

@@ -1424,6 +1424,9 @@ int64_t artis_model_npts_model(const artis_model *m) { return m->npts_model; }
 int artis_model_radfield_nbins(const artis_model *m) { return m->at.radfield_nbins; }
 int artis_model_total_nlte_levels(const artis_model *m) { return m->at.total_nlte_levels; }
 const int32_t *artis_model_ion_ionstage(const artis_model *m) { return m->at.ion_ionstage; }
+void artis_model_ion_ground_statweight(const artis_model *m, float *out) {
+  for (int ui = 0; ui < m->at.nions_total; ui++) out[ui] = m->at.level_stat_weight[m->at.ion_uniqueleveloffset[ui]];
+}
 void artis_model_config(const artis_model *m, artis_synth_config *out) { *out = m->cfg; }
 
 void artis_model_run_params(const artis_model *m, artis_run_params *p) {

@@ -85,6 +85,7 @@ int64_t artis_model_npts_model(const artis_model *m);
 int artis_model_radfield_nbins(const artis_model *m);
 int artis_model_total_nlte_levels(const artis_model *m);
 const int32_t *artis_model_ion_ionstage(const artis_model *m);
+void artis_model_ion_ground_statweight(const artis_model *m, float *out);  /* [nions_total] g of each ground level */
 /* the configuration the model was built with (after artis_model_from_files adopted input.txt's values) */
 void artis_model_config(const artis_model *m, artis_synth_config *out);
 

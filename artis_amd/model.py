@@ -45,6 +45,8 @@ def model_lib():
         lib.artis_model_total_nlte_levels.argtypes = [C.c_void_p]
         lib.artis_model_ion_ionstage.argtypes = [C.c_void_p]
         lib.artis_model_ion_ionstage.restype = C.c_void_p
+        lib.artis_model_ion_ground_statweight.argtypes = [C.c_void_p, C.c_void_p]
+        lib.artis_model_ion_ground_statweight.restype = None
         _model_lib = lib
     return _model_lib
 
@@ -164,6 +166,17 @@ class Model:
     def ion_ionstage(self):
         p = self._lib.artis_model_ion_ionstage(self._h)
         return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int32)), (self.nions_total,)).copy()
+
+    def ion_ground_statweight(self):
+        g = np.zeros(self.nions_total, dtype=np.float32)
+        self._lib.artis_model_ion_ground_statweight(self._h, g.ctypes.data)
+        return g
+
+    def ion_element(self):
+        """element index of every unique ion"""
+        hdr = ffi.AtomicHeader.from_address(self.atomic)
+        nions = np.ctypeslib.as_array(C.cast(hdr.elem_nions, C.POINTER(C.c_int32)), (self.nelements,))
+        return np.repeat(np.arange(self.nelements), nions)
 
     def close(self):
         if self._h:

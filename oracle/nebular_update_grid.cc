@@ -1254,10 +1254,15 @@ int nl_solve_nlte_pops_element(const Ctx &c, const NlteRun &r, int e, int mgi, s
   const bool solved = nlte_matrix_solve(A.data(), b.data(), D, popvec.data(), norm.data());
   if (const char *dump = getenv("ORACLE_NL_DUMP")) {
     // diagnostics: the first solve of each element (tools/nl_dump_cmp.py)
-    const std::string path = std::string(dump) + "_ora_e" + std::to_string(e) + ".bin";
-    if (FILE *probe = fopen(path.c_str(), "rb")) {
-      fclose(probe);
-    } else if (FILE *fp = fopen(path.c_str(), "wb")) {
+    static int ncalls[64] = {0};  // solves of each element so far under this prefix (a one-cell diagnostic run)
+    static std::string last;
+    if (last != dump) {
+      last = dump;
+      for (int q = 0; q < 64; q++) ncalls[q] = 0;
+    }
+    const int pass = e < 64 ? ncalls[e]++ : 99;
+    const std::string path = std::string(dump) + "_p" + std::to_string(pass) + "_ora_e" + std::to_string(e) + ".bin";
+    if (pass < 4) if (FILE *fp = fopen(path.c_str(), "wb")) {
       const int32_t hdr[2] = {D, solved ? 0 : 1};
       fwrite(hdr, sizeof hdr, 1, fp);
       fwrite(A.data(), 8, A.size(), fp);

@@ -7,7 +7,14 @@ import sys
 import numpy as np
 
 
-def main(prefix):
+def main(prefix, npass=1):
+    for p in range(npass):
+        if os.path.exists(f"{prefix}_p{p}_gpu.bin"):
+            print(f"--- pass {p}")
+            compare(f"{prefix}_p{p}")
+
+
+def compare(prefix):
     with open(prefix + "_gpu.bin", "rb") as f:
         ne, cell1, cell2, nl, ntg = np.frombuffer(f.read(20), np.int32)
         el_D = np.frombuffer(f.read(4 * ne), np.int32)
@@ -53,4 +60,4 @@ def main(prefix):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 4)
