@@ -1586,6 +1586,8 @@ int artis_gpu_update_grid_nlte(const artis_nt_shells *nt, const artis_nlte_param
   // Spencer-Fano tables
   SfDev S{};
   std::vector<int32_t> h_solve;
+  int sf_batch = 1;
+  std::vector<double> h_none;  // errbest seeds (-1: no solution yet)
   if (sf_on && nnl > 0) {
     const int n = nt->sfpts;
     S.n = n;
@@ -1740,16 +1742,25 @@ int artis_gpu_update_grid_nlte(const artis_nt_shells *nt, const artis_nlte_param
     rc |= up(&S.ion_binding, binding);
     rc |= up(&S.ion_binding_ok, binding_ok);
     S.anumber = D.anumber;
-    rc |= B.get(&S.nnion, (size_t)ni, (const double *)nullptr);
-    rc |= B.get(&S.incl, (size_t)ni, (const int32_t *)nullptr);
-    rc |= B.get(&S.tot_nion, 1, (const double *)nullptr);
-    rc |= B.get(&S.MT, (size_t)n * n, (const double *)nullptr);
-    rc |= B.get(&S.x, (size_t)n, (const double *)nullptr);
-    rc |= B.get(&S.best, (size_t)n, (const double *)nullptr);
-    rc |= B.get(&S.work, (size_t)n, (const double *)nullptr);
-    rc |= B.get(&S.res, (size_t)n, (const double *)nullptr);
-    rc |= B.get(&S.errbest, 1, (const double *)nullptr);
-    rc |= B.get(&S.dots, (size_t)std::max(1, S.nitems), (const double *)nullptr);
+    // cells solved together: their matrices (8 n^2 bytes each) within ARTIS_GPU_SF_BATCH_GB (default 8 GiB)
+    double sf_gb = 8.;
+    if (const char *v = getenv("ARTIS_GPU_SF_BATCH_GB")) sf_gb = std::max(0.0, atof(v));
+    sf_batch = (int)std::max<double>(1., std::min<double>(nnl, sf_gb * (double)(1ull << 30) / (8.0 * n * n)));
+    h_none.assign(sf_batch, -1.);
+    const size_t nbq = (size_t)sf_batch;
+    rc |= B.get((int32_t **)&S.bat_a, nbq, (const int32_t *)nullptr);
+    rc |= B.get((int32_t **)&S.bat_mgi, nbq, (const int32_t *)nullptr);
+    rc |= B.get(&S.nnion, nbq * ni, (const double *)nullptr);
+    rc |= B.get(&S.incl, nbq * ni, (const int32_t *)nullptr);
+    rc |= B.get(&S.tot_nion, nbq, (const double *)nullptr);
+    rc |= B.get(&S.MT, nbq * n * n, (const double *)nullptr);
+    rc |= B.get(&S.x, nbq * n, (const double *)nullptr);
+    rc |= B.get(&S.best, nbq * n, (const double *)nullptr);
+    rc |= B.get(&S.work, nbq * n, (const double *)nullptr);
+    rc |= B.get(&S.res, nbq * n, (const double *)nullptr);
+    rc |= B.get(&S.part, nbq * n * ((n + SF_RCHUNK - 1) / SF_RCHUNK), (const double *)nullptr);
+    rc |= B.get(&S.errbest, nbq, (const double *)nullptr);
+    rc |= B.get(&S.dots, nbq * std::max(1, S.nitems), (const double *)nullptr);
     rc |= B.get(&S.solve, (size_t)nact_max, (const int32_t *)nullptr);
     if (rc) return ARTIS_ERR_HIP;
   } else if (R.nt_on) {
@@ -1874,33 +1885,45 @@ int artis_gpu_update_grid_nlte(const artis_nt_shells *nt, const artis_nlte_param
         HIPCHK(hipStreamSynchronize(G.stream));
         if (d2h_vec(h_solve, S.solve, nact)) return ARTIS_ERR_HIP;
         const int n = S.n;
-        for (int a = 0; a < nact; a++) {
-          if (!h_solve[a]) continue;
-          const int mgi = act[a];
-          const double *cpops = d_pops + (int64_t)a * nl;
-          k_sf_ions<<<(ni + 63) / 64, 64, 0, G.stream>>>(KN, N, S, mgi);
+        std::vector<int32_t> sa, sm;  // the cells to solve: active position, model cell
+        for (int a = 0; a < nact; a++)
+          if (h_solve[a]) {
+            sa.push_back(a);
+            sm.push_back(act[a]);
+          }
+        for (size_t q0 = 0; q0 < sa.size(); q0 += sf_batch) {
+          const int nb = (int)std::min<size_t>(sf_batch, sa.size() - q0);
+          HIPCHK(hipMemcpy((void *)S.bat_a, sa.data() + q0, nb * sizeof(int32_t), hipMemcpyHostToDevice));
+          HIPCHK(hipMemcpy((void *)S.bat_mgi, sm.data() + q0, nb * sizeof(int32_t), hipMemcpyHostToDevice));
+          k_sf_ions<<<(nb * ni + 63) / 64, 64, 0, G.stream>>>(KN, N, S, nb);
           NLSTEP("k_sf_ions");
-          k_sf_matrix<<<dim3((unsigned)((n + 255) / 256), (unsigned)n), 256, 0, G.stream>>>(KN, N, S, mgi, cpops);
+          k_sf_matrix<<<dim3((unsigned)((n + 255) / 256), (unsigned)n, (unsigned)nb), 256, 0, G.stream>>>(KN, N, S,
+                                                                                                         d_pops);
           NLSTEP("k_sf_matrix");
-          HIPCHK(hipMemcpyAsync(S.x, S.rhs, n * sizeof(double), hipMemcpyDeviceToDevice, G.stream));
-          k_sf_backsub<<<1, SF_WG, 0, G.stream>>>(S.MT, n, S.x);
+          for (int q = 0; q < nb; q++)
+            HIPCHK(hipMemcpyAsync(S.x + (size_t)q * n, S.rhs, n * sizeof(double), hipMemcpyDeviceToDevice, G.stream));
+          k_sf_backsub<<<nb, SF_WG, 0, G.stream>>>(S.MT, n, S.x);
           NLSTEP("k_sf_backsub");
-          static const double none_yet = -1.;
-          HIPCHK(hipMemcpyAsync(S.errbest, &none_yet, sizeof(double), hipMemcpyHostToDevice, G.stream));
+          HIPCHK(hipMemcpyAsync(S.errbest, h_none.data(), nb * sizeof(double), hipMemcpyHostToDevice, G.stream));
+          const dim3 rgrid((unsigned)((n + 255) / 256), (unsigned)((n + SF_RCHUNK - 1) / SF_RCHUNK), (unsigned)nb);
+          const dim3 vgrid((unsigned)((n + 255) / 256), (unsigned)nb);
           for (int it = 0; it < 10; it++) {
             if (it > 0) {
-              k_sf_residual<<<(n + 255) / 256, 256, 0, G.stream>>>(S.MT, n, S.x, S.rhs, S.work);
-              k_sf_backsub<<<1, SF_WG, 0, G.stream>>>(S.MT, n, S.work);
-              k_sf_axpy<<<(n + 255) / 256, 256, 0, G.stream>>>(n, S.x, S.work);
+              k_sf_residual_part<<<rgrid, 256, 0, G.stream>>>(S.MT, n, S.x, S.part);
+              k_sf_residual_sum<<<vgrid, 256, 0, G.stream>>>(n, S.part, S.rhs, S.work);
+              k_sf_backsub<<<nb, SF_WG, 0, G.stream>>>(S.MT, n, S.work);
+              k_sf_axpy<<<vgrid, 256, 0, G.stream>>>(n, S.x, S.work);
             }
-            k_sf_residual<<<(n + 255) / 256, 256, 0, G.stream>>>(S.MT, n, S.x, S.rhs, S.res);
-            k_sf_best<<<1, 1024, 0, G.stream>>>(n, S.res, S.x, S.best, S.errbest);
+            k_sf_residual_part<<<rgrid, 256, 0, G.stream>>>(S.MT, n, S.x, S.part);
+            k_sf_residual_sum<<<vgrid, 256, 0, G.stream>>>(n, S.part, S.rhs, S.res);
+            k_sf_best<<<nb, 1024, 0, G.stream>>>(n, S.res, S.x, S.best, S.errbest);
             NLSTEP("Spencer-Fano refinement");
           }
-          k_sf_dots<<<(S.nitems + 63) / 64, 64, 0, G.stream>>>(S, S.best);
+          k_sf_dots<<<dim3((unsigned)((S.nitems + 63) / 64), (unsigned)nb), 64, 0, G.stream>>>(S, S.best);
           NLSTEP("k_sf_dots");
-          k_sf_combine<<<1, 64, 0, G.stream>>>(KN, N, S, mgi, cpops);
+          k_sf_combine<<<(nb + 63) / 64, 64, 0, G.stream>>>(KN, N, S, d_pops, nb);
           NLSTEP("k_sf_combine");
+          HIPCHK(hipStreamSynchronize(G.stream));  // the batch lists and errbest seeds are reused
         }
       }
       k_nl_ntrates<<<(nact + TB - 1) / TB, TB, 0, G.stream>>>(KN, N, S, d_act, nact);

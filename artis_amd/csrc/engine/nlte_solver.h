@@ -18,7 +18,7 @@
 //                      column-major (MT[j * n + i] = M[i][j]) for the column-oriented solves
 //     k_sf_backsub     the upper-triangular solve, one workgroup, blocked by 64 columns; every x_i still receives its
 //                      subtractions one at a time in descending column order (the column-oriented order, D11)
-//     k_sf_residual    A x - b, a workitem per row (row-serial sums, coalesced over the column-major matrix)
+//     k_sf_residual_*  A x - b: serial sums over 256-column chunks per (row, chunk), then the chunks in order
 //     k_sf_best        gsl_linalg_LU_refine's bookkeeping: x -= work, idamax, the best solution so far
 //     k_sf_dots        analyse_sf_solution's dot products (one workitem per shell / excitation transition, serial sums)
 //     k_sf_combine     the per-ion sums of analyse_sf_solution and calculate_eff_ionpot_auger_rates
@@ -149,7 +149,8 @@ __global__ void k_nl_bfnorm(Ctx K, NlDev N, const int32_t *list, int nlist) {
 
 // radfield.cc:945-979 planck_integral: the reference integrates the Planck function over a bin with GSL qag
 // (GK61, epsrel 1e-10).  The integrand is analytic on the whole bin, so the engine evaluates the integral directly
-// with the same 61-point Kronrod rule on panels at most 8 kT/h wide (deviation D14): on a bin qag accepts after its
+// with the same 61-point Kronrod rule on panels at most 24 kT/h wide (deviation D14; the rule integrates e^-x x^3
+// over such a panel to ~1e-30): on a bin qag accepts after its
 // first rule this is that rule's value, otherwise it agrees with qag's result to qag's 1e-10 tolerance.  Per lane, no
 // workspace; contributions beyond 800 kT/h above the lower edge (e^-800 of the integrand there) are dropped.
 DEVFN double nl_planck_integral(double T_R, double nu_lower, double nu_upper, bool times_nu) {
@@ -161,7 +162,7 @@ DEVFN double nl_planck_integral(double T_R, double nu_lower, double nu_upper, bo
   const double dnu_kT = T_R / ARTIS_HOVERKB;  // nu of one kT / h
   double b_end = nu_upper;
   if (b_end > nu_lower + 800. * dnu_kT) b_end = nu_lower + 800. * dnu_kT;
-  const int npan = (int)fmin(fmax(ceil((b_end - nu_lower) / (8. * dnu_kT)), 1.), 200.);
+  const int npan = (int)fmin(fmax(ceil((b_end - nu_lower) / (24. * dnu_kT)), 1.), 40.);
   const double width = (b_end - nu_lower) / npan;
   double integral = 0.;
   for (int p = 0; p < npan; p++) {
@@ -173,7 +174,9 @@ DEVFN double nl_planck_integral(double T_R, double nu_lower, double nu_upper, bo
       const double abscissa = half_length * c_qk61_xgk[j];
       result_kronrod += c_qk61_wgk[j] * (f(center - abscissa) + f(center + abscissa));
     }
-    integral += result_kronrod * half_length;
+    const double panel = result_kronrod * half_length;
+    integral += panel;
+    if (p > 0 && panel <= 1e-18 * integral) break;  // past the Wien peak: the rest is below the last bit
   }
   return integral;
 }
@@ -327,12 +330,16 @@ struct SfDev {
   const int32_t *ion_binding_ok;  // [ni] 0: the reference aborts if the work-function approximation is needed
   int32_t nsh, nitems;            // shell records; shells + transitions (k_sf_dots)
   const int32_t *anumber;         // [nelements]
-  // one cell's solve
-  double *nnion;    // [ni]
-  int32_t *incl;    // [ni]
-  double *tot_nion; // [1]
-  double *MT;       // [n * n] column-major
-  double *x, *best, *work, *res, *errbest, *dots;
+  // a batch of cells solved together, slot q: the cell's active position bat_a[q] and model cell bat_mgi[q]
+  const int32_t *bat_a, *bat_mgi;
+  double *nnion;    // [q * ni]
+  int32_t *incl;    // [q * ni]
+  double *tot_nion; // [q]
+  double *MT;       // [q * n * n] column-major
+  double *x, *best, *work, *res;  // [q * n]
+  double *errbest;  // [q]
+  double *dots;     // [q * nitems]
+  double *part;     // [q * nchunks * n] k_sf_residual_part
   int32_t *solve;   // [ncells] k_sf_decide's verdict
 };
 
@@ -406,27 +413,35 @@ __global__ void k_sf_decide(Ctx K, NlDev N, SfDev S, const int32_t *act, int nac
 }
 
 // the ion populations of the cell being solved and the ions solve_spencerfano includes (nonthermal.cc:2630-2640)
-__global__ void k_sf_ions(Ctx K, NlDev N, SfDev S, int mgi) {
-  const int ui = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ui >= K.T.nions_total) return;
+__global__ void k_sf_ions(Ctx K, NlDev N, SfDev S, int nbat) {
+  const int ni = K.T.nions_total;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= nbat * ni) return;
+  const int q = idx / ni, ui = idx % ni;
+  const int mgi = S.bat_mgi[q];
   const int e = K.T.ion_element[ui];
   const double tot_nion = nl_get_nntot(K, N, mgi);
   const double nnion = nl_ionstagepop(K, N, mgi, e, ui);
-  S.nnion[ui] = nnion;
-  S.incl[ui] = !(nnion < 1.e-8 * tot_nion);  // MINFRAC
-  if (ui == 0) S.tot_nion[0] = tot_nion;
+  S.nnion[idx] = nnion;
+  S.incl[idx] = !(nnion < 1.e-8 * tot_nion);  // MINFRAC
+  if (ui == 0) S.tot_nion[q] = tot_nion;
 }
 
 // nonthermal.cc:2617-2674 with sfmatrix_add_excitation (2282-2341) and sfmatrix_add_ionization (2343-2459): matrix
-// element (i, j >= i) in one workitem, its additions in the reference's order.  Grid: x over rows i, y = column j.
-// pops: the cell's level populations (k_levelpops of the solver state).
-__global__ __launch_bounds__(256) void k_sf_matrix(Ctx K, NlDev N, SfDev S, int mgi, const double *__restrict__ pops) {
+// element (i, j >= i) in one workitem, its additions in the reference's order.  Grid: x over rows i, y = column j,
+// z = batch slot.  pops0: the active cells' level populations (k_levelpops of the solver state).
+__global__ __launch_bounds__(256) void k_sf_matrix(Ctx K, NlDev N, SfDev S, const double *__restrict__ pops0) {
   const int j = blockIdx.y;
+  const int q = blockIdx.z;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = S.n;
   if (i >= n) return;
   if (i > j) return;  // the strictly lower part is never read
-  double *out = S.MT + (int64_t)j * n + i;
+  const int mgi = S.bat_mgi[q];
+  const double *pops = pops0 + (int64_t)S.bat_a[q] * K.T.nlevels_total;
+  const double *nnion_q = S.nnion + (int64_t)q * K.T.nions_total;
+  const int32_t *incl_q = S.incl + (int64_t)q * K.T.nions_total;
+  double *out = S.MT + (int64_t)q * n * n + (int64_t)j * n + i;
   const double DE = S.DE;
   const double en = S.envec[i];
   double m = 0.;
@@ -434,8 +449,8 @@ __global__ __launch_bounds__(256) void k_sf_matrix(Ctx K, NlDev N, SfDev S, int 
   const double endash = S.envec[j];
   const bool in_band = j - i <= S.band;
   for (int ui = 0; ui < K.T.nions_total; ui++) {
-    if (!S.incl[ui]) continue;
-    const double nnion = S.nnion[ui];
+    if (!incl_q[ui]) continue;
+    const double nnion = nnion_q[ui];
     // excitation: the band j - i <= max stop - start of the ion's transitions
     if (in_band) {
       for (int t = S.ion_tr_off[ui]; t < S.ion_tr_off[ui + 1]; t++) {
@@ -484,56 +499,103 @@ __global__ __launch_bounds__(256) void k_sf_matrix(Ctx K, NlDev N, SfDev S, int 
 
 // Upper-triangular solve M v = v in place (GSL LU_svx with the identity permutation: the unit-lower solve is the
 // identity; D11's column-oriented back substitution).  One workgroup; v staged in LDS.  Columns in blocks of 64 from
-// the right: wave 0 finishes the block's own unknowns (lane r holds x_{j0+r}; for each column j, top-down, x_j is
-// divided by the diagonal and broadcast, the block rows above it updated), then every row above the block receives the
-// block's 64 subtractions in descending column order -- per x_i the same sequence as the unblocked loop.
-__global__ __launch_bounds__(SF_WG) void k_sf_backsub(const double *__restrict__ MT, int n, double *v) {
+// the right: the block's 64 x 64 diagonal tile is staged in LDS by the whole workgroup, wave 0 finishes the block's own
+// unknowns from it (lane r holds x_{j0+r}; for each column j, top-down, x_j is divided by the diagonal and broadcast,
+// the block rows above it updated), then every row above the block receives the block's 64 subtractions in
+// descending column order -- per x_i the same sequence as the unblocked loop.
+__global__ __launch_bounds__(SF_WG) void k_sf_backsub(const double *__restrict__ MT0, int n, double *v0) {
+  const double *MT = MT0 + (int64_t)blockIdx.x * n * n;  // one workgroup per batch slot
+  double *v = v0 + (int64_t)blockIdx.x * n;
   __shared__ double x[SF_NMAX];
+  __shared__ double tile[64 * 65];  // tile[c * 65 + r] = M[j0 + r][j0 + c], padded against bank conflicts
   for (int i = threadIdx.x; i < n; i += SF_WG) x[i] = v[i];
-  __syncthreads();
   const int nblk = (n + 63) / 64;
   for (int jb = nblk - 1; jb >= 0; jb--) {
     const int j0 = jb * 64;
     const int j1 = min(j0 + 64, n);
+    for (int q = threadIdx.x; q < 64 * 64; q += SF_WG) {
+      const int c = q >> 6, r = q & 63;
+      if (j0 + c < j1 && r <= c) tile[c * 65 + r] = MT[(int64_t)(j0 + c) * n + j0 + r];
+    }
+    __syncthreads();
     if (threadIdx.x < 64) {
       const int lane = threadIdx.x;
       const int r = j0 + lane;
       double xr = r < j1 ? x[r] : 0.;
       for (int j = j1 - 1; j >= j0; j--) {
-        if (r == j) xr = xr / MT[(int64_t)j * n + j];
-        const double xj = __shfl(xr, j - j0, 64);
-        if (r < j) xr -= MT[(int64_t)j * n + r] * xj;
+        const int c = j - j0;
+        if (lane == c) xr = xr / tile[c * 65 + c];
+        const double xj = __shfl(xr, c, 64);
+        if (lane < c) xr -= tile[c * 65 + lane] * xj;
       }
       if (r < j1) x[r] = xr;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < j0; i += SF_WG) {
-      double xi = x[i];
-      for (int j = j1 - 1; j >= j0; j--) xi -= MT[(int64_t)j * n + i] * x[j];
-      x[i] = xi;
+    // rows above the block: up to 4 rows per workitem as independent chains, the column loads unrolled
+    for (int i0 = threadIdx.x; i0 < j0; i0 += 4 * SF_WG) {
+      double xr[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) xr[k] = (i0 + k * SF_WG < j0) ? x[i0 + k * SF_WG] : 0.;
+#pragma unroll 8
+      for (int j = j1 - 1; j >= j0; j--) {
+        const double xj = x[j];
+        const double *col = MT + (int64_t)j * n;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (i0 + k * SF_WG < j0) xr[k] -= col[i0 + k * SF_WG] * xj;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (i0 + k * SF_WG < j0) x[i0 + k * SF_WG] = xr[k];
     }
     __syncthreads();
   }
   for (int i = threadIdx.x; i < n; i += SF_WG) v[i] = x[i];
 }
-// res = M x - b (gsl_blas_dgemv, beta -1: res_i = -b_i + sum_{j >= i} x_j M_ij in j order); a workitem per row
-__global__ __launch_bounds__(256) void k_sf_residual(const double *__restrict__ MT, int n, const double *__restrict__ xv,
-                                                     const double *__restrict__ b, double *res) {
+// res = M x - b (gsl_blas_dgemv, beta -1): res_i = -b_i + sum_{j >= i} x_j M_ij.  The row sums are split into
+// SF_RCHUNK-column chunks, each summed serially (k_sf_residual_part, workitem = (row, chunk): coalesced over the
+// column-major matrix and enough waves to fill the chip), then the chunks added in column order (k_sf_residual_sum).
+#define SF_RCHUNK 256
+__global__ __launch_bounds__(256) void k_sf_residual_part(const double *__restrict__ MT0, int n,
+                                                          const double *__restrict__ xv0, double *part0) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.y;
+  if (i >= n) return;
+  const int q = blockIdx.z;
+  const int nch = (n + SF_RCHUNK - 1) / SF_RCHUNK;
+  const double *MT = MT0 + (int64_t)q * n * n;
+  const double *xv = xv0 + (int64_t)q * n;
+  double *part = part0 + (int64_t)q * nch * n;
+  const int ja = max(i, c * SF_RCHUNK), jb = min(n, (c + 1) * SF_RCHUNK);
+  double temp = 0.;
+#pragma unroll 8
+  for (int j = ja; j < jb; j++) temp += xv[j] * MT[(int64_t)j * n + i];
+  part[(int64_t)c * n + i] = temp;
+}
+__global__ __launch_bounds__(256) void k_sf_residual_sum(int n, const double *__restrict__ part0,
+                                                         const double *__restrict__ b, double *res0) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const int nch = (n + SF_RCHUNK - 1) / SF_RCHUNK;
+  const int q = blockIdx.y;
+  const double *part = part0 + (int64_t)q * nch * n;
+  double *res = res0 + (int64_t)q * n;
   double temp = 0.;
-  for (int j = i; j < n; j++) temp += xv[j] * MT[(int64_t)j * n + i];
+  for (int c = i / SF_RCHUNK; c < nch; c++) temp += part[(int64_t)c * n + i];
   res[i] = -b[i] + temp;
 }
 // x += -1 * work (gsl_blas_daxpy in gsl_linalg_LU_refine)
 __global__ void k_sf_axpy(int n, double *xv, const double *__restrict__ work) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) xv[i] += -1.0 * work[i];
+  const int64_t i = (int64_t)blockIdx.y * n + blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x * blockDim.x + threadIdx.x < n) xv[i] += -1.0 * work[i];
 }
 // nonthermal.cc:2490-2510: error = |res| at gsl_blas_idamax (first index of the largest), the best x so far kept;
 // errbest < 0: none yet.  One workgroup.
-__global__ __launch_bounds__(1024) void k_sf_best(int n, const double *__restrict__ res, const double *__restrict__ xv,
-                                                  double *best, double *errbest) {
+__global__ __launch_bounds__(1024) void k_sf_best(int n, const double *__restrict__ res0,
+                                                  const double *__restrict__ xv0, double *best0, double *errbest0) {
+  const int64_t off = (int64_t)blockIdx.x * n;  // one workgroup per batch slot
+  const double *res = res0 + off, *xv = xv0 + off;
+  double *best = best0 + off, *errbest = errbest0 + blockIdx.x;
   __shared__ double s_v[1024];
   __shared__ int s_i[1024];
   __shared__ int s_take;
@@ -572,9 +634,11 @@ __global__ __launch_bounds__(1024) void k_sf_best(int n, const double *__restric
 
 // analyse_sf_solution's dot products (nonthermal.cc:1333-1360 calculate_nt_frac_ionization_shell: y . xs_shell;
 // 1714-1744 calculate_nt_excitation_ratecoeff_perdeposition: xs_trans . y), one workitem each, serial in j
-__global__ void k_sf_dots(SfDev S, const double *__restrict__ y) {
+__global__ void k_sf_dots(SfDev S, const double *__restrict__ y0) {
   const int item = blockIdx.x * blockDim.x + threadIdx.x;
   if (item >= S.nitems) return;
+  const int q = blockIdx.y;
+  const double *y = y0 + (int64_t)q * S.n;
   const int nsh = S.nsh;
   double dot = 0.;
   if (item < nsh) {
@@ -584,7 +648,7 @@ __global__ void k_sf_dots(SfDev S, const double *__restrict__ y) {
     const int t = item - nsh;
     for (int j = 0; j < S.n; j++) dot += sf_xs_exc(S, t, j) * y[j];
   }
-  S.dots[item] = dot;
+  S.dots[(int64_t)q * S.nitems + item] = dot;
 }
 
 // nonthermal.cc:1311-1331 get_oneoverw (the ion's mean binding energy from the host, get_mean_binding_energy)
@@ -599,18 +663,22 @@ DEVFN double sf_oneoverw(const Ctx &K, const NlDev &N, const SfDev &S, int ui, i
 
 // nonthermal.cc:1996-2280 analyse_sf_solution (NT_EXCITATION_ON false, D12) with calculate_eff_ionpot_auger_rates
 // (1430-1556) for one cell: the per-ion combination of k_sf_dots' products, one workitem, the reference's order
-__global__ void k_sf_combine(Ctx K, NlDev N, SfDev S, int mgi, const double *__restrict__ pops) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+__global__ void k_sf_combine(Ctx K, NlDev N, SfDev S, const double *__restrict__ pops0, int nbat) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nbat) return;
+  const int mgi = S.bat_mgi[q];
+  const double *pops = pops0 + (int64_t)S.bat_a[q] * K.T.nlevels_total;
   const int ni = K.T.nions_total;
+  const double *dots = S.dots + (int64_t)q * S.nitems;
   const double DE = S.DE, E_init_ev = S.E_init_ev;
-  const double tot_nion = S.tot_nion[0];
+  const double tot_nion = S.tot_nion[q];
   double frac_excitation_total = 0., frac_ionization_total = 0.;
   bool bad = false;
   for (int e = 0; e < K.T.nelements; e++) {
     const int nions = K.T.elem_nions[e];
     for (int i = 0; i < nions; i++) {
       const int u = uion(K, e, i);
-      const double nnion = S.nnion[u];
+      const double nnion = S.nnion[(int64_t)q * ni + u];
       if (nnion <= 0.) continue;
       // calculate_eff_ionpot_auger_rates
       float *prob = N.nt_prob + ((int64_t)mgi * ni + u) * NL_A1;
@@ -626,7 +694,7 @@ __global__ void k_sf_combine(Ctx K, NlDev N, SfDev S, int mgi, const double *__r
       double eta_over_ionpot_sum = 0., eta_sum = 0.;
       const int r0 = S.ion_sh_off[u], r1 = S.ion_sh_off[u + 1];
       for (int r = r0; r < r1; r++) {
-        const double frac_ionization_shell = nnion * S.sh_ionpot_ev[r] * (S.dots[r] * DE) / E_init_ev;
+        const double frac_ionization_shell = nnion * S.sh_ionpot_ev[r] * (dots[r] * DE) / E_init_ev;
         eta_sum += frac_ionization_shell;
         const double ionpot_shell = S.sh_ionpot_ev[r] * ARTIS_EV;
         const double eta_over_ionpot = frac_ionization_shell / ionpot_shell;
@@ -664,7 +732,7 @@ __global__ void k_sf_combine(Ctx K, NlDev N, SfDev S, int mgi, const double *__r
       }
       // the ion's ionisation and excitation fractions
       double frac_ionization_ion = 0., frac_excitation_ion = 0.;
-      for (int r = r0; r < r1; r++) frac_ionization_ion += nnion * S.sh_ionpot_ev[r] * (S.dots[r] * DE) / E_init_ev;
+      for (int r = r0; r < r1; r++) frac_ionization_ion += nnion * S.sh_ionpot_ev[r] * (dots[r] * DE) / E_init_ev;
       if (i < nions - 1) {
         N.nt_fracdep[(int64_t)mgi * ni + u] = frac_ionization_ion;
         frac_ionization_total += frac_ionization_ion;
@@ -673,7 +741,7 @@ __global__ void k_sf_combine(Ctx K, NlDev N, SfDev S, int mgi, const double *__r
       }
       for (int t = S.ion_tr_off[u]; t < S.ion_tr_off[u + 1]; t++) {
         const double nnlevel = pops[S.tr_ul[t]];
-        const double ratecoeff = (S.dots[S.nsh + t] * DE) / E_init_ev / ARTIS_EV;
+        const double ratecoeff = (dots[S.nsh + t] * DE) / E_init_ev / ARTIS_EV;
         const double nt_frac_excitation_perlevelpop = S.tr_eps[t] * ratecoeff;
         frac_excitation_ion += nnlevel * nt_frac_excitation_perlevelpop;
       }

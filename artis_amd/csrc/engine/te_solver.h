@@ -691,10 +691,16 @@ __global__ void k_te_bfheat(Ctx K, TeDev D) {
 
 // one wave = 64 / g cells, g lanes each (g a power of two); every lane of a group runs its cell's solution
 __global__ __launch_bounds__(64, 4) void k_te_solve(const Ctx *__restrict__ Kp, const TeDev *__restrict__ Dp, int g) {
-  // context and parameters by device pointer: the solver's functions are not inlined (register pressure), and a
-  // by-value kernel argument referenced from them would be copied to scratch
-  const Ctx &K = *Kp;
-  const TeDev &D = *Dp;
+  // context and parameters by device pointer, copied into LDS: the solver's functions are not inlined (register
+  // pressure), and a by-value kernel argument referenced from them would be copied to scratch; read through the
+  // global copies every table pointer was a dependent global load in the per-line loops
+  CTX_IN_LDS(Kp);
+  __shared__ TeDev s_dev;
+  static_assert(sizeof(TeDev) % 8 == 0, "TeDev is copied in 8-byte words");
+  for (int i = threadIdx.x; i < (int)(sizeof(TeDev) / 8); i += blockDim.x)
+    reinterpret_cast<uint64_t *>(&s_dev)[i] = reinterpret_cast<const uint64_t *>(Dp)[i];
+  __syncthreads();
+  const TeDev &D = s_dev;
   const int lane = threadIdx.x;
   const int k = blockIdx.x * (64 / g) + lane / g;
   if (k >= D.ncells) return;  // whole groups leave together

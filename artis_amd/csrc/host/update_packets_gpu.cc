@@ -37,6 +37,11 @@ void PacketEngine::solve_temperatures(const artis_te_tables &tables, const artis
   check(artis_gpu_solve_temperatures(&tables, &params, &cells), "artis_gpu_solve_temperatures");
 }
 
+void PacketEngine::update_grid_nlte(const artis_nt_shells *shells, const artis_nlte_params &params,
+                                    artis_nlte_cells &cells) {
+  check(artis_gpu_update_grid_nlte(shells, &params, &cells), "artis_gpu_update_grid_nlte");
+}
+
 void PacketEngine::prepare_temperatures(const artis_te_tables &tables, const artis_te_params &params,
                                         const artis_ug_prepare &prep, const artis_te_cells &cells) {
   check(artis_gpu_prepare_temperatures(&tables, &params, &prep, &cells), "artis_gpu_prepare_temperatures");

@@ -51,6 +51,9 @@ class PacketEngine {
   // solve_temperatures, written to prep's *_out arrays
   void prepare_temperatures(const artis_te_tables &tables, const artis_te_params &params, const artis_ug_prepare &prep,
                             const artis_te_cells &cells);
+  // update_grid for the nebular options (artis_gpu_update_grid_nlte: update_grid.cc:1012-1205 with
+  // solve_Te_nltepops, nltepop.cc, nonthermal.cc's Spencer-Fano solution), cells in place
+  void update_grid_nlte(const artis_nt_shells *shells, const artis_nlte_params &params, artis_nlte_cells &cells);
 
   double last_transport_ms() const;
 };

@@ -797,3 +797,27 @@ class NlteArrays:
                 setattr(o, k, v.copy())
         o.params = NlteParams.from_buffer_copy(self.params)
         return o
+
+    # the artis_cell_state arrays the next transport step reads (update_grid's outputs)
+    _CELLSTATE = [("Te", "Te", C.c_float), ("TR", "TR", C.c_float), ("TJ", "TJ", C.c_float), ("W", "W", C.c_float),
+                  ("nne", "nne", C.c_float), ("nnetot", "nnetot", C.c_float),
+                  ("groundlevelpop", "groundlevelpop", C.c_float), ("partfunct", "partfunct", C.c_float),
+                  ("totalcooling", "totalcooling", C.c_double), ("cooling_contrib_ion", "cooling_contrib_ion", C.c_double),
+                  ("nlte_pops", "nlte_pops", C.c_double), ("radfield_bin_TR", "bin_TR", C.c_float),
+                  ("radfield_bin_W", "bin_W", C.c_float), ("bfrate_estimator", "bfrate_estimator", C.c_float),
+                  ("nt_deposition_rate_density", "deposition_rate_density", C.c_double),
+                  ("nt_ionization_ratecoeff", "nt_ionization_ratecoeff", C.c_double),
+                  ("nt_prob_num_auger", "nt_prob_num_auger", C.c_float),
+                  ("nt_ionenfrac_num_auger", "nt_ionenfrac_num_auger", C.c_float)]
+
+    def apply_to_cellstate(self, model):
+        """Write this block's solution into the model's cell state (in place), as update_grid leaves the grid for
+        the next update_packets."""
+        cs = CellState.from_address(model.cellstate)
+        for field, attr, ct in self._CELLSTATE:
+            src = getattr(self, attr)
+            ptr = getattr(cs, field)
+            if not ptr:
+                continue
+            view = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), (src.size,))
+            view[:] = src

@@ -15,6 +15,7 @@ import numpy as np
 import pytest
 
 import oracle_lib
+import parity
 from artis_amd import Engine, ffi
 from artis_amd.model import Model
 
@@ -283,3 +284,26 @@ def test_update_grid_nlte_subset_roundtrip():
             assert np.array_equal(g.reshape(m.npts_model, -1)[untouched], b0.reshape(m.npts_model, -1)[untouched]), f
         else:
             assert np.array_equal(g[untouched], b0[untouched]), f
+
+
+def test_transport_reads_the_gpu_solution():
+    """The next update_packets from the GPU's nebular update_grid output (NLTE / superlevel populations, the fitted
+    bins, the bf-rate estimators, the Spencer-Fano rates and Auger fractions, cooling): the engine's transport and
+    the oracle's, both reading that state, agree packet by packet (tests/parity.py)."""
+    m, p, nt, arr, nts = _onezone_case(4, pinned=False)
+    eng = Engine(m, params=p)
+    try:
+        ag = arr.copy()
+        eng.update_grid_nlte(nt, ag)
+        assert (ag.nlte_pops > -0.9).any() and (ag.bin_W > 0).any()
+        ag.apply_to_cellstate(m)
+        eng.upload_cellstate(nts)
+        pk = m.init_rpackets(nts, 4000, seed=91)
+        pg, po = pk.copy(), pk.copy()
+        eg = eng.update_packets(nts, pg)
+    finally:
+        eng.close()
+    eo, wo = oracle_lib.update_packets(m, nts, po, params=p, nthreads=16)
+    parity.assert_packets_match(pg, po)
+    parity.assert_estimators_match(eg, eo)
+    assert eo.radfield_count.sum() > 0
