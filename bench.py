@@ -147,6 +147,65 @@ def dry_launch(world, rank):
     del torch
 
 
+def nebular_update_grid(rank, cpu, progress):
+    """SURVEY §8(f) row 4 for the nebular options (artis_gpu_update_grid_nlte): update_grid of BASELINE config 3's
+    nebularonezone inputs and of every cell of a 136-cell synthetic nebular model (each with its Spencer-Fano solution),
+    from the raw estimators of a GPU transport step; the oracle on the same inputs for the CPU time and parity."""
+    from artis_amd import Engine, ffi
+    from artis_amd.model import Model
+
+    ref = os.path.join(REPO, "tests", "golden", "ref_inputs", "nebularonezone")
+    out = {}
+    cases = {
+        "onezone": dict(files=(os.path.join(ref, "input-newrun.txt"), os.path.join(ref, "model.txt"),
+                               os.path.join(ref, "abundances.txt")), ngrid_1d=10, nlevels_per_ion=30, n_ionising=10,
+                        max_lines=2000, nebular=1, nlte_level_max=12, ionpot_scale=0.5),
+        "synthetic_136_cells": dict(ngrid_1d=6, nlevels_per_ion=30, n_ionising=10, max_lines=2000, ntstep=20, nebular=1,
+                                    nlte_level_max=12, tmin_days=100., tmax_days=300., T0=6000., ionpot_scale=0.5),
+    }
+    for name, kw in cases.items():
+        m = Model(**kw)
+        nts = 6 if name == "onezone" else 12
+        p = ffi.RunParams.from_buffer_copy(m.params)
+        eng = Engine(m, params=p)
+        m.set_timestep(nts - 1)
+        eng.upload_cellstate(nts - 1)
+        est = eng.update_packets(nts - 1, m.init_rpackets(nts - 1, 20000 if name == "onezone" else 8000, seed=5))
+        m.set_timestep(nts)
+        nt = ffi.NtDataHandle(m)
+        arr = ffi.NlteArrays(m, nts, est=est, dep_scale=3e-4 if name == "onezone" else 1.0, seed=12)
+        arr.params.num_lte_timesteps = 4 if name == "onezone" else 2
+        eng.update_grid_nlte(nt, arr.copy())  # warm
+        ag = arr.copy()
+        ms = eng.update_grid_nlte(nt, ag)
+        eng.close()
+        cells = arr.mgi_list
+        rec = {"cells": int(len(cells)), "timestep": nts, "gpu_ms": ms, "passes_max": int(ag.iters[cells].max()),
+               "spencer_fano_sfpts": 4096}
+        if cpu:
+            sys.path.insert(0, os.path.join(REPO, "tests"))
+            import oracle_lib
+
+            nthreads, _ = cpu_share()
+            sub = arr.copy()
+            sub.mgi_list = cells[:: max(1, len(cells) // 8)][:8].copy()
+            t = time.perf_counter()
+            oracle_lib.update_grid_nlte(m, nt, sub, params=p, nthreads=nthreads)
+            dt = time.perf_counter() - t
+            g = sub.mgi_list
+            rec["cpu_baseline"] = {"cells": int(len(g)), "seconds": dt, "threads": nthreads, "kind": "port",
+                                   "cells_per_s": len(g) / dt}
+            rec["gpu_cells_per_s"] = len(cells) / (ms / 1e3)
+            rec["parity_sample"] = {"cells": int(len(g)),
+                                    "max_Te_rel": float(np.max(np.abs(ag.Te[g] - sub.Te[g]) / sub.Te[g])),
+                                    "max_nne_rel": float(np.max(np.abs(ag.nne[g] - sub.nne[g]) / sub.nne[g])),
+                                    "passes_equal": float(np.mean(ag.iters[g] == sub.iters[g]))}
+        out[name] = rec
+        progress(f"nebular update_grid {name}: {ms:.0f} ms")
+        m.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -364,6 +423,11 @@ def main():
             ugrid["gpu_cells_per_s"] = len(te.mgi_list) / (te_ms / 1e3)
             ugrid["parity_sample"] = {"cells": int(len(g)), "iterations_and_Te_agree": float(agree.mean())}
 
+    eng.close()
+    neb = None
+    if rank == 0 and not args.no_update_grid and vcfg is None:
+        neb = nebular_update_grid(rank, not args.no_cpu_baseline, progress)
+
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -419,6 +483,8 @@ def main():
         }
         if ugrid is not None:
             line["update_grid"] = ugrid
+        if neb is not None:
+            line["update_grid_nebular"] = neb
         if vcfg is not None:
             vms = float(np.mean([v[0] for v in vstats]))
             line["config"]["workload"] += (f"; virtual packets: {vcfg.nobs} observers x {vcfg.nspectra} spectra, "
@@ -429,7 +495,6 @@ def main():
             ntr = max(line["vpkt"]["traces"], 1)
             line["vpkt"]["work_per_trace"] = {k: float(np.mean([w[k] for w in vwork])) / ntr for k in vwork[0]}
         print(json.dumps(line), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
 
