@@ -1104,6 +1104,8 @@ bool nlte_matrix_solve(const double *A, const double *b, int n, double *popvec, 
   return true;
 }
 
+thread_local std::vector<double> tl_raw_matrix;  // the last rate matrix before normalisation (ORACLE_NL_DUMP)
+
 // the element's rate matrix, normalised, column-major, with its balance vector and LTE normalisation
 // (nltepop.cc:391-628, 832-920): the five process matrices summed in the reference's order (NT excitation is zero,
 // NT_EXCITATION_ON false)
@@ -1224,6 +1226,7 @@ int nlte_build(const Ctx &c, const NlteRun &r, int mgi, int e, std::vector<doubl
   }
   A.assign((size_t)D * D, 0.);
   for (size_t q = 0; q < A.size(); q++) A[q] = ((((A[q] + rad_bb[q]) + coll_bb[q]) + rad_bf[q]) + coll_bf[q]) + ntcoll_bf[q];
+  if (getenv("ORACLE_NL_DUMP")) tl_raw_matrix = A;  // diagnostics: the rate matrix before normalisation
   for (int col = 0; col < D; col++) A[(size_t)col * D + 0] = 1.0;  // normalisation row
   b.assign(D, 0.);
   b[0] = nl_elem_numberdens(c, r, mgi, e);
@@ -1269,6 +1272,7 @@ int nl_solve_nlte_pops_element(const Ctx &c, const NlteRun &r, int e, int mgi, s
       fwrite(b.data(), 8, b.size(), fp);
       fwrite(norm.data(), 8, norm.size(), fp);
       fwrite(popvec.data(), 8, popvec.size(), fp);
+      fwrite(tl_raw_matrix.data(), 8, tl_raw_matrix.size(), fp);
       fclose(fp);
     }
   }
@@ -1469,5 +1473,41 @@ int oracle_update_grid_nlte(const artis_atomic_tables *at, const artis_run_param
     if (in->nlte_iterations) in->nlte_iterations[mgi] = iters;
   }
   return rc;
+}
+
+// ---- pins of the restated numerical kernels (tests/test_nebular_update_grid.py) ----
+// nltepop_matrix_solve (LU with partial pivoting, refinement, D11) on a column-major n x n system, unit
+// normalisation; returns 1 if singular
+int oracle_nl_matrix_solve(const double *A, const double *b, int n, double *x) {
+  std::vector<double> norm(n, 1.);
+  return nlte_matrix_solve(A, b, n, x, norm.data()) ? 0 : 1;
+}
+// sfmatrix_solve on a row-major upper-triangular n x n system
+void oracle_sf_solve(const double *U, const double *b, int n, double *y) { sf_solve(U, b, n, y); }
+// radfield.cc planck_integral (GSL qag restated, epsrel 1e-10)
+double oracle_planck_integral(double T_R, double nu_lower, double nu_upper, int times_nu) {
+  return nl_planck_integral(T_R, nu_lower, nu_upper, times_nu != 0);
+}
+// the Spencer-Fano energy grid, source and loss terms: envec, sourcevec, the right-hand side and the loss diagonal
+// for an electron density nne; returns E_init_ev
+double oracle_sf_grid(int sfpts, double emin, double emax, double nne, double *envec, double *sourcevec, double *rhs,
+                      double *loss_diag) {
+  artis_nt_shells nt;
+  memset(&nt, 0, sizeof(nt));
+  nt.sfpts = sfpts;
+  nt.sf_emin = emin;
+  nt.sf_emax = emax;
+  SfGrid g;
+  sf_setup(g, &nt);
+  for (int i = 0; i < g.n; i++) {
+    envec[i] = g.envec[i];
+    sourcevec[i] = g.sourcevec[i];
+    double dasum = 0.;
+    if (i < g.n - 1)
+      for (int j = i + 1; j < g.n; j++) dasum += fabs(g.sourcevec[j]);
+    rhs[i] = (i < g.n - 1) ? dasum * g.delta_e : 0.;
+    loss_diag[i] = sf_electron_loss_rate(g.envec[i] * ARTIS_EV, nne) / ARTIS_EV;
+  }
+  return g.E_init_ev;
 }
 }  // extern "C"
