@@ -29,7 +29,7 @@ ABI_SYMBOLS = [
     "artis_estimator_block_average_scalars",
     "artis_gpu_comm_unique_id", "artis_gpu_comm_init", "artis_gpu_estimators_allreduce", "artis_gpu_comm_finalize",
     "artis_gpu_solve_temperatures", "artis_gpu_last_te_ms", "artis_gpu_prepare_temperatures",
-    "artis_gpu_update_grid_nlte", "artis_gpu_last_nlte_ms",
+    "artis_gpu_update_grid_nlte", "artis_gpu_last_nlte_ms", "artis_gpu_table_info",
 ]
 
 _gpu_lib = None
@@ -73,6 +73,7 @@ def gpu_lib():
         L.artis_gpu_last_transport_ms.restype = C.c_double
         L.artis_gpu_last_precompute_ms.restype = C.c_double
         L.artis_gpu_last_work_counts.argtypes = [vp]
+        L.artis_gpu_table_info.argtypes = [vp]
         L.artis_gpu_last_error.restype = C.c_char_p
         L.artis_gpu_last_rounds.restype = C.c_int64
         L.artis_gpu_spectrum.argtypes = [C.c_int, C.c_int, vp, vp, vp]
@@ -212,6 +213,14 @@ class Engine:
         w = np.zeros(ffi.ARTIS_WORK_COUNT, dtype=np.int64)
         self.lib.artis_gpu_last_work_counts(w.ctypes.data)
         return w
+
+    def table_info(self):
+        """Per-cell table coverage: {"cells", "linecoef_rows", "linecoef_bytes", "macache_rows", "macache_bytes",
+        "marates_bytes"} (artis_gpu_table_info)."""
+        w = np.zeros(8, dtype=np.int64)
+        self._check(self.lib.artis_gpu_table_info(w.ctypes.data), "table_info")
+        return dict(zip(("cells", "linecoef_rows", "linecoef_bytes", "macache_rows", "macache_bytes",
+                         "marates_bytes", "ma_activations_cached", "ma_activations"), (int(x) for x in w)))
 
     def spectrum(self, nnubins=1000, nprocs=1):
         """Device-binned spectrum [ntstep, nnubins] and light curves (lum, lumcmf) of the resident packets."""

@@ -260,19 +260,22 @@ __global__ void k_cooling(Ctx K) {
 // consecutive doubles); k_mapack then turns them into the compact key records.  Scratch positions:
 //   [9 totals | internal_down_same (nd) | internal_up_same (nu) | rad_deexc (nd) | rad_recomb (nr) |
 //    internal_down_lower (nr) | internal_up_higher (nt)]     (each array in the reference's order)
-__global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict__ S) {
+// One launch covers the kn cells cells[0 .. kn): the cached cells (row order) with cache = true (scratch stride
+// kn), the others with cache = false (totals into marates).
+__global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict__ S, const int32_t *__restrict__ cells,
+                          int kn, bool cache) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nl = K.T.nlevels_total;
   const int64_t nne_cells = K.C.n_nonempty;
-  if (idx >= nne_cells * nlev) return;
-  const int ul = ul0 + (int)(idx / nne_cells);
-  const int k = (int)(idx % nne_cells);
+  if (idx >= (int64_t)kn * nlev) return;
+  const int ul = ul0 + (int)(idx / kn);
+  const int kr = (int)(idx % kn);
+  const int k = cells[kr];
   const int mgi = K.C.ne_mgi[k];
   const double t_mid = K.G.ts_mid[nts];
-  const bool cache = K.C.have_macache;
   const MaMeta mm = K.T.ma_meta[ul];
-  double *rec = cache ? S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * nne_cells + k : nullptr;
-#define REC(p) rec[(int64_t)(p) * nne_cells]
+  double *rec = cache ? S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * kn + kr : nullptr;
+#define REC(p) rec[(int64_t)(p) * kn]
   const int cum_d = ARTIS_MA_ACTION_COUNT, cum_u = ARTIS_MA_ACTION_COUNT + mm.nd;
   const int cum_drad = ARTIS_MA_ACTION_COUNT + mm.nd + mm.nu, cum_rrad = cum_drad + mm.nd;
   const int cum_rint = cum_rrad + mm.nr, cum_uhi = cum_rint + mm.nr;
@@ -319,7 +322,7 @@ __global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, const double *__
   __shared__ double s_norm[ARTIS_MA_ACTION_COUNT][64];  // action totals per cell
   __shared__ uint32_t s_akey[ARTIS_MA_ACTION_COUNT][64];
   const int ul = ul0 + blockIdx.y;
-  const int64_t n_ne = K.C.n_nonempty;
+  const int64_t n_ne = K.C.ma_rows;  // the cached cells, the scratch's stride
   const MaMeta mm = K.T.ma_meta[ul];
   const int len = ARTIS_MA_ACTION_COUNT + 2 * mm.nd + mm.nu + 2 * mm.nr + mm.nt;
   const MaLayout lay = ma_layout(mm.nd, mm.nu, mm.nr, mm.nt);
@@ -379,7 +382,7 @@ __global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, const double *__
 __global__ __launch_bounds__(256) void k_linecoef(Ctx K) {
   const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (li >= K.C.linecoef_stride) return;
-  for (int k = blockIdx.y; k < K.C.n_nonempty; k += gridDim.y) {
+  for (int k = blockIdx.y; k < K.C.linecoef_rows; k += gridDim.y) {
     double v = 0.;
     if (li < K.T.nlines) {
       const LineTau r = K.T.line_tau[li];
@@ -534,6 +537,13 @@ struct Engine {
   bool ma_cache_ok = true;             // the atomic data fit the cache's record layout (engine_dev.h ma_layout)
   std::vector<int64_t> h_dbl_off;     // per level: offset (doubles) of its exact sums in the k_marates scratch
   double *d_marec_scratch = nullptr;  // k_marates output, [position][cell] per level (k_mapack input)
+  // macro-atom key-record placement (DevCells::ma_row / ma_bin): the cell of each bin (the cached cells, row
+  // order, then the rest), and with a partial cache the per-cell count of M-queue entries since the last placement
+  int32_t *d_ma_row = nullptr, *d_ma_bin = nullptr, *d_ma_bincell = nullptr;
+  uint32_t *d_ma_hist = nullptr;
+  std::vector<int32_t> h_ma_bincell;
+  int64_t ma_acts_cached = 0, ma_acts_total = 0;  // activations in cached cells / all, before the last re-placement
+  bool ma_hist_ready = false;
   int64_t marec_scratch_doubles = 0;
   double *d_estblock = nullptr;
   int32_t *d_target_ul = nullptr, *d_target_t = nullptr;
@@ -623,6 +633,42 @@ int dupload(const T **dst, const T *src, size_t count) {
   if (count && src) HIPCHK(hipMemcpy(d, src, count * sizeof(T), hipMemcpyHostToDevice));
   *dst = d;
   return 0;
+}
+
+// Give the macro-atom key records to the first ma_rows cells of `order` (the rest walk without records) and lay
+// the M-queue bins out cached cells first (DevCells::ma_row / ma_bin).  Placement never changes a result.
+int ma_place(const std::vector<int32_t> &order) {
+  const int n = G.K.C.n_nonempty, R = G.K.C.ma_rows;
+  std::vector<int32_t> row(n, -1), bin(n);
+  G.h_ma_bincell.assign(order.begin(), order.end());
+  for (int b = 0; b < n; b++) {
+    const int k = order[b];
+    if (b < R) row[k] = b;
+    bin[k] = b;
+  }
+  HIPCHK(hipMemcpy(G.d_ma_row, row.data(), n * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(G.d_ma_bin, bin.data(), n * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(G.d_ma_bincell, order.data(), n * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(G.d_ma_hist, 0, n * sizeof(uint32_t)));
+  G.ma_hist_ready = false;
+  return 0;
+}
+
+// With a partial key cache: re-place the records on the cells that received the most macro-atom activations
+// since the last placement (ties: the current order), before the precompute builds them.
+int ma_replace() {
+  const int n = G.K.C.n_nonempty;
+  if (!G.ma_hist_ready || G.K.C.ma_rows <= 0 || G.K.C.ma_rows >= n) return 0;
+  std::vector<uint32_t> h(n);
+  HIPCHK(hipMemcpy(h.data(), G.d_ma_hist, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  std::vector<int32_t> order = G.h_ma_bincell;
+  G.ma_acts_cached = G.ma_acts_total = 0;
+  for (int b = 0; b < n; b++) {
+    G.ma_acts_total += h[order[b]];
+    if (b < G.K.C.ma_rows) G.ma_acts_cached += h[order[b]];
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return h[a] > h[b]; });
+  return ma_place(order);
 }
 
 int64_t sum_i32(const int32_t *a, int n) {
@@ -818,6 +864,13 @@ int vpkt_collect(const unsigned long long before[8]) {
   return 0;
 }
 
+// activations per cell for the next placement of the key records: hist[cell of bin b] += count of bin b
+__global__ void k_ma_hist(const uint32_t *__restrict__ bins, const int32_t *__restrict__ bincell,
+                          uint32_t *__restrict__ hist, int n) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < n && bins[b]) hist[bincell[b]] += bins[b];
+}
+
 #define WAVE_MAX_ROUNDS 10000000
 int run_wavefront(int64_t n, int nts, double t2) {
   WaveState W = G.W;
@@ -858,6 +911,10 @@ int run_wavefront(int64_t n, int nts, double t2) {
       const int nne = G.K.C.n_nonempty;
       HIPCHK(hipMemsetAsync(W.bins, 0, (size_t)(nne + 1) * sizeof(uint32_t), G.stream));
       k_ma_bin<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa);
+      if (G.K.C.have_macache && G.K.C.ma_rows < nne) {
+        k_ma_hist<<<(unsigned)((nne + 255) / 256), 256, 0, G.stream>>>(W.bins, G.d_ma_bincell, G.d_ma_hist, nne);
+        G.ma_hist_ready = true;
+      }
       HIPCHK(hipcub::DeviceScan::ExclusiveSum(G.d_scan_tmp, G.scan_tmp_bytes, W.bins, G.d_binoffs, nne + 1,
                                               G.stream));
       k_ma_scatter<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, G.d_binoffs);
@@ -874,14 +931,19 @@ int run_wavefront(int64_t n, int nts, double t2) {
       return (v >= 1 && v <= 8) ? v : 4;
     }();
     const unsigned ma_grid = ma_waves ? (unsigned)(G.wave_grid / 8 * ma_waves) : grid;
+    // a partial key cache: the binned queue's cached-cell walks [0, split) through k_ma<true>, the rest through
+    // k_ma<false>; split = the start of cell ma_rows's bin, which k_ma_scatter's cursor of cell ma_rows - 1 ends on
+    const bool partial = G.K.C.have_macache && G.K.C.ma_rows < G.K.C.n_nonempty;
+    const uint32_t *split = partial ? G.d_binoffs + (G.K.C.ma_rows - 1) : nullptr;
     if (G.K.C.have_macache) {
       if (G.ma_occ == 8)
-        k_ma<true, 8><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+        k_ma<true, 8><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, split, partial ? 1 : 0);
       else
-        k_ma<true, 1><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
-    } else {
-      k_ma<false, 1><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+        k_ma<true, 1><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, split, partial ? 1 : 0);
     }
+    if (partial) HIPCHK(hipMemsetAsync(W.xhead, 0, 8 * sizeof(uint32_t), G.stream));
+    if (!G.K.C.have_macache || partial)
+      k_ma<false, 1><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, split, partial ? 2 : 0);
     TEND(1);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QM, 0, 2 * sizeof(uint32_t), G.stream));
     if (G.K.C.have_macache) {  // jumps the 32-bit keys could not decide (rare), exact; walks go back to M
@@ -1490,6 +1552,8 @@ int artis_gpu_update_grid_nlte(const artis_nt_shells *nt, const artis_nlte_param
   KN.C.depratio = d_depr;
   KN.C.ne_mgi = d_act;
   KN.C.n_nonempty = 0;
+  KN.C.linecoef = nullptr;
+  KN.C.linecoef_rows = 0;
   // the thermal-balance solver's view (te_solver.h) of the same state
   TeDev D{};
   rc |= B.get((int32_t **)&D.anumber, (size_t)ne, G.h_anumber.data());
@@ -2341,6 +2405,20 @@ int artis_gpu_last_kernel_times(double ms[4], int64_t launches[4]) {
   }
   return 0;
 }
+int artis_gpu_table_info(int64_t out[ARTIS_TABLE_INFO_COUNT]) {
+  if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
+  const DevCells &C = G.K.C;
+  out[0] = C.n_nonempty;
+  out[1] = C.linecoef_rows;
+  out[2] = (int64_t)C.linecoef_rows * C.linecoef_stride * 8;
+  out[3] = C.ma_rows;
+  out[4] = (int64_t)C.ma_rows * C.ma_key_stride * 2;
+  out[5] = C.marates ? (int64_t)C.n_nonempty * G.K.T.nlevels_total * ARTIS_MA_ACTION_COUNT * 8 : 0;
+  out[6] = G.ma_acts_cached;
+  out[7] = G.ma_acts_total;
+  return 0;
+}
+
 int artis_gpu_last_work_counts(int64_t out[ARTIS_WORK_COUNT]) {
   for (int k = 0; k < ARTIS_WORK_COUNT; k++) out[k] = G.last_work[k];
   return 0;
@@ -2757,19 +2835,29 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   G.nions_total = ni;
   G.nlines = nli;
   G.ngrid = g->ngrid;
-  // non-empty model cells: those referenced by a propagation cell
+  // non-empty model cells: those referenced by a propagation cell, numbered from the centre outwards (the
+  // distance of the cell's nearest propagation-cell centre at tmin, ties by mgi) -- the per-cell tables that only
+  // fit the HBM budget for some cells (line coefficients, macro-atom keys) hold the first rows, the cells where
+  // the packets start and the density peaks; every other cell takes the equivalent table-free path
   std::vector<int32_t> ne_index(np, -1), ne_mgi;
+  std::vector<double> rmin(np, DBL_MAX);
   for (int c = 0; c < g->ngrid; c++) {
     const int mgi = g->cell_mgi[c];
-    if (mgi >= 0 && mgi < np && ne_index[mgi] < 0) {
+    if (mgi >= 0 && mgi < np) {
+      double r2 = 0.;
+      for (int d = 0; d < 3; d++) {
+        double x = g->cell_pos_min[3 * (int64_t)c + d];
+        if (g->grid_type == ARTIS_GRID_UNIFORM) x += g->coordmax[d] / std::max(1, g->ncoordgrid[d]);
+        r2 += x * x;
+      }
+      rmin[mgi] = std::min(rmin[mgi], r2);
       ne_index[mgi] = 0;
     }
   }
   for (int mgi = 0; mgi < np; mgi++)
-    if (ne_index[mgi] == 0) {
-      ne_index[mgi] = (int)ne_mgi.size();
-      ne_mgi.push_back(mgi);
-    }
+    if (ne_index[mgi] == 0) ne_mgi.push_back(mgi);
+  std::stable_sort(ne_mgi.begin(), ne_mgi.end(), [&](int a, int b) { return rmin[a] < rmin[b]; });
+  for (size_t k = 0; k < ne_mgi.size(); k++) ne_index[ne_mgi[k]] = (int32_t)k;
   const int nne_cells = (int)ne_mgi.size();
   const int32_t *dnei, *dnem;
   rc |= dupload(&dnei, ne_index.data(), np);
@@ -2795,54 +2883,86 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   rc |= dalloc(&C.cooling, (size_t)nne_cells * a->ncoolingterms);
   C.ma_key_stride = G.ma_key_stride;
   C.have_macache = 0;
+  C.ma_rows = 0;
   C.ma_key = nullptr;
   C.marates = nullptr;
   {
     size_t freeb = 0, totalb = 0;
     (void)hipMemGetInfo(&freeb, &totalb);
-    const double need = (double)nne_cells * (double)C.ma_key_stride * 2.0;
+    const double row_bytes = (double)C.ma_key_stride * 2.0;
     // k_marates scratch (exact double sums of a batch of levels): at least the largest level's, by default
     // up to 2 GiB (ARTIS_GPU_MAREC_SCRATCH_MB)
     int64_t maxlev = 0;
     for (int ul = 0; ul < nl; ul++) maxlev = std::max(maxlev, G.h_dbl_off[ul + 1] - G.h_dbl_off[ul]);
-    int64_t scratch = std::min<int64_t>(G.h_dbl_off[nl] * nne_cells, ((int64_t)2 << 30) / 8);
-    if (const char *sm = getenv("ARTIS_GPU_MAREC_SCRATCH_MB")) scratch = (int64_t)(atof(sm) * (1 << 20) / 8);
-    scratch = std::max<int64_t>(maxlev * nne_cells, scratch);
+    int64_t cap = ((int64_t)2 << 30) / 8;
+    if (const char *sm = getenv("ARTIS_GPU_MAREC_SCRATCH_MB")) cap = (int64_t)(atof(sm) * (1 << 20) / 8);
+    auto scratch_for = [&](int64_t rows) {
+      return std::max<int64_t>(maxlev * rows, std::min<int64_t>(G.h_dbl_off[nl] * rows, cap));
+    };
     // the cache takes at most ARTIS_GPU_MACACHE_MAX_GB (default: half of the free HBM, the rest is left for the
-    // packet store); without it the walk recomputes the individual rates (k_ma<false>, identical results)
+    // packet store): records for as many cells as fit, centre outwards (ARTIS_GPU_MACACHE_ROWS caps the count);
+    // the walks in the other cells recompute the individual rates (k_ma<false>, identical results).  A partial
+    // cache needs the cell-binned M queue (the cached cells' walks come first in it).
     double budget = 0.5 * (double)freeb;
     if (const char *mx = getenv("ARTIS_GPU_MACACHE_MAX_GB")) budget = atof(mx) * (double)(1ull << 30);
-    const char *env = getenv("ARTIS_GPU_NO_MACACHE");
+    int64_t rows = (int64_t)std::max(0., std::floor((budget - 8.0 * (double)scratch_for(nne_cells)) / row_bytes));
+    rows = std::min<int64_t>(rows, nne_cells);
+    if (const char *mr = getenv("ARTIS_GPU_MACACHE_ROWS")) rows = std::min<int64_t>(rows, atoll(mr));
     // (k_ma addresses the cache by 32-bit 128-byte line indices; every level must fit the record layout)
-    if (!(env && env[0] == '1') && G.ma_cache_ok && need / 128.0 < 4.0e9 && need + 8.0 * (double)scratch < budget) {
+    while (rows > 0 && (double)rows * row_bytes / 128.0 >= 4.0e9) rows /= 2;
+    const char *env = getenv("ARTIS_GPU_NO_MACACHE");
+    if ((env && env[0] == '1') || !G.ma_cache_ok || (rows < nne_cells && !G.W.ma_binned)) rows = 0;
+    if (rows > 0) {
+      const int64_t scratch = scratch_for(rows);
       void *mc = nullptr, *sc = nullptr;
-      if (dmalloc(&mc, (size_t)need) == hipSuccess) {
+      if (dmalloc(&mc, (size_t)((double)rows * row_bytes)) == hipSuccess) {
         G.allocs.push_back(mc);
         if (dmalloc(&sc, (size_t)scratch * 8) == hipSuccess) {
           G.allocs.push_back(sc);
           C.ma_key = (uint16_t *)mc;
           C.have_macache = 1;
+          C.ma_rows = (int32_t)rows;
           G.d_marec_scratch = (double *)sc;
           G.marec_scratch_doubles = scratch;
         }
       }
     }
   }
-  if (!C.have_macache) rc |= dalloc(&C.marates, (size_t)nne_cells * nl * ARTIS_MA_ACTION_COUNT);
-  // per-cell line coefficients for the r-packet line walk: at most 30% of the HBM still free (the packet store
-  // comes later), ARTIS_GPU_NO_LINECOEF=1 switches them off
+  if (C.ma_rows < nne_cells) rc |= dalloc(&C.marates, (size_t)nne_cells * nl * ARTIS_MA_ACTION_COUNT);
+  rc |= dalloc(&G.d_ma_row, (size_t)nne_cells);
+  rc |= dalloc(&G.d_ma_bin, (size_t)nne_cells);
+  rc |= dalloc(&G.d_ma_bincell, (size_t)nne_cells);
+  rc |= dalloc(&G.d_ma_hist, (size_t)nne_cells);
+  C.ma_row = G.d_ma_row;
+  C.ma_bin = G.d_ma_bin;
+  if (!rc) {
+    std::vector<int32_t> order(nne_cells);
+    for (int k = 0; k < nne_cells; k++) order[k] = k;  // centre outwards
+    rc |= ma_place(order);
+  }
+  // per-cell line coefficients for the r-packet line walk: rows for the first linecoef_rows cells (centre
+  // outwards) within a budget of 30% of the HBM still free (the packet store comes later; ARTIS_GPU_LINECOEF_MAX_GB
+  // overrides it), ARTIS_GPU_NO_LINECOEF=1 switches them off.  Cells past the last row gather the two populations
+  // per line themselves (the same coefficient, bit for bit).
   C.linecoef = nullptr;
+  C.linecoef_rows = 0;
   C.linecoef_stride = ((int64_t)G.K.T.nlines + 7) / 8 * 8;
   {
     size_t freeb = 0, totalb = 0;
     (void)hipMemGetInfo(&freeb, &totalb);
-    const double need = (double)nne_cells * (double)C.linecoef_stride * 8.0;
+    double budget = 0.3 * (double)freeb;
+    if (const char *mx = getenv("ARTIS_GPU_LINECOEF_MAX_GB")) budget = atof(mx) * (double)(1ull << 30);
     const char *env = getenv("ARTIS_GPU_NO_LINECOEF");
-    if (!(env && env[0] == '1') && nne_cells > 0 && need < 0.3 * (double)freeb) {
+    const double row_bytes = (double)C.linecoef_stride * 8.0;
+    int rows = (int)std::min<double>((double)nne_cells, std::floor(budget / row_bytes));
+    if (const char *lr = getenv("ARTIS_GPU_LINECOEF_ROWS")) rows = std::min(rows, atoi(lr));
+    if (env && env[0] == '1') rows = 0;
+    if (rows > 0) {
       void *lc = nullptr;
-      if (dmalloc(&lc, (size_t)need) == hipSuccess) {
+      if (dmalloc(&lc, (size_t)rows * (size_t)row_bytes) == hipSuccess) {
         G.allocs.push_back(lc);
         C.linecoef = (double *)lc;
+        C.linecoef_rows = rows;
       }
     }
   }
@@ -3011,6 +3131,7 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
   }
   G.K.R.nts = nts;
   HIPCHK(hipStreamSynchronize(G.stream));
+  if (int rc = ma_replace()) return rc;
   HIPCHK(hipMemsetAsync(G.K.E.err, 0, 4 * sizeof(int32_t), G.stream));
   const int n_ne = G.K.C.n_nonempty;
   const int64_t nl = G.K.T.nlevels_total;
@@ -3034,20 +3155,25 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
       k_transpose<<<dim3((unsigned)((ntg + 63) / 64), (unsigned)((n_ne + 63) / 64)), 256, 0, G.stream>>>(
           G.K.C.corrphot, G.K.C.corrphotT, n_ne, ntg);
     if (G.K.C.linecoef)
-      k_linecoef<<<dim3((unsigned)((G.K.C.linecoef_stride + 255) / 256), (unsigned)std::min(n_ne, 32768)), 256, 0,
+      k_linecoef<<<dim3((unsigned)((G.K.C.linecoef_stride + 255) / 256),
+                        (unsigned)std::min(G.K.C.linecoef_rows, 32768)), 256, 0,
                     G.stream>>>(G.K);
-    if (!G.K.C.have_macache) {
-      k_marates<<<(unsigned)((nlv + 255) / 256), 256, 0, G.stream>>>(G.K, nts, 0, (int)nl, nullptr);
-    } else {
+    const int mr = G.K.C.ma_rows;
+    if (mr < n_ne) {  // the cells without cache records: per-level action totals
+      const int64_t nun = (int64_t)(n_ne - mr) * nl;
+      k_marates<<<(unsigned)((nun + 255) / 256), 256, 0, G.stream>>>(G.K, nts, 0, (int)nl, nullptr,
+                                                                     G.d_ma_bincell + mr, n_ne - mr, false);
+    }
+    if (mr > 0) {
       // batches of levels whose records fit the scratch
       for (int ul0 = 0; ul0 < nl;) {
         int ul1 = ul0 + 1;
-        while (ul1 < nl && (G.h_dbl_off[ul1 + 1] - G.h_dbl_off[ul0]) * n_ne <= G.marec_scratch_doubles) ul1++;
+        while (ul1 < nl && (G.h_dbl_off[ul1 + 1] - G.h_dbl_off[ul0]) * mr <= G.marec_scratch_doubles) ul1++;
         const int nlev = ul1 - ul0;
-        k_marates<<<(unsigned)(((int64_t)nlev * n_ne + 255) / 256), 256, 0, G.stream>>>(G.K, nts, ul0, nlev,
-                                                                                        G.d_marec_scratch);
-        k_mapack<<<dim3((unsigned)((n_ne + 63) / 64), (unsigned)nlev), 256, 0, G.stream>>>(G.K, ul0,
-                                                                                          G.d_marec_scratch);
+        k_marates<<<(unsigned)(((int64_t)nlev * mr + 255) / 256), 256, 0, G.stream>>>(
+            G.K, nts, ul0, nlev, G.d_marec_scratch, G.d_ma_bincell, mr, true);
+        k_mapack<<<dim3((unsigned)((mr + 63) / 64), (unsigned)nlev), 256, 0, G.stream>>>(G.K, ul0,
+                                                                                         G.d_marec_scratch);
         ul0 = ul1;
       }
     }

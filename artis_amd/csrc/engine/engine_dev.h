@@ -194,10 +194,12 @@ struct DevCells {
   double *corrphotT;   // [ntargets_total * n_nonempty]
   double *cooling;     // [n_nonempty * ncoolingterms]  cumulative cooling_contrib (kpkt.cc:167-308)
   // Sobolev coefficient of every line in every cell, (B_lu n_l - B_ul n_u) * HCLIGHTOVERFOURPI (rpkt.cc:168-187;
-  // tau_line = coefficient * t), rows padded to linecoef_stride = nlines rounded up to 8; nullptr when it does not
-  // fit the HBM budget (the line walk then gathers the two populations per line itself)
-  double *linecoef;    // [n_nonempty * linecoef_stride]
+  // tau_line = coefficient * t), rows padded to linecoef_stride = nlines rounded up to 8, for the first
+  // linecoef_rows non-empty cells (the HBM budget's share; the line walk of a cell k >= linecoef_rows gathers the
+  // two populations per line itself); nullptr when no row fits
+  double *linecoef;    // [linecoef_rows * linecoef_stride]
   int64_t linecoef_stride;
+  int32_t linecoef_rows;
   // macro-atom cache: per (cell, level) one compact record of 32-bit keys, 128-byte aligned.  A key is a running
   // sum of the reference's individual rates (the cellhistory individ_* arrays, globals.h:174-183, summed in the
   // reference's order, macroatom.cc:57-159) divided by its action's total and rounded to 32 bits; the first 9 are
@@ -213,8 +215,15 @@ struct DevCells {
   //   positions' low halves; the record padded to a multiple of 64 keys
   uint16_t *ma_key;    // [n_nonempty * ma_key_stride], or nullptr
   int64_t ma_key_stride;
-  int32_t have_macache;
-  double *marates;     // without the cache: [n_nonempty * nlevels_total * 9] totals only
+  int32_t have_macache;  // ma_rows > 0
+  // the cache holds ma_rows records (the HBM budget's share): cell k's is row ma_row[k], -1 for a cell without one,
+  // whose walks take the table-free path over marates.  The rows go to the cells with the most macro-atom
+  // activations of the previous timestep (centre outwards before the first).  ma_bin[k] is cell k's bin in the
+  // binned M queue: the cached cells' bins [0, ma_rows) in row order, the other cells' after them.
+  int32_t ma_rows;
+  const int32_t *ma_row;  // [n_nonempty]
+  const int32_t *ma_bin;  // [n_nonempty]
+  double *marates;     // cells without cache records: [n_nonempty * nlevels_total * 9] totals only (or nullptr)
   // nebular inputs (ABI 6; nullptr when the option is off), model-cell indexed like the arrays above
   const double *nlte_pops;    // [npts_model * total_nlte_levels]
   const float *rf_TR, *rf_W;  // [npts_model * rf_nbins]

@@ -591,7 +591,7 @@ DEVFN double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_even
   const double lnu_first = K.T.line_nu[0], lnu_last = K.T.line_nu[max(K.T.nlines - 1, 0)];
   unsigned long long nscanned = 0, ntaus = 0;
   double result;
-  if (x.win && K.C.linecoef) {
+  if (x.win && k < K.C.linecoef_rows) {
     // the context fields the walk reads, in registers: through the context pointer they are reloaded from memory
     // on every line (the compiler cannot prove the kernel's stores leave them unchanged)
     __attribute__((address_space(3))) double *win = x.win;
@@ -1976,12 +1976,12 @@ DEVNI void do_macroatom(Tx &x, Pkt &p) {
   int r;
   unsigned jumps;
   unsigned long long ntrans;
-  if (K.C.have_macache) {
+  if (K.C.ma_row[K.C.ne_index[mgi]] >= 0) {
     MaLaneC m;
     m.ul = ulev(K, p.ma_element, p.ma_ion, p.ma_level);
     m.rec_off = K.T.ma_meta[m.ul].rec_off;
     m.k = K.C.ne_index[mgi];
-    m.block = K.C.ma_key + (int64_t)m.k * K.C.ma_key_stride;
+    m.block = K.C.ma_key + (int64_t)K.C.ma_row[m.k] * K.C.ma_key_stride;
     m.jumps = 0;
     m.ntrans = 0;
     const double t_mid = K.G.ts_mid[x.nts];

@@ -253,7 +253,7 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
   // twice per PF lines instead of three to four times per line.  The tau sums are unchanged.
   int pf_base = -(1 << 20);
   const double lnu_first = K.T.line_nu[0], lnu_last = K.T.line_nu[max(K.T.nlines - 1, 0)];
-  if (K.C.linecoef) {
+  if (K.C.ne_index[v.mgi] < K.C.linecoef_rows) {
     // over the per-cell Sobolev coefficients (DevCells::linecoef, as get_event): an aligned window of LC_WIN lines'
     // frequencies and coefficients is eight independent 16-byte loads; dtau = coefficient * t_line is the
     // reference's (B_lu n_l - B_ul n_u) * HCLIGHTOVERFOURPI * t_line in the same operation order

@@ -291,8 +291,9 @@ __global__ void k_ma_bin(const Ctx *__restrict__ ctxp, WaveState W, const uint64
   for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x) {
     const int32_t idx = W.q[QM][slot];
     const int k = K.C.ne_index[cell_mgi(K, lo32(soa[PW(0, idx, 0)]))];  // hot group: no n term
-    W.ma_key[slot] = k;
-    atomicAdd(&W.bins[k], 1u);
+    const int b = K.C.ma_bin[k];
+    W.ma_key[slot] = b;
+    atomicAdd(&W.bins[b], 1u);
   }
 }
 // scatter into cell order using the exclusive prefix sum of the counts.  With the key cache, each slot becomes a
@@ -305,7 +306,8 @@ __global__ void k_ma_scatter(const Ctx *__restrict__ ctxp, WaveState W, const ui
   for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x) {
     const int32_t idx = W.q[QM][slot];
     const uint32_t pos = atomicAdd(&offs[W.ma_key[slot]], 1u);
-    if (!W.ma_tick) {
+    const int bin = W.ma_key[slot];
+    if (!W.ma_tick || bin >= K.C.ma_rows) {  // (no tickets for the walks of uncached cells)
       W.ma_sorted[pos] = idx;
       continue;
     }
@@ -330,7 +332,7 @@ __global__ void k_ma_scatter(const Ctx *__restrict__ ctxp, WaveState W, const ui
       tidx = -1;
     }
     W.ma_tick[2 * (int64_t)pos] = make_int4(tidx, ul, K.T.ma_meta[ul].rec_off, K.C.ne_index[mgi]);
-    W.ma_tick[2 * (int64_t)pos + 1] = make_int4(number, (int)W.rng_n[idx], (int)jumps, 0);
+    W.ma_tick[2 * (int64_t)pos + 1] = make_int4(number, (int)W.rng_n[idx], (int)jumps, bin);  // bin == key row
   }
 }
 
@@ -338,9 +340,11 @@ __global__ void k_ma_scatter(const Ctx *__restrict__ ctxp, WaveState W, const ui
 // The (binned) queue is cut into W.ma_ranges contiguous ranges; blocks start on range blockIdx % 8 -- the
 // XCD the block was dispatched to under round-robin placement, so one XCD's L2 sees a contiguous run of
 // cells -- and steal from the following ranges once theirs is exhausted.
+// part 0: the whole queue; with a partial key cache (DevCells::ma_rows) the binned queue holds the cached cells'
+// walks first: part 1 = [0, *split) (CACHE), part 2 = [*split, nq) (!CACHE).
 template <bool CACHE, int MINW>
 __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__ ctxp, WaveState W, const uint64_t *__restrict__ soa,
-                                                         int64_t n, int nts) {
+                                                         int64_t n, int nts, const uint32_t *split, int part) {
   CTX_IN_LDS(ctxp)
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
@@ -352,7 +356,9 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   L.ctr = &s_ctr[0];
   L.work = &s_work[0];
   lds_uint4 *line = CACHE ? (lds_uint4 *)&s_line[threadIdx.x >> 6][threadIdx.x & 63] : nullptr;
-  const uint32_t nq = W.ctr[2 * QM];
+  const uint32_t nq_all = W.ctr[2 * QM];
+  const uint32_t q0 = (part == 2) ? min(*split, nq_all) : 0u;
+  const uint32_t nq = ((part == 1) ? min(*split, nq_all) : nq_all) - q0;
   const int32_t *queue = W.ma_binned ? W.ma_sorted : W.q[QM];
   const int nr = W.ma_ranges;
   const double t_mid = K.G.ts_mid[nts];
@@ -384,7 +390,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
       wave_push(W, QX, pendX, idx);
       pendR = pendK = pendX = false;
       if (imask) {
-        const uint32_t lo = (uint32_t)((uint64_t)nq * cur / nr), hi = (uint32_t)((uint64_t)nq * (cur + 1) / nr);
+        const uint32_t lo = q0 + (uint32_t)((uint64_t)nq * cur / nr), hi = q0 + (uint32_t)((uint64_t)nq * (cur + 1) / nr);
         const uint32_t slot = wave_reserve(&W.xhead[cur], idle);
         const bool got = idle && lo + slot < hi;
         if (got && CACHE && W.ma_tick) {
@@ -396,7 +402,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
           rng.key1 = (uint32_t)t1.x;
           rng.n = (uint32_t)t1.y;
           mc.jumps = (unsigned)t1.z;
-          mc.block = K.C.ma_key + (int64_t)mc.k * K.C.ma_key_stride;
+          mc.block = K.C.ma_key + (int64_t)t1.w * K.C.ma_key_stride;
           mc.ntrans = 0;
           mc.sel = -1;
           mc.pline = 0;
@@ -421,7 +427,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
             }
             mc.rec_off = K.T.ma_meta[mc.ul].rec_off;
             mc.k = K.C.ne_index[mgi];
-            mc.block = K.C.ma_key + (int64_t)mc.k * K.C.ma_key_stride;
+            mc.block = K.C.ma_key + (int64_t)K.C.ma_row[mc.k] * K.C.ma_key_stride;
             mc.ntrans = 0;
             mc.sel = -1;
             mc.pline = 0;
@@ -574,7 +580,7 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
     m.jumps = W.pend_jumps[idx] + 1;
     m.k = K.C.ne_index[cell_mgi(K, where)];
     m.rec_off = K.T.ma_meta[m.ul].rec_off;
-    m.block = K.C.ma_key + (int64_t)m.k * K.C.ma_key_stride;
+    m.block = K.C.ma_key + (int64_t)K.C.ma_row[m.k] * K.C.ma_key_stride;
     m.ntrans = 0;
     const int ul = m.ul, k = m.k;
     const int mgi = K.C.ne_mgi[k];

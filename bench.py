@@ -147,6 +147,52 @@ def dry_launch(world, rank):
     del torch
 
 
+def survey_sized_workload(P, steps, nts, rank, progress):
+    """SURVEY §8(d)'s specified atom size beside the heavier default: ~100 levels per non-top ion (all level pairs
+    joined by a line: 44 550 lines), 56 ionising levels (504 continua), the same 50^3 grid, timestep and P packets
+    per GPU, timed like the main line (resident packets, per-step precompute + transport)."""
+    from artis_amd import Engine
+    from artis_amd.model import Model
+
+    m = Model(ngrid_1d=50, nlevels_per_ion=100, line_window=100, n_resonance=5, n_ionising=56)
+    m.set_timestep(nts)
+    prm = m.params
+    prm.rank = rank
+    pk = m.init_rpackets(nts, P, seed=3000 + rank)
+    eng = Engine(m, params=prm)
+    eng.upload_cellstate(nts)
+    eng.upload(pk)
+    eng.snapshot()
+    del pk
+    ms, kts, work = [], [], np.zeros(16, dtype=np.int64)
+    for k in range(steps + 1):
+        eng.restore()
+        eng.zero_estimators()
+        t = time.perf_counter()
+        eng.upload_cellstate(nts)
+        eng.step_resident(nts, my_rank=rank)
+        dt = time.perf_counter() - t
+        if k > 0:  # the first step warms up
+            ms.append(dt * 1e3)
+            kts.append(eng.last_kernel_times())
+            work[:] = eng.last_work()
+    tables = eng.table_info()
+    eng.close()
+    alg = byte_model(work, m.nions_total)
+    kt = {c: (float(np.mean([t[c][0] for t in kts])), float(np.mean([t[c][1] for t in kts]))) for c in ("rpkt", "ma")}
+    dom = max(kt, key=lambda c: kt[c][0])
+    launches = max(kt[dom][1], 1.)
+    gbs = alg[dom] / launches / max(kt[dom][0] / 1e3 / launches, 1e-12) / 1e9
+    out = {"levels_per_ion": 100, "levels": m.nlevels_total, "lines": m.nlines, "bf_continua": m.nbfcontinua,
+           "packets": P, "steps": steps, "ms_per_step": float(np.mean(ms)), "value": P / (float(np.mean(ms)) / 1e3),
+           "unit": "packets/s", "kernel_ms": {c: v[0] for c, v in kt.items()},
+           "roofline": {"kernel": KERNEL_NAME[dom], "achieved": gbs, "peak": HBM_PEAK_GBS, "frac": gbs / HBM_PEAK_GBS},
+           "macro_atom_jumps_per_packet": float(work[8]) / max(P, 1), "tables": tables}
+    progress(f"SURVEY-sized workload: {out['ms_per_step']:.0f} ms per step")
+    m.close()
+    return out
+
+
 def nebular_update_grid(rank, cpu, progress):
     """SURVEY §8(f) row 4 for the nebular options (artis_gpu_update_grid_nlte): update_grid of BASELINE config 3's
     nebularonezone inputs and of every cell of a 136-cell synthetic nebular model (each with its Spencer-Fano solution),
@@ -213,6 +259,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--packets", type=int, default=10_000_000, help="packets per GPU (SURVEY.md §8(d): 1e7)")
     ap.add_argument("--ngrid", type=int, default=50)
+    ap.add_argument("--line-window", type=int, default=None,
+                    help="synthetic atom: lines per level (default 22: 93 798 lines; 160: 470 745, 5x)")
+    ap.add_argument("--max-lines", type=int, default=None, help="synthetic atom: line cap (default 100 000)")
+    ap.add_argument("--nlevels-per-ion", type=int, default=None, help="synthetic atom: levels per ion (default 400)")
     ap.add_argument("--nts", type=int, default=10)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU time of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -221,6 +271,8 @@ def main():
     ap.add_argument("--vpkt", type=int, default=0,
                     help="virtual packets (BASELINE config 5, vpkt.cc) with this many observer directions; the "
                          "timestep must lie in the vspec window [10 d, 30 d] (e.g. --nts 30)")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the drop-in host-path timing and the SURVEY §8(d)-sized second workload")
     ap.add_argument("--dry-launch", action="store_true",
                     help="bring up the N ranks over gloo without a GPU and print them (tests the launcher)")
     args = ap.parse_args()
@@ -253,7 +305,9 @@ def main():
         if rank == 0:
             print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
-    model = Model(ngrid_1d=args.ngrid)
+    atom = {k: v for k, v in (("line_window", args.line_window), ("max_lines", args.max_lines),
+                                ("nlevels_per_ion", args.nlevels_per_ion)) if v is not None}
+    model = Model(ngrid_1d=args.ngrid, **atom)
     nts = args.nts
     model.set_timestep(nts)
     params = model.params
@@ -275,7 +329,8 @@ def main():
     eng.upload_cellstate(nts)
     eng.upload(packets)
     eng.snapshot()
-    progress("engine initialised, packets resident")
+    tables = eng.table_info()
+    progress(f"engine initialised, packets resident; per-cell tables {tables}")
 
     if world > 1:
         adist.join(eng, rank, world, dist)
@@ -319,6 +374,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    tables = eng.table_info()  # with the placement the last timed steps used
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -378,12 +434,27 @@ def main():
         eng.download(gpu_pk)
         gs = gpu_pk[:n_sample]
         bad = parity.discrete_mismatch(gs, sample)
+        # the CPU-vs-CPU noise floor: the same sample size from a different seed through the oracle
+        # (the same energy per packet as the engine's ensemble: etot scaled to the sample's share)
+        other = model.init_rpackets(nts, n_sample, seed=2000 + rank, etot=1e45 * n_sample / P)
+        oracle_lib.update_packets(model, nts, other, nthreads=nthreads)
+        lum = lambda pk: float(pk["e_rf"][pk["type"] == 32].sum())  # noqa: E731  escaped luminosity of the step
         parity_line = {
             "sample_packets": n_sample,
             "discrete_state_match": float(1.0 - bad.mean()),
             "max_fp_rel": max(parity.fp_max_rel(gs, sample, ~bad).values()),
             "spectrum_l1": parity.spectrum_l1(gs, sample),
-            "spectrum": "escaped-packet energy in 1000 log bins of nu_rf over [NU_MIN_R, NU_MAX_R] (spec.out binning)",
+            "spectrum_l1_100bin": float(np.abs(parity.spectrum(gs, 100) - parity.spectrum(sample, 100)).sum() /
+                                        max(parity.spectrum(sample, 100).sum(), 1e-300)),
+            "lightcurve_l1": abs(lum(gs) - lum(sample)) / max(lum(sample), 1e-300),
+            "cpu_two_seed_floor": {
+                "spectrum_l1": parity.spectrum_l1(other, sample),
+                "spectrum_l1_100bin": float(np.abs(parity.spectrum(other, 100) - parity.spectrum(sample, 100)).sum() /
+                                            max(parity.spectrum(sample, 100).sum(), 1e-300)),
+                "lightcurve_l1": abs(lum(other) - lum(sample)) / max(lum(sample), 1e-300),
+                "seeds": "ensemble seeds 1000+rank (the GPU's) and 2000+rank, same sample size, both on the oracle"},
+            "spectrum": "escaped-packet energy in 1000 (and 100) log bins of nu_rf over [NU_MIN_R, NU_MAX_R] "
+                        "(spec.out binning) for the one timestep; light curve: the step's escaped luminosity",
         }
         cpu = {
             "value": n_sample / cpu_dt,
@@ -393,6 +464,27 @@ def main():
             "kind": "port",
             "sample": f"first {n_sample} packets of the same ensemble, same timestep, {cpu_dt:.1f} s",
         }
+
+    dropin = None
+    if rank == 0 and vcfg is None and not args.no_extra:
+        # INTEGRATION.md's drop-in call: artis_gpu_update_packets on host AoS packets (H2D, AoS->SoA, transport,
+        # SoA->AoS, D2H, estimators added into host arrays) -- the resident path's transport plus the PCIe round trip
+        tms = []
+        for k in range(2):
+            host = packets.copy()
+            est_h = model.new_estimators()
+            t = time.perf_counter()
+            eng.update_packets(nts, host, est_h, my_rank=rank)
+            dt = time.perf_counter() - t
+            if k > 0:
+                tms.append((dt * 1e3, eng.last_transport_ms()))
+            del host
+        dropin = {"ms_per_step": tms[-1][0], "value": P / (tms[-1][0] / 1e3), "unit": "packets/s",
+                  "transport_ms": tms[-1][1], "host_transfer_ms": tms[-1][0] - tms[-1][1],
+                  "bytes_each_way": int(P) * 304,
+                  "note": "packets on the host in the reference's 304-byte layout; cell precompute not included "
+                          "(the cell state was uploaded once, as in the reference's loop)"}
+        progress(f"drop-in host path: {dropin['ms_per_step']:.0f} ms per step")
 
     ugrid = None
     if rank == 0 and not args.no_update_grid and vcfg is None:
@@ -427,6 +519,9 @@ def main():
     neb = None
     if rank == 0 and not args.no_update_grid and vcfg is None:
         neb = nebular_update_grid(rank, not args.no_cpu_baseline, progress)
+    survey8d = None
+    if rank == 0 and world == 1 and vcfg is None and not args.no_extra:
+        survey8d = survey_sized_workload(P, 2, nts, rank, progress)
 
     if rank == 0:
         line = {
@@ -485,6 +580,10 @@ def main():
             line["update_grid"] = ugrid
         if neb is not None:
             line["update_grid_nebular"] = neb
+        if dropin is not None:
+            line["dropin_host_path"] = dropin
+        if survey8d is not None:
+            line["workload_survey_8d"] = survey8d
         if vcfg is not None:
             vms = float(np.mean([v[0] for v in vstats]))
             line["config"]["workload"] += (f"; virtual packets: {vcfg.nobs} observers x {vcfg.nspectra} spectra, "
@@ -494,6 +593,7 @@ def main():
                             "traces_per_s": float(np.mean([v[2] for v in vstats])) / max(vms / 1e3, 1e-12)}
             ntr = max(line["vpkt"]["traces"], 1)
             line["vpkt"]["work_per_trace"] = {k: float(np.mean([w[k] for w in vwork])) / ntr for k in vwork[0]}
+        line["tables"] = tables
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -476,6 +476,15 @@ double artis_gpu_last_precompute_ms(void);
 /* Per-call event counts from the device (steps, lines scanned, kappa evaluations, ...), for the byte model. */
 #define ARTIS_WORK_COUNT 16
 int artis_gpu_last_work_counts(int64_t out[ARTIS_WORK_COUNT]);
+/* Coverage of the per-cell tables the engine sized at init (ABI 9): out[0] non-empty cells; out[1] cells with a
+ * row of line coefficients (numbered centre outwards; the rest gather populations in the line walk) and out[2]
+ * their bytes; out[3] cells with macro-atom key records and out[4] their bytes; out[5] bytes of the per-cell
+ * action totals the table-free macro-atom walk reads; out[6] / out[7] macro-atom activations in cells with
+ * records / in all cells between the last two placements of a partial cache (the records go to the cells with
+ * the most activations at each artis_gpu_upload_cellstate; 0 / 0 before the first re-placement).  The split
+ * never changes a result. */
+#define ARTIS_TABLE_INFO_COUNT 8
+int artis_gpu_table_info(int64_t out[ARTIS_TABLE_INFO_COUNT]);
 /* Emergent spectrum and light curve of the escaped r-packets among the resident packets, binned on the device:
  * the binning of write_partial_lightcurve_spectra (spectrum.cc:641-721) -- add_to_spec (spectrum.cc:339-362,
  * angle-averaged, no emission-resolved columns) and add_to_lc_res (light_curve.cc:34-54) -- over
@@ -723,7 +732,7 @@ typedef struct artis_nlte_cells {
 int artis_gpu_update_grid_nlte(const artis_nt_shells *nt, const artis_nlte_params *params, artis_nlte_cells *cells);
 double artis_gpu_last_nlte_ms(void);  /* device time (ms) of the last artis_gpu_update_grid_nlte */
 
-#define ARTIS_GPU_ABI_VERSION 8  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
+#define ARTIS_GPU_ABI_VERSION 9  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
                                     3: virtual packets (artis_vpkt_params / artis_vpkt_result);
                                     4: artis_run_params.excitation_temperature;
                                     5: host estimator block pack/unpack, RCCL communicator + all-reduce;
@@ -731,7 +740,8 @@ double artis_gpu_last_nlte_ms(void);  /* device time (ms) of the last artis_gpu_
                                        detailed bf estimators, NO_LUT photoionisation, non-thermal ionisation);
                                     7: update_grid's temperature / ionisation solution (artis_gpu_solve_temperatures);
                                     8: update_grid for the nebular options (artis_gpu_update_grid_nlte),
-                                       artis_te_params.direct_col_heat */
+                                       artis_te_params.direct_col_heat;
+                                    9: artis_gpu_table_info (per-cell table budgets) */
 int artis_gpu_abi_version(void);
 
 #ifdef __cplusplus

@@ -98,6 +98,62 @@ def test_without_macroatom_cache_is_identical(small_model, engine_factory, monke
     assert max(parity.fp_max_rel(a, b).values()) <= parity.FP_RTOL
 
 
+@pytest.mark.parametrize("env", [{"ARTIS_GPU_NO_LINECOEF": "1"}, {"ARTIS_GPU_LINECOEF_ROWS": "half"},
+                                 {"ARTIS_GPU_MACACHE_ROWS": "half"},
+                                 {"ARTIS_GPU_LINECOEF_ROWS": "1", "ARTIS_GPU_MACACHE_ROWS": "1"}],
+                         ids=["no_linecoef", "half_linecoef", "half_macache", "one_row_each"])
+def test_table_budgets_match_oracle(small_model, engine_factory, monkeypatch, env):
+    """Per-cell tables that only fit the HBM budget for some cells (line coefficients, macro-atom key records,
+    centre outwards) -- or for none (linecoef == nullptr) -- leave every other cell on the table-free path, with
+    the same packet histories as the oracle and the full-table engine."""
+    small_model.set_timestep(11)
+    pk = small_model.init_rpackets(11, 4000, seed=12)
+    probe = engine_factory(small_model)
+    full = probe.table_info()
+    probe.close()
+    assert full["linecoef_rows"] == full["cells"] and full["macache_rows"] == full["cells"]
+    for k, v in env.items():
+        monkeypatch.setenv(k, str(full["cells"] // 2) if v == "half" else v)
+    eng = engine_factory(small_model)
+    info = eng.table_info()
+    if "ARTIS_GPU_NO_LINECOEF" in env:
+        assert info["linecoef_rows"] == 0 and info["linecoef_bytes"] == 0
+    if "ARTIS_GPU_LINECOEF_ROWS" in env:
+        assert 0 < info["linecoef_rows"] < info["cells"]
+    if "ARTIS_GPU_MACACHE_ROWS" in env:
+        assert 0 < info["macache_rows"] < info["cells"] and info["marates_bytes"] > 0
+    eng.upload_cellstate(11)
+    pg, po = pk.copy(), pk.copy()
+    eg = eng.update_packets(11, pg)
+    eo, wo = oracle_lib.update_packets(small_model, 11, po, nthreads=16)
+    parity.assert_packets_match(pg, po)
+    parity.assert_estimators_match(eg, eo)
+    wg = eng.last_work()
+    keep = np.arange(len(wg)) != 9
+    assert (wg[keep] == wo[keep]).all(), (wg, wo)
+
+
+def test_partial_macroatom_cache_replaced_between_timesteps(small_model, engine_factory, monkeypatch):
+    """With key records for a third of the cells, each upload_cellstate re-places them on the cells with the most
+    macro-atom activations since the last placement; three chained timesteps stay on the oracle's histories."""
+    probe = engine_factory(small_model)
+    ncells = probe.table_info()["cells"]
+    probe.close()
+    monkeypatch.setenv("ARTIS_GPU_MACACHE_ROWS", str(ncells // 3))
+    eng = engine_factory(small_model)
+    assert eng.table_info()["macache_rows"] == ncells // 3
+    small_model.set_timestep(12)
+    pk = small_model.init_rpackets(12, 3000, seed=13)
+    pg, po = pk.copy(), pk.copy()
+    for nts in (12, 13, 14):
+        small_model.set_timestep(nts)
+        eng.upload_cellstate(nts)
+        eg = eng.update_packets(nts, pg)
+        eo, _ = oracle_lib.update_packets(small_model, nts, po, nthreads=16)
+        parity.assert_packets_match(pg, po)
+        parity.assert_estimators_match(eg, eo)
+
+
 def test_macroatom_records_in_many_batches_are_identical(small_model, engine_factory, monkeypatch):
     """k_marates writes the records in level batches through a scratch (k_marec transposes them); a scratch
     of one level's records forces one batch per level and must give the same packets."""
