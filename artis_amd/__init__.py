@@ -29,7 +29,7 @@ ABI_SYMBOLS = [
     "artis_estimator_block_average_scalars",
     "artis_gpu_comm_unique_id", "artis_gpu_comm_init", "artis_gpu_estimators_allreduce", "artis_gpu_comm_finalize",
     "artis_gpu_solve_temperatures", "artis_gpu_last_te_ms", "artis_gpu_prepare_temperatures",
-    "artis_gpu_update_grid_nlte", "artis_gpu_last_nlte_ms", "artis_gpu_table_info",
+    "artis_gpu_update_grid_nlte", "artis_gpu_last_nlte_ms", "artis_gpu_table_info", "artis_gpu_vpkt_last_drains",
 ]
 
 _gpu_lib = None
@@ -74,6 +74,7 @@ def gpu_lib():
         L.artis_gpu_last_precompute_ms.restype = C.c_double
         L.artis_gpu_last_work_counts.argtypes = [vp]
         L.artis_gpu_table_info.argtypes = [vp]
+        L.artis_gpu_vpkt_last_drains.restype = C.c_int64
         L.artis_gpu_last_error.restype = C.c_char_p
         L.artis_gpu_last_rounds.restype = C.c_int64
         L.artis_gpu_spectrum.argtypes = [C.c_int, C.c_int, vp, vp, vp]
@@ -265,6 +266,10 @@ class Engine:
         tr = C.c_int64()
         self.lib.artis_gpu_vpkt_last_stats(C.byref(ms), C.byref(sp), C.byref(tr))
         return ms.value, sp.value, tr.value
+
+    def vpkt_last_drains(self):
+        """Launches of the last update resumed after the virtual-packet spawn buffer filled."""
+        return int(self.lib.artis_gpu_vpkt_last_drains())
 
     def vpkt_last_work(self):
         """{segments, lines, bf_active, escaped} of the last update's virtual packets."""

@@ -596,6 +596,16 @@ struct Engine {
   std::vector<int32_t> h_line_elem;  // artis_atomic_tables.line_elementindex (virtual-packet line masks)
   double *d_vpkt_spawn = nullptr;
   uint32_t vpkt_spawn_cap = 0;
+  uint32_t *d_qsnap = nullptr;    // queue count when the current k_rpkt / k_kpkt launch started (vpkt_drain)
+  // spawn sort (DevVpkt::perm): keys / indices in and out, hipcub temp storage, sized for vpkt_spawn_cap
+  uint32_t *d_vkey = nullptr, *d_vkey2 = nullptr, *d_vidx = nullptr, *d_vperm = nullptr;
+  void *d_vsort_tmp = nullptr;
+  size_t vsort_tmp_bytes = 0;
+  uint32_t *h_vcount = nullptr;   // pinned: spawn count before a flush
+  bool vpkt_sort = true;          // ARTIS_VPKT_SORT=0: trace in buffer order
+  uint32_t *h_vfull = nullptr;    // pinned: DevVpkt::full after a launch
+  int64_t vpkt_drains = 0;        // launches resumed after a full spawn buffer (last update_packets)
+  bool r_binned = true;           // bin the R queue by cell before k_rpkt (ARTIS_GPU_R_BIN)
   std::vector<hipEvent_t> vev;  // (start, end) pairs around the k_vpkt launches of the last update
   size_t vev_used = 0;
   double last_vpkt_ms = 0.;
@@ -792,10 +802,35 @@ int tcollect() {
 #define TEND(c) \
   if (int rc_ = tmark(c)) return rc_
 
+// sort keys of the spawn records: propagation cell (high bits), then log nu_cmf in 4096 bins over [1e13, 1e17] Hz
+__global__ void k_vpkt_keys(const double *__restrict__ spawn, uint32_t cap, uint32_t n, uint32_t *__restrict__ key,
+                            uint32_t *__restrict__ idx) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const uint32_t where = (uint32_t)lo32(reinterpret_cast<const uint64_t *>(spawn)[11 * (uint64_t)cap + s]);
+  const double nu = spawn[6 * (uint64_t)cap + s];
+  const double f = log10(fmax(nu, 1e13) * 1e-13) * 0.25;  // [1e13, 1e17] -> [0, 1]
+  const uint32_t b = (uint32_t)fmin(4095., fmax(0., f * 4095.));
+  key[s] = (min(where, 0xfffffu) << 12) | b;  // (grids past 2^20 cells share the last cell key)
+  idx[s] = s;
+}
+
 // virtual packets: trace the spawn records appended since the last flush, then empty the buffer
 // (stream-ordered; the spawn count is read by the kernel itself)
 int vpkt_flush() {
   if (!G.K.V.on) return 0;
+  uint32_t ns = 0;
+  const bool sort = G.vpkt_sort && G.d_vperm;
+  if (sort) {
+    // the trace order (DevVpkt::perm): a host round trip for the count, then a radix sort of (cell, nu) keys
+    HIPCHK(hipMemcpyAsync(G.h_vcount, G.K.V.spawn_ctr, sizeof(uint32_t), hipMemcpyDeviceToHost, G.stream));
+    HIPCHK(hipStreamSynchronize(G.stream));
+    ns = std::min(*G.h_vcount, G.K.V.cap);
+    if (ns == 0) {
+      HIPCHK(hipMemsetAsync(G.K.V.spawn_ctr, 0, 2 * sizeof(uint32_t), G.stream));
+      return 0;
+    }
+  }
   if (G.vev_used + 2 > G.vev.size()) {
     for (int k = 0; k < 2; k++) {
       hipEvent_t e;
@@ -803,7 +838,13 @@ int vpkt_flush() {
       G.vev.push_back(e);
     }
   }
-  HIPCHK(hipEventRecord(G.vev[G.vev_used++], G.stream));
+  HIPCHK(hipEventRecord(G.vev[G.vev_used++], G.stream));  // (the sort counts as virtual-packet time)
+  if (sort) {
+    k_vpkt_keys<<<(ns + 255) / 256, 256, 0, G.stream>>>(G.K.V.spawn, G.K.V.cap, ns, G.d_vkey, G.d_vidx);
+    size_t tb = G.vsort_tmp_bytes;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(G.d_vsort_tmp, tb, G.d_vkey, G.d_vkey2, G.d_vidx, G.d_vperm, (int)ns,
+                                              0, 32, G.stream));
+  }
   // minimum waves per SIMD the virtual-packet kernel is compiled for (ARTIS_VPKT_OCC = 1, 2 or 3; more waves
   // hide more of the FP64 and memory latency of the walk at the price of register spills)
   static const int occ = [] {
@@ -825,7 +866,18 @@ int vpkt_flush() {
 // size the spawn buffer for n packets (artis_vpkt_params.spawn_capacity, default 16 per packet, >= 2^20)
 int vpkt_prepare(int64_t n) {
   if (!G.K.V.on) return 0;
+  // default: 16 spawns per packet, at most a quarter of the free HBM (a full buffer is traced and the launch
+  // resumed, vpkt_drain), at least 2^20 records and never below the overflow records' count
   int64_t cap = G.vpkt_cap_param > 0 ? G.vpkt_cap_param : std::max<int64_t>(16 * n, 1 << 20);
+  if (G.vpkt_cap_param <= 0) {
+    size_t freeb = 0, totalb = 0;
+    (void)hipMemGetInfo(&freeb, &totalb);
+    const int64_t have = G.vpkt_spawn_cap;  // a buffer already held counts as free
+    const double rec = VPKT_SPAWN_WORDS * sizeof(double) + 4 * sizeof(uint32_t);  // + the sort arrays
+    const int64_t fit = (int64_t)((0.25 * (double)freeb) / rec) + have / 4;
+    cap = std::max<int64_t>(std::min(cap, fit), 1 << 20);
+  }
+  cap = std::max<int64_t>(cap, G.K.V.ovf_cap);
   cap = std::min<int64_t>(cap, 0x7fffffff / 2);
   // k_vpkt's 32-bit fetch head runs over cap * nobs work items and overshoots by at most one wave per resident
   // wave: keep that below 2^32 so the head cannot wrap onto items already traced
@@ -838,12 +890,77 @@ int vpkt_prepare(int64_t n) {
     G.K.V.cap = 0;
     HIPCHK(dmalloc((void **)&G.d_vpkt_spawn, (size_t)cap * VPKT_SPAWN_WORDS * sizeof(double)));
     G.vpkt_spawn_cap = (uint32_t)cap;
+    const char *so = getenv("ARTIS_VPKT_SORT");
+    G.vpkt_sort = !(so && so[0] == '0');
+    for (uint32_t **a : {&G.d_vkey, &G.d_vkey2, &G.d_vidx, &G.d_vperm}) {
+      dfree(*a);
+      *a = nullptr;
+    }
+    dfree(G.d_vsort_tmp);
+    G.d_vsort_tmp = nullptr;
+    if (G.vpkt_sort) {
+      for (uint32_t **a : {&G.d_vkey, &G.d_vkey2, &G.d_vidx, &G.d_vperm})
+        HIPCHK(dmalloc((void **)a, (size_t)cap * sizeof(uint32_t)));
+      G.vsort_tmp_bytes = 0;
+      HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, G.vsort_tmp_bytes, G.d_vkey, G.d_vkey2, G.d_vidx,
+                                                G.d_vperm, (int)cap, 0, 32, G.stream));
+      HIPCHK(dmalloc(&G.d_vsort_tmp, std::max<size_t>(G.vsort_tmp_bytes, 16)));
+    }
   }
+  if (!G.h_vcount) HIPCHK(hipHostMalloc((void **)&G.h_vcount, sizeof(uint32_t), hipHostMallocDefault));
+  G.K.V.perm = G.vpkt_sort ? G.d_vperm : nullptr;
   G.K.V.spawn = G.d_vpkt_spawn;
   G.K.V.cap = G.vpkt_spawn_cap;
   HIPCHK(hipMemsetAsync(G.K.V.spawn_ctr, 0, 2 * sizeof(uint32_t), G.stream));
+  HIPCHK(hipMemsetAsync(G.K.V.ovf_ctr, 0, sizeof(uint32_t), G.stream));
+  HIPCHK(hipMemsetAsync(G.K.V.full, 0, sizeof(uint32_t), G.stream));
   G.vev_used = 0;
+  G.vpkt_drains = 0;
   return 0;
+}
+
+// overflow records -> the front of the (just traced and emptied) spawn buffer; then the counters
+__global__ void k_vpkt_ovf_copy(const double *__restrict__ ovf, uint32_t ovf_cap, const uint32_t *__restrict__ ovf_ctr,
+                                double *__restrict__ spawn, uint32_t cap) {
+  const uint64_t nrec = min(min(*ovf_ctr, ovf_cap), cap);
+  const uint64_t total = nrec * VPKT_SPAWN_WORDS;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t w = i / nrec, s = i % nrec;
+    spawn[w * cap + s] = ovf[w * ovf_cap + s];
+  }
+}
+__global__ void k_vpkt_ovf_reset(uint32_t *ovf_ctr, uint32_t ovf_cap, uint32_t *spawn_ctr, uint32_t cap, uint32_t *full,
+                                 uint32_t *qctr, const uint32_t *qsnap) {
+  if (threadIdx.x == 0) {
+    spawn_ctr[0] = min(min(*ovf_ctr, ovf_cap), cap);
+    spawn_ctr[1] = 0;
+    *ovf_ctr = 0;
+    *full = 0;
+    // the queue's untaken slots and the packets parked after its launch count: [min(head, count at launch), count)
+    if (qctr) qctr[1] = min(qctr[1], *qsnap);
+  }
+}
+
+// After a k_rpkt / k_kpkt launch over queue q: while its spawns filled the buffer, trace the buffer, move the
+// overflow records to its front and resume the launch on the slots it left.  A host round trip per launch, paid
+// only with virtual packets.
+template <typename F>
+int vpkt_drain(int q, F &&relaunch) {
+  if (!G.K.V.on) return 0;
+  while (true) {
+    HIPCHK(hipMemcpyAsync(G.h_vfull, G.K.V.full, sizeof(uint32_t), hipMemcpyDeviceToHost, G.stream));
+    HIPCHK(hipStreamSynchronize(G.stream));
+    if (!*G.h_vfull) return 0;
+    G.vpkt_drains++;
+    if (int rc = vpkt_flush()) return rc;
+    const DevVpkt &V = G.K.V;
+    k_vpkt_ovf_copy<<<1024, 256, 0, G.stream>>>(V.ovf, V.ovf_cap, V.ovf_ctr, V.spawn, V.cap);
+    k_vpkt_ovf_reset<<<1, 64, 0, G.stream>>>(V.ovf_ctr, V.ovf_cap, V.spawn_ctr, V.cap, V.full, G.W.ctr + 2 * q,
+                                             G.d_qsnap);
+    HIPCHK(hipMemcpyAsync(G.d_qsnap, G.W.ctr + 2 * q, sizeof(uint32_t), hipMemcpyDeviceToDevice, G.stream));
+    HIPCHK(hipGetLastError());
+    if (int rc = relaunch()) return rc;
+  }
 }
 int vpkt_collect(const unsigned long long before[8]) {
   G.last_vpkt_ms = 0.;
@@ -890,7 +1007,6 @@ int run_wavefront(int64_t n, int nts, double t2) {
   int64_t round = 0;
   bool done = false;
   for (; round < WAVE_MAX_ROUNDS && !done; round++) {
-    TSTART(0);
     // waves per SIMD k_rpkt is compiled for (ARTIS_GPU_RPKT_OCC = 1, 2 or 3).  The r-packet step needs ~300
     // registers; at 1 wave/SIMD nothing hides its FP64 latency, and forcing 2 (spilling to scratch) measured
     // 1.80 s -> 1.53 s per bench step on MI355X, so 2 is the default.
@@ -898,13 +1014,41 @@ int run_wavefront(int64_t n, int nts, double t2) {
       const char *e = getenv("ARTIS_GPU_RPKT_OCC");
       return (e && (e[0] == '1' || e[0] == '3')) ? e[0] - '0' : 2;
     }();
-    if (rpkt_occ == 3)
-      k_rpkt<3><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
-    else if (rpkt_occ == 2)
-      k_rpkt<2><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
-    else
-      k_rpkt<1><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+    // the R queue binned by cell (ARTIS_GPU_R_BIN=0: queue order); not with virtual packets, whose resumed
+    // launches read parked packets appended to the queue itself
+    W.r_binned = G.r_binned && !G.K.V.on && G.K.C.n_nonempty > 0;
+    if (W.r_binned) {
+      TSTART(3);
+      const int nne = G.K.C.n_nonempty;
+      HIPCHK(hipMemsetAsync(W.bins, 0, (size_t)(nne + 1) * sizeof(uint32_t), G.stream));
+      k_r_bin<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa);
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(G.d_scan_tmp, G.scan_tmp_bytes, W.bins, G.d_binoffs, nne + 1,
+                                              G.stream));
+      k_r_scatter<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_binoffs);
+      TEND(3);
+    }
+    auto launch_rpkt = [&]() -> int {
+      if (rpkt_occ == 3)
+        k_rpkt<3><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+      else if (rpkt_occ == 2)
+        k_rpkt<2><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+      else
+        k_rpkt<1><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+      return 0;
+    };
+    if (G.K.V.on)
+      HIPCHK(hipMemcpyAsync(G.d_qsnap, W.ctr + 2 * QR, sizeof(uint32_t), hipMemcpyDeviceToDevice, G.stream));
+    TSTART(0);
+    if (int rc = launch_rpkt()) return rc;
     TEND(0);
+    W.r_binned = 0;
+    if (int rc = vpkt_drain(QR, [&]() -> int {
+          TSTART(0);
+          if (int rc2 = launch_rpkt()) return rc2;
+          TEND(0);
+          return 0;
+        }))
+      return rc;
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QR, 0, 2 * sizeof(uint32_t), G.stream));
     TSTART(3);  // class 3: the macro-atom queue binning and the rare exact jumps (class 1 is k_ma alone)
     if (W.ma_binned) {
@@ -952,9 +1096,18 @@ int run_wavefront(int64_t n, int nts, double t2) {
       TEND(3);
       HIPCHK(hipMemsetAsync(W.ctr + 2 * QX, 0, 2 * sizeof(uint32_t), G.stream));
     }
+    if (G.K.V.on)
+      HIPCHK(hipMemcpyAsync(G.d_qsnap, W.ctr + 2 * QK, sizeof(uint32_t), hipMemcpyDeviceToDevice, G.stream));
     TSTART(2);
     k_kpkt<<<grid / 4, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
     TEND(2);
+    if (int rc = vpkt_drain(QK, [&]() -> int {
+          TSTART(2);
+          k_kpkt<<<grid / 4, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+          TEND(2);
+          return 0;
+        }))
+      return rc;
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QK, 0, 2 * sizeof(uint32_t), G.stream));
     if (int rc = vpkt_flush()) return rc;
     HIPCHK(hipGetLastError());
@@ -2337,6 +2490,12 @@ int artis_gpu_vpkt_init(const artis_vpkt_params *vp) {
   rc |= dalloc(&V.vgrid, (size_t)std::max<int64_t>(3 * V.vgrid_stride, 1));
   rc |= dalloc(&V.ctr, 8);
   rc |= dalloc(&V.spawn_ctr, 2);
+  V.ovf_cap = (uint32_t)((int64_t)G.wave_grid * WAVE_BLOCK);
+  rc |= dalloc(&V.ovf, (size_t)V.ovf_cap * VPKT_SPAWN_WORDS);
+  rc |= dalloc(&V.ovf_ctr, 1);
+  rc |= dalloc(&V.full, 1);
+  if (!G.d_qsnap) rc |= dalloc(&G.d_qsnap, 1);
+  if (!G.h_vfull) HIPCHK(hipHostMalloc((void **)&G.h_vfull, sizeof(uint32_t), hipHostMallocDefault));
   if (rc) return ARTIS_ERR_HIP;
   V.spawn = G.d_vpkt_spawn;
   V.cap = G.vpkt_spawn_cap;
@@ -2392,6 +2551,8 @@ int artis_gpu_vpkt_last_stats(double *ms, int64_t *spawns, int64_t *traces) {
   return 0;
 }
 
+int64_t artis_gpu_vpkt_last_drains(void) { return G.vpkt_drains; }
+
 int artis_gpu_vpkt_last_work(int64_t work[4]) {
   if (!work) return ARTIS_ERR_BAD_ARGUMENT;
   for (int i = 0; i < 4; i++) work[i] = G.last_vpkt_work[i];
@@ -2432,7 +2593,12 @@ void artis_gpu_finalize(void) {
   G.allocs.clear();
   free_packets();
   if (G.h_ctr) (void)hipHostFree(G.h_ctr);
+  if (G.h_vfull) (void)hipHostFree(G.h_vfull);
   if (G.d_vpkt_spawn) (void)hipFree(G.d_vpkt_spawn);
+  for (uint32_t *a : {G.d_vkey, G.d_vkey2, G.d_vidx, G.d_vperm})
+    if (a) (void)hipFree(a);
+  if (G.d_vsort_tmp) (void)hipFree(G.d_vsort_tmp);
+  if (G.h_vcount) (void)hipHostFree(G.h_vcount);
   for (hipEvent_t e : G.vev) (void)hipEventDestroy(e);
   for (hipEvent_t e : G.tev) (void)hipEventDestroy(e);
   for (int r = 0; r < 2; r++)
@@ -2463,12 +2629,16 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     int ncu = 256;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
     G.wave_grid = ncu * 8;  // 32 waves per CU of 256-thread blocks; late blocks find the queue drained
+    // (tests: ARTIS_GPU_WAVE_GRID=<blocks>, a multiple of 8, shrinks the persistent grids and the vpkt overflow records)
+    if (const char *wg = getenv("ARTIS_GPU_WAVE_GRID")) G.wave_grid = std::max(8, atoi(wg) / 8 * 8);
     const char *eng = getenv("ARTIS_GPU_ENGINE");
     G.use_megakernel = eng && std::string(eng) == "mega";
     // cell binning of the macro-atom queue (measured 5-15 % faster walks: lanes of a wave share a cell's
     // records) is on; per-XCD queue ranges measured neutral-to-negative and are off unless asked for
     const char *b = getenv("ARTIS_GPU_MA_BIN");
     G.W.ma_binned = !(b && b[0] == '0');
+    const char *rb = getenv("ARTIS_GPU_R_BIN");
+    G.r_binned = !(rb && rb[0] == '0');
     const char *xr = getenv("ARTIS_GPU_MA_XCD");
     G.W.ma_ranges = (xr && xr[0] == '1') ? 8 : 1;
     const char *rf = getenv("ARTIS_GPU_REFILL");
@@ -3267,6 +3437,12 @@ int artis_gpu_update_packets_resident(int my_rank, int nts) {
         G.d_ctx, G.d_soa, n, nts, t2);
     HIPCHK(hipGetLastError());
     if (int rc = vpkt_flush()) return rc;
+    if (G.K.V.on) {  // the megakernel does not park packets: trace the overflow records once all are done
+      const DevVpkt &V = G.K.V;
+      k_vpkt_ovf_copy<<<1024, 256, 0, G.stream>>>(V.ovf, V.ovf_cap, V.ovf_ctr, V.spawn, V.cap);
+      k_vpkt_ovf_reset<<<1, 64, 0, G.stream>>>(V.ovf_ctr, V.ovf_cap, V.spawn_ctr, V.cap, V.full, nullptr, nullptr);
+      if (int rc = vpkt_flush()) return rc;
+    }
   } else if (n > 0) {
     if (int rc = run_wavefront(n, nts, t2)) return rc;
   }

@@ -278,6 +278,18 @@ struct DevVpkt {
   double *spawn;
   uint32_t *spawn_ctr;      // [2]: appended, trace fetch head
   uint32_t cap;
+  // a full buffer: the spawn that found it full goes to the overflow records (same word-major layout, stride
+  // ovf_cap) and sets *full; k_rpkt / k_kpkt then take no new packets, k_rpkt parks each packet at its first
+  // overflow, and the host traces the buffer, moves the overflow records to its front and resumes the launch
+  // (engine.hip vpkt_drain).  ovf_cap covers one overflow per resident lane.
+  double *ovf;
+  // trace order: k_vpkt takes its work items observer-major over the spawns sorted by (propagation cell, log nu)
+  // (perm[j]: the j-th spawn in that order; nullptr: buffer order), so a wave traces parallel paths from one cell
+  // at nearby frequencies -- the same cells, linecoef rows and line windows
+  const uint32_t *perm;
+  uint32_t *ovf_ctr;        // [1]
+  uint32_t *full;           // [1]
+  uint32_t ovf_cap;
 };
 
 struct DevRun {

@@ -25,6 +25,7 @@ struct Tx {
   // k_rpkt: the J / nuJ / ffheating terms of the step's estimator segment are left here (est_mgi >= 0) and added
   // after the wave has converged (wave_flush_estimators), so that lanes in the same cell add once per wave
   bool defer_est = false;
+  bool vstop = false;  // a virtual-packet spawn found the buffer full (DevVpkt::full): park the packet
   int est_mgi = -1;
   double est_de = 0., est_denu = 0., est_deff = 0.;
 #ifdef ARTIS_STAMPS
@@ -927,14 +928,21 @@ DEVFN void vpkt_spawn(Tx &x, const Pkt &p, int realtype) {
     }
   }
   if (!any) return;
-  const uint32_t s = atomicAdd(&V.spawn_ctr[0], 1u);
-  if (s >= V.cap) {
-    fail(K, ERR_VPKT_OVERFLOW, p.number, (int)V.cap);
-    x.ok = false;
-    return;
-  }
-  const int64_t cap = V.cap;
+  uint32_t s = atomicAdd(&V.spawn_ctr[0], 1u);
+  int64_t cap = V.cap;
   double *sp = V.spawn;
+  if (s >= V.cap) {  // full: an overflow record, and the packet is parked by its kernel
+    *(volatile uint32_t *)V.full = 1u;
+    x.vstop = true;
+    s = atomicAdd(V.ovf_ctr, 1u);
+    if (s >= V.ovf_cap) {
+      fail(K, ERR_VPKT_OVERFLOW, p.number, (int)V.ovf_cap);
+      x.ok = false;
+      return;
+    }
+    cap = V.ovf_cap;
+    sp = V.ovf;
+  }
   for (int d = 0; d < 3; d++) {
     sp[d * cap + s] = p.pos[d];
     sp[(3 + d) * cap + s] = p.dir[d];

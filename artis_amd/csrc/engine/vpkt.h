@@ -400,8 +400,13 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
         const uint32_t slot = wave_reserve(&V.spawn_ctr[1], idle);
         if (idle) {
           if ((uint64_t)slot < nitems) {
-            v.s = slot / (uint32_t)V.nobs;
-            v.b = (int)(slot % (uint32_t)V.nobs);
+            if (V.perm) {
+              v.b = (int)(slot / nspawn);
+              v.s = V.perm[slot % nspawn];
+            } else {
+              v.s = slot / (uint32_t)V.nobs;
+              v.b = (int)(slot % (uint32_t)V.nobs);
+            }
             const double *sp = V.spawn;
             for (int k = 0; k < 3; k++) {
               v.pos0[k] = sp[k * cap + v.s];

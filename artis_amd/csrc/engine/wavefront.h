@@ -38,6 +38,7 @@ struct WaveState {
   uint32_t *xhead;     // [8] fetch heads of the per-XCD ranges of ma_sorted
   int ma_ranges;       // 8: blocks on XCD x take range x first (then steal), 1: one shared range
   int ma_binned;       // 1: k_ma reads ma_sorted, 0: k_ma reads q[QM]
+  int r_binned;        // 1: this k_rpkt launch reads the R queue binned by cell from ma_sorted (k_r_bin / k_r_scatter)
   int refill_min;      // a wave refetches work (and flushes its queue appends) once this many lanes are idle
   int refill_ma;       // the same for k_ma (a macro-atom refill is cheap: one coalesced ticket read)
   // cell-sorted macro-atom tickets written by k_ma_scatter when the key cache is on (else nullptr): per slot
@@ -170,7 +171,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
   const uint32_t nq = W.ctr[2 * QR];
   Pkt p;
   int32_t idx = -1;
-  bool have = false, drained = false, pendM = false, pendK = false;
+  bool have = false, drained = false, pendM = false, pendK = false, pendR = false;
   int steps = 0;
   double cmf_lum = 0.;
   unsigned long long st_pass = 0, st_busy = 0, st_refill = 0, st_trefill = 0, st_tstep = 0;
@@ -186,12 +187,16 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
       const unsigned long long tr0 = wave_clock();
       wave_push(W, QM, pendM, idx);  // appends deferred from the lanes' last retirement
       wave_push(W, QK, pendK, idx);
-      pendM = pendK = false;
-      if (imask) {
+      wave_push(W, QR, pendR, idx);  // packets parked on a full virtual-packet buffer (resumed by the host)
+      pendM = pendK = pendR = false;
+      // a full virtual-packet spawn buffer: take no new packets (wave-uniform read)
+      if (K.V.on && __builtin_amdgcn_readfirstlane(*(volatile uint32_t *)K.V.full)) {
+        drained = true;
+      } else if (imask) {
         const uint32_t slot = wave_reserve(&W.ctr[2 * QR + 1], idle);
         if (idle) {
           if (slot < nq) {
-            idx = W.q[QR][slot];
+            idx = W.r_binned ? W.ma_sorted[slot] : W.q[QR][slot];
             pkt_load_hot(soa, n, idx, p);
             x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
             x.rng.n = W.rng_n[idx];
@@ -215,12 +220,20 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
     x.tlast = ts0;
 #endif
     if (have) {
-      if (x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
+      if (!x.vstop && x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
         do_rpkt_step(x, p, t2, ColdSoa{soa, n, idx});
         STAMP(x, 4);
         if (++steps > RPKT_MAX_STEPS) x.err(ERR_STUCK, p.number, 1);
       }
-      if (!x.ok || p.type != ARTIS_TYPE_RPKT || !(p.prop_time < t2)) {
+      if (x.vstop && x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
+        // its spawn went to an overflow record: park the packet (between steps) for the resumed launch
+        pkt_store_hot(soa, n, idx, p);
+        W.rng_n[idx] = x.rng.n;
+        x.vstop = false;
+        pendR = true;
+        have = false;
+      } else if (!x.ok || p.type != ARTIS_TYPE_RPKT || !(p.prop_time < t2)) {
+        x.vstop = false;
         if (p.type == ARTIS_TYPE_ESCAPE) {
           cmf_lum += p.e_cmf;
           lwork(L, WK_ESCAPED, 1);
@@ -282,6 +295,27 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
     if (s != 0.) unsafeAtomicAdd(&K.E.scalars[0], s);
   }
   block_counters_flush(K, s_ctr, s_work);
+}
+
+// bin the R queue by cell before k_rpkt (the reference sorts its packets by cell before propagating them,
+// update_packets.cc:204-232): lanes of a wave start in one cell, on the same linecoef row and cell state.
+// Packets in empty cells share the last bin.  ma_key / ma_sorted are free while k_rpkt runs.
+__global__ void k_r_bin(const Ctx *__restrict__ ctxp, WaveState W, const uint64_t *__restrict__ soa) {
+  CTX_IN_LDS(ctxp)
+  const uint32_t nq = W.ctr[2 * QR];
+  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x) {
+    const int32_t idx = W.q[QR][slot];
+    const int mgi = cell_mgi(K, lo32(soa[PW(0, idx, 0)]));  // hot group: no n term
+    const int b = (mgi < K.G.npts_model) ? K.C.ne_index[mgi] : K.C.n_nonempty;
+    W.ma_key[slot] = b;
+    atomicAdd(&W.bins[b], 1u);
+  }
+}
+__global__ void k_r_scatter(const Ctx *__restrict__ ctxp, WaveState W, uint32_t *offs) {
+  CTX_IN_LDS(ctxp)
+  const uint32_t nq = W.ctr[2 * QR];
+  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x)
+    W.ma_sorted[atomicAdd(&offs[W.ma_key[slot]], 1u)] = W.q[QR][slot];
 }
 
 // bin the M queue by cell: count per cell and remember each slot's key
@@ -747,7 +781,22 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_kpkt(const Ctx *__restrict__ ctx
   L.ctr = &s_ctr[0];
   L.work = &s_work[0];
   const uint32_t nq = W.ctr[2 * QK];
-  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x) {
+  // with virtual packets the slots are taken 64 at a time from the fetch head, so that a full spawn buffer can stop
+  // the launch with the untaken slots [head, nq) left for the resumed launch (engine.hip vpkt_drain)
+  const bool dyn = K.V.on;
+  uint32_t slot = dyn ? 0u : blockIdx.x * blockDim.x + threadIdx.x;
+  for (;; slot += gridDim.x * blockDim.x) {
+    if (dyn) {
+      if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t *)K.V.full)) break;
+      uint32_t base = 0;
+      if (lane_id() == 0) base = atomicAdd(&W.ctr[2 * QK + 1], 64u);
+      base = __shfl(base, 0, 64);
+      if (base >= nq) break;
+      slot = base + (uint32_t)lane_id();
+      if (slot >= nq) continue;
+    } else if (slot >= nq) {
+      break;
+    }
     const int32_t idx = W.q[QK][slot];
     Pkt p;
     pkt_load(soa, n, idx, p);

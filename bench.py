@@ -305,6 +305,18 @@ def main():
         if rank == 0:
             print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
+    if rank == 0:  # a heartbeat while one long step runs (a 1.25e8-packet virtual-packet step takes minutes)
+        import threading
+
+        t_start = time.time()
+
+        def heartbeat():
+            while True:
+                time.sleep(60)
+                print(f"[bench] ... running, {time.time() - t_start:.0f} s", file=sys.stderr, flush=True)
+
+        threading.Thread(target=heartbeat, daemon=True).start()
+
     atom = {k: v for k, v in (("line_window", args.line_window), ("max_lines", args.max_lines),
                                 ("nlevels_per_ion", args.nlevels_per_ion)) if v is not None}
     model = Model(ngrid_1d=args.ngrid, **atom)
@@ -342,6 +354,7 @@ def main():
     ktimes = []
     vstats = []
     vwork = []
+    vdrains = []
 
     def step(record):
         eng.restore()
@@ -358,6 +371,7 @@ def main():
             ktimes.append(eng.last_kernel_times())
             if vcfg is not None:
                 vstats.append(eng.vpkt_last_stats())
+                vdrains.append(eng.vpkt_last_drains())
                 vwork.append(eng.vpkt_last_work())
 
     for w in range(args.warmup):
@@ -590,7 +604,8 @@ def main():
                                            f"vspec window 10-30 d, 3500-10000 A (vpkt.h defaults)")
             line["vpkt"] = {"ms": vms, "spawns": int(np.mean([v[1] for v in vstats])),
                             "traces": int(np.mean([v[2] for v in vstats])),
-                            "traces_per_s": float(np.mean([v[2] for v in vstats])) / max(vms / 1e3, 1e-12)}
+                            "traces_per_s": float(np.mean([v[2] for v in vstats])) / max(vms / 1e3, 1e-12),
+                            "buffer_drains": int(np.max(vdrains))}
             ntr = max(line["vpkt"]["traces"], 1)
             line["vpkt"]["work_per_trace"] = {k: float(np.mean([w[k] for w in vwork])) / ntr for k in vwork[0]}
         line["tables"] = tables

@@ -538,6 +538,9 @@ int artis_gpu_vpkt_last_stats(double *ms, int64_t *spawns, int64_t *traces);
 /* work counters of the last update's virtual packets: [0] cell segments (continuum-opacity evaluations),
  * [1] lines whose opacity was added, [2] active bf continua scanned, [3] virtual packets that escaped */
 int artis_gpu_vpkt_last_work(int64_t work[4]);
+/* launches of the last update resumed after the spawn buffer filled (ABI 9): the buffer was traced, the spawns
+ * that found it full moved to its front, and the r-packet / k-packet launch continued where it stopped */
+int64_t artis_gpu_vpkt_last_drains(void);
 
 int64_t artis_gpu_last_rounds(void);  /* event-queue rounds of the last update (0: megakernel path) */
 /* device time (ms, HIP events around every launch) and launch count of the last update per kernel class:
@@ -741,7 +744,8 @@ double artis_gpu_last_nlte_ms(void);  /* device time (ms) of the last artis_gpu_
                                     7: update_grid's temperature / ionisation solution (artis_gpu_solve_temperatures);
                                     8: update_grid for the nebular options (artis_gpu_update_grid_nlte),
                                        artis_te_params.direct_col_heat;
-                                    9: artis_gpu_table_info (per-cell table budgets) */
+                                    9: artis_gpu_table_info (per-cell table budgets), artis_gpu_vpkt_last_drains
+                                       (bounded virtual-packet spawn buffer) */
 int artis_gpu_abi_version(void);
 
 #ifdef __cplusplus

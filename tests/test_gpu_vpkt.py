@@ -108,16 +108,30 @@ def test_vpkt_multi_timestep_accumulates():
         eng.close()
 
 
-def test_vpkt_spawn_overflow_fails_loudly():
+def test_vpkt_full_spawn_buffer_drains_and_matches_oracle(monkeypatch):
+    """A spawn buffer far smaller than one round's spawns (2048 records, with the persistent grids shrunk to 2048
+    lanes so the overflow records are 2048 too): every launch that fills it is traced, its overflow records moved
+    to the front and the launch resumed where it stopped -- the packets, counters and spectra are the oracle's."""
+    monkeypatch.setenv("ARTIS_GPU_WAVE_GRID", "8")
     m = Model(**VCFG)
     m.set_timestep(NTS)
-    pk = m.init_rpackets(NTS, 2000, seed=44)
-    vc = ffi.VpktConfig(nz_obs=(0.3,), phi_obs_deg=(0.0,), spawn_capacity=16)
+    pk = m.init_rpackets(NTS, 40000, seed=44)
+    vc = ffi.VpktConfig(nz_obs=(0.3, -0.5), phi_obs_deg=(0.0, 120.0), exclude=(0.0, -1.0), spawn_capacity=16)
     eng = Engine(m)
     try:
         eng.vpkt_init(vc)
         eng.upload_cellstate(NTS)
-        with pytest.raises(Exception, match="device error code 15"):
-            eng.update_packets(NTS, pk.copy())
+        pg = pk.copy()
+        eg = eng.update_packets(NTS, pg)
+        vg = eng.vpkt_download()
+        drains = eng.vpkt_last_drains()
+        _, spawns, traces = eng.vpkt_last_stats()
     finally:
         eng.close()
+    po = pk.copy()
+    eo, vo, _ = oracle_lib.update_packets_vpkt(m, NTS, po, vc, nthreads=16)
+    parity.assert_packets_match(pg, po)
+    parity.assert_estimators_match(eg, eo)
+    _compare_vpkt(vg, vo)
+    assert drains > 0 and spawns > 2 * 2048, (drains, spawns)
+    assert traces == vo.counters()["nvpkt"]
