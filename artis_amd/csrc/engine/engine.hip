@@ -605,7 +605,7 @@ struct Engine {
   bool vpkt_sort = true;          // ARTIS_VPKT_SORT=0: trace in buffer order
   uint32_t *h_vfull = nullptr;    // pinned: DevVpkt::full after a launch
   int64_t vpkt_drains = 0;        // launches resumed after a full spawn buffer (last update_packets)
-  bool r_binned = true;           // bin the R queue by cell before k_rpkt (ARTIS_GPU_R_BIN)
+  bool r_binned = false;          // bin the R queue by cell before k_rpkt (ARTIS_GPU_R_BIN=1)
   std::vector<hipEvent_t> vev;  // (start, end) pairs around the k_vpkt launches of the last update
   size_t vev_used = 0;
   double last_vpkt_ms = 0.;
@@ -1014,7 +1014,7 @@ int run_wavefront(int64_t n, int nts, double t2) {
       const char *e = getenv("ARTIS_GPU_RPKT_OCC");
       return (e && (e[0] == '1' || e[0] == '3')) ? e[0] - '0' : 2;
     }();
-    // the R queue binned by cell (ARTIS_GPU_R_BIN=0: queue order); not with virtual packets, whose resumed
+    // the R queue binned by cell (ARTIS_GPU_R_BIN=1; default queue order); not with virtual packets, whose resumed
     // launches read parked packets appended to the queue itself
     W.r_binned = G.r_binned && !G.K.V.on && G.K.C.n_nonempty > 0;
     if (W.r_binned) {
@@ -2637,8 +2637,10 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     // records) is on; per-XCD queue ranges measured neutral-to-negative and are off unless asked for
     const char *b = getenv("ARTIS_GPU_MA_BIN");
     G.W.ma_binned = !(b && b[0] == '0');
+    // cell binning of the R queue before k_rpkt: measured no faster k_rpkt (1114 vs 1106 ms per bench step) and
+    // ~250 ms more binning per step (profiles/r03g_ab.txt), so off unless asked for (ARTIS_GPU_R_BIN=1)
     const char *rb = getenv("ARTIS_GPU_R_BIN");
-    G.r_binned = !(rb && rb[0] == '0');
+    G.r_binned = rb && rb[0] == '1';
     const char *xr = getenv("ARTIS_GPU_MA_XCD");
     G.W.ma_ranges = (xr && xr[0] == '1') ? 8 : 1;
     const char *rf = getenv("ARTIS_GPU_REFILL");

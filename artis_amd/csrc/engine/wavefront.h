@@ -50,11 +50,27 @@ struct WaveState {
 };
 
 DEVFN int lane_id() { return (int)__lane_id(); }
-DEVFN unsigned long long wave_clock() { return __builtin_amdgcn_s_memtime(); }
+// Per-pass wave diagnostics (passes, busy lanes, cycles per phase, lines scanned per pass; ARTIS_GPU_STATS=1
+// prints them) are compiled in only with -DARTIS_WAVE_STATS=1 or -DARTIS_STAMPS: the s_memtime reads wait on the
+// same counter as LDS traffic and the per-pass wave reductions cost LDS permutes in every pass.
+#ifndef ARTIS_WAVE_STATS
+#ifdef ARTIS_STAMPS
+#define ARTIS_WAVE_STATS 1
+#else
+#define ARTIS_WAVE_STATS 0
+#endif
+#endif
+DEVFN unsigned long long wave_clock() {
+#if ARTIS_WAVE_STATS
+  return __builtin_amdgcn_s_memtime();
+#else
+  return 0;
+#endif
+}
 DEVFN void wave_stats_flush(const WaveState &W, int c, unsigned long long passes, unsigned long long busy,
                             unsigned long long t0, unsigned long long refills, unsigned long long trefill,
                             unsigned long long tstep) {
-  if (lane_id() == 0) {
+  if (ARTIS_WAVE_STATS && lane_id() == 0) {
     atomicAdd(&W.stats[4 * c], passes);
     atomicAdd(&W.stats[4 * c + 1], busy);
     atomicAdd(&W.stats[4 * c + 2], wave_clock() - t0);
@@ -261,7 +277,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
     }
     wave_flush_estimators(x);  // the step's J / nuJ / ffheating terms, once per cell and wave where possible
     st_tstep += wave_clock() - ts0;
-    {
+    if (ARTIS_WAVE_STATS) {
       unsigned ml = x.wl, sl = x.wl, mb = x.wb, sb = x.wb;
       for (int off = 32; off > 0; off >>= 1) {
         ml = max(ml, (unsigned)__shfl_xor((int)ml, off, 64));
@@ -279,7 +295,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
   if (lane_id() == 0)
     for (int i = 0; i < 5; i++) atomicAdd(&W.stats[32 + i], x.st[i]);
 #endif
-  if (lane_id() == 0) {
+  if (ARTIS_WAVE_STATS && lane_id() == 0) {
     atomicAdd(&W.stats[24], st_lmax);
     atomicAdd(&W.stats[25], st_lsum);
     atomicAdd(&W.stats[26], st_bmax);
