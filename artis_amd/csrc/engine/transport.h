@@ -1072,92 +1072,104 @@ DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
   int snext = -1;
   double sdist = boundary_cross(x, p, &snext);
   STAMP(x, 0);
-  if (sdist == 0) {
+  // One inlined copy each of the cell change and of the move / estimator / move sequence, shared by the ways a
+  // step ends (the register pressure of k_rpkt grows with every inlined copy): cross = change cell (sdist == 0
+  // at once, or a step that ends on the boundary of another cell), boundary_step = the step ended on the boundary.
+  bool cross = (sdist == 0), boundary_step = false, find_nextline = false;
+  if (!cross) {
+    const double maxsdist = K.G.rmax * p.prop_time / K.G.tmin;
+    if (sdist > maxsdist) {
+      x.err(ERR_SDIST, p.number, p.where);
+      return false;
+    }
+    if (((snext != -99) && (snext < 0)) || (snext >= K.G.ngrid)) {
+      x.err(ERR_BADCELL, p.number, snext);
+      return false;
+    }
+    if (sdist > K.R.max_path_step) {
+      sdist = K.R.max_path_step;
+      snext = p.where;
+    }
+    const double tdist = (t2 - p.prop_time) * ARTIS_CLIGHT_PROP;
+    double edist;
+    int rpkt_eventtype = -1;
+    Kappa kap;
+    kap.nu = 0.;
+    kap.total = kap.es = kap.ff = kap.bf = kap.ffheating = 0.;
+    const int k = (mgi == npm) ? -1 : K.C.ne_index[mgi];
+    if (mgi == npm) {
+      edist = DBL_MAX;
+      find_nextline = true;
+    } else if (K.C.thick[mgi] == 1) {
+      // grey optically thick cell: electron scattering only (rpkt.cc:697-703); no continuum opacity is evaluated,
+      // so the estimator terms of this step use kappa = 0 (deviation D7)
+      const double kappa = K.C.kappagrey[mgi] * K.C.rho[mgi] * doppler_packet(K, p);
+      edist = (tau_next - 0.0) / kappa;
+      find_nextline = true;
+    } else {
+      edist = get_event(x, k, mgi, p, kap, &rpkt_eventtype, tau_next, fmin(tdist, sdist));
+      if (!x.ok) return false;
+    }
+    if (!(edist >= 0)) {
+      x.err(ERR_EDIST, p.number, 0);
+      return false;
+    }
+    // which distance ends the step (rpkt.cc:711-806: boundary, event, end of timestep)
+    int which;
+    double dist;
+    if ((sdist < tdist) && (sdist < edist)) {
+      which = 0;
+      dist = sdist;
+    } else if ((edist < sdist) && (edist < tdist)) {
+      which = 1;
+      dist = edist;
+    } else if ((tdist < sdist) && (tdist < edist)) {
+      which = 2;
+      dist = tdist;
+    } else {
+      x.err(ERR_NOEVENT, p.number, 1);
+      return false;
+    }
+    move_pkt_withtime(K, p, dist / 2.);
+    update_estimators(x, p, kap, dist);
+    if (which == 2) {
+      p.prop_time = t2;
+      move_pkt(K, p, dist / 2.);
+      p.last_event = p.last_event + 1000;
+      if (find_nextline) closest_transition_empty(K, p);
+      return false;
+    }
+    move_pkt_withtime(K, p, dist / 2.);
+    STAMP(x, 3);
+    if (which == 1) {
+      if (K.C.thick[mgi] == 1)
+        cold(x, p, [&](Tx &tx, Pkt &tp) { rpkt_event_thickcell(tx, tp); });
+      else if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_BB)
+        rpkt_event_boundbound(x, p);
+      else if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_CONT)
+        cold(x, p, [&](Tx &tx, Pkt &tp) {
+          const Kappa kc = kap;
+          rpkt_event_continuum(tx, tp, kc, k, mgi);
+        });
+      else
+        x.err(ERR_NOEVENT, p.number, 0);
+      return (x.ok && p.type == ARTIS_TYPE_RPKT && (mgi == npm || mgi == oldmgi));
+    }
+    boundary_step = true;
+    cross = (snext != p.where);
+  }
+  if (cross) {
     change_cell(x, p, snext);
     mgi = cell_mgi(K, p.where);
-    return (p.type == ARTIS_TYPE_RPKT && (mgi == npm || mgi == oldmgi));
   }
-  const double maxsdist = K.G.rmax * p.prop_time / K.G.tmin;
-  if (sdist > maxsdist) {
-    x.err(ERR_SDIST, p.number, p.where);
-    return false;
-  }
-  if (((snext != -99) && (snext < 0)) || (snext >= K.G.ngrid)) {
-    x.err(ERR_BADCELL, p.number, snext);
-    return false;
-  }
-  if (sdist > K.R.max_path_step) {
-    sdist = K.R.max_path_step;
-    snext = p.where;
-  }
-  const double tdist = (t2 - p.prop_time) * ARTIS_CLIGHT_PROP;
-  double edist;
-  int rpkt_eventtype = -1;
-  bool find_nextline = false;
-  Kappa kap;
-  kap.nu = 0.;
-  kap.total = kap.es = kap.ff = kap.bf = kap.ffheating = 0.;
-  const int k = (mgi == npm) ? -1 : K.C.ne_index[mgi];
-  if (mgi == npm) {
-    edist = DBL_MAX;
-    find_nextline = true;
-  } else if (K.C.thick[mgi] == 1) {
-    // grey optically thick cell: electron scattering only (rpkt.cc:697-703); no continuum opacity is evaluated,
-    // so the estimator terms of this step use kappa = 0 (deviation D7)
-    const double kappa = K.C.kappagrey[mgi] * K.C.rho[mgi] * doppler_packet(K, p);
-    edist = (tau_next - 0.0) / kappa;
-    find_nextline = true;
-  } else {
-    edist = get_event(x, k, mgi, p, kap, &rpkt_eventtype, tau_next, fmin(tdist, sdist));
-    if (!x.ok) return false;
-  }
-  if (!(edist >= 0)) {
-    x.err(ERR_EDIST, p.number, 0);
-    return false;
-  }
-  if ((sdist < tdist) && (sdist < edist)) {
-    move_pkt_withtime(K, p, sdist / 2.);
-    update_estimators(x, p, kap, sdist);
-    move_pkt_withtime(K, p, sdist / 2.);
-    STAMP(x, 3);
-    if (snext != p.where) {
-      change_cell(x, p, snext);
-      mgi = cell_mgi(K, p.where);
-    }
+  if (boundary_step) {
     p.scat_count = 0;
     p.last_event = p.last_event + 100;
     if (find_nextline) {
       if (mgi != npm && K.C.thick[mgi] != 1) closest_transition_empty(K, p);
     }
-    return (p.type == ARTIS_TYPE_RPKT && (mgi == npm || mgi == oldmgi));
-  } else if ((edist < sdist) && (edist < tdist)) {
-    move_pkt_withtime(K, p, edist / 2.);
-    update_estimators(x, p, kap, edist);
-    move_pkt_withtime(K, p, edist / 2.);
-    STAMP(x, 3);
-    if (K.C.thick[mgi] == 1)
-      cold(x, p, [&](Tx &tx, Pkt &tp) { rpkt_event_thickcell(tx, tp); });
-    else if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_BB)
-      rpkt_event_boundbound(x, p);
-    else if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_CONT)
-      cold(x, p, [&](Tx &tx, Pkt &tp) {
-        const Kappa kc = kap;
-        rpkt_event_continuum(tx, tp, kc, k, mgi);
-      });
-    else
-      x.err(ERR_NOEVENT, p.number, 0);
-    return (x.ok && p.type == ARTIS_TYPE_RPKT && (mgi == npm || mgi == oldmgi));
-  } else if ((tdist < sdist) && (tdist < edist)) {
-    move_pkt_withtime(K, p, tdist / 2.);
-    update_estimators(x, p, kap, tdist);
-    p.prop_time = t2;
-    move_pkt(K, p, tdist / 2.);
-    p.last_event = p.last_event + 1000;
-    if (find_nextline) closest_transition_empty(K, p);
-    return false;
   }
-  x.err(ERR_NOEVENT, p.number, 1);
-  return false;
+  return (p.type == ARTIS_TYPE_RPKT && (mgi == npm || mgi == oldmgi));
 }
 
 // ------------------------------------------------------------------------------------------ fb emission

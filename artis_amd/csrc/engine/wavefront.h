@@ -411,6 +411,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   const uint32_t nq = ((part == 1) ? min(*split, nq_all) : nq_all) - q0;
   const int32_t *queue = W.ma_binned ? W.ma_sorted : W.q[QM];
   const int nr = W.ma_ranges;
+  const int nr_log2 = (nr == 8) ? 3 : 0;  // W.ma_ranges is 1 or 8
   const double t_mid = K.G.ts_mid[nts];
   MaLane m;    // uncached walk
   MaLaneR mc;  // cached walk (resumable steps)
@@ -440,7 +441,9 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
       wave_push(W, QX, pendX, idx);
       pendR = pendK = pendX = false;
       if (imask) {
-        const uint32_t lo = q0 + (uint32_t)((uint64_t)nq * cur / nr), hi = q0 + (uint32_t)((uint64_t)nq * (cur + 1) / nr);
+        // (nr is 1 or 8: shifts, not the 64-bit division the compiler would expand into ~120 scalar instructions)
+        const uint32_t lo = q0 + (uint32_t)(((uint64_t)nq * cur) >> nr_log2),
+                       hi = q0 + (uint32_t)(((uint64_t)nq * (cur + 1)) >> nr_log2);
         const uint32_t slot = wave_reserve(&W.xhead[cur], idle);
         const bool got = idle && lo + slot < hi;
         if (got && CACHE && W.ma_tick) {
