@@ -2934,6 +2934,17 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   R.nt_on = rp->nt_on;
   R.nt_max_auger = rp->nt_max_auger_electrons;
   R.nts = -1;
+  R.comp_est = rp->comp_est;
+  R.comp_est_now = 0;
+  R.emiss_offset = rp->emiss_offset;
+  R.emiss_max = rp->emiss_max;
+  R.time_syn_first = rp->time_syn_first;
+  R.time_syn_last = rp->time_syn_last;
+  for (int d = 0; d < 3; d++) R.syn_dir[d] = rp->syn_dir[d];
+  if (R.comp_est && (R.emiss_max < 1 || R.emiss_max > ARTIS_EMISS_MAX)) {
+    G.last_error = "artis_run_params.emiss_max must be in [1, ARTIS_EMISS_MAX] with comp_est (input.cc:1821-1824)";
+    return ARTIS_ERR_BAD_ARGUMENT;
+  }
   if ((R.nlte_on && (!a->ion_nlevels_nlte || !a->ion_first_nlte || a->total_nlte_levels < 0)) ||
       (R.multibin && (a->radfield_nbins <= 0 || !a->radfield_nu_upper)) || R.nt_max_auger < 0) {
     G.last_error = "nebular run parameters without the atomic tables they need (ion_nlevels_nlte / radfield bins)";
@@ -2975,12 +2986,14 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   }
 
   // estimators: one double block [J | nuJ | ffheat | colheat | rpkt_emiss | gamma | bfheat | scalars(10) |
-  // bfrate_raw | radfield J_raw | nuJ_raw | contribcount] (the nebular sections only when their option is on)
+  // bfrate_raw | radfield J_raw | nuJ_raw | contribcount | compton_emiss] (the nebular sections only when their
+  // option is on)
   const int np = g->npts_model;
   const int64_t nion_est = (int64_t)np * ne * a->maxnions;
   G.nbf_est = R.detailed_bf ? nb : 0;
   G.nbins_est = T.rf_nbins;
-  G.n_est_doubles = 5 * (int64_t)np + 2 * nion_est + 10 + (int64_t)np * (G.nbf_est + 3 * G.nbins_est);
+  G.n_est_doubles = 5 * (int64_t)np + 2 * nion_est + 10 + (int64_t)np * (G.nbf_est + 3 * G.nbins_est) +
+                    ((int64_t)np + 1) * ARTIS_EMISS_MAX;
   rc |= dalloc(&G.d_estblock, G.n_est_doubles);
   DevEst &E = G.K.E;
   E.J = G.d_estblock;
@@ -2995,6 +3008,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   E.rfJ = E.bfrate + (int64_t)np * G.nbf_est;
   E.rfnuJ = E.rfJ + (int64_t)np * G.nbins_est;
   E.rfcount = E.rfnuJ + (int64_t)np * G.nbins_est;
+  E.compton = E.rfcount + (int64_t)np * G.nbins_est;
   rc |= dalloc(&E.ecounter, nli);
   rc |= dalloc(&E.acounter, nli);
   rc |= dalloc(&E.counters, ARTIS_COUNTER_COUNT + 1);
@@ -3241,6 +3255,20 @@ int artis_gpu_init_gamma(const artis_gamma_spectra *gs) {
   T.g_endecay = eg;
   T.g_energy = en;
   T.g_prob = pr;
+  // allnuc_gamma_line_list: every nuclide's lines sorted by energy (init_gamma_linelist, gammapkt.cc:192-211); the
+  // Compton emissivity bins by get_nul over its frequencies (gammapkt.cc:720-745)
+  std::vector<double> fs;
+  for (int k = 0; k < nn; k++)
+    for (int j = 0; j < gs->nuc_nlines[k]; j++) fs.push_back(gs->line_energy[gs->nuc_line_offset[k] + j]);
+  std::sort(fs.begin(), fs.end());
+  for (double &f : fs) f /= ARTIS_H;
+  T.g_nsorted = (int32_t)fs.size();
+  if (!fs.empty()) {
+    const double *dfs;
+    rc |= dupload(&dfs, fs.data(), fs.size());
+    if (rc) return ARTIS_ERR_HIP;
+    T.g_freq_sorted = dfs;
+  }
   return 0;
 }
 
@@ -3423,6 +3451,16 @@ int artis_gpu_update_packets_resident(int my_rank, int nts) {
   HIPCHK(hipMemcpy(&ts, G.K.G.ts_start + nts, sizeof(double), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(&tw, G.K.G.ts_width + nts, sizeof(double), hipMemcpyDeviceToHost));
   const double t2 = ts + tw;
+  {  // do_comp_est = do_r_lc ? false : estim_switch(nts) (sn3d.cc:539; emissivities.cc:250-257)
+    DevRun &R = G.K.R;
+    const double ts_want = R.time_syn_first * ((1. - G.K.G.rmax / G.K.G.tmin / ARTIS_CLIGHT_PROP));
+    const double te_want = R.time_syn_last * (1. + G.K.G.rmax / G.K.G.tmin / ARTIS_CLIGHT_PROP);
+    const int now = R.comp_est && !R.do_r_lc && ((ts > te_want) || (ts + tw < ts_want));
+    if (now != R.comp_est_now) {
+      R.comp_est_now = now;
+      if (int rc = sync_ctx()) return rc;
+    }
+  }
   HIPCHK(hipMemsetAsync(G.K.E.err, 0, 4 * sizeof(int32_t), G.stream));
   HIPCHK(hipMemsetAsync(G.K.E.work, 0, ARTIS_WORK_COUNT * sizeof(unsigned long long), G.stream));
   const int64_t n = G.npkts;
@@ -3500,6 +3538,11 @@ int artis_gpu_estimators_download(artis_estimators *est) {
     if (est->radfield_contribcount)
       for (int64_t j = 0; j < nbn; j++) est->radfield_contribcount[j] += (int64_t)llrint(blk[off_rf + 2 * nbn + j]);
   }
+  if (est->compton_emiss) {  // the double sums added to the caller's float array (globals::compton_emiss)
+    const int64_t off_ce = off_bf + (int64_t)np * (G.nbf_est + 3 * G.nbins_est);
+    for (int64_t j = 0; j < ((int64_t)np + 1) * ARTIS_EMISS_MAX; j++)
+      est->compton_emiss[j] = (float)((double)est->compton_emiss[j] + blk[off_ce + j]);
+  }
   std::vector<int32_t> lc(G.nlines);
   if (est->ecounter) {
     HIPCHK(hipMemcpy(lc.data(), G.K.E.ecounter, lc.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
@@ -3549,8 +3592,8 @@ int artis_gpu_estimator_block_from_device(const void *src) {
 // host mirror of the device block (artis_gpu_estimator_block_to_device / estimators_download)
 size_t artis_estimator_block_len(int np, int ne, int mi, int nl, int nbf, int nbins) {
   if (np < 0 || ne < 0 || mi < 0 || nl < 0 || nbf < 0 || nbins < 0) return 0;
-  return 5 * (size_t)np + 2 * (size_t)np * ne * mi + 10 + (size_t)np * (nbf + 3 * (size_t)nbins) + 2 * (size_t)nl +
-         ARTIS_COUNTER_COUNT + 1;
+  return 5 * (size_t)np + 2 * (size_t)np * ne * mi + 10 + (size_t)np * (nbf + 3 * (size_t)nbins) +
+         ((size_t)np + 1) * ARTIS_EMISS_MAX + 2 * (size_t)nl + ARTIS_COUNTER_COUNT + 1;
 }
 
 int artis_estimator_block_pack(const artis_estimators *est, int np, int ne, int mi, int nl, int nbf, int nbins,
@@ -3576,6 +3619,8 @@ int artis_estimator_block_pack(const artis_estimators *est, int np, int ne, int 
   put(est->radfield_nuJ_raw, (size_t)np * nbins);
   for (size_t j = 0; j < (size_t)np * nbins; j++)
     *b++ = est->radfield_contribcount ? (double)est->radfield_contribcount[j] : 0.;
+  for (size_t j = 0; j < ((size_t)np + 1) * ARTIS_EMISS_MAX; j++)
+    *b++ = est->compton_emiss ? (double)est->compton_emiss[j] : 0.;
   for (int j = 0; j < nl; j++) *b++ = est->ecounter ? est->ecounter[j] : 0.;
   for (int j = 0; j < nl; j++) *b++ = est->acounter ? est->acounter[j] : 0.;
   for (int j = 0; j < ARTIS_COUNTER_COUNT; j++) *b++ = (double)est->counters[j];
@@ -3623,6 +3668,9 @@ int artis_estimator_block_unpack(const double *b, int np, int ne, int mi, int nl
   for (size_t j = 0; j < (size_t)np * nbins; j++)
     if (est->radfield_contribcount) est->radfield_contribcount[j] = (int64_t)llrint(b[j]);
   b += (size_t)np * nbins;
+  for (size_t j = 0; j < ((size_t)np + 1) * ARTIS_EMISS_MAX; j++)
+    if (est->compton_emiss) est->compton_emiss[j] = (float)b[j];
+  b += ((size_t)np + 1) * ARTIS_EMISS_MAX;
   for (int j = 0; j < nl; j++)
     if (est->ecounter) est->ecounter[j] = (int32_t)llrint(b[j]);
   b += nl;

@@ -101,6 +101,8 @@ struct DevTab {
   int32_t g_nnuc;
   const int32_t *g_nlines, *g_off;
   const double *g_endecay, *g_energy, *g_prob;
+  int32_t g_nsorted;             // allnuc_gamma_line_list size (gammapkt.cc:192-211)
+  const double *g_freq_sorted;   // its frequencies (get_gam_freq, gammapkt.cc:702-718) in list order
 };
 
 // Record layout of the macro-atom key cache (DevCells::ma_key), in 16-bit key positions.  k_ma stages one 128-byte
@@ -241,6 +243,7 @@ struct DevEst {
   double *J, *nuJ, *ffheat, *colheat, *rpkt_emiss, *gamma, *bfheat;  // contiguous block, see engine.hip
   double *bfrate;                  // [npts_model * nbf] bfrate_raw (DETAILED_BF_ESTIMATORS_ON), in the block
   double *rfJ, *rfnuJ, *rfcount;   // [npts_model * rf_nbins] radfield bin estimators (contribcount as double)
+  double *compton;                 // [(npts_model + 1) * ARTIS_EMISS_MAX] compton_emiss (ABI 10), in the block
   int32_t *ecounter, *acounter;
   double *scalars;                 // [10] cmf_lum, gamma_dep, ... (artis_estimators order), nt_energy_deposited,
                                    // pellet_decays
@@ -306,6 +309,12 @@ struct DevRun {
   int32_t nts;     // timestep of the uploaded cell state (globals::nts_global for radfield / get_corrphotoioncoeff)
   int32_t nlte_on, multibin, first_nlte_rf, detailed_bf, detailed_bf_usefrom, no_lut_photoion, no_lut_bfheating;
   int32_t nt_on, nt_max_auger;
+  // ABI 10: Compton / pair-production emissivity estimators (emissivities.cc:14-136)
+  int32_t comp_est;      // the caller's switch (artis_run_params.comp_est)
+  int32_t comp_est_now;  // do_comp_est of the timestep being propagated (sn3d.cc:539, estim_switch)
+  int32_t emiss_offset, emiss_max;
+  double time_syn_first, time_syn_last;
+  double syn_dir[3];
 };
 
 #endif

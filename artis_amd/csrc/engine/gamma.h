@@ -339,6 +339,67 @@ DEVFN void rlc_emiss_gamma(const Ctx &K, const Pkt &p, double dist) {
   }
 }
 
+// get_nul (gammapkt.cc:720-745): the index of the line of allnuc_gamma_line_list to the red of freq
+#define GAMMA_RED_OF_LIST (-956)  // gammapkt.cc:33
+DEVFN int get_nul(const Ctx &K, double freq) {
+  const double *f = K.T.g_freq_sorted;
+  const int n = K.T.g_nsorted;
+  if (freq > f[n - 1]) return n - 1;
+  if (freq < f[0]) return GAMMA_RED_OF_LIST;
+  int too_high = n - 1, too_low = 0;
+  while (too_high != too_low + 1) {
+    const int tryindex = (too_high + too_low) / 2;
+    if (f[tryindex] >= freq)
+      too_high = tryindex;
+    else
+      too_low = tryindex;
+  }
+  return too_low;
+}
+
+// compton_emiss_cont (emissivities.cc:14-113): the Compton emissivity towards syn_dir of a gamma packet about to
+// travel dist, binned by the gamma-ray line to the red of the scattered frequency
+DEVNI void compton_emiss_cont(Tx &x, const Pkt &p, double dist) {
+  const Ctx &K = x.K;
+  const double t = p.prop_time;
+  const double vel_vec[3] = {p.pos[0] / t, p.pos[1] / t, p.pos[2] / t};
+  double cmf_dir[3], cmf_syn_dir[3];
+  angle_ab(p.dir, vel_vec, cmf_dir);
+  angle_ab(K.R.syn_dir, vel_vec, cmf_syn_dir);
+  const double mu_cmf = dot(cmf_dir, cmf_syn_dir);
+  if (mu_cmf > 1 || mu_cmf < -1) {  // "problem with Compton emissivity. Abort."
+    x.err(ERR_GAMMA, p.number, 20);
+    return;
+  }
+  const double f = 1 + (ARTIS_H * p.nu_cmf / ARTIS_ME / ARTIS_CLIGHT / ARTIS_CLIGHT * (1. - mu_cmf));
+  const double freq_out = p.nu_cmf / f;
+  const int lindex = get_nul(K, freq_out);
+  if ((lindex > K.R.emiss_offset - 1) && (lindex < K.R.emiss_offset + K.R.emiss_max - 1)) {
+    const double dsigma_domega_cmf = 0.0596831 * ARTIS_SIGMA_T / f / f * (f + (1. / f) + (mu_cmf * mu_cmf) - 1.);
+    const double dop_fac = doppler_pos_dir(K, p.pos, p.dir, p.prop_time);  // doppler_nucmf_on_nurf(dir, vel_vec)
+    const double emiss_cont = p.e_rf * dsigma_domega_cmf * dist * dop_fac * dop_fac / f;
+    if (lindex >= K.R.emiss_offset)  // (below: the reference's "scarily bad error" printout, nothing added)
+      safeadd(&K.E.compton[(int64_t)cell_mgi(K, p.where) * ARTIS_EMISS_MAX + lindex - K.R.emiss_offset], emiss_cont);
+  }
+}
+
+// pp_emiss_cont (emissivities.cc:115-136): pair-production emissivity in the last emissivity slot
+DEVFN void pp_emiss_cont(const Ctx &K, const Pkt &p, double dist) {
+  const double emiss_cont = sig_pair_prod(K, p) * (2.46636e+20 / p.nu_cmf) * p.e_rf * dist;
+  safeadd(&K.E.compton[(int64_t)cell_mgi(K, p.where) * ARTIS_EMISS_MAX + K.R.emiss_max - 1], 1.e-20 * emiss_cont);
+}
+
+// the estimators of one path segment of do_gamma (gammapkt.cc:618-625, 639-646, 653-660)
+DEVFN void gamma_segment_estimators(Tx &x, const Pkt &p, double dist, double kap_tot) {
+  if (kap_tot > 0) {
+    if (x.K.R.comp_est_now) {
+      compton_emiss_cont(x, p, dist);
+      pp_emiss_cont(x.K, p, dist);
+    }
+    if (x.K.R.do_rlc_est != 0) rlc_emiss_gamma(x.K, p, dist);
+  }
+}
+
 // gammapkt.cc:533-700: one step of a gamma packet (cell boundary, end of the timestep or an interaction)
 DEVNI void do_gamma(Tx &x, Pkt &p, double t2) {
   const Ctx &K = x.K;
@@ -376,24 +437,23 @@ DEVNI void do_gamma(Tx &x, Pkt &p, double t2) {
     x.err(ERR_EDIST, p.number, 11);
     return;
   }
-  const bool rlc = K.R.do_rlc_est != 0;
   if ((sdist < tdist) && (sdist < edist)) {
     p.prop_time += sdist / 2. / ARTIS_CLIGHT_PROP;
     move_pkt(K, p, sdist / 2.);
-    if (kap_tot > 0 && rlc) rlc_emiss_gamma(K, p, sdist);
+    gamma_segment_estimators(x, p, sdist, kap_tot);
     p.prop_time += sdist / 2. / ARTIS_CLIGHT_PROP;
     move_pkt(K, p, sdist / 2.);
     if (snext != p.where) change_cell(x, p, snext);
   } else if ((tdist < sdist) && (tdist < edist)) {
     p.prop_time += tdist / 2. / ARTIS_CLIGHT_PROP;
     move_pkt(K, p, tdist / 2.);
-    if (kap_tot > 0 && rlc) rlc_emiss_gamma(K, p, tdist);
+    gamma_segment_estimators(x, p, tdist, kap_tot);
     p.prop_time = t2;
     move_pkt(K, p, tdist / 2.);
   } else if ((edist < sdist) && (edist < tdist)) {
     p.prop_time += edist / 2. / ARTIS_CLIGHT_PROP;
     move_pkt(K, p, edist / 2.);
-    if (kap_tot > 0 && rlc) rlc_emiss_gamma(K, p, edist);
+    gamma_segment_estimators(x, p, edist, kap_tot);
     p.prop_time += edist / 2. / ARTIS_CLIGHT_PROP;
     move_pkt(K, p, edist / 2.);
     zrand = artis_rng_uniform(&x.rng);
@@ -543,10 +603,6 @@ DEVFN void do_gamma_family_step(Tx &x, Pkt &p, const PelletInfo &pi, double t2) 
       update_pellet(x, p, pi, t2);
       break;
     case ARTIS_TYPE_GAMMA:
-      if (!K.R.do_r_lc) {
-        x.err(ERR_UNSUPPORTED_TYPE, p.number, p.type);  // D8: Compton emissivity estimators not built
-        return;
-      }
       do_gamma(x, p, t2);
       if (p.type != ARTIS_TYPE_GAMMA && p.type != ARTIS_TYPE_ESCAPE) safeadd(&K.E.scalars[1], p.e_cmf);  // gamma_dep
       break;

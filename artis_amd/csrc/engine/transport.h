@@ -1653,7 +1653,11 @@ DEVFN void wave_fetch_issue(const void *base, uint32_t myline, WaveLines &w, lds
   const uint32_t ls[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
 #pragma unroll
   for (int i = 0; i < 8; i++)
+#ifdef ARTIS_MA_NT_FETCH  // A/B: streaming (non-temporal) line loads
+    w.c[i] = __builtin_nontemporal_load(&g[(size_t)(ls[i] == 0xffffffffu ? 0u : ls[i]) * 8 + (lane & 7)]);
+#else
     w.c[i] = g[(size_t)(ls[i] == 0xffffffffu ? 0u : ls[i]) * 8 + (lane & 7)];  // idle lanes: a harmless line-0 read
+#endif
 }
 DEVFN void wave_fetch_commit(const WaveLines &w, lds_uint4 *wl) {
   const int lane = (int)__lane_id();

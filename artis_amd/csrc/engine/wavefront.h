@@ -512,12 +512,20 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     if constexpr (CACHE) {
       // the level's metadata and, 8 lines per load instruction, every busy lane's record line; the lane's next two
       // draws are computed while they are in flight
+#ifdef ARTIS_MA_RNG_EARLY  // A/B: the draws before the loads are issued
+      if (have && mc.sel < 0) {
+        artis_rng r2 = rng;
+        z1 = artis_rng_uniform(&r2);
+        z2 = artis_rng_uniform(&r2);
+      }
+#endif
       if (have) meta = ma_meta_load(K, mc.ul);
       const uint32_t myline =
           have ? (uint32_t)(((uint64_t)(mc.block - K.C.ma_key) + (uint64_t)mc.rec_off) >> 6) + (uint32_t)mc.pline
                : 0xffffffffu;
       WaveLines wl;
       wave_fetch_issue(K.C.ma_key, myline, wl, (lds_u32 *)&s_xidx[threadIdx.x >> 6][0]);
+#ifndef ARTIS_MA_RNG_EARLY
       if (have && mc.sel < 0) {
 #ifdef ARTIS_DIAG_CHEAPRNG  // timing diagnostic only (wrong stream): the walk's cost without Philox
         uint64_t h = ((uint64_t)rng.key1 << 32) ^ rng.n;
@@ -531,6 +539,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
         z2 = artis_rng_uniform(&r2);
 #endif
       }
+#endif
       wave_fetch_commit(wl, line - (threadIdx.x & 63));
     }
 #ifdef ARTIS_STAMPS

@@ -90,9 +90,18 @@ class RunParams(C.Structure):
         ("nt_on", C.c_int32),
         ("nt_max_auger_electrons", C.c_int32),
         ("minpop", C.c_double),
+        # ABI 10: Compton / pair-production emissivity estimators (emissivities.cc:14-136)
+        ("comp_est", C.c_int32),
+        ("emiss_offset", C.c_int32),
+        ("emiss_max", C.c_int32),
+        ("_pad_comp", C.c_int32),
+        ("time_syn_first", C.c_double),
+        ("time_syn_last", C.c_double),
+        ("syn_dir", C.c_double * 3),
     ]
 
 
+EMISS_MAX = 2  # ARTIS_EMISS_MAX (globals.h:223)
 TEXC_TJ = 0
 TEXC_TE = 1
 
@@ -125,6 +134,8 @@ class Estimators(C.Structure):
         ("radfield_J_raw", C.POINTER(C.c_double)),
         ("radfield_nuJ_raw", C.POINTER(C.c_double)),
         ("radfield_contribcount", C.POINTER(C.c_int64)),
+        # ABI 10
+        ("compton_emiss", C.POINTER(C.c_float)),
     ]
 
 
@@ -202,6 +213,9 @@ class EstimatorArrays:
         s.gammaestimator, s.bfheatingestimator = dp(self.gamma), dp(self.bfheating)
         s.ecounter, s.acounter = ip(self.ecounter), ip(self.acounter)
         s.rpkt_emiss = dp(self.rpkt_emiss)
+        # globals::compton_emiss [(npts_model + 1) * EMISS_MAX] floats (grid.cc:1699)
+        self.compton_emiss = np.zeros((npts_model + 1) * EMISS_MAX, dtype=np.float32)
+        s.compton_emiss = self.compton_emiss.ctypes.data_as(C.POINTER(C.c_float))
         self.bfrate_raw = np.zeros(npts_model * nbfcontinua)
         self.radfield_J = np.zeros(npts_model * radfield_nbins)
         self.radfield_nuJ = np.zeros(npts_model * radfield_nbins)

@@ -296,6 +296,17 @@ typedef struct artis_run_params {
   double minpop;                        /* MINPOP: 1e-30 classic (artisoptions_classic.h:78), 1e-40 kilonova and
                                            nebular (artisoptions_kilonova_lte.h:79, artisoptions_nltenebular.h:82);
                                            0 is read as 1e-30 */
+  /* ABI 10: the Compton / pair-production emissivity estimators of gamma packets (compton_emiss_cont /
+     pp_emiss_cont, emissivities.cc:14-136, called from do_gamma, gammapkt.cc:619-657).  The reference sets
+     do_comp_est = do_r_lc ? false : estim_switch(nts) every timestep (sn3d.cc:539); the engine evaluates the same
+     rule per timestep when comp_est is 1 (0: never, for callers that do not ask for compton_emiss). */
+  int32_t comp_est;
+  int32_t emiss_offset;                 /* globals::emiss_offset = get_nul(nusyn_min) (input.cc:1813-1818) */
+  int32_t emiss_max;                    /* globals::emiss_max <= ARTIS_EMISS_MAX */
+  int32_t _pad_comp;
+  double time_syn_first, time_syn_last; /* time_syn[0], time_syn[nsyn_time - 1] of estim_switch
+                                           (emissivities.cc:250-257) */
+  double syn_dir[3];                    /* globals::syn_dir (the observer direction of compton_emiss_cont) */
 } artis_run_params;
 enum artis_excitation_temperature { ARTIS_TEXC_TJ = 0, ARTIS_TEXC_TE = 1 };
 
@@ -328,7 +339,11 @@ typedef struct artis_estimators {
   double *radfield_J_raw;      /* [npts_model * radfield_nbins] MULTIBIN_RADFIELD_MODEL_ON (radfield.cc:859-866) */
   double *radfield_nuJ_raw;
   int64_t *radfield_contribcount;
+  /* ABI 10 (may be NULL unless artis_run_params.comp_est is 1) */
+  float *compton_emiss;        /* [(npts_model + 1) * ARTIS_EMISS_MAX] globals::compton_emiss (grid.cc:1699), float as
+                                  the reference; the engine sums in double and adds its sum once */
 } artis_estimators;
+#define ARTIS_EMISS_MAX 2      /* EMISS_MAX (globals.h:223) */
 
 /* ------------------------------------------------------------------------------------------------------------ */
 /* Gamma-ray line spectra per nuclide, as read by read_gamma_spectrum (gammapkt.cc:58-89) into gamma_spectra    */
@@ -440,7 +455,8 @@ int artis_gpu_estimator_block_from_device(const void *src_device);
  *   [J | nuJ | ffheating | colheating | rpkt_emiss (npts_model each) | gammaestimator | bfheatingestimator
  *    (npts_model * nelements * maxnions each) | cmf_lum gamma_dep positron_dep electron_dep electron_emission
  *    alpha_dep alpha_emission gamma_emission nt_energy_deposited pellet_decays | bfrate_raw (npts_model * nbf_est)
- *   | radfield_J_raw | radfield_nuJ_raw | radfield_contribcount (npts_model * nbins_est each) | ecounter | acounter
+ *   | radfield_J_raw | radfield_nuJ_raw | radfield_contribcount (npts_model * nbins_est each)
+ *   | compton_emiss ((npts_model + 1) * ARTIS_EMISS_MAX, as float64; ABI 10) | ecounter | acounter
  *    (nlines each) | counters (ARTIS_COUNTER_COUNT) | nesc]   -- counts as float64 (exact below 2^53).
  * nbf_est = nbfcontinua under DETAILED_BF_ESTIMATORS_ON, else 0; nbins_est = radfield_nbins under
  * MULTIBIN_RADFIELD_MODEL_ON, else 0 (the engine's block has the sections its run parameters switch on).
@@ -735,7 +751,7 @@ typedef struct artis_nlte_cells {
 int artis_gpu_update_grid_nlte(const artis_nt_shells *nt, const artis_nlte_params *params, artis_nlte_cells *cells);
 double artis_gpu_last_nlte_ms(void);  /* device time (ms) of the last artis_gpu_update_grid_nlte */
 
-#define ARTIS_GPU_ABI_VERSION 9  /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
+#define ARTIS_GPU_ABI_VERSION 10 /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
                                     3: virtual packets (artis_vpkt_params / artis_vpkt_result);
                                     4: artis_run_params.excitation_temperature;
                                     5: host estimator block pack/unpack, RCCL communicator + all-reduce;
@@ -745,7 +761,9 @@ double artis_gpu_last_nlte_ms(void);  /* device time (ms) of the last artis_gpu_
                                     8: update_grid for the nebular options (artis_gpu_update_grid_nlte),
                                        artis_te_params.direct_col_heat;
                                     9: artis_gpu_table_info (per-cell table budgets), artis_gpu_vpkt_last_drains
-                                       (bounded virtual-packet spawn buffer) */
+                                       (bounded virtual-packet spawn buffer);
+                                   10: Compton / pair-production emissivity estimators (artis_run_params.comp_est,
+                                       artis_estimators.compton_emiss, a section of the estimator block) */
 int artis_gpu_abi_version(void);
 
 #ifdef __cplusplus

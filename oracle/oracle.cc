@@ -30,8 +30,8 @@
 //   D7 In a grey optically thick cell no continuum opacity is evaluated; the reference's update_estimators then
 //       adds ffheating / gamma / bfheating terms with the kappa its OpenMP thread computed last for some other
 //       packet (rpkt.cc:583, 1166), a per-thread artefact.  Here those terms are zero.
-//   D8 Gamma packets need do_r_lc (do_comp_est = false, sn3d.cc:539): the Compton emissivity estimators
-//       (emissivities.cc:14-137) are not restated; every reference test configuration sets do_r_lc.
+//   D8 (withdrawn in round 3: the Compton / pair-production emissivity estimators of emissivities.cc:14-136 are
+//       restated, artis_run_params.comp_est; gamma packets run with do_r_lc = 0.)
 //   D9 Virtual packets (vpkt.cc:76-406): when no redder line is left, rlc_emiss_vpkt's line loop ends and the
 //       virtual packet moves on to the cell boundary (the reference keeps ldist = 0 < sdist and spins forever);
 //       a spectrum bin index that rounds up to the array end is skipped (the reference writes past the array).
@@ -80,6 +80,8 @@ struct Ctx {
   std::vector<int32_t> slot_allcont;  // photoionisation target slot -> allcont index (get_bfcontindex)
   const artis_gamma_spectra *gs;  // may be NULL: no pellets / gamma packets in the ensemble
   const VpktCfg *vp = nullptr;    // NULL: VPKT_ON undefined
+  bool do_comp_est = false;       // globals::do_comp_est of this timestep (sn3d.cc:539)
+  std::vector<double> gam_freq;   // get_gam_freq over allnuc_gamma_line_list (gammapkt.cc:192-211, 702-718)
 };
 
 struct Est {
@@ -948,6 +950,10 @@ double col_ionization_ratecoeff(const Ctx &c, float T_e, float nne, int e, int i
 
 // --------------------------------------------------------------------------------------------- estimators
 inline void safeadd(double *p, double v) {
+#pragma omp atomic update
+  *p += v;
+}
+inline void safeadd(float *p, double v) {  // globals::compton_emiss is float (grid.cc:1699)
 #pragma omp atomic update
   *p += v;
 }
@@ -2970,6 +2976,56 @@ void rlc_emiss_gamma(const Ctx &c, Est &E, const artis_packet *p, double dist) {
   }
 }
 
+// gammapkt.cc:720-745
+constexpr int RED_OF_LIST = -956;  // gammapkt.cc:33
+int get_nul(const Ctx &c, double freq) {
+  const std::vector<double> &f = c.gam_freq;
+  const double freq_max = f[f.size() - 1];
+  const double freq_min = f[0];
+  if (freq > freq_max) return (int)f.size() - 1;
+  if (freq < freq_min) return RED_OF_LIST;
+  int too_high = (int)f.size() - 1;
+  int too_low = 0;
+  while (too_high != too_low + 1) {
+    const int tryindex = (too_high + too_low) / 2;
+    const double freq_try = f[tryindex];
+    if (freq_try >= freq)
+      too_high = tryindex;
+    else
+      too_low = tryindex;
+  }
+  return too_low;
+}
+
+// emissivities.cc:14-113
+void compton_emiss_cont(const Ctx &c, Est &E, const artis_packet *p, double dist) {
+  double vel_vec[3];
+  double cmf_dir[3];
+  double cmf_syn_dir[3];
+  get_velocity(p->pos, vel_vec, p->prop_time);
+  angle_ab(p->dir, vel_vec, cmf_dir);
+  angle_ab(c.rp.syn_dir, vel_vec, cmf_syn_dir);
+  const double mu_cmf = dot(cmf_dir, cmf_syn_dir);
+  if (mu_cmf > 1 || mu_cmf < -1) gamma_fatal("problem with Compton emissivity", p);
+  const double f = 1 + (ARTIS_H * p->nu_cmf / ARTIS_ME / ARTIS_CLIGHT / ARTIS_CLIGHT * (1. - mu_cmf));
+  const double freq_out = p->nu_cmf / f;
+  const int lindex = get_nul(c, freq_out);
+  if ((lindex > c.rp.emiss_offset - 1) && (lindex < c.rp.emiss_offset + c.rp.emiss_max - 1)) {
+    const double dsigma_domega_cmf = 0.0596831 * ARTIS_SIGMA_T / f / f * (f + (1. / f) + (mu_cmf * mu_cmf) - 1.);
+    const double dop_fac = doppler_nucmf_on_nurf(c, p->dir, vel_vec);
+    const double emiss_cont = p->e_rf * dsigma_domega_cmf * dist * dop_fac * dop_fac / f;
+    if (lindex >= c.rp.emiss_offset && E.e->compton_emiss)
+      safeadd(&E.e->compton_emiss[cell_mgi(c, p->where) * ARTIS_EMISS_MAX + lindex - c.rp.emiss_offset], emiss_cont);
+  }
+}
+
+// emissivities.cc:115-136
+void pp_emiss_cont(const Ctx &c, Est &E, const artis_packet *p, double dist) {
+  const double emiss_cont = sig_pair_prod(c, p) * (2.46636e+20 / p->nu_cmf) * p->e_rf * dist;
+  if (E.e->compton_emiss)
+    safeadd(&E.e->compton_emiss[cell_mgi(c, p->where) * ARTIS_EMISS_MAX + c.rp.emiss_max - 1], 1.e-20 * emiss_cont);
+}
+
 // gammapkt.cc:533-700: one step of a gamma packet (cell boundary, end of timestep or interaction)
 void do_gamma(const Ctx &c, Est &E, artis_rng *rng, artis_packet *p, double t2) {
   double zrand = artis_rng_uniform_pos(rng);
@@ -2998,20 +3054,38 @@ void do_gamma(const Ctx &c, Est &E, artis_rng *rng, artis_packet *p, double t2) 
   if ((sdist < tdist) && (sdist < edist)) {
     p->prop_time += sdist / 2. / ARTIS_CLIGHT_PROP;
     move_pkt(c, p, sdist / 2.);
-    if (kap_tot > 0 && rlc) rlc_emiss_gamma(c, E, p, sdist);
+    if (kap_tot > 0) {
+      if (c.do_comp_est) {
+        compton_emiss_cont(c, E, p, sdist);
+        pp_emiss_cont(c, E, p, sdist);
+      }
+      if (rlc) rlc_emiss_gamma(c, E, p, sdist);
+    }
     p->prop_time += sdist / 2. / ARTIS_CLIGHT_PROP;
     move_pkt(c, p, sdist / 2.);
     if (snext != p->where) change_cell(E, p, snext);
   } else if ((tdist < sdist) && (tdist < edist)) {
     p->prop_time += tdist / 2. / ARTIS_CLIGHT_PROP;
     move_pkt(c, p, tdist / 2.);
-    if (kap_tot > 0 && rlc) rlc_emiss_gamma(c, E, p, tdist);
+    if (kap_tot > 0) {
+      if (c.do_comp_est) {
+        compton_emiss_cont(c, E, p, tdist);
+        pp_emiss_cont(c, E, p, tdist);
+      }
+      if (rlc) rlc_emiss_gamma(c, E, p, tdist);
+    }
     p->prop_time = t2;
     move_pkt(c, p, tdist / 2.);
   } else if ((edist < sdist) && (edist < tdist)) {
     p->prop_time += edist / 2. / ARTIS_CLIGHT_PROP;
     move_pkt(c, p, edist / 2.);
-    if (kap_tot > 0 && rlc) rlc_emiss_gamma(c, E, p, edist);
+    if (kap_tot > 0) {
+      if (c.do_comp_est) {
+        compton_emiss_cont(c, E, p, edist);
+        pp_emiss_cont(c, E, p, edist);
+      }
+      if (rlc) rlc_emiss_gamma(c, E, p, edist);
+    }
     p->prop_time += edist / 2. / ARTIS_CLIGHT_PROP;
     move_pkt(c, p, edist / 2.);
     zrand = artis_rng_uniform(rng);
@@ -3173,7 +3247,7 @@ int do_packet(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_packe
       update_pellet(c, E, rng, p, nts, t2);
       return 0;
     case ARTIS_TYPE_GAMMA:
-      if (!c.gs || !c.rp.do_r_lc) return ARTIS_ERR_UNSUPPORTED;
+      if (!c.gs) return ARTIS_ERR_UNSUPPORTED;
       do_gamma(c, E, rng, p, t2);
       if (p->type != ARTIS_TYPE_GAMMA && p->type != ARTIS_TYPE_ESCAPE) safeadd(&E.e->gamma_dep, p->e_cmf);
       return 0;
@@ -3294,6 +3368,22 @@ int update_packets_impl(const artis_atomic_tables *at, const artis_geometry *geo
   c.nts = nts;
   c.minpop = rp->minpop > 0. ? rp->minpop : 1e-30;
   if (int rc = check_nebular_inputs(at, cs, rp, est)) return rc;
+  {
+    // do_comp_est = do_r_lc ? false : estim_switch(nts) (sn3d.cc:539, emissivities.cc:250-257)
+    const double tstart = geom->ts_start[nts];
+    const double tend = geom->ts_start[nts] + geom->ts_width[nts];
+    const double ts_want = rp->time_syn_first * ((1. - geom->rmax / geom->tmin / ARTIS_CLIGHT_PROP));
+    const double te_want = rp->time_syn_last * (1. + geom->rmax / geom->tmin / ARTIS_CLIGHT_PROP);
+    c.do_comp_est = rp->comp_est && !rp->do_r_lc && ((tstart > te_want) || (tend < ts_want));
+    if (c.do_comp_est && (!gs || rp->emiss_max < 1 || rp->emiss_max > ARTIS_EMISS_MAX)) return ARTIS_ERR_BAD_ARGUMENT;
+    if (c.do_comp_est) {  // allnuc_gamma_line_list sorted by energy (init_gamma_linelist, gammapkt.cc:192-211)
+      for (int k = 0; k < gs->nnuclides; k++)
+        for (int j = 0; j < gs->nuc_nlines[k]; j++) c.gam_freq.push_back(gs->line_energy[gs->nuc_line_offset[k] + j]);
+      std::sort(c.gam_freq.begin(), c.gam_freq.end());
+      for (double &f : c.gam_freq) f /= ARTIS_H;
+      if (c.gam_freq.empty()) return ARTIS_ERR_BAD_ARGUMENT;
+    }
+  }
   {
     // get_bfcontindex (radfield.cc:1329-1341): the allcont entry of each photoionisation target
     int64_t ntg = 0;

@@ -105,6 +105,12 @@ def assert_estimators_match(eg, eo, exact_counts=True, rtol=ESTIMATOR_RTOL):
         if y.size:
             scale = max(np.abs(y).max(), 1e-300)
             assert np.abs(x - y).max() <= rtol * scale, (name, np.abs(x - y).max() / scale)
+    # Compton / pair-production emissivities (float, as globals::compton_emiss): float rounding of the sums
+    x, y = getattr(eg, "compton_emiss", np.zeros(0)), getattr(eo, "compton_emiss", np.zeros(0))
+    if y.size and np.abs(y).max() > 0:
+        scale = float(np.abs(y).max())
+        assert np.abs(x.astype(np.float64) - y).max() <= max(rtol, 2e-6) * scale, (
+            "compton_emiss", np.abs(x.astype(np.float64) - y).max() / scale)
     if exact_counts and getattr(eo, "radfield_count", np.zeros(0)).size:
         assert np.array_equal(eg.radfield_count, eo.radfield_count)
     if exact_counts:

@@ -130,3 +130,25 @@ def test_pellets_without_gamma_spectra_fail_loudly(engine_factory):
     eng.upload_cellstate(0)
     with pytest.raises(EngineError):
         eng.update_packets(0, pk.copy())
+
+
+def test_compton_emissivity_estimators_match_oracle(engine_factory):
+    """Gamma-ray light-curve mode (do_r_lc = 0) with the Compton / pair-production emissivity estimators
+    (emissivities.cc:14-136) on: packets identical, compton_emiss within float rounding of the oracle's."""
+    from test_oracle_gamma import compton_params
+
+    m = Model(**GAMMA_CFG)
+    p = compton_params(m, outside_window=True)
+    eng = engine_factory(m, params=p)
+    pk = m.init_pellets(3000, seed=42)
+    pg, po = pk.copy(), pk.copy()
+    filled = 0
+    for nts in range(0, 4):
+        m.set_timestep(nts)
+        eng.upload_cellstate(nts)
+        eg = eng.update_packets(nts, pg)
+        eo, _ = oracle_lib.update_packets(m, nts, po, nthreads=16, params=p)
+        parity.assert_packets_match(pg, po)
+        parity.assert_estimators_match(eg, eo)
+        filled += int((eo.compton_emiss > 0).sum())
+    assert filled > 10

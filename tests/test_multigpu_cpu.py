@@ -86,7 +86,7 @@ def test_estimator_allreduce_world2(tmp_path):
     assert tot.struct.nesc == e0.struct.nesc + e1.struct.nesc
     assert (tot.acounter == e0.acounter + e1.acounter).all()
     assert np.allclose(tot.gamma, e0.gamma + e1.gamma, rtol=1e-14)
-    assert tot.struct.cmf_lum == b0[adist.block_len(m.npts_model, m.nelements, m.maxnions, 0) - 45]
+    assert tot.struct.cmf_lum == b0[off]
     assert tot.struct.cmf_lum == (e0.struct.cmf_lum + e1.struct.cmf_lum) / 2
     assert len(b0) == adist.block_len(m.npts_model, m.nelements, m.maxnions, m.nlines)
 
@@ -131,9 +131,11 @@ def test_block_layout_is_the_device_layout():
     for k in range(ffi.ARTIS_COUNTER_COUNT):
         s.counters[k] = 100 + k
     s.nesc = 23
+    est.compton_emiss[:] = np.arange(len(est.compton_emiss)) + 0.25  # ABI 10: (npts_model + 1) * EMISS_MAX floats
     b = adist.pack_estimators(est)
     ni = np_ * ne * mi
     expect = np.concatenate([np.repeat([1, 2, 3, 4, 5], np_), np.full(ni, 6), np.full(ni, 7), np.arange(11, 21),
+                             np.arange((np_ + 1) * ffi.EMISS_MAX) + 0.25,
                              np.full(nl, 21), np.full(nl, 22), 100 + np.arange(ffi.ARTIS_COUNTER_COUNT), [23]])
     assert np.array_equal(b, expect.astype(np.float64))
     back = adist.unpack_estimators(b, ffi.EstimatorArrays(np_, ne, mi, nl))
@@ -160,7 +162,8 @@ def test_block_layout_with_nebular_sections():
     off += np_ * nbf
     assert np.all(b[off:off + np_ * nbins] == 7) and np.all(b[off + np_ * nbins:off + 2 * np_ * nbins] == 8)
     assert np.array_equal(b[off + 2 * np_ * nbins:off + 3 * np_ * nbins], est.radfield_count.astype(np.float64))
-    assert np.all(b[off + 3 * np_ * nbins:off + 3 * np_ * nbins + nl] == 21)
+    off_ce = off + 3 * np_ * nbins  # the Compton emissivity section (ABI 10), then the line counters
+    assert np.all(b[off_ce + (np_ + 1) * ffi.EMISS_MAX:off_ce + (np_ + 1) * ffi.EMISS_MAX + nl] == 21)
     back = adist.unpack_estimators(b, ffi.EstimatorArrays(np_, ne, mi, nl, nbf, nbins))
     assert np.array_equal(back.radfield_count, est.radfield_count)
     assert np.array_equal(adist.pack_estimators(back), b)

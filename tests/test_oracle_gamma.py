@@ -63,3 +63,60 @@ def test_gamma_line_fixtures_match_reference_format():
                for j in range(6))
     assert np.isclose(gs.nuc_endecay_gamma[0], e_ni, rtol=1e-14)
     assert np.isclose(e_ni / 1.6021772e-6, 1.72812, rtol=1e-9)  # 56Ni: 1.728 MeV of gamma rays per decay
+
+
+ARTIS_H = 6.6260755e-27
+
+
+def gamma_line_freqs(m):
+    """get_gam_freq over allnuc_gamma_line_list: every line of the uploaded spectra sorted by energy
+    (init_gamma_linelist, gammapkt.cc:192-211)."""
+    gs = ffi.GammaSpectra.from_address(m.gamma_spectra)
+    en = [gs.line_energy[gs.nuc_line_offset[k] + j] for k in range(gs.nnuclides) for j in range(gs.nuc_nlines[k])]
+    return np.sort(np.array(en)) / ARTIS_H
+
+
+def compton_params(m, outside_window=True):
+    """Run parameters of a gamma-ray light-curve run (do_r_lc = 0) with the Compton / pair-production emissivity
+    estimators (sn3d.cc:539): the synthesis frequency range [nusyn_min, nusyn_max] spans the widest gap between two
+    consecutive gamma-ray lines, so emiss_offset = get_nul(nusyn_min) = i and emiss_max = 2 (input.cc:1813-1818);
+    the synthesis time window lies after the run (estim_switch true: estimators on) or around every timestep (off)."""
+    p = ffi.RunParams.from_buffer_copy(m.params)
+    f = gamma_line_freqs(m)
+    i = int(np.argmax(np.diff(np.log(f))))
+    p.do_r_lc = 0
+    p.comp_est = 1
+    p.emiss_offset = i
+    p.emiss_max = 2
+    p.syn_dir[:] = (0.0, 0.0, 1.0)
+    day = 86400.0
+    if outside_window:
+        p.time_syn_first = p.time_syn_last = 1e3 * m.cfg.tmax_days * day
+    else:
+        p.time_syn_first, p.time_syn_last = 0.0, 1e3 * m.cfg.tmax_days * day
+    return p
+
+
+def test_compton_emissivity_estimators():
+    """compton_emiss_cont / pp_emiss_cont (emissivities.cc:14-136) from do_gamma (gammapkt.cc:618-660): they add to
+    globals::compton_emiss only in timesteps outside the synthesis window (estim_switch) and never change a packet."""
+    m = Model(**CFG)
+    pk = m.init_pellets(1500, seed=41)
+    on = compton_params(m, outside_window=True)
+    off = compton_params(m, outside_window=False)
+    tot = np.zeros((m.npts_model + 1, ffi.EMISS_MAX))
+    for nts in range(0, 3):
+        m.set_timestep(nts)
+        a, b = pk.copy(), pk.copy()
+        ea, _ = oracle_lib.update_packets(m, nts, a, nthreads=4, params=on)
+        eb, _ = oracle_lib.update_packets(m, nts, b, nthreads=4, params=off)
+        assert a.tobytes() == b.tobytes()  # estimators only
+        assert not eb.compton_emiss.any()
+        ce = ea.compton_emiss.reshape(m.npts_model + 1, ffi.EMISS_MAX)
+        assert (ce >= 0).all()
+        tot += ce
+        pk = a
+    # both slots filled: Compton scatterings into the selected line gap, and pair production (nu > 1.022 MeV)
+    assert (tot[:, 0] > 0).sum() > 3 and (tot[:, 1] > 0).sum() > 3
+    # the empty-cell row (mgi == npts_model) only collects what packets in empty cells add
+    assert np.isfinite(tot).all()
