@@ -830,7 +830,8 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
       const double nu_max_phixs = nu_edge * K.T.last_phixs_nuovernuedge;
       if (nu >= nu_edge && nu <= nu_max_phixs) {
         double gc = 0., nnlevel;
-        if (!(kap.nu < nu_edge) && !bf_contribution(K, k, mgi, i, kap.nu, &nnlevel, &gc)) gc = 0.;
+        // (without do_r_lc no bf opacity is evaluated and the zero-initialised gamma_contr stays 0, rpkt.cc:1230)
+        if (!K.R.do_r_lc || (!(kap.nu < nu_edge) && !bf_contribution(K, k, mgi, i, kap.nu, &nnlevel, &gc))) gc = 0.;
         safeadd(&K.E.bfrate[row + i], gc * d_over_nu);
       } else if (nu < nu_edge) {
         break;
@@ -855,8 +856,9 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
       const int element = K.T.groundcont_element[g];
       if (K.C.elem_abundance[(int64_t)mgi * K.T.nelements + element] > 0) {
         // groundcont_gamma_contr[g] at the frequency the opacity was computed at (rpkt.cc:1166-1171)
+        // (zero without do_r_lc: calculate_kappa_bf_gammacontr never runs, input.cc:1462-1468, rpkt.cc:1230)
         double gcontr = 0.;
-        for (int q = K.T.gc_cont_off[g]; q < K.T.gc_cont_off[g + 1]; q++) {  // ascending allcont order
+        for (int q = K.T.gc_cont_off[g]; K.R.do_r_lc && q < K.T.gc_cont_off[g + 1]; q++) {  // ascending allcont order
           const int i = K.T.gc_cont[q];
           if (kap.nu < K.T.allcont_nu_edge[i]) break;
           double nnlevel, gc;
@@ -1676,11 +1678,21 @@ DEVFN T gload(const T *p) {
 struct MaMetaW {
   int4 w0, w1;
 };
+#ifdef ARTIS_MA_META3  // A/B: skip the unused rec_off word (no dead load destination for the allocator to reuse)
+typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+DEVFN MaMetaW ma_meta_load(const Ctx &K, int ul) {
+  glb_uint4 *mp = (glb_uint4 *)(K.T.ma_meta + ul);
+  const u32x3 a = *(const __attribute__((address_space(1))) u32x3 *)((const __attribute__((address_space(1))) uint32_t *)mp + 1);
+  const u32x4 b = mp[1];
+  return MaMetaW{make_int4(0, (int)a.x, (int)a.y, (int)a.z), make_int4((int)b.x, (int)b.y, (int)b.z, (int)b.w)};
+}
+#else
 DEVFN MaMetaW ma_meta_load(const Ctx &K, int ul) {
   glb_uint4 *mp = (glb_uint4 *)(K.T.ma_meta + ul);
   const u32x4 a = mp[0], b = mp[1];
   return MaMetaW{make_int4((int)a.x, (int)a.y, (int)a.z, (int)a.w), make_int4((int)b.x, (int)b.y, (int)b.z, (int)b.w)};
 }
+#endif
 
 // The cached walk as a resumable per-pass step (k_ma).  In SIMT every pass of a wave lasts as long as its slowest
 // lane; a search that probed record lines other than the staged one made one dependent trip to memory per probe,
