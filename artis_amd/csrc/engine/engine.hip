@@ -1167,8 +1167,8 @@ int run_wavefront(int64_t n, int nts, double t2) {
     }
 #endif
     if (st[41] + st[42] + st[43])
-      fprintf(stderr, "[artis_gpu] ma pass phases (cycles/pass): fetch %.0f, jump %.0f, rest %.0f\n",
-              (double)st[41] / st[4], (double)st[42] / st[4], (double)st[43] / st[4]);
+      fprintf(stderr, "[artis_gpu] ma pass phases (cycles/pass): fetch %.0f, jump %.0f, rest %.0f, load wait %.0f\n",
+              (double)st[41] / st[4], (double)st[42] / st[4], (double)st[43] / st[4], (double)st[44] / st[4]);
   }
   return tcollect();
 }

@@ -1511,9 +1511,11 @@ DEVFN int ma_apply_selection(const Ctx &K, const LocalCounters &L, MaLaneC &m, M
       m.rec_off = K.T.ma_meta[m.ul].rec_off;
       return MA_CONTINUE;
     case ARTIS_MA_ACTION_RADDEEXC:
+      // the line index is looked up by ma_finish (end.a = -1 - downtrans slot): a load here would hold the whole
+      // wave of k_ma for a round trip in most passes (some lane deactivates radiatively in ~2/3 of them)
       end.code = MA_END_BB;
       end.ion = 0;
-      end.a = K.T.downtrans_lineindex[doff + j];
+      end.a = -1 - (doff + j);
       end.b = ul;
       return MA_END_BB;
     case ARTIS_MA_ACTION_RADRECOMB:
@@ -1937,7 +1939,7 @@ DEVNI void ma_finish(Tx &x, Pkt &p, const MaEnd &e, unsigned jumps) {
   const int element = p.ma_element;
   p.interactions += (int)jumps;
   if (e.code == MA_END_BB) {
-    const int linelistindex = e.a, ul = e.b;
+    const int linelistindex = e.a >= 0 ? e.a : K.T.downtrans_lineindex[-1 - e.a], ul = e.b;
     const int ion = K.T.level_ui[ul] - K.T.elem_uniqueionoffset[element];
     if (K.R.record_linestat) atomicAdd(&K.E.ecounter[linelistindex], 1);
     const int lower = K.T.line_lower[linelistindex];

@@ -423,7 +423,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   unsigned long long jumps_sum = 0, trans_sum = 0;
   unsigned long long st_pass = 0, st_busy = 0, st_refill = 0, st_trefill = 0, st_tstep = 0;
 #ifdef ARTIS_STAMPS
-  unsigned long long ma_st[3] = {0, 0, 0};
+  unsigned long long ma_st[4] = {0, 0, 0, 0};
   __shared__ unsigned long long s_diag[48];
   for (int j = threadIdx.x; j < 48; j += blockDim.x) s_diag[j] = 0;
   __syncthreads();
@@ -533,6 +533,9 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
         h = (h ^ (h >> 27)) * 0x94d049bb133111ebull;
         z1 = (double)(h >> 11) * (1.0 / 9007199254740992.0);
         z2 = (double)((h * 0x9E3779B97F4A7C15ull) >> 11) * (1.0 / 9007199254740992.0);
+#elif defined(ARTIS_RNG_PAIRED)  // A/B: a jump's two draws from one Philox block (its counter aligned to even)
+        rng.n = (rng.n + 1u) & ~1u;
+        artis_rng_pair_aligned(&rng, &z1, &z2);
 #else
         artis_rng r2 = rng;
         z1 = artis_rng_uniform(&r2);
@@ -587,12 +590,20 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     }
     st_tstep += wave_clock() - ts0;
 #ifdef ARTIS_STAMPS
-    // k_ma phases (cycles per pass): fetch (metadata + record lines in LDS), jump, the rest of the pass
+    // k_ma phases (cycles per pass): fetch (metadata + record lines in LDS), jump, the rest of the pass; with
+    // ARTIS_STAMPS_TWAIT the pass first waits for every outstanding load (the transition-target loads) and that
+    // wait is its own phase
     {
       unsigned long long t2max = ts2;
       for (int off = 32; off > 0; off >>= 1) t2max = max(t2max, (unsigned long long)__shfl_xor((long long)t2max, off, 64));
       ma_st[0] += ts1 - ts0;
       ma_st[1] += t2max - ts1;
+#ifdef ARTIS_STAMPS_TWAIT
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      const unsigned long long tw = wave_clock();
+      ma_st[3] += tw - t2max;
+      t2max = tw;
+#endif
       ma_st[2] += wave_clock() - t2max;
     }
 #endif
@@ -600,6 +611,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
 #ifdef ARTIS_STAMPS
   if (lane_id() == 0)
     for (int i = 0; i < 3; i++) atomicAdd(&W.stats[41 + i], ma_st[i]);
+  if (lane_id() == 0) atomicAdd(&W.stats[44], ma_st[3]);
   __syncthreads();
   for (int j = threadIdx.x; j < 48; j += blockDim.x)
     if (s_diag[j]) atomicAdd(&g_ma_diag[j], s_diag[j]);

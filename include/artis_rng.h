@@ -61,6 +61,23 @@ ARTIS_HD artis_rng artis_rng_init(uint32_t seed, int32_t packet_number, int32_t 
   return s;
 }
 
+#ifdef ARTIS_RNG_PAIRED
+/* A/B variant: draw n is one half of Philox block n >> 1 */
+ARTIS_HD uint64_t artis_rng_next53(artis_rng *s) {
+  uint32_t c[4] = {s->n >> 1, 0x41525453u, s->nts, s->rank};
+  artis_philox4x32_10(c, s->key0, s->key1);
+  const uint64_t x = (s->n & 1u) ? (((uint64_t)c[3] << 32) | (uint64_t)c[2]) : (((uint64_t)c[1] << 32) | (uint64_t)c[0]);
+  s->n++;
+  return x >> 11;
+}
+/* draws n and n + 1 for an even n: one block */
+ARTIS_HD void artis_rng_pair_aligned(const artis_rng *s, double *z1, double *z2) {
+  uint32_t c[4] = {s->n >> 1, 0x41525453u, s->nts, s->rank};
+  artis_philox4x32_10(c, s->key0, s->key1);
+  *z1 = (double)((((uint64_t)c[1] << 32) | (uint64_t)c[0]) >> 11) * (1.0 / 9007199254740992.0);
+  *z2 = (double)((((uint64_t)c[3] << 32) | (uint64_t)c[2]) >> 11) * (1.0 / 9007199254740992.0);
+}
+#else
 /* 53-bit integer of draw number s->n, then advance */
 ARTIS_HD uint64_t artis_rng_next53(artis_rng *s) {
   uint32_t c[4] = {s->n, 0x41525453u, s->nts, s->rank};
@@ -69,6 +86,7 @@ ARTIS_HD uint64_t artis_rng_next53(artis_rng *s) {
   const uint64_t x = ((uint64_t)c[1] << 32) | (uint64_t)c[0];
   return x >> 11;
 }
+#endif
 
 /* gsl_rng_uniform: [0,1) */
 ARTIS_HD double artis_rng_uniform(artis_rng *s) { return (double)artis_rng_next53(s) * (1.0 / 9007199254740992.0); }
