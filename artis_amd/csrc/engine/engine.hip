@@ -1079,24 +1079,7 @@ int run_wavefront(int64_t n, int nts, double t2) {
     // k_ma<false>; split = the start of cell ma_rows's bin, which k_ma_scatter's cursor of cell ma_rows - 1 ends on
     const bool partial = G.K.C.have_macache && G.K.C.ma_rows < G.K.C.n_nonempty;
     const uint32_t *split = partial ? G.d_binoffs + (G.K.C.ma_rows - 1) : nullptr;
-    // ARTIS_GPU_MA_SLOTS=1: one walk per lane (k_ma<true>); default 2 (k_ma2: the target load of one walk overlaps
-    // the other walk's pass)
-    static const int ma_slots = [] {
-      const char *e = getenv("ARTIS_GPU_MA_SLOTS");
-      return (e && e[0] == '1') ? 1 : 2;
-    }();
-    // ARTIS_GPU_MA2_OCC=4: k_ma2 compiled for 4 waves per SIMD (register budget 128) instead of its natural 3
-    static const int ma2_occ = [] {
-      const char *e = getenv("ARTIS_GPU_MA2_OCC");
-      return (e && e[0] == '4') ? 4 : 1;
-    }();
-    if (G.K.C.have_macache && ma_slots == 2 && W.ma_tick) {
-      if (ma2_occ == 4)
-        k_ma2<4><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, split, partial ? 1 : 0, nts);
-      else
-        k_ma2<1><<<(unsigned)(G.wave_grid / 8 * std::min(ma_waves, 3)), WAVE_BLOCK, 0, G.stream>>>(
-            G.d_ctx, W, split, partial ? 1 : 0, nts);
-    } else if (G.K.C.have_macache) {
+    if (G.K.C.have_macache) {
       if (G.ma_occ == 8)
         k_ma<true, 8><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, split, partial ? 1 : 0);
       else
@@ -1181,6 +1164,9 @@ int run_wavefront(int64_t n, int nts, double t2) {
       for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++)
         fprintf(stderr, "[artis_gpu] ma action %d: searches %llu, pending %llu, probes %llu\n", a, dg[a], dg[16 + a],
                 dg[32 + a]);
+      if (dg[43])
+        fprintf(stderr, "[artis_gpu] ma step sections (cycles per wave step): action keys %.0f, search %.0f, rest %.0f\n",
+                (double)dg[40] / dg[43], (double)dg[41] / dg[43], (double)dg[42] / dg[43]);
     }
 #endif
     if (st[41] + st[42] + st[43])

@@ -1680,7 +1680,8 @@ DEVFN T gload(const T *p) {
 struct MaMetaW {
   int4 w0, w1;
 };
-#ifdef ARTIS_MA_META3  // A/B: skip the unused rec_off word (no dead load destination for the allocator to reuse)
+// (rec_off, w0.x, is not loaded: a dead load destination let the register allocator reuse it for the Philox
+// temporaries, which then waited for the record fetch; profiles/r03k_ab.txt: k_ma 1790 -> 1767 ms)
 typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
 DEVFN MaMetaW ma_meta_load(const Ctx &K, int ul) {
   glb_uint4 *mp = (glb_uint4 *)(K.T.ma_meta + ul);
@@ -1688,13 +1689,6 @@ DEVFN MaMetaW ma_meta_load(const Ctx &K, int ul) {
   const u32x4 b = mp[1];
   return MaMetaW{make_int4(0, (int)a.x, (int)a.y, (int)a.z), make_int4((int)b.x, (int)b.y, (int)b.z, (int)b.w)};
 }
-#else
-DEVFN MaMetaW ma_meta_load(const Ctx &K, int ul) {
-  glb_uint4 *mp = (glb_uint4 *)(K.T.ma_meta + ul);
-  const u32x4 a = mp[0], b = mp[1];
-  return MaMetaW{make_int4((int)a.x, (int)a.y, (int)a.z, (int)a.w), make_int4((int)b.x, (int)b.y, (int)b.z, (int)b.w)};
-}
-#endif
 
 // The cached walk as a resumable per-pass step (k_ma).  In SIMT every pass of a wave lasts as long as its slowest
 // lane; a search that probed record lines other than the staged one made one dependent trip to memory per probe,
@@ -1752,6 +1746,26 @@ struct KeysGlobal {
 template <class Keys>
 DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneR &m, MaEnd &end, int number,
                          const Keys &keys, const MaMetaW &meta, double z1, double z2) {
+#ifdef ARTIS_STAMPS_SUB  // diagnostic: cycles of the step's sections, added by the first active lane
+  struct SubStamp {
+    const LocalCounters &L;
+    unsigned long long t0, t1 = 0, t2 = 0;
+    DEVFN ~SubStamp() {
+      const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+      if (L.diag && (int)__lane_id() == __ffsll((long long)__ballot(1)) - 1) {
+        if (t1) atomicAdd(&L.diag[40], t1 - t0);
+        if (t2) atomicAdd(&L.diag[41], t2 - (t1 ? t1 : t0));
+        atomicAdd(&L.diag[42], t3 - (t2 ? t2 : (t1 ? t1 : t0)));
+        atomicAdd(&L.diag[43], 1ull);
+      }
+    }
+  } sub{L, __builtin_amdgcn_s_memtime()};
+#define SUB_STAMP(f) sub.f = __builtin_amdgcn_s_memtime()
+#else
+#define SUB_STAMP(f) \
+  do {               \
+  } while (0)
+#endif
   const uint16_t *rec = m.block + m.rec_off;
   const int doff = meta.w0.y, uoff = meta.w0.z, base_lower = meta.w0.w;
   const int nd = meta.w1.x, nu = meta.w1.y, nr = meta.w1.z, nt = meta.w1.w;
@@ -1816,6 +1830,7 @@ DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
     }
     m.hi = m.end;
   }
+  SUB_STAMP(t1);
   // binary search for the first entry above q2, resumed where it stopped.  The inner loop is the branch-light
   // common case (probe on the staged line, decided by the high half); it leaves for a probe off the line
   // (MA_PENDING) or a high half that needs its low half (rare).
@@ -1862,6 +1877,7 @@ DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
       lo = mid + 1;
   }
   m.ntrans += probes;
+  SUB_STAMP(t2);
   const int sel = m.sel;
   if (sel == ARTIS_MA_ACTION_INTERNALDOWNSAME || sel == ARTIS_MA_ACTION_INTERNALUPSAME) {
     const bool down = sel == ARTIS_MA_ACTION_INTERNALDOWNSAME;

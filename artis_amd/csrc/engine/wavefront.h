@@ -622,140 +622,6 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   block_counters_flush(K, s_ctr, s_work);
 }
 
-// k_ma2: the cached walk with TWO walks per lane (slots A and B), the wave alternating a pass of A with a pass of B.
-// A pass is: the record line (and the level's metadata) of each busy lane fetched into LDS, the search, and the load
-// of the selected transition's target level -- a chain of two dependent round trips to the memory system, of which
-// k_ma's single walk per lane exposes both.  Here the target load of one slot completes while the wave runs the
-// other slot's pass, so a pass waits only for its record fetch.  The walks, their draws and every result are
-// k_ma<true>'s; only the order in which a wave takes them differs.  One LDS line slot serves both walks (a pass
-// commits its lines after the previous pass's search has finished).
-struct MaSlot {
-  MaLaneR mc;
-  artis_rng rng;
-  int32_t idx;
-  bool have, pendR, pendK, pendX;
-};
-
-template <int MINW>
-__global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma2(const Ctx *__restrict__ ctxp, WaveState W,
-                                                          const uint32_t *split, int part, int nts) {
-  CTX_IN_LDS(ctxp)
-  __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
-  __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
-  __shared__ uint4 s_line[WAVE_BLOCK / 64][8 * 64];
-  __shared__ uint32_t s_xidx[WAVE_BLOCK / 64][64];
-  block_counters_init(s_ctr, s_work);
-  LocalCounters L;
-  L.ctr = &s_ctr[0];
-  L.work = &s_work[0];
-  lds_uint4 *line = (lds_uint4 *)&s_line[threadIdx.x >> 6][threadIdx.x & 63];
-  const uint32_t nq_all = W.ctr[2 * QM];
-  const uint32_t nq = (part == 1) ? min(*split, nq_all) : nq_all;
-  const int nr = W.ma_ranges;
-  const int nr_log2 = (nr == 8) ? 3 : 0;  // W.ma_ranges is 1 or 8
-  bool drained = false;
-  int cur = (int)(blockIdx.x % (unsigned)nr), tried = 0;
-  unsigned long long jumps_sum = 0, trans_sum = 0;
-  MaSlot A, B;
-  A.rng = B.rng = artis_rng_init(K.R.seed, 0, nts, K.R.rank);
-  A.idx = B.idx = -1;
-  A.have = B.have = A.pendR = A.pendK = A.pendX = B.pendR = B.pendK = B.pendX = false;
-  A.mc.sel = B.mc.sel = -1;
-  A.mc.pline = B.mc.pline = 0;
-
-  // idle lanes of slot S take tickets (k_ma_scatter) from the current range; finished walks are queued first
-  auto refill = [&](MaSlot &S) {
-    const bool idle = !S.have && !drained;
-    const unsigned long long imask = __ballot(idle);
-    if (__any(S.have) && __popcll(imask) < W.refill_ma) return;
-    wave_push(W, QR, S.pendR, S.idx);
-    wave_push(W, QK, S.pendK, S.idx);
-    wave_push(W, QX, S.pendX, S.idx);
-    S.pendR = S.pendK = S.pendX = false;
-    if (!imask) return;
-    const uint32_t lo = (uint32_t)(((uint64_t)nq * cur) >> nr_log2), hi = (uint32_t)(((uint64_t)nq * (cur + 1)) >> nr_log2);
-    const uint32_t slot = wave_reserve(&W.xhead[cur], idle);
-    const bool got = idle && lo + slot < hi;
-    if (got) {
-      const int4 t0 = W.ma_tick[2 * (int64_t)(lo + slot)], t1 = W.ma_tick[2 * (int64_t)(lo + slot) + 1];
-      S.idx = t0.x;
-      S.mc.ul = t0.y;
-      S.mc.rec_off = t0.z;
-      S.mc.k = t0.w;
-      S.rng.key1 = (uint32_t)t1.x;
-      S.rng.n = (uint32_t)t1.y;
-      S.mc.jumps = (unsigned)t1.z;
-      S.mc.block = K.C.ma_key + (int64_t)t1.w * K.C.ma_key_stride;
-      S.mc.ntrans = 0;
-      S.mc.sel = -1;
-      S.mc.pline = 0;
-      S.have = S.idx >= 0;
-    }
-    if (__any(idle && !got)) {  // this range is used up: move on (wave-uniform)
-      cur = (cur + 1) % nr;
-      if (++tried >= nr) drained = true;
-    }
-  };
-
-  // one pass of slot S: metadata + record lines (draws computed while they are in flight), search, target load
-  auto pass = [&](MaSlot &S) {
-    MaMetaW meta;
-    double z1 = 0., z2 = 0.;
-    if (S.have) meta = ma_meta_load(K, S.mc.ul);
-    const uint32_t myline =
-        S.have ? (uint32_t)(((uint64_t)(S.mc.block - K.C.ma_key) + (uint64_t)S.mc.rec_off) >> 6) + (uint32_t)S.mc.pline
-               : 0xffffffffu;
-    WaveLines wl;
-    wave_fetch_issue(K.C.ma_key, myline, wl, (lds_u32 *)&s_xidx[threadIdx.x >> 6][0]);
-    if (S.have && S.mc.sel < 0) {
-      artis_rng r2 = S.rng;
-      z1 = artis_rng_uniform(&r2);
-      z2 = artis_rng_uniform(&r2);
-    }
-    wave_fetch_commit(wl, line - (threadIdx.x & 63));
-    if (S.have) {
-      MaEnd e;
-      const int r = ma_step_cached(K, L, S.rng, S.mc, e, (int)S.rng.key1, KeysLds{line, S.mc.pline}, meta, z1, z2);
-      const unsigned jumps = S.mc.jumps;
-      if (r == MA_DEFER) {  // park the walk before this jump; k_ma_exact makes it with the exact sums
-        W.pend[S.idx] = make_int4(MA_RESUME, S.mc.ul, 0, 0);
-        W.pend_jumps[S.idx] = jumps;
-        W.rng_n[S.idx] = S.mc.n0;
-        trans_sum += S.mc.ntrans;
-        S.pendX = true;
-        S.have = false;
-      } else if (r != MA_PENDING && (r != MA_CONTINUE || jumps >= MA_MAX_JUMPS)) {
-        if (r == MA_CONTINUE) fail(K, ERR_STUCK, (int)S.rng.key1, 2);
-        if (r > 0) {
-          W.pend[S.idx] = make_int4(e.code, e.ion, e.a, e.b);
-          W.pend_jumps[S.idx] = jumps;
-          W.rng_n[S.idx] = S.rng.n;
-          S.pendR = (r == MA_END_BB || r == MA_END_FB);
-          S.pendK = (r == MA_END_COLDEEXC || r == MA_END_COLRECOMB);
-        }
-        jumps_sum += jumps;
-        trans_sum += S.mc.ntrans;
-        S.have = false;
-      }
-    }
-  };
-
-  while (true) {
-    refill(A);
-    if (__any(A.have)) pass(A);
-    refill(B);
-    if (__any(B.have)) pass(B);
-    if (drained && !__any(A.have) && !__any(B.have)) {
-      refill(A);  // (queues the walks that ended in the last passes)
-      refill(B);
-      break;
-    }
-  }
-  if (jumps_sum) atomicAdd(&s_work[WK_MA_JUMPS], jumps_sum);
-  if (trans_sum) atomicAdd(&s_work[WK_MA_TRANS], trans_sum);
-  block_counters_flush(K, s_ctr, s_work);
-}
-
 // macro-atom jumps whose key comparisons were undecided (QX): one jump each with the reference's exact sums, then
 // the walk is parked again for k_ma (-> M queue) or its deactivation deferred like k_ma's (-> R / K queue).
 // One wave per jump: the lanes evaluate the level's individual rates (ma_rate_at, the expressions of
