@@ -4,7 +4,7 @@
 # the plain bench line with the CPU baseline.
 cd /root/repo
 export TMPDIR=/tmp
-O=gpurun_out/${RUN_TAG:-r3j}
+O=gpurun_out/${RUN_TAG:-r3m}
 mkdir -p $O/pmc $O/vpmc
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 &&
 tail -3 $O/gpu_tests.log &&
