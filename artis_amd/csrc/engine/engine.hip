@@ -852,7 +852,20 @@ int vpkt_flush() {
     const int v = e ? atoi(e) : VPKT_OCC_DEFAULT;
     return (v == 2 || v == 3) ? v : 1;
   }();
-  if (occ == 3)
+  // every non-empty cell with a coefficient row: the kernel without the gather walk (whose PF-line prefetch arrays
+  // would otherwise set the register allocation of the whole kernel); ARTIS_VPKT_LCONLY=0 forces the general one
+  static const bool lc_ok = [] {
+    const char *e = getenv("ARTIS_VPKT_LCONLY");
+    return !(e && e[0] == '0');
+  }();
+  const bool lc_only = lc_ok && G.K.C.linecoef && G.K.C.linecoef_rows >= G.K.C.n_nonempty;
+  if (lc_only && occ == 3)
+    k_vpkt<0, 3><<<(unsigned)G.wave_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, G.W.refill_min);
+  else if (lc_only && occ == 2)
+    k_vpkt<0, 2><<<(unsigned)G.wave_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, G.W.refill_min);
+  else if (lc_only)
+    k_vpkt<0, 1><<<(unsigned)G.wave_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, G.W.refill_min);
+  else if (occ == 3)
     k_vpkt<VPKT_PF, 3><<<(unsigned)G.wave_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, G.W.refill_min);
   else if (occ == 2)
     k_vpkt<VPKT_PF, 2><<<(unsigned)G.wave_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, G.W.refill_min);

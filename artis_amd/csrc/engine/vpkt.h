@@ -311,6 +311,10 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
     }
     return vpkt_segment_end(x, v, sdist, snext);
   }
+  if constexpr (PF == 0) {  // launched only when every non-empty cell has a coefficient row
+    x.err(ERR_UNSUPPORTED_TYPE, -1, 7);
+    return VSEG_KILLED;
+  } else {
   LineTau r[PF];
   double pl[PF], pu[PF];
   int z[PF] = {};
@@ -371,6 +375,7 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
     if (!vpkt_alive(V, v.tau)) return VSEG_KILLED;
   }
   return vpkt_segment_end(x, v, sdist, snext);
+  }
 }
 
 // all (spawn, observer) work items of the spawn buffer; spawn_ctr[1] is the fetch head
