@@ -185,19 +185,23 @@ __global__ void k_ntcells(Ctx K) {
   K.C.nt_total[k] = ratesum;
 }
 
-// kpkt.cc:167-308 calculate_kpkt_rates_ion, one workitem per (cell, ion), cumulative from oldcoolingsum
+// kpkt.cc:167-308 calculate_kpkt_rates_ion, one workitem per (cell, ion), cumulative from oldcoolingsum.
+// Workitems are ion-major (consecutive lanes = the same ion in consecutive cells), as k_marates: the lanes of a wave
+// walk the same level and transition lists (uniform loads, no divergence) and read the populations from the
+// level-major copy popsT (coalesced).
 __global__ void k_cooling(Ctx K) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int ni = K.T.nions_total;
-  if (idx >= (int64_t)K.C.n_nonempty * ni) return;
-  const int k = (int)(idx / ni);
-  const int ui = (int)(idx % ni);
+  const int64_t nne_cells = K.C.n_nonempty;
+  if (idx >= nne_cells * ni) return;
+  const int ui = (int)(idx / nne_cells);
+  const int k = (int)(idx % nne_cells);
   const int mgi = K.C.ne_mgi[k];
   const int e = K.T.ion_element[ui];
   const int i = ui - K.T.elem_uniqueionoffset[e];
   const float nne = K.C.nne[mgi];
   const float T_e = K.C.Te[mgi];
-  const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
+  const double *popsT = K.C.popsT + k;  // popsT[u * nne_cells]: level u of this lane's cell
   double *cc = K.C.cooling + (int64_t)k * K.T.ncoolingterms;
   double oldcoolingsum = 0.;
   for (int u = 0; u < ui; u++) oldcoolingsum += K.C.cooling_contrib_ion[(int64_t)mgi * ni + u];
@@ -216,7 +220,7 @@ __global__ void k_cooling(Ctx K) {
   for (int level = 0; level < nlevels; level++) {
     const int ul = K.T.ion_uniqueleveloffset[ui] + level;
     const double epsilon_current = K.T.level_epsilon[ul];
-    const double nnlevel = pops[ul];
+    const double nnlevel = popsT[(int64_t)ul * nne_cells];
     const double statweight = K.T.level_stat_weight[ul];
     const int nuptrans = K.T.level_nuptrans[ul];
     if (nuptrans > 0) {
@@ -3362,11 +3366,11 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
     if (G.K.R.no_lut_photoion && G.qag_waves > 0)
       k_corrphot_integral<<<(unsigned)G.qag_waves, 64, 0, G.stream>>>(G.K, G.d_target_ul, G.d_target_t, G.qag);
     if (G.K.R.nt_on) k_ntcells<<<(n_ne + B - 1) / B, B, 0, G.stream>>>(G.K);
+    k_transpose<<<dim3((unsigned)((nl + 63) / 64), (unsigned)((n_ne + 63) / 64)), 256, 0, G.stream>>>(
+        G.K.C.pops, G.K.C.popsT, n_ne, nl);
     const int64_t nci = (int64_t)n_ne * ni;
     k_cooling<<<(unsigned)((nci + 63) / 64), 64, 0, G.stream>>>(G.K);
     const int64_t ntg = G.K.T.ntargets_total;
-    k_transpose<<<dim3((unsigned)((nl + 63) / 64), (unsigned)((n_ne + 63) / 64)), 256, 0, G.stream>>>(
-        G.K.C.pops, G.K.C.popsT, n_ne, nl);
     if (ntg > 0)
       k_transpose<<<dim3((unsigned)((ntg + 63) / 64), (unsigned)((n_ne + 63) / 64)), 256, 0, G.stream>>>(
           G.K.C.corrphot, G.K.C.corrphotT, n_ne, ntg);

@@ -13,5 +13,5 @@ for v in "$@"; do
     --no-cpu-baseline --no-update-grid --no-extra $BENCH_ARGS > gpurun_out/ab_$tag.json 2> gpurun_out/ab_$tag.err ||
     { echo "FAIL $v"; tail -5 gpurun_out/ab_$tag.err; exit 1; }
   grep "^\[artis_gpu\]" gpurun_out/ab_$tag.err | grep -v "^\[artis_gpu\] ma action [1-3578]" | sed "s/^/  $tag /"
-  python3 -c "import json,sys; d=json.loads(open('gpurun_out/ab_'+sys.argv[1]+'.json').read().strip().splitlines()[-1]); print(sys.argv[2], 'value', round(d['value']), 'ms', round(d['ms_per_step']), {k: round(x) for k, x in d['kernel_ms'].items()}, 'frac', round(d['roofline']['frac'], 4))" "$tag" "$v"
+  python3 -c "import json,sys; d=json.loads(open('gpurun_out/ab_'+sys.argv[1]+'.json').read().strip().splitlines()[-1]); print(sys.argv[2], 'value', round(d['value']), 'ms', round(d['ms_per_step']), 'precompute', round(d.get('precompute_ms', 0)), {k: round(x) for k, x in d['kernel_ms'].items()}, 'frac', round(d['roofline']['frac'], 4))" "$tag" "$v"
 done
