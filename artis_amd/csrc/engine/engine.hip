@@ -1109,9 +1109,7 @@ int run_wavefront(int64_t n, int nts, double t2) {
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QM, 0, 2 * sizeof(uint32_t), G.stream));
     if (G.K.C.have_macache) {  // jumps the 32-bit keys could not decide (rare), exact; walks go back to M
       TSTART(3);
-      // (grid-stride over a queue of a few jumps per round: 128 one-wave blocks, not one per SIMD, keep the launch of
-      // a near-empty queue cheap -- each block first copies the context into LDS)
-      k_ma_exact<<<std::min(grid / 4, 128u), 64, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+      k_ma_exact<<<grid / 4, 64, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
       TEND(3);
       HIPCHK(hipMemsetAsync(W.ctr + 2 * QX, 0, 2 * sizeof(uint32_t), G.stream));
     }
