@@ -344,6 +344,7 @@ DEVFN void rlc_emiss_gamma(const Ctx &K, const Pkt &p, double dist) {
 DEVFN int get_nul(const Ctx &K, double freq) {
   const double *f = K.T.g_freq_sorted;
   const int n = K.T.g_nsorted;
+  if (n < 1) return GAMMA_RED_OF_LIST;  // (no gamma-ray lines: no gamma packets either)
   if (freq > f[n - 1]) return n - 1;
   if (freq < f[0]) return GAMMA_RED_OF_LIST;
   int too_high = n - 1, too_low = 0;
