@@ -4,7 +4,7 @@
 # box's profiles/ so that the closing default bench line carries roofline.traffic
 cd /root/repo
 export TMPDIR=/tmp
-T=${RUN_TAG:-r3t}
+T=${RUN_TAG:-r3w}
 O=gpurun_out/$T
 mkdir -p $O/pmc
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 &&

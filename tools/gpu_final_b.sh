@@ -3,7 +3,7 @@
 # WRITE_SIZE passes -> pmc summary (copied into this box's profiles/), then its bench line under rocprofv3 statistics
 cd /root/repo
 export TMPDIR=/tmp
-T=${RUN_TAG:-r3t}
+T=${RUN_TAG:-r3w}
 O=gpurun_out/$T
 mkdir -p $O/vpmc
 V="python3 bench.py --packets 10000000 --nts 30 --vpkt 4 --steps 1 --warmup 0 --no-cpu-baseline --no-update-grid --no-extra" &&
