@@ -135,3 +135,21 @@ def test_vpkt_full_spawn_buffer_drains_and_matches_oracle(monkeypatch):
     _compare_vpkt(vg, vo)
     assert drains > 0 and spawns > 2 * 2048, (drains, spawns)
     assert traces == vo.counters()["nvpkt"]
+
+
+@pytest.mark.parametrize("env", [("ARTIS_GPU_NO_LINECOEF", "1"), ("ARTIS_VPKT_LCONLY", "0")])
+def test_vpkt_general_kernel_matches_oracle(monkeypatch, env):
+    """k_vpkt's general instantiation (population-gather line walk: cells without a coefficient row, or forced with
+    ARTIS_VPKT_LCONLY=0) against the oracle; the default table-only kernel runs in the other tests."""
+    monkeypatch.setenv(*env)
+    m = Model(**VCFG)
+    m.set_timestep(NTS)
+    pk = m.init_rpackets(NTS, 2000, seed=45)
+    vc = ffi.VpktConfig(nz_obs=(0.3, -0.7), phi_obs_deg=(10.0, 200.0), exclude=(0.0, -1.0, 26.0))
+    pg, eg, vg, _ = _run(m, NTS, pk, vc)
+    po = pk.copy()
+    eo, vo, _ = oracle_lib.update_packets_vpkt(m, NTS, po, vc, nthreads=16)
+    parity.assert_packets_match(pg, po)
+    parity.assert_estimators_match(eg, eo)
+    _compare_vpkt(vg, vo)
+    assert vo.counters()["nvpkt"] > 500
