@@ -1329,6 +1329,60 @@ void rebuild_gamma_spectra(Model &m) {
 
 struct artis_model : Model {};
 
+namespace {
+
+// Every floating-point table the engine and the oracle read must be finite: a NaN here would propagate into both
+// sides identically and hide (or fake) a parity mismatch.  Names the first offending array on stderr.
+template <class V>
+bool all_finite(const V &v, const char *name) {
+  for (size_t k = 0; k < v.size(); k++)
+    if (!std::isfinite((double)v[k])) {
+      std::fprintf(stderr, "artis_model: %s[%zu] = %g is not finite\n", name, k, (double)v[k]);
+      return false;
+    }
+  return true;
+}
+
+// the configuration's physical scalars: finite, and positive where the profile divides by or takes logs of them
+bool config_is_sane(const artis_synth_config &c) {
+  const double pos[] = {c.tmin_days, c.tmax_days, c.vmax, c.mass_msun, c.v_e, c.T0};
+  const char *names[] = {"tmin_days", "tmax_days", "vmax", "mass_msun", "v_e", "T0"};
+  for (int k = 0; k < 6; k++)
+    if (!(std::isfinite(pos[k]) && pos[k] > 0)) {
+      std::fprintf(stderr, "artis_model: config %s = %g must be finite and > 0\n", names[k], pos[k]);
+      return false;
+    }
+  const double nonneg[] = {c.ionpot_scale, c.thick_tau, c.kpktdiffusion_timescale, c.tj_scale, c.minpop, c.nu_min_r,
+                           c.nu_max_r};
+  for (double v : nonneg)
+    if (!(std::isfinite(v) && v >= 0)) {
+      std::fprintf(stderr, "artis_model: a config scalar (%g) is negative or not finite\n", v);
+      return false;
+    }
+  return c.tmax_days > c.tmin_days && c.ngrid_1d > 0 && c.ntstep > 0;
+}
+
+bool model_is_finite(const Model &m) {
+  // nlte_pops use -1 (no solution yet) and bin W < 0 (no fit): finite sentinels, checked like the rest
+  return all_finite(m.level_epsilon, "level_epsilon") && all_finite(m.level_stat_weight, "level_stat_weight") &&
+         all_finite(m.phixs_xs, "phixs_xs") && all_finite(m.phixstarget_probability, "phixstarget_probability") &&
+         all_finite(m.line_nu, "line_nu") && all_finite(m.line_A, "line_A") && all_finite(m.line_f, "line_f") &&
+         all_finite(m.line_coll, "line_coll") && all_finite(m.spontrecombcoeff, "spontrecombcoeff") &&
+         all_finite(m.corrphotoioncoeff, "corrphotoioncoeff") && all_finite(m.bfcooling_coeff, "bfcooling_coeff") &&
+         all_finite(m.Te, "Te") && all_finite(m.TR, "TR") && all_finite(m.TJ, "TJ") && all_finite(m.W, "W") &&
+         all_finite(m.nne, "nne") && all_finite(m.nnetot, "nnetot") && all_finite(m.rho, "rho") &&
+         all_finite(m.kappagrey, "kappagrey") && all_finite(m.elem_abundance, "elem_abundance") &&
+         all_finite(m.groundlevelpop, "groundlevelpop") && all_finite(m.partfunct, "partfunct") &&
+         all_finite(m.totalcooling, "totalcooling") && all_finite(m.cooling_contrib_ion, "cooling_contrib_ion") &&
+         all_finite(m.corrphotoionrenorm, "corrphotoionrenorm") && all_finite(m.nlte_pops, "nlte_pops") &&
+         all_finite(m.rf_TR, "radfield_bin_TR") && all_finite(m.rf_W, "radfield_bin_W") &&
+         all_finite(m.bfrate_est, "bfrate_estimator") && all_finite(m.nt_dep, "nt_deposition_rate_density") &&
+         all_finite(m.nt_Y, "nt_ionization_ratecoeff") && all_finite(m.nt_prob, "nt_prob_num_auger") &&
+         all_finite(m.nt_ionen, "nt_ionenfrac_num_auger");
+}
+
+}  // namespace
+
 extern "C" {
 
 void artis_synth_default_config(artis_synth_config *cfg) {
@@ -1400,10 +1454,15 @@ artis_model *artis_model_from_files(const artis_synth_config *cfg, const char *i
   finish_geometry(*m);
   compute_cellstate(*m, 0);
   rebuild_gamma_spectra(*m);
+  if (!model_is_finite(*m)) {
+    delete m;
+    return nullptr;
+  }
   return m;
 }
 
 artis_model *artis_model_synth(const artis_synth_config *cfg) {
+  if (!config_is_sane(*cfg)) return nullptr;
   artis_model *m = new artis_model();
   m->cfg = *cfg;
   std::mt19937_64 rng(cfg->seed);
@@ -1412,6 +1471,10 @@ artis_model *artis_model_synth(const artis_synth_config *cfg) {
   build_grid(*m);
   compute_cellstate(*m, 0);
   rebuild_gamma_spectra(*m);
+  if (!model_is_finite(*m)) {
+    delete m;
+    return nullptr;
+  }
   return m;
 }
 
@@ -1573,7 +1636,7 @@ int artis_model_init_pellets(const artis_model *m, int npkts, uint64_t seed, dou
 int artis_model_set_timestep(artis_model *m, int nts) {
   if (nts < 0 || nts >= m->cfg.ntstep) return ARTIS_ERR_BAD_ARGUMENT;
   compute_cellstate(*m, nts);
-  return 0;
+  return model_is_finite(*m) ? 0 : ARTIS_ERR_BAD_ARGUMENT;
 }
 
 int artis_model_init_rpackets(const artis_model *m, int nts, int npkts, uint64_t seed, double etot,

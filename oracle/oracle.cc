@@ -684,8 +684,9 @@ int gsl_qag61(const F &f, double a, double b, double epsabs, double epsrel, size
 constexpr size_t kGslWsSize = 16384;  // GSLWSIZE (artisoptions_nltenebular.h:75)
 
 // ratecoeff.cc:1159-1245 calculate_corrphotoioncoeff_integral (NO_LUT_PHOTOION)
-double calculate_corrphotoioncoeff_integral(const Ctx &c, const ThreadCache &tc, int e, int i, int l, int t, int mgi) {
-  constexpr double epsrel = 1e-3;
+// epsrel: the reference's 1e-3 (ratecoeff.cc:1199); the tests also call it at a tight tolerance
+double calculate_corrphotoioncoeff_integral(const Ctx &c, const ThreadCache &tc, int e, int i, int l, int t, int mgi,
+                                            double epsrel = 1e-3) {
   constexpr double epsabs = 0.;
   const double E_threshold = get_phixs_threshold(c, e, i, l, t);
   const double nu_threshold = ARTIS_ONEOVERH * E_threshold;
@@ -3493,10 +3494,16 @@ double oracle_qag61_test(int fn, double a, double b, double epsrel, int *status,
 }
 
 // get_corrphotoioncoeff of model cell mgi, unique level ul, target t at timestep nts (the oracle's
-// NO_LUT_PHOTOION integral or estimator, as the macro-atom sees it); brute != 0: the same integrand summed by
-// composite 8-point Gauss-Legendre over 4096 pieces per radiation-field bin crossing -- a quadrature check
+// NO_LUT_PHOTOION integral or estimator, as the macro-atom sees it); brute == 2: the integral by the same qag
+// restatement at epsrel 1e-10; brute == 1: the same integrand summed by
+// composite 8-point Gauss-Legendre over 4096 pieces per radiation-field bin crossing -- a quadrature check.
+// Returns NaN for a (level, target) that has no photoionisation target: get_corrphotoioncoeff is only reached for
+// t < get_nphixstargets (macroatom.cc:117-130), and a non-ionising level has no cross-section table
+// (level_phixstable = -1).  The caller raises on NaN; a non-finite quadrature result is returned as NaN too.
 double oracle_corrphotoioncoeff(const artis_atomic_tables *at, const artis_geometry *geom, const artis_cell_state *cs,
                                 const artis_run_params *rp, int nts, int mgi, int ul, int t, int brute) {
+  const double bad = std::numeric_limits<double>::quiet_NaN();
+  if (ul < 0 || ul >= at->nlevels_total || mgi < 0 || t < 0) return bad;
   Ctx c;
   c.at = at;
   c.g = geom;
@@ -3526,7 +3533,15 @@ double oracle_corrphotoioncoeff(const artis_atomic_tables *at, const artis_geome
   int i = 0;
   while (i + 1 < at->elem_nions[e] && at->ion_uniqueleveloffset[at->elem_uniqueionoffset[e] + i + 1] <= ul) i++;
   const int l = ul - at->ion_uniqueleveloffset[at->elem_uniqueionoffset[e] + i];
-  if (!brute) return get_corrphotoioncoeff(c, tc, e, i, l, t, mgi);
+  if (t >= get_nphixstargets(c, e, i, l) || at->level_phixstable[ul] < 0) return bad;
+  if (!brute) {
+    const double r = get_corrphotoioncoeff(c, tc, e, i, l, t, mgi);
+    return std::isfinite(r) ? r : bad;
+  }
+  if (brute == 2) {  // the same qag restatement at epsrel 1e-10: the integrand + bisection machinery to accuracy
+    const double r = calculate_corrphotoioncoeff_integral(c, tc, e, i, l, t, mgi, 1e-10);
+    return std::isfinite(r) ? r : bad;
+  }
   // brute-force quadrature of the same integrand
   const double nu_threshold = ARTIS_ONEOVERH * get_phixs_threshold(c, e, i, l, t);
   const double nu_max_phixs = nu_threshold * at->last_phixs_nuovernuedge;
@@ -3568,7 +3583,8 @@ double oracle_corrphotoioncoeff(const artis_atomic_tables *at, const artis_geome
       for (int q = 0; q < 8; q++) sum += gw[q] * 0.5 * h * f(mid + 0.5 * h * gx[q]);
     }
   }
-  return sum * ARTIS_FOURPI * get_phixsprobability(c, e, i, l, t);
+  const double r = sum * ARTIS_FOURPI * get_phixsprobability(c, e, i, l, t);
+  return std::isfinite(r) ? r : bad;
 }
 
 // ---- unit hooks for tests/ ---------------------------------------------------------------------------------

@@ -98,10 +98,36 @@ def qag61_test(fn, a, b, epsrel):
 
 
 def corrphotoioncoeff(model, nts, mgi, ul, t, brute=False, params=None):
-    """get_corrphotoioncoeff as the oracle's macro-atom sees it (brute: dense-quadrature check of the integral)."""
+    """get_corrphotoioncoeff as the oracle's macro-atom sees it.  brute=1: dense Gauss-Legendre quadrature of the
+    same integrand; brute=2: the same qag restatement at epsrel 1e-10 (the reference runs it at 1e-3)."""
     p = params if params is not None else model.params
-    return lib().oracle_corrphotoioncoeff(model.atomic, model.geometry, model.cellstate, C.byref(p),
-                                          int(nts), int(mgi), int(ul), int(t), int(brute))
+    r = lib().oracle_corrphotoioncoeff(model.atomic, model.geometry, model.cellstate, C.byref(p),
+                                       int(nts), int(mgi), int(ul), int(t), int(brute))
+    if not np.isfinite(r):
+        raise ValueError(f"oracle_corrphotoioncoeff(mgi={mgi}, level={ul}, target={t}): no photoionisation target "
+                         f"or a non-finite integral")
+    return r
+
+
+def ionising_levels(model):
+    """Unique indices of every level with photoionisation targets (level < ionisinglevels of a non-top ion)."""
+    class Hdr(C.Structure):  # leading fields of artis_atomic_tables (include/artis_gpu.h)
+        _fields_ = ffi.AtomicHeader._fields_ + [("ion_ionstage", C.c_void_p), ("ion_nlevels", C.c_void_p),
+                                                ("ion_uniqueleveloffset", C.c_void_p),
+                                                ("ion_ionisinglevels", C.c_void_p)]
+
+    hdr = Hdr.from_address(model.atomic)
+    n = lambda p, k: np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int32)), (k,))  # noqa: E731
+    nions = n(hdr.elem_nions, model.nelements)
+    ionoff = n(hdr.elem_uniqueionoffset, model.nelements)
+    lvoff = n(hdr.ion_uniqueleveloffset, model.nions_total)
+    nion = n(hdr.ion_ionisinglevels, model.nions_total)
+    out = []
+    for e in range(model.nelements):
+        for i in range(nions[e] - 1):
+            ui = ionoff[e] + i
+            out += list(range(lvoff[ui], lvoff[ui] + nion[ui]))
+    return out
 
 
 def spectra(model, packets, nnubins=1000, nprocs=1, abin=-1, syn_dir=(0., 0., 1.), emission_res=True, stokes=False):

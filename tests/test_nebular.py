@@ -42,22 +42,53 @@ def neb():
 @pytest.mark.parametrize("nts", [5, 14])
 def test_corrphot_integral_matches_dense_quadrature(neb, nts):
     """calculate_corrphotoioncoeff_integral (ratecoeff.cc:1184-1245) against 8-point Gauss-Legendre on 64 pieces
-    between every phixs node / radiation-field bin edge: within the reference's epsrel 1e-3."""
+    between every phixs node / radiation-field bin edge.
+
+    * the qag restatement run to epsrel 1e-10 equals the dense quadrature to 1e-7: integrand and bisection are right;
+    * at the reference's epsrel 1e-3 qag accepts its own error estimate, which is heuristic (|K61 - G30| rescaled,
+      GSL qk.c): on the binned J_nu (a jump at every radiation-field bin edge, timestep >= FIRST_NLTE_RADFIELD_TIMESTEP)
+      it can claim 1e-3 while the true error is several times that (5.7e-3 measured for one level).  The reference
+      returns that value, so the oracle and the engine do too; the test bounds it at 1e-2.
+    """
     neb.set_timestep(nts)
     p = copy.copy(neb.params)
     p.detailed_bf_usefromtimestep = 99  # the integral, not the estimator
     rows = []
-    for ul in range(0, 60, 3):  # ionising levels of the first ions (n_ionising = 10 of 30 per ion)
+    # every third ionising level; a level without a photoionisation target has no cross-section table and the
+    # oracle rejects it (test below)
+    for ul in oracle_lib.ionising_levels(neb)[::3]:
         for mgi in (0, 5):
             a = oracle_lib.corrphotoioncoeff(neb, nts, mgi, ul, 0, params=p)
-            b = oracle_lib.corrphotoioncoeff(neb, nts, mgi, ul, 0, brute=True, params=p)
-            rows.append((ul, mgi, a, b))
+            b = oracle_lib.corrphotoioncoeff(neb, nts, mgi, ul, 0, brute=1, params=p)
+            tight = oracle_lib.corrphotoioncoeff(neb, nts, mgi, ul, 0, brute=2, params=p)
+            rows.append((ul, mgi, a, b, tight))
     # Integrals 30+ decades below the largest (deep Wien tail, ~1e-66) are where GSL's qag itself may stop on its
     # roundoff test (status 18, accepted by ratecoeff.cc:1230); they are held to the scale of the set instead.
     scale = max(abs(r[3]) for r in rows)
-    for ul, mgi, a, b in rows:
-        assert abs(a - b) <= 1e-3 * abs(b) + 1e-30 * scale, (ul, mgi, a, b)
+    for ul, mgi, a, b, tight in rows:
+        assert abs(tight - b) <= 1e-7 * abs(b) + 1e-30 * scale, (ul, mgi, tight, b)
+        assert abs(a - b) <= 1e-2 * abs(b) + 1e-30 * scale, (ul, mgi, a, b)
     assert sum(r[3] > 0 for r in rows) > 5
+    # most integrands are smooth enough for qag's estimate to hold
+    assert np.mean([abs(a - b) <= 1e-3 * abs(b) + 1e-30 * scale for _, _, a, b, _ in rows]) >= 0.9
+
+
+def test_corrphot_rejects_levels_without_targets(neb):
+    """A non-ionising level (level_phixstable = -1) or a target past get_nphixstargets has no integral: the oracle
+    hook refuses it instead of reading before the cross-section table (the round-3 intermittent NaN)."""
+    ion = set(oracle_lib.ionising_levels(neb))
+    non = next(ul for ul in range(neb.nlevels_total) if ul not in ion)
+    for brute in (False, True):
+        with pytest.raises(ValueError):
+            oracle_lib.corrphotoioncoeff(neb, 5, 0, non, 0, brute=brute)
+        with pytest.raises(ValueError):
+            oracle_lib.corrphotoioncoeff(neb, 5, 0, min(ion), 99, brute=brute)
+
+
+def test_model_rejects_nonfinite_inputs():
+    """The model builder refuses non-finite tables (a NaN would reach the engine and the oracle alike)."""
+    with pytest.raises(RuntimeError):
+        Model(ngrid_1d=4, nlevels_per_ion=20, n_ionising=8, max_lines=800, ntstep=20, T0=float("nan"))
 
 
 def test_corrphot_uses_bfrate_estimator_from_usefromtimestep(neb):
@@ -67,7 +98,7 @@ def test_corrphot_uses_bfrate_estimator_from_usefromtimestep(neb):
     p = copy.copy(neb.params)
     p.detailed_bf_usefromtimestep = 99
     differs = 0
-    for ul in range(0, 60, 3):
+    for ul in oracle_lib.ionising_levels(neb)[:40:2]:
         a = oracle_lib.corrphotoioncoeff(neb, 14, 5, ul, 0)  # model cell 5: inside the ejecta
         b = oracle_lib.corrphotoioncoeff(neb, 14, 5, ul, 0, params=p)
         differs += a != b
