@@ -2630,8 +2630,34 @@ void artis_gpu_finalize(void) {
   G = Engine();
 }
 
+// Option values the engine does not propagate are refused at init instead of being accepted and ignored: the
+// reference's own input checks (input.cc:1976-1982 do_rlc_est in 0..3, grid.cc:627-677 opacity_case 0..5) plus
+// every switch being 0 / 1.  Runs before any HIP call.
+static const char *unsupported_run_param(const artis_run_params *rp) {
+  auto flag = [](int32_t v) { return v == 0 || v == 1; };
+  if (rp->do_rlc_est < 0 || rp->do_rlc_est > 3) return "do_rlc_est must be 0..3 (input.txt line 9 is 0..4)";
+  if (rp->opacity_case < 0 || rp->opacity_case > 5) return "opacity_case must be 0..5";
+  if (!flag(rp->do_r_lc) || !flag(rp->pol_dipole) || !flag(rp->relativistic_doppler) || !flag(rp->record_linestat) ||
+      !flag(rp->instant_particle_deposition) || !flag(rp->nt_solve_spencerfano) || !flag(rp->nlte_pops_on) ||
+      !flag(rp->multibin_radfield) || !flag(rp->detailed_bf_estimators) || !flag(rp->no_lut_photoion) ||
+      !flag(rp->no_lut_bfheating) || !flag(rp->nt_on) || !flag(rp->comp_est))
+    return "a boolean run parameter (do_r_lc, pol_dipole, relativistic_doppler, record_linestat, "
+           "instant_particle_deposition, nt_solve_spencerfano, nlte_pops_on, multibin_radfield, "
+           "detailed_bf_estimators, no_lut_photoion, no_lut_bfheating, nt_on, comp_est) is not 0 or 1";
+  if (rp->n_kpktdiffusion_timesteps < 0 || !(rp->kpktdiffusion_timescale >= 0.f))
+    return "kpkt diffusion parameters must be >= 0";
+  if (!(rp->max_path_step > 0.)) return "max_path_step must be > 0";
+  if (!std::isfinite(rp->gamma_grey) || !(rp->minpop >= 0.) || rp->rank < 0)
+    return "gamma_grey must be finite, minpop >= 0, rank >= 0";
+  return nullptr;
+}
+
 int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometry *g, const artis_run_params *rp) {
   if (!a || !g || !rp) return ARTIS_ERR_BAD_ARGUMENT;
+  if (const char *why = unsupported_run_param(rp)) {
+    G.last_error = why;
+    return ARTIS_ERR_UNSUPPORTED;
+  }
   if (G.initialised) artis_gpu_finalize();
   if (g->grid_type != ARTIS_GRID_UNIFORM) {
     G.last_error = "only GRID_UNIFORM is propagated by this build";

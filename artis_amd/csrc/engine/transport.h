@@ -1061,6 +1061,21 @@ DEVNI void rpkt_event_thickcell(Tx &x, Pkt &p) {
   p.em_time = (int)p.prop_time;
 }
 
+// grey_emissivities.cc:79-122 rlc_emiss_rpkt (do_rlc_est 1 or 2, rpkt.cc:739-741, 769-771, 791-793): the grey
+// destruction rate of r-packets, at the segment midpoint; kappagrey * rho is a float product as in the reference.
+// An empty cell would add rho = 0 to the reference's extra slot rpkt_emiss[npts_model]: skipped.
+DEVFN void rlc_emiss_rpkt(const Ctx &K, const Pkt &p, double dist) {
+  const int mgi = cell_mgi(K, p.where);
+  if (mgi == K.G.npts_model) return;
+  if (dist > 0.0) {
+    const double t = p.prop_time;
+    const double vel_vec[3] = {p.pos[0] / t, p.pos[1] / t, p.pos[2] / t};
+    double cont = (K.C.kappagrey[mgi] * K.C.rho[mgi]);
+    cont = cont * p.e_rf * dist * (1. - (2. * dot(vel_vec, p.dir) / ARTIS_CLIGHT));
+    safeadd(&K.E.rpkt_emiss[mgi], 1.e-20 * cont);
+  }
+}
+
 // rpkt.cc:623-813
 template <typename Cold = ColdFull>
 DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
@@ -1134,6 +1149,7 @@ DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
     }
     move_pkt_withtime(K, p, dist / 2.);
     update_estimators(x, p, kap, dist);
+    if (K.R.do_rlc_est == 1 || K.R.do_rlc_est == 2) rlc_emiss_rpkt(K, p, dist);
     if (which == 2) {
       p.prop_time = t2;
       move_pkt(K, p, dist / 2.);

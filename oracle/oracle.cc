@@ -1941,8 +1941,25 @@ void rpkt_event_thickcell(const Ctx &c, Est &E, artis_rng *rng, artis_packet *p)
   p->em_time = (int)p->prop_time;
 }
 
+// grey_emissivities.cc:79-122 rlc_emiss_rpkt: the rate at which grey opacity destroys (and re-creates) r-packets,
+// called at the midpoint of every r-packet path segment when do_rlc_est is 1 or 2 (rpkt.cc:739-741, 769-771,
+// 791-793).  kappagrey * rho is a float product, as grid::get_kappagrey / get_rho return floats.  An empty cell's
+// slot (rpkt_emiss[npts_model], grid.cc:1700) only ever receives 0 (rho = 0) and is not part of the ABI array.
+void rlc_emiss_rpkt(const Ctx &c, Est &E, const artis_packet *p, double dist) {
+  const int mgi = cell_mgi(c, p->where);
+  if (mgi == npts_model(c) || !E.e->rpkt_emiss) return;
+  if (dist > 0.0) {
+    double vel_vec[3];
+    get_velocity(p->pos, vel_vec, p->prop_time);
+    double cont = (c.cs->kappagrey[mgi] * c.cs->rho[mgi]);
+    cont = cont * p->e_rf * dist * (1. - (2. * dot(vel_vec, p->dir) / ARTIS_CLIGHT));
+    safeadd(&E.e->rpkt_emiss[mgi], 1.e-20 * cont);
+  }
+}
+
 // rpkt.cc:623-813
 bool do_rpkt_step(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_packet *p, double t2) {
+  const bool rlc = c.rp.do_rlc_est != 0 && c.rp.do_rlc_est != 3;
   const int cellindex = p->where;
   int mgi = cell_mgi(c, cellindex);
   const int oldmgi = mgi;
@@ -2001,6 +2018,7 @@ bool do_rpkt_step(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
   if ((sdist < tdist) && (sdist < edist)) {
     move_pkt_withtime(c, p, sdist / 2.);
     update_estimators(c, tc, E, p, sdist);
+    if (rlc) rlc_emiss_rpkt(c, E, p, sdist);
     move_pkt_withtime(c, p, sdist / 2.);
     if (snext != p->where) {
       change_cell(E, p, snext);
@@ -2015,6 +2033,7 @@ bool do_rpkt_step(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
   } else if ((edist < sdist) && (edist < tdist)) {
     move_pkt_withtime(c, p, edist / 2.);
     update_estimators(c, tc, E, p, edist);
+    if (rlc) rlc_emiss_rpkt(c, E, p, edist);
     move_pkt_withtime(c, p, edist / 2.);
     if (c.cs->thick[mgi] == 1)
       rpkt_event_thickcell(c, E, rng, p);
@@ -2030,6 +2049,7 @@ bool do_rpkt_step(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
   } else if ((tdist < sdist) && (tdist < edist)) {
     move_pkt_withtime(c, p, tdist / 2.);
     update_estimators(c, tc, E, p, tdist);
+    if (rlc) rlc_emiss_rpkt(c, E, p, tdist);
     p->prop_time = t2;
     move_pkt(c, p, tdist / 2.);
     p->last_event = p->last_event + 1000;

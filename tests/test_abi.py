@@ -117,3 +117,21 @@ def test_raw_tmp_packet_file_roundtrip(tmp_path, small_model):
     assert os.path.getsize(f) == 37 * 304
     back = np.fromfile(f, dtype=ffi.PACKET_DTYPE)
     assert back.tobytes() == pk.tobytes()
+
+
+def test_init_refuses_unsupported_run_params():
+    """artis_gpu_init returns ARTIS_ERR_UNSUPPORTED (before touching the GPU) for option values the engine does not
+    propagate, instead of accepting and ignoring them: do_rlc_est outside 0..3 (input.cc:1976-1982), opacity_case
+    outside 0..5 (grid.cc:627-677), a switch that is not 0/1."""
+    from artis_amd import gpu_lib
+    from artis_amd.model import Model
+
+    m = Model(ngrid_1d=4, nlevels_per_ion=10, n_ionising=4, max_lines=200, ntstep=10)
+    L = gpu_lib()
+    for field, val in (("do_rlc_est", 4), ("do_rlc_est", -1), ("opacity_case", 6), ("pol_dipole", 2),
+                       ("nlte_pops_on", 7), ("comp_est", -1), ("max_path_step", 0.0)):
+        p = ffi.RunParams.from_buffer_copy(m.params)
+        setattr(p, field, val)
+        rc = L.artis_gpu_init(0, m.atomic, m.geometry, C.byref(p))
+        assert rc == -6, (field, rc)  # ARTIS_ERR_UNSUPPORTED (include/artis_gpu.h)
+        assert L.artis_gpu_last_error().decode(), field

@@ -374,3 +374,22 @@ def test_estimator_block_roundtrip_and_rccl(small_model, engine_factory):
     eng.allreduce_estimators()
     again = eng.download_estimators()
     assert np.array_equal(adist.pack_estimators(again), 2 * hb)
+
+
+@pytest.mark.parametrize("rlc", [1, 2])
+def test_rlc_emiss_rpkt_vs_oracle(small_model, engine_factory, rlc):
+    """do_rlc_est 1 / 2 (input.txt line 9 = 2 / 3, input.cc:1976-1979): rlc_emiss_rpkt (grey_emissivities.cc:79-122)
+    on every r-packet segment; rpkt_emiss compared with the oracle, packets unchanged by the estimator."""
+    p = ffi.RunParams.from_buffer_copy(small_model.params)
+    p.do_rlc_est = rlc
+    eng = engine_factory(small_model, params=p)
+    small_model.set_timestep(9)
+    pk0 = small_model.init_rpackets(9, 3000, seed=17)
+    eng.upload_cellstate(9)
+    pg = pk0.copy()
+    eg = eng.update_packets(9, pg)
+    po = pk0.copy()
+    eo, _ = oracle_lib.update_packets(small_model, 9, po, nthreads=16, params=p)
+    parity.assert_packets_match(pg, po)
+    parity.assert_estimators_match(eg, eo)
+    assert (eo.rpkt_emiss > 0).sum() > 5

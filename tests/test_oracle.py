@@ -147,3 +147,35 @@ def test_shell_model_runs(shell_model):
     pk, est, work = _run(shell_model, 5, 800)
     assert est.struct.nesc == (pk["type"] == ffi.TYPE_ESCAPE).sum()
     assert work[1] > 0
+
+
+@pytest.mark.parametrize("rlc", [1, 2])
+def test_rlc_emiss_rpkt(small_model, rlc):
+    """rlc_emiss_rpkt (grey_emissivities.cc:79-122, called at rpkt.cc:739-741, 769-771, 791-793 when do_rlc_est is
+    1 or 2): rpkt_emiss gets 1e-20 kappagrey rho e_rf d (1 - 2 v.n/c) per r-packet segment, nothing changes in the
+    transport, and do_rlc_est 3 (the test configs) adds nothing.  To order v/c, e_rf (1 - 2 v.n/c) = e_cmf (1 - v.n/c),
+    so the estimator is 1e-20 kappagrey rho J within a few v/c (v/c <= 0.033 here)."""
+    m = small_model
+    m.set_timestep(8)
+    pk0 = m.init_rpackets(8, 800, seed=21)
+    p = ffi.RunParams.from_buffer_copy(m.params)
+    p.do_rlc_est = rlc
+    pa = pk0.copy()
+    ea, _ = oracle_lib.update_packets(m, 8, pa, params=p)
+    pb = pk0.copy()
+    eb, _ = oracle_lib.update_packets(m, 8, pb)  # do_rlc_est 3
+    assert pa.tobytes() == pb.tobytes()
+    assert not eb.rpkt_emiss.any()
+    kg_rho = _cell_array(m, "kappagrey") * _cell_array(m, "rho")
+    sel = ea.J > 0
+    assert sel.sum() > 5 and (ea.rpkt_emiss[~sel] == 0).all()
+    ratio = ea.rpkt_emiss[sel] / (1e-20 * kg_rho[sel] * ea.J[sel])
+    assert np.all(np.abs(ratio - 1) < 0.1), ratio
+
+
+def _cell_array(model, name):
+    """A float32 [npts_model] array of artis_cell_state (field order of include/artis_gpu.h)."""
+    order = ["Te", "TR", "TJ", "W", "nne", "nnetot", "rho", "kappagrey"]
+    ptrs = (C.c_void_p * len(order)).from_address(model.cellstate)
+    p = ptrs[order.index(name)]
+    return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), (model.npts_model,)).astype(np.float64)
