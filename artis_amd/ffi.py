@@ -662,7 +662,9 @@ class NlteCells(C.Structure):
 
 
 def nt_data_dir():
-    return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "nt_data")
+    """The reference's data/ tables read by the Spencer-Fano setup (collion.txt, binding_energies.txt,
+    auger-km1993-table2.txt), shipped as package data."""
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "nt_data")
 
 
 class NtDataHandle:

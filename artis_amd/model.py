@@ -105,11 +105,11 @@ class Model:
         self._load_gamma_lines()
         self.gamma_spectra = self._lib.artis_model_gamma_spectra(self._h)
 
-    # the reference's own gamma-line data files (data/ni56_lines.txt, data/co56_lines.txt), kept as fixtures
+    # the reference's own gamma-line data files (data/ni56_lines.txt, data/co56_lines.txt), package data
     GAMMA_LINE_FILES = {0: "ni56_lines.txt", 1: "co56_lines.txt"}
 
     def _load_gamma_lines(self):
-        d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "gamma_lines")
+        d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "gamma_lines")
         for nuc, fn in self.GAMMA_LINE_FILES.items():
             path = os.path.join(d, fn)
             if not os.path.exists(path):

@@ -53,7 +53,7 @@ def test_pellet_path_is_schedule_independent():
 
 
 def test_gamma_line_fixtures_match_reference_format():
-    """tests/golden/gamma_lines holds the reference's data/ni56_lines.txt and data/co56_lines.txt; the
+    """artis_amd/data/gamma_lines holds the reference's data/ni56_lines.txt and data/co56_lines.txt; the
     average gamma energy per decay is the line sum (gammapkt.cc:74-81)."""
     m = Model(**CFG)
     gs = ffi.GammaSpectra.from_address(m.gamma_spectra)

@@ -1,0 +1,94 @@
+#!/bin/bash
+# The GPU-box measurement script (run through gpurun from the repo root).  Subcommands, each run under its own
+# time limit, chained with && so that the first failure ends the call:
+#
+#   tools/gpu.sh tests [pytest paths / -k expr ...]  the -m gpu suite (or a selection)    -> $O/gpu_tests.log
+#   tools/gpu.sh bench [bench.py args ...]           one bench line                        -> $O/bench.json
+#   tools/gpu.sh prof [bench.py args ...]            the bench under rocprofv3 --stats     -> $O/prof/, $O/bench_prof.json
+#   tools/gpu.sh pmc  [bench.py args ...]            FETCH_SIZE / WRITE_SIZE passes (separate runs) summarised by
+#                                                    tools/pmc_summary.py, copied to profiles/pmc_$T_$NAME.json
+#   tools/gpu.sh sq   [bench.py args ...]            one SQ instruction-counter pass       -> $O/sq/
+#   tools/gpu.sh ab name1[:ENV=V] name2 ...          A/B of engine builds (tools/build_variants.sh) on the bench
+#   tools/gpu.sh final                               tests, prof, pmc, default bench line (the round-end set)
+#
+# Environment: T (tag, default "r4"), O (output dir, default gpurun_out/$T), NAME (pmc summary name, default
+# "bench"), P (packets for pmc / sq / ab, default 1e7), BENCH_ARGS (extra bench args for ab), ENVS (env for ab).
+cd /root/repo || exit 1
+export TMPDIR=/tmp
+T=${T:-r4}
+O=${O:-gpurun_out/$T}
+mkdir -p "$O"
+cmd=$1
+shift
+
+run_tests() {
+  timeout -k 10 900 python -u -m pytest ${@:-tests} -m gpu -x -v --timeout 300 --timeout-method thread \
+    > "$O/gpu_tests.log" 2>&1
+  local rc=$?
+  tail -1 "$O/gpu_tests.log"
+  return $rc
+}
+
+run_bench() {
+  timeout -k 10 900 python3 -u bench.py "$@" > "$O/bench.json" 2> "$O/bench.err" && tail -c 400 "$O/bench.json"
+}
+
+run_prof() {
+  timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 -u bench.py --no-cpu-baseline "$@" \
+    > "$O/bench_prof.json" 2> "$O/bench_prof.err"
+}
+
+# pmc [bench args]: the bench's defaults are --packets 1e7 --nts 10; the summary needs the same numbers
+run_pmc() {
+  local name=${NAME:-bench} packets=${P:-10000000} nts=10 vp=0 a
+  local args=("$@")
+  for ((i = 0; i < ${#args[@]}; i++)); do
+    a=${args[$i]}
+    case "$a" in
+      --packets) packets=${args[$((i + 1))]} ;;
+      --nts) nts=${args[$((i + 1))]} ;;
+      --vpkt) vp=${args[$((i + 1))]} ;;
+    esac
+  done
+  # (argparse keeps the last --packets, the one parsed above)
+  local B="python3 bench.py --packets $packets --steps 1 --warmup 0 --no-cpu-baseline --no-update-grid --no-extra $*"
+  mkdir -p "$O/pmc_$name"
+  rm -rf "$O/pmc_$name/fetch" "$O/pmc_$name/write"
+  timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$O/pmc_$name/fetch" -o run -- $B > "$O/pmc_$name/f.log" 2>&1 &&
+  timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$O/pmc_$name/write" -o run -- $B > "$O/pmc_$name/w.log" 2>&1 &&
+  python3 tools/pmc_summary.py --fetch "$O/pmc_$name/fetch" --write "$O/pmc_$name/write" --packets "$packets" --ngrid 50 \
+    --nts "$nts" $([ "$vp" != 0 ] && echo --vpkt "$vp") --out "$O/pmc_$name.json" &&
+  cp "$O/pmc_$name.json" "profiles/pmc_${T}_$name.json"
+}
+
+run_sq() {
+  rm -rf "$O/sq"
+  mkdir -p "$O/sq"
+  timeout -s KILL 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_VALU \
+    SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM --kernel-trace -d "$O/sq/db" -o run -- python3 bench.py \
+    --packets ${P:-2000000} --steps 1 --warmup 0 --no-cpu-baseline --no-update-grid --no-extra "$@" > "$O/sq/sq.log" 2>&1
+}
+
+run_ab() {
+  local v name envs so tag
+  for v in "$@"; do
+    name=${v%%:*}; envs=""; [[ "$v" == *:* ]] && envs=${v#*:}
+    so=build/ab/$name/libartis_gpu.so; [ "$name" = main ] && so=artis_amd/lib/libartis_gpu.so
+    tag=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')
+    env ARTIS_GPU_SO=$so $ENVS $envs timeout -k 10 400 python3 bench.py --packets ${P:-10000000} --steps 1 --warmup 1 \
+      --no-cpu-baseline --no-update-grid --no-extra $BENCH_ARGS > "$O/ab_$tag.json" 2> "$O/ab_$tag.err" ||
+      { echo "FAIL $v"; tail -5 "$O/ab_$tag.err"; return 1; }
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], 'value', round(d['value']), 'ms', round(d['ms_per_step']), 'precompute', round(d.get('precompute_ms', 0)), {k: round(x) for k, x in d['kernel_ms'].items()}, 'frac', round(d['roofline']['frac'], 4))" "$O/ab_$tag.json" "$v"
+  done
+}
+
+case "$cmd" in
+  tests) run_tests "$@" ;;
+  bench) run_bench "$@" ;;
+  prof) run_prof "$@" ;;
+  pmc) run_pmc "$@" ;;
+  sq) run_sq "$@" ;;
+  ab) run_ab "$@" ;;
+  final) run_tests && run_prof --no-extra && run_pmc && run_bench ;;
+  *) echo "usage: tools/gpu.sh tests|bench|prof|pmc|sq|ab|final [args]"; exit 2 ;;
+esac
