@@ -67,6 +67,10 @@ def vpkt_byte_model(vwork, traces, nions_total):
             + 88.0 * vwork["bf_active"] + 48.0 * vwork["escaped"])
 
 
+WORK_NAMES = ["active", "rpkt_steps", "lines_scanned", "line_taus", "kappa_evals", "bf_active", "est_segments",
+              "gc_updates", "ma_jumps", "ma_trans", "kpkt", "kpkt_terms", "escaped", "es_scat", "bb_events",
+              "cont_events"]
+
 KERNEL_NAME = {"rpkt": "k_rpkt<2>", "ma": "k_ma<true, 1>", "kpkt": "k_kpkt", "vpkt": "k_vpkt"}
 
 
@@ -147,24 +151,32 @@ def dry_launch(world, rank):
     del torch
 
 
-def survey_sized_workload(P, steps, nts, rank, progress):
-    """SURVEY §8(d)'s specified atom size beside the heavier default: ~100 levels per non-top ion (all level pairs
-    joined by a line: 44 550 lines), 56 ionising levels (504 continua), the same 50^3 grid, timestep and P packets
-    per GPU, timed like the main line (resident packets, per-step precompute + transport)."""
-    from artis_amd import Engine
-    from artis_amd.model import Model
+def ceiling(alg, P, value):
+    """The workload's own bound: algorithmic bytes per packet-timestep (every kernel class, SURVEY §8(d) figures)
+    and the packet-timesteps/s they allow at the 8 TB/s HBM peak; value as a fraction of it."""
+    per = sum(alg.values()) / max(P, 1)
+    lim = HBM_PEAK_GBS * 1e9 / max(per, 1e-300)
+    return {"alg_bytes_per_packet_timestep": per, "packets_per_s_at_hbm_peak": lim, "frac": value / lim,
+            "note": "the 1e8 packets/s/GPU target needs <= 80 KB per packet-timestep at 8 TB/s; this workload's "
+                    "macro-atom walks (jumps per packet in work_per_packet) set its bytes"}
 
-    m = Model(ngrid_1d=50, nlevels_per_ion=100, line_window=100, n_resonance=5, n_ionising=56)
+
+def timed_workload(m, P, nts, rank, steps, params=None, etot=None, seed=3000):
+    """P resident r-packets of model m at timestep nts, timed like the main line (restore, zero, upload_cellstate
+    with the per-cell precompute, transport): one warm step, then `steps` timed ones.  Packets/s, the kernel times,
+    the dominant kernel's roofline fraction (engine byte model) and the workload ceiling."""
+    from artis_amd import Engine
+
     m.set_timestep(nts)
-    prm = m.params
+    prm = ffi_params(m) if params is None else params
     prm.rank = rank
-    pk = m.init_rpackets(nts, P, seed=3000 + rank)
+    pk = m.init_rpackets(nts, P, seed=seed + rank, **({} if etot is None else {"etot": etot}))
     eng = Engine(m, params=prm)
     eng.upload_cellstate(nts)
     eng.upload(pk)
     eng.snapshot()
     del pk
-    ms, kts, work = [], [], np.zeros(16, dtype=np.int64)
+    ms, kts, pre, work = [], [], [], np.zeros(16, dtype=np.int64)
     for k in range(steps + 1):
         eng.restore()
         eng.zero_estimators()
@@ -175,22 +187,108 @@ def survey_sized_workload(P, steps, nts, rank, progress):
         if k > 0:  # the first step warms up
             ms.append(dt * 1e3)
             kts.append(eng.last_kernel_times())
+            pre.append(eng.last_precompute_ms())
             work[:] = eng.last_work()
     tables = eng.table_info()
     eng.close()
     alg = byte_model(work, m.nions_total)
-    kt = {c: (float(np.mean([t[c][0] for t in kts])), float(np.mean([t[c][1] for t in kts]))) for c in ("rpkt", "ma")}
-    dom = max(kt, key=lambda c: kt[c][0])
+    kt = {c: (float(np.mean([t[c][0] for t in kts])), float(np.mean([t[c][1] for t in kts])))
+          for c in ("rpkt", "ma", "kpkt")}
+    dom = max(("rpkt", "ma"), key=lambda c: kt[c][0])
     launches = max(kt[dom][1], 1.)
     gbs = alg[dom] / launches / max(kt[dom][0] / 1e3 / launches, 1e-12) / 1e9
-    out = {"levels_per_ion": 100, "levels": m.nlevels_total, "lines": m.nlines, "bf_continua": m.nbfcontinua,
-           "packets": P, "steps": steps, "ms_per_step": float(np.mean(ms)), "value": P / (float(np.mean(ms)) / 1e3),
-           "unit": "packets/s", "kernel_ms": {c: v[0] for c, v in kt.items()},
-           "roofline": {"kernel": KERNEL_NAME[dom], "achieved": gbs, "peak": HBM_PEAK_GBS, "frac": gbs / HBM_PEAK_GBS},
-           "macro_atom_jumps_per_packet": float(work[8]) / max(P, 1), "tables": tables}
+    value = P / (float(np.mean(ms)) / 1e3)
+    return {"npts_model": m.npts_model, "levels": m.nlevels_total, "lines": m.nlines, "bf_continua": m.nbfcontinua,
+            "packets": P, "timestep": nts, "steps": steps, "ms_per_step": float(np.mean(ms)), "value": value,
+            "unit": "packets/s", "precompute_ms": float(np.mean(pre)), "kernel_ms": {c: v[0] for c, v in kt.items()},
+            "roofline": {"kernel": KERNEL_NAME[dom], "achieved": gbs, "peak": HBM_PEAK_GBS, "frac": gbs / HBM_PEAK_GBS},
+            "ceiling": ceiling(alg, P, value),
+            "work_per_packet": {k: float(v) / max(P, 1) for k, v in zip(WORK_NAMES, work)}, "tables": tables}
+
+
+def ffi_params(m):
+    from artis_amd import ffi
+
+    return ffi.RunParams.from_buffer_copy(m.params)
+
+
+def survey_sized_workload(P, steps, nts, rank, progress):
+    """SURVEY §8(d)'s specified atom size beside the heavier default: ~100 levels per non-top ion (all level pairs
+    joined by a line: 44 550 lines), 56 ionising levels (504 continua), the same 50^3 grid, timestep and P packets
+    per GPU, timed like the main line (resident packets, per-step precompute + transport)."""
+    from artis_amd.model import Model
+
+    m = Model(ngrid_1d=50, nlevels_per_ion=100, line_window=100, n_resonance=5, n_ionising=56)
+    out = timed_workload(m, P, nts, rank, steps)
+    out["levels_per_ion"] = 100
+    out["macro_atom_jumps_per_packet"] = out["work_per_packet"]["ma_jumps"]
     progress(f"SURVEY-sized workload: {out['ms_per_step']:.0f} ms per step")
     m.close()
     return out
+
+
+def baseline_configs(P, rank, progress, which=("w7_100_shells", "nebular_onezone", "kilonova")):
+    """BASELINE.json configs 2-4 at their stated per-GPU sizes, each timed like the main line (synthetic atomic
+    data; the reference's own model / input files where the config names them):
+      config 2: classic LTE, 1D 100-shell W7-like model on the 50^3 cuboid, 1e7 r-packets;
+      config 3: tests/nebularonezone_inputfiles with the nebular options (NLTE populations, NO_LUT photoionisation
+                integrals, binned radiation field, detailed bf estimators, NT), 1e7 packets in its one zone;
+      config 4: tests/kilonova_inputfiles (25 shells, relativistic Doppler, excitation temperature T_e), the
+                1.25e7-packet per-GPU share of 1e8 on 8 GPUs."""
+    from artis_amd.model import Model
+
+    ref = os.path.join(REPO, "tests", "golden", "ref_inputs")
+
+    def files(name):
+        d = os.path.join(ref, name)
+        mf = os.path.join(d, "model.txt.xz" if os.path.exists(os.path.join(d, "model.txt.xz")) else "model.txt")
+        return (os.path.join(d, "input-newrun.txt"), mf, os.path.join(d, "abundances.txt"))
+
+    out = {}
+    for name in which:
+        if name == "w7_100_shells":
+            m, nts, n = Model(ngrid_1d=50, nshells_1d=100), 10, P
+        elif name == "nebular_onezone":
+            m, nts, n = Model(files=files("nebularonezone"), ngrid_1d=50, nebular=1), 6, P
+        else:
+            m, nts, n = Model(files=files("kilonova"), ngrid_1d=50, relativistic=1, excitation_te=1), 6, P * 5 // 4
+        rec = timed_workload(m, n, nts, rank, 1)
+        rec["config"] = {"w7_100_shells": 2, "nebular_onezone": 3, "kilonova": 4}[name]
+        out[name] = rec
+        progress(f"config {name}: {rec['ms_per_step']:.0f} ms per step, {rec['value']:.3g} packets/s")
+        m.close()
+    return out
+
+
+def timestep_loop(P, nts0, nsteps, rank, progress):
+    """The whole do_timestep body on the device (artis_amd.timestep.LteTimestepLoop, sn3d.cc:514-673): update_grid's
+    preparation + temperature solution from the previous step's raw estimators (GPU), upload_cellstate (per-cell
+    precompute), update_packets on the resident packets, over consecutive timesteps of the bench model; packet
+    energies normalised to the cell state's radiation field so the estimators feed update_grid consistently."""
+    from artis_amd import Engine
+    from artis_amd.model import Model
+    from artis_amd.timestep import LteTimestepLoop
+
+    m = Model(ngrid_1d=50)
+    m.set_timestep(nts0)
+    prm = ffi_params(m)
+    prm.rank = rank
+    eng = Engine(m, params=prm)
+    loop = LteTimestepLoop(m, eng, rank=rank)
+    pk = m.init_rpackets(nts0, P, seed=4000 + rank, etot=loop.radiation_energy(nts0))
+    eng.upload(pk)
+    del pk
+    t = time.perf_counter()
+    recs = loop.run(nts0, nsteps, progress=progress)
+    total = time.perf_counter() - t
+    eng.close()
+    m.close()
+    active = P * nsteps
+    return {"packets": P, "timesteps": [r["nts"] for r in recs], "wall_s": total,
+            "value": active / total, "unit": "packet-timesteps/s (each packet propagated through every timestep)",
+            "per_timestep": recs,
+            "note": "timestep k > 0: update_grid (GPU preparation + solution, host cell-state write) -> "
+                    "upload_cellstate -> update_packets (resident) -> raw estimators D2H"}
 
 
 def nebular_update_grid(rank, cpu, progress):
@@ -533,9 +631,11 @@ def main():
     neb = None
     if rank == 0 and not args.no_update_grid and vcfg is None:
         neb = nebular_update_grid(rank, not args.no_cpu_baseline, progress)
-    survey8d = None
+    survey8d = configs = tloop = None
     if rank == 0 and world == 1 and vcfg is None and not args.no_extra:
         survey8d = survey_sized_workload(P, 2, nts, rank, progress)
+        configs = baseline_configs(P, rank, progress)
+        tloop = timestep_loop(P, nts, 3, rank, progress)
 
     if rank == 0:
         line = {
@@ -585,10 +685,8 @@ def main():
             "transport_ms": float(np.mean(transport_ms)),
             "event_rounds": int(np.max(rounds)) if rounds else 0,
             "kernel_ms": {k: v[0] for k, v in kt.items()},
-            "work_per_packet": {k: float(v) / max(P, 1) for k, v in zip(
-                ["active", "rpkt_steps", "lines_scanned", "line_taus", "kappa_evals", "bf_active", "est_segments",
-                 "gc_updates", "ma_jumps", "ma_trans", "kpkt", "kpkt_terms", "escaped", "es_scat", "bb_events",
-                 "cont_events"], work)},
+            "work_per_packet": {k: float(v) / max(P, 1) for k, v in zip(WORK_NAMES, work)},
+            "ceiling": ceiling(alg, P, value / world),
         }
         if ugrid is not None:
             line["update_grid"] = ugrid
@@ -598,6 +696,10 @@ def main():
             line["dropin_host_path"] = dropin
         if survey8d is not None:
             line["workload_survey_8d"] = survey8d
+        if configs is not None:
+            line["baseline_configs"] = configs
+        if tloop is not None:
+            line["timestep_loop"] = tloop
         if vcfg is not None:
             vms = float(np.mean([v[0] for v in vstats]))
             line["config"]["workload"] += (f"; virtual packets: {vcfg.nobs} observers x {vcfg.nspectra} spectra, "

@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 import oracle_lib
+import parity
 from artis_amd import Engine, ffi
 from artis_amd.model import Model
 
@@ -206,3 +207,47 @@ def test_gpu_prepare_temperatures_fatal_nonfinite(small):
     finally:
         eng.close()
     assert np.array_equal(pg.TR_out, before)
+
+
+def test_timestep_loop_on_device_matches_oracle():
+    """sn3d.cc's do_timestep body with every per-timestep stage on the device (artis_amd.timestep.LteTimestepLoop):
+    update_grid's preparation + temperature solution from the previous step's raw estimators, upload_cellstate and
+    update_packets on resident packets, three consecutive timesteps.  Each update_grid against the oracle's replay
+    of the same inputs; each transport step against the oracle on the solved cell state."""
+    from artis_amd.timestep import LteTimestepLoop
+
+    m = Model(ngrid_1d=8, nlevels_per_ion=30, n_ionising=12, max_lines=3000, ntstep=20)
+    nts0 = 8
+    m.set_timestep(nts0)
+    eng = Engine(m)
+    try:
+        loop = LteTimestepLoop(m, eng)
+        pk0 = m.init_rpackets(nts0, 3000, seed=19, etot=loop.radiation_energy(nts0))
+        eng.upload(pk0)
+        po = pk0.copy()
+        est = None
+        for k in range(3):
+            nts = nts0 + k
+            if k > 0:
+                loop.update_grid(nts, est)
+                te_in, ug_in = loop.last_inputs
+                assert oracle_lib.prepare_temperatures(m, te_in, ug_in) == 0
+                te_in.TR, te_in.W, te_in.TJ = ug_in.TR_out, ug_in.W_out, ug_in.TJ_out
+                te_in.ffheating, te_in.colheating = ug_in.ff_out, ug_in.col_out
+                te_in.gamma, te_in.bfheating = ug_in.gamma_out, ug_in.bfheating_out
+                assert oracle_lib.solve_temperatures(m, te_in) == 0
+                gte, g = loop.solution, te_in.mgi_list
+                agree = (gte.iters[g] == te_in.iters[g]) & (np.abs(gte.Te[g] - te_in.Te[g]) <= 1e-9 * te_in.Te[g])
+                assert agree.mean() >= 0.99, agree.mean()
+                assert (gte.iters[g] != 0).all()  # every cell through call_T_e_finder (no LTE branch)
+            eng.upload_cellstate(nts)
+            eng.zero_estimators()
+            eng.step_resident(nts)
+            est = eng.download_estimators()
+            pg = np.zeros_like(pk0)
+            eng.download(pg)
+            eo, _ = oracle_lib.update_packets(m, nts, po, nthreads=16)
+            parity.assert_packets_match(pg, po)
+            parity.assert_estimators_match(est, eo)
+    finally:
+        eng.close()

@@ -5,6 +5,8 @@ the reference's solution satisfies.  CPU only; the GPU parity tests are in test_
 Parity unpinned for this row: the reference writes its solution only into estimators_*.out files of full runs with
 the downloaded atomic dataset (no fixture holds one); the checks here are the solver's own defining relations.
 """
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -168,3 +170,42 @@ def test_prepare_nonfinite_renorm_is_fatal(te_model):
     te.thick[te.mgi_list[1]] = 1
     prep = ffi.UgArrays(m, deltat=0.5 * DAY, tratmid=3.0, seed=3)
     assert oracle_lib.prepare_temperatures(m, te, prep) == 0
+
+
+def test_timestep_loop_update_grid_wiring_on_oracle():
+    """artis_amd.timestep.LteTimestepLoop.update_grid with the oracle standing in for the engine's two update_grid
+    calls (CPU): the previous step's raw estimators go through the preparation and the temperature solution, and the
+    solved state (T_e, n_e, radiation field, populations, cooling, renormalisation) lands in the model's cell state
+    that the next upload_cellstate reads."""
+    from artis_amd.timestep import LteTimestepLoop
+
+    m = Model(ngrid_1d=6, nlevels_per_ion=20, n_ionising=8, max_lines=800, ntstep=20)
+
+    class OracleEngine:
+        def prepare_temperatures(self, te, prep):
+            assert oracle_lib.prepare_temperatures(m, te, prep) == 0
+
+        def solve_temperatures(self, te):
+            assert oracle_lib.solve_temperatures(m, te) == 0
+            return 0.
+
+    loop = LteTimestepLoop(m, OracleEngine())
+    m.set_timestep(8)
+    pk = m.init_rpackets(8, 2000, seed=4, etot=loop.radiation_energy(8))
+    est, _ = oracle_lib.update_packets(m, 8, pk, nthreads=8)
+    loop.update_grid(9, est)
+    te = loop.solution
+    g = te.mgi_list
+    # every cell went through call_T_e_finder (-1: no root in [MINTEMP, MAXTEMP], which the synthetic atom's line
+    # cooling makes the common outcome; the reference then takes MINTEMP and damps against the previous T_e)
+    assert len(g) > 10 and (te.iters[g] != 0).all() and np.isfinite(te.Te[g]).all() and (te.Te[g] > 0).all()
+    cs = ffi.CellState.from_address(m.cellstate)
+    Te = np.ctypeslib.as_array(C.cast(cs.Te, C.POINTER(C.c_float)), (m.npts_model,))
+    TR = np.ctypeslib.as_array(C.cast(cs.TR, C.POINTER(C.c_float)), (m.npts_model,))
+    assert np.array_equal(Te[g], te.Te[g]) and np.array_equal(TR[g], te.TR[g])
+    # the prepared radiation field comes from this step's J / nuJ: T_R differs from the stand-in's
+    m2 = Model(ngrid_1d=6, nlevels_per_ion=20, n_ionising=8, max_lines=800, ntstep=20)
+    m2.set_timestep(9)
+    TR2 = np.ctypeslib.as_array(C.cast(ffi.CellState.from_address(m2.cellstate).TR, C.POINTER(C.c_float)),
+                                (m2.npts_model,))
+    assert not np.allclose(TR[g], TR2[g])
