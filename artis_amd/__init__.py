@@ -218,10 +218,11 @@ class Engine:
     def table_info(self):
         """Per-cell table coverage: {"cells", "linecoef_rows", "linecoef_bytes", "macache_rows", "macache_bytes",
         "marates_bytes"} (artis_gpu_table_info)."""
-        w = np.zeros(8, dtype=np.int64)
+        w = np.zeros(11, dtype=np.int64)
         self._check(self.lib.artis_gpu_table_info(w.ctypes.data), "table_info")
         return dict(zip(("cells", "linecoef_rows", "linecoef_bytes", "macache_rows", "macache_bytes",
-                         "marates_bytes", "ma_activations_cached", "ma_activations"), (int(x) for x in w)))
+                         "marates_bytes", "ma_jumps_sampled_recorded", "ma_jumps_sampled", "ma_level_records",
+                         "ma_level_bytes", "ma_pool_bytes"), (int(x) for x in w)))
 
     def spectrum(self, nnubins=1000, nprocs=1):
         """Device-binned spectrum [ntstep, nnubins] and light curves (lum, lumcmf) of the resident packets."""

@@ -380,6 +380,167 @@ __global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, const double *__
   }
 }
 
+// ---- level mode of the macro-atom key records (DevCells::ma_lptr): placement and build ----------------------
+// k_lvl_buckets: over every (cell, level) pair's sampled jump count c since the last placement: [0] the jumps on pairs
+// that had a record, [33] all jumps, [1 + floor(log2 c)] the pool lines the pairs of that count bucket would take
+__global__ __launch_bounds__(256) void k_lvl_buckets(Ctx K, const uint32_t *__restrict__ rec_lines,
+                                                     unsigned long long *__restrict__ out, int64_t npairs) {
+  __shared__ unsigned long long s[34];
+  if (threadIdx.x < 34) s[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t nl = K.T.nlevels_total;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = K.C.ma_lhist[i];
+    if (!c) continue;
+    atomicAdd(&s[33], (unsigned long long)c);
+    if (K.C.ma_lptr[i] != MA_NOLINE) atomicAdd(&s[0], (unsigned long long)c);
+    const uint32_t rl = rec_lines[i % nl];
+    if (rl) atomicAdd(&s[32 - __clz(c)], (unsigned long long)rl);
+  }
+  __syncthreads();
+  if (threadIdx.x < 34 && s[threadIdx.x]) atomicAdd(&out[threadIdx.x], s[threadIdx.x]);
+}
+
+// k_lvl_select: the new DevCells::ma_lptr and the list of records to build.  have_hist == 0 (no transport yet):
+// whole cells in nonempty-index order (centre outwards), pair (k, ul) at line k * row_lines + rl_off[ul] while it
+// fits the pool.  Otherwise: count bucket above bt, or bucket bt while `rest` lines of it last.
+// ctr: [0] pool lines taken, [1] records listed, [2] lines taken from bucket bt
+__global__ __launch_bounds__(256) void k_lvl_select(Ctx K, const uint32_t *__restrict__ rec_lines,
+                                                    const uint32_t *__restrict__ rl_off, uint32_t row_lines,
+                                                    uint32_t *__restrict__ lptr, uint32_t *__restrict__ ctr,
+                                                    int2 *__restrict__ list, int64_t list_cap, int64_t npairs, int bt,
+                                                    uint32_t rest, uint64_t pool_lines, int have_hist) {
+  const int64_t nl = K.T.nlevels_total;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += (int64_t)gridDim.x * blockDim.x) {
+    const int ul = (int)(i % nl), k = (int)(i / nl);
+    const uint32_t rl = rec_lines[ul];
+    uint32_t line = MA_NOLINE;
+    if (rl && !have_hist) {
+      const uint64_t l0 = (uint64_t)k * row_lines + rl_off[ul];
+      if (l0 + rl <= pool_lines) {
+        line = (uint32_t)l0;
+        atomicAdd(&ctr[0], rl);
+      }
+    } else if (rl) {
+      const uint32_t c = K.C.ma_lhist[i];
+      const int b = c ? 32 - __clz(c) : 0;
+      bool take = b > 0 && b > bt;
+      if (b > 0 && b == bt) take = atomicAdd(&ctr[2], rl) + rl <= rest;
+      if (take) line = atomicAdd(&ctr[0], rl);
+    }
+    lptr[i] = line;
+    if (line != MA_NOLINE) {
+      const uint32_t s = atomicAdd(&ctr[1], 1u);
+      if (s < list_cap) list[s] = make_int2(k, ul);
+    }
+  }
+}
+
+// k_ma_build: the key record of each listed (cell, level) pair, one wave per record -- what k_marates + k_mapack
+// compute for a whole row, for one pair: the lanes evaluate the level's individual rates (ma_rate_at) and stage
+// the terms of its eight action sums in LDS; eight lanes then add up one action each in the reference's list order
+// (macroatom.cc:57-159: every action's running sum only involves its own terms, so the chains are independent and
+// equal to ma_accumulate's sequence bit for bit); the lanes write the normalised 32-bit keys at their record
+// positions (ma_rec_pos, with the block separators).
+#define MA_BUILD_MAX_DOUBLES 6144  // LDS terms of one level (48 KiB); a level with more never gets a record
+__global__ __launch_bounds__(64) void k_ma_build(Ctx K, const int2 *__restrict__ list, uint32_t nlist, int nts) {
+  extern __shared__ double sb[];
+  const int lane = threadIdx.x;
+  const int64_t nl = K.T.nlevels_total;
+  const double t_mid = K.G.ts_mid[nts];
+  for (uint32_t e = blockIdx.x; e < nlist; e += gridDim.x) {
+    const int2 kl = list[e];
+    const int k = kl.x, ul = kl.y;
+    const int mgi = K.C.ne_mgi[k];
+    const MaMeta mm = K.T.ma_meta[ul];
+    const int nd = mm.nd, nr = mm.nr, nu = mm.nu, nt = mm.nt;
+    double *Drad = sb, *Dcol = Drad + nd, *Dsame = Dcol + nd, *Rint = Dsame + nd, *Rrad = Rint + nr,
+           *Rcol = Rrad + nr, *Usame = Rcol + nr, *Uhi = Usame + nu;
+    const double ec = K.T.level_epsilon[ul];
+    const double *pops = K.C.pops + (int64_t)k * nl;
+    const double *corr = K.C.corrphot + (int64_t)k * K.T.ntargets_total;
+    auto pop = [&](int u) { return pops[u]; };
+    auto cph = [&](int s) { return corr[s]; };
+    __syncthreads();  // the previous record's LDS reads are done
+    for (int pos = lane; pos < nd + nr + nu + nt; pos += 64) {
+      const MaItem it = ma_rate_at(K, mgi, ul, t_mid, pos, pop, cph);
+      if (it.kind == MA_KIND_DOWN) {
+        Drad[it.j] = it.R * it.et;
+        Dcol[it.j] = it.C * it.et;
+        Dsame[it.j] = (it.R + it.C) * it.eg;
+      } else if (it.kind == MA_KIND_RECOMB) {
+        Rint[it.j] = (it.R + it.C) * it.eg;
+        Rrad[it.j] = it.R * it.et;
+        Rcol[it.j] = it.C * it.et;
+      } else if (it.kind == MA_KIND_UP) {
+        Usame[it.j] = (it.R + it.C + 0.) * ec;
+      } else {
+        Uhi[it.j] = (it.R + it.C) * ec;
+      }
+    }
+    __syncthreads();
+    if (lane < 8) {  // one running sum per lane, in list order, in place
+      double *a = lane == 0 ? Drad : lane == 1 ? Dcol : lane == 2 ? Dsame : lane == 3 ? Rint : lane == 4 ? Rrad
+                  : lane == 5 ? Rcol : lane == 6 ? Usame : Uhi;
+      const int len = lane < 3 ? nd : lane < 6 ? nr : lane == 6 ? nu : nt;
+      double r = 0.;
+      for (int j = 0; j < len; j++) {
+        r += a[j];
+        a[j] = r;
+      }
+    }
+    __syncthreads();
+    double pr[ARTIS_MA_ACTION_COUNT];
+    pr[ARTIS_MA_ACTION_RADDEEXC] = nd ? Drad[nd - 1] : 0.;
+    pr[ARTIS_MA_ACTION_COLDEEXC] = nd ? Dcol[nd - 1] : 0.;
+    pr[ARTIS_MA_ACTION_INTERNALDOWNSAME] = nd ? Dsame[nd - 1] : 0.;
+    pr[ARTIS_MA_ACTION_INTERNALDOWNLOWER] = nr ? Rint[nr - 1] : 0.;
+    pr[ARTIS_MA_ACTION_RADRECOMB] = nr ? Rrad[nr - 1] : 0.;
+    pr[ARTIS_MA_ACTION_COLRECOMB] = nr ? Rcol[nr - 1] : 0.;
+    pr[ARTIS_MA_ACTION_INTERNALUPSAME] = nu ? Usame[nu - 1] : 0.;
+    pr[ARTIS_MA_ACTION_INTERNALUPHIGHER] = nt ? Uhi[nt - 1] : 0.;
+    pr[ARTIS_MA_ACTION_INTERNALUPHIGHERNT] = ma_nt_total(K, mgi, ul);
+    double total = 0.;
+    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) total += pr[a];
+    const MaLayout lay = ma_layout(nd, nu, nr, nt);
+    uint16_t *rec = K.C.ma_key + (size_t)K.C.ma_lptr[(int64_t)k * nl + ul] * 64;
+    // positions in k_marates' scratch order: [9 totals | down-same nd | up-same nu | rad_deexc nd | rad_recomb nr |
+    // internal_down_lower nr | internal_up_higher nt]
+    const int len = ARTIS_MA_ACTION_COUNT + 2 * nd + nu + 2 * nr + nt;
+    for (int p = lane; p < len; p += 64) {
+      uint32_t key;
+      if (p < ARTIS_MA_ACTION_COUNT) {
+        double rate = 0.;
+        for (int a = 0; a <= p; a++) rate += pr[a];
+        key = ma_key32(rate, total);
+      } else {
+        int q = p - ARTIS_MA_ACTION_COUNT;
+        if (q < nd) {
+          key = ma_key32(Dsame[q], pr[ARTIS_MA_ACTION_INTERNALDOWNSAME]);
+        } else if ((q -= nd) < nu) {
+          key = ma_key32(Usame[q], pr[ARTIS_MA_ACTION_INTERNALUPSAME]);
+        } else if ((q -= nu) < nd) {
+          key = ma_key32(Drad[q], pr[ARTIS_MA_ACTION_RADDEEXC]);
+        } else if ((q -= nd) < nr) {
+          key = ma_key32(Rrad[q], pr[ARTIS_MA_ACTION_RADRECOMB]);
+        } else if ((q -= nr) < nr) {
+          key = ma_key32(Rint[q], pr[ARTIS_MA_ACTION_INTERNALDOWNLOWER]);
+        } else {
+          key = ma_key32(Uhi[q - nr], pr[ARTIS_MA_ACTION_INTERNALUPHIGHER]);
+        }
+      }
+      int sp;
+      const int rp = ma_rec_pos(lay, p, nd, nu, &sp);
+      rec[rp] = (uint16_t)(key >> 16);
+      rec[lay.hot + rp] = (uint16_t)(key & 0xffffu);
+      if (sp >= 0) {
+        rec[sp] = (uint16_t)(key >> 16);
+        rec[lay.hot + sp] = (uint16_t)(key & 0xffffu);
+      }
+    }
+  }
+}
+
 // DevCells::linecoef: the Sobolev coefficient (B_lu n_l - B_ul n_u) * HCLIGHTOVERFOURPI of every line in every
 // non-empty cell, in get_event's operation order (rpkt.cc:168-187); lanes run along a cell's row (coalesced
 // writes, line records from L2, population gathers from the cell's 29 kB row)
@@ -541,13 +702,24 @@ struct Engine {
   bool ma_cache_ok = true;             // the atomic data fit the cache's record layout (engine_dev.h ma_layout)
   std::vector<int64_t> h_dbl_off;     // per level: offset (doubles) of its exact sums in the k_marates scratch
   double *d_marec_scratch = nullptr;  // k_marates output, [position][cell] per level (k_mapack input)
-  // macro-atom key-record placement (DevCells::ma_row / ma_bin): the cell of each bin (the cached cells, row
-  // order, then the rest), and with a partial cache the per-cell count of M-queue entries since the last placement
+  // macro-atom key records (DevCells::ma_row / ma_bin): row of each cell (row mode), the cell of each bin
   int32_t *d_ma_row = nullptr, *d_ma_bin = nullptr, *d_ma_bincell = nullptr;
-  uint32_t *d_ma_hist = nullptr;
-  std::vector<int32_t> h_ma_bincell;
-  int64_t ma_acts_cached = 0, ma_acts_total = 0;  // activations in cached cells / all, before the last re-placement
-  bool ma_hist_ready = false;
+  // level mode (DevCells::ma_lptr): pool capacity, record size per level in 128-byte lines (0: never recorded),
+  // the activity histogram of the walks since the last placement, and the placement's bookkeeping
+  uint32_t *d_ma_lptr = nullptr, *d_ma_lhist = nullptr, *d_lvl_ctr = nullptr;
+  const uint32_t *d_rec_lines = nullptr, *d_rl_off = nullptr;
+  uint32_t row_lines = 0;  // pool lines of one whole cell's records (the initial placement)
+  unsigned long long *d_lvl_buckets = nullptr;
+  int2 *d_build_list = nullptr;
+  int64_t build_list_cap = 0;
+  uint64_t ma_pool_lines = 0;
+  std::vector<uint32_t> h_rec_lines;
+  int64_t ma_build_lds_doubles = 0;
+  bool ma_lhist_ready = false;
+  bool ma_initial_placement = false;  // the current placement had no activity to go by (whole cells)
+  int64_t ma_level_records = 0, ma_level_lines = 0;  // records / pool lines of the current placement
+  // level mode: sampled jumps on pairs that had a record / on all pairs, over the transports before the last placement
+  int64_t ma_acts_cached = 0, ma_acts_total = 0;
   int64_t marec_scratch_doubles = 0;
   double *d_estblock = nullptr;
   int32_t *d_target_ul = nullptr, *d_target_t = nullptr;
@@ -649,40 +821,76 @@ int dupload(const T **dst, const T *src, size_t count) {
   return 0;
 }
 
-// Give the macro-atom key records to the first ma_rows cells of `order` (the rest walk without records) and lay
-// the M-queue bins out cached cells first (DevCells::ma_row / ma_bin).  Placement never changes a result.
+// The M-queue bins (DevCells::ma_bin, the cell of each bin ma_bincell) in `order`, and in row mode cell k's
+// records at row k.  Placement never changes a result.
 int ma_place(const std::vector<int32_t> &order) {
-  const int n = G.K.C.n_nonempty, R = G.K.C.ma_rows;
+  const int n = G.K.C.n_nonempty;
   std::vector<int32_t> row(n, -1), bin(n);
-  G.h_ma_bincell.assign(order.begin(), order.end());
   for (int b = 0; b < n; b++) {
     const int k = order[b];
-    if (b < R) row[k] = b;
+    if (G.K.C.ma_rows > 0) row[k] = k;
     bin[k] = b;
   }
   HIPCHK(hipMemcpy(G.d_ma_row, row.data(), n * sizeof(int32_t), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(G.d_ma_bin, bin.data(), n * sizeof(int32_t), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(G.d_ma_bincell, order.data(), n * sizeof(int32_t), hipMemcpyHostToDevice));
-  HIPCHK(hipMemset(G.d_ma_hist, 0, n * sizeof(uint32_t)));
-  G.ma_hist_ready = false;
   return 0;
 }
 
-// With a partial key cache: re-place the records on the cells that received the most macro-atom activations
-// since the last placement (ties: the current order), before the precompute builds them.
-int ma_replace() {
-  const int n = G.K.C.n_nonempty;
-  if (!G.ma_hist_ready || G.K.C.ma_rows <= 0 || G.K.C.ma_rows >= n) return 0;
-  std::vector<uint32_t> h(n);
-  HIPCHK(hipMemcpy(h.data(), G.d_ma_hist, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  std::vector<int32_t> order = G.h_ma_bincell;
-  G.ma_acts_cached = G.ma_acts_total = 0;
-  for (int b = 0; b < n; b++) {
-    G.ma_acts_total += h[order[b]];
-    if (b < G.K.C.ma_rows) G.ma_acts_cached += h[order[b]];
+// Level mode, every artis_gpu_upload_cellstate: which (cell, level) pairs get a key record (DevCells::ma_lptr) and
+// the list k_ma_build fills.  Before any transport: whole cells, centre outwards, while the pool lasts.  After:
+// the pairs with the most (sampled) jumps since the last placement -- a threshold on log2 of the count found from
+// the pool lines per count bucket, the pairs of the threshold bucket while the rest of the pool lasts.
+int ma_level_place() {
+  const int64_t npairs = (int64_t)G.K.C.n_nonempty * G.K.T.nlevels_total;
+  const unsigned B = 256, nb = (unsigned)std::min<int64_t>((npairs + B - 1) / B, 1 << 20);
+  HIPCHK(hipMemsetAsync(G.d_lvl_ctr, 0, 4 * sizeof(uint32_t), G.stream));
+  int bt = 33;  // threshold bucket (33: none -- the initial placement)
+  uint64_t rest = 0;
+  if (G.ma_lhist_ready) {
+    HIPCHK(hipMemsetAsync(G.d_lvl_buckets, 0, 34 * sizeof(unsigned long long), G.stream));
+    k_lvl_buckets<<<nb, B, 0, G.stream>>>(G.K, G.d_rec_lines, G.d_lvl_buckets, npairs);
+    unsigned long long h[34];
+    HIPCHK(hipMemcpyAsync(h, G.d_lvl_buckets, sizeof h, hipMemcpyDeviceToHost, G.stream));
+    HIPCHK(hipStreamSynchronize(G.stream));
+    // h[0]: sampled jumps on pairs with a record, h[33]: all, h[1..32]: pool lines wanted per log2 bucket
+    if (h[33] == 0) return 0;  // no walk since the last placement: keep it (its list rebuilds the records)
+    G.ma_acts_cached = (int64_t)h[0];
+    G.ma_acts_total = (int64_t)h[33];
+    uint64_t cum = 0;
+    bt = 0;
+    for (int b = 32; b >= 1; b--) {
+      if (cum + h[b] > G.ma_pool_lines) {
+        bt = b;
+        break;
+      }
+      cum += h[b];
+    }
+    rest = G.ma_pool_lines - cum;
   }
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return h[a] > h[b]; });
-  return ma_place(order);
+  k_lvl_select<<<nb, B, 0, G.stream>>>(G.K, G.d_rec_lines, G.d_rl_off, G.row_lines, G.d_ma_lptr, G.d_lvl_ctr,
+                                       G.d_build_list, G.build_list_cap, npairs, bt,
+                                       (uint32_t)std::min<uint64_t>(rest, 0xffffffffu), G.ma_pool_lines,
+                                       G.ma_lhist_ready ? 1 : 0);
+  uint32_t c[4];
+  HIPCHK(hipMemcpyAsync(c, G.d_lvl_ctr, sizeof c, hipMemcpyDeviceToHost, G.stream));
+  HIPCHK(hipMemsetAsync(G.d_ma_lhist, 0, npairs * sizeof(uint32_t), G.stream));
+  HIPCHK(hipStreamSynchronize(G.stream));
+  G.ma_level_lines = c[0];
+  G.ma_level_records = std::min<int64_t>(c[1], G.build_list_cap);
+  G.ma_initial_placement = !G.ma_lhist_ready;
+  G.ma_lhist_ready = true;  // the transports from now on count
+  return 0;
+}
+
+// the key records of the current level-mode placement (k_ma_build over the placement's list)
+int ma_level_build(int nts) {
+  if (G.ma_level_records > 0)
+    k_ma_build<<<(unsigned)std::min<int64_t>(G.ma_level_records, 1 << 16), 64,
+                 (size_t)std::max<int64_t>(1, G.ma_build_lds_doubles) * 8, G.stream>>>(
+        G.K, G.d_build_list, (uint32_t)G.ma_level_records, nts);
+  HIPCHK(hipGetLastError());
+  return 0;
 }
 
 int64_t sum_i32(const int32_t *a, int n) {
@@ -998,13 +1206,6 @@ int vpkt_collect(const unsigned long long before[8]) {
   return 0;
 }
 
-// activations per cell for the next placement of the key records: hist[cell of bin b] += count of bin b
-__global__ void k_ma_hist(const uint32_t *__restrict__ bins, const int32_t *__restrict__ bincell,
-                          uint32_t *__restrict__ hist, int n) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < n && bins[b]) hist[bincell[b]] += bins[b];
-}
-
 #define WAVE_MAX_ROUNDS 10000000
 int run_wavefront(int64_t n, int nts, double t2) {
   WaveState W = G.W;
@@ -1023,7 +1224,16 @@ int run_wavefront(int64_t n, int nts, double t2) {
   HIPCHK(hipGetLastError());
   int64_t round = 0;
   bool done = false;
+  const bool first_placement = G.ma_initial_placement;
   for (; round < WAVE_MAX_ROUNDS && !done; round++) {
+    // level mode: after the first rounds of a transport on the initial placement (and again a few rounds later),
+    // the records go to the pairs the walks have used so far (the rest of the timestep's walks use them;
+    // placement never changes a result).
+    // Between rounds no ticket holds a record line: k_ma_scatter looks them up again below.
+    if (G.K.C.ma_level_mode && first_placement && (round == 2 || round == 8)) {
+      if (int rc = ma_level_place()) return rc;
+      if (int rc = ma_level_build(nts)) return rc;
+    }
     // waves per SIMD k_rpkt is compiled for (ARTIS_GPU_RPKT_OCC = 1, 2 or 3).  The r-packet step needs ~300
     // registers; at 1 wave/SIMD nothing hides its FP64 latency, and forcing 2 (spilling to scratch) measured
     // 1.80 s -> 1.53 s per bench step on MI355X, so 2 is the default.
@@ -1072,10 +1282,6 @@ int run_wavefront(int64_t n, int nts, double t2) {
       const int nne = G.K.C.n_nonempty;
       HIPCHK(hipMemsetAsync(W.bins, 0, (size_t)(nne + 1) * sizeof(uint32_t), G.stream));
       k_ma_bin<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa);
-      if (G.K.C.have_macache && G.K.C.ma_rows < nne) {
-        k_ma_hist<<<(unsigned)((nne + 255) / 256), 256, 0, G.stream>>>(W.bins, G.d_ma_bincell, G.d_ma_hist, nne);
-        G.ma_hist_ready = true;
-      }
       HIPCHK(hipcub::DeviceScan::ExclusiveSum(G.d_scan_tmp, G.scan_tmp_bytes, W.bins, G.d_binoffs, nne + 1,
                                               G.stream));
       k_ma_scatter<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, G.d_binoffs);
@@ -1092,22 +1298,15 @@ int run_wavefront(int64_t n, int nts, double t2) {
       return (v >= 1 && v <= 8) ? v : 4;
     }();
     const unsigned ma_grid = ma_waves ? (unsigned)(G.wave_grid / 8 * ma_waves) : grid;
-    // a partial key cache: the binned queue's cached-cell walks [0, split) through k_ma<true>, the rest through
-    // k_ma<false>; split = the start of cell ma_rows's bin, which k_ma_scatter's cursor of cell ma_rows - 1 ends on
-    const bool partial = G.K.C.have_macache && G.K.C.ma_rows < G.K.C.n_nonempty;
-    const uint32_t *split = partial ? G.d_binoffs + (G.K.C.ma_rows - 1) : nullptr;
-    if (G.K.C.have_macache) {
-      if (G.ma_occ == 8)
-        k_ma<true, 8><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, split, partial ? 1 : 0);
-      else
-        k_ma<true, 1><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, split, partial ? 1 : 0);
-    }
-    if (partial) HIPCHK(hipMemsetAsync(W.xhead, 0, 8 * sizeof(uint32_t), G.stream));
-    if (!G.K.C.have_macache || partial)
-      k_ma<false, 1><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, split, partial ? 2 : 0);
+    if (G.K.C.ma_level_mode)
+      k_ma<4, true><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+    else if (G.ma_occ == 8)
+      k_ma<8, false><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+    else
+      k_ma<1, false><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
     TEND(1);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QM, 0, 2 * sizeof(uint32_t), G.stream));
-    if (G.K.C.have_macache) {  // jumps the 32-bit keys could not decide (rare), exact; walks go back to M
+    {  // jumps the 32-bit keys could not decide (rare), exact; walks go back to M
       TSTART(3);
       k_ma_exact<<<grid / 4, 64, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
       TEND(3);
@@ -2597,6 +2796,9 @@ int artis_gpu_table_info(int64_t out[ARTIS_TABLE_INFO_COUNT]) {
   out[5] = C.marates ? (int64_t)C.n_nonempty * G.K.T.nlevels_total * ARTIS_MA_ACTION_COUNT * 8 : 0;
   out[6] = G.ma_acts_cached;
   out[7] = G.ma_acts_total;
+  out[8] = C.ma_level_mode ? G.ma_level_records : 0;
+  out[9] = C.ma_level_mode ? G.ma_level_lines * 128 : 0;
+  out[10] = C.ma_level_mode ? (int64_t)G.ma_pool_lines * 128 : 0;
   return 0;
 }
 
@@ -2697,6 +2899,8 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     G.W.refill_ma = rfm ? std::max(1, std::min(64, atoi(rfm))) : 8;
     const char *oc = getenv("ARTIS_GPU_MA_OCC");
     G.ma_occ = (oc && oc[0] == '8') ? 8 : 1;
+    const char *cm = getenv("ARTIS_GPU_MA_COOP_MAX");
+    G.W.coop_max = cm ? std::max(1, std::min(64, atoi(cm))) : 64;
   }
   G.params = *rp;
   G.h_anumber.assign(a->nelements, 0);
@@ -3118,53 +3322,98 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   C.ma_rows = 0;
   C.ma_key = nullptr;
   C.marates = nullptr;
+  C.ma_lptr = nullptr;
+  C.ma_lhist = nullptr;
+  C.ma_level_mode = 0;
   {
+    // Macro-atom key records.  Row mode when every non-empty cell's records fit the budget (default: half of the
+    // free HBM, ARTIS_GPU_MACACHE_MAX_GB; the rest is left for the packet store): cell k's records at row k.
+    // Otherwise level mode: a pool of (cell, level) records within the same budget, less the per-pair action
+    // totals the walks without a record read (k_ma's cooperative jump) and the pointer / activity tables; the
+    // records go to the pairs the walks used most in the previous timestep (ma_level_place).
+    // ARTIS_GPU_MACACHE_ROWS=r (tests) caps the budget at r rows' worth; ARTIS_GPU_NO_MACACHE=1 leaves the pool
+    // empty (every jump cooperative, exact sums).  The split never changes a result.
     size_t freeb = 0, totalb = 0;
     (void)hipMemGetInfo(&freeb, &totalb);
     const double row_bytes = (double)C.ma_key_stride * 2.0;
-    // k_marates scratch (exact double sums of a batch of levels): at least the largest level's, by default
-    // up to 2 GiB (ARTIS_GPU_MAREC_SCRATCH_MB)
     int64_t maxlev = 0;
     for (int ul = 0; ul < nl; ul++) maxlev = std::max(maxlev, G.h_dbl_off[ul + 1] - G.h_dbl_off[ul]);
-    int64_t cap = ((int64_t)2 << 30) / 8;
+    int64_t cap = ((int64_t)2 << 30) / 8;  // k_marates scratch of row mode (ARTIS_GPU_MAREC_SCRATCH_MB)
     if (const char *sm = getenv("ARTIS_GPU_MAREC_SCRATCH_MB")) cap = (int64_t)(atof(sm) * (1 << 20) / 8);
-    auto scratch_for = [&](int64_t rows) {
-      return std::max<int64_t>(maxlev * rows, std::min<int64_t>(G.h_dbl_off[nl] * rows, cap));
-    };
-    // the cache takes at most ARTIS_GPU_MACACHE_MAX_GB (default: half of the free HBM, the rest is left for the
-    // packet store): records for as many cells as fit, centre outwards (ARTIS_GPU_MACACHE_ROWS caps the count);
-    // the walks in the other cells recompute the individual rates (k_ma<false>, identical results).  A partial
-    // cache needs the cell-binned M queue (the cached cells' walks come first in it).
+    const int64_t scratch = std::max<int64_t>(maxlev * nne_cells, std::min<int64_t>(G.h_dbl_off[nl] * nne_cells, cap));
     double budget = 0.5 * (double)freeb;
     if (const char *mx = getenv("ARTIS_GPU_MACACHE_MAX_GB")) budget = atof(mx) * (double)(1ull << 30);
-    int64_t rows = (int64_t)std::max(0., std::floor((budget - 8.0 * (double)scratch_for(nne_cells)) / row_bytes));
-    rows = std::min<int64_t>(rows, nne_cells);
-    if (const char *mr = getenv("ARTIS_GPU_MACACHE_ROWS")) rows = std::min<int64_t>(rows, atoll(mr));
-    // (k_ma addresses the cache by 32-bit 128-byte line indices; every level must fit the record layout)
-    while (rows > 0 && (double)rows * row_bytes / 128.0 >= 4.0e9) rows /= 2;
+    const char *mr = getenv("ARTIS_GPU_MACACHE_ROWS");
+    if (mr) budget = std::min(budget, (double)atoll(mr) * row_bytes);
     const char *env = getenv("ARTIS_GPU_NO_MACACHE");
-    if ((env && env[0] == '1') || !G.ma_cache_ok || (rows < nne_cells && !G.W.ma_binned)) rows = 0;
-    if (rows > 0) {
-      const int64_t scratch = scratch_for(rows);
-      void *mc = nullptr, *sc = nullptr;
-      if (dmalloc(&mc, (size_t)((double)rows * row_bytes)) == hipSuccess) {
-        G.allocs.push_back(mc);
-        if (dmalloc(&sc, (size_t)scratch * 8) == hipSuccess) {
-          G.allocs.push_back(sc);
-          C.ma_key = (uint16_t *)mc;
-          C.have_macache = 1;
-          C.ma_rows = (int32_t)rows;
-          G.d_marec_scratch = (double *)sc;
-          G.marec_scratch_doubles = scratch;
+    const bool none = env && env[0] == '1';
+    const bool rows_fit = !none && G.ma_cache_ok &&
+                          (double)nne_cells * row_bytes + 8.0 * (double)scratch <= budget &&
+                          (double)nne_cells * row_bytes / 128.0 < 4.0e9;
+    void *mc = nullptr, *sc = nullptr;
+    if (rows_fit && dmalloc(&mc, (size_t)((double)nne_cells * row_bytes)) == hipSuccess) {
+      G.allocs.push_back(mc);
+      if (dmalloc(&sc, (size_t)scratch * 8) == hipSuccess) {
+        G.allocs.push_back(sc);
+        C.ma_key = (uint16_t *)mc;
+        C.have_macache = 1;
+        C.ma_rows = nne_cells;
+        G.d_marec_scratch = (double *)sc;
+        G.marec_scratch_doubles = scratch;
+      }
+    }
+    if (!C.ma_rows) {
+      // level mode: per level, its record size in 128-byte lines (0: never a record -- a layout that does not fit,
+      // or more rate terms than k_ma_build stages in LDS)
+      G.h_rec_lines.assign(nl, 0);
+      G.ma_build_lds_doubles = 0;
+      std::vector<MaMeta> mm(nl);
+      HIPCHK(hipMemcpy(mm.data(), G.K.T.ma_meta, nl * sizeof(MaMeta), hipMemcpyDeviceToHost));
+      for (int ul = 0; ul < nl; ul++) {
+        const int64_t next = (ul + 1 < nl) ? mm[ul + 1].rec_off : G.ma_key_stride;
+        const int64_t need = 3 * ((int64_t)mm[ul].nd + mm[ul].nr) + mm[ul].nu + mm[ul].nt;
+        if (ma_layout_ok(mm[ul].nd, mm[ul].nu) && need <= MA_BUILD_MAX_DOUBLES) {
+          G.h_rec_lines[ul] = (uint32_t)((next - mm[ul].rec_off) / 64);
+          G.ma_build_lds_doubles = std::max<int64_t>(G.ma_build_lds_doubles, need);
         }
+      }
+      const double tables = (double)nne_cells * nl * (ARTIS_MA_ACTION_COUNT * 8.0 + 8.0);
+      // (ARTIS_GPU_MACACHE_ROWS: a pool of exactly that many rows' records)
+      const double pool = none ? 128.0 : mr ? std::max(128.0, budget) : std::max(128.0, budget - tables);
+      G.ma_pool_lines = (uint64_t)std::min(pool / 128.0, 4.0e9 - 1.0);
+      if (dmalloc(&mc, (size_t)G.ma_pool_lines * 128) == hipSuccess) {
+        G.allocs.push_back(mc);
+        C.ma_key = (uint16_t *)mc;
+        C.have_macache = 1;
+        C.ma_level_mode = 1;
+        rc |= dalloc(&C.marates, (size_t)nne_cells * nl * ARTIS_MA_ACTION_COUNT);
+        rc |= dalloc(&G.d_ma_lptr, (size_t)nne_cells * nl);
+        rc |= dalloc(&G.d_ma_lhist, (size_t)nne_cells * nl);
+        rc |= dupload(&G.d_rec_lines, G.h_rec_lines.data(), nl);
+        std::vector<uint32_t> rl_off(nl, 0);
+        uint64_t acc = 0;
+        for (int ul = 0; ul < nl; ul++) {
+          rl_off[ul] = (uint32_t)acc;
+          acc += G.h_rec_lines[ul];
+        }
+        G.row_lines = (uint32_t)acc;
+        rc |= dupload(&G.d_rl_off, rl_off.data(), nl);
+        rc |= dalloc(&G.d_lvl_ctr, (size_t)4);
+        rc |= dalloc(&G.d_lvl_buckets, (size_t)34);
+        rc |= dalloc(&G.d_build_list, (size_t)std::max<int64_t>(1, std::min<int64_t>((int64_t)nne_cells * nl,
+                                                                                   (int64_t)G.ma_pool_lines)));
+        G.build_list_cap = std::min<int64_t>((int64_t)nne_cells * nl, (int64_t)G.ma_pool_lines);
+        C.ma_lptr = G.d_ma_lptr;
+        C.ma_lhist = G.d_ma_lhist;
+        G.ma_lhist_ready = false;
+      } else {
+        rc |= ARTIS_ERR_HIP;
       }
     }
   }
-  if (C.ma_rows < nne_cells) rc |= dalloc(&C.marates, (size_t)nne_cells * nl * ARTIS_MA_ACTION_COUNT);
   rc |= dalloc(&G.d_ma_row, (size_t)nne_cells);
   rc |= dalloc(&G.d_ma_bin, (size_t)nne_cells);
   rc |= dalloc(&G.d_ma_bincell, (size_t)nne_cells);
-  rc |= dalloc(&G.d_ma_hist, (size_t)nne_cells);
   C.ma_row = G.d_ma_row;
   C.ma_bin = G.d_ma_bin;
   if (!rc) {
@@ -3377,7 +3626,8 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
   }
   G.K.R.nts = nts;
   HIPCHK(hipStreamSynchronize(G.stream));
-  if (int rc = ma_replace()) return rc;
+  if (G.K.C.ma_level_mode)
+    if (int rc = ma_level_place()) return rc;
   HIPCHK(hipMemsetAsync(G.K.E.err, 0, 4 * sizeof(int32_t), G.stream));
   const int n_ne = G.K.C.n_nonempty;
   const int64_t nl = G.K.T.nlevels_total;
@@ -3405,12 +3655,14 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
                         (unsigned)std::min(G.K.C.linecoef_rows, 32768)), 256, 0,
                     G.stream>>>(G.K);
     const int mr = G.K.C.ma_rows;
-    if (mr < n_ne) {  // the cells without cache records: per-level action totals
-      const int64_t nun = (int64_t)(n_ne - mr) * nl;
-      k_marates<<<(unsigned)((nun + 255) / 256), 256, 0, G.stream>>>(G.K, nts, 0, (int)nl, nullptr,
-                                                                     G.d_ma_bincell + mr, n_ne - mr, false);
-    }
-    if (mr > 0) {
+    if (G.K.C.ma_level_mode) {
+      // level mode: the action totals of every (cell, level) pair (the jumps without a record select from them),
+      // then the records the placement chose
+      const int64_t nun = (int64_t)n_ne * nl;
+      k_marates<<<(unsigned)((nun + 255) / 256), 256, 0, G.stream>>>(G.K, nts, 0, (int)nl, nullptr, G.d_ma_bincell,
+                                                                     n_ne, false);
+      if (int rc = ma_level_build(nts)) return rc;
+    } else if (mr > 0) {
       // batches of levels whose records fit the scratch
       for (int ul0 = 0; ul0 < nl;) {
         int ul1 = ul0 + 1;

@@ -121,6 +121,7 @@ struct MaLayout {
   int hot;       // high-half positions = offset of the low halves
 };
 #define MA_AREA 55
+#define MA_NOLINE 0xffffffffu  // DevCells::ma_lptr: no record for this (cell, level)
 static inline __host__ __device__ MaLayout ma_layout(int nd, int nu, int nr, int nt) {
   MaLayout L;
   if (nd + nu <= MA_AREA) {
@@ -218,14 +219,19 @@ struct DevCells {
   uint16_t *ma_key;    // [n_nonempty * ma_key_stride], or nullptr
   int64_t ma_key_stride;
   int32_t have_macache;  // ma_rows > 0
-  // the cache holds ma_rows records (the HBM budget's share): cell k's is row ma_row[k], -1 for a cell without one,
-  // whose walks take the table-free path over marates.  The rows go to the cells with the most macro-atom
-  // activations of the previous timestep (centre outwards before the first).  ma_bin[k] is cell k's bin in the
-  // binned M queue: the cached cells' bins [0, ma_rows) in row order, the other cells' after them.
+  // row mode: every non-empty cell's records, cell k's at row ma_row[k] (the records of one cell are contiguous,
+  // the level's at MaMeta::rec_off).  ma_bin[k] is cell k's bin in the binned M queue (centre outwards).
   int32_t ma_rows;
   const int32_t *ma_row;  // [n_nonempty]
   const int32_t *ma_bin;  // [n_nonempty]
-  double *marates;     // cells without cache records: [n_nonempty * nlevels_total * 9] totals only (or nullptr)
+  // level mode (the records of every cell do not fit the budget, ma_rows == 0): records per (cell, level) in the
+  // pool ma_key, for the pairs the walks used most in the previous timestep (engine.hip ma_level_place);
+  // ma_lptr[k * nlevels_total + ul] is the first 128-byte line of the record, MA_NOLINE for a pair without one
+  // (k_ma evaluates its rates with the whole wave, ma_coop_select); ma_lhist counts every 16th jump per pair
+  const uint32_t *ma_lptr;  // [n_nonempty * nlevels_total] or nullptr (row mode)
+  uint32_t *ma_lhist;       // [n_nonempty * nlevels_total] or nullptr
+  int32_t ma_level_mode;
+  double *marates;     // level mode: [n_nonempty * nlevels_total * 9] the per-pair action totals (or nullptr)
   // nebular inputs (ABI 6; nullptr when the option is off), model-cell indexed like the arrays above
   const double *nlte_pops;    // [npts_model * total_nlte_levels]
   const float *rf_TR, *rf_W;  // [npts_model * rf_nbins]

@@ -1253,16 +1253,9 @@ DEVFN int first_above(const double *cum, int n, double x, unsigned long long &pr
   }
   return lo;
 }
-// One macro-atom is walked jump by jump (ma_jump) and its deactivation applied to the packet afterwards
+// One macro-atom is walked jump by jump and its deactivation applied to the packet afterwards
 // (ma_finish).  The megakernel calls both back to back (do_macroatom); the wavefront engine runs the walk in a
 // lean kernel that never loads the 304-byte record and defers ma_finish to the kernel the packet moves to.
-struct MaLane {
-  int element, ion, level;
-  int k, mgi;
-  float T_e, nne;
-  unsigned jumps;
-  unsigned long long ntrans;
-};
 enum { MA_CONTINUE = 0, MA_END_BB = 1, MA_END_COLDEEXC = 2, MA_END_COLRECOMB = 3, MA_END_FB = 4, MA_FAILED = -1,
        MA_DEFER = -2, MA_PENDING = -3 };
 // WaveState::pend code of a walk parked between jumps (.y = unique level it stands on): set when a jump of the
@@ -1273,244 +1266,33 @@ struct MaEnd {
                         // FB: a = level of the lower ion, b = unique index of the recombining level
 };
 
-// macroatom.cc:416-482, one pass of the do_macroatom loop without the macro-atom cache: select a process from
-// the per-cell totals, then the transition by recomputing the individual rates in the reference's order
-// (ma_jump_cached below is the cached form)
-DEVFN int ma_jump(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLane &m, double t_mid, MaEnd &end,
-                  int number) {
-  m.jumps++;
-  const int element = m.element, ion = m.ion, level = m.level, k = m.k;
-  const double epsilon_current = epsilon(K, element, ion, level);
-  const int ul = ulev(K, element, ion, level);
-  const double *pr = K.C.marates + ((int64_t)k * K.T.nlevels_total + ul) * ARTIS_MA_ACTION_COUNT;
-  const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
-  double processrates[ARTIS_MA_ACTION_COUNT];
-  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) processrates[a] = pr[a];
-  double total_transitions = 0.;
-  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) total_transitions += processrates[a];
-  int selected_action = ARTIS_MA_ACTION_COUNT;
-  const double zrand = artis_rng_uniform(&rng);
-  const double randomrate = zrand * total_transitions;
-  double rate = 0.;
-  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
-    rate += processrates[a];
-    if (rate > randomrate) {
-      selected_action = a;
-      break;
-    }
-  }
-  if (rate <= randomrate) {
-    fail(K, ERR_MA_RANDOM, number, ul);
-    return MA_FAILED;
-  }
-  const float T_e = m.T_e, nne = m.nne;
-  if (selected_action == ARTIS_MA_ACTION_RADDEEXC) {
-    // macroatom.cc:222-296
-    const double zr = artis_rng_uniform(&rng);
-    int linelistindex = -99;
-    const int ndowntrans = K.T.level_ndowntrans[ul];
-    const int doff = K.T.level_downtrans_offset[ul];
-    {
-      double r = 0.;
-      for (int j = 0; j < ndowntrans; j++) {
-        const int li = K.T.downtrans_lineindex[doff + j];
-        const int lower = K.T.line_lower[li];
-        const double epsilon_trans = epsilon_current - epsilon(K, element, ion, lower);
-        const double R = rad_deexcitation_ratecoeff(K, pops, element, ion, level, lower, epsilon_trans, li, t_mid);
-        r += R * epsilon_trans;
-        m.ntrans++;
-        if (zr * processrates[ARTIS_MA_ACTION_RADDEEXC] < r) {
-          linelistindex = li;
-          break;
-        }
-      }
-    }
-    if (linelistindex < 0) {
-      fail(K, ERR_MA_SELECT, number, 1);
-      return MA_FAILED;
-    }
-    end.code = MA_END_BB;
-    end.ion = ion;
-    end.a = linelistindex;
-    end.b = ul;
-    return MA_END_BB;
-  }
-  if (selected_action == ARTIS_MA_ACTION_COLDEEXC || selected_action == ARTIS_MA_ACTION_COLRECOMB) {
-    end.code = (selected_action == ARTIS_MA_ACTION_COLDEEXC) ? MA_END_COLDEEXC : MA_END_COLRECOMB;
-    end.ion = ion;
-    end.a = end.b = 0;
-    return end.code;
-  }
-  if (selected_action == ARTIS_MA_ACTION_INTERNALDOWNSAME) {
-    // macroatom.cc:174-220
-    const double zr = artis_rng_uniform(&rng);
-    int lower = -99;
-    const int ndowntrans = K.T.level_ndowntrans[ul];
-    const int doff = K.T.level_downtrans_offset[ul];
-    {
-      const double statweight = stat_weight(K, element, ion, level);
-      double r = 0.;
-      for (int j = 0; j < ndowntrans; j++) {
-        const int li = K.T.downtrans_lineindex[doff + j];
-        const int lo = K.T.line_lower[li];
-        const double epsilon_target = epsilon(K, element, ion, lo);
-        const double epsilon_trans = epsilon_current - epsilon_target;
-        const double R = rad_deexcitation_ratecoeff(K, pops, element, ion, level, lo, epsilon_trans, li, t_mid);
-        const double C =
-            col_deexcitation_ratecoeff(K, T_e, nne, epsilon_trans, li, stat_weight(K, element, ion, lo), statweight);
-        r += (R + C) * epsilon_target;
-        m.ntrans++;
-        if (zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNSAME] < r) {
-          lower = lo;
-          break;
-        }
-      }
-    }
-    if (lower < 0) {
-      fail(K, ERR_MA_SELECT, number, 4);
-      return MA_FAILED;
-    }
-    m.level = lower;
-    return MA_CONTINUE;
-  }
-  if (selected_action == ARTIS_MA_ACTION_RADRECOMB) {
-    // macroatom.cc:298-380 (the frequency draw and emission happen in ma_finish)
-    const int upperion = ion;
-    const double zr = artis_rng_uniform(&rng);
-    double r = 0;
-    const int nlevels = get_ionisinglevels(K, element, upperion - 1);
-    int lower = 0;
-    {
-      for (lower = 0; lower < nlevels; lower++) {
-        const double epsilon_trans = epsilon_current - epsilon(K, element, upperion - 1, lower);
-        const double R = rad_recombination_ratecoeff(K, T_e, nne, element, upperion, level, lower);
-        r += R * epsilon_trans;
-        if (zr * processrates[ARTIS_MA_ACTION_RADRECOMB] < r) break;
-      }
-      m.ntrans += lower + 1;
-    }
-    if (zr * processrates[ARTIS_MA_ACTION_RADRECOMB] >= r) {
-      fail(K, ERR_MA_SELECT, number, 2);
-      return MA_FAILED;
-    }
-    end.code = MA_END_FB;
-    end.ion = upperion - 1;
-    end.a = lower;
-    end.b = ul;
-    return MA_END_FB;
-  }
-  if (selected_action == ARTIS_MA_ACTION_INTERNALDOWNLOWER) {
-    lctr(L, CTR_MA_STAT_INTERNALDOWNLOWER);
-    const double zr = artis_rng_uniform(&rng);
-    const int nlevels = get_ionisinglevels(K, element, ion - 1);
-    int lower;
-    {
-      double r = 0.;
-      for (lower = 0; lower < nlevels; lower++) {
-        const double epsilon_target = epsilon(K, element, ion - 1, lower);
-        const double epsilon_trans = epsilon_current - epsilon_target;
-        const double R = rad_recombination_ratecoeff(K, T_e, nne, element, ion, level, lower);
-        const double C = col_recombination_ratecoeff(K, m.mgi, element, ion, level, lower, epsilon_trans);
-        r += (R + C) * epsilon_target;
-        if (zr * processrates[ARTIS_MA_ACTION_INTERNALDOWNLOWER] < r) break;
-      }
-      m.ntrans += lower + 1;
-    }
-    if (lower >= nlevels) {
-      fail(K, ERR_MA_SELECT, number, 5);
-      return MA_FAILED;
-    }
-    m.ion = ion - 1;
-    m.level = lower;
-    return MA_CONTINUE;
-  }
-  if (selected_action == ARTIS_MA_ACTION_INTERNALUPSAME) {
-    const double zr = artis_rng_uniform(&rng);
-    int upper = -99;
-    const int nuptrans = K.T.level_nuptrans[ul];
-    const int uoff = K.T.level_uptrans_offset[ul];
-    {
-      const double statweight = stat_weight(K, element, ion, level);
-      double r = 0.;
-      for (int j = 0; j < nuptrans; j++) {
-        const int li = K.T.uptrans_lineindex[uoff + j];
-        const int up = K.T.line_upper[li];
-        const double epsilon_trans = epsilon(K, element, ion, up) - epsilon_current;
-        const double R = rad_excitation_ratecoeff(K, pops, m.mgi, element, ion, level, up, epsilon_trans, li, t_mid);
-        const double C =
-            col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, element, ion, up));
-        r += (R + C + 0.) * epsilon_current;
-        m.ntrans++;
-        if (zr * processrates[ARTIS_MA_ACTION_INTERNALUPSAME] < r) {
-          upper = up;
-          break;
-        }
-      }
-    }
-    if (upper < 0) {
-      fail(K, ERR_MA_SELECT, number, 6);
-      return MA_FAILED;
-    }
-    m.level = upper;
-    return MA_CONTINUE;
-  }
-  if (selected_action == ARTIS_MA_ACTION_INTERNALUPHIGHER) {
-    // macroatom.cc:382-414
-    lctr(L, CTR_MA_STAT_INTERNALUPHIGHER);
-    int upper = -1;
-    const double zr = artis_rng_uniform(&rng);
-    const int nt = get_nphixstargets(K, element, ion, level);
-    bool found;
-    {
-      double r = 0.;
-      const int slot0 = K.T.level_phixstargets_offset[ul];
-      for (int t = 0; t < nt; t++) {
-        upper = get_phixsupperlevel(K, element, ion, level, t);
-        const double epsilon_trans = get_phixs_threshold(K, element, ion, level, t);
-        const double R = K.C.corrphot[(int64_t)k * K.T.ntargets_total + slot0 + t];
-        const double C = col_ionization_ratecoeff(K, T_e, nne, element, ion, level, t, epsilon_trans);
-        r += (R + C) * epsilon_current;
-        if (zr * processrates[ARTIS_MA_ACTION_INTERNALUPHIGHER] < r) break;
-      }
-      found = zr * processrates[ARTIS_MA_ACTION_INTERNALUPHIGHER] < r;
-    }
-    if (!found) {
-      fail(K, ERR_MA_SELECT, number, 7);
-      return MA_FAILED;
-    }
-    m.ion = ion + 1;
-    m.level = upper;
-    return MA_CONTINUE;
-  }
-  if (selected_action == ARTIS_MA_ACTION_INTERNALUPHIGHERNT) {
-    // macroatom.cc:866-884
-    lctr(L, CTR_MA_STAT_INTERNALUPHIGHERNT);
-    const int upperion = nt_random_upperion(K, rng, m.mgi, element, ion, false);
-    if (upperion < 0) {
-      fail(K, ERR_MA_SELECT, number, 9);
-      return MA_FAILED;
-    }
-    m.ion = upperion;
-    m.level = 0;
-    return MA_CONTINUE;
-  }
-  fail(K, ERR_MA_SELECT, number, 100 + selected_action);
-  return MA_FAILED;
-}
-
-// The cached walk in its lean form: lane state = (unique level, record offset, cell key block).  Per jump: the
-// level's 32-byte MaMeta (L2-resident table) and its compact key record (DevCells::ma_key): the 9 action keys,
-// then a binary search over the keys of the selected action -- for the internal same-ion jumps (most jumps) on
-// the record's first 128-byte line, or via its separators there and one 64-key block line -- and one 8-byte load
-// of the target (level, record offset).  A comparison the 32-bit keys cannot decide sends the jump to
-// ma_jump_exact, which recomputes the reference's exact sums; the selections -- and so the RNG draws and every
-// result -- are those of the uncached ma_jump.
+// The cached walk in its lean form: lane state = (unique level, cell, record line).  Per jump: the level's
+// 32-byte MaMeta (L2-resident table) and its compact key record (DevCells::ma_key): the 9 action keys, then a
+// binary search over the keys of the selected action -- for the internal same-ion jumps (most jumps) on the
+// record's first 128-byte line, or via its separators there and one 64-key block line -- and one 8-byte load of
+// the target (level, record offset).  A comparison the 32-bit keys cannot decide sends the jump to ma_jump_exact,
+// which recomputes the reference's exact sums; the selections -- and so the RNG draws and every result -- are the
+// reference's linear scans over its running sums (macroatom.cc:502-525 and the do_macroatom_* searches).
 struct MaLaneC {
-  int ul, rec_off, k;
-  const uint16_t *block;  // K.C.ma_key + k * ma_key_stride
+  int ul, k;
+  uint32_t line;    // first 128-byte line of the current level's record in DevCells::ma_key (MA_NOLINE: none)
+  int32_t rowline;  // row mode: the first line of the cell's row; -1: level mode (DevCells::ma_lptr)
   unsigned jumps;
   unsigned long long ntrans;
 };
+// the record line of level ul (MaMeta::rec_off rec_off) in the walk's cell
+DEVFN uint32_t ma_line(const Ctx &K, int32_t rowline, int k, int ul, int rec_off) {
+  if (rowline >= 0) return (uint32_t)rowline + ((uint32_t)rec_off >> 6);
+  return K.C.ma_lptr ? K.C.ma_lptr[(int64_t)k * K.T.nlevels_total + ul] : MA_NOLINE;
+}
+DEVFN int32_t ma_rowline(const Ctx &K, int k) {
+  const int row = K.C.ma_row[k];
+  return row >= 0 ? (int32_t)(((int64_t)row * K.C.ma_key_stride) >> 6) : -1;
+}
+DEVFN void ma_set_level(const Ctx &K, MaLaneC &m, int ul) {
+  m.ul = ul;
+  m.line = ma_line(K, m.rowline, m.k, ul, K.T.ma_meta[ul].rec_off);
+}
 
 // the outcome of selecting transition j (reference list order) of action sel at level ul: MA_CONTINUE with the
 // lane moved to the target level, or a deactivation in `end` (macroatom.cc:174-414)
@@ -1519,12 +1301,10 @@ DEVFN int ma_apply_selection(const Ctx &K, const LocalCounters &L, MaLaneC &m, M
   const int ul = m.ul;
   switch (sel) {
     case ARTIS_MA_ACTION_INTERNALDOWNSAME:
-      m.ul = K.T.ion_uniqueleveloffset[K.T.level_ui[ul]] + K.T.line_lower[K.T.downtrans_lineindex[doff + j]];
-      m.rec_off = K.T.ma_meta[m.ul].rec_off;
+      ma_set_level(K, m, K.T.ion_uniqueleveloffset[K.T.level_ui[ul]] + K.T.line_lower[K.T.downtrans_lineindex[doff + j]]);
       return MA_CONTINUE;
     case ARTIS_MA_ACTION_INTERNALUPSAME:
-      m.ul = K.T.ion_uniqueleveloffset[K.T.level_ui[ul]] + K.T.line_upper[K.T.uptrans_lineindex[uoff + j]];
-      m.rec_off = K.T.ma_meta[m.ul].rec_off;
+      ma_set_level(K, m, K.T.ion_uniqueleveloffset[K.T.level_ui[ul]] + K.T.line_upper[K.T.uptrans_lineindex[uoff + j]]);
       return MA_CONTINUE;
     case ARTIS_MA_ACTION_RADDEEXC:
       // the line index is looked up by ma_finish (end.a = -1 - downtrans slot): a load here would hold the whole
@@ -1542,14 +1322,12 @@ DEVFN int ma_apply_selection(const Ctx &K, const LocalCounters &L, MaLaneC &m, M
       return MA_END_FB;
     case ARTIS_MA_ACTION_INTERNALDOWNLOWER:
       lctr(L, CTR_MA_STAT_INTERNALDOWNLOWER);
-      m.ul = base_lower + j;
-      m.rec_off = K.T.ma_meta[m.ul].rec_off;
+      ma_set_level(K, m, base_lower + j);
       return MA_CONTINUE;
     default: {  // INTERNALUPHIGHER (macroatom.cc:382-414)
       lctr(L, CTR_MA_STAT_INTERNALUPHIGHER);
       const int ui = K.T.level_ui[ul];
-      m.ul = K.T.ion_uniqueleveloffset[ui + 1] + K.T.phixstarget_levelindex[K.T.level_phixstargets_offset[ul] + j];
-      m.rec_off = K.T.ma_meta[m.ul].rec_off;
+      ma_set_level(K, m, K.T.ion_uniqueleveloffset[ui + 1] + K.T.phixstarget_levelindex[K.T.level_phixstargets_offset[ul] + j]);
       return MA_CONTINUE;
     }
   }
@@ -1566,8 +1344,7 @@ DEVFN int ma_apply_nt(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLa
     fail(K, ERR_MA_SELECT, number, 9);
     return MA_FAILED;
   }
-  m.ul = K.T.ion_uniqueleveloffset[ui + upperion - ion];
-  m.rec_off = K.T.ma_meta[m.ul].rec_off;
+  ma_set_level(K, m, K.T.ion_uniqueleveloffset[ui + upperion - ion]);
   return MA_CONTINUE;
 }
 
@@ -1744,6 +1521,160 @@ struct MaLaneR : MaLaneC {
   uint32_t q2h;
 };
 
+// ---- the jump of a walk whose (cell, level) has no key record (level mode), made by the whole wave ------------
+DEVFN double readlane_d(double v, int l) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+#define MA_COOP_RANDOM (-1)  // the action draw exceeds the total (the reference's abort, ERR_MA_RANDOM)
+#define MA_COOP_NOSEL (-2)   // no entry of the action's list exceeds the transition draw (ERR_MA_SELECT)
+// Wave-uniform: every lane of the wave calls it with the same (k, ul, z1, z2) and gets the same result.  The action
+// from the pair's exact totals (DevCells::marates, the sums of ma_foreach_rate in the reference's order,
+// macroatom.cc:502-525); for a transition action, the list entry: the lanes evaluate 64 individual rates at a time
+// (ma_rate_at: the expressions the totals were summed from) and the running sum is added in list order, one term
+// per step, read from the evaluating lane's register (v_readlane) -- the reference's linear scan
+// (do_macroatom_raddeexcitation etc.), the same double sums as ma_jump_exact.  Returns the action, *j the entry.
+// (out of line: inlined into k_ma, its rate expressions would raise the register allocation of the whole walk)
+#ifdef ARTIS_MA_COOP_INLINE
+DEVFN
+#else
+DEVNI
+#endif
+int ma_coop_select(const Ctx &K, int k, int ul, double z1, double z2, double t_mid, int *j, unsigned &probes) {
+  const int64_t nl = K.T.nlevels_total;
+  const double *tot = K.C.marates + ((int64_t)k * nl + ul) * ARTIS_MA_ACTION_COUNT;
+  double pr[ARTIS_MA_ACTION_COUNT];
+  double total = 0.;
+  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
+    pr[a] = tot[a];
+    total += pr[a];
+  }
+  const double randomrate = z1 * total;
+  double rate = 0.;
+  int sel = -1;
+  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
+    rate += pr[a];
+    if (rate > randomrate) {
+      sel = a;
+      break;
+    }
+  }
+  if (sel < 0) return MA_COOP_RANDOM;
+  if (sel == ARTIS_MA_ACTION_COLDEEXC || sel == ARTIS_MA_ACTION_COLRECOMB || sel == ARTIS_MA_ACTION_INTERNALUPHIGHERNT)
+    return sel;
+  const MaMeta mm = K.T.ma_meta[ul];
+  int base, cnt;
+  if (sel == ARTIS_MA_ACTION_RADDEEXC || sel == ARTIS_MA_ACTION_INTERNALDOWNSAME) {
+    base = 0;
+    cnt = mm.nd;
+  } else if (sel == ARTIS_MA_ACTION_RADRECOMB || sel == ARTIS_MA_ACTION_INTERNALDOWNLOWER) {
+    base = mm.nd;
+    cnt = mm.nr;
+  } else if (sel == ARTIS_MA_ACTION_INTERNALUPSAME) {
+    base = mm.nd + mm.nr;
+    cnt = mm.nu;
+  } else {  // INTERNALUPHIGHER
+    base = mm.nd + mm.nr + mm.nu;
+    cnt = mm.nt;
+  }
+  const double x = z2 * pr[sel];
+  const int mgi = K.C.ne_mgi[k];
+  const double ec = K.T.level_epsilon[ul];
+  const double *pops = K.C.pops + (int64_t)k * nl;
+  const double *corr = K.C.corrphot + (int64_t)k * K.T.ntargets_total;
+  auto pop = [&](int u) { return pops[u]; };
+  auto cph = [&](int s) { return corr[s]; };
+  const int lane = (int)__lane_id();
+  auto term_at = [&](int c0) {  // this lane's term of entries [c0, c0 + 64), 0 past the list
+    double term = 0.;
+    if (c0 + lane < cnt) {
+      const MaItem it = ma_rate_at(K, mgi, ul, t_mid, base + c0 + lane, pop, cph);
+      switch (sel) {  // the summand of ma_accumulate for this action
+        case ARTIS_MA_ACTION_RADDEEXC:
+        case ARTIS_MA_ACTION_RADRECOMB: term = it.R * it.et; break;
+        case ARTIS_MA_ACTION_INTERNALDOWNSAME:
+        case ARTIS_MA_ACTION_INTERNALDOWNLOWER: term = (it.R + it.C) * it.eg; break;
+        case ARTIS_MA_ACTION_INTERNALUPSAME: term = (it.R + it.C + 0.) * ec; break;
+        default: term = (it.R + it.C) * ec; break;
+      }
+    }
+    return term;
+  };
+  // Fast path: a wave prefix sum (six shuffle steps, its own rounding) finds the first entry whose running sum
+  // exceeds x.  All terms are >= 0, so the reference's sequential sums and the prefix sums both lie within
+  // (c0 + 70) u of the exact sums relative to the largest partial sum; when x is farther than twice that from
+  // the two sums around the crossing, the sequential scan crosses at the same entry.  Otherwise (or when no sum
+  // crosses), the exact path below adds the terms one at a time in list order.
+  double base_sum = 0.;
+  for (int c0 = 0; c0 < cnt; c0 += 64) {
+    double incl = term_at(c0);
+    for (int off = 1; off < 64; off <<= 1) {
+      const double t = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += t;
+    }
+    incl += base_sum;
+    const unsigned long long cross = __ballot(c0 + lane < cnt && incl > x);
+    if (cross) {
+      const int f = __ffsll((long long)cross) - 1;
+      const double s_f = readlane_d(incl, f);
+      const double s_prev = f > 0 ? readlane_d(incl, f - 1) : base_sum;
+      const double tol = 2.0 * (double)(c0 + 70) * 1.1102230246251565e-16 * s_f;
+      if (s_f - x > tol && x - s_prev > tol) {
+        probes += (unsigned)(c0 + f + 1);
+        *j = c0 + f;
+        return sel;
+      }
+      break;
+    }
+    base_sum = readlane_d(incl, min(63, cnt - c0 - 1));
+  }
+  // exact path: the reference's sequential running sum, one term per step from the evaluating lane's register
+  double run = 0.;
+  for (int c0 = 0; c0 < cnt; c0 += 64) {
+    const double term = term_at(c0);
+    const int n64 = min(64, cnt - c0);
+#pragma unroll 1
+    for (int q = 0; q < n64; q++) {
+      run += readlane_d(term, q);
+      if (run > x) {
+        probes += (unsigned)(c0 + q + 1);
+        *j = c0 + q;
+        return sel;
+      }
+    }
+  }
+  probes += (unsigned)cnt;
+  return MA_COOP_NOSEL;
+}
+// the lane's side of that jump: its RNG draws (the action draw, then the transition's or the NT ion's), the jump
+// count and histogram, and the selection applied as in the cached step
+DEVFN int ma_coop_apply(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneR &m, MaEnd &end, int number,
+                        int sel, int j, unsigned probes, const MaMetaW &meta) {
+  m.n0 = rng.n;
+  rng.n++;
+  m.ntrans += probes;
+  if (sel == MA_COOP_RANDOM) {
+    fail(K, ERR_MA_RANDOM, number, m.ul);
+    return MA_FAILED;
+  }
+  if (sel == MA_COOP_NOSEL) {
+    fail(K, ERR_MA_SELECT, number, 20);
+    return MA_FAILED;
+  }
+  m.jumps++;
+  if (K.C.ma_lhist) atomicAdd(&K.C.ma_lhist[(int64_t)m.k * K.T.nlevels_total + m.ul], 1u);
+  if (sel == ARTIS_MA_ACTION_COLDEEXC || sel == ARTIS_MA_ACTION_COLRECOMB) {
+    end.code = (sel == ARTIS_MA_ACTION_COLDEEXC) ? MA_END_COLDEEXC : MA_END_COLRECOMB;
+    end.ion = end.a = end.b = 0;
+    return end.code;
+  }
+  if (sel == ARTIS_MA_ACTION_INTERNALUPHIGHERNT) return ma_apply_nt(K, L, rng, m, number);
+  rng.n++;
+  return ma_apply_selection(K, L, m, end, sel, j, meta.w0.y, meta.w0.z, meta.w0.w);
+}
+
 // where a step reads record keys (high halves): k_ma's staged line, or the whole record in global memory
 struct KeysLds {
   lds_uint4 *line;
@@ -1782,7 +1713,7 @@ DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
   do {               \
   } while (0)
 #endif
-  const uint16_t *rec = m.block + m.rec_off;
+  const uint16_t *rec = K.C.ma_key + (size_t)m.line * 64;
   const int doff = meta.w0.y, uoff = meta.w0.z, base_lower = meta.w0.w;
   const int nd = meta.w1.x, nu = meta.w1.y, nr = meta.w1.z, nt = meta.w1.w;
   const MaLayout lay = ma_layout(nd, nu, nr, nt);
@@ -1819,6 +1750,8 @@ DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
     }
     if (sel < 0) return MA_DEFER;
     m.jumps++;
+    // level mode: every 16th jump of a walk credits its (cell, level) pair for the next record placement
+    if (K.C.ma_lhist && (m.jumps & 15u) == 0u) atomicAdd(&K.C.ma_lhist[(int64_t)m.k * K.T.nlevels_total + m.ul], 16u);
     if (sel == ARTIS_MA_ACTION_COLDEEXC || sel == ARTIS_MA_ACTION_COLRECOMB) {
       end.code = (sel == ARTIS_MA_ACTION_COLDEEXC) ? MA_END_COLDEEXC : MA_END_COLRECOMB;
       end.ion = end.a = end.b = 0;
@@ -1918,7 +1851,7 @@ DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
     typedef const __attribute__((address_space(1))) uint64_t glb_u64;
     const uint64_t tw = *(glb_u64 *)(down ? K.T.down_target + doff + j : K.T.up_target + uoff + j);
     m.ul = (int)(uint32_t)tw;
-    m.rec_off = (int)(uint32_t)(tw >> 32);
+    m.line = ma_line(K, m.rowline, m.k, m.ul, (int)(uint32_t)(tw >> 32));
     return MA_CONTINUE;
   }
   const bool found = lo < m.end;
@@ -1942,7 +1875,7 @@ DEVFN int ma_jump_cached_global(const Ctx &K, const LocalCounters &L, artis_rng 
   m.sel = -1;
   m.pline = 0;
   const MaMetaW meta = ma_meta_load(K, m.ul);
-  const KeysGlobal keys{m.block + m.rec_off};
+  const KeysGlobal keys{K.C.ma_key + (size_t)m.line * 64};
   int r;
   do {
     r = ma_step_cached(K, L, rng, m, end, number, keys, meta, z1, z2);
@@ -1952,17 +1885,6 @@ DEVFN int ma_jump_cached_global(const Ctx &K, const LocalCounters &L, artis_rng 
   return r;
 }
 
-DEVFN void ma_lane_init(const Ctx &K, MaLane &m, int where, int element, int ion, int level) {
-  m.mgi = cell_mgi(K, where);
-  m.k = K.C.ne_index[m.mgi];
-  m.T_e = K.C.Te[m.mgi];
-  m.nne = K.C.nne[m.mgi];
-  m.element = element;
-  m.ion = ion;
-  m.level = level;
-  m.jumps = 0;
-  m.ntrans = 0;
-}
 
 // the deactivation branches of do_macroatom (macroatom.cc:222-380, 445-462) and its trailer (macroatom.cc:475-482);
 // `jumps` passes of the loop each added one interaction
@@ -2046,31 +1968,24 @@ DEVNI void do_macroatom(Tx &x, Pkt &p) {
   int r;
   unsigned jumps;
   unsigned long long ntrans;
-  if (K.C.ma_row[K.C.ne_index[mgi]] >= 0) {
+  {
+    // the walk over the key records where the cell has them (row mode, or a (cell, level) record of level mode);
+    // a jump without a record or with an undecided key comparison is made with the exact sums (ma_jump_exact)
     MaLaneC m;
-    m.ul = ulev(K, p.ma_element, p.ma_ion, p.ma_level);
-    m.rec_off = K.T.ma_meta[m.ul].rec_off;
     m.k = K.C.ne_index[mgi];
-    m.block = K.C.ma_key + (int64_t)K.C.ma_row[m.k] * K.C.ma_key_stride;
+    m.rowline = ma_rowline(K, m.k);
+    ma_set_level(K, m, ulev(K, p.ma_element, p.ma_ion, p.ma_level));
     m.jumps = 0;
     m.ntrans = 0;
     const double t_mid = K.G.ts_mid[x.nts];
     while (true) {
       const uint32_t n0 = x.rng.n;
-      r = ma_jump_cached_global(K, x.L, x.rng, m, e, p.number);
+      r = (m.line == MA_NOLINE) ? MA_DEFER : ma_jump_cached_global(K, x.L, x.rng, m, e, p.number);
       if (r == MA_DEFER) {
         x.rng.n = n0;
         r = ma_jump_exact(K, x.L, x.rng, m, e, p.number, t_mid);
       }
       if (r != MA_CONTINUE || m.jumps >= MA_MAX_JUMPS) break;
-    }
-    jumps = m.jumps;
-    ntrans = m.ntrans;
-  } else {
-    MaLane m;
-    ma_lane_init(K, m, p.where, p.ma_element, p.ma_ion, p.ma_level);
-    const double t_mid = K.G.ts_mid[x.nts];
-    while ((r = ma_jump(K, x.L, x.rng, m, t_mid, e, p.number)) == MA_CONTINUE && m.jumps < MA_MAX_JUMPS) {
     }
     jumps = m.jumps;
     ntrans = m.ntrans;

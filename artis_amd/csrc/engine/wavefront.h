@@ -41,6 +41,8 @@ struct WaveState {
   int r_binned;        // 1: this k_rpkt launch reads the R queue binned by cell from ma_sorted (k_r_bin / k_r_scatter)
   int refill_min;      // a wave refetches work (and flushes its queue appends) once this many lanes are idle
   int refill_ma;       // the same for k_ma (a macro-atom refill is cheap: one coalesced ticket read)
+  int coop_max;        // level mode: at most this many cooperative jumps per k_ma pass (the other lanes without a
+                       // record wait for a later pass; ARTIS_GPU_MA_COOP_MAX, default 64 = all)
   // cell-sorted macro-atom tickets written by k_ma_scatter when the key cache is on (else nullptr): per slot
   // {packet index, unique level, record offset, nonempty cell}, {packet number, RNG counter, jumps so far, 0}
   int4 *ma_tick;       // [2N]
@@ -346,9 +348,9 @@ __global__ void k_ma_bin(const Ctx *__restrict__ ctxp, WaveState W, const uint64
     atomicAdd(&W.bins[b], 1u);
   }
 }
-// scatter into cell order using the exclusive prefix sum of the counts.  With the key cache, each slot becomes a
-// ticket holding everything k_ma's refill needs (the walk's level, record, cell, RNG stream and jump count), so a
-// k_ma lane starts a walk with one coalesced read instead of a chain of dependent packet and table loads.
+// scatter into cell order using the exclusive prefix sum of the counts.  Each slot becomes a ticket holding
+// everything k_ma's refill needs (the walk's level, record line, cell, RNG stream and jump count), so a k_ma lane
+// starts a walk with one coalesced read instead of a chain of dependent packet and table loads.
 __global__ void k_ma_scatter(const Ctx *__restrict__ ctxp, WaveState W, const uint64_t *__restrict__ soa, int64_t n,
                              uint32_t *offs) {
   CTX_IN_LDS(ctxp)
@@ -356,8 +358,7 @@ __global__ void k_ma_scatter(const Ctx *__restrict__ ctxp, WaveState W, const ui
   for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x) {
     const int32_t idx = W.q[QM][slot];
     const uint32_t pos = atomicAdd(&offs[W.ma_key[slot]], 1u);
-    const int bin = W.ma_key[slot];
-    if (!W.ma_tick || bin >= K.C.ma_rows) {  // (no tickets for the walks of uncached cells)
+    if (!W.ma_tick) {
       W.ma_sorted[pos] = idx;
       continue;
     }
@@ -381,20 +382,24 @@ __global__ void k_ma_scatter(const Ctx *__restrict__ ctxp, WaveState W, const ui
       fail(K, ERR_THICK_MA, number, mgi);
       tidx = -1;
     }
-    W.ma_tick[2 * (int64_t)pos] = make_int4(tidx, ul, K.T.ma_meta[ul].rec_off, K.C.ne_index[mgi]);
-    W.ma_tick[2 * (int64_t)pos + 1] = make_int4(number, (int)W.rng_n[idx], (int)jumps, bin);  // bin == key row
+    const int k = K.C.ne_index[mgi];
+    const int32_t rowline = ma_rowline(K, k);
+    W.ma_tick[2 * (int64_t)pos] = make_int4(tidx, ul, (int)ma_line(K, rowline, k, ul, K.T.ma_meta[ul].rec_off), k);
+    W.ma_tick[2 * (int64_t)pos + 1] = make_int4(number, (int)W.rng_n[idx], (int)jumps, rowline);
   }
 }
 
-// macro-atoms: persistent lanes, one jump per loop pass, lane state = MaLane + RNG counter.
+// macro-atoms: persistent lanes, one jump per loop pass, lane state = MaLaneR + RNG counter.
 // The (binned) queue is cut into W.ma_ranges contiguous ranges; blocks start on range blockIdx % 8 -- the
 // XCD the block was dispatched to under round-robin placement, so one XCD's L2 sees a contiguous run of
 // cells -- and steal from the following ranges once theirs is exhausted.
-// part 0: the whole queue; with a partial key cache (DevCells::ma_rows) the binned queue holds the cached cells'
-// walks first: part 1 = [0, *split) (CACHE), part 2 = [*split, nq) (!CACHE).
-template <bool CACHE, int MINW>
-__global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__ ctxp, WaveState W, const uint64_t *__restrict__ soa,
-                                                         int64_t n, int nts, const uint32_t *split, int part) {
+// A lane whose (cell, level) has a key record takes the cached step (ma_step_cached, its record line staged in
+// LDS by the wave's cooperative fetch); a lane without one (level mode, DevCells::ma_lptr) has its jump made by
+// the whole wave after the cached steps (ma_coop_select), one such lane after another.
+// COOP = false (row mode: every pair has a record) compiles without the cooperative jump.
+template <int MINW, bool COOP>
+__global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__ ctxp, WaveState W,
+                                                         const uint64_t *__restrict__ soa, int64_t n, int nts) {
   CTX_IN_LDS(ctxp)
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
@@ -405,16 +410,14 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   LocalCounters L;
   L.ctr = &s_ctr[0];
   L.work = &s_work[0];
-  lds_uint4 *line = CACHE ? (lds_uint4 *)&s_line[threadIdx.x >> 6][threadIdx.x & 63] : nullptr;
-  const uint32_t nq_all = W.ctr[2 * QM];
-  const uint32_t q0 = (part == 2) ? min(*split, nq_all) : 0u;
-  const uint32_t nq = ((part == 1) ? min(*split, nq_all) : nq_all) - q0;
+  lds_uint4 *line = (lds_uint4 *)&s_line[threadIdx.x >> 6][threadIdx.x & 63];
+  const uint32_t nq = W.ctr[2 * QM];
   const int32_t *queue = W.ma_binned ? W.ma_sorted : W.q[QM];
   const int nr = W.ma_ranges;
   const int nr_log2 = (nr == 8) ? 3 : 0;  // W.ma_ranges is 1 or 8
   const double t_mid = K.G.ts_mid[nts];
-  MaLane m;    // uncached walk
-  MaLaneR mc;  // cached walk (resumable steps)
+  [[maybe_unused]] const int lane = lane_id();
+  MaLaneR mc;
   artis_rng rng = artis_rng_init(K.R.seed, 0, nts, K.R.rank);
   int32_t idx = -1;
   bool have = false, drained = false;
@@ -433,7 +436,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   while (true) {
     const bool idle = !have && !drained;
     const unsigned long long imask = __ballot(idle);
-    if (!__any(have) || __popcll(imask) >= (CACHE ? W.refill_ma : W.refill_min)) {
+    if (!__any(have) || __popcll(imask) >= W.refill_ma) {
       st_refill++;
       const unsigned long long tr0 = wave_clock();
       wave_push(W, QR, pendR, idx);
@@ -442,20 +445,20 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
       pendR = pendK = pendX = false;
       if (imask) {
         // (nr is 1 or 8: shifts, not the 64-bit division the compiler would expand into ~120 scalar instructions)
-        const uint32_t lo = q0 + (uint32_t)(((uint64_t)nq * cur) >> nr_log2),
-                       hi = q0 + (uint32_t)(((uint64_t)nq * (cur + 1)) >> nr_log2);
+        const uint32_t lo = (uint32_t)(((uint64_t)nq * cur) >> nr_log2),
+                       hi = (uint32_t)(((uint64_t)nq * (cur + 1)) >> nr_log2);
         const uint32_t slot = wave_reserve(&W.xhead[cur], idle);
         const bool got = idle && lo + slot < hi;
-        if (got && CACHE && W.ma_tick) {
+        if (got && W.ma_tick) {
           const int4 t0 = W.ma_tick[2 * (int64_t)(lo + slot)], t1 = W.ma_tick[2 * (int64_t)(lo + slot) + 1];
           idx = t0.x;
           mc.ul = t0.y;
-          mc.rec_off = t0.z;
+          mc.line = (uint32_t)t0.z;
           mc.k = t0.w;
           rng.key1 = (uint32_t)t1.x;
           rng.n = (uint32_t)t1.y;
           mc.jumps = (unsigned)t1.z;
-          mc.block = K.C.ma_key + (int64_t)t1.w * K.C.ma_key_stride;
+          mc.rowline = t1.w;
           mc.ntrans = 0;
           mc.sel = -1;
           mc.pline = 0;
@@ -468,25 +471,20 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
           rng.key1 = (uint32_t)hi32(soa[PW(n, idx, 33)]);  // packet number
           rng.n = W.rng_n[idx];
           const int mgi = cell_mgi(K, where);
-          if constexpr (CACHE) {
-            const int4 pd = W.pend[idx];
-            if (pd.x == MA_RESUME) {  // a walk parked by k_ma_exact: continue from its level and jump count
-              mc.ul = pd.y;
-              mc.jumps = W.pend_jumps[idx];
-              W.pend[idx].x = 0;
-            } else {
-              mc.ul = ulev(K, lo32(w36), hi32(w36), lo32(w37));
-              mc.jumps = 0;
-            }
-            mc.rec_off = K.T.ma_meta[mc.ul].rec_off;
-            mc.k = K.C.ne_index[mgi];
-            mc.block = K.C.ma_key + (int64_t)K.C.ma_row[mc.k] * K.C.ma_key_stride;
-            mc.ntrans = 0;
-            mc.sel = -1;
-            mc.pline = 0;
+          const int4 pd = W.pend[idx];
+          mc.k = K.C.ne_index[mgi];
+          mc.rowline = ma_rowline(K, mc.k);
+          if (pd.x == MA_RESUME) {  // a walk parked by k_ma_exact: continue from its level and jump count
+            ma_set_level(K, mc, pd.y);
+            mc.jumps = W.pend_jumps[idx];
+            W.pend[idx].x = 0;
           } else {
-            ma_lane_init(K, m, where, lo32(w36), hi32(w36), lo32(w37));
+            ma_set_level(K, mc, ulev(K, lo32(w36), hi32(w36), lo32(w37)));
+            mc.jumps = 0;
           }
+          mc.ntrans = 0;
+          mc.sel = -1;
+          mc.pline = 0;
           have = true;
           if (K.C.thick[mgi] == 1) {
             fail(K, ERR_THICK_MA, (int)rng.key1, mgi);
@@ -507,25 +505,17 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     st_pass++;
     st_busy += __popcll(__ballot(have));
     const unsigned long long ts0 = wave_clock();
+    // a lane whose current level has no record: its jump is made by the whole wave below
+    const bool unc = COOP && have && mc.line == MA_NOLINE;
     MaMetaW meta;
     double z1 = 0., z2 = 0.;
-    if constexpr (CACHE) {
+    {
       // the level's metadata and, 8 lines per load instruction, every busy lane's record line; the lane's next two
       // draws are computed while they are in flight
-#ifdef ARTIS_MA_RNG_EARLY  // A/B: the draws before the loads are issued
-      if (have && mc.sel < 0) {
-        artis_rng r2 = rng;
-        z1 = artis_rng_uniform(&r2);
-        z2 = artis_rng_uniform(&r2);
-      }
-#endif
       if (have) meta = ma_meta_load(K, mc.ul);
-      const uint32_t myline =
-          have ? (uint32_t)(((uint64_t)(mc.block - K.C.ma_key) + (uint64_t)mc.rec_off) >> 6) + (uint32_t)mc.pline
-               : 0xffffffffu;
+      const uint32_t myline = (have && !unc) ? mc.line + (uint32_t)mc.pline : 0xffffffffu;
       WaveLines wl;
       wave_fetch_issue(K.C.ma_key, myline, wl, (lds_u32 *)&s_xidx[threadIdx.x >> 6][0]);
-#ifndef ARTIS_MA_RNG_EARLY
       if (have && mc.sel < 0) {
 #ifdef ARTIS_DIAG_CHEAPRNG  // timing diagnostic only (wrong stream): the walk's cost without Philox
         uint64_t h = ((uint64_t)rng.key1 << 32) ^ rng.n;
@@ -533,43 +523,50 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
         h = (h ^ (h >> 27)) * 0x94d049bb133111ebull;
         z1 = (double)(h >> 11) * (1.0 / 9007199254740992.0);
         z2 = (double)((h * 0x9E3779B97F4A7C15ull) >> 11) * (1.0 / 9007199254740992.0);
-#elif defined(ARTIS_RNG_PAIRED)  // A/B: a jump's two draws from one Philox block (its counter aligned to even)
-        rng.n = (rng.n + 1u) & ~1u;
-        artis_rng_pair_aligned(&rng, &z1, &z2);
 #else
         artis_rng r2 = rng;
         z1 = artis_rng_uniform(&r2);
         z2 = artis_rng_uniform(&r2);
 #endif
       }
-#endif
       wave_fetch_commit(wl, line - (threadIdx.x & 63));
     }
 #ifdef ARTIS_STAMPS
     const unsigned long long ts1 = wave_clock();
     unsigned long long ts2 = ts1;
 #endif
-    if (have) {
-      MaEnd e;
-      int r;
-      unsigned jumps;
-      if constexpr (CACHE) {
-        r = ma_step_cached(K, L, rng, mc, e, (int)rng.key1, KeysLds{line, mc.pline}, meta, z1, z2);
+    MaEnd e;
+    int r = MA_PENDING;
+    if (have && !unc) {
+      r = ma_step_cached(K, L, rng, mc, e, (int)rng.key1, KeysLds{line, mc.pline}, meta, z1, z2);
 #ifdef ARTIS_STAMPS
-        ts2 = wave_clock();
+      ts2 = wave_clock();
 #endif
-        jumps = mc.jumps;
-        if (r == MA_DEFER) {  // park the walk before this jump; k_ma_exact makes it with the exact sums
-          W.pend[idx] = make_int4(MA_RESUME, mc.ul, 0, 0);
-          W.pend_jumps[idx] = jumps;
-          W.rng_n[idx] = mc.n0;
-          trans_sum += mc.ntrans;
-          pendX = true;
-          have = false;
-        }
-      } else {
-        r = ma_jump(K, L, rng, m, t_mid, e, (int)rng.key1);
-        jumps = m.jumps;
+    }
+    // level mode: the jumps of the lanes without a record, each made by the whole wave (wave-uniform loop)
+    if constexpr (COOP) {
+      // (a rotating start, so that with coop_max < 64 every waiting lane gets its turn)
+      unsigned long long um = __ballot(unc);
+      const int rot = (int)(st_pass & 63);
+      um = (um >> rot) | (rot ? um << (64 - rot) : 0ull);
+      for (int done_coop = 0; um && done_coop < W.coop_max; um &= um - 1, done_coop++) {
+        const int ld = (__ffsll((long long)um) - 1 + rot) & 63;
+        const int ul = __builtin_amdgcn_readlane(mc.ul, ld), k = __builtin_amdgcn_readlane(mc.k, ld);
+        int j = -1;
+        unsigned probes = 0;
+        const int sel = ma_coop_select(K, k, ul, readlane_d(z1, ld), readlane_d(z2, ld), t_mid, &j, probes);
+        if (lane == ld) r = ma_coop_apply(K, L, rng, mc, e, (int)rng.key1, sel, j, probes, meta);
+      }
+    }
+    if (have) {
+      const unsigned jumps = mc.jumps;
+      if (r == MA_DEFER) {  // park the walk before this jump; k_ma_exact makes it with the exact sums
+        W.pend[idx] = make_int4(MA_RESUME, mc.ul, 0, 0);
+        W.pend_jumps[idx] = jumps;
+        W.rng_n[idx] = mc.n0;
+        trans_sum += mc.ntrans;
+        pendX = true;
+        have = false;
       }
       if (have && r != MA_PENDING && (r != MA_CONTINUE || jumps >= MA_MAX_JUMPS)) {
         if (r == MA_CONTINUE) fail(K, ERR_STUCK, (int)rng.key1, 2);
@@ -581,10 +578,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
           pendK = (r == MA_END_COLDEEXC || r == MA_END_COLRECOMB);
         }
         jumps_sum += jumps;
-        if constexpr (CACHE)
-          trans_sum += mc.ntrans;
-        else
-          trans_sum += m.ntrans;
+        trans_sum += mc.ntrans;
         have = false;
       }
     }
@@ -653,8 +647,8 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
     m.ul = W.pend[idx].y;
     m.jumps = W.pend_jumps[idx] + 1;
     m.k = K.C.ne_index[cell_mgi(K, where)];
-    m.rec_off = K.T.ma_meta[m.ul].rec_off;
-    m.block = K.C.ma_key + (int64_t)K.C.ma_row[m.k] * K.C.ma_key_stride;
+    m.rowline = ma_rowline(K, m.k);
+    m.line = MA_NOLINE;  // (the walk resumes in k_ma, whose ticket looks its record up again)
     m.ntrans = 0;
     const int ul = m.ul, k = m.k;
     const int mgi = K.C.ne_mgi[k];

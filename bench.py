@@ -685,6 +685,7 @@ def main():
             "transport_ms": float(np.mean(transport_ms)),
             "event_rounds": int(np.max(rounds)) if rounds else 0,
             "kernel_ms": {k: v[0] for k, v in kt.items()},
+            "ma_ps_per_jump": kt["ma"][0] * 1e9 / max(float(work[8]), 1.0),
             "work_per_packet": {k: float(v) / max(P, 1) for k, v in zip(WORK_NAMES, work)},
             "ceiling": ceiling(alg, P, value / world),
         }

@@ -492,14 +492,16 @@ double artis_gpu_last_precompute_ms(void);
 /* Per-call event counts from the device (steps, lines scanned, kappa evaluations, ...), for the byte model. */
 #define ARTIS_WORK_COUNT 16
 int artis_gpu_last_work_counts(int64_t out[ARTIS_WORK_COUNT]);
-/* Coverage of the per-cell tables the engine sized at init (ABI 9): out[0] non-empty cells; out[1] cells with a
- * row of line coefficients (numbered centre outwards; the rest gather populations in the line walk) and out[2]
- * their bytes; out[3] cells with macro-atom key records and out[4] their bytes; out[5] bytes of the per-cell
- * action totals the table-free macro-atom walk reads; out[6] / out[7] macro-atom activations in cells with
- * records / in all cells between the last two placements of a partial cache (the records go to the cells with
- * the most activations at each artis_gpu_upload_cellstate; 0 / 0 before the first re-placement).  The split
- * never changes a result. */
-#define ARTIS_TABLE_INFO_COUNT 8
+/* Coverage of the per-cell tables the engine sized at init (ABI 9, 11): out[0] non-empty cells; out[1] cells with
+ * a row of line coefficients (numbered centre outwards; the rest gather populations in the line walk) and out[2]
+ * their bytes; out[3] cells with a whole row of macro-atom key records (row mode: all of them) and out[4] their
+ * bytes.  Level mode (the rows do not fit the budget; ABI 11): records per (cell, level) pair, placed at every
+ * artis_gpu_upload_cellstate on the pairs the walks used most since the last placement (whole cells centre
+ * outwards before the first transport); out[5] bytes of the per-pair action totals a jump without a record reads;
+ * out[6] / out[7] sampled macro-atom jumps on pairs that had a record / on all pairs between the last two
+ * placements; out[8] records of the current placement, out[9] their bytes, out[10] the pool's bytes.  The
+ * split never changes a result. */
+#define ARTIS_TABLE_INFO_COUNT 11
 int artis_gpu_table_info(int64_t out[ARTIS_TABLE_INFO_COUNT]);
 /* Emergent spectrum and light curve of the escaped r-packets among the resident packets, binned on the device:
  * the binning of write_partial_lightcurve_spectra (spectrum.cc:641-721) -- add_to_spec (spectrum.cc:339-362,
@@ -751,7 +753,7 @@ typedef struct artis_nlte_cells {
 int artis_gpu_update_grid_nlte(const artis_nt_shells *nt, const artis_nlte_params *params, artis_nlte_cells *cells);
 double artis_gpu_last_nlte_ms(void);  /* device time (ms) of the last artis_gpu_update_grid_nlte */
 
-#define ARTIS_GPU_ABI_VERSION 10 /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
+#define ARTIS_GPU_ABI_VERSION 11 /* 2: gamma / pellet / non-thermal path (artis_gamma_spectra and appended fields);
                                     3: virtual packets (artis_vpkt_params / artis_vpkt_result);
                                     4: artis_run_params.excitation_temperature;
                                     5: host estimator block pack/unpack, RCCL communicator + all-reduce;
@@ -763,7 +765,9 @@ double artis_gpu_last_nlte_ms(void);  /* device time (ms) of the last artis_gpu_
                                     9: artis_gpu_table_info (per-cell table budgets), artis_gpu_vpkt_last_drains
                                        (bounded virtual-packet spawn buffer);
                                    10: Compton / pair-production emissivity estimators (artis_run_params.comp_est,
-                                       artis_estimators.compton_emiss, a section of the estimator block) */
+                                       artis_estimators.compton_emiss, a section of the estimator block);
+                                   11: artis_gpu_init refuses unsupported option values; rlc_emiss_rpkt into
+                                       rpkt_emiss for do_rlc_est 1 / 2; artis_gpu_table_info's level-mode entries */
 int artis_gpu_abi_version(void);
 
 #ifdef __cplusplus

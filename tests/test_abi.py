@@ -98,7 +98,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_library_loads_without_gpu_and_reports_version():
     lib = C.CDLL(GPU_SO)
-    assert lib.artis_gpu_abi_version() == 10
+    assert lib.artis_gpu_abi_version() == 11
     lib.artis_gpu_last_error.restype = C.c_char_p
     assert lib.artis_gpu_last_error() is not None
 

@@ -100,12 +100,14 @@ def test_without_macroatom_cache_is_identical(small_model, engine_factory, monke
 
 @pytest.mark.parametrize("env", [{"ARTIS_GPU_NO_LINECOEF": "1"}, {"ARTIS_GPU_LINECOEF_ROWS": "half"},
                                  {"ARTIS_GPU_MACACHE_ROWS": "half"},
-                                 {"ARTIS_GPU_LINECOEF_ROWS": "1", "ARTIS_GPU_MACACHE_ROWS": "1"}],
-                         ids=["no_linecoef", "half_linecoef", "half_macache", "one_row_each"])
+                                 {"ARTIS_GPU_LINECOEF_ROWS": "1", "ARTIS_GPU_MACACHE_ROWS": "1"},
+                                 {"ARTIS_GPU_NO_MACACHE": "1"}],
+                         ids=["no_linecoef", "half_linecoef", "half_macache", "one_row_each", "no_macache"])
 def test_table_budgets_match_oracle(small_model, engine_factory, monkeypatch, env):
-    """Per-cell tables that only fit the HBM budget for some cells (line coefficients, macro-atom key records,
-    centre outwards) -- or for none (linecoef == nullptr) -- leave every other cell on the table-free path, with
-    the same packet histories as the oracle and the full-table engine."""
+    """Per-cell tables that only fit the HBM budget for some cells -- line coefficients centre outwards, macro-atom
+    key records per (cell, level) in level mode -- or for none (no line coefficients; an empty record pool: every
+    macro-atom jump made by the whole wave from the exact sums, ma_coop_select) give the same packet histories as
+    the oracle and the full-table engine."""
     small_model.set_timestep(11)
     pk = small_model.init_rpackets(11, 4000, seed=12)
     probe = engine_factory(small_model)
@@ -120,9 +122,13 @@ def test_table_budgets_match_oracle(small_model, engine_factory, monkeypatch, en
         assert info["linecoef_rows"] == 0 and info["linecoef_bytes"] == 0
     if "ARTIS_GPU_LINECOEF_ROWS" in env:
         assert 0 < info["linecoef_rows"] < info["cells"]
-    if "ARTIS_GPU_MACACHE_ROWS" in env:
-        assert 0 < info["macache_rows"] < info["cells"] and info["marates_bytes"] > 0
+    if "ARTIS_GPU_MACACHE_ROWS" in env or "ARTIS_GPU_NO_MACACHE" in env:
+        assert info["macache_rows"] == 0 and info["ma_pool_bytes"] > 0 and info["marates_bytes"] > 0
     eng.upload_cellstate(11)
+    if "ARTIS_GPU_MACACHE_ROWS" in env:
+        assert eng.table_info()["ma_level_records"] > 0
+    if "ARTIS_GPU_NO_MACACHE" in env:
+        assert eng.table_info()["ma_level_records"] == 0
     pg, po = pk.copy(), pk.copy()
     eg = eng.update_packets(11, pg)
     eo, wo = oracle_lib.update_packets(small_model, 11, po, nthreads=16)
@@ -134,14 +140,15 @@ def test_table_budgets_match_oracle(small_model, engine_factory, monkeypatch, en
 
 
 def test_partial_macroatom_cache_replaced_between_timesteps(small_model, engine_factory, monkeypatch):
-    """With key records for a third of the cells, each upload_cellstate re-places them on the cells with the most
-    macro-atom activations since the last placement; three chained timesteps stay on the oracle's histories."""
+    """Level mode with a pool of a third of the rows: each upload_cellstate places the (cell, level) records on the
+    pairs the walks used most since the last placement; three chained timesteps stay on the oracle's histories, and
+    after the first re-placement most sampled jumps fall on pairs with a record."""
     probe = engine_factory(small_model)
     ncells = probe.table_info()["cells"]
     probe.close()
     monkeypatch.setenv("ARTIS_GPU_MACACHE_ROWS", str(ncells // 3))
     eng = engine_factory(small_model)
-    assert eng.table_info()["macache_rows"] == ncells // 3
+    assert eng.table_info()["macache_rows"] == 0
     small_model.set_timestep(12)
     pk = small_model.init_rpackets(12, 3000, seed=13)
     pg, po = pk.copy(), pk.copy()
@@ -152,6 +159,9 @@ def test_partial_macroatom_cache_replaced_between_timesteps(small_model, engine_
         eo, _ = oracle_lib.update_packets(small_model, nts, po, nthreads=16)
         parity.assert_packets_match(pg, po)
         parity.assert_estimators_match(eg, eo)
+    info = eng.table_info()
+    assert info["ma_level_records"] > 0 and info["ma_jumps_sampled"] > 0
+    assert info["ma_jumps_sampled_recorded"] >= 0.5 * info["ma_jumps_sampled"], info
 
 
 def test_macroatom_records_in_many_batches_are_identical(small_model, engine_factory, monkeypatch):
