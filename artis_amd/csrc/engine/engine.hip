@@ -1094,7 +1094,20 @@ int vpkt_prepare(int64_t n) {
   // default: 16 spawns per packet, at most a quarter of the free HBM (a full buffer is traced and the launch
   // resumed, vpkt_drain), at least 2^20 records and never below the overflow records' count
   int64_t cap = G.vpkt_cap_param > 0 ? G.vpkt_cap_param : std::max<int64_t>(16 * n, 1 << 20);
-  if (G.vpkt_cap_param <= 0) {
+  if (G.use_megakernel && G.vpkt_cap_param <= 0) {
+    // the megakernel never parks a packet on a full buffer (only the split kernels resume, vpkt_drain): keep the
+    // full 16 spawns per packet, or refuse the launch before it starts instead of overflowing inside it
+    size_t freeb = 0, totalb = 0;
+    (void)hipMemGetInfo(&freeb, &totalb);
+    const double rec = VPKT_SPAWN_WORDS * sizeof(double) + 4 * sizeof(uint32_t);
+    const double have = (double)G.vpkt_spawn_cap * rec;
+    if ((double)cap * rec > 0.9 * ((double)freeb + have)) {
+      G.last_error = "megakernel with virtual packets: " + std::to_string(cap) +
+                     " spawn records (16 per packet) do not fit in free device memory; use the default (split-kernel) "
+                     "engine or set the vpkt spawn_capacity";
+      return ARTIS_ERR_UNSUPPORTED;
+    }
+  } else if (G.vpkt_cap_param <= 0) {
     size_t freeb = 0, totalb = 0;
     (void)hipMemGetInfo(&freeb, &totalb);
     const int64_t have = G.vpkt_spawn_cap;  // a buffer already held counts as free

@@ -347,6 +347,9 @@ DEVFN int get_nul(const Ctx &K, double freq) {
   if (n < 1) return GAMMA_RED_OF_LIST;  // (no gamma-ray lines: no gamma packets either)
   if (freq > f[n - 1]) return n - 1;
   if (freq < f[0]) return GAMMA_RED_OF_LIST;
+  // one line and freq == f[0]: the reference's bisection below never ends (too_high == too_low == 0); the line
+  // itself is the one to the red
+  if (n == 1) return 0;
   int too_high = n - 1, too_low = 0;
   while (too_high != too_low + 1) {
     const int tryindex = (too_high + too_low) / 2;

@@ -169,6 +169,9 @@ DEVFN void vpkt_trace_finish(const Ctx &K, VLane &v) {
   const DevVpkt &V = K.V;
   if (v.realtype >= 1 && v.realtype <= 3) atomicAdd(&V.ctr[v.realtype], 1ull);  // nvpkt_esc1..3
   double t_arrive = 0.;
+  // unrolled so that v.tau is never indexed dynamically: one dynamic index here kept the whole lane state (tau,
+  // the dummy packet) in scratch for the entire kernel, the line walk included (488 B/lane at 1 wave per SIMD)
+#pragma unroll
   for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++) {
     if (ind >= V.nspectra) break;
     const double prob = v.pn * exp(-v.tau[ind]);

@@ -822,12 +822,9 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_kpkt(const Ctx *__restrict__ ctx
   for (;; slot += gridDim.x * blockDim.x) {
     if (dyn) {
       if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t *)K.V.full)) break;
-      uint32_t base = 0;
-      if (lane_id() == 0) base = atomicAdd(&W.ctr[2 * QK + 1], 64u);
-      base = __shfl(base, 0, 64);
-      if (base >= nq) break;
-      slot = base + (uint32_t)lane_id();
-      if (slot >= nq) continue;
+      // one atomic per wave, made by the first active lane (correct whichever lanes have left the loop)
+      slot = wave_reserve(&W.ctr[2 * QK + 1], true);
+      if (slot >= nq) break;
     } else if (slot >= nq) {
       break;
     }

@@ -3005,6 +3005,7 @@ int get_nul(const Ctx &c, double freq) {
   const double freq_min = f[0];
   if (freq > freq_max) return (int)f.size() - 1;
   if (freq < freq_min) return RED_OF_LIST;
+  if (f.size() == 1) return 0;  // the reference's bisection never ends here (deviation, as gamma.h get_nul)
   int too_high = (int)f.size() - 1;
   int too_low = 0;
   while (too_high != too_low + 1) {

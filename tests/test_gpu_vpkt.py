@@ -137,6 +137,25 @@ def test_vpkt_full_spawn_buffer_drains_and_matches_oracle(monkeypatch):
     assert traces == vo.counters()["nvpkt"]
 
 
+def test_vpkt_megakernel_full_buffer_fails_loudly(monkeypatch):
+    """The megakernel (ARTIS_GPU_ENGINE=mega) cannot park packets on a full spawn buffer: with a buffer far below
+    one round's spawns it must end the launch with an error, never hang or drop virtual packets silently."""
+    monkeypatch.setenv("ARTIS_GPU_WAVE_GRID", "8")
+    monkeypatch.setenv("ARTIS_GPU_ENGINE", "mega")
+    m = Model(**VCFG)
+    m.set_timestep(NTS)
+    pk = m.init_rpackets(NTS, 40000, seed=44)
+    vc = ffi.VpktConfig(nz_obs=(0.3, -0.5), phi_obs_deg=(0.0, 120.0), spawn_capacity=16)
+    eng = Engine(m)
+    try:
+        eng.vpkt_init(vc)
+        eng.upload_cellstate(NTS)
+        with pytest.raises(RuntimeError):
+            eng.update_packets(NTS, pk.copy())
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("env", [("ARTIS_GPU_NO_LINECOEF", "1"), ("ARTIS_VPKT_LCONLY", "0")])
 def test_vpkt_general_kernel_matches_oracle(monkeypatch, env):
     """k_vpkt's general instantiation (population-gather line walk: cells without a coefficient row, or forced with
