@@ -280,7 +280,7 @@ class Engine:
 
     def last_kernel_times(self):
         """{class: (ms, launches)} for the last transport: rpkt (k_rpkt), ma (k_ma), kpkt (k_kpkt), classify (the
-        rest: classify, gamma, macro-atom queue binning, exact jumps)."""
+        rest: classify, gamma, macro-atom queue binning, exact jumps, deactivations)."""
         ms = (C.c_double * 4)()
         nl = (C.c_int64 * 4)()
         self.lib.artis_gpu_last_kernel_times(ms, nl)

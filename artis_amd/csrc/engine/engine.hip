@@ -1325,6 +1325,21 @@ int run_wavefront(int64_t n, int nts, double t2) {
       TEND(3);
       HIPCHK(hipMemsetAsync(W.ctr + 2 * QX, 0, 2 * sizeof(uint32_t), G.stream));
     }
+    {  // the walks' deactivations -> R / K
+      TSTART(3);
+      if (G.K.V.on)
+        HIPCHK(hipMemcpyAsync(G.d_qsnap, W.ctr + 2 * QF, sizeof(uint32_t), hipMemcpyDeviceToDevice, G.stream));
+      k_ma_finish<<<grid / 4, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+      TEND(3);
+      if (int rc = vpkt_drain(QF, [&]() -> int {
+            TSTART(3);
+            k_ma_finish<<<grid / 4, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+            TEND(3);
+            return 0;
+          }))
+        return rc;
+      HIPCHK(hipMemsetAsync(W.ctr + 2 * QF, 0, 2 * sizeof(uint32_t), G.stream));
+    }
     if (G.K.V.on)
       HIPCHK(hipMemcpyAsync(G.d_qsnap, W.ctr + 2 * QK, sizeof(uint32_t), hipMemcpyDeviceToDevice, G.stream));
     TSTART(2);

@@ -1886,9 +1886,40 @@ DEVFN int ma_jump_cached_global(const Ctx &K, const LocalCounters &L, artis_rng 
 }
 
 
+// the fb deactivation (macroatom.cc:340-380): select_continuum_nu's quadrature, noinline (run on copies, cold_call)
+DEVNI void ma_finish_fb(Tx &x, Pkt &p, const MaEnd &e) {
+  const Ctx &K = x.K;
+  const int element = p.ma_element;
+  const int uiu = K.T.level_ui[e.b];
+  const int ion = uiu - K.T.elem_uniqueionoffset[element] - 1, lower = e.a;
+  const int upperionlevel = e.b - K.T.ion_uniqueleveloffset[uiu];
+  const float T_e = K.C.Te[cell_mgi(K, p.where)];
+  p.nu_cmf = select_continuum_nu(x, element, ion, lower, upperionlevel, T_e);
+  lctr(x.L, CTR_MA_STAT_DEACTIVATION_FB);
+  p.last_event = 2;
+  emitt_rpkt(x, p);
+  p.next_trans = 0;
+  {  // get_continuumindex (atomic.cc:16-30)
+    int target = 0;
+    for (int t = 0; t < get_nphixstargets(K, element, ion, lower); t++)
+      if (get_phixsupperlevel(K, element, ion, lower, t) == upperionlevel) {
+        target = t;
+        break;
+      }
+    p.emissiontype = K.T.level_cont_index[ulev(K, element, ion, lower)] - target;
+  }
+  p.em_pos[0] = p.pos[0];
+  p.em_pos[1] = p.pos[1];
+  p.em_pos[2] = p.pos[2];
+  p.em_time = (int)p.prop_time;
+  p.nscatterings = 0;
+  if (K.V.on) vpkt_spawn(x, p, 3);  // macroatom.cc:376-379
+}
+
 // the deactivation branches of do_macroatom (macroatom.cc:222-380, 445-462) and its trailer (macroatom.cc:475-482);
-// `jumps` passes of the loop each added one interaction
-DEVNI void ma_finish(Tx &x, Pkt &p, const MaEnd &e, unsigned jumps) {
+// `jumps` passes of the loop each added one interaction.  Inline (bb and collisional in the caller's registers);
+// ma_finish is the noinline form for the kernels that run it on a copy.
+DEVFN void ma_finish_inl(Tx &x, Pkt &p, const MaEnd &e, unsigned jumps) {
   const Ctx &K = x.K;
   const int element = p.ma_element;
   p.interactions += (int)jumps;
@@ -1921,30 +1952,7 @@ DEVNI void ma_finish(Tx &x, Pkt &p, const MaEnd &e, unsigned jumps) {
     p.type = ARTIS_TYPE_KPKT;
     safeadd(&K.E.colheat[cell_mgi(K, p.where)], p.e_cmf);
   } else if (e.code == MA_END_FB) {
-    const int uiu = K.T.level_ui[e.b];
-    const int ion = uiu - K.T.elem_uniqueionoffset[element] - 1, lower = e.a;
-    const int upperionlevel = e.b - K.T.ion_uniqueleveloffset[uiu];
-    const float T_e = K.C.Te[cell_mgi(K, p.where)];
-    p.nu_cmf = select_continuum_nu(x, element, ion, lower, upperionlevel, T_e);
-    lctr(x.L, CTR_MA_STAT_DEACTIVATION_FB);
-    p.last_event = 2;
-    emitt_rpkt(x, p);
-    p.next_trans = 0;
-    {  // get_continuumindex (atomic.cc:16-30)
-      int target = 0;
-      for (int t = 0; t < get_nphixstargets(K, element, ion, lower); t++)
-        if (get_phixsupperlevel(K, element, ion, lower, t) == upperionlevel) {
-          target = t;
-          break;
-        }
-      p.emissiontype = K.T.level_cont_index[ulev(K, element, ion, lower)] - target;
-    }
-    p.em_pos[0] = p.pos[0];
-    p.em_pos[1] = p.pos[1];
-    p.em_pos[2] = p.pos[2];
-    p.em_time = (int)p.prop_time;
-    p.nscatterings = 0;
-    if (K.V.on) vpkt_spawn(x, p, 3);  // macroatom.cc:376-379
+    cold_call(x, p, [&](Tx &tx, Pkt &tp) { ma_finish_fb(tx, tp, e); });
   }
   if (p.trueemissiontype < 0) {
     p.trueemissiontype = p.emissiontype;
@@ -1952,6 +1960,7 @@ DEVNI void ma_finish(Tx &x, Pkt &p, const MaEnd &e, unsigned jumps) {
     p.trueem_time = p.em_time;
   }
 }
+DEVNI void ma_finish(Tx &x, Pkt &p, const MaEnd &e, unsigned jumps) { ma_finish_inl(x, p, e, jumps); }
 
 #define MA_MAX_JUMPS 10000000u
 

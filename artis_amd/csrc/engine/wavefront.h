@@ -23,7 +23,8 @@
 
 #include "gamma.h"
 
-enum { QR = 0, QM = 1, QK = 2, QG = 3, QX = 4, NQUEUES = 5 };  // QX: macro-atom jumps for k_ma_exact
+// QX: macro-atom jumps for k_ma_exact; QF: macro-atom deactivations for k_ma_finish
+enum { QR = 0, QM = 1, QK = 2, QG = 3, QX = 4, QF = 5, NQUEUES = 6 };
 
 struct WaveState {
   uint32_t *rng_n;     // [N] draws consumed so far this timestep (artis_rng.n)
@@ -153,21 +154,6 @@ __global__ void k_classify(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *
   block_counters_flush(K, s_ctr, s_work);
 }
 
-template <typename Cold>
-DEVFN void apply_pending(Tx &x, const WaveState &W, int32_t idx, Pkt &p, const Cold &cold) {
-  const int4 pd = W.pend[idx];
-  if (pd.x != 0) {
-    MaEnd e;
-    e.code = pd.x;
-    e.ion = pd.y;
-    e.a = pd.z;
-    e.b = pd.w;
-    const unsigned jumps = W.pend_jumps[idx];
-    cold(x, p, [&](Tx &tx, Pkt &tp) { ma_finish(tx, tp, e, jumps); });
-    W.pend[idx].x = 0;
-  }
-}
-
 // r-packets: persistent lanes, one do_rpkt_step per loop pass
 template <int MINW>
 __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa, int64_t n,
@@ -220,8 +206,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
             x.rng.n = W.rng_n[idx];
             x.ok = true;
             steps = 0;
-            have = true;
-            apply_pending(x, W, idx, p, ColdSoa{soa, n, idx});
+            have = true;  // (a macro-atom deactivation was applied by k_ma_finish: no pending state here)
           } else {
             drained = true;
           }
@@ -422,7 +407,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   int32_t idx = -1;
   bool have = false, drained = false;
   int cur = (int)(blockIdx.x % (unsigned)nr), tried = 0;
-  bool pendR = false, pendK = false, pendX = false;
+  bool pendF = false, pendX = false;
   unsigned long long jumps_sum = 0, trans_sum = 0;
   unsigned long long st_pass = 0, st_busy = 0, st_refill = 0, st_trefill = 0, st_tstep = 0;
 #ifdef ARTIS_STAMPS
@@ -439,10 +424,9 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     if (!__any(have) || __popcll(imask) >= W.refill_ma) {
       st_refill++;
       const unsigned long long tr0 = wave_clock();
-      wave_push(W, QR, pendR, idx);
-      wave_push(W, QK, pendK, idx);
+      wave_push(W, QF, pendF, idx);
       wave_push(W, QX, pendX, idx);
-      pendR = pendK = pendX = false;
+      pendF = pendX = false;
       if (imask) {
         // (nr is 1 or 8: shifts, not the 64-bit division the compiler would expand into ~120 scalar instructions)
         const uint32_t lo = (uint32_t)(((uint64_t)nq * cur) >> nr_log2),
@@ -574,8 +558,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
           W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
           W.pend_jumps[idx] = jumps;
           W.rng_n[idx] = rng.n;
-          pendR = (r == MA_END_BB || r == MA_END_FB);
-          pendK = (r == MA_END_COLDEEXC || r == MA_END_COLRECOMB);
+          pendF = true;  // -> k_ma_finish
         }
         jumps_sum += jumps;
         trans_sum += mc.ntrans;
@@ -747,10 +730,53 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
       } else if (r > 0) {
         W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
         lwork(L, WK_MA_JUMPS, m.jumps);
-        const int q = (r == MA_END_BB || r == MA_END_FB) ? QR : QK;
-        W.q[q][atomicAdd(&W.ctr[2 * q], 1u)] = idx;
+        W.q[QF][atomicAdd(&W.ctr[2 * QF], 1u)] = idx;  // -> k_ma_finish
       }
     }
+  }
+  block_counters_flush(K, s_ctr, s_work);
+}
+
+// macro-atom deactivations (the F queue, filled by k_ma and k_ma_exact): the deactivation branches of do_macroatom
+// (macroatom.cc:222-380) and its trailer (macroatom.cc:475-482) on the whole packet in registers, one packet per
+// lane, then -> R (bb / fb emission) or K (collisional deactivation).  Until round 4 k_rpkt / k_kpkt applied the
+// deactivation when they picked the packet up, as a noinline call on a scratch copy of the packet: in k_rpkt that
+// copy (~400 B per lane written and read back once per macro-atom cycle) was most of the kernel's write traffic.
+// With virtual packets the slots are taken from the fetch head and a full spawn buffer stops the launch (each lane
+// spawns at most once, so the overflow records cover the lanes in flight), as in k_kpkt.
+__global__ __launch_bounds__(WAVE_BLOCK) void k_ma_finish(const Ctx *__restrict__ ctxp, WaveState W,
+                                                          uint64_t *__restrict__ soa, int64_t n, int nts, double t2) {
+  CTX_IN_LDS(ctxp)
+  __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
+  __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
+  block_counters_init(s_ctr, s_work);
+  LocalCounters L;
+  L.ctr = &s_ctr[0];
+  L.work = &s_work[0];
+  const uint32_t nq = W.ctr[2 * QF];
+  const bool dyn = K.V.on;
+  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;; slot += gridDim.x * blockDim.x) {
+    if (dyn) {
+      if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t *)K.V.full)) break;
+      slot = wave_reserve(&W.ctr[2 * QF + 1], true);
+    }
+    if (slot >= nq) break;
+    const int32_t idx = W.q[QF][slot];
+    Pkt p;
+    pkt_load(soa, n, idx, p);
+    Tx x(K, L);
+    x.nts = nts;
+    x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
+    x.rng.n = W.rng_n[idx];
+    const int4 pd = W.pend[idx];
+    const MaEnd e{pd.x, pd.y, pd.z, pd.w};
+    ma_finish_inl(x, p, e, W.pend_jumps[idx]);
+    W.pend[idx].x = 0;
+    pkt_store(soa, n, idx, p);
+    W.rng_n[idx] = x.rng.n;
+    const bool live = x.ok && p.prop_time < t2;
+    wave_push(W, QR, live && p.type == ARTIS_TYPE_RPKT, idx);
+    wave_push(W, QK, live && (p.type == ARTIS_TYPE_KPKT || p.type == ARTIS_TYPE_PRE_KPKT), idx);
   }
   block_counters_flush(K, s_ctr, s_work);
 }
@@ -835,7 +861,6 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_kpkt(const Ctx *__restrict__ ctx
     x.nts = nts;
     x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
     x.rng.n = W.rng_n[idx];
-    apply_pending(x, W, idx, p, ColdFull());
     int guard = 0;
     while (x.ok && (p.type == ARTIS_TYPE_KPKT || p.type == ARTIS_TYPE_PRE_KPKT) && p.prop_time < t2) {
       const int mgi = cell_mgi(K, p.where);

@@ -685,6 +685,12 @@ def main():
             "transport_ms": float(np.mean(transport_ms)),
             "event_rounds": int(np.max(rounds)) if rounds else 0,
             "kernel_ms": {k: v[0] for k, v in kt.items()},
+            "other_kernels_ms": float(np.mean([t["classify"][0] for t in ktimes])),
+            "kernel_roofline": {k: {"alg_bytes_per_launch": alg[k] / max(v[1], 1.0),
+                                    "avg_launch_ms": v[0] / max(v[1], 1.0),
+                                    "frac": alg[k] / max(v[1], 1.0) / max(v[0] / max(v[1], 1.0) / 1e3, 1e-12) / 1e9
+                                            / HBM_PEAK_GBS}
+                                for k, v in kt.items()},
             "ma_ps_per_jump": kt["ma"][0] * 1e9 / max(float(work[8]), 1.0),
             "work_per_packet": {k: float(v) / max(P, 1) for k, v in zip(WORK_NAMES, work)},
             "ceiling": ceiling(alg, P, value / world),

@@ -563,7 +563,7 @@ int64_t artis_gpu_vpkt_last_drains(void);
 int64_t artis_gpu_last_rounds(void);  /* event-queue rounds of the last update (0: megakernel path) */
 /* device time (ms, HIP events around every launch) and launch count of the last update per kernel class:
  * [0] r-packet (k_rpkt), [1] macro-atom (k_ma), [2] k-packet (k_kpkt), [3] other: classify, gamma, the macro-atom
- * queue binning (k_ma_bin / scan / k_ma_scatter) and the exact jumps (k_ma_exact) */
+ * queue binning (k_ma_bin / scan / k_ma_scatter), the exact jumps (k_ma_exact) and the deactivations (k_ma_finish) */
 int artis_gpu_last_kernel_times(double ms[4], int64_t launches[4]);
 const char *artis_gpu_last_error(void);
 
