@@ -381,29 +381,40 @@ __global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, const double *__
 }
 
 // ---- level mode of the macro-atom key records (DevCells::ma_lptr): placement and build ----------------------
-// k_lvl_buckets: over every (cell, level) pair's sampled jump count c since the last placement: [0] the jumps on pairs
-// that had a record, [33] all jumps, [1 + floor(log2 c)] the pool lines the pairs of that count bucket would take
+// A pair's value for the pool is its sampled jump count c per record line rl (a knapsack by density): bucket
+// 1 + 2 floor(log2 v) + (the next bit of v) for v = 256 c / rl, half-octave steps; 0 for v == 0 with c > 0.
+#define MA_LVL_NB 84
+DEVFN int ma_lvl_bucket(uint32_t c, uint32_t rl) {
+  const uint64_t v = ((uint64_t)c << 8) / rl;
+  if (!v) return 0;
+  const int e = 63 - __clzll((long long)v);
+  const int half = e >= 1 ? (int)((v >> (e - 1)) & 1u) : 0;
+  return 1 + 2 * e + half;
+}
+// k_lvl_buckets: over every (cell, level) pair's sampled jump count c since the last placement: [0] the jumps on
+// pairs that had a record, [1] all jumps, [2 + b] the pool lines the pairs of density bucket b would take
 __global__ __launch_bounds__(256) void k_lvl_buckets(Ctx K, const uint32_t *__restrict__ rec_lines,
                                                      unsigned long long *__restrict__ out, int64_t npairs) {
-  __shared__ unsigned long long s[34];
-  if (threadIdx.x < 34) s[threadIdx.x] = 0;
+  __shared__ unsigned long long s[2 + MA_LVL_NB];
+  for (int j = threadIdx.x; j < 2 + MA_LVL_NB; j += blockDim.x) s[j] = 0;
   __syncthreads();
   const int64_t nl = K.T.nlevels_total;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t c = K.C.ma_lhist[i];
     if (!c) continue;
-    atomicAdd(&s[33], (unsigned long long)c);
+    atomicAdd(&s[1], (unsigned long long)c);
     if (K.C.ma_lptr[i] != MA_NOLINE) atomicAdd(&s[0], (unsigned long long)c);
     const uint32_t rl = rec_lines[i % nl];
-    if (rl) atomicAdd(&s[32 - __clz(c)], (unsigned long long)rl);
+    if (rl) atomicAdd(&s[2 + ma_lvl_bucket(c, rl)], (unsigned long long)rl);
   }
   __syncthreads();
-  if (threadIdx.x < 34 && s[threadIdx.x]) atomicAdd(&out[threadIdx.x], s[threadIdx.x]);
+  for (int j = threadIdx.x; j < 2 + MA_LVL_NB; j += blockDim.x)
+    if (s[j]) atomicAdd(&out[j], s[j]);
 }
 
 // k_lvl_select: the new DevCells::ma_lptr and the list of records to build.  have_hist == 0 (no transport yet):
 // whole cells in nonempty-index order (centre outwards), pair (k, ul) at line k * row_lines + rl_off[ul] while it
-// fits the pool.  Otherwise: count bucket above bt, or bucket bt while `rest` lines of it last.
+// fits the pool.  Otherwise: density bucket above bt, or bucket bt while `rest` lines of it last.
 // ctr: [0] pool lines taken, [1] records listed, [2] lines taken from bucket bt
 __global__ __launch_bounds__(256) void k_lvl_select(Ctx K, const uint32_t *__restrict__ rec_lines,
                                                     const uint32_t *__restrict__ rl_off, uint32_t row_lines,
@@ -423,10 +434,12 @@ __global__ __launch_bounds__(256) void k_lvl_select(Ctx K, const uint32_t *__res
       }
     } else if (rl) {
       const uint32_t c = K.C.ma_lhist[i];
-      const int b = c ? 32 - __clz(c) : 0;
-      bool take = b > 0 && b > bt;
-      if (b > 0 && b == bt) take = atomicAdd(&ctr[2], rl) + rl <= rest;
-      if (take) line = atomicAdd(&ctr[0], rl);
+      if (c) {
+        const int b = ma_lvl_bucket(c, rl);
+        bool take = b > bt;
+        if (b == bt) take = atomicAdd(&ctr[2], rl) + rl <= rest;
+        if (take) line = atomicAdd(&ctr[0], rl);
+      }
     }
     lptr[i] = line;
     if (line != MA_NOLINE) {
@@ -532,10 +545,10 @@ __global__ __launch_bounds__(64) void k_ma_build(Ctx K, const int2 *__restrict__
       int sp;
       const int rp = ma_rec_pos(lay, p, nd, nu, &sp);
       rec[rp] = (uint16_t)(key >> 16);
-      rec[lay.hot + rp] = (uint16_t)(key & 0xffffu);
+      if (!K.C.ma_hi_only) rec[lay.hot + rp] = (uint16_t)(key & 0xffffu);
       if (sp >= 0) {
         rec[sp] = (uint16_t)(key >> 16);
-        rec[lay.hot + sp] = (uint16_t)(key & 0xffffu);
+        if (!K.C.ma_hi_only) rec[lay.hot + sp] = (uint16_t)(key & 0xffffu);
       }
     }
   }
@@ -845,26 +858,26 @@ int ma_level_place() {
   const int64_t npairs = (int64_t)G.K.C.n_nonempty * G.K.T.nlevels_total;
   const unsigned B = 256, nb = (unsigned)std::min<int64_t>((npairs + B - 1) / B, 1 << 20);
   HIPCHK(hipMemsetAsync(G.d_lvl_ctr, 0, 4 * sizeof(uint32_t), G.stream));
-  int bt = 33;  // threshold bucket (33: none -- the initial placement)
+  int bt = MA_LVL_NB;  // threshold bucket (none -- the initial placement)
   uint64_t rest = 0;
   if (G.ma_lhist_ready) {
-    HIPCHK(hipMemsetAsync(G.d_lvl_buckets, 0, 34 * sizeof(unsigned long long), G.stream));
+    HIPCHK(hipMemsetAsync(G.d_lvl_buckets, 0, (2 + MA_LVL_NB) * sizeof(unsigned long long), G.stream));
     k_lvl_buckets<<<nb, B, 0, G.stream>>>(G.K, G.d_rec_lines, G.d_lvl_buckets, npairs);
-    unsigned long long h[34];
+    unsigned long long h[2 + MA_LVL_NB];
     HIPCHK(hipMemcpyAsync(h, G.d_lvl_buckets, sizeof h, hipMemcpyDeviceToHost, G.stream));
     HIPCHK(hipStreamSynchronize(G.stream));
-    // h[0]: sampled jumps on pairs with a record, h[33]: all, h[1..32]: pool lines wanted per log2 bucket
-    if (h[33] == 0) return 0;  // no walk since the last placement: keep it (its list rebuilds the records)
+    // h[0]: sampled jumps on pairs with a record, h[1]: all, h[2 + b]: pool lines wanted per density bucket b
+    if (h[1] == 0) return 0;  // no walk since the last placement: keep it (its list rebuilds the records)
     G.ma_acts_cached = (int64_t)h[0];
-    G.ma_acts_total = (int64_t)h[33];
+    G.ma_acts_total = (int64_t)h[1];
     uint64_t cum = 0;
-    bt = 0;
-    for (int b = 32; b >= 1; b--) {
-      if (cum + h[b] > G.ma_pool_lines) {
+    bt = -1;  // (everything fits)
+    for (int b = MA_LVL_NB - 1; b >= 0; b--) {
+      if (cum + h[2 + b] > G.ma_pool_lines) {
         bt = b;
         break;
       }
-      cum += h[b];
+      cum += h[2 + b];
     }
     rest = G.ma_pool_lines - cum;
   }
@@ -3353,6 +3366,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   C.ma_lptr = nullptr;
   C.ma_lhist = nullptr;
   C.ma_level_mode = 0;
+  C.ma_hi_only = 0;
   {
     // Macro-atom key records.  Row mode when every non-empty cell's records fit the budget (default: half of the
     // free HBM, ARTIS_GPU_MACACHE_MAX_GB; the rest is left for the packet store): cell k's records at row k.
@@ -3395,13 +3409,17 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
       // or more rate terms than k_ma_build stages in LDS)
       G.h_rec_lines.assign(nl, 0);
       G.ma_build_lds_doubles = 0;
+      const char *lh = getenv("ARTIS_GPU_MA_LOWHALVES");
+      const bool hi_only = !(lh && lh[0] == '1');
       std::vector<MaMeta> mm(nl);
       HIPCHK(hipMemcpy(mm.data(), G.K.T.ma_meta, nl * sizeof(MaMeta), hipMemcpyDeviceToHost));
       for (int ul = 0; ul < nl; ul++) {
         const int64_t next = (ul + 1 < nl) ? mm[ul + 1].rec_off : G.ma_key_stride;
         const int64_t need = 3 * ((int64_t)mm[ul].nd + mm[ul].nr) + mm[ul].nu + mm[ul].nt;
         if (ma_layout_ok(mm[ul].nd, mm[ul].nu) && need <= MA_BUILD_MAX_DOUBLES) {
-          G.h_rec_lines[ul] = (uint32_t)((next - mm[ul].rec_off) / 64);
+          // (the high halves only, ARTIS_GPU_MA_LOWHALVES=1: the whole record)
+          const int64_t hot = ma_layout(mm[ul].nd, mm[ul].nu, mm[ul].nr, mm[ul].nt).hot;
+          G.h_rec_lines[ul] = (uint32_t)(hi_only ? (hot + 63) / 64 : (next - mm[ul].rec_off) / 64);
           G.ma_build_lds_doubles = std::max<int64_t>(G.ma_build_lds_doubles, need);
         }
       }
@@ -3414,6 +3432,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
         C.ma_key = (uint16_t *)mc;
         C.have_macache = 1;
         C.ma_level_mode = 1;
+        C.ma_hi_only = hi_only ? 1 : 0;
         rc |= dalloc(&C.marates, (size_t)nne_cells * nl * ARTIS_MA_ACTION_COUNT);
         rc |= dalloc(&G.d_ma_lptr, (size_t)nne_cells * nl);
         rc |= dalloc(&G.d_ma_lhist, (size_t)nne_cells * nl);
@@ -3427,7 +3446,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
         G.row_lines = (uint32_t)acc;
         rc |= dupload(&G.d_rl_off, rl_off.data(), nl);
         rc |= dalloc(&G.d_lvl_ctr, (size_t)4);
-        rc |= dalloc(&G.d_lvl_buckets, (size_t)34);
+        rc |= dalloc(&G.d_lvl_buckets, (size_t)(2 + MA_LVL_NB));
         rc |= dalloc(&G.d_build_list, (size_t)std::max<int64_t>(1, std::min<int64_t>((int64_t)nne_cells * nl,
                                                                                    (int64_t)G.ma_pool_lines)));
         G.build_list_cap = std::min<int64_t>((int64_t)nne_cells * nl, (int64_t)G.ma_pool_lines);

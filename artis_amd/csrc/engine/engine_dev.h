@@ -231,6 +231,8 @@ struct DevCells {
   const uint32_t *ma_lptr;  // [n_nonempty * nlevels_total] or nullptr (row mode)
   uint32_t *ma_lhist;       // [n_nonempty * nlevels_total] or nullptr
   int32_t ma_level_mode;
+  int32_t ma_hi_only;  // the records hold the high key halves only (level mode): a comparison that needs the low
+                       // half is undecided and the jump goes to k_ma_exact
   double *marates;     // level mode: [n_nonempty * nlevels_total * 9] the per-pair action totals (or nullptr)
   // nebular inputs (ABI 6; nullptr when the option is off), model-cell indexed like the arrays above
   const double *nlte_pops;    // [npts_model * total_nlte_levels]

@@ -913,6 +913,16 @@ DEVFN void wave_flush_estimators(Tx &x) {
 // windows.  A packet passing some window is recorded in the spawn buffer; the traversals themselves run in
 // k_vpkt (vpkt.h), which repeats the per-observer cuts.  The next_trans fix-up of vpkt.cc:853-858 only ever
 // writes 0 over 0 and is omitted.
+// one slot of counter *c per active lane, one atomic per wave (made by the first active lane)
+DEVFN uint32_t wave_slot(uint32_t *c) {
+  const unsigned long long mask = __ballot(1);
+  const int leader = __ffsll((long long)mask) - 1;
+  uint32_t base = 0;
+  if ((int)__lane_id() == leader) base = atomicAdd(c, (uint32_t)__popcll(mask));
+  base = __shfl(base, leader, 64);
+  return base + (uint32_t)__popcll(mask & ((1ull << __lane_id()) - 1ull));
+}
+
 DEVFN void vpkt_spawn(Tx &x, const Pkt &p, int realtype) {
   const Ctx &K = x.K;
   const DevVpkt &V = K.V;
@@ -930,7 +940,7 @@ DEVFN void vpkt_spawn(Tx &x, const Pkt &p, int realtype) {
     }
   }
   if (!any) return;
-  uint32_t s = atomicAdd(&V.spawn_ctr[0], 1u);
+  uint32_t s = wave_slot(&V.spawn_ctr[0]);  // (the buffer order is free: k_vpkt sorts or traces it in any order)
   int64_t cap = V.cap;
   double *sp = V.spawn;
   if (s >= V.cap) {  // full: an overflow record, and the packet is parked by its kernel
@@ -1530,21 +1540,12 @@ DEVFN double readlane_d(double v, int l) {
 }
 #define MA_COOP_RANDOM (-1)  // the action draw exceeds the total (the reference's abort, ERR_MA_RANDOM)
 #define MA_COOP_NOSEL (-2)   // no entry of the action's list exceeds the transition draw (ERR_MA_SELECT)
-// Wave-uniform: every lane of the wave calls it with the same (k, ul, z1, z2) and gets the same result.  The action
-// from the pair's exact totals (DevCells::marates, the sums of ma_foreach_rate in the reference's order,
-// macroatom.cc:502-525); for a transition action, the list entry: the lanes evaluate 64 individual rates at a time
-// (ma_rate_at: the expressions the totals were summed from) and the running sum is added in list order, one term
-// per step, read from the evaluating lane's register (v_readlane) -- the reference's linear scan
-// (do_macroatom_raddeexcitation etc.), the same double sums as ma_jump_exact.  Returns the action, *j the entry.
-// (out of line: inlined into k_ma, its rate expressions would raise the register allocation of the whole walk)
-#ifdef ARTIS_MA_COOP_INLINE
-DEVFN
-#else
-DEVNI
-#endif
-int ma_coop_select(const Ctx &K, int k, int ul, double z1, double z2, double t_mid, int *j, unsigned &probes) {
-  const int64_t nl = K.T.nlevels_total;
-  const double *tot = K.C.marates + ((int64_t)k * nl + ul) * ARTIS_MA_ACTION_COUNT;
+// The jump of a walk whose (cell, level) pair has no key record.  The action comes from the pair's exact totals
+// (DevCells::marates, the sums of ma_foreach_rate in the reference's order, macroatom.cc:502-525), drawn by each such
+// lane itself (ma_coop_action); only a transition action's list search is made by the whole wave (ma_coop_search).
+// ma_coop_action returns the action (or MA_COOP_RANDOM) and *x = z2 times the action's total, the search's target.
+DEVFN int ma_coop_action(const Ctx &K, int k, int ul, double z1, double z2, double *x) {
+  const double *tot = K.C.marates + ((int64_t)k * K.T.nlevels_total + ul) * ARTIS_MA_ACTION_COUNT;
   double pr[ARTIS_MA_ACTION_COUNT];
   double total = 0.;
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
@@ -1553,7 +1554,7 @@ int ma_coop_select(const Ctx &K, int k, int ul, double z1, double z2, double t_m
   }
   const double randomrate = z1 * total;
   double rate = 0.;
-  int sel = -1;
+  int sel = MA_COOP_RANDOM;
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
     rate += pr[a];
     if (rate > randomrate) {
@@ -1561,9 +1562,30 @@ int ma_coop_select(const Ctx &K, int k, int ul, double z1, double z2, double t_m
       break;
     }
   }
-  if (sel < 0) return MA_COOP_RANDOM;
-  if (sel == ARTIS_MA_ACTION_COLDEEXC || sel == ARTIS_MA_ACTION_COLRECOMB || sel == ARTIS_MA_ACTION_INTERNALUPHIGHERNT)
-    return sel;
+  double xs = 0.;
+#pragma unroll
+  for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++)
+    if (a == sel) xs = z2 * pr[a];
+  *x = xs;
+  return sel;
+}
+DEVFN bool ma_coop_needs_search(int sel) {
+  return sel >= 0 && sel != ARTIS_MA_ACTION_COLDEEXC && sel != ARTIS_MA_ACTION_COLRECOMB &&
+         sel != ARTIS_MA_ACTION_INTERNALUPHIGHERNT;
+}
+// Wave-uniform: every lane calls it with the same (k, ul, sel, x) and gets the same entry of action sel's list:
+// the lanes evaluate 64 individual rates at a time (ma_rate_at: the expressions the totals were summed from) and
+// the running sum is added in list order, one term per step, read from the evaluating lane's register (v_readlane)
+// -- the reference's linear scan (do_macroatom_raddeexcitation etc.), the same double sums as ma_jump_exact.
+// Returns sel, *j the entry (or MA_COOP_NOSEL).
+// (out of line: inlined into k_ma, its rate expressions would raise the register allocation of the whole walk)
+#ifdef ARTIS_MA_COOP_INLINE
+DEVFN
+#else
+DEVNI
+#endif
+int ma_coop_search(const Ctx &K, int k, int ul, int sel, double x, double t_mid, int *j, unsigned &probes) {
+  const int64_t nl = K.T.nlevels_total;
   const MaMeta mm = K.T.ma_meta[ul];
   int base, cnt;
   if (sel == ARTIS_MA_ACTION_RADDEEXC || sel == ARTIS_MA_ACTION_INTERNALDOWNSAME) {
@@ -1579,7 +1601,6 @@ int ma_coop_select(const Ctx &K, int k, int ul, double z1, double z2, double t_m
     base = mm.nd + mm.nr + mm.nu;
     cnt = mm.nt;
   }
-  const double x = z2 * pr[sel];
   const int mgi = K.C.ne_mgi[k];
   const double ec = K.T.level_epsilon[ul];
   const double *pops = K.C.pops + (int64_t)k * nl;
@@ -1720,6 +1741,7 @@ DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
   auto cmp = [&](int p, uint32_t hi, double q, uint32_t qh) -> int {
     if (hi < qh) return -1;
     if (hi > qh + 1) return 1;
+    if (K.C.ma_hi_only) return 0;  // level-mode records hold the high halves only: undecided -> exact jump
     return ma_key_cmp((hi << 16) | (uint32_t)gload(rec + lay.hot + p), q);
   };
   if (m.sel < 0) {  // a new jump: the action is the first of the 9 running-sum keys (line 0) above q
@@ -1812,7 +1834,7 @@ DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
       return MA_PENDING;
     }
     probes++;
-    const int c = ma_key_cmp((h << 16) | (uint32_t)gload(rec + lay.hot + p), m.q2);
+    const int c = K.C.ma_hi_only ? 0 : ma_key_cmp((h << 16) | (uint32_t)gload(rec + lay.hot + p), m.q2);
     if (c == 0) {
       m.ntrans += probes;
       m.jumps--;

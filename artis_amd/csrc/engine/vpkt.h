@@ -258,16 +258,27 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
   const double lnu_first = K.T.line_nu[0], lnu_last = K.T.line_nu[max(K.T.nlines - 1, 0)];
   if (K.C.ne_index[v.mgi] < K.C.linecoef_rows) {
     // over the per-cell Sobolev coefficients (DevCells::linecoef, as get_event): an aligned window of LC_WIN lines'
-    // frequencies and coefficients is eight independent 16-byte loads; dtau = coefficient * t_line is the
-    // reference's (B_lu n_l - B_ul n_u) * HCLIGHTOVERFOURPI * t_line in the same operation order
+    // frequencies and coefficients is staged in the lane's LDS column (eight independent 16-byte loads, as k_rpkt),
+    // so a line reads its two values with two LDS loads instead of selecting them out of 32 registers;
+    // dtau = coefficient * t_line is the reference's (B_lu n_l - B_ul n_u) * HCLIGHTOVERFOURPI * t_line in the same
+    // operation order.  vpkt_alive (vpkt.cc:293) is tested when the walk leaves a window and when it ends, not after
+    // every line: the tau only grow, so a virtual packet that dies inside a window is still dead there and is killed
+    // the same; only the lines added after its death (diagnostic count) differ from the reference's loop.
     const int nlines = K.T.nlines;
     const double *lnu = K.T.line_nu, *nu8 = K.T.line_nu8;
     const double *crow = K.C.linecoef + (int64_t)K.C.ne_index[v.mgi] * K.C.linecoef_stride;
     const uint8_t *lmask = V.line_mask;
     const int nspec = V.nspectra;
     const double tau_max = V.tau_max;
-    f64x2 wn[LC_WIN / 2], wc[LC_WIN / 2];
+    __attribute__((address_space(3))) double *win = x.win;
     uint64_t wm = 0;  // the window's 8 line masks
+    auto all_dead = [&]() {
+      int dead = 0;
+#pragma unroll
+      for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
+        if (ind < nspec && v.tau[ind] > tau_max) dead++;
+      return dead == nspec;
+    };
     while (ldist < sdist) {
       const int lineindex = closest_transition(nlines, lnu, d.nu_cmf, d.next_trans, lnu_first, lnu_last);
       if (lineindex < 0) {
@@ -275,22 +286,13 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
         break;  // D9
       }
       if ((unsigned)(lineindex - pf_base) >= (unsigned)LC_WIN) {
+        if (pf_base >= 0 && all_dead()) return VSEG_KILLED;
         pf_base = lineindex & ~(LC_WIN - 1);
-#pragma unroll
-        for (int q = 0; q < LC_WIN / 2; q++) {
-          wn[q] = ((glb_f64x2 *)(nu8 + pf_base))[q];
-          wc[q] = ((glb_f64x2 *)(crow + pf_base))[q];
-        }
+        lc_window(nu8 + pf_base, crow + pf_base, win);
         wm = *(const __attribute__((address_space(1))) uint64_t *)(lmask + pf_base);
       }
       const int pj = lineindex - pf_base;
-      double nutrans = wn[0].x, coef = wc[0].x;
-#pragma unroll
-      for (int q = 1; q < LC_WIN; q++)
-        if (pj == q) {
-          nutrans = (q & 1) ? wn[q >> 1].y : wn[q >> 1].x;
-          coef = (q & 1) ? wc[q >> 1].y : wc[q >> 1].x;
-        }
+      const double nutrans = win[pj * WAVE_BLOCK_T];
       const unsigned lm = (unsigned)(wm >> (8 * pj)) & 0xffu;
       d.next_trans = lineindex + 1;
       if (d.nu_cmf < nutrans)
@@ -303,15 +305,12 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
       }
       lines++;
       const double t_line = t_current + ldist / ARTIS_CLIGHT;
-      const double dtau = coef * t_line;
-      int dead = 0;
+      const double dtau = win[(LC_WIN + pj) * WAVE_BLOCK_T] * t_line;
 #pragma unroll
-      for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++) {
+      for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
         if ((lm >> ind) & 1u) v.tau[ind] += dtau;
-        if (ind < nspec && v.tau[ind] > tau_max) dead++;
-      }
-      if (dead == nspec) return VSEG_KILLED;  // vpkt_alive
     }
+    if (all_dead()) return VSEG_KILLED;
     return vpkt_segment_end(x, v, sdist, snext);
   }
   if constexpr (PF == 0) {  // launched only when every non-empty cell has a coefficient row
@@ -392,7 +391,10 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
   LocalCounters L;
   L.ctr = &s_ctr[0];
   L.work = &s_work[0];
+  __shared__ double s_win[2 * LC_WIN][WAVE_BLOCK];  // line windows of the walk over DevCells::linecoef
+  static_assert(WAVE_BLOCK == WAVE_BLOCK_T, "Tx::win column stride");
   Tx x(K, L);
+  x.win = (__attribute__((address_space(3))) double *)&s_win[0][threadIdx.x];
   const uint32_t nspawn = min(V.spawn_ctr[0], V.cap);
   const uint64_t nitems = (uint64_t)nspawn * (uint64_t)V.nobs;
   VLane v;

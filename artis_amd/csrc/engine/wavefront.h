@@ -529,16 +529,25 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     }
     // level mode: the jumps of the lanes without a record, each made by the whole wave (wave-uniform loop)
     if constexpr (COOP) {
+      // the action of every such lane from its pair's totals, lane by lane; a collisional / NT action (or the
+      // abort) is applied at once, a transition action waits for the wave's search of its list
+      int csel = MA_COOP_RANDOM;
+      double cx = 0.;
+      if (unc) {
+        csel = ma_coop_action(K, mc.k, mc.ul, z1, z2, &cx);
+        if (!ma_coop_needs_search(csel)) r = ma_coop_apply(K, L, rng, mc, e, (int)rng.key1, csel, -1, 0u, meta);
+      }
       // (a rotating start, so that with coop_max < 64 every waiting lane gets its turn)
-      unsigned long long um = __ballot(unc);
+      unsigned long long um = __ballot(unc && ma_coop_needs_search(csel));
       const int rot = (int)(st_pass & 63);
       um = (um >> rot) | (rot ? um << (64 - rot) : 0ull);
       for (int done_coop = 0; um && done_coop < W.coop_max; um &= um - 1, done_coop++) {
         const int ld = (__ffsll((long long)um) - 1 + rot) & 63;
         const int ul = __builtin_amdgcn_readlane(mc.ul, ld), k = __builtin_amdgcn_readlane(mc.k, ld);
+        const int sl = __builtin_amdgcn_readlane(csel, ld);
         int j = -1;
         unsigned probes = 0;
-        const int sel = ma_coop_select(K, k, ul, readlane_d(z1, ld), readlane_d(z2, ld), t_mid, &j, probes);
+        const int sel = ma_coop_search(K, k, ul, sl, readlane_d(cx, ld), t_mid, &j, probes);
         if (lane == ld) r = ma_coop_apply(K, L, rng, mc, e, (int)rng.key1, sel, j, probes, meta);
       }
     }
