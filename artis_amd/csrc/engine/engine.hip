@@ -3409,15 +3409,13 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
       // or more rate terms than k_ma_build stages in LDS)
       G.h_rec_lines.assign(nl, 0);
       G.ma_build_lds_doubles = 0;
-      const char *lh = getenv("ARTIS_GPU_MA_LOWHALVES");
-      const bool hi_only = !(lh && lh[0] == '1');
+      const bool hi_only = ARTIS_MA_HI_ONLY;  // (k_ma's level-mode instance compiles the same choice in)
       std::vector<MaMeta> mm(nl);
       HIPCHK(hipMemcpy(mm.data(), G.K.T.ma_meta, nl * sizeof(MaMeta), hipMemcpyDeviceToHost));
       for (int ul = 0; ul < nl; ul++) {
         const int64_t next = (ul + 1 < nl) ? mm[ul + 1].rec_off : G.ma_key_stride;
         const int64_t need = 3 * ((int64_t)mm[ul].nd + mm[ul].nr) + mm[ul].nu + mm[ul].nt;
         if (ma_layout_ok(mm[ul].nd, mm[ul].nu) && need <= MA_BUILD_MAX_DOUBLES) {
-          // (the high halves only, ARTIS_GPU_MA_LOWHALVES=1: the whole record)
           const int64_t hot = ma_layout(mm[ul].nd, mm[ul].nu, mm[ul].nr, mm[ul].nt).hot;
           G.h_rec_lines[ul] = (uint32_t)(hi_only ? (hot + 63) / 64 : (next - mm[ul].rec_off) / 64);
           G.ma_build_lds_doubles = std::max<int64_t>(G.ma_build_lds_doubles, need);

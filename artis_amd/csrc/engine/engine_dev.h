@@ -121,6 +121,11 @@ struct MaLayout {
   int hot;       // high-half positions = offset of the low halves
 };
 #define MA_AREA 55
+// level mode: the records hold the high key halves only (twice the records in the same pool; a comparison the high
+// half cannot decide is made from the exact sums by k_ma's cooperative jump)
+#ifndef ARTIS_MA_HI_ONLY
+#define ARTIS_MA_HI_ONLY 1
+#endif
 #define MA_NOLINE 0xffffffffu  // DevCells::ma_lptr: no record for this (cell, level)
 static inline __host__ __device__ MaLayout ma_layout(int nd, int nu, int nr, int nt) {
   MaLayout L;

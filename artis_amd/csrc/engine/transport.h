@@ -568,10 +568,30 @@ DEVFN void lc_window(const double *nu8, const double *coef, __attribute__((addre
   }
 }
 
-// rpkt.cc:67-328
-DEVFN double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_eventtype, double tau_rnd,
-                       double abort_dist) {
+// One r-packet step (rpkt.cc:623-813) in three parts, so that k_rpkt can spread its line walk over passes:
+// rpkt_step_begin (the draw, the boundary, the cases without a walk, get_event's prologue), get_event_walk (the
+// walk over the cell's coefficient row, resumable after a bounded number of lines) and rpkt_step_finish (the step's
+// end: move, estimators, event or boundary).  do_rpkt_step runs the three back to back.  RStep holds what crosses
+// from one part to the next.
+struct RStep {
+  double sdist, tdist, edist;
+  int snext, mgi, oldmgi, k, eventtype;
+  bool cross0, find_nextline;
+  Kappa kap;
+  // get_event's walk (rpkt.cc:112-325): the draw, the distance that ends the search, the comoving frequency there,
+  // the continuum opacity; the dummy packet's position, time and frequency, the next line, the staged window
+  double tau_rnd, abort_dist, nu_cmf_abort, kap_cont, tau, dist, dpos[3], dt, dnu;
+  int dnext, wb;
+};
+enum { RSTEP_DONE = 0, RSTEP_WALK = 1, RSTEP_END = 2 };
+
+// rpkt.cc:67-110 (get_event's prologue): true when the walk over the cell's coefficient row is set up in S
+// (get_event_walk runs it); otherwise the whole search ran here (the population-gather walk) and S.edist /
+// S.eventtype hold its result
+DEVFN bool get_event_begin(Tx &x, int k, int mgi, Pkt &p, RStep &S, double tau_rnd, double abort_dist) {
   const Ctx &K = x.K;
+  Kappa &kap = S.kap;
+  int *rpkt_eventtype = &S.eventtype;
   double tau = 0.;
   double dist = 0.;
   double nu_cmf_abort;
@@ -588,107 +608,24 @@ DEVFN double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_even
   calculate_kappa_rpkt_cont(x, p, k, mgi, kap);
   STAMP(x, 1);
   const double kap_cont = kap.total * doppler_packet(K, p);
+  if (x.win && k < K.C.linecoef_rows) {
+    S.tau_rnd = tau_rnd;
+    S.abort_dist = abort_dist;
+    S.nu_cmf_abort = nu_cmf_abort;
+    S.kap_cont = kap_cont;
+    S.tau = tau;
+    S.dist = dist;
+    for (int d = 0; d < 3; d++) S.dpos[d] = dpos[d];
+    S.dt = dt;
+    S.dnu = dnu;
+    S.dnext = dnext;
+    S.wb = -16;
+    return true;
+  }
   const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
   const double lnu_first = K.T.line_nu[0], lnu_last = K.T.line_nu[max(K.T.nlines - 1, 0)];
   unsigned long long nscanned = 0, ntaus = 0;
   double result;
-  if (x.win && k < K.C.linecoef_rows) {
-    // the context fields the walk reads, in registers: through the context pointer they are reloaded from memory
-    // on every line (the compiler cannot prove the kernel's stores leave them unchanged)
-    __attribute__((address_space(3))) double *win = x.win;
-    const bool rel = K.R.relativistic_doppler;
-    const int nlines = K.T.nlines;
-    const double *lnu = K.T.line_nu, *nu8 = K.T.line_nu8;
-    const double *crow = K.C.linecoef + (int64_t)k * K.C.linecoef_stride;
-    int wb = -16;
-    while (true) {
-      const int lineindex = closest_transition(nlines, lnu, dnu, dnext, lnu_first, lnu_last);
-      if (lineindex >= 0) {
-        nscanned++;
-        if ((unsigned)(lineindex - wb) >= (unsigned)LC_WIN) {
-          wb = lineindex & ~(LC_WIN - 1);
-          lc_window(nu8 + wb, crow + wb, win);
-        }
-        const int pj = lineindex - wb;
-        const double nu_trans = win[pj * WAVE_BLOCK_T];
-        dnext = lineindex + 1;
-        double ldist;
-        if (dnu <= nu_trans) {
-          ldist = 0;
-        } else if (!rel) {
-          ldist = ARTIS_CLIGHT * dt * (dnu / nu_trans - 1);
-        } else {
-          const double nu_r = nu_trans / p.nu_rf;
-          const double ct = ARTIS_CLIGHT * dt;
-          const double r = vec_len(dpos);
-          const double mu = dot(p.dir, dpos) / r;
-          ldist = -mu * r + (ct - nu_r * nu_r * sqrt(ct * ct - (1 + r * r * (1 - mu * mu) * (1 + pow(nu_r, -2))))) /
-                                (1 + nu_r * nu_r);
-        }
-        if (ldist < 0.) {
-          if (!(ldist >= -100.)) {
-            x.err(ERR_LDIST, p.number, lineindex);
-            result = 0.;
-            break;
-          }
-          ldist = 0.;
-        }
-        const double tau_cont = kap_cont * ldist;
-        if (tau_rnd - tau > tau_cont) {
-          if (nu_trans < nu_cmf_abort) {
-            dnext -= 1;
-            p.next_trans = dnext;
-            result = DBL_MAX;
-            break;
-          }
-          double tau_line = win[(LC_WIN + pj) * WAVE_BLOCK_T] * dt;
-          ntaus++;
-          if (tau_line < 0) tau_line = 0.;
-          if (tau_rnd - tau > tau_cont + tau_line) {
-            dist = dist + ldist;
-            tau += tau_cont + tau_line;
-            move_dummy(rel, dpos, p.dir, dt, dnu, p.nu_rf, ldist);
-          } else {
-            p.ma_element = K.T.line_elem[lineindex];
-            p.ma_ion = K.T.line_ion[lineindex];
-            p.ma_level = K.T.line_upper[lineindex];
-            p.ma_activatingline = lineindex;
-            double edist = dist + ldist;
-            if (edist >= abort_dist) edist = abort_dist * (1 - 2e-8);
-            *rpkt_eventtype = ARTIS_RPKT_EVENTTYPE_BB;
-            p.next_trans = dnext;
-            result = edist;
-            break;
-          }
-        } else {
-          const double edist = dist + (tau_rnd - tau) / kap_cont;
-          dnext -= 1;
-          *rpkt_eventtype = ARTIS_RPKT_EVENTTYPE_CONT;
-          p.next_trans = dnext;
-          result = edist;
-          break;
-        }
-      } else {
-        dnext = K.T.nlines + 1;
-        const double tau_cont = kap_cont * (abort_dist - dist);
-        double edist;
-        if (tau_rnd - tau > tau_cont) {
-          edist = DBL_MAX;
-        } else {
-          edist = dist + (tau_rnd - tau) / kap_cont;
-          *rpkt_eventtype = ARTIS_RPKT_EVENTTYPE_CONT;
-        }
-        p.next_trans = dnext;
-        result = edist;
-        break;
-      }
-    }
-    lwork(x.L, WK_LINES_SCANNED, nscanned);
-    lwork(x.L, WK_LINE_TAUS, ntaus);
-    x.wl += (unsigned)nscanned;
-    STAMP(x, 2);
-    return result;
-  }
   // The walk visits consecutive lines.  Their 32-byte records and the two level populations each needs (random
   // gathers into the cell's pops) are fetched four lines at a time, all loads independent, so a long walk
   // waits for memory twice per four lines instead of three times per line.
@@ -797,7 +734,133 @@ DEVFN double get_event(Tx &x, int k, int mgi, Pkt &p, Kappa &kap, int *rpkt_even
   lwork(x.L, WK_LINE_TAUS, ntaus);
   x.wl += (unsigned)nscanned;
   STAMP(x, 2);
-  return result;
+  S.edist = result;
+  return false;
+}
+
+
+// rpkt.cc:112-325 over the cell's coefficient row (DevCells::linecoef) in 8-line LDS windows: at most `budget`
+// lines per call; false when the budget ran out first (S holds the walk, the next call continues it), true when the
+// search ended (S.edist, S.eventtype; p.next_trans and, for a line event, the macro-atom activation fields set)
+DEVFN bool get_event_walk(Tx &x, Pkt &p, RStep &S, int budget) {
+  const Ctx &K = x.K;
+  int *rpkt_eventtype = &S.eventtype;
+  const double tau_rnd = S.tau_rnd, abort_dist = S.abort_dist, nu_cmf_abort = S.nu_cmf_abort, kap_cont = S.kap_cont;
+  double tau = S.tau, dist = S.dist;
+  double dpos[3] = {S.dpos[0], S.dpos[1], S.dpos[2]};
+  double dt = S.dt, dnu = S.dnu;
+  int dnext = S.dnext;
+  const double lnu_first = K.T.line_nu[0], lnu_last = K.T.line_nu[max(K.T.nlines - 1, 0)];
+  unsigned long long nscanned = 0, ntaus = 0;
+  double result = 0.;
+  bool done = true;
+  // the context fields the walk reads, in registers: through the context pointer they are reloaded from memory
+  // on every line (the compiler cannot prove the kernel's stores leave them unchanged)
+  __attribute__((address_space(3))) double *win = x.win;
+  const bool rel = K.R.relativistic_doppler;
+  const int nlines = K.T.nlines;
+  const double *lnu = K.T.line_nu, *nu8 = K.T.line_nu8;
+  const double *crow = K.C.linecoef + (int64_t)S.k * K.C.linecoef_stride;
+  int wb = S.wb;
+  while (true) {
+    if (budget-- == 0) {  // resume next call
+      done = false;
+      S.tau = tau;
+      S.dist = dist;
+      for (int d = 0; d < 3; d++) S.dpos[d] = dpos[d];
+      S.dt = dt;
+      S.dnu = dnu;
+      S.dnext = dnext;
+      S.wb = wb;
+      break;
+    }
+    const int lineindex = closest_transition(nlines, lnu, dnu, dnext, lnu_first, lnu_last);
+    if (lineindex >= 0) {
+      nscanned++;
+      if ((unsigned)(lineindex - wb) >= (unsigned)LC_WIN) {
+        wb = lineindex & ~(LC_WIN - 1);
+        lc_window(nu8 + wb, crow + wb, win);
+      }
+      const int pj = lineindex - wb;
+      const double nu_trans = win[pj * WAVE_BLOCK_T];
+      dnext = lineindex + 1;
+      double ldist;
+      if (dnu <= nu_trans) {
+        ldist = 0;
+      } else if (!rel) {
+        ldist = ARTIS_CLIGHT * dt * (dnu / nu_trans - 1);
+      } else {
+        const double nu_r = nu_trans / p.nu_rf;
+        const double ct = ARTIS_CLIGHT * dt;
+        const double r = vec_len(dpos);
+        const double mu = dot(p.dir, dpos) / r;
+        ldist = -mu * r + (ct - nu_r * nu_r * sqrt(ct * ct - (1 + r * r * (1 - mu * mu) * (1 + pow(nu_r, -2))))) /
+                              (1 + nu_r * nu_r);
+      }
+      if (ldist < 0.) {
+        if (!(ldist >= -100.)) {
+          x.err(ERR_LDIST, p.number, lineindex);
+          result = 0.;
+          break;
+        }
+        ldist = 0.;
+      }
+      const double tau_cont = kap_cont * ldist;
+      if (tau_rnd - tau > tau_cont) {
+        if (nu_trans < nu_cmf_abort) {
+          dnext -= 1;
+          p.next_trans = dnext;
+          result = DBL_MAX;
+          break;
+        }
+        double tau_line = win[(LC_WIN + pj) * WAVE_BLOCK_T] * dt;
+        ntaus++;
+        if (tau_line < 0) tau_line = 0.;
+        if (tau_rnd - tau > tau_cont + tau_line) {
+          dist = dist + ldist;
+          tau += tau_cont + tau_line;
+          move_dummy(rel, dpos, p.dir, dt, dnu, p.nu_rf, ldist);
+        } else {
+          p.ma_element = K.T.line_elem[lineindex];
+          p.ma_ion = K.T.line_ion[lineindex];
+          p.ma_level = K.T.line_upper[lineindex];
+          p.ma_activatingline = lineindex;
+          double edist = dist + ldist;
+          if (edist >= abort_dist) edist = abort_dist * (1 - 2e-8);
+          *rpkt_eventtype = ARTIS_RPKT_EVENTTYPE_BB;
+          p.next_trans = dnext;
+          result = edist;
+          break;
+        }
+      } else {
+        const double edist = dist + (tau_rnd - tau) / kap_cont;
+        dnext -= 1;
+        *rpkt_eventtype = ARTIS_RPKT_EVENTTYPE_CONT;
+        p.next_trans = dnext;
+        result = edist;
+        break;
+      }
+    } else {
+      dnext = K.T.nlines + 1;
+      const double tau_cont = kap_cont * (abort_dist - dist);
+      double edist;
+      if (tau_rnd - tau > tau_cont) {
+        edist = DBL_MAX;
+      } else {
+        edist = dist + (tau_rnd - tau) / kap_cont;
+        *rpkt_eventtype = ARTIS_RPKT_EVENTTYPE_CONT;
+      }
+      p.next_trans = dnext;
+      result = edist;
+      break;
+    }
+  }
+  lwork(x.L, WK_LINES_SCANNED, nscanned);
+  lwork(x.L, WK_LINE_TAUS, ntaus);
+  x.wl += (unsigned)nscanned;
+  STAMP(x, 2);
+  if (done) S.edist = result;
+  return done;
 }
 
 // rpkt.cc:557-621 + radfield.cc:831-876
@@ -1086,57 +1149,72 @@ DEVFN void rlc_emiss_rpkt(const Ctx &K, const Pkt &p, double dist) {
   }
 }
 
-// rpkt.cc:623-813
-template <typename Cold = ColdFull>
-DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
+// rpkt.cc:623-700: the step's draw, boundary and the cases without a line walk; RSTEP_WALK when get_event's walk is
+// set up in S, RSTEP_END when the step's end can run (rpkt_step_finish), RSTEP_DONE after an error
+DEVFN int rpkt_step_begin(Tx &x, Pkt &p, double t2, RStep &S) {
   const Ctx &K = x.K;
   const int npm = K.G.npts_model;
-  int mgi = cell_mgi(K, p.where);
-  const int oldmgi = mgi;
+  S.mgi = cell_mgi(K, p.where);
+  S.oldmgi = S.mgi;
   lwork(x.L, WK_RPKT_STEPS, 1);
   const double zrand = artis_rng_uniform_pos(&x.rng);
   const double tau_next = -1. * log(zrand);
-  int snext = -1;
-  double sdist = boundary_cross(x, p, &snext);
+  S.snext = -1;
+  S.sdist = boundary_cross(x, p, &S.snext);
   STAMP(x, 0);
+  S.cross0 = (S.sdist == 0);
+  S.find_nextline = false;
+  S.eventtype = -1;
+  if (S.cross0) return RSTEP_END;
+  const double maxsdist = K.G.rmax * p.prop_time / K.G.tmin;
+  if (S.sdist > maxsdist) {
+    x.err(ERR_SDIST, p.number, p.where);
+    return RSTEP_DONE;
+  }
+  if (((S.snext != -99) && (S.snext < 0)) || (S.snext >= K.G.ngrid)) {
+    x.err(ERR_BADCELL, p.number, S.snext);
+    return RSTEP_DONE;
+  }
+  if (S.sdist > K.R.max_path_step) {
+    S.sdist = K.R.max_path_step;
+    S.snext = p.where;
+  }
+  S.tdist = (t2 - p.prop_time) * ARTIS_CLIGHT_PROP;
+  S.kap.nu = 0.;
+  S.kap.total = S.kap.es = S.kap.ff = S.kap.bf = S.kap.ffheating = 0.;
+  const int mgi = S.mgi;
+  S.k = (mgi == npm) ? -1 : K.C.ne_index[mgi];
+  if (mgi == npm) {
+    S.edist = DBL_MAX;
+    S.find_nextline = true;
+    return RSTEP_END;
+  }
+  if (K.C.thick[mgi] == 1) {
+    // grey optically thick cell: electron scattering only (rpkt.cc:697-703); no continuum opacity is evaluated,
+    // so the estimator terms of this step use kappa = 0 (deviation D7)
+    const double kappa = K.C.kappagrey[mgi] * K.C.rho[mgi] * doppler_packet(K, p);
+    S.edist = (tau_next - 0.0) / kappa;
+    S.find_nextline = true;
+    return RSTEP_END;
+  }
+  if (get_event_begin(x, S.k, mgi, p, S, tau_next, fmin(S.tdist, S.sdist))) return RSTEP_WALK;
+  return x.ok ? RSTEP_END : RSTEP_DONE;
+}
+
+// rpkt.cc:700-813: the end of the step from S (the event distance and type, or the immediate cell change)
+template <typename Cold>
+DEVFN bool rpkt_step_finish(Tx &x, Pkt &p, double t2, RStep &S, const Cold &cold) {
+  const Ctx &K = x.K;
+  const int npm = K.G.npts_model;
+  int mgi = S.mgi;
+  const int oldmgi = S.oldmgi;
   // One inlined copy each of the cell change and of the move / estimator / move sequence, shared by the ways a
   // step ends (the register pressure of k_rpkt grows with every inlined copy): cross = change cell (sdist == 0
   // at once, or a step that ends on the boundary of another cell), boundary_step = the step ended on the boundary.
-  bool cross = (sdist == 0), boundary_step = false, find_nextline = false;
+  bool cross = S.cross0, boundary_step = false;
+  const bool find_nextline = S.find_nextline;
   if (!cross) {
-    const double maxsdist = K.G.rmax * p.prop_time / K.G.tmin;
-    if (sdist > maxsdist) {
-      x.err(ERR_SDIST, p.number, p.where);
-      return false;
-    }
-    if (((snext != -99) && (snext < 0)) || (snext >= K.G.ngrid)) {
-      x.err(ERR_BADCELL, p.number, snext);
-      return false;
-    }
-    if (sdist > K.R.max_path_step) {
-      sdist = K.R.max_path_step;
-      snext = p.where;
-    }
-    const double tdist = (t2 - p.prop_time) * ARTIS_CLIGHT_PROP;
-    double edist;
-    int rpkt_eventtype = -1;
-    Kappa kap;
-    kap.nu = 0.;
-    kap.total = kap.es = kap.ff = kap.bf = kap.ffheating = 0.;
-    const int k = (mgi == npm) ? -1 : K.C.ne_index[mgi];
-    if (mgi == npm) {
-      edist = DBL_MAX;
-      find_nextline = true;
-    } else if (K.C.thick[mgi] == 1) {
-      // grey optically thick cell: electron scattering only (rpkt.cc:697-703); no continuum opacity is evaluated,
-      // so the estimator terms of this step use kappa = 0 (deviation D7)
-      const double kappa = K.C.kappagrey[mgi] * K.C.rho[mgi] * doppler_packet(K, p);
-      edist = (tau_next - 0.0) / kappa;
-      find_nextline = true;
-    } else {
-      edist = get_event(x, k, mgi, p, kap, &rpkt_eventtype, tau_next, fmin(tdist, sdist));
-      if (!x.ok) return false;
-    }
+    const double sdist = S.sdist, tdist = S.tdist, edist = S.edist;
     if (!(edist >= 0)) {
       x.err(ERR_EDIST, p.number, 0);
       return false;
@@ -1158,7 +1236,7 @@ DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
       return false;
     }
     move_pkt_withtime(K, p, dist / 2.);
-    update_estimators(x, p, kap, dist);
+    update_estimators(x, p, S.kap, dist);
     if (K.R.do_rlc_est == 1 || K.R.do_rlc_est == 2) rlc_emiss_rpkt(K, p, dist);
     if (which == 2) {
       p.prop_time = t2;
@@ -1170,13 +1248,14 @@ DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
     move_pkt_withtime(K, p, dist / 2.);
     STAMP(x, 3);
     if (which == 1) {
+      const int k = S.k;
       if (K.C.thick[mgi] == 1)
         cold(x, p, [&](Tx &tx, Pkt &tp) { rpkt_event_thickcell(tx, tp); });
-      else if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_BB)
+      else if (S.eventtype == ARTIS_RPKT_EVENTTYPE_BB)
         rpkt_event_boundbound(x, p);
-      else if (rpkt_eventtype == ARTIS_RPKT_EVENTTYPE_CONT)
+      else if (S.eventtype == ARTIS_RPKT_EVENTTYPE_CONT)
         cold(x, p, [&](Tx &tx, Pkt &tp) {
-          const Kappa kc = kap;
+          const Kappa kc = S.kap;
           rpkt_event_continuum(tx, tp, kc, k, mgi);
         });
       else
@@ -1184,10 +1263,10 @@ DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
       return (x.ok && p.type == ARTIS_TYPE_RPKT && (mgi == npm || mgi == oldmgi));
     }
     boundary_step = true;
-    cross = (snext != p.where);
+    cross = (S.snext != p.where);
   }
   if (cross) {
-    change_cell(x, p, snext);
+    change_cell(x, p, S.snext);
     mgi = cell_mgi(K, p.where);
   }
   if (boundary_step) {
@@ -1198,6 +1277,18 @@ DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
     }
   }
   return (p.type == ARTIS_TYPE_RPKT && (mgi == npm || mgi == oldmgi));
+}
+
+// rpkt.cc:623-813, the whole step; true while the packet stays an r-packet in the same cell
+template <typename Cold = ColdFull>
+DEVFN bool do_rpkt_step(Tx &x, Pkt &p, double t2, const Cold &cold = Cold()) {
+  RStep S;
+  int r = rpkt_step_begin(x, p, t2, S);
+  if (r == RSTEP_WALK) {
+    get_event_walk(x, p, S, 1 << 30);
+    r = x.ok ? RSTEP_END : RSTEP_DONE;
+  }
+  return r == RSTEP_END ? rpkt_step_finish(x, p, t2, S, cold) : false;
 }
 
 // ------------------------------------------------------------------------------------------ fb emission
@@ -1697,14 +1788,17 @@ DEVFN int ma_coop_apply(const Ctx &K, const LocalCounters &L, artis_rng &rng, Ma
 }
 
 // where a step reads record keys (high halves): k_ma's staged line, or the whole record in global memory
+template <bool HI_ONLY>
 struct KeysLds {
   lds_uint4 *line;
   int pl;
+  DEVFN bool hi_only(const Ctx &) const { return HI_ONLY; }  // (level mode, the COOP instance of k_ma)
   DEVFN bool has(int p) const { return (p >> 6) == pl; }
   DEVFN uint32_t hi(int p) const { return (uint32_t)((lds_u16 *)(line + ((p & 63) >> 3) * 64))[p & 7]; }
 };
 struct KeysGlobal {
   const uint16_t *rec;
+  DEVFN bool hi_only(const Ctx &K) const { return K.C.ma_hi_only != 0; }
   DEVFN bool has(int) const { return true; }
   DEVFN uint32_t hi(int p) const { return (uint32_t)gload(rec + p); }
 };
@@ -1741,7 +1835,7 @@ DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
   auto cmp = [&](int p, uint32_t hi, double q, uint32_t qh) -> int {
     if (hi < qh) return -1;
     if (hi > qh + 1) return 1;
-    if (K.C.ma_hi_only) return 0;  // level-mode records hold the high halves only: undecided -> exact jump
+    if (keys.hi_only(K)) return 0;  // level-mode records hold the high halves only: undecided -> exact jump
     return ma_key_cmp((hi << 16) | (uint32_t)gload(rec + lay.hot + p), q);
   };
   if (m.sel < 0) {  // a new jump: the action is the first of the 9 running-sum keys (line 0) above q
@@ -1834,7 +1928,7 @@ DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
       return MA_PENDING;
     }
     probes++;
-    const int c = K.C.ma_hi_only ? 0 : ma_key_cmp((h << 16) | (uint32_t)gload(rec + lay.hot + p), m.q2);
+    const int c = keys.hi_only(K) ? 0 : ma_key_cmp((h << 16) | (uint32_t)gload(rec + lay.hot + p), m.q2);
     if (c == 0) {
       m.ntrans += probes;
       m.jumps--;

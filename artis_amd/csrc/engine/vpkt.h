@@ -95,6 +95,12 @@ struct VLane {
   double tau[VPKT_MAX_SPECTRA];
   double I, Q, U, pn, t_future;
   int mgi, cells;
+  // a line walk in progress over a coefficient row (resumed by the next pass): the segment's boundary distance and
+  // next cell, the last line distance, the staged window (its lines' masks; the values are in the lane's LDS column)
+  bool inlines;
+  int snext, pf_base;
+  double sdist, ldist;
+  uint64_t wm;
 };
 
 // rlc_emiss_vpkt prologue (vpkt.cc:93-193): the dummy packet, its Stokes vector and weight p_n
@@ -162,6 +168,7 @@ DEVFN void vpkt_trace_init(const Ctx &K, const LocalCounters &L, VLane &v) {
   v.mgi = cell_mgi(K, d.where);
   v.t_future = t_current;
   v.cells = 0;
+  v.inlines = false;
 }
 
 // the escape branch of rlc_emiss_vpkt (vpkt.cc:314-367)
@@ -191,7 +198,12 @@ DEVFN void vpkt_trace_finish(const Ctx &K, VLane &v) {
   }
 }
 
-enum { VSEG_CONTINUE = 0, VSEG_ESCAPED = 1, VSEG_KILLED = 2 };
+enum { VSEG_CONTINUE = 0, VSEG_ESCAPED = 1, VSEG_KILLED = 2, VSEG_PENDING = 3 };
+// lines a lane walks per pass of k_vpkt before the wave moves on (the walk resumes next pass): the lanes' walks
+// differ in length by orders of magnitude, and an unbounded walk holds the wave for its longest lane
+#ifndef VPKT_LINES_PER_PASS
+#define VPKT_LINES_PER_PASS 16
+#endif
 
 // the end of a pass of rlc_emiss_vpkt's cell loop: move to the cell boundary and into the next cell (vpkt.cc:296-312)
 DEVFN int vpkt_segment_end(Tx &x, VLane &v, double sdist, int snext) {
@@ -212,41 +224,17 @@ DEVFN int vpkt_segment_end(Tx &x, VLane &v, double sdist, int snext) {
   return end_packet ? VSEG_ESCAPED : VSEG_CONTINUE;
 }
 
-// one pass of rlc_emiss_vpkt's cell loop (vpkt.cc:195-312); deviation D9 for the line loop
+// the line walk of a cell without a coefficient row (population gathers), whole within one pass
 template <int PF>
-DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
+DEVFN int vpkt_gather_walk(Tx &x, VLane &v, unsigned long long &lines, double lnu_first, double lnu_last) {
   const Ctx &K = x.K;
   const DevVpkt &V = K.V;
   Pkt &d = v.d;
   const double t_current = v.t_current;
+  const double sdist = v.sdist;
+  const int snext = v.snext;
   double ldist = 0;
-  int snext = -1;
-  const double sdist = boundary_cross(x, d, &snext);
-  if (((snext != -99) && (snext < 0)) || (snext >= K.G.ngrid)) {
-    x.err(ERR_BADCELL, -1, snext);
-    return VSEG_KILLED;
-  }
-  const double tf = v.t_future;
-  const double s_cont = sdist * t_current * t_current * t_current / (tf * tf * tf);
-  Kappa kap;
-  calculate_kappa_rpkt_cont(x, d, K.C.ne_index[v.mgi], v.mgi, kap);
-  const double kap_cont = kap.total;
-  const double kap_cont_nobf = kap_cont - kap.bf;
-  const double kap_cont_noff = kap_cont - kap.ff;
-  const double kap_cont_noes = kap_cont - kap.es;
-  for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++) {
-    if (ind >= V.nspectra) break;
-    const double ex = V.exclude[ind];
-    if (ex == -2)
-      v.tau[ind] += kap_cont_nobf * s_cont;
-    else if (ex == -3)
-      v.tau[ind] += kap_cont_noff * s_cont;
-    else if (ex == -4)
-      v.tau[ind] += kap_cont_noes * s_cont;
-    else
-      v.tau[ind] += kap_cont * s_cont;
-  }
-  if (!vpkt_alive(V, v.tau)) return VSEG_KILLED;
+  int pf_base = -(1 << 20);
   const double *pops = K.C.pops + (int64_t)K.C.ne_index[v.mgi] * K.T.nlevels_total;
   bool anyex = false;
   for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
@@ -254,65 +242,6 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
   // As in get_event: the line records, the two populations each needs and (with element exclusions) the line's
   // atomic number are fetched PF consecutive lines at a time, all loads independent, so the walk waits for memory
   // twice per PF lines instead of three to four times per line.  The tau sums are unchanged.
-  int pf_base = -(1 << 20);
-  const double lnu_first = K.T.line_nu[0], lnu_last = K.T.line_nu[max(K.T.nlines - 1, 0)];
-  if (K.C.ne_index[v.mgi] < K.C.linecoef_rows) {
-    // over the per-cell Sobolev coefficients (DevCells::linecoef, as get_event): an aligned window of LC_WIN lines'
-    // frequencies and coefficients is staged in the lane's LDS column (eight independent 16-byte loads, as k_rpkt),
-    // so a line reads its two values with two LDS loads instead of selecting them out of 32 registers;
-    // dtau = coefficient * t_line is the reference's (B_lu n_l - B_ul n_u) * HCLIGHTOVERFOURPI * t_line in the same
-    // operation order.  vpkt_alive (vpkt.cc:293) is tested when the walk leaves a window and when it ends, not after
-    // every line: the tau only grow, so a virtual packet that dies inside a window is still dead there and is killed
-    // the same; only the lines added after its death (diagnostic count) differ from the reference's loop.
-    const int nlines = K.T.nlines;
-    const double *lnu = K.T.line_nu, *nu8 = K.T.line_nu8;
-    const double *crow = K.C.linecoef + (int64_t)K.C.ne_index[v.mgi] * K.C.linecoef_stride;
-    const uint8_t *lmask = V.line_mask;
-    const int nspec = V.nspectra;
-    const double tau_max = V.tau_max;
-    __attribute__((address_space(3))) double *win = x.win;
-    uint64_t wm = 0;  // the window's 8 line masks
-    auto all_dead = [&]() {
-      int dead = 0;
-#pragma unroll
-      for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
-        if (ind < nspec && v.tau[ind] > tau_max) dead++;
-      return dead == nspec;
-    };
-    while (ldist < sdist) {
-      const int lineindex = closest_transition(nlines, lnu, d.nu_cmf, d.next_trans, lnu_first, lnu_last);
-      if (lineindex < 0) {
-        d.next_trans = nlines + 1;
-        break;  // D9
-      }
-      if ((unsigned)(lineindex - pf_base) >= (unsigned)LC_WIN) {
-        if (pf_base >= 0 && all_dead()) return VSEG_KILLED;
-        pf_base = lineindex & ~(LC_WIN - 1);
-        lc_window(nu8 + pf_base, crow + pf_base, win);
-        wm = *(const __attribute__((address_space(1))) uint64_t *)(lmask + pf_base);
-      }
-      const int pj = lineindex - pf_base;
-      const double nutrans = win[pj * WAVE_BLOCK_T];
-      const unsigned lm = (unsigned)(wm >> (8 * pj)) & 0xffu;
-      d.next_trans = lineindex + 1;
-      if (d.nu_cmf < nutrans)
-        ldist = 0;
-      else
-        ldist = ARTIS_CLIGHT * t_current * (d.nu_cmf / nutrans - 1);
-      if (ldist > sdist) {
-        d.next_trans -= 1;
-        break;
-      }
-      lines++;
-      const double t_line = t_current + ldist / ARTIS_CLIGHT;
-      const double dtau = win[(LC_WIN + pj) * WAVE_BLOCK_T] * t_line;
-#pragma unroll
-      for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
-        if ((lm >> ind) & 1u) v.tau[ind] += dtau;
-    }
-    if (all_dead()) return VSEG_KILLED;
-    return vpkt_segment_end(x, v, sdist, snext);
-  }
   if constexpr (PF == 0) {  // launched only when every non-empty cell has a coefficient row
     x.err(ERR_UNSUPPORTED_TYPE, -1, 7);
     return VSEG_KILLED;
@@ -380,6 +309,136 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
   }
 }
 
+// one pass of rlc_emiss_vpkt's cell loop (vpkt.cc:195-312); deviation D9 for the line loop.  Over a coefficient
+// row the line walk is resumable: it stops after VPKT_LINES_PER_PASS lines (VSEG_PENDING) and the next call continues
+// it; the segment's start (boundary, continuum) runs only when no walk is in progress.
+template <int PF>
+DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
+  const Ctx &K = x.K;
+  const DevVpkt &V = K.V;
+  Pkt &d = v.d;
+  const double t_current = v.t_current;
+  const double lnu_first = K.T.line_nu[0], lnu_last = K.T.line_nu[max(K.T.nlines - 1, 0)];
+  const int nspec = V.nspectra;
+  const double tau_max = V.tau_max;
+  auto all_dead = [&]() {
+    int dead = 0;
+#pragma unroll
+    for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
+      if (ind < nspec && v.tau[ind] > tau_max) dead++;
+    return dead == nspec;
+  };
+  if (!v.inlines) {
+    int snext = -1;
+    const double sdist = boundary_cross(x, d, &snext);
+    if (((snext != -99) && (snext < 0)) || (snext >= K.G.ngrid)) {
+      x.err(ERR_BADCELL, -1, snext);
+      return VSEG_KILLED;
+    }
+    const double tf = v.t_future;
+    const double s_cont = sdist * t_current * t_current * t_current / (tf * tf * tf);
+    Kappa kap;
+    calculate_kappa_rpkt_cont(x, d, K.C.ne_index[v.mgi], v.mgi, kap);
+    const double kap_cont = kap.total;
+    const double kap_cont_nobf = kap_cont - kap.bf;
+    const double kap_cont_noff = kap_cont - kap.ff;
+    const double kap_cont_noes = kap_cont - kap.es;
+    for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++) {
+      if (ind >= V.nspectra) break;
+      const double ex = V.exclude[ind];
+      if (ex == -2)
+        v.tau[ind] += kap_cont_nobf * s_cont;
+      else if (ex == -3)
+        v.tau[ind] += kap_cont_noff * s_cont;
+      else if (ex == -4)
+        v.tau[ind] += kap_cont_noes * s_cont;
+      else
+        v.tau[ind] += kap_cont * s_cont;
+    }
+    if (!vpkt_alive(V, v.tau)) return VSEG_KILLED;
+    v.sdist = sdist;
+    v.snext = snext;
+    v.ldist = 0.;
+    v.pf_base = -(1 << 20);
+    v.wm = 0;
+    if (K.C.ne_index[v.mgi] < K.C.linecoef_rows) {
+      v.inlines = true;
+    } else {
+      return vpkt_gather_walk<PF>(x, v, lines, lnu_first, lnu_last);
+    }
+  }
+  {
+    // over the per-cell Sobolev coefficients (DevCells::linecoef, as get_event): an aligned window of LC_WIN lines'
+    // frequencies and coefficients is staged in the lane's LDS column (eight independent 16-byte loads, as k_rpkt),
+    // so a line reads its two values with two LDS loads instead of selecting them out of 32 registers;
+    // dtau = coefficient * t_line is the reference's (B_lu n_l - B_ul n_u) * HCLIGHTOVERFOURPI * t_line in the same
+    // operation order.  vpkt_alive (vpkt.cc:293) is tested when the walk leaves a window and when it ends, not after
+    // every line: the tau only grow, so a virtual packet that dies inside a window is still dead there and is killed
+    // the same; only the lines added after its death (diagnostic count) differ from the reference's loop.
+    const int nlines = K.T.nlines;
+    const double *lnu = K.T.line_nu, *nu8 = K.T.line_nu8;
+    const double *crow = K.C.linecoef + (int64_t)K.C.ne_index[v.mgi] * K.C.linecoef_stride;
+    const uint8_t *lmask = V.line_mask;
+    __attribute__((address_space(3))) double *win = x.win;
+    const double sdist = v.sdist;
+    double ldist = v.ldist;
+    int pf_base = v.pf_base;
+    uint64_t wm = v.wm;
+    int budget = VPKT_LINES_PER_PASS;
+    bool done = false;
+    while (true) {
+      if (!(ldist < sdist)) {
+        done = true;
+        break;
+      }
+      if (budget-- == 0) break;  // resume next pass
+      const int lineindex = closest_transition(nlines, lnu, d.nu_cmf, d.next_trans, lnu_first, lnu_last);
+      if (lineindex < 0) {
+        d.next_trans = nlines + 1;
+        done = true;
+        break;  // D9
+      }
+      if ((unsigned)(lineindex - pf_base) >= (unsigned)LC_WIN) {
+        if (pf_base >= 0 && all_dead()) {
+          v.inlines = false;
+          return VSEG_KILLED;
+        }
+        pf_base = lineindex & ~(LC_WIN - 1);
+        lc_window(nu8 + pf_base, crow + pf_base, win);
+        wm = *(const __attribute__((address_space(1))) uint64_t *)(lmask + pf_base);
+      }
+      const int pj = lineindex - pf_base;
+      const double nutrans = win[pj * WAVE_BLOCK_T];
+      const unsigned lm = (unsigned)(wm >> (8 * pj)) & 0xffu;
+      d.next_trans = lineindex + 1;
+      if (d.nu_cmf < nutrans)
+        ldist = 0;
+      else
+        ldist = ARTIS_CLIGHT * t_current * (d.nu_cmf / nutrans - 1);
+      if (ldist > sdist) {
+        d.next_trans -= 1;
+        done = true;
+        break;
+      }
+      lines++;
+      const double t_line = t_current + ldist / ARTIS_CLIGHT;
+      const double dtau = win[(LC_WIN + pj) * WAVE_BLOCK_T] * t_line;
+#pragma unroll
+      for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
+        if ((lm >> ind) & 1u) v.tau[ind] += dtau;
+    }
+    if (!done) {
+      v.ldist = ldist;
+      v.pf_base = pf_base;
+      v.wm = wm;
+      return VSEG_PENDING;
+    }
+    v.inlines = false;
+    if (all_dead()) return VSEG_KILLED;
+    return vpkt_segment_end(x, v, sdist, v.snext);
+  }
+}
+
 // all (spawn, observer) work items of the spawn buffer; spawn_ctr[1] is the fetch head
 template <int PF, int MINW>
 __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict__ ctxp, int refill_min) {
@@ -399,6 +458,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
   const uint64_t nitems = (uint64_t)nspawn * (uint64_t)V.nobs;
   VLane v;
   v.tracing = false;
+  v.inlines = false;
   bool have = false, drained = false;
   unsigned long long lines = 0;
   const int64_t cap = V.cap;
@@ -453,7 +513,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
         }
       } else {
         const int r = vpkt_trace_segment<PF>(x, v, lines);
-        if (r != VSEG_CONTINUE) {
+        if (r != VSEG_CONTINUE && r != VSEG_PENDING) {
           if (r == VSEG_ESCAPED) vpkt_trace_finish(K, v);
           v.tracing = false;
         }

@@ -154,7 +154,14 @@ __global__ void k_classify(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *
   block_counters_flush(K, s_ctr, s_work);
 }
 
-// r-packets: persistent lanes, one do_rpkt_step per loop pass
+// lines of get_event's walk a k_rpkt lane advances per pass; 0: whole steps (do_rpkt_step).  Measured at 2e6
+// packets (profiles/r4_ab.txt): whole steps 164 ms of k_rpkt per step, 16 lines per pass 186 ms, 8 or 32 no better --
+// the state a resumable walk keeps across passes costs more in spills than the divergence it removes
+#ifndef RPKT_LINES_PER_PASS
+#define RPKT_LINES_PER_PASS 0
+#endif
+
+// r-packets: persistent lanes, one r-packet step (or part of its line walk) per loop pass
 template <int MINW>
 __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa, int64_t n,
                                                      int nts, double t2) {
@@ -174,6 +181,8 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
   x.defer_est = true;
   const uint32_t nq = W.ctr[2 * QR];
   Pkt p;
+  RStep S;
+  bool walking = false;
   int32_t idx = -1;
   bool have = false, drained = false, pendM = false, pendK = false, pendR = false;
   int steps = 0;
@@ -223,12 +232,32 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
     x.tlast = ts0;
 #endif
     if (have) {
+      // a step starts when no walk is in progress; get_event's walk advances at most RPKT_LINES_PER_PASS lines per
+      // pass (a lane with a long walk no longer holds its wave while the others' short steps wait)
+      int r = -1;
+#if RPKT_LINES_PER_PASS > 0
+      if (!walking && !x.vstop && x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
+        r = rpkt_step_begin(x, p, t2, S);
+        walking = (r == RSTEP_WALK);
+      }
+      if (walking && get_event_walk(x, p, S, RPKT_LINES_PER_PASS)) {
+        walking = false;
+        r = x.ok ? RSTEP_END : RSTEP_DONE;
+      }
+      if (r == RSTEP_END) rpkt_step_finish(x, p, t2, S, ColdSoa{soa, n, idx});
+#else
       if (!x.vstop && x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
         do_rpkt_step(x, p, t2, ColdSoa{soa, n, idx});
+        r = RSTEP_DONE;
+      }
+#endif
+      if (r == RSTEP_END || r == RSTEP_DONE) {
         STAMP(x, 4);
         if (++steps > RPKT_MAX_STEPS) x.err(ERR_STUCK, p.number, 1);
       }
-      if (x.vstop && x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
+      if (walking) {
+        // (the step continues next pass)
+      } else if (x.vstop && x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
         // its spawn went to an overflow record: park the packet (between steps) for the resumed launch
         pkt_store_hot(soa, n, idx, p);
         W.rng_n[idx] = x.rng.n;
@@ -522,10 +551,19 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     MaEnd e;
     int r = MA_PENDING;
     if (have && !unc) {
-      r = ma_step_cached(K, L, rng, mc, e, (int)rng.key1, KeysLds{line, mc.pline}, meta, z1, z2);
+      r = ma_step_cached(K, L, rng, mc, e, (int)rng.key1, KeysLds<COOP && ARTIS_MA_HI_ONLY>{line, mc.pline}, meta,
+                         z1, z2);
 #ifdef ARTIS_STAMPS
       ts2 = wave_clock();
 #endif
+    }
+    // level mode: a jump the high key halves cannot decide is made by the wave below from the exact sums, with the
+    // lane's RNG counter back at the start of the jump (the same draws z1, z2), not parked for k_ma_exact
+    bool unc_now = unc;
+    if (COOP && r == MA_DEFER) {
+      rng.n = mc.n0;
+      unc_now = true;
+      r = MA_PENDING;
     }
     // level mode: the jumps of the lanes without a record, each made by the whole wave (wave-uniform loop)
     if constexpr (COOP) {
@@ -533,12 +571,12 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
       // abort) is applied at once, a transition action waits for the wave's search of its list
       int csel = MA_COOP_RANDOM;
       double cx = 0.;
-      if (unc) {
+      if (unc_now) {
         csel = ma_coop_action(K, mc.k, mc.ul, z1, z2, &cx);
         if (!ma_coop_needs_search(csel)) r = ma_coop_apply(K, L, rng, mc, e, (int)rng.key1, csel, -1, 0u, meta);
       }
       // (a rotating start, so that with coop_max < 64 every waiting lane gets its turn)
-      unsigned long long um = __ballot(unc && ma_coop_needs_search(csel));
+      unsigned long long um = __ballot(unc_now && ma_coop_needs_search(csel));
       const int rot = (int)(st_pass & 63);
       um = (um >> rot) | (rot ? um << (64 - rot) : 0ull);
       for (int done_coop = 0; um && done_coop < W.coop_max; um &= um - 1, done_coop++) {

@@ -22,7 +22,9 @@ cmd=$1
 shift
 
 run_tests() {
-  timeout -k 10 900 python -u -m pytest ${@:-tests} -m gpu -x -v --timeout 300 --timeout-method thread \
+  local args=("$@")
+  [ ${#args[@]} -eq 0 ] && args=(tests)
+  timeout -k 10 900 python -u -m pytest "${args[@]}" -m gpu -x -v --timeout 300 --timeout-method thread \
     > "$O/gpu_tests.log" 2>&1
   local rc=$?
   tail -1 "$O/gpu_tests.log"
