@@ -562,6 +562,10 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     bool unc_now = unc;
     if (COOP && r == MA_DEFER) {
       rng.n = mc.n0;
+      // (a search that began in an earlier pass has no draws computed in this one)
+      artis_rng r2 = rng;
+      z1 = artis_rng_uniform(&r2);
+      z2 = artis_rng_uniform(&r2);
       unc_now = true;
       r = MA_PENDING;
     }
