@@ -221,7 +221,7 @@ class Engine:
         w = np.zeros(11, dtype=np.int64)
         self._check(self.lib.artis_gpu_table_info(w.ctypes.data), "table_info")
         return dict(zip(("cells", "linecoef_rows", "linecoef_bytes", "macache_rows", "macache_bytes",
-                         "marates_bytes", "ma_jumps_sampled_recorded", "ma_jumps_sampled", "ma_level_records",
+                         "marates_bytes", "ma_jumps_recorded", "ma_jumps", "ma_level_records",
                          "ma_level_bytes", "ma_pool_bytes"), (int(x) for x in w)))
 
     def spectrum(self, nnubins=1000, nprocs=1):

@@ -412,6 +412,15 @@ __global__ __launch_bounds__(256) void k_lvl_buckets(Ctx K, const uint32_t *__re
     if (s[j]) atomicAdd(&out[j], s[j]);
 }
 
+// after a placement: the counts decay by half (rounded up, so a pair walked once keeps its place at the end of the
+// queue): pairs walked in earlier transports keep a claim on the pool, pairs walked often keep the front
+__global__ __launch_bounds__(256) void k_lvl_decay(uint32_t *__restrict__ hist, int64_t npairs) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = hist[i];
+    if (c) hist[i] = (c >> 1) + (c & 1u);
+  }
+}
+
 // k_lvl_select: the new DevCells::ma_lptr and the list of records to build.  have_hist == 0 (no transport yet):
 // whole cells in nonempty-index order (centre outwards), pair (k, ul) at line k * row_lines + rl_off[ul] while it
 // fits the pool.  Otherwise: density bucket above bt, or bucket bt while `rest` lines of it last.
@@ -762,6 +771,7 @@ struct Engine {
   hipEvent_t ev_round[2] = {nullptr, nullptr};
   int wave_grid = 2048;
   bool use_megakernel = false;
+  bool ma_level_coop = false;  // level mode: k_ma makes the jumps without a record itself (else k_ma_exact)
   Ctx *d_ctx = nullptr;           // device copy of K for the transport kernels
   int ma_occ = 1;                 // k_ma minimum waves per SIMD (launch bounds): 1 or 8
   uint32_t *d_binoffs = nullptr;  // exclusive prefix sums of W.bins
@@ -868,8 +878,6 @@ int ma_level_place() {
     HIPCHK(hipStreamSynchronize(G.stream));
     // h[0]: sampled jumps on pairs with a record, h[1]: all, h[2 + b]: pool lines wanted per density bucket b
     if (h[1] == 0) return 0;  // no walk since the last placement: keep it (its list rebuilds the records)
-    G.ma_acts_cached = (int64_t)h[0];
-    G.ma_acts_total = (int64_t)h[1];
     uint64_t cum = 0;
     bt = -1;  // (everything fits)
     for (int b = MA_LVL_NB - 1; b >= 0; b--) {
@@ -887,7 +895,7 @@ int ma_level_place() {
                                        G.ma_lhist_ready ? 1 : 0);
   uint32_t c[4];
   HIPCHK(hipMemcpyAsync(c, G.d_lvl_ctr, sizeof c, hipMemcpyDeviceToHost, G.stream));
-  HIPCHK(hipMemsetAsync(G.d_ma_lhist, 0, npairs * sizeof(uint32_t), G.stream));
+  k_lvl_decay<<<nb, B, 0, G.stream>>>(G.d_ma_lhist, npairs);
   HIPCHK(hipStreamSynchronize(G.stream));
   G.ma_level_lines = c[0];
   G.ma_level_records = std::min<int64_t>(c[1], G.build_list_cap);
@@ -1325,11 +1333,16 @@ int run_wavefront(int64_t n, int nts, double t2) {
     }();
     const unsigned ma_grid = ma_waves ? (unsigned)(G.wave_grid / 8 * ma_waves) : grid;
     if (G.K.C.ma_level_mode)
-      k_ma<4, true><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+      // (the whole-cell placement before the first transport covers few of the pairs walked: those walks would
+      // take a round per parked jump, so the first transport makes its exact-sum jumps inline)
+      if (G.ma_level_coop || first_placement)
+        k_ma<4, true, true><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+      else
+        k_ma<8, false, true><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
     else if (G.ma_occ == 8)
-      k_ma<8, false><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+      k_ma<8, false, false><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
     else
-      k_ma<1, false><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+      k_ma<1, false, false><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
     TEND(1);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QM, 0, 2 * sizeof(uint32_t), G.stream));
     {  // jumps the 32-bit keys could not decide (rare), exact; walks go back to M
@@ -2942,6 +2955,10 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     G.ma_occ = (oc && oc[0] == '8') ? 8 : 1;
     const char *cm = getenv("ARTIS_GPU_MA_COOP_MAX");
     G.W.coop_max = cm ? std::max(1, std::min(64, atoi(cm))) : 64;
+    // level mode: the jumps without a record made inline by k_ma's wave (ARTIS_GPU_MA_LEVEL_COOP=1), or parked
+    // for k_ma_exact (default: k_ma keeps the row kernel's register budget)
+    const char *lc = getenv("ARTIS_GPU_MA_LEVEL_COOP");
+    G.ma_level_coop = lc && lc[0] == '1';
   }
   G.params = *rp;
   G.h_anumber.assign(a->nelements, 0);
@@ -3839,6 +3856,14 @@ int artis_gpu_update_packets_resident(int my_rank, int nts) {
   unsigned long long w[ARTIS_WORK_COUNT];
   HIPCHK(hipMemcpy(w, G.K.E.work, sizeof(w), hipMemcpyDeviceToHost));
   for (int k = 0; k < ARTIS_WORK_COUNT; k++) G.last_work[k] = (int64_t)w[k];
+  if (G.K.C.ma_level_mode && n > 0 && !G.use_megakernel) {
+    // level mode: the last transport's jumps, and those made from a record (all but the wave's exact-sum jumps,
+    // WaveState::stats[45])
+    unsigned long long coop = 0;
+    HIPCHK(hipMemcpy(&coop, G.W.stats + 45, sizeof(coop), hipMemcpyDeviceToHost));
+    G.ma_acts_total = (int64_t)w[WK_MA_JUMPS];
+    G.ma_acts_cached = (int64_t)w[WK_MA_JUMPS] - (int64_t)coop;
+  }
   return check_kernel_error("update_packets");
 }
 

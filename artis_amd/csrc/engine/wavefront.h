@@ -10,8 +10,8 @@
 //   k_ma   : macro-atom jumps (macroatom.cc:416-482) on a 4-word lane state; never touches the packet record
 //   k_kpkt : k-packet cooling (kpkt.cc:477-797) -> r-packet (R queue) or macro-atom (M queue)
 //
-// A macro-atom's deactivation (emission direction, fb frequency, estimator terms) is deferred to the kernel
-// the packet moves to, which loads the full record anyway (ma_finish).  Every packet keeps its own RNG stream
+// A macro-atom's deactivation (emission direction, fb frequency, estimator terms) is deferred to k_ma_finish,
+// which loads the whole packet record (ma_finish_inl) and queues it as an r- or k-packet.  Every packet keeps its own RNG stream
 // (draw counter in rng_n), so the sequence of draws -- and hence every result -- is identical to the
 // megakernel and the CPU oracle.
 //
@@ -47,9 +47,10 @@ struct WaveState {
   // cell-sorted macro-atom tickets written by k_ma_scatter when the key cache is on (else nullptr): per slot
   // {packet index, unique level, record offset, nonempty cell}, {packet number, RNG counter, jumps so far, 0}
   int4 *ma_tick;       // [2N]
-  unsigned long long *stats;  // [32] diagnostics: per kernel class c: [4c] wave loop passes, [4c+1] busy
+  unsigned long long *stats;  // [48] diagnostics: per kernel class c: [4c] wave loop passes, [4c+1] busy
                               // lane-passes, [4c+2] wave cycles (s_memtime), [4c+3] refills;
-                              // [16 + 4c] cycles in refill blocks, [17 + 4c] cycles in the work step
+                              // [16 + 4c] cycles in refill blocks, [17 + 4c] cycles in the work step; [40] exact
+                              // jumps (k_ma_exact), [45] level mode: jumps made by the wave from the exact sums
 };
 
 DEVFN int lane_id() { return (int)__lane_id(); }
@@ -411,7 +412,9 @@ __global__ void k_ma_scatter(const Ctx *__restrict__ ctxp, WaveState W, const ui
 // LDS by the wave's cooperative fetch); a lane without one (level mode, DevCells::ma_lptr) has its jump made by
 // the whole wave after the cached steps (ma_coop_select), one such lane after another.
 // COOP = false (row mode: every pair has a record) compiles without the cooperative jump.
-template <int MINW, bool COOP>
+// LEVEL (level mode, DevCells::ma_lptr): a lane without a record -- or whose high key halves cannot decide -- makes
+// that jump in the wave's exact-sum path: inline in this pass (COOP), or parked on the QX queue for k_ma_exact.
+template <int MINW, bool COOP, bool LEVEL>
 __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__ ctxp, WaveState W,
                                                          const uint64_t *__restrict__ soa, int64_t n, int nts) {
   CTX_IN_LDS(ctxp)
@@ -437,7 +440,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   bool have = false, drained = false;
   int cur = (int)(blockIdx.x % (unsigned)nr), tried = 0;
   bool pendF = false, pendX = false;
-  unsigned long long jumps_sum = 0, trans_sum = 0;
+  unsigned long long jumps_sum = 0, trans_sum = 0, coop_sum = 0;
   unsigned long long st_pass = 0, st_busy = 0, st_refill = 0, st_trefill = 0, st_tstep = 0;
 #ifdef ARTIS_STAMPS
   unsigned long long ma_st[4] = {0, 0, 0, 0};
@@ -519,7 +522,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     st_busy += __popcll(__ballot(have));
     const unsigned long long ts0 = wave_clock();
     // a lane whose current level has no record: its jump is made by the whole wave below
-    const bool unc = COOP && have && mc.line == MA_NOLINE;
+    const bool unc = LEVEL && have && mc.line == MA_NOLINE;
     MaMetaW meta;
     double z1 = 0., z2 = 0.;
     {
@@ -551,7 +554,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     MaEnd e;
     int r = MA_PENDING;
     if (have && !unc) {
-      r = ma_step_cached(K, L, rng, mc, e, (int)rng.key1, KeysLds<COOP && ARTIS_MA_HI_ONLY>{line, mc.pline}, meta,
+      r = ma_step_cached(K, L, rng, mc, e, (int)rng.key1, KeysLds<LEVEL && ARTIS_MA_HI_ONLY>{line, mc.pline}, meta,
                          z1, z2);
 #ifdef ARTIS_STAMPS
       ts2 = wave_clock();
@@ -559,6 +562,10 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     }
     // level mode: a jump the high key halves cannot decide is made by the wave below from the exact sums, with the
     // lane's RNG counter back at the start of the jump (the same draws z1, z2), not parked for k_ma_exact
+    if (LEVEL && !COOP && unc) {  // -> k_ma_exact (a jump not yet begun: its draws start at the current counter)
+      mc.n0 = rng.n;
+      r = MA_DEFER;
+    }
     bool unc_now = unc;
     if (COOP && r == MA_DEFER) {
       rng.n = mc.n0;
@@ -577,7 +584,10 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
       double cx = 0.;
       if (unc_now) {
         csel = ma_coop_action(K, mc.k, mc.ul, z1, z2, &cx);
-        if (!ma_coop_needs_search(csel)) r = ma_coop_apply(K, L, rng, mc, e, (int)rng.key1, csel, -1, 0u, meta);
+        if (!ma_coop_needs_search(csel)) {
+          r = ma_coop_apply(K, L, rng, mc, e, (int)rng.key1, csel, -1, 0u, meta);
+          coop_sum++;
+        }
       }
       // (a rotating start, so that with coop_max < 64 every waiting lane gets its turn)
       unsigned long long um = __ballot(unc_now && ma_coop_needs_search(csel));
@@ -590,7 +600,10 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
         int j = -1;
         unsigned probes = 0;
         const int sel = ma_coop_search(K, k, ul, sl, readlane_d(cx, ld), t_mid, &j, probes);
-        if (lane == ld) r = ma_coop_apply(K, L, rng, mc, e, (int)rng.key1, sel, j, probes, meta);
+        if (lane == ld) {
+          r = ma_coop_apply(K, L, rng, mc, e, (int)rng.key1, sel, j, probes, meta);
+          coop_sum++;
+        }
       }
     }
     if (have) {
@@ -646,6 +659,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
 #endif
   wave_stats_flush(W, 1, st_pass, st_busy, st_t0, st_refill, st_trefill, st_tstep);
   if (jumps_sum) atomicAdd(&s_work[WK_MA_JUMPS], jumps_sum);
+  if (coop_sum) atomicAdd(&W.stats[45], coop_sum);  // (level mode: jumps made by the wave from the exact sums)
   if (trans_sum) atomicAdd(&s_work[WK_MA_TRANS], trans_sum);
   block_counters_flush(K, s_ctr, s_work);
 }
@@ -685,6 +699,43 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
     m.line = MA_NOLINE;  // (the walk resumes in k_ma, whose ticket looks its record up again)
     m.ntrans = 0;
     const int ul = m.ul, k = m.k;
+    if (K.C.ma_level_mode) {
+      // level mode (a pair without a record, or a comparison its high key halves could not decide): the action from
+      // the pair's exact totals, the transition by the wave's search -- k_ma's exact-sum jump (ma_coop_action /
+      // ma_coop_search / ma_coop_apply), the same draws and sums
+      artis_rng r2 = rng;
+      const double z1 = artis_rng_uniform(&r2), z2 = artis_rng_uniform(&r2);
+      double x = 0.;
+      int sel = ma_coop_action(K, k, ul, z1, z2, &x);
+      int j = -1;
+      unsigned probes = 0;
+      if (ma_coop_needs_search(sel)) sel = ma_coop_search(K, k, ul, sel, x, t_mid, &j, probes);
+      if (lane == 0) {
+        MaLaneR mr;
+        static_cast<MaLaneC &>(mr) = m;
+        mr.jumps = W.pend_jumps[idx];  // (ma_coop_apply counts the jump)
+        MaEnd e{};
+        const int r = ma_coop_apply(K, L, rng, mr, e, number, sel, j, probes, ma_meta_load(K, ul));
+        lwork(L, WK_MA_TRANS, mr.ntrans);
+        atomicAdd(&W.stats[40], 1ull);  // diagnostics: exact jumps
+        atomicAdd(&W.stats[45], 1ull);  // level mode: jumps made from the exact sums
+        W.rng_n[idx] = rng.n;
+        W.pend_jumps[idx] = mr.jumps;
+        if (r == MA_CONTINUE) {
+          if (mr.jumps >= MA_MAX_JUMPS) {
+            fail(K, ERR_STUCK, number, 2);
+          } else {
+            W.pend[idx] = make_int4(MA_RESUME, mr.ul, 0, 0);
+            W.q[QM][atomicAdd(&W.ctr[2 * QM], 1u)] = idx;
+          }
+        } else if (r > 0) {
+          W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
+          lwork(L, WK_MA_JUMPS, mr.jumps);
+          W.q[QF][atomicAdd(&W.ctr[2 * QF], 1u)] = idx;  // -> k_ma_finish
+        }
+      }
+      continue;
+    }
     const int mgi = K.C.ne_mgi[k];
     const MaMeta mm = K.T.ma_meta[ul];
     const int cnt = mm.nd + mm.nr + mm.nu + mm.nt;

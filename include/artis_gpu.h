@@ -496,11 +496,11 @@ int artis_gpu_last_work_counts(int64_t out[ARTIS_WORK_COUNT]);
  * a row of line coefficients (numbered centre outwards; the rest gather populations in the line walk) and out[2]
  * their bytes; out[3] cells with a whole row of macro-atom key records (row mode: all of them) and out[4] their
  * bytes.  Level mode (the rows do not fit the budget; ABI 11): records per (cell, level) pair, placed at every
- * artis_gpu_upload_cellstate on the pairs the walks used most since the last placement (whole cells centre
- * outwards before the first transport); out[5] bytes of the per-pair action totals a jump without a record reads;
- * out[6] / out[7] sampled macro-atom jumps on pairs that had a record / on all pairs between the last two
- * placements; out[8] records of the current placement, out[9] their bytes, out[10] the pool's bytes.  The
- * split never changes a result. */
+ * artis_gpu_upload_cellstate on the pairs with the most (sampled, decaying) jumps per record line in the past
+ * transports (whole cells centre outwards before the first transport); out[5] bytes of the per-pair action totals
+ * a jump without a record reads; out[6] / out[7] macro-atom jumps of the last transport made from a record / all
+ * its jumps; out[8] records of the current placement, out[9] their bytes, out[10] the pool's bytes.  The split
+ * never changes a result. */
 #define ARTIS_TABLE_INFO_COUNT 11
 int artis_gpu_table_info(int64_t out[ARTIS_TABLE_INFO_COUNT]);
 /* Emergent spectrum and light curve of the escaped r-packets among the resident packets, binned on the device:
