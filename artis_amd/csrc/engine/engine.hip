@@ -3360,6 +3360,22 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   C.ne_index = dnei;
   C.ne_mgi = dnem;
   C.n_nonempty = nne_cells;
+  {
+    // few-cell models: k_rpkt accumulates the estimators of every non-empty cell per block in LDS, as many of the
+    // sections as fit (ARTIS_GPU_NO_EST_LDS=1: none)
+    const char *ne = getenv("ARTIS_GPU_NO_EST_LDS");
+    const bool allow = !(ne && ne[0] == '1');
+    int64_t off = 0;
+    auto take = [&](bool want, int64_t n) -> int32_t {
+      if (!allow || !want || n <= 0 || off + n > EST_LDS_DOUBLES) return -1;
+      const int32_t o = (int32_t)off;
+      off += n;
+      return o;
+    };
+    C.est_lds_J = take(true, 3 * (int64_t)nne_cells);
+    C.est_lds_bf = take(G.K.R.detailed_bf != 0, (int64_t)nne_cells * G.K.T.nbf);
+    C.est_lds_rf = take(G.K.R.multibin != 0, 3 * (int64_t)nne_cells * G.K.T.rf_nbins);
+  }
   rc |= dalloc(&G.W.bins, (size_t)nne_cells + 1);
   rc |= dalloc(&G.d_binoffs, (size_t)nne_cells + 1);
   rc |= dalloc(&G.W.xhead, (size_t)8);

@@ -120,6 +120,9 @@ struct MaLayout {
   int sorted0;   // record position of the first rad_deexc key
   int hot;       // high-half positions = offset of the low halves
 };
+// k_rpkt's per-block estimator accumulator (few-cell models: every update of the same few addresses would otherwise
+// serialise in the memory system's atomics)
+#define EST_LDS_DOUBLES 2048
 #define MA_AREA 55
 // level mode: the records hold the high key halves only (twice the records in the same pool; a comparison the high
 // half cannot decide is made from the exact sums by k_ma's cooperative jump)
@@ -235,6 +238,9 @@ struct DevCells {
   // (k_ma evaluates its rates with the whole wave, ma_coop_select); ma_lhist counts every 16th jump per pair
   const uint32_t *ma_lptr;  // [n_nonempty * nlevels_total] or nullptr (row mode)
   uint32_t *ma_lhist;       // [n_nonempty * nlevels_total] or nullptr
+  // few-cell models: offsets (doubles) of the J / nuJ / ffheating, bfrate and radfield-bin estimators of every
+  // non-empty cell in k_rpkt's LDS accumulator (EST_LDS_DOUBLES), -1 where they do not fit (per-lane atomics)
+  int32_t est_lds_J, est_lds_bf, est_lds_rf;
   int32_t ma_level_mode;
   int32_t ma_hi_only;  // the records hold the high key halves only (level mode): a comparison that needs the low
                        // half is undecided and the jump goes to k_ma_exact

@@ -28,6 +28,7 @@ struct Tx {
   bool vstop = false;  // a virtual-packet spawn found the buffer full (DevVpkt::full): park the packet
   int est_mgi = -1;
   double est_de = 0., est_denu = 0., est_deff = 0.;
+  double *est_lds = nullptr;  // k_rpkt: the block's LDS estimator accumulator (DevCells::est_lds_*), or nullptr
 #ifdef ARTIS_STAMPS
   unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;  // diagnostic build: cycles per step phase
 #endif
@@ -872,7 +873,13 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
   lwork(x.L, WK_EST_SEGMENTS, 1);
   const double distance_e_cmf = distance * p.e_cmf;
   const double nu = p.nu_cmf;
-  if (x.defer_est) {
+  const int nne = K.C.n_nonempty;
+  if (x.est_lds && K.C.est_lds_J >= 0) {
+    double *e = x.est_lds + K.C.est_lds_J;
+    atomicAdd(&e[k], distance_e_cmf);
+    atomicAdd(&e[nne + k], distance_e_cmf * nu);
+    atomicAdd(&e[2 * nne + k], distance_e_cmf * kap.ffheating);
+  } else if (x.defer_est) {
     x.est_mgi = mgi;
     x.est_de = distance_e_cmf;
     x.est_denu = distance_e_cmf * nu;
@@ -895,7 +902,10 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
         double gc = 0., nnlevel;
         // (without do_r_lc no bf opacity is evaluated and the zero-initialised gamma_contr stays 0, rpkt.cc:1230)
         if (!K.R.do_r_lc || (!(kap.nu < nu_edge) && !bf_contribution(K, k, mgi, i, kap.nu, &nnlevel, &gc))) gc = 0.;
-        safeadd(&K.E.bfrate[row + i], gc * d_over_nu);
+        if (x.est_lds && K.C.est_lds_bf >= 0)
+          atomicAdd(&x.est_lds[K.C.est_lds_bf + (int64_t)k * K.T.nbf + i], gc * d_over_nu);
+        else
+          safeadd(&K.E.bfrate[row + i], gc * d_over_nu);
       } else if (nu < nu_edge) {
         break;
       }
@@ -903,7 +913,12 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
   }
   if (K.R.multibin) {  // radfield.cc:845-866
     const int b = rf_select_bin(K, nu);
-    if (b >= 0) {
+    if (b >= 0 && x.est_lds && K.C.est_lds_rf >= 0) {
+      double *e = x.est_lds + K.C.est_lds_rf + 3 * ((int64_t)k * K.T.rf_nbins + b);
+      atomicAdd(&e[0], distance_e_cmf);
+      atomicAdd(&e[1], distance_e_cmf * nu);
+      atomicAdd(&e[2], 1.);
+    } else if (b >= 0) {
       const int64_t mb = (int64_t)mgi * K.T.rf_nbins + b;
       safeadd(&K.E.rfJ[mb], distance_e_cmf);
       safeadd(&K.E.rfnuJ[mb], distance_e_cmf * nu);
@@ -969,6 +984,42 @@ DEVFN void wave_flush_estimators(Tx &x) {
     }
   }
   x.est_mgi = -1;
+}
+
+// the block's LDS estimator accumulator: zeroed at the start of k_rpkt, added to the estimators at its end (one
+// atomic per non-zero entry and block)
+DEVFN bool est_lds_on(const Ctx &K) { return K.C.est_lds_J >= 0 || K.C.est_lds_bf >= 0 || K.C.est_lds_rf >= 0; }
+DEVFN void est_lds_zero(double *e) {
+  for (int i = threadIdx.x; i < EST_LDS_DOUBLES; i += blockDim.x) e[i] = 0.;
+  __syncthreads();
+}
+DEVFN void est_lds_flush(const Ctx &K, const double *e) {
+  __syncthreads();
+  const int nne = K.C.n_nonempty;
+  if (K.C.est_lds_J >= 0)
+    for (int i = threadIdx.x; i < 3 * nne; i += blockDim.x) {
+      const double v = e[K.C.est_lds_J + i];
+      if (v == 0.) continue;
+      const int mgi = K.C.ne_mgi[i % nne];
+      safeadd(i < nne ? &K.E.J[mgi] : i < 2 * nne ? &K.E.nuJ[mgi] : &K.E.ffheat[mgi], v);
+    }
+  if (K.C.est_lds_bf >= 0) {
+    const int nbf = K.T.nbf;
+    for (int i = threadIdx.x; i < nne * nbf; i += blockDim.x) {
+      const double v = e[K.C.est_lds_bf + i];
+      if (v != 0.) safeadd(&K.E.bfrate[(int64_t)K.C.ne_mgi[i / nbf] * nbf + i % nbf], v);
+    }
+  }
+  if (K.C.est_lds_rf >= 0) {
+    const int nb = K.T.rf_nbins;
+    for (int i = threadIdx.x; i < 3 * nne * nb; i += blockDim.x) {
+      const double v = e[K.C.est_lds_rf + i];
+      if (v == 0.) continue;
+      const int cb = i / 3;
+      const int64_t mb = (int64_t)K.C.ne_mgi[cb / nb] * nb + cb % nb;
+      safeadd((i % 3) == 0 ? &K.E.rfJ[mb] : (i % 3) == 1 ? &K.E.rfnuJ[mb] : &K.E.rfcount[mb], v);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------ virtual packets

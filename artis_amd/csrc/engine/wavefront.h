@@ -180,6 +180,12 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
   x.nts = nts;
   x.win = (__attribute__((address_space(3))) double *)&s_win[0][threadIdx.x];
   x.defer_est = true;
+  __shared__ double s_est[EST_LDS_DOUBLES];  // few-cell models: the block's estimator accumulator
+  const bool est_lds = est_lds_on(K);
+  if (est_lds) {
+    est_lds_zero(s_est);
+    x.est_lds = s_est;
+  }
   const uint32_t nq = W.ctr[2 * QR];
   Pkt p;
   RStep S;
@@ -319,6 +325,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
     atomicAdd(&W.stats[27], st_bsum);
   }
   wave_stats_flush(W, 0, st_pass, st_busy, st_t0, st_refill, st_trefill, st_tstep);
+  if (est_lds) est_lds_flush(K, s_est);
   for (int off = 32; off > 0; off >>= 1) cmf_lum += __shfl_down(cmf_lum, off, 64);
   if ((threadIdx.x & 63) == 0) s_cmflum[threadIdx.x >> 6] = cmf_lum;
   __syncthreads();
