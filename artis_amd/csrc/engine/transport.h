@@ -1356,9 +1356,9 @@ DEVFN double alpha_sp_piece(const Ctx &K, const float *xs, double nu_threshold, 
   for (int q = 0; q < 4; q++) s += gw[q] * alpha_sp_E_integrand(K, xs, nu_threshold, T, mid + half * gx[q]);
   return s * half;
 }
-// ratecoeff.cc:628-684 with deviation D3 (see oracle/oracle.cc)
-DEVNI double select_continuum_nu(Tx &x, int e, int lowerion, int lower, int upperionlevel, float T_e) {
-  const Ctx &K = x.K;
+// ratecoeff.cc:628-684 with deviation D3 (see oracle/oracle.cc), for the draw zrand = 1 - uniform
+DEVFN double select_continuum_nu_z(const Ctx &K, int e, int lowerion, int lower, int upperionlevel, float T_e,
+                                   double zrand) {
   int target = 0;
   for (int t = 0; t < get_nphixstargets(K, e, lowerion, lower); t++)
     if (get_phixsupperlevel(K, e, lowerion, lower, t) == upperionlevel) {
@@ -1370,7 +1370,6 @@ DEVNI double select_continuum_nu(Tx &x, int e, int lowerion, int lower, int uppe
   const double nu_max_phixs = nu_threshold * K.T.last_phixs_nuovernuedge;
   const int npieces = K.T.nphixspoints;
   const float *xs = level_photoion_xs(K, e, lowerion, lower);
-  const double zrand = 1. - artis_rng_uniform(&x.rng);
   const double deltanu = (nu_max_phixs - nu_threshold) / npieces;
   const double half = 0.5 * deltanu;
   double head = 0.;
@@ -1388,6 +1387,83 @@ DEVNI double select_continuum_nu(Tx &x, int e, int lowerion, int lower, int uppe
   }
   const double nuoffset = (total_alpha_sp * zrand - alpha_sp_old) / (alpha_sp - alpha_sp_old) * deltanu;
   return nu_threshold + (i - 1) * deltanu + nuoffset;
+}
+
+// the same with its draw (the reference's order: the draw first)
+DEVNI double select_continuum_nu(Tx &x, int e, int lowerion, int lower, int upperionlevel, float T_e) {
+  const double zrand = 1. - artis_rng_uniform(&x.rng);
+  return select_continuum_nu_z(x.K, e, lowerion, lower, upperionlevel, T_e, zrand);
+}
+
+DEVFN double readlane_d(double v, int l) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// select_continuum_nu's integral for every lane of the wave that asks for one (want; every lane of the wave calls
+// this, convergent): the lanes evaluate the requesting lane's npieces quadrature pieces in parallel (pieces q,
+// q + 64, ...; the same alpha_sp_piece values as the serial loops), and the two running sums are then added in the
+// reference's order from the evaluating lanes' registers (v_readlane), so the result is select_continuum_nu's bit
+// for bit.  zrand is the requesting lane's draw (1 - uniform, drawn by the caller where select_continuum_nu draws
+// it).  One fb emission costs the wave ~npieces / 16 integrand evaluations per lane instead of 8 npieces in one lane.
+#define WAVE_FB_MAXR 4  // pieces per lane held in registers (npieces <= 256; more: the serial loops)
+DEVFN double wave_select_continuum_nu(const Ctx &K, bool want, int e, int lowerion, int lower, int upperionlevel,
+                                      float T_e, double zrand) {
+  double result = 0.;
+  unsigned long long m = __ballot(want);
+  const int lane = (int)__lane_id();
+  while (m) {
+    const int ld = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    const int le = __builtin_amdgcn_readlane(e, ld), li = __builtin_amdgcn_readlane(lowerion, ld);
+    const int ll = __builtin_amdgcn_readlane(lower, ld), lu = __builtin_amdgcn_readlane(upperionlevel, ld);
+    const float lT = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(T_e), ld));
+    const double lz = readlane_d(zrand, ld);
+    int target = 0;
+    for (int t = 0; t < get_nphixstargets(K, le, li, ll); t++)
+      if (get_phixsupperlevel(K, le, li, ll, t) == lu) {
+        target = t;
+        break;
+      }
+    const double E_threshold = get_phixs_threshold(K, le, li, ll, target);
+    const double nu_threshold = ARTIS_ONEOVERH * E_threshold;
+    const double nu_max_phixs = nu_threshold * K.T.last_phixs_nuovernuedge;
+    const int npieces = K.T.nphixspoints;
+    const float *xs = level_photoion_xs(K, le, li, ll);
+    const double deltanu = (nu_max_phixs - nu_threshold) / npieces;
+    const double half = 0.5 * deltanu;
+    double pc[WAVE_FB_MAXR];
+#pragma unroll
+    for (int r = 0; r < WAVE_FB_MAXR; r++) {
+      const int j = lane + 64 * r;
+      pc[r] = (j < npieces) ? alpha_sp_piece(K, xs, nu_threshold, lT, nu_threshold + j * deltanu, half) : 0.;
+    }
+    auto piece = [&](int j) {  // piece j from its lane (j wave-uniform); past the registers, evaluated here
+      if (npieces > 64 * WAVE_FB_MAXR) return alpha_sp_piece(K, xs, nu_threshold, lT, nu_threshold + j * deltanu, half);
+      double v = 0.;
+#pragma unroll
+      for (int r = 0; r < WAVE_FB_MAXR; r++)
+        if ((j >> 6) == r) v = readlane_d(pc[r], j & 63);
+      return v;
+    };
+    double head = 0.;
+    for (int j = 0; j < npieces; j++) head += piece(j);
+    const double total_alpha_sp = head;
+    double alpha_sp_old = total_alpha_sp;
+    double alpha_sp = total_alpha_sp;
+    head = 0.;
+    int i;
+    for (i = 1; i < npieces; i++) {
+      alpha_sp_old = alpha_sp;
+      head += piece(i - 1);
+      alpha_sp = total_alpha_sp - head;
+      if (lz >= alpha_sp / total_alpha_sp) break;
+    }
+    const double nuoffset = (total_alpha_sp * lz - alpha_sp_old) / (alpha_sp - alpha_sp_old) * deltanu;
+    if (lane == ld) result = nu_threshold + (i - 1) * deltanu + nuoffset;
+  }
+  return result;
 }
 
 // ------------------------------------------------------------------------------------------ macro-atom
@@ -1674,12 +1750,6 @@ struct MaLaneR : MaLaneC {
 };
 
 // ---- the jump of a walk whose (cell, level) has no key record (level mode), made by the whole wave ------------
-DEVFN double readlane_d(double v, int l) {
-  const uint64_t u = (uint64_t)__double_as_longlong(v);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
-  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
 #define MA_COOP_RANDOM (-1)  // the action draw exceeds the total (the reference's abort, ERR_MA_RANDOM)
 #define MA_COOP_NOSEL (-2)   // no entry of the action's list exceeds the transition draw (ERR_MA_SELECT)
 // The jump of a walk whose (cell, level) pair has no key record.  The action comes from the pair's exact totals
@@ -2054,14 +2124,14 @@ DEVFN int ma_jump_cached_global(const Ctx &K, const LocalCounters &L, artis_rng 
 
 
 // the fb deactivation (macroatom.cc:340-380): select_continuum_nu's quadrature, noinline (run on copies, cold_call)
-DEVNI void ma_finish_fb(Tx &x, Pkt &p, const MaEnd &e) {
+DEVNI void ma_finish_fb(Tx &x, Pkt &p, const MaEnd &e, double fb_nu) {
   const Ctx &K = x.K;
   const int element = p.ma_element;
   const int uiu = K.T.level_ui[e.b];
   const int ion = uiu - K.T.elem_uniqueionoffset[element] - 1, lower = e.a;
   const int upperionlevel = e.b - K.T.ion_uniqueleveloffset[uiu];
   const float T_e = K.C.Te[cell_mgi(K, p.where)];
-  p.nu_cmf = select_continuum_nu(x, element, ion, lower, upperionlevel, T_e);
+  p.nu_cmf = fb_nu >= 0. ? fb_nu : select_continuum_nu(x, element, ion, lower, upperionlevel, T_e);
   lctr(x.L, CTR_MA_STAT_DEACTIVATION_FB);
   p.last_event = 2;
   emitt_rpkt(x, p);
@@ -2086,7 +2156,7 @@ DEVNI void ma_finish_fb(Tx &x, Pkt &p, const MaEnd &e) {
 // the deactivation branches of do_macroatom (macroatom.cc:222-380, 445-462) and its trailer (macroatom.cc:475-482);
 // `jumps` passes of the loop each added one interaction.  Inline (bb and collisional in the caller's registers);
 // ma_finish is the noinline form for the kernels that run it on a copy.
-DEVFN void ma_finish_inl(Tx &x, Pkt &p, const MaEnd &e, unsigned jumps) {
+DEVFN void ma_finish_inl(Tx &x, Pkt &p, const MaEnd &e, unsigned jumps, double fb_nu = -1.) {
   const Ctx &K = x.K;
   const int element = p.ma_element;
   p.interactions += (int)jumps;
@@ -2119,7 +2189,7 @@ DEVFN void ma_finish_inl(Tx &x, Pkt &p, const MaEnd &e, unsigned jumps) {
     p.type = ARTIS_TYPE_KPKT;
     safeadd(&K.E.colheat[cell_mgi(K, p.where)], p.e_cmf);
   } else if (e.code == MA_END_FB) {
-    cold_call(x, p, [&](Tx &tx, Pkt &tp) { ma_finish_fb(tx, tp, e); });
+    cold_call(x, p, [&](Tx &tx, Pkt &tp) { ma_finish_fb(tx, tp, e, fb_nu); });
   }
   if (p.trueemissiontype < 0) {
     p.trueemissiontype = p.emissiontype;
@@ -2211,7 +2281,42 @@ DEVNI void do_kpkt_bb(Tx &x, Pkt &p) {
   p.nscatterings = 0;
 }
 // kpkt.cc:477-797 (cumulative cooling list from the per-cell table)
-DEVNI void do_kpkt(Tx &x, Pkt &p, double t2) {
+// an fb emission whose frequency the wave computes (wave_select_continuum_nu): the continuum and the draw
+struct FbReq {
+  bool want = false;
+  int e = 0, ion = 0, lower = 0, upper = 0;
+  float T_e = 0.f;
+  double zrand = 0.;
+};
+
+// kpkt.cc:661-700, the fb cooling branch after the frequency
+DEVFN void kpkt_fb_tail(Tx &x, Pkt &p, int el, int lowerion, int level, int upper, double nu) {
+  const Ctx &K = x.K;
+  p.nu_cmf = nu;
+  emitt_rpkt(x, p);
+  p.next_trans = 0;
+  lctr(x.L, CTR_K_STAT_TO_R_FB);
+  p.interactions += 1;
+  p.last_event = 7;
+  int target = 0;
+  for (int t = 0; t < get_nphixstargets(K, el, lowerion, level); t++)
+    if (get_phixsupperlevel(K, el, lowerion, level, t) == upper) {
+      target = t;
+      break;
+    }
+  p.emissiontype = K.T.level_cont_index[ulev(K, el, lowerion, level)] - target;
+  p.trueemissiontype = p.emissiontype;
+  p.em_pos[0] = p.pos[0];
+  p.em_pos[1] = p.pos[1];
+  p.em_pos[2] = p.pos[2];
+  p.em_time = (int)p.prop_time;
+  p.nscatterings = 0;
+  if (K.V.on) vpkt_spawn(x, p, 2);  // kpkt.cc:691-694
+}
+
+// kpkt.cc:477-797.  fb: nullptr -- the fb frequency is computed here (select_continuum_nu); otherwise an fb channel
+// stops after its draw with the request in *fb (the caller's wave computes the frequency, then kpkt_fb_tail)
+DEVNI void do_kpkt(Tx &x, Pkt &p, double t2, FbReq *fb = nullptr) {
   const Ctx &K = x.K;
   const double t1 = p.prop_time;
   const int mgi = cell_mgi(K, p.where);
@@ -2290,26 +2395,17 @@ DEVNI void do_kpkt(Tx &x, Pkt &p, double t2) {
     const int lowerion = K.T.cool_ion[icool];
     const int level = K.T.cool_level[icool];
     const int upper = K.T.cool_upper[icool];
-    p.nu_cmf = select_continuum_nu(x, el, lowerion, level, upper, T_e);
-    emitt_rpkt(x, p);
-    p.next_trans = 0;
-    lctr(x.L, CTR_K_STAT_TO_R_FB);
-    p.interactions += 1;
-    p.last_event = 7;
-    int target = 0;
-    for (int t = 0; t < get_nphixstargets(K, el, lowerion, level); t++)
-      if (get_phixsupperlevel(K, el, lowerion, level, t) == upper) {
-        target = t;
-        break;
-      }
-    p.emissiontype = K.T.level_cont_index[ulev(K, el, lowerion, level)] - target;
-    p.trueemissiontype = p.emissiontype;
-    p.em_pos[0] = p.pos[0];
-    p.em_pos[1] = p.pos[1];
-    p.em_pos[2] = p.pos[2];
-    p.em_time = (int)p.prop_time;
-    p.nscatterings = 0;
-    if (K.V.on) vpkt_spawn(x, p, 2);  // kpkt.cc:691-694
+    if (fb) {
+      fb->want = true;
+      fb->e = el;
+      fb->ion = lowerion;
+      fb->lower = level;
+      fb->upper = upper;
+      fb->T_e = T_e;
+      fb->zrand = 1. - artis_rng_uniform(&x.rng);  // select_continuum_nu's draw
+      return;
+    }
+    kpkt_fb_tail(x, p, el, lowerion, level, upper, select_continuum_nu(x, el, lowerion, level, upper, T_e));
   } else if (ctype == ARTIS_COOLINGTYPE_COLLEXC) {
     const float nne = K.C.nne[mgi];
     const double contrib_low = (icool > ilow) ? cc[icool - 1] : oldcoolingsum;

@@ -864,26 +864,50 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_ma_finish(const Ctx *__restrict_
   L.work = &s_work[0];
   const uint32_t nq = W.ctr[2 * QF];
   const bool dyn = K.V.on;
-  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;; slot += gridDim.x * blockDim.x) {
+  // a wave-uniform loop (the fb frequencies are computed by the whole wave, wave_select_continuum_nu)
+  for (uint32_t slot0 = blockIdx.x * blockDim.x + threadIdx.x;; slot0 += gridDim.x * blockDim.x) {
+    uint32_t slot = slot0;
     if (dyn) {
       if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t *)K.V.full)) break;
       slot = wave_reserve(&W.ctr[2 * QF + 1], true);
     }
-    if (slot >= nq) break;
-    const int32_t idx = W.q[QF][slot];
+    const bool have = slot < nq;
+    if (!__any(have)) break;
+    int32_t idx = -1;
     Pkt p;
-    pkt_load(soa, n, idx, p);
     Tx x(K, L);
-    x.nts = nts;
-    x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
-    x.rng.n = W.rng_n[idx];
-    const int4 pd = W.pend[idx];
-    const MaEnd e{pd.x, pd.y, pd.z, pd.w};
-    ma_finish_inl(x, p, e, W.pend_jumps[idx]);
-    W.pend[idx].x = 0;
-    pkt_store(soa, n, idx, p);
-    W.rng_n[idx] = x.rng.n;
-    const bool live = x.ok && p.prop_time < t2;
+    MaEnd e{};
+    FbReq fb;
+    unsigned jumps = 0;
+    if (have) {
+      idx = W.q[QF][slot];
+      pkt_load(soa, n, idx, p);
+      x.nts = nts;
+      x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
+      x.rng.n = W.rng_n[idx];
+      const int4 pd = W.pend[idx];
+      e = MaEnd{pd.x, pd.y, pd.z, pd.w};
+      jumps = W.pend_jumps[idx];
+      if (e.code == MA_END_FB) {  // ma_finish_fb's continuum and its first draw (select_continuum_nu's)
+        const int uiu = K.T.level_ui[e.b];
+        fb.want = true;
+        fb.e = p.ma_element;
+        fb.ion = uiu - K.T.elem_uniqueionoffset[p.ma_element] - 1;
+        fb.lower = e.a;
+        fb.upper = e.b - K.T.ion_uniqueleveloffset[uiu];
+        fb.T_e = K.C.Te[cell_mgi(K, p.where)];
+        fb.zrand = 1. - artis_rng_uniform(&x.rng);
+      }
+    }
+    const double fb_nu = wave_select_continuum_nu(K, fb.want, fb.e, fb.ion, fb.lower, fb.upper, fb.T_e, fb.zrand);
+    bool live = false;
+    if (have) {
+      ma_finish_inl(x, p, e, jumps, fb.want ? fb_nu : -1.);
+      W.pend[idx].x = 0;
+      pkt_store(soa, n, idx, p);
+      W.rng_n[idx] = x.rng.n;
+      live = x.ok && p.prop_time < t2;
+    }
     wave_push(W, QR, live && p.type == ARTIS_TYPE_RPKT, idx);
     wave_push(W, QK, live && (p.type == ARTIS_TYPE_KPKT || p.type == ARTIS_TYPE_PRE_KPKT), idx);
   }
@@ -950,41 +974,53 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_kpkt(const Ctx *__restrict__ ctx
   L.ctr = &s_ctr[0];
   L.work = &s_work[0];
   const uint32_t nq = W.ctr[2 * QK];
-  // with virtual packets the slots are taken 64 at a time from the fetch head, so that a full spawn buffer can stop
-  // the launch with the untaken slots [head, nq) left for the resumed launch (engine.hip vpkt_drain)
+  // with virtual packets the slots are taken a wave at a time from the fetch head, so that a full spawn buffer can
+  // stop the launch with the untaken slots [head, nq) left for the resumed launch (engine.hip vpkt_drain).  The loop
+  // is wave-uniform: an fb cooling emission's frequency is computed by the whole wave (wave_select_continuum_nu).
   const bool dyn = K.V.on;
-  uint32_t slot = dyn ? 0u : blockIdx.x * blockDim.x + threadIdx.x;
-  for (;; slot += gridDim.x * blockDim.x) {
+  for (uint32_t slot0 = blockIdx.x * blockDim.x + threadIdx.x;; slot0 += gridDim.x * blockDim.x) {
+    uint32_t slot = slot0;
     if (dyn) {
       if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t *)K.V.full)) break;
-      // one atomic per wave, made by the first active lane (correct whichever lanes have left the loop)
       slot = wave_reserve(&W.ctr[2 * QK + 1], true);
-      if (slot >= nq) break;
-    } else if (slot >= nq) {
-      break;
     }
-    const int32_t idx = W.q[QK][slot];
+    const bool have = slot < nq;
+    if (!__any(have)) break;
+    int32_t idx = -1;
     Pkt p;
-    pkt_load(soa, n, idx, p);
     Tx x(K, L);
-    x.nts = nts;
-    x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
-    x.rng.n = W.rng_n[idx];
+    if (have) {
+      idx = W.q[QK][slot];
+      pkt_load(soa, n, idx, p);
+      x.nts = nts;
+      x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
+      x.rng.n = W.rng_n[idx];
+    }
     int guard = 0;
-    while (x.ok && (p.type == ARTIS_TYPE_KPKT || p.type == ARTIS_TYPE_PRE_KPKT) && p.prop_time < t2) {
-      const int mgi = cell_mgi(K, p.where);
-      if (p.type == ARTIS_TYPE_PRE_KPKT || K.C.thick[mgi] == 1)
-        do_kpkt_bb(x, p);
-      else
-        do_kpkt(x, p, t2);
-      if (++guard > 1000) x.err(ERR_STUCK, p.number, 4);
+    while (true) {
+      const bool kp = have && x.ok && (p.type == ARTIS_TYPE_KPKT || p.type == ARTIS_TYPE_PRE_KPKT) && p.prop_time < t2;
+      if (!__any(kp)) break;
+      FbReq fb;
+      if (kp) {
+        const int mgi = cell_mgi(K, p.where);
+        if (p.type == ARTIS_TYPE_PRE_KPKT || K.C.thick[mgi] == 1)
+          do_kpkt_bb(x, p);
+        else
+          do_kpkt(x, p, t2, &fb);
+      }
+      const double nu = wave_select_continuum_nu(K, fb.want, fb.e, fb.ion, fb.lower, fb.upper, fb.T_e, fb.zrand);
+      if (fb.want) kpkt_fb_tail(x, p, fb.e, fb.ion, fb.lower, fb.upper, nu);
+      if (kp && ++guard > 1000) x.err(ERR_STUCK, p.number, 4);
     }
-    pkt_store(soa, n, idx, p);
-    W.rng_n[idx] = x.rng.n;
-    if (x.ok && p.prop_time < t2) {
-      if (p.type == ARTIS_TYPE_RPKT) W.q[QR][atomicAdd(&W.ctr[2 * QR], 1u)] = idx;
-      if (p.type == ARTIS_TYPE_MA) W.q[QM][atomicAdd(&W.ctr[2 * QM], 1u)] = idx;
+    bool toR = false, toM = false;
+    if (have) {
+      pkt_store(soa, n, idx, p);
+      W.rng_n[idx] = x.rng.n;
+      toR = x.ok && p.prop_time < t2 && p.type == ARTIS_TYPE_RPKT;
+      toM = x.ok && p.prop_time < t2 && p.type == ARTIS_TYPE_MA;
     }
+    wave_push(W, QR, toR, idx);
+    wave_push(W, QM, toM, idx);
   }
   block_counters_flush(K, s_ctr, s_work);
 }
