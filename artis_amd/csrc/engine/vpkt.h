@@ -48,6 +48,9 @@ DEVFN void add_to_vspecpol(const DevVpkt &V, double nu_rf, double e_rf, const do
       const double pktcontrib = e_rf / V.delta_t[nt] / V.delta_freq[nnu] / 4.e12 / ARTIS_PI / ARTIS_PARSEC /
                                 ARTIS_PARSEC / V.nprocs * 4 * ARTIS_PI;
       const int64_t idx = ((int64_t)nt * V.nobs * V.nspectra + ind_comb) * V.vmnubins + nnu;
+#ifdef ARTIS_DIAG_NO_VSTOKES  // timing diagnostic only (drops the spectra): the cost of the escape atomics
+      if (pktcontrib != 12345.) return;
+#endif
       unsafeAtomicAdd(&V.vstokes[idx], st[0] * pktcontrib);
       unsafeAtomicAdd(&V.vstokes[V.vstokes_stride + idx], st[1] * pktcontrib);
       unsafeAtomicAdd(&V.vstokes[2 * V.vstokes_stride + idx], st[2] * pktcontrib);
@@ -338,7 +341,12 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
     const double tf = v.t_future;
     const double s_cont = sdist * t_current * t_current * t_current / (tf * tf * tf);
     Kappa kap;
+#ifdef ARTIS_DIAG_VPKT_NOKAPPA  // timing diagnostic only (wrong opacities): the cost of the continuum evaluation
+    kap.nu = d.nu_cmf;
+    kap.total = kap.es = kap.ff = kap.bf = kap.ffheating = 1e-30;
+#else
     calculate_kappa_rpkt_cont(x, d, K.C.ne_index[v.mgi], v.mgi, kap);
+#endif
     const double kap_cont = kap.total;
     const double kap_cont_nobf = kap_cont - kap.bf;
     const double kap_cont_noff = kap_cont - kap.ff;
@@ -386,6 +394,9 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
     uint64_t wm = v.wm;
     int budget = VPKT_LINES_PER_PASS;
     bool done = false;
+#ifdef ARTIS_DIAG_VPKT_NOLINES  // timing diagnostic only (no line opacity): the cost of the line walk
+    ldist = sdist;
+#endif
     while (true) {
       if (!(ldist < sdist)) {
         done = true;
