@@ -1237,6 +1237,15 @@ int vpkt_collect(const unsigned long long before[8]) {
   G.last_vpkt_work[1] = (int64_t)(after[6] - before[6]);
   G.last_vpkt_work[2] = (int64_t)(after[7] - before[7]);
   G.last_vpkt_work[3] = (int64_t)((after[1] + after[2] + after[3]) - (before[1] + before[2] + before[3]));
+#ifdef ARTIS_DIAG_VPKT_PASSES
+  if (getenv("ARTIS_GPU_STATS")) {
+    unsigned long long dg[8];
+    HIPCHK(hipMemcpyFromSymbol(dg, HIP_SYMBOL(g_vpkt_diag), sizeof(dg)));
+    fprintf(stderr, "[artis_gpu] k_vpkt (cumulative): wave passes %llu, busy lanes/pass %.1f, tracing lanes/pass %.1f, "
+            "passes/refill %.1f, cycles/pass %.0f, refill cycles/pass %.0f\n", dg[0], (double)dg[1] / dg[0],
+            (double)dg[2] / dg[0], (double)dg[0] / dg[3], (double)dg[4] / dg[0], (double)dg[5] / dg[0]);
+  }
+#endif
   return 0;
 }
 

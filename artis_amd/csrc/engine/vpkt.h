@@ -450,6 +450,11 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
   }
 }
 
+#ifdef ARTIS_DIAG_VPKT_PASSES  // diagnostic build: [0] wave passes, [1] busy lane-passes, [2] tracing lane-passes,
+                               // [3] refills, [4] wave cycles (s_memtime), [5] cycles in refills
+__device__ unsigned long long g_vpkt_diag[8];
+#endif
+
 // all (spawn, observer) work items of the spawn buffer; spawn_ctr[1] is the fetch head
 template <int PF, int MINW>
 __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict__ ctxp, int refill_min) {
@@ -473,10 +478,23 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
   bool have = false, drained = false;
   unsigned long long lines = 0;
   const int64_t cap = V.cap;
+#ifdef ARTIS_DIAG_VPKT_PASSES
+  unsigned long long dg[6] = {0, 0, 0, 0, 0, 0};
+  const unsigned long long dg_t0 = __builtin_amdgcn_s_memtime();
+#endif
   while (true) {
     const bool idle = !have && !drained;
     const unsigned long long imask = __ballot(idle);
+#ifdef ARTIS_DIAG_VPKT_PASSES
+    dg[0]++;
+    dg[1] += __popcll(__ballot(have));
+    dg[2] += __popcll(__ballot(have && v.tracing));
+    const unsigned long long dg_r0 = __builtin_amdgcn_s_memtime();
+#endif
     if (!__any(have) || __popcll(imask) >= refill_min) {
+#ifdef ARTIS_DIAG_VPKT_PASSES
+      dg[3]++;
+#endif
       if (imask) {
         const uint32_t slot = wave_reserve(&V.spawn_ctr[1], idle);
         if (idle) {
@@ -506,6 +524,9 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
       }
       if (!__any(have)) break;
     }
+#ifdef ARTIS_DIAG_VPKT_PASSES
+    dg[5] += __builtin_amdgcn_s_memtime() - dg_r0;
+#endif
     if (have) {
       if (!v.tracing) {
         // vpkt.cc:872-888: the next frequency range this emission falls into, with the current observer vector
@@ -531,6 +552,11 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
       }
     }
   }
+#ifdef ARTIS_DIAG_VPKT_PASSES
+  dg[4] = __builtin_amdgcn_s_memtime() - dg_t0;
+  if (lane_id() == 0)
+    for (int i = 0; i < 6; i++) atomicAdd(&g_vpkt_diag[i], dg[i]);
+#endif
   if (lines) atomicAdd(&V.ctr[6], lines);
   if (blockIdx.x == 0 && threadIdx.x == 0 && nspawn) atomicAdd(&V.ctr[4], (unsigned long long)nspawn);
   __syncthreads();
