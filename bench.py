@@ -71,7 +71,9 @@ WORK_NAMES = ["active", "rpkt_steps", "lines_scanned", "line_taus", "kappa_evals
               "gc_updates", "ma_jumps", "ma_trans", "kpkt", "kpkt_terms", "escaped", "es_scat", "bb_events",
               "cont_events"]
 
-KERNEL_NAME = {"rpkt": "k_rpkt<2>", "ma": "k_ma<true, 1>", "kpkt": "k_kpkt", "vpkt": "k_vpkt"}
+# rocprof names (prefixes) of each class's kernel: k_ma's instance is k_ma<waves, coop, level> (row mode
+# k_ma<1, false, false>), k_vpkt's k_vpkt<prefetch, waves>
+KERNEL_NAME = {"rpkt": "k_rpkt<2>", "ma": "k_ma<", "kpkt": "k_kpkt", "vpkt": "k_vpkt<"}
 
 
 def cpu_share():
