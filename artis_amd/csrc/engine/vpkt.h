@@ -36,26 +36,40 @@ DEVFN bool vpkt_alive(const DevVpkt &V, const double *tau) {
   return count != V.nspectra;
 }
 
-// vpkt.cc:388-406 (deviation D9: a bin index rounded up to the array end is skipped)
-DEVFN void add_to_vspecpol(const DevVpkt &V, double nu_rf, double e_rf, const double st[3], int bin, int ind,
-                           double t_arrive) {
-  const int ind_comb = V.nspectra * bin + ind;
+// vpkt.cc:388-406 (deviation D9: a bin index rounded up to the array end is skipped), split in two: the time /
+// frequency bin and the packet's contribution, which do not depend on the spectrum (vspec_bin, once per escaped
+// virtual packet), and the three Stokes additions of one spectrum (vspec_add) -- the reference's expressions, so
+// the bins and sums are add_to_vspecpol's for every spectrum
+struct VspecBin {
+  bool ok;
+  int nt, nnu;
+  double pktcontrib;
+};
+DEVFN VspecBin vspec_bin(const DevVpkt &V, double nu_rf, double e_rf, double t_arrive) {
+  VspecBin b{false, 0, 0, 0.};
   if (t_arrive > V.tmin_vspec && t_arrive < V.tmax_vspec) {
     const int nt = (int)((log(t_arrive) - log(V.tmin_vspec)) / V.dlogt);
     if (nu_rf > V.numin_vspec && nu_rf < V.numax_vspec) {
       const int nnu = (int)((log(nu_rf) - log(V.numin_vspec)) / V.dlognu);
-      if (nt >= V.vmtbins || nnu >= V.vmnubins) return;
-      const double pktcontrib = e_rf / V.delta_t[nt] / V.delta_freq[nnu] / 4.e12 / ARTIS_PI / ARTIS_PARSEC /
-                                ARTIS_PARSEC / V.nprocs * 4 * ARTIS_PI;
-      const int64_t idx = ((int64_t)nt * V.nobs * V.nspectra + ind_comb) * V.vmnubins + nnu;
-#ifdef ARTIS_DIAG_NO_VSTOKES  // timing diagnostic only (drops the spectra): the cost of the escape atomics
-      if (pktcontrib != 12345.) return;
-#endif
-      unsafeAtomicAdd(&V.vstokes[idx], st[0] * pktcontrib);
-      unsafeAtomicAdd(&V.vstokes[V.vstokes_stride + idx], st[1] * pktcontrib);
-      unsafeAtomicAdd(&V.vstokes[2 * V.vstokes_stride + idx], st[2] * pktcontrib);
+      if (nt >= V.vmtbins || nnu >= V.vmnubins) return b;
+      b.ok = true;
+      b.nt = nt;
+      b.nnu = nnu;
+      b.pktcontrib = e_rf / V.delta_t[nt] / V.delta_freq[nnu] / 4.e12 / ARTIS_PI / ARTIS_PARSEC / ARTIS_PARSEC /
+                     V.nprocs * 4 * ARTIS_PI;
     }
   }
+  return b;
+}
+DEVFN void vspec_add(const DevVpkt &V, const VspecBin &b, const double st[3], int bin, int ind) {
+  const int ind_comb = V.nspectra * bin + ind;
+  const int64_t idx = ((int64_t)b.nt * V.nobs * V.nspectra + ind_comb) * V.vmnubins + b.nnu;
+#ifdef ARTIS_DIAG_NO_VSTOKES  // timing diagnostic only (drops the spectra): the cost of the escape atomics
+  if (b.pktcontrib != 12345.) return;
+#endif
+  unsafeAtomicAdd(&V.vstokes[idx], st[0] * b.pktcontrib);
+  unsafeAtomicAdd(&V.vstokes[V.vstokes_stride + idx], st[1] * b.pktcontrib);
+  unsafeAtomicAdd(&V.vstokes[2 * V.vstokes_stride + idx], st[2] * b.pktcontrib);
 }
 
 // vpkt.cc:581-627
@@ -128,7 +142,8 @@ DEVFN void vpkt_trace_init(const Ctx &K, const LocalCounters &L, VLane &v) {
   d.e_cmf = sp[7 * cap + s];
   d.number = -1;
   for (int i = 0; i < VPKT_MAX_SPECTRA; i++) v.tau[i] = 0.;
-  atomicAdd(&V.ctr[0], 1ull);  // nvpkt
+  // (nvpkt is counted by k_vpkt per lane and added once per lane at its end: a device-scope atomic on one address
+  // per traced virtual packet serialised the whole kernel)
   const double t_current = v.t_current;
   const double vel_vec[3] = {v.pos0[0] / t_current, v.pos0[1] / t_current, v.pos0[2] / t_current};
   d.nu_rf = d.nu_cmf / doppler_pos_dir(K, v.pos0, d.dir, t_current);
@@ -177,17 +192,23 @@ DEVFN void vpkt_trace_init(const Ctx &K, const LocalCounters &L, VLane &v) {
 // the escape branch of rlc_emiss_vpkt (vpkt.cc:314-367)
 DEVFN void vpkt_trace_finish(const Ctx &K, VLane &v) {
   const DevVpkt &V = K.V;
-  if (v.realtype >= 1 && v.realtype <= 3) atomicAdd(&V.ctr[v.realtype], 1ull);  // nvpkt_esc1..3
-  double t_arrive = 0.;
-  // unrolled so that v.tau is never indexed dynamically: one dynamic index here kept the whole lane state (tau,
-  // the dummy packet) in scratch for the entire kernel, the line walk included (488 B/lane at 1 wave per SIMD)
+#ifdef ARTIS_DIAG_VPKT_NOFINISH  // timing diagnostic only (no spectra): the cost of the escape code
+  if (v.pn != 12345.) return;
+#endif
+  // (nvpkt_esc1..3: counted by k_vpkt, as nvpkt)
+  // t_arrive, the bins and the contribution are the same for every spectrum (computed once; the escape code runs
+  // in the persistent loop's passes, where the whole wave executes it whenever one lane escapes).  Unrolled so that
+  // v.tau is never indexed dynamically: one dynamic index here kept the whole lane state in scratch.
+  const double t_arrive = v.t_current - (dot(v.pos0, v.d.dir) / ARTIS_CLIGHT_PROP);
+  const VspecBin vb = vspec_bin(V, v.d.nu_rf, v.d.e_rf, t_arrive);
+  if (vb.ok) {
 #pragma unroll
-  for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++) {
-    if (ind >= V.nspectra) break;
-    const double prob = v.pn * exp(-v.tau[ind]);
-    const double st[3] = {v.I * prob, v.Q * prob, v.U * prob};
-    t_arrive = v.t_current - (dot(v.pos0, v.d.dir) / ARTIS_CLIGHT_PROP);
-    add_to_vspecpol(V, v.d.nu_rf, v.d.e_rf, st, v.b, ind, t_arrive);
+    for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++) {
+      if (ind >= V.nspectra) break;
+      const double prob = v.pn * exp(-v.tau[ind]);
+      const double st[3] = {v.I * prob, v.Q * prob, v.U * prob};
+      vspec_add(V, vb, st, v.b, ind);
+    }
   }
   if (V.vgrid_flag == 1) {
     const double prob = v.pn * exp(-v.tau[0]);
@@ -476,7 +497,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
   v.tracing = false;
   v.inlines = false;
   bool have = false, drained = false;
-  unsigned long long lines = 0;
+  unsigned long long lines = 0, n_traced = 0, n_esc1 = 0, n_esc2 = 0, n_esc3 = 0;
   const int64_t cap = V.cap;
 #ifdef ARTIS_DIAG_VPKT_PASSES
   unsigned long long dg[6] = {0, 0, 0, 0, 0, 0};
@@ -539,6 +560,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
         if (v.range < V.nrange) {
           v.range++;
           vpkt_trace_init(K, L, v);
+          n_traced++;
           v.tracing = true;
         } else {
           have = false;
@@ -546,7 +568,12 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
       } else {
         const int r = vpkt_trace_segment<PF>(x, v, lines);
         if (r != VSEG_CONTINUE && r != VSEG_PENDING) {
-          if (r == VSEG_ESCAPED) vpkt_trace_finish(K, v);
+          if (r == VSEG_ESCAPED) {
+            vpkt_trace_finish(K, v);
+            n_esc1 += v.realtype == 1;
+            n_esc2 += v.realtype == 2;
+            n_esc3 += v.realtype == 3;
+          }
           v.tracing = false;
         }
       }
@@ -558,6 +585,10 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
     for (int i = 0; i < 6; i++) atomicAdd(&g_vpkt_diag[i], dg[i]);
 #endif
   if (lines) atomicAdd(&V.ctr[6], lines);
+  if (n_traced) atomicAdd(&V.ctr[0], n_traced);  // nvpkt
+  if (n_esc1) atomicAdd(&V.ctr[1], n_esc1);  // nvpkt_esc1..3
+  if (n_esc2) atomicAdd(&V.ctr[2], n_esc2);
+  if (n_esc3) atomicAdd(&V.ctr[3], n_esc3);
   if (blockIdx.x == 0 && threadIdx.x == 0 && nspawn) atomicAdd(&V.ctr[4], (unsigned long long)nspawn);
   __syncthreads();
   if (threadIdx.x == 0) {
