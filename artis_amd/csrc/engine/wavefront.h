@@ -692,8 +692,36 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
   const int lane = threadIdx.x & 63;
   const uint32_t nq = W.ctr[2 * QX];
   const double t_mid = K.G.ts_mid[nts];
+  unsigned long long n_exact = 0;  // exact jumps of this block (lane 0)
+  // the walks' next queue, gathered over the wave's lanes (lane j holds the j-th pending append) and appended 64 at a
+  // time: one queue atomic per 64 jumps instead of one per jump on the queue's counter
+  int32_t pm = -1, pf = -1;
+  int nm = 0, nf = 0;
+  auto flush = [&](bool all) {
+    if (all || nm == 64) {
+      wave_push(W, QM, lane < nm, pm);
+      nm = 0;
+    }
+    if (all || nf == 64) {
+      wave_push(W, QF, lane < nf, pf);
+      nf = 0;
+    }
+  };
+  auto collect = [&](int32_t to_m, int32_t to_f) {  // lane 0's decision for this slot
+    const int32_t m = __builtin_amdgcn_readlane(to_m, 0), f = __builtin_amdgcn_readlane(to_f, 0);
+    if (m >= 0) {
+      if (lane == nm) pm = m;
+      nm++;
+    }
+    if (f >= 0) {
+      if (lane == nf) pf = f;
+      nf++;
+    }
+    flush(false);
+  };
   for (uint32_t slot = blockIdx.x; slot < nq; slot += gridDim.x) {
     const int32_t idx = W.q[QX][slot];
+    int32_t to_m = -1, to_f = -1;  // (set by lane 0)
     const int where = lo32(soa[PW(n, idx, 0)]);
     artis_rng rng = artis_rng_init(K.R.seed, (int)hi32(soa[PW(n, idx, 33)]), nts, K.R.rank);
     rng.n = W.rng_n[idx];
@@ -724,8 +752,7 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
         MaEnd e{};
         const int r = ma_coop_apply(K, L, rng, mr, e, number, sel, j, probes, ma_meta_load(K, ul));
         lwork(L, WK_MA_TRANS, mr.ntrans);
-        atomicAdd(&W.stats[40], 1ull);  // diagnostics: exact jumps
-        atomicAdd(&W.stats[45], 1ull);  // level mode: jumps made from the exact sums
+        n_exact++;  // (stats[40], [45]: added once per block, not once per jump on one address)
         W.rng_n[idx] = rng.n;
         W.pend_jumps[idx] = mr.jumps;
         if (r == MA_CONTINUE) {
@@ -733,14 +760,15 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
             fail(K, ERR_STUCK, number, 2);
           } else {
             W.pend[idx] = make_int4(MA_RESUME, mr.ul, 0, 0);
-            W.q[QM][atomicAdd(&W.ctr[2 * QM], 1u)] = idx;
+            to_m = idx;
           }
         } else if (r > 0) {
           W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
           lwork(L, WK_MA_JUMPS, mr.jumps);
-          W.q[QF][atomicAdd(&W.ctr[2 * QF], 1u)] = idx;  // -> k_ma_finish
+          to_f = idx;  // -> k_ma_finish
         }
       }
+      collect(to_m, to_f);
       continue;
     }
     const int mgi = K.C.ne_mgi[k];
@@ -826,7 +854,7 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
     }
     if (lane == 0) {
       lwork(L, WK_MA_TRANS, m.ntrans);
-      atomicAdd(&W.stats[40], 1ull);  // diagnostics: exact jumps
+      n_exact++;
       W.rng_n[idx] = rng.n;
       W.pend_jumps[idx] = m.jumps;
       if (r == MA_CONTINUE) {
@@ -834,14 +862,20 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
           fail(K, ERR_STUCK, number, 2);
         } else {
           W.pend[idx] = make_int4(MA_RESUME, m.ul, 0, 0);
-          W.q[QM][atomicAdd(&W.ctr[2 * QM], 1u)] = idx;
+          to_m = idx;
         }
       } else if (r > 0) {
         W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
         lwork(L, WK_MA_JUMPS, m.jumps);
-        W.q[QF][atomicAdd(&W.ctr[2 * QF], 1u)] = idx;  // -> k_ma_finish
+        to_f = idx;  // -> k_ma_finish
       }
     }
+    collect(to_m, to_f);
+  }
+  flush(true);
+  if (lane == 0 && n_exact) {
+    atomicAdd(&W.stats[40], n_exact);                    // diagnostics: exact jumps
+    if (K.C.ma_level_mode) atomicAdd(&W.stats[45], n_exact);  // level mode: jumps made from the exact sums
   }
   block_counters_flush(K, s_ctr, s_work);
 }
