@@ -23,7 +23,8 @@ ABI_SYMBOLS = [
     "artis_gpu_packets_restore", "artis_gpu_update_packets_resident", "artis_gpu_estimators_zero",
     "artis_gpu_estimators_download", "artis_gpu_estimator_block_doubles", "artis_gpu_estimator_block_to_device",
     "artis_gpu_estimator_block_from_device", "artis_gpu_last_transport_ms", "artis_gpu_last_precompute_ms",
-    "artis_gpu_last_work_counts", "artis_gpu_last_rounds", "artis_gpu_spectrum", "artis_gpu_spectra", "artis_gpu_last_kernel_times", "artis_gpu_last_error", "artis_gpu_abi_version",
+    "artis_gpu_last_work_counts", "artis_gpu_last_rounds", "artis_gpu_spectrum", "artis_gpu_spectra", "artis_gpu_last_kernel_times",
+    "artis_gpu_last_kernel_class_times", "artis_gpu_last_error", "artis_gpu_abi_version",
     "artis_gpu_vpkt_init", "artis_gpu_vpkt_zero", "artis_gpu_vpkt_download", "artis_gpu_vpkt_last_stats", "artis_gpu_vpkt_last_work",
     "artis_estimator_block_len", "artis_estimator_block_pack", "artis_estimator_block_unpack",
     "artis_estimator_block_average_scalars",
@@ -285,6 +286,18 @@ class Engine:
         nl = (C.c_int64 * 4)()
         self.lib.artis_gpu_last_kernel_times(ms, nl)
         return {k: (ms[i], nl[i]) for i, k in enumerate(("rpkt", "ma", "kpkt", "classify"))}
+
+    KERNEL_CLASSES = ("rpkt", "ma", "kpkt", "classify", "binning", "exact", "finish")
+
+    def last_kernel_class_times(self):
+        """{class: (ms, launches)} for the last transport, finer than last_kernel_times: rpkt (k_rpkt), ma (k_ma),
+        kpkt (k_kpkt), classify (k_classify + k_gamma), binning (the M-queue counting sort), exact (k_ma_exact),
+        finish (k_ma_finish)."""
+        n = len(self.KERNEL_CLASSES)
+        ms = (C.c_double * n)()
+        nl = (C.c_int64 * n)()
+        self._check(self.lib.artis_gpu_last_kernel_class_times(ms, nl), "last_kernel_class_times")
+        return {k: (ms[i], nl[i]) for i, k in enumerate(self.KERNEL_CLASSES)}
 
     # multi-GPU (RCCL): one communicator per engine, the packed estimator block all-reduced in HBM
     def comm_init(self, rank, nranks, uid):

@@ -132,7 +132,14 @@ __global__ void k_bfcells(Ctx K, const int32_t *target_ul, const int32_t *target
     const double nnlevel = pops[ulev(K, element, ion, level)];
     const double nnupperionlevel = pops[ulev(K, element, ion + 1, upper)];
     const double sf = calculate_sahafact(K, element, ion, level, upper, T_e, ARTIS_H * K.T.allcont_nu_edge[i]);
-    K.C.depratio[(int64_t)k * nb + i] = nnupperionlevel / nnlevel * nne * sf;
+    // bf_contribution's inclusion rule (rpkt.cc:1116-1118): DETAILED_BF_ESTIMATORS_ON includes every continuum of
+    // an element present in the cell, otherwise the ion must hold > 1e-6 of the cell's nuclei (or the level is the
+    // ground level)
+    const int ui = uion(K, element, ion);
+    const bool incl = K.R.detailed_bf
+                          ? K.C.elem_abundance[(int64_t)mgi * K.T.nelements + element] > 0
+                          : ((K.C.ionpop[(int64_t)k * K.T.nions_total + ui] / (double)K.C.nnetot[mgi] > 1.e-6) || level == 0);
+    K.C.bfcell[(int64_t)k * nb + i] = make_double2(incl ? nnlevel : 0., nnupperionlevel / nnlevel * nne * sf);
   } else {
     const int slot = r - (int)nb;
     const int ul = target_ul[slot];
@@ -783,8 +790,8 @@ struct Engine {
   std::vector<hipEvent_t> tev;
   std::vector<int> tev_class;
   size_t tev_used = 0;
-  double last_kernel_ms[4] = {0, 0, 0, 0};
-  int64_t last_kernel_launches[4] = {0, 0, 0, 0};
+  double last_kernel_ms[ARTIS_KCLASS_COUNT] = {0};
+  int64_t last_kernel_launches[ARTIS_KCLASS_COUNT] = {0};
   double last_transport_ms = 0., last_precompute_ms = 0.;
   int64_t last_work[ARTIS_WORK_COUNT] = {0};
   // virtual packets (vpkt.h): device accumulators and the spawn buffer (sized per update)
@@ -805,6 +812,7 @@ struct Engine {
   uint32_t *h_vfull = nullptr;    // pinned: DevVpkt::full after a launch
   int64_t vpkt_drains = 0;        // launches resumed after a full spawn buffer (last update_packets)
   bool r_binned = false;          // bin the R queue by cell before k_rpkt (ARTIS_GPU_R_BIN=1)
+  bool ma_bin_blk = true;         // few cells: block-local M-queue binning (ARTIS_GPU_MA_BIN_BLK=0: per-entry atomics)
   std::vector<hipEvent_t> vev;  // (start, end) pairs around the k_vpkt launches of the last update
   size_t vev_used = 0;
   double last_vpkt_ms = 0.;
@@ -1017,7 +1025,7 @@ int tmark(int cls) {
 }
 // events come in (start, end) pairs; sum per class once the stream has drained
 int tcollect() {
-  for (int c = 0; c < 4; c++) {
+  for (int c = 0; c < ARTIS_KCLASS_COUNT; c++) {
     G.last_kernel_ms[c] = 0.;
     G.last_kernel_launches[c] = 0;
   }
@@ -1288,22 +1296,24 @@ int run_wavefront(int64_t n, int nts, double t2) {
     // launches read parked packets appended to the queue itself
     W.r_binned = G.r_binned && !G.K.V.on && G.K.C.n_nonempty > 0;
     if (W.r_binned) {
-      TSTART(3);
+      TSTART(4);
       const int nne = G.K.C.n_nonempty;
       HIPCHK(hipMemsetAsync(W.bins, 0, (size_t)(nne + 1) * sizeof(uint32_t), G.stream));
       k_r_bin<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa);
       HIPCHK(hipcub::DeviceScan::ExclusiveSum(G.d_scan_tmp, G.scan_tmp_bytes, W.bins, G.d_binoffs, nne + 1,
                                               G.stream));
       k_r_scatter<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_binoffs);
-      TEND(3);
+      TEND(4);
     }
+    // the per-block estimator accumulator of few-cell models (dynamic LDS, sized only when it is used)
+    const size_t est_shm = est_lds_on(G.K) ? EST_LDS_DOUBLES * sizeof(double) : 0;
     auto launch_rpkt = [&]() -> int {
       if (rpkt_occ == 3)
-        k_rpkt<3><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+        k_rpkt<3><<<grid, WAVE_BLOCK, est_shm, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
       else if (rpkt_occ == 2)
-        k_rpkt<2><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+        k_rpkt<2><<<grid, WAVE_BLOCK, est_shm, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
       else
-        k_rpkt<1><<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+        k_rpkt<1><<<grid, WAVE_BLOCK, est_shm, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
       return 0;
     };
     if (G.K.V.on)
@@ -1320,17 +1330,25 @@ int run_wavefront(int64_t n, int nts, double t2) {
         }))
       return rc;
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QR, 0, 2 * sizeof(uint32_t), G.stream));
-    TSTART(3);  // class 3: the macro-atom queue binning and the rare exact jumps (class 1 is k_ma alone)
+    TSTART(4);  // class 4: the macro-atom queue binning (class 1 is k_ma alone)
     if (W.ma_binned) {
       const int nne = G.K.C.n_nonempty;
       HIPCHK(hipMemsetAsync(W.bins, 0, (size_t)(nne + 1) * sizeof(uint32_t), G.stream));
-      k_ma_bin<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa);
+      // few cells: block-local counts (one device atomic per block and bin instead of one per queue entry)
+      const bool blk = G.ma_bin_blk && nne + 1 <= MA_BIN_LDS;
+      if (blk)
+        k_ma_bin_blk<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa);
+      else
+        k_ma_bin<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa);
       HIPCHK(hipcub::DeviceScan::ExclusiveSum(G.d_scan_tmp, G.scan_tmp_bytes, W.bins, G.d_binoffs, nne + 1,
                                               G.stream));
-      k_ma_scatter<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, G.d_binoffs);
+      if (blk)
+        k_ma_scatter_blk<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, G.d_binoffs);
+      else
+        k_ma_scatter<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, G.d_binoffs);
     }
     HIPCHK(hipMemsetAsync(W.xhead, 0, 8 * sizeof(uint32_t), G.stream));
-    TEND(3);
+    TEND(4);
     TSTART(1);
     // ARTIS_GPU_MA_WAVES=w (default 4): launch only w blocks per CU (w resident waves per SIMD) -- fewer
     // concurrent walks thrash the caches less; the walk is bound by the memory system, not by latency hiding
@@ -1355,21 +1373,21 @@ int run_wavefront(int64_t n, int nts, double t2) {
     TEND(1);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QM, 0, 2 * sizeof(uint32_t), G.stream));
     {  // jumps the 32-bit keys could not decide (rare), exact; walks go back to M
-      TSTART(3);
+      TSTART(5);
       k_ma_exact<<<grid / 4, 64, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
-      TEND(3);
+      TEND(5);
       HIPCHK(hipMemsetAsync(W.ctr + 2 * QX, 0, 2 * sizeof(uint32_t), G.stream));
     }
     {  // the walks' deactivations -> R / K
-      TSTART(3);
+      TSTART(6);
       if (G.K.V.on)
         HIPCHK(hipMemcpyAsync(G.d_qsnap, W.ctr + 2 * QF, sizeof(uint32_t), hipMemcpyDeviceToDevice, G.stream));
       k_ma_finish<<<grid / 4, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
-      TEND(3);
+      TEND(6);
       if (int rc = vpkt_drain(QF, [&]() -> int {
-            TSTART(3);
+            TSTART(6);
             k_ma_finish<<<grid / 4, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
-            TEND(3);
+            TEND(6);
             return 0;
           }))
         return rc;
@@ -1972,19 +1990,20 @@ int artis_gpu_update_grid_nlte(const artis_nt_shells *nt, const artis_nlte_param
   KN.C.nt_ionen = N.nt_ionen;
   const int nact_max = std::max(1, nnl);
   int32_t *d_act = nullptr, *d_actk = nullptr, *d_lte = nullptr, *d_nl = nullptr;
-  double *d_pops = nullptr, *d_corr = nullptr, *d_depr = nullptr, *d_hbc = nullptr;
+  double *d_pops = nullptr, *d_corr = nullptr, *d_hbc = nullptr;
+  double2 *d_depr = nullptr;
   rc |= B.get(&d_act, (size_t)nact_max, (const int32_t *)nullptr);
   rc |= B.get(&d_actk, (size_t)nact_max, (const int32_t *)nullptr);
   rc |= B.get(&d_lte, std::max<size_t>(1, lte_list.size()), lte_list.empty() ? nullptr : lte_list.data());
   rc |= B.get(&d_nl, (size_t)nact_max, nl_list.empty() ? nullptr : nl_list.data());
   rc |= B.get(&d_pops, (size_t)nact_max * nl, (const double *)nullptr);
   rc |= B.get(&d_corr, (size_t)nact_max * (ntg + 1), (const double *)nullptr);
-  rc |= B.get(&d_depr, (size_t)nact_max * std::max(1, nbf), (const double *)nullptr);
+  rc |= B.get(&d_depr, (size_t)nact_max * std::max(1, nbf), (const double2 *)nullptr);
   rc |= B.get(&d_hbc, std::max<size_t>(1, hb.size()) * nact_max, (const double *)nullptr);
   if (rc) return ARTIS_ERR_HIP;
   KN.C.pops = d_pops;
   KN.C.corrphot = d_corr;
-  KN.C.depratio = d_depr;
+  KN.C.bfcell = d_depr;
   KN.C.ne_mgi = d_act;
   KN.C.n_nonempty = 0;
   KN.C.linecoef = nullptr;
@@ -2846,6 +2865,18 @@ int artis_gpu_last_kernel_times(double ms[4], int64_t launches[4]) {
     ms[c] = G.last_kernel_ms[c];
     launches[c] = G.last_kernel_launches[c];
   }
+  for (int c = 4; c < ARTIS_KCLASS_COUNT; c++) {  // (classes 4-6 are class 3's parts)
+    ms[3] += G.last_kernel_ms[c];
+    launches[3] += G.last_kernel_launches[c];
+  }
+  return 0;
+}
+int artis_gpu_last_kernel_class_times(double ms[ARTIS_KCLASS_COUNT], int64_t launches[ARTIS_KCLASS_COUNT]) {
+  if (!ms || !launches) return ARTIS_ERR_BAD_ARGUMENT;
+  for (int c = 0; c < ARTIS_KCLASS_COUNT; c++) {
+    ms[c] = G.last_kernel_ms[c];
+    launches[c] = G.last_kernel_launches[c];
+  }
   return 0;
 }
 int artis_gpu_table_info(int64_t out[ARTIS_TABLE_INFO_COUNT]) {
@@ -2952,6 +2983,8 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     // ~250 ms more binning per step (profiles/r03g_ab.txt), so off unless asked for (ARTIS_GPU_R_BIN=1)
     const char *rb = getenv("ARTIS_GPU_R_BIN");
     G.r_binned = rb && rb[0] == '1';
+    const char *bb = getenv("ARTIS_GPU_MA_BIN_BLK");
+    G.ma_bin_blk = !(bb && bb[0] == '0');
     const char *xr = getenv("ARTIS_GPU_MA_XCD");
     G.W.ma_ranges = (xr && xr[0] == '1') ? 8 : 1;
     const char *rf = getenv("ARTIS_GPU_REFILL");
@@ -3160,6 +3193,17 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   rc |= dupload(&T.allcont_target, a->allcont_phixstargetindex, nb);
   rc |= dupload(&T.allcont_upperlevel, a->allcont_upperlevel, nb);
   rc |= dupload(&T.allcont_phixstable, a->allcont_phixstable, nb);
+  {
+    std::vector<BfCont> bc(std::max(1, nb));
+    for (int i = 0; i < nb; i++) {
+      bc[i].nu_edge = a->allcont_nu_edge[i];
+      bc[i].nu_max = a->allcont_nu_edge[i] * a->last_phixs_nuovernuedge;  // (bf_contribution's expression)
+      bc[i].probability = a->allcont_probability[i];
+      bc[i].xs_off = a->allcont_phixstable[i] * a->nphixspoints;
+      bc[i].pad = 0;
+    }
+    rc |= dupload(&T.bfc, bc.data(), bc.size());
+  }
   rc |= dupload(&T.allcont_groundindex, a->allcont_index_in_groundphixslist, nb);
   rc |= dupload(&T.groundcont_nu_edge, a->groundcont_nu_edge, a->nbfcontinua_ground);
   {
@@ -3395,7 +3439,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   rc |= dalloc(&C.pops, (size_t)nne_cells * nl);
   rc |= dalloc(&C.ionpop, (size_t)nne_cells * ni);
   rc |= dalloc(&C.ffsum, (size_t)nne_cells);
-  rc |= dalloc(&C.depratio, (size_t)nne_cells * nb);
+  rc |= dalloc(&C.bfcell, (size_t)nne_cells * nb);
   rc |= dalloc(&C.corrphot, (size_t)nne_cells * (ntg + 1));
   rc |= dalloc(&C.popsT, (size_t)nne_cells * nl);
   rc |= dalloc(&C.corrphotT, (size_t)nne_cells * (ntg + 1));

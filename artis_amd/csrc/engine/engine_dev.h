@@ -52,6 +52,14 @@ struct TeExcItem {
   int32_t forbidden;
 };
 
+// one bf continuum's constants for bf_contribution (rpkt.cc:1075-1207), one 32-byte load: its edge, the last
+// frequency of its cross-section table (nu_edge * last_phixs_nuovernuedge), probability, table offset
+struct BfCont {
+  double nu_edge, nu_max, probability;
+  int32_t xs_off;  // allcont_phixstable * nphixspoints
+  int32_t pad;
+};
+
 struct DevTab {
   int32_t nelements, maxnions, nions_total, nlevels_total, nlines, nbf, nbfg, ncoolingterms;
   int32_t nphixspoints, phixs_file_version, tablesize, ntargets_total;
@@ -83,6 +91,7 @@ struct DevTab {
   // order): (unique level index, offset of its macro-atom record in a cell block)
   const int2 *down_target, *up_target;
   const double *allcont_nu_edge, *allcont_probability;
+  const BfCont *bfc;  // [nbf]
   const int32_t *allcont_element, *allcont_ion, *allcont_level, *allcont_target, *allcont_upperlevel,
       *allcont_phixstable, *allcont_groundindex;
   const double *groundcont_nu_edge;
@@ -198,7 +207,9 @@ struct DevCells {
   double *pops;        // [n_nonempty * nlevels_total]  calculate_levelpop (ltepop.cc:417-430)
   double *ionpop;      // [n_nonempty * nions_total]    ionstagepop (ltepop.cc:558-564)
   double *ffsum;       // [n_nonempty]                  sum_ions Z^2 n_ion of calculate_kappa_ff (rpkt.cc:1036-1058)
-  double *depratio;    // [n_nonempty * nbf]            departure ratios (rpkt.cc:1140-1151)
+  // per (cell, continuum) {n_level if the continuum is included in the cell's kappa_bf (rpkt.cc:1116-1118) else 0,
+  // departure ratio (rpkt.cc:1140-1151)}: bf_contribution's cell data in one 16-byte load, no index chain
+  double2 *bfcell;     // [n_nonempty * nbf]
   double *corrphot;    // [n_nonempty * ntargets_total] get_corrphotoioncoeff (ratecoeff.cc:1247-1308)
   // level-major copies for k_marates, whose lanes run over consecutive cells of one level (coalesced reads)
   double *popsT;       // [nlevels_total * n_nonempty]
@@ -235,7 +246,10 @@ struct DevCells {
   // level mode (the records of every cell do not fit the budget, ma_rows == 0): records per (cell, level) in the
   // pool ma_key, for the pairs the walks used most in the previous timestep (engine.hip ma_level_place);
   // ma_lptr[k * nlevels_total + ul] is the first 128-byte line of the record, MA_NOLINE for a pair without one
-  // (k_ma evaluates its rates with the whole wave, ma_coop_select); ma_lhist counts every 16th jump per pair
+  // (k_ma evaluates its rates with the whole wave, ma_coop_select); ma_lhist counts the jumps per pair: a cached
+  // jump is sampled (every 16th jump of a walk adds 16), an exact-sum jump adds 1 (it is made by the whole wave over
+  // the level's rate list, so its one atomic is a small part of it, and the pairs without a record -- the ones the
+  // next placement must find -- are counted exactly)
   const uint32_t *ma_lptr;  // [n_nonempty * nlevels_total] or nullptr (row mode)
   uint32_t *ma_lhist;       // [n_nonempty * nlevels_total] or nullptr
   // few-cell models: offsets (doubles) of the J / nuJ / ffheating, bfrate and radfield-bin estimators of every

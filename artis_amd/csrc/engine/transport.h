@@ -390,32 +390,30 @@ DEVFN void change_cell(Tx &x, Pkt &p, int snext) {
 }
 
 // ------------------------------------------------------------------------------------------ opacity
-// rpkt.cc:1075-1207: one continuum's contribution sigma*prob*corr (returns false if not included / inactive)
-DEVFN bool bf_contribution(const Ctx &K, int k, int mgi, int i, double nu, double *nnlevel_out, double *gcontr_out) {
-  const int element = K.T.allcont_element[i];
-  const int ion = K.T.allcont_ion[i];
-  const int level = K.T.allcont_level[i];
-  const int ui = uion(K, element, ion);
-  // rpkt.cc:1116-1118: DETAILED_BF_ESTIMATORS_ON includes every continuum of an element present in the cell
-  if (K.R.detailed_bf) {
-    if (!(K.C.elem_abundance[(int64_t)mgi * K.T.nelements + element] > 0)) return false;
-  } else if (!((K.C.ionpop[(int64_t)k * K.T.nions_total + ui] / (double)K.C.nnetot[mgi] > 1.e-6) || (level == 0))) {
-    return false;
-  }
-  const double nu_edge = K.T.allcont_nu_edge[i];
-  const double nnlevel = K.C.pops[(int64_t)k * K.T.nlevels_total + K.T.ion_uniqueleveloffset[ui] + level];
-  const double nu_max_phixs = nu_edge * K.T.last_phixs_nuovernuedge;
-  if (!(nu <= nu_max_phixs && nnlevel > 0)) return false;
-  const double sigma_bf = photoionization_crosssection_fromtable(
-      K, K.T.phixs_xs + (int64_t)K.T.allcont_phixstable[i] * K.T.nphixspoints, nu_edge, nu);
-  const double probability = K.T.allcont_probability[i];
-  const double departure_ratio = K.C.depratio[(int64_t)k * K.T.nbf + i];
+// rpkt.cc:1075-1207: one continuum's contribution sigma*prob*corr (returns false if not included / inactive).
+// The cell's data come from its DevCells::bfcell row (n_level, or 0 when the inclusion rule of rpkt.cc:1116-1118
+// excludes the continuum, and the departure ratio), the continuum's from DevTab::bfc; `expfac` is
+// exp(-HOVERKB * nu / T_e), which the reference evaluates per continuum with the same arguments (BfCell::expfac).
+struct BfCell {
+  const double2 *row;  // DevCells::bfcell + k * nbf
+  double expfac;
+};
+DEVFN BfCell bf_cell(const Ctx &K, int k, int mgi, double nu) {
   const double T_e = K.C.Te[mgi];
-  const double stimfactor = departure_ratio * exp(-ARTIS_HOVERKB * nu / T_e);
+  return BfCell{K.C.bfcell + (int64_t)k * K.T.nbf, exp(-ARTIS_HOVERKB * nu / T_e)};
+}
+DEVFN bool bf_contribution(const Ctx &K, const BfCell &cell, int i, double nu, double *nnlevel_out,
+                           double *gcontr_out) {
+  const BfCont c = K.T.bfc[i];
+  const double2 cb = cell.row[i];
+  const double nnlevel = cb.x;
+  if (!(nu <= c.nu_max && nnlevel > 0)) return false;
+  const double sigma_bf = photoionization_crosssection_fromtable(K, K.T.phixs_xs + c.xs_off, c.nu_edge, nu);
+  const double stimfactor = cb.y * cell.expfac;
   double corrfactor = 1 - stimfactor;
   if (corrfactor < 0) corrfactor = 0.;
   *nnlevel_out = nnlevel;
-  *gcontr_out = sigma_bf * probability * corrfactor;
+  *gcontr_out = sigma_bf * c.probability * corrfactor;
   return true;
 }
 // rpkt.cc:1075-1207 calculate_kappa_bf_gammacontr: the kappa_bf total (the cumulative array is re-scanned on demand)
@@ -423,6 +421,7 @@ DEVFN double kappa_bf_total(Tx &x, int k, int mgi, double nu) {
   const Ctx &K = x.K;
   double kappa_bf_sum = 0.;
   unsigned long long nactive = 0;
+  const BfCell cell = bf_cell(K, k, mgi, nu);
   for (int i = 0; i < K.T.nbf; i++) {
     if (nu < K.T.allcont_nu_edge[i]) {
       // the reference breaks at the first included continuum with nu < nu_edge; sorted edges => nothing
@@ -431,7 +430,7 @@ DEVFN double kappa_bf_total(Tx &x, int k, int mgi, double nu) {
     }
     nactive++;
     double nnlevel, gc;
-    if (bf_contribution(K, k, mgi, i, nu, &nnlevel, &gc)) kappa_bf_sum += nnlevel * gc;
+    if (bf_contribution(K, cell, i, nu, &nnlevel, &gc)) kappa_bf_sum += nnlevel * gc;
   }
   lwork(x.L, WK_BF_ACTIVE, nactive);
   x.wb += (unsigned)nactive;
@@ -895,13 +894,14 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
     const double dopplerfactor = doppler_packet(K, p);
     const double d_over_nu = distance_e_cmf / nu * dopplerfactor;
     const int64_t row = (int64_t)mgi * K.T.nbf;
+    const BfCell cell = bf_cell(K, k, mgi, kap.nu);
     for (int i = 0; i < K.T.nbf; i++) {
       const double nu_edge = K.T.allcont_nu_edge[i];
       const double nu_max_phixs = nu_edge * K.T.last_phixs_nuovernuedge;
       if (nu >= nu_edge && nu <= nu_max_phixs) {
         double gc = 0., nnlevel;
         // (without do_r_lc no bf opacity is evaluated and the zero-initialised gamma_contr stays 0, rpkt.cc:1230)
-        if (!K.R.do_r_lc || (!(kap.nu < nu_edge) && !bf_contribution(K, k, mgi, i, kap.nu, &nnlevel, &gc))) gc = 0.;
+        if (!K.R.do_r_lc || (!(kap.nu < nu_edge) && !bf_contribution(K, cell, i, kap.nu, &nnlevel, &gc))) gc = 0.;
         if (x.est_lds && K.C.est_lds_bf >= 0)
           atomicAdd(&x.est_lds[K.C.est_lds_bf + (int64_t)k * K.T.nbf + i], gc * d_over_nu);
         else
@@ -928,6 +928,7 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
   // the ground-continuum estimators exist unless both NO_LUT_PHOTOION and NO_LUT_BFHEATING (rpkt.cc:573-614)
   if (K.R.no_lut_photoion && K.R.no_lut_bfheating) return;
   const double distance_e_cmf_over_nu = distance_e_cmf / nu;
+  const BfCell cell = bf_cell(K, k, mgi, kap.nu);
   for (int g = 0; g < K.T.nbfg; g++) {
     const double nu_edge = K.T.groundcont_nu_edge[g];
     if (nu > nu_edge) {
@@ -940,7 +941,7 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
           const int i = K.T.gc_cont[q];
           if (kap.nu < K.T.allcont_nu_edge[i]) break;
           double nnlevel, gc;
-          if (bf_contribution(K, k, mgi, i, kap.nu, &nnlevel, &gc)) gcontr += gc;
+          if (bf_contribution(K, cell, i, kap.nu, &nnlevel, &gc)) gcontr += gc;
         }
         const int ion = K.T.groundcont_ion[g];
         const int64_t idx = (int64_t)mgi * K.T.nelements * K.T.maxnions + element * K.T.maxnions + ion;
@@ -988,7 +989,7 @@ DEVFN void wave_flush_estimators(Tx &x) {
 
 // the block's LDS estimator accumulator: zeroed at the start of k_rpkt, added to the estimators at its end (one
 // atomic per non-zero entry and block)
-DEVFN bool est_lds_on(const Ctx &K) { return K.C.est_lds_J >= 0 || K.C.est_lds_bf >= 0 || K.C.est_lds_rf >= 0; }
+__host__ __device__ inline bool est_lds_on(const Ctx &K) { return K.C.est_lds_J >= 0 || K.C.est_lds_bf >= 0 || K.C.est_lds_rf >= 0; }
 DEVFN void est_lds_zero(double *e) {
   for (int i = threadIdx.x; i < EST_LDS_DOUBLES; i += blockDim.x) e[i] = 0.;
   __syncthreads();
@@ -1124,10 +1125,11 @@ DEVNI void rpkt_event_continuum(Tx &x, Pkt &p, const Kappa &kap, int k, int mgi)
     const int last = K.T.nbf - 1;
     int allcontindex = last;
     double running = 0.;
+    const BfCell cell = bf_cell(K, k, mgi, kap.nu);
     for (int i = 0; i < last; i++) {
       if (!(kap.nu < K.T.allcont_nu_edge[i])) {
         double nnlevel, gc;
-        if (bf_contribution(K, k, mgi, i, kap.nu, &nnlevel, &gc)) running += nnlevel * gc;
+        if (bf_contribution(K, cell, i, kap.nu, &nnlevel, &gc)) running += nnlevel * gc;
       }
       if (!(running < kappa_bf_rand)) {
         allcontindex = i;
@@ -1508,31 +1510,50 @@ struct MaLaneC {
   unsigned jumps;
   unsigned long long ntrans;
 };
+// The context fields a macro-atom jump reads, held in scalar registers by k_ma (ma_hot(*ctxp): loaded once from the
+// device context at kernel entry).  Read from the context copy in LDS instead, every use was an LDS load whose
+// result the compiler re-read after the kernel's LDS stores (the record-line staging), a dependent LDS round trip
+// in front of the jump's global loads; the pointers also lived in vector registers.
+struct MaHot {
+  const uint16_t *ma_key;
+  const MaMeta *ma_meta;
+  const int2 *down_target, *up_target;
+  const uint32_t *ma_lptr;
+  uint32_t *ma_lhist;
+  int32_t nlevels_total;
+};
+DEVFN MaHot ma_hot(const Ctx &K) {
+  return MaHot{K.C.ma_key, K.T.ma_meta, K.T.down_target, K.T.up_target, K.C.ma_lptr, K.C.ma_lhist, K.T.nlevels_total};
+}
 // the record line of level ul (MaMeta::rec_off rec_off) in the walk's cell
-DEVFN uint32_t ma_line(const Ctx &K, int32_t rowline, int k, int ul, int rec_off) {
+DEVFN uint32_t ma_line(const MaHot &H, int32_t rowline, int k, int ul, int rec_off) {
   if (rowline >= 0) return (uint32_t)rowline + ((uint32_t)rec_off >> 6);
-  return K.C.ma_lptr ? K.C.ma_lptr[(int64_t)k * K.T.nlevels_total + ul] : MA_NOLINE;
+  return H.ma_lptr ? H.ma_lptr[(int64_t)k * H.nlevels_total + ul] : MA_NOLINE;
+}
+DEVFN uint32_t ma_line(const Ctx &K, int32_t rowline, int k, int ul, int rec_off) {
+  return ma_line(ma_hot(K), rowline, k, ul, rec_off);
 }
 DEVFN int32_t ma_rowline(const Ctx &K, int k) {
   const int row = K.C.ma_row[k];
   return row >= 0 ? (int32_t)(((int64_t)row * K.C.ma_key_stride) >> 6) : -1;
 }
-DEVFN void ma_set_level(const Ctx &K, MaLaneC &m, int ul) {
+DEVFN void ma_set_level(const MaHot &H, MaLaneC &m, int ul) {
   m.ul = ul;
-  m.line = ma_line(K, m.rowline, m.k, ul, K.T.ma_meta[ul].rec_off);
+  m.line = ma_line(H, m.rowline, m.k, ul, H.ma_meta[ul].rec_off);
 }
+DEVFN void ma_set_level(const Ctx &K, MaLaneC &m, int ul) { ma_set_level(ma_hot(K), m, ul); }
 
 // the outcome of selecting transition j (reference list order) of action sel at level ul: MA_CONTINUE with the
 // lane moved to the target level, or a deactivation in `end` (macroatom.cc:174-414)
-DEVFN int ma_apply_selection(const Ctx &K, const LocalCounters &L, MaLaneC &m, MaEnd &end, int sel, int j, int doff,
-                             int uoff, int base_lower) {
+DEVFN int ma_apply_selection(const Ctx &K, const MaHot &H, const LocalCounters &L, MaLaneC &m, MaEnd &end, int sel,
+                             int j, int doff, int uoff, int base_lower) {
   const int ul = m.ul;
   switch (sel) {
     case ARTIS_MA_ACTION_INTERNALDOWNSAME:
-      ma_set_level(K, m, K.T.ion_uniqueleveloffset[K.T.level_ui[ul]] + K.T.line_lower[K.T.downtrans_lineindex[doff + j]]);
+      ma_set_level(H, m, K.T.ion_uniqueleveloffset[K.T.level_ui[ul]] + K.T.line_lower[K.T.downtrans_lineindex[doff + j]]);
       return MA_CONTINUE;
     case ARTIS_MA_ACTION_INTERNALUPSAME:
-      ma_set_level(K, m, K.T.ion_uniqueleveloffset[K.T.level_ui[ul]] + K.T.line_upper[K.T.uptrans_lineindex[uoff + j]]);
+      ma_set_level(H, m, K.T.ion_uniqueleveloffset[K.T.level_ui[ul]] + K.T.line_upper[K.T.uptrans_lineindex[uoff + j]]);
       return MA_CONTINUE;
     case ARTIS_MA_ACTION_RADDEEXC:
       // the line index is looked up by ma_finish (end.a = -1 - downtrans slot): a load here would hold the whole
@@ -1550,12 +1571,12 @@ DEVFN int ma_apply_selection(const Ctx &K, const LocalCounters &L, MaLaneC &m, M
       return MA_END_FB;
     case ARTIS_MA_ACTION_INTERNALDOWNLOWER:
       lctr(L, CTR_MA_STAT_INTERNALDOWNLOWER);
-      ma_set_level(K, m, base_lower + j);
+      ma_set_level(H, m, base_lower + j);
       return MA_CONTINUE;
     default: {  // INTERNALUPHIGHER (macroatom.cc:382-414)
       lctr(L, CTR_MA_STAT_INTERNALUPHIGHER);
       const int ui = K.T.level_ui[ul];
-      ma_set_level(K, m, K.T.ion_uniqueleveloffset[ui + 1] + K.T.phixstarget_levelindex[K.T.level_phixstargets_offset[ul] + j]);
+      ma_set_level(H, m, K.T.ion_uniqueleveloffset[ui + 1] + K.T.phixstarget_levelindex[K.T.level_phixstargets_offset[ul] + j]);
       return MA_CONTINUE;
     }
   }
@@ -1643,7 +1664,7 @@ DEVNI int ma_jump_exact(const Ctx &K, const LocalCounters &L, artis_rng &rng, Ma
     fail(K, ERR_MA_SELECT, number, 10 + sel);
     return MA_FAILED;
   }
-  return ma_apply_selection(K, L, m, end, sel, found, mm.doff, mm.uoff, mm.base_lower);
+  return ma_apply_selection(K, ma_hot(K), L, m, end, sel, found, mm.doff, mm.uoff, mm.base_lower);
 }
 
 // MA_DEFER: a key comparison was undecided; the jump has not happened (m.jumps unchanged) and the caller resets
@@ -1704,12 +1725,13 @@ struct MaMetaW {
 // (rec_off, w0.x, is not loaded: a dead load destination let the register allocator reuse it for the Philox
 // temporaries, which then waited for the record fetch; profiles/r03k_ab.txt: k_ma 1790 -> 1767 ms)
 typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
-DEVFN MaMetaW ma_meta_load(const Ctx &K, int ul) {
-  glb_uint4 *mp = (glb_uint4 *)(K.T.ma_meta + ul);
+DEVFN MaMetaW ma_meta_load(const MaMeta *ma_meta, int ul) {
+  glb_uint4 *mp = (glb_uint4 *)(ma_meta + ul);
   const u32x3 a = *(const __attribute__((address_space(1))) u32x3 *)((const __attribute__((address_space(1))) uint32_t *)mp + 1);
   const u32x4 b = mp[1];
   return MaMetaW{make_int4(0, (int)a.x, (int)a.y, (int)a.z), make_int4((int)b.x, (int)b.y, (int)b.z, (int)b.w)};
 }
+DEVFN MaMetaW ma_meta_load(const Ctx &K, int ul) { return ma_meta_load(K.T.ma_meta, ul); }
 
 // The cached walk as a resumable per-pass step (k_ma).  In SIMT every pass of a wave lasts as long as its slowest
 // lane; a search that probed record lines other than the staged one made one dependent trip to memory per probe,
@@ -1883,8 +1905,8 @@ int ma_coop_search(const Ctx &K, int k, int ul, int sel, double x, double t_mid,
 }
 // the lane's side of that jump: its RNG draws (the action draw, then the transition's or the NT ion's), the jump
 // count and histogram, and the selection applied as in the cached step
-DEVFN int ma_coop_apply(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneR &m, MaEnd &end, int number,
-                        int sel, int j, unsigned probes, const MaMetaW &meta) {
+DEVFN int ma_coop_apply(const Ctx &K, const MaHot &H, const LocalCounters &L, artis_rng &rng, MaLaneR &m, MaEnd &end,
+                        int number, int sel, int j, unsigned probes, const MaMetaW &meta) {
   m.n0 = rng.n;
   rng.n++;
   m.ntrans += probes;
@@ -1897,7 +1919,8 @@ DEVFN int ma_coop_apply(const Ctx &K, const LocalCounters &L, artis_rng &rng, Ma
     return MA_FAILED;
   }
   m.jumps++;
-  if (K.C.ma_lhist) atomicAdd(&K.C.ma_lhist[(int64_t)m.k * K.T.nlevels_total + m.ul], 1u);
+  // (counted exactly, not sampled like the cached jumps: see DevCells::ma_lhist)
+  if (H.ma_lhist) atomicAdd(&H.ma_lhist[(int64_t)m.k * H.nlevels_total + m.ul], 1u);
   if (sel == ARTIS_MA_ACTION_COLDEEXC || sel == ARTIS_MA_ACTION_COLRECOMB) {
     end.code = (sel == ARTIS_MA_ACTION_COLDEEXC) ? MA_END_COLDEEXC : MA_END_COLRECOMB;
     end.ion = end.a = end.b = 0;
@@ -1905,7 +1928,7 @@ DEVFN int ma_coop_apply(const Ctx &K, const LocalCounters &L, artis_rng &rng, Ma
   }
   if (sel == ARTIS_MA_ACTION_INTERNALUPHIGHERNT) return ma_apply_nt(K, L, rng, m, number);
   rng.n++;
-  return ma_apply_selection(K, L, m, end, sel, j, meta.w0.y, meta.w0.z, meta.w0.w);
+  return ma_apply_selection(K, H, L, m, end, sel, j, meta.w0.y, meta.w0.z, meta.w0.w);
 }
 
 // where a step reads record keys (high halves): k_ma's staged line, or the whole record in global memory
@@ -1927,8 +1950,8 @@ struct KeysGlobal {
 // meta: the level's MaMetaW (k_ma loads it beside the record-line fetch); z1, z2: the values of the lane's next two
 // draws (used only by a step that starts a jump; the RNG counter advances over the draws the jump consumes)
 template <class Keys>
-DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneR &m, MaEnd &end, int number,
-                         const Keys &keys, const MaMetaW &meta, double z1, double z2) {
+DEVFN int ma_step_cached(const Ctx &K, const MaHot &H, const LocalCounters &L, artis_rng &rng, MaLaneR &m, MaEnd &end,
+                         int number, const Keys &keys, const MaMetaW &meta, double z1, double z2) {
 #ifdef ARTIS_STAMPS_SUB  // diagnostic: cycles of the step's sections, added by the first active lane
   struct SubStamp {
     const LocalCounters &L;
@@ -1949,7 +1972,7 @@ DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
   do {               \
   } while (0)
 #endif
-  const uint16_t *rec = K.C.ma_key + (size_t)m.line * 64;
+  const uint16_t *rec = H.ma_key + (size_t)m.line * 64;
   const int doff = meta.w0.y, uoff = meta.w0.z, base_lower = meta.w0.w;
   const int nd = meta.w1.x, nu = meta.w1.y, nr = meta.w1.z, nt = meta.w1.w;
   const MaLayout lay = ma_layout(nd, nu, nr, nt);
@@ -1988,7 +2011,7 @@ DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
     if (sel < 0) return MA_DEFER;
     m.jumps++;
     // level mode: every 16th jump of a walk credits its (cell, level) pair for the next record placement
-    if (K.C.ma_lhist && (m.jumps & 15u) == 0u) atomicAdd(&K.C.ma_lhist[(int64_t)m.k * K.T.nlevels_total + m.ul], 16u);
+    if (H.ma_lhist && (m.jumps & 15u) == 0u) atomicAdd(&H.ma_lhist[(int64_t)m.k * H.nlevels_total + m.ul], 16u);
     if (sel == ARTIS_MA_ACTION_COLDEEXC || sel == ARTIS_MA_ACTION_COLRECOMB) {
       end.code = (sel == ARTIS_MA_ACTION_COLDEEXC) ? MA_END_COLDEEXC : MA_END_COLRECOMB;
       end.ion = end.a = end.b = 0;
@@ -2086,9 +2109,9 @@ DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
       return MA_FAILED;
     }
     typedef const __attribute__((address_space(1))) uint64_t glb_u64;
-    const uint64_t tw = *(glb_u64 *)(down ? K.T.down_target + doff + j : K.T.up_target + uoff + j);
+    const uint64_t tw = *(glb_u64 *)(down ? H.down_target + doff + j : H.up_target + uoff + j);
     m.ul = (int)(uint32_t)tw;
-    m.line = ma_line(K, m.rowline, m.k, m.ul, (int)(uint32_t)(tw >> 32));
+    m.line = ma_line(H, m.rowline, m.k, m.ul, (int)(uint32_t)(tw >> 32));
     return MA_CONTINUE;
   }
   const bool found = lo < m.end;
@@ -2098,7 +2121,7 @@ DEVFN int ma_step_cached(const Ctx &K, const LocalCounters &L, artis_rng &rng, M
     fail(K, ERR_MA_SELECT, number, 10 + sel);
     return MA_FAILED;
   }
-  return ma_apply_selection(K, L, m, end, sel, lo, doff, uoff, base_lower);
+  return ma_apply_selection(K, H, L, m, end, sel, lo, doff, uoff, base_lower);
 }
 
 // One whole jump of the cached walk from the record in global memory (the megakernel's do_macroatom): the step
@@ -2115,7 +2138,7 @@ DEVFN int ma_jump_cached_global(const Ctx &K, const LocalCounters &L, artis_rng 
   const KeysGlobal keys{K.C.ma_key + (size_t)m.line * 64};
   int r;
   do {
-    r = ma_step_cached(K, L, rng, m, end, number, keys, meta, z1, z2);
+    r = ma_step_cached(K, ma_hot(K), L, rng, m, end, number, keys, meta, z1, z2);
   } while (r == MA_PENDING);
   if (r == MA_DEFER) rng.n = m.n0;
   mc = static_cast<MaLaneC &>(m);

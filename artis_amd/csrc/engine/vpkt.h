@@ -402,8 +402,10 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
     // so a line reads its two values with two LDS loads instead of selecting them out of 32 registers;
     // dtau = coefficient * t_line is the reference's (B_lu n_l - B_ul n_u) * HCLIGHTOVERFOURPI * t_line in the same
     // operation order.  vpkt_alive (vpkt.cc:293) is tested when the walk leaves a window and when it ends, not after
-    // every line: the tau only grow, so a virtual packet that dies inside a window is still dead there and is killed
-    // the same; only the lines added after its death (diagnostic count) differ from the reference's loop.
+    // every line: the tau grow with every line of positive coefficient, so a virtual packet that dies inside a window
+    // is still dead there and is killed the same; a line of negative coefficient (population inversion) first checks
+    // whether the packet is already dead.  Only the lines added after its death (diagnostic count) differ from the
+    // reference's loop.
     const int nlines = K.T.nlines;
     const double *lnu = K.T.line_nu, *nu8 = K.T.line_nu8;
     const double *crow = K.C.linecoef + (int64_t)K.C.ne_index[v.mgi] * K.C.linecoef_stride;
@@ -455,6 +457,12 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
       lines++;
       const double t_line = t_current + ldist / ARTIS_CLIGHT;
       const double dtau = win[(LC_WIN + pj) * WAVE_BLOCK_T] * t_line;
+      // a population inversion (NLTE) gives a negative coefficient: the only way a tau can fall again, so a
+      // virtual packet that died at an earlier line of the window is killed here, before it could revive
+      if (dtau < 0. && all_dead()) {
+        v.inlines = false;
+        return VSEG_KILLED;
+      }
 #pragma unroll
       for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
         if ((lm >> ind) & 1u) v.tau[ind] += dtau;

@@ -180,7 +180,9 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
   x.nts = nts;
   x.win = (__attribute__((address_space(3))) double *)&s_win[0][threadIdx.x];
   x.defer_est = true;
-  __shared__ double s_est[EST_LDS_DOUBLES];  // few-cell models: the block's estimator accumulator
+  // few-cell models: the block's estimator accumulator, EST_LDS_DOUBLES of dynamic LDS (none is allocated when
+  // est_lds_on is false, so the other models keep k_rpkt's LDS at the line windows and the context)
+  extern __shared__ double s_est[];
   const bool est_lds = est_lds_on(K);
   if (est_lds) {
     est_lds_zero(s_est);
@@ -373,41 +375,129 @@ __global__ void k_ma_bin(const Ctx *__restrict__ ctxp, WaveState W, const uint64
 // scatter into cell order using the exclusive prefix sum of the counts.  Each slot becomes a ticket holding
 // everything k_ma's refill needs (the walk's level, record line, cell, RNG stream and jump count), so a k_ma lane
 // starts a walk with one coalesced read instead of a chain of dependent packet and table loads.
+DEVFN void ma_ticket(const Ctx &K, const WaveState &W, const uint64_t *__restrict__ soa, int64_t n, int32_t idx,
+                     uint32_t pos) {
+  if (!W.ma_tick) {
+    W.ma_sorted[pos] = idx;
+    return;
+  }
+  const int where = lo32(soa[PW(n, idx, 0)]);
+  const uint64_t w36 = soa[PW(n, idx, 36)], w37 = soa[PW(n, idx, 37)];
+  const int number = (int)hi32(soa[PW(n, idx, 33)]);
+  const int4 pd = W.pend[idx];
+  int ul;
+  unsigned jumps;
+  if (pd.x == MA_RESUME) {  // a walk parked by k_ma_exact: continue from its level and jump count
+    ul = pd.y;
+    jumps = W.pend_jumps[idx];
+    W.pend[idx].x = 0;
+  } else {
+    ul = ulev(K, lo32(w36), hi32(w36), lo32(w37));
+    jumps = 0;
+  }
+  const int mgi = cell_mgi(K, where);
+  int32_t tidx = idx;
+  if (K.C.thick[mgi] == 1) {
+    fail(K, ERR_THICK_MA, number, mgi);
+    tidx = -1;
+  }
+  const int k = K.C.ne_index[mgi];
+  const int32_t rowline = ma_rowline(K, k);
+  W.ma_tick[2 * (int64_t)pos] = make_int4(tidx, ul, (int)ma_line(K, rowline, k, ul, K.T.ma_meta[ul].rec_off), k);
+  W.ma_tick[2 * (int64_t)pos + 1] = make_int4(number, (int)W.rng_n[idx], (int)jumps, rowline);
+}
 __global__ void k_ma_scatter(const Ctx *__restrict__ ctxp, WaveState W, const uint64_t *__restrict__ soa, int64_t n,
                              uint32_t *offs) {
   CTX_IN_LDS(ctxp)
   const uint32_t nq = W.ctr[2 * QM];
-  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x) {
-    const int32_t idx = W.q[QM][slot];
-    const uint32_t pos = atomicAdd(&offs[W.ma_key[slot]], 1u);
-    if (!W.ma_tick) {
-      W.ma_sorted[pos] = idx;
-      continue;
+  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x)
+    ma_ticket(K, W, soa, n, W.q[QM][slot], atomicAdd(&offs[W.ma_key[slot]], 1u));
+}
+
+// Few-cell models (n_nonempty + 1 <= MA_BIN_LDS bins: the 1D shell models, the one-zone nebular model): the same
+// counting sort with block-local counts.  k_ma_bin / k_ma_scatter above add one device-scope atomic per queue entry
+// to W.bins / offs; with 1, 25 or 100 bins those land on a handful of addresses and serialise (round 4: ~3.4 s of a
+// 5.6 s W7-like step, ~35 s of a kilonova step).  Here each block counts a contiguous chunk of the queue in LDS and
+// adds one atomic per non-empty bin; the scatter counts its chunk again, reserves the block's run of each bin with
+// one atomic, and places its entries with LDS atomics.  A wave whose active lanes share one bin (the common case
+// with one or few cells) adds to the LDS count once.  The order within a bin stays arbitrary (each packet draws
+// from its own RNG stream: placement never changes a result).
+#define MA_BIN_LDS 8192
+DEVFN void ma_bin_chunk(uint32_t nq, uint32_t &lo, uint32_t &hi) {
+  // contiguous chunks of whole blocks' width, at least 1024 entries: a short queue occupies few blocks
+  uint32_t chunk = (nq + gridDim.x - 1) / gridDim.x;
+  chunk = max(1024u, (chunk + WAVE_BLOCK - 1) / WAVE_BLOCK * WAVE_BLOCK);
+  lo = min(nq, (uint32_t)blockIdx.x * chunk);
+  hi = min(nq, lo + chunk);
+}
+// add 1 to h[b] for every active lane, return the lane's previous count (its rank); wave-uniform call
+DEVFN uint32_t lds_bin_add(uint32_t *h, int b, bool active) {
+  const unsigned long long am = __ballot(active);
+  if (!am) return 0;
+  const int lead = __ffsll((long long)am) - 1;
+  const int b0 = __shfl(b, lead, 64);
+  if (__all(!active || b == b0)) {
+    uint32_t base = 0;
+    if (lane_id() == lead) base = atomicAdd(&h[b0], (uint32_t)__popcll(am));
+    base = __shfl(base, lead, 64);
+    return base + (uint32_t)__popcll(am & ((1ull << lane_id()) - 1ull));
+  }
+  return active ? atomicAdd(&h[b], 1u) : 0u;
+}
+__global__ __launch_bounds__(WAVE_BLOCK) void k_ma_bin_blk(const Ctx *__restrict__ ctxp, WaveState W,
+                                                           const uint64_t *__restrict__ soa) {
+  CTX_IN_LDS(ctxp)
+  __shared__ uint32_t h[MA_BIN_LDS];
+  const uint32_t nq = W.ctr[2 * QM];
+  uint32_t lo, hi;
+  ma_bin_chunk(nq, lo, hi);
+  if (lo >= hi) return;  // (block-uniform)
+  const int nb = K.C.n_nonempty + 1;
+  for (int j = threadIdx.x; j < nb; j += blockDim.x) h[j] = 0;
+  __syncthreads();
+  for (uint32_t s0 = lo; s0 < hi; s0 += blockDim.x) {
+    const uint32_t slot = s0 + threadIdx.x;
+    const bool act = slot < hi;
+    int b = 0;
+    if (act) {
+      const int32_t idx = W.q[QM][slot];
+      b = K.C.ma_bin[K.C.ne_index[cell_mgi(K, lo32(soa[PW(0, idx, 0)]))]];  // hot group: no n term
+      W.ma_key[slot] = b;
     }
-    const int where = lo32(soa[PW(n, idx, 0)]);
-    const uint64_t w36 = soa[PW(n, idx, 36)], w37 = soa[PW(n, idx, 37)];
-    const int number = (int)hi32(soa[PW(n, idx, 33)]);
-    const int4 pd = W.pend[idx];
-    int ul;
-    unsigned jumps;
-    if (pd.x == MA_RESUME) {  // a walk parked by k_ma_exact: continue from its level and jump count
-      ul = pd.y;
-      jumps = W.pend_jumps[idx];
-      W.pend[idx].x = 0;
-    } else {
-      ul = ulev(K, lo32(w36), hi32(w36), lo32(w37));
-      jumps = 0;
-    }
-    const int mgi = cell_mgi(K, where);
-    int32_t tidx = idx;
-    if (K.C.thick[mgi] == 1) {
-      fail(K, ERR_THICK_MA, number, mgi);
-      tidx = -1;
-    }
-    const int k = K.C.ne_index[mgi];
-    const int32_t rowline = ma_rowline(K, k);
-    W.ma_tick[2 * (int64_t)pos] = make_int4(tidx, ul, (int)ma_line(K, rowline, k, ul, K.T.ma_meta[ul].rec_off), k);
-    W.ma_tick[2 * (int64_t)pos + 1] = make_int4(number, (int)W.rng_n[idx], (int)jumps, rowline);
+    (void)lds_bin_add(h, b, act);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < nb; j += blockDim.x)
+    if (h[j]) atomicAdd(&W.bins[j], h[j]);
+}
+__global__ __launch_bounds__(WAVE_BLOCK) void k_ma_scatter_blk(const Ctx *__restrict__ ctxp, WaveState W,
+                                                               const uint64_t *__restrict__ soa, int64_t n,
+                                                               uint32_t *offs) {
+  CTX_IN_LDS(ctxp)
+  __shared__ uint32_t h[MA_BIN_LDS];
+  const uint32_t nq = W.ctr[2 * QM];
+  uint32_t lo, hi;
+  ma_bin_chunk(nq, lo, hi);
+  if (lo >= hi) return;
+  const int nb = K.C.n_nonempty + 1;
+  for (int j = threadIdx.x; j < nb; j += blockDim.x) h[j] = 0;
+  __syncthreads();
+  for (uint32_t s0 = lo; s0 < hi; s0 += blockDim.x) {
+    const uint32_t slot = s0 + threadIdx.x;
+    const bool act = slot < hi;
+    (void)lds_bin_add(h, act ? W.ma_key[slot] : 0, act);
+  }
+  __syncthreads();
+  // this block's run of every bin it holds: one device atomic per (block, bin)
+  for (int j = threadIdx.x; j < nb; j += blockDim.x)
+    if (h[j]) h[j] = atomicAdd(&offs[j], h[j]);
+  __syncthreads();
+  for (uint32_t s0 = lo; s0 < hi; s0 += blockDim.x) {
+    const uint32_t slot = s0 + threadIdx.x;
+    const bool act = slot < hi;
+    const int key = act ? W.ma_key[slot] : 0;
+    const uint32_t pos = lds_bin_add(h, key, act);
+    if (act) ma_ticket(K, W, soa, n, W.q[QM][slot], pos);
   }
 }
 
@@ -441,6 +531,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   const int nr_log2 = (nr == 8) ? 3 : 0;  // W.ma_ranges is 1 or 8
   const double t_mid = K.G.ts_mid[nts];
   [[maybe_unused]] const int lane = lane_id();
+  const MaHot H = ma_hot(*ctxp);  // (scalar loads from the device context: kept in SGPRs, MaHot)
   MaLaneR mc;
   artis_rng rng = artis_rng_init(K.R.seed, 0, nts, K.R.rank);
   int32_t idx = -1;
@@ -498,11 +589,11 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
           mc.k = K.C.ne_index[mgi];
           mc.rowline = ma_rowline(K, mc.k);
           if (pd.x == MA_RESUME) {  // a walk parked by k_ma_exact: continue from its level and jump count
-            ma_set_level(K, mc, pd.y);
+            ma_set_level(H, mc, pd.y);
             mc.jumps = W.pend_jumps[idx];
             W.pend[idx].x = 0;
           } else {
-            ma_set_level(K, mc, ulev(K, lo32(w36), hi32(w36), lo32(w37)));
+            ma_set_level(H, mc, ulev(K, lo32(w36), hi32(w36), lo32(w37)));
             mc.jumps = 0;
           }
           mc.ntrans = 0;
@@ -535,10 +626,10 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     {
       // the level's metadata and, 8 lines per load instruction, every busy lane's record line; the lane's next two
       // draws are computed while they are in flight
-      if (have) meta = ma_meta_load(K, mc.ul);
+      if (have) meta = ma_meta_load(H.ma_meta, mc.ul);
       const uint32_t myline = (have && !unc) ? mc.line + (uint32_t)mc.pline : 0xffffffffu;
       WaveLines wl;
-      wave_fetch_issue(K.C.ma_key, myline, wl, (lds_u32 *)&s_xidx[threadIdx.x >> 6][0]);
+      wave_fetch_issue(H.ma_key, myline, wl, (lds_u32 *)&s_xidx[threadIdx.x >> 6][0]);
       if (have && mc.sel < 0) {
 #ifdef ARTIS_DIAG_CHEAPRNG  // timing diagnostic only (wrong stream): the walk's cost without Philox
         uint64_t h = ((uint64_t)rng.key1 << 32) ^ rng.n;
@@ -561,7 +652,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     MaEnd e;
     int r = MA_PENDING;
     if (have && !unc) {
-      r = ma_step_cached(K, L, rng, mc, e, (int)rng.key1, KeysLds<LEVEL && ARTIS_MA_HI_ONLY>{line, mc.pline}, meta,
+      r = ma_step_cached(K, H, L, rng, mc, e, (int)rng.key1, KeysLds<LEVEL && ARTIS_MA_HI_ONLY>{line, mc.pline}, meta,
                          z1, z2);
 #ifdef ARTIS_STAMPS
       ts2 = wave_clock();
@@ -592,7 +683,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
       if (unc_now) {
         csel = ma_coop_action(K, mc.k, mc.ul, z1, z2, &cx);
         if (!ma_coop_needs_search(csel)) {
-          r = ma_coop_apply(K, L, rng, mc, e, (int)rng.key1, csel, -1, 0u, meta);
+          r = ma_coop_apply(K, H, L, rng, mc, e, (int)rng.key1, csel, -1, 0u, meta);
           coop_sum++;
         }
       }
@@ -608,7 +699,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
         unsigned probes = 0;
         const int sel = ma_coop_search(K, k, ul, sl, readlane_d(cx, ld), t_mid, &j, probes);
         if (lane == ld) {
-          r = ma_coop_apply(K, L, rng, mc, e, (int)rng.key1, sel, j, probes, meta);
+          r = ma_coop_apply(K, H, L, rng, mc, e, (int)rng.key1, sel, j, probes, meta);
           coop_sum++;
         }
       }
@@ -750,7 +841,7 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
         static_cast<MaLaneC &>(mr) = m;
         mr.jumps = W.pend_jumps[idx];  // (ma_coop_apply counts the jump)
         MaEnd e{};
-        const int r = ma_coop_apply(K, L, rng, mr, e, number, sel, j, probes, ma_meta_load(K, ul));
+        const int r = ma_coop_apply(K, ma_hot(K), L, rng, mr, e, number, sel, j, probes, ma_meta_load(K, ul));
         lwork(L, WK_MA_TRANS, mr.ntrans);
         n_exact++;  // (stats[40], [45]: added once per block, not once per jump on one address)
         W.rng_n[idx] = rng.n;
@@ -849,7 +940,8 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
         if (lane == 0) fail(K, ERR_MA_SELECT, number, 10 + sel);
         r = MA_FAILED;
       } else {
-        r = (lane == 0) ? ma_apply_selection(K, L, m, e, sel, found, mm.doff, mm.uoff, mm.base_lower) : MA_CONTINUE;
+        r = (lane == 0) ? ma_apply_selection(K, ma_hot(K), L, m, e, sel, found, mm.doff, mm.uoff, mm.base_lower)
+                        : MA_CONTINUE;
       }
     }
     if (lane == 0) {

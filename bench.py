@@ -56,7 +56,11 @@ def byte_model(work, nions_total, probe_bytes=8.0):
             + 32.0 * w[7])
     ma = 72.0 * w[8] + probe_bytes * w[9]
     kpkt = 16.0 * w[11]
-    return {"rpkt": rpkt, "ma": ma, "kpkt": kpkt}
+    # macro-atom activations (bound-bound + continuum absorptions): each is binned into the cell-sorted queue
+    # (queue slot, key, the packet's cell / level / number words, side state, the 32-byte ticket: 128 B) and
+    # deactivated by k_ma_finish (the 304-byte packet record read and written: 608 B + side state 32 B)
+    acts = w[14] + w[15]
+    return {"rpkt": rpkt, "ma": ma, "kpkt": kpkt, "binning": 128.0 * acts, "finish": 640.0 * acts}
 
 
 def vpkt_byte_model(vwork, traces, nions_total):
@@ -73,7 +77,8 @@ WORK_NAMES = ["active", "rpkt_steps", "lines_scanned", "line_taus", "kappa_evals
 
 # rocprof names (prefixes) of each class's kernel: k_ma's instance is k_ma<waves, coop, level> (row mode
 # k_ma<1, false, false>), k_vpkt's k_vpkt<prefetch, waves>
-KERNEL_NAME = {"rpkt": "k_rpkt<2>", "ma": "k_ma<", "kpkt": "k_kpkt", "vpkt": "k_vpkt<"}
+KERNEL_NAME = {"rpkt": "k_rpkt<2>", "ma": "k_ma<", "kpkt": "k_kpkt", "vpkt": "k_vpkt<", "binning": "k_ma_scatter",
+               "finish": "k_ma_finish"}
 
 
 def cpu_share():
@@ -188,24 +193,40 @@ def timed_workload(m, P, nts, rank, steps, params=None, etot=None, seed=3000):
         dt = time.perf_counter() - t
         if k > 0:  # the first step warms up
             ms.append(dt * 1e3)
-            kts.append(eng.last_kernel_times())
+            kts.append(eng.last_kernel_class_times())
             pre.append(eng.last_precompute_ms())
             work[:] = eng.last_work()
     tables = eng.table_info()
     eng.close()
     alg = byte_model(work, m.nions_total)
     kt = {c: (float(np.mean([t[c][0] for t in kts])), float(np.mean([t[c][1] for t in kts])))
-          for c in ("rpkt", "ma", "kpkt")}
-    dom = max(("rpkt", "ma"), key=lambda c: kt[c][0])
+          for c in kts[0]}
+    # the dominant kernel class over every class of the step (class_roofline: each class's fraction)
+    dom = max((c for c in kt if c in alg), key=lambda c: kt[c][0])
     launches = max(kt[dom][1], 1.)
     gbs = alg[dom] / launches / max(kt[dom][0] / 1e3 / launches, 1e-12) / 1e9
     value = P / (float(np.mean(ms)) / 1e3)
+    step_ms = float(np.mean(ms))
     return {"npts_model": m.npts_model, "levels": m.nlevels_total, "lines": m.nlines, "bf_continua": m.nbfcontinua,
-            "packets": P, "timestep": nts, "steps": steps, "ms_per_step": float(np.mean(ms)), "value": value,
+            "packets": P, "timestep": nts, "steps": steps, "ms_per_step": step_ms, "value": value,
             "unit": "packets/s", "precompute_ms": float(np.mean(pre)), "kernel_ms": {c: v[0] for c, v in kt.items()},
+            "kernel_share_of_step": {c: v[0] / step_ms for c, v in kt.items()},
             "roofline": {"kernel": KERNEL_NAME[dom], "achieved": gbs, "peak": HBM_PEAK_GBS, "frac": gbs / HBM_PEAK_GBS},
+            "class_roofline": class_roofline(alg, kt),
             "ceiling": ceiling(alg, P, value),
             "work_per_packet": {k: float(v) / max(P, 1) for k, v in zip(WORK_NAMES, work)}, "tables": tables}
+
+
+def class_roofline(alg, kt):
+    """Per kernel class with a byte model: algorithmic bytes per launch, average launch ms and the HBM fraction."""
+    out = {}
+    for c, (ms, nl) in kt.items():
+        if c not in alg or ms <= 0:
+            continue
+        nl = max(nl, 1.)
+        out[c] = {"alg_bytes_per_launch": alg[c] / nl, "avg_launch_ms": ms / nl,
+                  "frac": alg[c] / nl / (ms / nl / 1e3) / 1e9 / HBM_PEAK_GBS}
+    return out
 
 
 def ffi_params(m):
@@ -375,6 +396,9 @@ def main():
                     help="skip the drop-in host-path timing and the SURVEY §8(d)-sized second workload")
     ap.add_argument("--dry-launch", action="store_true",
                     help="bring up the N ranks over gloo without a GPU and print them (tests the launcher)")
+    ap.add_argument("--baseline-config", default=None,
+                    help="only the BASELINE config sub-lines named (comma-separated: w7_100_shells, nebular_onezone, "
+                         "kilonova), at --packets per GPU; prints them as one JSON line (for per-config profiles)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -404,6 +428,13 @@ def main():
     def progress(msg):  # rank 0, stderr: a long run shows its phases as they finish
         if rank == 0:
             print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    if args.baseline_config:
+        which = tuple(args.baseline_config.split(","))
+        configs = baseline_configs(args.packets, rank, progress, which=which)
+        if rank == 0:
+            print(json.dumps({"baseline_configs": configs, "engine_src_sha": engine_src_sha()}), flush=True)
+        return
 
     if rank == 0:  # a heartbeat while one long step runs (a 1.25e8-packet virtual-packet step takes minutes)
         import threading
@@ -468,7 +499,7 @@ def main():
             precompute_ms.append(eng.last_precompute_ms())
             work[:] = eng.last_work()
             rounds.append(eng.last_rounds())
-            ktimes.append(eng.last_kernel_times())
+            ktimes.append(eng.last_kernel_class_times())
             if vcfg is not None:
                 vstats.append(eng.vpkt_last_stats())
                 vdrains.append(eng.vpkt_last_drains())
@@ -500,13 +531,13 @@ def main():
     alg = byte_model(work, model.nions_total)
     alg_survey = byte_model(work, model.nions_total, probe_bytes=40.0)
     kt = {k: (float(np.mean([t[k][0] for t in ktimes])), float(np.mean([t[k][1] for t in ktimes])))
-          for k in ("rpkt", "ma", "kpkt")}
+          for k in ktimes[0]}
     if vcfg is not None:
         ntr = float(np.mean([v[2] for v in vstats]))
         vw = {k: float(np.mean([w[k] for w in vwork])) for k in vwork[0]}
         alg["vpkt"] = alg_survey["vpkt"] = vpkt_byte_model(vw, ntr, model.nions_total)
         kt["vpkt"] = (float(np.mean([v[0] for v in vstats])), float(max(np.mean(rounds), 1)))
-    dom = max((k for k in kt if k != "kpkt"), key=lambda k: kt[k][0])
+    dom = max((k for k in kt if k in alg), key=lambda k: kt[k][0])
     dom_ms, dom_launches = kt[dom]
     launches = max(dom_launches, 1.0)
     bytes_per_launch = alg[dom] / launches
@@ -687,12 +718,9 @@ def main():
             "transport_ms": float(np.mean(transport_ms)),
             "event_rounds": int(np.max(rounds)) if rounds else 0,
             "kernel_ms": {k: v[0] for k, v in kt.items()},
-            "other_kernels_ms": float(np.mean([t["classify"][0] for t in ktimes])),
-            "kernel_roofline": {k: {"alg_bytes_per_launch": alg[k] / max(v[1], 1.0),
-                                    "avg_launch_ms": v[0] / max(v[1], 1.0),
-                                    "frac": alg[k] / max(v[1], 1.0) / max(v[0] / max(v[1], 1.0) / 1e3, 1e-12) / 1e9
-                                            / HBM_PEAK_GBS}
-                                for k, v in kt.items()},
+            "other_kernels_ms": float(np.mean([sum(t[c][0] for c in ("classify", "binning", "exact", "finish"))
+                                               for t in ktimes])),
+            "kernel_roofline": class_roofline(alg, kt),
             "ma_ps_per_jump": kt["ma"][0] * 1e9 / max(float(work[8]), 1.0),
             "work_per_packet": {k: float(v) / max(P, 1) for k, v in zip(WORK_NAMES, work)},
             "ceiling": ceiling(alg, P, value / world),

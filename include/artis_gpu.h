@@ -565,6 +565,12 @@ int64_t artis_gpu_last_rounds(void);  /* event-queue rounds of the last update (
  * [0] r-packet (k_rpkt), [1] macro-atom (k_ma), [2] k-packet (k_kpkt), [3] other: classify, gamma, the macro-atom
  * queue binning (k_ma_bin / scan / k_ma_scatter), the exact jumps (k_ma_exact) and the deactivations (k_ma_finish) */
 int artis_gpu_last_kernel_times(double ms[4], int64_t launches[4]);
+/* the same split finer, ARTIS_KCLASS_COUNT classes: [0] k_rpkt, [1] k_ma, [2] k_kpkt, [3] classify + gamma family
+ * (k_classify, k_gamma), [4] queue binning (k_ma_bin(_blk) / scan / k_ma_scatter(_blk), k_r_bin / k_r_scatter),
+ * [5] exact jumps (k_ma_exact), [6] deactivations (k_ma_finish); classes 3-6 sum to artis_gpu_last_kernel_times'
+ * [3] */
+#define ARTIS_KCLASS_COUNT 7
+int artis_gpu_last_kernel_class_times(double ms[ARTIS_KCLASS_COUNT], int64_t launches[ARTIS_KCLASS_COUNT]);
 const char *artis_gpu_last_error(void);
 
 /* ------------------------------------------------------------------------------------------------------------ */

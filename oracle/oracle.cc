@@ -3628,6 +3628,34 @@ int oracle_select_continuum_nu_samples(const artis_atomic_tables *at, int elemen
   return 0;
 }
 
+// Test diagnostic: the (model cell, line) pairs whose Sobolev coefficient (B_lu n_l - B_ul n_u) is negative --
+// population inversions, which only the NLTE populations produce (the expression of vpkt.cc:280 / rpkt.cc:168-187
+// with calculate_levelpop's populations).  out[0]: inverted pairs, out[1]: pairs counted (cells with rho > 0).
+int oracle_inverted_lines(const artis_atomic_tables *at, const artis_geometry *geom, const artis_cell_state *cs,
+                          const artis_run_params *rp, int nts, int64_t out[2]) {
+  Ctx c;
+  c.at = at;
+  c.g = geom;
+  c.cs = cs;
+  c.rp = *rp;
+  c.nts = nts;
+  c.minpop = rp->minpop > 0. ? rp->minpop : 1e-30;
+  out[0] = out[1] = 0;
+  for (int mgi = 0; mgi < geom->npts_model; mgi++) {
+    if (!(cs->rho[mgi] > 0.f)) continue;
+    for (int li = 0; li < at->nlines; li++) {
+      const int e = at->line_elementindex[li], i = at->line_ionindex[li];
+      const int upper = at->line_upperlevelindex[li], lower = at->line_lowerlevelindex[li];
+      const double B_ul = ARTIS_CLIGHTSQUAREDOVERTWOH / pow(at->line_nu[li], 3) * at->line_einstein_A[li];
+      const double B_lu = stat_weight(c, e, i, upper) / stat_weight(c, e, i, lower) * B_ul;
+      const double n_u = calculate_levelpop(c, mgi, e, i, upper), n_l = calculate_levelpop(c, mgi, e, i, lower);
+      if (B_lu * n_l - B_ul * n_u < 0.) out[0]++;
+      out[1]++;
+    }
+  }
+  return 0;
+}
+
 // photoionisation cross section lookup (atomic.cc:87-155) for table row `table`
 double oracle_phixs(const artis_atomic_tables *at, int table, double nu_edge, double nu) {
   Ctx c;

@@ -90,6 +90,19 @@ def spectrum(model, packets, nnubins=1000, nprocs=1):
     return spec, lc, lccmf
 
 
+def inverted_lines(model, nts, params=None):
+    """(inverted, total): (model cell, line) pairs with a negative Sobolev coefficient (population inversion) under
+    the oracle's populations at timestep nts (call model.set_timestep(nts) first)."""
+    L = lib()
+    L.oracle_inverted_lines.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(ffi.RunParams), C.c_int,
+                                        C.c_void_p]
+    L.oracle_inverted_lines.restype = C.c_int
+    out = np.zeros(2, dtype=np.int64)
+    p = params if params is not None else model.params
+    L.oracle_inverted_lines(model.atomic, model.geometry, model.cellstate, C.byref(p), int(nts), out.ctypes.data)
+    return int(out[0]), int(out[1])
+
+
 def qag61_test(fn, a, b, epsrel):
     """The oracle's gsl_integration_qag(GAUSS61) restatement on closed-form test integrands."""
     st, err = C.c_int(), C.c_double()

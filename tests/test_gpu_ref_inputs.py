@@ -134,6 +134,51 @@ def test_w7_like_100_shells_subset(engine_factory):
     assert np.isclose(eg.struct.cmf_lum, pg["e_cmf"][esc].sum(), rtol=1e-9)
 
 
+def _full_atom_subset(engine_factory, m, nts, seed, P=100_000, nsub=1000):
+    """P packets on the engine with the bench's full synthetic atom (3603 levels, 93 798 lines); nsub of them re-run
+    on the oracle must match one for one (a); the same nsub on the engine alone: estimators and counters equal the
+    oracle's (b) -- for few-cell models these are k_rpkt's per-block LDS estimator sums at the timed atom size."""
+    m.set_timestep(nts)
+    pk0 = m.init_rpackets(nts, P, seed=seed)
+    eng = engine_factory(m)
+    eng.upload_cellstate(nts)
+    pg = pk0.copy()
+    eg = eng.update_packets(nts, pg)
+    esc = pg["type"] == ffi.TYPE_ESCAPE
+    assert eg.struct.nesc == esc.sum()
+    assert np.isclose(eg.struct.cmf_lum, pg["e_cmf"][esc].sum(), rtol=1e-9)
+    idx = np.sort(np.random.default_rng(seed).choice(P, size=nsub, replace=False))
+    po = pk0[idx].copy()
+    eo, wo = oracle_lib.update_packets(m, nts, po, nthreads=16)
+    parity.assert_packets_match(pg[idx], po)
+    eng.close()  # one engine per process (the C ABI binds one device context)
+    eng2 = engine_factory(m)
+    eng2.upload_cellstate(nts)
+    ps = pk0[idx].copy()
+    es = eng2.update_packets(nts, ps)
+    parity.assert_packets_match(ps, po)
+    parity.assert_estimators_match(es, eo)
+    return eo, wo
+
+
+def test_nebularonezone_full_atom_subset(engine_factory):
+    """BASELINE config 3 at the timed size: the nebularonezone inputs with the nebular options and the bench's full
+    atom (bench.py baseline_configs), 1e5 packets on the engine, 1000 re-run on the oracle."""
+    m = ref_model("nebularonezone", ngrid_1d=50, nebular=1)
+    assert m.npts_model == 1 and m.nlevels_total == 3603
+    eo, wo = _full_atom_subset(engine_factory, m, 6, seed=58)
+    assert wo[8] > 0 and wo[5] > 0 and eo.radfield_count.sum() > 0  # macro-atom jumps, bf continua, bin estimators
+
+
+def test_kilonova_full_atom_subset(engine_factory):
+    """BASELINE config 4 at the timed atom size: the kilonova inputs (25 shells, relativistic, T_e excitation) with
+    the bench's full atom, 1e5 packets on the engine, 1000 re-run on the oracle."""
+    m = ref_model("kilonova", ngrid_1d=50, relativistic=1, excitation_te=1)
+    assert m.npts_model == 25 and m.nlevels_total == 3603
+    eo, wo = _full_atom_subset(engine_factory, m, 6, seed=59)
+    assert wo[2] > 0 and wo[8] > 0
+
+
 def test_grid50_vpkt_pol_subset(engine_factory):
     """BASELINE config 5 shape: 50^3 grid, virtual packets with polarisation (4 observers x 4 spectra) at a
     timestep inside the vspec window.  (a) 1e5 packets on the engine; 600 of them re-run on the oracle must

@@ -9,13 +9,16 @@
 #                                                    tools/pmc_summary.py, copied to profiles/pmc_$T_$NAME.json
 #   tools/gpu.sh sq   [bench.py args ...]            one SQ instruction-counter pass       -> $O/sq/
 #   tools/gpu.sh ab name1[:ENV=V] name2 ...          A/B of engine builds (tools/build_variants.sh) on the bench
+#   tools/gpu.sh cfgprof name [bench.py args ...]    one BASELINE config sub-line (w7_100_shells, nebular_onezone,
+#                                                    kilonova) under rocprofv3 --stats -> $O/cfg_$name/, $O/cfg_$name.json
+#   tools/gpu.sh pcs  [bench.py args ...]            stochastic PC sampling (cycles) of a short bench run -> $O/pcs/
 #   tools/gpu.sh final                               tests, prof, pmc, default bench line (the round-end set)
 #
 # Environment: T (tag, default "r4"), O (output dir, default gpurun_out/$T), NAME (pmc summary name, default
 # "bench"), P (packets for pmc / sq / ab, default 1e7), BENCH_ARGS (extra bench args for ab), ENVS (env for ab).
 cd /root/repo || exit 1
 export TMPDIR=/tmp
-T=${T:-r4}
+T=${T:-r5}
 O=${O:-gpurun_out/$T}
 mkdir -p "$O"
 cmd=$1
@@ -38,6 +41,14 @@ run_bench() {
 run_prof() {
   timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 -u bench.py --no-cpu-baseline "$@" \
     > "$O/bench_prof.json" 2> "$O/bench_prof.err"
+}
+
+run_cfgprof() {
+  local name=$1
+  shift
+  rm -rf "$O/cfg_$name"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/cfg_$name" -o run -- python3 -u bench.py \
+    --baseline-config "$name" "$@" > "$O/cfg_$name.json" 2> "$O/cfg_$name.err" && tail -c 300 "$O/cfg_$name.json"
 }
 
 # pmc [bench args]: the bench's defaults are --packets 1e7 --nts 10; the summary needs the same numbers
@@ -71,6 +82,15 @@ run_sq() {
     --packets ${P:-2000000} --steps 1 --warmup 0 --no-cpu-baseline --no-update-grid --no-extra "$@" > "$O/sq/sq.log" 2>&1
 }
 
+run_pcs() {
+  rm -rf "$O/pcs"
+  mkdir -p "$O/pcs"
+  timeout -s KILL 120 rocprofv3 -L > "$O/pcs/list.txt" 2>&1
+  timeout -s KILL 400 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method stochastic --pc-sampling-unit cycles \
+    --pc-sampling-interval ${PCS_INTERVAL:-1048576} --output-format csv -d "$O/pcs/db" -o run -- python3 bench.py \
+    --packets ${P:-2000000} --steps 1 --warmup 0 --no-cpu-baseline --no-update-grid --no-extra "$@" > "$O/pcs/pcs.log" 2>&1
+}
+
 run_ab() {
   local v name envs so tag
   for v in "$@"; do
@@ -91,6 +111,8 @@ case "$cmd" in
   pmc) run_pmc "$@" ;;
   sq) run_sq "$@" ;;
   ab) run_ab "$@" ;;
+  cfgprof) run_cfgprof "$@" ;;
+  pcs) run_pcs "$@" ;;
   final) run_tests && run_prof --no-extra && run_pmc && run_bench ;;
   *) echo "usage: tools/gpu.sh tests|bench|prof|pmc|sq|ab|final [args]"; exit 2 ;;
 esac
