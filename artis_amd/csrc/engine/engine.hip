@@ -813,6 +813,7 @@ struct Engine {
   int64_t vpkt_drains = 0;        // launches resumed after a full spawn buffer (last update_packets)
   bool r_binned = false;          // bin the R queue by cell before k_rpkt (ARTIS_GPU_R_BIN=1)
   bool ma_bin_blk = true;         // few cells: block-local M-queue binning (ARTIS_GPU_MA_BIN_BLK=0: per-entry atomics)
+  bool ma_pre_on = true;          // M-queue pre-tickets (WaveState::ma_pre; ARTIS_GPU_MA_PRE=0: gathered by the scatter)
   std::vector<hipEvent_t> vev;  // (start, end) pairs around the k_vpkt launches of the last update
   size_t vev_used = 0;
   double last_vpkt_ms = 0.;
@@ -967,6 +968,7 @@ void free_packets() {
   dfree(G.W.ma_key);
   dfree(G.W.ma_sorted);
   dfree(G.W.ma_tick);
+  dfree(G.W.ma_pre);
   for (int q = 0; q < NQUEUES; q++) dfree(G.W.q[q]);
   G.cap_pkts = 0;
   G.npkts = 0;
@@ -987,7 +989,8 @@ int alloc_packets(int64_t n) {
                            {(void **)&G.W.pend_jumps, un * sizeof(uint32_t)},
                            {(void **)&G.W.ma_key, un * sizeof(int32_t)},
                            {(void **)&G.W.ma_sorted, un * sizeof(int32_t)},
-                           {(void **)&G.W.ma_tick, un * 2 * sizeof(int4)}};
+                           {(void **)&G.W.ma_tick, un * 2 * sizeof(int4)},
+                           {(void **)&G.W.ma_pre, un * 2 * sizeof(int4)}};
   for (int q = 0; q < NQUEUES; q++) reqs.push_back({(void **)&G.W.q[q], un * sizeof(int32_t)});
   const int nreq = (int)reqs.size();
   for (int r = 0; r < nreq; r++) {
@@ -1261,6 +1264,7 @@ int vpkt_collect(const unsigned long long before[8]) {
 int run_wavefront(int64_t n, int nts, double t2) {
   WaveState W = G.W;
   if (!(G.K.C.have_macache && W.ma_binned)) W.ma_tick = nullptr;  // tickets: cached walk over the binned queue
+  if (!W.ma_tick || !G.ma_pre_on) W.ma_pre = nullptr;            // pre-tickets written by the queue's producers
   const unsigned grid = (unsigned)G.wave_grid;
   if (int rc = sync_ctx()) return rc;
   G.tev_used = 0;
@@ -2983,6 +2987,8 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     // ~250 ms more binning per step (profiles/r03g_ab.txt), so off unless asked for (ARTIS_GPU_R_BIN=1)
     const char *rb = getenv("ARTIS_GPU_R_BIN");
     G.r_binned = rb && rb[0] == '1';
+    const char *mp = getenv("ARTIS_GPU_MA_PRE");
+    G.ma_pre_on = !(mp && mp[0] == '0');
     const char *bb = getenv("ARTIS_GPU_MA_BIN_BLK");
     G.ma_bin_blk = !(bb && bb[0] == '0');
     const char *xr = getenv("ARTIS_GPU_MA_XCD");
@@ -3203,6 +3209,10 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
       bc[i].pad = 0;
     }
     rc |= dupload(&T.bfc, bc.data(), bc.size());
+    const int ne2 = (nb / 4 + 1) * 4;  // at least one padding entry
+    std::vector<double2> e2(ne2, make_double2(INFINITY, INFINITY));
+    for (int i = 0; i < nb; i++) e2[i] = make_double2(bc[i].nu_edge, bc[i].nu_max);
+    rc |= dupload(&T.bf_edge2, e2.data(), e2.size());
   }
   rc |= dupload(&T.allcont_groundindex, a->allcont_index_in_groundphixslist, nb);
   rc |= dupload(&T.groundcont_nu_edge, a->groundcont_nu_edge, a->nbfcontinua_ground);

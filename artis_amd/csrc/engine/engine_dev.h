@@ -92,6 +92,8 @@ struct DevTab {
   const int2 *down_target, *up_target;
   const double *allcont_nu_edge, *allcont_probability;
   const BfCont *bfc;  // [nbf]
+  const double2 *bf_edge2;  // [nbf rounded up past a multiple of 4] {nu_edge, nu_max}, padded with infinities
+                            // (transport.h bf_range)
   const int32_t *allcont_element, *allcont_ion, *allcont_level, *allcont_target, *allcont_upperlevel,
       *allcont_phixstable, *allcont_groundindex;
   const double *groundcont_nu_edge;

@@ -416,19 +416,43 @@ DEVFN bool bf_contribution(const Ctx &K, const BfCell &cell, int i, double nu, d
   *gcontr_out = sigma_bf * c.probability * corrfactor;
   return true;
 }
+// The continua a frequency reaches: hi = the reference's loop length (it breaks at the first continuum with
+// nu < nu_edge, the edges ascending), lo = the first continuum whose cross-section table still covers nu
+// (nu <= nu_edge * last_phixs_nuovernuedge, ascending with the edges): below lo, bf_contribution is false (and the
+// detailed-bf window test fails), so the sums over [lo, hi) are the reference's sums over [0, hi).  A scan over
+// DevTab::bf_edge2 four continua per trip to memory (the table is padded with infinities).
+DEVFN void bf_range(const Ctx &K, double nu, int &lo, int &hi) {
+  const double2 *e = K.T.bf_edge2;
+  lo = 0;
+  hi = 0;
+  for (int i0 = 0;; i0 += 4) {
+    double2 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) v[q] = e[i0 + q];
+    bool stop = false;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if (!stop) {
+        if (nu < v[q].x) {
+          stop = true;
+        } else {
+          hi = i0 + q + 1;
+          if (nu > v[q].y) lo = i0 + q + 1;
+        }
+      }
+    }
+    if (stop) break;
+  }
+}
 // rpkt.cc:1075-1207 calculate_kappa_bf_gammacontr: the kappa_bf total (the cumulative array is re-scanned on demand)
 DEVFN double kappa_bf_total(Tx &x, int k, int mgi, double nu) {
   const Ctx &K = x.K;
   double kappa_bf_sum = 0.;
-  unsigned long long nactive = 0;
+  int lo, hi;
+  bf_range(K, nu, lo, hi);
+  const unsigned long long nactive = (unsigned)hi;  // (the continua the reference's loop visits)
   const BfCell cell = bf_cell(K, k, mgi, nu);
-  for (int i = 0; i < K.T.nbf; i++) {
-    if (nu < K.T.allcont_nu_edge[i]) {
-      // the reference breaks at the first included continuum with nu < nu_edge; sorted edges => nothing
-      // beyond contributes either
-      break;
-    }
-    nactive++;
+  for (int i = lo; i < hi; i++) {
     double nnlevel, gc;
     if (bf_contribution(K, cell, i, nu, &nnlevel, &gc)) kappa_bf_sum += nnlevel * gc;
   }
@@ -894,21 +918,20 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
     const double dopplerfactor = doppler_packet(K, p);
     const double d_over_nu = distance_e_cmf / nu * dopplerfactor;
     const int64_t row = (int64_t)mgi * K.T.nbf;
+    // the window nu_edge <= nu <= nu_max of the reference's loop is [lo, hi) (bf_range); gamma_contr is zero below
+    // the first continuum kap.nu reaches (lo_k), and adding zero changes no sum, so the loop starts at max(lo, lo_k)
+    // (without do_r_lc no bf opacity is evaluated and the zero-initialised gamma_contr stays 0, rpkt.cc:1230)
+    int lo, hi, lo_k, hi_k;
+    bf_range(K, nu, lo, hi);
+    bf_range(K, kap.nu, lo_k, hi_k);
     const BfCell cell = bf_cell(K, k, mgi, kap.nu);
-    for (int i = 0; i < K.T.nbf; i++) {
-      const double nu_edge = K.T.allcont_nu_edge[i];
-      const double nu_max_phixs = nu_edge * K.T.last_phixs_nuovernuedge;
-      if (nu >= nu_edge && nu <= nu_max_phixs) {
-        double gc = 0., nnlevel;
-        // (without do_r_lc no bf opacity is evaluated and the zero-initialised gamma_contr stays 0, rpkt.cc:1230)
-        if (!K.R.do_r_lc || (!(kap.nu < nu_edge) && !bf_contribution(K, cell, i, kap.nu, &nnlevel, &gc))) gc = 0.;
-        if (x.est_lds && K.C.est_lds_bf >= 0)
-          atomicAdd(&x.est_lds[K.C.est_lds_bf + (int64_t)k * K.T.nbf + i], gc * d_over_nu);
-        else
-          safeadd(&K.E.bfrate[row + i], gc * d_over_nu);
-      } else if (nu < nu_edge) {
-        break;
-      }
+    for (int i = max(lo, lo_k); K.R.do_r_lc && i < hi; i++) {
+      double gc = 0., nnlevel;
+      if (kap.nu < K.T.allcont_nu_edge[i] || !bf_contribution(K, cell, i, kap.nu, &nnlevel, &gc)) continue;
+      if (x.est_lds && K.C.est_lds_bf >= 0)
+        atomicAdd(&x.est_lds[K.C.est_lds_bf + (int64_t)k * K.T.nbf + i], gc * d_over_nu);
+      else
+        safeadd(&K.E.bfrate[row + i], gc * d_over_nu);
     }
   }
   if (K.R.multibin) {  // radfield.cc:845-866

@@ -47,6 +47,11 @@ struct WaveState {
   // cell-sorted macro-atom tickets written by k_ma_scatter when the key cache is on (else nullptr): per slot
   // {packet index, unique level, record offset, nonempty cell}, {packet number, RNG counter, jumps so far, 0}
   int4 *ma_tick;       // [2N]
+  // the same walks' pre-tickets in M-queue order, written by the kernel that appends the walk (wave_push_ma), so
+  // that the binning reads one sequential 32-byte record per slot instead of gathering the packet's words:
+  // {packet index, propagation cell, packet number, RNG counter}, then {element, ion, level, 0} for a new
+  // activation or {-1 - unique level, 0, 0, jumps so far} for a walk parked by k_ma_exact (nullptr: no tickets)
+  int4 *ma_pre;        // [2N]
   unsigned long long *stats;  // [48] diagnostics: per kernel class c: [4c] wave loop passes, [4c+1] busy
                               // lane-passes, [4c+2] wave cycles (s_memtime), [4c+3] refills;
                               // [16 + 4c] cycles in refill blocks, [17 + 4c] cycles in the work step; [40] exact
@@ -103,6 +108,19 @@ DEVFN void wave_push(const WaveState &W, int q, bool pred, int32_t idx) {
   const uint32_t slot = wave_reserve(&W.ctr[2 * q], pred);
   if (pred) W.q[q][slot] = idx;
 }
+// M-queue append with the walk's pre-ticket (WaveState::ma_pre): a new macro-atom activation of packet p
+DEVFN void wave_push_ma(const WaveState &W, bool pred, int32_t idx, int where, int number, uint32_t rng_n, int4 b) {
+  const uint32_t slot = wave_reserve(&W.ctr[2 * QM], pred);
+  if (pred) {
+    W.q[QM][slot] = idx;
+    if (W.ma_pre) {
+      W.ma_pre[2 * (int64_t)slot] = make_int4(idx, where, number, (int)rng_n);
+      W.ma_pre[2 * (int64_t)slot + 1] = b;
+    }
+  }
+}
+DEVFN int4 ma_pre_activation(int element, int ion, int level) { return make_int4(element, ion, level, 0); }
+DEVFN int4 ma_pre_resume(int ul, unsigned jumps) { return make_int4(-1 - ul, 0, 0, (int)jumps); }
 
 struct BlockCounters {
   unsigned long long *ctr, *work;
@@ -149,7 +167,17 @@ __global__ void k_classify(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *
     }
   }
   wave_push(W, QR, toR, (int32_t)i);
-  wave_push(W, QM, toM, (int32_t)i);
+  {
+    int where = 0, number = 0;
+    int4 b = make_int4(0, 0, 0, 0);
+    if (toM) {  // (an initial macro-atom: rare)
+      const uint64_t w0 = soa[PW(n, i, 0)], w36 = soa[PW(n, i, 36)], w37 = soa[PW(n, i, 37)];
+      where = lo32(w0);
+      number = hi32(soa[PW(n, i, 33)]);
+      b = ma_pre_activation(lo32(w36), hi32(w36), lo32(w37));
+    }
+    wave_push_ma(W, toM, (int32_t)i, where, number, 0u, b);
+  }
   wave_push(W, QK, toK, (int32_t)i);
   wave_push(W, QG, toG, (int32_t)i);
   block_counters_flush(K, s_ctr, s_work);
@@ -207,7 +235,8 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
     if (!__any(have) || __popcll(imask) >= W.refill_min) {
       st_refill++;
       const unsigned long long tr0 = wave_clock();
-      wave_push(W, QM, pendM, idx);  // appends deferred from the lanes' last retirement
+      // appends deferred from the lanes' last retirement (a macro-atom: p still holds the retired packet)
+      wave_push_ma(W, pendM, idx, p.where, p.number, x.rng.n, ma_pre_activation(p.ma_element, p.ma_ion, p.ma_level));
       wave_push(W, QK, pendK, idx);
       wave_push(W, QR, pendR, idx);  // packets parked on a full virtual-packet buffer (resumed by the host)
       pendM = pendK = pendR = false;
@@ -291,6 +320,12 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
           for (int d = 0; d < 3; d++) soa[PW(n, idx, 22 + d)] = asw(p.absorptiondir[d]);
           soa[PW(n, idx, 36)] = pack2(p.ma_element, p.ma_ion);
           soa[PW(n, idx, 37)] = pack2(p.ma_level, p.ma_activatingline);
+        } else if (p.type == ARTIS_TYPE_MA && W.ma_pre) {
+          // (the continuum event set the macro-atom state on the cold copy: the pre-ticket needs it in registers)
+          const uint64_t w36 = soa[PW(n, idx, 36)], w37 = soa[PW(n, idx, 37)];
+          p.ma_element = lo32(w36);
+          p.ma_ion = hi32(w36);
+          p.ma_level = lo32(w37);
         }
         W.rng_n[idx] = x.rng.n;
         if (x.ok && p.prop_time < t2) {
@@ -360,13 +395,17 @@ __global__ void k_r_scatter(const Ctx *__restrict__ ctxp, WaveState W, uint32_t 
     W.ma_sorted[atomicAdd(&offs[W.ma_key[slot]], 1u)] = W.q[QR][slot];
 }
 
+// the propagation cell of M-queue slot `slot`: from its pre-ticket, or the packet's hot word
+DEVFN int ma_slot_where(const WaveState &W, const uint64_t *__restrict__ soa, uint32_t slot) {
+  if (W.ma_pre) return W.ma_pre[2 * (int64_t)slot].y;
+  return lo32(soa[PW(0, W.q[QM][slot], 0)]);  // hot group: no n term
+}
 // bin the M queue by cell: count per cell and remember each slot's key
 __global__ void k_ma_bin(const Ctx *__restrict__ ctxp, WaveState W, const uint64_t *__restrict__ soa) {
   CTX_IN_LDS(ctxp)
   const uint32_t nq = W.ctr[2 * QM];
   for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x) {
-    const int32_t idx = W.q[QM][slot];
-    const int k = K.C.ne_index[cell_mgi(K, lo32(soa[PW(0, idx, 0)]))];  // hot group: no n term
+    const int k = K.C.ne_index[cell_mgi(K, ma_slot_where(W, soa, slot))];
     const int b = K.C.ma_bin[k];
     W.ma_key[slot] = b;
     atomicAdd(&W.bins[b], 1u);
@@ -375,6 +414,40 @@ __global__ void k_ma_bin(const Ctx *__restrict__ ctxp, WaveState W, const uint64
 // scatter into cell order using the exclusive prefix sum of the counts.  Each slot becomes a ticket holding
 // everything k_ma's refill needs (the walk's level, record line, cell, RNG stream and jump count), so a k_ma lane
 // starts a walk with one coalesced read instead of a chain of dependent packet and table loads.
+// the ticket of M-queue slot `slot` at sorted position pos: from the slot's pre-ticket (WaveState::ma_pre), or
+// gathered from the packet's record and side state
+DEVFN void ma_ticket(const Ctx &K, const WaveState &W, const uint64_t *__restrict__ soa, int64_t n, int32_t idx,
+                     uint32_t pos);
+DEVFN void ma_ticket_slot(const Ctx &K, const WaveState &W, const uint64_t *__restrict__ soa, int64_t n,
+                          uint32_t slot, uint32_t pos) {
+  if (!W.ma_pre || !W.ma_tick) {
+    ma_ticket(K, W, soa, n, W.q[QM][slot], pos);
+    return;
+  }
+  const int4 a = W.ma_pre[2 * (int64_t)slot], b = W.ma_pre[2 * (int64_t)slot + 1];
+  const int32_t idx = a.x;
+  const int where = a.y, number = a.z;
+  int ul;
+  unsigned jumps;
+  if (b.x < 0) {  // a walk parked by k_ma_exact: its level and jump count
+    ul = -1 - b.x;
+    jumps = (unsigned)b.w;
+    W.pend[idx].x = 0;
+  } else {
+    ul = ulev(K, b.x, b.y, b.z);
+    jumps = 0;
+  }
+  const int mgi = cell_mgi(K, where);
+  int32_t tidx = idx;
+  if (K.C.thick[mgi] == 1) {
+    fail(K, ERR_THICK_MA, number, mgi);
+    tidx = -1;
+  }
+  const int k = K.C.ne_index[mgi];
+  const int32_t rowline = ma_rowline(K, k);
+  W.ma_tick[2 * (int64_t)pos] = make_int4(tidx, ul, (int)ma_line(K, rowline, k, ul, K.T.ma_meta[ul].rec_off), k);
+  W.ma_tick[2 * (int64_t)pos + 1] = make_int4(number, a.w, (int)jumps, rowline);
+}
 DEVFN void ma_ticket(const Ctx &K, const WaveState &W, const uint64_t *__restrict__ soa, int64_t n, int32_t idx,
                      uint32_t pos) {
   if (!W.ma_tick) {
@@ -411,7 +484,7 @@ __global__ void k_ma_scatter(const Ctx *__restrict__ ctxp, WaveState W, const ui
   CTX_IN_LDS(ctxp)
   const uint32_t nq = W.ctr[2 * QM];
   for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nq; slot += gridDim.x * blockDim.x)
-    ma_ticket(K, W, soa, n, W.q[QM][slot], atomicAdd(&offs[W.ma_key[slot]], 1u));
+    ma_ticket_slot(K, W, soa, n, slot, atomicAdd(&offs[W.ma_key[slot]], 1u));
 }
 
 // Few-cell models (n_nonempty + 1 <= MA_BIN_LDS bins: the 1D shell models, the one-zone nebular model): the same
@@ -460,8 +533,7 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_ma_bin_blk(const Ctx *__restrict
     const bool act = slot < hi;
     int b = 0;
     if (act) {
-      const int32_t idx = W.q[QM][slot];
-      b = K.C.ma_bin[K.C.ne_index[cell_mgi(K, lo32(soa[PW(0, idx, 0)]))]];  // hot group: no n term
+      b = K.C.ma_bin[K.C.ne_index[cell_mgi(K, ma_slot_where(W, soa, slot))]];
       W.ma_key[slot] = b;
     }
     (void)lds_bin_add(h, b, act);
@@ -497,7 +569,7 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_ma_scatter_blk(const Ctx *__rest
     const bool act = slot < hi;
     const int key = act ? W.ma_key[slot] : 0;
     const uint32_t pos = lds_bin_add(h, key, act);
-    if (act) ma_ticket(K, W, soa, n, W.q[QM][slot], pos);
+    if (act) ma_ticket_slot(K, W, soa, n, slot, pos);
   }
 }
 
@@ -788,9 +860,11 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
   // time: one queue atomic per 64 jumps instead of one per jump on the queue's counter
   int32_t pm = -1, pf = -1;
   int nm = 0, nf = 0;
+  int pm_where = 0, pm_number = 0, pm_ul = 0;  // the pending M appends' pre-tickets (WaveState::ma_pre)
+  uint32_t pm_rng = 0, pm_jumps = 0;
   auto flush = [&](bool all) {
     if (all || nm == 64) {
-      wave_push(W, QM, lane < nm, pm);
+      wave_push_ma(W, lane < nm, pm, pm_where, pm_number, pm_rng, ma_pre_resume(pm_ul, pm_jumps));
       nm = 0;
     }
     if (all || nf == 64) {
@@ -798,10 +872,21 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
       nf = 0;
     }
   };
-  auto collect = [&](int32_t to_m, int32_t to_f) {  // lane 0's decision for this slot
+  // lane 0's decision for this slot; a walk parked again: its level, jump count and RNG counter (lane 0's) and
+  // cell / packet number (wave-uniform)
+  auto collect = [&](int32_t to_m, int32_t to_f, int where, int number, int ul, unsigned jumps, uint32_t rngn) {
     const int32_t m = __builtin_amdgcn_readlane(to_m, 0), f = __builtin_amdgcn_readlane(to_f, 0);
+    const int ul0 = __builtin_amdgcn_readlane(ul, 0);
+    const uint32_t j0 = (uint32_t)__builtin_amdgcn_readlane((int)jumps, 0), r0 = (uint32_t)__builtin_amdgcn_readlane((int)rngn, 0);
     if (m >= 0) {
-      if (lane == nm) pm = m;
+      if (lane == nm) {
+        pm = m;
+        pm_where = where;
+        pm_number = number;
+        pm_ul = ul0;
+        pm_jumps = j0;
+        pm_rng = r0;
+      }
       nm++;
     }
     if (f >= 0) {
@@ -836,6 +921,8 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
       int j = -1;
       unsigned probes = 0;
       if (ma_coop_needs_search(sel)) sel = ma_coop_search(K, k, ul, sel, x, t_mid, &j, probes);
+      int res_ul = 0;
+      unsigned res_jumps = 0;
       if (lane == 0) {
         MaLaneR mr;
         static_cast<MaLaneC &>(mr) = m;
@@ -858,8 +945,10 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
           lwork(L, WK_MA_JUMPS, mr.jumps);
           to_f = idx;  // -> k_ma_finish
         }
+        res_ul = mr.ul;
+        res_jumps = mr.jumps;
       }
-      collect(to_m, to_f);
+      collect(to_m, to_f, where, number, res_ul, res_jumps, rng.n);
       continue;
     }
     const int mgi = K.C.ne_mgi[k];
@@ -962,7 +1051,7 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
         to_f = idx;  // -> k_ma_finish
       }
     }
-    collect(to_m, to_f);
+    collect(to_m, to_f, where, number, m.ul, m.jumps, rng.n);
   }
   flush(true);
   if (lane == 0 && n_exact) {
@@ -1059,6 +1148,9 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_gamma(const Ctx *__restrict__ ct
   for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < nslots; slot += stride) {
     bool toR = false, toM = false, toK = false;
     int32_t idx = -1;
+    int m_where = 0, m_number = 0;  // the pre-ticket of a macro-atom (toM)
+    uint32_t m_rng = 0;
+    int4 m_b = make_int4(0, 0, 0, 0);
     if (slot < nq) {
       idx = W.q[QG][slot];
       Pkt p;
@@ -1081,9 +1173,13 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_gamma(const Ctx *__restrict__ ct
         toM = p.type == ARTIS_TYPE_MA;
         toK = p.type == ARTIS_TYPE_KPKT || p.type == ARTIS_TYPE_PRE_KPKT;
       }
+      m_where = p.where;
+      m_number = p.number;
+      m_rng = x.rng.n;
+      m_b = ma_pre_activation(p.ma_element, p.ma_ion, p.ma_level);
     }
     wave_push(W, QR, toR, idx);
-    wave_push(W, QM, toM, idx);
+    wave_push_ma(W, toM, idx, m_where, m_number, m_rng, m_b);
     wave_push(W, QK, toK, idx);
   }
   block_counters_flush(K, s_ctr, s_work);
@@ -1146,7 +1242,7 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_kpkt(const Ctx *__restrict__ ctx
       toM = x.ok && p.prop_time < t2 && p.type == ARTIS_TYPE_MA;
     }
     wave_push(W, QR, toR, idx);
-    wave_push(W, QM, toM, idx);
+    wave_push_ma(W, toM, idx, p.where, p.number, x.rng.n, ma_pre_activation(p.ma_element, p.ma_ion, p.ma_level));
   }
   block_counters_flush(K, s_ctr, s_work);
 }

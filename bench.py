@@ -283,6 +283,22 @@ def baseline_configs(P, rank, progress, which=("w7_100_shells", "nebular_onezone
     return out
 
 
+def level_mode_workload(rank, progress, P=1_000_000, nts=10):
+    """The macro-atom key records in level mode: the 50^3 grid with 5x the bench's lines (line window 160:
+    470 745 lines), whose whole-cell records do not fit the HBM budget, so records are kept per (cell, level) pair for
+    the pairs the walks use most; P packets per GPU, timed like the main line after one warm step (the placement of
+    the first transport is made from the walks of that step)."""
+    from artis_amd.model import Model
+
+    m = Model(ngrid_1d=50, line_window=160)
+    out = timed_workload(m, P, nts, rank, 1)
+    out["line_window"] = 160
+    out["level_mode"] = bool(out["tables"].get("ma_level_records", 0) > 0)
+    progress(f"level-mode workload (5x lines, {P} packets): {out['ms_per_step']:.0f} ms per step")
+    m.close()
+    return out
+
+
 def timestep_loop(P, nts0, nsteps, rank, progress):
     """The whole do_timestep body on the device (artis_amd.timestep.LteTimestepLoop, sn3d.cc:514-673): update_grid's
     preparation + temperature solution from the previous step's raw estimators (GPU), upload_cellstate (per-cell
@@ -398,7 +414,8 @@ def main():
                     help="bring up the N ranks over gloo without a GPU and print them (tests the launcher)")
     ap.add_argument("--baseline-config", default=None,
                     help="only the BASELINE config sub-lines named (comma-separated: w7_100_shells, nebular_onezone, "
-                         "kilonova), at --packets per GPU; prints them as one JSON line (for per-config profiles)")
+                         "kilonova; level_mode: the 5x-lines atom at min(--packets, 1e6)), at --packets per GPU; prints "
+                         "them as one JSON line (for per-config profiles)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -431,7 +448,9 @@ def main():
 
     if args.baseline_config:
         which = tuple(args.baseline_config.split(","))
-        configs = baseline_configs(args.packets, rank, progress, which=which)
+        configs = baseline_configs(args.packets, rank, progress, which=tuple(w for w in which if w != "level_mode"))
+        if "level_mode" in which:
+            configs["level_mode_5x_lines"] = level_mode_workload(rank, progress, P=min(args.packets, 1_000_000))
         if rank == 0:
             print(json.dumps({"baseline_configs": configs, "engine_src_sha": engine_src_sha()}), flush=True)
         return
@@ -664,11 +683,12 @@ def main():
     neb = None
     if rank == 0 and not args.no_update_grid and vcfg is None:
         neb = nebular_update_grid(rank, not args.no_cpu_baseline, progress)
-    survey8d = configs = tloop = None
+    survey8d = configs = tloop = lvl = None
     if rank == 0 and world == 1 and vcfg is None and not args.no_extra:
         survey8d = survey_sized_workload(P, 2, nts, rank, progress)
         configs = baseline_configs(P, rank, progress)
         tloop = timestep_loop(P, nts, 3, rank, progress)
+        lvl = level_mode_workload(rank, progress)
 
     if rank == 0:
         line = {
@@ -737,6 +757,8 @@ def main():
             line["baseline_configs"] = configs
         if tloop is not None:
             line["timestep_loop"] = tloop
+        if lvl is not None:
+            line["level_mode_5x_lines"] = lvl
         if vcfg is not None:
             vms = float(np.mean([v[0] for v in vstats]))
             line["config"]["workload"] += (f"; virtual packets: {vcfg.nobs} observers x {vcfg.nspectra} spectra, "
