@@ -273,24 +273,16 @@ __global__ void k_cooling(Ctx K) {
 //    internal_down_lower (nr) | internal_up_higher (nt)]     (each array in the reference's order)
 // One launch covers the kn cells cells[0 .. kn): the cached cells (row order) with cache = true (scratch stride
 // kn), the others with cache = false (totals into marates).
-__global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict__ S, const int32_t *__restrict__ cells,
-                          int kn, bool cache) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nl = K.T.nlevels_total;
+// k_marates' work for one (cell, level): the running sums into rec[p * stride] (cache), the action totals into pr
+DEVFN void marates_sums(const Ctx &K, int ul, int k, double t_mid, double *__restrict__ rec, int64_t stride, bool cache,
+                        double pr[ARTIS_MA_ACTION_COUNT]) {
   const int64_t nne_cells = K.C.n_nonempty;
-  if (idx >= (int64_t)kn * nlev) return;
-  const int ul = ul0 + (int)(idx / kn);
-  const int kr = (int)(idx % kn);
-  const int k = cells[kr];
   const int mgi = K.C.ne_mgi[k];
-  const double t_mid = K.G.ts_mid[nts];
   const MaMeta mm = K.T.ma_meta[ul];
-  double *rec = cache ? S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * kn + kr : nullptr;
-#define REC(p) rec[(int64_t)(p) * kn]
+#define REC(p) rec[(int64_t)(p) * stride]
   const int cum_d = ARTIS_MA_ACTION_COUNT, cum_u = ARTIS_MA_ACTION_COUNT + mm.nd;
   const int cum_drad = ARTIS_MA_ACTION_COUNT + mm.nd + mm.nu, cum_rrad = cum_drad + mm.nd;
   const int cum_rint = cum_rrad + mm.nr, cum_uhi = cum_rint + mm.nr;
-  double pr[ARTIS_MA_ACTION_COUNT];
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) pr[a] = 0.;
   const double *popsT = K.C.popsT + k;  // popsT[u * nne_cells]: level u of this lane's cell
   ma_foreach_rate(
@@ -298,7 +290,11 @@ __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict_
       [&](int slot) { return K.C.corrphotT[(int64_t)slot * nne_cells + k]; },
       [&](int kind, int j, double R, double C, double et, double eg, double ec) {
         ma_accumulate(pr, kind, R, C, et, eg, ec);
+#ifdef ARTIS_DIAG_MARATES_NOSTORE  // timing diagnostic only (the records are not written): the rates' compute alone
+        if (false) {
+#else
         if (cache) {
+#endif
           if (kind == MA_KIND_DOWN) {
             REC(cum_drad + j) = pr[ARTIS_MA_ACTION_RADDEEXC];
             REC(cum_d + j) = pr[ARTIS_MA_ACTION_INTERNALDOWNSAME];
@@ -314,44 +310,58 @@ __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict_
         return false;
       });
   pr[ARTIS_MA_ACTION_INTERNALUPHIGHERNT] = ma_nt_total(K, mgi, ul);
-  if (cache) {
+  if (cache)
     for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) REC(a) = pr[a];
-  } else {
-    double *out = K.C.marates + ((int64_t)k * nl + ul) * ARTIS_MA_ACTION_COUNT;
-    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) out[a] = pr[a];
-  }
 #undef REC
 }
 
-// Exact running sums (scratch) -> the compact key record of each (cell, level) of one k_marates batch
-// (engine_dev.h DevCells::ma_key): every sum divided by its action's total (the action totals by their grand
-// total, summed in the reference's order, macroatom.cc:515-525) and rounded to 32 bits, split into halves.  Block = (level
-// ul0 + blockIdx.y, 64 cells): 64 x 64 (position x cell) tiles through LDS, read along cells from the
-// position-major scratch, written along positions (64 consecutive keys of one record per row: coalesced).
-__global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, const double *__restrict__ S) {
-  __shared__ double tile[64][65];
-  __shared__ double s_norm[ARTIS_MA_ACTION_COUNT][64];  // action totals per cell
-  __shared__ uint32_t s_akey[ARTIS_MA_ACTION_COUNT][64];
-  const int ul = ul0 + blockIdx.y;
-  const int64_t n_ne = K.C.ma_rows;  // the cached cells, the scratch's stride
+__global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict__ S, const int32_t *__restrict__ cells,
+                          int kn, bool cache) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nl = K.T.nlevels_total;
+  if (idx >= (int64_t)kn * nlev) return;
+  const int ul = ul0 + (int)(idx / kn);
+  const int kr = (int)(idx % kn);
+  const int k = cells[kr];
+  double *rec = cache ? S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * kn + kr : nullptr;
+  double pr[ARTIS_MA_ACTION_COUNT];
+  marates_sums(K, ul, k, K.G.ts_mid[nts], rec, kn, cache, pr);
+  if (!cache) {
+    double *out = K.C.marates + ((int64_t)k * nl + ul) * ARTIS_MA_ACTION_COUNT;
+    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) out[a] = pr[a];
+  }
+}
+
+// Exact running sums (scratch) -> the compact key records (engine_dev.h DevCells::ma_key): every sum divided by its
+// action's total (the action totals by their grand total, summed in the reference's order, macroatom.cc:515-525) and
+// rounded to 32 bits, split into halves.  One (level ul, 64 rows) tile, run by a block of 256 threads: 64 x 64
+// (position x row) tiles through LDS, read along rows from the position-major scratch src (row stride n_s; rows
+// c0 .. c0 + 63 of it, the first nvalid valid), written along positions (64 consecutive keys of one record per row:
+// coalesced) into record rows row0 + c0 + j.
+struct MapackLds {
+  double tile[64][65];
+  double norm[ARTIS_MA_ACTION_COUNT][64];  // action totals per row
+  uint32_t akey[ARTIS_MA_ACTION_COUNT][64];
+};
+DEVFN void mapack_tile(const Ctx &K, int ul, const double *__restrict__ src, int64_t n_s, int64_t c0, int64_t nvalid,
+                       int64_t row0, MapackLds &S) {
   const MaMeta mm = K.T.ma_meta[ul];
   const int len = ARTIS_MA_ACTION_COUNT + 2 * mm.nd + mm.nu + 2 * mm.nr + mm.nt;
   const MaLayout lay = ma_layout(mm.nd, mm.nu, mm.nr, mm.nt);
-  const double *src = S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * n_ne;
-  const int64_t c0 = (int64_t)blockIdx.x * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  if (ty == 0 && c0 + tx < n_ne) {
+  __syncthreads();  // (the previous tile's readers of S are done)
+  if (ty == 0 && c0 + tx < nvalid) {
     double pr[ARTIS_MA_ACTION_COUNT];
     double total = 0.;
     for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
-      pr[a] = src[(int64_t)a * n_ne + c0 + tx];
-      s_norm[a][tx] = pr[a];
+      pr[a] = src[(int64_t)a * n_s + c0 + tx];
+      S.norm[a][tx] = pr[a];
       total += pr[a];
     }
     double rate = 0.;
     for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
       rate += pr[a];
-      s_akey[a][tx] = ma_key32(rate, total);
+      S.akey[a][tx] = ma_key32(rate, total);
     }
   }
   // segment boundaries of the record (positions >= 9): the action whose total normalises each
@@ -359,7 +369,7 @@ __global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, const double *__
   for (int p0 = 0; p0 < len; p0 += 64) {
     __syncthreads();
     for (int j = ty; j < 64; j += 4)
-      if (p0 + j < len && c0 + tx < n_ne) tile[j][tx] = src[(int64_t)(p0 + j) * n_ne + c0 + tx];
+      if (p0 + j < len && c0 + tx < nvalid) S.tile[j][tx] = src[(int64_t)(p0 + j) * n_s + c0 + tx];
     __syncthreads();
     const int p = p0 + tx;
     if (p < len) {
@@ -371,9 +381,9 @@ __global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, const double *__
                     : (p < b5)                 ? ARTIS_MA_ACTION_INTERNALDOWNLOWER
                                                : ARTIS_MA_ACTION_INTERNALUPHIGHER;
       for (int j = ty; j < 64; j += 4) {
-        if (c0 + j >= n_ne) break;
-        const uint32_t key = (a < 0) ? s_akey[p][j] : ma_key32(tile[tx][j], s_norm[a][j]);
-        uint16_t *rec = K.C.ma_key + (c0 + j) * K.C.ma_key_stride + mm.rec_off;
+        if (c0 + j >= nvalid) break;
+        const uint32_t key = (a < 0) ? S.akey[p][j] : ma_key32(S.tile[tx][j], S.norm[a][j]);
+        uint16_t *rec = K.C.ma_key + (row0 + c0 + j) * K.C.ma_key_stride + mm.rec_off;
         int sp;
         const int rp = ma_rec_pos(lay, p, mm.nd, mm.nu, &sp);
         rec[rp] = (uint16_t)(key >> 16);
@@ -384,6 +394,45 @@ __global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, const double *__
         }
       }
     }
+  }
+}
+
+// one k_marates batch's scratch -> key records: block = (level ul0 + blockIdx.y, 64 rows)
+__global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, const double *__restrict__ S) {
+  __shared__ MapackLds L;
+  const int ul = ul0 + blockIdx.y;
+  const int64_t n_ne = K.C.ma_rows;  // the cached cells, the scratch's stride
+  mapack_tile(K, ul, S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * n_ne, n_ne, (int64_t)blockIdx.x * 64, n_ne, 0,
+              L);
+}
+
+// k_marates + k_mapack fused (row mode): a persistent block takes (level, MAREC_ROWS rows) tasks, level-major.  Its
+// threads make the rows' running sums (one row each, as k_marates) into the block's own slab of the scratch
+// ([position][MAREC_ROWS], just written, so read back from the caches rather than HBM), then pack them into the key
+// records 64 rows at a time (mapack_tile).  The slabs hold the longest level: slab_doubles per block.
+#define MAREC_ROWS 256
+#ifndef MAREC_MINW
+#define MAREC_MINW 4  // waves per SIMD (the LDS allows 4 blocks per CU)
+#endif
+__global__ __launch_bounds__(MAREC_ROWS, MAREC_MINW) void k_marec(Ctx K, int nts, double *__restrict__ slabs, int64_t slab_doubles,
+                                                      const int32_t *__restrict__ cells) {
+  __shared__ MapackLds L;
+  const int64_t rows = K.C.ma_rows;
+  const int64_t ngroups = (rows + MAREC_ROWS - 1) / MAREC_ROWS;
+  const int64_t ntasks = ngroups * K.T.nlevels_total;
+  double *slab = slabs + (int64_t)blockIdx.x * slab_doubles;
+  const double t_mid = K.G.ts_mid[nts];
+  for (int64_t t = blockIdx.x; t < ntasks; t += gridDim.x) {
+    const int ul = (int)(t / ngroups);
+    const int64_t row0 = (t % ngroups) * MAREC_ROWS;
+    const int64_t nvalid = min((int64_t)MAREC_ROWS, rows - row0);
+    __syncthreads();  // (the previous task's pack has read the slab)
+    if (threadIdx.x < nvalid) {
+      double pr[ARTIS_MA_ACTION_COUNT];
+      marates_sums(K, ul, cells[row0 + threadIdx.x], t_mid, slab + threadIdx.x, MAREC_ROWS, true, pr);
+    }
+    __syncthreads();
+    for (int64_t c0 = 0; c0 < nvalid; c0 += 64) mapack_tile(K, ul, slab, MAREC_ROWS, c0, nvalid, row0, L);
   }
 }
 
@@ -571,20 +620,35 @@ __global__ __launch_bounds__(64) void k_ma_build(Ctx K, const int2 *__restrict__
 }
 
 // DevCells::linecoef: the Sobolev coefficient (B_lu n_l - B_ul n_u) * HCLIGHTOVERFOURPI of every line in every
-// non-empty cell, in get_event's operation order (rpkt.cc:168-187); lanes run along a cell's row (coalesced
-// writes, line records from L2, population gathers from the cell's 29 kB row)
-__global__ __launch_bounds__(256) void k_linecoef(Ctx K) {
-  const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (li >= K.C.linecoef_stride) return;
-  for (int k = blockIdx.y; k < K.C.linecoef_rows; k += gridDim.y) {
-    double v = 0.;
-    if (li < K.T.nlines) {
-      const LineTau r = K.T.line_tau[li];
-      const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
-      const double n_u = pops[r.ul_upper], n_l = pops[r.ul_lower];
-      v = (r.B_lu * n_l - r.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI;
+// non-empty cell, in get_event's operation order (rpkt.cc:168-187).  A block holds LINECOEF_PER lines per thread
+// (their records loaded once, in registers) and walks a run of rows: every store instruction writes 256 consecutive
+// doubles of one row, the population gathers come from that row's 29 kB (L1 / L2).  The blocks of one row run are
+// consecutive ids, so they walk the same rows at about the same time.
+#define LINECOEF_PER 4
+__global__ __launch_bounds__(256) void k_linecoef(Ctx K, int rows_per_block) {
+  const int64_t li0 = (int64_t)blockIdx.x * (256 * LINECOEF_PER) + threadIdx.x;
+  LineTau r[LINECOEF_PER];
+  bool in[LINECOEF_PER], st[LINECOEF_PER];
+#pragma unroll
+  for (int q = 0; q < LINECOEF_PER; q++) {
+    const int64_t li = li0 + q * 256;
+    in[q] = li < K.T.nlines;
+    st[q] = li < K.C.linecoef_stride;
+    if (in[q]) r[q] = K.T.line_tau[li];
+  }
+  const int k0 = blockIdx.y * rows_per_block, k1 = min(k0 + rows_per_block, K.C.linecoef_rows);
+  for (int k = k0; k < k1; k++) {
+    const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
+    double *out = K.C.linecoef + (int64_t)k * K.C.linecoef_stride + li0;
+#pragma unroll
+    for (int q = 0; q < LINECOEF_PER; q++) {
+      double v = 0.;
+      if (in[q]) {
+        const double n_u = pops[r[q].ul_upper], n_l = pops[r[q].ul_lower];
+        v = (r[q].B_lu * n_l - r[q].B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI;
+      }
+      if (st[q]) out[q * 256] = v;
     }
-    K.C.linecoef[(int64_t)k * K.C.linecoef_stride + li] = v;
   }
 }
 
@@ -750,6 +814,7 @@ struct Engine {
   // level mode: sampled jumps on pairs that had a record / on all pairs, over the transports before the last placement
   int64_t ma_acts_cached = 0, ma_acts_total = 0;
   int64_t marec_scratch_doubles = 0;
+  int64_t marec_slab_doubles = 0;     // k_marec: one block's slab (the longest level's positions x MAREC_ROWS)
   double *d_estblock = nullptr;
   int32_t *d_target_ul = nullptr, *d_target_t = nullptr;
   bool have_cells = false;
@@ -814,6 +879,10 @@ struct Engine {
   bool r_binned = false;          // bin the R queue by cell before k_rpkt (ARTIS_GPU_R_BIN=1)
   bool ma_bin_blk = true;         // few cells: block-local M-queue binning (ARTIS_GPU_MA_BIN_BLK=0: per-entry atomics)
   bool ma_pre_on = true;          // M-queue pre-tickets (WaveState::ma_pre; ARTIS_GPU_MA_PRE=0: gathered by the scatter)
+  bool marec_fused = false;       // row mode: k_marec (running sums through a per-block slab) instead of the
+                                  // k_marates + k_mapack batches (ARTIS_GPU_MAREC_FUSED=1)
+  int ncu = 256;
+  bool rpkt_coop = true;          // detailed-bf models: wave-made continuum sums in k_rpkt (ARTIS_GPU_RPKT_COOP=0: per lane)
   std::vector<hipEvent_t> vev;  // (start, end) pairs around the k_vpkt launches of the last update
   size_t vev_used = 0;
   double last_vpkt_ms = 0.;
@@ -1311,13 +1380,17 @@ int run_wavefront(int64_t n, int nts, double t2) {
     }
     // the per-block estimator accumulator of few-cell models (dynamic LDS, sized only when it is used)
     const size_t est_shm = est_lds_on(G.K) ? EST_LDS_DOUBLES * sizeof(double) : 0;
+    // detailed bf estimators (the nebular options): the instance whose continuum sums are made by the whole wave
+    const bool rpkt_coop = G.K.R.detailed_bf && G.K.T.nbf > 0 && G.K.R.do_r_lc && G.rpkt_coop;
     auto launch_rpkt = [&]() -> int {
-      if (rpkt_occ == 3)
-        k_rpkt<3><<<grid, WAVE_BLOCK, est_shm, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+      if (rpkt_coop)
+        k_rpkt<2, true><<<grid, WAVE_BLOCK, est_shm, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+      else if (rpkt_occ == 3)
+        k_rpkt<3, false><<<grid, WAVE_BLOCK, est_shm, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
       else if (rpkt_occ == 2)
-        k_rpkt<2><<<grid, WAVE_BLOCK, est_shm, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+        k_rpkt<2, false><<<grid, WAVE_BLOCK, est_shm, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
       else
-        k_rpkt<1><<<grid, WAVE_BLOCK, est_shm, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
+        k_rpkt<1, false><<<grid, WAVE_BLOCK, est_shm, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts, t2);
       return 0;
     };
     if (G.K.V.on)
@@ -1455,9 +1528,9 @@ int run_wavefront(int64_t n, int nts, double t2) {
     if (st[32] + st[33] + st[34] + st[35] + st[36])
       fprintf(stderr,
               "[artis_gpu] rpkt step phases (cycles/pass): boundary %.0f, kappa %.0f, line loop %.0f, move+estimators "
-              "%.0f, event %.0f\n",
+              "%.0f, event %.0f, wave continuum sums %.0f\n",
               (double)st[32] / st[0], (double)st[33] / st[0], (double)st[34] / st[0], (double)st[35] / st[0],
-              (double)st[36] / st[0]);
+              (double)st[36] / st[0], (double)st[37] / st[0]);
 #ifdef ARTIS_STAMPS
     {
       unsigned long long dg[48];
@@ -2974,6 +3047,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   {
     int ncu = 256;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+    G.ncu = ncu;
     G.wave_grid = ncu * 8;  // 32 waves per CU of 256-thread blocks; late blocks find the queue drained
     // (tests: ARTIS_GPU_WAVE_GRID=<blocks>, a multiple of 8, shrinks the persistent grids and the vpkt overflow records)
     if (const char *wg = getenv("ARTIS_GPU_WAVE_GRID")) G.wave_grid = std::max(8, atoi(wg) / 8 * 8);
@@ -2987,6 +3061,10 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     // ~250 ms more binning per step (profiles/r03g_ab.txt), so off unless asked for (ARTIS_GPU_R_BIN=1)
     const char *rb = getenv("ARTIS_GPU_R_BIN");
     G.r_binned = rb && rb[0] == '1';
+    const char *rc_ = getenv("ARTIS_GPU_RPKT_COOP");
+    G.rpkt_coop = !(rc_ && rc_[0] == '0');
+    const char *mf = getenv("ARTIS_GPU_MAREC_FUSED");
+    G.marec_fused = mf && mf[0] == '1';
     const char *mp = getenv("ARTIS_GPU_MA_PRE");
     G.ma_pre_on = !(mp && mp[0] == '0');
     const char *bb = getenv("ARTIS_GPU_MA_BIN_BLK");
@@ -3478,7 +3556,9 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     for (int ul = 0; ul < nl; ul++) maxlev = std::max(maxlev, G.h_dbl_off[ul + 1] - G.h_dbl_off[ul]);
     int64_t cap = ((int64_t)2 << 30) / 8;  // k_marates scratch of row mode (ARTIS_GPU_MAREC_SCRATCH_MB)
     if (const char *sm = getenv("ARTIS_GPU_MAREC_SCRATCH_MB")) cap = (int64_t)(atof(sm) * (1 << 20) / 8);
-    const int64_t scratch = std::max<int64_t>(maxlev * nne_cells, std::min<int64_t>(G.h_dbl_off[nl] * nne_cells, cap));
+    // (at least one k_marec slab)
+    const int64_t scratch = std::max<int64_t>(
+        {maxlev * nne_cells, maxlev * MAREC_ROWS, std::min<int64_t>(G.h_dbl_off[nl] * nne_cells, cap)});
     double budget = 0.5 * (double)freeb;
     if (const char *mx = getenv("ARTIS_GPU_MACACHE_MAX_GB")) budget = atof(mx) * (double)(1ull << 30);
     const char *mr = getenv("ARTIS_GPU_MACACHE_ROWS");
@@ -3498,6 +3578,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
         C.ma_rows = nne_cells;
         G.d_marec_scratch = (double *)sc;
         G.marec_scratch_doubles = scratch;
+        G.marec_slab_doubles = maxlev * MAREC_ROWS;
       }
     }
     if (!C.ma_rows) {
@@ -3791,10 +3872,13 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
     if (ntg > 0)
       k_transpose<<<dim3((unsigned)((ntg + 63) / 64), (unsigned)((n_ne + 63) / 64)), 256, 0, G.stream>>>(
           G.K.C.corrphot, G.K.C.corrphotT, n_ne, ntg);
-    if (G.K.C.linecoef)
-      k_linecoef<<<dim3((unsigned)((G.K.C.linecoef_stride + 255) / 256),
-                        (unsigned)std::min(G.K.C.linecoef_rows, 32768)), 256, 0,
-                    G.stream>>>(G.K);
+    if (G.K.C.linecoef) {
+      // about 16k blocks (64 per CU): each takes 1024 lines over a run of rows
+      const unsigned nx = (unsigned)((G.K.C.linecoef_stride + 256 * LINECOEF_PER - 1) / (256 * LINECOEF_PER));
+      const int ny = std::max(1, std::min(G.K.C.linecoef_rows, (int)((16384 + nx - 1) / nx)));
+      const int rpb = (G.K.C.linecoef_rows + ny - 1) / ny;
+      k_linecoef<<<dim3(nx, (unsigned)((G.K.C.linecoef_rows + rpb - 1) / rpb)), 256, 0, G.stream>>>(G.K, rpb);
+    }
     const int mr = G.K.C.ma_rows;
     if (G.K.C.ma_level_mode) {
       // level mode: the action totals of every (cell, level) pair (the jumps without a record select from them),
@@ -3803,6 +3887,12 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
       k_marates<<<(unsigned)((nun + 255) / 256), 256, 0, G.stream>>>(G.K, nts, 0, (int)nl, nullptr, G.d_ma_bincell,
                                                                      n_ne, false);
       if (int rc = ma_level_build(nts)) return rc;
+    } else if (mr > 0 && G.marec_fused && G.marec_slab_doubles > 0) {
+      // one persistent launch: 4 blocks per CU (k_marec's LDS), each with its slab of the scratch
+      const int64_t ntasks = (int64_t)(mr + MAREC_ROWS - 1) / MAREC_ROWS * nl;
+      const int64_t nblk = std::min<int64_t>({ntasks, (int64_t)G.ncu * 4, G.marec_scratch_doubles / G.marec_slab_doubles});
+      k_marec<<<(unsigned)nblk, MAREC_ROWS, 0, G.stream>>>(G.K, nts, G.d_marec_scratch, G.marec_slab_doubles,
+                                                             G.d_ma_bincell);
     } else if (mr > 0) {
       // batches of levels whose records fit the scratch
       for (int ul0 = 0; ul0 < nl;) {

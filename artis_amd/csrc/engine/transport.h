@@ -29,6 +29,19 @@ struct Tx {
   int est_mgi = -1;
   double est_de = 0., est_denu = 0., est_deff = 0.;
   double *est_lds = nullptr;  // k_rpkt: the block's LDS estimator accumulator (DevCells::est_lds_*), or nullptr
+  // k_rpkt, models with many bf continua per frequency (the nebular options): the continuum sums of a step are made
+  // by the whole wave (wave_kappa_bf before the step, wave_bf_estimators after it) over the wave's 64-slot LDS
+  // scratch (coop_d, coop_i), instead of by each lane over its own continua -- lanes at different frequencies
+  // reach very different numbers of continua, and the wave waited for its longest list
+  double *coop_d = nullptr;
+  int *coop_i = nullptr;
+  bool pre_on = false;      // kappa_bf of this step precomputed by the wave (pre_kbf; pre_hi: the continua reached)
+  double pre_kbf = 0.;
+  int pre_hi = 0;
+  bool defer_bf = false;    // the detailed-bf estimator terms of the step are left for wave_bf_estimators:
+  bool bf_pend = false;     // (cell, frequency, opacity frequency, distance * e_cmf / nu * doppler factor)
+  int bf_k = 0, bf_mgi = 0;
+  double bf_nu = 0., bf_kapnu = 0., bf_d = 0.;
 #ifdef ARTIS_STAMPS
   unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;  // diagnostic build: cycles per step phase
 #endif
@@ -447,6 +460,12 @@ DEVFN void bf_range(const Ctx &K, double nu, int &lo, int &hi) {
 // rpkt.cc:1075-1207 calculate_kappa_bf_gammacontr: the kappa_bf total (the cumulative array is re-scanned on demand)
 DEVFN double kappa_bf_total(Tx &x, int k, int mgi, double nu) {
   const Ctx &K = x.K;
+  if (x.pre_on) {  // made by the wave before the step (wave_kappa_bf): the same sum in the same order
+    x.pre_on = false;
+    lwork(x.L, WK_BF_ACTIVE, (unsigned long long)x.pre_hi);
+    x.wb += (unsigned)x.pre_hi;
+    return x.pre_kbf;
+  }
   double kappa_bf_sum = 0.;
   int lo, hi;
   bf_range(K, nu, lo, hi);
@@ -918,20 +937,30 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
     const double dopplerfactor = doppler_packet(K, p);
     const double d_over_nu = distance_e_cmf / nu * dopplerfactor;
     const int64_t row = (int64_t)mgi * K.T.nbf;
-    // the window nu_edge <= nu <= nu_max of the reference's loop is [lo, hi) (bf_range); gamma_contr is zero below
-    // the first continuum kap.nu reaches (lo_k), and adding zero changes no sum, so the loop starts at max(lo, lo_k)
-    // (without do_r_lc no bf opacity is evaluated and the zero-initialised gamma_contr stays 0, rpkt.cc:1230)
-    int lo, hi, lo_k, hi_k;
-    bf_range(K, nu, lo, hi);
-    bf_range(K, kap.nu, lo_k, hi_k);
-    const BfCell cell = bf_cell(K, k, mgi, kap.nu);
-    for (int i = max(lo, lo_k); K.R.do_r_lc && i < hi; i++) {
-      double gc = 0., nnlevel;
-      if (kap.nu < K.T.allcont_nu_edge[i] || !bf_contribution(K, cell, i, kap.nu, &nnlevel, &gc)) continue;
-      if (x.est_lds && K.C.est_lds_bf >= 0)
-        atomicAdd(&x.est_lds[K.C.est_lds_bf + (int64_t)k * K.T.nbf + i], gc * d_over_nu);
-      else
-        safeadd(&K.E.bfrate[row + i], gc * d_over_nu);
+    if (x.defer_bf) {  // (k_rpkt: added by the wave after the step, wave_bf_estimators)
+      x.bf_pend = K.R.do_r_lc != 0;
+      x.bf_k = k;
+      x.bf_mgi = mgi;
+      x.bf_nu = nu;
+      x.bf_kapnu = kap.nu;
+      x.bf_d = d_over_nu;
+    } else {
+      // the window nu_edge <= nu <= nu_max of the reference's loop is [lo, hi) (bf_range); gamma_contr is zero
+      // below the first continuum kap.nu reaches (lo_k), and adding zero changes no sum, so the loop starts at
+      // max(lo, lo_k) (without do_r_lc no bf opacity is evaluated and the zero-initialised gamma_contr stays 0,
+      // rpkt.cc:1230)
+      int lo, hi, lo_k, hi_k;
+      bf_range(K, nu, lo, hi);
+      bf_range(K, kap.nu, lo_k, hi_k);
+      const BfCell cell = bf_cell(K, k, mgi, kap.nu);
+      for (int i = max(lo, lo_k); K.R.do_r_lc && i < hi; i++) {
+        double gc = 0., nnlevel;
+        if (kap.nu < K.T.allcont_nu_edge[i] || !bf_contribution(K, cell, i, kap.nu, &nnlevel, &gc)) continue;
+        if (x.est_lds && K.C.est_lds_bf >= 0)
+          atomicAdd(&x.est_lds[K.C.est_lds_bf + (int64_t)k * K.T.nbf + i], gc * d_over_nu);
+        else
+          safeadd(&K.E.bfrate[row + i], gc * d_over_nu);
+      }
     }
   }
   if (K.R.multibin) {  // radfield.cc:845-866
@@ -1008,6 +1037,116 @@ DEVFN void wave_flush_estimators(Tx &x) {
     }
   }
   x.est_mgi = -1;
+}
+
+// ---- the continuum sums of a step made by the whole wave (k_rpkt, models with many bf continua per frequency) ----
+// Every lane contributes n consecutive items (its continua); the wave's items are laid out lane after lane
+// (exclusive prefix `pref` over the lanes), and each pass over them gives every lane one item -- so a wave spends
+// about total / 64 item evaluations instead of the longest lane's count.  Wave-uniform.
+DEVFN int wave_excl_prefix(int n, int &total) {
+  const int lane = (int)__lane_id();
+  int incl = n;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += t;
+  }
+  total = __shfl(incl, 63, 64);
+  return incl - n;
+}
+// the lane owning item j: the last lane whose prefix is <= j (lane prefixes in the wave's LDS slots s_pref[0..63])
+DEVFN int wave_item_owner(const int *s_pref, int j) {
+  int o = 0;
+#pragma unroll
+  for (int step = 32; step > 0; step >>= 1)
+    if (s_pref[o + step] <= j) o += step;
+  return o;
+}
+DEVFN const double2 *shfl_ptr(const double2 *p, int src) {
+  return (const double2 *)__shfl((long long)p, src, 64);
+}
+// calculate_kappa_bf_gammacontr's kappa_bf sum (rpkt.cc:1075-1207) of every lane with `want` (cell k / mgi,
+// frequency nu): the terms n_level * gamma_contr are evaluated by the wave 64 at a time into the LDS slots s_d, and
+// each lane adds its own terms in continuum order -- the reference's sum, term for term.  *hi: the continua the
+// reference's loop visits (the work counter).
+DEVFN double wave_kappa_bf(Tx &x, bool want, int k, int mgi, double nu, int &hi_out) {
+  const Ctx &K = x.K;
+  double *s_d = x.coop_d;
+  int *s_i = x.coop_i;
+  const int lane = (int)__lane_id();
+  int lo = 0, hi = 0;
+  if (want) bf_range(K, nu, lo, hi);
+  hi_out = hi;
+  const int n = hi - lo;
+  int total;
+  const int pref = wave_excl_prefix(n, total);
+  double sum = 0.;
+  if (total == 0) return sum;
+  const BfCell cell = want ? bf_cell(K, k, mgi, nu) : BfCell{K.C.bfcell, 0.};
+  s_i[lane] = pref;
+  __builtin_amdgcn_wave_barrier();
+  for (int c0 = 0; c0 < total; c0 += 64) {
+    const int j = min(c0 + lane, total - 1);
+    const int o = wave_item_owner(s_i, j);
+    const int lo_o = __shfl(lo, o, 64), pref_o = __shfl(pref, o, 64);
+    const double nu_o = __shfl(nu, o, 64), ef_o = __shfl(cell.expfac, o, 64);
+    const double2 *row_o = shfl_ptr(cell.row, o);
+    double term = 0.;
+    if (c0 + lane < total) {
+      double nn, gc;
+      if (bf_contribution(K, BfCell{row_o, ef_o}, lo_o + (j - pref_o), nu_o, &nn, &gc)) term = nn * gc;
+    }
+    s_d[lane] = term;
+    __builtin_amdgcn_wave_barrier();
+    const int a = max(pref, c0), b = min(pref + n, c0 + 64);
+    for (int jj = a; jj < b; jj++) sum += s_d[jj - c0];
+    __builtin_amdgcn_wave_barrier();
+  }
+  return sum;
+}
+// update_bfestimators (radfield.cc:764-829) of the step, deferred by update_estimators (Tx::defer_bf): the window
+// [max(lo(nu), lo(kap.nu)), hi(nu)) of every pending lane, gamma_contr at kap.nu, made by the wave 64 continua at a
+// time; each term is added to the estimator on its own (the additions are atomics, in no order, as per lane).
+DEVFN void wave_bf_estimators(Tx &x) {
+  const Ctx &K = x.K;
+  const int lane = (int)__lane_id();
+  const bool want = x.bf_pend;
+  x.bf_pend = false;
+  int start = 0, n = 0;
+  if (want) {
+    int lo, hi, lo_k, hi_k;
+    bf_range(K, x.bf_nu, lo, hi);
+    bf_range(K, x.bf_kapnu, lo_k, hi_k);
+    start = max(lo, lo_k);
+    n = max(0, hi - start);
+  }
+  int total;
+  const int pref = wave_excl_prefix(n, total);
+  if (total == 0) return;
+  const BfCell cell = want ? bf_cell(K, x.bf_k, x.bf_mgi, x.bf_kapnu) : BfCell{K.C.bfcell, 0.};
+  x.coop_i[lane] = pref;
+  __builtin_amdgcn_wave_barrier();
+  const int nbf = K.T.nbf;
+  const bool lds = x.est_lds && K.C.est_lds_bf >= 0;
+  for (int c0 = 0; c0 < total; c0 += 64) {
+    const int j = min(c0 + lane, total - 1);
+    const int o = wave_item_owner(x.coop_i, j);
+    const int start_o = __shfl(start, o, 64), pref_o = __shfl(pref, o, 64);
+    const int k_o = __shfl(x.bf_k, o, 64), mgi_o = __shfl(x.bf_mgi, o, 64);
+    const double kapnu_o = __shfl(x.bf_kapnu, o, 64), ef_o = __shfl(cell.expfac, o, 64);
+    const double d_o = __shfl(x.bf_d, o, 64);
+    const double2 *row_o = shfl_ptr(cell.row, o);
+    if (c0 + lane < total) {
+      const int i = start_o + (j - pref_o);
+      double nn, gc;
+      if (!(kapnu_o < K.T.allcont_nu_edge[i]) && bf_contribution(K, BfCell{row_o, ef_o}, i, kapnu_o, &nn, &gc)) {
+        if (lds)
+          atomicAdd(&x.est_lds[K.C.est_lds_bf + (int64_t)k_o * nbf + i], gc * d_o);
+        else
+          safeadd(&K.E.bfrate[(int64_t)mgi_o * nbf + i], gc * d_o);
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
 }
 
 // the block's LDS estimator accumulator: zeroed at the start of k_rpkt, added to the estimators at its end (one
@@ -1149,14 +1288,20 @@ DEVNI void rpkt_event_continuum(Tx &x, Pkt &p, const Kappa &kap, int k, int mgi)
     int allcontindex = last;
     double running = 0.;
     const BfCell cell = bf_cell(K, k, mgi, kap.nu);
-    for (int i = 0; i < last; i++) {
-      if (!(kap.nu < K.T.allcont_nu_edge[i])) {
+    // the terms are zero outside [lo, hi) (bf_range): below lo the running sum stays 0 (so the search ends at i = 0
+    // only for a zero draw), from hi on it stays at its total (the search then runs on to `last`)
+    int lo, hi;
+    bf_range(K, kap.nu, lo, hi);
+    if (!(running < kappa_bf_rand)) {
+      allcontindex = 0;
+    } else {
+      for (int i = lo; i < min(hi, last); i++) {
         double nnlevel, gc;
         if (bf_contribution(K, cell, i, kap.nu, &nnlevel, &gc)) running += nnlevel * gc;
-      }
-      if (!(running < kappa_bf_rand)) {
-        allcontindex = i;
-        break;
+        if (!(running < kappa_bf_rand)) {
+          allcontindex = i;
+          break;
+        }
       }
     }
     const double nu_edge = K.T.allcont_nu_edge[allcontindex];

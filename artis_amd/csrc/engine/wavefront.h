@@ -190,8 +190,10 @@ __global__ void k_classify(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *
 #define RPKT_LINES_PER_PASS 0
 #endif
 
-// r-packets: persistent lanes, one r-packet step (or part of its line walk) per loop pass
-template <int MINW>
+// r-packets: persistent lanes, one r-packet step (or part of its line walk) per loop pass.  COOP: the instance for
+// models with detailed bf estimators, whose continuum sums are made by the whole wave (wave_kappa_bf,
+// wave_bf_estimators); the others keep the registers of the plain step.
+template <int MINW, bool COOP>
 __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa, int64_t n,
                                                      int nts, double t2) {
   CTX_IN_LDS(ctxp)
@@ -216,6 +218,17 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
     est_lds_zero(s_est);
     x.est_lds = s_est;
   }
+  // models with many bf continua per frequency (detailed bf estimators: the nebular options): the step's continuum
+  // sums are made by the whole wave (transport.h wave_kappa_bf / wave_bf_estimators)
+  __shared__ double s_coopd[COOP ? WAVE_BLOCK : 1];
+  __shared__ int s_coopi[COOP ? WAVE_BLOCK : 1];
+  const bool coop = COOP && K.R.detailed_bf && K.T.nbf > 0 && K.R.do_r_lc;
+  if (coop) {
+    x.coop_d = &s_coopd[threadIdx.x & ~63];
+    x.coop_i = &s_coopi[threadIdx.x & ~63];
+    x.defer_bf = true;
+  }
+  const int npm = K.G.npts_model;
   const uint32_t nq = W.ctr[2 * QR];
   Pkt p;
   RStep S;
@@ -269,6 +282,25 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
 #ifdef ARTIS_STAMPS
     x.tlast = ts0;
 #endif
+    if (coop) {
+      // the continuum opacity of the step every stepping lane is about to take (its cell and frequency at the step's
+      // start, as get_event_begin evaluates it), made by the wave; unused by a step that ends before it
+      bool want = false;
+      int mgi = 0, k = 0;
+      if (have && !x.vstop && x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
+        mgi = cell_mgi(K, p.where);
+        if (mgi != npm && K.C.thick[mgi] != 1 && K.R.opacity_case == 4) {
+          want = true;
+          k = K.C.ne_index[mgi];
+        }
+      }
+      x.pre_kbf = wave_kappa_bf(x, want, k, mgi, p.nu_cmf, x.pre_hi);
+      x.pre_on = want;
+#ifdef ARTIS_STAMPS
+      x.tlast = wave_clock();
+      x.st[5] += x.tlast - ts0;
+#endif
+    }
     if (have) {
       // a step starts when no walk is in progress; get_event's walk advances at most RPKT_LINES_PER_PASS lines per
       // pass (a lane with a long walk no longer holds its wave while the others' short steps wait)
@@ -336,6 +368,15 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
       }
     }
     wave_flush_estimators(x);  // the step's J / nuJ / ffheating terms, once per cell and wave where possible
+    if (coop) {
+#ifdef ARTIS_STAMPS
+      const unsigned long long tb0 = wave_clock();
+#endif
+      wave_bf_estimators(x);
+#ifdef ARTIS_STAMPS
+      x.st[5] += wave_clock() - tb0;
+#endif
+    }
     st_tstep += wave_clock() - ts0;
     if (ARTIS_WAVE_STATS) {
       unsigned ml = x.wl, sl = x.wl, mb = x.wb, sb = x.wb;
@@ -353,7 +394,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
   }
 #ifdef ARTIS_STAMPS
   if (lane_id() == 0)
-    for (int i = 0; i < 5; i++) atomicAdd(&W.stats[32 + i], x.st[i]);
+    for (int i = 0; i < 6; i++) atomicAdd(&W.stats[32 + i], x.st[i]);
 #endif
   if (ARTIS_WAVE_STATS && lane_id() == 0) {
     atomicAdd(&W.stats[24], st_lmax);

@@ -77,7 +77,7 @@ WORK_NAMES = ["active", "rpkt_steps", "lines_scanned", "line_taus", "kappa_evals
 
 # rocprof names (prefixes) of each class's kernel: k_ma's instance is k_ma<waves, coop, level> (row mode
 # k_ma<1, false, false>), k_vpkt's k_vpkt<prefetch, waves>
-KERNEL_NAME = {"rpkt": "k_rpkt<2>", "ma": "k_ma<", "kpkt": "k_kpkt", "vpkt": "k_vpkt<", "binning": "k_ma_scatter",
+KERNEL_NAME = {"rpkt": "k_rpkt<2", "ma": "k_ma<", "kpkt": "k_kpkt", "vpkt": "k_vpkt<", "binning": "k_ma_scatter",
                "finish": "k_ma_finish"}
 
 

@@ -12,6 +12,10 @@
 #   tools/gpu.sh cfgprof name [bench.py args ...]    one BASELINE config sub-line (w7_100_shells, nebular_onezone,
 #                                                    kilonova) under rocprofv3 --stats -> $O/cfg_$name/, $O/cfg_$name.json
 #   tools/gpu.sh pcs  [bench.py args ...]            stochastic PC sampling (cycles) of a short bench run -> $O/pcs/
+#   tools/gpu.sh stamps name [bench.py args ...]     the cycle-stamp build (build/ab/stamps, -DARTIS_STAMPS) with
+#                                                    ARTIS_GPU_STATS=1 on a bench run -> $O/stamps_$name.{json,err}
+#   tools/gpu.sh pre name1[:ENV=V] name2 ...         the precompute alone (tools/precompute_ab.py) per engine build,
+#                                                    under rocprofv3 --stats -> $O/pre_<name>.{json,txt}
 #   tools/gpu.sh final                               tests, prof, pmc, default bench line (the round-end set)
 #
 # Environment: T (tag, default "r4"), O (output dir, default gpurun_out/$T), NAME (pmc summary name, default
@@ -82,6 +86,13 @@ run_sq() {
     --packets ${P:-2000000} --steps 1 --warmup 0 --no-cpu-baseline --no-update-grid --no-extra "$@" > "$O/sq/sq.log" 2>&1
 }
 
+run_stamps() {
+  local name=$1
+  shift
+  ARTIS_GPU_SO=build/ab/stamps/libartis_gpu.so ARTIS_GPU_STATS=1 timeout -k 10 600 python3 -u bench.py --no-cpu-baseline \
+    --no-update-grid --no-extra "$@" > "$O/stamps_$name.json" 2> "$O/stamps_$name.err" && grep "artis_gpu\]" "$O/stamps_$name.err" | tail -12
+}
+
 run_pcs() {
   rm -rf "$O/pcs"
   mkdir -p "$O/pcs"
@@ -104,6 +115,20 @@ run_ab() {
   done
 }
 
+run_pre() {
+  local v name envs so tag db
+  for v in "$@"; do
+    name=${v%%:*}; envs=""; [[ "$v" == *:* ]] && envs=${v#*:}
+    so=build/ab/$name/libartis_gpu.so; [ "$name" = main ] && so=artis_amd/lib/libartis_gpu.so
+    tag=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')
+    rm -rf "$O/pre_$tag"
+    env ARTIS_GPU_SO=$so $envs timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/pre_$tag" -o run -- python3 -u \
+      tools/precompute_ab.py > "$O/pre_$tag.json" 2> "$O/pre_$tag.err" || { echo "FAIL $v"; tail -5 "$O/pre_$tag.err"; return 1; }
+    db=$O/pre_$tag/run_results.db
+    { echo "$v $(tail -c 200 "$O/pre_$tag.json")"; python3 tools/kstat_short.py "$db" 12; } | tee "$O/pre_$tag.txt"
+  done
+}
+
 case "$cmd" in
   tests) run_tests "$@" ;;
   bench) run_bench "$@" ;;
@@ -113,6 +138,8 @@ case "$cmd" in
   ab) run_ab "$@" ;;
   cfgprof) run_cfgprof "$@" ;;
   pcs) run_pcs "$@" ;;
+  stamps) run_stamps "$@" ;;
+  pre) run_pre "$@" ;;
   final) run_tests && run_prof --no-extra && run_pmc && run_bench ;;
   *) echo "usage: tools/gpu.sh tests|bench|prof|pmc|sq|ab|final [args]"; exit 2 ;;
 esac
