@@ -315,13 +315,17 @@ DEVFN void marates_sums(const Ctx &K, int ul, int k, double t_mid, double *__res
 #undef REC
 }
 
+// The rows of each level are padded to a multiple of 64 (MARATES_PAD), so that a wave never straddles two levels: the
+// level index is then wave-uniform (readfirstlane), and the atomic data the rates read are scalar loads.
+#define MARATES_PAD(kn) (((int64_t)(kn) + 63) & ~(int64_t)63)
 __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict__ S, const int32_t *__restrict__ cells,
                           int kn, bool cache) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nl = K.T.nlevels_total;
-  if (idx >= (int64_t)kn * nlev) return;
-  const int ul = ul0 + (int)(idx / kn);
-  const int kr = (int)(idx % kn);
+  const int64_t knp = MARATES_PAD(kn);
+  const int ul = __builtin_amdgcn_readfirstlane(ul0 + (int)(idx / knp));
+  const int kr = (int)(idx % knp);
+  if (ul >= ul0 + nlev || kr >= kn) return;
   const int k = cells[kr];
   double *rec = cache ? S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * kn + kr : nullptr;
   double pr[ARTIS_MA_ACTION_COUNT];
@@ -404,36 +408,6 @@ __global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, const double *__
   const int64_t n_ne = K.C.ma_rows;  // the cached cells, the scratch's stride
   mapack_tile(K, ul, S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * n_ne, n_ne, (int64_t)blockIdx.x * 64, n_ne, 0,
               L);
-}
-
-// k_marates + k_mapack fused (row mode): a persistent block takes (level, MAREC_ROWS rows) tasks, level-major.  Its
-// threads make the rows' running sums (one row each, as k_marates) into the block's own slab of the scratch
-// ([position][MAREC_ROWS], just written, so read back from the caches rather than HBM), then pack them into the key
-// records 64 rows at a time (mapack_tile).  The slabs hold the longest level: slab_doubles per block.
-#define MAREC_ROWS 256
-#ifndef MAREC_MINW
-#define MAREC_MINW 4  // waves per SIMD (the LDS allows 4 blocks per CU)
-#endif
-__global__ __launch_bounds__(MAREC_ROWS, MAREC_MINW) void k_marec(Ctx K, int nts, double *__restrict__ slabs, int64_t slab_doubles,
-                                                      const int32_t *__restrict__ cells) {
-  __shared__ MapackLds L;
-  const int64_t rows = K.C.ma_rows;
-  const int64_t ngroups = (rows + MAREC_ROWS - 1) / MAREC_ROWS;
-  const int64_t ntasks = ngroups * K.T.nlevels_total;
-  double *slab = slabs + (int64_t)blockIdx.x * slab_doubles;
-  const double t_mid = K.G.ts_mid[nts];
-  for (int64_t t = blockIdx.x; t < ntasks; t += gridDim.x) {
-    const int ul = (int)(t / ngroups);
-    const int64_t row0 = (t % ngroups) * MAREC_ROWS;
-    const int64_t nvalid = min((int64_t)MAREC_ROWS, rows - row0);
-    __syncthreads();  // (the previous task's pack has read the slab)
-    if (threadIdx.x < nvalid) {
-      double pr[ARTIS_MA_ACTION_COUNT];
-      marates_sums(K, ul, cells[row0 + threadIdx.x], t_mid, slab + threadIdx.x, MAREC_ROWS, true, pr);
-    }
-    __syncthreads();
-    for (int64_t c0 = 0; c0 < nvalid; c0 += 64) mapack_tile(K, ul, slab, MAREC_ROWS, c0, nvalid, row0, L);
-  }
 }
 
 // ---- level mode of the macro-atom key records (DevCells::ma_lptr): placement and build ----------------------
@@ -620,35 +594,20 @@ __global__ __launch_bounds__(64) void k_ma_build(Ctx K, const int2 *__restrict__
 }
 
 // DevCells::linecoef: the Sobolev coefficient (B_lu n_l - B_ul n_u) * HCLIGHTOVERFOURPI of every line in every
-// non-empty cell, in get_event's operation order (rpkt.cc:168-187).  A block holds LINECOEF_PER lines per thread
-// (their records loaded once, in registers) and walks a run of rows: every store instruction writes 256 consecutive
-// doubles of one row, the population gathers come from that row's 29 kB (L1 / L2).  The blocks of one row run are
-// consecutive ids, so they walk the same rows at about the same time.
-#define LINECOEF_PER 4
-__global__ __launch_bounds__(256) void k_linecoef(Ctx K, int rows_per_block) {
-  const int64_t li0 = (int64_t)blockIdx.x * (256 * LINECOEF_PER) + threadIdx.x;
-  LineTau r[LINECOEF_PER];
-  bool in[LINECOEF_PER], st[LINECOEF_PER];
-#pragma unroll
-  for (int q = 0; q < LINECOEF_PER; q++) {
-    const int64_t li = li0 + q * 256;
-    in[q] = li < K.T.nlines;
-    st[q] = li < K.C.linecoef_stride;
-    if (in[q]) r[q] = K.T.line_tau[li];
-  }
-  const int k0 = blockIdx.y * rows_per_block, k1 = min(k0 + rows_per_block, K.C.linecoef_rows);
-  for (int k = k0; k < k1; k++) {
-    const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
-    double *out = K.C.linecoef + (int64_t)k * K.C.linecoef_stride + li0;
-#pragma unroll
-    for (int q = 0; q < LINECOEF_PER; q++) {
-      double v = 0.;
-      if (in[q]) {
-        const double n_u = pops[r[q].ul_upper], n_l = pops[r[q].ul_lower];
-        v = (r[q].B_lu * n_l - r[q].B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI;
-      }
-      if (st[q]) out[q * 256] = v;
+// non-empty cell, in get_event's operation order (rpkt.cc:168-187); lanes run along a cell's row (coalesced
+// writes, line records from L2, population gathers from the cell's 29 kB row)
+__global__ __launch_bounds__(256) void k_linecoef(Ctx K) {
+  const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= K.C.linecoef_stride) return;
+  for (int k = blockIdx.y; k < K.C.linecoef_rows; k += gridDim.y) {
+    double v = 0.;
+    if (li < K.T.nlines) {
+      const LineTau r = K.T.line_tau[li];
+      const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
+      const double n_u = pops[r.ul_upper], n_l = pops[r.ul_lower];
+      v = (r.B_lu * n_l - r.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI;
     }
+    K.C.linecoef[(int64_t)k * K.C.linecoef_stride + li] = v;
   }
 }
 
@@ -814,7 +773,6 @@ struct Engine {
   // level mode: sampled jumps on pairs that had a record / on all pairs, over the transports before the last placement
   int64_t ma_acts_cached = 0, ma_acts_total = 0;
   int64_t marec_scratch_doubles = 0;
-  int64_t marec_slab_doubles = 0;     // k_marec: one block's slab (the longest level's positions x MAREC_ROWS)
   double *d_estblock = nullptr;
   int32_t *d_target_ul = nullptr, *d_target_t = nullptr;
   bool have_cells = false;
@@ -879,8 +837,6 @@ struct Engine {
   bool r_binned = false;          // bin the R queue by cell before k_rpkt (ARTIS_GPU_R_BIN=1)
   bool ma_bin_blk = true;         // few cells: block-local M-queue binning (ARTIS_GPU_MA_BIN_BLK=0: per-entry atomics)
   bool ma_pre_on = true;          // M-queue pre-tickets (WaveState::ma_pre; ARTIS_GPU_MA_PRE=0: gathered by the scatter)
-  bool marec_fused = false;       // row mode: k_marec (running sums through a per-block slab) instead of the
-                                  // k_marates + k_mapack batches (ARTIS_GPU_MAREC_FUSED=1)
   int ncu = 256;
   bool rpkt_coop = true;          // detailed-bf models: wave-made continuum sums in k_rpkt (ARTIS_GPU_RPKT_COOP=0: per lane)
   std::vector<hipEvent_t> vev;  // (start, end) pairs around the k_vpkt launches of the last update
@@ -1348,6 +1304,8 @@ int run_wavefront(int64_t n, int nts, double t2) {
   HIPCHK(hipGetLastError());
   int64_t round = 0;
   bool done = false;
+  // the QX queue's length at the end of the round before last, as the host last read it (-1: not read yet)
+  int64_t qx_known = -1;
   const bool first_placement = G.ma_initial_placement;
   for (; round < WAVE_MAX_ROUNDS && !done; round++) {
     // level mode: after the first rounds of a transport on the initial placement (and again a few rounds later),
@@ -1449,7 +1407,11 @@ int run_wavefront(int64_t n, int nts, double t2) {
       k_ma<1, false, false><<<ma_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
     TEND(1);
     HIPCHK(hipMemsetAsync(W.ctr + 2 * QM, 0, 2 * sizeof(uint32_t), G.stream));
-    {  // jumps the 32-bit keys could not decide (rare), exact; walks go back to M
+    // jumps the 32-bit keys could not decide (rare), exact; walks go back to M.  Launched only when the queue may
+    // hold any: in the first two rounds, and whenever the host's last reading (the round before last) found entries.
+    // A round without the launch leaves its entries queued (QX is reset only after a launch) for a later one; the
+    // loop does not end while QX holds any.
+    if (round < 2 || qx_known != 0) {
       TSTART(5);
       k_ma_exact<<<grid / 4, 64, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
       TEND(5);
@@ -1493,14 +1455,15 @@ int run_wavefront(int64_t n, int nts, double t2) {
       const int prev = (int)((round - 1) & 1);
       HIPCHK(hipEventSynchronize(G.ev_round[prev]));
       const uint32_t *c = G.h_ctr + prev * NQUEUES * 2;
-      if (c[2 * QR] == 0 && c[2 * QM] == 0) done = true;
+      qx_known = c[2 * QX];
+      if (c[2 * QR] == 0 && c[2 * QM] == 0 && c[2 * QX] == 0) done = true;
     }
   }
   if (!done) {
     // the loop hit its cap: check the last round before declaring a stall
     HIPCHK(hipStreamSynchronize(G.stream));
     const uint32_t *c = G.h_ctr + ((round - 1) & 1) * NQUEUES * 2;
-    if (c[2 * QR] != 0 || c[2 * QM] != 0) {
+    if (c[2 * QR] != 0 || c[2 * QM] != 0 || c[2 * QX] != 0) {
       G.last_error = "wavefront transport did not converge";
       return ARTIS_ERR_PACKET_FAULT;
     }
@@ -3063,8 +3026,6 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     G.r_binned = rb && rb[0] == '1';
     const char *rc_ = getenv("ARTIS_GPU_RPKT_COOP");
     G.rpkt_coop = !(rc_ && rc_[0] == '0');
-    const char *mf = getenv("ARTIS_GPU_MAREC_FUSED");
-    G.marec_fused = mf && mf[0] == '1';
     const char *mp = getenv("ARTIS_GPU_MA_PRE");
     G.ma_pre_on = !(mp && mp[0] == '0');
     const char *bb = getenv("ARTIS_GPU_MA_BIN_BLK");
@@ -3556,9 +3517,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     for (int ul = 0; ul < nl; ul++) maxlev = std::max(maxlev, G.h_dbl_off[ul + 1] - G.h_dbl_off[ul]);
     int64_t cap = ((int64_t)2 << 30) / 8;  // k_marates scratch of row mode (ARTIS_GPU_MAREC_SCRATCH_MB)
     if (const char *sm = getenv("ARTIS_GPU_MAREC_SCRATCH_MB")) cap = (int64_t)(atof(sm) * (1 << 20) / 8);
-    // (at least one k_marec slab)
-    const int64_t scratch = std::max<int64_t>(
-        {maxlev * nne_cells, maxlev * MAREC_ROWS, std::min<int64_t>(G.h_dbl_off[nl] * nne_cells, cap)});
+    const int64_t scratch = std::max<int64_t>(maxlev * nne_cells, std::min<int64_t>(G.h_dbl_off[nl] * nne_cells, cap));
     double budget = 0.5 * (double)freeb;
     if (const char *mx = getenv("ARTIS_GPU_MACACHE_MAX_GB")) budget = atof(mx) * (double)(1ull << 30);
     const char *mr = getenv("ARTIS_GPU_MACACHE_ROWS");
@@ -3578,7 +3537,6 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
         C.ma_rows = nne_cells;
         G.d_marec_scratch = (double *)sc;
         G.marec_scratch_doubles = scratch;
-        G.marec_slab_doubles = maxlev * MAREC_ROWS;
       }
     }
     if (!C.ma_rows) {
@@ -3872,34 +3830,24 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
     if (ntg > 0)
       k_transpose<<<dim3((unsigned)((ntg + 63) / 64), (unsigned)((n_ne + 63) / 64)), 256, 0, G.stream>>>(
           G.K.C.corrphot, G.K.C.corrphotT, n_ne, ntg);
-    if (G.K.C.linecoef) {
-      // about 16k blocks (64 per CU): each takes 1024 lines over a run of rows
-      const unsigned nx = (unsigned)((G.K.C.linecoef_stride + 256 * LINECOEF_PER - 1) / (256 * LINECOEF_PER));
-      const int ny = std::max(1, std::min(G.K.C.linecoef_rows, (int)((16384 + nx - 1) / nx)));
-      const int rpb = (G.K.C.linecoef_rows + ny - 1) / ny;
-      k_linecoef<<<dim3(nx, (unsigned)((G.K.C.linecoef_rows + rpb - 1) / rpb)), 256, 0, G.stream>>>(G.K, rpb);
-    }
+    if (G.K.C.linecoef)
+      k_linecoef<<<dim3((unsigned)((G.K.C.linecoef_stride + 255) / 256),
+                        (unsigned)std::min(G.K.C.linecoef_rows, 32768)), 256, 0,
+                    G.stream>>>(G.K);
     const int mr = G.K.C.ma_rows;
     if (G.K.C.ma_level_mode) {
       // level mode: the action totals of every (cell, level) pair (the jumps without a record select from them),
       // then the records the placement chose
-      const int64_t nun = (int64_t)n_ne * nl;
-      k_marates<<<(unsigned)((nun + 255) / 256), 256, 0, G.stream>>>(G.K, nts, 0, (int)nl, nullptr, G.d_ma_bincell,
-                                                                     n_ne, false);
+      k_marates<<<(unsigned)((MARATES_PAD(n_ne) * nl + 255) / 256), 256, 0, G.stream>>>(G.K, nts, 0, (int)nl, nullptr,
+                                                                                       G.d_ma_bincell, n_ne, false);
       if (int rc = ma_level_build(nts)) return rc;
-    } else if (mr > 0 && G.marec_fused && G.marec_slab_doubles > 0) {
-      // one persistent launch: 4 blocks per CU (k_marec's LDS), each with its slab of the scratch
-      const int64_t ntasks = (int64_t)(mr + MAREC_ROWS - 1) / MAREC_ROWS * nl;
-      const int64_t nblk = std::min<int64_t>({ntasks, (int64_t)G.ncu * 4, G.marec_scratch_doubles / G.marec_slab_doubles});
-      k_marec<<<(unsigned)nblk, MAREC_ROWS, 0, G.stream>>>(G.K, nts, G.d_marec_scratch, G.marec_slab_doubles,
-                                                             G.d_ma_bincell);
     } else if (mr > 0) {
       // batches of levels whose records fit the scratch
       for (int ul0 = 0; ul0 < nl;) {
         int ul1 = ul0 + 1;
         while (ul1 < nl && (G.h_dbl_off[ul1 + 1] - G.h_dbl_off[ul0]) * mr <= G.marec_scratch_doubles) ul1++;
         const int nlev = ul1 - ul0;
-        k_marates<<<(unsigned)(((int64_t)nlev * mr + 255) / 256), 256, 0, G.stream>>>(
+        k_marates<<<(unsigned)((MARATES_PAD(mr) * nlev + 255) / 256), 256, 0, G.stream>>>(
             G.K, nts, ul0, nlev, G.d_marec_scratch, G.d_ma_bincell, mr, true);
         k_mapack<<<dim3((unsigned)((mr + 63) / 64), (unsigned)nlev), 256, 0, G.stream>>>(G.K, ul0,
                                                                                          G.d_marec_scratch);

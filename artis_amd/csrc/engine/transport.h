@@ -42,6 +42,12 @@ struct Tx {
   bool bf_pend = false;     // (cell, frequency, opacity frequency, distance * e_cmf / nu * doppler factor)
   int bf_k = 0, bf_mgi = 0;
   double bf_nu = 0., bf_kapnu = 0., bf_d = 0.;
+  // a bound-free absorption's continuum selection (rpkt_event_continuum) is left for the wave (wave_bf_select):
+  // (cell, opacity frequency, the draw zrand2 * kappa_bf)
+  bool defer_sel = false;
+  bool sel_pend = false;
+  int sel_k = 0, sel_mgi = 0;
+  double sel_nu = 0., sel_rand = 0.;
 #ifdef ARTIS_STAMPS
   unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;  // diagnostic build: cycles per step phase
 #endif
@@ -87,6 +93,7 @@ struct ColdSoa {
     tx.rng = x.rng;
     tx.nts = x.nts;
     tx.ok = x.ok;
+    tx.defer_sel = x.defer_sel;
     Pkt tp;
     pkt_copy_hot(tp, p);
     pkt_load_cold(soa, n, idx, tp);
@@ -95,6 +102,13 @@ struct ColdSoa {
     pkt_copy_hot(p, tp);
     x.rng = tx.rng;
     x.ok = tx.ok;
+    if (x.defer_sel && tx.sel_pend) {
+      x.sel_pend = true;
+      x.sel_k = tx.sel_k;
+      x.sel_mgi = tx.sel_mgi;
+      x.sel_nu = tx.sel_nu;
+      x.sel_rand = tx.sel_rand;
+    }
   }
 };
 
@@ -429,33 +443,76 @@ DEVFN bool bf_contribution(const Ctx &K, const BfCell &cell, int i, double nu, d
   *gcontr_out = sigma_bf * c.probability * corrfactor;
   return true;
 }
+// bf_contribution of U continua at once (the wave's item loops), staged so that the table loads of the U items are in
+// flight together: the records, then both cross-section points (indices clamped into the table; a value the
+// branch taken does not use is discarded).  The expressions are bf_contribution's and
+// photoionization_crosssection_fromtable's (version-2 tables; version 1 goes through the scalar function).
+template <int U>
+DEVFN void bf_contribution_batch(const Ctx &K, const BfCell (&cell)[U], const int (&ci)[U], const double (&nu)[U],
+                                 bool (&ok)[U], double (&nn)[U], double (&gc)[U]) {
+  if (K.T.phixs_file_version == 1) {
+#pragma unroll
+    for (int u = 0; u < U; u++) ok[u] = bf_contribution(K, cell[u], ci[u], nu[u], &nn[u], &gc[u]);
+    return;
+  }
+  BfCont c[U];
+  double2 cb[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    c[u] = K.T.bfc[ci[u]];
+    cb[u] = cell[u].row[ci[u]];
+  }
+  const int np = K.T.nphixspoints;
+  double ireal[U];
+  int ix[U];
+  float xa[U], xb[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    ireal[u] = (nu[u] / c[u].nu_edge - 1.0) / K.T.nphixsnuincrement;
+    ix[u] = (int)floor(ireal[u]);
+    const int la = ix[u] < 0 ? 0 : (ix[u] < np - 1 ? ix[u] : np - 1);
+    const float *xs = K.T.phixs_xs + max(c[u].xs_off, 0);
+    xa[u] = xs[la];
+    xb[u] = xs[min(la + 1, np - 1)];
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    ok[u] = nu[u] <= c[u].nu_max && cb[u].x > 0;
+    float sigma;
+    if (ix[u] < 0) {
+      sigma = 0.0;
+    } else if (ix[u] < np - 1) {
+      const double a = xa[u], b = xb[u];
+      const double factor_b = ireal[u] - ix[u];
+      sigma = ((1. - factor_b) * a) + (factor_b * b);
+    } else {
+      const double nu_max_phixs = c[u].nu_edge * K.T.last_phixs_nuovernuedge;
+      sigma = xa[u] * pow(nu_max_phixs / nu[u], 3);
+    }
+    const double sigma_bf = sigma;
+    const double stimfactor = cb[u].y * cell[u].expfac;
+    double corrfactor = 1 - stimfactor;
+    if (corrfactor < 0) corrfactor = 0.;
+    nn[u] = cb[u].x;
+    gc[u] = sigma_bf * c[u].probability * corrfactor;
+  }
+}
 // The continua a frequency reaches: hi = the reference's loop length (it breaks at the first continuum with
 // nu < nu_edge, the edges ascending), lo = the first continuum whose cross-section table still covers nu
 // (nu <= nu_edge * last_phixs_nuovernuedge, ascending with the edges): below lo, bf_contribution is false (and the
-// detailed-bf window test fails), so the sums over [lo, hi) are the reference's sums over [0, hi).  A scan over
-// DevTab::bf_edge2 four continua per trip to memory (the table is padded with infinities).
+// detailed-bf window test fails), so the sums over [lo, hi) are the reference's sums over [0, hi).  Two binary
+// searches over DevTab::bf_edge2 (nu_edge, nu_max), a fixed number of steps (no divergence between lanes).
 DEVFN void bf_range(const Ctx &K, double nu, int &lo, int &hi) {
   const double2 *e = K.T.bf_edge2;
-  lo = 0;
-  hi = 0;
-  for (int i0 = 0;; i0 += 4) {
-    double2 v[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) v[q] = e[i0 + q];
-    bool stop = false;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      if (!stop) {
-        if (nu < v[q].x) {
-          stop = true;
-        } else {
-          hi = i0 + q + 1;
-          if (nu > v[q].y) lo = i0 + q + 1;
-        }
-      }
-    }
-    if (stop) break;
+  const int nb = K.T.nbf;
+  // hi: the first continuum with nu < nu_edge (nb if none); lo: the first with nu <= nu_max, at most hi
+  int h = 0, l = 0;
+  for (int step = nb > 0 ? 1 << (31 - __clz(nb)) : 0; step > 0; step >>= 1) {
+    if (h + step <= nb && !(nu < e[h + step - 1].x)) h += step;
+    if (l + step <= nb && nu > e[l + step - 1].y) l += step;
   }
+  hi = h;
+  lo = min(l, h);
 }
 // rpkt.cc:1075-1207 calculate_kappa_bf_gammacontr: the kappa_bf total (the cumulative array is re-scanned on demand)
 DEVFN double kappa_bf_total(Tx &x, int k, int mgi, double nu) {
@@ -1039,6 +1096,12 @@ DEVFN void wave_flush_estimators(Tx &x) {
   x.est_mgi = -1;
 }
 
+DEVFN double readlane_d(double v, int l) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 // ---- the continuum sums of a step made by the whole wave (k_rpkt, models with many bf continua per frequency) ----
 // Every lane contributes n consecutive items (its continua); the wave's items are laid out lane after lane
 // (exclusive prefix `pref` over the lanes), and each pass over them gives every lane one item -- so a wave spends
@@ -1064,10 +1127,13 @@ DEVFN int wave_item_owner(const int *s_pref, int j) {
 DEVFN const double2 *shfl_ptr(const double2 *p, int src) {
   return (const double2 *)__shfl((long long)p, src, 64);
 }
+// The wave's item loops take COOP_UNR items per lane per trip (bf_contribution_batch: their table loads in flight
+// together); the LDS slots coop_d hold 64 * COOP_UNR terms per wave.
+#define COOP_UNR 4
 // calculate_kappa_bf_gammacontr's kappa_bf sum (rpkt.cc:1075-1207) of every lane with `want` (cell k / mgi,
-// frequency nu): the terms n_level * gamma_contr are evaluated by the wave 64 at a time into the LDS slots s_d, and
-// each lane adds its own terms in continuum order -- the reference's sum, term for term.  *hi: the continua the
-// reference's loop visits (the work counter).
+// frequency nu): the terms n_level * gamma_contr are evaluated by the wave 64 * COOP_UNR at a time into the LDS slots
+// s_d, and each lane adds its own terms in continuum order -- the reference's sum, term for term.  *hi: the continua
+// the reference's loop visits (the work counter).
 DEVFN double wave_kappa_bf(Tx &x, bool want, int k, int mgi, double nu, int &hi_out) {
   const Ctx &K = x.K;
   double *s_d = x.coop_d;
@@ -1084,28 +1150,34 @@ DEVFN double wave_kappa_bf(Tx &x, bool want, int k, int mgi, double nu, int &hi_
   const BfCell cell = want ? bf_cell(K, k, mgi, nu) : BfCell{K.C.bfcell, 0.};
   s_i[lane] = pref;
   __builtin_amdgcn_wave_barrier();
-  for (int c0 = 0; c0 < total; c0 += 64) {
-    const int j = min(c0 + lane, total - 1);
-    const int o = wave_item_owner(s_i, j);
-    const int lo_o = __shfl(lo, o, 64), pref_o = __shfl(pref, o, 64);
-    const double nu_o = __shfl(nu, o, 64), ef_o = __shfl(cell.expfac, o, 64);
-    const double2 *row_o = shfl_ptr(cell.row, o);
-    double term = 0.;
-    if (c0 + lane < total) {
-      double nn, gc;
-      if (bf_contribution(K, BfCell{row_o, ef_o}, lo_o + (j - pref_o), nu_o, &nn, &gc)) term = nn * gc;
+  constexpr int U = COOP_UNR;
+  for (int c0 = 0; c0 < total; c0 += 64 * U) {
+    BfCell cl[U];
+    int ci[U];
+    double nuu[U], nn[U], gc[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int j = min(c0 + u * 64 + lane, total - 1);
+      const int o = wave_item_owner(s_i, j);
+      ci[u] = __shfl(lo, o, 64) + (j - __shfl(pref, o, 64));
+      nuu[u] = __shfl(nu, o, 64);
+      cl[u] = BfCell{shfl_ptr(cell.row, o), __shfl(cell.expfac, o, 64)};
     }
-    s_d[lane] = term;
+    bf_contribution_batch<U>(K, cl, ci, nuu, ok, nn, gc);
+#pragma unroll
+    for (int u = 0; u < U; u++) s_d[u * 64 + lane] = (c0 + u * 64 + lane < total && ok[u]) ? nn[u] * gc[u] : 0.;
     __builtin_amdgcn_wave_barrier();
-    const int a = max(pref, c0), b = min(pref + n, c0 + 64);
+    const int a = max(pref, c0), b = min(pref + n, c0 + 64 * U);
     for (int jj = a; jj < b; jj++) sum += s_d[jj - c0];
     __builtin_amdgcn_wave_barrier();
   }
   return sum;
 }
 // update_bfestimators (radfield.cc:764-829) of the step, deferred by update_estimators (Tx::defer_bf): the window
-// [max(lo(nu), lo(kap.nu)), hi(nu)) of every pending lane, gamma_contr at kap.nu, made by the wave 64 continua at a
-// time; each term is added to the estimator on its own (the additions are atomics, in no order, as per lane).
+// [max(lo(nu), lo(kap.nu)), hi(nu)) of every pending lane, gamma_contr at kap.nu, made by the wave 64 * COOP_UNR
+// continua at a time; each term is added to the estimator on its own (the additions are atomics, in no order, as
+// per lane).
 DEVFN void wave_bf_estimators(Tx &x) {
   const Ctx &K = x.K;
   const int lane = (int)__lane_id();
@@ -1127,26 +1199,116 @@ DEVFN void wave_bf_estimators(Tx &x) {
   __builtin_amdgcn_wave_barrier();
   const int nbf = K.T.nbf;
   const bool lds = x.est_lds && K.C.est_lds_bf >= 0;
-  for (int c0 = 0; c0 < total; c0 += 64) {
-    const int j = min(c0 + lane, total - 1);
-    const int o = wave_item_owner(x.coop_i, j);
-    const int start_o = __shfl(start, o, 64), pref_o = __shfl(pref, o, 64);
-    const int k_o = __shfl(x.bf_k, o, 64), mgi_o = __shfl(x.bf_mgi, o, 64);
-    const double kapnu_o = __shfl(x.bf_kapnu, o, 64), ef_o = __shfl(cell.expfac, o, 64);
-    const double d_o = __shfl(x.bf_d, o, 64);
-    const double2 *row_o = shfl_ptr(cell.row, o);
-    if (c0 + lane < total) {
-      const int i = start_o + (j - pref_o);
-      double nn, gc;
-      if (!(kapnu_o < K.T.allcont_nu_edge[i]) && bf_contribution(K, BfCell{row_o, ef_o}, i, kapnu_o, &nn, &gc)) {
+  constexpr int U = COOP_UNR;
+  for (int c0 = 0; c0 < total; c0 += 64 * U) {
+    BfCell cl[U];
+    int ci[U], ko[U], mo[U];
+    double nuu[U], nn[U], gc[U], dd[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int j = min(c0 + u * 64 + lane, total - 1);
+      const int o = wave_item_owner(x.coop_i, j);
+      ci[u] = __shfl(start, o, 64) + (j - __shfl(pref, o, 64));
+      ko[u] = __shfl(x.bf_k, o, 64);
+      mo[u] = __shfl(x.bf_mgi, o, 64);
+      nuu[u] = __shfl(x.bf_kapnu, o, 64);
+      dd[u] = __shfl(x.bf_d, o, 64);
+      cl[u] = BfCell{shfl_ptr(cell.row, o), __shfl(cell.expfac, o, 64)};
+    }
+    bf_contribution_batch<U>(K, cl, ci, nuu, ok, nn, gc);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      // (the window's lower edges: the continua below kap.nu's, nu <= nu_edge excluded as update_bfestimators does)
+      if (c0 + u * 64 + lane < total && ok[u] && !(nuu[u] < K.T.allcont_nu_edge[ci[u]])) {
         if (lds)
-          atomicAdd(&x.est_lds[K.C.est_lds_bf + (int64_t)k_o * nbf + i], gc * d_o);
+          atomicAdd(&x.est_lds[K.C.est_lds_bf + (int64_t)ko[u] * nbf + ci[u]], gc[u] * dd[u]);
         else
-          safeadd(&K.E.bfrate[(int64_t)mgi_o * nbf + i], gc * d_o);
+          safeadd(&K.E.bfrate[(int64_t)mo[u] * nbf + ci[u]], gc[u] * dd[u]);
       }
     }
   }
   __builtin_amdgcn_wave_barrier();
+}
+// rpkt.cc:370-447, the continuum selection of a bound-free absorption (rpkt_event_continuum, deferred with
+// Tx::defer_sel), then the rest of that event.  For each pending lane in turn the wave evaluates the terms
+// n_level * gamma_contr 64 * COOP_UNR at a time into LDS, and every lane runs the reference's running sum over them
+// in order (the first continuum at which it reaches the draw; the last one if none): the reference's linear search,
+// term for term.  Wave-uniform.
+DEVFN void wave_bf_select(Tx &x, Pkt &p, uint64_t *__restrict__ soa, int64_t n, int64_t idx) {
+  const Ctx &K = x.K;
+  unsigned long long m = __ballot(x.sel_pend);
+  if (!m) return;
+  const int lane = (int)__lane_id();
+  const int last = K.T.nbf - 1;
+  constexpr int U = COOP_UNR;
+  int sel = last;
+  for (; m; m &= m - 1) {
+    const int o = __ffsll((long long)m) - 1;
+    const int k = __builtin_amdgcn_readlane(x.sel_k, o), mgi = __builtin_amdgcn_readlane(x.sel_mgi, o);
+    const double nu = readlane_d(x.sel_nu, o), rnd = readlane_d(x.sel_rand, o);
+    int found = last;
+    double running = 0.;
+    if (!(running < rnd)) {
+      found = 0;
+    } else {
+      int lo, hi;
+      bf_range(K, nu, lo, hi);
+      const int end = min(hi, last);
+      const BfCell cell = bf_cell(K, k, mgi, nu);
+      bool done = false;
+      for (int c0 = lo; c0 < end && !done; c0 += 64 * U) {
+        BfCell cl[U];
+        int ci[U];
+        double nuu[U], nn[U], gc[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          ci[u] = min(c0 + u * 64 + lane, end - 1);
+          nuu[u] = nu;
+          cl[u] = cell;
+        }
+        bf_contribution_batch<U>(K, cl, ci, nuu, ok, nn, gc);
+#pragma unroll
+        for (int u = 0; u < U; u++) x.coop_d[u * 64 + lane] = (c0 + u * 64 + lane < end && ok[u]) ? nn[u] * gc[u] : 0.;
+        __builtin_amdgcn_wave_barrier();
+        const int cend = min(end, c0 + 64 * U);
+        for (int i = c0; i < cend; i++) {
+          running += x.coop_d[i - c0];
+          if (!(running < rnd)) {
+            found = i;
+            done = true;
+            break;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    if (lane == o) sel = found;
+  }
+  if (x.sel_pend) {
+    x.sel_pend = false;
+    const int element = K.T.allcont_element[sel];
+    const int ion = K.T.allcont_ion[sel];
+    const double zrand3 = artis_rng_uniform(&x.rng);
+    if (zrand3 < K.T.allcont_nu_edge[sel] / p.nu_cmf) {
+      lctr(x.L, CTR_MA_STAT_ACTIVATION_BF);
+      p.interactions += 1;
+      p.last_event = 3;
+      p.type = ARTIS_TYPE_MA;
+      p.ma_element = element;
+      p.ma_ion = ion + 1;
+      p.ma_level = get_phixsupperlevel(K, element, ion, K.T.allcont_level[sel], K.T.allcont_target[sel]);
+      p.ma_activatingline = -99;
+      soa[PW(n, idx, 36)] = pack2(p.ma_element, p.ma_ion);  // (the record's macro-atom state, cold words)
+      soa[PW(n, idx, 37)] = pack2(p.ma_level, p.ma_activatingline);
+    } else {
+      lctr(x.L, CTR_K_STAT_FROM_BF);
+      p.interactions += 1;
+      p.last_event = 4;
+      p.type = ARTIS_TYPE_KPKT;
+    }
+  }
 }
 
 // the block's LDS estimator accumulator: zeroed at the start of k_rpkt, added to the estimators at its end (one
@@ -1282,6 +1444,14 @@ DEVNI void rpkt_event_continuum(Tx &x, Pkt &p, const Kappa &kap, int k, int mgi)
     const double kappa_bf_inrest = kap.bf;
     const double zrand2 = artis_rng_uniform(&x.rng);
     const double kappa_bf_rand = zrand2 * kappa_bf_inrest;
+    if (x.defer_sel) {  // (k_rpkt, detailed-bf models: the selection and the rest of the event by the wave)
+      x.sel_pend = true;
+      x.sel_k = k;
+      x.sel_mgi = mgi;
+      x.sel_nu = kap.nu;
+      x.sel_rand = kappa_bf_rand;
+      return;
+    }
     // lower_bound over kappa_bf_sum[0, nbf-1): re-scan the running sum of calculate_kappa_bf_gammacontr at the
     // frequency the opacity was computed at
     const int last = K.T.nbf - 1;
@@ -1565,12 +1735,6 @@ DEVNI double select_continuum_nu(Tx &x, int e, int lowerion, int lower, int uppe
   return select_continuum_nu_z(x.K, e, lowerion, lower, upperionlevel, T_e, zrand);
 }
 
-DEVFN double readlane_d(double v, int l) {
-  const uint64_t u = (uint64_t)__double_as_longlong(v);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
-  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
 // select_continuum_nu's integral for every lane of the wave that asks for one (want; every lane of the wave calls
 // this, convergent): the lanes evaluate the requesting lane's npieces quadrature pieces in parallel (pieces q,
 // q + 64, ...; the same alpha_sp_piece values as the serial loops), and the two running sums are then added in the

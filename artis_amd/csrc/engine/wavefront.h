@@ -219,14 +219,15 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
     x.est_lds = s_est;
   }
   // models with many bf continua per frequency (detailed bf estimators: the nebular options): the step's continuum
-  // sums are made by the whole wave (transport.h wave_kappa_bf / wave_bf_estimators)
-  __shared__ double s_coopd[COOP ? WAVE_BLOCK : 1];
+  // sums are made by the whole wave (transport.h wave_kappa_bf / wave_bf_estimators / wave_bf_select)
+  __shared__ double s_coopd[COOP ? WAVE_BLOCK * COOP_UNR : 1];
   __shared__ int s_coopi[COOP ? WAVE_BLOCK : 1];
   const bool coop = COOP && K.R.detailed_bf && K.T.nbf > 0 && K.R.do_r_lc;
   if (coop) {
-    x.coop_d = &s_coopd[threadIdx.x & ~63];
+    x.coop_d = &s_coopd[(threadIdx.x & ~63) * COOP_UNR];
     x.coop_i = &s_coopi[threadIdx.x & ~63];
     x.defer_bf = true;
+    x.defer_sel = true;
   }
   const int npm = K.G.npts_model;
   const uint32_t nq = W.ctr[2 * QR];
@@ -325,6 +326,18 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
         STAMP(x, 4);
         if (++steps > RPKT_MAX_STEPS) x.err(ERR_STUCK, p.number, 1);
       }
+    }
+    // a bound-free absorption of this step: its continuum selection and the rest of the event, by the wave
+    if (coop) {
+#ifdef ARTIS_STAMPS
+      const unsigned long long tb0 = wave_clock();
+#endif
+      wave_bf_select(x, p, soa, n, idx);
+#ifdef ARTIS_STAMPS
+      x.st[5] += wave_clock() - tb0;
+#endif
+    }
+    if (have) {
       if (walking) {
         // (the step continues next pass)
       } else if (x.vstop && x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
