@@ -327,9 +327,13 @@ __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict_
   const int kr = (int)(idx % knp);
   if (ul >= ul0 + nlev || kr >= kn) return;
   const int k = cells[kr];
-  double *rec = cache ? S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * kn + kr : nullptr;
+  // the scratch of level ul: 64-row groups, each [position][64 rows] (a wave's stores, and k_mapack's tile, are
+  // contiguous runs of memory)
+  const int64_t len = K.T.ma_dbl_off[ul + 1] - K.T.ma_dbl_off[ul];
+  double *rec = cache ? S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * knp + (int64_t)(kr >> 6) * len * 64 + (kr & 63)
+                      : nullptr;
   double pr[ARTIS_MA_ACTION_COUNT];
-  marates_sums(K, ul, k, K.G.ts_mid[nts], rec, kn, cache, pr);
+  marates_sums(K, ul, k, K.G.ts_mid[nts], rec, 64, cache, pr);
   if (!cache) {
     double *out = K.C.marates + ((int64_t)k * nl + ul) * ARTIS_MA_ACTION_COUNT;
     for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) out[a] = pr[a];
@@ -401,13 +405,21 @@ DEVFN void mapack_tile(const Ctx &K, int ul, const double *__restrict__ src, int
   }
 }
 
-// one k_marates batch's scratch -> key records: block = (level ul0 + blockIdx.y, 64 rows)
-__global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, const double *__restrict__ S) {
+// one k_marates batch's scratch -> key records: tiles (level ul0 + t / ngroups, 64-row group t % ngroups), a block
+// taking tiles grid-stride (a few blocks per CU over many short tiles: dispatching one block per tile cost as much as
+// the tiles' work)
+__global__ __launch_bounds__(256) void k_mapack(Ctx K, int ul0, int nlev, const double *__restrict__ S) {
   __shared__ MapackLds L;
-  const int ul = ul0 + blockIdx.y;
-  const int64_t n_ne = K.C.ma_rows;  // the cached cells, the scratch's stride
-  mapack_tile(K, ul, S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * n_ne, n_ne, (int64_t)blockIdx.x * 64, n_ne, 0,
-              L);
+  const int64_t n_ne = K.C.ma_rows;  // the cached cells
+  const int64_t ngroups = (n_ne + 63) / 64;
+  for (int64_t t = blockIdx.x; t < ngroups * nlev; t += gridDim.x) {
+    const int ul = ul0 + (int)(t / ngroups);
+    const int64_t g = t % ngroups;
+    const int64_t len = K.T.ma_dbl_off[ul + 1] - K.T.ma_dbl_off[ul];
+    // (the level's scratch: 64-row groups [position][64 rows], k_marates)
+    const double *src = S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * MARATES_PAD(n_ne) + g * len * 64;
+    mapack_tile(K, ul, src, 64, 0, min((int64_t)64, n_ne - g * 64), g * 64, L);
+  }
 }
 
 // ---- level mode of the macro-atom key records (DevCells::ma_lptr): placement and build ----------------------
@@ -608,6 +620,8 @@ __global__ __launch_bounds__(256) void k_linecoef(Ctx K) {
       v = (r.B_lu * n_l - r.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI;
     }
     K.C.linecoef[(int64_t)k * K.C.linecoef_stride + li] = v;
+    // (one atomic per wave until the flag is seen set: an atomic per wave on one address serialises the launch)
+    if (__any(v < 0.) && __lane_id() == 0 && !*(volatile int32_t *)K.C.linecoef_neg) atomicOr(K.C.linecoef_neg, 1);
   }
 }
 
@@ -1637,13 +1651,12 @@ int artis_gpu_solve_temperatures(const artis_te_tables *tab, const artis_te_para
     const int64_t nw = (int64_t)D.nhb * D.ncells;
     k_te_bfheat<<<(unsigned)((nw + 255) / 256), 256, 0, G.stream>>>(G.K, D);
   }
-  // lanes per cell: enough for the per-ion collisional-excitation sums of the cooling rate (te_cooling_rates);
-  // ARTIS_GPU_TE_LANES overrides (1 = one cell per lane)
-  int g = 1;
-  while (g < ni && g < 64) g *= 2;
+  // lanes per cell: one per ion for the per-ion collisional-excitation sums of the cooling rate (te_cooling_rates),
+  // floor(64 / g) cells per wave (12 ions: 5 cells on 60 lanes); ARTIS_GPU_TE_LANES overrides (1 = one cell per lane)
+  int g = te_lanes_per_cell(ni);
   if (const char *ev = getenv("ARTIS_GPU_TE_LANES")) {
     const int v = atoi(ev);
-    if (v >= 1 && v <= 64 && (v & (v - 1)) == 0) g = v;
+    if (v >= 1 && v <= 64) g = v;
   }
   const int cpw = 64 / g;
   Ctx *dK = nullptr;
@@ -2088,8 +2101,7 @@ int artis_gpu_update_grid_nlte(const artis_nt_shells *nt, const artis_nlte_param
   TeDev *dD = nullptr;
   NlDev *dN = nullptr;
   if (B.get(&dK, 1, &KN) || B.get(&dD, 1, (const TeDev *)nullptr) || B.get(&dN, 1, &N)) return ARTIS_ERR_HIP;
-  int g = 1;
-  while (g < ni && g < 64) g *= 2;
+  const int g = te_lanes_per_cell(ni);
   const int cpw = 64 / g;
   auto te_launch = [&](const int32_t *list, int n, int mode, const int32_t *hbk) -> int {
     if (n <= 0) return 0;
@@ -3517,7 +3529,8 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     for (int ul = 0; ul < nl; ul++) maxlev = std::max(maxlev, G.h_dbl_off[ul + 1] - G.h_dbl_off[ul]);
     int64_t cap = ((int64_t)2 << 30) / 8;  // k_marates scratch of row mode (ARTIS_GPU_MAREC_SCRATCH_MB)
     if (const char *sm = getenv("ARTIS_GPU_MAREC_SCRATCH_MB")) cap = (int64_t)(atof(sm) * (1 << 20) / 8);
-    const int64_t scratch = std::max<int64_t>(maxlev * nne_cells, std::min<int64_t>(G.h_dbl_off[nl] * nne_cells, cap));
+    const int64_t scratch = std::max<int64_t>(maxlev * MARATES_PAD(nne_cells),
+                                              std::min<int64_t>(G.h_dbl_off[nl] * MARATES_PAD(nne_cells), cap));
     double budget = 0.5 * (double)freeb;
     if (const char *mx = getenv("ARTIS_GPU_MACACHE_MAX_GB")) budget = atof(mx) * (double)(1ull << 30);
     const char *mr = getenv("ARTIS_GPU_MACACHE_ROWS");
@@ -3627,6 +3640,9 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
       }
     }
   }
+  C.linecoef_neg = nullptr;
+  rc |= dalloc(&C.linecoef_neg, (size_t)1);
+  if (C.linecoef_neg) HIPCHK(hipMemset(C.linecoef_neg, 0, sizeof(int32_t)));
   // cell-state input buffers
   rc |= dalloc(&G.W.ctr, (size_t)NQUEUES * 2);
   rc |= dalloc(&G.d_ctx, (size_t)1);
@@ -3830,6 +3846,7 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
     if (ntg > 0)
       k_transpose<<<dim3((unsigned)((ntg + 63) / 64), (unsigned)((n_ne + 63) / 64)), 256, 0, G.stream>>>(
           G.K.C.corrphot, G.K.C.corrphotT, n_ne, ntg);
+    if (G.K.C.linecoef) HIPCHK(hipMemsetAsync(G.K.C.linecoef_neg, 0, sizeof(int32_t), G.stream));
     if (G.K.C.linecoef)
       k_linecoef<<<dim3((unsigned)((G.K.C.linecoef_stride + 255) / 256),
                         (unsigned)std::min(G.K.C.linecoef_rows, 32768)), 256, 0,
@@ -3845,12 +3862,14 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
       // batches of levels whose records fit the scratch
       for (int ul0 = 0; ul0 < nl;) {
         int ul1 = ul0 + 1;
-        while (ul1 < nl && (G.h_dbl_off[ul1 + 1] - G.h_dbl_off[ul0]) * mr <= G.marec_scratch_doubles) ul1++;
+        while (ul1 < nl && (G.h_dbl_off[ul1 + 1] - G.h_dbl_off[ul0]) * MARATES_PAD(mr) <= G.marec_scratch_doubles) ul1++;
         const int nlev = ul1 - ul0;
         k_marates<<<(unsigned)((MARATES_PAD(mr) * nlev + 255) / 256), 256, 0, G.stream>>>(
             G.K, nts, ul0, nlev, G.d_marec_scratch, G.d_ma_bincell, mr, true);
-        k_mapack<<<dim3((unsigned)((mr + 63) / 64), (unsigned)nlev), 256, 0, G.stream>>>(G.K, ul0,
-                                                                                         G.d_marec_scratch);
+        // (4 blocks per CU: what its LDS lets be resident at once)
+        const int64_t tiles = (int64_t)(mr + 63) / 64 * nlev;
+        k_mapack<<<(unsigned)std::min<int64_t>(tiles, (int64_t)G.ncu * 4), 256, 0, G.stream>>>(G.K, ul0, nlev,
+                                                                                            G.d_marec_scratch);
         ul0 = ul1;
       }
     }
@@ -3861,6 +3880,11 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, G.ev0, G.ev1));
   G.last_precompute_ms = ms;
+  {
+    int32_t neg = 0;
+    if (G.K.C.linecoef) HIPCHK(hipMemcpy(&neg, G.K.C.linecoef_neg, sizeof(int32_t), hipMemcpyDeviceToHost));
+    G.K.V.neg_coef = neg;
+  }
   G.have_cells = true;
   G.cellstate_nts = nts;
   return 0;

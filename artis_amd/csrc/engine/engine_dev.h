@@ -224,6 +224,7 @@ struct DevCells {
   double *linecoef;    // [linecoef_rows * linecoef_stride]
   int64_t linecoef_stride;
   int32_t linecoef_rows;
+  int32_t *linecoef_neg;  // [1]: k_linecoef found a negative coefficient (a population inversion) in some row
   // macro-atom cache: per (cell, level) one compact record of 32-bit keys, 128-byte aligned.  A key is a running
   // sum of the reference's individual rates (the cellhistory individ_* arrays, globals.h:174-183, summed in the
   // reference's order, macroatom.cc:57-159) divided by its action's total and rounded to 32 bits; the first 9 are
@@ -328,6 +329,9 @@ struct DevVpkt {
   uint32_t *ovf_ctr;        // [1]
   uint32_t *full;           // [1]
   uint32_t ovf_cap;
+  // the coefficient table has a negative entry (DevCells::linecoef_neg, read back after the precompute): only then
+  // can a virtual packet's tau fall along a line walk over it (vpkt_trace_segment's per-line check)
+  int32_t neg_coef;
 };
 
 struct DevRun {

@@ -689,7 +689,10 @@ __global__ void k_te_bfheat(Ctx K, TeDev D) {
   D.hbc[(int64_t)j * D.ncells + k] = bfheatingcoeff;
 }
 
-// one wave = 64 / g cells, g lanes each (g a power of two); every lane of a group runs its cell's solution
+// lanes per cell of k_te_solve: one per ion (the per-ion sums of te_cooling_rates / te_heating_rates), at most 64
+static inline int te_lanes_per_cell(int nions) { return nions < 1 ? 1 : (nions > 64 ? 64 : nions); }
+// one wave = floor(64 / g) cells, g lanes each (the last 64 mod g lanes idle); every lane of a group runs its cell's
+// solution
 __global__ __launch_bounds__(64, 4) void k_te_solve(const Ctx *__restrict__ Kp, const TeDev *__restrict__ Dp, int g) {
   // context and parameters by device pointer, copied into LDS: the solver's functions are not inlined (register
   // pressure), and a by-value kernel argument referenced from them would be copied to scratch; read through the
@@ -702,13 +705,14 @@ __global__ __launch_bounds__(64, 4) void k_te_solve(const Ctx *__restrict__ Kp, 
   __syncthreads();
   const TeDev &D = s_dev;
   const int lane = threadIdx.x;
+  if (lane / g >= 64 / g) return;  // (lanes past the last whole group)
   const int k = blockIdx.x * (64 / g) + lane / g;
   if (k >= D.ncells) return;  // whole groups leave together
   TeState s;
   s.k = k;
   s.g = g;
-  s.sub = lane & (g - 1);
-  s.lane0 = lane & ~(g - 1);
+  s.sub = lane % g;
+  s.lane0 = lane - s.sub;
   extern __shared__ double te_lds[];
   s.phi = te_lds + (lane / g) * K.T.nions_total;
   s.mgi = D.mgi[k];

@@ -417,6 +417,7 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
     uint64_t wm = v.wm;
     int budget = VPKT_LINES_PER_PASS;
     bool done = false;
+    const bool negc = __builtin_amdgcn_readfirstlane(V.neg_coef) != 0;  // (wave-uniform: a scalar branch per line)
 #ifdef ARTIS_DIAG_VPKT_NOLINES  // timing diagnostic only (no line opacity): the cost of the line walk
     ldist = sdist;
 #endif
@@ -458,8 +459,9 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
       const double t_line = t_current + ldist / ARTIS_CLIGHT;
       const double dtau = win[(LC_WIN + pj) * WAVE_BLOCK_T] * t_line;
       // a population inversion (NLTE) gives a negative coefficient: the only way a tau can fall again, so a
-      // virtual packet that died at an earlier line of the window is killed here, before it could revive
-      if (dtau < 0. && all_dead()) {
+      // virtual packet that died at an earlier line of the window is killed here, before it could revive (tables
+      // without a negative coefficient skip the test)
+      if (negc && dtau < 0. && all_dead()) {
         v.inlines = false;
         return VSEG_KILLED;
       }

@@ -1122,7 +1122,10 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
 // copy (~400 B per lane written and read back once per macro-atom cycle) was most of the kernel's write traffic.
 // With virtual packets the slots are taken from the fetch head and a full spawn buffer stops the launch (each lane
 // spawns at most once, so the overflow records cover the lanes in flight), as in k_kpkt.
-__global__ __launch_bounds__(WAVE_BLOCK) void k_ma_finish(const Ctx *__restrict__ ctxp, WaveState W,
+#ifndef MA_FINISH_MINW
+#define MA_FINISH_MINW 1  // waves per SIMD k_ma_finish is compiled for
+#endif
+__global__ __launch_bounds__(WAVE_BLOCK, MA_FINISH_MINW) void k_ma_finish(const Ctx *__restrict__ ctxp, WaveState W,
                                                           uint64_t *__restrict__ soa, int64_t n, int nts, double t2) {
   CTX_IN_LDS(ctxp)
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];

@@ -910,6 +910,36 @@ double col_exc_over_nne(const Model &m, float T_e, int li, double epsilon_trans,
   return C;
 }
 
+// Fe-group fraction stand-in (the 56Ni-rich core of a W7-like model) and the grey opacity of opacity_case 4
+// style kappagrey = GREY_OP (0.9 ffegrp + 0.1) (grid.cc:629); a cell is thick when its grey optical depth
+// across one cell width exceeds thick_tau (input.txt cell_is_optically_thick).  rho: the density at time t (m.rho[mgi]
+// holds it rounded to float).
+static void cell_grey(Model &m, int nts, double t, int mgi, double rho) {
+  m.thick[mgi] = 0;
+  if (m.from_files) {
+    // model.txt X_Fegroup; calculate_kappagrey opacity_case 4 (grid.cc:670-673); the grey-depth thick-cell
+    // rule of update_grid_cell (update_grid.cc:1162-1197, 1209-1212)
+    m.ffegrp[mgi] = (float)m.mgi_ffegrp[mgi];
+    m.kappagrey[mgi] = (float)(((0.9 * m.mgi_ffegrp[mgi]) + 0.1) * ARTIS_GREY_OP / m.kappagrey_norm);
+    const double tratmid = t / m.tmin;
+    if (m.inp.opacity_case == 4) {
+      const double radial_pos = m.mgi_rpos[mgi] * tratmid;
+      const double grey_optical_depth = (double)m.kappagrey[mgi] * (double)m.rho[mgi] * (m.rmax * tratmid - radial_pos);
+      if (grey_optical_depth > m.inp.cell_is_optically_thick && nts < m.inp.num_grey_timesteps) m.thick[mgi] = 1;
+    } else {
+      m.thick[mgi] = 1;
+    }
+  } else {
+    const double v = m.mgi_vel[mgi];
+    m.ffegrp[mgi] = (float)(0.2 + 0.6 * exp(-(v / 6e8) * (v / 6e8)));
+    m.kappagrey[mgi] = (float)(0.1 * (0.9 * m.ffegrp[mgi] + 0.1));
+    if (m.cfg.thick_tau > 0) {
+      const double wid_t = 2 * m.geom.coordmax[0] / m.cfg.ngrid_1d * t / m.tmin;
+      if (m.kappagrey[mgi] * rho * wid_t > m.cfg.thick_tau) m.thick[mgi] = 1;
+    }
+  }
+}
+
 void compute_cellstate(Model &m, int nts) {
   const double t = m.ts_mid[nts];
   const int np = m.npts_model;
@@ -1025,31 +1055,7 @@ void compute_cellstate(Model &m, int nts) {
     ionfracs(nne_sol);
     m.nne[mgi] = (float)nne_sol;
     m.nnetot[mgi] = (float)nnetot;
-    // Fe-group fraction stand-in (the 56Ni-rich core of a W7-like model) and the grey opacity of opacity_case 4
-    // style kappagrey = GREY_OP (0.9 ffegrp + 0.1) (grid.cc:629); a cell is thick when its grey optical depth
-    // across one cell width exceeds thick_tau (input.txt cell_is_optically_thick)
-    if (m.from_files) {
-      // model.txt X_Fegroup; calculate_kappagrey opacity_case 4 (grid.cc:670-673); the grey-depth thick-cell
-      // rule of update_grid_cell (update_grid.cc:1162-1197, 1209-1212)
-      m.ffegrp[mgi] = (float)m.mgi_ffegrp[mgi];
-      m.kappagrey[mgi] = (float)(((0.9 * m.mgi_ffegrp[mgi]) + 0.1) * ARTIS_GREY_OP / m.kappagrey_norm);
-      const double tratmid = t / m.tmin;
-      if (m.inp.opacity_case == 4) {
-        const double radial_pos = m.mgi_rpos[mgi] * tratmid;
-        const double grey_optical_depth = (double)m.kappagrey[mgi] * (double)m.rho[mgi] * (m.rmax * tratmid - radial_pos);
-        if (grey_optical_depth > m.inp.cell_is_optically_thick && nts < m.inp.num_grey_timesteps) m.thick[mgi] = 1;
-      } else {
-        m.thick[mgi] = 1;
-      }
-    } else {
-      const double v = m.mgi_vel[mgi];
-      m.ffegrp[mgi] = (float)(0.2 + 0.6 * exp(-(v / 6e8) * (v / 6e8)));
-      m.kappagrey[mgi] = (float)(0.1 * (0.9 * m.ffegrp[mgi] + 0.1));
-      if (m.cfg.thick_tau > 0) {
-        const double wid_t = 2 * m.geom.coordmax[0] / m.cfg.ngrid_1d * t / m.tmin;
-        if (m.kappagrey[mgi] * rho * wid_t > m.cfg.thick_tau) m.thick[mgi] = 1;
-      }
-    }
+    cell_grey(m, nts, t, mgi, rho);
     for (int e = 0; e < ne; e++) {
       const int u0 = m.elem_uniqueionoffset[e];
       for (int ion = 0; ion < m.elem_nions[e]; ion++) {
@@ -1637,6 +1643,24 @@ int artis_model_set_timestep(artis_model *m, int nts) {
   if (nts < 0 || nts >= m->cfg.ntstep) return ARTIS_ERR_BAD_ARGUMENT;
   compute_cellstate(*m, nts);
   return model_is_finite(*m) ? 0 : ARTIS_ERR_BAD_ARGUMENT;
+}
+
+// The part of the cell state update_grid does not solve for, at timestep nts: the density rho(t) (the t^-3 expansion
+// of grid.cc), the grey opacity and the thick-cell flag; temperatures, populations and cooling are left as they are
+// (the timestep loop's update_grid writes them from its solution).  The abundances of the synthetic models do not
+// change with time.
+int artis_model_advance(artis_model *m, int nts) {
+  if (nts < 0 || nts >= m->cfg.ntstep) return ARTIS_ERR_BAD_ARGUMENT;
+  Model &mm = *m;
+  const double t = mm.ts_mid[nts];
+#pragma omp parallel for schedule(static)
+  for (int mgi = 0; mgi < mm.npts_model; mgi++) {
+    const double rho = mm.mgi_rho_tmin[mgi] * pow(mm.tmin / t, 3);
+    if (!(rho > 0)) continue;
+    mm.rho[mgi] = (float)rho;
+    cell_grey(mm, nts, t, mgi, rho);
+  }
+  return 0;
 }
 
 int artis_model_init_rpackets(const artis_model *m, int nts, int npkts, uint64_t seed, double etot,

@@ -74,6 +74,9 @@ void artis_model_run_params(const artis_model *m, artis_run_params *out);
 
 /* LTE update_grid stand-in for timestep nts (densities scaled to ts_mid[nts]). */
 int artis_model_set_timestep(artis_model *m, int nts);
+// update_grid's host bookkeeping at timestep nts (density, grey opacity, thick flag); the rest of the cell state is
+// left as it is
+int artis_model_advance(artis_model *m, int nts);
 
 /* Initial r-packets at the start of timestep nts: cell ~ rho*vol, isotropic direction, nu_cmf ~ Planck(T_e)
  * within [NU_MIN_R, NU_MAX_R], equal e_cmf (SURVEY.md §8(d) "pure r-packet benchmark"). */

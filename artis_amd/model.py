@@ -32,6 +32,7 @@ def model_lib():
             getattr(lib, fn).restype = C.c_void_p
         lib.artis_model_run_params.argtypes = [C.c_void_p, C.POINTER(ffi.RunParams)]
         lib.artis_model_set_timestep.argtypes = [C.c_void_p, C.c_int]
+        lib.artis_model_advance.argtypes = [C.c_void_p, C.c_int]
         lib.artis_model_init_rpackets.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_uint64, C.c_double, C.c_void_p]
         lib.artis_model_set_gamma_lines.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         lib.artis_model_gamma_spectra.argtypes = [C.c_void_p]
@@ -128,6 +129,14 @@ class Model:
         rc = self._lib.artis_model_set_timestep(self._h, int(nts))
         if rc != 0:
             raise RuntimeError(f"artis_model_set_timestep({nts}) -> {rc}")
+        self.nts = nts
+
+    def advance(self, nts):
+        """update_grid's host bookkeeping for timestep nts (rho(t), grey opacity, thick flag), leaving temperatures,
+        populations and cooling as they are (the timestep loop writes them from the GPU solution)."""
+        rc = self._lib.artis_model_advance(self._h, int(nts))
+        if rc != 0:
+            raise RuntimeError(f"artis_model_advance({nts}) -> {rc}")
         self.nts = nts
 
     def init_rpackets(self, nts, npkts, seed=1, etot=1e45):

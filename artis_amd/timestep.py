@@ -7,9 +7,9 @@ stage on the device: update_grid's estimator preparation and temperature / ionis
 Host work per timestep is what the reference's host does between those calls: the raw estimators come back
 (D2H, a few MB), the solved cell state goes into the model's cell-state arrays, and the per-cell tables are
 uploaded.  Cell quantities the LTE update_grid does not solve for -- the density at the new time, the grey opacity
-and thick-cell flag, the abundances (update_grid.cc:1012-1040: decay abundances, grey depth; host bookkeeping, out
-of scope) -- come from the synthetic model's update_grid stand-in (model_synth.cc compute_cellstate), exactly as
-tests/test_host_driver.py's C++ driver does with ARTIS_DRIVER_TE=1.
+and thick-cell flag (update_grid.cc:1012-1040, 1162-1212: host bookkeeping) -- come from the synthetic model's
+artis_model_advance (model_synth.cc: rho(t) and the grey-depth rule, without recomputing the rest of its synthetic
+cell state); the abundances of the synthetic models do not decay.
 """
 import ctypes as C
 import time
@@ -76,11 +76,14 @@ class LteTimestepLoop:
 
     def update_grid(self, nts, est):
         """update_grid for timestep nts from the raw estimators `est` of timestep nts - 1 (update_grid.cc:1316 pairs
-        them): the stand-in's density / opacity for nts, then the GPU preparation and solution on every non-empty
+        them): the density / opacity for nts (artis_model_advance), then the GPU preparation and solution on every non-empty
         cell; the solved state is written into the model's cell-state arrays.  Returns device milliseconds."""
         m, eng = self.m, self.eng
+        tp = {}
+        t = time.perf_counter()
         prev = {k: v.copy() for k, v in self._cell_arrays().items()}
-        m.set_timestep(nts)  # rho(t), kappagrey, thick, abundances at nts (host bookkeeping stand-in)
+        m.advance(nts)  # rho(t), kappagrey, thick at nts (host bookkeeping)
+        tp["advance"] = (time.perf_counter() - t) * 1e3
         te = ffi.TeArrays(m, t_current=float(self.ts_mid[nts - 1]))  # nts_for_te = nts - 1 (update_grid.cc:804)
         # the previous timestep's solution is the solver's starting state (the reference's modelgrid values)
         for k in ("TR", "W", "TJ", "Te"):
@@ -95,11 +98,16 @@ class LteTimestepLoop:
         ug.gamma, ug.bfheating = est.gamma, est.bfheating
         ug.nne, ug.partfunct = prev["nne"].copy(), prev["partfunct"].copy()
         self.last_inputs = (te.copy(), _copy_arrays(ug))  # for an oracle replay (tests)
-        t = time.perf_counter()
+        t1 = time.perf_counter()
+        tp["inputs"] = (t1 - t) * 1e3 - tp["advance"]
+        t = t1
         eng.prepare_temperatures(te, ug)
+        tp["prepare"] = (time.perf_counter() - t) * 1e3
         te.TR, te.W, te.TJ = ug.TR_out, ug.W_out, ug.TJ_out
         te.ffheating, te.colheating, te.gamma, te.bfheating = ug.ff_out, ug.col_out, ug.gamma_out, ug.bfheating_out
+        t2 = time.perf_counter()
         ms = eng.solve_temperatures(te)
+        tp["solve"] = (time.perf_counter() - t2) * 1e3
         host_ms = (time.perf_counter() - t) * 1e3
         cur = self._cell_arrays()
         g = te.mgi_list
@@ -112,6 +120,8 @@ class LteTimestepLoop:
         cur["cooling_contrib_ion"][rows] = te.cooling_contrib_ion[rows]
         rr = (g[:, None] * nel * mx + np.arange(nel * mx)[None, :]).ravel()
         cur["corrphotoionrenorm"][rr] = ug.renorm_out[rr]
+        tp["writeback"] = (time.perf_counter() - t) * 1e3 - host_ms
+        self.last_parts_ms = tp
         self.solution = te
         return ms, host_ms
 
@@ -139,6 +149,7 @@ class LteTimestepLoop:
                    "nesc": int(est.struct.nesc)}
             if k > 0:
                 te = self.solution
+                rec["update_grid_parts_ms"] = self.last_parts_ms
                 rec["cells_solved"] = int(len(te.mgi_list))
                 rec["Te_mean"] = float(np.mean(te.Te[te.mgi_list]))
             out.append(rec)

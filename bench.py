@@ -414,7 +414,8 @@ def main():
                     help="bring up the N ranks over gloo without a GPU and print them (tests the launcher)")
     ap.add_argument("--baseline-config", default=None,
                     help="only the BASELINE config sub-lines named (comma-separated: w7_100_shells, nebular_onezone, "
-                         "kilonova; level_mode: the 5x-lines atom at min(--packets, 1e6)), at --packets per GPU; prints "
+                         "kilonova; level_mode: the 5x-lines atom at min(--packets, 1e6); timestep_loop: update_grid -> "
+                         "upload_cellstate -> update_packets over three timesteps), at --packets per GPU; prints "
                          "them as one JSON line (for per-config profiles)")
     args = ap.parse_args()
 
@@ -448,9 +449,12 @@ def main():
 
     if args.baseline_config:
         which = tuple(args.baseline_config.split(","))
-        configs = baseline_configs(args.packets, rank, progress, which=tuple(w for w in which if w != "level_mode"))
+        configs = baseline_configs(args.packets, rank, progress,
+                                   which=tuple(w for w in which if w not in ("level_mode", "timestep_loop")))
         if "level_mode" in which:
             configs["level_mode_5x_lines"] = level_mode_workload(rank, progress, P=min(args.packets, 1_000_000))
+        if "timestep_loop" in which:
+            configs["timestep_loop"] = timestep_loop(args.packets, args.nts, 3, rank, progress)
         if rank == 0:
             print(json.dumps({"baseline_configs": configs, "engine_src_sha": engine_src_sha()}), flush=True)
         return
