@@ -507,6 +507,28 @@ DEVFN double te_col_exc(const TeExcItem &it, float T_e, float nne, double lowers
   }
   return C;
 }
+// te_col_exc for lanes on different lines (k_te_solve: a lane per ion): one exp -- of +eoverkt or -eoverkt, the
+// argument the line's branch takes -- and one log for every lane, instead of the three branches' transcendentals
+// executed one after the other by a divergent wave.  The same expressions on the same arguments: the same bits.
+DEVFN double te_col_exc_mixed(const TeExcItem &it, float T_e, float nne, double lowerstatweight) {
+  const double coll_strength = it.coll_str;
+  const double eoverkt = it.epsilon_trans / (ARTIS_KB * T_e);
+  const bool allowed = coll_strength < 0 && !it.forbidden;
+  const double ex = exp(allowed ? eoverkt : -eoverkt);
+  const double lg = log(eoverkt);
+  double C;
+  if (allowed) {
+    const double g_bar = 0.2;
+    const double test = 0.276 * ex * (-0.5772156649 - lg);
+    const double Gamma = g_bar > test ? g_bar : test;
+    C = ARTIS_C_0 * nne * sqrtf(T_e) * 14.51039491 * it.osc_f * it.P2 * eoverkt / ex * Gamma;
+  } else if (coll_strength < 0) {
+    C = nne * 8.629e-6 * 0.01 * ex * (double)it.upper_sw / sqrtf(T_e);
+  } else {
+    C = nne * 8.629e-6 * coll_strength * ex / lowerstatweight / sqrtf(T_e);
+  }
+  return C;
+}
 // kpkt.cc:41-67 get_cooling_ion_coll_exc for one ion: its own serial sum over levels and up-transitions
 DEVNI double te_coll_exc_ion(const Ctx &K, const TeDev &D, const TeState &s, int ui, float T_e, float nne) {
   const int e = K.T.ion_element[ui];
@@ -523,7 +545,7 @@ DEVNI double te_coll_exc_ion(const Ctx &K, const TeDev &D, const TeState &s, int
 #pragma unroll 2
     for (int ii = 0; ii < nuptrans; ii++) {
       const TeExcItem x = it[ii];
-      const double C = nnlevel * te_col_exc(x, T_e, nne, statweight) * x.epsilon_trans;
+      const double C = nnlevel * te_col_exc_mixed(x, T_e, nne, statweight) * x.epsilon_trans;
       C_exc += C;
     }
   }

@@ -183,17 +183,17 @@ __global__ void k_classify(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *
   block_counters_flush(K, s_ctr, s_work);
 }
 
-// lines of get_event's walk a k_rpkt lane advances per pass; 0: whole steps (do_rpkt_step).  Measured at 2e6
-// packets (profiles/r4_ab.txt): whole steps 164 ms of k_rpkt per step, 16 lines per pass 186 ms, 8 or 32 no better --
-// the state a resumable walk keeps across passes costs more in spills than the divergence it removes
-#ifndef RPKT_LINES_PER_PASS
-#define RPKT_LINES_PER_PASS 0
-#endif
+// WALK: lines of get_event's walk a k_rpkt lane advances per pass (the walk resumes next pass); 0: whole steps
+// (do_rpkt_step).  Which pays depends on the walks: on the bench (3.5 lines per step) whole steps (profiles/r4_ab.txt,
+// 2e6 packets: 164 ms of k_rpkt per step, 16 lines per pass 186 ms -- the state kept across passes spills), on the
+// kilonova inputs (16 lines per step, 122 for a wave's longest lane) the bounded walk (engine.hip launch_rpkt picks
+// it from the previous transport's lines per step).
+#define RPKT_WALK_LINES 16
 
 // r-packets: persistent lanes, one r-packet step (or part of its line walk) per loop pass.  COOP: the instance for
 // models with detailed bf estimators, whose continuum sums are made by the whole wave (wave_kappa_bf,
 // wave_bf_estimators); the others keep the registers of the plain step.
-template <int MINW, bool COOP>
+template <int MINW, bool COOP, int WALK = 0>
 __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa, int64_t n,
                                                      int nts, double t2) {
   CTX_IN_LDS(ctxp)
@@ -303,25 +303,25 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
 #endif
     }
     if (have) {
-      // a step starts when no walk is in progress; get_event's walk advances at most RPKT_LINES_PER_PASS lines per
-      // pass (a lane with a long walk no longer holds its wave while the others' short steps wait)
+      // a step starts when no walk is in progress; with WALK, get_event's walk advances at most WALK lines per pass
+      // (a lane with a long walk no longer holds its wave while the others' short steps wait)
       int r = -1;
-#if RPKT_LINES_PER_PASS > 0
-      if (!walking && !x.vstop && x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
-        r = rpkt_step_begin(x, p, t2, S);
-        walking = (r == RSTEP_WALK);
+      if constexpr (WALK > 0) {
+        if (!walking && !x.vstop && x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
+          r = rpkt_step_begin(x, p, t2, S);
+          walking = (r == RSTEP_WALK);
+        }
+        if (walking && get_event_walk(x, p, S, WALK)) {
+          walking = false;
+          r = x.ok ? RSTEP_END : RSTEP_DONE;
+        }
+        if (r == RSTEP_END) rpkt_step_finish(x, p, t2, S, ColdSoa{soa, n, idx});
+      } else {
+        if (!x.vstop && x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
+          do_rpkt_step(x, p, t2, ColdSoa{soa, n, idx});
+          r = RSTEP_DONE;
+        }
       }
-      if (walking && get_event_walk(x, p, S, RPKT_LINES_PER_PASS)) {
-        walking = false;
-        r = x.ok ? RSTEP_END : RSTEP_DONE;
-      }
-      if (r == RSTEP_END) rpkt_step_finish(x, p, t2, S, ColdSoa{soa, n, idx});
-#else
-      if (!x.vstop && x.ok && p.type == ARTIS_TYPE_RPKT && p.prop_time < t2) {
-        do_rpkt_step(x, p, t2, ColdSoa{soa, n, idx});
-        r = RSTEP_DONE;
-      }
-#endif
       if (r == RSTEP_END || r == RSTEP_DONE) {
         STAMP(x, 4);
         if (++steps > RPKT_MAX_STEPS) x.err(ERR_STUCK, p.number, 1);

@@ -403,3 +403,16 @@ def test_rlc_emiss_rpkt_vs_oracle(small_model, engine_factory, rlc):
     parity.assert_packets_match(pg, po)
     parity.assert_estimators_match(eg, eo)
     assert (eo.rpkt_emiss > 0).sum() > 5
+
+
+@pytest.mark.parametrize("walk", ["1", "0"])
+def test_bounded_line_walk_matches_oracle(shell_model, small_model, engine_factory, monkeypatch, walk):
+    """k_rpkt's bounded line walk (ARTIS_GPU_RPKT_WALK=1: at most RPKT_WALK_LINES lines of get_event's walk per pass,
+    the walk resumed next pass; chosen by default when the previous transport's steps scanned > 8 lines each) and the
+    whole-step instance both give the oracle's histories."""
+    monkeypatch.setenv("ARTIS_GPU_RPKT_WALK", walk)
+    for m, nts, seed in ((shell_model, 6, 61), (small_model, 10, 62)):
+        eng = engine_factory(m)
+        _, pg, eg, po, eo, _ = _pair(m, eng, nts, 3000, seed=seed)
+        parity.assert_packets_match(pg, po)
+        parity.assert_estimators_match(eg, eo)

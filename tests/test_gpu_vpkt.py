@@ -201,3 +201,30 @@ def test_vpkt_general_kernel_matches_oracle(monkeypatch, env):
     parity.assert_estimators_match(eg, eo)
     _compare_vpkt(vg, vo)
     assert vo.counters()["nvpkt"] > 500
+
+
+def test_vpkt_bounded_line_walk_full_buffer(monkeypatch):
+    """The bounded r-packet line walk (ARTIS_GPU_RPKT_WALK=1) with a spawn buffer that fills mid-launch: a packet is
+    parked only between steps, never inside a walk, and the results are the oracle's."""
+    monkeypatch.setenv("ARTIS_GPU_WAVE_GRID", "8")
+    monkeypatch.setenv("ARTIS_GPU_RPKT_WALK", "1")
+    m = Model(**VCFG)
+    m.set_timestep(NTS)
+    pk = m.init_rpackets(NTS, 20000, seed=45)
+    vc = ffi.VpktConfig(nz_obs=(0.3,), phi_obs_deg=(0.0,), spawn_capacity=16)
+    eng = Engine(m)
+    try:
+        eng.vpkt_init(vc)
+        eng.upload_cellstate(NTS)
+        pg = pk.copy()
+        eg = eng.update_packets(NTS, pg)
+        vg = eng.vpkt_download()
+        drains = eng.vpkt_last_drains()
+    finally:
+        eng.close()
+    po = pk.copy()
+    eo, vo, _ = oracle_lib.update_packets_vpkt(m, NTS, po, vc, nthreads=16)
+    parity.assert_packets_match(pg, po)
+    parity.assert_estimators_match(eg, eo)
+    _compare_vpkt(vg, vo)
+    assert drains > 0
