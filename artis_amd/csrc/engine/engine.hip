@@ -1139,7 +1139,10 @@ int vpkt_flush() {
     return !(e && e[0] == '0');
   }();
   const bool lc_only = lc_ok && G.K.C.linecoef && G.K.C.linecoef_rows >= G.K.C.n_nonempty;
-  if (lc_only && occ == 3)
+  // (at most 4 spectra at the default occupancy: the instance whose loops run over 4 spectra, not 8)
+  if (lc_only && occ == 2 && G.K.V.nspectra <= 4)
+    k_vpkt<0, 2, 4><<<(unsigned)G.wave_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, G.W.refill_min);
+  else if (lc_only && occ == 3)
     k_vpkt<0, 3><<<(unsigned)G.wave_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, G.W.refill_min);
   else if (lc_only && occ == 2)
     k_vpkt<0, 2><<<(unsigned)G.wave_grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, G.W.refill_min);

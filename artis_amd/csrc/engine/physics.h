@@ -385,6 +385,31 @@ DEVFN double col_recombination_ratecoeff(const Ctx &K, int mgi, int e, int upper
   }
   return 0.;
 }
+// lut_interp's temperature-only part (the bracketing table indices and temperatures) for one T, so that a loop over
+// many (level, target) pairs at the same T evaluates its log and exps once: lut_interp_at gives lut_interp's value
+// bit for bit (the same expressions on the same arguments)
+struct LutT {
+  int lowerindex;
+  double T_lower, T_upper;
+};
+DEVFN LutT lut_t(const Ctx &K, double T) {
+  LutT r;
+  r.lowerindex = (int)floor(log(T / K.T.mintemp) / K.T.T_step_log);
+  r.T_lower = r.T_upper = 0.;
+  if (r.lowerindex < K.T.tablesize - 1) {
+    r.T_lower = K.T.mintemp * exp(r.lowerindex * K.T.T_step_log);
+    r.T_upper = K.T.mintemp * exp((r.lowerindex + 1) * K.T.T_step_log);
+  }
+  return r;
+}
+DEVFN double lut_interp_at(const Ctx &K, const double *lut, int e, int i, int l, int t, double T, const LutT &lt) {
+  if (lt.lowerindex < K.T.tablesize - 1) {
+    const double f_upper = lut[get_bflutindex(K, lt.lowerindex + 1, e, i, l, t)];
+    const double f_lower = lut[get_bflutindex(K, lt.lowerindex, e, i, l, t)];
+    return (f_lower + (f_upper - f_lower) / (lt.T_upper - lt.T_lower) * (T - lt.T_lower));
+  }
+  return lut[get_bflutindex(K, K.T.tablesize - 1, e, i, l, t)];
+}
 // macroatom.cc:745-776
 DEVFN double col_ionization_ratecoeff(const Ctx &K, float T_e, float nne, int e, int i, int lower, int t,
                                       double epsilon_trans) {
@@ -399,6 +424,21 @@ DEVFN double col_ionization_ratecoeff(const Ctx &K, float T_e, float nne, int e,
   const double fac1 = epsilon_trans / ARTIS_KB / T_e;
   const double sigma_bf = level_photoion_xs(K, e, i, lower)[0] * get_phixsprobability(K, e, i, lower, t);
   return nne * 1.55e13 * pow((double)T_e, -0.5) * g * sigma_bf * exp(-fac1) / fac1;
+}
+// the same with pow(T_e, -0.5) given (rsqrtT), for loops at one T_e
+DEVFN double col_ionization_ratecoeff_r(const Ctx &K, float T_e, float nne, int e, int i, int lower, int t,
+                                        double epsilon_trans, double rsqrtT) {
+  double g;
+  const int ionstage = get_ionstage(K, e, i);
+  if (ionstage == 1)
+    g = 0.1;
+  else if (ionstage == 2)
+    g = 0.2;
+  else
+    g = 0.3;
+  const double fac1 = epsilon_trans / ARTIS_KB / T_e;
+  const double sigma_bf = level_photoion_xs(K, e, i, lower)[0] * get_phixsprobability(K, e, i, lower, t);
+  return nne * 1.55e13 * rsqrtT * g * sigma_bf * exp(-fac1) / fac1;
 }
 
 // calculate_macroatom_transitionrates (macroatom.cc:57-159): every individual rate of unique level ul in cell mgi,

@@ -559,6 +559,9 @@ DEVNI void te_cooling_rates(const Ctx &K, const TeDev &D, const TeState &s, TeRa
   const float T_e = s.Te;
   const int ni = K.T.nions_total;
   double C_total = 0., C_ff_all = 0., C_fb_all = 0., C_exc_all = 0., C_ionization_all = 0.;
+  // (T_e-only factors of the per-target terms, evaluated once: the same values the per-term calls compute)
+  const LutT lt = lut_t(K, T_e);
+  const double rsqrtT = pow((double)T_e, -0.5);
   for (int ub = 0; ub < ni; ub += s.g) {
     const int my_ui = ub + s.sub;
     double mine = 0.;
@@ -582,6 +585,7 @@ DEVNI void te_cooling_rates(const Ctx &K, const TeDev &D, const TeState &s, TeRa
       C_exc_all += C_exc;
       C_ion += C_exc;
       if (i < nions - 1) {
+        const double nnupperion = te_ionstagepop(K, D, s, e, ui + 1);  // (the same for every target)
         for (int level = 0; level < nionisinglevels; level++) {
           const double epsilon_current = K.T.level_epsilon[ul0 + level];
           const double nnlevel = te_levelpop(K, D, s, e, ui, level);
@@ -589,13 +593,13 @@ DEVNI void te_cooling_rates(const Ctx &K, const TeDev &D, const TeState &s, TeRa
           for (int t = 0; t < nt; t++) {
             const int upper = get_phixsupperlevel(K, e, i, level, t);
             const double epsilon_trans = epsilon(K, e, i + 1, upper) - epsilon_current;
-            const double C = nnlevel * col_ionization_ratecoeff(K, T_e, nne, e, i, level, t, epsilon_trans) * epsilon_trans;
+            const double C =
+                nnlevel * col_ionization_ratecoeff_r(K, T_e, nne, e, i, level, t, epsilon_trans, rsqrtT) * epsilon_trans;
             C_ionization_all += C;
             C_ion += C;
           }
           for (int t = 0; t < nt; t++) {
-            const double nnupperion = te_ionstagepop(K, D, s, e, ui + 1);
-            const double C = lut_interp(K, K.T.bfcooling_coeff, e, i, level, t, T_e) * nnupperion * nne;
+            const double C = lut_interp_at(K, K.T.bfcooling_coeff, e, i, level, t, T_e, lt) * nnupperion * nne;
             C_fb_all += C;
             C_ion += C;
           }

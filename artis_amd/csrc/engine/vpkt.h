@@ -29,9 +29,12 @@
 #define VPKT_OCC_DEFAULT 2
 
 // vpkt.cc:374-385
+// NS (the templates below): the spectra the loops run over, VPKT_MAX_SPECTRA or 4 when nspectra <= 4 -- the line
+// walk adds each line's tau to every spectrum, and a bound of 8 cost the walk 8 masked additions per line
+template <int NS = VPKT_MAX_SPECTRA>
 DEVFN bool vpkt_alive(const DevVpkt &V, const double *tau) {
   int count = 0;
-  for (int i = 0; i < VPKT_MAX_SPECTRA; i++)
+  for (int i = 0; i < NS; i++)
     if (i < V.nspectra && tau[i] > V.tau_max) count += 1;
   return count != V.nspectra;
 }
@@ -121,6 +124,7 @@ struct VLane {
 };
 
 // rlc_emiss_vpkt prologue (vpkt.cc:93-193): the dummy packet, its Stokes vector and weight p_n
+template <int NS>
 DEVFN void vpkt_trace_init(const Ctx &K, const LocalCounters &L, VLane &v) {
   const DevVpkt &V = K.V;
   const int64_t cap = V.cap;
@@ -141,7 +145,7 @@ DEVFN void vpkt_trace_init(const Ctx &K, const LocalCounters &L, VLane &v) {
   d.nu_cmf = sp[6 * cap + s];
   d.e_cmf = sp[7 * cap + s];
   d.number = -1;
-  for (int i = 0; i < VPKT_MAX_SPECTRA; i++) v.tau[i] = 0.;
+  for (int i = 0; i < NS; i++) v.tau[i] = 0.;
   // (nvpkt is counted by k_vpkt per lane and added once per lane at its end: a device-scope atomic on one address
   // per traced virtual packet serialised the whole kernel)
   const double t_current = v.t_current;
@@ -190,6 +194,7 @@ DEVFN void vpkt_trace_init(const Ctx &K, const LocalCounters &L, VLane &v) {
 }
 
 // the escape branch of rlc_emiss_vpkt (vpkt.cc:314-367)
+template <int NS>
 DEVFN void vpkt_trace_finish(const Ctx &K, VLane &v) {
   const DevVpkt &V = K.V;
 #ifdef ARTIS_DIAG_VPKT_NOFINISH  // timing diagnostic only (no spectra): the cost of the escape code
@@ -203,7 +208,7 @@ DEVFN void vpkt_trace_finish(const Ctx &K, VLane &v) {
   const VspecBin vb = vspec_bin(V, v.d.nu_rf, v.d.e_rf, t_arrive);
   if (vb.ok) {
 #pragma unroll
-    for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++) {
+    for (int ind = 0; ind < NS; ind++) {
       if (ind >= V.nspectra) break;
       const double prob = v.pn * exp(-v.tau[ind]);
       const double st[3] = {v.I * prob, v.Q * prob, v.U * prob};
@@ -249,7 +254,7 @@ DEVFN int vpkt_segment_end(Tx &x, VLane &v, double sdist, int snext) {
 }
 
 // the line walk of a cell without a coefficient row (population gathers), whole within one pass
-template <int PF>
+template <int PF, int NS>
 DEVFN int vpkt_gather_walk(Tx &x, VLane &v, unsigned long long &lines, double lnu_first, double lnu_last) {
   const Ctx &K = x.K;
   const DevVpkt &V = K.V;
@@ -261,7 +266,7 @@ DEVFN int vpkt_gather_walk(Tx &x, VLane &v, unsigned long long &lines, double ln
   int pf_base = -(1 << 20);
   const double *pops = K.C.pops + (int64_t)K.C.ne_index[v.mgi] * K.T.nlevels_total;
   bool anyex = false;
-  for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
+  for (int ind = 0; ind < NS; ind++)
     if (ind < V.nspectra && V.exclude[ind] != 0) anyex = true;
   // As in get_event: the line records, the two populations each needs and (with element exclusions) the line's
   // atomic number are fetched PF consecutive lines at a time, all loads independent, so the walk waits for memory
@@ -320,14 +325,14 @@ DEVFN int vpkt_gather_walk(Tx &x, VLane &v, unsigned long long &lines, double ln
     const double t_line = t_current + ldist / ARTIS_CLIGHT;
     const double dtau = (B_lu * n_l - B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_line;
     if (!anyex) {
-      for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
+      for (int ind = 0; ind < NS; ind++)
         if (ind < V.nspectra) v.tau[ind] += dtau;
     } else {
       const int anumber = V.anumber[zl];
-      for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
+      for (int ind = 0; ind < NS; ind++)
         if (ind < V.nspectra && V.exclude[ind] != -1 && (anumber != V.exclude[ind])) v.tau[ind] += dtau;
     }
-    if (!vpkt_alive(V, v.tau)) return VSEG_KILLED;
+    if (!vpkt_alive<NS>(V, v.tau)) return VSEG_KILLED;
   }
   return vpkt_segment_end(x, v, sdist, snext);
   }
@@ -336,7 +341,7 @@ DEVFN int vpkt_gather_walk(Tx &x, VLane &v, unsigned long long &lines, double ln
 // one pass of rlc_emiss_vpkt's cell loop (vpkt.cc:195-312); deviation D9 for the line loop.  Over a coefficient
 // row the line walk is resumable: it stops after VPKT_LINES_PER_PASS lines (VSEG_PENDING) and the next call continues
 // it; the segment's start (boundary, continuum) runs only when no walk is in progress.
-template <int PF>
+template <int PF, int NS>
 DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
   const Ctx &K = x.K;
   const DevVpkt &V = K.V;
@@ -348,7 +353,7 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
   auto all_dead = [&]() {
     int dead = 0;
 #pragma unroll
-    for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
+    for (int ind = 0; ind < NS; ind++)
       if (ind < nspec && v.tau[ind] > tau_max) dead++;
     return dead == nspec;
   };
@@ -372,7 +377,7 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
     const double kap_cont_nobf = kap_cont - kap.bf;
     const double kap_cont_noff = kap_cont - kap.ff;
     const double kap_cont_noes = kap_cont - kap.es;
-    for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++) {
+    for (int ind = 0; ind < NS; ind++) {
       if (ind >= V.nspectra) break;
       const double ex = V.exclude[ind];
       if (ex == -2)
@@ -384,7 +389,7 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
       else
         v.tau[ind] += kap_cont * s_cont;
     }
-    if (!vpkt_alive(V, v.tau)) return VSEG_KILLED;
+    if (!vpkt_alive<NS>(V, v.tau)) return VSEG_KILLED;
     v.sdist = sdist;
     v.snext = snext;
     v.ldist = 0.;
@@ -393,7 +398,7 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
     if (K.C.ne_index[v.mgi] < K.C.linecoef_rows) {
       v.inlines = true;
     } else {
-      return vpkt_gather_walk<PF>(x, v, lines, lnu_first, lnu_last);
+      return vpkt_gather_walk<PF, NS>(x, v, lines, lnu_first, lnu_last);
     }
   }
   {
@@ -466,7 +471,7 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
         return VSEG_KILLED;
       }
 #pragma unroll
-      for (int ind = 0; ind < VPKT_MAX_SPECTRA; ind++)
+      for (int ind = 0; ind < NS; ind++)
         if ((lm >> ind) & 1u) v.tau[ind] += dtau;
     }
     if (!done) {
@@ -487,7 +492,7 @@ __device__ unsigned long long g_vpkt_diag[8];
 #endif
 
 // all (spawn, observer) work items of the spawn buffer; spawn_ctr[1] is the fetch head
-template <int PF, int MINW>
+template <int PF, int MINW, int NS = VPKT_MAX_SPECTRA>
 __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict__ ctxp, int refill_min) {
   CTX_IN_LDS(ctxp)
   const DevVpkt &V = K.V;
@@ -569,17 +574,17 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
         }
         if (v.range < V.nrange) {
           v.range++;
-          vpkt_trace_init(K, L, v);
+          vpkt_trace_init<NS>(K, L, v);
           n_traced++;
           v.tracing = true;
         } else {
           have = false;
         }
       } else {
-        const int r = vpkt_trace_segment<PF>(x, v, lines);
+        const int r = vpkt_trace_segment<PF, NS>(x, v, lines);
         if (r != VSEG_CONTINUE && r != VSEG_PENDING) {
           if (r == VSEG_ESCAPED) {
-            vpkt_trace_finish(K, v);
+            vpkt_trace_finish<NS>(K, v);
             n_esc1 += v.realtype == 1;
             n_esc2 += v.realtype == 2;
             n_esc3 += v.realtype == 3;

@@ -498,7 +498,9 @@ class TeArrays:
     cell state as the previous timestep's solution) plus synthetic normalised heating / photoionisation estimators
     (seeded), and the output arrays.  The same block feeds the engine and the oracle."""
 
-    def __init__(self, model, t_current, seed=3, thick_frac=0.0, lte_all=False, gamma_zero_frac=0.1):
+    def __init__(self, model, t_current, seed=3, thick_frac=0.0, lte_all=False, gamma_zero_frac=0.1, synthetic=True):
+        """synthetic=False: the estimator inputs are left zero for the caller to fill (the timestep loop's own
+        prepared estimators), without drawing the seeded stand-ins."""
         m = model
         cs = CellState.from_address(m.cellstate)
         hdr = AtomicHeader.from_address(m.atomic)
@@ -510,21 +512,26 @@ class TeArrays:
         self.elem_abundance = f32(cs.elem_abundance, np_ * nel)
         self.groundlevelpop = f32(cs.groundlevelpop, np_ * ni)
         anum = np.ctypeslib.as_array(C.cast(hdr.elem_anumber, C.POINTER(C.c_int32)), (nel,)).copy()
-        rng = np.random.default_rng(seed)
-        self.thick = (rng.random(np_) < thick_frac).astype(np.int16)
-        if lte_all:
-            self.thick[:] = 1
         # initstablemeannucmass stand-in: A ~ 2.1 Z nucleons
         self.elem_meanweight = np.tile((2.1 * anum * MH).astype(np.float32), np_)
         self.vol_init = np.full(np_, 1e45)
         self.mgi_list = np.nonzero(self.rho > 0)[0].astype(np.int32)
-        # normalised estimators: heating terms of the order of the cell's LTE bf heating, spread per cell
-        self.ffheating = 10 ** rng.uniform(-12, -9, np_) * self.rho / 1e-14
-        self.colheating = 10 ** rng.uniform(-12, -9, np_) * self.rho / 1e-14
-        cell_scale = np.repeat(10 ** rng.uniform(-1.5, 3.0, np_), nel * mx)  # some cells balance inside [T_min, T_max]
-        self.bfheating = cell_scale * 10 ** rng.uniform(-0.3, 0.3, np_ * nel * mx)
-        self.gamma = 10 ** rng.uniform(-4., 1., np_ * nel * mx)
-        self.gamma[rng.random(np_ * nel * mx) < gamma_zero_frac] = 0.
+        if synthetic:
+            rng = np.random.default_rng(seed)
+            self.thick = (rng.random(np_) < thick_frac).astype(np.int16)
+            if lte_all:
+                self.thick[:] = 1
+            # normalised estimators: heating terms of the order of the cell's LTE bf heating, spread per cell
+            self.ffheating = 10 ** rng.uniform(-12, -9, np_) * self.rho / 1e-14
+            self.colheating = 10 ** rng.uniform(-12, -9, np_) * self.rho / 1e-14
+            cell_scale = np.repeat(10 ** rng.uniform(-1.5, 3.0, np_), nel * mx)  # some cells balance inside [T_min, T_max]
+            self.bfheating = cell_scale * 10 ** rng.uniform(-0.3, 0.3, np_ * nel * mx)
+            self.gamma = 10 ** rng.uniform(-4., 1., np_ * nel * mx)
+            self.gamma[rng.random(np_ * nel * mx) < gamma_zero_frac] = 0.
+        else:
+            self.thick = np.zeros(np_, np.int16)
+            self.ffheating, self.colheating = np.zeros(np_), np.zeros(np_)
+            self.bfheating, self.gamma = np.zeros(np_ * nel * mx), np.zeros(np_ * nel * mx)
         self.heating_dep = None
         self.nne = np.zeros(np_, np.float32)
         self.nnetot = np.zeros(np_, np.float32)
@@ -576,23 +583,28 @@ class UgArrays:
     """Raw transport estimators for artis_ug_prepare (seeded, of the magnitude a 1e4-packet step accumulates per cell
     of a small model) plus the previous n_e / partition functions of the model's cell state, and the outputs."""
 
-    def __init__(self, model, deltat, tratmid, seed=6):
+    def __init__(self, model, deltat, tratmid, seed=6, synthetic=True):
+        """synthetic=False: the raw estimators are left zero for the caller to fill (the timestep loop's own)."""
         m = model
         cs = CellState.from_address(m.cellstate)
         np_, nel, ni, mx = m.npts_model, m.nelements, m.nions_total, m.maxnions
         f32 = lambda p, n: np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), (n,)).copy()  # noqa: E731
-        rng = np.random.default_rng(seed)
         self.deltat, self.tratmid, self.nprocs = float(deltat), float(tratmid), 1
         self.nne = f32(cs.nne, np_)
         self.partfunct = f32(cs.partfunct, np_ * ni)
-        # J ~ 4 pi sigma T^4 / pi * volume * deltat, with nubar giving T_R ~ 5000-15000 K
-        T = rng.uniform(5e3, 1.5e4, np_)
-        self.J = 4 * np.pi * 5.6704e-5 * T ** 4 / np.pi * 1e45 * deltat * rng.uniform(0.5, 1.5, np_)
-        self.nuJ = self.J * (1.38064852e-16 * 3.832229494 * T * rng.uniform(0.8, 1.2, np_) / 6.6260755e-27)
-        self.ffheating = self.J * 1e-18
-        self.colheating = self.J * 1e-17
-        self.gamma = self.J.repeat(nel * mx) * 10 ** rng.uniform(-22, -20, np_ * nel * mx)
-        self.bfheating = self.J.repeat(nel * mx) * 10 ** rng.uniform(-20, -18, np_ * nel * mx)
+        if synthetic:
+            rng = np.random.default_rng(seed)
+            # J ~ 4 pi sigma T^4 / pi * volume * deltat, with nubar giving T_R ~ 5000-15000 K
+            T = rng.uniform(5e3, 1.5e4, np_)
+            self.J = 4 * np.pi * 5.6704e-5 * T ** 4 / np.pi * 1e45 * deltat * rng.uniform(0.5, 1.5, np_)
+            self.nuJ = self.J * (1.38064852e-16 * 3.832229494 * T * rng.uniform(0.8, 1.2, np_) / 6.6260755e-27)
+            self.ffheating = self.J * 1e-18
+            self.colheating = self.J * 1e-17
+            self.gamma = self.J.repeat(nel * mx) * 10 ** rng.uniform(-22, -20, np_ * nel * mx)
+            self.bfheating = self.J.repeat(nel * mx) * 10 ** rng.uniform(-20, -18, np_ * nel * mx)
+        else:
+            self.J, self.nuJ, self.ffheating, self.colheating = (np.zeros(np_) for _ in range(4))
+            self.gamma, self.bfheating = np.zeros(np_ * nel * mx), np.zeros(np_ * nel * mx)
         self.TR_out = np.zeros(np_, np.float32)
         self.W_out = np.zeros(np_, np.float32)
         self.TJ_out = np.zeros(np_, np.float32)

@@ -40,8 +40,11 @@ def _copy_arrays(obj):
 class LteTimestepLoop:
     """update_grid (GPU) -> upload_cellstate -> update_packets (resident) over consecutive timesteps."""
 
-    def __init__(self, model, eng, rank=0):
+    def __init__(self, model, eng, rank=0, keep_inputs=False):
+        """keep_inputs: keep a copy of each update_grid's inputs (last_inputs, for an oracle replay in the tests)."""
         self.m, self.eng, self.rank = model, eng, rank
+        self.keep_inputs = keep_inputs
+        self.last_inputs = None
         g = ffi.Geometry.from_address(model.geometry)
         np_ = model.npts_model
         cell_mgi = np.ctypeslib.as_array(g.cell_mgi, (g.ngrid,))
@@ -76,15 +79,16 @@ class LteTimestepLoop:
 
     def update_grid(self, nts, est):
         """update_grid for timestep nts from the raw estimators `est` of timestep nts - 1 (update_grid.cc:1316 pairs
-        them): the density / opacity for nts (artis_model_advance), then the GPU preparation and solution on every non-empty
-        cell; the solved state is written into the model's cell-state arrays.  Returns device milliseconds."""
+        them): the density / opacity for nts (artis_model_advance), then the GPU preparation and solution on every
+        non-empty cell; the solved state is written into the model's cell-state arrays.  Returns device milliseconds."""
         m, eng = self.m, self.eng
         tp = {}
         t = time.perf_counter()
         prev = {k: v.copy() for k, v in self._cell_arrays().items()}
         m.advance(nts)  # rho(t), kappagrey, thick at nts (host bookkeeping)
         tp["advance"] = (time.perf_counter() - t) * 1e3
-        te = ffi.TeArrays(m, t_current=float(self.ts_mid[nts - 1]))  # nts_for_te = nts - 1 (update_grid.cc:804)
+        # nts_for_te = nts - 1 (update_grid.cc:804)
+        te = ffi.TeArrays(m, t_current=float(self.ts_mid[nts - 1]), synthetic=False)
         # the previous timestep's solution is the solver's starting state (the reference's modelgrid values)
         for k in ("TR", "W", "TJ", "Te"):
             setattr(te, k, prev[k].copy())
@@ -93,11 +97,13 @@ class LteTimestepLoop:
         te.thick = np.ctypeslib.as_array(C.cast(ffi.CellState.from_address(m.cellstate).thick, C.POINTER(C.c_int16)),
                                          (m.npts_model,)).copy()
         te.mgi_list = np.nonzero((te.rho > 0) & (self.vol_init > 0))[0].astype(np.int32)
-        ug = ffi.UgArrays(m, deltat=float(self.ts_width[nts - 1]), tratmid=float(self.ts_mid[nts] / self.tmin))
+        ug = ffi.UgArrays(m, deltat=float(self.ts_width[nts - 1]), tratmid=float(self.ts_mid[nts] / self.tmin),
+                          synthetic=False)
         ug.J, ug.nuJ, ug.ffheating, ug.colheating = est.J, est.nuJ, est.ffheating, est.colheating
         ug.gamma, ug.bfheating = est.gamma, est.bfheating
         ug.nne, ug.partfunct = prev["nne"].copy(), prev["partfunct"].copy()
-        self.last_inputs = (te.copy(), _copy_arrays(ug))  # for an oracle replay (tests)
+        if self.keep_inputs:
+            self.last_inputs = (te.copy(), _copy_arrays(ug))  # for an oracle replay (tests)
         t1 = time.perf_counter()
         tp["inputs"] = (t1 - t) * 1e3 - tp["advance"]
         t = t1

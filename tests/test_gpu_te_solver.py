@@ -221,7 +221,7 @@ def test_timestep_loop_on_device_matches_oracle():
     m.set_timestep(nts0)
     eng = Engine(m)
     try:
-        loop = LteTimestepLoop(m, eng)
+        loop = LteTimestepLoop(m, eng, keep_inputs=True)
         pk0 = m.init_rpackets(nts0, 3000, seed=19, etot=loop.radiation_energy(nts0))
         eng.upload(pk0)
         po = pk0.copy()

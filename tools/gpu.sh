@@ -16,6 +16,7 @@
 #                                                    ARTIS_GPU_STATS=1 on a bench run -> $O/stamps_$name.{json,err}
 #   tools/gpu.sh pre name1[:ENV=V] name2 ...         the precompute alone (tools/precompute_ab.py) per engine build,
 #                                                    under rocprofv3 --stats -> $O/pre_<name>.{json,txt}
+#   tools/gpu.sh sqpy name script.py [args]          one SQ instruction-counter pass over a python script -> $O/sq_<name>.txt
 #   tools/gpu.sh final                               tests, prof, pmc, default bench line (the round-end set)
 #
 # Environment: T (tag, default "r4"), O (output dir, default gpurun_out/$T), NAME (pmc summary name, default
@@ -86,6 +87,17 @@ run_sq() {
     --packets ${P:-2000000} --steps 1 --warmup 0 --no-cpu-baseline --no-update-grid --no-extra "$@" > "$O/sq/sq.log" 2>&1
 }
 
+# sqpy name script.py [args]: one SQ counter pass over any python script (e.g. tools/precompute_ab.py)
+run_sqpy() {
+  local name=$1
+  shift
+  rm -rf "$O/sq_$name"
+  mkdir -p "$O/sq_$name"
+  timeout -s KILL 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_VALU \
+    SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM --kernel-trace -d "$O/sq_$name/db" -o run -- python3 "$@" \
+    > "$O/sq_$name/run.log" 2>&1 && python3 tools/sq_summary.py "$O/sq_$name/db" | tee "$O/sq_$name.txt"
+}
+
 run_stamps() {
   local name=$1
   shift
@@ -140,6 +152,7 @@ case "$cmd" in
   pcs) run_pcs "$@" ;;
   stamps) run_stamps "$@" ;;
   pre) run_pre "$@" ;;
+  sqpy) run_sqpy "$@" ;;
   final) run_tests && run_prof --no-extra && run_pmc && run_bench ;;
   *) echo "usage: tools/gpu.sh tests|bench|prof|pmc|sq|ab|final [args]"; exit 2 ;;
 esac
