@@ -346,38 +346,45 @@ __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict_
 // (position x row) tiles through LDS, read along rows from the position-major scratch src (row stride n_s; rows
 // c0 .. c0 + 63 of it, the first nvalid valid), written along positions (64 consecutive keys of one record per row:
 // coalesced) into record rows row0 + c0 + j.
+#ifndef MAPACK_P
+#define MAPACK_P 32  // record positions per LDS tile (32: 24 KB of LDS per block, 6 blocks per CU)
+#endif
 struct MapackLds {
-  double tile[64][65];
+  double tile[MAPACK_P][65];
   double norm[ARTIS_MA_ACTION_COUNT][64];  // action totals per row
   uint32_t akey[ARTIS_MA_ACTION_COUNT][64];
 };
 DEVFN void mapack_tile(const Ctx &K, int ul, const double *__restrict__ src, int64_t n_s, int64_t c0, int64_t nvalid,
                        int64_t row0, MapackLds &S) {
+  constexpr int P = MAPACK_P, RS = 256 / MAPACK_P;  // positions per tile; rows a pass of the block covers
   const MaMeta mm = K.T.ma_meta[ul];
   const int len = ARTIS_MA_ACTION_COUNT + 2 * mm.nd + mm.nu + 2 * mm.nr + mm.nt;
   const MaLayout lay = ma_layout(mm.nd, mm.nu, mm.nr, mm.nt);
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int tx = threadIdx.x % P, ty = threadIdx.x / P;
   __syncthreads();  // (the previous tile's readers of S are done)
-  if (ty == 0 && c0 + tx < nvalid) {
+  if (threadIdx.x < 64 && c0 + threadIdx.x < nvalid) {
+    const int r = threadIdx.x;
     double pr[ARTIS_MA_ACTION_COUNT];
     double total = 0.;
     for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
-      pr[a] = src[(int64_t)a * n_s + c0 + tx];
-      S.norm[a][tx] = pr[a];
+      pr[a] = src[(int64_t)a * n_s + c0 + r];
+      S.norm[a][r] = pr[a];
       total += pr[a];
     }
     double rate = 0.;
     for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
       rate += pr[a];
-      S.akey[a][tx] = ma_key32(rate, total);
+      S.akey[a][r] = ma_key32(rate, total);
     }
   }
   // segment boundaries of the record (positions >= 9): the action whose total normalises each
   const int b1 = ARTIS_MA_ACTION_COUNT + mm.nd, b2 = b1 + mm.nu, b3 = b2 + mm.nd, b4 = b3 + mm.nr, b5 = b4 + mm.nr;
-  for (int p0 = 0; p0 < len; p0 += 64) {
+  for (int p0 = 0; p0 < len; p0 += P) {
     __syncthreads();
-    for (int j = ty; j < 64; j += 4)
-      if (p0 + j < len && c0 + tx < nvalid) S.tile[j][tx] = src[(int64_t)(p0 + j) * n_s + c0 + tx];
+    for (int q = threadIdx.x; q < P * 64; q += 256) {  // (64 consecutive rows of one position per wave: coalesced)
+      const int pp = q / 64, rr = q % 64;
+      if (p0 + pp < len && c0 + rr < nvalid) S.tile[pp][rr] = src[(int64_t)(p0 + pp) * n_s + c0 + rr];
+    }
     __syncthreads();
     const int p = p0 + tx;
     if (p < len) {
@@ -388,12 +395,12 @@ DEVFN void mapack_tile(const Ctx &K, int ul, const double *__restrict__ src, int
                     : (p < b4)                 ? ARTIS_MA_ACTION_RADRECOMB
                     : (p < b5)                 ? ARTIS_MA_ACTION_INTERNALDOWNLOWER
                                                : ARTIS_MA_ACTION_INTERNALUPHIGHER;
-      for (int j = ty; j < 64; j += 4) {
+      int sp;
+      const int rp = ma_rec_pos(lay, p, mm.nd, mm.nu, &sp);
+      for (int j = ty; j < 64; j += RS) {
         if (c0 + j >= nvalid) break;
         const uint32_t key = (a < 0) ? S.akey[p][j] : ma_key32(S.tile[tx][j], S.norm[a][j]);
         uint16_t *rec = K.C.ma_key + (row0 + c0 + j) * K.C.ma_key_stride + mm.rec_off;
-        int sp;
-        const int rp = ma_rec_pos(lay, p, mm.nd, mm.nu, &sp);
         rec[rp] = (uint16_t)(key >> 16);
         rec[lay.hot + rp] = (uint16_t)(key & 0xffffu);
         if (sp >= 0) {  // also a block separator on the record's first line
@@ -603,22 +610,37 @@ __global__ __launch_bounds__(64) void k_ma_build(Ctx K, const int2 *__restrict__
 
 // DevCells::linecoef: the Sobolev coefficient (B_lu n_l - B_ul n_u) * HCLIGHTOVERFOURPI of every line in every
 // non-empty cell, in get_event's operation order (rpkt.cc:168-187); lanes run along a cell's row (coalesced
-// writes, line records from L2, population gathers from the cell's 29 kB row)
+// writes, line records from L2, population gathers from the cell's 29 kB row).  A block takes 256 lines of
+// LINECOEF_R consecutive rows: the line record is loaded once, and the rows' population gathers are all in flight
+// before the stores (one row per block and thread: the launch was bound by dispatching 12.8 M short blocks).
+#ifndef LINECOEF_R
+#define LINECOEF_R 8
+#endif
 __global__ __launch_bounds__(256) void k_linecoef(Ctx K) {
   const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (li >= K.C.linecoef_stride) return;
-  for (int k = blockIdx.y; k < K.C.linecoef_rows; k += gridDim.y) {
-    double v = 0.;
-    if (li < K.T.nlines) {
-      const LineTau r = K.T.line_tau[li];
-      const double *pops = K.C.pops + (int64_t)k * K.T.nlevels_total;
-      const double n_u = pops[r.ul_upper], n_l = pops[r.ul_lower];
-      v = (r.B_lu * n_l - r.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI;
+  const bool in = li < K.T.nlines;
+  LineTau r{};
+  if (in) r = K.T.line_tau[li];
+  bool neg = false;
+  for (int k0 = blockIdx.y * LINECOEF_R; k0 < K.C.linecoef_rows; k0 += gridDim.y * LINECOEF_R) {
+    double v[LINECOEF_R];
+#pragma unroll
+    for (int q = 0; q < LINECOEF_R; q++) {
+      v[q] = 0.;
+      if (in && k0 + q < K.C.linecoef_rows) {
+        const double *pops = K.C.pops + (int64_t)(k0 + q) * K.T.nlevels_total;
+        const double n_u = pops[r.ul_upper], n_l = pops[r.ul_lower];
+        v[q] = (r.B_lu * n_l - r.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI;
+        neg = neg || v[q] < 0.;
+      }
     }
-    K.C.linecoef[(int64_t)k * K.C.linecoef_stride + li] = v;
-    // (one atomic per wave until the flag is seen set: an atomic per wave on one address serialises the launch)
-    if (__any(v < 0.) && __lane_id() == 0 && !*(volatile int32_t *)K.C.linecoef_neg) atomicOr(K.C.linecoef_neg, 1);
+#pragma unroll
+    for (int q = 0; q < LINECOEF_R; q++)
+      if (k0 + q < K.C.linecoef_rows) K.C.linecoef[(int64_t)(k0 + q) * K.C.linecoef_stride + li] = v[q];
   }
+  // (one atomic per wave until the flag is seen set: an atomic per wave on one address serialises the launch)
+  if (__any(neg) && __lane_id() == 0 && !*(volatile int32_t *)K.C.linecoef_neg) atomicOr(K.C.linecoef_neg, 1);
 }
 
 // out[c * rows + r] = in[r * cols + c], through a 64x64 LDS tile (one wave reads rows, writes columns)
@@ -847,7 +869,6 @@ struct Engine {
   bool r_binned = false;          // bin the R queue by cell before k_rpkt (ARTIS_GPU_R_BIN=1)
   bool ma_bin_blk = true;         // few cells: block-local M-queue binning (ARTIS_GPU_MA_BIN_BLK=0: per-entry atomics)
   bool ma_pre_on = true;          // M-queue pre-tickets (WaveState::ma_pre; ARTIS_GPU_MA_PRE=0: gathered by the scatter)
-  int ncu = 256;
   int rpkt_walk = -1;             // k_rpkt's bounded line walk: -1 by the previous transport's lines per step, 0 off, 1 on
   bool rpkt_coop = true;          // detailed-bf models: wave-made continuum sums in k_rpkt (ARTIS_GPU_RPKT_COOP=0: per lane)
   std::vector<hipEvent_t> vev;  // (start, end) pairs around the k_vpkt launches of the last update
@@ -3029,7 +3050,6 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   {
     int ncu = 256;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
-    G.ncu = ncu;
     G.wave_grid = ncu * 8;  // 32 waves per CU of 256-thread blocks; late blocks find the queue drained
     // (tests: ARTIS_GPU_WAVE_GRID=<blocks>, a multiple of 8, shrinks the persistent grids and the vpkt overflow records)
     if (const char *wg = getenv("ARTIS_GPU_WAVE_GRID")) G.wave_grid = std::max(8, atoi(wg) / 8 * 8);
@@ -3858,7 +3878,7 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
     if (G.K.C.linecoef) HIPCHK(hipMemsetAsync(G.K.C.linecoef_neg, 0, sizeof(int32_t), G.stream));
     if (G.K.C.linecoef)
       k_linecoef<<<dim3((unsigned)((G.K.C.linecoef_stride + 255) / 256),
-                        (unsigned)std::min(G.K.C.linecoef_rows, 32768)), 256, 0,
+                        (unsigned)std::min((G.K.C.linecoef_rows + LINECOEF_R - 1) / LINECOEF_R, 32768)), 256, 0,
                     G.stream>>>(G.K);
     const int mr = G.K.C.ma_rows;
     if (G.K.C.ma_level_mode) {

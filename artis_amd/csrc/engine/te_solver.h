@@ -507,25 +507,38 @@ DEVFN double te_col_exc(const TeExcItem &it, float T_e, float nne, double lowers
   }
   return C;
 }
-// te_col_exc for lanes on different lines (k_te_solve: a lane per ion): one exp -- of +eoverkt or -eoverkt, the
+// te_col_exc for k_te_solve, whose lanes are on different ions' lines: one exp -- of +eoverkt or -eoverkt, the
 // argument the line's branch takes -- and one log for every lane, instead of the three branches' transcendentals
-// executed one after the other by a divergent wave.  The same expressions on the same arguments: the same bits.
-DEVFN double te_col_exc_mixed(const TeExcItem &it, float T_e, float nne, double lowerstatweight) {
+// run one after another by a divergent wave; the T_e-only factors of the branches evaluated once per sum (TeExcT), the
+// divisions by k T_e and by the level's statistical weight made multiplications: the reference's expression up to
+// the order of its products (ulp-level differences; update_grid's parity bar is identical Brent iteration counts and T_e within
+// 1e-9, tests/test_gpu_te_solver.py).  k_cooling, whose cooling lists feed the k-packet selection, keeps te_col_exc.
+struct TeExcT {
+  double inv_kT, A1, A2, A3;
+};
+DEVFN TeExcT te_exc_t(float T_e, float nne) {
+  TeExcT f;
+  f.inv_kT = 1. / (ARTIS_KB * T_e);
+  f.A1 = ARTIS_C_0 * nne * sqrtf(T_e) * 14.51039491;
+  f.A2 = nne * 8.629e-6 * 0.01 / sqrtf(T_e);
+  f.A3 = nne * 8.629e-6 / sqrtf(T_e);
+  return f;
+}
+DEVFN double te_col_exc_fast(const TeExcItem &it, const TeExcT &f, double inv_lsw) {
   const double coll_strength = it.coll_str;
-  const double eoverkt = it.epsilon_trans / (ARTIS_KB * T_e);
+  const double eoverkt = it.epsilon_trans * f.inv_kT;
   const bool allowed = coll_strength < 0 && !it.forbidden;
   const double ex = exp(allowed ? eoverkt : -eoverkt);
   const double lg = log(eoverkt);
   double C;
   if (allowed) {
-    const double g_bar = 0.2;
     const double test = 0.276 * ex * (-0.5772156649 - lg);
-    const double Gamma = g_bar > test ? g_bar : test;
-    C = ARTIS_C_0 * nne * sqrtf(T_e) * 14.51039491 * it.osc_f * it.P2 * eoverkt / ex * Gamma;
+    const double Gamma = 0.2 > test ? 0.2 : test;
+    C = f.A1 * it.osc_f * it.P2 * eoverkt / ex * Gamma;
   } else if (coll_strength < 0) {
-    C = nne * 8.629e-6 * 0.01 * ex * (double)it.upper_sw / sqrtf(T_e);
+    C = f.A2 * ex * (double)it.upper_sw;
   } else {
-    C = nne * 8.629e-6 * coll_strength * ex / lowerstatweight / sqrtf(T_e);
+    C = f.A3 * coll_strength * ex * inv_lsw;
   }
   return C;
 }
@@ -535,17 +548,18 @@ DEVNI double te_coll_exc_ion(const Ctx &K, const TeDev &D, const TeState &s, int
   const int ul0 = K.T.ion_uniqueleveloffset[ui];
   double C_exc = 0.;
   const int nlevels = K.T.ion_nlevels[ui];
+  const TeExcT f = te_exc_t(T_e, nne);
   for (int level = 0; level < nlevels; level++) {
     const int ul = ul0 + level;
     const int nuptrans = K.T.level_nuptrans[ul];
     if (nuptrans == 0) continue;
     const double nnlevel = te_levelpop(K, D, s, e, ui, level);
-    const double statweight = K.T.level_stat_weight[ul];
+    const double inv_lsw = 1. / (double)K.T.level_stat_weight[ul];
     const TeExcItem *it = K.T.exc_items + K.T.level_uptrans_offset[ul];
 #pragma unroll 2
     for (int ii = 0; ii < nuptrans; ii++) {
       const TeExcItem x = it[ii];
-      const double C = nnlevel * te_col_exc_mixed(x, T_e, nne, statweight) * x.epsilon_trans;
+      const double C = nnlevel * te_col_exc_fast(x, f, inv_lsw) * x.epsilon_trans;
       C_exc += C;
     }
   }

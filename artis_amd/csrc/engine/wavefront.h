@@ -188,7 +188,9 @@ __global__ void k_classify(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *
 // 2e6 packets: 164 ms of k_rpkt per step, 16 lines per pass 186 ms -- the state kept across passes spills), on the
 // kilonova inputs (16 lines per step, 122 for a wave's longest lane) the bounded walk (engine.hip launch_rpkt picks
 // it from the previous transport's lines per step).
+#ifndef RPKT_WALK_LINES
 #define RPKT_WALK_LINES 16
+#endif
 
 // r-packets: persistent lanes, one r-packet step (or part of its line walk) per loop pass.  COOP: the instance for
 // models with detailed bf estimators, whose continuum sums are made by the whole wave (wave_kappa_bf,

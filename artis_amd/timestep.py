@@ -97,6 +97,12 @@ class LteTimestepLoop:
         te.thick = np.ctypeslib.as_array(C.cast(ffi.CellState.from_address(m.cellstate).thick, C.POINTER(C.c_int16)),
                                          (m.npts_model,)).copy()
         te.mgi_list = np.nonzero((te.rho > 0) & (self.vol_init > 0))[0].astype(np.int32)
+        if self.solution is not None:
+            # cells in the order of their previous solution's Brent iteration count: a wave of k_te_solve runs as
+            # many thermal-balance evaluations as its slowest cell needs, and a cell's count changes little from one
+            # timestep to the next (the order changes no result: the cells are independent)
+            prev_iters = self.solution.iters[te.mgi_list]
+            te.mgi_list = te.mgi_list[np.argsort(prev_iters, kind="stable")]
         ug = ffi.UgArrays(m, deltat=float(self.ts_width[nts - 1]), tratmid=float(self.ts_mid[nts] / self.tmin),
                           synthetic=False)
         ug.J, ug.nuJ, ug.ffheating, ug.colheating = est.J, est.nuJ, est.ffheating, est.colheating

@@ -43,9 +43,12 @@ run_bench() {
   timeout -k 10 900 python3 -u bench.py "$@" > "$O/bench.json" 2> "$O/bench.err" && tail -c 400 "$O/bench.json"
 }
 
+# (the rocpd database is summarised into $O/kernel_stats.csv and removed: gpurun merges at most 64 MiB back)
 run_prof() {
+  rm -rf "$O/prof"
   timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 -u bench.py --no-cpu-baseline "$@" \
-    > "$O/bench_prof.json" 2> "$O/bench_prof.err"
+    > "$O/bench_prof.json" 2> "$O/bench_prof.err" &&
+  python3 tools/rocpd_stats.py "$O/prof/run_results.db" --csv "$O/kernel_stats.csv" && rm -rf "$O/prof"
 }
 
 run_cfgprof() {
@@ -76,7 +79,7 @@ run_pmc() {
   timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$O/pmc_$name/write" -o run -- $B > "$O/pmc_$name/w.log" 2>&1 &&
   python3 tools/pmc_summary.py --fetch "$O/pmc_$name/fetch" --write "$O/pmc_$name/write" --packets "$packets" --ngrid 50 \
     --nts "$nts" $([ "$vp" != 0 ] && echo --vpkt "$vp") --out "$O/pmc_$name.json" &&
-  cp "$O/pmc_$name.json" "profiles/pmc_${T}_$name.json"
+  cp "$O/pmc_$name.json" "profiles/pmc_${T}_$name.json" && rm -rf "$O/pmc_$name/fetch" "$O/pmc_$name/write"
 }
 
 run_sq() {
