@@ -104,7 +104,7 @@ run_sqpy() {
 run_stamps() {
   local name=$1
   shift
-  ARTIS_GPU_SO=build/ab/stamps/libartis_gpu.so ARTIS_GPU_STATS=1 timeout -k 10 600 python3 -u bench.py --no-cpu-baseline \
+  ARTIS_GPU_SO=${STAMPS_SO:-build/ab/stamps/libartis_gpu.so} ARTIS_GPU_STATS=1 timeout -k 10 600 python3 -u bench.py --no-cpu-baseline \
     --no-update-grid --no-extra "$@" > "$O/stamps_$name.json" 2> "$O/stamps_$name.err" && grep "artis_gpu\]" "$O/stamps_$name.err" | tail -12
 }
 
