@@ -869,6 +869,7 @@ struct Engine {
   bool r_binned = false;          // bin the R queue by cell before k_rpkt (ARTIS_GPU_R_BIN=1)
   bool ma_bin_blk = true;         // few cells: block-local M-queue binning (ARTIS_GPU_MA_BIN_BLK=0: per-entry atomics)
   bool ma_pre_on = true;          // M-queue pre-tickets (WaveState::ma_pre; ARTIS_GPU_MA_PRE=0: gathered by the scatter)
+  bool mf_rec_on = true;          // F-queue records (WaveState::mf_rec; ARTIS_GPU_MF_REC=0: the per-packet pend arrays)
   int rpkt_walk = -1;             // k_rpkt's bounded line walk: -1 by the previous transport's lines per step, 0 off, 1 on
   bool rpkt_coop = true;          // detailed-bf models: wave-made continuum sums in k_rpkt (ARTIS_GPU_RPKT_COOP=0: per lane)
   std::vector<hipEvent_t> vev;  // (start, end) pairs around the k_vpkt launches of the last update
@@ -1026,6 +1027,7 @@ void free_packets() {
   dfree(G.W.ma_sorted);
   dfree(G.W.ma_tick);
   dfree(G.W.ma_pre);
+  dfree(G.W.mf_rec);
   for (int q = 0; q < NQUEUES; q++) dfree(G.W.q[q]);
   G.cap_pkts = 0;
   G.npkts = 0;
@@ -1047,7 +1049,8 @@ int alloc_packets(int64_t n) {
                            {(void **)&G.W.ma_key, un * sizeof(int32_t)},
                            {(void **)&G.W.ma_sorted, un * sizeof(int32_t)},
                            {(void **)&G.W.ma_tick, un * 2 * sizeof(int4)},
-                           {(void **)&G.W.ma_pre, un * 2 * sizeof(int4)}};
+                           {(void **)&G.W.ma_pre, un * 2 * sizeof(int4)},
+                           {(void **)&G.W.mf_rec, un * 2 * sizeof(int4)}};
   for (int q = 0; q < NQUEUES; q++) reqs.push_back({(void **)&G.W.q[q], un * sizeof(int32_t)});
   const int nreq = (int)reqs.size();
   for (int r = 0; r < nreq; r++) {
@@ -1325,6 +1328,7 @@ int run_wavefront(int64_t n, int nts, double t2) {
   WaveState W = G.W;
   if (!(G.K.C.have_macache && W.ma_binned)) W.ma_tick = nullptr;  // tickets: cached walk over the binned queue
   if (!W.ma_tick || !G.ma_pre_on) W.ma_pre = nullptr;            // pre-tickets written by the queue's producers
+  if (!G.mf_rec_on) W.mf_rec = nullptr;                           // F-queue records (else pend / pend_jumps / rng_n)
   const unsigned grid = (unsigned)G.wave_grid;
   if (int rc = sync_ctx()) return rc;
   G.tev_used = 0;
@@ -1543,6 +1547,12 @@ int run_wavefront(int64_t n, int nts, double t2) {
       for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++)
         fprintf(stderr, "[artis_gpu] ma action %d: searches %llu, pending %llu, probes %llu\n", a, dg[a], dg[16 + a],
                 dg[32 + a]);
+      if (dg[9])
+        fprintf(stderr,
+                "[artis_gpu] ma up-same selections of blocked arrays %llu: in the line-0 suffix %llu, first 16 %llu, "
+                "last 16 %llu, first suffix-size %llu, mean size %.1f, mean suffix %.1f, quarters %llu %llu %llu %llu\n",
+                dg[9], dg[10], dg[11], dg[12], dg[13], (double)dg[14] / dg[9], (double)dg[15] / dg[9], dg[25], dg[26],
+                dg[27], dg[28]);
       if (dg[43])
         fprintf(stderr, "[artis_gpu] ma step sections (cycles per wave step): action keys %.0f, search %.0f, rest %.0f\n",
                 (double)dg[40] / dg[43], (double)dg[41] / dg[43], (double)dg[42] / dg[43]);
@@ -3069,6 +3079,8 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     G.rpkt_coop = !(rc_ && rc_[0] == '0');
     const char *mp = getenv("ARTIS_GPU_MA_PRE");
     G.ma_pre_on = !(mp && mp[0] == '0');
+    const char *mf = getenv("ARTIS_GPU_MF_REC");
+    G.mf_rec_on = !(mf && mf[0] == '0');
     const char *bb = getenv("ARTIS_GPU_MA_BIN_BLK");
     G.ma_bin_blk = !(bb && bb[0] == '0');
     const char *xr = getenv("ARTIS_GPU_MA_XCD");

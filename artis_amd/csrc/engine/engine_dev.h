@@ -119,18 +119,46 @@ struct DevTab {
 // Record layout of the macro-atom key cache (DevCells::ma_key), in 16-bit key positions.  k_ma stages one 128-byte
 // line (64 positions) of a record per lane and pass, so the layout puts what most jumps need on the first line:
 //   line 0:  [0, 9) the action keys | [9, 9 + sd) down-same area | [9 + sd, 9 + sd + su) up-same area
-//   lines 1 .. nbd:            the down-same keys in 64-key blocks (only if the array does not fit its area)
-//   lines nbd + 1 .. nbd+nbu:  the up-same keys in 64-key blocks (likewise)
+//   lines 1 .. nbd:            the down-same keys before the area's suffix in 64-key blocks (if it overflows the area)
+//   lines nbd + 1 .. nbd+nbu:  the up-same keys likewise
 //   from line 1 + nbd + nbu:   rad_deexc (nd) | rad_recomb (nr) | internal_down_lower (nr) | internal_up_higher (nt)
 // then the low halves of all positions (offset `hot`).  A same-ion array that fits its area (most levels) is
-// stored there whole; otherwise its area holds the last key of every block but the last (separators), so a search
-// reads line 0, then at most one block line: two passes.  The 55 area slots go to whichever array needs them.
+// stored there whole.  One that does not keeps the last key of every block (separators) there, followed by its last
+// md / mu keys (the suffix): separators and suffix are one ascending sequence, so a search of line 0 either ends in
+// the suffix (one pass) or names the block that holds the key (a second pass).  The suffix is what a blocked array's
+// share of line 0 adds to the layout of round 4 (separators only: every search of such an array took two passes,
+// 38 % of the up-same searches of the bench).  A suffix, because these are the low levels' upward arrays, and the
+// selections fall at their ends (stamps build, profiles/r5p1_stamps.txt: 80 % in the last quarter of arrays of
+// ~400 keys, 30 % in the last 48 keys; 0.0002 % in the first 48).  The 55 area slots go to whichever array needs them.
+#ifndef ARTIS_MA_SUFFIX
+#define ARTIS_MA_SUFFIX 1
+#endif
 struct MaLayout {
-  int sd, su;    // line-0 slots of the down / up array (its keys, or its block separators)
+  int sd, su;    // line-0 slots of the down / up array (its keys, or its block separators and suffix)
   int nbd, nbu;  // 64-key blocks of the down / up array outside line 0 (0: the array is on line 0)
+  int md, mu;    // keys of the down / up array stored whole on line 0 (the array's size if it fits)
   int sorted0;   // record position of the first rad_deexc key
   int hot;       // high-half positions = offset of the low halves
 };
+// blocks of an array of c keys whose line-0 area has s slots, and its line-0 suffix *m (negative: does not fit)
+static inline __host__ __device__ int ma_blocks(int c, int s, int *m) {
+  if (c <= s) {
+    *m = c;
+    return 0;
+  }
+#if ARTIS_MA_SUFFIX
+  // nb blocks of 64 and a suffix of s - nb keys: the least nb with 64 nb + s - nb >= c
+  const int nb = (c - s + 62) / 63;
+#else
+  const int nb = (c + 63) / 64;  // (round 4: the separators of all blocks but the last, no suffix)
+  if (nb - 1 > s) {
+    *m = -1;
+    return nb;
+  }
+#endif
+  *m = ARTIS_MA_SUFFIX ? s - nb : 0;
+  return nb;
+}
 // k_rpkt's per-block estimator accumulator (few-cell models: every update of the same few addresses would otherwise
 // serialise in the memory system's atomics)
 #define EST_LDS_DOUBLES 2048
@@ -156,34 +184,34 @@ static inline __host__ __device__ MaLayout ma_layout(int nd, int nu, int nr, int
     L.sd = MA_AREA / 2;
     L.su = MA_AREA - MA_AREA / 2;
   }
-  L.nbd = nd > L.sd ? (nd + 63) / 64 : 0;
-  L.nbu = nu > L.su ? (nu + 63) / 64 : 0;
+  L.nbd = ma_blocks(nd, L.sd, &L.md);
+  L.nbu = ma_blocks(nu, L.su, &L.mu);
   L.sorted0 = 64 * (1 + L.nbd + L.nbu);
   L.hot = L.sorted0 + nd + 2 * nr + nt;
   return L;
 }
-// a blocked array needs one separator slot per block but the last
+// a blocked array needs one separator slot per block but the last beside its prefix
 static inline __host__ __device__ bool ma_layout_ok(int nd, int nu) {
   const MaLayout L = ma_layout(nd, nu, 0, 0);
-  return (L.nbd == 0 || L.nbd - 1 <= L.sd) && (L.nbu == 0 || L.nbu - 1 <= L.su);
+  return L.md >= 0 && L.mu >= 0;
 }
-// record position of scratch position p (k_marates order: [9 totals | down nd | up nu | the sorted arrays]);
-// *sep: the separator position on line 0 the key is also stored at, or -1
+// separators on line 0 of a blocked array of nb blocks
+static inline __host__ __device__ int ma_nsep(int nb) { return ARTIS_MA_SUFFIX ? nb : nb - 1; }
+// key j of a same-ion array of c keys (area at a0, suffix m, nb blocks from record line lb): its record position;
+// *sep the separator position on line 0 the key is also stored at, or -1
+static inline __host__ __device__ int ma_same_pos(int j, int c, int a0, int m, int nb, int lb, int *sep) {
+  if (!nb) return a0 + j;
+  const int cb = c - m;  // keys in the blocks
+  if (j >= cb) return a0 + ma_nsep(nb) + (j - cb);
+  if (((j & 63) == 63 || j == cb - 1) && (j >> 6) < ma_nsep(nb)) *sep = a0 + (j >> 6);
+  return 64 * (lb + (j >> 6)) + (j & 63);
+}
+// record position of scratch position p (k_marates order: [9 totals | down nd | up nu | the sorted arrays])
 static inline __host__ __device__ int ma_rec_pos(const MaLayout &L, int p, int nd, int nu, int *sep) {
   *sep = -1;
   if (p < 9) return p;
-  if (p < 9 + nd) {  // down-same key j
-    const int j = p - 9;
-    if (!L.nbd) return 9 + j;
-    if ((j & 63) == 63 && (j >> 6) < L.nbd - 1) *sep = 9 + (j >> 6);
-    return 64 * (1 + (j >> 6)) + (j & 63);
-  }
-  if (p < 9 + nd + nu) {  // up-same key j
-    const int j = p - 9 - nd;
-    if (!L.nbu) return 9 + L.sd + j;
-    if ((j & 63) == 63 && (j >> 6) < L.nbu - 1) *sep = 9 + L.sd + (j >> 6);
-    return 64 * (1 + L.nbd + (j >> 6)) + (j & 63);
-  }
+  if (p < 9 + nd) return ma_same_pos(p - 9, nd, 9, L.md, L.nbd, 1, sep);                               // down-same
+  if (p < 9 + nd + nu) return ma_same_pos(p - 9 - nd, nu, 9 + L.sd, L.mu, L.nbu, 1 + L.nbd, sep);  // up-same
   return L.sorted0 + (p - 9 - nd - nu);
 }
 

@@ -2361,7 +2361,7 @@ DEVFN int ma_step_cached(const Ctx &K, const MaHot &H, const LocalCounters &L, a
       const bool down = sel == ARTIS_MA_ACTION_INTERNALDOWNSAME;
       const int nb = down ? lay.nbd : lay.nbu;
       m.base = down ? 9 : 9 + lay.sd;
-      m.end = nb ? nb - 1 : (down ? nd : nu);  // the separators, or the whole array
+      m.end = nb ? ma_nsep(nb) + (down ? lay.md : lay.mu) : (down ? nd : nu);  // separators and suffix, or the array
     } else {
       m.base = lay.sorted0 + ((sel == ARTIS_MA_ACTION_RADDEEXC)            ? 0
                               : (sel == ARTIS_MA_ACTION_RADRECOMB)         ? nd
@@ -2422,18 +2422,35 @@ DEVFN int ma_step_cached(const Ctx &K, const MaHot &H, const LocalCounters &L, a
   const int sel = m.sel;
   if (sel == ARTIS_MA_ACTION_INTERNALDOWNSAME || sel == ARTIS_MA_ACTION_INTERNALUPSAME) {
     const bool down = sel == ARTIS_MA_ACTION_INTERNALDOWNSAME;
-    const int cnt = down ? nd : nu, nb = down ? lay.nbd : lay.nbu;
-    if (nb && m.blk < 0) {  // separators searched: the key is in block lo (the last if no separator is above q2)
+    const int cnt = down ? nd : nu, nb = down ? lay.nbd : lay.nbu, suf = down ? lay.md : lay.mu;
+    // separators and suffix searched: the key is in block lo (round-4 layout: the last if no separator is above
+    // q2), or suffix entry lo - nb
+    if (nb && m.blk < 0 && lo < nb) {
       m.blk = lo;
       m.base = 64 * (1 + (down ? 0 : lay.nbd) + lo);
       m.lo = 0;
-      m.end = m.hi = min(64, cnt - 64 * lo);
+      m.end = m.hi = min(64, cnt - suf - 64 * lo);
       m.pline = m.base >> 6;
       MA_DIAG(16 + sel);
       return MA_PENDING;
     }
-    const int j = (m.blk >= 0 ? 64 * m.blk : 0) + lo;
+    const int j = !nb ? lo : (m.blk >= 0) ? 64 * m.blk + lo : cnt - suf + (lo - nb);
     const bool found = lo < m.end;
+#ifdef ARTIS_STAMPS
+    // where the up-same selections of blocked arrays fall: [9] count, [10] in the line-0 suffix, [11] the first
+    // 16, [12] the last 16, [13] the first `suffix` entries, [14] the sum of the array sizes, [15] the sum of the
+    // suffix sizes, [25 + q] quarter q of the array
+    if (!down && nb && L.diag && found) {
+      MA_DIAG(9);
+      if (j >= cnt - suf) MA_DIAG(10);
+      if (j < 16) MA_DIAG(11);
+      if (j >= cnt - 16) MA_DIAG(12);
+      if (j < suf) MA_DIAG(13);
+      atomicAdd(&L.diag[14], (unsigned long long)cnt);
+      atomicAdd(&L.diag[15], (unsigned long long)suf);
+      MA_DIAG(25 + min(3, 4 * j / cnt));
+    }
+#endif
     m.sel = -1;
     m.pline = 0;
     if (!found) {

@@ -52,6 +52,10 @@ struct WaveState {
   // {packet index, propagation cell, packet number, RNG counter}, then {element, ion, level, 0} for a new
   // activation or {-1 - unique level, 0, 0, jumps so far} for a walk parked by k_ma_exact (nullptr: no tickets)
   int4 *ma_pre;        // [2N]
+  // the F queue's records, written by the kernel that appends the deactivation (wave_push_mf): per slot
+  // {MaEnd code, ion, a, b}, {jumps, RNG counter, 0, 0} -- k_ma_finish reads them with the slot, coalesced, instead of
+  // gathering pend / pend_jumps / rng_n by packet index (three 64-byte sectors for 24 bytes); nullptr: those arrays
+  int4 *mf_rec;        // [2N]
   unsigned long long *stats;  // [48] diagnostics: per kernel class c: [4c] wave loop passes, [4c+1] busy
                               // lane-passes, [4c+2] wave cycles (s_memtime), [4c+3] refills;
                               // [16 + 4c] cycles in refill blocks, [17 + 4c] cycles in the work step; [40] exact
@@ -117,6 +121,15 @@ DEVFN void wave_push_ma(const WaveState &W, bool pred, int32_t idx, int where, i
       W.ma_pre[2 * (int64_t)slot] = make_int4(idx, where, number, (int)rng_n);
       W.ma_pre[2 * (int64_t)slot + 1] = b;
     }
+  }
+}
+// F-queue append with the deactivation's record (WaveState::mf_rec)
+DEVFN void wave_push_mf(const WaveState &W, bool pred, int32_t idx, int4 e, uint32_t jumps, uint32_t rng_n) {
+  const uint32_t slot = wave_reserve(&W.ctr[2 * QF], pred);
+  if (pred) {
+    W.q[QF][slot] = idx;
+    W.mf_rec[2 * (int64_t)slot] = e;
+    W.mf_rec[2 * (int64_t)slot + 1] = make_int4((int)jumps, (int)rng_n, 0, 0);
   }
 }
 DEVFN int4 ma_pre_activation(int element, int ion, int level) { return make_int4(element, ion, level, 0); }
@@ -666,6 +679,8 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   bool have = false, drained = false;
   int cur = (int)(blockIdx.x % (unsigned)nr), tried = 0;
   bool pendF = false, pendX = false;
+  int4 fe = make_int4(0, 0, 0, 0);  // a deactivation waiting for the F-queue append: its record (WaveState::mf_rec)
+  uint32_t fjumps = 0, frng = 0;
   unsigned long long jumps_sum = 0, trans_sum = 0, coop_sum = 0;
   unsigned long long st_pass = 0, st_busy = 0, st_refill = 0, st_trefill = 0, st_tstep = 0;
 #ifdef ARTIS_STAMPS
@@ -682,7 +697,10 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     if (!__any(have) || __popcll(imask) >= W.refill_ma) {
       st_refill++;
       const unsigned long long tr0 = wave_clock();
-      wave_push(W, QF, pendF, idx);
+      if (W.mf_rec)
+        wave_push_mf(W, pendF, idx, fe, fjumps, frng);
+      else
+        wave_push(W, QF, pendF, idx);
       wave_push(W, QX, pendX, idx);
       pendF = pendX = false;
       if (imask) {
@@ -845,9 +863,15 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
       if (have && r != MA_PENDING && (r != MA_CONTINUE || jumps >= MA_MAX_JUMPS)) {
         if (r == MA_CONTINUE) fail(K, ERR_STUCK, (int)rng.key1, 2);
         if (r > 0) {
-          W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
-          W.pend_jumps[idx] = jumps;
-          W.rng_n[idx] = rng.n;
+          if (W.mf_rec) {
+            fe = make_int4(e.code, e.ion, e.a, e.b);
+            fjumps = jumps;
+            frng = rng.n;
+          } else {
+            W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
+            W.pend_jumps[idx] = jumps;
+            W.rng_n[idx] = rng.n;
+          }
           pendF = true;  // -> k_ma_finish
         }
         jumps_sum += jumps;
@@ -916,6 +940,8 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
   // time: one queue atomic per 64 jumps instead of one per jump on the queue's counter
   int32_t pm = -1, pf = -1;
   int nm = 0, nf = 0;
+  int4 pf_e = make_int4(0, 0, 0, 0);  // the pending F appends' records (WaveState::mf_rec)
+  uint32_t pf_jumps = 0, pf_rng = 0;
   int pm_where = 0, pm_number = 0, pm_ul = 0;  // the pending M appends' pre-tickets (WaveState::ma_pre)
   uint32_t pm_rng = 0, pm_jumps = 0;
   auto flush = [&](bool all) {
@@ -924,13 +950,17 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
       nm = 0;
     }
     if (all || nf == 64) {
-      wave_push(W, QF, lane < nf, pf);
+      if (W.mf_rec)
+        wave_push_mf(W, lane < nf, pf, pf_e, pf_jumps, pf_rng);
+      else
+        wave_push(W, QF, lane < nf, pf);
       nf = 0;
     }
   };
   // lane 0's decision for this slot; a walk parked again: its level, jump count and RNG counter (lane 0's) and
   // cell / packet number (wave-uniform)
-  auto collect = [&](int32_t to_m, int32_t to_f, int where, int number, int ul, unsigned jumps, uint32_t rngn) {
+  auto collect = [&](int32_t to_m, int32_t to_f, int where, int number, int ul, unsigned jumps, uint32_t rngn,
+                     int4 fe) {
     const int32_t m = __builtin_amdgcn_readlane(to_m, 0), f = __builtin_amdgcn_readlane(to_f, 0);
     const int ul0 = __builtin_amdgcn_readlane(ul, 0);
     const uint32_t j0 = (uint32_t)__builtin_amdgcn_readlane((int)jumps, 0), r0 = (uint32_t)__builtin_amdgcn_readlane((int)rngn, 0);
@@ -946,7 +976,14 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
       nm++;
     }
     if (f >= 0) {
-      if (lane == nf) pf = f;
+      const int4 e0 = make_int4(__builtin_amdgcn_readlane(fe.x, 0), __builtin_amdgcn_readlane(fe.y, 0),
+                                __builtin_amdgcn_readlane(fe.z, 0), __builtin_amdgcn_readlane(fe.w, 0));
+      if (lane == nf) {
+        pf = f;
+        pf_e = e0;
+        pf_jumps = j0;
+        pf_rng = r0;
+      }
       nf++;
     }
     flush(false);
@@ -979,6 +1016,7 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
       if (ma_coop_needs_search(sel)) sel = ma_coop_search(K, k, ul, sel, x, t_mid, &j, probes);
       int res_ul = 0;
       unsigned res_jumps = 0;
+      int4 res_e = make_int4(0, 0, 0, 0);
       if (lane == 0) {
         MaLaneR mr;
         static_cast<MaLaneC &>(mr) = m;
@@ -997,14 +1035,15 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
             to_m = idx;
           }
         } else if (r > 0) {
-          W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
+          res_e = make_int4(e.code, e.ion, e.a, e.b);
+          if (!W.mf_rec) W.pend[idx] = res_e;
           lwork(L, WK_MA_JUMPS, mr.jumps);
           to_f = idx;  // -> k_ma_finish
         }
         res_ul = mr.ul;
         res_jumps = mr.jumps;
       }
-      collect(to_m, to_f, where, number, res_ul, res_jumps, rng.n);
+      collect(to_m, to_f, where, number, res_ul, res_jumps, rng.n, res_e);
       continue;
     }
     const int mgi = K.C.ne_mgi[k];
@@ -1102,12 +1141,12 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
           to_m = idx;
         }
       } else if (r > 0) {
-        W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
+        if (!W.mf_rec) W.pend[idx] = make_int4(e.code, e.ion, e.a, e.b);
         lwork(L, WK_MA_JUMPS, m.jumps);
         to_f = idx;  // -> k_ma_finish
       }
     }
-    collect(to_m, to_f, where, number, m.ul, m.jumps, rng.n);
+    collect(to_m, to_f, where, number, m.ul, m.jumps, rng.n, make_int4(e.code, e.ion, e.a, e.b));
   }
   flush(true);
   if (lane == 0 && n_exact) {
@@ -1158,10 +1197,17 @@ __global__ __launch_bounds__(WAVE_BLOCK, MA_FINISH_MINW) void k_ma_finish(const 
       pkt_load(soa, n, idx, p);
       x.nts = nts;
       x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
-      x.rng.n = W.rng_n[idx];
-      const int4 pd = W.pend[idx];
-      e = MaEnd{pd.x, pd.y, pd.z, pd.w};
-      jumps = W.pend_jumps[idx];
+      if (W.mf_rec) {
+        const int4 pd = W.mf_rec[2 * (int64_t)slot], pj = W.mf_rec[2 * (int64_t)slot + 1];
+        e = MaEnd{pd.x, pd.y, pd.z, pd.w};
+        jumps = (unsigned)pj.x;
+        x.rng.n = (uint32_t)pj.y;
+      } else {
+        x.rng.n = W.rng_n[idx];
+        const int4 pd = W.pend[idx];
+        e = MaEnd{pd.x, pd.y, pd.z, pd.w};
+        jumps = W.pend_jumps[idx];
+      }
       if (e.code == MA_END_FB) {  // ma_finish_fb's continuum and its first draw (select_continuum_nu's)
         const int uiu = K.T.level_ui[e.b];
         fb.want = true;
@@ -1177,7 +1223,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MA_FINISH_MINW) void k_ma_finish(const 
     bool live = false;
     if (have) {
       ma_finish_inl(x, p, e, jumps, fb.want ? fb_nu : -1.);
-      W.pend[idx].x = 0;
+      if (!W.mf_rec) W.pend[idx].x = 0;
       pkt_store(soa, n, idx, p);
       W.rng_n[idx] = x.rng.n;
       live = x.ok && p.prop_time < t2;
