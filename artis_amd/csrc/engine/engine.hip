@@ -870,6 +870,7 @@ struct Engine {
   bool ma_bin_blk = true;         // few cells: block-local M-queue binning (ARTIS_GPU_MA_BIN_BLK=0: per-entry atomics)
   bool ma_pre_on = true;          // M-queue pre-tickets (WaveState::ma_pre; ARTIS_GPU_MA_PRE=0: gathered by the scatter)
   bool mf_rec_on = true;          // F-queue records (WaveState::mf_rec; ARTIS_GPU_MF_REC=0: the per-packet pend arrays)
+  bool bin_push_on = true;        // M queue binned by its producers (WaveState::bin_push; ARTIS_GPU_BIN_PUSH=0: k_ma_bin)
   int rpkt_walk = -1;             // k_rpkt's bounded line walk: -1 by the previous transport's lines per step, 0 off, 1 on
   bool rpkt_coop = true;          // detailed-bf models: wave-made continuum sums in k_rpkt (ARTIS_GPU_RPKT_COOP=0: per lane)
   std::vector<hipEvent_t> vev;  // (start, end) pairs around the k_vpkt launches of the last update
@@ -1329,11 +1330,16 @@ int run_wavefront(int64_t n, int nts, double t2) {
   if (!(G.K.C.have_macache && W.ma_binned)) W.ma_tick = nullptr;  // tickets: cached walk over the binned queue
   if (!W.ma_tick || !G.ma_pre_on) W.ma_pre = nullptr;            // pre-tickets written by the queue's producers
   if (!G.mf_rec_on) W.mf_rec = nullptr;                           // F-queue records (else pend / pend_jumps / rng_n)
+  // the M queue's producers bin it as they append (many cells only: the block-local binning of few-cell models
+  // counts in LDS; not with the binned R queue, which uses the same counts array)
+  W.bin_push = W.ma_binned && G.bin_push_on && !G.r_binned && G.K.C.n_nonempty > 0 &&
+               !(G.ma_bin_blk && G.K.C.n_nonempty + 1 <= MA_BIN_LDS);
   const unsigned grid = (unsigned)G.wave_grid;
   if (int rc = sync_ctx()) return rc;
   G.tev_used = 0;
   HIPCHK(hipMemsetAsync(W.stats, 0, 48 * sizeof(unsigned long long), G.stream));
   HIPCHK(hipMemsetAsync(W.ctr, 0, NQUEUES * 2 * sizeof(uint32_t), G.stream));
+  if (W.bin_push) HIPCHK(hipMemsetAsync(W.bins, 0, (size_t)(G.K.C.n_nonempty + 1) * sizeof(uint32_t), G.stream));
   TSTART(3);
   k_classify<<<(unsigned)((n + WAVE_BLOCK - 1) / WAVE_BLOCK), WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, t2);
   if (G.K.T.g_nlines) {  // pellets / gammas / leptons -> k-packets ahead of the rounds (counted with classify)
@@ -1414,15 +1420,20 @@ int run_wavefront(int64_t n, int nts, double t2) {
     TSTART(4);  // class 4: the macro-atom queue binning (class 1 is k_ma alone)
     if (W.ma_binned) {
       const int nne = G.K.C.n_nonempty;
-      HIPCHK(hipMemsetAsync(W.bins, 0, (size_t)(nne + 1) * sizeof(uint32_t), G.stream));
       // few cells: block-local counts (one device atomic per block and bin instead of one per queue entry)
       const bool blk = G.ma_bin_blk && nne + 1 <= MA_BIN_LDS;
-      if (blk)
-        k_ma_bin_blk<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa);
-      else
-        k_ma_bin<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa);
+      if (!W.bin_push) {
+        HIPCHK(hipMemsetAsync(W.bins, 0, (size_t)(nne + 1) * sizeof(uint32_t), G.stream));
+        if (blk)
+          k_ma_bin_blk<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa);
+        else
+          k_ma_bin<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa);
+      }
       HIPCHK(hipcub::DeviceScan::ExclusiveSum(G.d_scan_tmp, G.scan_tmp_bytes, W.bins, G.d_binoffs, nne + 1,
                                               G.stream));
+      // (the counts are the scan's input only: the next round's appends -- k_ma_exact's and k_kpkt's in this
+      // round, then k_rpkt's -- count from zero)
+      if (W.bin_push) HIPCHK(hipMemsetAsync(W.bins, 0, (size_t)(nne + 1) * sizeof(uint32_t), G.stream));
       if (blk)
         k_ma_scatter_blk<<<grid, WAVE_BLOCK, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, G.d_binoffs);
       else
@@ -3081,6 +3092,8 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     G.ma_pre_on = !(mp && mp[0] == '0');
     const char *mf = getenv("ARTIS_GPU_MF_REC");
     G.mf_rec_on = !(mf && mf[0] == '0');
+    const char *bp = getenv("ARTIS_GPU_BIN_PUSH");
+    G.bin_push_on = !(bp && bp[0] == '0');
     const char *bb = getenv("ARTIS_GPU_MA_BIN_BLK");
     G.ma_bin_blk = !(bb && bb[0] == '0');
     const char *xr = getenv("ARTIS_GPU_MA_XCD");

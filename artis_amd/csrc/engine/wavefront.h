@@ -39,6 +39,8 @@ struct WaveState {
   uint32_t *xhead;     // [8] fetch heads of the per-XCD ranges of ma_sorted
   int ma_ranges;       // 8: blocks on XCD x take range x first (then steal), 1: one shared range
   int ma_binned;       // 1: k_ma reads ma_sorted, 0: k_ma reads q[QM]
+  int bin_push;        // 1: the M queue's producers write each slot's bin (ma_key) and count it (bins) as they append
+                       // it, so the binning is the scan and k_ma_scatter (no k_ma_bin pass over the queue)
   int r_binned;        // 1: this k_rpkt launch reads the R queue binned by cell from ma_sorted (k_r_bin / k_r_scatter)
   int refill_min;      // a wave refetches work (and flushes its queue appends) once this many lanes are idle
   int refill_ma;       // the same for k_ma (a macro-atom refill is cheap: one coalesced ticket read)
@@ -113,10 +115,16 @@ DEVFN void wave_push(const WaveState &W, int q, bool pred, int32_t idx) {
   if (pred) W.q[q][slot] = idx;
 }
 // M-queue append with the walk's pre-ticket (WaveState::ma_pre): a new macro-atom activation of packet p
-DEVFN void wave_push_ma(const WaveState &W, bool pred, int32_t idx, int where, int number, uint32_t rng_n, int4 b) {
+// bin: the walk's M-queue bin (ma_push_bin), or -1 when the producers do not bin
+DEVFN void wave_push_ma(const WaveState &W, bool pred, int32_t idx, int where, int number, uint32_t rng_n, int4 b,
+                        int bin) {
   const uint32_t slot = wave_reserve(&W.ctr[2 * QM], pred);
   if (pred) {
     W.q[QM][slot] = idx;
+    if (bin >= 0) {
+      W.ma_key[slot] = bin;
+      atomicAdd(&W.bins[bin], 1u);
+    }
     if (W.ma_pre) {
       W.ma_pre[2 * (int64_t)slot] = make_int4(idx, where, number, (int)rng_n);
       W.ma_pre[2 * (int64_t)slot + 1] = b;
@@ -131,6 +139,11 @@ DEVFN void wave_push_mf(const WaveState &W, bool pred, int32_t idx, int4 e, uint
     W.mf_rec[2 * (int64_t)slot] = e;
     W.mf_rec[2 * (int64_t)slot + 1] = make_int4((int)jumps, (int)rng_n, 0, 0);
   }
+}
+// the M-queue bin of a walk in propagation cell `where` (DevCells::ma_bin) when the producers bin
+// (WaveState::bin_push), else -1
+DEVFN int ma_push_bin(const Ctx &K, const WaveState &W, bool pred, int where) {
+  return (W.bin_push && pred) ? K.C.ma_bin[K.C.ne_index[cell_mgi(K, where)]] : -1;
 }
 DEVFN int4 ma_pre_activation(int element, int ion, int level) { return make_int4(element, ion, level, 0); }
 DEVFN int4 ma_pre_resume(int ul, unsigned jumps) { return make_int4(-1 - ul, 0, 0, (int)jumps); }
@@ -189,7 +202,7 @@ __global__ void k_classify(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *
       number = hi32(soa[PW(n, i, 33)]);
       b = ma_pre_activation(lo32(w36), hi32(w36), lo32(w37));
     }
-    wave_push_ma(W, toM, (int32_t)i, where, number, 0u, b);
+    wave_push_ma(W, toM, (int32_t)i, where, number, 0u, b, ma_push_bin(K, W, toM, where));
   }
   wave_push(W, QK, toK, (int32_t)i);
   wave_push(W, QG, toG, (int32_t)i);
@@ -265,7 +278,8 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
       st_refill++;
       const unsigned long long tr0 = wave_clock();
       // appends deferred from the lanes' last retirement (a macro-atom: p still holds the retired packet)
-      wave_push_ma(W, pendM, idx, p.where, p.number, x.rng.n, ma_pre_activation(p.ma_element, p.ma_ion, p.ma_level));
+      wave_push_ma(W, pendM, idx, p.where, p.number, x.rng.n, ma_pre_activation(p.ma_element, p.ma_ion, p.ma_level),
+                   ma_push_bin(K, W, pendM, p.where));
       wave_push(W, QK, pendK, idx);
       wave_push(W, QR, pendR, idx);  // packets parked on a full virtual-packet buffer (resumed by the host)
       pendM = pendK = pendR = false;
@@ -946,7 +960,8 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
   uint32_t pm_rng = 0, pm_jumps = 0;
   auto flush = [&](bool all) {
     if (all || nm == 64) {
-      wave_push_ma(W, lane < nm, pm, pm_where, pm_number, pm_rng, ma_pre_resume(pm_ul, pm_jumps));
+      wave_push_ma(W, lane < nm, pm, pm_where, pm_number, pm_rng, ma_pre_resume(pm_ul, pm_jumps),
+                   ma_push_bin(K, W, lane < nm, pm_where));
       nm = 0;
     }
     if (all || nf == 64) {
@@ -1284,7 +1299,7 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_gamma(const Ctx *__restrict__ ct
       m_b = ma_pre_activation(p.ma_element, p.ma_ion, p.ma_level);
     }
     wave_push(W, QR, toR, idx);
-    wave_push_ma(W, toM, idx, m_where, m_number, m_rng, m_b);
+    wave_push_ma(W, toM, idx, m_where, m_number, m_rng, m_b, ma_push_bin(K, W, toM, m_where));
     wave_push(W, QK, toK, idx);
   }
   block_counters_flush(K, s_ctr, s_work);
@@ -1347,7 +1362,8 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_kpkt(const Ctx *__restrict__ ctx
       toM = x.ok && p.prop_time < t2 && p.type == ARTIS_TYPE_MA;
     }
     wave_push(W, QR, toR, idx);
-    wave_push_ma(W, toM, idx, p.where, p.number, x.rng.n, ma_pre_activation(p.ma_element, p.ma_ion, p.ma_level));
+    wave_push_ma(W, toM, idx, p.where, p.number, x.rng.n, ma_pre_activation(p.ma_element, p.ma_ion, p.ma_level),
+                 ma_push_bin(K, W, toM, p.where));
   }
   block_counters_flush(K, s_ctr, s_work);
 }
