@@ -3101,9 +3101,10 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     const char *rf = getenv("ARTIS_GPU_REFILL");
     G.W.refill_min = rf ? std::max(1, std::min(64, atoi(rf))) : 32;
     // k_ma refills from one coalesced ticket read, so it refills early (1e7-packet bench, before tickets:
-    // 32 idle lanes 2212 ms, 16: 2064 ms, 8: 2042 ms)
+    // 32 idle lanes 2212 ms, 16: 2064 ms, 8: 2042 ms; round 5, with the line-0 suffix and the F-queue records:
+    // 4: 2578 ms, 8: 1694, 12: 1559, 14: 1568, 16: 1581, 20: 1617, 24: 1659; profiles/r5s_refill_sweep.txt)
     const char *rfm = getenv("ARTIS_GPU_REFILL_MA");
-    G.W.refill_ma = rfm ? std::max(1, std::min(64, atoi(rfm))) : 8;
+    G.W.refill_ma = rfm ? std::max(1, std::min(64, atoi(rfm))) : 12;
     const char *oc = getenv("ARTIS_GPU_MA_OCC");
     G.ma_occ = (oc && oc[0] == '8') ? 8 : 1;
     const char *cm = getenv("ARTIS_GPU_MA_COOP_MAX");
