@@ -135,11 +135,18 @@ __global__ void k_bfcells(Ctx K, const int32_t *target_ul, const int32_t *target
     // bf_contribution's inclusion rule (rpkt.cc:1116-1118): DETAILED_BF_ESTIMATORS_ON includes every continuum of
     // an element present in the cell, otherwise the ion must hold > 1e-6 of the cell's nuclei (or the level is the
     // ground level)
+    const double depratio = nnupperionlevel / nnlevel * nne * sf;
+    if (!K.C.ionpop) {
+      // the nebular update_grid's context (artis_gpu_update_grid_nlte): no ion populations of its active cells, and
+      // only the departure ratio is read there
+      K.C.bfcell[(int64_t)k * nb + i].y = depratio;
+      return;
+    }
     const int ui = uion(K, element, ion);
     const bool incl = K.R.detailed_bf
                           ? K.C.elem_abundance[(int64_t)mgi * K.T.nelements + element] > 0
                           : ((K.C.ionpop[(int64_t)k * K.T.nions_total + ui] / (double)K.C.nnetot[mgi] > 1.e-6) || level == 0);
-    K.C.bfcell[(int64_t)k * nb + i] = make_double2(incl ? nnlevel : 0., nnupperionlevel / nnlevel * nne * sf);
+    K.C.bfcell[(int64_t)k * nb + i] = make_double2(incl ? nnlevel : 0., depratio);
   } else {
     const int slot = r - (int)nb;
     const int ul = target_ul[slot];
@@ -2106,6 +2113,7 @@ int artis_gpu_update_grid_nlte(const artis_nt_shells *nt, const artis_nlte_param
   KN.C.pops = d_pops;
   KN.C.corrphot = d_corr;
   KN.C.bfcell = d_depr;
+  KN.C.ionpop = nullptr;  // (k_bfcells writes only the departure ratios here)
   KN.C.ne_mgi = d_act;
   KN.C.n_nonempty = 0;
   KN.C.linecoef = nullptr;
@@ -2902,6 +2910,9 @@ int artis_gpu_vpkt_init(const artis_vpkt_params *vp) {
   V.spawn = G.d_vpkt_spawn;
   V.cap = G.vpkt_spawn_cap;
   V.on = 1;
+  // the negative-coefficient flag belongs to the per-cell tables (read back by artis_gpu_upload_cellstate), not to
+  // the vpkt parameters: keep it when vpkt_init runs after an upload
+  V.neg_coef = G.K.V.neg_coef;
   G.K.V = V;
   G.vpkt_cap_param = vp->spawn_capacity;
   return artis_gpu_vpkt_zero();
@@ -3056,9 +3067,23 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     return ARTIS_ERR_UNSUPPORTED;
   }
   if (G.initialised) artis_gpu_finalize();
-  if (g->grid_type != ARTIS_GRID_UNIFORM) {
-    G.last_error = "only GRID_UNIFORM is propagated by this build";
+  if (g->grid_type != ARTIS_GRID_UNIFORM && g->grid_type != ARTIS_GRID_SPHERICAL1D) {
+    G.last_error = "grid_type must be GRID_UNIFORM or GRID_SPHERICAL1D";
     return ARTIS_ERR_UNSUPPORTED;
+  }
+  if (g->grid_type == ARTIS_GRID_SPHERICAL1D) {
+    // spherical1d_grid_setup (grid.cc:2104-2131): one propagation cell per model shell, cellindex == mgi (or
+    // npts_model for an empty shell), the radial extent at tmin of every shell given
+    bool ok = g->ncoordgrid[0] == g->ngrid && g->ncoordgrid[1] == 1 && g->ncoordgrid[2] == 1 &&
+              g->ngrid == g->npts_model && g->modelcell_wid_init && g->cell_mgi && g->cell_pos_min;
+    for (int c = 0; ok && c < g->ngrid; c++)
+      ok = (g->cell_mgi[c] == c || g->cell_mgi[c] == g->npts_model) && g->modelcell_wid_init[c] > 0 &&
+           g->cell_pos_min[3 * (int64_t)c] >= 0;
+    if (!ok) {
+      G.last_error = "GRID_SPHERICAL1D needs ncoordgrid = {npts_model, 1, 1}, cell_mgi[c] in {c, npts_model}, "
+                     "modelcell_wid_init > 0 and radii >= 0";
+      return ARTIS_ERR_BAD_ARGUMENT;
+    }
   }
   G.device = device;
   HIPCHK(hipSetDevice(device));
@@ -3367,6 +3392,9 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   GG.npts_model = g->npts_model;
   rc |= dupload(&GG.cell_pos_min, g->cell_pos_min, (size_t)g->ngrid * 3);
   rc |= dupload(&GG.cell_mgi, g->cell_mgi, g->ngrid);
+  GG.spherical = g->grid_type == ARTIS_GRID_SPHERICAL1D;
+  GG.cell_wid = nullptr;
+  if (GG.spherical) rc |= dupload(&GG.cell_wid, g->modelcell_wid_init, g->ngrid);
   GG.coordmax0 = g->coordmax[0];
   GG.tmin = g->tmin;
   GG.tmax = g->tmax;
@@ -3508,10 +3536,14 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     const int mgi = g->cell_mgi[c];
     if (mgi >= 0 && mgi < np) {
       double r2 = 0.;
-      for (int d = 0; d < 3; d++) {
-        double x = g->cell_pos_min[3 * (int64_t)c + d];
-        if (g->grid_type == ARTIS_GRID_UNIFORM) x += g->coordmax[d] / std::max(1, g->ncoordgrid[d]);
-        r2 += x * x;
+      if (g->grid_type == ARTIS_GRID_SPHERICAL1D) {
+        const double r = g->cell_pos_min[3 * (int64_t)c] + 0.5 * g->modelcell_wid_init[c];  // get_cellradialpos
+        r2 = r * r;
+      } else {
+        for (int d = 0; d < 3; d++) {
+          const double x = g->cell_pos_min[3 * (int64_t)c + d] + g->coordmax[d] / std::max(1, g->ncoordgrid[d]);
+          r2 += x * x;
+        }
       }
       rmin[mgi] = std::min(rmin[mgi], r2);
       ne_index[mgi] = 0;

@@ -218,7 +218,9 @@ static inline __host__ __device__ int ma_rec_pos(const MaLayout &L, int p, int n
 struct DevGeom {
   int32_t ncoordgrid[3];
   int32_t ngrid, npts_model;
+  int32_t spherical;        // GRID_SPHERICAL1D (boundary.cc:136-140, 234-244): radial shells, cellindex == mgi
   const double *cell_pos_min;
+  const double *cell_wid;   // [ngrid] wid_init(cellindex) of the spherical grid (grid.cc:76-91); nullptr otherwise
   const int32_t *cell_mgi;
   double coordmax0, tmin, rmax, wid, tmax, vmax;
   const double *ts_start, *ts_width, *ts_mid;

@@ -412,7 +412,7 @@ DEVNI void do_gamma(Tx &x, Pkt &p, double t2) {
   const double tau_current = 0.0;
   int snext = -1;
   double sdist = boundary_cross(x, p, &snext);
-  const double maxsdist = K.G.rmax * p.prop_time / K.G.tmin;
+  const double maxsdist = max_sdist(K, p, sdist);
   if (sdist > maxsdist) {
     x.err(ERR_SDIST, p.number, p.where);
     return;

@@ -37,6 +37,7 @@ enum : int32_t {
   ERR_NONFINITE = 13,
   ERR_GAMMA = 14,  // an abort() path of the pellet / gamma code (aux = which)
   ERR_VPKT_OVERFLOW = 15,  // the virtual-packet spawn buffer of one event round is full
+  ERR_SHELL = 16,  // get_shellcrossdist's consistency checks (boundary.cc:19, 34, 61-62, 95: assert_always)
 };
 
 struct __attribute__((aligned(16))) Ctx {

@@ -542,8 +542,10 @@ DEVFN double te_col_exc_fast(const TeExcItem &it, const TeExcT &f, double inv_ls
   }
   return C;
 }
-// kpkt.cc:41-67 get_cooling_ion_coll_exc for one ion: its own serial sum over levels and up-transitions
-DEVNI double te_coll_exc_ion(const Ctx &K, const TeDev &D, const TeState &s, int ui, float T_e, float nne) {
+// kpkt.cc:41-67 get_cooling_ion_coll_exc for one ion: its own serial sum over levels and up-transitions.  exact: the
+// reference's expression term for term (te_col_exc, as k_cooling) -- the stored evaluation, whose totalcooling and
+// cooling_contrib_ion the next transport's k-packet ion selection reads; the Brent iterations take te_col_exc_fast.
+DEVNI double te_coll_exc_ion(const Ctx &K, const TeDev &D, const TeState &s, int ui, float T_e, float nne, bool exact) {
   const int e = K.T.ion_element[ui];
   const int ul0 = K.T.ion_uniqueleveloffset[ui];
   double C_exc = 0.;
@@ -554,8 +556,16 @@ DEVNI double te_coll_exc_ion(const Ctx &K, const TeDev &D, const TeState &s, int
     const int nuptrans = K.T.level_nuptrans[ul];
     if (nuptrans == 0) continue;
     const double nnlevel = te_levelpop(K, D, s, e, ui, level);
-    const double inv_lsw = 1. / (double)K.T.level_stat_weight[ul];
+    const double statweight = K.T.level_stat_weight[ul];
+    const double inv_lsw = 1. / statweight;
     const TeExcItem *it = K.T.exc_items + K.T.level_uptrans_offset[ul];
+    if (exact) {
+      for (int ii = 0; ii < nuptrans; ii++) {
+        const TeExcItem x = it[ii];
+        C_exc += nnlevel * te_col_exc(x, T_e, nne, statweight) * x.epsilon_trans;
+      }
+      continue;
+    }
 #pragma unroll 2
     for (int ii = 0; ii < nuptrans; ii++) {
       const TeExcItem x = it[ii];
@@ -579,7 +589,7 @@ DEVNI void te_cooling_rates(const Ctx &K, const TeDev &D, const TeState &s, TeRa
   for (int ub = 0; ub < ni; ub += s.g) {
     const int my_ui = ub + s.sub;
     double mine = 0.;
-    if (my_ui < ni) mine = te_coll_exc_ion(K, D, s, my_ui, T_e, nne);
+    if (my_ui < ni) mine = te_coll_exc_ion(K, D, s, my_ui, T_e, nne, store);
     for (int j = 0; j < s.g && ub + j < ni; j++) {
       const double C_exc = __shfl(mine, s.lane0 + j, 64);
       const int ui = ub + j;

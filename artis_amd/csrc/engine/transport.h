@@ -331,9 +331,127 @@ DEVNI void escat_rpkt(Tx &x, Pkt &p) {
 }
 
 // ------------------------------------------------------------------------------------------ boundary
-// boundary.cc:101-330 (GRID_UNIFORM)
+// boundary.cc:14-99 get_shellcrossdist: the closest forward distance of the ray to an expanding spherical shell, -1
+// without a forward intersection (or a tangential one).  The reference's assert_always checks set *bad (-> ERR_SHELL).
+DEVFN double get_shellcrossdist(const double pos[3], const double dir[3], const double shellradius,
+                                const bool isinnerboundary, const double tstart, bool *bad) {
+  if (!(shellradius > 0)) *bad = true;
+  const double speed = vec_len(dir) * ARTIS_CLIGHT_PROP;
+  const double a = dot(dir, dir) - pow(shellradius / tstart / speed, 2);
+  const double b = 2 * (dot(dir, pos) - pow(shellradius, 2) / tstart / speed);
+  const double c = dot(pos, pos) - pow(shellradius, 2);
+  const double discriminant = pow(b, 2) - 4 * a * c;
+  if (discriminant < 0) {
+    if (!(shellradius < vec_len(pos))) *bad = true;
+    return -1;
+  }
+  if (discriminant > 0) {
+    double d1 = (-b + sqrt(discriminant)) / 2 / a;
+    double d2 = (-b - sqrt(discriminant)) / 2 / a;
+    double posfinal1[3], posfinal2[3];
+    for (int d = 0; d < 3; d++) {  // cblas_dcopy + cblas_daxpy
+      posfinal1[d] = pos[d] + d1 * dir[d];
+      posfinal2[d] = pos[d] + d2 * dir[d];
+    }
+    const double shellradiusfinal1 = shellradius / tstart * (tstart + d1 / speed);
+    const double shellradiusfinal2 = shellradius / tstart * (tstart + d2 / speed);
+    if (!(fabs(vec_len(posfinal1) / shellradiusfinal1 - 1.) < 1e-3)) *bad = true;
+    if (!(fabs(vec_len(posfinal2) / shellradiusfinal2 - 1.) < 1e-3)) *bad = true;
+    // solutions that would enter the boundary from the wrong radial direction do not count
+    if (isinnerboundary) {
+      if (dot(posfinal1, dir) > 0.) d1 = -1;
+      if (dot(posfinal2, dir) > 0.) d2 = -1;
+    } else {
+      if (dot(posfinal1, dir) < 0.) d1 = -1;
+      if (dot(posfinal2, dir) < 0.) d2 = -1;
+    }
+    if (d1 < 0 && d2 < 0) return -1;
+    if (d2 < 0) return d1;
+    if (d1 < 0) return d2;
+    return fmin(d1, d2);
+  }
+  // exactly one (tangential) intersection: ignored
+  if (!(shellradius <= vec_len(pos))) *bad = true;
+  return -1.;
+}
+
+// boundary.cc:101-330, GRID_SPHERICAL1D: the radial coordinate and the two expanding shells of the cell
+DEVFN double boundary_cross_sph(const Ctx &K, Pkt &p, int *snext, bool *bad) {
+  const double tstart = p.prop_time;
+  const int cellindex = p.where;
+  const double tmin = K.G.tmin;
+  const int n0 = K.G.ncoordgrid[0];
+  const double initpos = vec_len(p.pos);
+  const double cmin = K.G.cell_pos_min[(int64_t)cellindex * 3];
+  const double cmax = cmin + K.G.cell_wid[cellindex];  // get_cellcoordmax: pos_min + wid_init(cellindex)
+  const double vel = dot(p.pos, p.dir) / vec_len(p.pos) * ARTIS_CLIGHT_PROP;  // radial velocity
+  int last_cross = p.last_cross;
+  for (int flip = 0; flip < 2; flip++) {
+    const int direction = flip ? ARTIS_POS_X : ARTIS_NEG_X;
+    const int invdirection = !flip ? ARTIS_POS_X : ARTIS_NEG_X;
+    const int cellindexstride = flip ? -1 : 1;
+    bool outside;
+    if (flip)
+      outside = initpos < (cmin / tmin * tstart - 10.);
+    else
+      outside = initpos > (cmax / tmin * tstart + 10.);
+    if (outside && (last_cross != direction)) {
+      if ((vel - (initpos / tstart)) > 0) {
+        if ((cellindex == (n0 - 1) && cellindexstride > 0) || (cellindex == 0 && cellindexstride < 0)) {
+          *snext = -99;
+          return 0;
+        }
+        *snext = p.where + cellindexstride;
+        p.last_cross = invdirection;
+        return 0;
+      }
+      last_cross = direction;
+    }
+  }
+  last_cross = ARTIS_NONE;  // the shell distances below exclude the wrong radial directions themselves
+  const double r_inner = cmin * tstart / tmin;
+  const double d_inner = (r_inner > 0.) ? get_shellcrossdist(p.pos, p.dir, r_inner, true, tstart, bad) : -1.;
+  const double tminb = d_inner / ARTIS_CLIGHT_PROP;
+  const double r_outer = cmax * tstart / tmin;
+  const double d_outer = get_shellcrossdist(p.pos, p.dir, r_outer, false, tstart, bad);
+  const double tmaxb = d_outer / ARTIS_CLIGHT_PROP;
+  double time = 1.e99;
+  if ((tmaxb > 0) && (tmaxb < time) && (last_cross != ARTIS_NEG_X)) {
+    time = tmaxb;
+    if (cellindex == (n0 - 1)) {
+      *snext = -99;
+    } else {
+      *snext = p.where + 1;
+      p.last_cross = ARTIS_POS_X;
+    }
+  }
+  if ((tminb > 0) && (tminb < time) && (last_cross != ARTIS_POS_X)) {
+    time = tminb;
+    if (cellindex == 0) {
+      *snext = -99;
+    } else {
+      *snext = p.where - 1;
+      p.last_cross = ARTIS_NEG_X;
+    }
+  }
+  return ARTIS_CLIGHT_PROP * time;
+}
+
+// rpkt.cc:659-661, gammapkt.cc:551-553: the largest plausible boundary distance of a step
+DEVFN double max_sdist(const Ctx &K, const Pkt &p, double sdist) {
+  return K.G.spherical ? 2 * K.G.rmax * (p.prop_time + sdist / ARTIS_CLIGHT_PROP) / K.G.tmin
+                       : K.G.rmax * p.prop_time / K.G.tmin;
+}
+
+// boundary.cc:101-330 (GRID_UNIFORM; GRID_SPHERICAL1D in boundary_cross_sph)
 DEVFN double boundary_cross(Tx &x, Pkt &p, int *snext) {
   const Ctx &K = x.K;
+  if (__builtin_expect(__builtin_amdgcn_readfirstlane(K.G.spherical), 0)) {
+    bool bad = false;
+    const double d = boundary_cross_sph(K, p, snext, &bad);
+    if (bad) x.err(ERR_SHELL, p.number, p.where);
+    return d;
+  }
   const double tstart = p.prop_time;
   const int cellindex = p.where;
   const double tmin = K.G.tmin;
@@ -1557,7 +1675,7 @@ DEVFN int rpkt_step_begin(Tx &x, Pkt &p, double t2, RStep &S) {
   S.find_nextline = false;
   S.eventtype = -1;
   if (S.cross0) return RSTEP_END;
-  const double maxsdist = K.G.rmax * p.prop_time / K.G.tmin;
+  const double maxsdist = max_sdist(K, p, S.sdist);
   if (S.sdist > maxsdist) {
     x.err(ERR_SDIST, p.number, p.where);
     return RSTEP_DONE;

@@ -1252,7 +1252,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MA_FINISH_MINW) void k_ma_finish(const 
 // pellets, gamma rays and non-thermal leptons (gamma.h): one packet per workitem, grid-stride over the G queue,
 // each advanced until it becomes a k-packet (-> K queue), escapes or reaches t2.  Runs once per timestep before
 // the r-packet / macro-atom / k-packet rounds (nothing on those paths turns back into this family).
-__global__ __launch_bounds__(WAVE_BLOCK) void k_gamma(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa,
+__global__ __launch_bounds__(WAVE_BLOCK, 3) void k_gamma(const Ctx *__restrict__ ctxp, WaveState W, uint64_t *__restrict__ soa,
                                                       int64_t n, int nts, double t2) {
   CTX_IN_LDS(ctxp)
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];

@@ -69,6 +69,7 @@ struct Model {
   // ---- grid
   int ngrid = 0, npts_model = 0;
   std::vector<double> cell_pos_min;
+  std::vector<double> cell_wid;  // GRID_SPHERICAL1D: wid_init(cellindex) = (vout - v_inner) tmin (grid.cc:76-91)
   std::vector<int32_t> cell_mgi;
   std::vector<double> ts_start, ts_width, ts_mid;
   std::vector<double> mgi_rho_tmin;  // density at tmin
@@ -669,6 +670,35 @@ void build_atomic(Model &m, std::mt19937_64 &rng) {
 
 void finish_geometry(Model &m);
 
+// GRID_SPHERICAL1D: spherical1d_grid_setup (grid.cc:2104-2131) with the spherical branch of map_1dmodeltogrid
+// (grid.cc:910-940): one propagation cell per shell, cellindex == mgi (npts_model for a shell without density),
+// pos_min[0] = v_inner tmin, wid_init = (vout - v_inner) tmin
+static bool spherical(const Model &m) { return m.geom.grid_type == ARTIS_GRID_SPHERICAL1D; }
+
+static void spherical_grid(Model &m, const double *vout) {
+  const int np = m.npts_model;
+  m.ngrid = np;
+  m.cell_pos_min.assign((size_t)np * 3, 0.);
+  m.cell_wid.assign(np, 0.);
+  m.cell_mgi.assign(np, np);
+  for (int c = 0; c < np; c++) {
+    const double v_inner = c > 0 ? vout[c - 1] : 0.;
+    m.cell_pos_min[(size_t)c * 3] = v_inner * m.tmin;
+    m.cell_wid[c] = (vout[c] - v_inner) * m.tmin;
+    m.cell_mgi[c] = (vout[c] >= 0. && m.mgi_rho_tmin[c] > 0) ? c : np;
+  }
+  m.geom.grid_type = ARTIS_GRID_SPHERICAL1D;
+}
+
+// vol_init_gridcell (grid.cc:112-124) at tmin
+static double cell_volume(const Model &m, int c) {
+  if (spherical(m)) {
+    const double r_in = m.cell_pos_min[(size_t)c * 3], r_out = r_in + m.cell_wid[c];
+    return 4. / 3. * ARTIS_PI * (pow(r_out, 3) - pow(r_in, 3));
+  }
+  return pow(2 * m.geom.coordmax[0] / m.cfg.ngrid_1d, 3);
+}
+
 void build_grid(Model &m) {
   const artis_synth_config &c = m.cfg;
   m.tmin = c.tmin_days * ARTIS_DAY;
@@ -724,6 +754,11 @@ void build_grid(Model &m) {
       m.mgi_rho_tmin[s] = rho_at_v(vmid);
       X_at_v(vmid, &m.mgi_X[(size_t)s * 3]);
       m.mgi_tclass[s] = tclass_of_v(vmid);
+    }
+    if (c.grid_spherical) {
+      spherical_grid(m, vout.data());
+      finish_geometry(m);
+      return;
     }
     for (int idx = 0; idx < m.ngrid; idx++) {  // map_1dmodeltogrid (grid.cc:910-940)
       const double rpos = radialpos(idx);
@@ -800,7 +835,11 @@ int build_grid_from_model(Model &m, const artis_ejecta_model &em, const std::vec
   }
   std::vector<int> nassoc(np, 0);
   m.cell_mgi.assign(m.ngrid, np);
-  for (int idx = 0; idx < m.ngrid; idx++) {
+  if (c.grid_spherical && em.model_type == 1) {
+    spherical_grid(m, em.vout);
+    for (int mgi = 0; mgi < np; mgi++) nassoc[mgi] = (m.cell_mgi[mgi] == mgi) ? 1 : 0;
+  }
+  for (int idx = 0; idx < (spherical(m) ? 0 : m.ngrid); idx++) {
     const double rpos = radialpos(idx);
     int mgi = np;
     if (em.model_type == 1) {
@@ -866,14 +905,22 @@ void finish_geometry(Model &m) {
     m.ts_width[i] = (m.tmin * exp((i + 1) * dlogt)) - m.ts_start[i];
   }
   artis_geometry &g = m.geom;
-  g.grid_type = ARTIS_GRID_UNIFORM;
-  g.ncoordgrid[0] = g.ncoordgrid[1] = g.ncoordgrid[2] = n;
   g.ngrid = m.ngrid;
   g.npts_model = m.npts_model;
   g.cell_pos_min = m.cell_pos_min.data();
   g.cell_mgi = m.cell_mgi.data();
-  g.modelcell_wid_init = nullptr;
-  for (int ax = 0; ax < 3; ax++) g.coordmax[ax] = m.rmax;
+  if (spherical(m)) {  // spherical1d_grid_setup: ncoordgrid = {npts_model, 1, 1}, coordmax = {rmax, 0, 0}
+    g.ncoordgrid[0] = m.ngrid;
+    g.ncoordgrid[1] = g.ncoordgrid[2] = 1;
+    g.modelcell_wid_init = m.cell_wid.data();
+    g.coordmax[0] = m.rmax;
+    g.coordmax[1] = g.coordmax[2] = 0.;
+  } else {
+    g.grid_type = ARTIS_GRID_UNIFORM;
+    g.ncoordgrid[0] = g.ncoordgrid[1] = g.ncoordgrid[2] = n;
+    g.modelcell_wid_init = nullptr;
+    for (int ax = 0; ax < 3; ax++) g.coordmax[ax] = m.rmax;
+  }
   g.tmin = m.tmin;
   g.tmax = m.tmax;
   g.rmax = m.rmax;
@@ -923,7 +970,12 @@ static void cell_grey(Model &m, int nts, double t, int mgi, double rho) {
     m.kappagrey[mgi] = (float)(((0.9 * m.mgi_ffegrp[mgi]) + 0.1) * ARTIS_GREY_OP / m.kappagrey_norm);
     const double tratmid = t / m.tmin;
     if (m.inp.opacity_case == 4) {
-      const double radial_pos = m.mgi_rpos[mgi] * tratmid;
+      double radial_pos = m.mgi_rpos[mgi] * tratmid;
+      if (spherical(m)) {  // the volume-averaged mean radius of the shell (update_grid.cc:1164-1169)
+        const double r_inner = m.cell_pos_min[(size_t)mgi * 3] * tratmid;
+        const double r_outer = r_inner + m.cell_wid[mgi] * tratmid;
+        radial_pos = 3. / 4 * (pow(r_outer, 4.) - pow(r_inner, 4.)) / (pow(r_outer, 3) - pow(r_inner, 3.));
+      }
       const double grey_optical_depth = (double)m.kappagrey[mgi] * (double)m.rho[mgi] * (m.rmax * tratmid - radial_pos);
       if (grey_optical_depth > m.inp.cell_is_optically_thick && nts < m.inp.num_grey_timesteps) m.thick[mgi] = 1;
     } else {
@@ -934,7 +986,7 @@ static void cell_grey(Model &m, int nts, double t, int mgi, double rho) {
     m.ffegrp[mgi] = (float)(0.2 + 0.6 * exp(-(v / 6e8) * (v / 6e8)));
     m.kappagrey[mgi] = (float)(0.1 * (0.9 * m.ffegrp[mgi] + 0.1));
     if (m.cfg.thick_tau > 0) {
-      const double wid_t = 2 * m.geom.coordmax[0] / m.cfg.ngrid_1d * t / m.tmin;
+      const double wid_t = (spherical(m) ? m.cell_wid[mgi] : 2 * m.geom.coordmax[0] / m.cfg.ngrid_1d) * t / m.tmin;
       if (m.kappagrey[mgi] * rho * wid_t > m.cfg.thick_tau) m.thick[mgi] = 1;
     }
   }
@@ -1425,6 +1477,7 @@ void artis_synth_default_config(artis_synth_config *cfg) {
   cfg->minpop = 0.;
   cfg->nu_min_r = 0.;
   cfg->nu_max_r = 0.;
+  cfg->grid_spherical = 0;
 }
 
 artis_model *artis_model_from_files(const artis_synth_config *cfg, const char *input_txt, const char *model_txt,
@@ -1561,10 +1614,12 @@ int artis_model_init_pellets(const artis_model *m, int npkts, uint64_t seed, dou
     const int mgi = m->cell_mgi[c];
     if (mgi < m->npts_model) {
       const double v = m->mgi_vel[mgi];
+      // (vol_init_gridcell x rhoinit x q, packet.cc:99; the uniform grid's equal volumes drop out)
+      const double vol = spherical(*m) ? cell_volume(*m, c) : 1.;
       if (m->from_files)
-        acc += m->mgi_rho_tmin[mgi] * m->mgi_ni56[mgi];  // model.txt X_Ni56
+        acc += vol * m->mgi_rho_tmin[mgi] * m->mgi_ni56[mgi];  // model.txt X_Ni56
       else
-        acc += m->mgi_rho_tmin[mgi] * 0.6 * exp(-(v / 6e8) * (v / 6e8));
+        acc += vol * m->mgi_rho_tmin[mgi] * 0.6 * exp(-(v / 6e8) * (v / 6e8));
     }
     cdf[c] = acc;
   }
@@ -1592,7 +1647,18 @@ int artis_model_init_pellets(const artis_model *m, int npkts, uint64_t seed, dou
     p.number = i;
     p.prop_time = m->tmin;
     p.originated_from_particlenotgamma = 0;
-    for (int ax = 0; ax < 3; ax++) p.pos[ax] = m->cell_pos_min[(size_t)c * 3 + ax] + upos() * wid;
+    if (spherical(*m)) {  // a radius uniform in volume within the shell, isotropic direction (packet.cc:29-38)
+      const double zrand3 = U(rng);
+      const double r_inner = m->cell_pos_min[(size_t)c * 3];
+      const double r_outer = r_inner + m->cell_wid[c];
+      const double radius = pow(zrand3 * pow(r_inner, 3) + (1. - zrand3) * pow(r_outer, 3), 1 / 3.);
+      const double mu = -1 + 2. * U(rng), phi = 2 * ARTIS_PI * U(rng), st = sqrt(1. - mu * mu);
+      p.pos[0] = radius * st * cos(phi);
+      p.pos[1] = radius * st * sin(phi);
+      p.pos[2] = radius * mu;
+    } else {
+      for (int ax = 0; ax < 3; ax++) p.pos[ax] = m->cell_pos_min[(size_t)c * 3 + ax] + upos() * wid;
+    }
     // setup_radioactive_pellet (decay.cc:1371-1458)
     if (U(rng) < frac_initial) {
       p.tdecay = m->tmin;
@@ -1669,12 +1735,12 @@ int artis_model_init_rpackets(const artis_model *m, int nts, int npkts, uint64_t
   const double t = m->ts_start[nts];
   const int n = m->cfg.ngrid_1d;
   const double wid = 2 * m->geom.coordmax[0] / n;
-  // cell CDF by rho * volume (uniform volume)
+  // cell CDF by rho * volume (the uniform grid's equal volumes drop out)
   std::vector<double> cdf(m->ngrid);
   double acc = 0.;
   for (int c = 0; c < m->ngrid; c++) {
     const int mgi = m->cell_mgi[c];
-    acc += (mgi < m->npts_model) ? m->rho[mgi] : 0.;
+    acc += (mgi < m->npts_model) ? m->rho[mgi] * (spherical(*m) ? cell_volume(*m, c) : 1.) : 0.;
     cdf[c] = acc;
   }
   if (!(acc > 0)) return ARTIS_ERR_BAD_ARGUMENT;
@@ -1691,9 +1757,20 @@ int artis_model_init_rpackets(const artis_model *m, int nts, int npkts, uint64_t
     p.where = c;
     p.type = ARTIS_TYPE_RPKT;
     p.last_cross = ARTIS_NONE;
-    for (int ax = 0; ax < 3; ax++) {
-      const double lo = m->cell_pos_min[(size_t)c * 3 + ax] * t / m->tmin;
-      p.pos[ax] = lo + (0.05 + 0.9 * U(rng)) * wid * t / m->tmin;
+    if (spherical(*m)) {  // a radius uniform in volume within the shell (away from its faces), isotropic position
+      const double z = 0.05 + 0.9 * U(rng);
+      const double r_inner = m->cell_pos_min[(size_t)c * 3] * t / m->tmin;
+      const double r_outer = (m->cell_pos_min[(size_t)c * 3] + m->cell_wid[c]) * t / m->tmin;
+      const double radius = pow(z * pow(r_inner, 3) + (1. - z) * pow(r_outer, 3), 1 / 3.);
+      const double pmu = -1 + 2. * U(rng), pphi = 2 * ARTIS_PI * U(rng), pst = sqrt(1. - pmu * pmu);
+      p.pos[0] = radius * pst * cos(pphi);
+      p.pos[1] = radius * pst * sin(pphi);
+      p.pos[2] = radius * pmu;
+    } else {
+      for (int ax = 0; ax < 3; ax++) {
+        const double lo = m->cell_pos_min[(size_t)c * 3 + ax] * t / m->tmin;
+        p.pos[ax] = lo + (0.05 + 0.9 * U(rng)) * wid * t / m->tmin;
+      }
     }
     const double mu = -1 + 2. * U(rng);
     const double phi = 2 * ARTIS_PI * U(rng);

@@ -52,6 +52,9 @@ typedef struct artis_synth_config {
   int32_t detailed_bf_usefromtimestep;   /* DETAILED_BF_ESTIMATORS_USEFROMTIMESTEP (default 13) */
   double minpop;             /* MINPOP (0: 1e-30 classic, 1e-40 nebular) */
   double nu_min_r, nu_max_r; /* NU_MIN_R / NU_MAX_R (0: 1e14 / 5e15 classic; nebular 1e13 / 5e15) */
+  int32_t grid_spherical;    /* 1D models only: GRID_SPHERICAL1D propagation grid, one radial cell per shell
+                                (spherical1d_grid_setup, grid.cc:2104-2131) instead of the shells mapped onto the
+                                ngrid_1d^3 cuboid (map_1dmodeltogrid) */
 } artis_synth_config;
 
 typedef struct artis_model artis_model;

@@ -173,6 +173,7 @@ class SynthConfig(C.Structure):
         ("minpop", C.c_double),
         ("nu_min_r", C.c_double),
         ("nu_max_r", C.c_double),
+        ("grid_spherical", C.c_int32),
     ]
 
 
@@ -713,11 +714,19 @@ class NtDataHandle:
             pass
 
 
+GRID_UNIFORM, GRID_SPHERICAL1D = 1, 2
+
+
 def model_vol_init(model):
-    """vol_init_modelcell (grid.cc): the uniform grid's cell volume at tmin times the number of propagation cells
-    mapped to each model cell."""
+    """vol_init_modelcell (grid.cc:94-110): the uniform grid's cell volume at tmin times the number of propagation
+    cells mapped to each model cell; on the spherical grid the shell volume 4/3 pi (r_out^3 - r_in^3) at tmin."""
     g = Geometry.from_address(model.geometry)
     mgi = np.ctypeslib.as_array(g.cell_mgi, (g.ngrid,))
+    if g.grid_type == GRID_SPHERICAL1D:
+        r_in = np.ctypeslib.as_array(g.cell_pos_min, (g.ngrid * 3,))[0::3].copy()
+        r_out = r_in + np.ctypeslib.as_array(g.modelcell_wid_init, (g.ngrid,))
+        vol = 4. / 3. * np.pi * (r_out ** 3 - r_in ** 3)
+        return np.where(mgi < g.npts_model, vol, 0.)[:g.npts_model]
     counts = np.bincount(mgi[mgi < g.npts_model], minlength=g.npts_model)[:g.npts_model]
     wid = [2 * g.coordmax[d] / g.ncoordgrid[d] for d in range(3)]
     return counts * (wid[0] * wid[1] * wid[2])

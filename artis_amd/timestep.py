@@ -46,11 +46,7 @@ class LteTimestepLoop:
         self.keep_inputs = keep_inputs
         self.last_inputs = None
         g = ffi.Geometry.from_address(model.geometry)
-        np_ = model.npts_model
-        cell_mgi = np.ctypeslib.as_array(g.cell_mgi, (g.ngrid,))
-        count = np.bincount(cell_mgi, minlength=np_ + 1)[:np_]
-        wid = 2 * g.coordmax[0] / g.ncoordgrid[0]
-        self.vol_init = wid ** 3 * count.astype(np.float64)  # vol_init of each model cell (grid.cc:1009)
+        self.vol_init = ffi.model_vol_init(model).astype(np.float64)  # vol_init_modelcell (grid.cc:94-110)
         self.ts_mid = np.ctypeslib.as_array(g.ts_mid, (g.ntstep,)).copy()
         self.ts_width = np.ctypeslib.as_array(g.ts_width, (g.ntstep,)).copy()
         self.tmin = g.tmin

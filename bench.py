@@ -229,6 +229,33 @@ def class_roofline(alg, kt):
     return out
 
 
+def find_traffic(src_sha, P, ngrid, nts, vpkt, kernel_prefix):
+    """Measured HBM bytes per launch of the kernel named kernel_prefix from a PMC summary (profiles/pmc_*.json,
+    tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE) made from the same engine sources and workload; (bytes, file)."""
+    traffic, src = None, None
+    for prof in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json"))):
+        try:
+            pm = json.load(open(prof))
+        except Exception:
+            continue
+        if (pm.get("engine_src_sha") == src_sha and pm.get("packets") == P and pm.get("ngrid") == ngrid
+                and pm.get("nts") == nts and pm.get("vpkt", 0) == vpkt):
+            kd = next((v for k, v in pm.get("kernels", {}).items() if k.startswith(kernel_prefix)), None)
+            if kd:
+                traffic = kd["hbm_bytes_per_launch"]
+                src = os.path.relpath(prof, REPO)
+    return traffic, src
+
+
+def traffic_fields(traffic, src, alg_per_launch, launch_ms):
+    """The roofline fields the PMC traffic gives: the fraction of peak by measured bytes beside the byte model's."""
+    if traffic is None:
+        return {"traffic": None, "traffic_profile": None, "frac_by_traffic": None, "traffic_over_alg": None}
+    return {"traffic": traffic, "traffic_profile": src,
+            "frac_by_traffic": traffic / max(launch_ms / 1e3, 1e-12) / 1e9 / HBM_PEAK_GBS,
+            "traffic_over_alg": traffic / max(alg_per_launch, 1e-300)}
+
+
 def ffi_params(m):
     from artis_amd import ffi
 
@@ -283,6 +310,95 @@ def baseline_configs(P, rank, progress, which=("w7_100_shells", "nebular_onezone
     return out
 
 
+def vpkt_config5(rank, progress, P=10_000_000, nts=30, nobs=4, ngrid=50):
+    """BASELINE config 5 (3D 50^3 grid, virtual packets + polarisation, vpkt.cc:76-406, 837-896) at 1e7 packets on one
+    GPU, the same workload as `bench.py --vpkt 4 --nts 30` (so its PMC summary applies); the 1e9-packet run's per-GPU
+    share of 1.25e8 packets is that command with --packets 125000000.  One warm step, one timed step, timed like the
+    main line; the dominant kernel (k_vpkt) with its roofline fraction by the byte model and by measured traffic."""
+    from artis_amd import Engine, engine_src_sha, ffi
+    from artis_amd.model import Model
+
+    m = Model(ngrid_1d=ngrid)
+    m.set_timestep(nts)
+    prm = ffi_params(m)
+    prm.rank = rank
+    pk = m.init_rpackets(nts, P, seed=1000 + rank)
+    eng = Engine(m, params=prm)
+    vcfg = ffi.VpktConfig(nz_obs=tuple(np.linspace(-0.9, 0.9, nobs)), phi_obs_deg=tuple(np.linspace(0.0, 300.0, nobs)),
+                          exclude=(0.0, -1.0, -2.0, 26.0), nprocs=1)
+    eng.vpkt_init(vcfg)
+    eng.upload_cellstate(nts)
+    eng.upload(pk)
+    eng.snapshot()
+    del pk
+    ms, kts, vst, vwk, rnd, work = [], [], [], [], [], np.zeros(16, dtype=np.int64)
+    for k in range(2):
+        eng.restore()
+        eng.zero_estimators()
+        t = time.perf_counter()
+        eng.upload_cellstate(nts)
+        eng.step_resident(nts, my_rank=rank)
+        dt = time.perf_counter() - t
+        if k > 0:
+            ms.append(dt * 1e3)
+            kts.append(eng.last_kernel_class_times())
+            vst.append(eng.vpkt_last_stats())
+            vwk.append(eng.vpkt_last_work())
+            rnd.append(eng.last_rounds())
+            work[:] = eng.last_work()
+    eng.close()
+    alg = byte_model(work, m.nions_total)
+    ntr = float(np.mean([v[2] for v in vst]))
+    vw = {k: float(np.mean([w[k] for w in vwk])) for k in vwk[0]}
+    alg["vpkt"] = vpkt_byte_model(vw, ntr, m.nions_total)
+    kt = {c: (float(np.mean([t[c][0] for t in kts])), float(np.mean([t[c][1] for t in kts]))) for c in kts[0]}
+    kt["vpkt"] = (float(np.mean([v[0] for v in vst])), float(max(np.mean(rnd), 1)))
+    dom = max((c for c in kt if c in alg), key=lambda c: kt[c][0])
+    launches = max(kt[dom][1], 1.)
+    per_launch = alg[dom] / launches
+    launch_ms = kt[dom][0] / launches
+    gbs = per_launch / max(launch_ms / 1e3, 1e-12) / 1e9
+    traffic, src = find_traffic(engine_src_sha(), P, ngrid, nts, nobs, KERNEL_NAME[dom])
+    step_ms = float(np.mean(ms))
+    out = {"config": 5, "packets": P, "timestep": nts, "observers": nobs, "spectra": int(vcfg.nspectra),
+           "ms_per_step": step_ms, "value": P / (step_ms / 1e3), "unit": "packets/s",
+           "kernel_ms": {c: v[0] for c, v in kt.items()}, "kernel_share_of_step": {c: v[0] / step_ms for c, v in kt.items()},
+           "vpkt": {"ms": kt["vpkt"][0], "traces": int(ntr), "traces_per_s": ntr / max(kt["vpkt"][0] / 1e3, 1e-12),
+                    "work_per_trace": {k: v / max(ntr, 1.) for k, v in vw.items()}},
+           "roofline": {"kernel": KERNEL_NAME[dom], "achieved": gbs, "peak": HBM_PEAK_GBS, "frac": gbs / HBM_PEAK_GBS,
+                        "alg_bytes_per_launch": per_launch, "avg_launch_ms": launch_ms,
+                        **traffic_fields(traffic, src, per_launch, launch_ms)},
+           "note": "the 1e9-packet config runs 1.25e8 packets per GPU on 8 GPUs: `bench.py --vpkt 4 --nts 30 --packets "
+                   "125000000` (profiles/*_bench_vpkt_125M.json)"}
+    progress(f"config 5 shape (vpkt, {P} packets): {step_ms:.0f} ms per step")
+    m.close()
+    return out
+
+
+def allreduce_cost(eng, rank, iters=20):
+    """SURVEY §8(d) 'with and without the RCCL all-reduce' at world size 1: the packed estimator block's size and the
+    time of the engine's all-reduce path (block gathered from the estimator arrays, ncclAllReduce, scalars averaged,
+    block scattered back) on a one-rank communicator; the xGMI term of N ranks is bounded from the block size."""
+    import torch
+    from artis_amd import comm_unique_id
+
+    eng.comm_init(0, 1, comm_unique_id())
+    eng.allreduce_estimators()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(iters):
+        eng.allreduce_estimators()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) / iters * 1e3
+    nbytes = 8 * eng.estimator_block_doubles()
+    # ring all-reduce over 8 ranks: every rank sends and receives 2 (N-1)/N of the block; one xGMI link ~153 GB/s
+    # (MI355X_MICROARCH.md) as the per-rank bound of one ring
+    ring8_ms = 2 * 7 / 8 * nbytes / 153e9 * 1e3
+    return {"block_bytes": nbytes, "world1_ms": ms, "ring8_one_link_bound_ms": ring8_ms,
+            "note": "world size 1: the gather / scatter of the block around the collective; ring8 bound: the data an "
+                    "8-rank ring moves per rank over one 153 GB/s xGMI link"}
+
+
 def level_mode_workload(rank, progress, P=1_000_000, nts=10):
     """The macro-atom key records in level mode: the 50^3 grid with 5x the bench's lines (line window 160:
     470 745 lines), whose whole-cell records do not fit the HBM budget, so records are kept per (cell, level) pair for
@@ -290,7 +406,8 @@ def level_mode_workload(rank, progress, P=1_000_000, nts=10):
     the first transport is made from the walks of that step)."""
     from artis_amd.model import Model
 
-    m = Model(ngrid_1d=50, line_window=160)
+    # (the generator caps the line count at 100 000 unless told otherwise: the 5x atom needs the cap lifted)
+    m = Model(ngrid_1d=50, line_window=160, max_lines=1_000_000)
     out = timed_workload(m, P, nts, rank, 1)
     out["line_window"] = 160
     out["level_mode"] = bool(out["tables"].get("ma_level_records", 0) > 0)
@@ -415,7 +532,8 @@ def main():
     ap.add_argument("--baseline-config", default=None,
                     help="only the BASELINE config sub-lines named (comma-separated: w7_100_shells, nebular_onezone, "
                          "kilonova; level_mode: the 5x-lines atom at min(--packets, 1e6); timestep_loop: update_grid -> "
-                         "upload_cellstate -> update_packets over three timesteps), at --packets per GPU; prints "
+                         "upload_cellstate -> update_packets over three timesteps; vpkt5: the config-5 shape, 4 observers at timestep 30), "
+                         "at --packets per GPU; prints "
                          "them as one JSON line (for per-config profiles)")
     args = ap.parse_args()
 
@@ -450,11 +568,13 @@ def main():
     if args.baseline_config:
         which = tuple(args.baseline_config.split(","))
         configs = baseline_configs(args.packets, rank, progress,
-                                   which=tuple(w for w in which if w not in ("level_mode", "timestep_loop")))
+                                   which=tuple(w for w in which if w not in ("level_mode", "timestep_loop", "vpkt5")))
         if "level_mode" in which:
             configs["level_mode_5x_lines"] = level_mode_workload(rank, progress, P=min(args.packets, 1_000_000))
         if "timestep_loop" in which:
             configs["timestep_loop"] = timestep_loop(args.packets, args.nts, 3, rank, progress)
+        if "vpkt5" in which:
+            configs["vpkt_config5_shape"] = vpkt_config5(rank, progress, P=args.packets)
         if rank == 0:
             print(json.dumps({"baseline_configs": configs, "engine_src_sha": engine_src_sha()}), flush=True)
         return
@@ -568,18 +688,12 @@ def main():
     achieved_gbs = bytes_per_launch / max(avg_launch_s, 1e-12) / 1e9
     achieved_survey = alg_survey[dom] / launches / max(avg_launch_s, 1e-12) / 1e9
     src_sha = engine_src_sha()
-    traffic, traffic_src = None, None
-    for prof in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json"))):
-        try:
-            pm = json.load(open(prof))
-        except Exception:
-            continue
-        if (pm.get("engine_src_sha") == src_sha and pm.get("packets") == P and pm.get("ngrid") == args.ngrid
-                and pm.get("nts") == nts and pm.get("vpkt", 0) == args.vpkt):
-            kd = next((v for k, v in pm.get("kernels", {}).items() if k.startswith(KERNEL_NAME[dom])), None)
-            if kd:
-                traffic = kd["hbm_bytes_per_launch"]
-                traffic_src = os.path.relpath(prof, REPO)
+    traffic, traffic_src = find_traffic(src_sha, P, args.ngrid, nts, args.vpkt, KERNEL_NAME[dom])
+    allreduce = None
+    if world == 1 and not args.no_extra:
+        allreduce = allreduce_cost(eng, rank)
+        progress(f"estimator block all-reduce (world 1): {allreduce['world1_ms']:.2f} ms for "
+                 f"{allreduce['block_bytes'] / 1e6:.1f} MB")
     cpu = None
     parity_line = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and vcfg is None:
@@ -693,6 +807,7 @@ def main():
         configs = baseline_configs(P, rank, progress)
         tloop = timestep_loop(P, nts, 3, rank, progress)
         lvl = level_mode_workload(rank, progress)
+        configs["vpkt_config5_shape"] = vpkt_config5(rank, progress)
 
     if rank == 0:
         line = {
@@ -725,8 +840,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "traffic_profile": traffic_src,
+                **traffic_fields(traffic, traffic_src, bytes_per_launch, avg_launch_s * 1e3),
                 "engine_src_sha": src_sha,
                 "kernel": KERNEL_NAME[dom],
                 "achieved_survey_model": achieved_survey,
@@ -749,6 +863,8 @@ def main():
             "work_per_packet": {k: float(v) / max(P, 1) for k, v in zip(WORK_NAMES, work)},
             "ceiling": ceiling(alg, P, value / world),
         }
+        if allreduce is not None:
+            line["estimator_allreduce"] = allreduce
         if ugrid is not None:
             line["update_grid"] = ugrid
         if neb is not None:

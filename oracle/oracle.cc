@@ -1183,8 +1183,132 @@ void escat_rpkt(const Ctx &c, artis_rng *rng, artis_packet *p) {
 }
 
 // ------------------------------------------------------------------------------------------------ boundary
-// boundary.cc:101-330 (GRID_UNIFORM)
+[[noreturn]] static void shell_fatal(const char *what, double shellradius, const double pos[3]) {
+  fprintf(stderr, "oracle: [fatal] get_shellcrossdist: %s (shellradius %g, |pos| %g)\n", what, shellradius,
+          sqrt(dot(pos, pos)));
+  abort();
+}
+
+// boundary.cc:14-99 get_shellcrossdist: the closest forward distance to the intersection of a ray with an expanding
+// spherical shell; -1 if there is no forward intersection (or a tangential one)
+static double get_shellcrossdist(const double pos[3], const double dir[3], const double shellradius,
+                                 const bool isinnerboundary, const double tstart) {
+  if (!(shellradius > 0)) shell_fatal("shellradius > 0", shellradius, pos);
+  const double speed = vec_len(dir) * ARTIS_CLIGHT_PROP;
+  const double a = dot(dir, dir) - pow(shellradius / tstart / speed, 2);
+  const double b = 2 * (dot(dir, pos) - pow(shellradius, 2) / tstart / speed);
+  const double cc = dot(pos, pos) - pow(shellradius, 2);
+  const double discriminant = pow(b, 2) - 4 * a * cc;
+  if (discriminant < 0) {
+    // no intersection
+    if (!(shellradius < vec_len(pos))) shell_fatal("no intersection inside the shell", shellradius, pos);
+    return -1;
+  } else if (discriminant > 0) {
+    // two intersections
+    double d1 = (-b + sqrt(discriminant)) / 2 / a;
+    double d2 = (-b - sqrt(discriminant)) / 2 / a;
+    double posfinal1[3], posfinal2[3];
+    for (int d = 0; d < 3; d++) {  // cblas_dcopy, then cblas_daxpy (y += alpha x)
+      posfinal1[d] = pos[d];
+      posfinal1[d] += d1 * dir[d];
+      posfinal2[d] = pos[d];
+      posfinal2[d] += d2 * dir[d];
+    }
+    const double shellradiusfinal1 = shellradius / tstart * (tstart + d1 / speed);
+    const double shellradiusfinal2 = shellradius / tstart * (tstart + d2 / speed);
+    if (!(fabs(vec_len(posfinal1) / shellradiusfinal1 - 1.) < 1e-3)) shell_fatal("solution 1 off the shell", shellradius, pos);
+    if (!(fabs(vec_len(posfinal2) / shellradiusfinal2 - 1.) < 1e-3)) shell_fatal("solution 2 off the shell", shellradius, pos);
+    // invalidate any solutions that require entering the boundary from the wrong radial direction
+    if (isinnerboundary) {
+      if (dot(posfinal1, dir) > 0.) d1 = -1;
+      if (dot(posfinal2, dir) > 0.) d2 = -1;
+    } else {
+      if (dot(posfinal1, dir) < 0.) d1 = -1;
+      if (dot(posfinal2, dir) < 0.) d2 = -1;
+    }
+    // negative d means in the reverse direction along the ray
+    if (d1 < 0 && d2 < 0) return -1;
+    if (d2 < 0) return d1;
+    if (d1 < 0) return d2;
+    return fmin(d1, d2);
+  }
+  // exactly one intersection: ignored (the packet stays in its cell)
+  if (!(shellradius <= vec_len(pos))) shell_fatal("single intersection inside the shell", shellradius, pos);
+  return -1.;
+}
+
+// rpkt.cc:659-661, gammapkt.cc:551-553
+static double max_sdist(const Ctx &c, const artis_packet *p, double sdist) {
+  return (c.g->grid_type == ARTIS_GRID_SPHERICAL1D) ? 2 * c.g->rmax * (p->prop_time + sdist / ARTIS_CLIGHT_PROP) / c.g->tmin
+                                                     : c.g->rmax * p->prop_time / c.g->tmin;
+}
+
+// boundary.cc:101-330, GRID_SPHERICAL1D: one radial coordinate (get_ngriddimensions() == 1), cellindex == shell,
+// cellcoordmax = pos_min + wid_init(cellindex), get_cellcoordpointnum = cellindex, index increment 1
+static double boundary_cross_spherical(const Ctx &c, artis_packet *p, int *snext) {
+  const double tstart = p->prop_time;
+  const int cellindex = p->where;
+  const double tmin = c.g->tmin;
+  const int n0 = c.g->ncoordgrid[0];
+  const double initpos = vec_len(p->pos);
+  const double cellcoordmin = c.g->cell_pos_min[(size_t)cellindex * 3];
+  const double cellcoordmax = cellcoordmin + c.g->modelcell_wid_init[cellindex];
+  const double vel = dot(p->pos, p->dir) / vec_len(p->pos) * ARTIS_CLIGHT_PROP;  // radial velocity
+  int last_cross = p->last_cross;
+  for (int flip = 0; flip < 2; flip++) {
+    const int direction = flip ? ARTIS_POS_X : ARTIS_NEG_X;
+    const int invdirection = !flip ? ARTIS_POS_X : ARTIS_NEG_X;
+    const int cellindexstride = flip ? -1 : 1;
+    bool isoutside_thisside;
+    if (flip)
+      isoutside_thisside = initpos < (cellcoordmin / tmin * tstart - 10.);
+    else
+      isoutside_thisside = initpos > (cellcoordmax / tmin * tstart + 10.);
+    if (isoutside_thisside && (last_cross != direction)) {
+      if ((vel - (initpos / tstart)) > 0) {
+        if ((cellindex == (n0 - 1) && cellindexstride > 0) || (cellindex == 0 && cellindexstride < 0)) {
+          *snext = -99;
+          return 0;
+        }
+        *snext = p->where + cellindexstride;
+        p->last_cross = invdirection;
+        return 0;
+      }
+      last_cross = direction;
+    }
+  }
+  last_cross = ARTIS_NONE;  // handled by d_inner / d_outer being negative for invalid directions
+  const double r_inner = cellcoordmin * tstart / tmin;
+  const double d_inner = (r_inner > 0.) ? get_shellcrossdist(p->pos, p->dir, r_inner, true, tstart) : -1.;
+  const double t_coordminboundary = d_inner / ARTIS_CLIGHT_PROP;
+  const double r_outer = cellcoordmax * tstart / tmin;
+  const double d_outer = get_shellcrossdist(p->pos, p->dir, r_outer, false, tstart);
+  const double t_coordmaxboundary = d_outer / ARTIS_CLIGHT_PROP;
+  double time = 1.e99;
+  if ((t_coordmaxboundary > 0) && (t_coordmaxboundary < time) && (last_cross != ARTIS_NEG_X)) {
+    time = t_coordmaxboundary;
+    if (cellindex == (n0 - 1)) {
+      *snext = -99;
+    } else {
+      *snext = p->where + 1;
+      p->last_cross = ARTIS_POS_X;
+    }
+  }
+  if ((t_coordminboundary > 0) && (t_coordminboundary < time) && (last_cross != ARTIS_POS_X)) {
+    time = t_coordminboundary;
+    if (cellindex == 0) {
+      *snext = -99;
+    } else {
+      *snext = p->where - 1;
+      p->last_cross = ARTIS_NEG_X;
+    }
+  }
+  return ARTIS_CLIGHT_PROP * time;
+}
+
+// boundary.cc:101-330 (GRID_UNIFORM; GRID_SPHERICAL1D in boundary_cross_spherical)
 double boundary_cross(const Ctx &c, Est &E, artis_packet *p, int *snext) {
+  if (c.g->grid_type == ARTIS_GRID_SPHERICAL1D) return boundary_cross_spherical(c, p, snext);
   const double tstart = p->prop_time;
   const int cellindex = p->where;
   const double tmin = c.g->tmin;
@@ -1974,7 +2098,7 @@ bool do_rpkt_step(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
     mgi = cell_mgi(c, p->where);
     return (p->type == ARTIS_TYPE_RPKT && (mgi == npm || mgi == oldmgi));
   }
-  const double maxsdist = c.g->rmax * p->prop_time / c.g->tmin;
+  const double maxsdist = max_sdist(c, p, sdist);
   if (sdist > maxsdist) {
     fprintf(stderr, "oracle: [fatal] do_rpkt: Unreasonably large sdist for packet %d. %g %g %g\n", p->number,
             c.g->rmax, p->prop_time / c.g->tmin, sdist);
@@ -3055,7 +3179,7 @@ void do_gamma(const Ctx &c, Est &E, artis_rng *rng, artis_packet *p, double t2) 
   const double tau_current = 0.0;
   int snext;
   double sdist = boundary_cross(c, E, p, &snext);
-  const double maxsdist = c.g->rmax * p->prop_time / c.g->tmin;
+  const double maxsdist = max_sdist(c, p, sdist);
   if (sdist > maxsdist) gamma_fatal("Unreasonably large sdist (gamma)", p);
   if (sdist < 0) sdist = 0;
   if (((snext < 0) && (snext != -99)) || (snext >= c.g->ngrid)) gamma_fatal("Heading for inappropriate grid cell", p);

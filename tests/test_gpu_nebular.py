@@ -104,3 +104,18 @@ def test_nebularonezone_inputfiles(engine_factory):
     _pair(m, eng, 5, pk)
     pe = m.init_pellets(3000, seed=66)
     _pair(m, eng, 0, pe)
+
+
+@pytest.mark.parametrize("env", [{"ARTIS_GPU_RPKT_COOP": "0"}, {"ARTIS_GPU_RPKT_COOP": "0", "ARTIS_GPU_MA_PRE": "0",
+                                                                   "ARTIS_GPU_MF_REC": "0"}])
+def test_nebular_detailed_bf_fallbacks(engine_factory, monkeypatch, env):
+    """The detailed-bf model's fallback paths: per-lane continuum sums in k_rpkt instead of the wave-cooperative
+    instance (RPKT_COOP=0), gathered tickets and per-packet deactivation side arrays -- the oracle's results."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    m = Model(**NEB)
+    eng = engine_factory(m)
+    m.set_timestep(14)
+    pk = m.init_rpackets(14, 3000, seed=66)
+    _, eg, eo, _ = _pair(m, eng, 14, pk)
+    assert eo.bfrate_raw.sum() > 0

@@ -416,3 +416,33 @@ def test_bounded_line_walk_matches_oracle(shell_model, small_model, engine_facto
         _, pg, eg, po, eo, _ = _pair(m, eng, nts, 3000, seed=seed)
         parity.assert_packets_match(pg, po)
         parity.assert_estimators_match(eg, eo)
+
+
+@pytest.fixture(scope="module")
+def many_cell_model():
+    """26^3 grid: 9 200 non-empty cells, more than the few-cell binning's MA_BIN_LDS (8 192), so the macro-atom queue
+    takes the many-cell binning (the producers' bin counts and k_ma_scatter)."""
+    from artis_amd.model import Model
+
+    return Model(ngrid_1d=26, nlevels_per_ion=40, n_ionising=15, max_lines=4000, ntstep=30)
+
+
+# the engine's A/B switches (DESIGN.md §5, INTEGRATION.md) select fallback paths the default run never takes:
+# gathered tickets instead of the producers' pre-tickets (MA_PRE), the per-packet deactivation side arrays instead of
+# the F-queue records (MF_REC), the per-entry binning pass instead of the producers' bin counts (BIN_PUSH, many cells)
+# and the device-atomic binning instead of the block-local LDS counts (MA_BIN_BLK, few cells)
+FALLBACKS = [{"ARTIS_GPU_MA_PRE": "0"}, {"ARTIS_GPU_MF_REC": "0"}, {"ARTIS_GPU_BIN_PUSH": "0"},
+             {"ARTIS_GPU_MA_BIN_BLK": "0"}, {"ARTIS_GPU_MA_PRE": "0", "ARTIS_GPU_MF_REC": "0", "ARTIS_GPU_BIN_PUSH": "0"}]
+
+
+@pytest.mark.parametrize("cells", ["few", "many"])
+@pytest.mark.parametrize("env", FALLBACKS, ids=lambda e: "+".join(k[9:] + "=" + v for k, v in e.items()))
+def test_fallback_switches_match_oracle(small_model, many_cell_model, engine_factory, monkeypatch, cells, env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    m = small_model if cells == "few" else many_cell_model
+    eng = engine_factory(m)
+    _, pg, eg, po, eo, _ = _pair(m, eng, 10, 3000, seed=71)
+    parity.assert_packets_match(pg, po)
+    parity.assert_estimators_match(eg, eo)
+    assert eo.counters[4] > 1000 and eo.counters[11] > 1000  # bound-bound activations, internal up-jumps

@@ -31,13 +31,17 @@ def _compare_vpkt(vg, vo):
         assert np.abs(a[fb] - b[fb]).max(initial=0.0) <= parity.ESTIMATOR_RTOL * scale
 
 
-def _run(m, nts, pk, vc, engine_env=None, monkeypatch=None):
+def _run(m, nts, pk, vc, engine_env=None, monkeypatch=None, upload_first=False):
     if engine_env and monkeypatch:
         monkeypatch.setenv("ARTIS_GPU_ENGINE", engine_env)
     eng = Engine(m)
     try:
-        eng.vpkt_init(vc)
-        eng.upload_cellstate(nts)
+        if upload_first:  # the per-cell tables (and their negative-coefficient flag) before the vpkt parameters
+            eng.upload_cellstate(nts)
+            eng.vpkt_init(vc)
+        else:
+            eng.vpkt_init(vc)
+            eng.upload_cellstate(nts)
         pg = pk.copy()
         eg = eng.update_packets(nts, pg)
         vg = eng.vpkt_download()
@@ -160,11 +164,13 @@ def test_vpkt_megakernel_full_buffer_fails_loudly(monkeypatch):
         eng.close()
 
 
-def test_vpkt_nlte_inverted_lines_match_oracle():
+@pytest.mark.parametrize("upload_first", [False, True])
+def test_vpkt_nlte_inverted_lines_match_oracle(upload_first):
     """Virtual packets through NLTE populations with population inversions (negative Sobolev coefficients: the only
     case in which a virtual packet's tau can fall again).  The reference kills a virtual packet at the first line
     after which every spectrum's tau exceeds tau_max (vpkt.cc:280-283); k_vpkt tests at window ends and before
-    every negative-coefficient line -- the same kills, so the spectra and counters are the oracle's."""
+    every negative-coefficient line -- the same kills, so the spectra and counters are the oracle's.  Both call
+    orders: vpkt_init after upload_cellstate must keep the table's negative-coefficient flag."""
     neb = dict(ngrid_1d=6, nlevels_per_ion=30, n_ionising=10, max_lines=2000, ntstep=20, nebular=1,
                nlte_level_max=12, tmin_days=100., tmax_days=300., T0=6000., ionpot_scale=0.5, mass_msun=50.)
     m = Model(**neb)
@@ -175,7 +181,7 @@ def test_vpkt_nlte_inverted_lines_match_oracle():
     pk = m.init_rpackets(nts, 2000, seed=46)
     vc = ffi.VpktConfig(nz_obs=(0.3, -0.7), phi_obs_deg=(10.0, 200.0), exclude=(0.0, -1.0, 26.0), tmin_days=100.0,
                         tmax_days=300.0, lambda_min=1000.0, lambda_max=30000.0, tau_max=1.0)
-    pg, eg, vg, _ = _run(m, nts, pk, vc)
+    pg, eg, vg, _ = _run(m, nts, pk, vc, upload_first=upload_first)
     po = pk.copy()
     eo, vo, _ = oracle_lib.update_packets_vpkt(m, nts, po, vc, nthreads=16)
     parity.assert_packets_match(pg, po)
