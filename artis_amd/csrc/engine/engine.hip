@@ -3294,6 +3294,12 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
       }
     }
   rc |= dupload(&T.ma_meta, mm.data(), nl);
+  {
+    std::vector<MaWalk> mw(nl);
+    for (int ul = 0; ul < nl; ul++)
+      if (!ma_walk_make(mm[ul], &mw[ul])) ma_cache_ok = false;
+    rc |= dupload(&T.ma_walk, mw.data(), nl);
+  }
   for (int ul = 0; ul < nl; ul++) dbl_off[ul + 1] += dbl_off[ul];
   rc |= dupload(&T.ma_dbl_off, dbl_off.data(), nl + 1);
   G.h_dbl_off = dbl_off;

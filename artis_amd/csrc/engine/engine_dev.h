@@ -25,6 +25,15 @@ struct __attribute__((aligned(16))) MaMeta {
   int32_t nd, nu, nr, nt;  // #downtrans, #uptrans, #recombination targets, #ionisation targets
 };
 
+// what one cached-walk step (k_ma's ma_step_cached) reads of a level, with its record layout (ma_layout below) worked
+// out on the host: the same two 16-byte loads as MaMeta, and no layout arithmetic (a division by 63 among it) in the
+// pass.  w0 = (nd | nu << 16, doff, uoff, base_lower); w1 = (nr | nt << 16, sd | md << 8 | mu << 16 | nbd << 24,
+// nbu | end_d << 8 | end_u << 16, hot), end_d / end_u: the line-0 entries of the same-ion searches (separators and
+// suffix of a blocked array, else the array)
+struct __attribute__((aligned(16))) MaWalk {
+  int32_t w[8];
+};
+
 // one 32-byte record per line for the line walk of get_event (two 16-byte loads)
 struct __attribute__((aligned(16))) LineTau {
   double nu;    // line frequency (linelist_entry.nu)
@@ -86,6 +95,7 @@ struct DevTab {
   // per level: offset (doubles) of its macro-atom record inside a cell's record block, #downtrans, #uptrans,
   // #recombination targets (ionising levels of the lower ion, 0 if the level does not recombine)
   const MaMeta *ma_meta;  // [nlevels_total]
+  const MaWalk *ma_walk;  // [nlevels_total]
   const int64_t *ma_dbl_off;  // [nlevels_total + 1] offset (doubles) of each level's exact record in k_marates' scratch
   // targets of the internal same-ion jumps in the order of their level's cumulative arrays (downtrans / uptrans
   // order): (unique level index, offset of its macro-atom record in a cell block)
@@ -190,13 +200,30 @@ static inline __host__ __device__ MaLayout ma_layout(int nd, int nu, int nr, int
   L.hot = L.sorted0 + nd + 2 * nr + nt;
   return L;
 }
+// separators on line 0 of a blocked array of nb blocks
+static inline __host__ __device__ int ma_nsep(int nb) { return ARTIS_MA_SUFFIX ? nb : nb - 1; }
+// the level's MaWalk record; false if a field does not fit its bits
+static inline __host__ __device__ bool ma_walk_make(const MaMeta &m, MaWalk *w) {
+  const MaLayout L = ma_layout(m.nd, m.nu, m.nr, m.nt);
+  const int end_d = L.nbd ? ma_nsep(L.nbd) + L.md : m.nd, end_u = L.nbu ? ma_nsep(L.nbu) + L.mu : m.nu;
+  const bool ok = m.nd < 65536 && m.nu < 65536 && m.nr < 65536 && m.nt < 65536 && L.sd < 256 && L.md >= 0 &&
+                  L.md < 256 && L.mu >= 0 && L.mu < 256 && L.nbd < 256 && L.nbu < 256 && end_d < 256 && end_u < 256 &&
+                  L.sorted0 < 65536;
+  w->w[0] = m.nd | (m.nu << 16);
+  w->w[1] = m.doff;
+  w->w[2] = m.uoff;
+  w->w[3] = m.base_lower;
+  w->w[4] = m.nr | (m.nt << 16);
+  w->w[5] = L.sd | (L.md << 8) | (L.mu << 16) | (L.nbd << 24);
+  w->w[6] = L.nbu | (end_d << 8) | (end_u << 16);
+  w->w[7] = L.hot;
+  return ok;
+}
 // a blocked array needs one separator slot per block but the last beside its prefix
 static inline __host__ __device__ bool ma_layout_ok(int nd, int nu) {
   const MaLayout L = ma_layout(nd, nu, 0, 0);
   return L.md >= 0 && L.mu >= 0;
 }
-// separators on line 0 of a blocked array of nb blocks
-static inline __host__ __device__ int ma_nsep(int nb) { return ARTIS_MA_SUFFIX ? nb : nb - 1; }
 // key j of a same-ion array of c keys (area at a0, suffix m, nb blocks from record line lb): its record position;
 // *sep the separator position on line 0 the key is also stored at, or -1
 static inline __host__ __device__ int ma_same_pos(int j, int c, int a0, int m, int nb, int lb, int *sep) {

@@ -1967,13 +1967,15 @@ struct MaLaneC {
 struct MaHot {
   const uint16_t *ma_key;
   const MaMeta *ma_meta;
+  const MaWalk *ma_walk;
   const int2 *down_target, *up_target;
   const uint32_t *ma_lptr;
   uint32_t *ma_lhist;
   int32_t nlevels_total;
 };
 DEVFN MaHot ma_hot(const Ctx &K) {
-  return MaHot{K.C.ma_key, K.T.ma_meta, K.T.down_target, K.T.up_target, K.C.ma_lptr, K.C.ma_lhist, K.T.nlevels_total};
+  return MaHot{K.C.ma_key,   K.T.ma_meta, K.T.ma_walk,    K.T.down_target,
+               K.T.up_target, K.C.ma_lptr, K.C.ma_lhist, K.T.nlevels_total};
 }
 // the record line of level ul (MaMeta::rec_off rec_off) in the walk's cell
 DEVFN uint32_t ma_line(const MaHot &H, int32_t rowline, int k, int ul, int rec_off) {
@@ -2070,7 +2072,9 @@ DEVNI int ma_jump_exact(const Ctx &K, const LocalCounters &L, artis_rng &rng, Ma
   pr[ARTIS_MA_ACTION_INTERNALUPHIGHERNT] = ma_nt_total(K, mgi, ul);
   double total_transitions = 0.;
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) total_transitions += pr[a];
-  const double zrand = artis_rng_uniform(&rng);
+  double zrand, zr;
+  artis_rng_jump_pair(&rng, &zrand, &zr);  // (the action draw and the transition draw)
+  rng.n++;
   const double randomrate = zrand * total_transitions;
   double rate = 0.;
   int sel = ARTIS_MA_ACTION_COUNT;
@@ -2092,7 +2096,7 @@ DEVNI int ma_jump_exact(const Ctx &K, const LocalCounters &L, artis_rng &rng, Ma
   }
   if (sel == ARTIS_MA_ACTION_INTERNALUPHIGHERNT) return ma_apply_nt(K, L, rng, m, number);
   // the transition: first running sum of action sel above zr * total, in the reference's list order
-  const double zr = artis_rng_uniform(&rng);
+  rng.n++;
   const double x = zr * pr[sel];
   const int kind = (sel == ARTIS_MA_ACTION_RADDEEXC || sel == ARTIS_MA_ACTION_INTERNALDOWNSAME) ? MA_KIND_DOWN
                    : (sel == ARTIS_MA_ACTION_RADRECOMB || sel == ARTIS_MA_ACTION_INTERNALDOWNLOWER) ? MA_KIND_RECOMB
@@ -2128,8 +2132,8 @@ typedef __attribute__((address_space(3))) u32x4 lds_uint4;
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 typedef const __attribute__((address_space(1))) u32x4 glb_uint4;
 
-// Wave-cooperative fetch of one 128-byte line per lane (line index `myline` in units of 128 bytes from `base`,
-// 0xffffffff: none) into the wave's chunk-major LDS image wl[chunk * 64 + lane].  Instruction i has lanes
+// Wave-cooperative fetch of one 128-byte line per lane (line index `myline` in units of 128 bytes from `base`; a lane
+// without a line names line 0) into the wave's chunk-major LDS image wl[chunk * 64 + lane].  Instruction i has lanes
 // 8j..8j+7 read the eight 16-byte chunks of the line of lane 8i + j, so each load instruction touches 8 lines
 // instead of 64.  The memory system's rate is set by the (instruction, line) pairs it serves: random 128-byte
 // lines fetched this way arrive at 45 G lines/s (5.8 TB/s) on MI355X against 9.7 G lines/s (1.24 TB/s) when every
@@ -2150,9 +2154,9 @@ DEVFN void wave_fetch_issue(const void *base, uint32_t myline, WaveLines &w, lds
 #pragma unroll
   for (int i = 0; i < 8; i++)
 #ifdef ARTIS_MA_NT_FETCH  // A/B: streaming (non-temporal) line loads
-    w.c[i] = __builtin_nontemporal_load(&g[(size_t)(ls[i] == 0xffffffffu ? 0u : ls[i]) * 8 + (lane & 7)]);
+    w.c[i] = __builtin_nontemporal_load(&g[(size_t)ls[i] * 8 + (lane & 7)]);
 #else
-    w.c[i] = g[(size_t)(ls[i] == 0xffffffffu ? 0u : ls[i]) * 8 + (lane & 7)];  // idle lanes: a harmless line-0 read
+    w.c[i] = g[(size_t)ls[i] * 8 + (lane & 7)];  // (an idle lane names line 0)
 #endif
 }
 DEVFN void wave_fetch_commit(const WaveLines &w, lds_uint4 *wl) {
@@ -2168,20 +2172,18 @@ DEVFN T gload(const T *p) {
   return *(const __attribute__((address_space(1))) T *)p;
 }
 
-// the level's MaMeta words the cached walk reads: (rec_off, doff, uoff, base_lower), (nd, nu, nr, nt)
+// the level's MaWalk words the cached walk reads (engine_dev.h): w0 = (nd | nu << 16, doff, uoff, base_lower),
+// w1 = the packed record layout.  (Until round 6 this was MaMeta's (doff, uoff, base_lower), (nd, nu, nr, nt), and every
+// step worked out ma_layout from the counts.)
 struct MaMetaW {
   int4 w0, w1;
 };
-// (rec_off, w0.x, is not loaded: a dead load destination let the register allocator reuse it for the Philox
-// temporaries, which then waited for the record fetch; profiles/r03k_ab.txt: k_ma 1790 -> 1767 ms)
-typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
-DEVFN MaMetaW ma_meta_load(const MaMeta *ma_meta, int ul) {
-  glb_uint4 *mp = (glb_uint4 *)(ma_meta + ul);
-  const u32x3 a = *(const __attribute__((address_space(1))) u32x3 *)((const __attribute__((address_space(1))) uint32_t *)mp + 1);
-  const u32x4 b = mp[1];
-  return MaMetaW{make_int4(0, (int)a.x, (int)a.y, (int)a.z), make_int4((int)b.x, (int)b.y, (int)b.z, (int)b.w)};
+DEVFN MaMetaW ma_walk_load(const MaWalk *ma_walk, int ul) {
+  glb_uint4 *mp = (glb_uint4 *)(ma_walk + ul);
+  const u32x4 a = mp[0], b = mp[1];
+  return MaMetaW{make_int4((int)a.x, (int)a.y, (int)a.z, (int)a.w), make_int4((int)b.x, (int)b.y, (int)b.z, (int)b.w)};
 }
-DEVFN MaMetaW ma_meta_load(const Ctx &K, int ul) { return ma_meta_load(K.T.ma_meta, ul); }
+DEVFN MaMetaW ma_walk_load(const Ctx &K, int ul) { return ma_walk_load(K.T.ma_walk, ul); }
 
 // The cached walk as a resumable per-pass step (k_ma).  In SIMT every pass of a wave lasts as long as its slowest
 // lane; a search that probed record lines other than the staged one made one dependent trip to memory per probe,
@@ -2389,13 +2391,42 @@ struct KeysLds {
   DEVFN bool hi_only(const Ctx &) const { return HI_ONLY; }  // (level mode, the COOP instance of k_ma)
   DEVFN bool has(int p) const { return (p >> 6) == pl; }
   DEVFN uint32_t hi(int p) const { return (uint32_t)((lds_u16 *)(line + ((p & 63) >> 3) * 64))[p & 7]; }
+  // the 9 action keys (line 0): positions 0-7 packed two per word (one 16-byte LDS read), position 8
+  DEVFN void first9(u32x4 &k07, uint32_t &k8) const {
+    k07 = line[0];
+    k8 = (uint32_t)((lds_u16 *)(line + 64))[0];
+  }
 };
 struct KeysGlobal {
   const uint16_t *rec;
   DEVFN bool hi_only(const Ctx &K) const { return K.C.ma_hi_only != 0; }
   DEVFN bool has(int) const { return true; }
   DEVFN uint32_t hi(int p) const { return (uint32_t)gload(rec + p); }
+  DEVFN void first9(u32x4 &k07, uint32_t &k8) const {
+    k07 = *(glb_uint4 *)rec;
+    k8 = hi(8);
+  }
 };
+
+// Counts of the 9 action keys (16-bit high halves, non-decreasing) below qh and below qh + 2, in packed 16-bit
+// arithmetic: per word of two keys a saturating subtraction from the threshold (non-zero iff key < threshold), a
+// min with 1 and a packed add -- no per-key compare / carry chains (each a VCC write the next VALU instruction must
+// wait for on gfx950).  nund = keys equal to qh or qh + 1 (undecided at 16 bits).
+// (written as VOP3P instructions: from the equivalent C the compiler makes two compares, two selects and a permute
+// per word)
+DEVFN uint32_t pk_below(uint32_t tt, uint32_t k, uint32_t one) {  // per 16-bit half: k < t ? 1 : 0
+  uint32_t d, r;
+  asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(d) : "v"(tt), "v"(k));
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(d), "v"(one));
+  return r;
+}
+DEVFN uint32_t ma_count_below(const u32x4 &k07, uint32_t k8, uint32_t t) {
+  // t <= 0xffff: the count of keys < t
+  const uint32_t tt = t | (t << 16), one = 0x00010001u;
+  const uint32_t a = pk_below(tt, k07.x, one) + pk_below(tt, k07.y, one) + pk_below(tt, k07.z, one) +
+                     pk_below(tt, k07.w, one);  // (halves <= 4: no carry between them)
+  return (a & 0xffffu) + (a >> 16) + (k8 < t ? 1u : 0u);
+}
 
 // meta: the level's MaMetaW (k_ma loads it beside the record-line fetch); z1, z2: the values of the lane's next two
 // draws (used only by a step that starts a jump; the RNG counter advances over the draws the jump consumes)
@@ -2424,33 +2455,37 @@ DEVFN int ma_step_cached(const Ctx &K, const MaHot &H, const LocalCounters &L, a
 #endif
   const uint16_t *rec = H.ma_key + (size_t)m.line * 64;
   const int doff = meta.w0.y, uoff = meta.w0.z, base_lower = meta.w0.w;
-  const int nd = meta.w1.x, nu = meta.w1.y, nr = meta.w1.z, nt = meta.w1.w;
-  const MaLayout lay = ma_layout(nd, nu, nr, nt);
+  const uint32_t wnd = (uint32_t)meta.w0.x, wnr = (uint32_t)meta.w1.x, wl1 = (uint32_t)meta.w1.y,
+                 wl2 = (uint32_t)meta.w1.z;
+  const int nd = (int)(wnd & 0xffffu), nu = (int)(wnd >> 16), nr = (int)(wnr & 0xffffu), nt = (int)(wnr >> 16);
+  // the record layout (engine_dev.h ma_layout, MaWalk): only the fields the step reads
+  const int lay_sd = (int)(wl1 & 0xffu), lay_md = (int)((wl1 >> 8) & 0xffu), lay_mu = (int)((wl1 >> 16) & 0xffu),
+            lay_nbd = (int)(wl1 >> 24), lay_nbu = (int)(wl2 & 0xffu);
+  const int lay_hot = meta.w1.w;
   auto cmp = [&](int p, uint32_t hi, double q, uint32_t qh) -> int {
     if (hi < qh) return -1;
     if (hi > qh + 1) return 1;
     if (keys.hi_only(K)) return 0;  // level-mode records hold the high halves only: undecided -> exact jump
-    return ma_key_cmp((hi << 16) | (uint32_t)gload(rec + lay.hot + p), q);
+    return ma_key_cmp((hi << 16) | (uint32_t)gload(rec + lay_hot + p), q);
   };
   if (m.sel < 0) {  // a new jump: the action is the first of the 9 running-sum keys (line 0) above q
     m.n0 = rng.n;
     const double q = z1 * MA_KEY_SCALE;
     const uint32_t qh = ma_qh(q);
     rng.n++;
-    uint32_t hk[ARTIS_MA_ACTION_COUNT];
-    int nless = 0, nund = 0;
-#pragma unroll
-    for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) {
-      hk[a] = keys.hi(a);
-      nless += hk[a] < qh ? 1 : 0;
-      nund += (hk[a] - qh) <= 1u ? 1 : 0;
-    }
+    u32x4 k07;
+    uint32_t k8;
+    keys.first9(k07, k8);
+    const int nless = (int)ma_count_below(k07, k8, qh);
+    // (keys < qh + 2; every 16-bit key is when qh + 2 passes 0xffff)
+    const int nle1 = (int)ma_count_below(k07, k8, min(qh + 2, 0xffffu));
+    const int nund = (qh >= 0xfffeu ? ARTIS_MA_ACTION_COUNT : nle1) - nless;
     int sel = -1;
     if (nund == 0) {  // the keys are non-decreasing: the first nless are decided below q, the next above
       if (nless < ARTIS_MA_ACTION_COUNT) sel = nless;
     } else {
       for (int a = nless; a < ARTIS_MA_ACTION_COUNT; a++) {
-        const int c = cmp(a, hk[a], q, qh);
+        const int c = cmp(a, keys.hi(a), q, qh);
         if (c > 0) {
           sel = a;
           break;
@@ -2477,14 +2512,14 @@ DEVFN int ma_step_cached(const Ctx &K, const MaHot &H, const LocalCounters &L, a
     m.blk = -1;
     if (sel == ARTIS_MA_ACTION_INTERNALDOWNSAME || sel == ARTIS_MA_ACTION_INTERNALUPSAME) {
       const bool down = sel == ARTIS_MA_ACTION_INTERNALDOWNSAME;
-      const int nb = down ? lay.nbd : lay.nbu;
-      m.base = down ? 9 : 9 + lay.sd;
-      m.end = nb ? ma_nsep(nb) + (down ? lay.md : lay.mu) : (down ? nd : nu);  // separators and suffix, or the array
+      m.base = down ? 9 : 9 + lay_sd;
+      m.end = (int)((wl2 >> (down ? 8 : 16)) & 0xffu);  // separators and suffix, or the array
     } else {
-      m.base = lay.sorted0 + ((sel == ARTIS_MA_ACTION_RADDEEXC)            ? 0
-                              : (sel == ARTIS_MA_ACTION_RADRECOMB)         ? nd
-                              : (sel == ARTIS_MA_ACTION_INTERNALDOWNLOWER) ? nd + nr
-                                                                           : nd + 2 * nr);  // INTERNALUPHIGHER
+      const int sorted0 = 64 * (1 + lay_nbd + lay_nbu);
+      m.base = sorted0 + ((sel == ARTIS_MA_ACTION_RADDEEXC)            ? 0
+                          : (sel == ARTIS_MA_ACTION_RADRECOMB)         ? nd
+                          : (sel == ARTIS_MA_ACTION_INTERNALDOWNLOWER) ? nd + nr
+                                                                       : nd + 2 * nr);  // INTERNALUPHIGHER
       m.end = (sel == ARTIS_MA_ACTION_RADDEEXC) ? nd : (sel == ARTIS_MA_ACTION_INTERNALUPHIGHER) ? nt : nr;
     }
     m.hi = m.end;
@@ -2522,7 +2557,7 @@ DEVFN int ma_step_cached(const Ctx &K, const MaHot &H, const LocalCounters &L, a
       return MA_PENDING;
     }
     probes++;
-    const int c = keys.hi_only(K) ? 0 : ma_key_cmp((h << 16) | (uint32_t)gload(rec + lay.hot + p), m.q2);
+    const int c = keys.hi_only(K) ? 0 : ma_key_cmp((h << 16) | (uint32_t)gload(rec + lay_hot + p), m.q2);
     if (c == 0) {
       m.ntrans += probes;
       m.jumps--;
@@ -2540,12 +2575,12 @@ DEVFN int ma_step_cached(const Ctx &K, const MaHot &H, const LocalCounters &L, a
   const int sel = m.sel;
   if (sel == ARTIS_MA_ACTION_INTERNALDOWNSAME || sel == ARTIS_MA_ACTION_INTERNALUPSAME) {
     const bool down = sel == ARTIS_MA_ACTION_INTERNALDOWNSAME;
-    const int cnt = down ? nd : nu, nb = down ? lay.nbd : lay.nbu, suf = down ? lay.md : lay.mu;
+    const int cnt = down ? nd : nu, nb = down ? lay_nbd : lay_nbu, suf = down ? lay_md : lay_mu;
     // separators and suffix searched: the key is in block lo (round-4 layout: the last if no separator is above
     // q2), or suffix entry lo - nb
     if (nb && m.blk < 0 && lo < nb) {
       m.blk = lo;
-      m.base = 64 * (1 + (down ? 0 : lay.nbd) + lo);
+      m.base = 64 * (1 + (down ? 0 : lay_nbd) + lo);
       m.lo = 0;
       m.end = m.hi = min(64, cnt - suf - 64 * lo);
       m.pline = m.base >> 6;
@@ -2595,13 +2630,13 @@ DEVFN int ma_step_cached(const Ctx &K, const MaHot &H, const LocalCounters &L, a
 // never waits for a line, so it runs to the end of the jump (the block of a two-level array: a second call).
 DEVFN int ma_jump_cached_global(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneC &mc, MaEnd &end,
                                 int number) {
-  artis_rng r2 = rng;
-  const double z1 = artis_rng_uniform(&r2), z2 = artis_rng_uniform(&r2);
+  double z1, z2;
+  artis_rng_jump_pair(&rng, &z1, &z2);
   MaLaneR m;
   static_cast<MaLaneC &>(m) = mc;
   m.sel = -1;
   m.pline = 0;
-  const MaMetaW meta = ma_meta_load(K, m.ul);
+  const MaMetaW meta = ma_walk_load(K, m.ul);
   const KeysGlobal keys{K.C.ma_key + (size_t)m.line * 64};
   int r;
   do {

@@ -786,8 +786,8 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     {
       // the level's metadata and, 8 lines per load instruction, every busy lane's record line; the lane's next two
       // draws are computed while they are in flight
-      if (have) meta = ma_meta_load(H.ma_meta, mc.ul);
-      const uint32_t myline = (have && !unc) ? mc.line + (uint32_t)mc.pline : 0xffffffffu;
+      if (have) meta = ma_walk_load(H.ma_walk, mc.ul);
+      const uint32_t myline = (have && !unc) ? mc.line + (uint32_t)mc.pline : 0u;  // (idle lanes: a harmless line 0)
       WaveLines wl;
       wave_fetch_issue(H.ma_key, myline, wl, (lds_u32 *)&s_xidx[threadIdx.x >> 6][0]);
       if (have && mc.sel < 0) {
@@ -798,9 +798,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
         z1 = (double)(h >> 11) * (1.0 / 9007199254740992.0);
         z2 = (double)((h * 0x9E3779B97F4A7C15ull) >> 11) * (1.0 / 9007199254740992.0);
 #else
-        artis_rng r2 = rng;
-        z1 = artis_rng_uniform(&r2);
-        z2 = artis_rng_uniform(&r2);
+        artis_rng_jump_pair(&rng, &z1, &z2);  // (the jump's two draws, one Philox block: include/artis_rng.h)
 #endif
       }
       wave_fetch_commit(wl, line - (threadIdx.x & 63));
@@ -828,9 +826,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     if (COOP && r == MA_DEFER) {
       rng.n = mc.n0;
       // (a search that began in an earlier pass has no draws computed in this one)
-      artis_rng r2 = rng;
-      z1 = artis_rng_uniform(&r2);
-      z2 = artis_rng_uniform(&r2);
+      artis_rng_jump_pair(&rng, &z1, &z2);
       unc_now = true;
       r = MA_PENDING;
     }
@@ -1022,8 +1018,8 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
       // level mode (a pair without a record, or a comparison its high key halves could not decide): the action from
       // the pair's exact totals, the transition by the wave's search -- k_ma's exact-sum jump (ma_coop_action /
       // ma_coop_search / ma_coop_apply), the same draws and sums
-      artis_rng r2 = rng;
-      const double z1 = artis_rng_uniform(&r2), z2 = artis_rng_uniform(&r2);
+      double z1, z2;
+      artis_rng_jump_pair(&rng, &z1, &z2);
       double x = 0.;
       int sel = ma_coop_action(K, k, ul, z1, z2, &x);
       int j = -1;
@@ -1037,7 +1033,7 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
         static_cast<MaLaneC &>(mr) = m;
         mr.jumps = W.pend_jumps[idx];  // (ma_coop_apply counts the jump)
         MaEnd e{};
-        const int r = ma_coop_apply(K, ma_hot(K), L, rng, mr, e, number, sel, j, probes, ma_meta_load(K, ul));
+        const int r = ma_coop_apply(K, ma_hot(K), L, rng, mr, e, number, sel, j, probes, ma_walk_load(K, ul));
         lwork(L, WK_MA_TRANS, mr.ntrans);
         n_exact++;  // (stats[40], [45]: added once per block, not once per jump on one address)
         W.rng_n[idx] = rng.n;
@@ -1092,7 +1088,9 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
     pr[ARTIS_MA_ACTION_INTERNALUPHIGHERNT] = ma_nt_total(K, mgi, ul);
     double total_transitions = 0.;
     for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) total_transitions += pr[a];
-    const double zrand = artis_rng_uniform(&rng);
+    double zrand, zr;
+    artis_rng_jump_pair(&rng, &zrand, &zr);  // (the action draw and the transition draw)
+    rng.n++;
     const double randomrate = zrand * total_transitions;
     double rate = 0.;
     int sel = ARTIS_MA_ACTION_COUNT;
@@ -1115,7 +1113,7 @@ __global__ __launch_bounds__(64) void k_ma_exact(const Ctx *__restrict__ ctxp, W
       r = (lane == 0) ? ma_apply_nt(K, L, rng, m, number) : MA_CONTINUE;
     } else {
       // the transition: first running sum of action sel above zr * total, in the reference's list order
-      const double zr = artis_rng_uniform(&rng);
+      rng.n++;
       const double x = zr * pr[sel];
       const int kind = (sel == ARTIS_MA_ACTION_RADDEEXC || sel == ARTIS_MA_ACTION_INTERNALDOWNSAME) ? MA_KIND_DOWN
                        : (sel == ARTIS_MA_ACTION_RADRECOMB || sel == ARTIS_MA_ACTION_INTERNALDOWNLOWER) ? MA_KIND_RECOMB

@@ -61,23 +61,6 @@ ARTIS_HD artis_rng artis_rng_init(uint32_t seed, int32_t packet_number, int32_t 
   return s;
 }
 
-#ifdef ARTIS_RNG_PAIRED
-/* A/B variant: draw n is one half of Philox block n >> 1 */
-ARTIS_HD uint64_t artis_rng_next53(artis_rng *s) {
-  uint32_t c[4] = {s->n >> 1, 0x41525453u, s->nts, s->rank};
-  artis_philox4x32_10(c, s->key0, s->key1);
-  const uint64_t x = (s->n & 1u) ? (((uint64_t)c[3] << 32) | (uint64_t)c[2]) : (((uint64_t)c[1] << 32) | (uint64_t)c[0]);
-  s->n++;
-  return x >> 11;
-}
-/* draws n and n + 1 for an even n: one block */
-ARTIS_HD void artis_rng_pair_aligned(const artis_rng *s, double *z1, double *z2) {
-  uint32_t c[4] = {s->n >> 1, 0x41525453u, s->nts, s->rank};
-  artis_philox4x32_10(c, s->key0, s->key1);
-  *z1 = (double)((((uint64_t)c[1] << 32) | (uint64_t)c[0]) >> 11) * (1.0 / 9007199254740992.0);
-  *z2 = (double)((((uint64_t)c[3] << 32) | (uint64_t)c[2]) >> 11) * (1.0 / 9007199254740992.0);
-}
-#else
 /* 53-bit integer of draw number s->n, then advance */
 ARTIS_HD uint64_t artis_rng_next53(artis_rng *s) {
   uint32_t c[4] = {s->n, 0x41525453u, s->nts, s->rank};
@@ -86,7 +69,19 @@ ARTIS_HD uint64_t artis_rng_next53(artis_rng *s) {
   const uint64_t x = ((uint64_t)c[1] << 32) | (uint64_t)c[0];
   return x >> 11;
 }
-#endif
+
+/* The two draws of one macro-atom jump (do_macroatom, macroatom.cc:416-901: the action, then the transition within
+ * it) at counters n and n + 1 come from one Philox block, block n: the action draw is words 0-1 (what
+ * artis_rng_uniform returns at counter n), the transition draw words 2-3.  Block n + 1 is never evaluated for a jump:
+ * one Philox evaluation per jump instead of two, on the engine's busiest kernel (part of deviation D1: the stream is
+ * this library's definition, the same on both sides).  The caller advances s->n over the draws it consumes, as with
+ * artis_rng_uniform; a jump that consumes only the action draw leaves counter n + 1 to the next draw. */
+ARTIS_HD void artis_rng_jump_pair(const artis_rng *s, double *z1, double *z2) {
+  uint32_t c[4] = {s->n, 0x41525453u, s->nts, s->rank};
+  artis_philox4x32_10(c, s->key0, s->key1);
+  *z1 = (double)((((uint64_t)c[1] << 32) | (uint64_t)c[0]) >> 11) * (1.0 / 9007199254740992.0);
+  *z2 = (double)((((uint64_t)c[3] << 32) | (uint64_t)c[2]) >> 11) * (1.0 / 9007199254740992.0);
+}
 
 /* gsl_rng_uniform: [0,1) */
 ARTIS_HD double artis_rng_uniform(artis_rng *s) { return (double)artis_rng_next53(s) * (1.0 / 9007199254740992.0); }

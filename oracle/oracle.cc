@@ -2372,7 +2372,15 @@ void do_macroatom(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
     double total_transitions = 0.;
     for (int action = 0; action < ARTIS_MA_ACTION_COUNT; action++) total_transitions += processrates[action];
     int selected_action = ARTIS_MA_ACTION_COUNT;
-    double zrand = artis_rng_uniform(rng);
+    // the jump's action draw and transition draw come from one Philox block (include/artis_rng.h
+    // artis_rng_jump_pair); each advances the counter by one as it is taken
+    double zrand, zpair;
+    artis_rng_jump_pair(rng, &zrand, &zpair);
+    rng->n++;
+    auto transition_draw = [&]() {
+      rng->n++;
+      return zpair;
+    };
     const double randomrate = zrand * total_transitions;
     double rate = 0.;
     for (int action = 0; action < ARTIS_MA_ACTION_COUNT; action++) {
@@ -2390,7 +2398,7 @@ void do_macroatom(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
     switch (selected_action) {
       case ARTIS_MA_ACTION_RADDEEXC: {
         // macroatom.cc:222-296
-        const double zr = artis_rng_uniform(rng);
+        const double zr = transition_draw();
         double r = 0.;
         int linelistindex = -99;
         const int ndowntrans = a.level_ndowntrans[ul];
@@ -2447,7 +2455,7 @@ void do_macroatom(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
       case ARTIS_MA_ACTION_INTERNALDOWNSAME: {
         // macroatom.cc:174-220
         p->interactions += 1;
-        const double zr = artis_rng_uniform(rng);
+        const double zr = transition_draw();
         int lower = -99;
         double r = 0.;
         const int ndowntrans = a.level_ndowntrans[ul];
@@ -2466,7 +2474,7 @@ void do_macroatom(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
         // macroatom.cc:298-380
         const int upperion = ion;
         const int upperionlevel = level;
-        const double zr = artis_rng_uniform(rng);
+        const double zr = transition_draw();
         double r = 0;
         const int nlevels = get_ionisinglevels(c, element, upperion - 1);
         int lower = 0;
@@ -2513,7 +2521,7 @@ void do_macroatom(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
       case ARTIS_MA_ACTION_INTERNALDOWNLOWER: {
         p->interactions += 1;
         counter_inc(E, CTR_MA_STAT_INTERNALDOWNLOWER);
-        zrand = artis_rng_uniform(rng);
+        zrand = transition_draw();
         rate = 0.;
         const int nlevels = get_ionisinglevels(c, element, ion - 1);
         int lower;
@@ -2536,7 +2544,7 @@ void do_macroatom(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
       }
       case ARTIS_MA_ACTION_INTERNALUPSAME: {
         p->interactions += 1;
-        zrand = artis_rng_uniform(rng);
+        zrand = transition_draw();
         int upper = -99;
         rate = 0.;
         const int uoff = a.level_uptrans_offset[ul];
@@ -2555,7 +2563,7 @@ void do_macroatom(const Ctx &c, ThreadCache &tc, Est &E, artis_rng *rng, artis_p
         p->interactions += 1;
         counter_inc(E, CTR_MA_STAT_INTERNALUPHIGHER);
         int upper = -1;
-        const double zr = artis_rng_uniform(rng);
+        const double zr = transition_draw();
         double r = 0.;
         for (int t = 0; t < get_nphixstargets(c, element, ion, level); t++) {
           upper = get_phixsupperlevel(c, element, ion, level, t);

@@ -24,6 +24,9 @@ CASES = {
                    nts=[6, 7], npkts=256, seed=21),
     "shells1d": dict(cfg=dict(ngrid_1d=10, nshells_1d=10, nlevels_per_ion=30, n_ionising=12, max_lines=2000,
                               ntstep=30), nts=[4], npkts=256, seed=22),
+    # GRID_SPHERICAL1D (round 6): the shells as radial propagation cells
+    "sphere1d": dict(cfg=dict(nshells_1d=20, grid_spherical=1, nlevels_per_ion=30, n_ionising=12, max_lines=2000,
+                              ntstep=30), nts=[4, 5], npkts=256, seed=23),
 }
 
 

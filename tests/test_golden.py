@@ -15,7 +15,7 @@ import parity
 from artis_amd import ffi
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASES = ["grid3d", "shells1d"]
+CASES = ["grid3d", "shells1d", "sphere1d"]
 
 
 def _load(name):

@@ -245,7 +245,8 @@ def test_edge_cases(small_model, engine_factory):
 
 def test_bench_size_subset_parity(engine_factory):
     """Full bench model (50^3 cells, 3 elements x 4 ions x ~300 levels, ~9.4e4 lines): 2e5 packets on the
-    engine; 1500 randomly chosen of them re-run on the oracle must match one for one."""
+    engine; 1500 randomly chosen of them re-run on the oracle must match one for one, with no discrete mismatch
+    (rounds 3-5 allowed one; tools/mismatch_probe.py on this sample and the two below found none, so it is gone)."""
     from artis_amd.model import Model
 
     m = Model()
@@ -261,7 +262,7 @@ def test_bench_size_subset_parity(engine_factory):
     idx = np.sort(rng.choice(P, size=1500, replace=False))
     po = pk0[idx].copy()
     oracle_lib.update_packets(m, nts, po, nthreads=16)
-    parity.assert_packets_match(pg[idx], po, max_discrete_mismatch=1)
+    parity.assert_packets_match(pg[idx], po)
     # size-independent properties of the whole ensemble
     esc = pg["type"] == ffi.TYPE_ESCAPE
     assert eg.struct.nesc == esc.sum()
@@ -445,4 +446,4 @@ def test_fallback_switches_match_oracle(small_model, many_cell_model, engine_fac
     _, pg, eg, po, eo, _ = _pair(m, eng, 10, 3000, seed=71)
     parity.assert_packets_match(pg, po)
     parity.assert_estimators_match(eg, eo)
-    assert eo.counters[4] > 1000 and eo.counters[11] > 1000  # bound-bound activations, internal up-jumps
+    assert eo.counters[4] > 1000 and eo.counters[9] > 1000  # bound-bound activations and deactivations
