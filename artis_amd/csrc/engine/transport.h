@@ -1081,6 +1081,11 @@ DEVFN bool get_event_walk(Tx &x, Pkt &p, RStep &S, int budget) {
   return done;
 }
 
+// ARTIS_RPKT_EST_ACC: k_rpkt lanes keep the J / nuJ / ffheating sums of consecutive segments in one cell and add
+// them when the cell changes or the packet retires (instead of after every step)
+#ifndef ARTIS_RPKT_EST_ACC
+#define ARTIS_RPKT_EST_ACC 0
+#endif
 // rpkt.cc:557-621 + radfield.cc:831-876
 DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double distance) {
   const Ctx &K = x.K;
@@ -1097,10 +1102,27 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
     atomicAdd(&e[nne + k], distance_e_cmf * nu);
     atomicAdd(&e[2 * nne + k], distance_e_cmf * kap.ffheating);
   } else if (x.defer_est) {
-    x.est_mgi = mgi;
-    x.est_de = distance_e_cmf;
-    x.est_denu = distance_e_cmf * nu;
-    x.est_deff = distance_e_cmf * kap.ffheating;
+#if ARTIS_RPKT_EST_ACC
+    // the lane keeps adding the segments of one cell (its next steps are mostly in the same cell: line events);
+    // a step in another cell first adds the kept sums (k_rpkt flushes what a retiring lane still holds)
+    if (x.est_mgi >= 0 && x.est_mgi != mgi) {
+      safeadd(&K.E.J[x.est_mgi], x.est_de);
+      safeadd(&K.E.nuJ[x.est_mgi], x.est_denu);
+      safeadd(&K.E.ffheat[x.est_mgi], x.est_deff);
+      x.est_mgi = -1;
+    }
+    if (x.est_mgi == mgi) {
+      x.est_de += distance_e_cmf;
+      x.est_denu += distance_e_cmf * nu;
+      x.est_deff += distance_e_cmf * kap.ffheating;
+    } else
+#endif
+    {
+      x.est_mgi = mgi;
+      x.est_de = distance_e_cmf;
+      x.est_denu = distance_e_cmf * nu;
+      x.est_deff = distance_e_cmf * kap.ffheating;
+    }
   } else {
     safeadd(&K.E.J[mgi], distance_e_cmf);
     safeadd(&K.E.nuJ[mgi], distance_e_cmf * nu);
@@ -1186,9 +1208,9 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
 // the wave's contributing lanes are in one cell -- the common case of few-cell models, where per-lane atomics on
 // the same three addresses serialise -- the terms are summed across the wave and added by one lane; otherwise
 // every lane adds its own.  Float atomics are unordered either way, so the sums agree to rounding.
-DEVFN void wave_flush_estimators(Tx &x) {
+DEVFN void wave_flush_estimators(Tx &x, bool keep = false) {
   const Ctx &K = x.K;
-  const bool pend = x.est_mgi >= 0;
+  const bool pend = x.est_mgi >= 0 && !keep;
   const unsigned long long pm = __ballot(pend);
   if (pm) {
     const int leader = __ffsll((long long)pm) - 1;
@@ -1211,7 +1233,7 @@ DEVFN void wave_flush_estimators(Tx &x) {
       safeadd(&K.E.ffheat[x.est_mgi], x.est_deff);
     }
   }
-  x.est_mgi = -1;
+  if (!keep) x.est_mgi = -1;
 }
 
 DEVFN double readlane_d(double v, int l) {
