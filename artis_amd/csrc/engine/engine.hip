@@ -473,15 +473,23 @@ __global__ __launch_bounds__(256) void k_lvl_decay(uint32_t *__restrict__ hist, 
   }
 }
 
+#define MA_BUILD_MAX_DOUBLES 6144  // LDS terms of one level (48 KiB); a level with more never gets a record
+// k_ma_build's LDS terms of a level (below).  The levels whose terms take at most 20 KiB are built by their own launch of that LDS size: 8 blocks per CU (the
+// 169-VGPR kernel's limit of 2 waves per SIMD), where sizing every block for the largest level of a large atom
+// left 3 blocks per CU
+#define MA_BUILD_SMALL 2560
+static inline __host__ __device__ int64_t ma_build_doubles(const MaMeta &m) { return 3 * ((int64_t)m.nd + m.nr) + m.nu + m.nt; }
 // k_lvl_select: the new DevCells::ma_lptr and the list of records to build.  have_hist == 0 (no transport yet):
 // whole cells in nonempty-index order (centre outwards), pair (k, ul) at line k * row_lines + rl_off[ul] while it
 // fits the pool.  Otherwise: density bucket above bt, or bucket bt while `rest` lines of it last.
-// ctr: [0] pool lines taken, [1] records listed, [2] lines taken from bucket bt
+// ctr: [0] pool lines taken, [1] records listed from the front (levels whose k_ma_build terms fit MA_BUILD_SMALL
+// doubles of LDS), [2] lines taken from bucket bt, [3] records listed from the back (the larger levels)
 __global__ __launch_bounds__(256) void k_lvl_select(Ctx K, const uint32_t *__restrict__ rec_lines,
                                                     const uint32_t *__restrict__ rl_off, uint32_t row_lines,
                                                     uint32_t *__restrict__ lptr, uint32_t *__restrict__ ctr,
                                                     int2 *__restrict__ list, int64_t list_cap, int64_t npairs, int bt,
-                                                    uint32_t rest, uint64_t pool_lines, int have_hist) {
+                                                    uint32_t rest, uint64_t pool_lines, int have_hist,
+                                                    int64_t small_max) {
   const int64_t nl = K.T.nlevels_total;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += (int64_t)gridDim.x * blockDim.x) {
     const int ul = (int)(i % nl), k = (int)(i / nl);
@@ -504,8 +512,14 @@ __global__ __launch_bounds__(256) void k_lvl_select(Ctx K, const uint32_t *__res
     }
     lptr[i] = line;
     if (line != MA_NOLINE) {
-      const uint32_t s = atomicAdd(&ctr[1], 1u);
-      if (s < list_cap) list[s] = make_int2(k, ul);
+      const MaMeta mm = K.T.ma_meta[ul];
+      if (ma_build_doubles(mm) <= small_max) {
+        const uint32_t s = atomicAdd(&ctr[1], 1u);
+        if (s < list_cap) list[s] = make_int2(k, ul);
+      } else {
+        const uint32_t s = atomicAdd(&ctr[3], 1u);
+        if (s < list_cap) list[list_cap - 1 - s] = make_int2(k, ul);
+      }
     }
   }
 }
@@ -516,7 +530,6 @@ __global__ __launch_bounds__(256) void k_lvl_select(Ctx K, const uint32_t *__res
 // (macroatom.cc:57-159: every action's running sum only involves its own terms, so the chains are independent and
 // equal to ma_accumulate's sequence bit for bit); the lanes write the normalised 32-bit keys at their record
 // positions (ma_rec_pos, with the block separators).
-#define MA_BUILD_MAX_DOUBLES 6144  // LDS terms of one level (48 KiB); a level with more never gets a record
 __global__ __launch_bounds__(64) void k_ma_build(Ctx K, const int2 *__restrict__ list, uint32_t nlist, int nts) {
   extern __shared__ double sb[];
   const int lane = threadIdx.x;
@@ -803,6 +816,7 @@ struct Engine {
   unsigned long long *d_lvl_buckets = nullptr;
   int2 *d_build_list = nullptr;
   int64_t build_list_cap = 0;
+  int64_t ma_level_small = 0, ma_level_large = 0;  // the build list's front (small levels) and back (large) parts
   uint64_t ma_pool_lines = 0;
   std::vector<uint32_t> h_rec_lines;
   int64_t ma_build_lds_doubles = 0;
@@ -935,6 +949,13 @@ int ma_place(const std::vector<int32_t> &order) {
   return 0;
 }
 
+// the small-level threshold of the build list (ARTIS_GPU_MA_BUILD_SMALL doubles overrides MA_BUILD_SMALL: tests run
+// both launches on small atoms)
+int64_t ma_build_small() {
+  const char *e = getenv("ARTIS_GPU_MA_BUILD_SMALL");
+  return e ? std::max<int64_t>(0, atoll(e)) : (int64_t)MA_BUILD_SMALL;
+}
+
 // Level mode, every artis_gpu_upload_cellstate: which (cell, level) pairs get a key record (DevCells::ma_lptr) and
 // the list k_ma_build fills.  Before any transport: whole cells, centre outwards, while the pool lasts.  After:
 // the pairs with the most (sampled) jumps since the last placement -- a threshold on log2 of the count found from
@@ -967,13 +988,15 @@ int ma_level_place() {
   k_lvl_select<<<nb, B, 0, G.stream>>>(G.K, G.d_rec_lines, G.d_rl_off, G.row_lines, G.d_ma_lptr, G.d_lvl_ctr,
                                        G.d_build_list, G.build_list_cap, npairs, bt,
                                        (uint32_t)std::min<uint64_t>(rest, 0xffffffffu), G.ma_pool_lines,
-                                       G.ma_lhist_ready ? 1 : 0);
+                                       G.ma_lhist_ready ? 1 : 0, ma_build_small());
   uint32_t c[4];
   HIPCHK(hipMemcpyAsync(c, G.d_lvl_ctr, sizeof c, hipMemcpyDeviceToHost, G.stream));
   k_lvl_decay<<<nb, B, 0, G.stream>>>(G.d_ma_lhist, npairs);
   HIPCHK(hipStreamSynchronize(G.stream));
   G.ma_level_lines = c[0];
-  G.ma_level_records = std::min<int64_t>(c[1], G.build_list_cap);
+  G.ma_level_small = std::min<int64_t>(c[1], G.build_list_cap);
+  G.ma_level_large = std::min<int64_t>(c[3], G.build_list_cap - G.ma_level_small);
+  G.ma_level_records = G.ma_level_small + G.ma_level_large;
   G.ma_initial_placement = !G.ma_lhist_ready;
   G.ma_lhist_ready = true;  // the transports from now on count
   return 0;
@@ -981,10 +1004,14 @@ int ma_level_place() {
 
 // the key records of the current level-mode placement (k_ma_build over the placement's list)
 int ma_level_build(int nts) {
-  if (G.ma_level_records > 0)
-    k_ma_build<<<(unsigned)std::min<int64_t>(G.ma_level_records, 1 << 16), 64,
+  const int64_t lds_small = std::min<int64_t>(G.ma_build_lds_doubles, ma_build_small());
+  if (G.ma_level_small > 0)
+    k_ma_build<<<(unsigned)std::min<int64_t>(G.ma_level_small, 1 << 16), 64, (size_t)std::max<int64_t>(1, lds_small) * 8,
+                 G.stream>>>(G.K, G.d_build_list, (uint32_t)G.ma_level_small, nts);
+  if (G.ma_level_large > 0)
+    k_ma_build<<<(unsigned)std::min<int64_t>(G.ma_level_large, 1 << 16), 64,
                  (size_t)std::max<int64_t>(1, G.ma_build_lds_doubles) * 8, G.stream>>>(
-        G.K, G.d_build_list, (uint32_t)G.ma_level_records, nts);
+        G.K, G.d_build_list + (G.build_list_cap - G.ma_level_large), (uint32_t)G.ma_level_large, nts);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1477,7 +1504,9 @@ int run_wavefront(int64_t n, int nts, double t2) {
     // loop does not end while QX holds any.
     if (round < 2 || qx_known != 0) {
       TSTART(5);
-      k_ma_exact<<<grid / 4, 64, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
+      // (one wave per block and queue entry, 2 waves per SIMD: the 256-VGPR kernel's limit.  A quarter of that grid
+      // left half the SIMDs without a wave, and the exact jumps of a large atom's level mode are latency chains)
+      k_ma_exact<<<grid, 64, 0, G.stream>>>(G.d_ctx, W, G.d_soa, n, nts);
       TEND(5);
       HIPCHK(hipMemsetAsync(W.ctr + 2 * QX, 0, 2 * sizeof(uint32_t), G.stream));
     }
@@ -3655,7 +3684,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
       HIPCHK(hipMemcpy(mm.data(), G.K.T.ma_meta, nl * sizeof(MaMeta), hipMemcpyDeviceToHost));
       for (int ul = 0; ul < nl; ul++) {
         const int64_t next = (ul + 1 < nl) ? mm[ul + 1].rec_off : G.ma_key_stride;
-        const int64_t need = 3 * ((int64_t)mm[ul].nd + mm[ul].nr) + mm[ul].nu + mm[ul].nt;
+        const int64_t need = ma_build_doubles(mm[ul]);
         if (ma_layout_ok(mm[ul].nd, mm[ul].nu) && need <= MA_BUILD_MAX_DOUBLES) {
           const int64_t hot = ma_layout(mm[ul].nd, mm[ul].nu, mm[ul].nr, mm[ul].nt).hot;
           G.h_rec_lines[ul] = (uint32_t)(hi_only ? (hot + 63) / 64 : (next - mm[ul].rec_off) / 64);

@@ -273,6 +273,28 @@ DEVFN double col_excitation_ratecoeff(const Ctx &K, float T_e, float nne, int li
   }
   return C;
 }
+// macroatom.h:107-150 col_excitation_ratecoeff on a packed item (TeExcItem, indexed like uptrans_lineindex): the same
+// expressions as col_excitation_ratecoeff above on the same values (epsilon_trans = epsilon(upper) - epsilon(level),
+// the line's P2, collision strength, oscillator strength and upper statistical weight), from one load per line
+DEVFN double te_col_exc(const TeExcItem &it, float T_e, float nne, double lowerstatweight) {
+  double C = 0.;
+  const double coll_strength = it.coll_str;
+  const double eoverkt = it.epsilon_trans / (ARTIS_KB * T_e);
+  if (coll_strength < 0) {
+    if (!it.forbidden) {
+      const double g_bar = 0.2;
+      const double exp_eoverkt = exp(eoverkt);
+      const double test = 0.276 * exp_eoverkt * (-0.5772156649 - log(eoverkt));
+      const double Gamma = g_bar > test ? g_bar : test;
+      C = ARTIS_C_0 * nne * sqrtf(T_e) * 14.51039491 * it.osc_f * it.P2 * eoverkt / exp_eoverkt * Gamma;
+    } else {
+      C = nne * 8.629e-6 * 0.01 * exp(-eoverkt) * (double)it.upper_sw / sqrtf(T_e);
+    }
+  } else {
+    C = nne * 8.629e-6 * coll_strength * exp(-eoverkt) / lowerstatweight / sqrtf(T_e);
+  }
+  return C;
+}
 // macroatom.cc:503-548 (populations from the per-cell table, B coefficients from LineMA)
 DEVFN double rad_deexcitation_ratecoeff_n(const Ctx &K, double n_u, double n_l, int li, double t_current) {
   double R = 0.0;

@@ -487,26 +487,7 @@ struct TeRates {
   double cooling_collisional, cooling_fb, cooling_ff, cooling_adiabatic, heating_collisional, heating_bf, heating_ff,
       heating_dep;
 };
-// macroatom.h:107-150 col_excitation_ratecoeff on a packed item (the same expressions)
-DEVFN double te_col_exc(const TeExcItem &it, float T_e, float nne, double lowerstatweight) {
-  double C = 0.;
-  const double coll_strength = it.coll_str;
-  const double eoverkt = it.epsilon_trans / (ARTIS_KB * T_e);
-  if (coll_strength < 0) {
-    if (!it.forbidden) {
-      const double g_bar = 0.2;
-      const double exp_eoverkt = exp(eoverkt);
-      const double test = 0.276 * exp_eoverkt * (-0.5772156649 - log(eoverkt));
-      const double Gamma = g_bar > test ? g_bar : test;
-      C = ARTIS_C_0 * nne * sqrtf(T_e) * 14.51039491 * it.osc_f * it.P2 * eoverkt / exp_eoverkt * Gamma;
-    } else {
-      C = nne * 8.629e-6 * 0.01 * exp(-eoverkt) * (double)it.upper_sw / sqrtf(T_e);
-    }
-  } else {
-    C = nne * 8.629e-6 * coll_strength * exp(-eoverkt) / lowerstatweight / sqrtf(T_e);
-  }
-  return C;
-}
+// (te_col_exc, the exact collisional-excitation term on a packed item: physics.h)
 // te_col_exc for k_te_solve, whose lanes are on different ions' lines: one exp -- of +eoverkt or -eoverkt, the
 // argument the line's branch takes -- and one log for every lane, instead of the three branches' transcendentals
 // run one after another by a divergent wave; the T_e-only factors of the branches evaluated once per sum (TeExcT), the

@@ -1081,11 +1081,6 @@ DEVFN bool get_event_walk(Tx &x, Pkt &p, RStep &S, int budget) {
   return done;
 }
 
-// ARTIS_RPKT_EST_ACC: k_rpkt lanes keep the J / nuJ / ffheating sums of consecutive segments in one cell and add
-// them when the cell changes or the packet retires (instead of after every step)
-#ifndef ARTIS_RPKT_EST_ACC
-#define ARTIS_RPKT_EST_ACC 0
-#endif
 // rpkt.cc:557-621 + radfield.cc:831-876
 DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double distance) {
   const Ctx &K = x.K;
@@ -1102,27 +1097,10 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
     atomicAdd(&e[nne + k], distance_e_cmf * nu);
     atomicAdd(&e[2 * nne + k], distance_e_cmf * kap.ffheating);
   } else if (x.defer_est) {
-#if ARTIS_RPKT_EST_ACC
-    // the lane keeps adding the segments of one cell (its next steps are mostly in the same cell: line events);
-    // a step in another cell first adds the kept sums (k_rpkt flushes what a retiring lane still holds)
-    if (x.est_mgi >= 0 && x.est_mgi != mgi) {
-      safeadd(&K.E.J[x.est_mgi], x.est_de);
-      safeadd(&K.E.nuJ[x.est_mgi], x.est_denu);
-      safeadd(&K.E.ffheat[x.est_mgi], x.est_deff);
-      x.est_mgi = -1;
-    }
-    if (x.est_mgi == mgi) {
-      x.est_de += distance_e_cmf;
-      x.est_denu += distance_e_cmf * nu;
-      x.est_deff += distance_e_cmf * kap.ffheating;
-    } else
-#endif
-    {
-      x.est_mgi = mgi;
-      x.est_de = distance_e_cmf;
-      x.est_denu = distance_e_cmf * nu;
-      x.est_deff = distance_e_cmf * kap.ffheating;
-    }
+    x.est_mgi = mgi;
+    x.est_de = distance_e_cmf;
+    x.est_denu = distance_e_cmf * nu;
+    x.est_deff = distance_e_cmf * kap.ffheating;
   } else {
     safeadd(&K.E.J[mgi], distance_e_cmf);
     safeadd(&K.E.nuJ[mgi], distance_e_cmf * nu);
@@ -1208,9 +1186,9 @@ DEVFN void update_estimators(Tx &x, const Pkt &p, const Kappa &kap, double dista
 // the wave's contributing lanes are in one cell -- the common case of few-cell models, where per-lane atomics on
 // the same three addresses serialise -- the terms are summed across the wave and added by one lane; otherwise
 // every lane adds its own.  Float atomics are unordered either way, so the sums agree to rounding.
-DEVFN void wave_flush_estimators(Tx &x, bool keep = false) {
+DEVFN void wave_flush_estimators(Tx &x) {
   const Ctx &K = x.K;
-  const bool pend = x.est_mgi >= 0 && !keep;
+  const bool pend = x.est_mgi >= 0;
   const unsigned long long pm = __ballot(pend);
   if (pm) {
     const int leader = __ffsll((long long)pm) - 1;
@@ -1233,7 +1211,7 @@ DEVFN void wave_flush_estimators(Tx &x, bool keep = false) {
       safeadd(&K.E.ffheat[x.est_mgi], x.est_deff);
     }
   }
-  if (!keep) x.est_mgi = -1;
+  x.est_mgi = -1;
 }
 
 DEVFN double readlane_d(double v, int l) {
@@ -2405,6 +2383,9 @@ DEVFN int ma_coop_apply(const Ctx &K, const MaHot &H, const LocalCounters &L, ar
   return ma_apply_selection(K, H, L, m, end, sel, j, meta.w0.y, meta.w0.z, meta.w0.w);
 }
 
+#ifndef ARTIS_MA_SEARCH4
+#define ARTIS_MA_SEARCH4 0
+#endif
 // where a step reads record keys (high halves): k_ma's staged line, or the whole record in global memory
 template <bool HI_ONLY>
 struct KeysLds {
@@ -2554,6 +2535,29 @@ DEVFN int ma_step_cached(const Ctx &K, const MaHot &H, const LocalCounters &L, a
   const int base = m.base;
   const uint32_t q2h = m.q2h;
   unsigned probes = 0;
+#if ARTIS_MA_SEARCH4
+  // 4-ary steps (three probes per LDS round trip) while the range lies on the staged line, is 4 entries or longer
+  // and its probes are decided by their high halves; the binary loop below finishes (the same entry: every
+  // narrowing is an exact comparison of sorted keys)
+  while (hi - lo >= 4 && keys.has(base + lo) && keys.has(base + hi - 1)) {
+    const int len = hi - lo;
+    const int m1 = lo + (len >> 2), m2 = lo + (len >> 1), m3 = lo + ((3 * len) >> 2);
+    const uint32_t h1 = keys.hi(base + m1), h2 = keys.hi(base + m2), h3 = keys.hi(base + m3);
+    if ((h1 - q2h) <= 1u || (h2 - q2h) <= 1u || (h3 - q2h) <= 1u) break;
+    probes += 3;
+    if (h1 > q2h) {
+      hi = m1;
+    } else if (h2 > q2h) {
+      lo = m1 + 1;
+      hi = m2;
+    } else if (h3 > q2h) {
+      lo = m2 + 1;
+      hi = m3;
+    } else {
+      lo = m3 + 1;
+    }
+  }
+#endif
   while (true) {
     int mid = 0, p = 0;
     uint32_t h = 0;
@@ -2958,28 +2962,31 @@ DEVNI void do_kpkt(Tx &x, Pkt &p, double t2, FbReq *fb = nullptr) {
     const double contrib_low = (icool > ilow) ? cc[icool - 1] : oldcoolingsum;
     double contrib = contrib_low;
     const int level = K.T.cool_level[icool];
-    const double epsilon_current = epsilon(K, element, ion, level);
     const int ul = ulev(K, element, ion, level);
     const double nnlevel = K.C.pops[(int64_t)k * K.T.nlevels_total + ul];
     const double statweight = stat_weight(K, element, ion, level);
     int upper = -1;
     const int nuptrans = K.T.level_nuptrans[ul];
     const int uoff = K.T.level_uptrans_offset[ul];
-    for (int ii = 0; ii < nuptrans; ii++) {
-      const int li = K.T.uptrans_lineindex[uoff + ii];
-      const int tmpupper = K.T.line_upper[li];
-      const double epsilon_trans = epsilon(K, element, ion, tmpupper) - epsilon_current;
-      const double C = nnlevel *
-                       col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight,
-                                                stat_weight(K, element, ion, tmpupper)) *
-                       epsilon_trans;
-      contrib += C;
-      if (contrib >= rndcool) {
-        upper = tmpupper;
-        break;
+    // the running sum over the level's up-transitions (kpkt.cc:660-700) from the packed excitation items: one
+    // independent 32-byte load per line, four in flight (the line index -> upper level -> its epsilon and statistical
+    // weight chain of three dependent loads per line made this loop the k-packet's cost on large atoms); the upper level
+    // of the selected line only is looked up
+    const TeExcItem *items = K.T.exc_items + uoff;
+    int sel = -1;
+    for (int i0 = 0; i0 < nuptrans && sel < 0; i0 += 4) {
+      TeExcItem it[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) it[q] = items[min(i0 + q, nuptrans - 1)];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        if (i0 + q >= nuptrans || sel >= 0) break;
+        contrib += nnlevel * te_col_exc(it[q], T_e, nne, statweight) * it[q].epsilon_trans;
+        if (contrib >= rndcool) sel = i0 + q;
       }
     }
-    if (upper < 0 && nuptrans > 0) upper = K.T.line_upper[K.T.uptrans_lineindex[uoff + nuptrans - 1]];  // D6
+    if (sel < 0 && nuptrans > 0) sel = nuptrans - 1;  // D6
+    if (sel >= 0) upper = K.T.line_upper[K.T.uptrans_lineindex[uoff + sel]];
     if (upper < 0) {
       x.err(ERR_KPKT, p.number, 1);
       return;

@@ -409,9 +409,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
         have = false;
       }
     }
-    // the step's J / nuJ / ffheating terms, once per cell and wave where possible (ARTIS_RPKT_EST_ACC: only a
-    // retired lane's; the others keep adding)
-    wave_flush_estimators(x, ARTIS_RPKT_EST_ACC && have);
+    wave_flush_estimators(x);  // the step's J / nuJ / ffheating terms, once per cell and wave where possible
     if (coop) {
 #ifdef ARTIS_STAMPS
       const unsigned long long tb0 = wave_clock();

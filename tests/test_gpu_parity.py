@@ -100,12 +100,16 @@ def test_without_macroatom_cache_is_identical(small_model, engine_factory, monke
 
 @pytest.mark.parametrize("env", [{"ARTIS_GPU_NO_LINECOEF": "1"}, {"ARTIS_GPU_LINECOEF_ROWS": "half"},
                                  {"ARTIS_GPU_MACACHE_ROWS": "half"},
+                                 {"ARTIS_GPU_MACACHE_ROWS": "half", "ARTIS_GPU_MA_BUILD_SMALL": "0"},
+                                 {"ARTIS_GPU_MACACHE_ROWS": "half", "ARTIS_GPU_MA_BUILD_SMALL": "64"},
                                  {"ARTIS_GPU_LINECOEF_ROWS": "1", "ARTIS_GPU_MACACHE_ROWS": "1"},
                                  {"ARTIS_GPU_NO_MACACHE": "1"}],
-                         ids=["no_linecoef", "half_linecoef", "half_macache", "one_row_each", "no_macache"])
+                         ids=["no_linecoef", "half_linecoef", "half_macache", "half_macache_large_builds",
+                              "half_macache_mixed_builds", "one_row_each", "no_macache"])
 def test_table_budgets_match_oracle(small_model, engine_factory, monkeypatch, env):
     """Per-cell tables that only fit the HBM budget for some cells -- line coefficients centre outwards, macro-atom
-    key records per (cell, level) in level mode -- or for none (no line coefficients; an empty record pool: every
+    key records per (cell, level) in level mode, built by the small-level and the large-level launch
+    (ARTIS_GPU_MA_BUILD_SMALL moves the split) -- or for none (no line coefficients; an empty record pool: every
     macro-atom jump made by the whole wave from the exact sums, ma_coop_select) give the same packet histories as
     the oracle and the full-table engine."""
     small_model.set_timestep(11)
