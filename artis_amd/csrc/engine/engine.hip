@@ -1076,7 +1076,7 @@ int alloc_packets(int64_t n) {
     void **p;
     size_t bytes;
   };
-  std::vector<Req> reqs = {{(void **)&G.d_soa, un * PKT_WORDS * 8},
+  std::vector<Req> reqs = {{(void **)&G.d_soa, un * PKT_STORE_WORDS * 8},
                            {(void **)&G.d_aos, un * PKT_WORDS * 8},
                            {(void **)&G.W.rng_n, un * sizeof(uint32_t)},
                            {(void **)&G.W.pend, un * sizeof(int4)},
@@ -4036,8 +4036,9 @@ int artis_gpu_packets_download(artis_packet *packets, int npkts) {
 
 int artis_gpu_packets_snapshot(void) {
   if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
-  if (!G.d_snapshot) HIPCHK(dmalloc((void **)&G.d_snapshot, (size_t)G.cap_pkts * PKT_WORDS * 8));
-  HIPCHK(hipMemcpyAsync(G.d_snapshot, G.d_soa, (size_t)G.npkts * PKT_WORDS * 8, hipMemcpyDeviceToDevice, G.stream));
+  if (!G.d_snapshot) HIPCHK(dmalloc((void **)&G.d_snapshot, (size_t)G.cap_pkts * PKT_STORE_WORDS * 8));
+  HIPCHK(hipMemcpyAsync(G.d_snapshot, G.d_soa, (size_t)G.npkts * PKT_STORE_WORDS * 8, hipMemcpyDeviceToDevice,
+                        G.stream));
   HIPCHK(hipStreamSynchronize(G.stream));
   G.have_snapshot = true;
   return 0;
@@ -4046,7 +4047,8 @@ int artis_gpu_packets_snapshot(void) {
 int artis_gpu_packets_restore(void) {
   if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
   if (!G.have_snapshot) return ARTIS_ERR_BAD_ARGUMENT;
-  HIPCHK(hipMemcpyAsync(G.d_soa, G.d_snapshot, (size_t)G.npkts * PKT_WORDS * 8, hipMemcpyDeviceToDevice, G.stream));
+  HIPCHK(hipMemcpyAsync(G.d_soa, G.d_snapshot, (size_t)G.npkts * PKT_STORE_WORDS * 8, hipMemcpyDeviceToDevice,
+                        G.stream));
   return 0;
 }
 

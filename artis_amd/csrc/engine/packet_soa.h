@@ -3,11 +3,18 @@
 //
 // Layout: the 38 words of every packet are grouped by how the event-queue kernels touch them --
 //   hot  (16 words, 128 B = one cache line per packet): what every r-packet step reads and writes
-//   cold (20 words, 160 B): emission/absorption records, Stokes/pol_dir, escape record, macro-atom state
+//   cold (20 words in a 24-word, 192-byte record of three 64-byte sectors, each written by one kind of event):
+//     sector 0 (words 19, 21-24, 36, 37, 20): the absorption record and macro-atom state a line absorption writes
+//              (k_rpkt), with the trueemission words beside them;
+//     sector 1 (words 14-17, 25-28) and the first two of sector 2 (29, 30): the emission record, Stokes vector and
+//              polarisation direction a deactivation writes (k_ma_finish);
+//     sector 2 also holds the escape record (32) and word 35.
 //   rest (2 words): tdecay and the pellet bookkeeping, never touched by this path
 // each group stored packet-major ([group base + packet * group width + slot]).  The queues hand packets to
 // kernels in arbitrary order, so a word-major (SoA) layout would cost one 128-byte line per 8-byte word;
-// grouped, a packet's hot state is one line and its cold state two.
+// grouped, a packet's hot state is one line, and an event's cold writes fill one sector instead of touching
+// three lines of a 160-byte record (round 6: k_rpkt wrote 0.80 GB per launch for the absorption record alone,
+// profiles/r6h_write_diag.txt).
 #ifndef ARTIS_PACKET_SOA_H
 #define ARTIS_PACKET_SOA_H
 
@@ -16,21 +23,25 @@
 
 #include "engine_dev.h"
 
+#define PKT_COLD_WIDTH 24
+#define PKT_STORE_WORDS (16 + PKT_COLD_WIDTH + 2)  // words of the packet store per packet (PKT_WORDS of payload)
+
 // word -> group (0 hot, 1 cold, 2 rest) and slot within the group; constant-folded for literal words
 __host__ __device__ constexpr int pkt_word_group(int w) {
   return (w == 31 || w == 34) ? 2 : ((w >= 14 && w <= 17) || (w >= 19 && w <= 30) || w == 32 || w >= 35) ? 1 : 0;
 }
 __host__ __device__ constexpr int pkt_word_slot(int w) {
-  return w <= 13 ? w : w == 18 ? 14 : w == 33 ? 15           // hot
-       : w <= 17 ? w - 14                                    // cold: em_pos[3], em_time
-       : w <= 30 ? w - 15                                    // cold: 19..30 -> 4..15
-       : w == 32 ? 16 : w == 35 ? 17 : w == 36 ? 18 : w == 37 ? 19
-       : w == 31 ? 0 : 1;                                    // rest: 31, 34
+  return w <= 13 ? w : w == 18 ? 14 : w == 33 ? 15                              // hot
+       : w == 19 ? 0 : (w >= 21 && w <= 24) ? w - 20 : w == 36 ? 5 : w == 37 ? 6  // cold sector 0
+       : w == 20 ? 7
+       : (w >= 14 && w <= 17) ? w - 6 : (w >= 25 && w <= 28) ? w - 13           // cold sector 1
+       : (w == 29 || w == 30) ? w - 13 : w == 32 ? 18 : w == 35 ? 19             // cold sector 2
+       : w == 31 ? 0 : 1;                                                       // rest: 31, 34
 }
 __host__ __device__ constexpr int64_t pkt_word_index(int64_t n, int64_t i, int w) {
   return pkt_word_group(w) == 0   ? i * 16 + pkt_word_slot(w)
-         : pkt_word_group(w) == 1 ? 16 * n + i * 20 + pkt_word_slot(w)
-                                  : 36 * n + i * 2 + pkt_word_slot(w);
+         : pkt_word_group(w) == 1 ? 16 * n + i * PKT_COLD_WIDTH + pkt_word_slot(w)
+                                  : (16 + PKT_COLD_WIDTH) * n + i * 2 + pkt_word_slot(w);
 }
 #define PW(n, i, w) pkt_word_index((n), (i), (w))
 
@@ -236,6 +247,55 @@ __device__ __forceinline__ void pkt_store_cold(uint64_t *__restrict__ soa, int64
   W(37) = pack2(p.ma_level, p.ma_activatingline);
 #undef W
 }
+// k_ma_finish (a macro-atom deactivation): the hot line and what the deactivation reads of sector 0 (the macro-atom
+// state, trueemissiontype); a packet's first deactivation also reads the emission record and trueemission words it
+// turns into the trueemission record (macroatom.cc:475-482).  The other cold fields stay unread and unwritten.
+__device__ __forceinline__ void pkt_load_finish(const uint64_t *__restrict__ soa, int64_t n, int64_t i, Pkt &p) {
+#define W(k) soa[pkt_word_index(n, i, (k))]
+  pkt_load_hot(soa, n, i, p);
+  uint64_t w = W(19);
+  p.absorptiontype = lo32(w);
+  p.trueemissiontype = hi32(w);
+  w = W(36);
+  p.ma_element = lo32(w);
+  p.ma_ion = hi32(w);
+  w = W(37);
+  p.ma_level = lo32(w);
+  p.ma_activatingline = hi32(w);
+  if (p.trueemissiontype < 0) {
+    for (int d = 0; d < 3; d++) p.em_pos[d] = asd(W(14 + d));
+    w = W(17);
+    p.em_time = lo32(w);
+    p.pad0 = hi32(w);
+    w = W(20);
+    p.trueem_time = lo32(w);
+    p.pad1 = hi32(w);
+    w = W(35);
+    p.pellet_nucindex = lo32(w);
+    p.trueemissionvelocity = __int_as_float(hi32(w));
+  }
+#undef W
+}
+// emitted: an r-packet left the deactivation (bb / fb: emission record, Stokes vector, polarisation direction);
+// first: the packet's first deactivation (pkt_load_finish read the trueemission words)
+__device__ __forceinline__ void pkt_store_finish(uint64_t *__restrict__ soa, int64_t n, int64_t i, const Pkt &p,
+                                                 bool emitted, bool first) {
+#define W(k) soa[pkt_word_index(n, i, (k))]
+  pkt_store_hot(soa, n, i, p);
+  if (emitted) {
+    for (int d = 0; d < 3; d++) W(14 + d) = asw(p.em_pos[d]);
+    reinterpret_cast<int32_t *>(&W(17))[0] = p.em_time;  // (the word's upper half is padding: left as it is)
+    for (int d = 0; d < 3; d++) W(25 + d) = asw(p.stokes[d]);
+    for (int d = 0; d < 3; d++) W(28 + d) = asw(p.pol_dir[d]);
+  }
+  if (first) {
+    W(19) = pack2(p.absorptiontype, p.trueemissiontype);
+    W(20) = pack2(p.trueem_time, p.pad1);
+    W(35) = pack2(p.pellet_nucindex, __float_as_int(p.trueemissionvelocity));
+  }
+#undef W
+}
+
 // hot fields only (the cold ones of `dst` are left as they are)
 __device__ __forceinline__ void pkt_copy_hot(Pkt &dst, const Pkt &src) {
   dst.where = src.where;

@@ -2141,24 +2141,44 @@ typedef const __attribute__((address_space(1))) u32x4 glb_uint4;
 struct WaveLines {
   u32x4 c[8];
 };
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+#ifndef ARTIS_MA_FETCH_ADDR
+#define ARTIS_MA_FETCH_ADDR 0
+#endif
+#if ARTIS_MA_FETCH_ADDR
+// xa: the wave's 64-entry LDS exchange slot for the lines' byte addresses (lane L's at (L & 7) * 8 + (L >> 3), so
+// that the eight addresses a lane loads for are contiguous).  Each lane forms its own line's 64-bit address once; a
+// reader adds its chunk offset, one 64-bit add per line (A/B: no faster than exchanging indices, the default)
+DEVFN void wave_fetch_issue(const void *base, uint32_t myline, WaveLines &w, lds_u64 *xa) {
+  const int lane = (int)__lane_id();
+  xa[(lane & 7) * 8 + (lane >> 3)] = (uint64_t)(uintptr_t)base + ((uint64_t)myline << 7);
+  __builtin_amdgcn_wave_barrier();
+  const lds_uint4 *xr = (const lds_uint4 *)(xa + 8 * (lane >> 3));
+  const u32x4 a0 = xr[0], a1 = xr[1], a2 = xr[2], a3 = xr[3];
+  const uint64_t ad[8] = {a0.x | (uint64_t)a0.y << 32, a0.z | (uint64_t)a0.w << 32, a1.x | (uint64_t)a1.y << 32,
+                          a1.z | (uint64_t)a1.w << 32, a2.x | (uint64_t)a2.y << 32, a2.z | (uint64_t)a2.w << 32,
+                          a3.x | (uint64_t)a3.y << 32, a3.z | (uint64_t)a3.w << 32};
+  const uint64_t coff = (uint64_t)(lane & 7) * 16;
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    w.c[i] = *(glb_uint4 *)(uintptr_t)(ad[i] + coff);  // (an idle lane names line 0)
+}
+#else
 // xi: the wave's 64-word LDS exchange slot for the line indices (lane L's index at (L & 7) * 8 + (L >> 3), so
 // that the eight indices a lane loads for are contiguous: one write, two 16-byte reads, one wait)
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-DEVFN void wave_fetch_issue(const void *base, uint32_t myline, WaveLines &w, lds_u32 *xi) {
+DEVFN void wave_fetch_issue(const void *base, uint32_t myline, WaveLines &w, lds_u64 *xa) {
   const int lane = (int)__lane_id();
+  lds_u32 *xi = (lds_u32 *)xa;
   glb_uint4 *g = (glb_uint4 *)base;
   xi[(lane & 7) * 8 + (lane >> 3)] = myline;
   __builtin_amdgcn_wave_barrier();
   const u32x4 i0 = ((lds_uint4 *)xi)[2 * (lane >> 3)], i1 = ((lds_uint4 *)xi)[2 * (lane >> 3) + 1];
   const uint32_t ls[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
 #pragma unroll
-  for (int i = 0; i < 8; i++)
-#ifdef ARTIS_MA_NT_FETCH  // A/B: streaming (non-temporal) line loads
-    w.c[i] = __builtin_nontemporal_load(&g[(size_t)ls[i] * 8 + (lane & 7)]);
-#else
-    w.c[i] = g[(size_t)ls[i] * 8 + (lane & 7)];  // (an idle lane names line 0)
-#endif
+  for (int i = 0; i < 8; i++) w.c[i] = g[(size_t)ls[i] * 8 + (lane & 7)];  // (an idle lane names line 0)
 }
+#endif
 DEVFN void wave_fetch_commit(const WaveLines &w, lds_uint4 *wl) {
   const int lane = (int)__lane_id();
 #pragma unroll
@@ -2198,6 +2218,16 @@ DEVFN MaMetaW ma_walk_load(const Ctx &K, int ul) { return ma_walk_load(K.T.ma_wa
 // least 1 below q (decided "not greater"); above qh + 1, at least 65536 above q (decided "greater"); only a high
 // half of qh or qh + 1 needs the low half and the banded comparison ma_key_cmp (~2 in 65536 comparisons).
 DEVFN uint32_t ma_qh(double q) { return ((uint32_t)q) >> 16; }
+// The walk's draws stay Philox words (artis_rng_jump_words) until a comparison needs the value itself:
+// q = z * MA_KEY_SCALE (z = artis_rng_word_unit(lo, hi), the reference-order expression), and a lower bound of its
+// high half from the word hi alone.  With T = hi = floor(m / 2^21) for the draw's 53-bit integer m, the exact
+// product m (2^32 - 1) / 2^53 lies in (T - 1, T + 1), and its double rounding moves it by less than 2^-21, so
+// floor(q) is T - 2, T - 1 or T and ma_qh_draw <= ma_qh(q) <= ma_qh_draw + 1.  A lower qh is still exact: it can
+// only be ma_qh(q) - 1 when q lies less than 3 above a multiple of 65536, so every high half it decides (below qh, or
+// above qh + 1) is decided the same way by ma_qh(q), and every other goes to the banded comparison with q as before
+// -- the same selections and the same undecided (deferred) jumps, without the conversions to double per jump.
+DEVFN uint32_t ma_qh_draw(uint32_t hi) { return (hi < 2u ? 0u : hi - 2u) >> 16; }
+DEVFN double ma_q_draw(uint32_t lo, uint32_t hi) { return artis_rng_word_unit(lo, hi) * MA_KEY_SCALE; }
 
 #ifdef ARTIS_STAMPS
 // diagnostic build: per selected action, [a] searches, [16 + a] MA_PENDING returns, [32 + a] probes
@@ -2219,7 +2249,7 @@ struct MaLaneR : MaLaneC {
   int lo, hi, end;     // binary search in progress over entries [lo, hi) of a range of `end` entries ...
   int base;            // ... at record positions base + i
   int blk;             // same-ion array in blocks: -1 while its separators are searched, then the block
-  double q2;           // the transition draw on the key scale
+  uint32_t q2lo, q2hi;  // the transition draw's Philox words (its value on the key scale: ma_q_draw)
   uint32_t q2h;
 };
 
@@ -2435,7 +2465,7 @@ DEVFN uint32_t ma_count_below(const u32x4 &k07, uint32_t k8, uint32_t t) {
 // draws (used only by a step that starts a jump; the RNG counter advances over the draws the jump consumes)
 template <class Keys>
 DEVFN int ma_step_cached(const Ctx &K, const MaHot &H, const LocalCounters &L, artis_rng &rng, MaLaneR &m, MaEnd &end,
-                         int number, const Keys &keys, const MaMetaW &meta, double z1, double z2) {
+                         int number, const Keys &keys, const MaMetaW &meta, const u32x4 &zw) {
 #ifdef ARTIS_STAMPS_SUB  // diagnostic: cycles of the step's sections, added by the first active lane
   struct SubStamp {
     const LocalCounters &L;
@@ -2465,16 +2495,16 @@ DEVFN int ma_step_cached(const Ctx &K, const MaHot &H, const LocalCounters &L, a
   const int lay_sd = (int)(wl1 & 0xffu), lay_md = (int)((wl1 >> 8) & 0xffu), lay_mu = (int)((wl1 >> 16) & 0xffu),
             lay_nbd = (int)(wl1 >> 24), lay_nbu = (int)(wl2 & 0xffu);
   const int lay_hot = meta.w1.w;
-  auto cmp = [&](int p, uint32_t hi, double q, uint32_t qh) -> int {
+  auto cmp = [&](int p, uint32_t hi, auto q, uint32_t qh) -> int {
     if (hi < qh) return -1;
     if (hi > qh + 1) return 1;
     if (keys.hi_only(K)) return 0;  // level-mode records hold the high halves only: undecided -> exact jump
-    return ma_key_cmp((hi << 16) | (uint32_t)gload(rec + lay_hot + p), q);
+    return ma_key_cmp((hi << 16) | (uint32_t)gload(rec + lay_hot + p), q());
   };
   if (m.sel < 0) {  // a new jump: the action is the first of the 9 running-sum keys (line 0) above q
     m.n0 = rng.n;
-    const double q = z1 * MA_KEY_SCALE;
-    const uint32_t qh = ma_qh(q);
+    const auto q = [&]() { return ma_q_draw(zw.x, zw.y); };
+    const uint32_t qh = ma_qh_draw(zw.y);
     rng.n++;
     u32x4 k07;
     uint32_t k8;
@@ -2506,8 +2536,9 @@ DEVFN int ma_step_cached(const Ctx &K, const MaHot &H, const LocalCounters &L, a
       return end.code;
     }
     if (sel == ARTIS_MA_ACTION_INTERNALUPHIGHERNT) return ma_apply_nt(K, L, rng, m, number);
-    m.q2 = z2 * MA_KEY_SCALE;
-    m.q2h = ma_qh(m.q2);
+    m.q2lo = zw.z;
+    m.q2hi = zw.w;
+    m.q2h = ma_qh_draw(zw.w);
     rng.n++;
     m.sel = sel;
     MA_DIAG(sel);
@@ -2583,7 +2614,7 @@ DEVFN int ma_step_cached(const Ctx &K, const MaHot &H, const LocalCounters &L, a
       return MA_PENDING;
     }
     probes++;
-    const int c = keys.hi_only(K) ? 0 : ma_key_cmp((h << 16) | (uint32_t)gload(rec + lay_hot + p), m.q2);
+    const int c = keys.hi_only(K) ? 0 : ma_key_cmp((h << 16) | (uint32_t)gload(rec + lay_hot + p), ma_q_draw(m.q2lo, m.q2hi));
     if (c == 0) {
       m.ntrans += probes;
       m.jumps--;
@@ -2656,8 +2687,8 @@ DEVFN int ma_step_cached(const Ctx &K, const MaHot &H, const LocalCounters &L, a
 // never waits for a line, so it runs to the end of the jump (the block of a two-level array: a second call).
 DEVFN int ma_jump_cached_global(const Ctx &K, const LocalCounters &L, artis_rng &rng, MaLaneC &mc, MaEnd &end,
                                 int number) {
-  double z1, z2;
-  artis_rng_jump_pair(&rng, &z1, &z2);
+  u32x4 zw;
+  artis_rng_jump_words(&rng, (uint32_t *)&zw);
   MaLaneR m;
   static_cast<MaLaneC &>(m) = mc;
   m.sel = -1;
@@ -2666,7 +2697,7 @@ DEVFN int ma_jump_cached_global(const Ctx &K, const LocalCounters &L, artis_rng 
   const KeysGlobal keys{K.C.ma_key + (size_t)m.line * 64};
   int r;
   do {
-    r = ma_step_cached(K, ma_hot(K), L, rng, m, end, number, keys, meta, z1, z2);
+    r = ma_step_cached(K, ma_hot(K), L, rng, m, end, number, keys, meta, zw);
   } while (r == MA_PENDING);
   if (r == MA_DEFER) rng.n = m.n0;
   mc = static_cast<MaLaneC &>(m);

@@ -389,9 +389,11 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
         // continuum-event call, which already wrote its cold words; the registers do not hold them.
         if (p.type == ARTIS_TYPE_ESCAPE) soa[PW(n, idx, 32)] = pack2(p.escape_type, p.escape_time);
         if (p.type == ARTIS_TYPE_MA && p.last_event == 1) {
+#ifndef ARTIS_DIAG_NO_ABSREC  // write-traffic diagnostic only (no absorption record): its share of k_rpkt's writes
           reinterpret_cast<int32_t *>(&soa[PW(n, idx, 19)])[0] = p.absorptiontype;
           soa[PW(n, idx, 21)] = asw(p.absorptionfreq);
           for (int d = 0; d < 3; d++) soa[PW(n, idx, 22 + d)] = asw(p.absorptiondir[d]);
+#endif
           soa[PW(n, idx, 36)] = pack2(p.ma_element, p.ma_ion);
           soa[PW(n, idx, 37)] = pack2(p.ma_level, p.ma_activatingline);
         } else if (p.type == ARTIS_TYPE_MA && W.ma_pre) {
@@ -401,15 +403,21 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_rpkt(const Ctx *__restrict
           p.ma_ion = hi32(w36);
           p.ma_level = lo32(w37);
         }
-        W.rng_n[idx] = x.rng.n;
         if (x.ok && p.prop_time < t2) {
           pendM = p.type == ARTIS_TYPE_MA;
           pendK = p.type == ARTIS_TYPE_KPKT || p.type == ARTIS_TYPE_PRE_KPKT;
         }
+        // the RNG counter for the packet's next kernel: a macro-atom with pre-tickets carries it in its ticket
+        // (wave_push_ma), and a packet that escaped or reached t2 draws nothing more this timestep
+        if (pendK || (pendM && !W.ma_pre)) W.rng_n[idx] = x.rng.n;
         have = false;
       }
     }
+#ifndef ARTIS_DIAG_NO_EST  // write-traffic diagnostic only (no J / nuJ / ffheating sums): their share of the writes
     wave_flush_estimators(x);  // the step's J / nuJ / ffheating terms, once per cell and wave where possible
+#else
+    x.est_mgi = -1;
+#endif
     if (coop) {
 #ifdef ARTIS_STAMPS
       const unsigned long long tb0 = wave_clock();
@@ -674,7 +682,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
   // per wave: the 128-byte hot line of each lane's current macro-atom record (ma_jump_cached), chunk-major
   __shared__ uint4 s_line[WAVE_BLOCK / 64][8 * 64];
-  __shared__ uint32_t s_xidx[WAVE_BLOCK / 64][64];  // line indices exchanged for the cooperative fetch
+  __shared__ __attribute__((aligned(16))) uint64_t s_xidx[WAVE_BLOCK / 64][64];  // line addresses exchanged for the cooperative fetch
   block_counters_init(s_ctr, s_work);
   LocalCounters L;
   L.ctr = &s_ctr[0];
@@ -705,10 +713,12 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
   L.diag = s_diag;
 #endif
   const unsigned long long st_t0 = wave_clock();
+  int refill_ma = W.refill_ma;
+  asm volatile("" : "+s"(refill_ma));  // (held in an SGPR: not reloaded from the kernel arguments every pass)
   while (true) {
     const bool idle = !have && !drained;
     const unsigned long long imask = __ballot(idle);
-    if (!__any(have) || __popcll(imask) >= W.refill_ma) {
+    if (!__any(have) || __popcll(imask) >= refill_ma) {
       st_refill++;
       const unsigned long long tr0 = wave_clock();
       if (W.mf_rec)
@@ -782,23 +792,22 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     // a lane whose current level has no record: its jump is made by the whole wave below
     const bool unc = LEVEL && have && mc.line == MA_NOLINE;
     MaMetaW meta;
-    double z1 = 0., z2 = 0.;
+    u32x4 zw = {0u, 0u, 0u, 0u};
     {
       // the level's metadata and, 8 lines per load instruction, every busy lane's record line; the lane's next two
       // draws are computed while they are in flight
       if (have) meta = ma_walk_load(H.ma_walk, mc.ul);
       const uint32_t myline = (have && !unc) ? mc.line + (uint32_t)mc.pline : 0u;  // (idle lanes: a harmless line 0)
       WaveLines wl;
-      wave_fetch_issue(H.ma_key, myline, wl, (lds_u32 *)&s_xidx[threadIdx.x >> 6][0]);
+      wave_fetch_issue(H.ma_key, myline, wl, (lds_u64 *)&s_xidx[threadIdx.x >> 6][0]);
       if (have && mc.sel < 0) {
 #ifdef ARTIS_DIAG_CHEAPRNG  // timing diagnostic only (wrong stream): the walk's cost without Philox
         uint64_t h = ((uint64_t)rng.key1 << 32) ^ rng.n;
         h = (h ^ (h >> 30)) * 0xbf58476d1ce4e5b9ull;
-        h = (h ^ (h >> 27)) * 0x94d049bb133111ebull;
-        z1 = (double)(h >> 11) * (1.0 / 9007199254740992.0);
-        z2 = (double)((h * 0x9E3779B97F4A7C15ull) >> 11) * (1.0 / 9007199254740992.0);
+        zw = u32x4{(uint32_t)h, (uint32_t)(h >> 32), (uint32_t)(h >> 16), (uint32_t)(h >> 40)};
 #else
-        artis_rng_jump_pair(&rng, &z1, &z2);  // (the jump's two draws, one Philox block: include/artis_rng.h)
+        // (the jump's two draws, one Philox block, kept as words: include/artis_rng.h, ma_qh_draw)
+        artis_rng_jump_words(&rng, (uint32_t *)&zw);
 #endif
       }
       wave_fetch_commit(wl, line - (threadIdx.x & 63));
@@ -811,13 +820,13 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     int r = MA_PENDING;
     if (have && !unc) {
       r = ma_step_cached(K, H, L, rng, mc, e, (int)rng.key1, KeysLds<LEVEL && ARTIS_MA_HI_ONLY>{line, mc.pline}, meta,
-                         z1, z2);
+                         zw);
 #ifdef ARTIS_STAMPS
       ts2 = wave_clock();
 #endif
     }
     // level mode: a jump the high key halves cannot decide is made by the wave below from the exact sums, with the
-    // lane's RNG counter back at the start of the jump (the same draws z1, z2), not parked for k_ma_exact
+    // lane's RNG counter back at the start of the jump (the same draws), not parked for k_ma_exact
     if (LEVEL && !COOP && unc) {  // -> k_ma_exact (a jump not yet begun: its draws start at the current counter)
       mc.n0 = rng.n;
       r = MA_DEFER;
@@ -826,7 +835,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
     if (COOP && r == MA_DEFER) {
       rng.n = mc.n0;
       // (a search that began in an earlier pass has no draws computed in this one)
-      artis_rng_jump_pair(&rng, &z1, &z2);
+      artis_rng_jump_words(&rng, (uint32_t *)&zw);
       unc_now = true;
       r = MA_PENDING;
     }
@@ -837,7 +846,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_ma(const Ctx *__restrict__
       int csel = MA_COOP_RANDOM;
       double cx = 0.;
       if (unc_now) {
-        csel = ma_coop_action(K, mc.k, mc.ul, z1, z2, &cx);
+        csel = ma_coop_action(K, mc.k, mc.ul, artis_rng_word_unit(zw.x, zw.y), artis_rng_word_unit(zw.z, zw.w), &cx);
         if (!ma_coop_needs_search(csel)) {
           r = ma_coop_apply(K, H, L, rng, mc, e, (int)rng.key1, csel, -1, 0u, meta);
           coop_sum++;
@@ -1207,7 +1216,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MA_FINISH_MINW) void k_ma_finish(const 
     unsigned jumps = 0;
     if (have) {
       idx = W.q[QF][slot];
-      pkt_load(soa, n, idx, p);
+      pkt_load_finish(soa, n, idx, p);
       x.nts = nts;
       x.rng = artis_rng_init(K.R.seed, p.number, nts, K.R.rank);
       if (W.mf_rec) {
@@ -1235,9 +1244,10 @@ __global__ __launch_bounds__(WAVE_BLOCK, MA_FINISH_MINW) void k_ma_finish(const 
     const double fb_nu = wave_select_continuum_nu(K, fb.want, fb.e, fb.ion, fb.lower, fb.upper, fb.T_e, fb.zrand);
     bool live = false;
     if (have) {
+      const bool first = p.trueemissiontype < 0;
       ma_finish_inl(x, p, e, jumps, fb.want ? fb_nu : -1.);
       if (!W.mf_rec) W.pend[idx].x = 0;
-      pkt_store(soa, n, idx, p);
+      pkt_store_finish(soa, n, idx, p, e.code == MA_END_BB || e.code == MA_END_FB, first);
       W.rng_n[idx] = x.rng.n;
       live = x.ok && p.prop_time < t2;
     }

@@ -76,11 +76,22 @@ ARTIS_HD uint64_t artis_rng_next53(artis_rng *s) {
  * one Philox evaluation per jump instead of two, on the engine's busiest kernel (part of deviation D1: the stream is
  * this library's definition, the same on both sides).  The caller advances s->n over the draws it consumes, as with
  * artis_rng_uniform; a jump that consumes only the action draw leaves counter n + 1 to the next draw. */
+ARTIS_HD void artis_rng_jump_words(const artis_rng *s, uint32_t w[4]) {
+  w[0] = s->n;
+  w[1] = 0x41525453u;
+  w[2] = s->nts;
+  w[3] = s->rank;
+  artis_philox4x32_10(w, s->key0, s->key1);
+}
+/* the uniform draw of words (lo, hi) of a block: the top 53 bits over 2^53 */
+ARTIS_HD double artis_rng_word_unit(uint32_t lo, uint32_t hi) {
+  return (double)((((uint64_t)hi << 32) | (uint64_t)lo) >> 11) * (1.0 / 9007199254740992.0);
+}
 ARTIS_HD void artis_rng_jump_pair(const artis_rng *s, double *z1, double *z2) {
-  uint32_t c[4] = {s->n, 0x41525453u, s->nts, s->rank};
-  artis_philox4x32_10(c, s->key0, s->key1);
-  *z1 = (double)((((uint64_t)c[1] << 32) | (uint64_t)c[0]) >> 11) * (1.0 / 9007199254740992.0);
-  *z2 = (double)((((uint64_t)c[3] << 32) | (uint64_t)c[2]) >> 11) * (1.0 / 9007199254740992.0);
+  uint32_t c[4];
+  artis_rng_jump_words(s, c);
+  *z1 = artis_rng_word_unit(c[0], c[1]);
+  *z2 = artis_rng_word_unit(c[2], c[3]);
 }
 
 /* gsl_rng_uniform: [0,1) */
