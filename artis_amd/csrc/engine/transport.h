@@ -1854,24 +1854,30 @@ DEVNI double select_continuum_nu(Tx &x, int e, int lowerion, int lower, int uppe
 }
 
 // select_continuum_nu's integral for every lane of the wave that asks for one (want; every lane of the wave calls
-// this, convergent): the lanes evaluate the requesting lane's npieces quadrature pieces in parallel (pieces q,
-// q + 64, ...; the same alpha_sp_piece values as the serial loops), and the two running sums are then added in the
-// reference's order from the evaluating lanes' registers (v_readlane), so the result is select_continuum_nu's bit
-// for bit.  zrand is the requesting lane's draw (1 - uniform, drawn by the caller where select_continuum_nu draws
-// it).  One fb emission costs the wave ~npieces / 16 integrand evaluations per lane instead of 8 npieces in one lane.
-#define WAVE_FB_MAXR 4  // pieces per lane held in registers (npieces <= 256; more: the serial loops)
+// this, convergent).  The requests are taken one continuum at a time: the lanes evaluate the continuum's npieces
+// quadrature pieces in parallel (pieces q, q + 64, ...; the same alpha_sp_piece values as the serial loops), one
+// pass adds them in the reference's order into the running sums P[i] (pieces 0 .. i-1) in the wave's LDS slot P,
+// and every lane asking for that continuum at the same T_e then finds its own frequency by a binary search over
+// them with its own draw.  alpha_sp after i pieces is total - P[i] and the reference's test zrand >= alpha_sp /
+// total flips once along i (the pieces are non-negative, so the rounded sums only grow), so the search stops where
+// the serial loop breaks and the result is select_continuum_nu's bit for bit.  zrand is the lane's draw (1 -
+// uniform, drawn by the caller where select_continuum_nu draws it).  A one-zone model's deactivations share a few
+// continua, so the serial pass is paid once per continuum and wave pass instead of twice per request.
+#define WAVE_FB_MAXR 4  // pieces per lane held in registers (npieces <= 256; more: evaluated in the serial pass)
+#define WAVE_FB_MAXP 256  // pieces whose running sums fit the LDS slot (more: the serial search per request)
+typedef __attribute__((address_space(3))) double lds_double;
 DEVFN double wave_select_continuum_nu(const Ctx &K, bool want, int e, int lowerion, int lower, int upperionlevel,
-                                      float T_e, double zrand) {
+                                      float T_e, double zrand, lds_double *P) {
   double result = 0.;
-  unsigned long long m = __ballot(want);
+  bool todo = want;
+  unsigned long long m = __ballot(todo);
   const int lane = (int)__lane_id();
   while (m) {
     const int ld = __ffsll((long long)m) - 1;
-    m &= m - 1;
     const int le = __builtin_amdgcn_readlane(e, ld), li = __builtin_amdgcn_readlane(lowerion, ld);
     const int ll = __builtin_amdgcn_readlane(lower, ld), lu = __builtin_amdgcn_readlane(upperionlevel, ld);
-    const float lT = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(T_e), ld));
-    const double lz = readlane_d(zrand, ld);
+    const int lTb = __builtin_amdgcn_readlane(__float_as_int(T_e), ld);
+    const float lT = __int_as_float(lTb);
     int target = 0;
     for (int t = 0; t < get_nphixstargets(K, le, li, ll); t++)
       if (get_phixsupperlevel(K, le, li, ll, t) == lu) {
@@ -1899,21 +1905,62 @@ DEVFN double wave_select_continuum_nu(const Ctx &K, bool want, int e, int loweri
         if ((j >> 6) == r) v = readlane_d(pc[r], j & 63);
       return v;
     };
-    double head = 0.;
-    for (int j = 0; j < npieces; j++) head += piece(j);
-    const double total_alpha_sp = head;
-    double alpha_sp_old = total_alpha_sp;
-    double alpha_sp = total_alpha_sp;
-    head = 0.;
-    int i;
-    for (i = 1; i < npieces; i++) {
-      alpha_sp_old = alpha_sp;
-      head += piece(i - 1);
-      alpha_sp = total_alpha_sp - head;
-      if (lz >= alpha_sp / total_alpha_sp) break;
+    // the lanes served by this pass: the same continuum at the same temperature (or only the first, when the running
+    // sums do not fit the LDS slot)
+    const bool shared = npieces >= 2 && npieces <= WAVE_FB_MAXP;
+    const bool same = todo && (shared ? (e == le && lowerion == li && lower == ll && upperionlevel == lu &&
+                                         __float_as_int(T_e) == lTb)
+                                      : lane == ld);
+    if (shared) {
+      double head = 0.;
+      if (lane == 0) P[0] = 0.;
+      for (int j = 0; j < npieces; j++) {
+        head += piece(j);
+        if (lane == 0) P[j + 1] = head;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const double total = head;
+      if (same) {
+        // the serial loop breaks at the first i in [1, npieces) with zrand >= (total - P[i]) / total
+        int lo = 1, hi = npieces;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (zrand >= (total - P[mid]) / total)
+            hi = mid;
+          else
+            lo = mid + 1;
+        }
+        // (no break: the loop ends with i = npieces, alpha_sp_old and alpha_sp of pieces npieces - 2 and npieces - 1)
+        const int i = lo, k = (i == npieces) ? npieces - 1 : i;
+        const double alpha_sp_old = total - P[k - 1], alpha_sp = total - P[k];
+        const double nuoffset = (total * zrand - alpha_sp_old) / (alpha_sp - alpha_sp_old) * deltanu;
+        result = nu_threshold + (i - 1) * deltanu + nuoffset;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();  // (the slot's readers are done before the next continuum's sums)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+      const double lz = readlane_d(zrand, ld);
+      double head = 0.;
+      for (int j = 0; j < npieces; j++) head += piece(j);
+      const double total_alpha_sp = head;
+      double alpha_sp_old = total_alpha_sp;
+      double alpha_sp = total_alpha_sp;
+      head = 0.;
+      int i;
+      for (i = 1; i < npieces; i++) {
+        alpha_sp_old = alpha_sp;
+        head += piece(i - 1);
+        alpha_sp = total_alpha_sp - head;
+        if (lz >= alpha_sp / total_alpha_sp) break;
+      }
+      const double nuoffset = (total_alpha_sp * lz - alpha_sp_old) / (alpha_sp - alpha_sp_old) * deltanu;
+      if (lane == ld) result = nu_threshold + (i - 1) * deltanu + nuoffset;
     }
-    const double nuoffset = (total_alpha_sp * lz - alpha_sp_old) / (alpha_sp - alpha_sp_old) * deltanu;
-    if (lane == ld) result = nu_threshold + (i - 1) * deltanu + nuoffset;
+    m &= ~__ballot(same);
+    todo = todo && !same;
   }
   return result;
 }

@@ -1193,6 +1193,8 @@ __global__ __launch_bounds__(WAVE_BLOCK, MA_FINISH_MINW) void k_ma_finish(const 
   CTX_IN_LDS(ctxp)
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
+  __shared__ double s_fbP[WAVE_BLOCK / 64][WAVE_FB_MAXP + 1];  // the waves' fb running sums (wave_select_continuum_nu)
+  lds_double *fbP = (lds_double *)&s_fbP[threadIdx.x >> 6][0];
   block_counters_init(s_ctr, s_work);
   LocalCounters L;
   L.ctr = &s_ctr[0];
@@ -1241,7 +1243,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MA_FINISH_MINW) void k_ma_finish(const 
         fb.zrand = 1. - artis_rng_uniform(&x.rng);
       }
     }
-    const double fb_nu = wave_select_continuum_nu(K, fb.want, fb.e, fb.ion, fb.lower, fb.upper, fb.T_e, fb.zrand);
+    const double fb_nu = wave_select_continuum_nu(K, fb.want, fb.e, fb.ion, fb.lower, fb.upper, fb.T_e, fb.zrand, fbP);
     bool live = false;
     if (have) {
       const bool first = p.trueemissiontype < 0;
@@ -1319,6 +1321,8 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_kpkt(const Ctx *__restrict__ ctx
   CTX_IN_LDS(ctxp)
   __shared__ unsigned long long s_ctr[ARTIS_COUNTER_COUNT + 1];
   __shared__ unsigned long long s_work[ARTIS_WORK_COUNT];
+  __shared__ double s_fbP[WAVE_BLOCK / 64][WAVE_FB_MAXP + 1];  // the waves' fb running sums (wave_select_continuum_nu)
+  lds_double *fbP = (lds_double *)&s_fbP[threadIdx.x >> 6][0];
   block_counters_init(s_ctr, s_work);
   LocalCounters L;
   L.ctr = &s_ctr[0];
@@ -1358,7 +1362,7 @@ __global__ __launch_bounds__(WAVE_BLOCK) void k_kpkt(const Ctx *__restrict__ ctx
         else
           do_kpkt(x, p, t2, &fb);
       }
-      const double nu = wave_select_continuum_nu(K, fb.want, fb.e, fb.ion, fb.lower, fb.upper, fb.T_e, fb.zrand);
+      const double nu = wave_select_continuum_nu(K, fb.want, fb.e, fb.ion, fb.lower, fb.upper, fb.T_e, fb.zrand, fbP);
       if (fb.want) kpkt_fb_tail(x, p, fb.e, fb.ion, fb.lower, fb.upper, nu);
       if (kp && ++guard > 1000) x.err(ERR_STUCK, p.number, 4);
     }
