@@ -1348,11 +1348,14 @@ int vpkt_collect(const unsigned long long before[8]) {
   G.last_vpkt_work[3] = (int64_t)((after[1] + after[2] + after[3]) - (before[1] + before[2] + before[3]));
 #ifdef ARTIS_DIAG_VPKT_PASSES
   if (getenv("ARTIS_GPU_STATS")) {
-    unsigned long long dg[8];
+    unsigned long long dg[16];
     HIPCHK(hipMemcpyFromSymbol(dg, HIP_SYMBOL(g_vpkt_diag), sizeof(dg)));
     fprintf(stderr, "[artis_gpu] k_vpkt (cumulative): wave passes %llu, busy lanes/pass %.1f, tracing lanes/pass %.1f, "
             "passes/refill %.1f, cycles/pass %.0f, refill cycles/pass %.0f\n", dg[0], (double)dg[1] / dg[0],
             (double)dg[2] / dg[0], (double)dg[0] / dg[3], (double)dg[4] / dg[0], (double)dg[5] / dg[0]);
+    fprintf(stderr, "[artis_gpu] k_vpkt cycles/pass by phase: trace start %.0f, boundary + continuum %.0f, line walk %.0f, "
+            "segment end %.0f, escape %.0f\n", (double)dg[6] / dg[0], (double)dg[7] / dg[0], (double)dg[8] / dg[0],
+            (double)dg[9] / dg[0], (double)dg[10] / dg[0]);
   }
 #endif
   return 0;
@@ -2911,9 +2914,9 @@ int artis_gpu_vpkt_init(const artis_vpkt_params *vp) {
   rc |= dupload(&V.anumber, anum.data(), anum.size());
   {
     // per line, the spectra whose optical depth its opacity enters (vpkt.cc:283-294: exclude -1 drops every
-    // line, exclude Z the lines of element Z); padded for the walk's 8-line windows
+    // line, exclude Z the lines of element Z); padded for the walk's 16-line windows
     const size_t nli = G.h_line_elem.size();
-    std::vector<uint8_t> mask((nli + 7) / 8 * 8 + 8, 0);
+    std::vector<uint8_t> mask((nli + 15) / 16 * 16 + 16, 0);
     for (size_t li = 0; li < nli; li++) {
       const int an = anum.empty() ? 0 : anum[G.h_line_elem[li]];
       uint8_t m = 0;
@@ -3230,7 +3233,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   rc |= dupload(&T.phixs_xs, a->phixs_xs, (size_t)ntables * a->nphixspoints);
   rc |= dupload(&T.line_nu, a->line_nu, nli);
   {
-    std::vector<double> nu8((size_t)(nli + 7) / 8 * 8 + 8, 0.);
+    std::vector<double> nu8((size_t)(nli + 15) / 16 * 16 + 16, 0.);  // (padded for 16-line windows, k_vpkt)
     std::copy(a->line_nu, a->line_nu + nli, nu8.begin());
     rc |= dupload(&T.line_nu8, nu8.data(), nu8.size());
   }
@@ -3742,7 +3745,7 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
   // per line themselves (the same coefficient, bit for bit).
   C.linecoef = nullptr;
   C.linecoef_rows = 0;
-  C.linecoef_stride = ((int64_t)G.K.T.nlines + 7) / 8 * 8;
+  C.linecoef_stride = ((int64_t)G.K.T.nlines + 15) / 16 * 16;  // (whole 16-line windows: k_vpkt)
   {
     size_t freeb = 0, totalb = 0;
     (void)hipMemGetInfo(&freeb, &totalb);

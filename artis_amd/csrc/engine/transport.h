@@ -768,22 +768,26 @@ DEVFN void move_dummy(const Ctx &K, double pos[3], const double dir[3], double &
 #define WAVE_BLOCK_T 256  // threads per block of the kernels that set Tx::win (k_rpkt: WAVE_BLOCK)
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(1))) f64x2 glb_f64x2;
-DEVFN void lc_window(const double *nu8, const double *coef, __attribute__((address_space(3))) double *win) {
+template <int WIN>
+DEVFN void lc_window_n(const double *nu8, const double *coef, __attribute__((address_space(3))) double *win) {
   glb_f64x2 *nu = (glb_f64x2 *)nu8;
   glb_f64x2 *co = (glb_f64x2 *)coef;
-  f64x2 a[LC_WIN / 2], b[LC_WIN / 2];
+  f64x2 a[WIN / 2], b[WIN / 2];
 #pragma unroll
-  for (int i = 0; i < LC_WIN / 2; i++) {
+  for (int i = 0; i < WIN / 2; i++) {
     a[i] = nu[i];
     b[i] = co[i];
   }
 #pragma unroll
-  for (int i = 0; i < LC_WIN / 2; i++) {
+  for (int i = 0; i < WIN / 2; i++) {
     win[(2 * i) * WAVE_BLOCK_T] = a[i].x;
     win[(2 * i + 1) * WAVE_BLOCK_T] = a[i].y;
-    win[(LC_WIN + 2 * i) * WAVE_BLOCK_T] = b[i].x;
-    win[(LC_WIN + 2 * i + 1) * WAVE_BLOCK_T] = b[i].y;
+    win[(WIN + 2 * i) * WAVE_BLOCK_T] = b[i].x;
+    win[(WIN + 2 * i + 1) * WAVE_BLOCK_T] = b[i].y;
   }
+}
+DEVFN void lc_window(const double *nu8, const double *coef, __attribute__((address_space(3))) double *win) {
+  lc_window_n<LC_WIN>(nu8, coef, win);
 }
 
 // One r-packet step (rpkt.cc:623-813) in three parts, so that k_rpkt can spread its line walk over passes:

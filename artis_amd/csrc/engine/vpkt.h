@@ -120,7 +120,10 @@ struct VLane {
   bool inlines;
   int snext, pf_base;
   double sdist, ldist;
-  uint64_t wm;
+  uint64_t wm, wm2;  // the window's line masks (lines 0-7, 8-15)
+#ifdef ARTIS_DIAG_VPKT_PASSES
+  unsigned long long vst[5] = {0, 0, 0, 0, 0};
+#endif
 };
 
 // rlc_emiss_vpkt prologue (vpkt.cc:93-193): the dummy packet, its Stokes vector and weight p_n
@@ -228,6 +231,31 @@ DEVFN void vpkt_trace_finish(const Ctx &K, VLane &v) {
 }
 
 enum { VSEG_CONTINUE = 0, VSEG_ESCAPED = 1, VSEG_KILLED = 2, VSEG_PENDING = 3 };
+// lines per LDS window of the walk over a coefficient row: one memory round trip per VLC_WIN lines (k_rpkt: LC_WIN).
+// The phase stamps (ARTIS_DIAG_VPKT_PASSES) put 54 % of a pass in the line walk; 16-line windows (half the window
+// round trips) made k_vpkt 2 % slower (3802 -> 3871 ms per 2e6-packet config-5 step, profiles/r6n_vpkt_phases.txt):
+// the walk waits on its per-line dependency chain, not on the windows
+#ifndef VLC_WIN
+#define VLC_WIN 8
+#endif
+static_assert(VLC_WIN == 8 || VLC_WIN == 16, "line masks: two 64-bit words");
+#ifdef ARTIS_DIAG_VPKT_PASSES  // diagnostic build: wave cycles per phase of a pass, kept by the phase's first active lane
+                               // (VLane::vst) and added to g_vpkt_diag once per lane at the end
+__device__ unsigned long long g_vpkt_diag[16];
+#define VSTAMP_T0(t) const unsigned long long t = __builtin_amdgcn_s_memtime()
+#define VSTAMP_ADD(t, slot)                                                              \
+  do {                                                                                   \
+    const unsigned long long _dt = __builtin_amdgcn_s_memtime() - (t);                   \
+    if ((int)__lane_id() == __ffsll((long long)__ballot(1)) - 1) v.vst[(slot) - 6] += _dt;        \
+  } while (0)
+#else
+#define VSTAMP_T0(t) \
+  do {               \
+  } while (0)
+#define VSTAMP_ADD(t, slot) \
+  do {                      \
+  } while (0)
+#endif
 // lines a lane walks per pass of k_vpkt before the wave moves on (the walk resumes next pass): the lanes' walks
 // differ in length by orders of magnitude, and an unbounded walk holds the wave for its longest lane
 #ifndef VPKT_LINES_PER_PASS
@@ -358,6 +386,7 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
     return dead == nspec;
   };
   if (!v.inlines) {
+    VSTAMP_T0(vt_seg);
     int snext = -1;
     const double sdist = boundary_cross(x, d, &snext);
     if (((snext != -99) && (snext < 0)) || (snext >= K.G.ngrid)) {
@@ -389,12 +418,13 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
       else
         v.tau[ind] += kap_cont * s_cont;
     }
+    VSTAMP_ADD(vt_seg, 7);
     if (!vpkt_alive<NS>(V, v.tau)) return VSEG_KILLED;
     v.sdist = sdist;
     v.snext = snext;
     v.ldist = 0.;
     v.pf_base = -(1 << 20);
-    v.wm = 0;
+    v.wm = v.wm2 = 0;
     if (K.C.ne_index[v.mgi] < K.C.linecoef_rows) {
       v.inlines = true;
     } else {
@@ -419,10 +449,11 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
     const double sdist = v.sdist;
     double ldist = v.ldist;
     int pf_base = v.pf_base;
-    uint64_t wm = v.wm;
+    uint64_t wm = v.wm, wm2 = v.wm2;
     int budget = VPKT_LINES_PER_PASS;
     bool done = false;
     const bool negc = __builtin_amdgcn_readfirstlane(V.neg_coef) != 0;  // (wave-uniform: a scalar branch per line)
+    VSTAMP_T0(vt_walk);
 #ifdef ARTIS_DIAG_VPKT_NOLINES  // timing diagnostic only (no line opacity): the cost of the line walk
     ldist = sdist;
 #endif
@@ -438,18 +469,24 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
         done = true;
         break;  // D9
       }
-      if ((unsigned)(lineindex - pf_base) >= (unsigned)LC_WIN) {
+      if ((unsigned)(lineindex - pf_base) >= (unsigned)VLC_WIN) {
         if (pf_base >= 0 && all_dead()) {
           v.inlines = false;
           return VSEG_KILLED;
         }
-        pf_base = lineindex & ~(LC_WIN - 1);
-        lc_window(nu8 + pf_base, crow + pf_base, win);
-        wm = *(const __attribute__((address_space(1))) uint64_t *)(lmask + pf_base);
+        pf_base = lineindex & ~(VLC_WIN - 1);
+        lc_window_n<VLC_WIN>(nu8 + pf_base, crow + pf_base, win);
+        if constexpr (VLC_WIN == 8) {
+          wm = *(const __attribute__((address_space(1))) uint64_t *)(lmask + pf_base);
+        } else {
+          const u32x4 mw = *(glb_uint4 *)(lmask + pf_base);
+          wm = mw.x | ((uint64_t)mw.y << 32);
+          wm2 = mw.z | ((uint64_t)mw.w << 32);
+        }
       }
       const int pj = lineindex - pf_base;
       const double nutrans = win[pj * WAVE_BLOCK_T];
-      const unsigned lm = (unsigned)(wm >> (8 * pj)) & 0xffu;
+      const unsigned lm = (unsigned)((pj < 8 ? wm : wm2) >> (8 * (pj & 7))) & 0xffu;
       d.next_trans = lineindex + 1;
       if (d.nu_cmf < nutrans)
         ldist = 0;
@@ -462,7 +499,7 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
       }
       lines++;
       const double t_line = t_current + ldist / ARTIS_CLIGHT;
-      const double dtau = win[(LC_WIN + pj) * WAVE_BLOCK_T] * t_line;
+      const double dtau = win[(VLC_WIN + pj) * WAVE_BLOCK_T] * t_line;
       // a population inversion (NLTE) gives a negative coefficient: the only way a tau can fall again, so a
       // virtual packet that died at an earlier line of the window is killed here, before it could revive (tables
       // without a negative coefficient skip the test)
@@ -474,22 +511,27 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
       for (int ind = 0; ind < NS; ind++)
         if ((lm >> ind) & 1u) v.tau[ind] += dtau;
     }
+    VSTAMP_ADD(vt_walk, 8);
     if (!done) {
       v.ldist = ldist;
       v.pf_base = pf_base;
       v.wm = wm;
+      v.wm2 = wm2;
       return VSEG_PENDING;
     }
     v.inlines = false;
     if (all_dead()) return VSEG_KILLED;
-    return vpkt_segment_end(x, v, sdist, v.snext);
+    VSTAMP_T0(vt_end);
+    const int rend = vpkt_segment_end(x, v, sdist, v.snext);
+    VSTAMP_ADD(vt_end, 9);
+    return rend;
   }
 }
 
-#ifdef ARTIS_DIAG_VPKT_PASSES  // diagnostic build: [0] wave passes, [1] busy lane-passes, [2] tracing lane-passes,
-                               // [3] refills, [4] wave cycles (s_memtime), [5] cycles in refills
-__device__ unsigned long long g_vpkt_diag[8];
-#endif
+// ARTIS_DIAG_VPKT_PASSES: g_vpkt_diag [0] wave passes, [1] busy lane-passes, [2] tracing lane-passes, [3] refills,
+// [4] wave cycles (s_memtime), [5] cycles in refills; wave cycles in [6] the trace start (range + vpkt_trace_init),
+// [7] the segment's boundary + continuum, [8] the line walk, [9] the segment's end (move, change_cell), [10] the
+// escape (vpkt_trace_finish)
 
 // all (spawn, observer) work items of the spawn buffer; spawn_ctr[1] is the fetch head
 template <int PF, int MINW, int NS = VPKT_MAX_SPECTRA>
@@ -502,7 +544,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
   LocalCounters L;
   L.ctr = &s_ctr[0];
   L.work = &s_work[0];
-  __shared__ double s_win[2 * LC_WIN][WAVE_BLOCK];  // line windows of the walk over DevCells::linecoef
+  __shared__ double s_win[2 * VLC_WIN][WAVE_BLOCK];  // line windows of the walk over DevCells::linecoef
   static_assert(WAVE_BLOCK == WAVE_BLOCK_T, "Tx::win column stride");
   Tx x(K, L);
   x.win = (__attribute__((address_space(3))) double *)&s_win[0][threadIdx.x];
@@ -565,6 +607,7 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
 #endif
     if (have) {
       if (!v.tracing) {
+        VSTAMP_T0(vt_init);
         // vpkt.cc:872-888: the next frequency range this emission falls into, with the current observer vector
         const double nu_cmf = V.spawn[6 * cap + v.s];
         while (v.range < V.nrange) {
@@ -580,11 +623,14 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
         } else {
           have = false;
         }
+        VSTAMP_ADD(vt_init, 6);
       } else {
         const int r = vpkt_trace_segment<PF, NS>(x, v, lines);
         if (r != VSEG_CONTINUE && r != VSEG_PENDING) {
           if (r == VSEG_ESCAPED) {
+            VSTAMP_T0(vt_fin);
             vpkt_trace_finish<NS>(K, v);
+            VSTAMP_ADD(vt_fin, 10);
             n_esc1 += v.realtype == 1;
             n_esc2 += v.realtype == 2;
             n_esc3 += v.realtype == 3;
@@ -598,6 +644,8 @@ __global__ __launch_bounds__(WAVE_BLOCK, MINW) void k_vpkt(const Ctx *__restrict
   dg[4] = __builtin_amdgcn_s_memtime() - dg_t0;
   if (lane_id() == 0)
     for (int i = 0; i < 6; i++) atomicAdd(&g_vpkt_diag[i], dg[i]);
+  for (int i = 0; i < 5; i++)
+    if (v.vst[i]) atomicAdd(&g_vpkt_diag[6 + i], v.vst[i]);
 #endif
   if (lines) atomicAdd(&V.ctr[6], lines);
   if (n_traced) atomicAdd(&V.ctr[0], n_traced);  // nvpkt
