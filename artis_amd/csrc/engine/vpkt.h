@@ -238,6 +238,9 @@ enum { VSEG_CONTINUE = 0, VSEG_ESCAPED = 1, VSEG_KILLED = 2, VSEG_PENDING = 3 };
 #ifndef VLC_WIN
 #define VLC_WIN 8
 #endif
+#ifndef VPKT_LINE_BATCH
+#define VPKT_LINE_BATCH VLC_WIN  // lines of a window evaluated side by side (1: the serial loop)
+#endif
 static_assert(VLC_WIN == 8 || VLC_WIN == 16, "line masks: two 64-bit words");
 #ifdef ARTIS_DIAG_VPKT_PASSES  // diagnostic build: wave cycles per phase of a pass, kept by the phase's first active lane
                                // (VLane::vst) and added to g_vpkt_diag once per lane at the end
@@ -484,6 +487,60 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
           wm2 = mw.z | ((uint64_t)mw.w << 32);
         }
       }
+#if VPKT_LINE_BATCH > 1
+      // the next lines of the window as one batch: the lines are consecutive (closest_transition returns next_trans
+      // once the walk is past its first line), so their distances, line times and optical depths are independent
+      // and are computed side by side -- the per-line chain of two FP64 divisions was the walk's latency -- and then
+      // taken in order exactly as the serial loop takes them (break at ldist > sdist, the dead-packet test at a
+      // negative coefficient, the tau sums line by line)
+      const int pj0 = lineindex - pf_base;
+      const int nb = min(min(VLC_WIN - pj0, budget + 1), nlines - lineindex);
+      budget -= nb - 1;
+      const double nu_cmf = d.nu_cmf;
+      double lq[VPKT_LINE_BATCH], dq[VPKT_LINE_BATCH];
+#pragma unroll
+      for (int q = 0; q < VPKT_LINE_BATCH; q++) {
+        const int pq = min(pj0 + q, VLC_WIN - 1);
+        const double nutrans = win[pq * WAVE_BLOCK_T];
+        lq[q] = (nu_cmf < nutrans) ? 0. : ARTIS_CLIGHT * t_current * (nu_cmf / nutrans - 1);
+        const double t_line = t_current + lq[q] / ARTIS_CLIGHT;
+        dq[q] = win[(VLC_WIN + pq) * WAVE_BLOCK_T] * t_line;
+      }
+      bool stop = false, killed = false;
+#pragma unroll
+      for (int q = 0; q < VPKT_LINE_BATCH; q++) {
+        if (q < nb && !stop) {
+          if (q > 0 && !(ldist < sdist)) {
+            done = stop = true;
+          } else {
+            d.next_trans = lineindex + q + 1;
+            if (lq[q] > sdist) {
+              ldist = lq[q];
+              d.next_trans -= 1;
+              done = stop = true;
+            } else {
+              ldist = lq[q];
+              lines++;
+              const int pj = pj0 + q;
+              const unsigned lm = (unsigned)((pj < 8 ? wm : wm2) >> (8 * (pj & 7))) & 0xffu;
+              if (negc && dq[q] < 0. && all_dead()) {
+                killed = stop = true;
+              } else {
+#pragma unroll
+                for (int ind = 0; ind < NS; ind++)
+                  if ((lm >> ind) & 1u) v.tau[ind] += dq[q];
+              }
+            }
+          }
+        }
+      }
+      if (killed) {
+        v.inlines = false;
+        return VSEG_KILLED;
+      }
+      if (done) break;
+    }
+#else
       const int pj = lineindex - pf_base;
       const double nutrans = win[pj * WAVE_BLOCK_T];
       const unsigned lm = (unsigned)((pj < 8 ? wm : wm2) >> (8 * (pj & 7))) & 0xffu;
@@ -511,6 +568,7 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
       for (int ind = 0; ind < NS; ind++)
         if ((lm >> ind) & 1u) v.tau[ind] += dtau;
     }
+#endif
     VSTAMP_ADD(vt_walk, 8);
     if (!done) {
       v.ldist = ldist;
