@@ -623,7 +623,13 @@ DEVFN void bf_contribution_batch(const Ctx &K, const BfCell (&cell)[U], const in
 DEVFN void bf_range(const Ctx &K, double nu, int &lo, int &hi) {
   const double2 *e = K.T.bf_edge2;
   const int nb = K.T.nbf;
-  // hi: the first continuum with nu < nu_edge (nb if none); lo: the first with nu <= nu_max, at most hi
+  // hi: the first continuum with nu < nu_edge (nb if none); lo: the first with nu <= nu_max, at most hi.  Below
+  // the lowest edge both are 0 (one load instead of the search's chain of dependent ones: the virtual packets of
+  // config 5 and every r-packet redward of the continua)
+  if (nb == 0 || nu < e[0].x) {
+    lo = hi = 0;
+    return;
+  }
   int h = 0, l = 0;
   for (int step = nb > 0 ? 1 << (31 - __clz(nb)) : 0; step > 0; step >>= 1) {
     if (h + step <= nb && !(nu < e[h + step - 1].x)) h += step;
