@@ -498,7 +498,7 @@ DEVFN int vpkt_trace_segment(Tx &x, VLane &v, unsigned long long &lines) {
       // taken in order exactly as the serial loop takes them (break at ldist > sdist, the dead-packet test at a
       // negative coefficient, the tau sums line by line)
       const int pj0 = lineindex - pf_base;
-      const int nb = min(min(VLC_WIN - pj0, budget + 1), nlines - lineindex);
+      const int nb = min(min(min(VLC_WIN - pj0, VPKT_LINE_BATCH), budget + 1), nlines - lineindex);
       budget -= nb - 1;
       const double nu_cmf = d.nu_cmf;
       double lq[VPKT_LINE_BATCH], dq[VPKT_LINE_BATCH];
