@@ -281,7 +281,10 @@ __global__ void k_cooling(Ctx K) {
 // One launch covers the kn cells cells[0 .. kn): the cached cells (row order) with cache = true (scratch stride
 // kn), the others with cache = false (totals into marates).
 // k_marates' work for one (cell, level): the running sums into rec[p * stride] (cache), the action totals into pr
-DEVFN void marates_sums(const Ctx &K, int ul, int k, double t_mid, double *__restrict__ rec, int64_t stride, bool cache,
+// (cache a template parameter: each instance's transition loop has one path, so the population loaded for the next
+// transition is waited for without waiting for the running-sum stores issued after it)
+template <bool cache>
+DEVFN void marates_sums(const Ctx &K, int ul, int k, double t_mid, double *__restrict__ rec, int64_t stride,
                         double pr[ARTIS_MA_ACTION_COUNT]) {
   const int64_t nne_cells = K.C.n_nonempty;
   const int mgi = K.C.ne_mgi[k];
@@ -292,7 +295,11 @@ DEVFN void marates_sums(const Ctx &K, int ul, int k, double t_mid, double *__res
   const int cum_rint = cum_rrad + mm.nr, cum_uhi = cum_rint + mm.nr;
   for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) pr[a] = 0.;
   const double *popsT = K.C.popsT + k;  // popsT[u * nne_cells]: level u of this lane's cell
+#ifdef ARTIS_MARATES_PLAIN  // A/B: the plain ma_foreach_rate loop
   ma_foreach_rate(
+#else
+  ma_foreach_rate_pf(
+#endif
       K, mgi, ul, t_mid, [&](int u) { return popsT[(int64_t)u * nne_cells]; },
       [&](int slot) { return K.C.corrphotT[(int64_t)slot * nne_cells + k]; },
       [&](int kind, int j, double R, double C, double et, double eg, double ec) {
@@ -300,7 +307,7 @@ DEVFN void marates_sums(const Ctx &K, int ul, int k, double t_mid, double *__res
 #ifdef ARTIS_DIAG_MARATES_NOSTORE  // timing diagnostic only (the records are not written): the rates' compute alone
         if (false) {
 #else
-        if (cache) {
+        if constexpr (cache) {
 #endif
           if (kind == MA_KIND_DOWN) {
             REC(cum_drad + j) = pr[ARTIS_MA_ACTION_RADDEEXC];
@@ -317,7 +324,7 @@ DEVFN void marates_sums(const Ctx &K, int ul, int k, double t_mid, double *__res
         return false;
       });
   pr[ARTIS_MA_ACTION_INTERNALUPHIGHERNT] = ma_nt_total(K, mgi, ul);
-  if (cache)
+  if constexpr (cache)
     for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) REC(a) = pr[a];
 #undef REC
 }
@@ -325,8 +332,9 @@ DEVFN void marates_sums(const Ctx &K, int ul, int k, double t_mid, double *__res
 // The rows of each level are padded to a multiple of 64 (MARATES_PAD), so that a wave never straddles two levels: the
 // level index is then wave-uniform (readfirstlane), and the atomic data the rates read are scalar loads.
 #define MARATES_PAD(kn) (((int64_t)(kn) + 63) & ~(int64_t)63)
+template <bool cache>
 __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict__ S, const int32_t *__restrict__ cells,
-                          int kn, bool cache) {
+                          int kn) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nl = K.T.nlevels_total;
   const int64_t knp = MARATES_PAD(kn);
@@ -340,8 +348,8 @@ __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict_
   double *rec = cache ? S + (K.T.ma_dbl_off[ul] - K.T.ma_dbl_off[ul0]) * knp + (int64_t)(kr >> 6) * len * 64 + (kr & 63)
                       : nullptr;
   double pr[ARTIS_MA_ACTION_COUNT];
-  marates_sums(K, ul, k, K.G.ts_mid[nts], rec, 64, cache, pr);
-  if (!cache) {
+  marates_sums<cache>(K, ul, k, K.G.ts_mid[nts], rec, 64, pr);
+  if constexpr (!cache) {
     double *out = K.C.marates + ((int64_t)k * nl + ul) * ARTIS_MA_ACTION_COUNT;
     for (int a = 0; a < ARTIS_MA_ACTION_COUNT; a++) out[a] = pr[a];
   }
@@ -368,6 +376,19 @@ DEVFN void mapack_tile(const Ctx &K, int ul, const double *__restrict__ src, int
   const int len = ARTIS_MA_ACTION_COUNT + 2 * mm.nd + mm.nu + 2 * mm.nr + mm.nt;
   const MaLayout lay = ma_layout(mm.nd, mm.nu, mm.nr, mm.nt);
   const int tx = threadIdx.x % P, ty = threadIdx.x / P;
+  // the tiles are double-buffered through registers: the next tile's loads are in flight while the current one is
+  // converted and stored (the first one's with the action totals' loads)
+  constexpr int NB = P * 64 / 256;  // doubles per thread and tile
+  double buf[NB];
+  auto fetch = [&](int p0) {
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      const int q = threadIdx.x + b * 256;  // (64 consecutive rows of one position per wave: coalesced)
+      const int pp = q / 64, rr = q % 64;
+      buf[b] = (p0 + pp < len && c0 + rr < nvalid) ? src[(int64_t)(p0 + pp) * n_s + c0 + rr] : 0.;
+    }
+  };
+  fetch(0);
   __syncthreads();  // (the previous tile's readers of S are done)
   if (threadIdx.x < 64 && c0 + threadIdx.x < nvalid) {
     const int r = threadIdx.x;
@@ -388,11 +409,13 @@ DEVFN void mapack_tile(const Ctx &K, int ul, const double *__restrict__ src, int
   const int b1 = ARTIS_MA_ACTION_COUNT + mm.nd, b2 = b1 + mm.nu, b3 = b2 + mm.nd, b4 = b3 + mm.nr, b5 = b4 + mm.nr;
   for (int p0 = 0; p0 < len; p0 += P) {
     __syncthreads();
-    for (int q = threadIdx.x; q < P * 64; q += 256) {  // (64 consecutive rows of one position per wave: coalesced)
-      const int pp = q / 64, rr = q % 64;
-      if (p0 + pp < len && c0 + rr < nvalid) S.tile[pp][rr] = src[(int64_t)(p0 + pp) * n_s + c0 + rr];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      const int q = threadIdx.x + b * 256;
+      S.tile[q / 64][q % 64] = buf[b];
     }
     __syncthreads();
+    if (p0 + P < len) fetch(p0 + P);
     const int p = p0 + tx;
     if (p < len) {
       const int a = (p < ARTIS_MA_ACTION_COUNT) ? -1
@@ -3297,6 +3320,56 @@ int artis_gpu_init(int device, const artis_atomic_tables *a, const artis_geometr
     }
     rc |= dupload(&T.exc_items, items.data(), items.size());
   }
+  {
+    // k_marates' packed transition items (MaDownItem / MaUpItem) indexed like downtrans_lineindex / uptrans_lineindex
+    size_t nd_items = 1, nu_items = 1;
+    for (int ul = 0; ul < nl; ul++) {
+      nd_items = std::max(nd_items, (size_t)a->level_downtrans_offset[ul] + (size_t)a->level_ndowntrans[ul]);
+      nu_items = std::max(nu_items, (size_t)a->level_uptrans_offset[ul] + (size_t)a->level_nuptrans[ul]);
+    }
+    std::vector<MaDownItem> di(nd_items);
+    std::vector<MaUpItem> ui_(nu_items);
+    for (int ui = 0; ui < a->nions_total; ui++) {
+      const int ul0 = a->ion_uniqueleveloffset[ui];
+      for (int l = 0; l < a->ion_nlevels[ui]; l++) {
+        const int ul = ul0 + l;
+        for (int j = 0; j < a->level_ndowntrans[ul]; j++) {
+          const int li = a->downtrans_lineindex[a->level_downtrans_offset[ul] + j];
+          const int lo = a->line_lowerlevelindex[li];
+          MaDownItem &x = di[a->level_downtrans_offset[ul] + j];
+          x = MaDownItem{};
+          x.lower = lo;
+          x.forbidden = a->line_forbidden[li];
+          x.A = a->line_einstein_A[li];
+          x.coll = a->line_coll_str[li];
+          x.osc_f = a->line_osc_strength[li];
+          x.lower_sw = a->level_stat_weight[ul0 + lo];
+          x.eps_target = a->level_epsilon[ul0 + lo];
+          x.B_ul = lm[li].B_ul;
+          x.B_lu = lm[li].B_lu;
+          x.P2 = lm[li].P2;
+        }
+        for (int j = 0; j < a->level_nuptrans[ul]; j++) {
+          const int li = a->uptrans_lineindex[a->level_uptrans_offset[ul] + j];
+          const int up = a->line_upperlevelindex[li];
+          MaUpItem &x = ui_[a->level_uptrans_offset[ul] + j];
+          x = MaUpItem{};
+          x.upper = up;
+          x.forbidden = a->line_forbidden[li];
+          x.coll = a->line_coll_str[li];
+          x.osc_f = a->line_osc_strength[li];
+          x.upper_sw = a->level_stat_weight[ul0 + up];
+          x.eps_upper = a->level_epsilon[ul0 + up];
+          x.B_ul = lm[li].B_ul;
+          x.B_lu = lm[li].B_lu;
+          x.nu3 = lm[li].nu3;
+          x.P2 = lm[li].P2;
+        }
+      }
+    }
+    rc |= dupload(&T.ma_down, di.data(), di.size());
+    rc |= dupload(&T.ma_up, ui_.data(), ui_.size());
+  }
   // macro-atom records per level (engine_dev.h DevCells::ma_rec): recombination targets are the ionising levels
   // of the lower ion for levels l <= maxrecombininglevel of ions i > 0 (macroatom.cc:104-124); up-higher targets
   // are the phixs targets of ionising levels of non-top ions (get_nphixstargets)
@@ -3980,8 +4053,8 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
     if (G.K.C.ma_level_mode) {
       // level mode: the action totals of every (cell, level) pair (the jumps without a record select from them),
       // then the records the placement chose
-      k_marates<<<(unsigned)((MARATES_PAD(n_ne) * nl + 255) / 256), 256, 0, G.stream>>>(G.K, nts, 0, (int)nl, nullptr,
-                                                                                       G.d_ma_bincell, n_ne, false);
+      k_marates<false><<<(unsigned)((MARATES_PAD(n_ne) * nl + 255) / 256), 256, 0, G.stream>>>(
+          G.K, nts, 0, (int)nl, nullptr, G.d_ma_bincell, n_ne);
       if (int rc = ma_level_build(nts)) return rc;
     } else if (mr > 0) {
       // batches of levels whose records fit the scratch
@@ -3989,8 +4062,8 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
         int ul1 = ul0 + 1;
         while (ul1 < nl && (G.h_dbl_off[ul1 + 1] - G.h_dbl_off[ul0]) * MARATES_PAD(mr) <= G.marec_scratch_doubles) ul1++;
         const int nlev = ul1 - ul0;
-        k_marates<<<(unsigned)((MARATES_PAD(mr) * nlev + 255) / 256), 256, 0, G.stream>>>(
-            G.K, nts, ul0, nlev, G.d_marec_scratch, G.d_ma_bincell, mr, true);
+        k_marates<true><<<(unsigned)((MARATES_PAD(mr) * nlev + 255) / 256), 256, 0, G.stream>>>(
+            G.K, nts, ul0, nlev, G.d_marec_scratch, G.d_ma_bincell, mr);
         k_mapack<<<dim3((unsigned)((mr + 63) / 64), (unsigned)nlev), 256, 0, G.stream>>>(G.K, ul0,
                                                                                          G.d_marec_scratch);
         ul0 = ul1;

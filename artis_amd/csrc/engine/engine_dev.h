@@ -61,6 +61,25 @@ struct TeExcItem {
   int32_t forbidden;
 };
 
+// k_marates' packed transition items (one 64-byte scalar load per transition, independent of the previous one, so
+// the next item and its population are fetched while the current rates are evaluated): what ma_foreach_rate reads of
+// a down transition (at level_downtrans_offset + j) and of an up transition (at level_uptrans_offset + j), the same
+// values from the same tables (macroatom.cc:57-159 via rad_deexc_core / col_deexc_core / rad_exc_core / col_exc_core)
+struct __attribute__((aligned(64))) MaDownItem {
+  int32_t lower;      // ion-local index of the lower level
+  int32_t forbidden;  // line_forbidden
+  float A, coll, osc_f, lower_sw;  // line_einstein_A, line_coll_str, line_osc_strength, stat weight of the lower level
+  double eps_target;  // epsilon of the lower level
+  double B_ul, B_lu, P2;  // LineMA
+};
+struct __attribute__((aligned(64))) MaUpItem {
+  int32_t upper;      // ion-local index of the upper level
+  int32_t forbidden;
+  float coll, osc_f, upper_sw, pad;
+  double eps_upper;   // epsilon of the upper level
+  double B_ul, B_lu, nu3, P2;  // LineMA
+};
+
 // one bf continuum's constants for bf_contribution (rpkt.cc:1075-1207), one 32-byte load: its edge, the last
 // frequency of its cross-section table (nu_edge * last_phixs_nuovernuedge), probability, table offset
 struct BfCont {
@@ -92,6 +111,8 @@ struct DevTab {
   const LineTau *line_tau;
   const LineMA *line_ma;
   const TeExcItem *exc_items;  // [sum nuptrans] indexed like uptrans_lineindex (k_cooling, k_te_solve)
+  const MaDownItem *ma_down;  // [sum ndowntrans] indexed like downtrans_lineindex (k_marates)
+  const MaUpItem *ma_up;      // [sum nuptrans] indexed like uptrans_lineindex (k_marates)
   // per level: offset (doubles) of its macro-atom record inside a cell's record block, #downtrans, #uptrans,
   // #recombination targets (ionising levels of the lower ion, 0 if the level does not recombine)
   const MaMeta *ma_meta;  // [nlevels_total]

@@ -230,19 +230,18 @@ DEVFN double calculate_sahafact(const Ctx &K, int e, int i, int l, int upperionl
   const double g_upper = stat_weight(K, e, i + 1, upperionlevel);
   return ARTIS_SAHACONST * g_lower / g_upper * pow(T, -1.5) * exp(E_threshold / ARTIS_KB / T);
 }
-// macroatom.h:52-105
-DEVFN double col_deexcitation_ratecoeff(const Ctx &K, float T_e, float nne, double epsilon_trans, int li,
-                                        double lowerstatweight, double upperstatweight) {
+// macroatom.h:52-105, on the line's values (coll_str_thisline, forbidden, osc_f, P2): col_deexcitation_ratecoeff
+// below reads them from the line tables, k_marates from its packed transition items (MaDownItem) -- one expression
+DEVFN double col_deexc_core(float T_e, float nne, double epsilon_trans, double coll_str_thisline, bool forbidden,
+                            float osc_f, double P2, double lowerstatweight, double upperstatweight) {
   double C = 0.;
-  const double coll_str_thisline = K.T.line_coll[li];
   if (coll_str_thisline < 0) {
-    if (!K.T.line_forbidden[li]) {
+    if (!forbidden) {
       const double eoverkt = epsilon_trans / (ARTIS_KB * T_e);
       const double g_bar = 0.2;
       const double gauntfac = (eoverkt > 0.33421) ? g_bar : 0.276 * exp(eoverkt) * (-0.5772156649 - log(eoverkt));
       const double g_ratio = lowerstatweight / upperstatweight;
-      C = ARTIS_C_0 * 14.51039491 * nne * sqrtf(T_e) * K.T.line_f[li] * K.T.line_ma[li].P2 * eoverkt * g_ratio *
-          gauntfac;
+      C = ARTIS_C_0 * 14.51039491 * nne * sqrtf(T_e) * osc_f * P2 * eoverkt * g_ratio * gauntfac;
     } else {
       C = nne * 8.629e-6 * 0.01 * lowerstatweight / sqrtf(T_e);
     }
@@ -251,20 +250,23 @@ DEVFN double col_deexcitation_ratecoeff(const Ctx &K, float T_e, float nne, doub
   }
   return C;
 }
-// macroatom.h:107-150
-DEVFN double col_excitation_ratecoeff(const Ctx &K, float T_e, float nne, int li, double epsilon_trans,
-                                      double lowerstatweight, double upperstatweight) {
+DEVFN double col_deexcitation_ratecoeff(const Ctx &K, float T_e, float nne, double epsilon_trans, int li,
+                                        double lowerstatweight, double upperstatweight) {
+  return col_deexc_core(T_e, nne, epsilon_trans, K.T.line_coll[li], K.T.line_forbidden[li] != 0, K.T.line_f[li],
+                        K.T.line_ma[li].P2, lowerstatweight, upperstatweight);
+}
+// macroatom.h:107-150, on the line's values as col_deexc_core
+DEVFN double col_exc_core(float T_e, float nne, double coll_strength, bool forbidden, float osc_f, double P2,
+                          double epsilon_trans, double lowerstatweight, double upperstatweight) {
   double C = 0.;
-  const double coll_strength = K.T.line_coll[li];
   const double eoverkt = epsilon_trans / (ARTIS_KB * T_e);
   if (coll_strength < 0) {
-    if (!K.T.line_forbidden[li]) {
+    if (!forbidden) {
       const double g_bar = 0.2;
       const double exp_eoverkt = exp(eoverkt);
       const double test = 0.276 * exp_eoverkt * (-0.5772156649 - log(eoverkt));
       const double Gamma = g_bar > test ? g_bar : test;
-      C = ARTIS_C_0 * nne * sqrtf(T_e) * 14.51039491 * K.T.line_f[li] * K.T.line_ma[li].P2 * eoverkt / exp_eoverkt *
-          Gamma;
+      C = ARTIS_C_0 * nne * sqrtf(T_e) * 14.51039491 * osc_f * P2 * eoverkt / exp_eoverkt * Gamma;
     } else {
       C = nne * 8.629e-6 * 0.01 * exp(-eoverkt) * upperstatweight / sqrtf(T_e);
     }
@@ -272,6 +274,11 @@ DEVFN double col_excitation_ratecoeff(const Ctx &K, float T_e, float nne, int li
     C = nne * 8.629e-6 * coll_strength * exp(-eoverkt) / lowerstatweight / sqrtf(T_e);
   }
   return C;
+}
+DEVFN double col_excitation_ratecoeff(const Ctx &K, float T_e, float nne, int li, double epsilon_trans,
+                                      double lowerstatweight, double upperstatweight) {
+  return col_exc_core(T_e, nne, K.T.line_coll[li], K.T.line_forbidden[li] != 0, K.T.line_f[li], K.T.line_ma[li].P2,
+                      epsilon_trans, lowerstatweight, upperstatweight);
 }
 // macroatom.h:107-150 col_excitation_ratecoeff on a packed item (TeExcItem, indexed like uptrans_lineindex): the same
 // expressions as col_excitation_ratecoeff above on the same values (epsilon_trans = epsilon(upper) - epsilon(level),
@@ -296,16 +303,18 @@ DEVFN double te_col_exc(const TeExcItem &it, float T_e, float nne, double lowers
   return C;
 }
 // macroatom.cc:503-548 (populations from the per-cell table, B coefficients from LineMA)
-DEVFN double rad_deexcitation_ratecoeff_n(const Ctx &K, double n_u, double n_l, int li, double t_current) {
+DEVFN double rad_deexc_core(double n_u, double n_l, double B_lu, double B_ul, double A_ul, double t_current) {
   double R = 0.0;
-  const LineMA lm = K.T.line_ma[li];
-  const double A_ul = K.T.line_A[li];
-  const double tau_sobolev = (lm.B_lu * n_l - lm.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_current;
+  const double tau_sobolev = (B_lu * n_l - B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_current;
   if (tau_sobolev > 1e-100) {
     const double beta = 1.0 / tau_sobolev * (-expm1(-tau_sobolev));
     R = A_ul * beta;
   }
   return R;
+}
+DEVFN double rad_deexcitation_ratecoeff_n(const Ctx &K, double n_u, double n_l, int li, double t_current) {
+  const LineMA lm = K.T.line_ma[li];
+  return rad_deexc_core(n_u, n_l, lm.B_lu, lm.B_ul, K.T.line_A[li], t_current);
 }
 DEVFN double rad_deexcitation_ratecoeff(const Ctx &K, const double *pops, int e, int i, int upper, int lower,
                                         double epsilon_trans, int li, double t_current) {
@@ -349,22 +358,26 @@ DEVFN double radfield_J(const Ctx &K, int mgi, double nu) {
 }
 // macroatom.cc:550-643 (J_nu = radfield(nu_trans), radfield.cc:898-943 / radfield.h:44-48, with pow(nu, 3)
 // precomputed per line)
-DEVFN double rad_excitation_ratecoeff_n(const Ctx &K, int mgi, double n_u, double n_l, double epsilon_trans, int li,
-                                        double t_current) {
+DEVFN double rad_exc_core(const Ctx &K, int mgi, double n_u, double n_l, double epsilon_trans, double B_lu, double B_ul,
+                          double nu3, double t_current) {
   double R = 0.0;
-  const LineMA lm = K.T.line_ma[li];
-  const double tau_sobolev = (lm.B_lu * n_l - lm.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_current;
+  const double tau_sobolev = (B_lu * n_l - B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI * t_current;
   if (tau_sobolev > 1e-100) {
     const double beta = 1.0 / tau_sobolev * (-expm1(-tau_sobolev));
-    const double R_over_J_nu = n_l > 0. ? (lm.B_lu - lm.B_ul * n_u / n_l) * beta : lm.B_lu * beta;
+    const double R_over_J_nu = n_l > 0. ? (B_lu - B_ul * n_u / n_l) * beta : B_lu * beta;
     const double nu_trans = epsilon_trans / ARTIS_H;
     float T_R, W;
     if (radfield_TW(K, mgi, nu_trans, T_R, W))
-      R = R_over_J_nu * (W * ARTIS_TWOHOVERCLIGHTSQUARED * lm.nu3 / expm1(ARTIS_HOVERKB * nu_trans / T_R));
+      R = R_over_J_nu * (W * ARTIS_TWOHOVERCLIGHTSQUARED * nu3 / expm1(ARTIS_HOVERKB * nu_trans / T_R));
     else
       R = R_over_J_nu * 0.;
   }
   return R;
+}
+DEVFN double rad_excitation_ratecoeff_n(const Ctx &K, int mgi, double n_u, double n_l, double epsilon_trans, int li,
+                                        double t_current) {
+  const LineMA lm = K.T.line_ma[li];
+  return rad_exc_core(K, mgi, n_u, n_l, epsilon_trans, lm.B_lu, lm.B_ul, lm.nu3, t_current);
 }
 DEVFN double rad_excitation_ratecoeff(const Ctx &K, const double *pops, int mgi, int e, int i, int lower, int upper,
                                       double epsilon_trans, int li, double t_current) {
@@ -514,6 +527,81 @@ DEVFN void ma_foreach_rate(const Ctx &K, int mgi, int ul, double t_mid, Pop pop,
     const double R = rad_excitation_ratecoeff_n(K, mgi, n_u, n_self, epsilon_trans, li, t_mid);
     const double C = col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, e, i, upper));
     if (f(MA_KIND_UP, j, R, C, epsilon_trans, 0., epsilon_current)) return;
+  }
+  if (i < K.T.elem_nions[e] - 1 && l < K.T.ion_ionisinglevels[ui]) {
+    const int nt = K.T.level_nphixstargets[ul];
+    const int slot0 = K.T.level_phixstargets_offset[ul];
+    for (int t = 0; t < nt; t++) {
+      const double epsilon_trans = get_phixs_threshold(K, e, i, l, t);
+      const double R = corrphot(slot0 + t);
+      const double C = col_ionization_ratecoeff(K, T_e, nne, e, i, l, t, epsilon_trans);
+      if (f(MA_KIND_UPHIGHER, t, R, C, epsilon_trans, 0., epsilon_current)) return;
+    }
+  }
+}
+
+// ma_foreach_rate for k_marates (the lanes of a wave on one level, so the transition data are wave-uniform): the same
+// calls of f with the same values, the down and up transitions read from the packed items (MaDownItem / MaUpItem)
+// and software-pipelined -- the item two transitions ahead and the population one ahead are in flight while the
+// current rates are evaluated (the plain loop waited on a chain of three dependent loads per transition).  The
+// population load is issued before the next item's scalar load: a wait for scalar loads covers all of them.
+template <typename Pop, typename Corr, typename F>
+DEVFN void ma_foreach_rate_pf(const Ctx &K, int mgi, int ul, double t_mid, Pop pop, Corr corrphot, F f) {
+  const int ui = K.T.level_ui[ul];
+  const int e = K.T.ion_element[ui];
+  const int i = ui - K.T.elem_uniqueionoffset[e];
+  const int l = ul - K.T.ion_uniqueleveloffset[ui];
+  const int base = ul - l;
+  const float T_e = K.C.Te[mgi];
+  const float nne = K.C.nne[mgi];
+  const double n_self = pop(ul);
+  const double epsilon_current = K.T.level_epsilon[ul];
+  const double statweight = K.T.level_stat_weight[ul];
+  const int ndowntrans = K.T.level_ndowntrans[ul];
+  if (ndowntrans > 0) {
+    const MaDownItem *DI = K.T.ma_down + K.T.level_downtrans_offset[ul];
+    MaDownItem c = DI[0], n1 = DI[ndowntrans > 1 ? 1 : 0];
+    double pc = pop(base + c.lower);
+    for (int j = 0; j < ndowntrans; j++) {
+      const double pn = pop(base + n1.lower);
+      const MaDownItem n2 = DI[min(j + 2, ndowntrans - 1)];
+      const double epsilon_trans = epsilon_current - c.eps_target;
+      const double R = rad_deexc_core(n_self, pc, c.B_lu, c.B_ul, c.A, t_mid);
+      const double C = col_deexc_core(T_e, nne, epsilon_trans, c.coll, c.forbidden != 0, c.osc_f, c.P2,
+                                      (double)c.lower_sw, statweight);
+      if (f(MA_KIND_DOWN, j, R, C, epsilon_trans, c.eps_target, epsilon_current)) return;
+      c = n1;
+      n1 = n2;
+      pc = pn;
+    }
+  }
+  if (i > 0 && l <= K.T.ion_maxrecombininglevel[ui]) {
+    const int nlevels = get_ionisinglevels(K, e, i - 1);
+    for (int lower = 0; lower < nlevels; lower++) {
+      const double epsilon_target = epsilon(K, e, i - 1, lower);
+      const double epsilon_trans = epsilon_current - epsilon_target;
+      const double R = rad_recombination_ratecoeff(K, T_e, nne, e, i, l, lower);
+      const double C = col_recombination_ratecoeff(K, mgi, e, i, l, lower, epsilon_trans);
+      if (f(MA_KIND_RECOMB, lower, R, C, epsilon_trans, epsilon_target, epsilon_current)) return;
+    }
+  }
+  const int nuptrans = K.T.level_nuptrans[ul];
+  if (nuptrans > 0) {
+    const MaUpItem *UI = K.T.ma_up + K.T.level_uptrans_offset[ul];
+    MaUpItem c = UI[0], n1 = UI[nuptrans > 1 ? 1 : 0];
+    double pc = pop(base + c.upper);
+    for (int j = 0; j < nuptrans; j++) {
+      const double pn = pop(base + n1.upper);
+      const MaUpItem n2 = UI[min(j + 2, nuptrans - 1)];
+      const double epsilon_trans = c.eps_upper - epsilon_current;
+      const double R = rad_exc_core(K, mgi, pc, n_self, epsilon_trans, c.B_lu, c.B_ul, c.nu3, t_mid);
+      const double C = col_exc_core(T_e, nne, c.coll, c.forbidden != 0, c.osc_f, c.P2, epsilon_trans, statweight,
+                                    (double)c.upper_sw);
+      if (f(MA_KIND_UP, j, R, C, epsilon_trans, 0., epsilon_current)) return;
+      c = n1;
+      n1 = n2;
+      pc = pn;
+    }
   }
   if (i < K.T.elem_nions[e] - 1 && l < K.T.ion_ionisinglevels[ui]) {
     const int nt = K.T.level_nphixstargets[ul];
