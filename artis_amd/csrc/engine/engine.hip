@@ -362,7 +362,8 @@ __global__ void k_marates(Ctx K, int nts, int ul0, int nlev, double *__restrict_
 // c0 .. c0 + 63 of it, the first nvalid valid), written along positions (64 consecutive keys of one record per row:
 // coalesced) into record rows row0 + c0 + j.
 #ifndef MAPACK_P
-#define MAPACK_P 32  // record positions per LDS tile (32: 24 KB of LDS per block, 6 blocks per CU)
+#define MAPACK_P 64  // record positions per LDS tile (64: a wave stores whole 128-byte lines of a record row, 41 KB of
+                     // LDS per block; 32: 24 KB, 6 blocks per CU, 7 % slower, profiles/r6y_precompute_ab.txt)
 #endif
 struct MapackLds {
   double tile[MAPACK_P][65];
