@@ -594,8 +594,23 @@ __global__ __launch_bounds__(64) void k_ma_build(Ctx K, const int2 *__restrict__
       double *a = lane == 0 ? Drad : lane == 1 ? Dcol : lane == 2 ? Dsame : lane == 3 ? Rint : lane == 4 ? Rrad
                   : lane == 5 ? Rcol : lane == 6 ? Usame : Uhi;
       const int len = lane < 3 ? nd : lane < 6 ? nr : lane == 6 ? nu : nt;
+      // (eight terms read at a time, then added one after another and written back: one LDS round trip per eight
+      // additions instead of one per addition -- the same sums in the same order)
       double r = 0.;
-      for (int j = 0; j < len; j++) {
+      int j = 0;
+      for (; j + 8 <= len; j += 8) {
+        double x[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) x[q] = a[j + q];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          r += x[q];
+          x[q] = r;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++) a[j + q] = x[q];
+      }
+      for (; j < len; j++) {
         r += a[j];
         a[j] = r;
       }

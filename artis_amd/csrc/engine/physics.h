@@ -634,16 +634,16 @@ DEVFN MaItem ma_rate_at(const Ctx &K, int mgi, int ul, double t_mid, int pos, Po
   const double statweight = K.T.level_stat_weight[ul];
   MaItem it;
   const int ndowntrans = K.T.level_ndowntrans[ul];
+  // (the down / up transitions from k_marates' packed items: one load before the population, not a chain of three)
   if (pos < ndowntrans) {
-    const int li = K.T.downtrans_lineindex[K.T.level_downtrans_offset[ul] + pos];
-    const int lower = K.T.line_lower[li];
-    const double epsilon_target = epsilon(K, e, i, lower);
-    const double epsilon_trans = epsilon_current - epsilon_target;
+    const MaDownItem c = K.T.ma_down[K.T.level_downtrans_offset[ul] + pos];
+    const double epsilon_trans = epsilon_current - c.eps_target;
     const double n_self = pop(ul);
-    const double n_l = pop(ul - l + lower);
-    it = {MA_KIND_DOWN, pos, rad_deexcitation_ratecoeff_n(K, n_self, n_l, li, t_mid),
-          col_deexcitation_ratecoeff(K, T_e, nne, epsilon_trans, li, stat_weight(K, e, i, lower), statweight),
-          epsilon_trans, epsilon_target};
+    const double n_l = pop(ul - l + c.lower);
+    it = {MA_KIND_DOWN, pos, rad_deexc_core(n_self, n_l, c.B_lu, c.B_ul, c.A, t_mid),
+          col_deexc_core(T_e, nne, epsilon_trans, c.coll, c.forbidden != 0, c.osc_f, c.P2, (double)c.lower_sw,
+                         statweight),
+          epsilon_trans, c.eps_target};
     return it;
   }
   pos -= ndowntrans;
@@ -659,13 +659,13 @@ DEVFN MaItem ma_rate_at(const Ctx &K, int mgi, int ul, double t_mid, int pos, Po
   pos -= nrl;
   const int nuptrans = K.T.level_nuptrans[ul];
   if (pos < nuptrans) {
-    const int li = K.T.uptrans_lineindex[K.T.level_uptrans_offset[ul] + pos];
-    const int upper = K.T.line_upper[li];
-    const double epsilon_trans = epsilon(K, e, i, upper) - epsilon_current;
+    const MaUpItem c = K.T.ma_up[K.T.level_uptrans_offset[ul] + pos];
+    const double epsilon_trans = c.eps_upper - epsilon_current;
     const double n_self = pop(ul);
-    const double n_u = pop(ul - l + upper);
-    it = {MA_KIND_UP, pos, rad_excitation_ratecoeff_n(K, mgi, n_u, n_self, epsilon_trans, li, t_mid),
-          col_excitation_ratecoeff(K, T_e, nne, li, epsilon_trans, statweight, stat_weight(K, e, i, upper)),
+    const double n_u = pop(ul - l + c.upper);
+    it = {MA_KIND_UP, pos, rad_exc_core(K, mgi, n_u, n_self, epsilon_trans, c.B_lu, c.B_ul, c.nu3, t_mid),
+          col_exc_core(T_e, nne, c.coll, c.forbidden != 0, c.osc_f, c.P2, epsilon_trans, statweight,
+                       (double)c.upper_sw),
           epsilon_trans, 0.};
     return it;
   }
