@@ -719,15 +719,58 @@ __global__ __launch_bounds__(256) void k_transpose(const double *__restrict__ in
   }
 }
 
-__global__ void k_aos_to_soa(const uint64_t *__restrict__ aos, uint64_t *__restrict__ soa, int64_t n) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  for (int w = 0; w < PKT_WORDS; w++) soa[PW(n, i, w)] = aos[i * PKT_WORDS + w];
+// The drop-in boundary's packet array (AoS, 304-byte records) <-> the packet store (packet_soa.h groups), 64 packets
+// per block through LDS: the block's 19 kB of records are read (or written) as one contiguous run, and each group's
+// words as contiguous runs of that group (one packet per thread touched 38 records' lines once per word: the
+// transpose fetched 15x the array, profiles/pmc_r5x_bench.json).  Slot -> word maps of the groups:
+__constant__ int8_t c_hot_word[16] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 18, 33};
+__constant__ int8_t c_cold_word[20] = {19, 21, 22, 23, 24, 36, 37, 20, 14, 15, 16, 17, 25, 26, 27, 28, 29, 30, 32, 35};
+__constant__ int8_t c_rest_word[2] = {31, 34};
+constexpr int8_t h_hot_word[16] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 18, 33};
+constexpr int8_t h_cold_word[20] = {19, 21, 22, 23, 24, 36, 37, 20, 14, 15, 16, 17, 25, 26, 27, 28, 29, 30, 32, 35};
+constexpr int8_t h_rest_word[2] = {31, 34};
+constexpr bool pkt_maps_ok() {
+  for (int s = 0; s < 16; s++)
+    if (pkt_word_group(h_hot_word[s]) != 0 || pkt_word_slot(h_hot_word[s]) != s) return false;
+  for (int s = 0; s < 20; s++)
+    if (pkt_word_group(h_cold_word[s]) != 1 || pkt_word_slot(h_cold_word[s]) != s) return false;
+  for (int s = 0; s < 2; s++)
+    if (pkt_word_group(h_rest_word[s]) != 2 || pkt_word_slot(h_rest_word[s]) != s) return false;
+  return 16 + 20 + 2 == PKT_WORDS;
 }
-__global__ void k_soa_to_aos(const uint64_t *__restrict__ soa, uint64_t *__restrict__ aos, int64_t n) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  for (int w = 0; w < PKT_WORDS; w++) aos[i * PKT_WORDS + w] = soa[PW(n, i, w)];
+static_assert(pkt_maps_ok(), "slot -> word maps agree with packet_soa.h");
+#define XPOSE_PKTS 64
+__global__ __launch_bounds__(256) void k_aos_to_soa(const uint64_t *__restrict__ aos, uint64_t *__restrict__ soa,
+                                                    int64_t n) {
+  __shared__ uint64_t s[XPOSE_PKTS * PKT_WORDS];
+  const int64_t p0 = (int64_t)blockIdx.x * XPOSE_PKTS;
+  const int np = (int)min((int64_t)XPOSE_PKTS, n - p0);
+  for (int q = threadIdx.x; q < np * PKT_WORDS; q += blockDim.x) s[q] = aos[p0 * PKT_WORDS + q];
+  __syncthreads();
+  for (int q = threadIdx.x; q < np * 16; q += blockDim.x)
+    soa[p0 * 16 + q] = s[(q >> 4) * PKT_WORDS + c_hot_word[q & 15]];
+  for (int q = threadIdx.x; q < np * 20; q += blockDim.x) {
+    const int p = q / 20, sl = q % 20;
+    soa[16 * n + (p0 + p) * PKT_COLD_WIDTH + sl] = s[p * PKT_WORDS + c_cold_word[sl]];
+  }
+  for (int q = threadIdx.x; q < np * 2; q += blockDim.x)
+    soa[(16 + PKT_COLD_WIDTH) * n + p0 * 2 + q] = s[(q >> 1) * PKT_WORDS + c_rest_word[q & 1]];
+}
+__global__ __launch_bounds__(256) void k_soa_to_aos(const uint64_t *__restrict__ soa, uint64_t *__restrict__ aos,
+                                                    int64_t n) {
+  __shared__ uint64_t s[XPOSE_PKTS * PKT_WORDS];
+  const int64_t p0 = (int64_t)blockIdx.x * XPOSE_PKTS;
+  const int np = (int)min((int64_t)XPOSE_PKTS, n - p0);
+  for (int q = threadIdx.x; q < np * 16; q += blockDim.x)
+    s[(q >> 4) * PKT_WORDS + c_hot_word[q & 15]] = soa[p0 * 16 + q];
+  for (int q = threadIdx.x; q < np * 20; q += blockDim.x) {
+    const int p = q / 20, sl = q % 20;
+    s[p * PKT_WORDS + c_cold_word[sl]] = soa[16 * n + (p0 + p) * PKT_COLD_WIDTH + sl];
+  }
+  for (int q = threadIdx.x; q < np * 2; q += blockDim.x)
+    s[(q >> 1) * PKT_WORDS + c_rest_word[q & 1]] = soa[(16 + PKT_COLD_WIDTH) * n + p0 * 2 + q];
+  __syncthreads();
+  for (int q = threadIdx.x; q < np * PKT_WORDS; q += blockDim.x) aos[p0 * PKT_WORDS + q] = s[q];
 }
 
 // update_packets.cc:234-333 (pass loop flattened, deviation D5) + do_packet update_packets.cc:137-202
@@ -4109,7 +4152,7 @@ int artis_gpu_packets_upload(const artis_packet *packets, int npkts) {
   G.npkts = npkts;
   if (npkts == 0) return 0;
   HIPCHK(hipMemcpyAsync(G.d_aos, packets, (size_t)npkts * sizeof(artis_packet), hipMemcpyHostToDevice, G.stream));
-  k_aos_to_soa<<<(unsigned)((npkts + 255) / 256), 256, 0, G.stream>>>(G.d_aos, G.d_soa, npkts);
+  k_aos_to_soa<<<(unsigned)((npkts + XPOSE_PKTS - 1) / XPOSE_PKTS), 256, 0, G.stream>>>(G.d_aos, G.d_soa, npkts);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(G.stream));
   return 0;
@@ -4119,7 +4162,7 @@ int artis_gpu_packets_download(artis_packet *packets, int npkts) {
   if (!G.initialised) return ARTIS_ERR_NOT_INITIALISED;
   if (npkts != G.npkts) return ARTIS_ERR_BAD_ARGUMENT;
   if (npkts == 0) return 0;
-  k_soa_to_aos<<<(unsigned)((npkts + 255) / 256), 256, 0, G.stream>>>(G.d_soa, G.d_aos, npkts);
+  k_soa_to_aos<<<(unsigned)((npkts + XPOSE_PKTS - 1) / XPOSE_PKTS), 256, 0, G.stream>>>(G.d_soa, G.d_aos, npkts);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(packets, G.d_aos, (size_t)npkts * sizeof(artis_packet), hipMemcpyDeviceToHost, G.stream));
   HIPCHK(hipStreamSynchronize(G.stream));
