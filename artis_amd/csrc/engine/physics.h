@@ -255,6 +255,9 @@ DEVFN double col_deexcitation_ratecoeff(const Ctx &K, float T_e, float nne, doub
   return col_deexc_core(T_e, nne, epsilon_trans, K.T.line_coll[li], K.T.line_forbidden[li] != 0, K.T.line_f[li],
                         K.T.line_ma[li].P2, lowerstatweight, upperstatweight);
 }
+// col_excitation_ratecoeff's Gaunt factor max(g_bar, 0.276 e^x (-gamma_E - ln x)) is g_bar for every x with
+// ln x > -gamma_E = -0.5772 (x > 0.5615): from x > 0.57 on (ln 0.57 = -0.5621) the log is skipped
+#define MA_GAUNT_NOLOG 0.57
 // macroatom.h:107-150, on the line's values as col_deexc_core
 DEVFN double col_exc_core(float T_e, float nne, double coll_strength, bool forbidden, float osc_f, double P2,
                           double epsilon_trans, double lowerstatweight, double upperstatweight) {
@@ -264,7 +267,10 @@ DEVFN double col_exc_core(float T_e, float nne, double coll_strength, bool forbi
     if (!forbidden) {
       const double g_bar = 0.2;
       const double exp_eoverkt = exp(eoverkt);
-      const double test = 0.276 * exp_eoverkt * (-0.5772156649 - log(eoverkt));
+      // (above MA_GAUNT_NOLOG the log exceeds -0.5621 > -0.5772: test is negative and Gamma is g_bar whatever its
+      // value, so the log is not evaluated -- the same Gamma, bit for bit)
+      const double test =
+          eoverkt > MA_GAUNT_NOLOG ? -1. : 0.276 * exp_eoverkt * (-0.5772156649 - log(eoverkt));
       const double Gamma = g_bar > test ? g_bar : test;
       C = ARTIS_C_0 * nne * sqrtf(T_e) * 14.51039491 * osc_f * P2 * eoverkt / exp_eoverkt * Gamma;
     } else {
@@ -291,7 +297,8 @@ DEVFN double te_col_exc(const TeExcItem &it, float T_e, float nne, double lowers
     if (!it.forbidden) {
       const double g_bar = 0.2;
       const double exp_eoverkt = exp(eoverkt);
-      const double test = 0.276 * exp_eoverkt * (-0.5772156649 - log(eoverkt));
+      const double test =
+          eoverkt > MA_GAUNT_NOLOG ? -1. : 0.276 * exp_eoverkt * (-0.5772156649 - log(eoverkt));  // (col_exc_core)
       const double Gamma = g_bar > test ? g_bar : test;
       C = ARTIS_C_0 * nne * sqrtf(T_e) * 14.51039491 * it.osc_f * it.P2 * eoverkt / exp_eoverkt * Gamma;
     } else {

@@ -510,10 +510,10 @@ DEVFN double te_col_exc_fast(const TeExcItem &it, const TeExcT &f, double inv_ls
   const double eoverkt = it.epsilon_trans * f.inv_kT;
   const bool allowed = coll_strength < 0 && !it.forbidden;
   const double ex = exp(allowed ? eoverkt : -eoverkt);
-  const double lg = log(eoverkt);
+  const double lg = (allowed && eoverkt <= MA_GAUNT_NOLOG) ? log(eoverkt) : 0.;  // (Gamma = 0.2 above: physics.h)
   double C;
   if (allowed) {
-    const double test = 0.276 * ex * (-0.5772156649 - lg);
+    const double test = eoverkt > MA_GAUNT_NOLOG ? -1. : 0.276 * ex * (-0.5772156649 - lg);
     const double Gamma = 0.2 > test ? 0.2 : test;
     C = f.A1 * it.osc_f * it.P2 * eoverkt / ex * Gamma;
   } else if (coll_strength < 0) {
