@@ -428,15 +428,34 @@ DEVFN void mapack_tile(const Ctx &K, int ul, const double *__restrict__ src, int
                                                : ARTIS_MA_ACTION_INTERNALUPHIGHER;
       int sp;
       const int rp = ma_rec_pos(lay, p, mm.nd, mm.nu, &sp);
-      for (int j = ty; j < 64; j += RS) {
-        if (c0 + j >= nvalid) break;
-        const uint32_t key = (a < 0) ? S.akey[p][j] : ma_key32(S.tile[tx][j], S.norm[a][j]);
-        uint16_t *rec = K.C.ma_key + (row0 + c0 + j) * K.C.ma_key_stride + mm.rec_off;
-        rec[rp] = (uint16_t)(key >> 16);
-        rec[lay.hot + rp] = (uint16_t)(key & 0xffffu);
-        if (sp >= 0) {  // also a block separator on the record's first line
-          rec[sp] = (uint16_t)(key >> 16);
-          rec[lay.hot + sp] = (uint16_t)(key & 0xffffu);
+      // the rows of this position U at a time: their LDS terms and norms read together, then the keys (branch-free
+      // ma_key32_nb) and stores -- one LDS round trip per U keys instead of two dependent ones per key
+      constexpr int U = 4;
+      static_assert(64 % (U * RS) == 0, "row groups of U");
+      const int an = a < 0 ? 0 : a, pa = p < ARTIS_MA_ACTION_COUNT ? p : 0;
+      for (int j0 = ty; j0 < 64; j0 += U * RS) {
+        double v[U], nv[U];
+        uint32_t ak[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int j = j0 + u * RS;
+          v[u] = S.tile[tx][j];
+          nv[u] = S.norm[an][j];
+          ak[u] = S.akey[pa][j];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int j = j0 + u * RS;
+          if (c0 + j < nvalid) {
+            const uint32_t key = (a < 0) ? ak[u] : ma_key32_nb(v[u], nv[u]);
+            uint16_t *rec = K.C.ma_key + (row0 + c0 + j) * K.C.ma_key_stride + mm.rec_off;
+            rec[rp] = (uint16_t)(key >> 16);
+            rec[lay.hot + rp] = (uint16_t)(key & 0xffffu);
+            if (sp >= 0) {  // also a block separator on the record's first line
+              rec[sp] = (uint16_t)(key >> 16);
+              rec[lay.hot + sp] = (uint16_t)(key & 0xffffu);
+            }
+          }
         }
       }
     }

@@ -746,6 +746,13 @@ DEVFN uint32_t ma_key32(double v, double norm) {
   const double q = floor(v / norm * MA_KEY_SCALE + 0.5);
   return (uint32_t)(q < 0. ? 0. : (q > MA_KEY_SCALE ? MA_KEY_SCALE : q));
 }
+// the same key without the branch (k_mapack's unrolled rows): the quotient is formed for every norm and replaced by
+// 0 where ma_key32 returns 0
+DEVFN uint32_t ma_key32_nb(double v, double norm) {
+  const double q = floor(v / norm * MA_KEY_SCALE + 0.5);
+  const double qc = (norm > 0.) ? q : 0.;
+  return (uint32_t)(qc < 0. ? 0. : (qc > MA_KEY_SCALE ? MA_KEY_SCALE : qc));
+}
 // Decides `running sum > x` for x = u * norm (u the uniform draw, q = u * MA_KEY_SCALE) from the key: +1 greater,
 // -1 not greater, 0 undecided.  A key is within 0.5 (+ ~1e-5 of rounding in the divisions) of the exact value on
 // the 2^32 scale, and q within ~1e-5 of x / norm on that scale.  ma_key_cmp_hi decides from the high half alone
