@@ -721,6 +721,43 @@ __global__ __launch_bounds__(256) void k_linecoef(Ctx K) {
   if (__any(neg) && __lane_id() == 0 && !*(volatile int32_t *)K.C.linecoef_neg) atomicOr(K.C.linecoef_neg, 1);
 }
 
+// k_linecoef with the populations in LDS: a block copies LINECOEF_LDS_R consecutive rows of populations (contiguous
+// in DevCells::pops) into LDS once and walks every line for them, the line records from L2.  The gathers of the
+// kernel above -- two per line and row, ~60 distinct cache lines per wave instruction -- bound it at the vector
+// memory pipeline (27 ms per upload of the bench model for a 49 GB table); from LDS they cost a few cycles, and the
+// kernel is left with its stores.  The same expression, so the same table bit for bit.  nr_max rows fit the
+// LINECOEF_LDS_DOUBLES of LDS (host: models whose levels do not fit one row take the kernel above).
+#define LINECOEF_LDS_DOUBLES 18432  // 144 KiB: 5 rows of the bench's 3 603 levels
+__global__ __launch_bounds__(1024) void k_linecoef_lds(Ctx K, int nr_max) {
+  __shared__ double sp[LINECOEF_LDS_DOUBLES];
+  const int64_t nl = K.T.nlevels_total, rows = K.C.linecoef_rows, stride = K.C.linecoef_stride;
+  const int nlines = K.T.nlines;
+  bool neg = false;
+  for (int64_t k0 = (int64_t)blockIdx.x * nr_max; k0 < rows; k0 += (int64_t)gridDim.x * nr_max) {
+    const int nr = (int)min((int64_t)nr_max, rows - k0);
+    __syncthreads();  // (the previous rows' readers are done)
+    const double *src = K.C.pops + k0 * nl;
+    for (int64_t q = threadIdx.x; q < nr * nl; q += blockDim.x) sp[q] = src[q];
+    __syncthreads();
+    for (int64_t li = threadIdx.x; li < stride; li += blockDim.x) {
+      const bool in = li < nlines;
+      LineTau r{};
+      if (in) r = K.T.line_tau[li];
+      double *out = K.C.linecoef + k0 * stride + li;
+      for (int q = 0; q < nr; q++) {
+        double v = 0.;
+        if (in) {
+          const double n_u = sp[q * nl + r.ul_upper], n_l = sp[q * nl + r.ul_lower];
+          v = (r.B_lu * n_l - r.B_ul * n_u) * ARTIS_HCLIGHTOVERFOURPI;
+          neg = neg || v < 0.;
+        }
+        out[q * stride] = v;
+      }
+    }
+  }
+  if (__any(neg) && __lane_id() == 0 && !*(volatile int32_t *)K.C.linecoef_neg) atomicOr(K.C.linecoef_neg, 1);
+}
+
 // out[c * rows + r] = in[r * cols + c], through a 64x64 LDS tile (one wave reads rows, writes columns)
 __global__ __launch_bounds__(256) void k_transpose(const double *__restrict__ in, double *__restrict__ out,
                                                    int64_t rows, int64_t cols) {
@@ -4123,10 +4160,18 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
       k_transpose<<<dim3((unsigned)((ntg + 63) / 64), (unsigned)((n_ne + 63) / 64)), 256, 0, G.stream>>>(
           G.K.C.corrphot, G.K.C.corrphotT, n_ne, ntg);
     if (G.K.C.linecoef) HIPCHK(hipMemsetAsync(G.K.C.linecoef_neg, 0, sizeof(int32_t), G.stream));
-    if (G.K.C.linecoef)
-      k_linecoef<<<dim3((unsigned)((G.K.C.linecoef_stride + 255) / 256),
-                        (unsigned)std::min((G.K.C.linecoef_rows + LINECOEF_R - 1) / LINECOEF_R, 32768)), 256, 0,
-                    G.stream>>>(G.K);
+    if (G.K.C.linecoef) {
+      const int lc_rows_lds = (int)std::min<int64_t>(5, LINECOEF_LDS_DOUBLES / std::max<int64_t>(1, nl));
+      static const bool lc_gather = getenv("ARTIS_GPU_LINECOEF_GATHER") && atoi(getenv("ARTIS_GPU_LINECOEF_GATHER"));
+      if (lc_rows_lds >= 1 && !lc_gather)
+        k_linecoef_lds<<<(unsigned)std::min<int64_t>((G.K.C.linecoef_rows + lc_rows_lds - 1) / lc_rows_lds,
+                                                     (int64_t)G.wave_grid / 2),  // (4 blocks per CU; one fits)
+                         1024, 0, G.stream>>>(G.K, lc_rows_lds);
+      else
+        k_linecoef<<<dim3((unsigned)((G.K.C.linecoef_stride + 255) / 256),
+                          (unsigned)std::min((G.K.C.linecoef_rows + LINECOEF_R - 1) / LINECOEF_R, 32768)), 256, 0,
+                      G.stream>>>(G.K);
+    }
     const int mr = G.K.C.ma_rows;
     if (G.K.C.ma_level_mode) {
       // level mode: the action totals of every (cell, level) pair (the jumps without a record select from them),
