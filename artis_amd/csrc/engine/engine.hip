@@ -4162,7 +4162,8 @@ int artis_gpu_upload_cellstate(int nts, const artis_cell_state *cs) {
     if (G.K.C.linecoef) HIPCHK(hipMemsetAsync(G.K.C.linecoef_neg, 0, sizeof(int32_t), G.stream));
     if (G.K.C.linecoef) {
       const int lc_rows_lds = (int)std::min<int64_t>(5, LINECOEF_LDS_DOUBLES / std::max<int64_t>(1, nl));
-      static const bool lc_gather = getenv("ARTIS_GPU_LINECOEF_GATHER") && atoi(getenv("ARTIS_GPU_LINECOEF_GATHER"));
+      const char *lcg = getenv("ARTIS_GPU_LINECOEF_GATHER");  // (A/B and test switch: the gather kernel)
+      const bool lc_gather = lcg && atoi(lcg);
       if (lc_rows_lds >= 1 && !lc_gather)
         k_linecoef_lds<<<(unsigned)std::min<int64_t>((G.K.C.linecoef_rows + lc_rows_lds - 1) / lc_rows_lds,
                                                      (int64_t)G.wave_grid / 2),  // (4 blocks per CU; one fits)

@@ -103,13 +103,16 @@ def test_without_macroatom_cache_is_identical(small_model, engine_factory, monke
                                  {"ARTIS_GPU_MACACHE_ROWS": "half", "ARTIS_GPU_MA_BUILD_SMALL": "0"},
                                  {"ARTIS_GPU_MACACHE_ROWS": "half", "ARTIS_GPU_MA_BUILD_SMALL": "64"},
                                  {"ARTIS_GPU_LINECOEF_ROWS": "1", "ARTIS_GPU_MACACHE_ROWS": "1"},
-                                 {"ARTIS_GPU_NO_MACACHE": "1"}],
+                                 {"ARTIS_GPU_NO_MACACHE": "1"}, {"ARTIS_GPU_LINECOEF_GATHER": "1"},
+                                 {"ARTIS_GPU_LINECOEF_GATHER": "1", "ARTIS_GPU_LINECOEF_ROWS": "half"}],
                          ids=["no_linecoef", "half_linecoef", "half_macache", "half_macache_large_builds",
-                              "half_macache_mixed_builds", "one_row_each", "no_macache"])
+                              "half_macache_mixed_builds", "one_row_each", "no_macache", "linecoef_gather_kernel",
+                              "half_linecoef_gather_kernel"])
 def test_table_budgets_match_oracle(small_model, engine_factory, monkeypatch, env):
     """Per-cell tables that only fit the HBM budget for some cells -- line coefficients centre outwards, macro-atom
     key records per (cell, level) in level mode, built by the small-level and the large-level launch
-    (ARTIS_GPU_MA_BUILD_SMALL moves the split) -- or for none (no line coefficients; an empty record pool: every
+    (ARTIS_GPU_MA_BUILD_SMALL moves the split); the line coefficients also by the gather kernel that
+    k_linecoef_lds replaced (ARTIS_GPU_LINECOEF_GATHER) -- or for none (no line coefficients; an empty record pool: every
     macro-atom jump made by the whole wave from the exact sums, ma_coop_select) give the same packet histories as
     the oracle and the full-table engine."""
     small_model.set_timestep(11)
