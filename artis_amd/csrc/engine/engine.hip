@@ -517,10 +517,11 @@ __global__ __launch_bounds__(256) void k_lvl_decay(uint32_t *__restrict__ hist, 
 }
 
 #define MA_BUILD_MAX_DOUBLES 6144  // LDS terms of one level (48 KiB); a level with more never gets a record
-// k_ma_build's LDS terms of a level (below).  The levels whose terms take at most 20 KiB are built by their own launch of that LDS size: 8 blocks per CU (the
-// 169-VGPR kernel's limit of 2 waves per SIMD), where sizing every block for the largest level of a large atom
-// left 3 blocks per CU
-#define MA_BUILD_SMALL 2560
+// k_ma_build's LDS terms of a level (below).  The levels whose terms take at most 10 KiB are built by their own
+// launch of that LDS size: 16 blocks per CU, 4 waves per SIMD with the kernel's 128 VGPRs (MA_BUILD_MINW), where
+// sizing every block for the largest level of a large atom left 3 blocks per CU (round 6 until its last session: 20
+// KiB and 169 VGPRs, 2 waves per SIMD)
+#define MA_BUILD_SMALL 1280
 static inline __host__ __device__ int64_t ma_build_doubles(const MaMeta &m) { return 3 * ((int64_t)m.nd + m.nr) + m.nu + m.nt; }
 // k_lvl_select: the new DevCells::ma_lptr and the list of records to build.  have_hist == 0 (no transport yet):
 // whole cells in nonempty-index order (centre outwards), pair (k, ul) at line k * row_lines + rl_off[ul] while it
@@ -573,7 +574,12 @@ __global__ __launch_bounds__(256) void k_lvl_select(Ctx K, const uint32_t *__res
 // (macroatom.cc:57-159: every action's running sum only involves its own terms, so the chains are independent and
 // equal to ma_accumulate's sequence bit for bit); the lanes write the normalised 32-bit keys at their record
 // positions (ma_rec_pos, with the block separators).
-__global__ __launch_bounds__(64) void k_ma_build(Ctx K, const int2 *__restrict__ list, uint32_t nlist, int nts) {
+#ifndef MA_BUILD_MINW
+#define MA_BUILD_MINW 4  // waves per SIMD k_ma_build is compiled for (128 VGPRs; with the small launch's 10 KiB of LDS, 4
+                         // waves per SIMD: level-mode precompute 1.69 -> 1.34 s, profiles/r6u_level_mode_ab.txt)
+#endif
+__global__ __launch_bounds__(64, MA_BUILD_MINW) void k_ma_build(Ctx K, const int2 *__restrict__ list, uint32_t nlist,
+                                                              int nts) {
   extern __shared__ double sb[];
   const int lane = threadIdx.x;
   const int64_t nl = K.T.nlevels_total;
